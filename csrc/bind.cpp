@@ -1,0 +1,200 @@
+// Python bindings (pybind11) for the native parts of log_parser_amd:
+//   * the Java-regex compiler (csrc/regex)
+//   * gfx950 kernel launchers and their host twins (csrc/kernels)
+//   * host line splitter for request batches and the JSON result emitter (csrc/io)
+// Tensors cross the boundary as raw pointers (torch .data_ptr()) plus the HIP stream handle, so
+// the module does not depend on libtorch headers and compiles in seconds.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "io/json_emit.h"
+#include "kernels/lp_api.h"
+#include "regex/jregex.h"
+
+namespace py = pybind11;
+using namespace lp;
+
+template <typename T>
+static T* P(uint64_t v) { return reinterpret_cast<T*>(v); }
+
+static PfTables pf_from(const py::tuple& t) {
+  PfTables T;
+  T.bloom = P<const uint32_t>(t[0].cast<uint64_t>());
+  T.bloom_bits = t[1].cast<int>();
+  T.ht_key = P<const uint64_t>(t[2].cast<uint64_t>());
+  T.ht_val = P<const int32_t>(t[3].cast<uint64_t>());
+  T.ht_cnt = P<const int32_t>(t[4].cast<uint64_t>());
+  T.ht_mask = t[5].cast<uint32_t>();
+  T.gram_lits = P<const int32_t>(t[6].cast<uint64_t>());
+  T.lit_off = P<const int32_t>(t[7].cast<uint64_t>());
+  T.lit_bytes = P<const uint8_t>(t[8].cast<uint64_t>());
+  T.lit_reg_off = P<const int32_t>(t[9].cast<uint64_t>());
+  T.lit_reg = P<const int32_t>(t[10].cast<uint64_t>());
+  T.gmask = t[11].cast<int>();
+  return T;
+}
+
+static DfaPool dfa_from(const py::tuple& t) {
+  DfaPool D;
+  D.meta = P<const int32_t>(t[0].cast<uint64_t>());
+  D.bytemap = P<const uint8_t>(t[1].cast<uint64_t>());
+  D.trans = P<const uint16_t>(t[2].cast<uint64_t>());
+  D.acc = P<const uint8_t>(t[3].cast<uint64_t>());
+  return D;
+}
+
+static ScoreTables st_from(const py::tuple& t) {
+  ScoreTables T;
+  int i = 0;
+  auto nx = [&]() { return t[i++].cast<uint64_t>(); };
+  T.conf = P<const double>(nx()); T.sev = P<const double>(nx());
+  T.ctx_before = P<const int32_t>(nx()); T.ctx_after = P<const int32_t>(nx());
+  T.sec_off = P<const int32_t>(nx()); T.sec_reg = P<const int32_t>(nx()); T.sec_w = P<const int32_t>(nx());
+  T.sec_weight = P<const double>(nx());
+  T.seq_off = P<const int32_t>(nx()); T.seq_bonus = P<const double>(nx()); T.seq_ev_off = P<const int32_t>(nx());
+  T.seq_ev_reg = P<const int32_t>(nx()); T.seq_carry = P<const uint8_t>(nx());
+  T.hit_off = P<const int64_t>(nx()); T.hit_line = P<const int32_t>(nx()); T.feat = P<const uint8_t>(nx());
+  T.seg_lo = P<const int32_t>(nx()); T.seg_hi = P<const int32_t>(nx()); T.seg_own_lo = P<const int32_t>(nx());
+  T.seg_g0 = P<const int64_t>(nx()); T.seg_n = P<const int64_t>(nx());
+  return T;
+}
+
+static ScoreParams sp_from(const py::tuple& t) {
+  ScoreParams S;
+  S.decay = t[0].cast<double>(); S.early = t[1].cast<double>(); S.maxearly = t[2].cast<double>();
+  S.penalty = t[3].cast<double>(); S.max_ctx = t[4].cast<double>(); S.fthr = t[5].cast<double>();
+  S.fmaxp = t[6].cast<double>(); S.fwin = t[7].cast<double>();
+  return S;
+}
+
+static py::bytes vbytes(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
+
+static py::dict compile_regex(const std::string& pat, int max_states, int max_positions) {
+  Compiled c = compile(pat, max_states, max_positions);
+  py::dict d;
+  d["kind"] = (int)c.kind;
+  d["error"] = c.error;
+  py::list lits;
+  for (auto& s : c.literals) lits.append(py::bytes(s));
+  d["literals"] = lits;
+  d["has_literals"] = c.has_literals;
+  if (c.kind == Kind::DFA) {
+    d["nstates"] = c.dfa.nstates;
+    d["nclasses"] = c.dfa.nclasses;
+    d["bytemap"] = vbytes(c.dfa.bytemap.data(), c.dfa.bytemap.size());
+    d["trans"] = vbytes(c.dfa.trans.data(), c.dfa.trans.size() * 2);
+    d["acc"] = vbytes(c.dfa.accflags.data(), c.dfa.accflags.size());
+    d["anchored"] = c.dfa.anchored;
+  }
+  if (c.kind == Kind::DFA || c.kind == Kind::NFA) {
+    d["npos"] = c.nfa.npos;
+    std::string cls;
+    for (auto& b : c.nfa.cls) cls.append(reinterpret_cast<const char*>(b.w), 32);
+    d["nfa_cls"] = py::bytes(cls);
+    py::list first, last, follow;
+    for (auto& e : c.nfa.first) first.append(py::make_tuple(e.to, e.cond));
+    for (auto& e : c.nfa.last) last.append(py::make_tuple(e.to, e.cond));
+    for (auto& v : c.nfa.follow) {
+      py::list l;
+      for (auto& e : v) l.append(py::make_tuple(e.to, e.cond));
+      follow.append(l);
+    }
+    d["nfa_first"] = first;
+    d["nfa_last"] = last;
+    d["nfa_follow"] = follow;
+    d["nfa_nullable"] = c.nfa.nullable;
+  }
+  return d;
+}
+
+static bool dfa_find_py(const std::string& pat, const std::string& line, int max_states) {
+  Compiled c = compile(pat, max_states, 4096);
+  if (c.kind != Kind::DFA) throw std::runtime_error("not a DFA regex: " + c.error);
+  return dfa_find(c.dfa, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size());
+}
+
+// Split each document of a concatenated buffer with Java String.split("\\r?\\n") semantics.
+// Returns (line_start int64[L], line_len int32[L], doc_line_off int64[D+1]).
+static py::tuple split_docs(uint64_t buf, py::array_t<int64_t> doc_off) {
+  const uint8_t* b = P<const uint8_t>(buf);
+  auto off = doc_off.unchecked<1>();
+  const int64_t D = off.shape(0) - 1;
+  std::vector<int64_t> st;
+  std::vector<int32_t> ln;
+  std::vector<int64_t> dl(D + 1, 0);
+  for (int64_t d = 0; d < D; ++d) {
+    const int64_t s0 = off(d), s1 = off(d + 1);
+    const size_t first = st.size();
+    int64_t start = s0;
+    bool any = false;
+    for (;;) {
+      const void* q = memchr(b + start, '\n', (size_t)(s1 - start));
+      if (!q) break;
+      any = true;
+      int64_t nl = static_cast<const uint8_t*>(q) - b;
+      int64_t end = nl;
+      if (end > start && b[end - 1] == '\r') --end;
+      st.push_back(start);
+      ln.push_back((int32_t)(end - start));
+      start = nl + 1;
+    }
+    st.push_back(start);
+    ln.push_back((int32_t)(s1 - start));
+    if (any) {
+      while (st.size() > first && ln.back() == 0) { st.pop_back(); ln.pop_back(); }
+    }
+    dl[d + 1] = (int64_t)st.size();
+  }
+  py::array_t<int64_t> a(st.size());
+  py::array_t<int32_t> l(ln.size());
+  py::array_t<int64_t> o(dl.size());
+  if (!st.empty()) { memcpy(a.mutable_data(), st.data(), st.size() * 8); memcpy(l.mutable_data(), ln.data(), ln.size() * 4); }
+  memcpy(o.mutable_data(), dl.data(), dl.size() * 8);
+  return py::make_tuple(a, l, o);
+}
+
+PYBIND11_MODULE(_lpnative, m) {
+  m.doc() = "log_parser_amd native core: Java-regex compiler, gfx950 kernels, host twins, JSON emitter";
+  m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
+  m.def("dfa_find", &dfa_find_py, py::arg("pattern"), py::arg("line"), py::arg("max_states") = 4096);
+  m.def("split_docs", &split_docs);
+  m.def("nl_tiles", &nl_tiles);
+
+  // ---- device launchers
+  m.def("nl_count_dev", [](uint64_t text, int64_t n, uint64_t cnt, uint64_t s) { nl_count_dev(P<const uint8_t>(text), n, P<int32_t>(cnt), s); });
+  m.def("nl_write_dev", [](uint64_t text, int64_t n, uint64_t off, uint64_t pos, uint64_t s) {
+    nl_write_dev(P<const uint8_t>(text), n, P<const int64_t>(off), P<int64_t>(pos), s); });
+  m.def("prefilter_dev", [](uint64_t text, int64_t n, py::tuple pf, uint64_t ls, int64_t nl, uint64_t cand, int64_t cap,
+                            uint64_t count, int grid, uint64_t s) {
+    prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
+                  P<unsigned long long>(count), grid, s); });
+  m.def("verify_dev", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out, uint64_t s) {
+    verify_dev(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out), s); });
+  m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
+                       uint64_t out, int64_t cap, uint64_t count, uint64_t s) {
+    scan_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs), nregs,
+             dfa_from(dfa), P<int64_t>(out), cap, P<unsigned long long>(count), s); });
+  m.def("score_dev", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t ef, int64_t n, py::tuple st, py::tuple sp,
+                        uint64_t out, uint64_t fac, uint64_t s) {
+    score_dev(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), P<const int64_t>(ef), n, st_from(st),
+              sp_from(sp), P<double>(out), P<double>(fac), s); });
+
+  // ---- host twins
+  m.def("nl_positions_host", [](uint64_t text, int64_t n, uint64_t pos) { return nl_positions_host(P<const uint8_t>(text), n, P<int64_t>(pos)); });
+  m.def("prefilter_host", [](uint64_t text, int64_t n, py::tuple pf, uint64_t ls, int64_t nl, uint64_t cand, int64_t cap) {
+    return prefilter_host(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap); });
+  m.def("verify_host", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out) {
+    verify_host(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out)); });
+  m.def("scan_host", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
+                        uint64_t out, int64_t cap) {
+    return scan_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs),
+                     nregs, dfa_from(dfa), P<int64_t>(out), cap); });
+  m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t ef, int64_t n, py::tuple st, py::tuple sp,
+                         uint64_t out, uint64_t fac) {
+    score_host(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), P<const int64_t>(ef), n, st_from(st),
+               sp_from(sp), P<double>(out), P<double>(fac)); });
+
+  // ---- JSON result emitter
+  m.def("emit_events_json", &emit_events_json_py);
+}

@@ -1,0 +1,32 @@
+// Launch / host entry points of lp_kernels.hip (bound to Python in csrc/bind.cpp).
+#pragma once
+#include <stdint.h>
+
+#include "lp_core.h"
+
+namespace lp {
+
+int64_t nl_tiles(int64_t nbytes);
+void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream);
+void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, uint64_t stream);
+void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
+                   int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
+void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+                const DfaPool& P, uint8_t* out, uint64_t stream);
+void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+              const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
+              uint64_t stream);
+void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+               const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream);
+
+int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
+int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
+                       int64_t nlines, int64_t* cand, int64_t cap);
+void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start,
+                 const int32_t* line_len, const DfaPool& P, uint8_t* out);
+int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+                  const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap);
+void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+                const ScoreTables& T, const ScoreParams& S, double* out, double* factors);
+
+}  // namespace lp

@@ -1,0 +1,285 @@
+// Shared host/device building blocks of the log-analysis pipeline.
+//
+// Every routine here is compiled twice from the same source: into gfx950 kernels (HIP) and into
+// the host (CPU) backend used by CPU-only tests and as the availability fallback. Keeping one
+// source guarantees the CPU tests exercise the exact arithmetic the GPU runs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LP_HD __host__ __device__ __forceinline__
+
+namespace lp {
+
+// --------------------------------------------------------------------------------------------
+// DFA pool (all regexes of a library, concatenated).  meta[r*4 + {0,1,2,3}] =
+//   {trans offset (uint16 units), nclasses, accflags offset, flags(bit0 anchored)}
+struct DfaPool {
+  const int32_t* meta;
+  const uint8_t* bytemap;   // [R][256]
+  const uint16_t* trans;
+  const uint8_t* acc;
+};
+
+LP_HD int final_term_len(const uint8_t* s, int n) {
+  if (n >= 1 && s[n - 1] == '\r') return 1;
+  if (n >= 2 && s[n - 2] == 0xC2 && s[n - 1] == 0x85) return 2;
+  if (n >= 3 && s[n - 3] == 0xE2 && s[n - 2] == 0x80 && (s[n - 1] == 0xA8 || s[n - 1] == 0xA9)) return 3;
+  return 0;
+}
+
+// find() of regex r over one line (java.util.regex Matcher.find semantics, see jregex.h)
+LP_HD bool dfa_run(const DfaPool& P, int r, const uint8_t* s, int n) {
+  const int32_t* m = P.meta + 4 * r;
+  const uint16_t* T = P.trans + m[0];
+  const int nc = m[1];
+  const uint8_t* A = P.acc + m[2];
+  const uint8_t* bm = P.bytemap + 256 * r;
+  int ft = n - final_term_len(s, n);
+  if (ft == n) ft = -1;
+  int st = 2;
+  for (int t = 0; t < n; ++t) {
+    if (t == ft && (A[st] & 2)) return true;
+    st = T[st * nc + bm[s[t]]];
+    if (st < 2) return st == 1;
+  }
+  return (A[st] & 1) != 0;
+}
+
+// --------------------------------------------------------------------------------------------
+// literal prefilter tables
+struct PfTables {
+  const uint32_t* bloom;    // 1<<bloom_bits bits
+  int bloom_bits;
+  const uint64_t* ht_key;   // open addressing, EMPTY = ~0
+  const int32_t* ht_val;    // start into gram_lits
+  const int32_t* ht_cnt;
+  uint32_t ht_mask;
+  const int32_t* gram_lits;
+  const int32_t* lit_off;   // [nlit+1] into lit_bytes
+  const uint8_t* lit_bytes; // ASCII-lowercased
+  const int32_t* lit_reg_off;
+  const int32_t* lit_reg;
+  int gmask;                // bit g set when grams of length g (2..4) exist
+};
+
+LP_HD uint32_t gram_mask(int g) { return g >= 4 ? 0xFFFFFFFFu : ((1u << (8 * g)) - 1u); }
+LP_HD uint32_t bloom_h1(uint32_t key, int g, int bits) {
+  return ((key ^ (uint32_t)g * 0x9E3779B9u) * 0x85EBCA6Bu) >> (32 - bits);
+}
+LP_HD uint32_t bloom_h2(uint32_t key, int g, int bits) {
+  return ((key + (uint32_t)g * 0x27D4EB2Fu) * 0xC2B2AE35u) >> (32 - bits);
+}
+LP_HD uint32_t ht_hash(uint32_t key, int g) {
+  uint32_t h = key * 0x9E3779B1u ^ ((uint32_t)g * 0x7FEB352Du);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h;
+}
+LP_HD int lower_byte(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+// SWAR ASCII lower-casing of 4 packed bytes (bytes >= 0x80 untouched)
+LP_HD uint32_t lower4(uint32_t x) {
+  uint32_t hi = 0x80808080u;
+  uint32_t ge_A = ((x | hi) - 0x41414141u) & hi;   // byte >= 'A' (for < 0x80)
+  uint32_t ge_Z1 = ((x | hi) - 0x5B5B5B5Bu) & hi;  // byte >= 'Z'+1
+  uint32_t up = ge_A & ~ge_Z1 & ~x & hi;
+  return x | (up >> 2);
+}
+
+// largest index i in [0,n) with a[i] <= v  (a sorted ascending); -1 if none
+LP_HD int64_t upper_idx(const int64_t* a, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1;
+}
+// first index in [lo,hi) with a[i] >= v
+LP_HD int64_t lower_bound32(const int32_t* a, int64_t lo, int64_t hi, int32_t v) {
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Probe one gram hit at text position p; appends (regex<<32 | line) candidates.
+template <typename AppendFn>
+LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, uint32_t gram, int g,
+                    const int64_t* line_start, int64_t nlines, AppendFn&& append) {
+  uint64_t key = (uint64_t)gram | ((uint64_t)g << 32);
+  uint32_t h = ht_hash(gram, g) & T.ht_mask;
+  for (;;) {
+    uint64_t kk = T.ht_key[h];
+    if (kk == ~0ull) return;
+    if (kk == key) break;
+    h = (h + 1) & T.ht_mask;
+  }
+  const int s = T.ht_val[h], c = T.ht_cnt[h];
+  int64_t line = -1;
+  for (int j = 0; j < c; ++j) {
+    const int lit = T.gram_lits[s + j];
+    const int lo = T.lit_off[lit], len = T.lit_off[lit + 1] - lo;
+    if (p + len > nbytes) continue;
+    bool ok = true;
+    for (int q = g; q < len; ++q)
+      if (lower_byte(text[p + q]) != T.lit_bytes[lo + q]) { ok = false; break; }
+    if (!ok) continue;
+    if (line < 0) line = upper_idx(line_start, nlines, p);
+    if (line < 0) line = 0;
+    for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
+      append(((int64_t)T.lit_reg[r] << 32) | line);
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// scoring (fp64, Java double semantics, left-to-right product: ScoringService.java:102-109)
+struct ScoreParams {
+  double decay;          // scoring.proximity.decay-constant
+  double early, maxearly, penalty;   // chronological
+  double max_ctx;        // scoring.context.max-context-factor
+  double fthr, fmaxp, fwin;          // frequency
+};
+
+struct ScoreTables {
+  // per pattern
+  const double* conf; const double* sev;
+  const int32_t* ctx_before; const int32_t* ctx_after;   // -1: rules null
+  const int32_t* sec_off; const int32_t* sec_reg; const int32_t* sec_w; const double* sec_weight;
+  const int32_t* seq_off; const double* seq_bonus; const int32_t* seq_ev_off; const int32_t* seq_ev_reg;
+  const uint8_t* seq_carry;   // per sequence event slot: chain satisfiable in earlier shards
+  // per regex hit lists (CSR, lines ascending)
+  const int64_t* hit_off; const int32_t* hit_line;
+  const uint8_t* feat;        // per local line: 1 ERR, 2 WARN, 4 STACK, 8 EXC
+  // per segment (document / shard)
+  const int32_t* seg_lo; const int32_t* seg_hi; const int32_t* seg_own_lo;
+  const int64_t* seg_g0; const int64_t* seg_n;
+};
+
+LP_HD double chrono_factor(int64_t gi, int64_t n, const ScoreParams& S) {
+  const double pos = (double)gi / (double)n;
+  if (pos <= S.early) return 1.5 + (S.early - pos) * ((S.maxearly - 1.5) / S.early);
+  if (pos <= S.penalty) return 1.0 + (S.penalty - pos) * (0.5 / (S.penalty - S.early));
+  return 0.5 + (1.0 - pos);
+}
+
+// any hit of regex r within local [a,b)
+LP_HD bool any_hit(const ScoreTables& T, int r, int32_t a, int32_t b) {
+  if (r < 0 || a >= b) return false;
+  const int64_t lo = T.hit_off[r], hi = T.hit_off[r + 1];
+  const int64_t i = lower_bound32(T.hit_line, lo, hi, a);
+  return i < hi && T.hit_line[i] < b;
+}
+
+// nearest hit distance of regex r to x within [a,b), x excluded; -1 if none
+LP_HD int32_t nearest_hit(const ScoreTables& T, int r, int32_t x, int32_t a, int32_t b) {
+  if (r < 0 || a >= b) return -1;
+  const int64_t lo = T.hit_off[r], hi = T.hit_off[r + 1];
+  int64_t i = lower_bound32(T.hit_line, lo, hi, x);
+  int32_t best = -1;
+  int64_t j = i;
+  if (j < hi && T.hit_line[j] == x) ++j;
+  if (j < hi && T.hit_line[j] < b) best = T.hit_line[j] - x;
+  if (i - 1 >= lo) {
+    const int32_t y = T.hit_line[i - 1];
+    if (y >= a && (best < 0 || x - y < best)) best = x - y;
+  }
+  return best;
+}
+
+// largest hit of regex r in [a, c); -1 if none
+LP_HD int32_t pred_hit(const ScoreTables& T, int r, int32_t a, int32_t c) {
+  if (r < 0 || a >= c) return -1;
+  const int64_t lo = T.hit_off[r], hi = T.hit_off[r + 1];
+  const int64_t i = lower_bound32(T.hit_line, lo, hi, c);
+  if (i - 1 >= lo && T.hit_line[i - 1] >= a) return T.hit_line[i - 1];
+  return -1;
+}
+
+LP_HD double score_event(const ScoreTables& T, const ScoreParams& S, int32_t x, int32_t p, int32_t s,
+                         int64_t freq_before, double* factors /* optional [7] */) {
+  const int32_t lo = T.seg_lo[s], hi = T.seg_hi[s], own_lo = T.seg_own_lo[s];
+  const int64_t gi = T.seg_g0[s] + (x - lo);
+  const double conf = T.conf[p];
+  const double sev = T.sev[p];
+  const double chrono = chrono_factor(gi, T.seg_n[s], S);
+  // proximity (ScoringService.java:161-190,315-347)
+  double prox = 1.0;
+  {
+    const int32_t a0 = T.sec_off[p], a1 = T.sec_off[p + 1];
+    if (a1 > a0) {
+      double tot = 0.0;
+      for (int32_t k = a0; k < a1; ++k) {
+        const int32_t w = T.sec_w[k];
+        const int64_t aa = (int64_t)x - w, bb = (int64_t)x + w + 1;
+        const int32_t a = (int32_t)(aa < lo ? lo : aa), b = (int32_t)(bb > hi ? hi : bb);
+        const int32_t d = nearest_hit(T, T.sec_reg[k], x, a, b);
+        if (d >= 0) tot += T.sec_weight[k] * exp(-(double)d / S.decay);
+      }
+      prox = 1.0 + tot;
+    }
+  }
+  // temporal (ScoringService.java:199-305)
+  double temp = 1.0;
+  {
+    const int32_t q0 = T.seq_off[p], q1 = T.seq_off[p + 1];
+    if (q1 > q0) {
+      double tot = 0.0;
+      for (int32_t q = q0; q < q1; ++q) {
+        const int32_t e0 = T.seq_ev_off[q], e1 = T.seq_ev_off[q + 1];
+        const int n = e1 - e0;
+        if (n <= 0) continue;
+        const int32_t a = x - 5 < lo ? lo : x - 5, b = x + 6 > hi ? hi : x + 6;
+        if (!any_hit(T, T.seq_ev_reg[e1 - 1], a, b)) continue;
+        bool ok = true;
+        int32_t cur = x;
+        for (int k = n - 2; k >= 0; --k) {
+          const int32_t f = pred_hit(T, T.seq_ev_reg[e0 + k], own_lo, cur);
+          if (f < 0) { ok = T.seq_carry[e0 + k] != 0; break; }
+          cur = f;
+        }
+        if (ok) tot += T.seq_bonus[q];
+      }
+      temp = 1.0 + tot;
+    }
+  }
+  // context (ContextAnalysisService.java:46-117)
+  double ctx;
+  {
+    int32_t a = x, b = x + 1;
+    const int32_t before = T.ctx_before[p], after = T.ctx_after[p];
+    if (before >= 0) {
+      a = x - before < lo ? lo : x - before;
+      b = x + 1 + after > hi ? hi : x + 1 + after;
+    }
+    double sc = 0.0;
+    int err = 0, stack = 0;
+    for (int32_t j = a; j < b; ++j) {
+      const uint8_t f = T.feat[j];
+      if (f & 1) { ++err; sc += 0.4; }
+      else if (f & 2) { sc += 0.2; }
+      if (f & 4) { ++stack; sc += 0.1; }
+      if (f & 8) { sc += 0.3; }
+    }
+    if (stack > 0) { const double sb = stack * 0.1; sc += sb < 0.5 ? sb : 0.5; }
+    const int total = b - a;
+    if (total > 10 && (double)(stack + err) > total * 0.7) sc *= 0.8;
+    ctx = 1.0 + sc;
+    if (ctx > S.max_ctx) ctx = S.max_ctx;
+  }
+  // frequency penalty (FrequencyTrackingService.java:64-93), penalty before record
+  double pen = 0.0;
+  if (freq_before >= 0) {
+    const double rate = (double)freq_before / S.fwin;
+    if (rate > S.fthr) { const double v = (rate - S.fthr) / S.fthr; pen = v < S.fmaxp ? v : S.fmaxp; }
+  }
+  if (factors) {
+    factors[0] = conf; factors[1] = sev; factors[2] = chrono; factors[3] = prox;
+    factors[4] = temp; factors[5] = ctx; factors[6] = pen;
+  }
+  return conf * sev * chrono * prox * temp * ctx * (1.0 - pen);
+}
+
+}  // namespace lp

@@ -1,0 +1,341 @@
+// gfx950 (MI355X) kernels of the log-analysis pipeline + their host (CPU backend) twins.
+//
+// Hot loops of the reference and the kernel that replaces each:
+//   K1 line split     AnalysisService.java:53              -> k_nl_count / k_nl_write
+//   K3 primary match  AnalysisService.java:89-95           -> k_prefilter (literal bloom in LDS)
+//                                                             + k_verify (byte DFA)
+//   K4/K5 aux match   ScoringService.java:272-347          -> same engine, all aux regexes
+//   K6 context feats  ContextAnalysisService.java:27-83    -> 4 internal regexes, same engine
+//   K7-K9 scoring     ScoringService.java:63-151           -> k_score (fp64, one thread / event)
+// Wave64 throughout; block sizes are multiples of 64; persistent grid-stride grids sized to the
+// 256 CUs so the LDS-resident bloom filter is loaded once per block, not once per tile.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lp_api.h"
+#include "lp_core.h"
+
+namespace lp {
+
+#define LP_CHECK(x)                                                                           \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------------------------------------
+// K1: newline index.  16 KiB tile per 256-thread block, 64 B per thread (4 x dwordx4 loads).
+constexpr int NL_THREADS = 256;
+constexpr int NL_BYTES_PER_THREAD = 64;
+constexpr int NL_TILE = NL_THREADS * NL_BYTES_PER_THREAD;
+
+__device__ __forceinline__ uint32_t zero_byte_mask(uint32_t t) {
+  // exact: high bit set in every byte of t that is 0x00
+  uint32_t y = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(y | t | 0x7F7F7F7Fu);
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int t = __shfl_up(v, d, 64);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(NL_THREADS) void k_nl_count(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                         int32_t* __restrict__ blk_cnt) {
+  const int64_t base = (int64_t)blockIdx.x * NL_TILE + (int64_t)threadIdx.x * NL_BYTES_PER_THREAD;
+  int c = 0;
+  if (base < nbytes) {
+    const uint4* p = reinterpret_cast<const uint4*>(text + base);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint4 v = p[k];
+      c += __popc(zero_byte_mask(v.x ^ 0x0A0A0A0Au)) + __popc(zero_byte_mask(v.y ^ 0x0A0A0A0Au)) +
+           __popc(zero_byte_mask(v.z ^ 0x0A0A0A0Au)) + __popc(zero_byte_mask(v.w ^ 0x0A0A0A0Au));
+    }
+  }
+  // block reduce
+  __shared__ int ws[NL_THREADS / 64];
+  int s = wave_incl_scan(c);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < NL_THREADS / 64; ++w) t += ws[w];
+    blk_cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                         const int64_t* __restrict__ blk_off,
+                                                         int64_t* __restrict__ nl_pos) {
+  const int64_t base = (int64_t)blockIdx.x * NL_TILE + (int64_t)threadIdx.x * NL_BYTES_PER_THREAD;
+  uint32_t m[16];
+  int c = 0;
+  if (base < nbytes) {
+    const uint4* p = reinterpret_cast<const uint4*>(text + base);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint4 v = p[k];
+      m[4 * k + 0] = zero_byte_mask(v.x ^ 0x0A0A0A0Au);
+      m[4 * k + 1] = zero_byte_mask(v.y ^ 0x0A0A0A0Au);
+      m[4 * k + 2] = zero_byte_mask(v.z ^ 0x0A0A0A0Au);
+      m[4 * k + 3] = zero_byte_mask(v.w ^ 0x0A0A0A0Au);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c += __popc(m[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = 0;
+  }
+  __shared__ int ws[NL_THREADS / 64];
+  int incl = wave_incl_scan(c);
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) ws[wid] = incl;
+  __syncthreads();
+  int woff = 0;
+  for (int w = 0; w < wid; ++w) woff += ws[w];
+  int64_t o = blk_off[blockIdx.x] + woff + incl - c;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint32_t mm = m[k];
+    while (mm) {
+      int b = __ffs(mm) - 1;          // bit 7, 15, 23 or 31
+      nl_pos[o++] = base + 4 * k + (b >> 3);
+      mm &= mm - 1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3a: literal prefilter.  Bloom filter (2 hashes) of every literal's leading 2/3/4-gram lives
+// in LDS; each lane scans 16 consecutive positions from one dwordx4 (+1 dword look-ahead),
+// ASCII-lower-cased with SWAR, grams extracted with v_alignbyte. Bloom hits (rare) probe the
+// global hash table and verify the whole literal; survivors append (regex, line) candidates.
+constexpr int PF_THREADS = 512;
+
+struct Appender {
+  int64_t* out;
+  int64_t cap;
+  unsigned long long* count;
+  __device__ void operator()(int64_t v) const {
+    unsigned long long i = atomicAdd(count, 1ull);
+    if ((int64_t)i < cap) out[i] = v;
+  }
+};
+
+template <int G>
+__device__ __forceinline__ void pf_try(const uint32_t* bl, const PfTables& T, const uint8_t* text, int64_t nbytes,
+                                       int64_t p, uint32_t g4, const int64_t* line_start, int64_t nlines,
+                                       const Appender& app) {
+  const uint32_t key = g4 & gram_mask(G);
+  const uint32_t h1 = bloom_h1(key, G, T.bloom_bits), h2 = bloom_h2(key, G, T.bloom_bits);
+  if (((bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u) == 0) return;
+  pf_probe(T, text, nbytes, p, key, G, line_start, nlines, app);
+}
+
+__global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                          PfTables T, const int64_t* __restrict__ line_start,
+                                                          int64_t nlines, int64_t* cand, int64_t cap,
+                                                          unsigned long long* count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t bl[];
+  const int nwords = (1 << T.bloom_bits) >> 5;
+  for (int i = threadIdx.x * 4; i < nwords; i += blockDim.x * 4)
+    *reinterpret_cast<uint4*>(bl + i) = *reinterpret_cast<const uint4*>(T.bloom + i);
+  __syncthreads();
+  const Appender app{cand, cap, count};
+  const int64_t nunits = (nbytes + 15) >> 4;
+  const bool g2 = T.gmask & 4, g3 = T.gmask & 8, g4on = T.gmask & 16;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p0 = u << 4;
+    const uint4 v = *reinterpret_cast<const uint4*>(text + p0);
+    const uint32_t nx = *reinterpret_cast<const uint32_t*>(text + p0 + 16);
+    const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int64_t p = p0 + k;
+      const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
+      if (p < nbytes) {
+        if (g4on) pf_try<4>(bl, T, text, nbytes, p, gram, line_start, nlines, app);
+        if (g3) pf_try<3>(bl, T, text, nbytes, p, gram, line_start, nlines, app);
+        if (g2) pf_try<2>(bl, T, text, nbytes, p, gram, line_start, nlines, app);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K3b: verify candidates (one lane per (regex, line) candidate, byte DFA)
+__global__ __launch_bounds__(256) void k_verify(const int64_t* __restrict__ cand, int64_t n,
+                                                const uint8_t* __restrict__ text,
+                                                const int64_t* __restrict__ line_start,
+                                                const int32_t* __restrict__ line_len, DfaPool P,
+                                                uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t k = cand[i];
+  const int r = (int)(k >> 32);
+  const int64_t line = k & 0xFFFFFFFFll;
+  out[i] = dfa_run(P, r, text + line_start[line], line_len[line]) ? 1 : 0;
+}
+
+// K3c: regexes without a usable literal: every line x every scan regex
+__global__ __launch_bounds__(256) void k_scan(const uint8_t* __restrict__ text,
+                                              const int64_t* __restrict__ line_start,
+                                              const int32_t* __restrict__ line_len, int64_t nlines,
+                                              const int32_t* __restrict__ regs, int nregs, DfaPool P,
+                                              int64_t* out, int64_t cap, unsigned long long* count) {
+  const int64_t line = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (line >= nlines) return;
+  const uint8_t* s = text + line_start[line];
+  const int n = line_len[line];
+  const Appender app{out, cap, count};
+  for (int j = 0; j < nregs; ++j) {
+    const int r = regs[j];
+    if (dfa_run(P, r, s, n)) app(((int64_t)r << 32) | line);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K7-K9: fused score epilogue, one lane per event
+__global__ __launch_bounds__(256) void k_score(const int32_t* __restrict__ ev_line, const int32_t* __restrict__ ev_pat,
+                                               const int32_t* __restrict__ ev_seg, const int64_t* __restrict__ ev_freq,
+                                               int64_t n, ScoreTables T, ScoreParams S, double* __restrict__ out,
+                                               double* __restrict__ factors) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
+}
+
+// ==========================================================================================
+// launchers (device) and host twins
+static int num_blocks(int64_t n, int t) { return (int)std::max<int64_t>(1, (n + t - 1) / t); }
+
+int64_t nl_tiles(int64_t nbytes) { return (nbytes + NL_TILE - 1) / NL_TILE; }
+
+void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream) {
+  int64_t nb = nl_tiles(nbytes);
+  if (nb == 0) return;
+  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_THREADS), 0, as_stream(stream), text, nbytes, blk_cnt);
+  LP_CHECK(hipGetLastError());
+}
+
+void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, uint64_t stream) {
+  int64_t nb = nl_tiles(nbytes);
+  if (nb == 0) return;
+  hipLaunchKernelGGL(k_nl_write, dim3((unsigned)nb), dim3(NL_THREADS), 0, as_stream(stream), text, nbytes, blk_off, nl_pos);
+  LP_CHECK(hipGetLastError());
+}
+
+void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
+                   int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream) {
+  if (nbytes <= 0) return;
+  const size_t lds = (size_t(1) << T.bloom_bits) / 8;
+  int64_t units = (nbytes + 15) / 16;
+  int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS));
+  hipLaunchKernelGGL(k_prefilter, dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, line_start,
+                     nlines, cand, cap, count);
+  LP_CHECK(hipGetLastError());
+}
+
+void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+                const DfaPool& P, uint8_t* out, uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_verify, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), cand, n, text, line_start,
+                     line_len, P, out);
+  LP_CHECK(hipGetLastError());
+}
+
+void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+              const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
+              uint64_t stream) {
+  if (nlines <= 0 || nregs <= 0) return;
+  hipLaunchKernelGGL(k_scan, dim3(num_blocks(nlines, 256)), dim3(256), 0, as_stream(stream), text, line_start,
+                     line_len, nlines, regs, nregs, P, out, cap, count);
+  LP_CHECK(hipGetLastError());
+}
+
+void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+               const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_score, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ev_line, ev_pat, ev_seg,
+                     ev_freq, n, T, S, out, factors);
+  LP_CHECK(hipGetLastError());
+}
+
+// ---------------- host twins (CPU backend) ----------------
+int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos) {
+  int64_t c = 0;
+  const uint8_t* p = text;
+  const uint8_t* e = text + nbytes;
+  while (p < e) {
+    const void* q = memchr(p, '\n', e - p);
+    if (!q) break;
+    const uint8_t* qq = static_cast<const uint8_t*>(q);
+    if (nl_pos) nl_pos[c] = qq - text;
+    ++c;
+    p = qq + 1;
+  }
+  return c;
+}
+
+int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
+                       int64_t nlines, int64_t* cand, int64_t cap) {
+  int64_t count = 0;
+  auto app = [&](int64_t v) { if (count < cap) cand[count] = v; ++count; };
+  const uint32_t* bl = T.bloom;
+  for (int64_t p = 0; p < nbytes; ++p) {
+    uint32_t g4 = 0;
+    for (int k = 3; k >= 0; --k) g4 = (g4 << 8) | (uint32_t)(p + k < nbytes ? lower_byte(text[p + k]) : 0);
+    for (int g = 4; g >= 2; --g) {
+      if (!(T.gmask & (1 << g))) continue;
+      const uint32_t key = g4 & gram_mask(g);
+      const uint32_t h1 = bloom_h1(key, g, T.bloom_bits), h2 = bloom_h2(key, g, T.bloom_bits);
+      if (((bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u) == 0) continue;
+      pf_probe(T, text, nbytes, p, key, g, line_start, nlines, app);
+    }
+  }
+  return count;
+}
+
+void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start,
+                 const int32_t* line_len, const DfaPool& P, uint8_t* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t k = cand[i];
+    const int r = (int)(k >> 32);
+    const int64_t line = k & 0xFFFFFFFFll;
+    out[i] = dfa_run(P, r, text + line_start[line], line_len[line]) ? 1 : 0;
+  }
+}
+
+int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+                  const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap) {
+  int64_t c = 0;
+  for (int64_t line = 0; line < nlines; ++line)
+    for (int j = 0; j < nregs; ++j)
+      if (dfa_run(P, regs[j], text + line_start[line], line_len[line])) {
+        if (c < cap) out[c] = ((int64_t)regs[j] << 32) | line;
+        ++c;
+      }
+  return c;
+}
+
+void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+                const ScoreTables& T, const ScoreParams& S, double* out, double* factors) {
+  for (int64_t i = 0; i < n; ++i)
+    out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
+}
+
+}  // namespace lp

@@ -1,0 +1,83 @@
+// java.util.regex (Java 21 defaults) -> byte-level automata for the MI355X log engine.
+//
+// Pipeline (host C++, run once per distinct regex at library load — the reference recompiles
+// every regex on every request, AnalysisService.java:55-86):
+//   parse (Java syntax subset) -> AST
+//   AST -> required-literal factor set (prefilter keys)
+//   AST -> Glushkov position NFA whose edges carry *boundary-context* conditions
+//          (^ $ \b \B \A \z \Z as zero-width assertions)
+//   NFA -> byte DFA (subset construction, previous-byte wordness folded into the state,
+//          absorbing DEAD=0 / ACCEPT=1 states, per-state accept flags for end-of-line).
+//
+// Only boolean find() is ever used by the reference (AnalysisService.java:95,
+// ScoringService.java:281,300,330), so language membership of ".*R.*" is all that matters and
+// an automaton is exact for the regular subset. Non-regular / language-changing constructs
+// (backrefs, lookaround, possessive, atomic groups) raise Unsupported -> host fallback.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace lp {
+
+struct SyntaxError : std::runtime_error { using std::runtime_error::runtime_error; };
+struct Unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
+
+// Boundary contexts: prev in {BOS=0, W=1, N=2} x next in {EOS=0, FT=1, W=2, N=3}
+// ctx index = prev*4 + next (12 contexts). FT = "before the final line terminator".
+enum : int { P_BOS = 0, P_W = 1, P_N = 2 };
+enum : int { N_EOS = 0, N_FT = 1, N_W = 2, N_N = 3 };
+constexpr uint16_t CTX_ALL = 0x0FFF;
+inline int ctx_index(int prev, int next) { return prev * 4 + next; }
+
+struct ByteSet {
+  uint64_t w[4] = {0, 0, 0, 0};
+  void set(int b) { w[b >> 6] |= 1ull << (b & 63); }
+  bool test(int b) const { return (w[b >> 6] >> (b & 63)) & 1; }
+  void set_range(int lo, int hi) { for (int b = lo; b <= hi; ++b) set(b); }
+  ByteSet operator|(const ByteSet& o) const { ByteSet r; for (int i = 0; i < 4; ++i) r.w[i] = w[i] | o.w[i]; return r; }
+  bool operator==(const ByteSet& o) const { return w[0]==o.w[0]&&w[1]==o.w[1]&&w[2]==o.w[2]&&w[3]==o.w[3]; }
+  bool empty() const { return !(w[0] | w[1] | w[2] | w[3]); }
+  int count() const { return __builtin_popcountll(w[0]) + __builtin_popcountll(w[1]) + __builtin_popcountll(w[2]) + __builtin_popcountll(w[3]); }
+};
+
+enum class Kind : int { DFA = 0, NFA = 1, FALLBACK = 2, INVALID = 3 };
+
+struct Edge { int to; uint16_t cond; };
+
+struct Nfa {
+  int npos = 0;
+  std::vector<ByteSet> cls;                 // per position byte class
+  std::vector<std::vector<Edge>> follow;    // per position
+  std::vector<Edge> first;                  // (pos, cond)
+  std::vector<Edge> last;                   // (pos, cond)
+  uint16_t nullable = 0;                    // contexts in which the empty string matches
+};
+
+struct Dfa {
+  int nstates = 0;                          // incl. DEAD(0) ACCEPT(1) INIT(2)
+  int nclasses = 0;
+  std::vector<uint8_t> bytemap;             // 256 -> class
+  std::vector<uint16_t> trans;              // nstates * nclasses
+  std::vector<uint8_t> accflags;            // per state: bit0 accept at EOS, bit1 accept before FT
+  bool anchored = false;                    // no restart after BOS -> DEAD reachable
+};
+
+struct Compiled {
+  Kind kind = Kind::INVALID;
+  std::string error;                        // reason for FALLBACK / INVALID
+  std::vector<std::string> literals;        // OR-set of required factors (ASCII-lowercased bytes)
+  bool has_literals = false;
+  Nfa nfa;
+  Dfa dfa;
+};
+
+Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions);
+
+// Host-side exact match of one line with a compiled DFA (CPU backend + tests).
+bool dfa_find(const Dfa& d, const uint8_t* s, int64_t n);
+// Length in bytes of a final line terminator (\r, U+0085, U+2028, U+2029) ending s[0..n), or 0.
+int final_terminator_len(const uint8_t* s, int64_t n);
+
+}  // namespace lp

@@ -1,0 +1,333 @@
+"""Pattern library -> immutable device tables (compiled once at load, never per request).
+
+The reference recompiles every primary / secondary / sequence regex on every request and
+stores the compiled object on shared singletons (``AnalysisService.java:55-86``; a data race
+noted in SURVEY §5.2). Here the whole library is compiled once into:
+
+* a **regex registry**: every distinct regex string (primary, secondary, sequence event, plus
+  the 4 built-in context regexes of ``ContextAnalysisService.java:27-34`` at ids 0..3) gets one
+  id; its hits are computed once per request and shared by every pattern that references it;
+* a **DFA pool** (byte DFAs of all regexes, concatenated) for the verify/scan kernels;
+* **prefilter tables**: required literal factors of each regex, their leading 2/3/4-grams in a
+  2-hash bloom filter (LDS-resident in the kernel) and an open-addressed hash table;
+* **pattern tables** for the fused score kernel (confidence, severity multiplier, context rules,
+  secondary / sequence descriptors, frequency key).
+
+Regexes the automaton engine cannot express (backrefs, lookaround, possessive/atomic groups,
+DFA blow-up) are matched by the host fallback (``regex/javacompat.py``); syntactically invalid
+regexes never match and are reported at load (the reference would fail every request with a
+``PatternSyntaxException`` -> HTTP 500).
+"""
+from __future__ import annotations
+
+import logging
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..golden import CONTEXT_REGEXES, SEVERITY_MULTIPLIERS, severity_key
+from ..native import N
+from ..utils.config import ScoringParams
+from .schema import Pattern, PatternSet, pattern_to_json
+
+log = logging.getLogger("log_parser_amd.compiled")
+
+KIND_DFA, KIND_NFA, KIND_FALLBACK, KIND_INVALID = 0, 1, 2, 3
+BLOOM_BITS = 18
+
+
+def _minimize_literals(lits: List[bytes]) -> List[bytes]:
+    """Drop literals that contain another literal of the same OR-set (redundant for a filter)."""
+    s = sorted(set(lits), key=len)
+    out: List[bytes] = []
+    for x in s:
+        if not any(y in x for y in out):
+            out.append(x)
+    return out
+
+
+def _gram(lit: bytes) -> Tuple[int, int]:
+    g = min(4, len(lit))
+    key = int.from_bytes(lit[:g], "little")
+    return key, g
+
+
+def _u32(x):
+    return x & 0xFFFFFFFF
+
+
+def bloom_h1(key, g, bits):
+    return _u32((key ^ _u32(g * 0x9E3779B9)) * 0x85EBCA6B) >> (32 - bits)
+
+
+def bloom_h2(key, g, bits):
+    return _u32((key + _u32(g * 0x27D4EB2F)) * 0xC2B2AE35) >> (32 - bits)
+
+
+def ht_hash(key, g):
+    h = _u32(key * 0x9E3779B1) ^ _u32(g * 0x7FEB352D)
+    h ^= h >> 15
+    h = _u32(h * 0x2C1B3C6D)
+    h ^= h >> 12
+    return h
+
+
+@dataclass
+class RegexInfo:
+    pattern: str
+    kind: int
+    error: str = ""
+    literals: List[bytes] = field(default_factory=list)
+    nstates: int = 0
+    roles: set = field(default_factory=set)
+
+
+class CompiledLibrary:
+    def __init__(self, pattern_sets: List[PatternSet], params: ScoringParams, max_dfa_states: int = 2048):
+        self.pattern_sets = pattern_sets
+        self.params = params
+        self.max_dfa_states = max_dfa_states
+        self.patterns: List[Pattern] = []
+        self.pattern_set_index: List[int] = []
+        for si, ps in enumerate(pattern_sets):
+            for p in (ps.patterns or []):
+                if p.primary_pattern is None or p.primary_pattern.regex is None:
+                    log.error("pattern %r has no primary regex; skipped", p.id)
+                    continue
+                self.patterns.append(p)
+                self.pattern_set_index.append(si)
+        self.library_ids = [(ps.metadata.library_id if ps.metadata else None) for ps in pattern_sets]
+        self._reg_ids: Dict[str, int] = {}
+        self.regexes: List[RegexInfo] = []
+        for rx in CONTEXT_REGEXES:
+            self._reg(rx, "context")
+        self._build_pattern_tables()
+        self._compile_regexes()
+        self._build_prefilter()
+        self.pattern_json = [_json_bytes(pattern_to_json(p)) for p in self.patterns]
+        self._device_cache: Dict[str, dict] = {}
+
+    # ------------------------------------------------------------------ registry
+    def _reg(self, rx: Optional[str], role: str) -> int:
+        if rx is None:
+            return -1
+        i = self._reg_ids.get(rx)
+        if i is None:
+            i = len(self.regexes)
+            self._reg_ids[rx] = i
+            self.regexes.append(RegexInfo(pattern=rx, kind=-1))
+        self.regexes[i].roles.add(role)
+        return i
+
+    def _build_pattern_tables(self):
+        P = len(self.patterns)
+        p = self.params
+        self.conf = np.zeros(P, np.float64)
+        self.sev = np.zeros(P, np.float64)
+        self.severity = []
+        self.ctx_before = np.full(P, -1, np.int32)
+        self.ctx_after = np.full(P, -1, np.int32)
+        sec_off, sec_reg, sec_w, sec_weight = [0], [], [], []
+        seq_off, seq_bonus, seq_ev_off, seq_ev_reg = [0], [], [0], []
+        self.primary_reg = np.zeros(P, np.int32)
+        self.freq_key = np.full(P, -1, np.int32)
+        self.freq_ids: List[str] = []
+        fid: Dict[str, int] = {}
+        halo = 5
+        for i, pat in enumerate(self.patterns):
+            self.conf[i] = float(pat.primary_pattern.confidence)
+            sk = severity_key(pat.severity)
+            self.severity.append(sk)
+            self.sev[i] = SEVERITY_MULTIPLIERS.get(sk, 1.0)
+            ce = pat.context_extraction
+            if ce is not None:
+                self.ctx_before[i] = max(0, int(ce.lines_before))
+                self.ctx_after[i] = max(0, int(ce.lines_after))
+                halo = max(halo, self.ctx_before[i], self.ctx_after[i])
+            self.primary_reg[i] = self._reg(pat.primary_pattern.regex, "primary")
+            for s in (pat.secondary_patterns or []):
+                sec_reg.append(self._reg(s.regex, "secondary"))
+                w = min(p.max_window, int(s.proximity_window))
+                sec_w.append(w)
+                sec_weight.append(float(s.weight))
+                halo = max(halo, w)
+            sec_off.append(len(sec_reg))
+            for q in (pat.sequence_patterns or []):
+                seq_bonus.append(float(q.bonus_multiplier))
+                for ev in (q.events or []):
+                    seq_ev_reg.append(self._reg(ev.regex, "sequence"))
+                seq_ev_off.append(len(seq_ev_reg))
+            seq_off.append(len(seq_bonus))
+            if pat.id is not None and pat.id.strip() != "":
+                if pat.id not in fid:
+                    fid[pat.id] = len(self.freq_ids)
+                    self.freq_ids.append(pat.id)
+                self.freq_key[i] = fid[pat.id]
+        self.sec_off = np.array(sec_off, np.int32)
+        self.sec_reg = np.array(sec_reg or [0], np.int32)
+        self.sec_w = np.array(sec_w or [0], np.int32)
+        self.sec_weight = np.array(sec_weight or [0.0], np.float64)
+        self.seq_off = np.array(seq_off, np.int32)
+        self.seq_bonus = np.array(seq_bonus or [0.0], np.float64)
+        self.seq_ev_off = np.array(seq_ev_off, np.int32)
+        self.seq_ev_reg = np.array(seq_ev_reg or [0], np.int32)
+        self.n_seq_events = len(seq_ev_reg)
+        self.halo = int(halo)
+        # primary regex -> patterns (ascending pattern index = reference event order)
+        R = len(self.regexes)
+        cnt = np.zeros(R, np.int64)
+        for r in self.primary_reg:
+            cnt[r] += 1
+        self.prim_off = np.zeros(R + 1, np.int64)
+        np.cumsum(cnt, out=self.prim_off[1:])
+        self.prim_pats = np.argsort(self.primary_reg, kind="stable").astype(np.int32)
+
+    def _compile_regexes(self):
+        meta, bytemaps, trans, accs = [], [], [], []
+        toff = aoff = 0
+        self.scan_regs: List[int] = []
+        self.host_regs: List[int] = []
+        for i, ri in enumerate(self.regexes):
+            d = N.compile_regex(ri.pattern, self.max_dfa_states, 4096)
+            ri.kind = d["kind"]
+            ri.error = d["error"]
+            if ri.kind == KIND_DFA:
+                ri.nstates = d["nstates"]
+                nc = d["nclasses"]
+                meta.append([toff, nc, aoff, 1 if d["anchored"] else 0])
+                bytemaps.append(np.frombuffer(d["bytemap"], np.uint8))
+                t = np.frombuffer(d["trans"], np.uint16)
+                trans.append(t)
+                a = np.frombuffer(d["acc"], np.uint8)
+                accs.append(a)
+                toff += t.size
+                aoff += a.size
+                lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
+                # anchored regexes (e.g. '^\\s*at\\s+...') die within a few bytes of every line:
+                # scanning all lines beats a short, unselective literal.
+                if d["anchored"] and lits and min(len(x) for x in lits) < 4:
+                    lits = []
+                ri.literals = lits
+                if not lits:
+                    self.scan_regs.append(i)
+            else:
+                meta.append([0, 1, 0, 0])
+                bytemaps.append(np.zeros(256, np.uint8))
+                if ri.kind == KIND_INVALID:
+                    log.error("invalid regex %r: %s (never matches)", ri.pattern, ri.error)
+                else:
+                    log.warning("regex %r uses the host fallback (%s)", ri.pattern, ri.error)
+                    self.host_regs.append(i)
+        # a dummy DFA for non-DFA regexes: state 2 -> DEAD on every byte (never read: not scanned)
+        if not trans:
+            trans.append(np.zeros(1, np.uint16))
+            accs.append(np.zeros(1, np.uint8))
+        self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
+        self.dfa_bytemap = np.concatenate(bytemaps)
+        self.dfa_trans = np.concatenate(trans)
+        self.dfa_acc = np.concatenate(accs)
+
+    def _build_prefilter(self):
+        lit_ids: Dict[bytes, int] = {}
+        lit_regs: List[List[int]] = []
+        for i, ri in enumerate(self.regexes):
+            for lit in ri.literals:
+                j = lit_ids.get(lit)
+                if j is None:
+                    j = len(lit_regs)
+                    lit_ids[lit] = j
+                    lit_regs.append([])
+                lit_regs[j].append(i)
+        lits = [None] * len(lit_ids)
+        for k, v in lit_ids.items():
+            lits[v] = k
+        self.literals = lits
+        lit_off = np.zeros(len(lits) + 1, np.int32)
+        for i, l in enumerate(lits):
+            lit_off[i + 1] = lit_off[i] + len(l)
+        lit_bytes = np.frombuffer(b"".join(lits) or b"\0", np.uint8).copy()
+        lit_reg_off = np.zeros(len(lits) + 1, np.int32)
+        for i, rr in enumerate(lit_regs):
+            lit_reg_off[i + 1] = lit_reg_off[i] + len(rr)
+        lit_reg = np.array([r for rr in lit_regs for r in rr] or [0], np.int32)
+        grams: Dict[Tuple[int, int], List[int]] = {}
+        gmask = 0
+        for i, l in enumerate(lits):
+            key, g = _gram(l)
+            grams.setdefault((key, g), []).append(i)
+            gmask |= 1 << g
+        bits = BLOOM_BITS
+        bloom = np.zeros((1 << bits) // 32, np.uint32)
+        H = 16
+        while H < 2 * max(1, len(grams)):
+            H *= 2
+        ht_key = np.full(H, np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64)
+        ht_val = np.zeros(H, np.int32)
+        ht_cnt = np.zeros(H, np.int32)
+        gram_lits: List[int] = []
+        for (key, g), ids in grams.items():
+            for h in (bloom_h1(key, g, bits), bloom_h2(key, g, bits)):
+                bloom[h >> 5] |= np.uint32(1 << (h & 31))
+            h = ht_hash(key, g) & (H - 1)
+            while ht_key[h] != np.uint64(0xFFFFFFFFFFFFFFFF):
+                h = (h + 1) & (H - 1)
+            ht_key[h] = np.uint64(key | (g << 32))
+            ht_val[h] = len(gram_lits)
+            ht_cnt[h] = len(ids)
+            gram_lits.extend(ids)
+        self.pf = dict(bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
+                       gram_lits=np.array(gram_lits or [0], np.int32), lit_off=lit_off, lit_bytes=lit_bytes,
+                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask)
+
+    # ------------------------------------------------------------------ device tables
+    def device_tables(self, device: torch.device) -> dict:
+        key = str(device)
+        t = self._device_cache.get(key)
+        if t is not None:
+            return t
+
+        def T(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+
+        t = {}
+        pf = self.pf
+        t["pf_arrays"] = [T(pf["bloom"]), T(pf["ht_key"].view(np.int64)), T(pf["ht_val"]), T(pf["ht_cnt"]),
+                          T(pf["gram_lits"]), T(pf["lit_off"]), T(pf["lit_bytes"]), T(pf["lit_reg_off"]),
+                          T(pf["lit_reg"])]
+        a = t["pf_arrays"]
+        t["pf"] = (a[0].data_ptr(), pf["bits"], a[1].data_ptr(), a[2].data_ptr(), a[3].data_ptr(), pf["ht_mask"],
+                   a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"])
+        t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc)]
+        d = t["dfa_arrays"]
+        t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr())
+        t["scan_regs"] = T(np.array(self.scan_regs, np.int32))
+        t["conf"], t["sev"] = T(self.conf), T(self.sev)
+        t["ctx_before"], t["ctx_after"] = T(self.ctx_before), T(self.ctx_after)
+        t["sec_off"], t["sec_reg"], t["sec_w"], t["sec_weight"] = T(self.sec_off), T(self.sec_reg), T(self.sec_w), T(self.sec_weight)
+        t["seq_off"], t["seq_bonus"], t["seq_ev_off"], t["seq_ev_reg"] = T(self.seq_off), T(self.seq_bonus), T(self.seq_ev_off), T(self.seq_ev_reg)
+        t["prim_off"], t["prim_pats"] = T(self.prim_off), T(self.prim_pats)
+        t["prim_cnt"] = T(np.diff(self.prim_off))
+        t["freq_key"] = T(self.freq_key)
+        t["is_primary"] = T(np.diff(self.prim_off) > 0)
+        self._device_cache[key] = t
+        return t
+
+    @property
+    def n_regexes(self) -> int:
+        return len(self.regexes)
+
+    def summary(self) -> dict:
+        kinds = [r.kind for r in self.regexes]
+        return {
+            "patterns": len(self.patterns), "pattern_sets": len(self.pattern_sets), "regexes": len(self.regexes),
+            "dfa": kinds.count(KIND_DFA), "host_fallback": len(self.host_regs),
+            "invalid": kinds.count(KIND_INVALID), "scan_all": len(self.scan_regs), "literals": len(self.literals),
+            "halo": self.halo,
+        }
+
+
+def _json_bytes(obj) -> bytes:
+    import json
+    return json.dumps(obj, ensure_ascii=False, separators=(",", ":"), allow_nan=True).encode("utf-8")

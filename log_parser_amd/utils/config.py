@@ -1,0 +1,177 @@
+"""Dotted-key configuration system (MicroProfile-Config compatible key names).
+
+Reference parity: the reference reads 10 keys through ``@ConfigProperty`` with in-code
+defaults that mirror ``src/main/resources/application.properties:1-20``
+(``PatternService.java:35-36``, ``ScoringService.java:38-51``,
+``ContextAnalysisService.java:24``, ``FrequencyTrackingService.java:27-34``).
+
+Resolution order (highest wins), same as MicroProfile Config ordinals:
+  1. explicit overrides (``-Dkey=value`` on the CLI, or ``Config(overrides=...)``)
+  2. environment variables, MicroProfile mapping: ``scoring.proximity.max-window`` is also
+     looked up as ``SCORING_PROXIMITY_MAX_WINDOW`` (non-alphanumerics -> ``_``, upper-cased)
+  3. an ``application.properties`` file (``LP_CONFIG`` env var or ``config/application.properties``)
+  4. in-code defaults below.
+
+New keys live under ``engine.*`` (device / parallel / batching knobs) and ``server.*``.
+"""
+from __future__ import annotations
+
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Any, Dict, Mapping, Optional
+
+# key -> (default, type)
+REFERENCE_KEYS: Dict[str, tuple] = {
+    "pattern.directory": ("/shared/patterns", str),
+    "scoring.proximity.decay-constant": (10.0, float),
+    "scoring.proximity.max-window": (100, int),
+    "scoring.chronological.early-bonus-threshold": (0.2, float),
+    "scoring.chronological.max-early-bonus": (2.5, float),
+    "scoring.chronological.penalty-threshold": (0.5, float),
+    "scoring.context.max-context-factor": (2.5, float),
+    "scoring.frequency.threshold": (10.0, float),
+    "scoring.frequency.max-penalty": (0.8, float),
+    "scoring.frequency.time-window-hours": (1, int),
+}
+
+ENGINE_KEYS: Dict[str, tuple] = {
+    # "auto" -> cuda if available else cpu. "cuda" fails loudly without the HIP extension.
+    "engine.device": ("auto", str),
+    # bytes per streamed H2D chunk for long logs (double-buffered pinned staging)
+    "engine.chunk-bytes": (256 << 20, int),
+    # capacity hint for candidate (line, regex) pairs per chunk; grown on overflow
+    "engine.candidate-capacity": (1 << 22, int),
+    # max DFA states per regex before it is routed to the NFA (MFMA) path
+    "engine.dfa-max-states": (2048, int),
+    # continuous batching
+    "engine.batch.max-requests": (256, int),
+    "engine.batch.max-bytes": (64 << 20, int),
+    "engine.batch.max-wait-ms": (2.0, float),
+    # top-k events kept by the distributed reduction (0 = all events)
+    "engine.topk": (100, int),
+    # persist frequency state (snapshot path, empty = disabled, reference default)
+    "engine.frequency.snapshot-path": ("", str),
+    # max request body (reference: Quarkus default 10 MiB)
+    "server.max-body-bytes": (1 << 30, int),
+    "server.port": (8080, int),
+    "server.host": ("0.0.0.0", str),
+    # reference logs one INFO line per match (AnalysisService.java:96-99); we log it at DEBUG
+    "server.log-matches": (False, bool),
+}
+
+ALL_KEYS: Dict[str, tuple] = {**REFERENCE_KEYS, **ENGINE_KEYS}
+
+
+def env_name(key: str) -> str:
+    """MicroProfile Config env-var mapping: non-alphanumerics -> '_', upper-case."""
+    return re.sub(r"[^A-Za-z0-9]", "_", key).upper()
+
+
+def _coerce(value: Any, typ: type) -> Any:
+    if typ is bool:
+        if isinstance(value, bool):
+            return value
+        return str(value).strip().lower() in ("1", "true", "yes", "on")
+    if typ is int:
+        return int(float(value)) if isinstance(value, str) and "." in value else int(value)
+    return typ(value)
+
+
+def parse_properties(text: str) -> Dict[str, str]:
+    """Minimal java.util.Properties parser (key=value / key: value, # and ! comments)."""
+    out: Dict[str, str] = {}
+    for raw in text.splitlines():
+        line = raw.strip()
+        if not line or line[0] in "#!":
+            continue
+        m = re.match(r"([^=:\s]+)\s*[=:\s]\s*(.*)$", line)
+        if m:
+            out[m.group(1)] = m.group(2).strip()
+    return out
+
+
+@dataclass(frozen=True)
+class Config:
+    values: Mapping[str, Any] = field(default_factory=dict)
+
+    @staticmethod
+    def load(overrides: Optional[Mapping[str, Any]] = None,
+             properties_path: Optional[str] = None,
+             environ: Optional[Mapping[str, str]] = None) -> "Config":
+        environ = os.environ if environ is None else environ
+        vals: Dict[str, Any] = {k: d for k, (d, _) in ALL_KEYS.items()}
+        path = properties_path or environ.get("LP_CONFIG") or os.path.join("config", "application.properties")
+        if path and os.path.isfile(path):
+            with open(path, "r", encoding="utf-8") as f:
+                for k, v in parse_properties(f.read()).items():
+                    vals[k] = v
+        for k in ALL_KEYS:
+            e = env_name(k)
+            if e in environ:
+                vals[k] = environ[e]
+        if overrides:
+            for k, v in overrides.items():
+                vals[k] = v
+        typed = {}
+        for k, v in vals.items():
+            typ = ALL_KEYS[k][1] if k in ALL_KEYS else str
+            typed[k] = _coerce(v, typ)
+        return Config(values=typed)
+
+    def __getitem__(self, key: str) -> Any:
+        return self.values[key]
+
+    def get(self, key: str, default: Any = None) -> Any:
+        return self.values.get(key, default)
+
+    def with_overrides(self, **kv: Any) -> "Config":
+        d = dict(self.values)
+        for k, v in kv.items():
+            d[k.replace("__", ".").replace("_", "-")] = v
+        return Config(values=d)
+
+    def replace(self, mapping: Mapping[str, Any]) -> "Config":
+        d = dict(self.values)
+        for k, v in mapping.items():
+            typ = ALL_KEYS[k][1] if k in ALL_KEYS else type(v)
+            d[k] = _coerce(v, typ)
+        return Config(values=d)
+
+    # ---- typed views used by the scoring code -------------------------------------------
+    @property
+    def scoring(self) -> "ScoringParams":
+        return ScoringParams(
+            decay_constant=float(self["scoring.proximity.decay-constant"]),
+            max_window=int(self["scoring.proximity.max-window"]),
+            early_bonus_threshold=float(self["scoring.chronological.early-bonus-threshold"]),
+            max_early_bonus=float(self["scoring.chronological.max-early-bonus"]),
+            penalty_threshold=float(self["scoring.chronological.penalty-threshold"]),
+            max_context_factor=float(self["scoring.context.max-context-factor"]),
+            freq_threshold=float(self["scoring.frequency.threshold"]),
+            freq_max_penalty=float(self["scoring.frequency.max-penalty"]),
+            freq_window_hours=int(self["scoring.frequency.time-window-hours"]),
+        )
+
+
+@dataclass(frozen=True)
+class ScoringParams:
+    decay_constant: float = 10.0
+    max_window: int = 100
+    early_bonus_threshold: float = 0.2
+    max_early_bonus: float = 2.5
+    penalty_threshold: float = 0.5
+    max_context_factor: float = 2.5
+    freq_threshold: float = 10.0
+    freq_max_penalty: float = 0.8
+    freq_window_hours: int = 1
+
+
+def parse_cli_overrides(argv) -> Dict[str, str]:
+    """Collect ``-Dkey=value`` arguments (Quarkus/MicroProfile style)."""
+    out = {}
+    for a in argv:
+        if a.startswith("-D") and "=" in a:
+            k, v = a[2:].split("=", 1)
+            out[k] = v
+    return out

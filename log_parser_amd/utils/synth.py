@@ -1,0 +1,135 @@
+"""Synthetic pod logs and randomly generated pattern libraries (BASELINE.json configs).
+
+There is no network and the reference ships no fixtures, so tests and the bench
+use generated data of the configured shape: ``n_patterns`` patterns (with secondary and
+sequence patterns and context rules) and logs of ``n_lines`` realistic-looking lines into which
+pattern triggers are planted at a controlled rate.
+"""
+from __future__ import annotations
+
+import random
+from typing import List, Optional, Tuple
+
+from ..models.schema import PatternSet
+
+LEVELS = ["INFO", "DEBUG", "WARN", "ERROR", "TRACE", "INFO", "INFO", "DEBUG"]
+COMPONENTS = ["kubelet", "controller", "scheduler", "api-server", "etcd", "ingress", "app", "worker", "db-pool",
+              "cache", "auth", "gateway"]
+WORDS = ["request", "handled", "user", "session", "started", "completed", "processing", "batch", "queue", "item",
+         "connection", "pool", "cache", "hit", "miss", "retry", "timeout", "latency", "bytes", "sent", "received",
+         "config", "reload", "metrics", "flush", "checkpoint", "shard", "replica", "leader", "follower", "sync",
+         "node", "pod", "container", "image", "pulled", "volume", "mounted", "probe", "ready", "healthy"]
+SEVERITIES = ["CRITICAL", "HIGH", "MEDIUM", "LOW", "INFO"]
+EXC = ["java.lang.NullPointerException", "java.io.IOException", "java.lang.IllegalStateException",
+       "java.util.concurrent.TimeoutException", "java.lang.OutOfMemoryError"]
+
+
+def _token(rng: random.Random, i: int) -> str:
+    syl = ["ka", "ze", "tor", "vin", "qua", "mel", "dro", "pix", "lun", "sar", "bex", "fyr", "gol", "hup"]
+    return "".join(rng.choice(syl) for _ in range(3)).capitalize() + str(i)
+
+
+def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate: float = 0.7,
+                 sequence_rate: float = 0.4, feature_mix: bool = True) -> Tuple[List[PatternSet], List[dict]]:
+    """Returns (pattern sets, trigger descriptions used by ``make_log`` to plant matches)."""
+    rng = random.Random(seed)
+    sets = [{"metadata": {"library_id": f"synthetic-lib-{s}", "version": "1.0"}, "patterns": []}
+            for s in range(n_sets)]
+    triggers = []
+    for i in range(n_patterns):
+        tok = _token(rng, i)
+        style = rng.randrange(8) if feature_mix else 0
+        if style == 0:
+            regex, sample = tok + "Failure", f"{tok}Failure detected"
+        elif style == 1:
+            regex, sample = rf"(?i)\b{tok}\s+(crashed|aborted)\b", f"{tok.upper()} crashed unexpectedly"
+        elif style == 2:
+            regex, sample = rf"{tok}: code=\d{{3,5}}", f"{tok}: code={rng.randint(100, 99999)}"
+        elif style == 3:
+            regex, sample = rf"(Fatal|Severe) {tok} (state|status)", f"Fatal {tok} status reached"
+        elif style == 4:
+            regex, sample = rf"{tok}[A-Z]+Exception", f"caught {tok}PANICException in handler"
+        elif style == 5:
+            regex, sample = rf"^\[{tok}\] .*rejected", f"[{tok}] request was rejected"
+        elif style == 6:
+            regex, sample = rf"{tok}\.(conn|sock)[0-9]+ (lost|closed)$", f"{tok}.conn{rng.randint(0, 99)} lost"
+        else:
+            regex, sample = rf"{tok}-[a-f0-9]{{4}} timed? ?out", f"{tok}-{rng.randrange(16**4):04x} timed out"
+        pat = {
+            "id": f"pat-{i:05d}" if rng.random() > 0.02 else f"pat-{i // 2:05d}",
+            "name": f"Synthetic failure {i}",
+            "severity": rng.choice(SEVERITIES) if rng.random() > 0.03 else "weird",
+            "primary_pattern": {"regex": regex, "confidence": round(rng.uniform(0.3, 0.95), 3)},
+            "remediation": {"description": f"fix {tok}", "common_causes": ["synthetic"]},
+        }
+        secs, seqs = [], []
+        if rng.random() < secondary_rate:
+            for k in range(rng.randint(1, 3)):
+                stok = f"{tok}Aux{k}"
+                secs.append({"regex": stok if k else rf"(?i){stok}\b", "weight": round(rng.uniform(0.1, 0.9), 2),
+                             "proximity_window": rng.choice([3, 5, 10, 20, 50, 200])})
+            pat["secondary_patterns"] = secs
+        if rng.random() < sequence_rate:
+            evs = [{"regex": f"{tok}Step{k}"} for k in range(rng.randint(1, 3))]
+            seqs.append({"description": f"{tok} lifecycle", "bonus_multiplier": round(rng.uniform(0.2, 1.5), 2),
+                         "events": evs})
+            pat["sequence_patterns"] = seqs
+        if rng.random() < 0.8:
+            pat["context_extraction"] = {"lines_before": rng.randint(0, 8), "lines_after": rng.randint(0, 6),
+                                         "include_stack_trace": rng.random() < 0.5}
+        sets[i % n_sets]["patterns"].append(pat)
+        triggers.append({"sample": sample, "secondary": [s["regex"].replace("(?i)", "").replace("\\b", "")
+                                                         for s in secs],
+                         "sequence": [e["regex"] for q in seqs for e in q["events"]]})
+    return [PatternSet.model_validate(s) for s in sets], triggers
+
+
+def _noise_line(rng: random.Random, i: int) -> str:
+    lvl = rng.choice(LEVELS)
+    comp = rng.choice(COMPONENTS)
+    msg = " ".join(rng.choice(WORDS) for _ in range(rng.randint(4, 12)))
+    return f"2025-09-19T12:{(i // 60) % 60:02d}:{i % 60:02d}.{i % 1000:03d}Z {lvl:5s} [{comp}] {msg} id={rng.randint(0, 1 << 30)}"
+
+
+def make_log(n_lines: int, triggers: List[dict], seed: int = 0, hit_rate: float = 0.01,
+             aux_rate: float = 0.01, stack_rate: float = 0.01, crlf_rate: float = 0.0) -> str:
+    rng = random.Random(seed)
+    out = []
+    i = 0
+    while i < n_lines:
+        r = rng.random()
+        if triggers and r < hit_rate:
+            t = rng.choice(triggers)
+            if t["sequence"] and rng.random() < 0.6:
+                for ev in t["sequence"][:-1]:
+                    out.append(f"INFO [app] {ev} reached")
+                    i += 1
+            out.append(_noise_line(rng, i)[:40] + " " + t["sample"])
+            if t["sequence"] and rng.random() < 0.6:
+                out.append(f"INFO [app] {t['sequence'][-1]} reached")
+                i += 1
+            if t["secondary"] and rng.random() < 0.7:
+                out.append(f"WARN [app] saw {rng.choice(t['secondary'])} nearby")
+                i += 1
+        elif triggers and r < hit_rate + aux_rate:
+            t = rng.choice(triggers)
+            if t["secondary"]:
+                out.append(f"DEBUG [app] {rng.choice(t['secondary'])} event")
+            else:
+                out.append(_noise_line(rng, i))
+        elif r < hit_rate + aux_rate + stack_rate:
+            out.append(f"ERROR [app] {rng.choice(EXC)}: boom")
+            for k in range(rng.randint(1, 6)):
+                out.append(f"\tat com.example.svc{k}.Handler$Inner.run(Handler.java:{rng.randint(1, 999)})")
+                i += 1
+        else:
+            out.append(_noise_line(rng, i))
+        i += 1
+    sep = "\n"
+    if crlf_rate > 0:
+        parts = []
+        for line in out:
+            parts.append(line)
+            parts.append("\r\n" if rng.random() < crlf_rate else "\n")
+        return "".join(parts)
+    return sep.join(out) + sep

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Headline benchmark: log-lines/sec parsed+scored (whole node), 1k-pattern library.
+
+Config (BASELINE.json configs[2], weak-scaled): every rank (one process per GPU) owns a shard of
+``--lines-per-gpu`` lines (default 12.5M -> 100M lines on 8 GPUs) of one logical synthetic pod
+log, analysed against a randomly generated 1,000-pattern library (primary + secondary +
+sequence patterns, context rules). A timed step is the complete pipeline for the shard:
+
+  pinned host -> HBM copy of the raw log bytes (PCIe ingest, H2D)
+  -> line index -> literal prefilter -> DFA verify / scan -> hit CSR -> events
+  -> packed RCCL all_gather (global N, frequency carry, sequence-chain carry)
+  -> fused fp64 scoring -> RCCL all_reduce (severity + frequency histograms)
+  -> RCCL all_gather top-k -> persistent frequency-state update.
+
+Nothing is cached between steps (the frequency state evolves exactly as the reference's would).
+Rank 0 prints one JSON line; ``value`` is total lines/s over all ranks (max step time across
+ranks). The reference publishes no number, so ``vs_baseline`` is null.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--lines-per-gpu", type=int, default=12_500_000)
+    ap.add_argument("--patterns", type=int, default=1000)
+    ap.add_argument("--block-lines", type=int, default=250_000, help="unique synthetic lines, tiled to the shard")
+    ap.add_argument("--hit-rate", type=float, default=0.004)
+    ap.add_argument("--topk", type=int, default=100)
+    ap.add_argument("--profile", action="store_true", help="per-stage timings (adds syncs; not for the headline)")
+    ap.add_argument("--device", default="auto")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from log_parser_amd.engine import Engine
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.ops import kernels as K
+    from log_parser_amd.parallel.dp import ShardedAnalyzer
+    from log_parser_amd.utils.config import Config, ScoringParams
+    from log_parser_amd.utils.synth import make_library, make_log
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() and args.device != "cpu"
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group("nccl" if use_cuda else "gloo", rank=rank, world_size=world)
+
+    params = ScoringParams()
+    sets, trig = make_library(args.patterns, seed=7)
+    lib = CompiledLibrary(sets, params)
+    cfg = Config.load(overrides={"engine.device": str(device)})
+    eng = Engine(lib, cfg, device=device)
+    eng.profile = args.profile
+    sa = ShardedAnalyzer(eng)
+
+    # ---- synthetic shard: block tiled to lines_per_gpu, plus halo lines from the neighbours
+    block = make_log(args.block_lines, trig, seed=11, hit_rate=args.hit_rate, aux_rate=0.01, stack_rate=0.01)
+    block_b = block.encode()
+    blines = block_b.split(b"\n")[:-1]
+    reps = max(1, args.lines_per_gpu // len(blines))
+    own = block_b * reps
+    own_lines = len(blines) * reps
+    H = lib.halo
+    head = b"\n".join(blines[:H]) + b"\n"
+    tail = b"\n".join(blines[-H:]) + b"\n"
+    hl = H if rank > 0 else 0
+    hr = H if rank < world - 1 else 0
+    data = (tail if hl else b"") + own + (head if hr else b"")
+    nbytes = len(data)
+    size = K.padded_len(nbytes)
+    host = torch.zeros(size, dtype=torch.uint8, pin_memory=use_cuda)
+    host[:nbytes].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    del data, own
+    text = torch.empty(size, dtype=torch.uint8, device=device)
+
+    def step():
+        text.copy_(host, non_blocking=True)                     # PCIe ingest (timed)
+        ls, ll = K.split_lines(text, nbytes)
+        out = sa.step(text, nbytes, ls, ll, hl, hr, topk=args.topk)
+        if rank == 0 and out.topk_score is not None:
+            out.topk_score.cpu()                                 # results land on the host
+        return out
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = step()
+    barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    total_lines = last.total_lines
+    ms = dt / args.steps * 1e3
+    value = total_lines * args.steps / dt
+    if rank == 0:
+        rec = {
+            "metric": "log-lines/sec parsed+scored (whole node), 1k-pattern library",
+            "value": round(value, 1), "unit": "lines/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp64", "data": "synthetic",
+            "config": {"model": f"log-parser {args.patterns}-pattern random library (secondary+sequence+context)",
+                       "global_batch": total_lines, "seq_len": round(nbytes / max(own_lines, 1), 1),
+                       "parallelism": f"dp{world}", "lines_per_gpu": own_lines, "bytes_per_gpu": nbytes,
+                       "events_per_step": int(last.pattern_counts.sum().item()),
+                       "library": lib.summary(), "device": str(device)},
+        }
+        if args.profile:
+            rec["timings_ms_last_step_rank0"] = {k: round(v, 3) for k, v in last.result.timings.items()}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

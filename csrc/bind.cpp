@@ -195,6 +195,16 @@ PYBIND11_MODULE(_lpnative, m) {
     score_host(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), P<const int64_t>(ef), n, st_from(st),
                sp_from(sp), P<double>(out), P<double>(fac)); });
 
+  m.def("seq_chain", [](uint64_t slot_seq, uint64_t off, uint64_t reg, uint64_t hoff, uint64_t hline, int32_t lo,
+                        int32_t hi, int n, uint64_t out, uint64_t s, bool dev) {
+    if (dev)
+      seq_chain_dev(P<const int32_t>(slot_seq), P<const int32_t>(off), P<const int32_t>(reg), P<const int64_t>(hoff),
+                    P<const int32_t>(hline), lo, hi, n, P<int32_t>(out), s);
+    else
+      seq_chain_host(P<const int32_t>(slot_seq), P<const int32_t>(off), P<const int32_t>(reg), P<const int64_t>(hoff),
+                     P<const int32_t>(hline), lo, hi, n, P<int32_t>(out));
+  });
+
   // ---- JSON result emitter
   m.def("emit_events_json", &emit_events_json_py);
 }

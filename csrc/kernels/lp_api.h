@@ -19,6 +19,12 @@ void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* lin
 void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
                const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream);
 
+void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
+                   const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
+                   int32_t* out, uint64_t stream);
+void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
+                    const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
+                    int32_t* out);
 int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap);

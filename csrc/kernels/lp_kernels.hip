@@ -219,6 +219,37 @@ __global__ __launch_bounds__(256) void k_score(const int32_t* __restrict__ ev_li
   out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Cross-shard sequence carry: for every sequence-event slot j = (sequence q,
+// event k) run the reference's backward chain (ScoringService.java:252-257, 296-305) from the
+// END of this rank's owned lines needing events k..0; out[j] = first event index still unmatched
+// when the owned range is exhausted (-1: chain complete). Ranks all-gather these tables and
+// compose them right-to-left, which reproduces the unbounded backward search across shards.
+__global__ __launch_bounds__(256) void k_seq_chain(const int32_t* __restrict__ slot_seq,
+                                                   const int32_t* __restrict__ seq_ev_off,
+                                                   const int32_t* __restrict__ seq_ev_reg,
+                                                   const int64_t* __restrict__ hit_off,
+                                                   const int32_t* __restrict__ hit_line, int32_t own_lo,
+                                                   int32_t own_hi, int nslots, int32_t* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nslots) return;
+  ScoreTables T;
+  T.hit_off = hit_off;
+  T.hit_line = hit_line;
+  const int q = slot_seq[j];
+  const int e0 = seq_ev_off[q];
+  int k = j - e0;
+  int32_t cur = own_hi;
+  while (k >= 0) {
+    const int32_t f = pred_hit(T, seq_ev_reg[e0 + k], own_lo, cur);
+    if (f < 0) break;
+    cur = f;
+    --k;
+  }
+  out[j] = k;
+}
+
 // ==========================================================================================
 // launchers (device) and host twins
 static int num_blocks(int64_t n, int t) { return (int)std::max<int64_t>(1, (n + t - 1) / t); }
@@ -275,7 +306,36 @@ void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_
   LP_CHECK(hipGetLastError());
 }
 
+void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
+                   const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
+                   int32_t* out, uint64_t stream) {
+  if (nslots <= 0) return;
+  hipLaunchKernelGGL(k_seq_chain, dim3(num_blocks(nslots, 256)), dim3(256), 0, as_stream(stream), slot_seq,
+                     seq_ev_off, seq_ev_reg, hit_off, hit_line, own_lo, own_hi, nslots, out);
+  LP_CHECK(hipGetLastError());
+}
+
 // ---------------- host twins (CPU backend) ----------------
+void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
+                    const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
+                    int32_t* out) {
+  ScoreTables T;
+  T.hit_off = hit_off;
+  T.hit_line = hit_line;
+  for (int j = 0; j < nslots; ++j) {
+    const int q = slot_seq[j];
+    const int e0 = seq_ev_off[q];
+    int k = j - e0;
+    int32_t cur = own_hi;
+    while (k >= 0) {
+      const int32_t f = pred_hit(T, seq_ev_reg[e0 + k], own_lo, cur);
+      if (f < 0) break;
+      cur = f;
+      --k;
+    }
+    out[j] = k;
+  }
+}
 int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos) {
   int64_t c = 0;
   const uint8_t* p = text;

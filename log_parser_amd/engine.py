@@ -83,6 +83,22 @@ class Segments:
 
 
 @dataclass
+class Prepared:
+    ev_line: torch.Tensor
+    ev_pat: torch.Tensor
+    ev_seg: torch.Tensor
+    ev_rank: torch.Tensor               # rank among earlier in-batch events of the same freq key
+    ev_fkey: torch.Tensor               # freq key per event (-1: none)
+    freq_counts: torch.Tensor
+    hits: torch.Tensor
+    hit_off: torch.Tensor
+    hit_line: torch.Tensor
+    feat: torch.Tensor
+    n_lines: int
+    timings: Dict[str, float] = field(default_factory=dict)
+
+
+@dataclass
 class RunResult:
     """Device-resident output of one pipeline run (events in reference order)."""
     ev_line: torch.Tensor
@@ -186,8 +202,11 @@ class Engine:
         return torch.tensor(keys, dtype=torch.int64, device=text.device)
 
     # ------------------------------------------------------------------ core run
-    def run(self, text, nbytes, ls, ll, segs: Segments, freq_carry: torch.Tensor,
-            seq_carry: Optional[torch.Tensor] = None, host_lines=None, with_factors=False) -> RunResult:
+    def prepare(self, text, nbytes, ls, ll, segs: Segments, host_lines=None) -> "Prepared":
+        """Local phase: matching, hit CSR, context features, events, in-batch frequency ranks.
+
+        Needs no global information, so the data-parallel path runs it before its collectives.
+        """
         timings: Dict[str, float] = {}
         dev = text.device
         L = ls.numel()
@@ -202,21 +221,22 @@ class Engine:
         # context features from the 4 built-in regexes (ids 0..3)
         feat32 = torch.zeros(max(L, 1), dtype=torch.int32, device=dev)
         cmask = hit_reg < 4
-        if bool(cmask.any()):
-            bits = torch.tensor([1, 2, 4, 8], dtype=torch.int32, device=dev)
-            feat32.index_put_((hit_line[cmask].long(),), bits[hit_reg[cmask].long()], accumulate=True)
-        feat = feat32.to(torch.uint8)
-        # primary events
-        line_seg, owned = segs.line_seg_and_owned(max(L, 1))
-        prim = tabs["is_primary"][hit_reg.long()] if hits.numel() else torch.zeros(0, dtype=torch.bool, device=dev)
         if hits.numel():
-            prim &= owned[hit_line.long()]
+            bits = torch.tensor([1, 2, 4, 8, 0], dtype=torch.int32, device=dev)
+            feat32.index_put_((hit_line.long(),), bits[hit_reg.clamp(max=4).long()] * cmask, accumulate=True)
+        feat = feat32.to(torch.uint8)
+        # primary events on owned lines, reference order (line, then pattern index)
+        line_seg, owned = segs.line_seg_and_owned(max(L, 1))
+        if hits.numel():
+            prim = tabs["is_primary"][hit_reg.long()] & owned[hit_line.long()]
+        else:
+            prim = torch.zeros(0, dtype=torch.bool, device=dev)
         ph_reg = hit_reg[prim].long()
         ph_line = hit_line[prim]
         cnt = tabs["prim_cnt"][ph_reg]
         total = int(cnt.sum().item()) if cnt.numel() else 0
         if total:
-            rep = torch.repeat_interleave(torch.arange(ph_reg.numel(), device=dev), cnt)
+            rep = torch.repeat_interleave(torch.arange(ph_reg.numel(), device=dev), cnt, output_size=total)
             start = torch.cumsum(cnt, 0) - cnt
             within = torch.arange(total, device=dev) - start[rep]
             ev_pat = tabs["prim_pats"][tabs["prim_off"][ph_reg][rep] + within].to(torch.int32)
@@ -224,40 +244,79 @@ class Engine:
             order = torch.argsort(ev_line.long() * P + ev_pat.long())
             ev_line = ev_line[order].contiguous()
             ev_pat = ev_pat[order].contiguous()
+            ev_seg = line_seg[ev_line.long()].contiguous()
         else:
             ev_line = torch.empty(0, dtype=torch.int32, device=dev)
             ev_pat = torch.empty(0, dtype=torch.int32, device=dev)
-        ev_seg = line_seg[ev_line.long()].contiguous() if total else torch.empty(0, dtype=torch.int32, device=dev)
+            ev_seg = torch.empty(0, dtype=torch.int32, device=dev)
         t = self._tick(timings, "events", t)
-        # frequency: count_before = carry[key] + rank among earlier events of the same key
+        # frequency: rank of each event among earlier events with the same key (in-batch part of
+        # the segmented exclusive scan); the carry is added in finish()
         nkeys = len(self.lib.freq_ids)
-        fk = tabs["freq_key"][ev_pat.long()] if total else torch.empty(0, dtype=torch.int32, device=dev)
-        ev_freq = torch.full((total,), -1, dtype=torch.int64, device=dev)
+        ev_rank = torch.full((total,), -1, dtype=torch.int64, device=dev)
+        ev_fkey = torch.full((total,), -1, dtype=torch.int64, device=dev)
         freq_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
         if total and nkeys:
+            fk = tabs["freq_key"][ev_pat.long()].long()
             vi = torch.nonzero(fk >= 0).flatten()
             if vi.numel():
-                fkv = fk[vi].long()
+                fkv = fk[vi]
                 sk, perm = torch.sort(fkv, stable=True)
                 first = torch.searchsorted(sk, sk)
                 rank_sorted = torch.arange(sk.numel(), device=dev) - first
                 rank = torch.empty_like(rank_sorted)
                 rank[perm] = rank_sorted
-                ev_freq[vi] = freq_carry[fkv] + rank
-                freq_counts = torch.bincount(fkv, minlength=nkeys)
-        t = self._tick(timings, "frequency", t)
+                ev_rank[vi] = rank
+                ev_fkey[vi] = fkv
+                freq_counts = torch.bincount(fkv, minlength=max(nkeys, 1))
+        self._tick(timings, "frequency", t)
+        hit_line_c = hit_line.contiguous() if hit_line.numel() else torch.zeros(1, dtype=torch.int32, device=dev)
+        return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
+                        hit_line_c, feat, L, timings)
+
+    def seq_chain_table(self, prep: "Prepared", own_lo: int, own_hi: int) -> torch.Tensor:
+        """Per sequence-event slot: event index still unmatched after this shard (-1 = done)."""
+        tabs = self.tabs
+        n = self.lib.n_seq_events
+        out = torch.full((max(n, 1),), -1, dtype=torch.int32, device=prep.hit_off.device)
+        if n == 0:
+            return out
+        dev = prep.hit_off.is_cuda
+        s = torch.cuda.current_stream(prep.hit_off.device).cuda_stream if dev else 0
+        N.seq_chain(tabs["slot_seq"].data_ptr(), tabs["seq_ev_off"].data_ptr(), tabs["seq_ev_reg"].data_ptr(),
+                    prep.hit_off.data_ptr(), prep.hit_line.data_ptr(), int(own_lo), int(own_hi), n,
+                    out.data_ptr(), s, dev)
+        return out
+
+    def finish(self, prep: "Prepared", segs: Segments, freq_carry: torch.Tensor,
+               seq_carry: Optional[torch.Tensor] = None, with_factors: bool = False) -> RunResult:
+        """Global phase: fused fp64 score kernel (needs N, global offsets and carries)."""
+        t = time.perf_counter()
+        tabs = self.tabs
+        dev = prep.hit_off.device
+        ev_freq = prep.ev_rank
+        if ev_freq.numel():
+            ev_freq = torch.where(prep.ev_fkey >= 0, freq_carry[prep.ev_fkey.clamp(min=0)] + prep.ev_rank,
+                                  torch.full_like(prep.ev_rank, -1))
         if seq_carry is None:
             seq_carry = torch.zeros(max(self.lib.n_seq_events, 1), dtype=torch.uint8, device=dev)
-        hit_line_c = hit_line.contiguous() if hit_line.numel() else torch.zeros(1, dtype=torch.int32, device=dev)
         st = (tabs["conf"].data_ptr(), tabs["sev"].data_ptr(), tabs["ctx_before"].data_ptr(),
               tabs["ctx_after"].data_ptr(), tabs["sec_off"].data_ptr(), tabs["sec_reg"].data_ptr(),
               tabs["sec_w"].data_ptr(), tabs["sec_weight"].data_ptr(), tabs["seq_off"].data_ptr(),
               tabs["seq_bonus"].data_ptr(), tabs["seq_ev_off"].data_ptr(), tabs["seq_ev_reg"].data_ptr(),
-              seq_carry.data_ptr(), hit_off.data_ptr(), hit_line_c.data_ptr(), feat.data_ptr(),
+              seq_carry.data_ptr(), prep.hit_off.data_ptr(), prep.hit_line.data_ptr(), prep.feat.data_ptr(),
               segs.lo.data_ptr(), segs.hi.data_ptr(), segs.own_lo.data_ptr(), segs.g0.data_ptr(), segs.n.data_ptr())
-        score, factors = K.score(ev_line, ev_pat, ev_seg, ev_freq, st, self.sp_tuple, with_factors)
+        score, factors = K.score(prep.ev_line, prep.ev_pat, prep.ev_seg, ev_freq.contiguous(), st, self.sp_tuple,
+                                 with_factors)
+        timings = dict(prep.timings)
         self._tick(timings, "score", t)
-        return RunResult(ev_line, ev_pat, ev_seg, score, factors, freq_counts[:nkeys], hits, hit_off, L, timings)
+        return RunResult(prep.ev_line, prep.ev_pat, prep.ev_seg, score, factors,
+                         prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings)
+
+    def run(self, text, nbytes, ls, ll, segs: Segments, freq_carry: torch.Tensor,
+            seq_carry: Optional[torch.Tensor] = None, host_lines=None, with_factors=False) -> RunResult:
+        prep = self.prepare(text, nbytes, ls, ll, segs, host_lines)
+        return self.finish(prep, segs, freq_carry, seq_carry, with_factors)
 
     # ------------------------------------------------------------------ request API
     def freq_carry(self) -> torch.Tensor:

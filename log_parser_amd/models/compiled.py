@@ -307,6 +307,10 @@ class CompiledLibrary:
         t["ctx_before"], t["ctx_after"] = T(self.ctx_before), T(self.ctx_after)
         t["sec_off"], t["sec_reg"], t["sec_w"], t["sec_weight"] = T(self.sec_off), T(self.sec_reg), T(self.sec_w), T(self.sec_weight)
         t["seq_off"], t["seq_bonus"], t["seq_ev_off"], t["seq_ev_reg"] = T(self.seq_off), T(self.seq_bonus), T(self.seq_ev_off), T(self.seq_ev_reg)
+        slot_seq = np.zeros(max(self.n_seq_events, 1), np.int32)
+        for q in range(len(self.seq_off) and (self.seq_ev_off.size - 1)):
+            slot_seq[self.seq_ev_off[q]:self.seq_ev_off[q + 1]] = q
+        t["slot_seq"] = T(slot_seq)
         t["prim_off"], t["prim_pats"] = T(self.prim_off), T(self.prim_pats)
         t["prim_cnt"] = T(np.diff(self.prim_off))
         t["freq_key"] = T(self.freq_key)

@@ -1,0 +1,174 @@
+"""Line-sharded data parallelism over the GPUs of one node (RCCL over xGMI).
+
+The reference is single-threaded per request; this module is new. One logical log
+is split into contiguous line ranges, one per rank (one process per GPU), each with ``H`` halo
+lines on both sides (``H = CompiledLibrary.halo`` = max of proximity window, context lines and
+the ±5 sequence window). Every cross-shard dependency of the reference's sequential semantics is
+resolved with collectives:
+
+  C1  global N / line offsets  (ScoringService.java:125)      \\
+  C3  frequency ordering       (ScoringService.java:84-88)     } ONE packed all_gather, int64
+  C4  backward sequence chain  (ScoringService.java:296-305)  /   [own_lines | freq counts | chain]
+  C5/C6 severity histogram + frequency histogram               -> all_reduce(sum)
+  C7  top-k events                                             -> all_gather of k rows, merge
+
+Every message but the top-k rows is a few KB, so each step pays ~3 latency-bound collectives
+regardless of log size; xGMI bandwidth is irrelevant, PCIe ingest and HBM are what scale.
+The backend is whatever ``torch.distributed`` was initialised with: ``nccl`` (= RCCL on ROCm)
+on GPUs, ``gloo`` for the CPU tests.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..engine import Engine, RunResult, Segments
+
+
+def world() -> tuple:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
+    """all_gather of a 1-D tensor -> [world, n] (RCCL all_gather_into_tensor on GPU)."""
+    r, w = world()
+    if w == 1:
+        return t.unsqueeze(0)
+    out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    if t.is_cuda:
+        dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
+    return out
+
+
+def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+    if world()[1] > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t
+
+
+@dataclass
+class StepOutput:
+    result: RunResult
+    total_lines: int
+    own_start: int                 # global index of this rank's first owned line
+    pattern_counts: torch.Tensor   # global (all-reduced) events per pattern
+    topk_score: Optional[torch.Tensor] = None   # rank 0: merged global top-k
+    topk_line: Optional[torch.Tensor] = None    # 0-based global line
+    topk_pat: Optional[torch.Tensor] = None
+    summary: Optional[dict] = None
+
+
+class ShardedAnalyzer:
+    def __init__(self, engine: Engine, group=None):
+        self.engine = engine
+        self.group = group
+        lib = engine.lib
+        # per sequence-event slot: first slot of its sequence and its event index
+        off = lib.seq_ev_off
+        e0 = np.zeros(max(lib.n_seq_events, 1), np.int64)
+        kk = np.zeros(max(lib.n_seq_events, 1), np.int64)
+        for q in range(off.size - 1):
+            e0[off[q]:off[q + 1]] = off[q]
+            kk[off[q]:off[q + 1]] = np.arange(off[q + 1] - off[q])
+        dev = engine.device
+        self.slot_e0 = torch.from_numpy(e0).to(dev)
+        self.slot_k = torch.from_numpy(kk).to(dev)
+
+    def _compose_chain(self, chains: torch.Tensor, rank: int) -> torch.Tensor:
+        """carry[j] = 1 iff the chain needing events k..0 completes in ranks < rank."""
+        k = self.slot_k.clone()
+        for q in range(rank - 1, -1, -1):
+            idx = self.slot_e0 + k.clamp(min=0)
+            nk = chains[q].to(torch.int64)[idx]
+            k = torch.where(k >= 0, nk, k)
+        return (k < 0).to(torch.uint8)
+
+    def step(self, text: torch.Tensor, nbytes: int, ls: torch.Tensor, ll: torch.Tensor,
+             halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False) -> StepOutput:
+        eng = self.engine
+        lib = eng.lib
+        rank, wsize = world()
+        dev = text.device
+        L = ls.numel()
+        own_lo, own_hi = halo_left, L - halo_right
+        i32 = lambda v: torch.tensor([v], dtype=torch.int32, device=dev)  # noqa: E731
+        i64 = lambda v: torch.tensor([v], dtype=torch.int64, device=dev)  # noqa: E731
+        segs = Segments(i32(0), i32(L), i32(own_lo), i32(own_hi), i64(0), i64(1))
+        prep = eng.prepare(text, nbytes, ls, ll, segs)
+        chain = eng.seq_chain_table(prep, own_lo, own_hi)
+        nk = len(lib.freq_ids)
+        pack = torch.cat([i64(own_hi - own_lo), prep.freq_counts[:nk].to(torch.int64), chain.to(torch.int64)])
+        g = all_gather_rows(pack, self.group)                      # C1 + C3 + C4 in one collective
+        own_counts = g[:, 0]
+        own_start = int(own_counts[:rank].sum().item())
+        total = int(own_counts.sum().item())
+        carry = eng.freq_carry()
+        if nk:
+            carry = carry + g[:rank, 1:1 + nk].sum(0)
+        seq_carry = self._compose_chain(g[:, 1 + nk:].to(torch.int32), rank)
+        segs.g0 = i64(own_start - halo_left)
+        segs.n = i64(max(total, 1))
+        res = eng.finish(prep, segs, carry, seq_carry, with_factors)
+        # C5/C6 + frequency histogram: one all-reduce
+        P = len(lib.patterns)
+        pc = torch.bincount(res.ev_pat.long(), minlength=P) if res.ev_pat.numel() else torch.zeros(P, dtype=torch.int64, device=dev)
+        red = torch.cat([pc.to(torch.int64), prep.freq_counts[:nk].to(torch.int64)])
+        red = all_reduce_sum(red, self.group)
+        pattern_counts = red[:P]
+        eng.commit_frequency(red[P:])
+        out = StepOutput(res, total, own_start, pattern_counts)
+        # C7: top-k
+        if topk > 0:
+            k = min(topk, res.score.numel())
+            rows = torch.full((topk, 3), -1.0, dtype=torch.float64, device=dev)
+            rows[:, 0] = float("-inf")
+            if k:
+                v, idx = torch.topk(res.score, k)
+                rows[:k, 0] = v
+                rows[:k, 1] = (res.ev_line[idx].to(torch.int64) - own_lo + own_start).to(torch.float64)
+                rows[:k, 2] = res.ev_pat[idx].to(torch.float64)
+            allrows = all_gather_rows(rows.flatten(), self.group).view(-1, 3)
+            if rank == 0:
+                kk = min(topk, int(torch.isfinite(allrows[:, 0]).sum().item()))
+                v, idx = torch.topk(allrows[:, 0], kk)
+                out.topk_score = v
+                out.topk_line = allrows[idx, 1].to(torch.int64)
+                out.topk_pat = allrows[idx, 2].to(torch.int64)
+        return out
+
+    def summary(self, pattern_counts: torch.Tensor, first_pat: Optional[int] = None) -> dict:
+        lib = self.engine.lib
+        pc = pattern_counts.cpu().numpy()
+        n = int(pc.sum())
+        if n == 0:
+            return {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
+        from ..golden import SEVERITY_ORDER
+        dist_: dict = {}
+        for p in np.nonzero(pc)[0]:
+            s = lib.severity[p]
+            dist_[s] = dist_.get(s, 0) + int(pc[p])
+        best_idx, best = -1, None
+        for s in dist_:
+            if s in SEVERITY_ORDER and SEVERITY_ORDER.index(s) > best_idx:
+                best_idx, best = SEVERITY_ORDER.index(s), s
+        if best is None and first_pat is not None:
+            best = lib.severity[first_pat]
+        return {"significantEvents": n, "highestSeverity": best, "severityDistribution": dist_}
+
+
+def shard_bounds(n_lines: int, world_size: int, rank: int, halo: int):
+    """Contiguous balanced line ranges; returns (lo, hi, halo_left, halo_right) in global lines."""
+    base, rem = divmod(n_lines, world_size)
+    lo = rank * base + min(rank, rem)
+    hi = lo + base + (1 if rank < rem else 0)
+    hl = min(halo, lo)
+    hr = min(halo, n_lines - hi)
+    return lo, hi, hl, hr

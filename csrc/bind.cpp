@@ -32,6 +32,7 @@ static PfTables pf_from(const py::tuple& t) {
   T.lit_reg_off = P<const int32_t>(t[9].cast<uint64_t>());
   T.lit_reg = P<const int32_t>(t[10].cast<uint64_t>());
   T.gmask = t[11].cast<int>();
+  T.lit_goff = P<const int32_t>(t[12].cast<uint64_t>());
   return T;
 }
 
@@ -169,6 +170,10 @@ PYBIND11_MODULE(_lpnative, m) {
                             uint64_t count, int grid, uint64_t s) {
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
                   P<unsigned long long>(count), grid, s); });
+  m.def("pf_verify_dev", [](uint64_t gh, int64_t n, uint64_t text, int64_t nb, py::tuple pf, uint64_t ls, int64_t nl,
+                            uint64_t cand, int64_t cap, uint64_t count, uint64_t s) {
+    pf_verify_dev(P<const int64_t>(gh), n, P<const uint8_t>(text), nb, pf_from(pf), P<const int64_t>(ls), nl,
+                  P<int64_t>(cand), cap, P<unsigned long long>(count), s); });
   m.def("verify_dev", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out, uint64_t s) {
     verify_dev(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out), s); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
@@ -203,6 +208,12 @@ PYBIND11_MODULE(_lpnative, m) {
     else
       seq_chain_host(P<const int32_t>(slot_seq), P<const int32_t>(off), P<const int32_t>(reg), P<const int64_t>(hoff),
                      P<const int32_t>(hline), lo, hi, n, P<int32_t>(out));
+  });
+
+  m.def("feat", [](uint64_t lines, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t feat,
+                   uint64_t s, bool dev) {
+    if (dev) feat_dev(P<const int32_t>(lines), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(feat), s);
+    else feat_host(P<const int32_t>(lines), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(feat));
   });
 
   // ---- JSON result emitter

@@ -11,6 +11,9 @@ void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_
 void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, uint64_t stream);
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
+void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
+                   const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap, unsigned long long* count,
+                   uint64_t stream);
 void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
                 const DfaPool& P, uint8_t* out, uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
@@ -25,6 +28,10 @@ void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int
 void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
                     const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
                     int32_t* out);
+void feat_dev(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+              const DfaPool& P, uint8_t* feat, uint64_t stream);
+void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+               const DfaPool& P, uint8_t* feat);
 int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap);

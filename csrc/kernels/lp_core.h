@@ -61,6 +61,7 @@ struct PfTables {
   const int32_t* lit_reg_off;
   const int32_t* lit_reg;
   int gmask;                // bit g set when grams of length g (2..4) exist
+  const int32_t* lit_goff;  // offset of each literal's gram window inside the literal
 };
 
 LP_HD uint32_t gram_mask(int g) { return g >= 4 ? 0xFFFFFFFFu : ((1u << (8 * g)) - 1u); }
@@ -122,12 +123,13 @@ LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int6
   for (int j = 0; j < c; ++j) {
     const int lit = T.gram_lits[s + j];
     const int lo = T.lit_off[lit], len = T.lit_off[lit + 1] - lo;
-    if (p + len > nbytes) continue;
+    const int64_t st = p - T.lit_goff[lit];
+    if (st < 0 || st + len > nbytes) continue;
     bool ok = true;
-    for (int q = g; q < len; ++q)
-      if (lower_byte(text[p + q]) != T.lit_bytes[lo + q]) { ok = false; break; }
+    for (int q = 0; q < len; ++q)
+      if (lower_byte(text[st + q]) != T.lit_bytes[lo + q]) { ok = false; break; }
     if (!ok) continue;
-    if (line < 0) line = upper_idx(line_start, nlines, p);
+    if (line < 0) line = upper_idx(line_start, nlines, st);
     if (line < 0) line = 0;
     for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
       append(((int64_t)T.lit_reg[r] << 32) | line);

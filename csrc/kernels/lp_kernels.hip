@@ -136,44 +136,141 @@ struct Appender {
   }
 };
 
-template <int G>
-__device__ __forceinline__ void pf_try(const uint32_t* bl, const PfTables& T, const uint8_t* text, int64_t nbytes,
-                                       int64_t p, uint32_t g4, const int64_t* line_start, int64_t nlines,
-                                       const Appender& app) {
-  const uint32_t key = g4 & gram_mask(G);
-  const uint32_t h1 = bloom_h1(key, G, T.bloom_bits), h2 = bloom_h2(key, G, T.bloom_bits);
-  if (((bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u) == 0) return;
-  pf_probe(T, text, nbytes, p, key, G, line_start, nlines, app);
+// Block-level candidate staging: LDS atomics per candidate, ONE global atomic per flush.
+constexpr int PF_BUF = 1024;
+struct LdsAppender {
+  int64_t* buf;
+  int* cnt;
+  int64_t* out;
+  int64_t cap;
+  unsigned long long* gcount;
+  __device__ void operator()(int64_t v) const {
+    const int s = atomicAdd(cnt, 1);
+    if (s < PF_BUF) {
+      buf[s] = v;
+    } else {  // overflow inside one iteration: spill straight to global
+      unsigned long long i = atomicAdd(gcount, 1ull);
+      if ((int64_t)i < cap) out[i] = v;
+    }
+  }
+};
+
+__device__ __forceinline__ void pf_flush(int64_t* buf, int* cnt, unsigned long long* gbase, int c, int64_t* out,
+                                         int64_t cap, unsigned long long* gcount) {
+  const int m = c < PF_BUF ? c : PF_BUF;
+  if (threadIdx.x == 0) *gbase = atomicAdd(gcount, (unsigned long long)m);
+  __syncthreads();
+  const unsigned long long base = *gbase;
+  for (int i = threadIdx.x; i < m; i += blockDim.x)
+    if ((int64_t)(base + i) < cap) out[base + i] = buf[i];
+  __syncthreads();
+  if (threadIdx.x == 0) *cnt = 0;
+  __syncthreads();
 }
 
+template <int G>
+__device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint32_t g4) {
+  const uint32_t key = g4 & gram_mask(G);
+  const uint32_t h1 = bloom_h1(key, G, bits), h2 = bloom_h2(key, G, bits);
+  return (bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u;
+}
+
+// Hot loop: only bloom tests (tight, fully unrolled: ~12 VALU + 2 ds_read_b32 per position and
+// gram length). Rare path: one non-unrolled loop over the hit bitmask probes the global hash
+// table, so the probe/verify/append code exists once in the binary (no I-cache blow-up).
+// GM = set of gram lengths present in the library (bit g), a compile-time constant so the
+// unrolled bloom loop is branch-free and its 16 x 2 LDS reads pipeline behind one wait.
+template <int GM>
 __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,
                                                           int64_t nlines, int64_t* cand, int64_t cap,
                                                           unsigned long long* count) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t bl[];
-  const int nwords = (1 << T.bloom_bits) >> 5;
+  // dynamic LDS: [bloom (1<<bits)/8 B][candidate buffer PF_BUF x 8 B][cnt 4 B | pad | gbase 8 B]
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* bl = smem;
+  const int bits = T.bloom_bits;
+  const int nwords = (1 << bits) >> 5;
+  int64_t* buf = reinterpret_cast<int64_t*>(smem + nwords);
+  int* cnt = reinterpret_cast<int*>(buf + PF_BUF);
+  unsigned long long* gbase = reinterpret_cast<unsigned long long*>(buf + PF_BUF + 1);
   for (int i = threadIdx.x * 4; i < nwords; i += blockDim.x * 4)
     *reinterpret_cast<uint4*>(bl + i) = *reinterpret_cast<const uint4*>(T.bloom + i);
+  if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
-  const Appender app{cand, cap, count};
+  const LdsAppender app{buf, cnt, cand, cap, count};
   const int64_t nunits = (nbytes + 15) >> 4;
-  const bool g2 = T.gmask & 4, g3 = T.gmask & 8, g4on = T.gmask & 16;
-  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < nunits; u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p0 = u << 4;
-    const uint4 v = *reinterpret_cast<const uint4*>(text + p0);
-    const uint32_t nx = *reinterpret_cast<const uint32_t*>(text + p0 + 16);
-    const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
+  constexpr bool g2 = GM & 4, g3 = GM & 8, g4on = GM & 16;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t ub = (int64_t)blockIdx.x * blockDim.x; ub < nunits; ub += stride) {
+    const int64_t u = ub + threadIdx.x;
+    if (u < nunits) {
+      const int64_t p0 = u << 4;
+      const uint4 v = *reinterpret_cast<const uint4*>(text + p0);
+      const uint32_t nx = *reinterpret_cast<const uint32_t*>(text + p0 + 16);
+      const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
+      uint32_t m4 = 0, m3 = 0, m2 = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int64_t p = p0 + k;
-      const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
-      if (p < nbytes) {
-        if (g4on) pf_try<4>(bl, T, text, nbytes, p, gram, line_start, nlines, app);
-        if (g3) pf_try<3>(bl, T, text, nbytes, p, gram, line_start, nlines, app);
-        if (g2) pf_try<2>(bl, T, text, nbytes, p, gram, line_start, nlines, app);
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
+        if constexpr (g4on) m4 |= pf_bloom<4>(bl, bits, gram) << k;
+        if constexpr (g3) m3 |= pf_bloom<3>(bl, bits, gram) << k;
+        if constexpr (g2) m2 |= pf_bloom<2>(bl, bits, gram) << k;
+      }
+      const int64_t rem = nbytes - p0;
+      const uint32_t valid = rem >= 16 ? 0xFFFFu : ((1u << rem) - 1u);
+      uint64_t hm = ((uint64_t)(m4 & valid) << 32) | ((uint64_t)(m3 & valid) << 16) | (uint64_t)(m2 & valid);
+      while (hm) {  // rare: stage the gram hit; literal verification runs in k_pf_verify
+        const int b = __ffsll((unsigned long long)hm) - 1;
+        hm &= hm - 1;
+        app(((p0 + (b & 15)) << 2) | (int64_t)(b >> 4));   // (position, gram length - 2)
       }
     }
+    __syncthreads();
+    const int c = *reinterpret_cast<volatile int*>(cnt);
+    if (c >= PF_BUF / 2) pf_flush(buf, cnt, gbase, c, cand, cap, count);
   }
+  __syncthreads();
+  const int c = *reinterpret_cast<volatile int*>(cnt);
+  if (c > 0) pf_flush(buf, cnt, gbase, c, cand, cap, count);
+}
+
+// K3a': literal verification of staged gram hits (one lane per hit): hash-table probe, full
+// literal compare at the literal's start (hit position - gram offset), candidate append.
+__global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ ghits, int64_t n,
+                                                   const uint8_t* __restrict__ text, int64_t nbytes, PfTables T,
+                                                   const int64_t* __restrict__ line_start, int64_t nlines,
+                                                   int64_t* cand, int64_t cap, unsigned long long* count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t h = ghits[i];
+  const int64_t p = h >> 2;
+  const int G = 2 + (int)(h & 3);
+  uint32_t g4 = 0;
+  for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
+  const Appender app{cand, cap, count};
+  pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, app);
+}
+
+// ------------------------------------------------------------------------------------------
+// K6: context features, computed lazily for the lines inside some event's context window only
+// (ContextAnalysisService.java:62-83): bit0 ERROR, bit1 WARN (only evaluated when not ERROR: the
+// reference's else-if), bit2 stack-trace line, bit3 exception/error class name.
+__global__ __launch_bounds__(256) void k_feat(const int32_t* __restrict__ lines, int64_t n,
+                                              const uint8_t* __restrict__ text,
+                                              const int64_t* __restrict__ line_start,
+                                              const int32_t* __restrict__ line_len, DfaPool P,
+                                              uint8_t* __restrict__ feat) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t line = lines[i];
+  const uint8_t* s = text + line_start[line];
+  const int len = line_len[line];
+  uint8_t f = 0;
+  if (dfa_run(P, 0, s, len)) f |= 1;
+  else if (dfa_run(P, 1, s, len)) f |= 2;
+  if (dfa_run(P, 2, s, len)) f |= 4;
+  if (dfa_run(P, 3, s, len)) f |= 8;
+  feat[line] = f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -273,11 +370,51 @@ void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, i
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream) {
   if (nbytes <= 0) return;
-  const size_t lds = (size_t(1) << T.bloom_bits) / 8;
+  const size_t lds = (size_t(1) << T.bloom_bits) / 8 + PF_BUF * 8 + 16;
   int64_t units = (nbytes + 15) / 16;
   int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS));
-  hipLaunchKernelGGL(k_prefilter, dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, line_start,
-                     nlines, cand, cap, count);
+#define LP_PF_CASE(GMV)                                                                                     \
+  case GMV:                                                                                                 \
+    hipLaunchKernelGGL(k_prefilter<GMV>, dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, \
+                       line_start, nlines, cand, cap, count);                                               \
+    break;
+  switch (T.gmask & 28) {
+    LP_PF_CASE(4) LP_PF_CASE(8) LP_PF_CASE(12) LP_PF_CASE(16) LP_PF_CASE(20) LP_PF_CASE(24) LP_PF_CASE(28)
+    default: return;  // no literals: nothing to prefilter
+  }
+#undef LP_PF_CASE
+  LP_CHECK(hipGetLastError());
+}
+
+void feat_dev(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+              const DfaPool& P, uint8_t* feat, uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_feat, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), lines, n, text, line_start,
+                     line_len, P, feat);
+  LP_CHECK(hipGetLastError());
+}
+
+void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+               const DfaPool& P, uint8_t* feat) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t line = lines[i];
+    const uint8_t* s = text + line_start[line];
+    const int len = line_len[line];
+    uint8_t f = 0;
+    if (dfa_run(P, 0, s, len)) f |= 1;
+    else if (dfa_run(P, 1, s, len)) f |= 2;
+    if (dfa_run(P, 2, s, len)) f |= 4;
+    if (dfa_run(P, 3, s, len)) f |= 8;
+    feat[line] = f;
+  }
+}
+
+void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
+                   const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap, unsigned long long* count,
+                   uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_pf_verify, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ghits, n, text, nbytes,
+                     T, line_start, nlines, cand, cap, count);
   LP_CHECK(hipGetLastError());
 }
 

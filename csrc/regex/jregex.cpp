@@ -76,15 +76,15 @@ bool is_word_byte(int c) {
 uint16_t mask_where(bool (*f)(int, int)) {
   uint16_t m = 0;
   for (int p = 0; p < 3; ++p)
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < 5; ++n)
       if (f(p, n)) m |= (uint16_t)(1u << ctx_index(p, n));
   return m;
 }
-bool f_bos(int p, int) { return p == P_BOS; }
+bool f_bos(int p, int n) { return p == P_BOS && n != N_C; }
 bool f_eol(int, int n) { return n == N_EOS || n == N_FT; }
 bool f_eos(int, int n) { return n == N_EOS; }
-bool f_wb(int p, int n) { return (p == P_W) != (n == N_W); }
-bool f_nwb(int p, int n) { return (p == P_W) == (n == N_W); }
+bool f_wb(int p, int n) { return n != N_C && (p == P_W) != (n == N_W); }
+bool f_nwb(int p, int n) { return n != N_C && (p == P_W) == (n == N_W); }
 
 struct Flags { bool ci = false, dotall = false, comments = false, multiline = false, unixl = false; };
 
@@ -819,6 +819,7 @@ Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
     sig.reserve(dcls.size() + 1);
     for (auto& x : dcls) sig.push_back(x.test(b));
     sig.push_back(is_word_byte(b));
+    sig.push_back(b >= 0x80 && b <= 0xBF);
     auto it = sig2cls.find(sig);
     int k;
     if (it == sig2cls.end()) { k = (int)rep.size(); sig2cls[sig] = k; rep.push_back(b); }
@@ -828,8 +829,8 @@ Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
   d.nclasses = (int)rep.size();
   if (d.nclasses > 256) throw Unsupported("too many byte classes");
 
-  bool restartable = (nfa.nullable & 0x0FF0) != 0;
-  for (auto& e : nfa.first) if (e.cond & 0x0FF0) restartable = true;
+  bool restartable = (nfa.nullable & CTX_NOT_BOS) != 0;
+  for (auto& e : nfa.first) if (e.cond & CTX_NOT_BOS) restartable = true;
   d.anchored = !restartable;
 
   // ACCEPT check helper
@@ -870,7 +871,7 @@ Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
     std::vector<uint16_t> row(d.nclasses, 0);
     for (int k = 0; k < d.nclasses; ++k) {
       int c = rep[k];
-      int nk = is_word_byte(c) ? N_W : N_N;
+      int nk = is_word_byte(c) ? N_W : (c >= 0x80 && c <= 0xBF) ? N_C : N_N;
       if (accepts(A, prev, nk)) { row[k] = 1; continue; }
       uint16_t bit = (uint16_t)(1u << ctx_index(prev, nk));
       std::vector<uint64_t> B(nw, 0);

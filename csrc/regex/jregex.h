@@ -24,12 +24,15 @@ namespace lp {
 struct SyntaxError : std::runtime_error { using std::runtime_error::runtime_error; };
 struct Unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
 
-// Boundary contexts: prev in {BOS=0, W=1, N=2} x next in {EOS=0, FT=1, W=2, N=3}
-// ctx index = prev*4 + next (12 contexts). FT = "before the final line terminator".
+// Boundary contexts: prev in {BOS=0, W=1, N=2} x next in {EOS=0, FT=1, W=2, N=3, C=4}
+// ctx index = prev*5 + next (15 contexts). FT = "before the final line terminator".
 enum : int { P_BOS = 0, P_W = 1, P_N = 2 };
-enum : int { N_EOS = 0, N_FT = 1, N_W = 2, N_N = 3 };
-constexpr uint16_t CTX_ALL = 0x0FFF;
-inline int ctx_index(int prev, int next) { return prev * 4 + next; }
+// N_C: the next byte is a UTF-8 continuation byte (a boundary inside one code point); no
+// assertion holds there, so assertions are only ever evaluated between whole characters.
+enum : int { N_EOS = 0, N_FT = 1, N_W = 2, N_N = 3, N_C = 4 };
+constexpr uint16_t CTX_ALL = 0x7FFF;                    // 15 contexts
+constexpr uint16_t CTX_NOT_BOS = 0x7FE0;                // prev != BOS
+inline int ctx_index(int prev, int next) { return prev * 5 + next; }
 
 struct ByteSet {
   uint64_t w[4] = {0, 0, 0, 0};

@@ -218,13 +218,6 @@ class Engine:
         hit_reg = (hits >> 32).to(torch.int32)
         hit_line = (hits & 0xFFFFFFFF).to(torch.int32)
         hit_off = torch.searchsorted(hit_reg, torch.arange(R + 1, dtype=torch.int32, device=dev)).to(torch.int64)
-        # context features from the 4 built-in regexes (ids 0..3)
-        feat32 = torch.zeros(max(L, 1), dtype=torch.int32, device=dev)
-        cmask = hit_reg < 4
-        if hits.numel():
-            bits = torch.tensor([1, 2, 4, 8, 0], dtype=torch.int32, device=dev)
-            feat32.index_put_((hit_line.long(),), bits[hit_reg.clamp(max=4).long()] * cmask, accumulate=True)
-        feat = feat32.to(torch.uint8)
         # primary events on owned lines, reference order (line, then pattern index)
         line_seg, owned = segs.line_seg_and_owned(max(L, 1))
         if hits.numel():
@@ -250,6 +243,9 @@ class Engine:
             ev_pat = torch.empty(0, dtype=torch.int32, device=dev)
             ev_seg = torch.empty(0, dtype=torch.int32, device=dev)
         t = self._tick(timings, "events", t)
+        # context features (ContextAnalysisService) only for lines inside some event's window
+        feat = self._context_features(text, ls, ll, ev_line, ev_pat, ev_seg, segs, L)
+        t = self._tick(timings, "context", t)
         # frequency: rank of each event among earlier events with the same key (in-batch part of
         # the segmented exclusive scan); the carry is added in finish()
         nkeys = len(self.lib.freq_ids)
@@ -273,6 +269,26 @@ class Engine:
         hit_line_c = hit_line.contiguous() if hit_line.numel() else torch.zeros(1, dtype=torch.int32, device=dev)
         return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
                         hit_line_c, feat, L, timings)
+
+    def _context_features(self, text, ls, ll, ev_line, ev_pat, ev_seg, segs: Segments, L: int) -> torch.Tensor:
+        dev = text.device
+        if ev_line.numel() == 0:
+            return torch.zeros(max(L, 1), dtype=torch.uint8, device=dev)
+        x = ev_line.long()
+        p = ev_pat.long()
+        s = ev_seg.long()
+        before = self.tabs["ctx_before"][p].long()
+        after = self.tabs["ctx_after"][p].long()
+        null = before < 0
+        a = torch.where(null, x, torch.maximum(segs.lo[s].long(), x - before))
+        b = torch.where(null, x + 1, torch.minimum(segs.hi[s].long(), x + after + 1))
+        diff = torch.zeros(L + 1, dtype=torch.int32, device=dev)
+        one = torch.ones_like(a, dtype=torch.int32)
+        diff.index_add_(0, a, one)
+        diff.index_add_(0, b, -one)
+        need = torch.cumsum(diff[:L], 0) > 0
+        lines = torch.nonzero(need).flatten().to(torch.int32)
+        return K.context_features(lines, L, text, ls, ll, self.tabs["dfa"])
 
     def seq_chain_table(self, prep: "Prepared", own_lo: int, own_hi: int) -> torch.Tensor:
         """Per sequence-event slot: event index still unmatched after this shard (-1 = done)."""
@@ -354,10 +370,52 @@ class Engine:
         self.commit_frequency(res.freq_counts)
         return res, ls, ll
 
+    # documents larger than this are line-indexed on the GPU (k_nl_count/k_nl_write); smaller
+    # batches are split on the host while they are being packed (memchr, no extra pass)
+    GPU_SPLIT_BYTES = 32 << 20
+
+    def analyze_batch_json(self, logs_list: Sequence[str]) -> List[bytes]:
+        """Continuous-batching entry: many requests -> ONE device batch -> one JSON per request.
+
+        Requests become segments of a single line batch (windows never cross a segment, each
+        keeps its own N); frequency updates follow the batch (= arrival) order, which is the
+        deterministic version of the reference's concurrent-request interleaving.
+        """
+        t0 = time.time()
+        datas = [l.encode("utf-8", errors="surrogatepass") for l in logs_list]
+        if len(datas) == 1 and len(datas[0]) >= self.GPU_SPLIT_BYTES:
+            return [self.analyze_json(logs_list[0])]
+        doc_off = np.zeros(len(datas) + 1, np.int64)
+        np.cumsum([len(d) for d in datas], out=doc_off[1:])
+        blob = b"".join(datas)
+        hb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+        ls_h, ll_h, dl = N.split_docs(hb.ctypes.data, doc_off)
+        text, n = self.stage_text(blob)
+        ls = torch.from_numpy(ls_h).to(self.device)
+        ll = torch.from_numpy(ll_h).to(self.device)
+        segs = Segments.from_doc_offsets(dl, self.device)
+        res = self.run(text, n, ls, ll, segs, self.freq_carry())
+        self.commit_frequency(res.freq_counts)
+        ev_line = res.ev_line.cpu().numpy()
+        ev_pat = res.ev_pat.cpu().numpy()
+        score = res.score.cpu().numpy()
+        ev_seg = res.ev_seg.cpu().numpy()
+        bounds = np.searchsorted(ev_seg, np.arange(len(datas) + 1))
+        out = []
+        for d in range(len(datas)):
+            e0, e1 = bounds[d], bounds[d + 1]
+            ej = N.emit_events_json(hb.ctypes.data, ls_h, ll_h, int(dl[d]), int(dl[d + 1]), ev_line[e0:e1],
+                                    ev_pat[e0:e1], score[e0:e1], self.lib.pattern_json, self.lib.ctx_before,
+                                    self.lib.ctx_after)
+            out.append(self._wrap(ej, ev_pat[e0:e1], int(dl[d + 1] - dl[d]), t0))
+        return out
+
     def analyze_json(self, logs: str, library_ids: Optional[List] = None) -> bytes:
         """Full AnalysisResult as JSON bytes (camelCase result, snake_case matchedPattern)."""
-        t0 = time.time()
         data = logs.encode("utf-8", errors="surrogatepass")
+        if len(data) < self.GPU_SPLIT_BYTES:
+            return self.analyze_batch_json([logs])[0]
+        t0 = time.time()
         res, ls, ll = self.analyze_bytes(data)
         ev_line = res.ev_line.cpu().numpy()
         ev_pat = res.ev_pat.cpu().numpy()

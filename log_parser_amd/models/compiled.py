@@ -48,10 +48,37 @@ def _minimize_literals(lits: List[bytes]) -> List[bytes]:
     return out
 
 
-def _gram(lit: bytes) -> Tuple[int, int]:
-    g = min(4, len(lit))
-    key = int.from_bytes(lit[:g], "little")
-    return key, g
+# Approximate byte frequencies (percent) of lower-cased log text: English letter frequencies
+# scaled by the letter share, plus spaces, digits (timestamps, ids) and log punctuation. The
+# prefilter gram of a literal is the window with the smallest estimated frequency.
+_FREQ = {**{c: f * 0.55 for c, f in zip(b"etaoinshrdlcumwfgypbvkjxqz",
+                                         (12.7, 9.1, 8.2, 7.5, 7.0, 6.7, 6.3, 6.1, 6.0, 4.3, 4.0, 2.8, 2.8, 2.4,
+                                          2.4, 2.2, 2.0, 2.0, 1.9, 1.5, 1.0, 0.8, 0.15, 0.15, 0.1, 0.07))},
+         **{c: 1.2 for c in b"0123456789"}, ord(" "): 14.0, ord("."): 1.5, ord(":"): 1.5, ord("-"): 1.2,
+         ord("="): 0.6, ord("/"): 0.6, ord("_"): 0.5, ord("["): 0.4, ord("]"): 0.4, ord(","): 0.5,
+         ord("("): 0.3, ord(")"): 0.3, ord("\t"): 0.5}
+
+
+def _choose_grams(lits: List[bytes]) -> List[Tuple[int, int, int]]:
+    """Pick each literal's 4-byte window (key, g, offset): rarest estimated text frequency, with
+    a mild penalty for windows already shared by other literals (each sharer costs a compare)."""
+    import math
+    used: Dict[Tuple[int, int], int] = {}
+    out = []
+    for lit in lits:
+        g = min(4, len(lit))
+        best = None
+        for i in range(len(lit) - g + 1):
+            w = lit[i:i + g]
+            key = int.from_bytes(w, "little")
+            lp = sum(math.log2(_FREQ.get(c, 0.05) / 100.0) for c in w)
+            cost = (lp + 0.5 * math.log2(1 + used.get((key, g), 0)), i)
+            if best is None or cost < best[0]:
+                best = (cost, key, i)
+        _, key, off = best
+        used[(key, g)] = used.get((key, g), 0) + 1
+        out.append((key, g, off))
+    return out
 
 
 def _u32(x):
@@ -209,6 +236,11 @@ class CompiledLibrary:
                 # scanning all lines beats a short, unselective literal.
                 if d["anchored"] and lits and min(len(x) for x in lits) < 4:
                     lits = []
+                if ri.roles == {"context"}:
+                    # built-in context regexes are evaluated lazily, only on lines inside some
+                    # event's context window (k_feat), never by the whole-log match stage
+                    ri.literals = []
+                    continue
                 ri.literals = lits
                 if not lits:
                     self.scan_regs.append(i)
@@ -254,10 +286,11 @@ class CompiledLibrary:
         lit_reg = np.array([r for rr in lit_regs for r in rr] or [0], np.int32)
         grams: Dict[Tuple[int, int], List[int]] = {}
         gmask = 0
-        for i, l in enumerate(lits):
-            key, g = _gram(l)
+        lit_goff = np.zeros(max(len(lits), 1), np.int32)
+        for i, (key, g, off) in enumerate(_choose_grams(lits)):
             grams.setdefault((key, g), []).append(i)
             gmask |= 1 << g
+            lit_goff[i] = off
         bits = BLOOM_BITS
         bloom = np.zeros((1 << bits) // 32, np.uint32)
         H = 16
@@ -279,7 +312,7 @@ class CompiledLibrary:
             gram_lits.extend(ids)
         self.pf = dict(bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
                        gram_lits=np.array(gram_lits or [0], np.int32), lit_off=lit_off, lit_bytes=lit_bytes,
-                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask)
+                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, lit_goff=lit_goff)
 
     # ------------------------------------------------------------------ device tables
     def device_tables(self, device: torch.device) -> dict:
@@ -295,10 +328,11 @@ class CompiledLibrary:
         pf = self.pf
         t["pf_arrays"] = [T(pf["bloom"]), T(pf["ht_key"].view(np.int64)), T(pf["ht_val"]), T(pf["ht_cnt"]),
                           T(pf["gram_lits"]), T(pf["lit_off"]), T(pf["lit_bytes"]), T(pf["lit_reg_off"]),
-                          T(pf["lit_reg"])]
+                          T(pf["lit_reg"]), T(pf["lit_goff"])]
         a = t["pf_arrays"]
         t["pf"] = (a[0].data_ptr(), pf["bits"], a[1].data_ptr(), a[2].data_ptr(), a[3].data_ptr(), pf["ht_mask"],
-                   a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"])
+                   a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"],
+                   a[9].data_ptr())
         t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc)]
         d = t["dfa_arrays"]
         t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr())

@@ -73,13 +73,31 @@ def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Te
 
 
 def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) -> torch.Tensor:
+    """Literal prefilter -> (regex << 32 | line) candidates.
+
+    GPU: k_prefilter streams the text and stages bloom gram hits (position, gram length);
+    k_pf_verify then checks whole literals, one lane per hit (keeps the streaming kernel tight).
+    """
     nlines = line_start.numel()
     if text.is_cuda:
+        gcap = cap
+        while True:
+            gh = torch.empty(max(gcap, 1), dtype=torch.int64, device=text.device)
+            cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
+            N.prefilter_dev(text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines, gh.data_ptr(), gcap,
+                            cnt.data_ptr(), grid, _s(text))
+            c = int(cnt.item())
+            if c <= gcap:
+                gh = gh[:c]
+                break
+            gcap = c
+        if gh.numel() == 0:
+            return torch.empty(0, dtype=torch.int64, device=text.device)
         while True:
             cand = torch.empty(max(cap, 1), dtype=torch.int64, device=text.device)
             cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
-            N.prefilter_dev(text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines, cand.data_ptr(), cap,
-                            cnt.data_ptr(), grid, _s(text))
+            N.pf_verify_dev(gh.data_ptr(), gh.numel(), text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(),
+                            nlines, cand.data_ptr(), cap, cnt.data_ptr(), _s(text))
             c = int(cnt.item())
             if c <= cap:
                 return cand[:c]
@@ -126,6 +144,15 @@ def scan(text, line_start, line_len, regs: torch.Tensor, dfa_tuple, cap: int) ->
         if c <= cap:
             return out[:c]
         cap = c
+
+
+def context_features(lines: torch.Tensor, L: int, text, line_start, line_len, dfa_tuple) -> torch.Tensor:
+    """uint8 feature bits per line (ERR 1, WARN 2, STACK 4, EXC 8) for the given line ids; 0 elsewhere."""
+    feat = torch.zeros(max(L, 1), dtype=torch.uint8, device=text.device)
+    if lines.numel():
+        N.feat(lines.data_ptr(), lines.numel(), text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(),
+               dfa_tuple, feat.data_ptr(), _s(text), text.is_cuda)
+    return feat
 
 
 def score(ev_line, ev_pat, ev_seg, ev_freq, st_tuple, sp_tuple, with_factors: bool = False):

@@ -236,7 +236,7 @@ def to_python(pattern: str) -> str:
             out.append(body)
             continue
         if c == ".":
-            out.append(".") if sc["s"] else out.append(DOT_UNIX if sc["d"] else DOT)
+            out.append("(?s:.)") if sc["s"] else out.append(DOT_UNIX if sc["d"] else DOT)
             i += 1
             continue
         if c == "$":

@@ -1,0 +1,210 @@
+"""REST service: ``POST /parse`` (reference ``Parse.java:23-62``) plus health, metrics and admin.
+
+Behaviour kept from the reference:
+* ``POST /parse`` consumes/produces ``application/json`` (``Parse.java:41-44``);
+* body or ``pod`` null -> HTTP 400 ``{"error":"Invalid PodFailureData provided"}`` (``:45-49``);
+* otherwise 200 + ``AnalysisResult`` (``:60``); INFO log per request (``:51,55-58``).
+
+Additions: ``/health``, ``/ready``, Prometheus ``/metrics``,
+``/admin/frequency`` statistics/reset (the reference has the service methods but no endpoint),
+and a **continuous batcher**: concurrent requests arriving within ``engine.batch.max-wait-ms``
+are packed into one device batch (``Engine.analyze_batch_json``), so 10k concurrent small
+requests cost a few large kernel launches instead of 10k small ones.
+
+Deliberate differences: ``logs`` null -> 400 (the reference NPEs into a 500); a pod without
+``metadata`` is accepted (logged as ``<unknown>``); per-match logging is DEBUG, not INFO.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import threading
+import time
+from concurrent.futures import Future
+from typing import List, Optional
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, Response
+
+from ..engine import Engine
+from ..models.compiled import CompiledLibrary
+from ..models.library import load_pattern_directory
+from ..utils.config import Config
+from ..utils.metrics import Metrics
+
+log = logging.getLogger("log_parser_amd.server")
+
+INVALID = b'{"error":"Invalid PodFailureData provided"}'
+
+
+class Batcher:
+    """Packs concurrently submitted requests into one engine batch (one worker thread owns the GPU)."""
+
+    def __init__(self, engine: Engine, max_requests: int, max_bytes: int, max_wait_ms: float, metrics: Metrics):
+        self.engine = engine
+        self.max_requests = max_requests
+        self.max_bytes = max_bytes
+        self.max_wait = max_wait_ms / 1000.0
+        self.metrics = metrics
+        self._q: List[tuple] = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self._t = threading.Thread(target=self._loop, name="lp-batcher", daemon=True)
+        self._t.start()
+
+    def submit(self, logs: str) -> Future:
+        fut: Future = Future()
+        with self._cv:
+            self._q.append((logs, fut, time.perf_counter()))
+            self._cv.notify()
+        return fut
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._t.join(timeout=5)
+
+    def _take(self) -> List[tuple]:
+        with self._cv:
+            while not self._q and not self._stop:
+                self._cv.wait()
+            if self._stop and not self._q:
+                return []
+            deadline = self._q[0][2] + self.max_wait
+            while len(self._q) < self.max_requests and time.perf_counter() < deadline:
+                self._cv.wait(timeout=max(0.0, deadline - time.perf_counter()))
+            batch, size = [], 0
+            while self._q and len(batch) < self.max_requests:
+                item = self._q[0]
+                if batch and size + len(item[0]) > self.max_bytes:
+                    break
+                batch.append(self._q.pop(0))
+                size += len(item[0])
+            return batch
+
+    def _loop(self):
+        while True:
+            batch = self._take()
+            if not batch:
+                if self._stop:
+                    return
+                continue
+            try:
+                t0 = time.perf_counter()
+                outs = self.engine.analyze_batch_json([b[0] for b in batch])
+                self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
+                for (_, fut, _), o in zip(batch, outs):
+                    fut.set_result(o)
+            except Exception as e:  # noqa: BLE001 - propagate to every waiter
+                log.exception("batch failed")
+                for _, fut, _ in batch:
+                    if not fut.done():
+                        fut.set_exception(e)
+
+
+def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None) -> FastAPI:
+    config = config or Config.load()
+    app = FastAPI(title="log_parser_amd", version="0.1.0")
+    metrics = Metrics()
+    state = {"engine": engine, "batcher": None}
+
+    def _engine() -> Engine:
+        if state["engine"] is None:
+            sets = load_pattern_directory(config["pattern.directory"])
+            lib = CompiledLibrary(sets, config.scoring, max_dfa_states=int(config["engine.dfa-max-states"]))
+            log.info("compiled library: %s", lib.summary())
+            state["engine"] = Engine(lib, config)
+        return state["engine"]
+
+    def _batcher() -> Batcher:
+        if state["batcher"] is None:
+            state["batcher"] = Batcher(_engine(), int(config["engine.batch.max-requests"]),
+                                       int(config["engine.batch.max-bytes"]), float(config["engine.batch.max-wait-ms"]),
+                                       metrics)
+        return state["batcher"]
+
+    @app.on_event("startup")
+    def _startup():
+        _batcher()
+
+    @app.on_event("shutdown")
+    def _shutdown():
+        if state["batcher"] is not None:
+            state["batcher"].close()
+        path = config["engine.frequency.snapshot-path"]
+        if path and state["engine"] is not None:
+            state["engine"].freq.snapshot(path)
+
+    @app.post("/parse")
+    async def parse(request: Request):
+        t0 = time.perf_counter()
+        body = await request.body()
+        if len(body) > int(config["server.max-body-bytes"]):
+            return JSONResponse({"error": "request body too large"}, status_code=413)
+        try:
+            import json
+            data = json.loads(body) if body else None
+        except ValueError:
+            metrics.observe_request(400, time.perf_counter() - t0, 0)
+            return Response(INVALID, status_code=400, media_type="application/json")
+        if not isinstance(data, dict) or data.get("pod") is None:
+            metrics.observe_request(400, time.perf_counter() - t0, 0)
+            return Response(INVALID, status_code=400, media_type="application/json")
+        logs = data.get("logs")
+        if not isinstance(logs, str):
+            metrics.observe_request(400, time.perf_counter() - t0, 0)
+            return JSONResponse({"error": "PodFailureData.logs must be a string"}, status_code=400)
+        pod = data["pod"] if isinstance(data["pod"], dict) else {}
+        name = ((pod.get("metadata") or {}).get("name")) or "<unknown>"
+        log.info("Received analysis request for pod: %s", name)
+        fut = _batcher().submit(logs)
+        out = await asyncio.wrap_future(fut)
+        metrics.observe_request(200, time.perf_counter() - t0, len(logs))
+        log.info("Analysis complete for pod: %s.", name)
+        return Response(out, media_type="application/json")
+
+    @app.get("/health")
+    def health():
+        return {"status": "UP"}
+
+    @app.get("/ready")
+    def ready():
+        e = state["engine"]
+        if e is None:
+            return JSONResponse({"status": "DOWN", "reason": "library not loaded"}, status_code=503)
+        return {"status": "UP", "device": str(e.device), "library": e.lib.summary()}
+
+    @app.get("/metrics")
+    def prom():
+        e = state["engine"]
+        if e is not None:
+            metrics.set_frequency(e.freq.statistics())
+        return PlainTextResponse(metrics.render(), media_type="text/plain; version=0.0.4")
+
+    @app.get("/admin/frequency")
+    def freq_stats():
+        return _engine().freq.statistics()
+
+    @app.get("/admin/frequency/{pid}")
+    def freq_one(pid: str):
+        r = _engine().freq.get_pattern_frequency(pid)
+        if r is None:
+            return JSONResponse({"error": "unknown pattern id"}, status_code=404)
+        return r
+
+    @app.delete("/admin/frequency/{pid}")
+    def freq_reset(pid: str):
+        _engine().freq.reset(pid)
+        return {"reset": pid}
+
+    @app.delete("/admin/frequency")
+    def freq_reset_all():
+        _engine().freq.reset_all()
+        return {"reset": "all"}
+
+    @app.get("/admin/config")
+    def cfg():
+        return dict(config.values)
+
+    return app

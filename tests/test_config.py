@@ -1,0 +1,27 @@
+from log_parser_amd.utils.config import Config, env_name, parse_cli_overrides
+
+
+def test_defaults_match_reference_properties():
+    c = Config.load(environ={})
+    assert c["pattern.directory"] == "/shared/patterns"
+    p = c.scoring
+    assert (p.decay_constant, p.max_window) == (10.0, 100)
+    assert (p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold) == (0.2, 2.5, 0.5)
+    assert p.max_context_factor == 2.5
+    assert (p.freq_threshold, p.freq_max_penalty, p.freq_window_hours) == (10.0, 0.8, 1)
+
+
+def test_env_mapping_and_precedence(tmp_path):
+    props = tmp_path / "application.properties"
+    props.write_text("# comment\nscoring.proximity.max-window=50\nscoring.frequency.threshold = 3.5\n")
+    env = {"SCORING_FREQUENCY_THRESHOLD": "7"}
+    c = Config.load(properties_path=str(props), environ=env)
+    assert c.scoring.max_window == 50
+    assert c.scoring.freq_threshold == 7.0          # env beats properties
+    c2 = Config.load(overrides={"scoring.frequency.threshold": "9"}, properties_path=str(props), environ=env)
+    assert c2.scoring.freq_threshold == 9.0         # -D beats env
+    assert env_name("scoring.proximity.decay-constant") == "SCORING_PROXIMITY_DECAY_CONSTANT"
+
+
+def test_cli_overrides():
+    assert parse_cli_overrides(["-Dpattern.directory=/x", "foo", "-Da=b=c"]) == {"pattern.directory": "/x", "a": "b=c"}

@@ -1,0 +1,80 @@
+"""Correctness anchors from SURVEY §6.2 / BASELINE.md (the reference's code, not its doc errata)."""
+import math
+
+from log_parser_amd import golden
+from log_parser_amd.frequency import FrequencyState
+from log_parser_amd.utils.config import ScoringParams
+
+P = ScoringParams()
+
+
+def test_chronological_anchors():
+    assert golden.chronological_factor(0, 100, P) == 2.5
+    assert math.isclose(golden.chronological_factor(20, 100, P), 1.5)
+    assert math.isclose(golden.chronological_factor(50, 100, P), 1.0)
+    assert math.isclose(golden.chronological_factor(15, 100, P), 1.75)   # doc says ~2.1 (erratum)
+    assert math.isclose(golden.chronological_factor(99, 100, P), 0.51)
+
+
+def test_proximity_anchor():
+    assert math.isclose(1.0 + 0.8 * math.exp(-5 / 10.0), 1.48522, rel_tol=1e-5)
+
+
+def test_worked_example_code_consistent():
+    # 0.8 x 3.0 x chrono 1.75 x prox 1.4445 x 1.0 x ctx 2.0 = 12.1337 (doc's 21.17 is an arithmetic error)
+    assert math.isclose(0.8 * 3.0 * 1.75 * 1.4445 * 1.0 * 2.0, 12.1338, rel_tol=1e-4)
+    assert math.isclose(0.8 * 3.0 * 2.1 * 1.4 * 1.0 * 1.5, 10.584, rel_tol=1e-9)
+
+
+def test_context_factor_two_errors_one_stack():
+    lines = ["ERROR one", "ERROR two", "    at com.x.Y.z(Y.java:1)"]
+    # 1 + 0.4 + 0.4 + 0.1 + min(0.1, 0.5) = 2.0 (doc says ~1.5)
+    assert math.isclose(golden.context_factor(lines, P), 2.0)
+
+
+def test_frequency_penalty_schedule():
+    t = [1000.0]
+    tr = golden.FrequencyTracker(P, clock=lambda: t[0])
+    pens = []
+    for _ in range(25):
+        pens.append(tr.penalty("x"))
+        tr.record("x")
+    assert pens[:11] == [0.0] * 11
+    for k in range(11, 25):
+        assert math.isclose(pens[k], min(0.8, (k - 10) / 10.0))
+    t[0] += 3601
+    assert tr.penalty("x") == 0.0      # slid out of the 1 h window
+
+
+def test_split_lines_java_semantics():
+    assert golden.split_lines("") == [""]
+    assert golden.split_lines("\n") == []
+    assert golden.split_lines("\n\n\r\n") == []
+    assert golden.split_lines("a\r\nb\n\nc\n\n") == ["a", "b", "", "c"]
+    assert golden.split_lines("a\rb") == ["a\rb"]
+    assert golden.split_lines("\na") == ["", "a"]
+    assert golden.split_lines("a\r\r\n") == ["a\r"]
+
+
+def test_summary_rules():
+    mk = lambda s: {"matchedPattern": {"severity": s}}  # noqa: E731
+    assert golden.build_summary([])["highestSeverity"] == "NONE"
+    s = golden.build_summary([mk("low"), mk("HIGH"), mk("weird")])
+    assert s["highestSeverity"] == "HIGH" and s["severityDistribution"] == {"LOW": 1, "HIGH": 1, "WEIRD": 1}
+    assert golden.build_summary([mk("b"), mk("a")])["highestSeverity"] == "B"
+
+
+def test_frequency_state_snapshot(tmp_path):
+    t = [0.0]
+    st = FrequencyState(1, clock=lambda: t[0])
+    st.record_counts(["a", "b"], [3, 0])
+    st.record_counts(["a"], [2])
+    assert list(st.carry(["a", "b", "c"])) == [5, 0, 0]
+    p = str(tmp_path / "f.json")
+    st.snapshot(p)
+    st2 = FrequencyState(1, clock=lambda: t[0])
+    st2.restore(p)
+    assert list(st2.carry(["a"])) == [5]
+    t[0] = 3600.5
+    assert list(st2.carry(["a"])) == [0]
+    assert st.get_pattern_frequency("zzz") is None

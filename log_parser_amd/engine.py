@@ -156,7 +156,7 @@ class Engine:
     def _tick(self, timings, name, t0):
         if self.profile:
             if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
+                torch.cuda.current_stream(self.device).synchronize()   # not the ingest copy stream
             t1 = time.perf_counter()
             timings[name] = timings.get(name, 0.0) + (t1 - t0) * 1e3
             return t1

@@ -1,0 +1,99 @@
+"""REST API parity with the reference (Parse.java:23-62) + service extras."""
+import json
+import math
+import os
+
+import pytest
+import torch
+import yaml
+from fastapi.testclient import TestClient
+
+from log_parser_amd import golden
+from log_parser_amd.serve.app import create_app
+from log_parser_amd.utils.config import Config, ScoringParams
+from log_parser_amd.utils.synth import make_library, make_log
+
+
+@pytest.fixture(scope="module")
+def lib_dir(tmp_path_factory):
+    d = tmp_path_factory.mktemp("patterns")
+    sets, trig = make_library(30, seed=5, n_sets=3)
+    sub = d / "nested"
+    sub.mkdir()
+    for i, s in enumerate(sets):
+        target = (sub if i == 2 else d) / f"set{i}.{'yaml' if i else 'yml'}"
+        target.write_text(yaml.safe_dump(s.model_dump(by_alias=True, exclude_none=True)))
+    (d / "broken.yaml").write_text("patterns: [unclosed")
+    (d / "ignored.txt").write_text("not a pattern file")
+    return str(d), trig
+
+
+@pytest.fixture(scope="module")
+def client(lib_dir):
+    cfg = Config.load(overrides={"pattern.directory": lib_dir[0], "engine.device": "cpu",
+                                 "engine.batch.max-wait-ms": 1.0})
+    with TestClient(create_app(cfg)) as c:
+        yield c
+
+
+def test_invalid_requests(client):
+    for body in [b"", b"null", b'{"logs": "x"}', b'{"pod": null, "logs": "x"}', b"{not json"]:
+        r = client.post("/parse", content=body, headers={"content-type": "application/json"})
+        assert r.status_code == 400
+        assert r.json() == {"error": "Invalid PodFailureData provided"}
+
+
+def test_parse_matches_golden(client, lib_dir):
+    from log_parser_amd.models.library import load_pattern_directory
+    sets = load_pattern_directory(lib_dir[0])
+    assert len(sets) == 3   # broken.yaml skipped, .txt ignored, nested dir walked
+    logs = make_log(1500, lib_dir[1], seed=8, hit_rate=0.06)
+    client.delete("/admin/frequency")
+    r = client.post("/parse", json={"pod": {"metadata": {"name": "p1"}}, "logs": logs})
+    assert r.status_code == 200
+    res = r.json()
+    g = golden.analyze(logs, sets, ScoringParams(), golden.FrequencyTracker(ScoringParams()))
+    assert res["summary"] == g["summary"]
+    assert res["metadata"]["totalLines"] == g["metadata"]["totalLines"]
+    assert res["metadata"]["patternsUsed"] == g["metadata"]["patternsUsed"]
+    assert len(res["analysisId"]) == 36
+    assert len(res["events"]) == len(g["events"]) > 0
+    for a, b in zip(res["events"], g["events"]):
+        assert a["lineNumber"] == b["lineNumber"]
+        assert a["matchedPattern"] == b["matchedPattern"]
+        assert a["context"] == b["context"]
+        assert math.isclose(a["score"], b["score"], rel_tol=1e-12)
+
+
+def test_health_ready_metrics_admin(client):
+    assert client.get("/health").json()["status"] == "UP"
+    rd = client.get("/ready").json()
+    assert rd["status"] == "UP" and rd["library"]["patterns"] == 30
+    client.post("/parse", json={"pod": {}, "logs": "nothing to see"})
+    m = client.get("/metrics").text
+    assert "lp_requests_total" in m and "lp_batches_total" in m
+    stats = client.get("/admin/frequency").json()
+    assert isinstance(stats, dict)
+    assert client.delete("/admin/frequency").json() == {"reset": "all"}
+    assert client.get("/admin/frequency/nope").status_code == 404
+
+
+def test_concurrent_requests_are_batched(client, lib_dir):
+    import concurrent.futures as cf
+    logs = [make_log(200, lib_dir[1], seed=100 + i, hit_rate=0.05) for i in range(24)]
+    with cf.ThreadPoolExecutor(8) as ex:
+        rs = list(ex.map(lambda l: client.post("/parse", json={"pod": {"metadata": {"name": "x"}}, "logs": l}), logs))
+    assert all(r.status_code == 200 for r in rs)
+    m = client.get("/metrics").text
+    batches = int([l for l in m.splitlines() if l.startswith("lp_batches_total")][0].split()[1])
+    reqs = int([l for l in m.splitlines() if l.startswith("lp_batched_requests_total")][0].split()[1])
+    assert reqs >= 24 and batches <= reqs
+
+
+def test_missing_pattern_directory_tolerated(tmp_path):
+    cfg = Config.load(overrides={"pattern.directory": str(tmp_path / "nope"), "engine.device": "cpu"})
+    with TestClient(create_app(cfg)) as c:
+        r = c.post("/parse", json={"pod": {}, "logs": "a\nb\n"})
+        assert r.status_code == 200
+        j = r.json()
+        assert j["events"] == [] and j["summary"]["highestSeverity"] == "NONE" and j["metadata"]["totalLines"] == 2

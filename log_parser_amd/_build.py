@@ -54,7 +54,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
         headers = _headers()
         objs = []
         procs = []
-        base = ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__"]
+        # -ffp-contract=off: Java double arithmetic never fuses a*b+c; keep GPU == CPU == reference
+        base = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__"]
         for rel, kind in SOURCES:
             src = os.path.join(CSRC, rel)
             if not os.path.exists(src):

@@ -72,6 +72,24 @@ def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Te
     return starts[:L].contiguous(), lens[:L].to(torch.int32).contiguous()
 
 
+def split_chunk_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Line index of a chunk made of complete lines (streaming): no trailing-empty trimming; a
+    final '\\n' terminates the last line instead of opening an empty one."""
+    dev = text.device
+    nl = newline_positions(text, nbytes)
+    zero = torch.zeros(1, dtype=torch.int64, device=dev)
+    starts = torch.cat([zero, nl + 1])
+    ends = torch.cat([nl, torch.full((1,), nbytes, dtype=torch.int64, device=dev)])
+    if nl.numel():
+        prev = text[(nl - 1).clamp(min=0)]
+        cr = (nl > starts[:-1]) & (prev == 13)
+        ends[:-1] -= cr.to(torch.int64)
+    L = starts.numel()
+    if nl.numel() and int(nl[-1].item()) == nbytes - 1:
+        L -= 1
+    return starts[:L].contiguous(), (ends - starts)[:L].to(torch.int32).contiguous()
+
+
 def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) -> torch.Tensor:
     """Literal prefilter -> (regex << 32 | line) candidates.
 

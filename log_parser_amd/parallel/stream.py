@@ -1,0 +1,267 @@
+"""Long-log streaming ("sequence parallel" for logs; BASELINE config #4).
+
+A log far larger than one request (100 GB, 1B lines) is processed in line-aligned chunks of
+``engine.chunk-bytes``. A chunk is handled exactly like a data-parallel shard that runs after
+all previous ones (parallel/dp.py), so the result equals the single-pass reference semantics:
+
+* halos: ``CompiledLibrary.halo`` lines of the previous / next chunk are staged with each chunk
+  (proximity ≤ max-window, context lines, ±5 sequence window);
+* frequency: the running per-id match count of earlier chunks is the scan carry;
+* backward sequence search: a running per-slot state composed with each chunk's chain table
+  (``state'[j] = 1 if f[j] < 0 else state[slot(q, f[j])]``) replaces the unbounded scan;
+* chronological factor: needs the total line count N, unknown until the end, so the chunk pass
+  keeps every event's factors (k_score with factors) and the final pass recomputes
+  ``conf*sev*chrono*prox*temp*ctx*(1-pen)`` in the reference's left-to-right order — one pass
+  over the bytes, no re-read.
+
+Ingest is pipelined: a host thread stages chunk k+1 into pinned memory while the GPU analyses
+chunk k; the H2D copy runs on its own HIP stream.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import numpy as np
+import torch
+
+from ..engine import Engine, Segments
+from ..ops import kernels as K
+
+
+def _eff_end(src) -> int:
+    """End of the content that survives Java's trailing-empty-line removal."""
+    n = len(src)
+    i = n
+    while i > 0 and src[i - 1] == 10:
+        i -= 1
+        if i > 0 and src[i - 1] == 13:
+            i -= 1
+    return i
+
+
+class RepeatBuffer:
+    """A virtual buffer: ``block`` repeated to ``total`` bytes (synthetic multi-GB streams)."""
+
+    def __init__(self, block: bytes, total: int):
+        self.block = block
+        self.total = total
+
+    def __len__(self):
+        return self.total
+
+    def __getitem__(self, idx):
+        if isinstance(idx, int):
+            return self.block[idx % len(self.block)]
+        start, stop, _ = idx.indices(self.total)
+        if start >= stop:
+            return b""
+        B = len(self.block)
+        out = bytearray()
+        pos = start
+        while pos < stop:
+            o = pos % B
+            take = min(B - o, stop - pos)
+            out += self.block[o:o + take]
+            pos += take
+        return bytes(out)
+
+    def find(self, sub: bytes, start: int) -> int:
+        B = len(self.block)
+        pos = start
+        while pos < self.total:
+            o = pos % B
+            j = self.block.find(sub, o)
+            if j >= 0 and pos + (j - o) < self.total:
+                return pos + (j - o)
+            pos += B - o
+        return -1
+
+    def rfind(self, sub: bytes, start: int, end: int) -> int:
+        B = len(self.block)
+        pos = end
+        while pos > start:
+            o = (pos - 1) % B
+            j = self.block.rfind(sub, 0, o + 1)
+            if j >= 0:
+                r = pos - 1 - (o - j)
+                return r if r >= start else -1
+            pos -= o + 1
+        return -1
+
+
+@dataclass
+class StreamResult:
+    total_lines: int
+    n_events: int
+    summary: dict
+    topk_score: np.ndarray
+    topk_line: np.ndarray
+    topk_pat: np.ndarray
+    chunks: int
+    bytes: int
+    seconds: float
+    events: Optional[tuple] = None          # (global line int64, pattern int32, score f64) if kept
+    timings: dict = field(default_factory=dict)
+
+
+class StreamAnalyzer:
+    def __init__(self, engine: Engine, chunk_bytes: Optional[int] = None, topk: int = 100,
+                 keep_events: bool = True):
+        self.engine = engine
+        self.chunk_bytes = int(chunk_bytes or engine.config["engine.chunk-bytes"])
+        self.topk = topk
+        self.keep_events = keep_events
+        lib = engine.lib
+        off = lib.seq_ev_off
+        e0 = np.zeros(max(lib.n_seq_events, 1), np.int64)
+        for q in range(off.size - 1):
+            e0[off[q]:off[q + 1]] = off[q]
+        self.slot_e0 = torch.from_numpy(e0).to(engine.device)
+
+    # ------------------------------------------------------------------ chunk planning
+    def _plan(self, src, eff: int):
+        H = self.engine.lib.halo
+        pos = 0
+        while pos < eff or (pos == 0 and eff == 0):
+            end = min(eff, pos + self.chunk_bytes)
+            if end < eff:
+                j = src.find(b"\n", end - 1)
+                end = eff if (j < 0 or j + 1 > eff) else j + 1
+            r_end, rh = end, 0
+            while rh < H and r_end < eff:
+                j = src.find(b"\n", r_end)
+                r_end = eff if (j < 0 or j + 1 > eff) else j + 1
+                rh += 1
+            l_start, lh = pos, 0
+            while lh < H and l_start > 0:
+                j = src.rfind(b"\n", 0, l_start - 1)
+                l_start = 0 if j < 0 else j + 1
+                lh += 1
+            yield l_start, pos, end, r_end, lh, rh
+            if end >= eff:
+                break
+            pos = end
+
+    def _producer(self, src, eff, q: "queue.Queue"):
+        try:
+            for l_start, pos, end, r_end, lh, rh in self._plan(src, eff):
+                data = src[l_start:r_end]
+                n = len(data)
+                pinned = torch.empty(K.padded_len(n), dtype=torch.uint8,
+                                     pin_memory=self.engine.device.type == "cuda")
+                if n:
+                    pinned[:n].copy_(torch.frombuffer(bytearray(data) if isinstance(data, bytes) else data,
+                                                      dtype=torch.uint8))
+                pinned[n:].zero_()
+                q.put((pinned, n, lh, rh))
+            q.put(None)
+        except BaseException as e:  # noqa: BLE001
+            q.put(e)
+
+    # ------------------------------------------------------------------ run
+    def run(self, src, on_chunk: Optional[Callable] = None) -> StreamResult:
+        t0 = time.perf_counter()
+        eng = self.engine
+        lib = eng.lib
+        dev = eng.device
+        eff = _eff_end(src)
+        if eff == 0 and len(src) > 0 and src.find(b"\n", 0) >= 0:
+            empty = {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
+            z = np.zeros(0)
+            return StreamResult(0, 0, empty, z, z.astype(np.int64), z.astype(np.int64), 0, len(src), 0.0)
+        q: "queue.Queue" = queue.Queue(maxsize=2)
+        th = threading.Thread(target=self._producer, args=(src, eff, q), daemon=True)
+        th.start()
+        copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        freq_carry = eng.freq_carry()
+        nkeys = len(lib.freq_ids)
+        run_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
+        seq_state = torch.zeros(max(lib.n_seq_events, 1), dtype=torch.uint8, device=dev)
+        line_base = 0
+        ev_gl, ev_pat, ev_fac = [], [], []
+        chunks = 0
+        nbytes_total = 0
+
+        def fetch():
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            if item is None:
+                return None
+            pinned, n, lh, rh = item
+            if copy_stream is not None:
+                with torch.cuda.stream(copy_stream):
+                    d = torch.empty(pinned.numel(), dtype=torch.uint8, device=dev)
+                    d.copy_(pinned, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(copy_stream)
+                return d, n, lh, rh, ev, pinned
+            return pinned, n, lh, rh, None, pinned
+
+        nxt = fetch()
+        while nxt is not None:
+            text, n, lh, rh, ev, _pin = nxt
+            if ev is not None:
+                torch.cuda.current_stream(dev).wait_event(ev)
+                text.record_stream(torch.cuda.current_stream(dev))
+            nxt = fetch()                      # stage + copy the next chunk meanwhile
+            ls, ll = K.split_chunk_lines(text, n)
+            L = ls.numel()
+            own_lo, own_hi = lh, L - rh
+            i32 = lambda v: torch.tensor([v], dtype=torch.int32, device=dev)  # noqa: E731
+            i64 = lambda v: torch.tensor([v], dtype=torch.int64, device=dev)  # noqa: E731
+            segs = Segments(i32(0), i32(L), i32(own_lo), i32(own_hi), i64(line_base - own_lo), i64(1 << 62))
+            prep = eng.prepare(text, n, ls, ll, segs)
+            chain = eng.seq_chain_table(prep, own_lo, own_hi)
+            res = eng.finish(prep, segs, freq_carry + run_counts, seq_state, with_factors=True)
+            if lib.n_seq_events:
+                k = chain.to(torch.int64)
+                prev = seq_state[(self.slot_e0 + k.clamp(min=0))]
+                seq_state = torch.where(k < 0, torch.ones_like(seq_state), prev)
+            run_counts = run_counts + prep.freq_counts[:max(nkeys, 1)]
+            if res.ev_line.numel():
+                ev_gl.append(res.ev_line.to(torch.int64) - own_lo + line_base)
+                ev_pat.append(res.ev_pat)
+                ev_fac.append(res.factors)
+            if on_chunk is not None:
+                on_chunk(chunks, line_base, own_hi - own_lo)
+            line_base += own_hi - own_lo
+            nbytes_total += n
+            chunks += 1
+        th.join()
+        N = max(line_base, 1)
+        if ev_gl:
+            gl = torch.cat(ev_gl)
+            pat = torch.cat(ev_pat)
+            fac = torch.cat(ev_fac)
+            score = self._final_scores(gl, fac, N)
+        else:
+            gl = torch.zeros(0, dtype=torch.int64, device=dev)
+            pat = torch.zeros(0, dtype=torch.int32, device=dev)
+            score = torch.zeros(0, dtype=torch.float64, device=dev)
+        eng.commit_frequency(run_counts[:nkeys])
+        k = min(self.topk, score.numel())
+        v, idx = torch.topk(score, k) if k else (score[:0], torch.zeros(0, dtype=torch.int64, device=dev))
+        pc = torch.bincount(pat.long(), minlength=len(lib.patterns)) if pat.numel() else None
+        pat_h = pat.cpu().numpy()
+        summary = eng.summary(pat_h) if pc is not None else eng.summary(np.zeros(0, np.int32))
+        out = StreamResult(line_base, int(score.numel()), summary, v.cpu().numpy(), gl[idx].cpu().numpy(),
+                           pat[idx].cpu().numpy(), chunks, nbytes_total, time.perf_counter() - t0)
+        if self.keep_events:
+            out.events = (gl.cpu().numpy(), pat_h, score.cpu().numpy())
+        return out
+
+    def _final_scores(self, gl: torch.Tensor, fac: torch.Tensor, N: int) -> torch.Tensor:
+        """Reference product order with the true chronological factor (ScoringService.java:102-151)."""
+        p = self.engine.params
+        pos = gl.to(torch.float64) / float(N)
+        e, m, t = p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold
+        early = 1.5 + (e - pos) * ((m - 1.5) / e)
+        mid = 1.0 + (t - pos) * (0.5 / (t - e))
+        late = 0.5 + (1.0 - pos)
+        chrono = torch.where(pos <= e, early, torch.where(pos <= t, mid, late))
+        return fac[:, 0] * fac[:, 1] * chrono * fac[:, 3] * fac[:, 4] * fac[:, 5] * (1.0 - fac[:, 6])

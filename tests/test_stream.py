@@ -1,0 +1,58 @@
+"""Chunked streaming (parallel/stream.py) == single-pass analysis of the whole log."""
+import numpy as np
+import pytest
+import torch
+
+from log_parser_amd.engine import Engine, Segments
+from log_parser_amd.models.compiled import CompiledLibrary
+from log_parser_amd.ops import kernels as K
+from log_parser_amd.parallel.stream import RepeatBuffer, StreamAnalyzer
+from log_parser_amd.utils.config import Config, ScoringParams
+from log_parser_amd.utils.synth import make_library, make_log
+
+
+def _eng(lib, dev="cpu"):
+    return Engine(lib, Config.load(overrides={"engine.device": dev}), device=torch.device(dev))
+
+
+@pytest.mark.parametrize("chunk,crlf", [(4096, 0.0), (20000, 0.3), (1 << 20, 0.0)])
+def test_stream_equals_single_pass(chunk, crlf):
+    sets, trig = make_library(40, seed=41, sequence_rate=0.8)
+    lib = CompiledLibrary(sets, ScoringParams())
+    logs = make_log(2500, trig, seed=42, hit_rate=0.08, crlf_rate=crlf) + "\n\n\r\n"
+    data = logs.encode()
+    e1 = _eng(lib)
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    ls, ll = K.split_lines(t, len(data))
+    ref = e1.run(t, len(data), ls, ll, Segments.single(ls.numel(), t.device), e1.freq_carry())
+    e2 = _eng(lib)
+    out = StreamAnalyzer(e2, chunk_bytes=chunk, topk=7).run(data)
+    assert out.total_lines == ls.numel()
+    if chunk < len(data):
+        assert out.chunks > 1
+    gl, pat, score = out.events
+    np.testing.assert_array_equal(gl, ref.ev_line.numpy())
+    np.testing.assert_array_equal(pat, ref.ev_pat.numpy())
+    np.testing.assert_allclose(score, ref.score.numpy(), rtol=1e-15, atol=0)
+    np.testing.assert_allclose(out.topk_score, np.sort(ref.score.numpy())[::-1][:7], rtol=1e-15)
+    assert out.summary == e1.summary(ref.ev_pat.numpy())
+    e1.commit_frequency(ref.freq_counts)   # frequency state advanced identically
+    assert e1.freq.statistics() == e2.freq.statistics()
+
+
+def test_stream_edge_inputs():
+    sets, trig = make_library(5, seed=1)
+    lib = CompiledLibrary(sets, ScoringParams())
+    for s, n in [(b"", 1), (b"\n\n", 0), (b"abc", 1), (b"a\n\nb\n\n", 3), (b"a\r\r\n", 1)]:
+        assert StreamAnalyzer(_eng(lib), chunk_bytes=2).run(s).total_lines == n, s
+
+
+def test_repeat_buffer():
+    blk = b"ab\ncd\n\nxyz\n"
+    rb = RepeatBuffer(blk, 100)
+    full = (blk * 20)[:100]
+    assert rb[3:57] == full[3:57] and len(rb) == 100 and rb[5] == full[5]
+    for st in range(0, 100, 7):
+        assert rb.find(b"\n", st) == full.find(b"\n", st)
+        assert rb.rfind(b"\n", 0, st) == full.rfind(b"\n", 0, st)

@@ -216,6 +216,20 @@ PYBIND11_MODULE(_lpnative, m) {
     else feat_host(P<const int32_t>(lines), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(feat));
   });
 
+  m.def("nfa", [](uint64_t groups, uint64_t glist, int ng, int ncls, uint64_t lines, int64_t nsel, uint64_t text,
+                  uint64_t ls, uint64_t ll, uint64_t feat, uint64_t hits, int64_t cap, uint64_t count, uint64_t s,
+                  bool dev) -> int64_t {
+    if (dev) {
+      nfa_mfma_dev(P<const uint64_t>(groups), P<const int32_t>(glist), ng, ncls, P<const int32_t>(lines), nsel,
+                   P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), P<uint8_t>(feat),
+                   P<int64_t>(hits), cap, P<unsigned long long>(count), s);
+      return -1;
+    }
+    return nfa_host(P<const uint64_t>(groups), P<const int32_t>(glist), ng, P<const int32_t>(lines), nsel,
+                    P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), P<uint8_t>(feat),
+                    P<int64_t>(hits), cap);
+  });
+
   // ---- JSON result emitter
   m.def("emit_events_json", &emit_events_json_py);
 }

@@ -43,3 +43,12 @@ void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev
                 const ScoreTables& T, const ScoreParams& S, double* out, double* factors);
 
 }  // namespace lp
+
+namespace lp {
+void nfa_mfma_dev(const uint64_t* groups, const int32_t* group_list, int ngroups, int ncls, const int32_t* lines,
+                  int64_t nsel, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
+                  uint8_t* feat, int64_t* hits, int64_t cap, unsigned long long* count, uint64_t stream);
+int64_t nfa_host(const uint64_t* groups, const int32_t* group_list, int ngroups, const int32_t* lines, int64_t nsel,
+                 const uint8_t* text, const int64_t* line_start, const int32_t* line_len, uint8_t* feat,
+                 int64_t* hits, int64_t cap);
+}  // namespace lp

@@ -123,6 +123,8 @@ class Engine:
         self.freq = freq or FrequencyState(self.params.freq_window_hours)
         self.cand_cap = int(self.config["engine.candidate-capacity"])
         self.profile = False
+        # context features: "mfma" = NFA state-transition GEMM (k_nfa_mfma), "dfa" = 4 byte DFAs (k_feat)
+        self.context_engine = str(self.config["engine.context-engine"])
         self.tabs = library.device_tables(self.device)
         p = self.params
         self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
@@ -174,6 +176,9 @@ class Engine:
             parts.append(cand[ok.bool()])
         t = self._tick(timings, "verify", t)
         parts.append(K.scan(text, ls, ll, self.tabs["scan_regs"], self.tabs["dfa"], max(1024, ls.numel())))
+        for ncls, glist in self.tabs["nfa_scan_lists"].items():       # DFA blow-up regexes: MFMA NFA
+            if glist.numel():
+                parts.append(K.nfa_scan(self.tabs["nfa_tables"], glist, ncls, text, ls, ll, max(1024, ls.numel())))
         t = self._tick(timings, "scan", t)
         if self.lib.host_regs:
             parts.append(self._host_fallback(text, nbytes, ls, ll, host_lines))
@@ -288,6 +293,9 @@ class Engine:
         diff.index_add_(0, b, -one)
         need = torch.cumsum(diff[:L], 0) > 0
         lines = torch.nonzero(need).flatten().to(torch.int32)
+        if self.context_engine == "mfma":
+            return K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],
+                                  self.lib.nfa_group_ncls[0])
         return K.context_features(lines, L, text, ls, ll, self.tabs["dfa"])
 
     def seq_chain_table(self, prep: "Prepared", own_lo: int, own_hi: int) -> torch.Tensor:

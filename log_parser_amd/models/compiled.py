@@ -30,6 +30,7 @@ import torch
 from ..golden import CONTEXT_REGEXES, SEVERITY_MULTIPLIERS, severity_key
 from ..native import N
 from ..utils.config import ScoringParams
+from .nfa import build_group, fits_group, pack_groups
 from .schema import Pattern, PatternSet, pattern_to_json
 
 log = logging.getLogger("log_parser_amd.compiled")
@@ -216,10 +217,14 @@ class CompiledLibrary:
         toff = aoff = 0
         self.scan_regs: List[int] = []
         self.host_regs: List[int] = []
+        nfa_members: List[Tuple[int, dict]] = []
+        ctx_members: List[Tuple[int, dict]] = []
         for i, ri in enumerate(self.regexes):
             d = N.compile_regex(ri.pattern, self.max_dfa_states, 4096)
             ri.kind = d["kind"]
             ri.error = d["error"]
+            if i < 4:
+                ctx_members.append((i, d))
             if ri.kind == KIND_DFA:
                 ri.nstates = d["nstates"]
                 nc = d["nclasses"]
@@ -249,6 +254,9 @@ class CompiledLibrary:
                 bytemaps.append(np.zeros(256, np.uint8))
                 if ri.kind == KIND_INVALID:
                     log.error("invalid regex %r: %s (never matches)", ri.pattern, ri.error)
+                elif ri.kind == KIND_NFA and fits_group(d):
+                    # DFA blow-up: simulate the NFA with the MFMA state-transition kernel
+                    nfa_members.append((i, d))
                 else:
                     log.warning("regex %r uses the host fallback (%s)", ri.pattern, ri.error)
                     self.host_regs.append(i)
@@ -256,6 +264,13 @@ class CompiledLibrary:
         if not trans:
             trans.append(np.zeros(1, np.uint16))
             accs.append(np.zeros(1, np.uint8))
+        # NFA groups for the MFMA kernel: group 0 = the 4 context regexes, then DFA-blow-up regexes
+        groups = [ctx_members] + pack_groups(nfa_members)
+        tabs, ncls = zip(*[build_group(g) for g in groups])
+        self.nfa_tables = np.concatenate(tabs)
+        self.nfa_group_ncls = list(ncls)
+        self.nfa_scan_groups = list(range(1, len(groups)))
+        self.nfa_regs = [rid for g in groups[1:] for rid, _ in g]
         self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
         self.dfa_bytemap = np.concatenate(bytemaps)
         self.dfa_trans = np.concatenate(trans)
@@ -349,6 +364,10 @@ class CompiledLibrary:
         t["prim_cnt"] = T(np.diff(self.prim_off))
         t["freq_key"] = T(self.freq_key)
         t["is_primary"] = T(np.diff(self.prim_off) > 0)
+        t["nfa_tables"] = T(self.nfa_tables.view(np.int64))
+        t["nfa_ctx_list"] = T(np.zeros(1, np.int32))
+        t["nfa_scan_lists"] = {k: T(np.array([g for g in self.nfa_scan_groups if self.nfa_group_ncls[g] == k], np.int32))
+                               for k in (1, 2, 3)}
         self._device_cache[key] = t
         return t
 
@@ -362,6 +381,7 @@ class CompiledLibrary:
             "patterns": len(self.patterns), "pattern_sets": len(self.pattern_sets), "regexes": len(self.regexes),
             "dfa": kinds.count(KIND_DFA), "host_fallback": len(self.host_regs),
             "invalid": kinds.count(KIND_INVALID), "scan_all": len(self.scan_regs), "literals": len(self.literals),
+            "nfa_mfma": len(self.nfa_regs), "nfa_groups": len(self.nfa_scan_groups),
             "halo": self.halo,
         }
 

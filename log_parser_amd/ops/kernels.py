@@ -186,3 +186,34 @@ def score(ev_line, ev_pat, ev_seg, ev_freq, st_tuple, sp_tuple, with_factors: bo
         N.score_host(ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_freq.data_ptr(), n, st_tuple,
                      sp_tuple, out.data_ptr(), _p(fac))
     return out, fac
+
+
+def nfa_features(groups: torch.Tensor, lines: torch.Tensor, L: int, text, line_start, line_len,
+                 group_list: torch.Tensor, ncls: int) -> torch.Tensor:
+    """Context features via the MFMA NFA kernel (group 0 = the 4 context regexes): uint8 bits per line."""
+    feat = torch.zeros(max(L, 1), dtype=torch.uint8, device=text.device)
+    if lines.numel():
+        N.nfa(groups.data_ptr(), group_list.data_ptr(), 1, ncls, lines.data_ptr(), lines.numel(), text.data_ptr(),
+              line_start.data_ptr(), line_len.data_ptr(), feat.data_ptr(), 0, 0, 0, _s(text), text.is_cuda)
+    return feat
+
+
+def nfa_scan(groups: torch.Tensor, group_list: torch.Tensor, ncls: int, text, line_start, line_len,
+             cap: int) -> torch.Tensor:
+    """All lines x NFA groups -> (regex << 32 | line) hits (MFMA kernel on GPU, bitset twin on CPU)."""
+    nl = line_start.numel()
+    if group_list.numel() == 0 or nl == 0:
+        return torch.empty(0, dtype=torch.int64, device=text.device)
+    while True:
+        out = torch.empty(max(cap, 1), dtype=torch.int64, device=text.device)
+        if text.is_cuda:
+            cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
+            N.nfa(groups.data_ptr(), group_list.data_ptr(), group_list.numel(), ncls, 0, nl, text.data_ptr(),
+                  line_start.data_ptr(), line_len.data_ptr(), 0, out.data_ptr(), cap, cnt.data_ptr(), _s(text), True)
+            c = int(cnt.item())
+        else:
+            c = N.nfa(groups.data_ptr(), group_list.data_ptr(), group_list.numel(), ncls, 0, nl, text.data_ptr(),
+                      line_start.data_ptr(), line_len.data_ptr(), 0, out.data_ptr(), cap, 0, 0, False)
+        if c <= cap:
+            return out[:c]
+        cap = c

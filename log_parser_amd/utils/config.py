@@ -44,6 +44,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.candidate-capacity": (1 << 22, int),
     # max DFA states per regex before it is routed to the NFA (MFMA) path
     "engine.dfa-max-states": (2048, int),
+    # context-feature engine: "mfma" (NFA state-transition GEMM on matrix cores) or "dfa"
+    "engine.context-engine": ("dfa", str),
     # continuous batching
     "engine.batch.max-requests": (256, int),
     "engine.batch.max-bytes": (64 << 20, int),

@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmarks for the five BASELINE.json configs (the headline is ../bench.py = config 3).
+
+  rest        config 1: 10k-line log, 20 YAML patterns, CPU-only POST /parse (plumbing), p50 latency
+  single      config 2: 1M-line log, 256 patterns, 1 GPU (resident and with PCIe ingest)
+  stream      config 4: long stream (default 1B lines, scale with --lines), 4k patterns with secondary
+              + sequence patterns, chunked through HBM with carries (parallel/stream.py)
+  concurrent  config 5: 10k concurrent /parse requests of mixed sizes through the continuous batcher;
+              p50 / p99 request latency and aggregate lines/s
+  golden      comparator (b) of BASELINE.md: this repo's pure-Python golden model (the reference
+              publishes no numbers and no JVM is available here), lines/s on config-1 data
+
+Every mode prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from log_parser_amd import golden  # noqa: E402
+from log_parser_amd.engine import Engine, Segments  # noqa: E402
+from log_parser_amd.models.compiled import CompiledLibrary  # noqa: E402
+from log_parser_amd.ops import kernels as K  # noqa: E402
+from log_parser_amd.utils.config import Config, ScoringParams  # noqa: E402
+from log_parser_amd.utils.synth import make_library, make_log  # noqa: E402
+
+
+def _dev(args):
+    if args.device == "auto":
+        return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    return torch.device(args.device)
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def _engine(n_patterns, dev, seed=7):
+    sets, trig = make_library(n_patterns, seed=seed)
+    lib = CompiledLibrary(sets, ScoringParams())
+    return Engine(lib, Config.load(overrides={"engine.device": str(dev)}), device=dev), sets, trig
+
+
+def mode_rest(args):
+    from fastapi.testclient import TestClient
+    import tempfile
+    import yaml
+    from log_parser_amd.serve.app import create_app
+    sets, trig = make_library(20, seed=3, n_sets=2)
+    d = tempfile.mkdtemp()
+    for i, s in enumerate(sets):
+        with open(os.path.join(d, f"s{i}.yaml"), "w") as f:
+            yaml.safe_dump(s.model_dump(by_alias=True, exclude_none=True), f)
+    logs = make_log(10_000, trig, seed=4, hit_rate=0.01)
+    cfg = Config.load(overrides={"pattern.directory": d, "engine.device": "cpu"})
+    lat = []
+    with TestClient(create_app(cfg)) as c:
+        body = {"pod": {"metadata": {"name": "bench"}}, "logs": logs}
+        for _ in range(3):
+            c.post("/parse", json=body)
+        for _ in range(args.requests):
+            t = time.perf_counter()
+            r = c.post("/parse", json=body)
+            lat.append(time.perf_counter() - t)
+            assert r.status_code == 200
+    lat = np.array(lat)
+    print(json.dumps({"config": "rest-10k-lines-20-patterns-cpu", "p50_ms": round(float(np.median(lat)) * 1e3, 3),
+                      "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 3),
+                      "lines_per_s": round(10_000 / float(np.median(lat)), 1), "requests": args.requests}))
+
+
+def mode_single(args):
+    dev = _dev(args)
+    eng, _, trig = _engine(256, dev)
+    data = make_log(args.lines, trig, seed=5, hit_rate=0.004, aux_rate=0.01, stack_rate=0.01).encode()
+    text, n = eng.stage_text(data)
+    ls, ll = K.split_lines(text, n)
+    segs = Segments.single(ls.numel(), dev)
+
+    def once(resident: bool):
+        t = text
+        if not resident:
+            t, _ = eng.stage_text(data)
+        a, b = K.split_lines(t, n)
+        res = eng.run(t, n, a, b, segs, eng.freq_carry())
+        eng.commit_frequency(res.freq_counts)
+        return res
+
+    out = {"config": f"single-{args.lines}-lines-256-patterns", "device": str(dev), "bytes": n}
+    for resident in (True, False):
+        for _ in range(2):
+            once(resident)
+        _sync(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = once(resident)
+        _sync(dev)
+        dt = (time.perf_counter() - t0) / args.steps
+        out["resident" if resident else "with_h2d_from_pageable"] = {
+            "ms": round(dt * 1e3, 3), "lines_per_s": round(ls.numel() / dt, 1), "events": int(res.score.numel())}
+    print(json.dumps(out))
+
+
+def mode_stream(args):
+    from log_parser_amd.parallel.stream import RepeatBuffer, StreamAnalyzer
+    dev = _dev(args)
+    eng, _, trig = _engine(args.patterns, dev)
+    block = make_log(200_000, trig, seed=6, hit_rate=0.004, aux_rate=0.01, stack_rate=0.01).encode()
+    lines_per_block = block.count(b"\n")
+    total = len(block) * max(1, args.lines // lines_per_block)
+    src = RepeatBuffer(block, total)
+    sa = StreamAnalyzer(eng, chunk_bytes=args.chunk_mb << 20, topk=100, keep_events=False)
+    t0 = time.perf_counter()
+    res = sa.run(src)
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"config": f"stream-{res.total_lines}-lines-{args.patterns}-patterns", "device": str(dev),
+                      "seconds": round(dt, 3), "lines_per_s": round(res.total_lines / dt, 1),
+                      "bytes": res.bytes, "GB_per_s": round(res.bytes / dt / 1e9, 3), "chunks": res.chunks,
+                      "events": res.n_events, "summary": res.summary}))
+
+
+def mode_concurrent(args):
+    from log_parser_amd.serve.app import Batcher
+    from log_parser_amd.utils.metrics import Metrics
+    dev = _dev(args)
+    eng, _, trig = _engine(1000, dev)
+    rng = np.random.default_rng(0)
+    sizes = rng.choice([20, 100, 500, 2000, 10000], size=args.requests, p=[0.3, 0.3, 0.2, 0.15, 0.05])
+    pool = {s: [make_log(int(s), trig, seed=int(s) + k, hit_rate=0.01) for k in range(4)] for s in set(sizes.tolist())}
+    reqs = [pool[int(s)][i % 4] for i, s in enumerate(sizes)]
+    b = Batcher(eng, int(eng.config["engine.batch.max-requests"]), int(eng.config["engine.batch.max-bytes"]),
+                float(eng.config["engine.batch.max-wait-ms"]), Metrics())
+    for f in [b.submit(r) for r in reqs[:64]]:
+        f.result()
+    lat = [0.0] * len(reqs)
+    done = threading.Semaphore(0)
+
+    def cb(i, t0):
+        def _f(_fut):
+            lat[i] = time.perf_counter() - t0
+            done.release()
+        return _f
+
+    t_start = time.perf_counter()
+    for i, r in enumerate(reqs):              # all requests in flight at once (10k concurrent)
+        t0 = time.perf_counter()
+        b.submit(r).add_done_callback(cb(i, t0))
+    for _ in reqs:
+        done.acquire()
+    wall = time.perf_counter() - t_start
+    b.close()
+    lat = np.array(lat)
+    print(json.dumps({"config": f"concurrent-{args.requests}-requests-mixed", "device": str(dev),
+                      "p50_ms": round(float(np.median(lat)) * 1e3, 3), "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 3),
+                      "requests_per_s": round(len(reqs) / wall, 1), "lines_per_s": round(float(sizes.sum()) / wall, 1)}))
+
+
+def mode_golden(args):
+    sets, trig = make_library(20, seed=3, n_sets=2)
+    logs = make_log(args.lines, trig, seed=4, hit_rate=0.01)
+    p = ScoringParams()
+    t0 = time.perf_counter()
+    r = golden.analyze(logs, sets, p, golden.FrequencyTracker(p))
+    dt = time.perf_counter() - t0
+    print(json.dumps({"config": f"golden-python-proxy-{args.lines}-lines-20-patterns", "seconds": round(dt, 3),
+                      "lines_per_s": round(r["metadata"]["totalLines"] / dt, 1)}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["rest", "single", "stream", "concurrent", "golden"])
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--lines", type=int, default=None)
+    ap.add_argument("--patterns", type=int, default=4000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--requests", type=int, default=None)
+    ap.add_argument("--chunk-mb", type=int, default=512)
+    args = ap.parse_args()
+    defaults = {"rest": (10_000, 50), "single": (1_000_000, None), "stream": (1_000_000_000, None),
+                "concurrent": (None, 10_000), "golden": (10_000, None)}
+    dl, dr = defaults[args.mode]
+    args.lines = args.lines or dl
+    args.requests = args.requests or dr
+    globals()["mode_" + args.mode](args)
+
+
+if __name__ == "__main__":
+    main()

@@ -171,9 +171,9 @@ PYBIND11_MODULE(_lpnative, m) {
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
                   P<unsigned long long>(count), grid, s); });
   m.def("pf_verify_dev", [](uint64_t gh, int64_t n, uint64_t text, int64_t nb, py::tuple pf, uint64_t ls, int64_t nl,
-                            uint64_t cand, int64_t cap, uint64_t count, uint64_t s) {
+                            uint64_t blk, uint64_t cand, int64_t cap, uint64_t count, uint64_t s) {
     pf_verify_dev(P<const int64_t>(gh), n, P<const uint8_t>(text), nb, pf_from(pf), P<const int64_t>(ls), nl,
-                  P<int64_t>(cand), cap, P<unsigned long long>(count), s); });
+                  P<const int32_t>(blk), P<int64_t>(cand), cap, P<unsigned long long>(count), s); });
   m.def("verify_dev", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out, uint64_t s) {
     verify_dev(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out), s); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
@@ -231,5 +231,8 @@ PYBIND11_MODULE(_lpnative, m) {
   });
 
   // ---- JSON result emitter
+  py::class_<PatternTable>(m, "PatternTable")
+      .def(py::init<py::list, py::array_t<int32_t>, py::array_t<int32_t>>());
   m.def("emit_events_json", &emit_events_json_py);
+  m.def("emit_batch_json", &emit_batch_json_py);
 }

@@ -47,59 +47,83 @@ void put_int(std::string& o, int64_t v) {
   o.append(b, r.ptr);
 }
 
+// events [e0, e1) of one document whose lines are [doc_lo, doc_hi) of the line index
+void emit_events(std::string& o, const uint8_t* b, const int64_t* LS, const int32_t* LL, int64_t doc_lo,
+                 int64_t doc_hi, const int32_t* EL, const int32_t* EP, const double* ES, int64_t e0, int64_t e1,
+                 const PatternTable& T) {
+  auto line = [&](int64_t j) { put_str(o, b + LS[j], LL[j]); };
+  o.push_back('[');
+  for (int64_t e = e0; e < e1; ++e) {
+    if (e > e0) o.push_back(',');
+    const int64_t x = EL[e];
+    const int32_t p = EP[e];
+    o.append("{\"lineNumber\":");
+    put_int(o, x - doc_lo + 1);
+    o.append(",\"matchedPattern\":");
+    o.append(T.json[p]);
+    o.append(",\"context\":{\"matchedLine\":");
+    line(x);
+    const int32_t bf = T.before[p], af = T.after[p];
+    if (bf < 0) {
+      o.append(",\"linesBefore\":null,\"linesAfter\":null}");
+    } else {
+      o.append(",\"linesBefore\":[");
+      const int64_t a = x - bf < doc_lo ? doc_lo : x - bf;
+      for (int64_t j = a; j < x; ++j) { if (j > a) o.push_back(','); line(j); }
+      o.append("],\"linesAfter\":[");
+      const int64_t z = x + 1 + af > doc_hi ? doc_hi : x + 1 + af;
+      for (int64_t j = x + 1; j < z; ++j) { if (j > x + 1) o.push_back(','); line(j); }
+      o.append("]}");
+    }
+    o.append(",\"score\":");
+    put_double(o, ES[e]);
+    o.push_back('}');
+  }
+  o.push_back(']');
+}
+
 }  // namespace
 
-py::bytes emit_events_json_py(uint64_t buf, py::array_t<int64_t> line_start, py::array_t<int32_t> line_len,
-                              int64_t doc_lo, int64_t doc_hi, py::array_t<int32_t> ev_line,
-                              py::array_t<int32_t> ev_pat, py::array_t<double> ev_score, py::list pattern_json,
-                              py::array_t<int32_t> ctx_before, py::array_t<int32_t> ctx_after) {
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(buf);
-  auto LS = line_start.unchecked<1>();
-  auto LL = line_len.unchecked<1>();
-  auto EL = ev_line.unchecked<1>();
-  auto EP = ev_pat.unchecked<1>();
-  auto ES = ev_score.unchecked<1>();
-  auto CB = ctx_before.unchecked<1>();
-  auto CA = ctx_after.unchecked<1>();
-  std::vector<std::string> pj;
-  pj.reserve(pattern_json.size());
-  for (auto h : pattern_json) pj.push_back(h.cast<std::string>());
-  const int64_t n = EL.shape(0);
+PatternTable::PatternTable(py::list pattern_json, py::array_t<int32_t> ctx_before, py::array_t<int32_t> ctx_after) {
+  json.reserve(pattern_json.size());
+  for (auto h : pattern_json) json.push_back(h.cast<std::string>());
+  auto B = ctx_before.unchecked<1>();
+  auto A = ctx_after.unchecked<1>();
+  for (py::ssize_t i = 0; i < B.shape(0); ++i) { before.push_back(B(i)); after.push_back(A(i)); }
+}
+
+py::bytes emit_events_json_py(const PatternTable& T, uint64_t buf, py::array_t<int64_t> line_start,
+                              py::array_t<int32_t> line_len, int64_t doc_lo, int64_t doc_hi,
+                              py::array_t<int32_t> ev_line, py::array_t<int32_t> ev_pat,
+                              py::array_t<double> ev_score) {
+  const int64_t n = ev_line.shape(0);
   std::string o;
   o.reserve((size_t)n * 512 + 16);
   {
     py::gil_scoped_release nogil;
-    auto line = [&](int64_t j) { put_str(o, b + LS(j), LL(j)); };
-    o.push_back('[');
-    for (int64_t e = 0; e < n; ++e) {
-      if (e) o.push_back(',');
-      const int64_t x = EL(e);
-      const int32_t p = EP(e);
-      o.append("{\"lineNumber\":");
-      put_int(o, x - doc_lo + 1);
-      o.append(",\"matchedPattern\":");
-      o.append(pj[p]);
-      o.append(",\"context\":{\"matchedLine\":");
-      line(x);
-      const int32_t bf = CB(p), af = CA(p);
-      if (bf < 0) {
-        o.append(",\"linesBefore\":null,\"linesAfter\":null}");
-      } else {
-        o.append(",\"linesBefore\":[");
-        int64_t a = x - bf < doc_lo ? doc_lo : x - bf;
-        for (int64_t j = a; j < x; ++j) { if (j > a) o.push_back(','); line(j); }
-        o.append("],\"linesAfter\":[");
-        int64_t z = x + 1 + af > doc_hi ? doc_hi : x + 1 + af;
-        for (int64_t j = x + 1; j < z; ++j) { if (j > x + 1) o.push_back(','); line(j); }
-        o.append("]}");
-      }
-      o.append(",\"score\":");
-      put_double(o, ES(e));
-      o.push_back('}');
-    }
-    o.push_back(']');
+    emit_events(o, reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), doc_lo, doc_hi,
+                ev_line.data(), ev_pat.data(), ev_score.data(), 0, n, T);
   }
   return py::bytes(o);
+}
+
+py::list emit_batch_json_py(const PatternTable& T, uint64_t buf, py::array_t<int64_t> line_start,
+                            py::array_t<int32_t> line_len, py::array_t<int64_t> doc_line_off,
+                            py::array_t<int32_t> ev_line, py::array_t<int32_t> ev_pat,
+                            py::array_t<double> ev_score, py::array_t<int64_t> ev_doc_off) {
+  const int64_t D = doc_line_off.shape(0) - 1;
+  std::vector<std::string> outs(D);
+  {
+    py::gil_scoped_release nogil;
+    const int64_t* dl = doc_line_off.data();
+    const int64_t* eo = ev_doc_off.data();
+    for (int64_t d = 0; d < D; ++d)
+      emit_events(outs[d], reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), dl[d],
+                  dl[d + 1], ev_line.data(), ev_pat.data(), ev_score.data(), eo[d], eo[d + 1], T);
+  }
+  py::list r;
+  for (auto& s : outs) r.append(py::bytes(s));
+  return r;
 }
 
 }  // namespace lp

@@ -1,15 +1,32 @@
 // Native JSON emitter for AnalysisResult.events (reference: Jackson serialization of
 // MatchedEvent/EventContext, AnalysisService.java:100-107,132-156). Context lines are gathered
 // straight from the request byte buffer via the line index, so a large result never
-// materialises per-line Python strings.
+// materialises per-line Python strings. The pattern echo (matchedPattern, snake_case JSON) is
+// serialised once per library into a PatternTable and spliced per event.
 #pragma once
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <string>
+#include <vector>
+
 namespace lp {
-pybind11::bytes emit_events_json_py(uint64_t buf, pybind11::array_t<int64_t> line_start,
+
+struct PatternTable {
+  std::vector<std::string> json;
+  std::vector<int32_t> before, after;   // context rules, -1 = null rules
+  PatternTable(pybind11::list pattern_json, pybind11::array_t<int32_t> ctx_before,
+               pybind11::array_t<int32_t> ctx_after);
+};
+
+pybind11::bytes emit_events_json_py(const PatternTable& T, uint64_t buf, pybind11::array_t<int64_t> line_start,
                                     pybind11::array_t<int32_t> line_len, int64_t doc_lo, int64_t doc_hi,
                                     pybind11::array_t<int32_t> ev_line, pybind11::array_t<int32_t> ev_pat,
-                                    pybind11::array_t<double> ev_score, pybind11::list pattern_json,
-                                    pybind11::array_t<int32_t> ctx_before, pybind11::array_t<int32_t> ctx_after);
-}
+                                    pybind11::array_t<double> ev_score);
+
+// one call per request batch: returns the events array JSON of every document
+pybind11::list emit_batch_json_py(const PatternTable& T, uint64_t buf, pybind11::array_t<int64_t> line_start,
+                                  pybind11::array_t<int32_t> line_len, pybind11::array_t<int64_t> doc_line_off,
+                                  pybind11::array_t<int32_t> ev_line, pybind11::array_t<int32_t> ev_pat,
+                                  pybind11::array_t<double> ev_score, pybind11::array_t<int64_t> ev_doc_off);
+}  // namespace lp

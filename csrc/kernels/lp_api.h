@@ -12,8 +12,8 @@ void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, i
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
-                   const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap, unsigned long long* count,
-                   uint64_t stream);
+                   const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
+                   unsigned long long* count, uint64_t stream);
 void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
                 const DfaPool& P, uint8_t* out, uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,

@@ -106,10 +106,25 @@ LP_HD int64_t lower_bound32(const int32_t* a, int64_t lo, int64_t hi, int32_t v)
   return lo;
 }
 
+// Line containing byte `pos`. With a coarse index blk[b] = line containing byte b << 12 (built
+// once per request) the search covers one 4 KiB block's lines instead of all L lines.
+constexpr int LINE_BLK_SHIFT = 12;
+LP_HD int64_t locate_line(const int64_t* ls, int64_t n, const int32_t* blk, int64_t pos) {
+  if (!blk) return upper_idx(ls, n, pos);
+  const int64_t b = pos >> LINE_BLK_SHIFT;
+  int64_t lo = blk[b], hi = (int64_t)blk[b + 1] + 1;
+  if (hi > n) hi = n;
+  while (lo + 1 < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (ls[mid] <= pos) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
 // Probe one gram hit at text position p; appends (regex<<32 | line) candidates.
 template <typename AppendFn>
 LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, uint32_t gram, int g,
-                    const int64_t* line_start, int64_t nlines, AppendFn&& append) {
+                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, AppendFn&& append) {
   uint64_t key = (uint64_t)gram | ((uint64_t)g << 32);
   uint32_t h = ht_hash(gram, g) & T.ht_mask;
   for (;;) {
@@ -129,7 +144,7 @@ LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int6
     for (int q = 0; q < len; ++q)
       if (lower_byte(text[st + q]) != T.lit_bytes[lo + q]) { ok = false; break; }
     if (!ok) continue;
-    if (line < 0) line = upper_idx(line_start, nlines, st);
+    if (line < 0) line = locate_line(line_start, nlines, blk_line, st);
     if (line < 0) line = 0;
     for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
       append(((int64_t)T.lit_reg[r] << 32) | line);

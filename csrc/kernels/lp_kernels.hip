@@ -239,7 +239,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
 __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ ghits, int64_t n,
                                                    const uint8_t* __restrict__ text, int64_t nbytes, PfTables T,
                                                    const int64_t* __restrict__ line_start, int64_t nlines,
-                                                   int64_t* cand, int64_t cap, unsigned long long* count) {
+                                                   const int32_t* __restrict__ blk_line, int64_t* cand, int64_t cap,
+                                                   unsigned long long* count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t h = ghits[i];
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
   uint32_t g4 = 0;
   for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
   const Appender app{cand, cap, count};
-  pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, app);
+  pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, blk_line, app);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -410,11 +411,11 @@ void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64
 }
 
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
-                   const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap, unsigned long long* count,
-                   uint64_t stream) {
+                   const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
+                   unsigned long long* count, uint64_t stream) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_pf_verify, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ghits, n, text, nbytes,
-                     T, line_start, nlines, cand, cap, count);
+                     T, line_start, nlines, blk_line, cand, cap, count);
   LP_CHECK(hipGetLastError());
 }
 
@@ -501,7 +502,7 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
       const uint32_t key = g4 & gram_mask(g);
       const uint32_t h1 = bloom_h1(key, g, T.bloom_bits), h2 = bloom_h2(key, g, T.bloom_bits);
       if (((bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u) == 0) continue;
-      pf_probe(T, text, nbytes, p, key, g, line_start, nlines, app);
+      pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
     }
   }
   return count;

@@ -408,15 +408,18 @@ class Engine:
         ev_pat = res.ev_pat.cpu().numpy()
         score = res.score.cpu().numpy()
         ev_seg = res.ev_seg.cpu().numpy()
-        bounds = np.searchsorted(ev_seg, np.arange(len(datas) + 1))
-        out = []
-        for d in range(len(datas)):
-            e0, e1 = bounds[d], bounds[d + 1]
-            ej = N.emit_events_json(hb.ctypes.data, ls_h, ll_h, int(dl[d]), int(dl[d + 1]), ev_line[e0:e1],
-                                    ev_pat[e0:e1], score[e0:e1], self.lib.pattern_json, self.lib.ctx_before,
-                                    self.lib.ctx_after)
-            out.append(self._wrap(ej, ev_pat[e0:e1], int(dl[d + 1] - dl[d]), t0))
-        return out
+        bounds = np.searchsorted(ev_seg, np.arange(len(datas) + 1)).astype(np.int64)
+        ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h, np.ascontiguousarray(dl, np.int64),
+                                ev_line, ev_pat, score, bounds)
+        return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0)
+                for d in range(len(datas))]
+
+    def _pattern_table(self):
+        pt = getattr(self.lib, "_native_pattern_table", None)
+        if pt is None:
+            pt = N.PatternTable(self.lib.pattern_json, self.lib.ctx_before, self.lib.ctx_after)
+            self.lib._native_pattern_table = pt
+        return pt
 
     def analyze_json(self, logs: str, library_ids: Optional[List] = None) -> bytes:
         """Full AnalysisResult as JSON bytes (camelCase result, snake_case matchedPattern)."""
@@ -431,8 +434,8 @@ class Engine:
         ls_h = ls.cpu().numpy()
         ll_h = ll.cpu().numpy()
         buf = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
-        events_json = N.emit_events_json(buf.ctypes.data, ls_h, ll_h, 0, int(ls_h.size), ev_line, ev_pat, score,
-                                         self.lib.pattern_json, self.lib.ctx_before, self.lib.ctx_after)
+        events_json = N.emit_events_json(self._pattern_table(), buf.ctypes.data, ls_h, ll_h, 0, int(ls_h.size),
+                                         ev_line, ev_pat, score)
         return self._wrap(events_json, ev_pat, int(ls_h.size), t0)
 
     def _wrap(self, events_json: bytes, ev_pat: np.ndarray, total_lines: int, t0: float) -> bytes:

@@ -90,6 +90,17 @@ def split_chunk_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, to
     return starts[:L].contiguous(), (ends - starts)[:L].to(torch.int32).contiguous()
 
 
+LINE_BLK_SHIFT = 12
+
+
+def line_block_index(line_start: torch.Tensor, nbytes: int) -> torch.Tensor:
+    """blk[b] = line containing byte b << 12 (int32), for O(log lines-per-4KiB) line lookups."""
+    nblk = (max(nbytes, 1) >> LINE_BLK_SHIFT) + 2
+    pos = torch.arange(nblk, dtype=torch.int64, device=line_start.device) << LINE_BLK_SHIFT
+    idx = torch.searchsorted(line_start, pos, right=True) - 1
+    return idx.clamp(min=0).to(torch.int32)
+
+
 def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) -> torch.Tensor:
     """Literal prefilter -> (regex << 32 | line) candidates.
 
@@ -111,11 +122,12 @@ def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) ->
             gcap = c
         if gh.numel() == 0:
             return torch.empty(0, dtype=torch.int64, device=text.device)
+        blk = line_block_index(line_start, nbytes)
         while True:
             cand = torch.empty(max(cap, 1), dtype=torch.int64, device=text.device)
             cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
             N.pf_verify_dev(gh.data_ptr(), gh.numel(), text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(),
-                            nlines, cand.data_ptr(), cap, cnt.data_ptr(), _s(text))
+                            nlines, blk.data_ptr(), cand.data_ptr(), cap, cnt.data_ptr(), _s(text))
             c = int(cnt.item())
             if c <= cap:
                 return cand[:c]

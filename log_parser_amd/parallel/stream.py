@@ -69,6 +69,19 @@ class RepeatBuffer:
             pos += take
         return bytes(out)
 
+    def copy_into(self, dst: torch.Tensor, start: int, stop: int) -> None:
+        """dst[0:stop-start] = self[start:stop] with tensor copies (no Python byte strings)."""
+        if not hasattr(self, "_bt"):
+            self._bt = torch.from_numpy(np.frombuffer(self.block, dtype=np.uint8))
+        B = len(self.block)
+        pos, o = start, 0
+        while pos < stop:
+            b = pos % B
+            take = min(B - b, stop - pos)
+            dst[o:o + take].copy_(self._bt[b:b + take])
+            pos += take
+            o += take
+
     def find(self, sub: bytes, start: int) -> int:
         B = len(self.block)
         pos = start
@@ -148,14 +161,19 @@ class StreamAnalyzer:
 
     def _producer(self, src, eff, q: "queue.Queue"):
         try:
+            flat = None
+            if not isinstance(src, RepeatBuffer):
+                # zero-copy view of bytes / bytearray / memoryview / mmap
+                flat = torch.from_numpy(np.frombuffer(src, dtype=np.uint8)) if len(src) else None
             for l_start, pos, end, r_end, lh, rh in self._plan(src, eff):
-                data = src[l_start:r_end]
-                n = len(data)
+                n = r_end - l_start
                 pinned = torch.empty(K.padded_len(n), dtype=torch.uint8,
                                      pin_memory=self.engine.device.type == "cuda")
                 if n:
-                    pinned[:n].copy_(torch.frombuffer(bytearray(data) if isinstance(data, bytes) else data,
-                                                      dtype=torch.uint8))
+                    if flat is not None:
+                        pinned[:n].copy_(flat[l_start:r_end])       # one (multi-threaded) copy
+                    else:
+                        src.copy_into(pinned, l_start, r_end)
                 pinned[n:].zero_()
                 q.put((pinned, n, lh, rh))
             q.put(None)

@@ -170,9 +170,7 @@ __device__ __forceinline__ void pf_flush(int64_t* buf, int* cnt, unsigned long l
 
 template <int G>
 __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint32_t g4) {
-  const uint32_t key = g4 & gram_mask(G);
-  const uint32_t h1 = bloom_h1(key, G, bits), h2 = bloom_h2(key, G, bits);
-  return (bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u;
+  return bloom_test(bl, g4 & gram_mask(G), G, bits) ? 1u : 0u;
 }
 
 // Hot loop: only bloom tests (tight, fully unrolled: ~12 VALU + 2 ds_read_b32 per position and
@@ -500,8 +498,7 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
     for (int g = 4; g >= 2; --g) {
       if (!(T.gmask & (1 << g))) continue;
       const uint32_t key = g4 & gram_mask(g);
-      const uint32_t h1 = bloom_h1(key, g, T.bloom_bits), h2 = bloom_h2(key, g, T.bloom_bits);
-      if (((bl[h1 >> 5] >> (h1 & 31)) & (bl[h2 >> 5] >> (h2 & 31)) & 1u) == 0) continue;
+      if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
       pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
     }
   }

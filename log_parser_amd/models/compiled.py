@@ -86,12 +86,14 @@ def _u32(x):
     return x & 0xFFFFFFFF
 
 
-def bloom_h1(key, g, bits):
-    return _u32((key ^ _u32(g * 0x9E3779B9)) * 0x85EBCA6B) >> (32 - bits)
+def bloom_word(key, g, bits):
+    """Blocked bloom filter (csrc/kernels/lp_core.h): word index for a gram key."""
+    return _u32((key ^ _u32(g * 0x9E3779B9)) * 0x85EBCA6B) >> (32 - (bits - 5))
 
 
-def bloom_h2(key, g, bits):
-    return _u32((key + _u32(g * 0x27D4EB2F)) * 0xC2B2AE35) >> (32 - bits)
+def bloom_bits2(key, g):
+    h = _u32((key + _u32(g * 0x27D4EB2F)) * 0xC2B2AE35)
+    return (1 << (h >> 27)) | (1 << ((h >> 22) & 31))
 
 
 def ht_hash(key, g):
@@ -316,8 +318,7 @@ class CompiledLibrary:
         ht_cnt = np.zeros(H, np.int32)
         gram_lits: List[int] = []
         for (key, g), ids in grams.items():
-            for h in (bloom_h1(key, g, bits), bloom_h2(key, g, bits)):
-                bloom[h >> 5] |= np.uint32(1 << (h & 31))
+            bloom[bloom_word(key, g, bits)] |= np.uint32(bloom_bits2(key, g))
             h = ht_hash(key, g) & (H - 1)
             while ht_key[h] != np.uint64(0xFFFFFFFFFFFFFFFF):
                 h = (h + 1) & (H - 1)

@@ -125,6 +125,7 @@ class Engine:
         self.profile = False
         # context features: "mfma" = NFA state-transition GEMM (k_nfa_mfma), "dfa" = 4 byte DFAs (k_feat)
         self.context_engine = str(self.config["engine.context-engine"])
+        self.log_matches = bool(self.config["server.log-matches"])
         self.tabs = library.device_tables(self.device)
         p = self.params
         self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
@@ -402,7 +403,10 @@ class Engine:
         ls = torch.from_numpy(ls_h).to(self.device)
         ll = torch.from_numpy(ll_h).to(self.device)
         segs = Segments.from_doc_offsets(dl, self.device)
-        res = self.run(text, n, ls, ll, segs, self.freq_carry())
+        verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
+        res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose)
+        if verbose:
+            self._log_events(res, dl)
         self.commit_frequency(res.freq_counts)
         ev_line = res.ev_line.cpu().numpy()
         ev_pat = res.ev_pat.cpu().numpy()
@@ -413,6 +417,24 @@ class Engine:
                                 ev_line, ev_pat, score, bounds)
         return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0)
                 for d in range(len(datas))]
+
+    def _log_events(self, res: RunResult, doc_line_off) -> None:
+        """Reference-style match / factor logs (AnalysisService.java:96-99 INFO per match,
+        ScoringService.java:90-99 DEBUG factor breakdown); opt-in via server.log-matches or DEBUG."""
+        ev_line = res.ev_line.cpu().numpy()
+        ev_pat = res.ev_pat.cpu().numpy()
+        ev_seg = res.ev_seg.cpu().numpy()
+        fac = res.factors.cpu().numpy() if res.factors is not None else None
+        lvl = logging.INFO if self.log_matches else logging.DEBUG
+        for e in range(ev_line.size):
+            pat = self.lib.patterns[int(ev_pat[e])]
+            ln = int(ev_line[e] - doc_line_off[ev_seg[e]]) + 1
+            log.log(lvl, "Line %d: Found match for pattern '%s'", ln, pat.name)
+            if fac is not None and log.isEnabledFor(logging.DEBUG):
+                f = fac[e]
+                log.debug("Pattern '%s': Base Confidence=%s, Severity Multiplier=%s, Chronological Factor=%s, "
+                          "Proximity Factor=%s, Temporal Factor=%s, Context Factor=%s, Frequency Penalty=%s",
+                          pat.name, *[float(x) for x in f])
 
     def _pattern_table(self):
         pt = getattr(self.lib, "_native_pattern_table", None)

@@ -97,3 +97,15 @@ def test_missing_pattern_directory_tolerated(tmp_path):
         assert r.status_code == 200
         j = r.json()
         assert j["events"] == [] and j["summary"]["highestSeverity"] == "NONE" and j["metadata"]["totalLines"] == 2
+
+
+def test_match_logging(caplog):
+    import logging
+    from log_parser_amd import LogParser
+    sets, trig = make_library(5, seed=2)
+    lp = LogParser(sets, config=Config.load(overrides={"engine.device": "cpu", "server.log-matches": "true"}))
+    with caplog.at_level(logging.DEBUG, logger="log_parser_amd.engine"):
+        r = lp.parse(make_log(200, trig, seed=3, hit_rate=0.2))
+    msgs = [m for m in caplog.messages if "Found match for pattern" in m]
+    assert len(msgs) == len(r["events"]) > 0
+    assert any("Chronological Factor=" in m for m in caplog.messages)

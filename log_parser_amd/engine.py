@@ -357,9 +357,16 @@ class Engine:
     def summary(self, ev_pat_host: np.ndarray) -> dict:
         if ev_pat_host.size == 0:
             return {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
-        counts = np.bincount(ev_pat_host, minlength=len(self.lib.patterns))
         dist: Dict[str, int] = {}
-        for p in np.nonzero(counts)[0]:
+        if ev_pat_host.size < 256:       # small requests: no P-sized histogram
+            sev = self.lib.severity
+            for p in ev_pat_host.tolist():
+                s = sev[p]
+                dist[s] = dist.get(s, 0) + 1
+            counts = None
+        else:
+            counts = np.bincount(ev_pat_host, minlength=len(self.lib.patterns))
+        for p in (np.nonzero(counts)[0] if counts is not None else ()):
             s = self.lib.severity[p]
             dist[s] = dist.get(s, 0) + int(counts[p])
         best_idx, best = -1, None
@@ -460,14 +467,22 @@ class Engine:
                                          ev_line, ev_pat, score)
         return self._wrap(events_json, ev_pat, int(ls_h.size), t0)
 
+    _EMPTY_SUMMARY = b',"summary":{"significantEvents":0,"highestSeverity":"NONE","severityDistribution":{}}}'
+
     def _wrap(self, events_json: bytes, ev_pat: np.ndarray, total_lines: int, t0: float) -> bytes:
+        """AnalysisResult JSON around the natively emitted events array (AnalysisService.java:115-121)."""
         import json
-        meta = {"processingTimeMs": int((time.time() - t0) * 1000), "totalLines": total_lines,
-                "analyzedAt": datetime.now(timezone.utc).isoformat().replace("+00:00", "Z"),
-                "patternsUsed": self.lib.library_ids}
-        head = json.dumps({"analysisId": str(uuid.uuid4()), "metadata": meta}, separators=(",", ":"))
+        pu = getattr(self, "_patterns_used_json", None)
+        if pu is None:
+            pu = self._patterns_used_json = json.dumps(self.lib.library_ids, separators=(",", ":"))
+        now = time.time()
+        ts = datetime.fromtimestamp(now, timezone.utc).isoformat().replace("+00:00", "Z")
+        head = (f'{{"analysisId":"{uuid.uuid4()}","metadata":{{"processingTimeMs":{int((now - t0) * 1000)},'
+                f'"totalLines":{total_lines},"analyzedAt":"{ts}","patternsUsed":{pu}}},"events":').encode()
+        if ev_pat.size == 0:
+            return head + events_json + self._EMPTY_SUMMARY
         summ = json.dumps(self.summary(ev_pat), separators=(",", ":"))
-        return (head[:-1] + ',"events":').encode() + events_json + (',"summary":' + summ + "}").encode()
+        return head + events_json + (',"summary":' + summ + "}").encode()
 
     def analyze(self, logs: str) -> dict:
         import json

@@ -47,8 +47,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # context-feature engine: "mfma" (NFA state-transition GEMM on matrix cores) or "dfa"
     "engine.context-engine": ("dfa", str),
     # continuous batching
-    "engine.batch.max-requests": (256, int),
-    "engine.batch.max-bytes": (64 << 20, int),
+    "engine.batch.max-requests": (2048, int),
+    "engine.batch.max-bytes": (256 << 20, int),
     "engine.batch.max-wait-ms": (2.0, float),
     # top-k events kept by the distributed reduction (0 = all events)
     "engine.topk": (100, int),

@@ -28,6 +28,8 @@ void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int
 void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
                     const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
                     int32_t* out);
+void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
+               unsigned long long* last_nonempty, uint64_t stream);
 void feat_dev(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
               const DfaPool& P, uint8_t* feat, uint64_t stream);
 void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,

@@ -119,6 +119,35 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restri
   }
 }
 
+// K1b: newline positions -> Java split("\\r?\\n") line index in one pass: line i spans
+// (nl[i-1], nl[i]) minus a '\r' right before nl[i]; the last line runs to nbytes. The highest
+// non-empty line index is reduced with an atomic so the caller can drop trailing empty lines.
+__global__ __launch_bounds__(256) void k_lines(const int64_t* __restrict__ nl, int64_t n_nl,
+                                               const uint8_t* __restrict__ text, int64_t nbytes,
+                                               int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+                                               unsigned long long* last_nonempty) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t best = -1;
+  if (i <= n_nl) {
+    const int64_t st = i == 0 ? 0 : nl[i - 1] + 1;
+    int64_t en = nbytes;
+    if (i < n_nl) {
+      en = nl[i];
+      if (en > st && text[en - 1] == '\r') --en;
+    }
+    starts[i] = st;
+    lens[i] = (int32_t)(en - st);
+    if (en > st) best = i;
+  }
+  // wave max, one atomic per wave
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const long long o = __shfl_xor((long long)best, off, 64);
+    best = best > o ? best : o;
+  }
+  if ((threadIdx.x & 63) == 0 && best >= 0) atomicMax(last_nonempty, (unsigned long long)(best + 1));
+}
+
 // ------------------------------------------------------------------------------------------
 // K3a: literal prefilter.  Bloom filter (2 hashes) of every literal's leading 2/3/4-gram lives
 // in LDS; each lane scans 16 consecutive positions from one dwordx4 (+1 dword look-ahead),
@@ -239,15 +268,26 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
                                                    const int64_t* __restrict__ line_start, int64_t nlines,
                                                    const int32_t* __restrict__ blk_line, int64_t* cand, int64_t cap,
                                                    unsigned long long* count) {
+  // candidates staged in LDS, one global atomic per block (a per-candidate atomic on one counter
+  // serialises ~1M appends per step at the L2)
+  __shared__ int64_t buf[PF_BUF];
+  __shared__ int cnt;
+  __shared__ unsigned long long gbase;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const LdsAppender app{buf, &cnt, cand, cap, count};
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int64_t h = ghits[i];
-  const int64_t p = h >> 2;
-  const int G = 2 + (int)(h & 3);
-  uint32_t g4 = 0;
-  for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
-  const Appender app{cand, cap, count};
-  pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, blk_line, app);
+  if (i < n) {
+    const int64_t h = ghits[i];
+    const int64_t p = h >> 2;
+    const int G = 2 + (int)(h & 3);
+    uint32_t g4 = 0;
+    for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
+    pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, blk_line, app);
+  }
+  __syncthreads();
+  const int c = *reinterpret_cast<volatile int*>(&cnt);
+  if (c > 0) pf_flush(buf, &cnt, &gbase, c, cand, cap, count);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -382,6 +422,13 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
     default: return;  // no literals: nothing to prefilter
   }
 #undef LP_PF_CASE
+  LP_CHECK(hipGetLastError());
+}
+
+void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
+               unsigned long long* last_nonempty, uint64_t stream) {
+  hipLaunchKernelGGL(k_lines, dim3(num_blocks(n_nl + 1, 256)), dim3(256), 0, as_stream(stream), nl, n_nl, text, nbytes,
+                     starts, lens, last_nonempty);
   LP_CHECK(hipGetLastError());
 }
 

@@ -73,12 +73,13 @@ class Segments:
         n = torch.from_numpy((doc_line_off[1:] - doc_line_off[:-1]).astype(np.int64)).to(device)
         return Segments(lo, hi, lo.clone(), hi.clone(), torch.zeros_like(n), n)
 
-    def line_seg_and_owned(self, L: int) -> Tuple[torch.Tensor, torch.Tensor]:
-        dev = self.lo.device
-        lines = torch.arange(L, dtype=torch.int32, device=dev)
-        seg = torch.searchsorted(self.lo, lines, right=True).to(torch.int32) - 1
-        seg = seg.clamp(min=0)
-        owned = (lines >= self.own_lo[seg]) & (lines < self.own_hi[seg])
+    def seg_and_owned(self, lines: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Segment id and ownership of the given line ids (only hit lines, never all L lines)."""
+        if self.lo.numel() == 1:
+            seg = torch.zeros_like(lines)
+        else:
+            seg = (torch.searchsorted(self.lo, lines, right=True).to(torch.int32) - 1).clamp(min=0)
+        owned = (lines >= self.own_lo[seg.long()]) & (lines < self.own_hi[seg.long()])
         return seg, owned
 
 
@@ -225,9 +226,10 @@ class Engine:
         hit_line = (hits & 0xFFFFFFFF).to(torch.int32)
         hit_off = torch.searchsorted(hit_reg, torch.arange(R + 1, dtype=torch.int32, device=dev)).to(torch.int64)
         # primary events on owned lines, reference order (line, then pattern index)
-        line_seg, owned = segs.line_seg_and_owned(max(L, 1))
         if hits.numel():
-            prim = tabs["is_primary"][hit_reg.long()] & owned[hit_line.long()]
+            prim = tabs["is_primary"][hit_reg.long()]
+            _, owned = segs.seg_and_owned(hit_line)
+            prim &= owned
         else:
             prim = torch.zeros(0, dtype=torch.bool, device=dev)
         ph_reg = hit_reg[prim].long()
@@ -243,7 +245,7 @@ class Engine:
             order = torch.argsort(ev_line.long() * P + ev_pat.long())
             ev_line = ev_line[order].contiguous()
             ev_pat = ev_pat[order].contiguous()
-            ev_seg = line_seg[ev_line.long()].contiguous()
+            ev_seg = segs.seg_and_owned(ev_line)[0].to(torch.int32).contiguous()
         else:
             ev_line = torch.empty(0, dtype=torch.int32, device=dev)
             ev_pat = torch.empty(0, dtype=torch.int32, device=dev)
@@ -288,12 +290,20 @@ class Engine:
         null = before < 0
         a = torch.where(null, x, torch.maximum(segs.lo[s].long(), x - before))
         b = torch.where(null, x + 1, torch.minimum(segs.hi[s].long(), x + after + 1))
-        diff = torch.zeros(L + 1, dtype=torch.int32, device=dev)
-        one = torch.ones_like(a, dtype=torch.int32)
-        diff.index_add_(0, a, one)
-        diff.index_add_(0, b, -one)
-        need = torch.cumsum(diff[:L], 0) > 0
-        lines = torch.nonzero(need).flatten().to(torch.int32)
+        # union of the event windows, O(events): sort by start, clip each start to the running max
+        # of previous ends, expand the remaining runs (no L-sized arrays)
+        order = torch.argsort(a)
+        a, b = a[order], b[order]
+        prev_end = torch.cummax(b, 0).values
+        start = torch.maximum(a, torch.cat([a[:1], prev_end[:-1]]))
+        run = (b - start).clamp(min=0)
+        total = int(run.sum().item())
+        if total == 0:
+            lines = torch.zeros(0, dtype=torch.int32, device=dev)
+        else:
+            rep = torch.repeat_interleave(torch.arange(run.numel(), device=dev), run, output_size=total)
+            offs = torch.cumsum(run, 0) - run
+            lines = (start[rep] + torch.arange(total, device=dev) - offs[rep]).to(torch.int32)
         if self.context_engine == "mfma":
             return K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],
                                   self.lib.nfa_group_ncls[0])

@@ -60,6 +60,15 @@ def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Te
     if nl.numel() == 0:
         return (torch.zeros(1, dtype=torch.int64, device=dev),
                 torch.full((1,), nbytes, dtype=torch.int32, device=dev))
+    if text.is_cuda:                       # fused k_lines: starts, lens, last non-empty line
+        n = nl.numel()
+        starts = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        lens = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        last = torch.zeros(1, dtype=torch.int64, device=dev)
+        N.lines_dev(nl.data_ptr(), n, text.data_ptr(), nbytes, starts.data_ptr(), lens.data_ptr(), last.data_ptr(),
+                    _s(text))
+        L = int(last.item())
+        return starts[:L], lens[:L]
     zero = torch.zeros(1, dtype=torch.int64, device=dev)
     starts = torch.cat([zero, nl + 1])
     ends = torch.cat([nl, torch.full((1,), nbytes, dtype=torch.int64, device=dev)])

@@ -127,6 +127,8 @@ class Engine:
         # context features: "mfma" = NFA state-transition GEMM (k_nfa_mfma), "dfa" = 4 byte DFAs (k_feat)
         self.context_engine = str(self.config["engine.context-engine"])
         self.log_matches = bool(self.config["server.log-matches"])
+        self.fault_every = int(self.config["engine.fault-inject-every"])   # tests: injected device faults
+        self._batches = 0
         self.tabs = library.device_tables(self.device)
         p = self.params
         self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
@@ -408,6 +410,9 @@ class Engine:
         deterministic version of the reference's concurrent-request interleaving.
         """
         t0 = time.time()
+        self._batches += 1
+        if self.fault_every and self._batches % self.fault_every == 0:
+            raise RuntimeError("injected device fault (engine.fault-inject-every)")
         datas = [l.encode("utf-8", errors="surrogatepass") for l in logs_list]
         if len(datas) == 1 and len(datas[0]) >= self.GPU_SPLIT_BYTES:
             return [self.analyze_json(logs_list[0])]

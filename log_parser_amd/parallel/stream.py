@@ -136,9 +136,9 @@ class StreamAnalyzer:
         self.slot_e0 = torch.from_numpy(e0).to(engine.device)
 
     # ------------------------------------------------------------------ chunk planning
-    def _plan(self, src, eff: int):
+    def _plan(self, src, eff: int, start: int = 0):
         H = self.engine.lib.halo
-        pos = 0
+        pos = start
         while pos < eff or (pos == 0 and eff == 0):
             end = min(eff, pos + self.chunk_bytes)
             if end < eff:
@@ -159,13 +159,13 @@ class StreamAnalyzer:
                 break
             pos = end
 
-    def _producer(self, src, eff, q: "queue.Queue"):
+    def _producer(self, src, eff, q: "queue.Queue", start: int = 0):
         try:
             flat = None
             if not isinstance(src, RepeatBuffer):
                 # zero-copy view of bytes / bytearray / memoryview / mmap
                 flat = torch.from_numpy(np.frombuffer(src, dtype=np.uint8)) if len(src) else None
-            for l_start, pos, end, r_end, lh, rh in self._plan(src, eff):
+            for l_start, pos, end, r_end, lh, rh in self._plan(src, eff, start):
                 n = r_end - l_start
                 pinned = torch.empty(K.padded_len(n), dtype=torch.uint8,
                                      pin_memory=self.engine.device.type == "cuda")
@@ -175,13 +175,22 @@ class StreamAnalyzer:
                     else:
                         src.copy_into(pinned, l_start, r_end)
                 pinned[n:].zero_()
-                q.put((pinned, n, lh, rh))
+                q.put((pinned, n, lh, rh, end))
             q.put(None)
         except BaseException as e:  # noqa: BLE001
             q.put(e)
 
     # ------------------------------------------------------------------ run
-    def run(self, src, on_chunk: Optional[Callable] = None) -> StreamResult:
+    def run(self, src, on_chunk: Optional[Callable] = None, checkpoint: Optional[str] = None,
+            checkpoint_every: int = 1, resume: Optional[str] = None,
+            fail_after_chunks: Optional[int] = None) -> StreamResult:
+        """Analyse ``src`` (bytes-like, mmap or RepeatBuffer).
+
+        checkpoint / checkpoint_every: after every N chunks write the stream cursor and all carries
+        (global line offset, running frequency counts, sequence-chain state, the frequency carry
+        the stream started with, events so far) to an ``.npz``; ``resume`` continues from it and
+        produces exactly the uninterrupted result. ``fail_after_chunks`` injects a
+        failure (tests)."""
         t0 = time.perf_counter()
         eng = self.engine
         lib = eng.lib
@@ -191,18 +200,44 @@ class StreamAnalyzer:
             empty = {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
             z = np.zeros(0)
             return StreamResult(0, 0, empty, z, z.astype(np.int64), z.astype(np.int64), 0, len(src), 0.0)
+        nkeys = len(lib.freq_ids)
+        start = 0
+        if resume:
+            with np.load(resume, allow_pickle=False) as ck:
+                start = int(ck["pos"])
+                line_base = int(ck["line_base"])
+                chunks = int(ck["chunks"])
+                nbytes_total = int(ck["nbytes"])
+                freq_carry = torch.from_numpy(ck["freq_carry"]).to(dev)
+                run_counts = torch.from_numpy(ck["run_counts"]).to(dev)
+                seq_state = torch.from_numpy(ck["seq_state"]).to(dev)
+                ev_gl = [torch.from_numpy(ck["gl"]).to(dev)]
+                ev_pat = [torch.from_numpy(ck["pat"]).to(dev)]
+                ev_fac = [torch.from_numpy(ck["fac"]).to(dev)]
+        else:
+            freq_carry = eng.freq_carry()
+            run_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
+            seq_state = torch.zeros(max(lib.n_seq_events, 1), dtype=torch.uint8, device=dev)
+            line_base = 0
+            ev_gl, ev_pat, ev_fac = [], [], []
+            chunks = 0
+            nbytes_total = 0
         q: "queue.Queue" = queue.Queue(maxsize=2)
-        th = threading.Thread(target=self._producer, args=(src, eff, q), daemon=True)
+        th = threading.Thread(target=self._producer, args=(src, eff, q, start), daemon=True)
         th.start()
         copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
-        freq_carry = eng.freq_carry()
-        nkeys = len(lib.freq_ids)
-        run_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
-        seq_state = torch.zeros(max(lib.n_seq_events, 1), dtype=torch.uint8, device=dev)
-        line_base = 0
-        ev_gl, ev_pat, ev_fac = [], [], []
-        chunks = 0
-        nbytes_total = 0
+
+        def save(pos_next):
+            def cat(xs, dt, shape):
+                return torch.cat(xs).cpu().numpy() if xs else np.zeros(shape, dt)
+            tmp = checkpoint + ".tmp"
+            with open(tmp, "wb") as f:
+                np.savez(f, pos=pos_next, line_base=line_base, chunks=chunks, nbytes=nbytes_total,
+                         freq_carry=freq_carry.cpu().numpy(), run_counts=run_counts.cpu().numpy(),
+                         seq_state=seq_state.cpu().numpy(), gl=cat(ev_gl, np.int64, (0,)),
+                         pat=cat(ev_pat, np.int32, (0,)), fac=cat(ev_fac, np.float64, (0, 7)))
+            import os
+            os.replace(tmp, checkpoint)
 
         def fetch():
             item = q.get()
@@ -210,19 +245,19 @@ class StreamAnalyzer:
                 raise item
             if item is None:
                 return None
-            pinned, n, lh, rh = item
+            pinned, n, lh, rh, end = item
             if copy_stream is not None:
                 with torch.cuda.stream(copy_stream):
                     d = torch.empty(pinned.numel(), dtype=torch.uint8, device=dev)
                     d.copy_(pinned, non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(copy_stream)
-                return d, n, lh, rh, ev, pinned
-            return pinned, n, lh, rh, None, pinned
+                return d, n, lh, rh, ev, end
+            return pinned, n, lh, rh, None, end
 
         nxt = fetch()
         while nxt is not None:
-            text, n, lh, rh, ev, _pin = nxt
+            text, n, lh, rh, ev, chunk_end = nxt
             if ev is not None:
                 torch.cuda.current_stream(dev).wait_event(ev)
                 text.record_stream(torch.cuda.current_stream(dev))
@@ -250,6 +285,10 @@ class StreamAnalyzer:
             line_base += own_hi - own_lo
             nbytes_total += n
             chunks += 1
+            if checkpoint and chunks % max(1, checkpoint_every) == 0:
+                save(chunk_end)
+            if fail_after_chunks is not None and chunks >= fail_after_chunks:
+                raise RuntimeError("injected stream failure after chunk %d" % chunks)
         th.join()
         N = max(line_base, 1)
         if ev_gl:

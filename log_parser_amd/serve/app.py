@@ -23,6 +23,7 @@ import time
 from concurrent.futures import Future
 from typing import List, Optional
 
+import torch
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, Response
 
@@ -46,6 +47,8 @@ class Batcher:
         self.max_bytes = max_bytes
         self.max_wait = max_wait_ms / 1000.0
         self.metrics = metrics
+        self.fallback_cpu = bool(engine.config.get("engine.fallback-cpu", True))
+        self._cpu_engine: Optional[Engine] = None
         self._q: List[tuple] = []
         self._cv = threading.Condition()
         self._stop = False
@@ -92,7 +95,7 @@ class Batcher:
                 continue
             try:
                 t0 = time.perf_counter()
-                outs = self.engine.analyze_batch_json([b[0] for b in batch])
+                outs = self._analyze([b[0] for b in batch])
                 self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
                 for (_, fut, _), o in zip(batch, outs):
                     fut.set_result(o)
@@ -101,6 +104,23 @@ class Batcher:
                 for _, fut, _ in batch:
                     if not fut.done():
                         fut.set_exception(e)
+
+    def _analyze(self, logs: List[str]) -> List[bytes]:
+        """GPU batch; on a device failure (HIP error, OOM, lost device) serve the batch from the CPU
+        backend — same library tables and the same frequency state — for availability only
+        (SURVEY §5.3), and report it in /metrics."""
+        try:
+            return self.engine.analyze_batch_json(logs)
+        except Exception:  # noqa: BLE001
+            if not self.fallback_cpu:
+                raise
+            log.exception("device batch failed; serving it from the CPU backend")
+            self.metrics.device_failures += 1
+            if self._cpu_engine is None:
+                self._cpu_engine = Engine(self.engine.lib, self.engine.config, device=torch.device("cpu"),
+                                          freq=self.engine.freq)
+                self._cpu_engine.fault_every = 0
+            return self._cpu_engine.analyze_batch_json(logs)
 
 
 def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None) -> FastAPI:

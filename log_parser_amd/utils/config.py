@@ -46,6 +46,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.dfa-max-states": (2048, int),
     # context-feature engine: "mfma" (NFA state-transition GEMM on matrix cores) or "dfa"
     "engine.context-engine": ("dfa", str),
+    # serve a batch from the CPU backend when the device path fails (availability)
+    "engine.fallback-cpu": (True, bool),
+    # fault injection for tests: fail the device path every N-th batch (0 = off)
+    "engine.fault-inject-every": (0, int),
     # continuous batching
     "engine.batch.max-requests": (2048, int),
     "engine.batch.max-bytes": (256 << 20, int),

@@ -42,6 +42,7 @@ class Metrics:
         self.batch_latency = _Hist()
         self.batches = 0
         self.batched_requests = 0
+        self.device_failures = 0
         self.freq: Dict[str, int] = {}
 
     def observe_request(self, code: int, seconds: float, nbytes: int):
@@ -73,6 +74,7 @@ class Metrics:
                     "# TYPE lp_batched_requests_total counter", f"lp_batched_requests_total {self.batched_requests}",
                     "# TYPE lp_batch_seconds histogram"]
             self.batch_latency.render("lp_batch_seconds", out)
+            out += ["# TYPE lp_device_failures_total counter", f"lp_device_failures_total {self.device_failures}"]
             out.append("# TYPE lp_pattern_frequency gauge")
             for k, v in sorted(self.freq.items()):
                 out.append(f'lp_pattern_frequency{{pattern_id="{k}"}} {v}')

@@ -124,28 +124,43 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restri
 // non-empty line index is reduced with an atomic so the caller can drop trailing empty lines.
 __global__ __launch_bounds__(256) void k_lines(const int64_t* __restrict__ nl, int64_t n_nl,
                                                const uint8_t* __restrict__ text, int64_t nbytes,
-                                               int64_t* __restrict__ starts, int32_t* __restrict__ lens,
-                                               unsigned long long* last_nonempty) {
+                                               int64_t* __restrict__ starts, int32_t* __restrict__ lens) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t best = -1;
-  if (i <= n_nl) {
-    const int64_t st = i == 0 ? 0 : nl[i - 1] + 1;
-    int64_t en = nbytes;
-    if (i < n_nl) {
-      en = nl[i];
-      if (en > st && text[en - 1] == '\r') --en;
-    }
-    starts[i] = st;
-    lens[i] = (int32_t)(en - st);
-    if (en > st) best = i;
+  if (i > n_nl) return;
+  const int64_t st = i == 0 ? 0 : nl[i - 1] + 1;
+  int64_t en = nbytes;
+  if (i < n_nl) {
+    en = nl[i];
+    if (en > st && text[en - 1] == '\r') --en;
   }
-  // wave max, one atomic per wave
+  starts[i] = st;
+  lens[i] = (int32_t)(en - st);
+}
+
+// Number of lines up to and including the last non-empty one (Java String.split drops trailing
+// empty strings). One workgroup walks back from the end 256 lines at a time -- trailing empty
+// lines are rare, so this is one iteration in practice and needs no global atomics.
+__global__ __launch_bounds__(256) void k_last_nonempty(const int32_t* __restrict__ lens, int64_t n,
+                                                       unsigned long long* __restrict__ out) {
+  __shared__ int64_t wmax[4];
+  for (int64_t hi = n; hi > 0; hi -= 256) {
+    const int64_t i = hi - 1 - threadIdx.x;
+    int64_t best = (i >= 0 && lens[i] > 0) ? i : -1;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const long long o = __shfl_xor((long long)best, off, 64);
-    best = best > o ? best : o;
+    for (int off = 32; off > 0; off >>= 1) {
+      const long long o = __shfl_xor((long long)best, off, 64);
+      best = best > o ? best : o;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = best;
+    __syncthreads();
+    const int64_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (b >= 0) {
+      if (threadIdx.x == 0) *out = (unsigned long long)(b + 1);
+      return;
+    }
+    __syncthreads();
   }
-  if ((threadIdx.x & 63) == 0 && best >= 0) atomicMax(last_nonempty, (unsigned long long)(best + 1));
+  if (threadIdx.x == 0) *out = 0ull;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -428,7 +443,9 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
 void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
                unsigned long long* last_nonempty, uint64_t stream) {
   hipLaunchKernelGGL(k_lines, dim3(num_blocks(n_nl + 1, 256)), dim3(256), 0, as_stream(stream), nl, n_nl, text, nbytes,
-                     starts, lens, last_nonempty);
+                     starts, lens);
+  LP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_last_nonempty, dim3(1), dim3(256), 0, as_stream(stream), lens, n_nl + 1, last_nonempty);
   LP_CHECK(hipGetLastError());
 }
 

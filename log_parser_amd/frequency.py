@@ -94,6 +94,16 @@ class FrequencyState:
             self._rec.clear()
             self._tot.clear()
 
+    # ---- in-memory capture / rollback (elastic DP re-runs a step after a rank failure)
+    def capture(self) -> dict:
+        with self._lock:
+            return {k: list(v) for k, v in self._rec.items()}
+
+    def rollback(self, state: dict) -> None:
+        with self._lock:
+            self._rec = {k: deque(v) for k, v in state.items()}
+            self._tot = {k: sum(c for _, c in v) for k, v in state.items()}
+
     # ---- checkpoint / resume
     def snapshot(self, path: str) -> None:
         with self._lock:

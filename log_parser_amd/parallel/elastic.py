@@ -1,0 +1,232 @@
+"""Elastic line-sharded DP: a rank failure degrades the job to the survivors instead of killing it.
+
+The reference has no failure handling beyond HTTP 400/500. Here a DP job over N
+GPUs (one process per GPU, ``torch.distributed``: ``nccl`` = RCCL on ROCm, ``gloo`` on CPU) keeps
+going when a rank dies or hangs:
+
+* **Detection.** Every step ends in a commit vote through a key-value store that outlives the
+  ranks (a ``TCPStore`` hosted by the launcher, :func:`launch`). A rank whose step raised (a peer's
+  socket closed, a collective timed out, a HIP error) votes *abort*; a step commits only when every
+  member voted *ok*. ``compare_set`` makes the decision single-valued, so all survivors agree on
+  whether the step happened -- no rank can run ahead of another by one step.
+* **Recovery.** On abort every survivor rolls the frequency state back to the start of the step
+  (the only cross-step state, ``FrequencyState.capture/rollback``), tears the communicator down
+  (``destroy_process_group`` = ``ncclCommAbort`` for RCCL), checks in under a new generation, and
+  the first survivor to decide publishes the new member list; the process group is re-created over
+  the survivors (``PrefixStore`` per generation) and the step is re-run with the log re-sharded over
+  fewer ranks. Results are bit-identical to an uninterrupted run (tests/test_elastic.py).
+* **Fault injection.** ``LP_FAULT_RANK=k LP_FAULT_STEP=n`` makes original rank ``k`` exit at the
+  start of step ``n`` (``LP_FAULT_MODE=hang`` makes it stop responding for ``LP_FAULT_HANG_S`` seconds instead,
+  exercising the collective-timeout path).
+
+Under ``torchrun`` the launcher tears the whole job down when a worker dies, so elastic mode uses
+its own launcher; plain :class:`~log_parser_amd.parallel.dp.ShardedAnalyzer` is the torchrun path.
+"""
+from __future__ import annotations
+
+import os
+import time
+from datetime import timedelta
+from typing import Callable, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..engine import Engine
+from ..ops import kernels as K
+from .dp import ShardedAnalyzer, StepOutput, shard_bounds
+
+
+class RankExcluded(RuntimeError):
+    """This rank missed the membership decision of a rebuild and must leave the job."""
+
+
+def _maybe_inject(orig_rank: int, step: int) -> None:
+    r, s = os.environ.get("LP_FAULT_RANK"), os.environ.get("LP_FAULT_STEP")
+    if r is None or s is None or int(r) != orig_rank or int(s) != step:
+        return
+    if os.environ.get("LP_FAULT_MODE", "exit") == "hang":
+        time.sleep(float(os.environ.get("LP_FAULT_HANG_S", "86400")))
+        os._exit(18)
+    os._exit(17)
+
+
+class ElasticGroup:
+    """Membership + communicator of an elastic job, keyed by generation in a shared store."""
+
+    def __init__(self, store: dist.Store, rank: int, world: int, backend: str = "gloo",
+                 timeout_s: float = 60.0, grace_s: float = 2.0, device: Optional[torch.device] = None):
+        self.store = store
+        self.orig_rank = rank
+        self.members: List[int] = list(range(world))
+        self.backend = backend
+        self.timeout_s = timeout_s
+        self.grace_s = grace_s
+        self.device = device
+        self.gen = 0
+        self.attempt = 0
+        self._init_pg()
+
+    @property
+    def rank(self) -> int:
+        return self.members.index(self.orig_rank)
+
+    @property
+    def size(self) -> int:
+        return len(self.members)
+
+    def _init_pg(self) -> None:
+        kw = {}
+        if self.backend == "nccl" and self.device is not None:
+            kw["device_id"] = self.device
+        dist.init_process_group(self.backend, store=dist.PrefixStore(f"lp/pg/{self.gen}", self.store),
+                                rank=self.rank, world_size=self.size,
+                                timeout=timedelta(seconds=self.timeout_s), **kw)
+        self.attempt = 0
+
+    # ---- commit vote -------------------------------------------------------------------------
+    def _key(self, what: str) -> str:
+        return f"lp/{what}/{self.gen}/{self.attempt}"
+
+    def vote(self, ok: bool) -> bool:
+        """Single-valued decision for the current attempt; True iff every member voted ok."""
+        key = self._key("commit")
+        if not ok:
+            decided = self.store.compare_set(key, b"", b"abort")
+        else:
+            n_ok = self.store.add(self._key("ok"), 1)
+            deadline = time.monotonic() + self.timeout_s
+            decided = None
+            while decided is None:
+                if self.store.check([key]):
+                    decided = self.store.get(key)
+                elif n_ok >= self.size:
+                    decided = self.store.compare_set(key, b"", b"ok")
+                elif time.monotonic() > deadline:
+                    decided = self.store.compare_set(key, b"", b"abort")
+                else:
+                    time.sleep(0.001)
+                    n_ok = self.store.add(self._key("ok"), 0)
+        self.attempt += 1
+        return bytes(decided) == b"ok"
+
+    # ---- rebuild over the survivors ----------------------------------------------------------
+    def rebuild(self) -> None:
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 - a broken communicator may refuse a clean shutdown
+            pass
+        old = self.members
+        self.gen += 1
+        g = self.gen
+        self.store.set(f"lp/alive/{g}/{self.orig_rank}", b"1")
+        n = self.store.add(f"lp/nalive/{g}", 1)
+        key = f"lp/members/{g}"
+        deadline = time.monotonic() + self.grace_s
+        while n < len(old) and time.monotonic() < deadline and not self.store.check([key]):
+            time.sleep(0.005)
+            n = self.store.add(f"lp/nalive/{g}", 0)
+        alive = [r for r in old if self.store.check([f"lp/alive/{g}/{r}"])]
+        decided = self.store.compare_set(key, b"", ",".join(map(str, alive)).encode())
+        members = [int(x) for x in bytes(decided).decode().split(",") if x]
+        if self.orig_rank not in members:
+            raise RankExcluded(f"rank {self.orig_rank} missed generation {g} (members {members})")
+        self.members = members
+        self._init_pg()
+
+    def close(self) -> None:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+class ElasticAnalyzer:
+    """Runs ShardedAnalyzer steps on the full log held by every rank, re-sharding on failure."""
+
+    def __init__(self, engine: Engine, group: ElasticGroup, max_rebuilds: int = 8):
+        self.engine = engine
+        self.group = group
+        self.sa = ShardedAnalyzer(engine)
+        self.max_rebuilds = max_rebuilds
+        self.rebuilds = 0
+        self.step_idx = 0
+        self._index = None
+        self.halo_left = 0      # halo of the last committed step (local line -> global line)
+
+    def _global_index(self, data) -> tuple:
+        if self._index is None or self._index[0] is not data:
+            t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+            if len(data):
+                t[:len(data)] = torch.frombuffer(memoryview(data), dtype=torch.uint8)
+            ls, ll = K.split_lines(t, len(data))
+            self._index = (data, ls, ll)
+        return self._index[1], self._index[2]
+
+    def _shard(self, data, gls, gll):
+        """This rank's line range + halos under the current membership, on the engine device."""
+        L = gls.numel()
+        lo, hi, hl, hr = shard_bounds(L, self.group.size, self.group.rank, self.engine.lib.halo)
+        a, b = lo - hl, hi + hr
+        base = int(gls[a]) if a < L else len(data)
+        end = int(gls[b]) if b < L else len(data)
+        t = torch.zeros(K.padded_len(end - base), dtype=torch.uint8)
+        if end > base:
+            t[:end - base] = torch.frombuffer(memoryview(data)[base:end], dtype=torch.uint8)
+        dev = self.engine.device
+        return (t.to(dev), end - base, (gls[a:b] - base).contiguous().to(dev), gll[a:b].contiguous().to(dev),
+                hl, hr)
+
+    def step(self, data, topk: int = 100, with_factors: bool = False) -> StepOutput:
+        freq0 = self.engine.freq.capture()
+        gls, gll = self._global_index(data)
+        while True:
+            out, ok = None, True
+            try:
+                _maybe_inject(self.group.orig_rank, self.step_idx)
+                t, nb, ls, ll, hl, hr = self._shard(data, gls, gll)
+                self.halo_left = hl
+                out = self.sa.step(t, nb, ls, ll, hl, hr, topk=topk, with_factors=with_factors)
+                if t.is_cuda:
+                    torch.cuda.synchronize(t.device)
+            except (RuntimeError, dist.DistError):
+                ok = False
+            if self.group.vote(ok):
+                self.step_idx += 1
+                return out
+            self.engine.freq.rollback(freq0)
+            self.rebuilds += 1
+            if self.rebuilds > self.max_rebuilds:
+                raise RuntimeError("elastic DP: too many rebuilds")
+            self.group.rebuild()
+
+
+def launch(fn: Callable, nprocs: int, args: Sequence = (), env: Optional[dict] = None,
+           join_timeout: Optional[float] = None) -> List[Optional[int]]:
+    """Start ``nprocs`` workers ``fn(rank, world, host, port, *args)`` around a launcher-hosted
+    TCPStore (it outlives any worker). Returns the workers' exit codes."""
+    import multiprocessing as mp
+    store = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False,
+                          timeout=timedelta(seconds=300))
+    ctx = mp.get_context("spawn")
+    old = dict(os.environ)
+    os.environ.update(env or {})
+    try:
+        procs = [ctx.Process(target=fn, args=(r, nprocs, "127.0.0.1", store.port) + tuple(args)) for r in range(nprocs)]
+        for p in procs:
+            p.start()
+    finally:
+        os.environ.clear()
+        os.environ.update(old)
+    for p in procs:
+        p.join(join_timeout)
+    codes = []
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join()
+        codes.append(p.exitcode)
+    del store
+    return codes
+
+
+def connect(host: str, port: int) -> dist.TCPStore:
+    return dist.TCPStore(host, port, is_master=False, timeout=timedelta(seconds=300))

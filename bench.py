@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--block-lines", type=int, default=250_000, help="unique synthetic lines, tiled to the shard")
     ap.add_argument("--hit-rate", type=float, default=0.004)
     ap.add_argument("--topk", type=int, default=100)
-    ap.add_argument("--profile", action="store_true", help="per-stage timings (adds syncs; not for the headline)")
+    ap.add_argument("--profile", action="store_true", help="per-stage HIP-event timings (no extra syncs)")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
     return ap.parse_args()
 
@@ -54,6 +55,7 @@ def main():
     from log_parser_amd.ops import kernels as K
     from log_parser_amd.parallel.dp import ShardedAnalyzer
     from log_parser_amd.utils.config import Config, ScoringParams
+    from log_parser_amd.utils import tracing as TR
     from log_parser_amd.utils.synth import make_library, make_log
 
     rank = int(os.environ.get("RANK", "0"))
@@ -171,8 +173,12 @@ def main():
                        "library": lib.summary(), "device": str(device)},
         }
         if args.profile:
-            rec["timings_ms_last_step_rank0"] = {k: round(v, 3) for k, v in last.result.timings.items()}
+            rec["timings_ms_last_step_rank0"] = {k: round(v, 3) for k, v in TR.resolve(last.result.timings).items()}
         print(json.dumps(rec), flush=True)
+    if args.torch_trace:                                         # untimed, after the measurement
+        with TR.torch_profile(args.torch_trace.replace(".json", f".rank{rank}.json"), device):
+            step()
+            barrier()
     if world > 1:
         dist.destroy_process_group()
 

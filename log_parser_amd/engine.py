@@ -40,6 +40,7 @@ from .models.compiled import CompiledLibrary
 from .native import N
 from .ops import kernels as K
 from .regex.javacompat import compile_java
+from .utils import tracing as TR
 from .utils.config import Config, ScoringParams
 
 log = logging.getLogger("log_parser_amd.engine")
@@ -123,7 +124,9 @@ class Engine:
         self.device = device if device is not None else resolve_device(self.config["engine.device"])
         self.freq = freq or FrequencyState(self.params.freq_window_hours)
         self.cand_cap = int(self.config["engine.candidate-capacity"])
-        self.profile = False
+        # per-stage HIP-event timers (utils/tracing.py); engine.trace also reports them per response
+        self.trace = bool(self.config.get("engine.trace", False))
+        self.profile = self.trace
         # context features: "mfma" = NFA state-transition GEMM (k_nfa_mfma), "dfa" = 4 byte DFAs (k_feat)
         self.context_engine = str(self.config["engine.context-engine"])
         self.log_matches = bool(self.config["server.log-matches"])
@@ -159,18 +162,20 @@ class Engine:
         return buf, n
 
     # ------------------------------------------------------------------ matching
-    def _tick(self, timings, name, t0):
+    def _start(self, timings) -> float:
         if self.profile:
-            if self.device.type == "cuda":
-                torch.cuda.current_stream(self.device).synchronize()   # not the ingest copy stream
-            t1 = time.perf_counter()
-            timings[name] = timings.get(name, 0.0) + (t1 - t0) * 1e3
-            return t1
+            TR.start(timings, self.device)
+        return 0.0
+
+    def _tick(self, timings, name, t0):
+        """Stage boundary: a HIP event on the compute stream (no sync; read in tracing.resolve)."""
+        if self.profile:
+            TR.mark(timings, name, self.device)
         return t0
 
     def match_hits(self, text, nbytes, ls, ll, host_lines=None, timings=None) -> torch.Tensor:
         timings = {} if timings is None else timings
-        t = time.perf_counter()
+        t = self._start(timings)
         parts = []
         cand = K.prefilter(text, nbytes, self.tabs["pf"], ls, self.cand_cap, self.pf_grid)
         t = self._tick(timings, "prefilter", t)
@@ -211,16 +216,17 @@ class Engine:
         return torch.tensor(keys, dtype=torch.int64, device=text.device)
 
     # ------------------------------------------------------------------ core run
-    def prepare(self, text, nbytes, ls, ll, segs: Segments, host_lines=None) -> "Prepared":
+    def prepare(self, text, nbytes, ls, ll, segs: Segments, host_lines=None,
+                timings: Optional[dict] = None) -> "Prepared":
         """Local phase: matching, hit CSR, context features, events, in-batch frequency ranks.
 
         Needs no global information, so the data-parallel path runs it before its collectives.
         """
-        timings: Dict[str, float] = {}
+        timings = {} if timings is None else timings
         dev = text.device
         L = ls.numel()
         hits = self.match_hits(text, nbytes, ls, ll, host_lines, timings)
-        t = time.perf_counter()
+        t = 0.0
         tabs = self.tabs
         R = self.lib.n_regexes
         P = len(self.lib.patterns)
@@ -328,7 +334,10 @@ class Engine:
     def finish(self, prep: "Prepared", segs: Segments, freq_carry: torch.Tensor,
                seq_carry: Optional[torch.Tensor] = None, with_factors: bool = False) -> RunResult:
         """Global phase: fused fp64 score kernel (needs N, global offsets and carries)."""
-        t = time.perf_counter()
+        timings = dict(prep.timings)
+        if TR._MARKS in timings:
+            timings[TR._MARKS] = list(timings[TR._MARKS])
+        t = self._start(timings)
         tabs = self.tabs
         dev = prep.hit_off.device
         ev_freq = prep.ev_rank
@@ -345,14 +354,14 @@ class Engine:
               segs.lo.data_ptr(), segs.hi.data_ptr(), segs.own_lo.data_ptr(), segs.g0.data_ptr(), segs.n.data_ptr())
         score, factors = K.score(prep.ev_line, prep.ev_pat, prep.ev_seg, ev_freq.contiguous(), st, self.sp_tuple,
                                  with_factors)
-        timings = dict(prep.timings)
         self._tick(timings, "score", t)
         return RunResult(prep.ev_line, prep.ev_pat, prep.ev_seg, score, factors,
                          prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings)
 
     def run(self, text, nbytes, ls, ll, segs: Segments, freq_carry: torch.Tensor,
-            seq_carry: Optional[torch.Tensor] = None, host_lines=None, with_factors=False) -> RunResult:
-        prep = self.prepare(text, nbytes, ls, ll, segs, host_lines)
+            seq_carry: Optional[torch.Tensor] = None, host_lines=None, with_factors=False,
+            timings: Optional[dict] = None) -> RunResult:
+        prep = self.prepare(text, nbytes, ls, ll, segs, host_lines, timings)
         return self.finish(prep, segs, freq_carry, seq_carry, with_factors)
 
     # ------------------------------------------------------------------ request API
@@ -420,24 +429,40 @@ class Engine:
         np.cumsum([len(d) for d in datas], out=doc_off[1:])
         blob = b"".join(datas)
         hb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
-        ls_h, ll_h, dl = N.split_docs(hb.ctypes.data, doc_off)
+        tm = {} if self.profile else None
+        with TR.HostTimer(tm, "line_index"):
+            ls_h, ll_h, dl = N.split_docs(hb.ctypes.data, doc_off)
+        if tm is not None:
+            self._start(tm)
         text, n = self.stage_text(blob)
         ls = torch.from_numpy(ls_h).to(self.device)
         ll = torch.from_numpy(ll_h).to(self.device)
         segs = Segments.from_doc_offsets(dl, self.device)
+        if tm is not None:
+            self._tick(tm, "h2d", 0.0)
         verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
-        res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose)
+        res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose, timings=tm)
         if verbose:
             self._log_events(res, dl)
         self.commit_frequency(res.freq_counts)
-        ev_line = res.ev_line.cpu().numpy()
-        ev_pat = res.ev_pat.cpu().numpy()
-        score = res.score.cpu().numpy()
-        ev_seg = res.ev_seg.cpu().numpy()
-        bounds = np.searchsorted(ev_seg, np.arange(len(datas) + 1)).astype(np.int64)
-        ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h, np.ascontiguousarray(dl, np.int64),
-                                ev_line, ev_pat, score, bounds)
-        return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0)
+        with TR.HostTimer(tm, "d2h"):
+            ev_line = res.ev_line.cpu().numpy()
+            ev_pat = res.ev_pat.cpu().numpy()
+            score = res.score.cpu().numpy()
+            ev_seg = res.ev_seg.cpu().numpy()
+        with TR.HostTimer(tm, "json"):
+            bounds = np.searchsorted(ev_seg, np.arange(len(datas) + 1)).astype(np.int64)
+            ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,
+                                    np.ascontiguousarray(dl, np.int64), ev_line, ev_pat, score, bounds)
+        extra = b""
+        if tm is not None:
+            import json
+            st = {k: round(v, 4) for k, v in TR.resolve(res.timings).items()}
+            st.update({k: round(v, 4) for k, v in TR.resolve(tm).items()})
+            st["batchRequests"] = len(datas)
+            log.debug("stage timings (ms): %s", st)
+            extra = (',"stageTimingsMs":' + json.dumps(st, separators=(",", ":"))).encode()
+        return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0, extra)
                 for d in range(len(datas))]
 
     def _log_events(self, res: RunResult, doc_line_off) -> None:
@@ -484,7 +509,8 @@ class Engine:
 
     _EMPTY_SUMMARY = b',"summary":{"significantEvents":0,"highestSeverity":"NONE","severityDistribution":{}}}'
 
-    def _wrap(self, events_json: bytes, ev_pat: np.ndarray, total_lines: int, t0: float) -> bytes:
+    def _wrap(self, events_json: bytes, ev_pat: np.ndarray, total_lines: int, t0: float,
+              extra_meta: bytes = b"") -> bytes:
         """AnalysisResult JSON around the natively emitted events array (AnalysisService.java:115-121)."""
         import json
         pu = getattr(self, "_patterns_used_json", None)
@@ -493,7 +519,8 @@ class Engine:
         now = time.time()
         ts = datetime.fromtimestamp(now, timezone.utc).isoformat().replace("+00:00", "Z")
         head = (f'{{"analysisId":"{uuid.uuid4()}","metadata":{{"processingTimeMs":{int((now - t0) * 1000)},'
-                f'"totalLines":{total_lines},"analyzedAt":"{ts}","patternsUsed":{pu}}},"events":').encode()
+                f'"totalLines":{total_lines},"analyzedAt":"{ts}","patternsUsed":{pu}').encode() \
+            + extra_meta + b'},"events":'
         if ev_pat.size == 0:
             return head + events_json + self._EMPTY_SUMMARY
         summ = json.dumps(self.summary(ev_pat), separators=(",", ":"))

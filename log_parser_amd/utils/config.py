@@ -48,6 +48,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.context-engine": ("dfa", str),
     # serve a batch from the CPU backend when the device path fails (availability)
     "engine.fallback-cpu": (True, bool),
+    # per-stage HIP-event timers, reported in response metadata as stageTimingsMs (opt-in)
+    "engine.trace": (False, bool),
     # fault injection for tests: fail the device path every N-th batch (0 = off)
     "engine.fault-inject-every": (0, int),
     # continuous batching

@@ -109,3 +109,26 @@ def test_match_logging(caplog):
     msgs = [m for m in caplog.messages if "Found match for pattern" in m]
     assert len(msgs) == len(r["events"]) > 0
     assert any("Chronological Factor=" in m for m in caplog.messages)
+
+
+def test_stage_timings_opt_in(tmp_path):
+    """engine.trace=true adds metadata.stageTimingsMs; default responses are unchanged."""
+    import json as _json
+    import torch
+    from log_parser_amd.engine import Engine
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.utils.config import Config, ScoringParams
+    from log_parser_amd.utils.synth import make_library, make_log
+    sets, trig = make_library(10, seed=5)
+    lib = CompiledLibrary(sets, ScoringParams())
+    logs = make_log(200, trig, seed=6, hit_rate=0.1)
+    on = Engine(lib, Config.load(overrides={"engine.device": "cpu", "engine.trace": "true"}), device=torch.device("cpu"))
+    off = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    a = _json.loads(on.analyze_batch_json([logs, logs])[0])
+    b = _json.loads(off.analyze_batch_json([logs])[0])
+    st = a["metadata"]["stageTimingsMs"]
+    for k in ("line_index", "h2d", "prefilter", "verify", "score", "d2h", "json"):
+        assert k in st and st[k] >= 0.0, (k, st)
+    assert st["batchRequests"] == 2
+    assert "stageTimingsMs" not in b["metadata"]
+    assert [e["lineNumber"] for e in a["events"]] == [e["lineNumber"] for e in b["events"]]

@@ -65,6 +65,8 @@ def main():
     if use_cuda:
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
+        from log_parser_amd.utils.numa import bind_to_gpu_numa
+        bind_to_gpu_numa(local_rank)          # pinned ingest buffers on the GPU's own socket
     else:
         device = torch.device("cpu")
     if world > 1:

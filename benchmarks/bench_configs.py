@@ -36,8 +36,13 @@ from log_parser_amd.utils.synth import make_library, make_log  # noqa: E402
 
 def _dev(args):
     if args.device == "auto":
-        return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    return torch.device(args.device)
+        dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    else:
+        dev = torch.device(args.device)
+    if dev.type == "cuda":
+        from log_parser_amd.utils.numa import bind_to_gpu_numa
+        bind_to_gpu_numa(dev.index or 0)
+    return dev
 
 
 def _sync(dev):

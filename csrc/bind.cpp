@@ -163,13 +163,16 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("nl_tiles", &nl_tiles);
 
   // ---- device launchers
+  m.def("pull_dev", [](uint64_t src, uint64_t dst, int64_t n, int grid, uint64_t s) {
+    pull_dev(P<const uint8_t>(src), P<uint8_t>(dst), n, grid, s);
+  });
   m.def("nl_count_dev", [](uint64_t text, int64_t n, uint64_t cnt, uint64_t s) { nl_count_dev(P<const uint8_t>(text), n, P<int32_t>(cnt), s); });
   m.def("lines_dev", [](uint64_t nl, int64_t n_nl, uint64_t text, int64_t nb, uint64_t st, uint64_t ln, uint64_t last,
                         uint64_t s) {
     lines_dev(P<const int64_t>(nl), n_nl, P<const uint8_t>(text), nb, P<int64_t>(st), P<int32_t>(ln),
               P<unsigned long long>(last), s); });
-  m.def("nl_write_dev", [](uint64_t text, int64_t n, uint64_t off, uint64_t pos, uint64_t s) {
-    nl_write_dev(P<const uint8_t>(text), n, P<const int64_t>(off), P<int64_t>(pos), s); });
+  m.def("nl_write_dev", [](uint64_t text, int64_t n, uint64_t off, uint64_t pos, int flag_cr, uint64_t s) {
+    nl_write_dev(P<const uint8_t>(text), n, P<const int64_t>(off), P<int64_t>(pos), flag_cr, s); });
   m.def("prefilter_dev", [](uint64_t text, int64_t n, py::tuple pf, uint64_t ls, int64_t nl, uint64_t cand, int64_t cap,
                             uint64_t count, int grid, uint64_t s) {
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,

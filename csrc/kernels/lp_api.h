@@ -7,8 +7,11 @@
 namespace lp {
 
 int64_t nl_tiles(int64_t nbytes);
+void pull_dev(const uint8_t* host_src, uint8_t* dst, int64_t nbytes, int grid, uint64_t stream);
 void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream);
-void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, uint64_t stream);
+// flag_cr: set bit 62 of a position when the '\n' follows a '\r' (consumed by lines_dev)
+void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, int flag_cr,
+                  uint64_t stream);
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,

@@ -36,6 +36,7 @@ static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStr
 constexpr int NL_THREADS = 256;
 constexpr int NL_BYTES_PER_THREAD = 64;
 constexpr int NL_TILE = NL_THREADS * NL_BYTES_PER_THREAD;
+constexpr int64_t LP_NL_CR = int64_t(1) << 62;   // flag in a newline position: preceded by '\r'
 
 __device__ __forceinline__ uint32_t zero_byte_mask(uint32_t t) {
   // exact: high bit set in every byte of t that is 0x00
@@ -80,9 +81,9 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_count(const uint8_t* __restri
 
 __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restrict__ text, int64_t nbytes,
                                                          const int64_t* __restrict__ blk_off,
-                                                         int64_t* __restrict__ nl_pos) {
+                                                         int64_t* __restrict__ nl_pos, int flag_cr) {
   const int64_t base = (int64_t)blockIdx.x * NL_TILE + (int64_t)threadIdx.x * NL_BYTES_PER_THREAD;
-  uint32_t m[16];
+  uint32_t m[16], cr[16];
   int c = 0;
   if (base < nbytes) {
     const uint4* p = reinterpret_cast<const uint4*>(text + base);
@@ -93,12 +94,16 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restri
       m[4 * k + 1] = zero_byte_mask(v.y ^ 0x0A0A0A0Au);
       m[4 * k + 2] = zero_byte_mask(v.z ^ 0x0A0A0A0Au);
       m[4 * k + 3] = zero_byte_mask(v.w ^ 0x0A0A0A0Au);
+      cr[4 * k + 0] = zero_byte_mask(v.x ^ 0x0D0D0D0Du);
+      cr[4 * k + 1] = zero_byte_mask(v.y ^ 0x0D0D0D0Du);
+      cr[4 * k + 2] = zero_byte_mask(v.z ^ 0x0D0D0D0Du);
+      cr[4 * k + 3] = zero_byte_mask(v.w ^ 0x0D0D0D0Du);
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) c += __popc(m[k]);
   } else {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) m[k] = 0;
+    for (int k = 0; k < 16; ++k) m[k] = cr[k] = 0;
   }
   __shared__ int ws[NL_THREADS / 64];
   int incl = wave_incl_scan(c);
@@ -111,9 +116,14 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restri
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     uint32_t mm = m[k];
+    // bit 31 of the previous dword = '\r' in the byte before this dword
+    const uint32_t prev_cr = k > 0 ? (cr[k - 1] >> 31) : (flag_cr && base > 0 && text[base - 1] == '\r');
+    const uint32_t crb = (cr[k] << 8) | (prev_cr << 7);   // '\r' right before byte j -> bit 8j+7
     while (mm) {
       int b = __ffs(mm) - 1;          // bit 7, 15, 23 or 31
-      nl_pos[o++] = base + 4 * k + (b >> 3);
+      int64_t v = base + 4 * k + (b >> 3);
+      if (flag_cr && ((crb >> b) & 1u)) v |= LP_NL_CR;
+      nl_pos[o++] = v;
       mm &= mm - 1;
     }
   }
@@ -127,14 +137,33 @@ __global__ __launch_bounds__(256) void k_lines(const int64_t* __restrict__ nl, i
                                                int64_t* __restrict__ starts, int32_t* __restrict__ lens) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i > n_nl) return;
-  const int64_t st = i == 0 ? 0 : nl[i - 1] + 1;
+  const int64_t st = i == 0 ? 0 : (nl[i - 1] & ~LP_NL_CR) + 1;
   int64_t en = nbytes;
   if (i < n_nl) {
-    en = nl[i];
-    if (en > st && text[en - 1] == '\r') --en;
+    const int64_t v = nl[i];
+    en = (v & ~LP_NL_CR) - (v >> 62);   // k_nl_write flagged a '\r' before this '\n'
   }
   starts[i] = st;
   lens[i] = (int32_t)(en - st);
+}
+
+// Host -> device "pull" copy: the GPU reads pinned host memory directly over PCIe (no SDMA
+// engine). Four 16-byte loads in flight per lane to cover the ~µs PCIe read latency.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_pull(const v4u* __restrict__ src, v4u* __restrict__ dst, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const v4u a = __builtin_nontemporal_load(src + i);
+    const v4u b = __builtin_nontemporal_load(src + i + stride);
+    const v4u c = __builtin_nontemporal_load(src + i + 2 * stride);
+    const v4u d = __builtin_nontemporal_load(src + i + 3 * stride);
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
 
 // Number of lines up to and including the last non-empty one (Java String.split drops trailing
@@ -414,10 +443,12 @@ void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_
   LP_CHECK(hipGetLastError());
 }
 
-void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, uint64_t stream) {
+void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, int flag_cr,
+                  uint64_t stream) {
   int64_t nb = nl_tiles(nbytes);
   if (nb == 0) return;
-  hipLaunchKernelGGL(k_nl_write, dim3((unsigned)nb), dim3(NL_THREADS), 0, as_stream(stream), text, nbytes, blk_off, nl_pos);
+  hipLaunchKernelGGL(k_nl_write, dim3((unsigned)nb), dim3(NL_THREADS), 0, as_stream(stream), text, nbytes, blk_off, nl_pos,
+                     flag_cr);
   LP_CHECK(hipGetLastError());
 }
 
@@ -437,6 +468,16 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
     default: return;  // no literals: nothing to prefilter
   }
 #undef LP_PF_CASE
+  LP_CHECK(hipGetLastError());
+}
+
+void pull_dev(const uint8_t* host_src, uint8_t* dst, int64_t nbytes, int grid, uint64_t stream) {
+  if (nbytes <= 0) return;
+  // callers pass 16-byte aligned buffers padded to a multiple of 16 (K.padded_len)
+  const int64_t n16 = (nbytes + 15) / 16;
+  const int g = (int)std::min<int64_t>(grid, num_blocks(n16, 256));
+  hipLaunchKernelGGL(k_pull, dim3(g), dim3(256), 0, as_stream(stream), reinterpret_cast<const v4u*>(host_src),
+                     reinterpret_cast<v4u*>(dst), n16);
   LP_CHECK(hipGetLastError());
 }
 

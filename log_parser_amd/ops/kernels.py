@@ -29,8 +29,9 @@ def padded_len(nbytes: int) -> int:
     return ((max(nbytes, 1) + NL_TILE - 1) // NL_TILE) * NL_TILE + TEXT_PAD
 
 
-def newline_positions(text: torch.Tensor, nbytes: int) -> torch.Tensor:
-    """Positions of every '\\n' in text[0:nbytes] (int64, ascending)."""
+def newline_positions(text: torch.Tensor, nbytes: int, flag_cr: bool = False) -> torch.Tensor:
+    """Positions of every '\\n' in text[0:nbytes] (int64, ascending). ``flag_cr`` (device only):
+    bit 62 marks a '\\n' preceded by '\\r' -- the input format of ``lines_dev``."""
     if text.is_cuda:
         nb = N.nl_tiles(nbytes)
         if nb == 0:
@@ -41,7 +42,7 @@ def newline_positions(text: torch.Tensor, nbytes: int) -> torch.Tensor:
         total = int(off[-1].item())
         off = off - cnt.to(torch.int64)
         pos = torch.empty(total, dtype=torch.int64, device=text.device)
-        N.nl_write_dev(text.data_ptr(), nbytes, off.data_ptr(), pos.data_ptr(), _s(text))
+        N.nl_write_dev(text.data_ptr(), nbytes, off.data_ptr(), pos.data_ptr(), int(flag_cr), _s(text))
         return pos
     c = N.nl_positions_host(text.data_ptr(), nbytes, 0)
     pos = torch.empty(c, dtype=torch.int64)
@@ -56,11 +57,11 @@ def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Te
     without any newline is one line (possibly empty).
     """
     dev = text.device
-    nl = newline_positions(text, nbytes)
+    nl = newline_positions(text, nbytes, flag_cr=text.is_cuda)
     if nl.numel() == 0:
         return (torch.zeros(1, dtype=torch.int64, device=dev),
                 torch.full((1,), nbytes, dtype=torch.int32, device=dev))
-    if text.is_cuda:                       # fused k_lines: starts, lens, last non-empty line
+    if text.is_cuda:                       # k_lines (CR flags from k_nl_write) + k_last_nonempty
         n = nl.numel()
         starts = torch.empty(n + 1, dtype=torch.int64, device=dev)
         lens = torch.empty(n + 1, dtype=torch.int32, device=dev)

@@ -1,0 +1,63 @@
+"""Pin a rank's host threads (and therefore its pinned staging buffers) to its GPU's NUMA node.
+
+Ingest is PCIe-bound (docs/PERFORMANCE.md): every log byte crosses the host->GPU link once.
+Pinned buffers are placed on the NUMA node of the allocating thread, so a rank whose staging
+memory sits on the far socket pays an extra inter-socket hop on every H2D transfer -- and with 8
+ranks, half of them would. Call :func:`bind_to_gpu_numa` before allocating pinned memory.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Set
+
+
+def _parse_cpulist(s: str) -> Set[int]:
+    out: Set[int] = set()
+    for part in s.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            out.update(range(int(a), int(b) + 1))
+        else:
+            out.add(int(part))
+    return out
+
+
+def gpu_pci_path(index: int) -> Optional[str]:
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(index)
+        dom, bus, dev = int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)
+    except Exception:  # noqa: BLE001 - older torch / no device
+        return None
+    path = f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:{dev:02x}.0"
+    return path if os.path.isdir(path) else None
+
+
+def gpu_numa_cpus(index: int) -> Set[int]:
+    path = gpu_pci_path(index)
+    if path is None:
+        return set()
+    try:
+        with open(os.path.join(path, "local_cpulist")) as f:
+            return _parse_cpulist(f.read())
+    except OSError:
+        return set()
+
+
+def bind_to_gpu_numa(index: int) -> Optional[Set[int]]:
+    """Restrict this process to the CPUs local to GPU ``index`` (intersected with the CPUs it may
+    already use). Returns the new CPU set, or None when nothing was changed."""
+    if os.environ.get("LP_NUMA_BIND", "1") == "0":
+        return None
+    local = gpu_numa_cpus(index)
+    try:
+        allowed = os.sched_getaffinity(0)
+    except AttributeError:
+        return None
+    cpus = local & allowed
+    if not cpus or cpus == allowed:
+        return None
+    os.sched_setaffinity(0, cpus)
+    return cpus

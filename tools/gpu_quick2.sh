@@ -1,0 +1,8 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 && echo PYTEST_OK &&
+timeout -k 10 300 python tools/stream_probe.py > gpurun_out/stream_probe.log 2>&1 && echo PROBE_OK &&
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-overlap > gpurun_out/bench_serial.json 2> gpurun_out/bench_serial.err && echo SERIAL_OK &&
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err && echo BENCH_OK

@@ -8,6 +8,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "io/docs.h"
 #include "io/json_emit.h"
 #include "kernels/lp_api.h"
 #include "regex/jregex.h"
@@ -155,11 +156,60 @@ static py::tuple split_docs(uint64_t buf, py::array_t<int64_t> doc_off) {
   return py::make_tuple(a, l, o);
 }
 
+// Pack request bodies (str via their cached UTF-8 buffer -- no copy for ASCII -- or bytes) into
+// dst and split them. Returns None if a str is not UTF-8 encodable (lone surrogates: the caller
+// falls back to str.encode(surrogatepass)), the needed byte count (int) if it exceeds cap, or
+// (line_start, line_len, doc_line_off, doc_off).
+static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, int nthreads) {
+  const int64_t D = (int64_t)docs.size();
+  std::vector<const char*> src(D);
+  std::vector<int64_t> off(D + 1, 0);
+  for (int64_t i = 0; i < D; ++i) {
+    PyObject* o = docs[i].ptr();
+    Py_ssize_t n = 0;
+    const char* p = nullptr;
+    if (PyUnicode_Check(o)) {
+      p = PyUnicode_AsUTF8AndSize(o, &n);
+      if (!p) {
+        PyErr_Clear();
+        return py::none();
+      }
+    } else if (PyBytes_Check(o)) {
+      char* q = nullptr;
+      PyBytes_AsStringAndSize(o, &q, &n);
+      p = q;
+    } else {
+      throw std::invalid_argument("pack_split_docs: str or bytes expected");
+    }
+    src[i] = p;
+    off[i + 1] = off[i] + (int64_t)n;
+  }
+  if (off[D] > cap) return py::int_(off[D]);
+  DocBatchIndex ix;
+  {
+    py::gil_scoped_release nogil;   // `docs` keeps every buffer alive
+    pack_split_docs(src.data(), off.data(), D, P<uint8_t>(dst), nthreads, ix);
+  }
+  py::array_t<int64_t> a(ix.line_start.size());
+  py::array_t<int32_t> l(ix.line_len.size());
+  py::array_t<int64_t> o(ix.doc_line_off.size());
+  py::array_t<int64_t> d(off.size());
+  if (!ix.line_start.empty()) {
+    memcpy(a.mutable_data(), ix.line_start.data(), ix.line_start.size() * 8);
+    memcpy(l.mutable_data(), ix.line_len.data(), ix.line_len.size() * 4);
+  }
+  memcpy(o.mutable_data(), ix.doc_line_off.data(), ix.doc_line_off.size() * 8);
+  memcpy(d.mutable_data(), off.data(), off.size() * 8);
+  return py::make_tuple(a, l, o, d);
+}
+
 PYBIND11_MODULE(_lpnative, m) {
   m.doc() = "log_parser_amd native core: Java-regex compiler, gfx950 kernels, host twins, JSON emitter";
   m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
   m.def("dfa_find", &dfa_find_py, py::arg("pattern"), py::arg("line"), py::arg("max_states") = 4096);
   m.def("split_docs", &split_docs);
+  m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
+        py::arg("nthreads") = 8);
   m.def("nl_tiles", &nl_tiles);
 
   // ---- device launchers
@@ -241,5 +291,7 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<PatternTable>(m, "PatternTable")
       .def(py::init<py::list, py::array_t<int32_t>, py::array_t<int32_t>>());
   m.def("emit_events_json", &emit_events_json_py);
-  m.def("emit_batch_json", &emit_batch_json_py);
+  m.def("emit_batch_json", &emit_batch_json_py, py::arg("table"), py::arg("buf"), py::arg("line_start"),
+        py::arg("line_len"), py::arg("doc_line_off"), py::arg("ev_line"), py::arg("ev_pat"), py::arg("ev_score"),
+        py::arg("ev_doc_off"), py::arg("nthreads") = 1);
 }

@@ -1,6 +1,8 @@
 #include "json_emit.h"
 
+#include <algorithm>
 #include <charconv>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -9,11 +11,25 @@ namespace py = pybind11;
 namespace lp {
 namespace {
 
+// bytes that need a JSON escape: '"', '\\' and control characters
+struct EscTable {
+  bool esc[256];
+  constexpr EscTable() : esc() {
+    for (int c = 0; c < 256; ++c) esc[c] = c < 0x20 || c == '"' || c == '\\';
+  }
+};
+constexpr EscTable kEsc;
+
 void put_str(std::string& o, const uint8_t* s, int64_t n) {
   static const char* hex = "0123456789abcdef";
   o.push_back('"');
-  for (int64_t i = 0; i < n; ++i) {
-    const uint8_t c = s[i];
+  int64_t i = 0;
+  while (i < n) {
+    int64_t j = i;
+    while (j < n && !kEsc.esc[s[j]]) ++j;       // copy clean runs in one append
+    if (j > i) o.append(reinterpret_cast<const char*>(s + i), (size_t)(j - i));
+    if (j >= n) break;
+    const uint8_t c = s[j];
     switch (c) {
       case '"': o.append("\\\""); break;
       case '\\': o.append("\\\\"); break;
@@ -23,14 +39,11 @@ void put_str(std::string& o, const uint8_t* s, int64_t n) {
       case '\b': o.append("\\b"); break;
       case '\f': o.append("\\f"); break;
       default:
-        if (c < 0x20) {
-          o.append("\\u00");
-          o.push_back(hex[c >> 4]);
-          o.push_back(hex[c & 15]);
-        } else {
-          o.push_back((char)c);
-        }
+        o.append("\\u00");
+        o.push_back(hex[c >> 4]);
+        o.push_back(hex[c & 15]);
     }
+    i = j + 1;
   }
   o.push_back('"');
 }
@@ -110,16 +123,33 @@ py::bytes emit_events_json_py(const PatternTable& T, uint64_t buf, py::array_t<i
 py::list emit_batch_json_py(const PatternTable& T, uint64_t buf, py::array_t<int64_t> line_start,
                             py::array_t<int32_t> line_len, py::array_t<int64_t> doc_line_off,
                             py::array_t<int32_t> ev_line, py::array_t<int32_t> ev_pat,
-                            py::array_t<double> ev_score, py::array_t<int64_t> ev_doc_off) {
+                            py::array_t<double> ev_score, py::array_t<int64_t> ev_doc_off, int nthreads) {
   const int64_t D = doc_line_off.shape(0) - 1;
   std::vector<std::string> outs(D);
   {
     py::gil_scoped_release nogil;
     const int64_t* dl = doc_line_off.data();
     const int64_t* eo = ev_doc_off.data();
-    for (int64_t d = 0; d < D; ++d)
-      emit_events(outs[d], reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), dl[d],
-                  dl[d + 1], ev_line.data(), ev_pat.data(), ev_score.data(), eo[d], eo[d + 1], T);
+    auto run = [&](int64_t a, int64_t z) {
+      for (int64_t d = a; d < z; ++d)
+        emit_events(outs[d], reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), dl[d],
+                    dl[d + 1], ev_line.data(), ev_pat.data(), ev_score.data(), eo[d], eo[d + 1], T);
+    };
+    // documents are independent: split them into ranges of ~equal event counts
+    const int64_t E = eo[D];
+    const int T_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nthreads, D, 1 + E / 2048}));
+    if (T_ == 1) {
+      run(0, D);
+    } else {
+      std::vector<int64_t> cut(T_ + 1, D);
+      cut[0] = 0;
+      for (int t = 1; t < T_; ++t)
+        cut[t] = std::max(cut[t - 1], (int64_t)(std::upper_bound(eo, eo + D + 1, E / T_ * t) - eo - 1));
+      std::vector<std::thread> th;
+      for (int t = 0; t < T_; ++t)
+        if (cut[t + 1] > cut[t]) th.emplace_back(run, cut[t], cut[t + 1]);
+      for (auto& x : th) x.join();
+    }
   }
   py::list r;
   for (auto& s : outs) r.append(py::bytes(s));

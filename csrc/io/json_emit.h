@@ -28,5 +28,6 @@ pybind11::bytes emit_events_json_py(const PatternTable& T, uint64_t buf, pybind1
 pybind11::list emit_batch_json_py(const PatternTable& T, uint64_t buf, pybind11::array_t<int64_t> line_start,
                                   pybind11::array_t<int32_t> line_len, pybind11::array_t<int64_t> doc_line_off,
                                   pybind11::array_t<int32_t> ev_line, pybind11::array_t<int32_t> ev_pat,
-                                  pybind11::array_t<double> ev_score, pybind11::array_t<int64_t> ev_doc_off);
+                                  pybind11::array_t<double> ev_score, pybind11::array_t<int64_t> ev_doc_off,
+                                  int nthreads);
 }  // namespace lp

@@ -26,6 +26,7 @@ SOURCES = [
     ("kernels/lp_kernels.hip", "hip"),
     ("kernels/nfa_mfma.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
+    ("io/docs.cpp", "cpp"),
     ("bind.cpp", "cpp"),
 ]
 
@@ -55,7 +56,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
         objs = []
         procs = []
         # -ffp-contract=off: Java double arithmetic never fuses a*b+c; keep GPU == CPU == reference
-        base = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__"]
+        base = ["-O3", "-fPIC", "-pthread", "-std=c++17", "-ffp-contract=off", "-Wno-unused-result", "-D__HIP_PLATFORM_AMD__"]
         for rel, kind in SOURCES:
             src = os.path.join(CSRC, rel)
             if not os.path.exists(src):
@@ -78,7 +79,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
             if verbose and out:
                 sys.stdout.write(out.decode(errors="replace"))
         if force or procs or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
-            cmd = [HIPCC, "-shared", "-fPIC", "--offload-arch=" + ARCH] + objs + ["-o", OUT + ".tmp"]
+            cmd = [HIPCC, "-shared", "-fPIC", "-pthread", "--offload-arch=" + ARCH] + objs + ["-o", OUT + ".tmp"]
             if verbose:
                 print(" ".join(cmd), flush=True)
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)

@@ -25,6 +25,7 @@ and every stage is a bulk kernel over the whole batch:
 from __future__ import annotations
 
 import logging
+import os
 import time
 import uuid
 from dataclasses import dataclass, field
@@ -137,6 +138,7 @@ class Engine:
         self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
                          p.max_context_factor, p.freq_threshold, p.freq_max_penalty, float(p.freq_window_hours))
         self._pinned: Optional[torch.Tensor] = None
+        self._bstage: Optional[torch.Tensor] = None     # batch staging (pinned on GPU), reused
         if self.device.type == "cuda":
             props = torch.cuda.get_device_properties(self.device)
             self.pf_grid = int(props.multi_processor_count) * 4
@@ -422,19 +424,18 @@ class Engine:
         self._batches += 1
         if self.fault_every and self._batches % self.fault_every == 0:
             raise RuntimeError("injected device fault (engine.fault-inject-every)")
-        datas = [l.encode("utf-8", errors="surrogatepass") for l in logs_list]
-        if len(datas) == 1 and len(datas[0]) >= self.GPU_SPLIT_BYTES:
+        if len(logs_list) == 1 and len(logs_list[0]) >= self.GPU_SPLIT_BYTES:
             return [self.analyze_json(logs_list[0])]
-        doc_off = np.zeros(len(datas) + 1, np.int64)
-        np.cumsum([len(d) for d in datas], out=doc_off[1:])
-        blob = b"".join(datas)
-        hb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
         tm = {} if self.profile else None
         with TR.HostTimer(tm, "line_index"):
-            ls_h, ll_h, dl = N.split_docs(hb.ctypes.data, doc_off)
+            staged = self._stage_docs(logs_list)
+            if staged is None:              # lone surrogates: encode in Python
+                staged = self._stage_docs([l.encode("utf-8", errors="surrogatepass") for l in logs_list])
+        hb, ls_h, ll_h, dl, n = staged
+        ndocs = len(logs_list)
         if tm is not None:
             self._start(tm)
-        text, n = self.stage_text(blob)
+        text = self._stage_h2d(n)
         ls = torch.from_numpy(ls_h).to(self.device)
         ll = torch.from_numpy(ll_h).to(self.device)
         segs = Segments.from_doc_offsets(dl, self.device)
@@ -451,19 +452,51 @@ class Engine:
             score = res.score.cpu().numpy()
             ev_seg = res.ev_seg.cpu().numpy()
         with TR.HostTimer(tm, "json"):
-            bounds = np.searchsorted(ev_seg, np.arange(len(datas) + 1)).astype(np.int64)
+            bounds = np.searchsorted(ev_seg, np.arange(ndocs + 1)).astype(np.int64)
             ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,
-                                    np.ascontiguousarray(dl, np.int64), ev_line, ev_pat, score, bounds)
+                                    np.ascontiguousarray(dl, np.int64), ev_line, ev_pat, score, bounds,
+                                    self._STAGE_THREADS)
         extra = b""
         if tm is not None:
             import json
             st = {k: round(v, 4) for k, v in TR.resolve(res.timings).items()}
             st.update({k: round(v, 4) for k, v in TR.resolve(tm).items()})
-            st["batchRequests"] = len(datas)
+            st["batchRequests"] = ndocs
             log.debug("stage timings (ms): %s", st)
             extra = (',"stageTimingsMs":' + json.dumps(st, separators=(",", ":"))).encode()
-        return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0, extra)
-                for d in range(len(datas))]
+        clk = self._clock()
+        return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0, extra, clk)
+                for d in range(ndocs)]
+
+    _STAGE_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8))
+
+    def _stage_docs(self, docs):
+        """Pack request bodies into the (pinned) batch staging buffer and build the per-document
+        line index, in native code with the GIL released (csrc/io/docs.cpp): one host copy per
+        byte. Returns (host view, line_start, line_len, doc_line_off, nbytes) or None."""
+        if self._bstage is None:
+            self._bstage = torch.empty(K.padded_len(1 << 20), dtype=torch.uint8,
+                                       pin_memory=self.device.type == "cuda")
+        cap = self._bstage.numel() - K.TEXT_PAD - K.NL_TILE
+        r = N.pack_split_docs(docs, self._bstage.data_ptr(), cap, self._STAGE_THREADS)
+        if r is None:
+            return None
+        if isinstance(r, int):
+            size = K.padded_len(max(int(r), 1 << 20) * 5 // 4)
+            self._bstage = torch.empty(size, dtype=torch.uint8, pin_memory=self.device.type == "cuda")
+            r = N.pack_split_docs(docs, self._bstage.data_ptr(), size - K.TEXT_PAD - K.NL_TILE, self._STAGE_THREADS)
+        ls_h, ll_h, dl, doc_off = r
+        n = int(doc_off[-1])
+        return self._bstage.numpy(), ls_h, ll_h, dl, n
+
+    def _stage_h2d(self, n: int) -> torch.Tensor:
+        size = K.padded_len(n)
+        self._bstage[n:size].zero_()
+        if self.device.type == "cuda":
+            dev = torch.empty(size, dtype=torch.uint8, device=self.device)
+            dev.copy_(self._bstage[:size], non_blocking=True)
+            return dev
+        return self._bstage[:size]
 
     def _log_events(self, res: RunResult, doc_line_off) -> None:
         """Reference-style match / factor logs (AnalysisService.java:96-99 INFO per match,
@@ -507,17 +540,22 @@ class Engine:
                                          ev_line, ev_pat, score)
         return self._wrap(events_json, ev_pat, int(ls_h.size), t0)
 
+    @staticmethod
+    def _clock() -> tuple:
+        now = time.time()
+        return now, datetime.fromtimestamp(now, timezone.utc).isoformat().replace("+00:00", "Z")
+
     _EMPTY_SUMMARY = b',"summary":{"significantEvents":0,"highestSeverity":"NONE","severityDistribution":{}}}'
 
     def _wrap(self, events_json: bytes, ev_pat: np.ndarray, total_lines: int, t0: float,
-              extra_meta: bytes = b"") -> bytes:
-        """AnalysisResult JSON around the natively emitted events array (AnalysisService.java:115-121)."""
+              extra_meta: bytes = b"", clock: Optional[tuple] = None) -> bytes:
+        """AnalysisResult JSON around the natively emitted events array (AnalysisService.java:115-121).
+        ``clock`` = (now, ISO timestamp) shared by every request of a batch (they finish together)."""
         import json
         pu = getattr(self, "_patterns_used_json", None)
         if pu is None:
             pu = self._patterns_used_json = json.dumps(self.lib.library_ids, separators=(",", ":"))
-        now = time.time()
-        ts = datetime.fromtimestamp(now, timezone.utc).isoformat().replace("+00:00", "Z")
+        now, ts = clock if clock is not None else self._clock()
         head = (f'{{"analysisId":"{uuid.uuid4()}","metadata":{{"processingTimeMs":{int((now - t0) * 1000)},'
                 f'"totalLines":{total_lines},"analyzedAt":"{ts}","patternsUsed":{pu}').encode() \
             + extra_meta + b'},"events":'

@@ -20,6 +20,7 @@ import asyncio
 import logging
 import threading
 import time
+from collections import deque
 from concurrent.futures import Future
 from typing import List, Optional
 
@@ -49,7 +50,7 @@ class Batcher:
         self.metrics = metrics
         self.fallback_cpu = bool(engine.config.get("engine.fallback-cpu", True))
         self._cpu_engine: Optional[Engine] = None
-        self._q: List[tuple] = []
+        self._q: "deque[tuple]" = deque()
         self._cv = threading.Condition()
         self._stop = False
         self._t = threading.Thread(target=self._loop, name="lp-batcher", daemon=True)
@@ -82,7 +83,7 @@ class Batcher:
                 item = self._q[0]
                 if batch and size + len(item[0]) > self.max_bytes:
                     break
-                batch.append(self._q.pop(0))
+                batch.append(self._q.popleft())
                 size += len(item[0])
             return batch
 

@@ -78,3 +78,30 @@ def test_frequency_state_snapshot(tmp_path):
     t[0] = 3600.5
     assert list(st2.carry(["a"])) == [0]
     assert st.get_pattern_frequency("zzz") is None
+
+
+def test_pack_split_docs_equals_java_split():
+    """Native batch staging (csrc/io/docs.cpp) == Java String.split per document, for str and
+    bytes bodies, across the parallel document partition."""
+    import random
+    import numpy as np
+    from log_parser_amd.native import N
+    from log_parser_amd import golden
+    rng = random.Random(3)
+    docs = ["", "\n", "\n\n", "a", "a\n", "a\r\n\r\n", "\r\n", "x\ry\n", "é\nü\r\n"]
+    for _ in range(400):
+        parts = [rng.choice(["", "a", "\r", "é", "line with words", "日本"]) * rng.randint(0, 4) +
+                 rng.choice(["\n", "\r\n", "\n", ""]) for _ in range(rng.randint(0, 60))]
+        docs.append("".join(parts))
+    docs += ["z" * 300000 + "\n" + "y" * 10] * 12          # > 1 MiB total: several threads
+    total = sum(len(d.encode()) for d in docs)
+    buf = np.zeros(total + 64, np.uint8)
+    for nthreads in (1, 8):
+        ls, ll, dl, off = N.pack_split_docs(docs, buf.ctypes.data, buf.size, nthreads)
+        blob = buf[:total].tobytes()
+        assert blob == "".join(docs).encode()
+        for d, s in enumerate(docs):
+            got = [blob[a:a + b].decode() for a, b in zip(ls[dl[d]:dl[d + 1]], ll[dl[d]:dl[d + 1]])]
+            assert got == golden.split_lines(s), (d, s[:40])
+    assert N.pack_split_docs(docs, buf.ctypes.data, 10, 1) == total       # too small: needed size
+    assert N.pack_split_docs(["a\ud800b"], buf.ctypes.data, buf.size, 1) is None   # lone surrogate

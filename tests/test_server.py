@@ -132,3 +132,21 @@ def test_stage_timings_opt_in(tmp_path):
     assert st["batchRequests"] == 2
     assert "stageTimingsMs" not in b["metadata"]
     assert [e["lineNumber"] for e in a["events"]] == [e["lineNumber"] for e in b["events"]]
+
+
+def test_parse_special_characters_roundtrip(client, lib_dir):
+    """Context lines with quotes, backslashes, control characters and non-ASCII text survive the
+    native JSON emitter (csrc/io/json_emit.cpp) exactly."""
+    from log_parser_amd.models.library import load_pattern_directory
+    sets = load_pattern_directory(lib_dir[0])
+    base = make_log(400, lib_dir[1], seed=9, hit_rate=0.1).split("\n")
+    junk = [' "quoted" ', "back\\slash", "\ttab", "\x01\x1f\x7f", "é日本😀", "\\\"", "\b\f"]
+    logs = "\n".join(l + junk[i % len(junk)] for i, l in enumerate(base))
+    client.delete("/admin/frequency")
+    r = client.post("/parse", json={"pod": {"metadata": {"name": "p2"}}, "logs": logs})
+    assert r.status_code == 200
+    res = r.json()
+    g = golden.analyze(logs, sets, ScoringParams(), golden.FrequencyTracker(ScoringParams()))
+    assert len(res["events"]) == len(g["events"]) > 0
+    for a, b in zip(res["events"], g["events"]):
+        assert a["context"] == b["context"]

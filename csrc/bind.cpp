@@ -208,6 +208,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
   m.def("dfa_find", &dfa_find_py, py::arg("pattern"), py::arg("line"), py::arg("max_states") = 4096);
   m.def("split_docs", &split_docs);
+  m.def("set_host_threads", &set_host_threads);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8);
   m.def("nl_tiles", &nl_tiles);

@@ -7,6 +7,8 @@
 namespace lp {
 
 int64_t nl_tiles(int64_t nbytes);
+// worker threads of the host twins (CPU backend)
+void set_host_threads(int n);
 void pull_dev(const uint8_t* host_src, uint8_t* dst, int64_t nbytes, int grid, uint64_t stream);
 void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream);
 // flag_cr: set bit 62 of a position when the '\n' follows a '\r' (consumed by lines_dev)

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "lp_api.h"
@@ -30,6 +31,25 @@ namespace lp {
   } while (0)
 
 static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- host twins: the CPU backend (no-GPU serving, availability fallback, tests). Parallel over
+// independent items with plain threads; results are order-insensitive (callers sort/unique).
+static int g_host_threads = 8;
+void set_host_threads(int n) { g_host_threads = std::max(1, n); }
+
+template <class F>
+static void host_parallel(int64_t n, int64_t grain, F&& fn) {
+  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(g_host_threads, n / std::max<int64_t>(grain, 1)));
+  if (T <= 1) {
+    fn(0, 0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int t = 0; t < T; ++t) th.emplace_back([&, t] { fn(t, n * t / T, n * (t + 1) / T); });
+  for (auto& x : th) x.join();
+}
+
 
 // ------------------------------------------------------------------------------------------
 // K1: newline index.  16 KiB tile per 256-thread block, 64 B per thread (4 x dwordx4 loads).
@@ -500,17 +520,19 @@ void feat_dev(const int32_t* lines, int64_t n, const uint8_t* text, const int64_
 
 void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
                const DfaPool& P, uint8_t* feat) {
-  for (int64_t i = 0; i < n; ++i) {
-    const int32_t line = lines[i];
-    const uint8_t* s = text + line_start[line];
-    const int len = line_len[line];
-    uint8_t f = 0;
-    if (dfa_run(P, 0, s, len)) f |= 1;
-    else if (dfa_run(P, 1, s, len)) f |= 2;
-    if (dfa_run(P, 2, s, len)) f |= 4;
-    if (dfa_run(P, 3, s, len)) f |= 8;
-    feat[line] = f;
-  }
+  host_parallel(n, 2048, [&](int, int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const int32_t line = lines[i];
+      const uint8_t* s = text + line_start[line];
+      const int len = line_len[line];
+      uint8_t f = 0;
+      if (dfa_run(P, 0, s, len)) f |= 1;
+      else if (dfa_run(P, 1, s, len)) f |= 2;
+      if (dfa_run(P, 2, s, len)) f |= 4;
+      if (dfa_run(P, 3, s, len)) f |= 8;
+      feat[line] = f;
+    }
+  });
 }
 
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
@@ -594,48 +616,70 @@ int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos) 
 
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap) {
-  int64_t count = 0;
-  auto app = [&](int64_t v) { if (count < cap) cand[count] = v; ++count; };
-  const uint32_t* bl = T.bloom;
-  for (int64_t p = 0; p < nbytes; ++p) {
+  std::vector<std::vector<int64_t>> part(std::max(1, g_host_threads));
+  host_parallel(nbytes, 1 << 18, [&](int t, int64_t a, int64_t b) {
+    auto& out = part[t];
+    auto app = [&](int64_t v) { out.push_back(v); };
+    const uint32_t* bl = T.bloom;
+    // rolling lower-cased 4-gram starting at p (bytes past the end read as 0)
     uint32_t g4 = 0;
-    for (int k = 3; k >= 0; --k) g4 = (g4 << 8) | (uint32_t)(p + k < nbytes ? lower_byte(text[p + k]) : 0);
-    for (int g = 4; g >= 2; --g) {
-      if (!(T.gmask & (1 << g))) continue;
-      const uint32_t key = g4 & gram_mask(g);
-      if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
-      pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
+    for (int k = 3; k >= 0; --k) g4 = (g4 << 8) | (uint32_t)(a + k < nbytes ? lower_byte(text[a + k]) : 0);
+    for (int64_t p = a; p < b; ++p) {
+      for (int g = 4; g >= 2; --g) {
+        if (!(T.gmask & (1 << g))) continue;
+        const uint32_t key = g4 & gram_mask(g);
+        if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
+        pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
+      }
+      g4 = (g4 >> 8) | ((uint32_t)(p + 4 < nbytes ? lower_byte(text[p + 4]) : 0) << 24);
     }
-  }
+  });
+  int64_t count = 0;
+  for (auto& v : part)
+    for (int64_t x : v) {
+      if (count < cap) cand[count] = x;
+      ++count;
+    }
   return count;
 }
 
 void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start,
                  const int32_t* line_len, const DfaPool& P, uint8_t* out) {
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t k = cand[i];
-    const int r = (int)(k >> 32);
-    const int64_t line = k & 0xFFFFFFFFll;
-    out[i] = dfa_run(P, r, text + line_start[line], line_len[line]) ? 1 : 0;
-  }
+  host_parallel(n, 4096, [&](int, int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      const int64_t k = cand[i];
+      const int r = (int)(k >> 32);
+      const int64_t line = k & 0xFFFFFFFFll;
+      out[i] = dfa_run(P, r, text + line_start[line], line_len[line]) ? 1 : 0;
+    }
+  });
 }
 
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                   const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap) {
+  if (nregs == 0) return 0;
+  std::vector<std::vector<int64_t>> part(std::max(1, g_host_threads));
+  host_parallel(nlines, 2048, [&](int t, int64_t a, int64_t b) {
+    for (int64_t line = a; line < b; ++line)
+      for (int j = 0; j < nregs; ++j)
+        if (dfa_run(P, regs[j], text + line_start[line], line_len[line]))
+          part[t].push_back(((int64_t)regs[j] << 32) | line);
+  });
   int64_t c = 0;
-  for (int64_t line = 0; line < nlines; ++line)
-    for (int j = 0; j < nregs; ++j)
-      if (dfa_run(P, regs[j], text + line_start[line], line_len[line])) {
-        if (c < cap) out[c] = ((int64_t)regs[j] << 32) | line;
-        ++c;
-      }
+  for (auto& v : part)
+    for (int64_t x : v) {
+      if (c < cap) out[c] = x;
+      ++c;
+    }
   return c;
 }
 
 void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
                 const ScoreTables& T, const ScoreParams& S, double* out, double* factors) {
-  for (int64_t i = 0; i < n; ++i)
-    out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
+  host_parallel(n, 1024, [&](int, int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i)
+      out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
+  });
 }
 
 }  // namespace lp

@@ -35,6 +35,9 @@ def load():
         from . import _build
         _build.build()
     _mod = importlib.import_module("log_parser_amd._lpnative")
+    # CPU-backend worker threads: this process's CPU share, at most 16 (LP_HOST_THREADS overrides)
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
+    _mod.set_host_threads(int(os.environ.get("LP_HOST_THREADS", min(16, n))))
     return _mod
 
 

@@ -28,6 +28,7 @@ import logging
 import os
 import time
 import uuid
+import warnings
 from dataclasses import dataclass, field
 from datetime import datetime, timezone
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -116,6 +117,13 @@ class RunResult:
     timings: Dict[str, float] = field(default_factory=dict)
 
 
+def _ro_view(data) -> torch.Tensor:
+    """uint8 tensor view of a bytes-like object without copying (never written through)."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")            # "non-writable buffer" -- we only read it
+        return torch.from_numpy(np.frombuffer(data, dtype=np.uint8))
+
+
 class Engine:
     def __init__(self, library: CompiledLibrary, config: Optional[Config] = None,
                  device: Optional[torch.device] = None, freq: Optional[FrequencyState] = None):
@@ -150,7 +158,8 @@ class Engine:
         """Copy request bytes into a padded device buffer (pinned staging + async H2D)."""
         n = len(data)
         size = K.padded_len(n)
-        src = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.empty(0, dtype=torch.uint8)
+        # read-only zero-copy view of the request bytes; copied once (multi-threaded) into staging
+        src = _ro_view(data) if n else torch.empty(0, dtype=torch.uint8)
         if self.device.type == "cuda":
             if self._pinned is None or self._pinned.numel() < size:
                 self._pinned = torch.empty(max(size, 1 << 20), dtype=torch.uint8, pin_memory=True)

@@ -1,0 +1,103 @@
+// Host-side self test for the sanitizer builds: ASan+UBSan and TSan binaries built by
+// tools/sanitize_host.sh / tests/test_sanitizers.py from the pure-C++ sources (no HIP, no Python).
+//
+//  * fuzzes the Java-regex compiler (parser, Glushkov builder, subset construction) with random
+//    token strings, and checks the prefilter soundness invariant on random subjects: a line the
+//    DFA matches contains at least one of the regex's required literals (ASCII-lowercased);
+//  * runs the parallel request-batch packer/splitter (csrc/io/docs.cpp) with 1 and 8 threads on
+//    random documents and requires identical results (TSan watches the worker threads).
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "io/docs.h"
+#include "regex/jregex.h"
+
+using namespace lp;
+
+static int failures = 0;
+#define CHECK(c, ...)                         \
+  do {                                        \
+    if (!(c)) {                               \
+      std::fprintf(stderr, "FAIL: " __VA_ARGS__); \
+      std::fprintf(stderr, "\n");             \
+      ++failures;                             \
+    }                                         \
+  } while (0)
+
+static std::string lower(const std::string& s) {
+  std::string o = s;
+  for (auto& c : o)
+    if (c >= 'A' && c <= 'Z') c = (char)(c + 32);
+  return o;
+}
+
+static void fuzz_regex(int iters, uint32_t seed) {
+  static const char* toks[] = {"a", "b", "c", "ab", "Error", "x", ".", "*", "+", "?", "|", "(", ")", "(?:", "[",
+                               "]", "[a-c]", "[^x]", "\\d", "\\w", "\\s", "\\b", "\\B", "^", "$", "{2}", "{1,3}",
+                               "\\.", "(?i)", "é", "\\Q.*\\E", "[[a]&&[b]]", "\\p{L}", "-", "0", "9", " "};
+  const int ntok = sizeof(toks) / sizeof(toks[0]);
+  std::mt19937 rng(seed);
+  int dfa = 0, invalid = 0;
+  for (int it = 0; it < iters; ++it) {
+    std::string p;
+    const int n = 1 + rng() % 10;
+    for (int i = 0; i < n; ++i) p += toks[rng() % ntok];
+    Compiled c = compile(p, 256, 512);
+    if (c.kind == Kind::INVALID) { ++invalid; continue; }
+    if (c.kind != Kind::DFA) continue;
+    ++dfa;
+    for (int s = 0; s < 40; ++s) {
+      std::string subj;
+      const int m = rng() % 24;
+      for (int i = 0; i < m; ++i) subj += "abcxE rRo.9_\n"[rng() % 13];
+      if (rng() % 3 == 0) subj += "Error";
+      const bool hit = dfa_find(c.dfa, reinterpret_cast<const uint8_t*>(subj.data()), (int64_t)subj.size());
+      if (hit && c.has_literals) {
+        const std::string ls = lower(subj);
+        bool any = false;
+        for (auto& lit : c.literals) any |= ls.find(lit) != std::string::npos;
+        CHECK(any, "regex %s matched '%s' without any required literal", p.c_str(), subj.c_str());
+      }
+    }
+  }
+  std::printf("regex fuzz: %d patterns, %d DFA, %d invalid\n", iters, dfa, invalid);
+}
+
+static void docs_threads(uint32_t seed) {
+  std::mt19937 rng(seed);
+  std::vector<std::string> docs;
+  for (int d = 0; d < 3000; ++d) {
+    std::string s;
+    const int parts = rng() % 40;
+    for (int i = 0; i < parts; ++i) {
+      s += std::string(rng() % 12, "ab\r x"[rng() % 5]);
+      s += (rng() % 4) ? "\n" : "\r\n";
+    }
+    if (d % 97 == 0) s += std::string(400000, 'z');
+    docs.push_back(s);
+  }
+  std::vector<const char*> src;
+  std::vector<int64_t> off(1, 0);
+  for (auto& s : docs) { src.push_back(s.data()); off.push_back(off.back() + (int64_t)s.size()); }
+  std::vector<uint8_t> b1(off.back() + 1), b8(off.back() + 1);
+  DocBatchIndex i1, i8;
+  pack_split_docs(src.data(), off.data(), (int64_t)docs.size(), b1.data(), 1, i1);
+  pack_split_docs(src.data(), off.data(), (int64_t)docs.size(), b8.data(), 8, i8);
+  CHECK(b1 == b8, "packed bytes differ between 1 and 8 threads");
+  CHECK(i1.line_start == i8.line_start && i1.line_len == i8.line_len && i1.doc_line_off == i8.doc_line_off,
+        "line index differs between 1 and 8 threads");
+  std::printf("docs: %zu docs, %zu lines\n", docs.size(), i8.line_start.size());
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 3000;
+  fuzz_regex(iters, 12345);
+  docs_threads(777);
+  const uint8_t t[] = {'a', 0xE2, 0x80, 0xA8};
+  CHECK(final_terminator_len(t, 4) == 3, "U+2028 final terminator");
+  std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
+  return failures ? 1 : 0;
+}

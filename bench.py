@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--profile", action="store_true", help="per-stage HIP-event timings (no extra syncs)")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--parse-requests", type=int, default=30,
+                    help="rank 0: p50 latency of N single 10k-line /parse requests after the timed loop (0 = off)")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
     return ap.parse_args()
@@ -176,6 +178,21 @@ def main():
         }
         if args.profile:
             rec["timings_ms_last_step_rank0"] = {k: round(v, 3) for k, v in TR.resolve(last.result.timings).items()}
+        if args.parse_requests > 0:
+            # second half of the BASELINE metric: p50 latency of one /parse request (10k-line pod
+            # log, same 1k-pattern library) through the serving engine path (staging, kernels,
+            # JSON). Measured after the timed loop, outside it; HTTP framing excluded.
+            req = make_log(10_000, trig, seed=13, hit_rate=0.01)
+            for _ in range(3):
+                eng.analyze_batch_json([req])
+            lat = []
+            for _ in range(args.parse_requests):
+                t1 = time.perf_counter()
+                eng.analyze_batch_json([req])
+                lat.append(time.perf_counter() - t1)
+            rec["p50_parse_ms"] = round(float(np.median(lat)) * 1e3, 3)
+            rec["p99_parse_ms"] = round(float(np.percentile(lat, 99)) * 1e3, 3)
+            rec["config"]["parse_request_lines"] = 10_000
         print(json.dumps(rec), flush=True)
     if args.torch_trace:                                         # untimed, after the measurement
         with TR.torch_profile(args.torch_trace.replace(".json", f".rank{rank}.json"), device):

@@ -382,9 +382,21 @@ class Engine:
             c = np.zeros(1, np.int64)
         return torch.from_numpy(c).to(self.device)
 
-    def commit_frequency(self, counts: torch.Tensor) -> None:
-        if counts.numel():
-            self.freq.record_counts(self.lib.freq_ids, counts.cpu().numpy())
+    def commit_frequency(self, counts) -> None:
+        """Record this batch's per-id match counts (tensor or host array) in the sliding window."""
+        if len(counts):
+            self.freq.record_counts(self.lib.freq_ids, counts.cpu().numpy() if torch.is_tensor(counts) else counts)
+
+    @staticmethod
+    def _results_to_host(res: "RunResult"):
+        """events (line, pattern, segment: int32; score: f64) + frequency counts (int64) in ONE
+        device->host copy (one sync instead of five)."""
+        n = res.ev_line.numel()
+        parts = [res.ev_line.to(torch.int32), res.ev_pat.to(torch.int32), res.ev_seg.to(torch.int32),
+                 res.score.contiguous().view(torch.int32), res.freq_counts.to(torch.int64).contiguous().view(torch.int32)]
+        h = torch.cat(parts).cpu().numpy()
+        return (h[:n], h[n:2 * n], h[2 * n:3 * n], h[3 * n:5 * n].view(np.float64),
+                h[5 * n:].view(np.int64))
 
     def summary(self, ev_pat_host: np.ndarray) -> dict:
         if ev_pat_host.size == 0:
@@ -454,12 +466,9 @@ class Engine:
         res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose, timings=tm)
         if verbose:
             self._log_events(res, dl)
-        self.commit_frequency(res.freq_counts)
         with TR.HostTimer(tm, "d2h"):
-            ev_line = res.ev_line.cpu().numpy()
-            ev_pat = res.ev_pat.cpu().numpy()
-            score = res.score.cpu().numpy()
-            ev_seg = res.ev_seg.cpu().numpy()
+            ev_line, ev_pat, ev_seg, score, counts = self._results_to_host(res)
+        self.commit_frequency(counts)
         with TR.HostTimer(tm, "json"):
             bounds = np.searchsorted(ev_seg, np.arange(ndocs + 1)).astype(np.int64)
             ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,

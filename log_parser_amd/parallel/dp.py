@@ -11,6 +11,9 @@ resolved with collectives:
   C4  backward sequence chain  (ScoringService.java:296-305)  /   [own_lines | freq counts | chain]
   C5/C6 severity histogram + frequency histogram               -> all_reduce(sum)
   C7  top-k events                                             -> all_gather of k rows, merge
+  C2  halos: by default every rank stages its halo lines from the shared host source together
+      with its own lines (no extra collective); ``exchange_halos`` is the point-to-point variant
+      (batch_isend_irecv with both neighbours) for ranks that only hold their own lines
 
 Every message but the top-k rows is a few KB, so each step pays ~3 latency-bound collectives
 regardless of log size; xGMI bandwidth is irrelevant, PCIe ingest and HBM are what scale.
@@ -162,6 +165,76 @@ class ShardedAnalyzer:
         if best is None and first_pat is not None:
             best = lib.severity[first_pat]
         return {"significantEvents": n, "highestSeverity": best, "severityDistribution": dist_}
+
+
+def halo_bytes(data, n_lines: int) -> tuple:
+    """(head, tail): byte length of the first / last ``n_lines`` lines of ``data`` (a shard made of
+    complete '\\n'-terminated lines, the last rank's final line may be unterminated)."""
+    n = len(data)
+    head, pos = 0, 0
+    for _ in range(n_lines):
+        j = data.find(b"\n", pos)
+        if j < 0:
+            head = n
+            break
+        head = pos = j + 1
+    end = n
+    start = n
+    for _ in range(n_lines):
+        j = data.rfind(b"\n", 0, start - 1) if start > 0 else -1
+        start = j + 1
+        if start == 0:
+            break
+    return head, end - start
+
+
+def exchange_halos(own: torch.Tensor, own_nbytes: int, head: int, tail: int, group=None):
+    """C2: point-to-point halo exchange with the neighbour ranks (RCCL send/recv over
+    one xGMI hop; gloo on CPU). Sends ``own[:head]`` (first H lines) to rank-1 and
+    ``own[own_nbytes-tail:own_nbytes]`` (last H lines) to rank+1; returns (left, right) halos.
+    Sizes travel first in one tiny all_gather so every receive is posted with its exact length."""
+    r, w = world()
+    dev = own.device
+    if w == 1:
+        z = torch.empty(0, dtype=torch.uint8, device=dev)
+        return z, z
+    sizes = all_gather_rows(torch.tensor([head, tail], dtype=torch.int64, device=dev), group).cpu()
+    lsize = int(sizes[r - 1, 1]) if r > 0 else 0
+    rsize = int(sizes[r + 1, 0]) if r < w - 1 else 0
+    left = torch.empty(lsize, dtype=torch.uint8, device=dev)
+    right = torch.empty(rsize, dtype=torch.uint8, device=dev)
+    peer = (lambda x: dist.get_global_rank(group, x)) if group is not None else (lambda x: x)
+    ops = []
+    if r > 0 and head:
+        ops.append(dist.P2POp(dist.isend, own[:head].contiguous(), peer(r - 1), group))
+    if r > 0 and lsize:
+        ops.append(dist.P2POp(dist.irecv, left, peer(r - 1), group))
+    if r < w - 1 and tail:
+        ops.append(dist.P2POp(dist.isend, own[own_nbytes - tail:own_nbytes].contiguous(), peer(r + 1), group))
+    if r < w - 1 and rsize:
+        ops.append(dist.P2POp(dist.irecv, right, peer(r + 1), group))
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    return left, right
+
+
+def assemble_shard(own: torch.Tensor, own_nbytes: int, left: torch.Tensor, right: torch.Tensor):
+    """[left halo | own | right halo | zero pad] as one padded device text + its line index and
+    halo line counts (halo lines are complete, so they are counted by their '\\n's)."""
+    from ..ops import kernels as K
+    n = left.numel() + own_nbytes + right.numel()
+    text = torch.zeros(K.padded_len(n), dtype=torch.uint8, device=own.device)
+    a = left.numel()
+    text[:a] = left
+    text[a:a + own_nbytes] = own[:own_nbytes]
+    text[a + own_nbytes:n] = right
+    ls, ll = K.split_lines(text, n)
+    hl = int((left == 10).sum().item()) if a else 0
+    hr = 0
+    if right.numel():
+        hr = int((right == 10).sum().item()) + (0 if int(right[-1].item()) == 10 else 1)
+    return text, n, ls, ll, hl, hr
 
 
 def shard_bounds(n_lines: int, world_size: int, rank: int, halo: int):

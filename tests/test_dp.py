@@ -112,3 +112,55 @@ def test_sharded_equals_single(world):
         np.testing.assert_allclose(scores, rs, rtol=1e-13, atol=0)
         top = np.sort(rs)[::-1][:5]
         np.testing.assert_allclose(got[0][s][4], top, rtol=1e-13)
+
+
+def _worker_p2p(rank, world, port, q):
+    """Each rank holds ONLY its own lines; halos come from the neighbours over send/recv (C2)."""
+    from log_parser_amd.parallel.dp import assemble_shard, exchange_halos, halo_bytes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lib, data = _setup()
+        eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+        full = _text(data)
+        gls, gll = K.split_lines(full, len(data))
+        L = gls.numel()
+        lo, hi, _, _ = shard_bounds(L, world, rank, lib.halo)
+        base = int(gls[lo])
+        end = int(gls[hi]) if hi < L else len(data)
+        own_b = data[base:end]
+        head, tail = halo_bytes(own_b, lib.halo)
+        own = _text(own_b)
+        left, right = exchange_halos(own, len(own_b), head, tail)
+        t, n, ls, ll, hl, hr = assemble_shard(own, len(own_b), left, right)
+        sa = ShardedAnalyzer(eng)
+        res = []
+        for _ in range(STEPS):
+            out = sa.step(t, n, ls, ll, hl, hr, topk=5)
+            r = out.result
+            gl = (r.ev_line.numpy().astype(np.int64) - hl + out.own_start)
+            res.append((gl, r.ev_pat.numpy(), r.score.numpy(), out.total_lines,
+                        None if out.topk_score is None else out.topk_score.numpy()))
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_p2p_halo_exchange_equals_single(world):
+    ref = _reference()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_p2p, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for s in range(STEPS):
+        rl, rp, rs = ref[s]
+        np.testing.assert_array_equal(np.concatenate([got[r][s][0] for r in range(world)]), rl)
+        np.testing.assert_array_equal(np.concatenate([got[r][s][1] for r in range(world)]), rp)
+        np.testing.assert_allclose(np.concatenate([got[r][s][2] for r in range(world)]), rs, rtol=1e-13, atol=0)

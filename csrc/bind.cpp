@@ -70,6 +70,24 @@ static ScoreParams sp_from(const py::tuple& t) {
   return S;
 }
 
+// (prim_off, prim_pats, freq_key, ctx_before, ctx_after, seg_lo, seg_hi, own_lo, own_hi, nseg, nkeys, pbits)
+static EvTables ev_from(const py::tuple& t) {
+  EvTables E;
+  E.prim_off = P<const int64_t>(t[0].cast<uint64_t>());
+  E.prim_pats = P<const int32_t>(t[1].cast<uint64_t>());
+  E.freq_key = P<const int32_t>(t[2].cast<uint64_t>());
+  E.ctx_before = P<const int32_t>(t[3].cast<uint64_t>());
+  E.ctx_after = P<const int32_t>(t[4].cast<uint64_t>());
+  E.seg_lo = P<const int32_t>(t[5].cast<uint64_t>());
+  E.seg_hi = P<const int32_t>(t[6].cast<uint64_t>());
+  E.own_lo = P<const int32_t>(t[7].cast<uint64_t>());
+  E.own_hi = P<const int32_t>(t[8].cast<uint64_t>());
+  E.nseg = t[9].cast<int>();
+  E.nkeys = t[10].cast<int>();
+  E.pbits = t[11].cast<int>();
+  return E;
+}
+
 static py::bytes vbytes(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
 
 static py::dict compile_regex(const std::string& pat, int max_states, int max_positions) {
@@ -229,18 +247,23 @@ PYBIND11_MODULE(_lpnative, m) {
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
                   P<unsigned long long>(count), grid, s); });
   m.def("pf_verify_dev", [](uint64_t gh, int64_t n, uint64_t text, int64_t nb, py::tuple pf, uint64_t ls, int64_t nl,
-                            uint64_t blk, uint64_t cand, int64_t cap, uint64_t count, uint64_t s) {
+                            uint64_t blk, uint64_t cand, int64_t cap, uint64_t count, uint64_t s, uint64_t dn) {
     pf_verify_dev(P<const int64_t>(gh), n, P<const uint8_t>(text), nb, pf_from(pf), P<const int64_t>(ls), nl,
-                  P<const int32_t>(blk), P<int64_t>(cand), cap, P<unsigned long long>(count), s); });
+                  P<const int32_t>(blk), P<int64_t>(cand), cap, P<unsigned long long>(count), s,
+                  P<const unsigned long long>(dn)); }, py::arg("gh"), py::arg("n"), py::arg("text"), py::arg("nb"),
+        py::arg("pf"), py::arg("ls"), py::arg("nl"), py::arg("blk"), py::arg("cand"), py::arg("cap"), py::arg("count"),
+        py::arg("s"), py::arg("dn") = 0);
   m.def("verify_dev", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out, uint64_t s) {
     verify_dev(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out), s); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
                        uint64_t out, int64_t cap, uint64_t count, uint64_t s) {
     scan_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs), nregs,
              dfa_from(dfa), P<int64_t>(out), cap, P<unsigned long long>(count), s); });
-  m.def("score_dev", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t ef, int64_t n, py::tuple st, py::tuple sp,
-                        uint64_t out, uint64_t fac, uint64_t s) {
-    score_dev(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), P<const int64_t>(ef), n, st_from(st),
+  // ev_rank / ev_fkey / carry: frequency count before each event = carry[fkey] + rank (fused)
+  m.def("score_dev", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry, int64_t n,
+                        py::tuple st, py::tuple sp, uint64_t out, uint64_t fac, uint64_t s) {
+    const FreqIn F{P<const int64_t>(rank), P<const int64_t>(fkey), P<const int64_t>(carry)};
+    score_dev(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), F, n, st_from(st),
               sp_from(sp), P<double>(out), P<double>(fac), s); });
 
   // ---- host twins
@@ -253,10 +276,50 @@ PYBIND11_MODULE(_lpnative, m) {
                         uint64_t out, int64_t cap) {
     return scan_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs),
                      nregs, dfa_from(dfa), P<int64_t>(out), cap); });
-  m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t ef, int64_t n, py::tuple st, py::tuple sp,
-                         uint64_t out, uint64_t fac) {
-    score_host(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), P<const int64_t>(ef), n, st_from(st),
+  m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry,
+                         int64_t n, py::tuple st, py::tuple sp, uint64_t out, uint64_t fac) {
+    const FreqIn F{P<const int64_t>(rank), P<const int64_t>(fkey), P<const int64_t>(carry)};
+    score_host(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), F, n, st_from(st),
                sp_from(sp), P<double>(out), P<double>(fac)); });
+
+  // ---- post-match pipeline (lp_post.hip); device calls return the workspace bytes they need and
+  // only run when ws_bytes suffices
+  m.def("bits_for", &bits_for);
+  m.def("post_hits", [](uint64_t cand, int64_t n, int64_t pre_from, int lbits, int rbits, int R, uint64_t text,
+                        uint64_t ls, uint64_t ll, py::tuple dfa, py::tuple ev, uint64_t hits, uint64_t hit_line,
+                        uint64_t hit_off, uint64_t ev_cnt, uint64_t ev_end, uint64_t counters, uint64_t ws,
+                        size_t ws_bytes, uint64_t s, bool dev) -> size_t {
+    HitsArgs A;
+    A.cand = P<const int64_t>(cand); A.n = n; A.pre_from = pre_from; A.lbits = lbits; A.rbits = rbits; A.R = R;
+    A.text = P<const uint8_t>(text); A.ls = P<const int64_t>(ls); A.ll = P<const int32_t>(ll);
+    A.dfa = dfa_from(dfa); A.ev = ev_from(ev);
+    A.hits = P<int64_t>(hits); A.hit_line = P<int32_t>(hit_line); A.hit_off = P<int64_t>(hit_off);
+    A.ev_cnt = P<int64_t>(ev_cnt); A.ev_end = P<int64_t>(ev_end); A.counters = P<int64_t>(counters);
+    if (dev) return hits_dev(A, P<void>(ws), ws_bytes, s);
+    py::gil_scoped_release nogil;
+    hits_host(A);
+    return 0;
+  });
+  m.def("post_events", [](uint64_t hits, int64_t nh, uint64_t ev_cnt, uint64_t ev_end, int64_t ne, int64_t L, int lbits,
+                          py::tuple ev, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t ev_line,
+                          uint64_t ev_pat, uint64_t ev_seg, uint64_t ev_rank, uint64_t ev_fkey, uint64_t freq_counts,
+                          uint64_t feat, uint64_t cov, uint64_t ws, size_t ws_bytes, uint64_t s, bool dev) -> size_t {
+    EventsArgs A;
+    A.hits = P<const int64_t>(hits); A.nh = nh; A.ev_cnt = P<const int64_t>(ev_cnt);
+    A.ev_end = P<const int64_t>(ev_end); A.ne = ne; A.L = L; A.lbits = lbits; A.ev = ev_from(ev);
+    A.text = P<const uint8_t>(text); A.ls = P<const int64_t>(ls); A.ll = P<const int32_t>(ll); A.dfa = dfa_from(dfa);
+    A.ev_line = P<int32_t>(ev_line); A.ev_pat = P<int32_t>(ev_pat); A.ev_seg = P<int32_t>(ev_seg);
+    A.ev_rank = P<int64_t>(ev_rank); A.ev_fkey = P<int64_t>(ev_fkey); A.freq_counts = P<int64_t>(freq_counts);
+    A.feat = P<uint8_t>(feat); A.cov = P<int32_t>(cov);
+    if (dev) return events_dev(A, P<void>(ws), ws_bytes, s);
+    py::gil_scoped_release nogil;
+    events_host(A);
+    return 0;
+  });
+  m.def("blk_index", [](uint64_t ls, int64_t L, int64_t nblocks, uint64_t blk, uint64_t s, bool dev) {
+    if (dev) blk_index_dev(P<const int64_t>(ls), L, nblocks, P<int32_t>(blk), s);
+    else blk_index_host(P<const int64_t>(ls), L, nblocks, P<int32_t>(blk));
+  });
 
   m.def("seq_chain", [](uint64_t slot_seq, uint64_t off, uint64_t reg, uint64_t hoff, uint64_t hline, int32_t lo,
                         int32_t hi, int n, uint64_t out, uint64_t s, bool dev) {

@@ -18,13 +18,13 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
-                   unsigned long long* count, uint64_t stream);
+                   unsigned long long* count, uint64_t stream, const unsigned long long* dn = nullptr);
 void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
                 const DfaPool& P, uint8_t* out, uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
               const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
               uint64_t stream);
-void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,
                const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream);
 
 void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
@@ -46,7 +46,7 @@ void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int6
                  const int32_t* line_len, const DfaPool& P, uint8_t* out);
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                   const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap);
-void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,
                 const ScoreTables& T, const ScoreParams& S, double* out, double* factors);
 
 }  // namespace lp
@@ -58,4 +58,55 @@ void nfa_mfma_dev(const uint64_t* groups, const int32_t* group_list, int ngroups
 int64_t nfa_host(const uint64_t* groups, const int32_t* group_list, int ngroups, const int32_t* lines, int64_t nsel,
                  const uint8_t* text, const int64_t* line_start, const int32_t* line_len, uint8_t* feat,
                  int64_t* hits, int64_t cap);
+}  // namespace lp
+
+// ---- post-match pipeline (lp_post.hip): hit CSR, events, frequency ranks, context features
+namespace lp {
+struct EvTables {
+  const int64_t* prim_off;   // [R+1] patterns whose primary regex is r: prim_pats[prim_off[r]..]
+  const int32_t* prim_pats;
+  const int32_t* freq_key;   // [P] frequency key, -1 = pattern without id
+  const int32_t* ctx_before; // [P] -1 = no context rules
+  const int32_t* ctx_after;
+  const int32_t* seg_lo; const int32_t* seg_hi; const int32_t* own_lo; const int32_t* own_hi;
+  int nseg;
+  int nkeys;
+  int pbits;                 // bits of a pattern index
+};
+
+struct HitsArgs {
+  const int64_t* cand;       // (regex << 32 | line): [0, pre_from) to DFA-verify, [pre_from, n) pre-verified
+  int64_t n, pre_from;
+  int lbits, rbits, R;
+  const uint8_t* text; const int64_t* ls; const int32_t* ll;
+  DfaPool dfa;
+  EvTables ev;
+  // outputs (capacity n; hit_off R+1)
+  int64_t* hits; int32_t* hit_line; int64_t* hit_off; int64_t* ev_cnt; int64_t* ev_end;
+  int64_t* counters;         // [0] unique verified hits, [1] events
+};
+
+struct EventsArgs {
+  const int64_t* hits; int64_t nh;
+  const int64_t* ev_cnt; const int64_t* ev_end;
+  int64_t ne, L;
+  int lbits;
+  EvTables ev;
+  const uint8_t* text; const int64_t* ls; const int32_t* ll;
+  DfaPool dfa;
+  // outputs
+  int32_t* ev_line; int32_t* ev_pat; int32_t* ev_seg; int64_t* ev_rank; int64_t* ev_fkey;
+  int64_t* freq_counts;      // [nkeys]
+  uint8_t* feat;             // [L] context features (nullptr: coverage only)
+  int32_t* cov;              // [L] optional: window coverage out
+};
+
+int bits_for(int64_t n);
+// device versions return the workspace bytes they need; they only run when ws_bytes suffices
+size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
+size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
+void blk_index_dev(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk, uint64_t stream);
+void hits_host(const HitsArgs& A);
+void events_host(const EventsArgs& A);
+void blk_index_host(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk);
 }  // namespace lp

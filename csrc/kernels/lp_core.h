@@ -46,6 +46,18 @@ LP_HD bool dfa_run(const DfaPool& P, int r, const uint8_t* s, int n) {
   return (A[st] & 1) != 0;
 }
 
+// Context features of one line (ContextAnalysisService.java:62-83); DFAs 0..3 of the pool are the
+// four internal regexes: bit0 ERROR, bit1 WARN (only when not ERROR: the reference's else-if),
+// bit2 stack-trace line, bit3 exception/error class name.
+LP_HD uint8_t context_feat(const DfaPool& P, const uint8_t* s, int len) {
+  uint8_t f = 0;
+  if (dfa_run(P, 0, s, len)) f |= 1;
+  else if (dfa_run(P, 1, s, len)) f |= 2;
+  if (dfa_run(P, 2, s, len)) f |= 4;
+  if (dfa_run(P, 3, s, len)) f |= 8;
+  return f;
+}
+
 // --------------------------------------------------------------------------------------------
 // literal prefilter tables
 struct PfTables {
@@ -181,6 +193,19 @@ struct ScoreTables {
   const int32_t* seg_lo; const int32_t* seg_hi; const int32_t* seg_own_lo;
   const int64_t* seg_g0; const int64_t* seg_n;
 };
+
+// Frequency input of the score: penalty count of event i = carry[key] (matches recorded before
+// this batch/shard, persistent + earlier ranks) + rank among earlier same-key events of the batch;
+// -1 = pattern without id (no penalty). FrequencyTrackingService.java:64-93, ScoringService.java:84-88.
+struct FreqIn {
+  const int64_t* rank;
+  const int64_t* fkey;
+  const int64_t* carry;
+};
+LP_HD int64_t freq_before(const FreqIn& F, int64_t i) {
+  const int64_t k = F.fkey[i];
+  return k >= 0 ? F.carry[k] + F.rank[i] : -1;
+}
 
 LP_HD double chrono_factor(int64_t gi, int64_t n, const ScoreParams& S) {
   const double pos = (double)gi / (double)n;

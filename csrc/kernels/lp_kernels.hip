@@ -21,6 +21,7 @@
 
 #include "lp_api.h"
 #include "lp_core.h"
+#include "lp_host.h"
 
 namespace lp {
 
@@ -33,23 +34,8 @@ namespace lp {
 static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---- host twins: the CPU backend (no-GPU serving, availability fallback, tests). Parallel over
-// independent items with plain threads; results are order-insensitive (callers sort/unique).
-static int g_host_threads = 8;
-void set_host_threads(int n) { g_host_threads = std::max(1, n); }
-
-template <class F>
-static void host_parallel(int64_t n, int64_t grain, F&& fn) {
-  const int T = (int)std::max<int64_t>(1, std::min<int64_t>(g_host_threads, n / std::max<int64_t>(grain, 1)));
-  if (T <= 1) {
-    fn(0, 0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  th.reserve(T);
-  for (int t = 0; t < T; ++t) th.emplace_back([&, t] { fn(t, n * t / T, n * (t + 1) / T); });
-  for (auto& x : th) x.join();
-}
-
+// independent items with plain threads (lp_host.h); results are order-insensitive (callers sort).
+void set_host_threads(int n) { host_threads() = std::max(1, n); }
 
 // ------------------------------------------------------------------------------------------
 // K1: newline index.  16 KiB tile per 256-thread block, 64 B per thread (4 x dwordx4 loads).
@@ -328,26 +314,38 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
 // K3a': literal verification of staged gram hits (one lane per hit): hash-table probe, full
 // literal compare at the literal's start (hit position - gram offset), candidate append.
 __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ ghits, int64_t n,
+                                                   const unsigned long long* __restrict__ dn,
                                                    const uint8_t* __restrict__ text, int64_t nbytes, PfTables T,
                                                    const int64_t* __restrict__ line_start, int64_t nlines,
                                                    const int32_t* __restrict__ blk_line, int64_t* cand, int64_t cap,
                                                    unsigned long long* count) {
-  // candidates staged in LDS, one global atomic per block (a per-candidate atomic on one counter
-  // serialises ~1M appends per step at the L2)
+  // candidates staged in LDS, one global atomic per flush (a per-candidate atomic on one counter
+  // serialises ~1M appends per step at the L2). With `dn` the hit count is read on the device
+  // (capped at the buffer size n) and the grid strides over it: no host round trip in between.
   __shared__ int64_t buf[PF_BUF];
   __shared__ int cnt;
   __shared__ unsigned long long gbase;
   if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
+  if (dn) {
+    const int64_t d = (int64_t)*dn;
+    n = d < n ? d : n;
+  }
   const LdsAppender app{buf, &cnt, cand, cap, count};
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const int64_t h = ghits[i];
-    const int64_t p = h >> 2;
-    const int G = 2 + (int)(h & 3);
-    uint32_t g4 = 0;
-    for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
-    pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, blk_line, app);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    if (i < n) {
+      const int64_t h = ghits[i];
+      const int64_t p = h >> 2;
+      const int G = 2 + (int)(h & 3);
+      uint32_t g4 = 0;
+      for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
+      pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, blk_line, app);
+    }
+    __syncthreads();
+    const int c = *reinterpret_cast<volatile int*>(&cnt);
+    if (c >= PF_BUF / 2) pf_flush(buf, &cnt, &gbase, c, cand, cap, count);
   }
   __syncthreads();
   const int c = *reinterpret_cast<volatile int*>(&cnt);
@@ -368,12 +366,7 @@ __global__ __launch_bounds__(256) void k_feat(const int32_t* __restrict__ lines,
   const int32_t line = lines[i];
   const uint8_t* s = text + line_start[line];
   const int len = line_len[line];
-  uint8_t f = 0;
-  if (dfa_run(P, 0, s, len)) f |= 1;
-  else if (dfa_run(P, 1, s, len)) f |= 2;
-  if (dfa_run(P, 2, s, len)) f |= 4;
-  if (dfa_run(P, 3, s, len)) f |= 8;
-  feat[line] = f;
+  feat[line] = context_feat(P, s, len);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -411,12 +404,12 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t* __restrict__ text,
 // ------------------------------------------------------------------------------------------
 // K7-K9: fused score epilogue, one lane per event
 __global__ __launch_bounds__(256) void k_score(const int32_t* __restrict__ ev_line, const int32_t* __restrict__ ev_pat,
-                                               const int32_t* __restrict__ ev_seg, const int64_t* __restrict__ ev_freq,
+                                               const int32_t* __restrict__ ev_seg, FreqIn F,
                                                int64_t n, ScoreTables T, ScoreParams S, double* __restrict__ out,
                                                double* __restrict__ factors) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
+  out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], freq_before(F, i), factors ? factors + 7 * i : nullptr);
 }
 
 
@@ -525,22 +518,19 @@ void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64
       const int32_t line = lines[i];
       const uint8_t* s = text + line_start[line];
       const int len = line_len[line];
-      uint8_t f = 0;
-      if (dfa_run(P, 0, s, len)) f |= 1;
-      else if (dfa_run(P, 1, s, len)) f |= 2;
-      if (dfa_run(P, 2, s, len)) f |= 4;
-      if (dfa_run(P, 3, s, len)) f |= 8;
-      feat[line] = f;
+      feat[line] = context_feat(P, s, len);
     }
   });
 }
 
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
-                   unsigned long long* count, uint64_t stream) {
+                   unsigned long long* count, uint64_t stream, const unsigned long long* dn) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_pf_verify, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ghits, n, text, nbytes,
-                     T, line_start, nlines, blk_line, cand, cap, count);
+  // with a device-side count the grid is sized for the buffer but capped (grid-stride loop)
+  const int g = dn ? (int)std::min<int64_t>(num_blocks(n, 256), 8192) : num_blocks(n, 256);
+  hipLaunchKernelGGL(k_pf_verify, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
+                     line_start, nlines, blk_line, cand, cap, count);
   LP_CHECK(hipGetLastError());
 }
 
@@ -561,11 +551,11 @@ void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* lin
   LP_CHECK(hipGetLastError());
 }
 
-void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,
                const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_score, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ev_line, ev_pat, ev_seg,
-                     ev_freq, n, T, S, out, factors);
+                     F, n, T, S, out, factors);
   LP_CHECK(hipGetLastError());
 }
 
@@ -616,7 +606,7 @@ int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos) 
 
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap) {
-  std::vector<std::vector<int64_t>> part(std::max(1, g_host_threads));
+  std::vector<std::vector<int64_t>> part(std::max(1, host_threads()));
   host_parallel(nbytes, 1 << 18, [&](int t, int64_t a, int64_t b) {
     auto& out = part[t];
     auto app = [&](int64_t v) { out.push_back(v); };
@@ -658,7 +648,7 @@ void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int6
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                   const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap) {
   if (nregs == 0) return 0;
-  std::vector<std::vector<int64_t>> part(std::max(1, g_host_threads));
+  std::vector<std::vector<int64_t>> part(std::max(1, host_threads()));
   host_parallel(nlines, 2048, [&](int t, int64_t a, int64_t b) {
     for (int64_t line = a; line < b; ++line)
       for (int j = 0; j < nregs; ++j)
@@ -674,11 +664,12 @@ int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t*
   return c;
 }
 
-void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const int64_t* ev_freq, int64_t n,
+void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,
                 const ScoreTables& T, const ScoreParams& S, double* out, double* factors) {
   host_parallel(n, 1024, [&](int, int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i)
-      out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], ev_freq[i], factors ? factors + 7 * i : nullptr);
+      out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], freq_before(F, i),
+                           factors ? factors + 7 * i : nullptr);
   });
 }
 

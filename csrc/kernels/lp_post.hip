@@ -1,0 +1,468 @@
+// Post-match pipeline: candidates -> hit CSR -> events in reference order -> in-batch frequency
+// ranks -> context coverage -> context features. Replaces ~150 small framework ops and ~15 host
+// round trips per batch with a handful of gfx950 kernels + rocPRIM device primitives on ONE
+// stream and ONE 16-byte host read in the middle (sizes for the event buffers).
+//
+//   hits_dev    pack (regex, line) + "pre-verified" bit into a (1 + rbits + lbits)-bit key, radix
+//               sort (only the bits in use), dedupe + DFA-verify the first key of every run
+//               (k_dedupe_verify), select -> sorted unique hits = per-regex line CSR shared by the
+//               primary / secondary / sequence roles; CSR offsets + per-hit event counts
+//               (primary role x owned line, k_csr_evcount); inclusive scan -> event offsets.
+//   events_dev  expand (line << pbits | pattern) keys (k_expand); radix sort = the reference's
+//               event order (line, then pattern: AnalysisService.java:89-113); per event segment,
+//               frequency key and context window (k_ev_post; window bounds go into a difference
+//               array); stable radix sort by frequency key -> rank among earlier same-key events and
+//               per-key counts (k_rank: the in-batch part of the penalty-before-record scan,
+//               ScoringService.java:84-88); inclusive scan of the difference array = window
+//               coverage; features only for covered lines (k_feat_cov, ContextAnalysisService.java:
+//               46-117 reads the 4 features of window lines only).
+//
+// The host twins below run the same element functions (the LP_HD helpers in this file) with
+// std::sort, so CPU tests exercise the GPU arithmetic and ordering rules.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <rocprim/rocprim.hpp>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lp_api.h"
+#include "lp_core.h"
+#include "lp_host.h"
+
+namespace lp {
+
+#define LP_PCHECK(x)                                                                                            \
+  do {                                                                                                          \
+    hipError_t e_ = (x);                                                                                        \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+  } while (0)
+
+static inline hipStream_t pstream(uint64_t s) { return reinterpret_cast<hipStream_t>(s); }
+static inline unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+int bits_for(int64_t n) {  // bits needed to hold values 0..n-1 (>= 1)
+  int b = 1;
+  while (b < 62 && (int64_t(1) << b) < n) ++b;
+  return b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// element functions (host + device)
+
+// segment of local line x: the last segment whose first line is <= x (documents are never empty:
+// Java split gives an empty document one line)
+LP_HD int seg_of(const int32_t* lo, int nseg, int32_t x) {
+  int a = 0, b = nseg;
+  while (b - a > 1) {
+    const int m = (a + b) >> 1;
+    if (lo[m] <= x) a = m; else b = m;
+  }
+  return a;
+}
+
+LP_HD int64_t lower_bound64(const int64_t* a, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (a[m] < v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+LP_HD int64_t lower_bound_u32(const uint32_t* a, int64_t n, uint32_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (a[m] < v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// events a hit produces: one per pattern whose primary regex it is, on lines the segment owns
+LP_HD int64_t hit_event_count(const EvTables& E, int64_t key) {
+  const int r = (int)(key >> 32);
+  const int32_t x = (int32_t)(key & 0xFFFFFFFFll);
+  const int64_t c = E.prim_off[r + 1] - E.prim_off[r];
+  if (c == 0) return 0;
+  const int s = seg_of(E.seg_lo, E.nseg, x);
+  return (x >= E.own_lo[s] && x < E.own_hi[s]) ? c : 0;
+}
+
+// context window [a, b) of an event (AnalysisService.java:132-156 clipping; [x, x+1) when the
+// pattern has no context rules)
+LP_HD void event_window(const EvTables& E, int32_t x, int p, int s, int32_t& a, int32_t& b) {
+  const int32_t before = E.ctx_before[p], after = E.ctx_after[p];
+  if (before < 0) {
+    a = x;
+    b = x + 1;
+    return;
+  }
+  const int64_t aa = (int64_t)x - before, bb = (int64_t)x + 1 + after;
+  a = (int32_t)(aa < E.seg_lo[s] ? E.seg_lo[s] : aa);
+  b = (int32_t)(bb > E.seg_hi[s] ? E.seg_hi[s] : bb);
+}
+
+// ---------------------------------------------------------------------------------------------
+// kernels
+
+__global__ __launch_bounds__(256) void k_pack(const int64_t* __restrict__ cand, int64_t n, int64_t pre_from, int lbits,
+                                              uint64_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = (uint64_t)cand[i];
+  keys[i] = ((((k >> 32) << lbits) | (k & 0xFFFFFFFFull)) << 1) | (i >= pre_from ? 1ull : 0ull);
+}
+
+LP_HD bool dedupe_verify_one(const uint64_t* keys, int64_t n, int64_t i, int lbits, const uint8_t* text,
+                             const int64_t* ls, const int32_t* ll, const DfaPool& P, int64_t* std_key) {
+  const uint64_t k = keys[i] >> 1;
+  if (i > 0 && (keys[i - 1] >> 1) == k) return false;
+  bool pre = false;  // pre-verified copies sort last inside a run
+  for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j) pre |= (keys[j] & 1) != 0;
+  const int r = (int)(k >> lbits);
+  const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
+  *std_key = ((int64_t)r << 32) | x;
+  return pre || dfa_run(P, r, text + ls[x], ll[x]);
+}
+
+__global__ __launch_bounds__(256) void k_dedupe_verify(const uint64_t* __restrict__ keys, int64_t n, int lbits,
+                                                       const uint8_t* __restrict__ text,
+                                                       const int64_t* __restrict__ ls, const int32_t* __restrict__ ll,
+                                                       DfaPool P, int64_t* __restrict__ std_key,
+                                                       uint8_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t sk = 0;
+  flag[i] = dedupe_verify_one(keys, n, i, lbits, text, ls, ll, P, &sk) ? 1 : 0;
+  std_key[i] = sk;
+}
+
+__global__ __launch_bounds__(256) void k_csr_evcount(const int64_t* __restrict__ hits,
+                                                     const int64_t* __restrict__ counters, int64_t n, int R, EvTables E,
+                                                     int64_t* __restrict__ hit_off, int32_t* __restrict__ hit_line,
+                                                     int64_t* __restrict__ ev_cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nh = counters[0];
+  if (i <= R) hit_off[i] = lower_bound64(hits, nh, (int64_t)i << 32);
+  if (i < n) {
+    if (i < nh) {
+      const int64_t k = hits[i];
+      hit_line[i] = (int32_t)(k & 0xFFFFFFFFll);
+      ev_cnt[i] = hit_event_count(E, k);
+    } else {
+      ev_cnt[i] = 0;
+    }
+  }
+}
+
+__global__ void k_total(const int64_t* __restrict__ ev_end, int64_t n, int64_t* __restrict__ counters) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) counters[1] = n > 0 ? ev_end[n - 1] : 0;
+}
+
+__global__ __launch_bounds__(256) void k_expand(const int64_t* __restrict__ hits, int64_t nh,
+                                                const int64_t* __restrict__ ev_cnt, const int64_t* __restrict__ ev_end,
+                                                EvTables E, uint64_t* __restrict__ evk) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nh) return;
+  const int64_t c = ev_cnt[i];
+  if (c == 0) return;
+  const int64_t k = hits[i];
+  const int r = (int)(k >> 32);
+  const uint64_t x = (uint64_t)(k & 0xFFFFFFFFll);
+  const int64_t base = ev_end[i] - c, p0 = E.prim_off[r];
+  for (int64_t j = 0; j < c; ++j) evk[base + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
+}
+
+LP_HD void ev_post_one(const EvTables& E, uint64_t key, int64_t e, int32_t* ev_line, int32_t* ev_pat, int32_t* ev_seg,
+                       uint32_t* fsort, int32_t& a, int32_t& b) {
+  const int32_t x = (int32_t)(key >> E.pbits);
+  const int p = (int)(key & ((1ull << E.pbits) - 1));
+  const int s = seg_of(E.seg_lo, E.nseg, x);
+  ev_line[e] = x;
+  ev_pat[e] = p;
+  ev_seg[e] = s;
+  const int32_t fk = E.freq_key[p];
+  fsort[e] = fk >= 0 ? (uint32_t)fk : (uint32_t)E.nkeys;
+  event_window(E, x, p, s, a, b);
+}
+
+__global__ __launch_bounds__(256) void k_ev_post(const uint64_t* __restrict__ evk, int64_t ne, EvTables E,
+                                                 int32_t* __restrict__ ev_line, int32_t* __restrict__ ev_pat,
+                                                 int32_t* __restrict__ ev_seg, uint32_t* __restrict__ fsort,
+                                                 int32_t* __restrict__ idx, int32_t* __restrict__ diff) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  int32_t a, b;
+  ev_post_one(E, evk[e], e, ev_line, ev_pat, ev_seg, fsort, a, b);
+  idx[e] = (int32_t)e;
+  if (a < b) {
+    atomicAdd(diff + a, 1);
+    atomicAdd(diff + b, -1);
+  }
+}
+
+LP_HD void rank_one(const uint32_t* fs, const int32_t* idx, int64_t ne, int64_t j, int nkeys, int64_t* ev_rank,
+                    int64_t* ev_fkey, int64_t* freq_counts) {
+  const uint32_t fk = fs[j];
+  const int32_t e = idx[j];
+  if ((int)fk >= nkeys) {
+    ev_rank[e] = -1;
+    ev_fkey[e] = -1;
+    return;
+  }
+  const int64_t start = lower_bound_u32(fs, j, fk);
+  ev_rank[e] = j - start;
+  ev_fkey[e] = fk;
+  if (j + 1 == ne || fs[j + 1] != fk) freq_counts[fk] = j - start + 1;
+}
+
+__global__ __launch_bounds__(256) void k_rank(const uint32_t* __restrict__ fs, const int32_t* __restrict__ idx,
+                                              int64_t ne, int nkeys, int64_t* __restrict__ ev_rank,
+                                              int64_t* __restrict__ ev_fkey, int64_t* __restrict__ freq_counts) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < ne) rank_one(fs, idx, ne, j, nkeys, ev_rank, ev_fkey, freq_counts);
+}
+
+// Context features of covered lines. A block owns FC_LINES consecutive lines: it compacts the
+// covered ones into an LDS list (uncovered lines get 0) and then runs the 4 DFAs with every lane
+// busy -- covered lines come in short runs, so one lane per line would idle most of each wave.
+constexpr int FC_LINES = 4096;
+__global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ cov, int64_t L,
+                                                  const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
+                                                  const int32_t* __restrict__ ll, DfaPool P,
+                                                  uint8_t* __restrict__ feat) {
+  __shared__ int32_t list[FC_LINES];
+  __shared__ int n;
+  if (threadIdx.x == 0) n = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * FC_LINES;
+  for (int k = threadIdx.x; k < FC_LINES; k += blockDim.x) {
+    const int64_t x = base + k;
+    if (x < L) {
+      if (cov[x] > 0) list[atomicAdd(&n, 1)] = k;
+      else feat[x] = 0;
+    }
+  }
+  __syncthreads();
+  const int m = n;
+  for (int j = threadIdx.x; j < m; j += blockDim.x) {
+    const int64_t x = base + list[j];
+    feat[x] = context_feat(P, text + ls[x], ll[x]);
+  }
+}
+
+// coarse byte-block -> line index (blk[b] = line containing byte b << 12), one lane per block
+__global__ __launch_bounds__(256) void k_blk_index(const int64_t* __restrict__ ls, int64_t L, int64_t nblk,
+                                                   int32_t* __restrict__ blk) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const int64_t i = upper_idx(ls, L, b << LINE_BLK_SHIFT);
+  blk[b] = (int32_t)(i < 0 ? 0 : i);
+}
+
+// ---------------------------------------------------------------------------------------------
+// workspace carving: the same code path sizes (base == nullptr) and carves
+
+struct Carve {
+  uint8_t* base;
+  size_t used = 0;
+  template <class T>
+  T* take(size_t n) {
+    const size_t off = (used + 255) & ~size_t(255);
+    used = off + std::max<size_t>(n, 1) * sizeof(T);
+    return base ? reinterpret_cast<T*>(base + off) : nullptr;
+  }
+  void* take_bytes(size_t n) { return take<uint8_t>(n); }
+};
+
+size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
+  const int64_t n = A.n;
+  const int kbits = 1 + A.lbits + A.rbits;
+  Carve C{static_cast<uint8_t*>(ws)};
+  hipStream_t st = pstream(stream);
+  uint64_t* kin = C.take<uint64_t>(n);
+  uint64_t* kout = C.take<uint64_t>(n);
+  int64_t* stdk = C.take<int64_t>(n);
+  uint8_t* flag = C.take<uint8_t>(n);
+  size_t t_sort = 0, t_sel = 0, t_scan = 0;
+  if (n > 0) {
+    LP_PCHECK(rocprim::radix_sort_keys(nullptr, t_sort, kin, kout, (size_t)n, 0, kbits, st));
+    LP_PCHECK(rocprim::select(nullptr, t_sel, stdk, flag, A.hits, A.counters, (size_t)n, st));
+    LP_PCHECK(rocprim::inclusive_scan(nullptr, t_scan, A.ev_cnt, A.ev_end, (size_t)n, rocprim::plus<int64_t>(), st));
+  }
+  void* tmp = C.take_bytes(std::max(t_sort, std::max(t_sel, t_scan)));
+  if (!ws || C.used > ws_bytes) return C.used;
+  if (n == 0) {
+    LP_PCHECK(hipMemsetAsync(A.counters, 0, 2 * sizeof(int64_t), st));
+    LP_PCHECK(hipMemsetAsync(A.hit_off, 0, (size_t)(A.R + 1) * sizeof(int64_t), st));
+    return C.used;
+  }
+  hipLaunchKernelGGL(k_pack, dim3(nblk(n)), dim3(256), 0, st, A.cand, n, A.pre_from, A.lbits, kin);
+  LP_PCHECK(hipGetLastError());
+  size_t tb = t_sort;
+  LP_PCHECK(rocprim::radix_sort_keys(tmp, tb, kin, kout, (size_t)n, 0, kbits, st));
+  hipLaunchKernelGGL(k_dedupe_verify, dim3(nblk(n)), dim3(256), 0, st, kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa,
+                     stdk, flag);
+  LP_PCHECK(hipGetLastError());
+  tb = t_sel;
+  LP_PCHECK(rocprim::select(tmp, tb, stdk, flag, A.hits, A.counters, (size_t)n, st));
+  hipLaunchKernelGGL(k_csr_evcount, dim3(nblk(std::max<int64_t>(n, A.R + 1))), dim3(256), 0, st, A.hits, A.counters,
+                     n, A.R, A.ev, A.hit_off, A.hit_line, A.ev_cnt);
+  LP_PCHECK(hipGetLastError());
+  tb = t_scan;
+  LP_PCHECK(rocprim::inclusive_scan(tmp, tb, A.ev_cnt, A.ev_end, (size_t)n, rocprim::plus<int64_t>(), st));
+  hipLaunchKernelGGL(k_total, dim3(1), dim3(64), 0, st, A.ev_end, n, A.counters);
+  LP_PCHECK(hipGetLastError());
+  return C.used;
+}
+
+size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
+  const int64_t ne = A.ne, L = A.L;
+  const EvTables& E = A.ev;
+  const int ebits = E.pbits + A.lbits;
+  const int fbits = bits_for((int64_t)E.nkeys + 1);
+  Carve C{static_cast<uint8_t*>(ws)};
+  hipStream_t st = pstream(stream);
+  uint64_t* kin = C.take<uint64_t>(ne);
+  uint64_t* kout = C.take<uint64_t>(ne);
+  uint32_t* fin = C.take<uint32_t>(ne);
+  uint32_t* fout = C.take<uint32_t>(ne);
+  int32_t* iin = C.take<int32_t>(ne);
+  int32_t* iout = C.take<int32_t>(ne);
+  int32_t* diff = C.take<int32_t>(L + 1);
+  int32_t* cov = A.cov ? A.cov : C.take<int32_t>(L);
+  size_t t_sort = 0, t_pairs = 0, t_scan = 0;
+  if (ne > 0) {
+    LP_PCHECK(rocprim::radix_sort_keys(nullptr, t_sort, kin, kout, (size_t)ne, 0, ebits, st));
+    LP_PCHECK(rocprim::radix_sort_pairs(nullptr, t_pairs, fin, fout, iin, iout, (size_t)ne, 0, fbits, st));
+  }
+  if (L > 0) LP_PCHECK(rocprim::inclusive_scan(nullptr, t_scan, diff, cov, (size_t)L, rocprim::plus<int32_t>(), st));
+  void* tmp = C.take_bytes(std::max(t_sort, std::max(t_pairs, t_scan)));
+  if (!ws || C.used > ws_bytes) return C.used;
+  if (E.nkeys > 0) LP_PCHECK(hipMemsetAsync(A.freq_counts, 0, (size_t)E.nkeys * sizeof(int64_t), st));
+  if (L > 0) LP_PCHECK(hipMemsetAsync(diff, 0, (size_t)(L + 1) * sizeof(int32_t), st));
+  if (ne > 0) {
+    hipLaunchKernelGGL(k_expand, dim3(nblk(A.nh)), dim3(256), 0, st, A.hits, A.nh, A.ev_cnt, A.ev_end, E, kin);
+    LP_PCHECK(hipGetLastError());
+    size_t tb = t_sort;
+    LP_PCHECK(rocprim::radix_sort_keys(tmp, tb, kin, kout, (size_t)ne, 0, ebits, st));
+    hipLaunchKernelGGL(k_ev_post, dim3(nblk(ne)), dim3(256), 0, st, kout, ne, E, A.ev_line, A.ev_pat, A.ev_seg, fin,
+                       iin, diff);
+    LP_PCHECK(hipGetLastError());
+    tb = t_pairs;
+    LP_PCHECK(rocprim::radix_sort_pairs(tmp, tb, fin, fout, iin, iout, (size_t)ne, 0, fbits, st));
+    hipLaunchKernelGGL(k_rank, dim3(nblk(ne)), dim3(256), 0, st, fout, iout, ne, E.nkeys, A.ev_rank, A.ev_fkey,
+                       A.freq_counts);
+    LP_PCHECK(hipGetLastError());
+  }
+  if (L > 0) {
+    size_t tb = t_scan;
+    LP_PCHECK(rocprim::inclusive_scan(tmp, tb, diff, cov, (size_t)L, rocprim::plus<int32_t>(), st));
+    if (A.feat) {
+      hipLaunchKernelGGL(k_feat_cov, dim3(nblk(L, FC_LINES)), dim3(256), 0, st, cov, L, A.text, A.ls, A.ll, A.dfa, A.feat);
+      LP_PCHECK(hipGetLastError());
+    }
+  }
+  return C.used;
+}
+
+void blk_index_dev(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk, uint64_t stream) {
+  if (nblocks <= 0) return;
+  hipLaunchKernelGGL(k_blk_index, dim3(nblk(nblocks)), dim3(256), 0, pstream(stream), ls, L, nblocks, blk);
+  LP_PCHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// host twins
+
+void hits_host(const HitsArgs& A) {
+  const int64_t n = A.n;
+  std::vector<uint64_t> keys(n);
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t k = (uint64_t)A.cand[i];
+    keys[i] = ((((k >> 32) << A.lbits) | (k & 0xFFFFFFFFull)) << 1) | (i >= A.pre_from ? 1ull : 0ull);
+  }
+  std::sort(keys.begin(), keys.end());
+  std::vector<int64_t> stdk(n);
+  std::vector<uint8_t> flag(n);
+  host_parallel(n, 4096, [&](int, int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i)
+      flag[i] = dedupe_verify_one(keys.data(), n, i, A.lbits, A.text, A.ls, A.ll, A.dfa, &stdk[i]) ? 1 : 0;
+  });
+  int64_t nh = 0;
+  for (int64_t i = 0; i < n; ++i)
+    if (flag[i]) A.hits[nh++] = stdk[i];
+  A.counters[0] = nh;
+  for (int r = 0; r <= A.R; ++r) A.hit_off[r] = lower_bound64(A.hits, nh, (int64_t)r << 32);
+  int64_t run = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i < nh) {
+      A.hit_line[i] = (int32_t)(A.hits[i] & 0xFFFFFFFFll);
+      A.ev_cnt[i] = hit_event_count(A.ev, A.hits[i]);
+    } else {
+      A.ev_cnt[i] = 0;
+    }
+    run += A.ev_cnt[i];
+    A.ev_end[i] = run;
+  }
+  A.counters[1] = run;
+}
+
+void events_host(const EventsArgs& A) {
+  const int64_t ne = A.ne, L = A.L;
+  const EvTables& E = A.ev;
+  std::vector<uint64_t> evk(ne);
+  for (int64_t i = 0; i < A.nh; ++i) {
+    const int64_t c = A.ev_cnt[i];
+    if (!c) continue;
+    const int64_t k = A.hits[i];
+    const int r = (int)(k >> 32);
+    const uint64_t x = (uint64_t)(k & 0xFFFFFFFFll);
+    const int64_t base = A.ev_end[i] - c, p0 = E.prim_off[r];
+    for (int64_t j = 0; j < c; ++j) evk[base + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
+  }
+  std::sort(evk.begin(), evk.end());
+  std::vector<uint32_t> fs(ne);
+  std::vector<int32_t> idx(ne);
+  std::vector<int32_t> diff(L + 1, 0);
+  for (int64_t e = 0; e < ne; ++e) {
+    int32_t a, b;
+    ev_post_one(E, evk[e], e, A.ev_line, A.ev_pat, A.ev_seg, fs.data(), a, b);
+    if (a < b) {
+      ++diff[a];
+      --diff[b];
+    }
+  }
+  std::iota(idx.begin(), idx.end(), 0);
+  std::stable_sort(idx.begin(), idx.end(), [&](int32_t u, int32_t v) { return fs[u] < fs[v]; });
+  std::vector<uint32_t> fsorted(ne);
+  for (int64_t j = 0; j < ne; ++j) fsorted[j] = fs[idx[j]];
+  for (int k = 0; k < E.nkeys; ++k) A.freq_counts[k] = 0;
+  for (int64_t j = 0; j < ne; ++j) rank_one(fsorted.data(), idx.data(), ne, j, E.nkeys, A.ev_rank, A.ev_fkey,
+                                            A.freq_counts);
+  std::vector<int32_t> covv;
+  int32_t* cov = A.cov;
+  if (!cov) {
+    covv.resize(std::max<int64_t>(L, 1));
+    cov = covv.data();
+  }
+  int32_t c = 0;
+  for (int64_t x = 0; x < L; ++x) cov[x] = (c += diff[x]);
+  if (A.feat)
+    host_parallel(L, 4096, [&](int, int64_t a, int64_t b) {
+      for (int64_t x = a; x < b; ++x) A.feat[x] = cov[x] > 0 ? context_feat(A.dfa, A.text + A.ls[x], A.ll[x]) : 0;
+    });
+}
+
+void blk_index_host(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk) {
+  for (int64_t b = 0; b < nblocks; ++b) {
+    const int64_t i = upper_idx(ls, L, b << LINE_BLK_SHIFT);
+    blk[b] = (int32_t)(i < 0 ? 0 : i);
+  }
+}
+
+}  // namespace lp

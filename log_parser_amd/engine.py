@@ -65,16 +65,22 @@ class Segments:
 
     @staticmethod
     def single(L: int, device) -> "Segments":
-        i32 = lambda v: torch.tensor([v], dtype=torch.int32, device=device)  # noqa: E731
-        i64 = lambda v: torch.tensor([v], dtype=torch.int64, device=device)  # noqa: E731
-        return Segments(i32(0), i32(L), i32(0), i32(L), i64(0), i64(L))
+        t32 = torch.tensor([0, L, 0, L], dtype=torch.int32, device=device)
+        t64 = torch.tensor([0, L], dtype=torch.int64, device=device)
+        return Segments(t32[0:1], t32[1:2], t32[2:3], t32[3:4], t64[0:1], t64[1:2])
+
+    @staticmethod
+    def doc_arrays(doc_line_off: np.ndarray):
+        """Host arrays (lo, hi, g0, n) of a batch of whole documents (every line owned)."""
+        lo = doc_line_off[:-1].astype(np.int32)
+        hi = doc_line_off[1:].astype(np.int32)
+        n = (doc_line_off[1:] - doc_line_off[:-1]).astype(np.int64)
+        return lo, hi, np.zeros_like(n), n
 
     @staticmethod
     def from_doc_offsets(doc_line_off: np.ndarray, device) -> "Segments":
-        lo = torch.from_numpy(doc_line_off[:-1].astype(np.int32)).to(device)
-        hi = torch.from_numpy(doc_line_off[1:].astype(np.int32)).to(device)
-        n = torch.from_numpy((doc_line_off[1:] - doc_line_off[:-1]).astype(np.int64)).to(device)
-        return Segments(lo, hi, lo.clone(), hi.clone(), torch.zeros_like(n), n)
+        lo, hi, g0, n = (torch.from_numpy(a).to(device) for a in Segments.doc_arrays(doc_line_off))
+        return Segments(lo, hi, lo, hi, g0, n)
 
     def seg_and_owned(self, lines: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """Segment id and ownership of the given line ids (only hit lines, never all L lines)."""
@@ -142,6 +148,8 @@ class Engine:
         self.fault_every = int(self.config["engine.fault-inject-every"])   # tests: injected device faults
         self._batches = 0
         self.tabs = library.device_tables(self.device)
+        self.ws = K.Workspace(self.device)          # post-match pipeline scratch (grow-only)
+        self.upload = K.Uploader(self.device)       # batch line index / segments / carry: one H2D
         p = self.params
         self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
                          p.max_context_factor, p.freq_threshold, p.freq_max_penalty, float(p.freq_window_hours))
@@ -184,29 +192,36 @@ class Engine:
             TR.mark(timings, name, self.device)
         return t0
 
-    def match_hits(self, text, nbytes, ls, ll, host_lines=None, timings=None) -> torch.Tensor:
+    def match_candidates(self, text, nbytes, ls, ll, host_lines=None, timings=None) -> Tuple[torch.Tensor, int]:
+        """(regex << 32 | line) candidates: ``[:pre_from]`` prefilter candidates still to DFA-verify
+        (verified inside the post-match pipeline), ``[pre_from:]`` hits of engines that verify
+        themselves (literal-free DFA scan, MFMA NFA, host fallback). Duplicates allowed."""
         timings = {} if timings is None else timings
         t = self._start(timings)
-        parts = []
         cand = K.prefilter(text, nbytes, self.tabs["pf"], ls, self.cand_cap, self.pf_grid)
         t = self._tick(timings, "prefilter", t)
-        if cand.numel():
-            cand = torch.unique(cand)
-            ok = K.verify(cand, text, ls, ll, self.tabs["dfa"])
-            parts.append(cand[ok.bool()])
-        t = self._tick(timings, "verify", t)
-        parts.append(K.scan(text, ls, ll, self.tabs["scan_regs"], self.tabs["dfa"], max(1024, ls.numel())))
+        extra = []
+        if self.tabs["scan_regs"].numel():
+            extra.append(K.scan(text, ls, ll, self.tabs["scan_regs"], self.tabs["dfa"], max(1024, ls.numel())))
         for ncls, glist in self.tabs["nfa_scan_lists"].items():       # DFA blow-up regexes: MFMA NFA
             if glist.numel():
-                parts.append(K.nfa_scan(self.tabs["nfa_tables"], glist, ncls, text, ls, ll, max(1024, ls.numel())))
-        t = self._tick(timings, "scan", t)
+                extra.append(K.nfa_scan(self.tabs["nfa_tables"], glist, ncls, text, ls, ll, max(1024, ls.numel())))
         if self.lib.host_regs:
-            parts.append(self._host_fallback(text, nbytes, ls, ll, host_lines))
-            t = self._tick(timings, "host_fallback", t)
-        hits = torch.cat(parts) if parts else torch.empty(0, dtype=torch.int64, device=text.device)
-        hits = torch.unique(hits)
-        self._tick(timings, "hits_sort", t)
-        return hits
+            extra.append(self._host_fallback(text, nbytes, ls, ll, host_lines))
+        if extra:
+            t = self._tick(timings, "scan", t)
+            return torch.cat([cand] + extra), cand.numel()
+        return cand, cand.numel()
+
+    def _ev_tables(self, segs: "Segments") -> tuple:
+        return K.ev_tables(self.tabs, segs, len(self.lib.freq_ids), len(self.lib.patterns))
+
+    def match_hits(self, text, nbytes, ls, ll, host_lines=None, timings=None) -> torch.Tensor:
+        """Sorted unique verified (regex << 32 | line) hit keys of every library regex."""
+        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_lines, timings)
+        segs = Segments.single(ls.numel(), text.device)
+        return K.post_hits(cand, pre, ls.numel(), self.lib.n_regexes, text, ls, ll, self.tabs["dfa"],
+                           self._ev_tables(segs), self.ws)[0]
 
     def _host_fallback(self, text, nbytes, ls, ll, host_lines) -> torch.Tensor:
         if host_lines is None:
@@ -229,104 +244,31 @@ class Engine:
     # ------------------------------------------------------------------ core run
     def prepare(self, text, nbytes, ls, ll, segs: Segments, host_lines=None,
                 timings: Optional[dict] = None) -> "Prepared":
-        """Local phase: matching, hit CSR, context features, events, in-batch frequency ranks.
+        """Local phase: matching, hit CSR, events, in-batch frequency ranks, context features.
 
         Needs no global information, so the data-parallel path runs it before its collectives.
+        After matching it is the native post-match pipeline (csrc/kernels/lp_post.hip): one host
+        read of (hit, event) counts in the middle, everything else stream-ordered on the device.
         """
         timings = {} if timings is None else timings
-        dev = text.device
         L = ls.numel()
-        hits = self.match_hits(text, nbytes, ls, ll, host_lines, timings)
+        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_lines, timings)
         t = 0.0
-        tabs = self.tabs
-        R = self.lib.n_regexes
-        P = len(self.lib.patterns)
-        hit_reg = (hits >> 32).to(torch.int32)
-        hit_line = (hits & 0xFFFFFFFF).to(torch.int32)
-        hit_off = torch.searchsorted(hit_reg, torch.arange(R + 1, dtype=torch.int32, device=dev)).to(torch.int64)
-        # primary events on owned lines, reference order (line, then pattern index)
-        if hits.numel():
-            prim = tabs["is_primary"][hit_reg.long()]
-            _, owned = segs.seg_and_owned(hit_line)
-            prim &= owned
-        else:
-            prim = torch.zeros(0, dtype=torch.bool, device=dev)
-        ph_reg = hit_reg[prim].long()
-        ph_line = hit_line[prim]
-        cnt = tabs["prim_cnt"][ph_reg]
-        total = int(cnt.sum().item()) if cnt.numel() else 0
-        if total:
-            rep = torch.repeat_interleave(torch.arange(ph_reg.numel(), device=dev), cnt, output_size=total)
-            start = torch.cumsum(cnt, 0) - cnt
-            within = torch.arange(total, device=dev) - start[rep]
-            ev_pat = tabs["prim_pats"][tabs["prim_off"][ph_reg][rep] + within].to(torch.int32)
-            ev_line = ph_line[rep]
-            order = torch.argsort(ev_line.long() * P + ev_pat.long())
-            ev_line = ev_line[order].contiguous()
-            ev_pat = ev_pat[order].contiguous()
-            ev_seg = segs.seg_and_owned(ev_line)[0].to(torch.int32).contiguous()
-        else:
-            ev_line = torch.empty(0, dtype=torch.int32, device=dev)
-            ev_pat = torch.empty(0, dtype=torch.int32, device=dev)
-            ev_seg = torch.empty(0, dtype=torch.int32, device=dev)
-        t = self._tick(timings, "events", t)
-        # context features (ContextAnalysisService) only for lines inside some event's window
-        feat = self._context_features(text, ls, ll, ev_line, ev_pat, ev_seg, segs, L)
-        t = self._tick(timings, "context", t)
-        # frequency: rank of each event among earlier events with the same key (in-batch part of
-        # the segmented exclusive scan); the carry is added in finish()
+        evt = self._ev_tables(segs)
+        hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(
+            cand, pre, L, self.lib.n_regexes, text, ls, ll, self.tabs["dfa"], evt, self.ws)
+        t = self._tick(timings, "verify_csr", t)
         nkeys = len(self.lib.freq_ids)
-        ev_rank = torch.full((total,), -1, dtype=torch.int64, device=dev)
-        ev_fkey = torch.full((total,), -1, dtype=torch.int64, device=dev)
-        freq_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
-        if total and nkeys:
-            fk = tabs["freq_key"][ev_pat.long()].long()
-            vi = torch.nonzero(fk >= 0).flatten()
-            if vi.numel():
-                fkv = fk[vi]
-                sk, perm = torch.sort(fkv, stable=True)
-                first = torch.searchsorted(sk, sk)
-                rank_sorted = torch.arange(sk.numel(), device=dev) - first
-                rank = torch.empty_like(rank_sorted)
-                rank[perm] = rank_sorted
-                ev_rank[vi] = rank
-                ev_fkey[vi] = fkv
-                freq_counts = torch.bincount(fkv, minlength=max(nkeys, 1))
-        self._tick(timings, "frequency", t)
-        hit_line_c = hit_line.contiguous() if hit_line.numel() else torch.zeros(1, dtype=torch.int32, device=dev)
-        return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
-                        hit_line_c, feat, L, timings)
-
-    def _context_features(self, text, ls, ll, ev_line, ev_pat, ev_seg, segs: Segments, L: int) -> torch.Tensor:
-        dev = text.device
-        if ev_line.numel() == 0:
-            return torch.zeros(max(L, 1), dtype=torch.uint8, device=dev)
-        x = ev_line.long()
-        p = ev_pat.long()
-        s = ev_seg.long()
-        before = self.tabs["ctx_before"][p].long()
-        after = self.tabs["ctx_after"][p].long()
-        null = before < 0
-        a = torch.where(null, x, torch.maximum(segs.lo[s].long(), x - before))
-        b = torch.where(null, x + 1, torch.minimum(segs.hi[s].long(), x + after + 1))
-        # union of the event windows, O(events): sort by start, clip each start to the running max
-        # of previous ends, expand the remaining runs (no L-sized arrays)
-        order = torch.argsort(a)
-        a, b = a[order], b[order]
-        prev_end = torch.cummax(b, 0).values
-        start = torch.maximum(a, torch.cat([a[:1], prev_end[:-1]]))
-        run = (b - start).clamp(min=0)
-        total = int(run.sum().item())
-        if total == 0:
-            lines = torch.zeros(0, dtype=torch.int32, device=dev)
-        else:
-            rep = torch.repeat_interleave(torch.arange(run.numel(), device=dev), run, output_size=total)
-            offs = torch.cumsum(run, 0) - run
-            lines = (start[rep] + torch.arange(total, device=dev) - offs[rep]).to(torch.int32)
-        if self.context_engine == "mfma":
-            return K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],
+        dfa_feats = self.context_engine != "mfma"
+        ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts, feat, cov = K.post_events(
+            hits, nh, ev_cnt, ev_end, ne, L, evt, text, ls, ll, self.tabs["dfa"], nkeys, self.ws, features=dfa_feats)
+        if not dfa_feats:           # A/B engine: context features on the MFMA NFA kernel
+            lines = torch.nonzero(cov[:L] > 0).flatten().to(torch.int32)
+            feat = K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],
                                   self.lib.nfa_group_ncls[0])
-        return K.context_features(lines, L, text, ls, ll, self.tabs["dfa"])
+        self._tick(timings, "events_context_freq", t)
+        return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
+                        hit_line, feat, L, timings)
 
     def seq_chain_table(self, prep: "Prepared", own_lo: int, own_hi: int) -> torch.Tensor:
         """Per sequence-event slot: event index still unmatched after this shard (-1 = done)."""
@@ -351,10 +293,6 @@ class Engine:
         t = self._start(timings)
         tabs = self.tabs
         dev = prep.hit_off.device
-        ev_freq = prep.ev_rank
-        if ev_freq.numel():
-            ev_freq = torch.where(prep.ev_fkey >= 0, freq_carry[prep.ev_fkey.clamp(min=0)] + prep.ev_rank,
-                                  torch.full_like(prep.ev_rank, -1))
         if seq_carry is None:
             seq_carry = torch.zeros(max(self.lib.n_seq_events, 1), dtype=torch.uint8, device=dev)
         st = (tabs["conf"].data_ptr(), tabs["sev"].data_ptr(), tabs["ctx_before"].data_ptr(),
@@ -363,8 +301,8 @@ class Engine:
               tabs["seq_bonus"].data_ptr(), tabs["seq_ev_off"].data_ptr(), tabs["seq_ev_reg"].data_ptr(),
               seq_carry.data_ptr(), prep.hit_off.data_ptr(), prep.hit_line.data_ptr(), prep.feat.data_ptr(),
               segs.lo.data_ptr(), segs.hi.data_ptr(), segs.own_lo.data_ptr(), segs.g0.data_ptr(), segs.n.data_ptr())
-        score, factors = K.score(prep.ev_line, prep.ev_pat, prep.ev_seg, ev_freq.contiguous(), st, self.sp_tuple,
-                                 with_factors)
+        score, factors = K.score_fused(prep.ev_line, prep.ev_pat, prep.ev_seg, prep.ev_rank, prep.ev_fkey,
+                                       freq_carry, st, self.sp_tuple, with_factors)
         self._tick(timings, "score", t)
         return RunResult(prep.ev_line, prep.ev_pat, prep.ev_seg, score, factors,
                          prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings)
@@ -457,13 +395,15 @@ class Engine:
         if tm is not None:
             self._start(tm)
         text = self._stage_h2d(n)
-        ls = torch.from_numpy(ls_h).to(self.device)
-        ll = torch.from_numpy(ll_h).to(self.device)
-        segs = Segments.from_doc_offsets(dl, self.device)
+        carry = self.freq.carry(self.lib.freq_ids)
+        lo, hi, g0, nn = Segments.doc_arrays(dl)
+        ls, ll, lo, hi, g0, nn, carry = self.upload(
+            [ls_h, ll_h, lo, hi, g0, nn, carry if carry.size else np.zeros(1, np.int64)])
+        segs = Segments(lo, hi, lo, hi, g0, nn)
         if tm is not None:
             self._tick(tm, "h2d", 0.0)
         verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
-        res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose, timings=tm)
+        res = self.run(text, n, ls, ll, segs, carry, with_factors=verbose, timings=tm)
         if verbose:
             self._log_events(res, dl)
         with TR.HostTimer(tm, "d2h"):

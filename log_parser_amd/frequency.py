@@ -4,11 +4,13 @@ The reference keeps a process-global ``ConcurrentHashMap<patternId, PatternFrequ
 survives across requests (``FrequencyTrackingService.java:25``) and computes a pattern's
 penalty from its hourly rate *before* recording the current match (``ScoringService.java:84-88``).
 
-Here the state is a per-id deque of ``(timestamp, count)`` records at request (batch)
-granularity — every match of one request carries the same instant, which is what the
-reference's per-match timestamps amount to within one request. The device pipeline turns the
-order dependency into a segmented exclusive scan: for the k-th match of id X in a batch,
-``count_before = carry[X] + k`` with ``carry[X]`` = matches of X still inside the window.
+Here the state is vectorised over id slots: a running total per slot plus a queue of batch
+records ``(timestamp, slots, counts)`` at request (batch) granularity -- every match of one
+request carries the same instant, which is what the reference's per-match timestamps amount to
+within one request. ``carry`` / ``record_counts`` cost O(ids touched), not a Python loop over
+the whole library per request. The device pipeline turns the order dependency into a segmented
+exclusive scan: for the k-th match of id X in a batch, ``count_before = carry[X] + k`` with
+``carry[X]`` = matches of X still inside the window.
 
 Extras over the reference: statistics / reset APIs exposed to the
 admin endpoints, optional snapshot/restore to a JSON file (off by default, like the reference).
@@ -30,85 +32,121 @@ class FrequencyState:
         self.window_s = float(window_hours) * 3600.0
         self.window_hours = window_hours
         self.clock = clock
-        self._rec: Dict[str, deque] = {}
-        self._tot: Dict[str, int] = {}
+        self._slot: Dict[str, int] = {}           # id -> slot (ids ever recorded or queried)
+        self._names: List[str] = []
+        self._seen = np.zeros(0, bool)            # slot recorded at least once (reference: map entry exists)
+        self._tot = np.zeros(0, np.int64)         # matches inside the window per slot
+        self._q: deque = deque()                  # (t, slots int64[], counts int64[]) per batch
+        self._ids_cache = (None, None)
         self._lock = threading.RLock()
 
-    def _prune(self, pid: str, now: float) -> None:
-        dq = self._rec.get(pid)
-        if not dq:
-            return
-        horizon = now - self.window_s
-        while dq and dq[0][0] <= horizon:
-            _, c = dq.popleft()
-            self._tot[pid] -= c
+    # ---- slots
+    def _slots(self, ids: List[str]) -> np.ndarray:
+        obj, sl = self._ids_cache
+        if obj is ids and sl is not None and sl.size == len(ids):
+            return sl
+        sl = np.fromiter((self._slot_of(p) for p in ids), np.int64, count=len(ids))
+        self._ids_cache = (ids, sl)
+        return sl
 
+    def _slot_of(self, pid: str) -> int:
+        s = self._slot.get(pid)
+        if s is None:
+            s = self._slot[pid] = len(self._names)
+            self._names.append(pid)
+            if s >= self._tot.size:
+                grow = max(64, self._tot.size)
+                self._tot = np.concatenate([self._tot, np.zeros(grow, np.int64)])
+                self._seen = np.concatenate([self._seen, np.zeros(grow, bool)])
+        return s
+
+    def _prune(self, now: float) -> None:
+        horizon = now - self.window_s
+        q = self._q
+        while q and q[0][0] <= horizon:
+            _, sl, c = q.popleft()
+            np.subtract.at(self._tot, sl, c)
+
+    # ---- device pipeline interface
     def carry(self, ids: List[str]) -> np.ndarray:
         """Matches inside the window for each id (the exclusive-scan carry)."""
         now = self.clock()
-        out = np.zeros(len(ids), np.int64)
         with self._lock:
-            for i, pid in enumerate(ids):
-                if pid in self._rec:
-                    self._prune(pid, now)
-                    out[i] = self._tot[pid]
-        return out
+            sl = self._slots(ids)
+            self._prune(now)
+            return self._tot[sl].copy()
 
     def record_counts(self, ids: List[str], counts: Iterable[int], now: Optional[float] = None) -> None:
         now = self.clock() if now is None else now
+        c = np.asarray(counts if not isinstance(counts, (list, tuple)) else np.array(counts), np.int64).reshape(-1)
+        c = c[:len(ids)]
+        nz = np.flatnonzero(c > 0)
+        if nz.size == 0:
+            return
         with self._lock:
-            for pid, c in zip(ids, counts):
-                c = int(c)
-                if c <= 0:
-                    continue
-                if pid not in self._rec:
-                    self._rec[pid] = deque()
-                    self._tot[pid] = 0
-                self._rec[pid].append((now, c))
-                self._tot[pid] += c
+            sl = self._slots(ids)[nz]
+            cc = c[nz].copy()
+            np.add.at(self._tot, sl, cc)
+            self._seen[sl] = True
+            self._q.append((now, sl, cc))
 
     # ---- reference API surface (FrequencyTrackingService.java:101-161)
     def get_pattern_frequency(self, pid: str) -> Optional[dict]:
         with self._lock:
-            if pid not in self._rec:
+            s = self._slot.get(pid)
+            if s is None or not self._seen[s]:
                 return None
-            self._prune(pid, self.clock())
-            c = self._tot[pid]
+            self._prune(self.clock())
+            c = int(self._tot[s])
             return {"patternId": pid, "currentCount": c, "hourlyRate": c / float(self.window_hours)}
 
     def statistics(self) -> Dict[str, int]:
-        now = self.clock()
         with self._lock:
-            for pid in list(self._rec):
-                self._prune(pid, now)
-            return dict(self._tot)
+            self._prune(self.clock())
+            return {self._names[s]: int(self._tot[s]) for s in np.flatnonzero(self._seen[:len(self._names)])}
 
     def reset(self, pid: str) -> None:
         with self._lock:
-            if pid in self._rec:
-                self._rec[pid].clear()
-                self._tot[pid] = 0
+            s = self._slot.get(pid)
+            if s is None:
+                return
+            self._tot[s] = 0
+            for _, sl, c in self._q:              # queued records of this id no longer count
+                c[sl == s] = 0
 
     def reset_all(self) -> None:
         with self._lock:
-            self._rec.clear()
-            self._tot.clear()
+            self._q.clear()
+            self._tot[:] = 0
+            self._seen[:] = False
 
     # ---- in-memory capture / rollback (elastic DP re-runs a step after a rank failure)
     def capture(self) -> dict:
         with self._lock:
-            return {k: list(v) for k, v in self._rec.items()}
+            return {"q": [(t, sl.copy(), c.copy()) for t, sl, c in self._q], "tot": self._tot.copy(),
+                    "seen": self._seen.copy(), "n": len(self._names)}
 
     def rollback(self, state: dict) -> None:
         with self._lock:
-            self._rec = {k: deque(v) for k, v in state.items()}
-            self._tot = {k: sum(c for _, c in v) for k, v in state.items()}
+            self._q = deque((t, sl.copy(), c.copy()) for t, sl, c in state["q"])
+            tot = np.zeros_like(self._tot)
+            seen = np.zeros_like(self._seen)
+            tot[:state["tot"].size] = state["tot"]
+            seen[:state["seen"].size] = state["seen"]
+            self._tot, self._seen = tot, seen
 
-    # ---- checkpoint / resume (SURVEY §5.4)
+    # ---- checkpoint / resume (SURVEY §5.4): {"records": {id: [[t, count], ...]}}
+    def _records(self) -> Dict[str, list]:
+        rec: Dict[str, list] = {self._names[s]: [] for s in np.flatnonzero(self._seen[:len(self._names)])}
+        for t, sl, c in self._q:
+            for s, k in zip(sl.tolist(), c.tolist()):
+                if k > 0:
+                    rec[self._names[s]].append([t, k])
+        return rec
+
     def snapshot(self, path: str) -> None:
         with self._lock:
-            data = {"window_hours": self.window_hours,
-                    "records": {k: list(map(list, v)) for k, v in self._rec.items()}}
+            data = {"window_hours": self.window_hours, "records": self._records()}
         tmp = path + ".tmp"
         with open(tmp, "w") as f:
             json.dump(data, f)
@@ -120,8 +158,14 @@ class FrequencyState:
         with open(path) as f:
             data = json.load(f)
         with self._lock:
-            self._rec.clear()
-            self._tot.clear()
+            self.reset_all()
+            ev = []
             for k, v in data.get("records", {}).items():
-                self._rec[k] = deque((float(t), int(c)) for t, c in v)
-                self._tot[k] = sum(int(c) for _, c in v)
+                s = self._slot_of(k)
+                self._seen[s] = True
+                ev += [(float(t), s, int(c)) for t, c in v]
+            for t, s, c in sorted(ev):
+                sl = np.array([s], np.int64)
+                cc = np.array([c], np.int64)
+                self._tot[s] += c
+                self._q.append((t, sl, cc))

@@ -106,42 +106,36 @@ LINE_BLK_SHIFT = 12
 def line_block_index(line_start: torch.Tensor, nbytes: int) -> torch.Tensor:
     """blk[b] = line containing byte b << 12 (int32), for O(log lines-per-4KiB) line lookups."""
     nblk = (max(nbytes, 1) >> LINE_BLK_SHIFT) + 2
-    pos = torch.arange(nblk, dtype=torch.int64, device=line_start.device) << LINE_BLK_SHIFT
-    idx = torch.searchsorted(line_start, pos, right=True) - 1
-    return idx.clamp(min=0).to(torch.int32)
+    blk = torch.empty(nblk, dtype=torch.int32, device=line_start.device)
+    N.blk_index(line_start.data_ptr(), line_start.numel(), nblk, blk.data_ptr(), _s(line_start), line_start.is_cuda)
+    return blk
 
 
 def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) -> torch.Tensor:
-    """Literal prefilter -> (regex << 32 | line) candidates.
+    """Literal prefilter -> (regex << 32 | line) candidates (unverified, may repeat).
 
     GPU: k_prefilter streams the text and stages bloom gram hits (position, gram length);
-    k_pf_verify then checks whole literals, one lane per hit (keeps the streaming kernel tight).
+    k_pf_verify then checks whole literals, one lane per hit, reading the gram-hit count on the
+    device (grid-stride) -- both counts come back in ONE host read.
     """
     nlines = line_start.numel()
     if text.is_cuda:
+        dev = text.device
         gcap = cap
-        while True:
-            gh = torch.empty(max(gcap, 1), dtype=torch.int64, device=text.device)
-            cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
-            N.prefilter_dev(text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines, gh.data_ptr(), gcap,
-                            cnt.data_ptr(), grid, _s(text))
-            c = int(cnt.item())
-            if c <= gcap:
-                gh = gh[:c]
-                break
-            gcap = c
-        if gh.numel() == 0:
-            return torch.empty(0, dtype=torch.int64, device=text.device)
         blk = line_block_index(line_start, nbytes)
         while True:
-            cand = torch.empty(max(cap, 1), dtype=torch.int64, device=text.device)
-            cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
-            N.pf_verify_dev(gh.data_ptr(), gh.numel(), text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(),
-                            nlines, blk.data_ptr(), cand.data_ptr(), cap, cnt.data_ptr(), _s(text))
-            c = int(cnt.item())
-            if c <= cap:
-                return cand[:c]
-            cap = c
+            gh = torch.empty(max(gcap, 1), dtype=torch.int64, device=dev)
+            cand = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+            cnt = torch.zeros(2, dtype=torch.int64, device=dev)        # [gram hits, candidates]
+            N.prefilter_dev(text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines, gh.data_ptr(), gcap,
+                            cnt.data_ptr(), grid, _s(text))
+            N.pf_verify_dev(gh.data_ptr(), gcap, text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines,
+                            blk.data_ptr(), cand.data_ptr(), cap, cnt.data_ptr() + 8, _s(text), cnt.data_ptr())
+            c = cnt.cpu()
+            g, k = int(c[0]), int(c[1])
+            if g <= gcap and k <= cap:
+                return cand[:k]
+            gcap, cap = max(gcap, g), max(cap, k)
     while True:
         cand = torch.empty(max(cap, 1), dtype=torch.int64)
         c = N.prefilter_host(text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines, cand.data_ptr(), cap)
@@ -239,3 +233,154 @@ def nfa_scan(groups: torch.Tensor, group_list: torch.Tensor, ncls: int, text, li
         if c <= cap:
             return out[:c]
         cap = c
+
+
+# ---------------------------------------------------------------------------------------------
+# post-match pipeline (csrc/kernels/lp_post.hip): hit CSR, events, frequency ranks, features
+
+class Uploader:
+    """Several small host arrays -> device with ONE async H2D copy through a grow-only pinned
+    buffer (line index, segment table, frequency carry of a request batch). CPU: zero-copy views.
+    Reusing the pinned buffer is safe: every batch ends with a blocking read of its results,
+    which orders after this copy on the same stream."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.pinned: Optional[torch.Tensor] = None
+
+    def __call__(self, arrays):
+        import numpy as np
+        arrays = [np.ascontiguousarray(a) for a in arrays]
+        if self.device.type != "cuda":
+            return [torch.from_numpy(a) for a in arrays]
+        offs, o = [], 0
+        for a in arrays:
+            offs.append(o)
+            o += (a.nbytes + 255) // 256 * 256
+        o = max(o, 256)
+        if self.pinned is None or self.pinned.numel() < o:
+            self.pinned = torch.empty(max(o * 5 // 4, 1 << 16), dtype=torch.uint8, pin_memory=True)
+        hv = self.pinned.numpy()
+        for a, off in zip(arrays, offs):
+            hv[off:off + a.nbytes] = a.reshape(-1).view(np.uint8)
+        dev = torch.empty(o, dtype=torch.uint8, device=self.device)
+        dev.copy_(self.pinned[:o], non_blocking=True)
+        return [dev[off:off + a.nbytes].view(_TORCH_DTYPE[a.dtype.str]) for a, off in zip(arrays, offs)]
+
+
+_TORCH_DTYPE = {"<i8": torch.int64, "<i4": torch.int32, "<u1": torch.uint8, "<f8": torch.float64, "|u1": torch.uint8,
+                "|b1": torch.bool}
+
+
+class Workspace:
+    """Grow-only device scratch buffer for the post-match kernels' temporaries (rocPRIM temp
+    storage, sort ping-pong buffers, window difference array). One per engine; stream-ordered
+    reuse is safe because every batch ends with a host read of its results."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int) -> Tuple[int, int]:
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(int(nbytes * 5 // 4), 1 << 20), dtype=torch.uint8, device=self.device)
+        return self.buf.data_ptr(), self.buf.numel()
+
+    def ptr(self) -> Tuple[int, int]:
+        return (0, 0) if self.buf is None else (self.buf.data_ptr(), self.buf.numel())
+
+
+def _run_ws(call, ws: Optional[Workspace]):
+    """Device calls report the workspace they need and run only when it suffices."""
+    p, n = ws.ptr()
+    need = call(p, n)
+    if need > n:
+        p, n = ws.get(need)
+        call(p, n)
+
+
+def ev_tables(tabs: dict, segs, nkeys: int, npat: int) -> tuple:
+    return (tabs["prim_off"].data_ptr(), tabs["prim_pats"].data_ptr(), tabs["freq_key"].data_ptr(),
+            tabs["ctx_before"].data_ptr(), tabs["ctx_after"].data_ptr(), segs.lo.data_ptr(), segs.hi.data_ptr(),
+            segs.own_lo.data_ptr(), segs.own_hi.data_ptr(), segs.lo.numel(), nkeys, N.bits_for(max(npat, 1)))
+
+
+def post_hits(cand: torch.Tensor, pre_from: int, L: int, R: int, text, line_start, line_len, dfa_tuple,
+              evt: tuple, ws: Optional[Workspace]):
+    """Candidates -> (hits, hit_line, hit_off, ev_cnt, ev_end, n_hits, n_events).
+
+    ``cand[:pre_from]`` are prefilter candidates still to DFA-verify, ``cand[pre_from:]`` hits of
+    engines that verified already (scan / MFMA NFA / host fallback). Duplicates are allowed.
+    Output hits are sorted unique (regex << 32 | line); one 16-byte host read for the counts."""
+    dev = cand.device
+    n = cand.numel()
+    m = max(n, 1)
+    hits = torch.empty(m, dtype=torch.int64, device=dev)
+    hit_line = torch.empty(m, dtype=torch.int32, device=dev)
+    hit_off = torch.empty(R + 1, dtype=torch.int64, device=dev)
+    ev_cnt = torch.empty(m, dtype=torch.int64, device=dev)
+    ev_end = torch.empty(m, dtype=torch.int64, device=dev)
+    counters = torch.zeros(2, dtype=torch.int64, device=dev)
+    lbits, rbits = N.bits_for(max(L, 1)), N.bits_for(max(R, 1))
+
+    def call(wp, wn):
+        return N.post_hits(cand.data_ptr(), n, pre_from, lbits, rbits, R, text.data_ptr(), line_start.data_ptr(),
+                           line_len.data_ptr(), dfa_tuple, evt, hits.data_ptr(), hit_line.data_ptr(),
+                           hit_off.data_ptr(), ev_cnt.data_ptr(), ev_end.data_ptr(), counters.data_ptr(), wp, wn,
+                           _s(cand), cand.is_cuda)
+
+    if cand.is_cuda:
+        _run_ws(call, ws)
+        c = counters.cpu()
+    else:
+        call(0, 0)
+        c = counters
+    nh, ne = int(c[0]), int(c[1])
+    return hits[:nh], hit_line, hit_off, ev_cnt, ev_end, nh, ne
+
+
+def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text, line_start, line_len, dfa_tuple,
+                nkeys: int, ws: Optional[Workspace], features: bool = True):
+    """Events in reference order + segment, frequency rank/key, per-key counts and context features
+    (or, with ``features=False``, the int32 window coverage per line for another feature engine)."""
+    dev = text.device
+    ev_line = torch.empty(ne, dtype=torch.int32, device=dev)
+    ev_pat = torch.empty(ne, dtype=torch.int32, device=dev)
+    ev_seg = torch.empty(ne, dtype=torch.int32, device=dev)
+    ev_rank = torch.empty(ne, dtype=torch.int64, device=dev)
+    ev_fkey = torch.empty(ne, dtype=torch.int64, device=dev)
+    freq_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
+    # k_feat_cov writes every line (0 outside windows); the host twin too
+    feat = torch.empty(max(L, 1), dtype=torch.uint8, device=dev) if features and L else \
+        torch.zeros(max(L, 1), dtype=torch.uint8, device=dev)
+    cov = None if features else torch.zeros(max(L, 1), dtype=torch.int32, device=dev)
+    lbits = N.bits_for(max(L, 1))
+
+    def call(wp, wn):
+        return N.post_events(hits.data_ptr() if nh else 0, nh, ev_cnt.data_ptr(), ev_end.data_ptr(), ne, L, lbits,
+                             evt, text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), dfa_tuple,
+                             ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_rank.data_ptr(),
+                             ev_fkey.data_ptr(), freq_counts.data_ptr(), feat.data_ptr() if features else 0,
+                             _p(cov), wp, wn, _s(text), text.is_cuda)
+
+    if text.is_cuda:
+        _run_ws(call, ws)
+    else:
+        call(0, 0)
+    return ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts, feat, cov
+
+
+def score_fused(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_carry, st_tuple, sp_tuple, with_factors=False):
+    """k_score with the frequency count fused in: freq = carry[fkey] + rank (-1 without a key)."""
+    n = ev_line.numel()
+    out = torch.empty(n, dtype=torch.float64, device=ev_line.device)
+    fac = torch.empty((n, 7), dtype=torch.float64, device=ev_line.device) if with_factors else None
+    if n == 0:
+        return out, fac
+    args = (ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_rank.data_ptr(), ev_fkey.data_ptr(),
+            freq_carry.data_ptr(), n, st_tuple, sp_tuple, out.data_ptr(), _p(fac))
+    if ev_line.is_cuda:
+        N.score_dev(*args, _s(ev_line))
+    else:
+        N.score_host(*args)
+    return out, fac

@@ -247,12 +247,13 @@ PYBIND11_MODULE(_lpnative, m) {
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
                   P<unsigned long long>(count), grid, s); });
   m.def("pf_verify_dev", [](uint64_t gh, int64_t n, uint64_t text, int64_t nb, py::tuple pf, uint64_t ls, int64_t nl,
-                            uint64_t blk, uint64_t cand, int64_t cap, uint64_t count, uint64_t s, uint64_t dn) {
+                            uint64_t blk, uint64_t cand, int64_t cap, uint64_t count, uint64_t s, uint64_t dn,
+                            int max_grid) {
     pf_verify_dev(P<const int64_t>(gh), n, P<const uint8_t>(text), nb, pf_from(pf), P<const int64_t>(ls), nl,
                   P<const int32_t>(blk), P<int64_t>(cand), cap, P<unsigned long long>(count), s,
-                  P<const unsigned long long>(dn)); }, py::arg("gh"), py::arg("n"), py::arg("text"), py::arg("nb"),
-        py::arg("pf"), py::arg("ls"), py::arg("nl"), py::arg("blk"), py::arg("cand"), py::arg("cap"), py::arg("count"),
-        py::arg("s"), py::arg("dn") = 0);
+                  P<const unsigned long long>(dn), max_grid); }, py::arg("gh"), py::arg("n"), py::arg("text"),
+        py::arg("nb"), py::arg("pf"), py::arg("ls"), py::arg("nl"), py::arg("blk"), py::arg("cand"), py::arg("cap"),
+        py::arg("count"), py::arg("s"), py::arg("dn") = 0, py::arg("max_grid") = 8192);
   m.def("verify_dev", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out, uint64_t s) {
     verify_dev(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out), s); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
@@ -303,8 +304,10 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("post_events", [](uint64_t hits, int64_t nh, uint64_t ev_cnt, uint64_t ev_end, int64_t ne, int64_t L, int lbits,
                           py::tuple ev, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t ev_line,
                           uint64_t ev_pat, uint64_t ev_seg, uint64_t ev_rank, uint64_t ev_fkey, uint64_t freq_counts,
-                          uint64_t feat, uint64_t cov, uint64_t ws, size_t ws_bytes, uint64_t s, bool dev) -> size_t {
+                          uint64_t feat, uint64_t cov, int ctx_trans, int ctx_acc, uint64_t ws, size_t ws_bytes,
+                          uint64_t s, bool dev) -> size_t {
     EventsArgs A;
+    A.ctx_trans = ctx_trans; A.ctx_acc = ctx_acc;
     A.hits = P<const int64_t>(hits); A.nh = nh; A.ev_cnt = P<const int64_t>(ev_cnt);
     A.ev_end = P<const int64_t>(ev_end); A.ne = ne; A.L = L; A.lbits = lbits; A.ev = ev_from(ev);
     A.text = P<const uint8_t>(text); A.ls = P<const int64_t>(ls); A.ll = P<const int32_t>(ll); A.dfa = dfa_from(dfa);

@@ -6,75 +6,124 @@
 
 namespace lp {
 
-// Java logs.split("\\r?\\n") of b[s0, s1): trailing empty strings removed, a document without
-// any '\n' is one line (possibly empty). emit(start, len) for the first `limit` kept lines;
-// returns the number of kept lines.
-template <class F>
-static int64_t split_doc(const uint8_t* b, int64_t s0, int64_t s1, int64_t limit, F&& emit) {
-  int64_t start = s0, n = 0, kept = 0;
-  bool any = false;
-  for (;;) {
-    const void* q = memchr(b + start, '\n', (size_t)(s1 - start));
-    if (!q) break;
-    any = true;
-    const int64_t nl = static_cast<const uint8_t*>(q) - b;
-    int64_t end = nl;
-    if (end > start && b[end - 1] == '\r') --end;
-    if (n < limit) emit(start, end - start);
-    ++n;
-    if (end > start) kept = n;
-    start = nl + 1;
-  }
-  if (n < limit) emit(start, s1 - start);
-  ++n;
-  if (s1 > start || !any) kept = n;
-  return kept;
-}
+// Work unit: one document, or a ~256 KiB slice of a large one (so a single big request also
+// copies and splits on several threads).
+struct Unit {
+  int64_t doc, a, b;           // bytes [a, b) of document `doc` (absolute packed offsets)
+  std::vector<int64_t> nl;     // '\n' positions inside [a, b)
+  int64_t first_nl = 0;        // index of nl[0] among the document's newlines
+  int64_t prev = 0;            // position of the newline before this unit (doc start - 1 if none)
+};
 
 template <class F>
-static void parallel_docs(const int64_t* doc_off, int64_t D, int nthreads, F&& fn) {
-  const int64_t total = doc_off[D];
-  int T = std::max(1, std::min<int>(nthreads, (int)std::min<int64_t>(D, 1 + total / (1 << 20))));
+static void parallel_units(std::vector<Unit>& U, int64_t total, int nthreads, F&& fn) {
+  const int64_t n = (int64_t)U.size();
+  const int T = std::max(1, std::min<int>(nthreads, (int)std::min<int64_t>(n, 1 + total / (512 << 10))));
   if (T == 1) {
-    fn(0, D);
+    for (int64_t u = 0; u < n; ++u) fn(U[u]);
     return;
   }
-  // contiguous document ranges of ~equal bytes
-  std::vector<int64_t> cut(T + 1, D);
+  // contiguous unit ranges of ~equal bytes
+  std::vector<int64_t> cut(T + 1, n);
   cut[0] = 0;
-  for (int t = 1; t < T; ++t) {
-    const int64_t target = total / T * t;
-    cut[t] = std::max(cut[t - 1], (int64_t)(std::upper_bound(doc_off, doc_off + D + 1, target) - doc_off - 1));
+  int64_t acc = 0, t = 1;
+  for (int64_t u = 0; u < n && t < T; ++u) {
+    acc += U[u].b - U[u].a;
+    if (acc >= total / T * t) cut[t++] = u + 1;
   }
   std::vector<std::thread> th;
   th.reserve(T);
-  for (int t = 0; t < T; ++t)
-    if (cut[t + 1] > cut[t]) th.emplace_back([&, t] { fn(cut[t], cut[t + 1]); });
+  for (int k = 0; k < T; ++k)
+    if (cut[k + 1] > cut[k])
+      th.emplace_back([&, k] {
+        for (int64_t u = cut[k]; u < cut[k + 1]; ++u) fn(U[u]);
+      });
   for (auto& x : th) x.join();
 }
 
 void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, uint8_t* dst, int nthreads,
                      DocBatchIndex& out) {
-  std::vector<int64_t> cnt(D);
-  parallel_docs(doc_off, D, nthreads, [&](int64_t a, int64_t b) {
-    for (int64_t d = a; d < b; ++d) {
-      const int64_t s0 = doc_off[d], s1 = doc_off[d + 1];
-      if (s1 > s0) memcpy(dst + s0, src[d], (size_t)(s1 - s0));
-      cnt[d] = split_doc(dst, s0, s1, 0, [](int64_t, int64_t) {});
+  constexpr int64_t SLICE = 256 << 10;
+  std::vector<Unit> U;
+  U.reserve(D);
+  for (int64_t d = 0; d < D; ++d) {
+    const int64_t s0 = doc_off[d], s1 = doc_off[d + 1];
+    const int64_t k = nthreads > 1 ? std::max<int64_t>(1, (s1 - s0) / SLICE) : 1;
+    for (int64_t i = 0; i < k; ++i) U.push_back(Unit{d, s0 + (s1 - s0) * i / k, s0 + (s1 - s0) * (i + 1) / k, {}});
+  }
+  const int64_t total = doc_off[D];
+  // phase 1: copy + newline positions, one pass over the bytes (the slice is hot in cache)
+  parallel_units(U, total, nthreads, [&](Unit& u) {
+    const int64_t s0 = doc_off[u.doc];
+    if (u.b > u.a) memcpy(dst + u.a, src[u.doc] + (u.a - s0), (size_t)(u.b - u.a));
+    u.nl.reserve((size_t)((u.b - u.a) / 64 + 4));
+    const uint8_t* p = dst + u.a;
+    const uint8_t* e = dst + u.b;
+    while (p < e) {
+      const void* q = memchr(p, '\n', (size_t)(e - p));
+      if (!q) break;
+      const uint8_t* qq = static_cast<const uint8_t*>(q);
+      u.nl.push_back(qq - dst);
+      p = qq + 1;
     }
   });
+  // per document: newline numbering, kept lines (Java split: trailing empty strings dropped; a
+  // document without any '\n' is one line, possibly empty)
+  auto line_end = [&](int64_t nlpos, int64_t start) {   // '\r' before '\n' excluded
+    return (nlpos > start && dst[nlpos - 1] == '\r') ? nlpos - 1 : nlpos;
+  };
   out.doc_line_off.assign(D + 1, 0);
-  for (int64_t d = 0; d < D; ++d) out.doc_line_off[d + 1] = out.doc_line_off[d] + cnt[d];
+  std::vector<int64_t> kept(D, 0);
+  for (size_t i = 0; i < U.size();) {
+    const int64_t d = U[i].doc, s0 = doc_off[d], s1 = doc_off[d + 1];
+    size_t j = i;
+    int64_t nnl = 0, prev = s0 - 1;
+    for (; j < U.size() && U[j].doc == d; ++j) {
+      U[j].first_nl = nnl;
+      U[j].prev = prev;
+      nnl += (int64_t)U[j].nl.size();
+      if (!U[j].nl.empty()) prev = U[j].nl.back();
+    }
+    int64_t k = 0;
+    if (nnl == 0) {
+      k = 1;
+    } else if (s1 > prev + 1) {
+      k = nnl + 1;                       // last line (after the last '\n') is non-empty
+    } else {                             // walk back over the newlines to the last non-empty line
+      for (size_t v = j; v-- > i && k == 0;) {
+        const auto& nl = U[v].nl;
+        for (int64_t w = (int64_t)nl.size() - 1; w >= 0; --w) {
+          const int64_t start = w > 0 ? nl[w - 1] + 1 : U[v].prev + 1;
+          if (line_end(nl[w], start) > start) {
+            k = U[v].first_nl + w + 1;
+            break;
+          }
+        }
+      }
+    }
+    kept[d] = k;
+    i = j;
+  }
+  for (int64_t d = 0; d < D; ++d) out.doc_line_off[d + 1] = out.doc_line_off[d] + kept[d];
   out.line_start.resize(out.doc_line_off[D]);
   out.line_len.resize(out.doc_line_off[D]);
-  parallel_docs(doc_off, D, nthreads, [&](int64_t a, int64_t b) {
-    for (int64_t d = a; d < b; ++d) {
-      int64_t o = out.doc_line_off[d];
-      split_doc(dst, doc_off[d], doc_off[d + 1], cnt[d], [&](int64_t s, int64_t l) {
-        out.line_start[o] = s;
-        out.line_len[o] = (int32_t)l;
-        ++o;
-      });
+  // phase 2: line starts / lengths, each unit writes its own newlines' lines
+  parallel_units(U, total, nthreads, [&](Unit& u) {
+    const int64_t k = kept[u.doc], base = out.doc_line_off[u.doc];
+    int64_t start = u.prev + 1;
+    for (size_t w = 0; w < u.nl.size(); ++w) {
+      const int64_t g = u.first_nl + (int64_t)w;
+      if (g >= k) return;
+      out.line_start[base + g] = start;
+      out.line_len[base + g] = (int32_t)(line_end(u.nl[w], start) - start);
+      start = u.nl[w] + 1;
+    }
+    // the line after the document's last newline belongs to the document's last unit
+    const bool last_unit = u.b == doc_off[u.doc + 1];
+    const int64_t g = u.first_nl + (int64_t)u.nl.size();
+    if (last_unit && g < k) {
+      out.line_start[base + g] = start;
+      out.line_len[base + g] = (int32_t)(u.b - start);
     }
   });
 }

@@ -18,7 +18,8 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
-                   unsigned long long* count, uint64_t stream, const unsigned long long* dn = nullptr);
+                   unsigned long long* count, uint64_t stream, const unsigned long long* dn = nullptr,
+                   int max_grid = 8192);
 void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
                 const DfaPool& P, uint8_t* out, uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
@@ -94,6 +95,7 @@ struct EventsArgs {
   EvTables ev;
   const uint8_t* text; const int64_t* ls; const int32_t* ll;
   DfaPool dfa;
+  int ctx_trans, ctx_acc;    // table extents of the 4 context DFAs (pool entries 0..3), for LDS staging
   // outputs
   int32_t* ev_line; int32_t* ev_pat; int32_t* ev_seg; int64_t* ev_rank; int64_t* ev_fkey;
   int64_t* freq_counts;      // [nkeys]

@@ -28,34 +28,118 @@ LP_HD int final_term_len(const uint8_t* s, int n) {
   return 0;
 }
 
+// One DFA of the pool: transition rows (nc classes per state), byte -> class map, accept flags
+// (bit0: accepting at end of line, bit1: accepting before a final line terminator). States 0
+// (dead) and 1 (match found) are terminal.
+struct DfaRef {
+  const uint16_t* T;
+  const uint8_t* bm;
+  const uint8_t* A;
+  int nc;
+};
+LP_HD DfaRef dfa_ref(const DfaPool& P, int r) {
+  const int32_t* m = P.meta + 4 * r;
+  return DfaRef{P.trans + m[0], P.bytemap + 256 * r, P.acc + m[2], m[1]};
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// Advance K DFAs together over bytes s[0, e). Device form of the walk: bytes come from 16-byte
+// ALIGNED vector loads one block ahead (a 1-byte load per step would put a memory round trip on
+// the dependency chain); every step is branch-free (terminal states absorb via a select) and the
+// K chains are independent, so a step costs ~6 instructions per DFA and the table reads of the K
+// walks overlap. The earlier byte-at-a-time walk with per-step early exits compiled to ~500
+// instructions per step (~1900 cycles, tools/feat_probe). Callers' buffers are padded (text:
+// TEXT_PAD) so the look-ahead load stays in bounds.
+template <int K>
+__device__ __forceinline__ void dfa_advance(const DfaRef (&D)[K], const uint8_t* s, int e, int (&st)[K]) {
+  if (e <= 0) return;
+  const int sh = (int)((uintptr_t)s & 15);
+  const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
+  uint4 cur = blk[0];
+  for (int t0 = -sh; t0 < e; t0 += 16) {
+    const uint4 nxt = blk[1];
+    ++blk;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int t = t0 + j;
+      const bool on = (t >= 0) & (t < e);
+      const uint32_t w = (j < 4) ? cur.x : (j < 8) ? cur.y : (j < 12) ? cur.z : cur.w;
+      const int c = (int)((w >> (8 * (j & 3))) & 0xFFu);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int nx = D[k].T[st[k] * D[k].nc + D[k].bm[c]];
+        st[k] = (on && st[k] >= 2) ? nx : st[k];
+      }
+    }
+    cur = nxt;
+    bool alive = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) alive |= st[k] >= 2;
+    if (!alive) return;
+  }
+}
+
+// find() over one line for K DFAs: res bit k = DFA k matches (java.util.regex Matcher.find
+// semantics, see jregex.h): accept before a final line terminator, then at end of line.
+template <int K>
+__device__ __forceinline__ uint32_t dfa_find_k(const DfaRef (&D)[K], const uint8_t* s, int n) {
+  int st[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) st[k] = 2;
+  const int ftl = final_term_len(s, n);
+  const int ft = ftl ? n - ftl : n;
+  dfa_advance<K>(D, s, ft, st);
+  if (ftl) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (st[k] >= 2 && (D[k].A[st[k]] & 2)) st[k] = 1;
+    dfa_advance<K>(D, s + ft, ftl, st);
+  }
+  uint32_t res = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (st[k] == 1 || (st[k] >= 2 && (D[k].A[st[k]] & 1))) res |= 1u << k;
+  return res;
+}
+#endif
+
 // find() of regex r over one line (java.util.regex Matcher.find semantics, see jregex.h)
 LP_HD bool dfa_run(const DfaPool& P, int r, const uint8_t* s, int n) {
-  const int32_t* m = P.meta + 4 * r;
-  const uint16_t* T = P.trans + m[0];
-  const int nc = m[1];
-  const uint8_t* A = P.acc + m[2];
-  const uint8_t* bm = P.bytemap + 256 * r;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const DfaRef D[1] = {dfa_ref(P, r)};
+  return dfa_find_k<1>(D, s, n) != 0;
+#else
+  const DfaRef D = dfa_ref(P, r);
   int ft = n - final_term_len(s, n);
   if (ft == n) ft = -1;
   int st = 2;
   for (int t = 0; t < n; ++t) {
-    if (t == ft && (A[st] & 2)) return true;
-    st = T[st * nc + bm[s[t]]];
+    if (t == ft && (D.A[st] & 2)) return true;
+    st = D.T[st * D.nc + D.bm[s[t]]];
     if (st < 2) return st == 1;
   }
-  return (A[st] & 1) != 0;
+  return (D.A[st] & 1) != 0;
+#endif
 }
 
 // Context features of one line (ContextAnalysisService.java:62-83); DFAs 0..3 of the pool are the
 // four internal regexes: bit0 ERROR, bit1 WARN (only when not ERROR: the reference's else-if),
-// bit2 stack-trace line, bit3 exception/error class name.
+// bit2 stack-trace line, bit3 exception/error class name. On the device the 4 walks advance
+// together over one byte stream (4 independent dependency chains per step instead of 4 passes).
 LP_HD uint8_t context_feat(const DfaPool& P, const uint8_t* s, int len) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const DfaRef D[4] = {dfa_ref(P, 0), dfa_ref(P, 1), dfa_ref(P, 2), dfa_ref(P, 3)};
+  const uint32_t res = dfa_find_k<4>(D, s, len);
+  const uint8_t f = (res & 1u) ? 1 : ((res & 2u) ? 2 : 0);
+  return (uint8_t)(f | (res & 12u));
+#else
   uint8_t f = 0;
   if (dfa_run(P, 0, s, len)) f |= 1;
   else if (dfa_run(P, 1, s, len)) f |= 2;
   if (dfa_run(P, 2, s, len)) f |= 4;
   if (dfa_run(P, 3, s, len)) f |= 8;
   return f;
+#endif
 }
 
 // --------------------------------------------------------------------------------------------
@@ -140,30 +224,84 @@ LP_HD int64_t locate_line(const int64_t* ls, int64_t n, const int32_t* blk, int6
   return lo;
 }
 
-// Probe one gram hit at text position p; appends (regex<<32 | line) candidates.
-template <typename AppendFn>
-LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, uint32_t gram, int g,
-                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, AppendFn&& append) {
-  uint64_t key = (uint64_t)gram | ((uint64_t)g << 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+// 16 bytes starting at p (any alignment) from two aligned vector loads + byte funnel shifts
+__device__ __forceinline__ void load16u(const uint8_t* p, uint32_t out[4]) {
+  const int sh = (int)((uintptr_t)p & 15);
+  const uint4* b = reinterpret_cast<const uint4*>(p - sh);
+  const uint4 x = b[0], y = b[1];
+  uint32_t a0 = x.x, a1 = x.y, a2 = x.z, a3 = x.w, a4 = y.x, a5 = y.y, a6 = y.z, a7 = y.w;
+  const int q = sh >> 2, r = sh & 3;
+  if (q & 2) { a0 = a2; a1 = a3; a2 = a4; a3 = a5; a4 = a6; a5 = a7; }
+  if (q & 1) { a0 = a1; a1 = a2; a2 = a3; a3 = a4; a4 = a5; }
+  out[0] = __builtin_amdgcn_alignbyte(a1, a0, r);
+  out[1] = __builtin_amdgcn_alignbyte(a2, a1, r);
+  out[2] = __builtin_amdgcn_alignbyte(a3, a2, r);
+  out[3] = __builtin_amdgcn_alignbyte(a4, a3, r);
+}
+// ASCII-case-insensitive compare of text against a lower-cased literal, 16 bytes per round trip
+// (a byte-at-a-time loop with early exit is one dependent memory round trip per byte)
+__device__ __forceinline__ bool lit_match16(const uint8_t* t, const uint8_t* lit, int len) {
+  for (int q = 0; q < len; q += 16) {
+    uint32_t a[4], b[4];
+    load16u(t + q, a);
+    load16u(lit + q, b);
+    const int rem = len - q;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = rem - 4 * i;
+      const uint32_t m = k >= 4 ? 0xFFFFFFFFu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u));
+      diff |= (lower4(a[i]) ^ b[i]) & m;
+    }
+    if (diff) return false;
+  }
+  return true;
+}
+#endif
+
+// Hash-table bucket of a gram hit: literals gram_lits[s .. s+c) share that gram (c = 0: none).
+LP_HD void pf_bucket(const PfTables& T, uint32_t gram, int g, int& s, int& c) {
+  const uint64_t key = (uint64_t)gram | ((uint64_t)g << 32);
   uint32_t h = ht_hash(gram, g) & T.ht_mask;
+  s = 0;
+  c = 0;
   for (;;) {
-    uint64_t kk = T.ht_key[h];
+    const uint64_t kk = T.ht_key[h];
     if (kk == ~0ull) return;
     if (kk == key) break;
     h = (h + 1) & T.ht_mask;
   }
-  const int s = T.ht_val[h], c = T.ht_cnt[h];
+  s = T.ht_val[h];
+  c = T.ht_cnt[h];
+}
+
+// Does literal `lit` occur with its gram window at text position p (ASCII case-insensitive)?
+LP_HD bool pf_lit_at(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, int lit) {
+  const int lo = T.lit_off[lit], len = T.lit_off[lit + 1] - lo;
+  const int64_t st = p - T.lit_goff[lit];
+  if (st < 0 || st + len > nbytes) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return lit_match16(text + st, T.lit_bytes + lo, len);
+#else
+  for (int q = 0; q < len; ++q)
+    if (lower_byte(text[st + q]) != T.lit_bytes[lo + q]) return false;
+  return true;
+#endif
+}
+
+// Probe one gram hit at text position p; appends (regex<<32 | line) candidates. A literal never
+// contains '\n', so every literal of the bucket that matches lies on the line of p.
+template <typename AppendFn>
+LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, uint32_t gram, int g,
+                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, AppendFn&& append) {
+  int s, c;
+  pf_bucket(T, gram, g, s, c);
   int64_t line = -1;
   for (int j = 0; j < c; ++j) {
     const int lit = T.gram_lits[s + j];
-    const int lo = T.lit_off[lit], len = T.lit_off[lit + 1] - lo;
-    const int64_t st = p - T.lit_goff[lit];
-    if (st < 0 || st + len > nbytes) continue;
-    bool ok = true;
-    for (int q = 0; q < len; ++q)
-      if (lower_byte(text[st + q]) != T.lit_bytes[lo + q]) { ok = false; break; }
-    if (!ok) continue;
-    if (line < 0) line = locate_line(line_start, nlines, blk_line, st);
+    if (!pf_lit_at(T, text, nbytes, p, lit)) continue;
+    if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
     if (line < 0) line = 0;
     for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
       append(((int64_t)T.lit_reg[r] << 32) | line);

@@ -311,8 +311,11 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
   if (c > 0) pf_flush(buf, cnt, gbase, c, cand, cap, count);
 }
 
-// K3a': literal verification of staged gram hits (one lane per hit): hash-table probe, full
-// literal compare at the literal's start (hit position - gram offset), candidate append.
+// K3a': literal verification of staged gram hits. A 16-lane group takes one gram hit: all lanes
+// probe the (small) hash table together, then the bucket's literals are split across the lanes --
+// a hit's cost is ~4 dependent memory round trips instead of ~3 per literal in the bucket, which
+// decides the latency of small requests (shared grams give buckets of up to ~70 literals).
+constexpr int PV_LANES = 16;
 __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ ghits, int64_t n,
                                                    const unsigned long long* __restrict__ dn,
                                                    const uint8_t* __restrict__ text, int64_t nbytes, PfTables T,
@@ -332,16 +335,27 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
     n = d < n ? d : n;
   }
   const LdsAppender app{buf, &cnt, cand, cap, count};
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const int64_t i = base + threadIdx.x;
+  constexpr int HITS_PER_BLOCK = 256 / PV_LANES;
+  const int sub = threadIdx.x / PV_LANES, lane = threadIdx.x % PV_LANES;
+  const int64_t stride = (int64_t)gridDim.x * HITS_PER_BLOCK;
+  for (int64_t base = (int64_t)blockIdx.x * HITS_PER_BLOCK; base < n; base += stride) {
+    const int64_t i = base + sub;
     if (i < n) {
       const int64_t h = ghits[i];
       const int64_t p = h >> 2;
       const int G = 2 + (int)(h & 3);
       uint32_t g4 = 0;
       for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
-      pf_probe(T, text, nbytes, p, g4 & gram_mask(G), G, line_start, nlines, blk_line, app);
+      int s, c;
+      pf_bucket(T, g4 & gram_mask(G), G, s, c);
+      int64_t line = -1;
+      for (int j = lane; j < c; j += PV_LANES) {
+        const int lit = T.gram_lits[s + j];
+        if (!pf_lit_at(T, text, nbytes, p, lit)) continue;
+        if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
+        if (line < 0) line = 0;
+        for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r) app(((int64_t)T.lit_reg[r] << 32) | line);
+      }
     }
     __syncthreads();
     const int c = *reinterpret_cast<volatile int*>(&cnt);
@@ -525,10 +539,11 @@ void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64
 
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
-                   unsigned long long* count, uint64_t stream, const unsigned long long* dn) {
+                   unsigned long long* count, uint64_t stream, const unsigned long long* dn, int max_grid) {
   if (n <= 0) return;
   // with a device-side count the grid is sized for the buffer but capped (grid-stride loop)
-  const int g = dn ? (int)std::min<int64_t>(num_blocks(n, 256), 8192) : num_blocks(n, 256);
+  const int64_t need = (n + 256 / PV_LANES - 1) / (256 / PV_LANES);   // blocks for one pass over n hits
+  const int g = dn ? (int)std::min<int64_t>(need, std::max(1, max_grid)) : (int)std::max<int64_t>(1, need);
   hipLaunchKernelGGL(k_pf_verify, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
                      line_start, nlines, blk_line, cand, cap, count);
   LP_CHECK(hipGetLastError());

@@ -53,8 +53,8 @@ int bits_for(int64_t n) {  // bits needed to hold values 0..n-1 (>= 1)
 // ---------------------------------------------------------------------------------------------
 // element functions (host + device)
 
-// segment of local line x: the last segment whose first line is <= x (documents are never empty:
-// Java split gives an empty document one line)
+// segment of local line x: the last segment whose first line is <= x (a document with zero kept
+// lines, e.g. "\n\n" under Java split, has lo == hi and is skipped by taking the last match)
 LP_HD int seg_of(const int32_t* lo, int nseg, int32_t x) {
   int a = 0, b = nseg;
   while (b - a > 1) {
@@ -227,20 +227,35 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t* __restrict__ fs, c
   if (j < ne) rank_one(fs, idx, ne, j, nkeys, ev_rank, ev_fkey, freq_counts);
 }
 
-// Context features of covered lines. A block owns FC_LINES consecutive lines: it compacts the
+// Context features of covered lines. A block owns `per_block` consecutive lines: it compacts the
 // covered ones into an LDS list (uncovered lines get 0) and then runs the 4 DFAs with every lane
 // busy -- covered lines come in short runs, so one lane per line would idle most of each wave.
-constexpr int FC_LINES = 4096;
-__global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ cov, int64_t L,
+// The 4 context DFAs (~2 KB) are staged in LDS: a DFA walk is a chain of dependent table loads,
+// ~64-cycle LDS hits instead of ~500-cycle L2 trips (a 10k-line request ran 136 us -> see profiles).
+constexpr int FC_MAX_LINES = 4096;
+constexpr int FC_TRANS = 8192;   // uint16 entries
+constexpr int FC_ACC = 1024;
+__global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ cov, int64_t L, int per_block,
                                                   const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
-                                                  const int32_t* __restrict__ ll, DfaPool P,
-                                                  uint8_t* __restrict__ feat) {
-  __shared__ int32_t list[FC_LINES];
+                                                  const int32_t* __restrict__ ll, DfaPool P, int ctx_trans,
+                                                  int ctx_acc, uint8_t* __restrict__ feat) {
+  __shared__ int32_t list[FC_MAX_LINES];
   __shared__ int n;
+  __shared__ int32_t s_meta[16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_bm[4 * 256];
+  __shared__ uint16_t s_trans[FC_TRANS];
+  __shared__ uint8_t s_acc[FC_ACC];
+  const bool lds = ctx_trans <= FC_TRANS && ctx_acc <= FC_ACC;
   if (threadIdx.x == 0) n = 0;
+  if (lds) {
+    if (threadIdx.x < 16) s_meta[threadIdx.x] = P.meta[threadIdx.x];
+    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) s_bm[i] = P.bytemap[i];
+    for (int i = threadIdx.x; i < ctx_trans; i += blockDim.x) s_trans[i] = P.trans[i];
+    for (int i = threadIdx.x; i < ctx_acc; i += blockDim.x) s_acc[i] = P.acc[i];
+  }
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * FC_LINES;
-  for (int k = threadIdx.x; k < FC_LINES; k += blockDim.x) {
+  const int64_t base = (int64_t)blockIdx.x * per_block;
+  for (int k = threadIdx.x; k < per_block; k += blockDim.x) {
     const int64_t x = base + k;
     if (x < L) {
       if (cov[x] > 0) list[atomicAdd(&n, 1)] = k;
@@ -249,9 +264,19 @@ __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ co
   }
   __syncthreads();
   const int m = n;
-  for (int j = threadIdx.x; j < m; j += blockDim.x) {
-    const int64_t x = base + list[j];
-    feat[x] = context_feat(P, text + ls[x], ll[x]);
+  // two call sites, each with a provable address space: the LDS copy compiles to ds_read (a
+  // runtime select between LDS and global pointers degrades every table read to a flat load)
+  if (lds) {
+    const DfaPool Q{s_meta, s_bm, s_trans, s_acc};
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+      const int64_t x = base + list[j];
+      feat[x] = context_feat(Q, text + ls[x], ll[x]);
+    }
+  } else {
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+      const int64_t x = base + list[j];
+      feat[x] = context_feat(P, text + ls[x], ll[x]);
+    }
   }
 }
 
@@ -363,7 +388,11 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
     size_t tb = t_scan;
     LP_PCHECK(rocprim::inclusive_scan(tmp, tb, diff, cov, (size_t)L, rocprim::plus<int32_t>(), st));
     if (A.feat) {
-      hipLaunchKernelGGL(k_feat_cov, dim3(nblk(L, FC_LINES)), dim3(256), 0, st, cov, L, A.text, A.ls, A.ll, A.dfa, A.feat);
+      // lines per block: enough blocks to spread a small request over the CUs, 4096 for big ones
+      int per = (int)std::min<int64_t>(FC_MAX_LINES, std::max<int64_t>(256, L / 1024));
+      per = (per + 255) / 256 * 256;
+      hipLaunchKernelGGL(k_feat_cov, dim3(nblk(L, per)), dim3(256), 0, st, cov, L, per, A.text, A.ls, A.ll, A.dfa,
+                         A.ctx_trans, A.ctx_acc, A.feat);
       LP_PCHECK(hipGetLastError());
     }
   }

@@ -261,7 +261,8 @@ class Engine:
         nkeys = len(self.lib.freq_ids)
         dfa_feats = self.context_engine != "mfma"
         ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts, feat, cov = K.post_events(
-            hits, nh, ev_cnt, ev_end, ne, L, evt, text, ls, ll, self.tabs["dfa"], nkeys, self.ws, features=dfa_feats)
+            hits, nh, ev_cnt, ev_end, ne, L, evt, text, ls, ll, self.tabs["dfa"], nkeys, self.ws, features=dfa_feats,
+            ctx_ext=self.lib.ctx_dfa_extent)
         if not dfa_feats:           # A/B engine: context features on the MFMA NFA kernel
             lines = torch.nonzero(cov[:L] > 0).flatten().to(torch.int32)
             feat = K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],

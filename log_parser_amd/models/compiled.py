@@ -296,7 +296,8 @@ class CompiledLibrary:
         lit_off = np.zeros(len(lits) + 1, np.int32)
         for i, l in enumerate(lits):
             lit_off[i + 1] = lit_off[i] + len(l)
-        lit_bytes = np.frombuffer(b"".join(lits) or b"\0", np.uint8).copy()
+        # 32 zero bytes of padding: the device literal compare reads 16-byte blocks past the end
+        lit_bytes = np.frombuffer(b"".join(lits) + bytes(32), np.uint8).copy()
         lit_reg_off = np.zeros(len(lits) + 1, np.int32)
         for i, rr in enumerate(lit_regs):
             lit_reg_off[i + 1] = lit_reg_off[i] + len(rr)
@@ -371,6 +372,15 @@ class CompiledLibrary:
                                for k in (1, 2, 3)}
         self._device_cache[key] = t
         return t
+
+    @property
+    def ctx_dfa_extent(self) -> Tuple[int, int]:
+        """(trans, acc) entries spanned by the 4 context DFAs (pool entries 0..3, offset 0): the
+        context-feature kernel stages exactly this prefix of the pool in LDS."""
+        m = self.dfa_meta.reshape(-1, 4)
+        if m.shape[0] > 4:
+            return int(m[4, 0]), int(m[4, 2])
+        return int(self.dfa_trans.size), int(self.dfa_acc.size)
 
     @property
     def n_regexes(self) -> int:

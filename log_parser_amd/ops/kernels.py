@@ -130,7 +130,8 @@ def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) ->
             N.prefilter_dev(text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines, gh.data_ptr(), gcap,
                             cnt.data_ptr(), grid, _s(text))
             N.pf_verify_dev(gh.data_ptr(), gcap, text.data_ptr(), nbytes, pf_tuple, line_start.data_ptr(), nlines,
-                            blk.data_ptr(), cand.data_ptr(), cap, cnt.data_ptr() + 8, _s(text), cnt.data_ptr())
+                            blk.data_ptr(), cand.data_ptr(), cap, cnt.data_ptr() + 8, _s(text), cnt.data_ptr(),
+                            max(16, min(8192, nbytes >> 13)))   # grid-stride over the device count
             c = cnt.cpu()
             g, k = int(c[0]), int(c[1])
             if g <= gcap and k <= cap:
@@ -320,7 +321,7 @@ def post_hits(cand: torch.Tensor, pre_from: int, L: int, R: int, text, line_star
     hit_off = torch.empty(R + 1, dtype=torch.int64, device=dev)
     ev_cnt = torch.empty(m, dtype=torch.int64, device=dev)
     ev_end = torch.empty(m, dtype=torch.int64, device=dev)
-    counters = torch.zeros(2, dtype=torch.int64, device=dev)
+    counters = torch.empty(2, dtype=torch.int64, device=dev)      # written by the pipeline
     lbits, rbits = N.bits_for(max(L, 1)), N.bits_for(max(R, 1))
 
     def call(wp, wn):
@@ -340,16 +341,17 @@ def post_hits(cand: torch.Tensor, pre_from: int, L: int, R: int, text, line_star
 
 
 def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text, line_start, line_len, dfa_tuple,
-                nkeys: int, ws: Optional[Workspace], features: bool = True):
+                nkeys: int, ws: Optional[Workspace], features: bool = True, ctx_ext: Tuple[int, int] = (1 << 30, 1 << 30)):
     """Events in reference order + segment, frequency rank/key, per-key counts and context features
-    (or, with ``features=False``, the int32 window coverage per line for another feature engine)."""
+    (or, with ``features=False``, the int32 window coverage per line for another feature engine).
+    ``ctx_ext`` = table extents of the 4 context DFAs (trans, acc entries) for LDS staging."""
     dev = text.device
     ev_line = torch.empty(ne, dtype=torch.int32, device=dev)
     ev_pat = torch.empty(ne, dtype=torch.int32, device=dev)
     ev_seg = torch.empty(ne, dtype=torch.int32, device=dev)
     ev_rank = torch.empty(ne, dtype=torch.int64, device=dev)
     ev_fkey = torch.empty(ne, dtype=torch.int64, device=dev)
-    freq_counts = torch.zeros(max(nkeys, 1), dtype=torch.int64, device=dev)
+    freq_counts = (torch.empty if nkeys else torch.zeros)(max(nkeys, 1), dtype=torch.int64, device=dev)
     # k_feat_cov writes every line (0 outside windows); the host twin too
     feat = torch.empty(max(L, 1), dtype=torch.uint8, device=dev) if features and L else \
         torch.zeros(max(L, 1), dtype=torch.uint8, device=dev)
@@ -361,7 +363,7 @@ def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text
                              evt, text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), dfa_tuple,
                              ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_rank.data_ptr(),
                              ev_fkey.data_ptr(), freq_counts.data_ptr(), feat.data_ptr() if features else 0,
-                             _p(cov), wp, wn, _s(text), text.is_cuda)
+                             _p(cov), ctx_ext[0], ctx_ext[1], wp, wn, _s(text), text.is_cuda)
 
     if text.is_cuda:
         _run_ws(call, ws)

@@ -179,3 +179,33 @@ def test_post_pipeline_gpu_equals_host_twin(gpu_device, seed):
     rd = eng_d.finish(pd, segs_d, carry.to(gpu_device))
     rc = eng_c.finish(pc, segs_c, carry)
     assert torch.equal(rd.score.cpu(), rc.score)     # bit-identical fp64 (no FMA contraction either side)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_pack_split_docs_sliced_large_documents(seed):
+    """Large documents are copied/split in 256 KiB slices on several threads: slice boundaries
+    inside '\\r\\n', runs of empty lines and trailing empties must still give Java's split."""
+    from log_parser_amd import golden
+    from log_parser_amd.native import N
+    rng = random.Random(seed)
+    docs = []
+    for _ in range(4):
+        parts = []
+        size = 0
+        target = rng.randint(300_000, 900_000)
+        while size < target:
+            x = rng.choice(["a", "line with words", "\r", "é", ""]) * rng.randint(0, 30) + \
+                rng.choice(["\n", "\r\n", "\n\n\n", "\r\n\r\n"])
+            parts.append(x)
+            size += len(x)
+        docs.append("".join(parts) + rng.choice(["", "\n\n\n", "\r\n", "tail", "\n\r"]))
+    docs.append("\n" * 600_000)                      # only empty lines: zero kept lines
+    docs.append("x" * 700_000)                        # no newline at all: one line
+    total = sum(len(d.encode()) for d in docs)
+    buf = np.zeros(total + 64, np.uint8)
+    for nthreads in (1, 4, 16):
+        ls, ll, dl, off = N.pack_split_docs(docs, buf.ctypes.data, buf.size, nthreads)
+        raw = buf.tobytes()
+        for d, doc in enumerate(docs):
+            got = [raw[a:a + b].decode() for a, b in zip(ls[dl[d]:dl[d + 1]], ll[dl[d]:dl[d + 1]])]
+            assert got == golden.split_lines(doc), (nthreads, d)

@@ -64,10 +64,15 @@ class Segments:
     n: torch.Tensor
 
     @staticmethod
-    def single(L: int, device) -> "Segments":
-        t32 = torch.tensor([0, L, 0, L], dtype=torch.int32, device=device)
-        t64 = torch.tensor([0, L], dtype=torch.int64, device=device)
+    def scalar(lo: int, hi: int, own_lo: int, own_hi: int, g0: int, n: int, device) -> "Segments":
+        """One segment (two small host->device copies instead of six)."""
+        t32 = torch.tensor([lo, hi, own_lo, own_hi], dtype=torch.int32, device=device)
+        t64 = torch.tensor([g0, n], dtype=torch.int64, device=device)
         return Segments(t32[0:1], t32[1:2], t32[2:3], t32[3:4], t64[0:1], t64[1:2])
+
+    @staticmethod
+    def single(L: int, device) -> "Segments":
+        return Segments.scalar(0, L, 0, L, 0, L, device)
 
     @staticmethod
     def doc_arrays(doc_line_off: np.ndarray):

@@ -60,13 +60,22 @@ def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
 @dataclass
 class StepOutput:
     result: RunResult
-    total_lines: int
-    own_start: int                 # global index of this rank's first owned line
+    own_counts: torch.Tensor       # owned lines per rank (C1 all-gather), stays on the device
+    rank: int
     pattern_counts: torch.Tensor   # global (all-reduced) events per pattern
     topk_score: Optional[torch.Tensor] = None   # rank 0: merged global top-k
     topk_line: Optional[torch.Tensor] = None    # 0-based global line
     topk_pat: Optional[torch.Tensor] = None
     summary: Optional[dict] = None
+
+    # host integers on demand (a host read here would stall the step's launch queue)
+    @property
+    def total_lines(self) -> int:
+        return int(self.own_counts.sum().item())
+
+    @property
+    def own_start(self) -> int:
+        return int(self.own_counts[:self.rank].sum().item())
 
 
 class ShardedAnalyzer:
@@ -102,23 +111,21 @@ class ShardedAnalyzer:
         dev = text.device
         L = ls.numel()
         own_lo, own_hi = halo_left, L - halo_right
-        i32 = lambda v: torch.tensor([v], dtype=torch.int32, device=dev)  # noqa: E731
-        i64 = lambda v: torch.tensor([v], dtype=torch.int64, device=dev)  # noqa: E731
-        segs = Segments(i32(0), i32(L), i32(own_lo), i32(own_hi), i64(0), i64(1))
+        segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev)
         prep = eng.prepare(text, nbytes, ls, ll, segs)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
-        pack = torch.cat([i64(own_hi - own_lo), prep.freq_counts[:nk].to(torch.int64), chain.to(torch.int64)])
+        pack = torch.cat([segs.own_hi.to(torch.int64) - own_lo, prep.freq_counts[:nk].to(torch.int64),
+                          chain.to(torch.int64)])
         g = all_gather_rows(pack, self.group)                      # C1 + C3 + C4 in one collective
         own_counts = g[:, 0]
-        own_start = int(own_counts[:rank].sum().item())
-        total = int(own_counts.sum().item())
+        own_start = own_counts[:rank].sum(0, keepdim=True)        # device scalars: no host round trip
         carry = eng.freq_carry()
         if nk:
             carry = carry + g[:rank, 1:1 + nk].sum(0)
         seq_carry = self._compose_chain(g[:, 1 + nk:].to(torch.int32), rank)
-        segs.g0 = i64(own_start - halo_left)
-        segs.n = i64(max(total, 1))
+        segs.g0 = own_start - halo_left
+        segs.n = own_counts.sum(0, keepdim=True).clamp(min=1)
         res = eng.finish(prep, segs, carry, seq_carry, with_factors)
         # C5/C6 + frequency histogram: one all-reduce
         P = len(lib.patterns)
@@ -127,7 +134,7 @@ class ShardedAnalyzer:
         red = all_reduce_sum(red, self.group)
         pattern_counts = red[:P]
         eng.commit_frequency(red[P:])
-        out = StepOutput(res, total, own_start, pattern_counts)
+        out = StepOutput(res, own_counts, rank, pattern_counts)
         # C7: top-k
         if topk > 0:
             k = min(topk, res.score.numel())

@@ -139,8 +139,13 @@ class StreamAnalyzer:
     def _plan(self, src, eff: int, start: int = 0):
         H = self.engine.lib.halo
         pos = start
+        k = 0
         while pos < eff or (pos == 0 and eff == 0):
-            end = min(eff, pos + self.chunk_bytes)
+            # ramp-up: the first chunks are 1/8, 1/4, 1/2 of chunk_bytes so the staging -> H2D ->
+            # compute pipeline fills in milliseconds instead of one full-size host copy
+            size = max(min(self.chunk_bytes, 16 << 20), self.chunk_bytes >> max(0, self.RAMP - k))
+            k += 1
+            end = min(eff, pos + size)
             if end < eff:
                 j = src.find(b"\n", end - 1)
                 end = eff if (j < 0 or j + 1 > eff) else j + 1
@@ -160,6 +165,7 @@ class StreamAnalyzer:
             pos = end
 
     PINNED_BUFFERS = 3          # one being filled, one in the H2D copy, one spare
+    RAMP = 3                    # chunk-size ramp-up steps (halving)
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None):
         """Stages line-aligned chunks (+ halos) into pinned buffers. On GPU the buffers come from a
@@ -284,9 +290,7 @@ class StreamAnalyzer:
             ls, ll = K.split_chunk_lines(text, n)
             L = ls.numel()
             own_lo, own_hi = lh, L - rh
-            i32 = lambda v: torch.tensor([v], dtype=torch.int32, device=dev)  # noqa: E731
-            i64 = lambda v: torch.tensor([v], dtype=torch.int64, device=dev)  # noqa: E731
-            segs = Segments(i32(0), i32(L), i32(own_lo), i32(own_hi), i64(line_base - own_lo), i64(1 << 62))
+            segs = Segments.scalar(0, L, own_lo, own_hi, line_base - own_lo, 1 << 62, dev)
             prep = eng.prepare(text, n, ls, ll, segs)
             chain = eng.seq_chain_table(prep, own_lo, own_hi)
             res = eng.finish(prep, segs, freq_carry + run_counts, seq_state, with_factors=True)

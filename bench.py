@@ -47,6 +47,9 @@ def parse():
                     help="rank 0: p50 latency of N single 10k-line /parse requests after the timed loop (0 = off)")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend: auto = nccl (RCCL) on GPUs; gloo = host-staged collectives, "
+                         "only to rehearse several ranks on ONE GPU")
     return ap.parse_args()
 
 
@@ -65,14 +68,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available() and args.device != "cpu"
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        local_gpu = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local_gpu)
+        device = torch.device("cuda", local_gpu)
         from log_parser_amd.utils.numa import bind_to_gpu_numa
-        bind_to_gpu_numa(local_rank)          # pinned ingest buffers on the GPU's own socket
+        bind_to_gpu_numa(local_gpu)          # pinned ingest buffers on the GPU's own socket
     else:
         device = torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl" if use_cuda else "gloo", rank=rank, world_size=world)
+        backend = args.backend if args.backend != "auto" else ("nccl" if use_cuda else "gloo")
+        dist.init_process_group(backend, rank=rank, world_size=world)
 
     params = ScoringParams()
     sets, trig = make_library(args.patterns, seed=7)
@@ -158,6 +163,8 @@ def main():
     dt = time.perf_counter() - t0
     dt_t = torch.tensor([dt], dtype=torch.float64, device=device)
     if world > 1:
+        if dist.get_backend() == "gloo":
+            dt_t = dt_t.cpu()
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     total_lines = last.total_lines

@@ -38,22 +38,36 @@ def world() -> tuple:
     return 0, 1
 
 
+def host_staged(group=None) -> bool:
+    """True when the process group cannot move device tensors (gloo): collectives then stage
+    through host memory. Production GPU runs use nccl (= RCCL) and never take this path; it lets
+    the multi-rank GPU pipeline be exercised with several ranks on ONE GPU (tests/test_dp.py)."""
+    return dist.get_backend(group) == "gloo"
+
+
 def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
     """all_gather of a 1-D tensor -> [world, n] (RCCL all_gather_into_tensor on GPU)."""
     r, w = world()
     if w == 1:
         return t.unsqueeze(0)
-    out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-    if t.is_cuda:
+    if t.is_cuda and not host_staged(group):
+        out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous(), group=group)
-    else:
-        dist.all_gather(list(out.unbind(0)), t.contiguous(), group=group)
-    return out
+        return out
+    src = t.detach().cpu().contiguous()
+    out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype)
+    dist.all_gather(list(out.unbind(0)), src, group=group)
+    return out.to(t.device)
 
 
 def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
     if world()[1] > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        if t.is_cuda and host_staged(group):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return t
 
 
@@ -211,18 +225,25 @@ def exchange_halos(own: torch.Tensor, own_nbytes: int, head: int, tail: int, gro
     left = torch.empty(lsize, dtype=torch.uint8, device=dev)
     right = torch.empty(rsize, dtype=torch.uint8, device=dev)
     peer = (lambda x: dist.get_global_rank(group, x)) if group is not None else (lambda x: x)
-    ops = []
+    plan = []                                           # (isend | irecv, device tensor, peer)
     if r > 0 and head:
-        ops.append(dist.P2POp(dist.isend, own[:head].contiguous(), peer(r - 1), group))
+        plan.append((dist.isend, own[:head].contiguous(), peer(r - 1)))
     if r > 0 and lsize:
-        ops.append(dist.P2POp(dist.irecv, left, peer(r - 1), group))
+        plan.append((dist.irecv, left, peer(r - 1)))
     if r < w - 1 and tail:
-        ops.append(dist.P2POp(dist.isend, own[own_nbytes - tail:own_nbytes].contiguous(), peer(r + 1), group))
+        plan.append((dist.isend, own[own_nbytes - tail:own_nbytes].contiguous(), peer(r + 1)))
     if r < w - 1 and rsize:
-        ops.append(dist.P2POp(dist.irecv, right, peer(r + 1), group))
-    if ops:
+        plan.append((dist.irecv, right, peer(r + 1)))
+    if plan:
+        staged = dev.type == "cuda" and host_staged(group)   # gloo p2p moves host tensors only
+        bufs = [t.cpu() if staged else t for _, t, _ in plan]
+        ops = [dist.P2POp(fn, b_, pr, group) for (fn, _, pr), b_ in zip(plan, bufs)]
         for q in dist.batch_isend_irecv(ops):
             q.wait()
+        if staged:
+            for (fn, t, _), b_ in zip(plan, bufs):
+                if fn is dist.irecv:
+                    t.copy_(b_)
     return left, right
 
 

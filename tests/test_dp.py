@@ -50,13 +50,14 @@ def _reference():
     return outs
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, dev="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         lib, data = _setup()
-        eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
-        full = _text(data)
+        device = torch.device(dev)
+        eng = Engine(lib, Config.load(overrides={"engine.device": dev}), device=device)
+        full = _text(data).to(device)
         gls, gll = K.split_lines(full, len(data))
         L = gls.numel()
         lo, hi, hl, hr = shard_bounds(L, world, rank, lib.halo)
@@ -64,7 +65,7 @@ def _worker(rank, world, port, q):
         base = int(gls[a])
         end = int(gls[b]) if b < L else len(data)
         shard = data[base:end]
-        t = _text(shard)
+        t = _text(shard).to(device)
         ls = (gls[a:b] - base).contiguous()
         ll = gll[a:b].contiguous()
         sa = ShardedAnalyzer(eng)
@@ -72,9 +73,9 @@ def _worker(rank, world, port, q):
         for _ in range(STEPS):
             out = sa.step(t, len(shard), ls, ll, hl, hr, topk=5)
             r = out.result
-            gl = (r.ev_line.numpy().astype(np.int64) - hl + out.own_start)
-            res.append((gl, r.ev_pat.numpy(), r.score.numpy(), out.total_lines,
-                        None if out.topk_score is None else out.topk_score.numpy()))
+            gl = (r.ev_line.cpu().numpy().astype(np.int64) - hl + out.own_start)
+            res.append((gl, r.ev_pat.cpu().numpy(), r.score.cpu().numpy(), out.total_lines,
+                        None if out.topk_score is None else out.topk_score.cpu().numpy()))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -88,13 +89,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_equals_single(world):
+def _run_sharded(world, dev):
     ref = _reference()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dev)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))
@@ -114,15 +114,29 @@ def test_sharded_equals_single(world):
         np.testing.assert_allclose(got[0][s][4], top, rtol=1e-13)
 
 
-def _worker_p2p(rank, world, port, q):
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_equals_single(world):
+    _run_sharded(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_sharded_equals_single_gpu_ranks(gpu_device):
+    """2 ranks on the one GPU of the test box: the gfx950 pipeline of every rank + the packed
+    carries / histograms / top-k collectives (host-staged gloo here; RCCL on a multi-GPU node)
+    must reproduce the single-process CPU reference event for event."""
+    _run_sharded(2, "cuda:0")
+
+
+def _worker_p2p(rank, world, port, q, dev="cpu"):
     """Each rank holds ONLY its own lines; halos come from the neighbours over send/recv (C2)."""
     from log_parser_amd.parallel.dp import assemble_shard, exchange_halos, halo_bytes
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         lib, data = _setup()
-        eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
-        full = _text(data)
+        device = torch.device(dev)
+        eng = Engine(lib, Config.load(overrides={"engine.device": dev}), device=device)
+        full = _text(data).to(device)
         gls, gll = K.split_lines(full, len(data))
         L = gls.numel()
         lo, hi, _, _ = shard_bounds(L, world, rank, lib.halo)
@@ -130,7 +144,7 @@ def _worker_p2p(rank, world, port, q):
         end = int(gls[hi]) if hi < L else len(data)
         own_b = data[base:end]
         head, tail = halo_bytes(own_b, lib.halo)
-        own = _text(own_b)
+        own = _text(own_b).to(device)
         left, right = exchange_halos(own, len(own_b), head, tail)
         t, n, ls, ll, hl, hr = assemble_shard(own, len(own_b), left, right)
         sa = ShardedAnalyzer(eng)
@@ -138,9 +152,9 @@ def _worker_p2p(rank, world, port, q):
         for _ in range(STEPS):
             out = sa.step(t, n, ls, ll, hl, hr, topk=5)
             r = out.result
-            gl = (r.ev_line.numpy().astype(np.int64) - hl + out.own_start)
-            res.append((gl, r.ev_pat.numpy(), r.score.numpy(), out.total_lines,
-                        None if out.topk_score is None else out.topk_score.numpy()))
+            gl = (r.ev_line.cpu().numpy().astype(np.int64) - hl + out.own_start)
+            res.append((gl, r.ev_pat.cpu().numpy(), r.score.cpu().numpy(), out.total_lines,
+                        None if out.topk_score is None else out.topk_score.cpu().numpy()))
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -148,11 +162,20 @@ def _worker_p2p(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_p2p_halo_exchange_equals_single(world):
+    _run_p2p(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_p2p_halo_exchange_gpu_ranks(gpu_device):
+    _run_p2p(2, "cuda:0")
+
+
+def _run_p2p(world, dev):
     ref = _reference()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_p2p, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_p2p, args=(r, world, port, q, dev)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))

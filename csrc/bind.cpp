@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include "io/docs.h"
+#include "io/json_in.h"
 #include "io/json_emit.h"
 #include "kernels/lp_api.h"
 #include "regex/jregex.h"
@@ -221,6 +222,23 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   return py::make_tuple(a, l, o, d);
 }
 
+// POST /parse body -> (status, pod_nonnull, pod_name | None, logs_kind, logs bytes | None);
+// status: 0 ok, 1 invalid JSON, 2 JSON but not an object, 3 fall back to json.loads
+static py::tuple parse_pod_request_py(py::bytes body) {
+  char* p = nullptr;
+  Py_ssize_t n = 0;
+  PyBytes_AsStringAndSize(body.ptr(), &p, &n);
+  PodRequest r;
+  int st;
+  {
+    py::gil_scoped_release nogil;
+    st = parse_pod_request(reinterpret_cast<const uint8_t*>(p), (size_t)n, r);
+  }
+  py::object name = r.has_name ? py::object(py::str(r.pod_name)) : py::object(py::none());
+  py::object logs = r.logs_kind == 1 ? py::object(py::bytes(r.logs)) : py::object(py::none());
+  return py::make_tuple(st, r.pod_nonnull, name, r.logs_kind, logs);
+}
+
 PYBIND11_MODULE(_lpnative, m) {
   m.doc() = "log_parser_amd native core: Java-regex compiler, gfx950 kernels, host twins, JSON emitter";
   m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
@@ -230,6 +248,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8);
   m.def("nl_tiles", &nl_tiles);
+  m.def("parse_pod_request", &parse_pod_request_py);
 
   // ---- device launchers
   m.def("pull_dev", [](uint64_t src, uint64_t dst, int64_t n, int grid, uint64_t s) {

@@ -5,7 +5,10 @@
 //    token strings, and checks the prefilter soundness invariant on random subjects: a line the
 //    DFA matches contains at least one of the regex's required literals (ASCII-lowercased);
 //  * runs the parallel request-batch packer/splitter (csrc/io/docs.cpp) with 1 and 8 threads on
-//    random documents and requires identical results (TSan watches the worker threads).
+//    random documents and requires identical results (TSan watches the worker threads);
+//  * fuzzes the /parse body decoder (csrc/io/json_in.cpp, untrusted network input) with random
+//    byte mutations of valid requests: every input must return one of the 4 statuses without an
+//    out-of-bounds access, and the unmutated requests must decode their `logs` exactly.
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -13,6 +16,7 @@
 #include <vector>
 
 #include "io/docs.h"
+#include "io/json_in.h"
 #include "regex/jregex.h"
 
 using namespace lp;
@@ -92,10 +96,43 @@ static void docs_threads(uint32_t seed) {
   std::printf("docs: %zu docs, %zu lines\n", docs.size(), i8.line_start.size());
 }
 
+static void fuzz_json_in(int iters, uint32_t seed) {
+  std::mt19937 rng(seed);
+  const std::string base[] = {
+      "{\"pod\":{\"metadata\":{\"name\":\"p-1\"}},\"logs\":\"line 1\\nERROR x\\u00e9\\\"q\\\"\\r\\n\"}",
+      "{\"logs\":\"a\",\"pod\":{\"spec\":[1,2.5e3,true,null,{\"k\":[]}]},\"events\":[]}",
+      " { \"pod\" : { } , \"logs\" : \"\" } "};
+  const std::string want[] = {"line 1\nERROR x\xc3\xa9\"q\"\r\n", "a", ""};
+  for (int b = 0; b < 3; ++b) {
+    PodRequest r;
+    const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(base[b].data()), base[b].size(), r);
+    CHECK(st == JIN_OK && r.pod_nonnull && r.logs_kind == 1 && r.logs == want[b], "json_in base %d", b);
+  }
+  static const char bytes[] = "{}[]\",:\\un0123456789.eE+-tfalsrn \t\n\x01\xc3\xa9\xff\xed";
+  for (int it = 0; it < iters; ++it) {
+    std::string s = base[rng() % 3];
+    const int muts = 1 + rng() % 4;
+    for (int m = 0; m < muts && !s.empty(); ++m) {
+      const size_t at = rng() % s.size();
+      switch (rng() % 3) {
+        case 0: s[at] = bytes[rng() % (sizeof(bytes) - 1)]; break;
+        case 1: s.erase(at, 1 + rng() % 3); break;
+        default: s.insert(at, 1, bytes[rng() % (sizeof(bytes) - 1)]); break;
+      }
+    }
+    // exact-size heap copy so ASan flags any read past the end
+    std::vector<uint8_t> buf(s.begin(), s.end());
+    PodRequest r;
+    const int st = parse_pod_request(buf.data(), buf.size(), r);
+    CHECK(st >= JIN_OK && st <= JIN_FALLBACK, "json_in status %d", st);
+  }
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 3000;
   fuzz_regex(iters, 12345);
   docs_threads(777);
+  fuzz_json_in(iters * 10, 4242);
   const uint8_t t[] = {'a', 0xE2, 0x80, 0xA8};
   CHECK(final_terminator_len(t, 4) == 3, "U+2028 final terminator");
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);

@@ -28,6 +28,7 @@ SOURCES = [
     ("kernels/lp_post.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),
+    ("io/json_in.cpp", "cpp"),
     ("bind.cpp", "cpp"),
 ]
 

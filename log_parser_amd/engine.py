@@ -395,7 +395,8 @@ class Engine:
         with TR.HostTimer(tm, "line_index"):
             staged = self._stage_docs(logs_list)
             if staged is None:              # lone surrogates: encode in Python
-                staged = self._stage_docs([l.encode("utf-8", errors="surrogatepass") for l in logs_list])
+                staged = self._stage_docs([l if isinstance(l, (bytes, bytearray)) else
+                                           l.encode("utf-8", errors="surrogatepass") for l in logs_list])
         hb, ls_h, ll_h, dl, n = staged
         ndocs = len(logs_list)
         if tm is not None:
@@ -487,9 +488,9 @@ class Engine:
             self.lib._native_pattern_table = pt
         return pt
 
-    def analyze_json(self, logs: str, library_ids: Optional[List] = None) -> bytes:
+    def analyze_json(self, logs, library_ids: Optional[List] = None) -> bytes:
         """Full AnalysisResult as JSON bytes (camelCase result, snake_case matchedPattern)."""
-        data = logs.encode("utf-8", errors="surrogatepass")
+        data = logs if isinstance(logs, (bytes, bytearray)) else logs.encode("utf-8", errors="surrogatepass")
         if len(data) < self.GPU_SPLIT_BYTES:
             return self.analyze_batch_json([logs])[0]
         t0 = time.time()

@@ -7,9 +7,10 @@ Behaviour kept from the reference:
 
 Additions: ``/health``, ``/ready``, Prometheus ``/metrics``,
 ``/admin/frequency`` statistics/reset (the reference has the service methods but no endpoint),
-and a **continuous batcher**: concurrent requests arriving within ``engine.batch.max-wait-ms``
-are packed into one device batch (``Engine.analyze_batch_json``), so 10k concurrent small
-requests cost a few large kernel launches instead of 10k small ones.
+and a **continuous batcher**: requests that queue while a batch runs on the GPU are packed into
+the next device batch (``Engine.analyze_batch_json``), so 10k concurrent small requests cost a few
+large kernel launches instead of 10k small ones, while a request reaching an idle server starts
+at once (``engine.batch.max-wait-ms`` > 0 additionally holds a batch open that long).
 
 Deliberate differences: ``logs`` null -> 400 (the reference NPEs into a 500); a pod without
 ``metadata`` is accepted (logged as ``<unknown>``); per-match logging is DEBUG, not INFO.
@@ -32,6 +33,7 @@ from fastapi.responses import JSONResponse, PlainTextResponse, Response
 from ..engine import Engine
 from ..models.compiled import CompiledLibrary
 from ..models.library import load_pattern_directory
+from ..native import N
 from ..utils.config import Config
 from ..utils.metrics import Metrics
 
@@ -175,21 +177,32 @@ def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None)
         body = await request.body()
         if len(body) > int(config["server.max-body-bytes"]):
             return JSONResponse({"error": "request body too large"}, status_code=413)
-        try:
-            import json
-            data = json.loads(body) if body else None
-        except ValueError:
+        # native single-pass decode (csrc/io/json_in.cpp): validates the JSON and returns the
+        # `logs` string as UTF-8 bytes without building the object tree; unusual bodies
+        # (non-UTF-8 encodings, NaN literals, surrogate escapes) go through json.loads
+        st, pod_ok, name, logs_kind, logs = N.parse_pod_request(body) if body else (1, False, None, 0, None)
+        if st == 3:
+            try:
+                import json
+                data = json.loads(body)
+            except ValueError:
+                data = None
+            st = 0 if isinstance(data, dict) else 1
+            if st == 0:
+                pod_ok = data.get("pod") is not None
+                logs = data.get("logs")
+                logs_kind = 1 if isinstance(logs, str) else (0 if logs is None else 2)
+                pod = data["pod"] if isinstance(data.get("pod"), dict) else {}
+                md = pod.get("metadata")
+                name = md.get("name") if isinstance(md, dict) else None
+                name = name if isinstance(name, str) else None
+        if st != 0 or not pod_ok:
             metrics.observe_request(400, time.perf_counter() - t0, 0)
             return Response(INVALID, status_code=400, media_type="application/json")
-        if not isinstance(data, dict) or data.get("pod") is None:
-            metrics.observe_request(400, time.perf_counter() - t0, 0)
-            return Response(INVALID, status_code=400, media_type="application/json")
-        logs = data.get("logs")
-        if not isinstance(logs, str):
+        if logs_kind != 1:
             metrics.observe_request(400, time.perf_counter() - t0, 0)
             return JSONResponse({"error": "PodFailureData.logs must be a string"}, status_code=400)
-        pod = data["pod"] if isinstance(data["pod"], dict) else {}
-        name = ((pod.get("metadata") or {}).get("name")) or "<unknown>"
+        name = name or "<unknown>"
         log.info("Received analysis request for pod: %s", name)
         fut = _batcher().submit(logs)
         out = await asyncio.wrap_future(fut)

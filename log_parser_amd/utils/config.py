@@ -55,7 +55,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # continuous batching
     "engine.batch.max-requests": (2048, int),
     "engine.batch.max-bytes": (256 << 20, int),
-    "engine.batch.max-wait-ms": (2.0, float),
+    # extra wait for more requests after the first one; 0 = greedy continuous batching (a batch
+    # forms from whatever queued while the previous one ran; an idle server answers at once)
+    "engine.batch.max-wait-ms": (0.0, float),
     # top-k events kept by the distributed reduction (0 = all events)
     "engine.topk": (100, int),
     # persist frequency state (snapshot path, empty = disabled, reference default)

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t* __restrict__ fs, c
 // The 4 context DFAs (~2 KB) are staged in LDS: a DFA walk is a chain of dependent table loads,
 // ~64-cycle LDS hits instead of ~500-cycle L2 trips (a 10k-line request ran 136 us -> see profiles).
 constexpr int FC_MAX_LINES = 4096;
-constexpr int FC_TRANS = 8192;   // uint16 entries
+constexpr int FC_TRANS = 4096;   // uint16 entries (context DFAs need ~900)
 constexpr int FC_ACC = 1024;
 __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ cov, int64_t L, int per_block,
                                                   const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,

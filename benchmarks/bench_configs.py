@@ -197,7 +197,12 @@ def mode_concurrent(args):
     sizes = rng.choice([20, 100, 500, 2000, 10000], size=args.requests, p=[0.3, 0.3, 0.2, 0.15, 0.05])
     pool = {s: [make_log(int(s), trig, seed=int(s) + k, hit_rate=0.01) for k in range(4)] for s in set(sizes.tolist())}
     reqs = [pool[int(s)][i % 4] for i, s in enumerate(sizes)]
-    b = Batcher(eng, int(eng.config["engine.batch.max-requests"]), int(eng.config["engine.batch.max-bytes"]),
+    engines = [eng]
+    ngpu = torch.cuda.device_count() if dev.type == "cuda" else 0
+    for i in range(1, args.engines):     # one engine per GPU; several per GPU on a 1-GPU box
+        d = torch.device("cuda", i % ngpu) if ngpu else dev
+        engines.append(Engine(eng.lib, eng.config, device=d, freq=eng.freq))
+    b = Batcher(engines, int(eng.config["engine.batch.max-requests"]), int(eng.config["engine.batch.max-bytes"]),
                 float(eng.config["engine.batch.max-wait-ms"]), Metrics())
     for f in [b.submit(r) for r in reqs[:64]]:
         f.result()
@@ -219,7 +224,7 @@ def mode_concurrent(args):
     wall = time.perf_counter() - t_start
     b.close()
     lat = np.array(lat)
-    print(json.dumps({"config": f"concurrent-{args.requests}-requests-mixed", "device": str(dev),
+    print(json.dumps({"config": f"concurrent-{args.requests}-requests-mixed", "device": str(dev), "engines": args.engines,
                       "p50_ms": round(float(np.median(lat)) * 1e3, 3), "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 3),
                       "requests_per_s": round(len(reqs) / wall, 1), "lines_per_s": round(float(sizes.sum()) / wall, 1)}))
 
@@ -244,6 +249,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--requests", type=int, default=None)
     ap.add_argument("--chunk-mb", type=int, default=512)
+    ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
     args = ap.parse_args()
     defaults = {"rest": (10_000, 50), "rest_gpu": (10_000, 100), "single": (1_000_000, None), "stream": (1_000_000_000, None),
                 "concurrent": (None, 10_000), "golden": (10_000, None)}

@@ -13,19 +13,23 @@ Here one request (or a batch of requests, or one rank's shard of a huge log) is 
 
 and every stage is a bulk kernel over the whole batch:
 
-  1. k_prefilter   literal bloom/hash filter  -> (regex, line) candidates
-  2. k_verify      byte DFA on unique candidates; k_scan for literal-free regexes
-  3. hits          sorted unique (regex, line) keys -> CSR per regex (shared by primary,
-                   secondary, sequence and context roles)
-  4. events        primary hits x patterns, owned lines only, (line, pattern) order
-  5. frequency     segmented exclusive scan of per-id match counts (+ persistent carry)
-  6. k_score       fused fp64 7-factor score, one lane per event
-  7. summary       severity histogram / highest severity / top-k
+  1. k_prefilter / k_pf_verify   literal bloom + hash filter -> (regex, line) candidates
+  2. post-match pipeline         (csrc/kernels/lp_post.hip) sort + dedupe + DFA verify ->
+                                 CSR per regex (shared by primary, secondary, sequence roles),
+                                 events in (line, pattern) order on owned lines, in-batch
+                                 frequency ranks, context features of window lines only
+  3. k_score                     fused fp64 7-factor score, one lane per event, frequency carry fused
+  4. summary                     severity histogram / highest severity / top-k
+
+``prepare`` (1-2) needs no global information; ``finish`` (3) takes the line count N, the
+frequency carry and the sequence-chain carry, which the data-parallel, streaming and
+multi-engine serving drivers produce in between.
 """
 from __future__ import annotations
 
 import logging
 import os
+import threading
 import time
 import uuid
 import warnings
@@ -133,6 +137,35 @@ def _ro_view(data) -> torch.Tensor:
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")            # "non-writable buffer" -- we only read it
         return torch.from_numpy(np.frombuffer(data, dtype=np.uint8))
+
+
+class FrequencyTurn:
+    """Arrival-order gate for the frequency state when several engines (GPUs) analyse batches
+    concurrently: batch `seq` reads the persistent carry and records its counts only after every
+    earlier batch recorded theirs (penalty before record, ScoringService.java:84-88, in request
+    arrival order). Matching, events and context features run before the gate, concurrently;
+    only the fused score kernel + the counts read-back are serialised."""
+
+    def __init__(self):
+        self._cv = threading.Condition()
+        self._next = 0
+        self._done: set = set()
+
+    def wait(self, seq: int) -> None:
+        with self._cv:
+            while self._next < seq:
+                self._cv.wait()
+
+    def done(self, seq: int) -> None:
+        """Idempotent; may be called out of order (a failed batch releases its slot)."""
+        with self._cv:
+            if seq < self._next:
+                return
+            self._done.add(seq)
+            while self._next in self._done:
+                self._done.discard(self._next)
+                self._next += 1
+            self._cv.notify_all()
 
 
 class Engine:
@@ -378,19 +411,27 @@ class Engine:
     # batches are split on the host while they are being packed (memchr, no extra pass)
     GPU_SPLIT_BYTES = 32 << 20
 
-    def analyze_batch_json(self, logs_list: Sequence[str]) -> List[bytes]:
+    def analyze_batch_json(self, logs_list: Sequence[str], turn: Optional[FrequencyTurn] = None,
+                           seq: int = 0) -> List[bytes]:
         """Continuous-batching entry: many requests -> ONE device batch -> one JSON per request.
 
         Requests become segments of a single line batch (windows never cross a segment, each
         keeps its own N); frequency updates follow the batch (= arrival) order, which is the
-        deterministic version of the reference's concurrent-request interleaving.
+        deterministic version of the reference's concurrent-request interleaving. With ``turn``
+        (several engines serving concurrently) the frequency carry of batch ``seq`` is read and
+        its counts recorded inside the turn; the caller releases the turn on failure.
         """
         t0 = time.time()
         self._batches += 1
         if self.fault_every and self._batches % self.fault_every == 0:
             raise RuntimeError("injected device fault (engine.fault-inject-every)")
         if len(logs_list) == 1 and len(logs_list[0]) >= self.GPU_SPLIT_BYTES:
-            return [self.analyze_json(logs_list[0])]
+            if turn is not None:
+                turn.wait(seq)
+            out = [self.analyze_json(logs_list[0])]
+            if turn is not None:
+                turn.done(seq)
+            return out
         tm = {} if self.profile else None
         with TR.HostTimer(tm, "line_index"):
             staged = self._stage_docs(logs_list)
@@ -402,20 +443,33 @@ class Engine:
         if tm is not None:
             self._start(tm)
         text = self._stage_h2d(n)
-        carry = self.freq.carry(self.lib.freq_ids)
         lo, hi, g0, nn = Segments.doc_arrays(dl)
-        ls, ll, lo, hi, g0, nn, carry = self.upload(
-            [ls_h, ll_h, lo, hi, g0, nn, carry if carry.size else np.zeros(1, np.int64)])
-        segs = Segments(lo, hi, lo, hi, g0, nn)
-        if tm is not None:
-            self._tick(tm, "h2d", 0.0)
         verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
-        res = self.run(text, n, ls, ll, segs, carry, with_factors=verbose, timings=tm)
+        if turn is None:
+            carry = self.freq.carry(self.lib.freq_ids)
+            ls, ll, lo, hi, g0, nn, carry = self.upload(
+                [ls_h, ll_h, lo, hi, g0, nn, carry if carry.size else np.zeros(1, np.int64)])
+            segs = Segments(lo, hi, lo, hi, g0, nn)
+            if tm is not None:
+                self._tick(tm, "h2d", 0.0)
+            res = self.run(text, n, ls, ll, segs, carry, with_factors=verbose, timings=tm)
+            with TR.HostTimer(tm, "d2h"):
+                ev_line, ev_pat, ev_seg, score, counts = self._results_to_host(res)
+            self.commit_frequency(counts)
+        else:
+            ls, ll, lo, hi, g0, nn = self.upload([ls_h, ll_h, lo, hi, g0, nn])
+            segs = Segments(lo, hi, lo, hi, g0, nn)
+            if tm is not None:
+                self._tick(tm, "h2d", 0.0)
+            prep = self.prepare(text, n, ls, ll, segs, timings=tm)
+            turn.wait(seq)                     # earlier batches have recorded their counts
+            res = self.finish(prep, segs, self.freq_carry(), with_factors=verbose)
+            with TR.HostTimer(tm, "d2h"):
+                ev_line, ev_pat, ev_seg, score, counts = self._results_to_host(res)
+            self.commit_frequency(counts)
+            turn.done(seq)
         if verbose:
             self._log_events(res, dl)
-        with TR.HostTimer(tm, "d2h"):
-            ev_line, ev_pat, ev_seg, score, counts = self._results_to_host(res)
-        self.commit_frequency(counts)
         with TR.HostTimer(tm, "json"):
             bounds = np.searchsorted(ev_seg, np.arange(ndocs + 1)).astype(np.int64)
             ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,

@@ -30,7 +30,7 @@ import torch
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, Response
 
-from ..engine import Engine
+from ..engine import Engine, FrequencyTurn
 from ..models.compiled import CompiledLibrary
 from ..models.library import load_pattern_directory
 from ..native import N
@@ -43,35 +43,46 @@ INVALID = b'{"error":"Invalid PodFailureData provided"}'
 
 
 class Batcher:
-    """Packs concurrently submitted requests into one engine batch (one worker thread owns the GPU)."""
+    """Continuous batcher. One worker thread per engine; each engine owns one GPU (or the CPU).
 
-    def __init__(self, engine: Engine, max_requests: int, max_bytes: int, max_wait_ms: float, metrics: Metrics):
-        self.engine = engine
+    With several engines (``engine.serve-devices``) batches are analysed concurrently on all
+    GPUs of the node; every batch gets an arrival sequence number and reads / records the shared
+    frequency state inside a ``FrequencyTurn`` in that order, so results are identical to serving
+    the same batches one after another on one GPU."""
+
+    def __init__(self, engines, max_requests: int, max_bytes: int, max_wait_ms: float, metrics: Metrics):
+        self.engines: List[Engine] = list(engines) if isinstance(engines, (list, tuple)) else [engines]
+        self.engine = self.engines[0]
+        self.turn: Optional[FrequencyTurn] = FrequencyTurn() if len(self.engines) > 1 else None
         self.max_requests = max_requests
         self.max_bytes = max_bytes
         self.max_wait = max_wait_ms / 1000.0
         self.metrics = metrics
-        self.fallback_cpu = bool(engine.config.get("engine.fallback-cpu", True))
+        self.fallback_cpu = bool(self.engine.config.get("engine.fallback-cpu", True))
         self._cpu_engine: Optional[Engine] = None
+        self._cpu_lock = threading.Lock()
         self._q: "deque[tuple]" = deque()
         self._cv = threading.Condition()
         self._stop = False
-        if bool(engine.config.get("server.gc-tuning", True)):
+        self._seq = 0
+        if bool(self.engine.config.get("server.gc-tuning", True)):
             # Every in-flight request holds a Future (+ Condition + RLock); with thousands in flight
             # the cyclic GC's full passes over the (torch-heavy) heap dominate submit cost
             # (12 us -> 2.6 us per request). Freeze the startup heap, collect young objects lazily.
             gc.collect()
             gc.freeze()
             gc.set_threshold(50_000, 50, 100)
-        self._t = threading.Thread(target=self._loop, name="lp-batcher", daemon=True)
-        self._t.start()
+        self._threads = [threading.Thread(target=self._loop, args=(e,), name=f"lp-batcher-{i}", daemon=True)
+                         for i, e in enumerate(self.engines)]
+        for t in self._threads:
+            t.start()
 
-    def submit(self, logs: str) -> Future:
+    def submit(self, logs) -> Future:
         fut: Future = Future()
         with self._cv:
             self._q.append((logs, fut, time.perf_counter()))
-            # wake the worker only when it can act: first request of a batch, or a full batch.
-            # Notifying on every submit makes the worker thread contend for the GIL 10k times.
+            # wake a worker only when it can act: first request of a batch, or a full batch.
+            # Notifying on every submit makes the worker threads contend for the GIL 10k times.
             n = len(self._q)
             if n == 1 or n == self.max_requests:
                 self._cv.notify()
@@ -80,15 +91,16 @@ class Batcher:
     def close(self):
         with self._cv:
             self._stop = True
-            self._cv.notify()
-        self._t.join(timeout=5)
+            self._cv.notify_all()
+        for t in self._threads:
+            t.join(timeout=5)
 
-    def _take(self) -> List[tuple]:
+    def _take(self):
         with self._cv:
             while not self._q and not self._stop:
                 self._cv.wait()
             if self._stop and not self._q:
-                return []
+                return 0, []
             deadline = self._q[0][2] + self.max_wait
             while len(self._q) < self.max_requests and time.perf_counter() < deadline:
                 self._cv.wait(timeout=max(0.0, deadline - time.perf_counter()))
@@ -99,18 +111,26 @@ class Batcher:
                     break
                 batch.append(self._q.popleft())
                 size += len(item[0])
-            return batch
+            seq = self._seq
+            self._seq += 1
+            if self._q:
+                self._cv.notify()          # more queued: let another (idle) worker take it
+            return seq, batch
 
-    def _loop(self):
+    def _loop(self, eng: Engine):
+        if eng.device.type == "cuda":
+            torch.cuda.set_device(eng.device)
+            if len(self.engines) > 1:      # own stream per worker: engines sharing a GPU overlap
+                torch.cuda.set_stream(torch.cuda.Stream(eng.device))
         while True:
-            batch = self._take()
+            seq, batch = self._take()
             if not batch:
                 if self._stop:
                     return
                 continue
             try:
                 t0 = time.perf_counter()
-                outs = self._analyze([b[0] for b in batch])
+                outs = self._analyze(eng, [b[0] for b in batch], seq)
                 self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
                 for (_, fut, _), o in zip(batch, outs):
                     fut.set_result(o)
@@ -119,23 +139,38 @@ class Batcher:
                 for _, fut, _ in batch:
                     if not fut.done():
                         fut.set_exception(e)
+            finally:
+                if self.turn is not None:
+                    self.turn.done(seq)    # no-op after a successful batch; unblocks later ones
 
-    def _analyze(self, logs: List[str]) -> List[bytes]:
+    def _analyze(self, eng: Engine, logs: List[str], seq: int) -> List[bytes]:
         """GPU batch; on a device failure (HIP error, OOM, lost device) serve the batch from the CPU
         backend — same library tables and the same frequency state — for availability only
         (SURVEY §5.3), and report it in /metrics."""
         try:
-            return self.engine.analyze_batch_json(logs)
+            return eng.analyze_batch_json(logs, self.turn, seq)
         except Exception:  # noqa: BLE001
             if not self.fallback_cpu:
                 raise
             log.exception("device batch failed; serving it from the CPU backend")
-            self.metrics.device_failures += 1
-            if self._cpu_engine is None:
-                self._cpu_engine = Engine(self.engine.lib, self.engine.config, device=torch.device("cpu"),
-                                          freq=self.engine.freq)
-                self._cpu_engine.fault_every = 0
-            return self._cpu_engine.analyze_batch_json(logs)
+            with self._cpu_lock:
+                self.metrics.device_failures += 1
+                if self._cpu_engine is None:
+                    self._cpu_engine = Engine(eng.lib, eng.config, device=torch.device("cpu"), freq=eng.freq)
+                    self._cpu_engine.fault_every = 0
+                return self._cpu_engine.analyze_batch_json(logs, self.turn, seq)
+
+
+def serve_devices(config: Config) -> List[torch.device]:
+    """``engine.serve-devices``: "" = the single ``engine.device``; "all" = every visible GPU;
+    or a comma list ("cuda:0,cuda:1")."""
+    spec = str(config.get("engine.serve-devices", "") or "").strip()
+    if not spec:
+        return []
+    if spec == "all":
+        n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+        return [torch.device("cuda", i) for i in range(n)] or [torch.device("cpu")]
+    return [torch.device(x.strip()) for x in spec.split(",") if x.strip()]
 
 
 def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None) -> FastAPI:
@@ -154,7 +189,13 @@ def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None)
 
     def _batcher() -> Batcher:
         if state["batcher"] is None:
-            state["batcher"] = Batcher(_engine(), int(config["engine.batch.max-requests"]),
+            engines = [_engine()]
+            for dev in serve_devices(config):     # data-parallel serving: one engine per GPU
+                if dev != engines[0].device:
+                    engines.append(Engine(engines[0].lib, config, device=dev, freq=engines[0].freq))
+            if len(engines) > 1:
+                log.info("serving on %d engines: %s", len(engines), [str(e.device) for e in engines])
+            state["batcher"] = Batcher(engines, int(config["engine.batch.max-requests"]),
                                        int(config["engine.batch.max-bytes"]), float(config["engine.batch.max-wait-ms"]),
                                        metrics)
         return state["batcher"]

@@ -38,6 +38,8 @@ REFERENCE_KEYS: Dict[str, tuple] = {
 ENGINE_KEYS: Dict[str, tuple] = {
     # "auto" -> cuda if available else cpu. "cuda" fails loudly without the HIP extension.
     "engine.device": ("auto", str),
+    # data-parallel serving: "" = engine.device only, "all" = every visible GPU, or "cuda:0,cuda:1"
+    "engine.serve-devices": ("", str),
     # bytes per streamed H2D chunk for long logs (double-buffered pinned staging)
     "engine.chunk-bytes": (256 << 20, int),
     # capacity hint for candidate (line, regex) pairs per chunk; grown on overflow

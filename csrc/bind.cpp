@@ -209,15 +209,18 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
     py::gil_scoped_release nogil;   // `docs` keeps every buffer alive
     pack_split_docs(src.data(), off.data(), D, P<uint8_t>(dst), nthreads, ix);
   }
-  py::array_t<int64_t> a(ix.line_start.size());
-  py::array_t<int32_t> l(ix.line_len.size());
-  py::array_t<int64_t> o(ix.doc_line_off.size());
+  // hand the native buffers to numpy (capsule owns them): no copy of the line index
+  auto own = [](auto& buf) {
+    using T = std::remove_reference_t<decltype(buf[0])>;
+    const size_t n = buf.size();
+    T* ptr = buf.release();
+    py::capsule cap(ptr, [](void* q) { delete[] static_cast<T*>(q); });
+    return py::array_t<T>({(py::ssize_t)n}, {(py::ssize_t)sizeof(T)}, ptr, cap);
+  };
+  py::array_t<int64_t> a = own(ix.line_start);
+  py::array_t<int32_t> l = own(ix.line_len);
+  py::array_t<int64_t> o = own(ix.doc_line_off);
   py::array_t<int64_t> d(off.size());
-  if (!ix.line_start.empty()) {
-    memcpy(a.mutable_data(), ix.line_start.data(), ix.line_start.size() * 8);
-    memcpy(l.mutable_data(), ix.line_len.data(), ix.line_len.size() * 4);
-  }
-  memcpy(o.mutable_data(), ix.doc_line_off.data(), ix.doc_line_off.size() * 8);
   memcpy(d.mutable_data(), off.data(), off.size() * 8);
   return py::make_tuple(a, l, o, d);
 }
@@ -375,7 +378,11 @@ PYBIND11_MODULE(_lpnative, m) {
 
   // ---- JSON result emitter
   py::class_<PatternTable>(m, "PatternTable")
-      .def(py::init<py::list, py::array_t<int32_t>, py::array_t<int32_t>>());
+      .def(py::init<py::list, py::array_t<int32_t>, py::array_t<int32_t>>())
+      .def("set_severity", &PatternTable::set_severity);
+  m.def("emit_batch_results", &emit_batch_results_py, py::arg("table"), py::arg("buf"), py::arg("line_start"),
+        py::arg("line_len"), py::arg("doc_line_off"), py::arg("ev_line"), py::arg("ev_pat"), py::arg("ev_score"),
+        py::arg("ev_doc_off"), py::arg("processing_ms"), py::arg("meta_tail"), py::arg("nthreads") = 1);
   m.def("emit_events_json", &emit_events_json_py);
   m.def("emit_batch_json", &emit_batch_json_py, py::arg("table"), py::arg("buf"), py::arg("line_start"),
         py::arg("line_len"), py::arg("doc_line_off"), py::arg("ev_line"), py::arg("ev_pat"), py::arg("ev_score"),

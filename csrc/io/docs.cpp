@@ -4,7 +4,44 @@
 #include <cstring>
 #include <thread>
 
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
+
 namespace lp {
+
+// Copy src[0, n) to dst and record the absolute position (base + i) of every '\n', in ONE pass
+// over the bytes: 64-byte blocks are loaded once, stored, and compared with SSE2 into a bit
+// mask whose set bits are the newlines (a memchr call per ~100-byte log line costs more than the
+// bytes themselves: 1.9M calls per 2k-request batch).
+static void copy_scan_nl(const uint8_t* src, uint8_t* dst, int64_t n, int64_t base, std::vector<int64_t>& nl) {
+  int64_t i = 0;
+#if defined(__SSE2__)
+  const __m128i NL = _mm_set1_epi8('\n');
+  for (; i + 64 <= n; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i), a);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    uint64_t m = (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(a, NL)) |
+                 ((uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(b, NL)) << 16) |
+                 ((uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(c, NL)) << 32) |
+                 ((uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(d, NL)) << 48);
+    while (m) {
+      nl.push_back(base + i + __builtin_ctzll(m));
+      m &= m - 1;
+    }
+  }
+#endif
+  for (; i < n; ++i) {
+    dst[i] = src[i];
+    if (src[i] == '\n') nl.push_back(base + i);
+  }
+}
 
 // Work unit: one document, or a ~256 KiB slice of a large one (so a single big request also
 // copies and splits on several threads).
@@ -16,9 +53,11 @@ struct Unit {
 };
 
 template <class F>
-static void parallel_units(std::vector<Unit>& U, int64_t total, int nthreads, F&& fn) {
+static void parallel_units(std::vector<Unit>& U, int64_t total, int nthreads, int64_t per_thread, F&& fn) {
   const int64_t n = (int64_t)U.size();
-  const int T = std::max(1, std::min<int>(nthreads, (int)std::min<int64_t>(n, 1 + total / (512 << 10))));
+  // >= per_thread bytes per thread (4 MB default): below that, spawning threads costs more than
+  // the copy itself
+  const int T = std::max(1, std::min<int>(nthreads, (int)std::min<int64_t>(n, 1 + total / std::max<int64_t>(1, per_thread))));
   if (T == 1) {
     for (int64_t u = 0; u < n; ++u) fn(U[u]);
     return;
@@ -42,7 +81,7 @@ static void parallel_units(std::vector<Unit>& U, int64_t total, int nthreads, F&
 }
 
 void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, uint8_t* dst, int nthreads,
-                     DocBatchIndex& out) {
+                     DocBatchIndex& out, int64_t min_bytes_per_thread) {
   constexpr int64_t SLICE = 256 << 10;
   std::vector<Unit> U;
   U.reserve(D);
@@ -52,27 +91,19 @@ void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, 
     for (int64_t i = 0; i < k; ++i) U.push_back(Unit{d, s0 + (s1 - s0) * i / k, s0 + (s1 - s0) * (i + 1) / k, {}});
   }
   const int64_t total = doc_off[D];
-  // phase 1: copy + newline positions, one pass over the bytes (the slice is hot in cache)
-  parallel_units(U, total, nthreads, [&](Unit& u) {
+  // phase 1: copy + newline positions, one pass over the bytes
+  parallel_units(U, total, nthreads, min_bytes_per_thread, [&](Unit& u) {
     const int64_t s0 = doc_off[u.doc];
-    if (u.b > u.a) memcpy(dst + u.a, src[u.doc] + (u.a - s0), (size_t)(u.b - u.a));
     u.nl.reserve((size_t)((u.b - u.a) / 64 + 4));
-    const uint8_t* p = dst + u.a;
-    const uint8_t* e = dst + u.b;
-    while (p < e) {
-      const void* q = memchr(p, '\n', (size_t)(e - p));
-      if (!q) break;
-      const uint8_t* qq = static_cast<const uint8_t*>(q);
-      u.nl.push_back(qq - dst);
-      p = qq + 1;
-    }
+    copy_scan_nl(reinterpret_cast<const uint8_t*>(src[u.doc]) + (u.a - s0), dst + u.a, u.b - u.a, u.a, u.nl);
   });
   // per document: newline numbering, kept lines (Java split: trailing empty strings dropped; a
   // document without any '\n' is one line, possibly empty)
   auto line_end = [&](int64_t nlpos, int64_t start) {   // '\r' before '\n' excluded
     return (nlpos > start && dst[nlpos - 1] == '\r') ? nlpos - 1 : nlpos;
   };
-  out.doc_line_off.assign(D + 1, 0);
+  out.doc_line_off.alloc(D + 1);
+  out.doc_line_off[0] = 0;
   std::vector<int64_t> kept(D, 0);
   for (size_t i = 0; i < U.size();) {
     const int64_t d = U[i].doc, s0 = doc_off[d], s1 = doc_off[d + 1];
@@ -105,10 +136,10 @@ void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, 
     i = j;
   }
   for (int64_t d = 0; d < D; ++d) out.doc_line_off[d + 1] = out.doc_line_off[d] + kept[d];
-  out.line_start.resize(out.doc_line_off[D]);
-  out.line_len.resize(out.doc_line_off[D]);
+  out.line_start.alloc(out.doc_line_off[D]);
+  out.line_len.alloc(out.doc_line_off[D]);
   // phase 2: line starts / lengths, each unit writes its own newlines' lines
-  parallel_units(U, total, nthreads, [&](Unit& u) {
+  parallel_units(U, total, nthreads, min_bytes_per_thread, [&](Unit& u) {
     const int64_t k = kept[u.doc], base = out.doc_line_off[u.doc];
     int64_t start = u.prev + 1;
     for (size_t w = 0; w < u.nl.size(); ++w) {

@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <charconv>
+#include <random>
+#include <stdexcept>
 #include <thread>
 #include <string>
 #include <vector>
@@ -95,7 +97,132 @@ void emit_events(std::string& o, const uint8_t* b, const int64_t* LS, const int3
   o.push_back(']');
 }
 
+// RFC 4122 version-4 UUID (UUID.randomUUID, AnalysisService.java:117)
+void put_uuid4(std::string& o, std::mt19937_64& rng) {
+  static const char* hex = "0123456789abcdef";
+  uint64_t a = rng(), b = rng();
+  a = (a & 0xFFFFFFFFFFFF0FFFull) | 0x0000000000004000ull;   // version 4
+  b = (b & 0x3FFFFFFFFFFFFFFFull) | 0x8000000000000000ull;   // variant 10
+  char u[36];
+  int k = 0;
+  for (int i = 0; i < 32; ++i) {
+    if (i == 8 || i == 12 || i == 16 || i == 20) u[k++] = '-';
+    const uint64_t w = i < 16 ? a : b;
+    u[k++] = hex[(w >> (60 - 4 * (i & 15))) & 15];
+  }
+  o.append(u, 36);
+}
+
+// summary of events [e0, e1) (AnalysisService.java:188-215): count, severity histogram in
+// first-occurrence order, highest = max rank among known severities, else the first event's
+void put_summary(std::string& o, const int32_t* EP, int64_t e0, int64_t e1, const PatternTable& T) {
+  o.append("\"summary\":{\"significantEvents\":");
+  put_int(o, e1 - e0);
+  if (e1 == e0) {
+    o.append(",\"highestSeverity\":\"NONE\",\"severityDistribution\":{}}");
+    return;
+  }
+  std::vector<std::pair<const std::string*, int64_t>> dist;   // distinct severities, in order
+  std::vector<int32_t> rank;
+  for (int64_t e = e0; e < e1; ++e) {
+    const std::string* s = &T.sev_json[EP[e]];
+    bool found = false;
+    for (auto& kv : dist)
+      if (*kv.first == *s) { ++kv.second; found = true; break; }
+    if (!found) {
+      dist.emplace_back(s, 1);
+      rank.push_back(T.sev_rank[EP[e]]);
+    }
+  }
+  size_t best = 0;
+  int32_t br = -1;
+  for (size_t i = 0; i < dist.size(); ++i)
+    if (rank[i] > br) { br = rank[i]; best = i; }
+  o.append(",\"highestSeverity\":");
+  o.append(br >= 0 ? *dist[best].first : T.sev_json[EP[e0]]);
+  o.append(",\"severityDistribution\":{");
+  for (size_t i = 0; i < dist.size(); ++i) {
+    if (i) o.push_back(',');
+    o.append(*dist[i].first);
+    o.push_back(':');
+    put_int(o, dist[i].second);
+  }
+  o.append("}}");
+}
+
+template <class F>
+void parallel_docs(const int64_t* eo, int64_t D, int nthreads, F&& run) {
+  // documents are independent: split them into ranges of ~equal event counts
+  const int64_t E = eo[D];
+  const int T_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nthreads, D, 1 + (E + D) / 2048}));
+  if (T_ == 1) {
+    run(0, D);
+    return;
+  }
+  std::vector<int64_t> cut(T_ + 1, D);
+  cut[0] = 0;
+  for (int t = 1; t < T_; ++t) cut[t] = std::max(cut[t - 1], D * t / T_);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T_; ++t)
+    if (cut[t + 1] > cut[t]) th.emplace_back(run, cut[t], cut[t + 1]);
+  for (auto& x : th) x.join();
+}
+
 }  // namespace
+
+void PatternTable::set_severity(py::list sev, py::array_t<int32_t> rank) {
+  sev_json.clear();
+  sev_rank.clear();
+  auto R = rank.unchecked<1>();
+  py::ssize_t i = 0;
+  for (auto h : sev) {
+    const std::string s = h.cast<std::string>();
+    std::string j;
+    put_str(j, reinterpret_cast<const uint8_t*>(s.data()), (int64_t)s.size());
+    sev_json.push_back(j);
+    sev_rank.push_back(R(i++));
+  }
+}
+
+py::list emit_batch_results_py(const PatternTable& T, uint64_t buf, py::array_t<int64_t> line_start,
+                               py::array_t<int32_t> line_len, py::array_t<int64_t> doc_line_off,
+                               py::array_t<int32_t> ev_line, py::array_t<int32_t> ev_pat,
+                               py::array_t<double> ev_score, py::array_t<int64_t> ev_doc_off,
+                               int64_t processing_ms, const std::string& meta_tail, int nthreads) {
+  const int64_t D = doc_line_off.shape(0) - 1;
+  if ((int64_t)T.sev_json.size() < (int64_t)T.json.size()) throw std::runtime_error("PatternTable: severities not set");
+  std::vector<std::string> outs(D);
+  {
+    py::gil_scoped_release nogil;
+    const int64_t* dl = doc_line_off.data();
+    const int64_t* eo = ev_doc_off.data();
+    std::random_device rd;
+    const uint64_t seed = ((uint64_t)rd() << 32) ^ rd();
+    parallel_docs(eo, D, nthreads, [&](int64_t a, int64_t z) {
+      std::mt19937_64 rng(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(a + 1)));
+      for (int64_t d = a; d < z; ++d) {
+        std::string& o = outs[d];
+        o.reserve(256 + (size_t)(eo[d + 1] - eo[d]) * 512);
+        o.append("{\"analysisId\":\"");
+        put_uuid4(o, rng);
+        o.append("\",\"metadata\":{\"processingTimeMs\":");
+        put_int(o, processing_ms);
+        o.append(",\"totalLines\":");
+        put_int(o, dl[d + 1] - dl[d]);
+        o.append(meta_tail);
+        o.append("},\"events\":");
+        emit_events(o, reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), dl[d], dl[d + 1],
+                    ev_line.data(), ev_pat.data(), ev_score.data(), eo[d], eo[d + 1], T);
+        o.push_back(',');
+        put_summary(o, ev_pat.data(), eo[d], eo[d + 1], T);
+        o.push_back('}');
+      }
+    });
+  }
+  py::list r;
+  for (auto& s : outs) r.append(py::bytes(s));
+  return r;
+}
 
 PatternTable::PatternTable(py::list pattern_json, py::array_t<int32_t> ctx_before, py::array_t<int32_t> ctx_after) {
   json.reserve(pattern_json.size());

@@ -470,11 +470,6 @@ class Engine:
             turn.done(seq)
         if verbose:
             self._log_events(res, dl)
-        with TR.HostTimer(tm, "json"):
-            bounds = np.searchsorted(ev_seg, np.arange(ndocs + 1)).astype(np.int64)
-            ejs = N.emit_batch_json(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,
-                                    np.ascontiguousarray(dl, np.int64), ev_line, ev_pat, score, bounds,
-                                    self._STAGE_THREADS)
         extra = b""
         if tm is not None:
             import json
@@ -483,9 +478,14 @@ class Engine:
             st["batchRequests"] = ndocs
             log.debug("stage timings (ms): %s", st)
             extra = (',"stageTimingsMs":' + json.dumps(st, separators=(",", ":"))).encode()
-        clk = self._clock()
-        return [self._wrap(ejs[d], ev_pat[bounds[d]:bounds[d + 1]], int(dl[d + 1] - dl[d]), t0, extra, clk)
-                for d in range(ndocs)]
+        now, ts = self._clock()
+        # every response of the batch (uuid, metadata, events with context lines, summary) in one
+        # native call with the GIL released (csrc/io/json_emit.cpp)
+        bounds = np.searchsorted(ev_seg, np.arange(ndocs + 1)).astype(np.int64)
+        tail = f',"analyzedAt":"{ts}","patternsUsed":{self._patterns_used()}'.encode() + extra
+        return N.emit_batch_results(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,
+                                    np.ascontiguousarray(dl, np.int64), ev_line, ev_pat, score, bounds,
+                                    int((now - t0) * 1000), tail, self._STAGE_THREADS)
 
     _STAGE_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8))
 
@@ -539,8 +539,18 @@ class Engine:
         pt = getattr(self.lib, "_native_pattern_table", None)
         if pt is None:
             pt = N.PatternTable(self.lib.pattern_json, self.lib.ctx_before, self.lib.ctx_after)
+            rank = np.array([SEVERITY_ORDER.index(s) if s in SEVERITY_ORDER else -1 for s in self.lib.severity],
+                            np.int32)
+            pt.set_severity(list(self.lib.severity), rank)
             self.lib._native_pattern_table = pt
         return pt
+
+    def _patterns_used(self) -> str:
+        pu = getattr(self, "_patterns_used_json", None)
+        if pu is None:
+            import json
+            pu = self._patterns_used_json = json.dumps(self.lib.library_ids, separators=(",", ":"))
+        return pu
 
     def analyze_json(self, logs, library_ids: Optional[List] = None) -> bytes:
         """Full AnalysisResult as JSON bytes (camelCase result, snake_case matchedPattern)."""
@@ -571,9 +581,7 @@ class Engine:
         """AnalysisResult JSON around the natively emitted events array (AnalysisService.java:115-121).
         ``clock`` = (now, ISO timestamp) shared by every request of a batch (they finish together)."""
         import json
-        pu = getattr(self, "_patterns_used_json", None)
-        if pu is None:
-            pu = self._patterns_used_json = json.dumps(self.lib.library_ids, separators=(",", ":"))
+        pu = self._patterns_used()
         now, ts = clock if clock is not None else self._clock()
         head = (f'{{"analysisId":"{uuid.uuid4()}","metadata":{{"processingTimeMs":{int((now - t0) * 1000)},'
                 f'"totalLines":{total_lines},"analyzedAt":"{ts}","patternsUsed":{pu}').encode() \

@@ -192,7 +192,7 @@ def test_pack_split_docs_sliced_large_documents(seed):
     for _ in range(4):
         parts = []
         size = 0
-        target = rng.randint(300_000, 900_000)
+        target = rng.randint(2_000_000, 4_000_000)   # > 4 MB total per thread: several threads
         while size < target:
             x = rng.choice(["a", "line with words", "\r", "é", ""]) * rng.randint(0, 30) + \
                 rng.choice(["\n", "\r\n", "\n\n\n", "\r\n\r\n"])
@@ -209,3 +209,28 @@ def test_pack_split_docs_sliced_large_documents(seed):
         for d, doc in enumerate(docs):
             got = [raw[a:a + b].decode() for a, b in zip(ls[dl[d]:dl[d + 1]], ll[dl[d]:dl[d + 1]])]
             assert got == golden.split_lines(doc), (nthreads, d)
+
+
+def test_native_batch_results_match_golden_and_uuid4():
+    """emit_batch_results (csrc/io/json_emit.cpp) writes the whole AnalysisResult natively:
+    version-4 UUIDs unique per response, metadata, and the summary of every document equal to the
+    sequential golden model (severity histogram, highest severity incl. unknown severities)."""
+    import json
+    import re
+    from log_parser_amd import golden
+    sets, trig = make_library(30, seed=17)
+    lib = CompiledLibrary(sets, ScoringParams())
+    eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    docs = [make_log(150 + 40 * i, trig, seed=170 + i, hit_rate=0.1 * (i % 3)) for i in range(7)] + ["", "\n\n"]
+    outs = [json.loads(o) for o in eng.analyze_batch_json(docs)]
+    tracker = golden.FrequencyTracker(ScoringParams())
+    ids = set()
+    for d, o in zip(docs, outs):
+        g = golden.analyze(d, sets, ScoringParams(), tracker)
+        assert re.fullmatch(r"[0-9a-f]{8}-[0-9a-f]{4}-4[0-9a-f]{3}-[89ab][0-9a-f]{3}-[0-9a-f]{12}", o["analysisId"])
+        ids.add(o["analysisId"])
+        assert o["summary"] == g["summary"]
+        assert o["metadata"]["totalLines"] == g["metadata"]["totalLines"]
+        assert o["metadata"]["patternsUsed"] == g["metadata"]["patternsUsed"]
+        assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
+    assert len(ids) == len(docs)

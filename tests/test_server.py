@@ -127,7 +127,7 @@ def test_stage_timings_opt_in(tmp_path):
     a = _json.loads(on.analyze_batch_json([logs, logs])[0])
     b = _json.loads(off.analyze_batch_json([logs])[0])
     st = a["metadata"]["stageTimingsMs"]
-    for k in ("line_index", "h2d", "prefilter", "verify_csr", "events_context_freq", "score", "d2h", "json"):
+    for k in ("line_index", "h2d", "prefilter", "verify_csr", "events_context_freq", "score", "d2h"):
         assert k in st and st[k] >= 0.0, (k, st)
     assert st["batchRequests"] == 2
     assert "stageTimingsMs" not in b["metadata"]

@@ -86,7 +86,8 @@ def _rest(args, n_patterns, device, name):
     sk.close()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     srv = subprocess.Popen([sys.executable, "-m", "log_parser_amd.serve", f"-Dpattern.directory={d}",
-                            f"-Dengine.device={device}", "-Dserver.host=127.0.0.1", f"-Dserver.port={port}"],
+                            f"-Dengine.device={device}", "-Dserver.host=127.0.0.1", f"-Dserver.port={port}",
+                            f"-Dserver.http={args.http}"],
                            cwd=root, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     try:
         deadline = time.time() + 240
@@ -130,7 +131,7 @@ def _rest(args, n_patterns, device, name):
     print(json.dumps({"config": name, "p50_ms": round(float(np.median(lat)) * 1e3, 3),
                       "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 3),
                       "lines_per_s": round(10_000 / float(np.median(lat)), 1), "requests": args.requests,
-                      "transport": "uvicorn HTTP/1.1 keep-alive on 127.0.0.1"}))
+                      "transport": f"{args.http} HTTP front end, HTTP/1.1 keep-alive on 127.0.0.1"}))
 
 
 def mode_single(args):
@@ -250,6 +251,7 @@ def main():
     ap.add_argument("--requests", type=int, default=None)
     ap.add_argument("--chunk-mb", type=int, default=512)
     ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
+    ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="rest: HTTP front end")
     args = ap.parse_args()
     defaults = {"rest": (10_000, 50), "rest_gpu": (10_000, 100), "single": (1_000_000, None), "stream": (1_000_000_000, None),
                 "concurrent": (None, 10_000), "golden": (10_000, None)}

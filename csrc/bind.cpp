@@ -10,6 +10,7 @@
 
 #include "io/docs.h"
 #include "io/json_in.h"
+#include "io/http_server.h"
 #include "io/json_emit.h"
 #include "kernels/lp_api.h"
 #include "regex/jregex.h"
@@ -308,6 +309,46 @@ PYBIND11_MODULE(_lpnative, m) {
   // ---- post-match pipeline (lp_post.hip); device calls return the workspace bytes they need and
   // only run when ws_bytes suffices
   m.def("bits_for", &bits_for);
+
+  // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
+  py::class_<HttpServer>(m, "HttpServer")
+      .def(py::init<const std::string&, int, int, int64_t>(), py::arg("host"), py::arg("port"),
+           py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30)
+      .def_property_readonly("port", &HttpServer::port)
+      .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms) {
+        std::vector<HttpRequest> v;
+        {
+          py::gil_scoped_release nogil;
+          v = s.next_requests(max_n, timeout_ms);
+        }
+        py::list out;
+        for (auto& r : v) {
+          if (r.kind == 0)
+            out.append(py::make_tuple(r.id, 0, py::bytes(r.logs), r.pod_name, r.t_arrival));
+          else
+            out.append(py::make_tuple(r.id, 1, r.method, r.path, py::bytes(r.body), r.t_arrival));
+        }
+        return out;
+      }, py::arg("max_n") = 4096, py::arg("timeout_ms") = 100)
+      .def("respond", [](HttpServer& s, uint64_t id, int status, const std::string& ctype, py::bytes body) {
+        char* p = nullptr;
+        Py_ssize_t n = 0;
+        PyBytes_AsStringAndSize(body.ptr(), &p, &n);
+        std::string b(p, (size_t)n);
+        py::gil_scoped_release nogil;
+        s.respond(id, status, ctype, b);
+      })
+      .def("stats", [](HttpServer& s) {
+        py::dict d;
+        d["accepted"] = s.stats.accepted.load();
+        d["requests"] = s.stats.requests.load();
+        d["native_400"] = s.stats.native_400.load();
+        return d;
+      })
+      .def("stop", [](HttpServer& s) {
+        py::gil_scoped_release nogil;
+        s.stop();
+      });
   m.def("post_hits", [](uint64_t cand, int64_t n, int64_t pre_from, int lbits, int rbits, int R, uint64_t text,
                         uint64_t ls, uint64_t ll, py::tuple dfa, py::tuple ev, uint64_t hits, uint64_t hit_line,
                         uint64_t hit_off, uint64_t ev_cnt, uint64_t ev_end, uint64_t counters, uint64_t ws,

@@ -1,0 +1,473 @@
+// Native HTTP/1.1 front end (see http_server.h). Level-triggered epoll, one listener per IO thread
+// (SO_REUSEPORT: the kernel spreads connections), keep-alive, `Expect: 100-continue`, one request
+// in flight per connection (responses therefore stay in request order without pipelining state).
+#include "io/http_server.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+
+#include "io/json_in.h"
+
+namespace lp {
+
+namespace {
+constexpr size_t kMaxHeader = 64 << 10;
+constexpr int kMaxIo = 255;
+const char kInvalid[] = "{\"error\":\"Invalid PodFailureData provided\"}";
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+const char* reason(int s) {
+  switch (s) {
+    case 100: return "Continue";
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 411: return "Length Required";
+    case 413: return "Payload Too Large";
+    case 431: return "Request Header Fields Too Large";
+    case 500: return "Internal Server Error";
+    case 503: return "Service Unavailable";
+    default: return "Status";
+  }
+}
+
+bool ieq(const char* a, size_t n, const char* lit) {
+  const size_t m = strlen(lit);
+  if (n != m) return false;
+  for (size_t i = 0; i < n; ++i)
+    if (tolower((unsigned char)a[i]) != lit[i]) return false;
+  return true;
+}
+
+std::string trim(const char* a, size_t n) {
+  size_t i = 0, j = n;
+  while (i < j && (a[i] == ' ' || a[i] == '\t')) ++i;
+  while (j > i && (a[j - 1] == ' ' || a[j - 1] == '\t')) --j;
+  return std::string(a + i, j - i);
+}
+}  // namespace
+
+struct HttpServer::Conn {
+  int fd = -1;
+  uint64_t id = 0;
+  std::string in, out;
+  size_t out_off = 0;
+  bool busy = false;        // a request is with the Python side
+  bool keep = true;         // keep-alive of the request in flight
+  bool sent_continue = false;
+  bool closing = false;     // close once `out` is flushed
+  bool want_out = false;
+  bool paused = false;      // EPOLLIN off: too much pipelined input while a request is in flight
+  bool dead = false;        // closed; freed at the end of the event-loop iteration
+};
+
+struct HttpServer::Io {
+  int ep = -1, lfd = -1, efd = -1, index = 0;
+  uint64_t next_conn = 1;
+  std::unordered_map<uint64_t, Conn*> conns;
+  std::vector<Conn*> graveyard;   // closed this iteration (callers may still hold the pointer)
+  std::mutex om;
+  struct Out {
+    uint64_t conn;
+    std::string data;
+    bool keep;
+  };
+  std::vector<Out> outbox;
+};
+
+HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body)
+    : host_(host), port_(port), max_body_(max_body) {
+  io_threads = std::max(1, std::min(io_threads, kMaxIo));
+  for (int i = 0; i < io_threads; ++i) {
+    auto io = std::make_unique<Io>();
+    io->index = i;
+    io->lfd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+    if (io->lfd < 0) throw std::runtime_error("socket() failed");
+    int one = 1;
+    setsockopt(io->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    setsockopt(io->lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port_);
+    if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) a.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (bind(io->lfd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0)
+      throw std::runtime_error(std::string("bind() failed: ") + strerror(errno));
+    if (port_ == 0) {  // ephemeral: every further listener binds the port the first one got
+      socklen_t len = sizeof(a);
+      getsockname(io->lfd, reinterpret_cast<sockaddr*>(&a), &len);
+      port_ = ntohs(a.sin_port);
+    }
+    if (listen(io->lfd, 1024) != 0) throw std::runtime_error("listen() failed");
+    io->ep = epoll_create1(EPOLL_CLOEXEC);
+    io->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = 0;  // 0 = listener
+    epoll_ctl(io->ep, EPOLL_CTL_ADD, io->lfd, &ev);
+    ev.data.u64 = 1;  // 1 = wake-up eventfd
+    epoll_ctl(io->ep, EPOLL_CTL_ADD, io->efd, &ev);
+    ios_.push_back(std::move(io));
+  }
+  for (auto& io : ios_) threads_.emplace_back([this, p = io.get()] { io_loop(p); });
+}
+
+HttpServer::~HttpServer() { stop(); }
+
+void HttpServer::stop() {
+  if (stop_.exchange(true)) return;
+  for (auto& io : ios_) {
+    uint64_t one = 1;
+    (void)!write(io->efd, &one, 8);
+  }
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  for (auto& io : ios_) {
+    for (auto& kv : io->conns) {
+      close(kv.second->fd);
+      delete kv.second;
+    }
+    io->conns.clear();
+    close(io->lfd);
+    close(io->efd);
+    close(io->ep);
+  }
+  qcv_.notify_all();
+}
+
+std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(qm_);
+  if (q_.empty())
+    qcv_.wait_for(lk, std::chrono::milliseconds(std::max(0, timeout_ms)), [&] { return !q_.empty() || stop_; });
+  std::vector<HttpRequest> r;
+  while (!q_.empty() && (int)r.size() < max_n) {
+    r.push_back(std::move(q_.front()));
+    q_.pop_front();
+  }
+  return r;
+}
+
+static std::string head(int status, const std::string& ctype, size_t n, bool keep) {
+  std::string h = "HTTP/1.1 " + std::to_string(status) + " " + reason(status) + "\r\nContent-Type: " + ctype +
+                  "\r\nContent-Length: " + std::to_string(n) + "\r\n";
+  if (!keep) h += "Connection: close\r\n";
+  h += "\r\n";
+  return h;
+}
+
+void HttpServer::respond(uint64_t id, int status, const std::string& content_type, const std::string& body) {
+  const int ioi = (int)(id & 0xFF);
+  if (ioi >= (int)ios_.size()) return;
+  Io* io = ios_[ioi].get();
+  const bool keep = (id >> 63) == 0;
+  std::string data = head(status, content_type, body.size(), keep);
+  data += body;
+  {
+    std::lock_guard<std::mutex> lk(io->om);
+    io->outbox.push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep});
+  }
+  uint64_t one = 1;
+  (void)!write(io->efd, &one, 8);
+}
+
+void HttpServer::send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body,
+                          bool keep) {
+  c->out += head(status, ctype, body.size(), keep);
+  c->out += body;
+  if (!keep) c->closing = true;
+  flush(io, c);
+}
+
+void HttpServer::flush(Io* io, Conn* c) {
+  if (c->dead) return;
+  while (c->out_off < c->out.size()) {
+    const ssize_t k = ::send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+    if (k > 0) {
+      c->out_off += (size_t)k;
+      continue;
+    }
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    if (k < 0 && errno == EINTR) continue;
+    close_conn(io, c);
+    return;
+  }
+  if (c->out_off >= c->out.size()) {
+    c->out.clear();
+    c->out_off = 0;
+    if (c->closing) {
+      close_conn(io, c);
+      return;
+    }
+  }
+  const bool want = !c->out.empty();
+  if (want != c->want_out) {
+    c->want_out = want;
+    set_events(io, c);
+  }
+}
+
+void HttpServer::set_events(Io* io, Conn* c) {
+  epoll_event ev{};
+  ev.events = EPOLLRDHUP | (c->paused ? 0 : EPOLLIN) | (c->want_out ? EPOLLOUT : 0);
+  ev.data.u64 = c->id;
+  epoll_ctl(io->ep, EPOLL_CTL_MOD, c->fd, &ev);
+}
+
+void HttpServer::close_conn(Io* io, Conn* c) {
+  if (c->dead) return;
+  c->dead = true;
+  epoll_ctl(io->ep, EPOLL_CTL_DEL, c->fd, nullptr);
+  close(c->fd);
+  io->conns.erase(c->id);
+  io->graveyard.push_back(c);
+}
+
+// Parses one complete request from c->in; false when more bytes are needed or the connection
+// was closed.
+bool HttpServer::parse_one(Io* io, Conn* c) {
+  const size_t he = c->in.find("\r\n\r\n");
+  if (he == std::string::npos) {
+    if (c->in.size() > kMaxHeader) send_now(io, c, 431, "application/json", "{\"error\":\"headers too large\"}", false);
+    return false;
+  }
+  const char* s = c->in.data();
+  const size_t le = c->in.find("\r\n");
+  // request line
+  const char* sp1 = (const char*)memchr(s, ' ', le);
+  const char* sp2 = sp1 ? (const char*)memchr(sp1 + 1, ' ', le - (sp1 + 1 - s)) : nullptr;
+  if (!sp1 || !sp2) {
+    send_now(io, c, 400, "application/json", "{\"error\":\"malformed request line\"}", false);
+    return false;
+  }
+  std::string method(s, sp1 - s), path(sp1 + 1, sp2 - sp1 - 1), version(sp2 + 1, s + le - sp2 - 1);
+  bool keep = version != "HTTP/1.0";
+  int64_t clen = 0;
+  bool has_len = false, chunked = false, expect = false;
+  size_t p = le + 2;
+  while (p < he) {
+    const size_t e = c->in.find("\r\n", p);
+    const char* l = s + p;
+    const size_t n = e - p;
+    const char* colon = (const char*)memchr(l, ':', n);
+    if (colon) {
+      const size_t kn = colon - l;
+      const std::string v = trim(colon + 1, n - kn - 1);
+      if (ieq(l, kn, "content-length")) {
+        has_len = true;
+        clen = 0;
+        for (char ch : v) {
+          if (ch < '0' || ch > '9' || clen > (int64_t(1) << 50)) {
+            clen = -1;
+            break;
+          }
+          clen = clen * 10 + (ch - '0');
+        }
+      } else if (ieq(l, kn, "connection")) {
+        std::string lv;
+        for (char ch : v) lv.push_back((char)tolower((unsigned char)ch));
+        if (lv.find("close") != std::string::npos) keep = false;
+        if (lv.find("keep-alive") != std::string::npos) keep = true;
+      } else if (ieq(l, kn, "transfer-encoding")) {
+        chunked = true;
+      } else if (ieq(l, kn, "expect")) {
+        expect = true;
+      }
+    }
+    p = e + 2;
+  }
+  if (chunked) {
+    send_now(io, c, 411, "application/json", "{\"error\":\"chunked bodies are not supported; send Content-Length\"}",
+             false);
+    return false;
+  }
+  if (clen < 0) {
+    send_now(io, c, 400, "application/json", "{\"error\":\"bad Content-Length\"}", false);
+    return false;
+  }
+  if (clen > max_body_) {
+    send_now(io, c, 413, "application/json", "{\"error\":\"request body too large\"}", false);
+    return false;
+  }
+  const size_t total = he + 4 + (size_t)clen;
+  if (c->in.size() < total) {
+    if (expect && !c->sent_continue) {
+      c->out += "HTTP/1.1 100 Continue\r\n\r\n";
+      c->sent_continue = true;
+      flush(io, c);
+    }
+    return false;
+  }
+  c->sent_continue = false;
+  std::string body = c->in.substr(he + 4, (size_t)clen);
+  c->in.erase(0, total);
+  stats.requests++;
+  const size_t q = path.find('?');
+  const std::string route = q == std::string::npos ? path : path.substr(0, q);
+  if (method == "GET" && route == "/health") {
+    send_now(io, c, 200, "application/json", "{\"status\":\"UP\"}", keep);
+    return !c->closing && !c->dead;
+  }
+  HttpRequest r;
+  r.t_arrival = now_s();
+  if (method == "POST" && route == "/parse") {
+    PodRequest pr;
+    const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(body.data()), body.size(), pr);
+    if (st == JIN_OK && (!pr.pod_nonnull || pr.logs_kind != 1)) {
+      stats.native_400++;
+      if (!pr.pod_nonnull)
+        send_now(io, c, 400, "application/json", kInvalid, keep);
+      else
+        send_now(io, c, 400, "application/json", "{\"error\":\"PodFailureData.logs must be a string\"}", keep);
+      return !c->closing && !c->dead;
+    }
+    if (st == JIN_INVALID || st == JIN_NOT_OBJECT || body.empty()) {
+      stats.native_400++;
+      send_now(io, c, 400, "application/json", kInvalid, keep);
+      return !c->closing && !c->dead;
+    }
+    if (st == JIN_OK) {
+      r.kind = 0;
+      r.logs = std::move(pr.logs);
+      r.pod_name = pr.has_name ? pr.pod_name : std::string();
+    } else {
+      r.kind = 1;  // JIN_FALLBACK: the Python route decodes it with json.loads
+    }
+  } else {
+    r.kind = 1;
+  }
+  r.method = std::move(method);
+  r.path = std::move(path);
+  if (r.kind == 1) r.body = std::move(body);
+  r.id = (c->id << 8) | (uint64_t)io->index | (keep ? 0 : (uint64_t(1) << 63));
+  c->busy = true;
+  c->keep = keep;
+  {
+    std::lock_guard<std::mutex> lk(qm_);
+    q_.push_back(std::move(r));
+  }
+  qcv_.notify_one();
+  return false;
+}
+
+void HttpServer::handle_readable(Io* io, Conn* c) {
+  if (c->dead) return;
+  char buf[65536];
+  for (;;) {
+    const ssize_t k = ::recv(c->fd, buf, sizeof(buf), 0);
+    if (k > 0) {
+      c->in.append(buf, (size_t)k);
+      if ((int64_t)c->in.size() > max_body_ + (int64_t)kMaxHeader + 4) {
+        if (c->busy) {  // stop reading until the in-flight request is answered
+          c->paused = true;
+          set_events(io, c);
+        }
+        break;  // not busy: parse_one answers 413
+      }
+      continue;
+    }
+    if (k == 0) {  // peer closed
+      close_conn(io, c);
+      return;
+    }
+    if (errno == EINTR) continue;
+    if (errno == EAGAIN || errno == EWOULDBLOCK) break;
+    close_conn(io, c);
+    return;
+  }
+  while (!c->dead && !c->busy && !c->closing) {
+    if (!parse_one(io, c)) break;
+  }
+}
+
+void HttpServer::io_loop(Io* io) {
+  epoll_event evs[256];
+  while (!stop_) {
+    const int n = epoll_wait(io->ep, evs, 256, 200);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t tag = evs[i].data.u64;
+      if (tag == 0) {  // accept
+        for (;;) {
+          const int fd = accept4(io->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (fd < 0) break;
+          int one = 1;
+          setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          Conn* c = new Conn();
+          c->fd = fd;
+          c->id = (io->next_conn++) + 1;  // ids 0 / 1 are the listener / eventfd tags
+          io->conns[c->id] = c;
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.u64 = c->id;
+          epoll_ctl(io->ep, EPOLL_CTL_ADD, fd, &ev);
+          stats.accepted++;
+        }
+        continue;
+      }
+      if (tag == 1) {  // responses from Python
+        uint64_t cnt;
+        (void)!read(io->efd, &cnt, 8);
+        std::vector<Io::Out> out;
+        {
+          std::lock_guard<std::mutex> lk(io->om);
+          out.swap(io->outbox);
+        }
+        for (auto& o : out) {
+          auto it = io->conns.find(o.conn);
+          if (it == io->conns.end()) continue;  // client went away
+          Conn* c = it->second;
+          c->busy = false;
+          if (c->paused) {
+            c->paused = false;
+            set_events(io, c);
+          }
+          c->out += o.data;
+          if (!o.keep) c->closing = true;
+          flush(io, c);
+          // next request already buffered on this keep-alive connection
+          while (!c->dead && !c->busy && !c->closing) {
+            if (!parse_one(io, c)) break;
+          }
+        }
+        continue;
+      }
+      auto it = io->conns.find(tag);
+      if (it == io->conns.end()) continue;
+      Conn* c = it->second;
+      if (evs[i].events & EPOLLOUT) {
+        flush(io, c);
+        if (c->dead) continue;
+      }
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+        if (c->busy) {
+          // a request is in flight: keep reading (pipelined bytes wait in `in`), detect hang-up
+          if (evs[i].events & (EPOLLHUP | EPOLLERR)) {
+            close_conn(io, c);
+            continue;
+          }
+        }
+        handle_readable(io, c);
+      }
+    }
+    for (Conn* c : io->graveyard) delete c;
+    io->graveyard.clear();
+  }
+  for (Conn* c : io->graveyard) delete c;
+  io->graveyard.clear();
+}
+
+}  // namespace lp

@@ -1,0 +1,72 @@
+// Native HTTP/1.1 front end of the REST service (reference: Quarkus REST on Vert.x, Parse.java).
+//
+// epoll IO threads (one SO_REUSEPORT listener each) parse requests and decode POST /parse bodies
+// natively (json_in.cpp); decoded requests wait in one queue that the Python side drains in
+// batches with the GIL released (`next_requests`), then answers with `respond`. The analysis
+// engine, batching and every other route stay in Python; the per-request HTTP + JSON work of the
+// hot path does not.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace lp {
+
+struct HttpRequest {
+  uint64_t id = 0;          // reply handle
+  int kind = 0;             // 0 = decoded POST /parse, 1 = other route (raw method/path/body)
+  std::string method, path, body;
+  std::string logs;         // kind 0: UTF-8 log text
+  std::string pod_name;     // kind 0: pod.metadata.name or "" (unknown)
+  double t_arrival = 0;     // monotonic seconds, when the body was complete
+};
+
+struct HttpStats {
+  std::atomic<uint64_t> accepted{0}, requests{0}, bad_requests{0}, native_400{0};
+};
+
+class HttpServer {
+ public:
+  HttpServer(const std::string& host, int port, int io_threads, int64_t max_body);
+  ~HttpServer();
+  int port() const { return port_; }
+  // up to `max_n` pending requests; waits up to `timeout_ms` for the first one
+  std::vector<HttpRequest> next_requests(int max_n, int timeout_ms);
+  // queue the response of request `id` (ignored if its connection is gone)
+  void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
+  void stop();
+  HttpStats stats;
+
+  struct Conn;
+  struct Io;
+
+ private:
+  void io_loop(Io* io);
+  void handle_readable(Io* io, Conn* c);
+  bool parse_one(Io* io, Conn* c);
+  void send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body, bool keep);
+  void flush(Io* io, Conn* c);
+  void set_events(Io* io, Conn* c);
+  void close_conn(Io* io, Conn* c);
+
+  std::string host_;
+  int port_;
+  int64_t max_body_;
+  std::atomic<bool> stop_{false};
+  std::vector<std::unique_ptr<Io>> ios_;
+  std::vector<std::thread> threads_;
+  // pending requests (Python side drains)
+  std::mutex qm_;
+  std::condition_variable qcv_;
+  std::deque<HttpRequest> q_;
+  std::atomic<uint64_t> next_id_{1};
+};
+
+}  // namespace lp

@@ -13,6 +13,10 @@
 
 #include <cstring>
 
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
+
 namespace lp {
 namespace {
 
@@ -60,6 +64,22 @@ bool str(Cur& c, std::string* out) {
   ++c.p;
   for (;;) {
     const uint8_t* run = c.p;
+#if defined(__SSE2__)
+    // 16 bytes per step: '"', '\\', control bytes and bytes >= 0x80 (signed < 0x20) end the run
+    {
+      const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), sp = _mm_set1_epi8(0x20);
+      while (c.e - c.p >= 16) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(c.p));
+        const __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, bs)), _mm_cmplt_epi8(v, sp));
+        const int bits = _mm_movemask_epi8(m);
+        if (bits) {
+          c.p += __builtin_ctz((unsigned)bits);
+          break;
+        }
+        c.p += 16;
+      }
+    }
+#endif
     while (c.p < c.e && *c.p != '"' && *c.p != '\\' && *c.p >= 0x20 && *c.p < 0x80) ++c.p;
     if (out && c.p > run) out->append(reinterpret_cast<const char*>(run), c.p - run);
     if (c.p >= c.e) return false;
@@ -269,6 +289,7 @@ int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out) {
     if (key == "logs") {
       if (cc.p < cc.e && *cc.p == '"') {
         out.logs.clear();
+        out.logs.reserve((size_t)(cc.e - cc.p));   // one allocation for the (large) log text
         out.logs_kind = 1;
         return str(cc, &out.logs);
       }

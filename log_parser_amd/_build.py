@@ -29,6 +29,7 @@ SOURCES = [
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),
     ("io/json_in.cpp", "cpp"),
+    ("io/http_server.cpp", "cpp"),
     ("bind.cpp", "cpp"),
 ]
 

@@ -28,7 +28,7 @@ from typing import List, Optional
 
 import torch
 from fastapi import FastAPI, Request
-from fastapi.responses import JSONResponse, PlainTextResponse, Response
+from fastapi.responses import Response
 
 from ..engine import Engine, FrequencyTurn
 from ..models.compiled import CompiledLibrary
@@ -173,58 +173,78 @@ def serve_devices(config: Config) -> List[torch.device]:
     return [torch.device(x.strip()) for x in spec.split(",") if x.strip()]
 
 
-def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None) -> FastAPI:
-    config = config or Config.load()
-    app = FastAPI(title="log_parser_amd", version="0.1.0")
-    metrics = Metrics()
-    state = {"engine": engine, "batcher": None}
+class Service:
+    """The service logic shared by both HTTP front ends (FastAPI/uvicorn and the native epoll
+    server, ``serve/native_http.py``): library + engines + batcher + metrics, the /parse flow and
+    the health / metrics / admin routes (reference surface: Parse.java; additions SURVEY §5.3-5.5)."""
 
-    def _engine() -> Engine:
-        if state["engine"] is None:
-            sets = load_pattern_directory(config["pattern.directory"])
-            lib = CompiledLibrary(sets, config.scoring, max_dfa_states=int(config["engine.dfa-max-states"]))
-            log.info("compiled library: %s", lib.summary())
-            state["engine"] = Engine(lib, config)
-        return state["engine"]
+    JSON = "application/json"
 
-    def _batcher() -> Batcher:
-        if state["batcher"] is None:
-            engines = [_engine()]
-            for dev in serve_devices(config):     # data-parallel serving: one engine per GPU
-                if dev != engines[0].device:
-                    engines.append(Engine(engines[0].lib, config, device=dev, freq=engines[0].freq))
-            if len(engines) > 1:
-                log.info("serving on %d engines: %s", len(engines), [str(e.device) for e in engines])
-            state["batcher"] = Batcher(engines, int(config["engine.batch.max-requests"]),
-                                       int(config["engine.batch.max-bytes"]), float(config["engine.batch.max-wait-ms"]),
-                                       metrics)
-        return state["batcher"]
+    def __init__(self, config: Optional[Config] = None, engine: Optional[Engine] = None):
+        self.config = config or Config.load()
+        self.metrics = Metrics()
+        self._engine = engine
+        self._batcher: Optional[Batcher] = None
+        self._lock = threading.Lock()
 
-    @app.on_event("startup")
-    def _startup():
-        _batcher()
+    # ---- lifecycle
+    def engine(self) -> Engine:
+        with self._lock:
+            if self._engine is None:
+                cfg = self.config
+                sets = load_pattern_directory(cfg["pattern.directory"])
+                lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]))
+                log.info("compiled library: %s", lib.summary())
+                self._engine = Engine(lib, cfg)
+            return self._engine
 
-    @app.on_event("shutdown")
-    def _shutdown():
-        if state["batcher"] is not None:
-            state["batcher"].close()
-        path = config["engine.frequency.snapshot-path"]
-        if path and state["engine"] is not None:
-            state["engine"].freq.snapshot(path)
+    def batcher(self) -> Batcher:
+        eng = self.engine()
+        with self._lock:
+            if self._batcher is None:
+                cfg = self.config
+                engines = [eng]
+                for dev in serve_devices(cfg):     # data-parallel serving: one engine per GPU
+                    if dev != engines[0].device:
+                        engines.append(Engine(engines[0].lib, cfg, device=dev, freq=engines[0].freq))
+                if len(engines) > 1:
+                    log.info("serving on %d engines: %s", len(engines), [str(e.device) for e in engines])
+                self._batcher = Batcher(engines, int(cfg["engine.batch.max-requests"]),
+                                        int(cfg["engine.batch.max-bytes"]), float(cfg["engine.batch.max-wait-ms"]),
+                                        self.metrics)
+            return self._batcher
 
-    @app.post("/parse")
-    async def parse(request: Request):
-        t0 = time.perf_counter()
-        body = await request.body()
-        if len(body) > int(config["server.max-body-bytes"]):
-            return JSONResponse({"error": "request body too large"}, status_code=413)
-        # native single-pass decode (csrc/io/json_in.cpp): validates the JSON and returns the
-        # `logs` string as UTF-8 bytes without building the object tree; unusual bodies
-        # (non-UTF-8 encodings, NaN literals, surrogate escapes) go through json.loads
+    def close(self):
+        if self._batcher is not None:
+            self._batcher.close()
+        path = self.config["engine.frequency.snapshot-path"]
+        if path and self._engine is not None:
+            self._engine.freq.snapshot(path)
+
+    # ---- POST /parse (Parse.java:41-61)
+    def submit_parse(self, logs, name: str, t0: float) -> Future:
+        """A decoded request: INFO log, batch submission, metrics on completion."""
+        log.info("Received analysis request for pod: %s", name or "<unknown>")
+        fut = self.batcher().submit(logs)
+        n = len(logs)
+
+        def _done(f):
+            if f.exception() is None:
+                self.metrics.observe_request(200, time.perf_counter() - t0, n)
+                log.info("Analysis complete for pod: %s.", name or "<unknown>")
+        fut.add_done_callback(_done)
+        return fut
+
+    def parse_body(self, body: bytes, t0: float):
+        """Raw /parse body -> (status, content type, bytes) or a Future of the JSON bytes. The body
+        is decoded natively (csrc/io/json_in.cpp); unusual bodies (non-UTF-8 encodings, NaN
+        literals, surrogate escapes) go through json.loads."""
+        if len(body) > int(self.config["server.max-body-bytes"]):
+            return 413, self.JSON, b'{"error":"request body too large"}'
         st, pod_ok, name, logs_kind, logs = N.parse_pod_request(body) if body else (1, False, None, 0, None)
         if st == 3:
+            import json
             try:
-                import json
                 data = json.loads(body)
             except ValueError:
                 data = None
@@ -238,60 +258,78 @@ def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None)
                 name = md.get("name") if isinstance(md, dict) else None
                 name = name if isinstance(name, str) else None
         if st != 0 or not pod_ok:
-            metrics.observe_request(400, time.perf_counter() - t0, 0)
-            return Response(INVALID, status_code=400, media_type="application/json")
+            self.metrics.observe_request(400, time.perf_counter() - t0, 0)
+            return 400, self.JSON, INVALID
         if logs_kind != 1:
-            metrics.observe_request(400, time.perf_counter() - t0, 0)
-            return JSONResponse({"error": "PodFailureData.logs must be a string"}, status_code=400)
-        name = name or "<unknown>"
-        log.info("Received analysis request for pod: %s", name)
-        fut = _batcher().submit(logs)
-        out = await asyncio.wrap_future(fut)
-        metrics.observe_request(200, time.perf_counter() - t0, len(logs))
-        log.info("Analysis complete for pod: %s.", name)
-        return Response(out, media_type="application/json")
+            self.metrics.observe_request(400, time.perf_counter() - t0, 0)
+            return 400, self.JSON, b'{"error":"PodFailureData.logs must be a string"}'
+        return self.submit_parse(logs, name, t0)
 
-    @app.get("/health")
-    def health():
-        return {"status": "UP"}
+    # ---- other routes
+    def route(self, method: str, path: str, body: bytes = b""):
+        import json
+        path = path.split("?", 1)[0]
+        j = lambda obj, code=200: (code, self.JSON, json.dumps(obj, separators=(",", ":")).encode())  # noqa: E731
+        if path == "/health" and method == "GET":
+            return j({"status": "UP"})
+        if path == "/ready" and method == "GET":
+            e = self._engine
+            if e is None:
+                return j({"status": "DOWN", "reason": "library not loaded"}, 503)
+            return j({"status": "UP", "device": str(e.device), "library": e.lib.summary()})
+        if path == "/metrics" and method == "GET":
+            if self._engine is not None:
+                self.metrics.set_frequency(self._engine.freq.statistics())
+            return 200, "text/plain; version=0.0.4", self.metrics.render().encode()
+        if path == "/admin/config" and method == "GET":
+            return j(dict(self.config.values))
+        if path == "/admin/frequency":
+            if method == "GET":
+                return j(self.engine().freq.statistics())
+            if method == "DELETE":
+                self.engine().freq.reset_all()
+                return j({"reset": "all"})
+        if path.startswith("/admin/frequency/"):
+            from urllib.parse import unquote
+            pid = unquote(path[len("/admin/frequency/"):])
+            if method == "GET":
+                r = self.engine().freq.get_pattern_frequency(pid)
+                return j(r) if r is not None else j({"error": "unknown pattern id"}, 404)
+            if method == "DELETE":
+                self.engine().freq.reset(pid)
+                return j({"reset": pid})
+        return j({"error": "not found"}, 404)
 
-    @app.get("/ready")
-    def ready():
-        e = state["engine"]
-        if e is None:
-            return JSONResponse({"status": "DOWN", "reason": "library not loaded"}, status_code=503)
-        return {"status": "UP", "device": str(e.device), "library": e.lib.summary()}
 
-    @app.get("/metrics")
-    def prom():
-        e = state["engine"]
-        if e is not None:
-            metrics.set_frequency(e.freq.statistics())
-        return PlainTextResponse(metrics.render(), media_type="text/plain; version=0.0.4")
+def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None,
+               service: Optional[Service] = None) -> FastAPI:
+    """FastAPI front end (uvicorn) over ``Service``; ``server.http=native`` uses the epoll server."""
+    svc = service or Service(config, engine)
+    app = FastAPI(title="log_parser_amd", version="0.1.0")
+    app.state.service = svc
 
-    @app.get("/admin/frequency")
-    def freq_stats():
-        return _engine().freq.statistics()
+    @app.on_event("startup")
+    def _startup():
+        svc.batcher()
 
-    @app.get("/admin/frequency/{pid}")
-    def freq_one(pid: str):
-        r = _engine().freq.get_pattern_frequency(pid)
-        if r is None:
-            return JSONResponse({"error": "unknown pattern id"}, status_code=404)
-        return r
+    @app.on_event("shutdown")
+    def _shutdown():
+        svc.close()
 
-    @app.delete("/admin/frequency/{pid}")
-    def freq_reset(pid: str):
-        _engine().freq.reset(pid)
-        return {"reset": pid}
+    def _resp(r):
+        code, ctype, data = r
+        return Response(data, status_code=code, media_type=ctype)
 
-    @app.delete("/admin/frequency")
-    def freq_reset_all():
-        _engine().freq.reset_all()
-        return {"reset": "all"}
+    @app.post("/parse")
+    async def parse(request: Request):
+        t0 = time.perf_counter()
+        r = svc.parse_body(await request.body(), t0)
+        if isinstance(r, tuple):
+            return _resp(r)
+        return Response(await asyncio.wrap_future(r), media_type="application/json")
 
-    @app.get("/admin/config")
-    def cfg():
-        return dict(config.values)
+    @app.api_route("/{path:path}", methods=["GET", "DELETE"])
+    def other(path: str, request: Request):
+        return _resp(svc.route(request.method, "/" + path))
 
     return app

@@ -1,0 +1,116 @@
+"""Native HTTP/1.1 front end of the REST service (``server.http=native``, the default).
+
+The C++ epoll server (``csrc/io/http_server.cpp``) owns the sockets: it parses requests, answers
+``GET /health`` and malformed ``/parse`` bodies itself (HTTP 400, ``Parse.java:45-49``), and decodes
+valid ``POST /parse`` bodies to UTF-8 log bytes (``csrc/io/json_in.cpp``). One Python pump thread
+drains the decoded requests in bulk with the GIL released and hands them to the continuous
+batcher; responses go back through ``HttpServer.respond`` from the batcher's completion callbacks.
+Every other route (``/ready``, ``/metrics``, ``/admin/*``, the json.loads fallback of exotic
+``/parse`` bodies) is served by the same ``Service`` methods as the FastAPI front end.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Optional
+
+from ..native import N
+from .app import Service
+
+log = logging.getLogger("log_parser_amd.server")
+
+
+class NativeHttpFrontend:
+    def __init__(self, service: Service, host: str = "0.0.0.0", port: int = 8080, io_threads: int = 2):
+        self.svc = service
+        self.svc.batcher()                               # compile the library before accepting
+        self.srv = N.HttpServer(host, port, io_threads, int(service.config["server.max-body-bytes"]))
+        self.port = self.srv.port
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._pump, name="lp-http-pump", daemon=True)
+        self._t.start()
+        log.info("native HTTP front end on %s:%d (%d IO threads)", host, self.port, io_threads)
+
+    def _reply(self, rid: int, r) -> None:
+        code, ctype, data = r
+        self.srv.respond(rid, code, ctype, data)
+
+    def _on_done(self, rid: int):
+        def cb(fut):
+            try:
+                self.srv.respond(rid, 200, "application/json", fut.result())
+            except Exception as e:  # noqa: BLE001 - the batch failed: 500 to this client
+                log.error("request failed: %s", e)
+                self.srv.respond(rid, 500, "application/json", b'{"error":"internal error"}')
+        return cb
+
+    def _pump(self) -> None:
+        b = self.svc.batcher()
+        direct = len(b.engines) == 1 and b.turn is None
+        while not self._stop.is_set():
+            reqs = self.srv.next_requests(b.max_requests, 100)
+            if not reqs:
+                continue
+            batch = []
+            for req in reqs:
+                rid, kind = req[0], req[1]
+                t0 = time.perf_counter()
+                try:
+                    if kind == 0:                            # decoded POST /parse
+                        _, _, logs, name, _ = req
+                        if direct:
+                            log.info("Received analysis request for pod: %s", name or "<unknown>")
+                            batch.append((rid, logs, name, t0))
+                        else:
+                            self.svc.submit_parse(logs, name, t0).add_done_callback(self._on_done(rid))
+                        continue
+                    _, _, method, path, body, _ = req
+                    if path.split("?", 1)[0] == "/parse":
+                        if method != "POST":
+                            self._reply(rid, (405, "application/json", b'{"error":"method not allowed"}'))
+                            continue
+                        r = self.svc.parse_body(body, t0)
+                        if isinstance(r, tuple):
+                            self._reply(rid, r)
+                        else:
+                            r.add_done_callback(self._on_done(rid))
+                        continue
+                    self._reply(rid, self.svc.route(method, path, body))
+                except Exception as e:  # noqa: BLE001
+                    log.exception("request handling failed")
+                    self._reply(rid, (500, "application/json", ('{"error":"%s"}' % type(e).__name__).encode()))
+            if batch:
+                self._run_direct(b, batch)
+
+    def _run_direct(self, b, batch) -> None:
+        """Single engine: the pump thread is the continuous batcher -- everything that queued while
+        the previous batch ran is analysed as one batch, with no further thread hand-off."""
+        t0 = time.perf_counter()
+        try:
+            outs = b._analyze(b.engine, [x[1] for x in batch], 0)
+        except Exception as e:  # noqa: BLE001
+            log.exception("batch failed")
+            for rid, _, _, _ in batch:
+                self.srv.respond(rid, 500, "application/json", ('{"error":"%s"}' % type(e).__name__).encode())
+            return
+        self.svc.metrics.observe_batch(len(batch), time.perf_counter() - t0)
+        for (rid, logs, name, ta), out in zip(batch, outs):
+            self.srv.respond(rid, 200, "application/json", out)
+            self.svc.metrics.observe_request(200, time.perf_counter() - ta, len(logs))
+            log.info("Analysis complete for pod: %s.", name or "<unknown>")
+
+    def close(self) -> None:
+        self._stop.set()
+        self._t.join(timeout=5)
+        self.srv.stop()
+        self.svc.close()
+
+    def serve_forever(self, stop: Optional[threading.Event] = None) -> None:
+        try:
+            while not (stop or self._stop).wait(1.0):
+                pass
+        except KeyboardInterrupt:
+            pass
+        finally:
+            self.close()

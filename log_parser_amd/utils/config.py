@@ -68,6 +68,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.max-body-bytes": (1 << 30, int),
     "server.port": (8080, int),
     "server.host": ("0.0.0.0", str),
+    # HTTP front end: "native" (C++ epoll server, csrc/io/http_server.cpp) or "uvicorn" (FastAPI)
+    "server.http": ("native", str),
+    "server.io-threads": (2, int),
     # freeze the startup heap + raise GC thresholds in the batching server (submit-path latency)
     "server.gc-tuning": (True, bool),
     # reference logs one INFO line per match (AnalysisService.java:96-99); we log it at DEBUG

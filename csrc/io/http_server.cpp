@@ -152,8 +152,11 @@ void HttpServer::stop() {
 
 std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
   std::unique_lock<std::mutex> lk(qm_);
+  // system_clock deadline: pthread_cond_timedwait (steady-clock waits map to pthread_cond_clockwait,
+  // which the ThreadSanitizer runtime of this toolchain does not intercept); a short poll anyway
   if (q_.empty())
-    qcv_.wait_for(lk, std::chrono::milliseconds(std::max(0, timeout_ms)), [&] { return !q_.empty() || stop_; });
+    qcv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms)),
+                    [&] { return !q_.empty() || stop_; });
   std::vector<HttpRequest> r;
   while (!q_.empty() && (int)r.size() < max_n) {
     r.push_back(std::move(q_.front()));

@@ -8,7 +8,10 @@
 //    random documents and requires identical results (TSan watches the worker threads);
 //  * fuzzes the /parse body decoder (csrc/io/json_in.cpp, untrusted network input) with random
 //    byte mutations of valid requests: every input must return one of the 4 statuses without an
-//    out-of-bounds access, and the unmutated requests must decode their `logs` exactly.
+//    out-of-bounds access, and the unmutated requests must decode their `logs` exactly;
+//  * runs the native HTTP front end (csrc/io/http_server.cpp) with 2 IO threads, a responder
+//    thread playing the Python side and 8 client threads on keep-alive connections (TSan watches
+//    the queue / outbox / eventfd hand-offs, ASan the connection lifetime).
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -17,6 +20,14 @@
 
 #include "io/docs.h"
 #include "io/json_in.h"
+#include "io/http_server.h"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+#include <atomic>
+#include <thread>
 #include "regex/jregex.h"
 
 using namespace lp;
@@ -131,11 +142,62 @@ static void fuzz_json_in(int iters, uint32_t seed) {
   }
 }
 
+static void http_selftest(int rounds) {
+  HttpServer srv("127.0.0.1", 0, 2, 1 << 20);
+  std::atomic<bool> done{false};
+  std::atomic<int> served{0};
+  std::thread responder([&] {
+    while (!done) {
+      for (auto& r : srv.next_requests(64, 20)) {
+        const std::string body = r.kind == 0 ? "{\"n\":" + std::to_string(r.logs.size()) + "}" : "{}";
+        srv.respond(r.id, 200, "application/json", body);
+        ++served;
+      }
+    }
+  });
+  std::atomic<int> ok{0};
+  std::vector<std::thread> clients;
+  for (int t = 0; t < 8; ++t)
+    clients.emplace_back([&, t] {
+      const int fd = socket(AF_INET, SOCK_STREAM, 0);
+      sockaddr_in a{};
+      a.sin_family = AF_INET;
+      a.sin_port = htons((uint16_t)srv.port());
+      inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+      if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) return;
+      for (int i = 0; i < rounds; ++i) {
+        const std::string logs(100 + 37 * ((t + i) % 11), 'x');
+        const std::string body = "{\"pod\":{},\"logs\":\"" + logs + "\"}";
+        const std::string req = (i % 5 == 4) ? std::string("GET /health HTTP/1.1\r\n\r\n")
+                                             : "POST /parse HTTP/1.1\r\nContent-Length: " +
+                                                   std::to_string(body.size()) + "\r\n\r\n" + body;
+        if (send(fd, req.data(), req.size(), 0) != (ssize_t)req.size()) break;
+        std::string resp;
+        char b[4096];
+        while (resp.find("\r\n\r\n") == std::string::npos || resp.back() != '}') {
+          const ssize_t k = recv(fd, b, sizeof(b), 0);
+          if (k <= 0) break;
+          resp.append(b, (size_t)k);
+        }
+        const std::string want = (i % 5 == 4) ? "{\"status\":\"UP\"}" : "{\"n\":" + std::to_string(logs.size()) + "}";
+        if (resp.rfind(want) != std::string::npos) ++ok;
+      }
+      close(fd);
+    });
+  for (auto& c : clients) c.join();
+  done = true;
+  responder.join();
+  srv.stop();
+  CHECK(ok == 8 * rounds, "http: %d of %d responses", ok.load(), 8 * rounds);
+  std::printf("http: %d requests over 8 keep-alive connections\n", ok.load());
+}
+
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 3000;
   fuzz_regex(iters, 12345);
   docs_threads(777);
   fuzz_json_in(iters * 10, 4242);
+  http_selftest(iters / 20 + 10);
   const uint8_t t[] = {'a', 0xE2, 0x80, 0xA8};
   CHECK(final_terminator_len(t, 4) == 3, "U+2028 final terminator");
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);

@@ -315,7 +315,9 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
 // probe the (small) hash table together, then the bucket's literals are split across the lanes --
 // a hit's cost is ~4 dependent memory round trips instead of ~3 per literal in the bucket, which
 // decides the latency of small requests (shared grams give buckets of up to ~70 literals).
-constexpr int PV_LANES = 16;
+// LANES per gram hit: 16 for small inputs (latency: a 67-literal bucket is 5 rounds), 4 for large
+// ones (throughput: the typical bucket holds ~3 literals, so 16 lanes would idle 13 of them).
+template <int PV_LANES>
 __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ ghits, int64_t n,
                                                    const unsigned long long* __restrict__ dn,
                                                    const uint8_t* __restrict__ text, int64_t nbytes, PfTables T,
@@ -542,10 +544,15 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn, int max_grid) {
   if (n <= 0) return;
   // with a device-side count the grid is sized for the buffer but capped (grid-stride loop)
-  const int64_t need = (n + 256 / PV_LANES - 1) / (256 / PV_LANES);   // blocks for one pass over n hits
+  const int lanes = nbytes >= (int64_t(64) << 20) ? 4 : 16;
+  const int64_t need = (n + 256 / lanes - 1) / (256 / lanes);   // blocks for one pass over n hits
   const int g = dn ? (int)std::min<int64_t>(need, std::max(1, max_grid)) : (int)std::max<int64_t>(1, need);
-  hipLaunchKernelGGL(k_pf_verify, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
-                     line_start, nlines, blk_line, cand, cap, count);
+  if (lanes == 4)
+    hipLaunchKernelGGL(k_pf_verify<4>, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
+                       line_start, nlines, blk_line, cand, cap, count);
+  else
+    hipLaunchKernelGGL(k_pf_verify<16>, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
+                       line_start, nlines, blk_line, cand, cap, count);
   LP_CHECK(hipGetLastError());
 }
 

@@ -312,8 +312,8 @@ PYBIND11_MODULE(_lpnative, m) {
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
   py::class_<HttpServer>(m, "HttpServer")
-      .def(py::init<const std::string&, int, int, int64_t>(), py::arg("host"), py::arg("port"),
-           py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30)
+      .def(py::init<const std::string&, int, int, int64_t, double>(), py::arg("host"), py::arg("port"),
+           py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30, py::arg("idle_timeout_s") = 60.0)
       .def_property_readonly("port", &HttpServer::port)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms) {
         std::vector<HttpRequest> v;

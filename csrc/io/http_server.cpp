@@ -75,6 +75,7 @@ struct HttpServer::Conn {
   bool want_out = false;
   bool paused = false;      // EPOLLIN off: too much pipelined input while a request is in flight
   bool dead = false;        // closed; freed at the end of the event-loop iteration
+  double last = 0;          // last read / write activity (idle-timeout sweep)
 };
 
 struct HttpServer::Io {
@@ -82,6 +83,7 @@ struct HttpServer::Io {
   uint64_t next_conn = 1;
   std::unordered_map<uint64_t, Conn*> conns;
   std::vector<Conn*> graveyard;   // closed this iteration (callers may still hold the pointer)
+  double last_sweep = 0;
   std::mutex om;
   struct Out {
     uint64_t conn;
@@ -91,8 +93,8 @@ struct HttpServer::Io {
   std::vector<Out> outbox;
 };
 
-HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body)
-    : host_(host), port_(port), max_body_(max_body) {
+HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s)
+    : host_(host), port_(port), max_body_(max_body), idle_timeout_s_(idle_timeout_s) {
   io_threads = std::max(1, std::min(io_threads, kMaxIo));
   for (int i = 0; i < io_threads; ++i) {
     auto io = std::make_unique<Io>();
@@ -373,6 +375,7 @@ void HttpServer::handle_readable(Io* io, Conn* c) {
   for (;;) {
     const ssize_t k = ::recv(c->fd, buf, sizeof(buf), 0);
     if (k > 0) {
+      c->last = now_s();
       c->in.append(buf, (size_t)k);
       if ((int64_t)c->in.size() > max_body_ + (int64_t)kMaxHeader + 4) {
         if (c->busy) {  // stop reading until the in-flight request is answered
@@ -411,6 +414,7 @@ void HttpServer::io_loop(Io* io) {
           setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
           Conn* c = new Conn();
           c->fd = fd;
+          c->last = now_s();
           c->id = (io->next_conn++) + 1;  // ids 0 / 1 are the listener / eventfd tags
           io->conns[c->id] = c;
           epoll_event ev{};
@@ -439,6 +443,7 @@ void HttpServer::io_loop(Io* io) {
             set_events(io, c);
           }
           c->out += o.data;
+          c->last = now_s();
           if (!o.keep) c->closing = true;
           flush(io, c);
           // next request already buffered on this keep-alive connection
@@ -465,6 +470,16 @@ void HttpServer::io_loop(Io* io) {
         }
         handle_readable(io, c);
       }
+    }
+    // idle sweep (slow / stalled clients): a connection without a request in flight and without
+    // traffic for idle_timeout_s is closed
+    const double t = now_s();
+    if (t - io->last_sweep > 1.0) {
+      io->last_sweep = t;
+      std::vector<Conn*> idle;
+      for (auto& kv : io->conns)
+        if (!kv.second->busy && t - kv.second->last > idle_timeout_s_) idle.push_back(kv.second);
+      for (Conn* c : idle) close_conn(io, c);
     }
     for (Conn* c : io->graveyard) delete c;
     io->graveyard.clear();

@@ -34,7 +34,7 @@ struct HttpStats {
 
 class HttpServer {
  public:
-  HttpServer(const std::string& host, int port, int io_threads, int64_t max_body);
+  HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s = 60.0);
   ~HttpServer();
   int port() const { return port_; }
   // up to `max_n` pending requests; waits up to `timeout_ms` for the first one
@@ -59,6 +59,7 @@ class HttpServer {
   std::string host_;
   int port_;
   int64_t max_body_;
+  double idle_timeout_s_;
   std::atomic<bool> stop_{false};
   std::vector<std::unique_ptr<Io>> ios_;
   std::vector<std::thread> threads_;

@@ -25,7 +25,8 @@ class NativeHttpFrontend:
     def __init__(self, service: Service, host: str = "0.0.0.0", port: int = 8080, io_threads: int = 2):
         self.svc = service
         self.svc.batcher()                               # compile the library before accepting
-        self.srv = N.HttpServer(host, port, io_threads, int(service.config["server.max-body-bytes"]))
+        self.srv = N.HttpServer(host, port, io_threads, int(service.config["server.max-body-bytes"]),
+                                float(service.config["server.idle-timeout-s"]))
         self.port = self.srv.port
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._pump, name="lp-http-pump", daemon=True)

@@ -71,6 +71,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # HTTP front end: "native" (C++ epoll server, csrc/io/http_server.cpp) or "uvicorn" (FastAPI)
     "server.http": ("native", str),
     "server.io-threads": (2, int),
+    # native front end: close keep-alive connections idle this long (no request in flight)
+    "server.idle-timeout-s": (60.0, float),
     # freeze the startup heap + raise GC thresholds in the batching server (submit-path latency)
     "server.gc-tuning": (True, bool),
     # reference logs one INFO line per match (AnalysisService.java:96-99); we log it at DEBUG

@@ -143,3 +143,19 @@ def test_concurrent_clients(server):
     for t in th:
         t.join(timeout=300)
     assert not errs, errs[:3]
+
+
+def test_idle_connections_are_closed():
+    sets, _ = make_library(5, seed=29)
+    lib = CompiledLibrary(sets, ScoringParams())
+    cfg = Config.load(overrides={"engine.device": "cpu", "server.idle-timeout-s": 0.5})
+    fe = NativeHttpFrontend(Service(cfg, Engine(lib, cfg, device=torch.device("cpu"))), "127.0.0.1", 0, 1)
+    try:
+        s = socket.create_connection(("127.0.0.1", fe.port), timeout=10)
+        s.sendall(b"GET /health HTTP/1.1\r\n\r\n")
+        assert b"200 OK" in s.recv(4096)
+        s.settimeout(10)
+        assert s.recv(4096) == b""                        # closed by the idle sweep (~0.5-1.5 s)
+        s.close()
+    finally:
+        fe.close()

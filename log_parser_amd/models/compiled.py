@@ -86,14 +86,19 @@ def _u32(x):
     return x & 0xFFFFFFFF
 
 
+def bloom_hash(key, g):
+    """Blocked bloom filter (csrc/kernels/lp_core.h): one 32-bit multiply per gram key."""
+    return _u32((key ^ _u32(g * 0x9E3779B9)) * 0x85EBCA6B)
+
+
 def bloom_word(key, g, bits):
-    """Blocked bloom filter (csrc/kernels/lp_core.h): word index for a gram key."""
-    return _u32((key ^ _u32(g * 0x9E3779B9)) * 0x85EBCA6B) >> (32 - (bits - 5))
+    return bloom_hash(key, g) >> (32 - (bits - 5))
 
 
 def bloom_bits2(key, g):
-    h = _u32((key + _u32(g * 0x27D4EB2F)) * 0xC2B2AE35)
-    return (1 << (h >> 27)) | (1 << ((h >> 22) & 31))
+    p = bloom_hash(key, g)
+    q = p ^ (p >> 15)
+    return (1 << (q & 31)) | (1 << ((q >> 5) & 31))
 
 
 def ht_hash(key, g):

@@ -127,3 +127,42 @@ def test_sharded_single_rank_equals_engine(gpu_device):
     torch.testing.assert_close(out.result.score, ref.score, rtol=0, atol=0)
     top = torch.topk(ref.score, 10).values
     torch.testing.assert_close(out.topk_score, top)
+
+
+def _strip(o):
+    o = dict(o)
+    o.pop("analysisId")
+    o["metadata"] = {k: v for k, v in o["metadata"].items() if k not in ("processingTimeMs", "analyzedAt")}
+    return o
+
+
+def test_batch_edge_cases_gpu_equal_cpu_and_golden(gpu_device):
+    """One device batch of awkward documents (empty, newline-only, CRLF, multi-byte UTF-8, a
+    200 KB line, event windows at document edges) with the shipped example pattern library:
+    GPU responses == CPU-backend responses == golden model."""
+    import json
+    import os
+    from log_parser_amd.models.library import load_pattern_directory
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sets = load_pattern_directory(os.path.join(root, "patterns", "examples"))
+    p = ScoringParams()
+    lib = CompiledLibrary(sets, p)
+    oom = "java.lang.OutOfMemoryError: Java heap space"
+    docs = ["", "\n", "\n\n\r\n", oom, oom + "\r\n", "é" * 1000 + " " + oom + "\n\tat com.x.Y(Z.java:1)\n",
+            ("INFO ok\r\n" * 50) + oom + "\r\n" + ("WARN later\r\n" * 3),
+            "x" * 200_000 + " OutOfMemoryError\n" + "ERROR Exception in thread main\n" * 5,
+            "\n".join(["CrashLoopBackOff", "Back-off restarting failed container", "OOMKilled"] * 30)]
+    outs = {}
+    for dev in (gpu_device, torch.device("cpu")):
+        eng = _eng(lib, dev)
+        outs["gpu" if dev is gpu_device else "cpu"] = [_strip(json.loads(o)) for o in eng.analyze_batch_json(docs)]
+    assert outs["gpu"] == outs["cpu"]
+    tracker = golden.FrequencyTracker(p)
+    for d, o in zip(docs, outs["gpu"]):
+        g = golden.analyze(d, sets, p, tracker)
+        assert o["summary"] == g["summary"]
+        assert [(e["lineNumber"], e["matchedPattern"]["id"], e["context"]) for e in o["events"]] == \
+               [(e["lineNumber"], e["matchedPattern"]["id"], e["context"]) for e in g["events"]]
+        for a, b in zip(o["events"], g["events"]):
+            assert math.isclose(a["score"], b["score"], rel_tol=1e-12)
+    assert sum(len(o["events"]) for o in outs["gpu"]) > 10

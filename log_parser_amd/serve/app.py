@@ -130,7 +130,7 @@ class Batcher:
                 continue
             try:
                 t0 = time.perf_counter()
-                outs = self._analyze(eng, [b[0] for b in batch], seq)
+                outs = self.analyze(eng, [b[0] for b in batch], seq)
                 self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
                 for (_, fut, _), o in zip(batch, outs):
                     fut.set_result(o)
@@ -143,7 +143,7 @@ class Batcher:
                 if self.turn is not None:
                     self.turn.done(seq)    # no-op after a successful batch; unblocks later ones
 
-    def _analyze(self, eng: Engine, logs: List[str], seq: int) -> List[bytes]:
+    def analyze(self, eng: Engine, logs: List[str], seq: int) -> List[bytes]:
         """GPU batch; on a device failure (HIP error, OOM, lost device) serve the batch from the CPU
         backend — same library tables and the same frequency state — for availability only
         (SURVEY §5.3), and report it in /metrics."""
@@ -235,10 +235,10 @@ class Service:
         fut.add_done_callback(_done)
         return fut
 
-    def parse_body(self, body: bytes, t0: float):
-        """Raw /parse body -> (status, content type, bytes) or a Future of the JSON bytes. The body
-        is decoded natively (csrc/io/json_in.cpp); unusual bodies (non-UTF-8 encodings, NaN
-        literals, surrogate escapes) go through json.loads."""
+    def decode_body(self, body: bytes, t0: float):
+        """Raw /parse body -> (logs, pod name) or an immediate (status, content type, bytes) error.
+        Decoded natively (csrc/io/json_in.cpp); unusual bodies (non-UTF-8 encodings, NaN literals,
+        surrogate escapes) go through json.loads."""
         if len(body) > int(self.config["server.max-body-bytes"]):
             return 413, self.JSON, b'{"error":"request body too large"}'
         st, pod_ok, name, logs_kind, logs = N.parse_pod_request(body) if body else (1, False, None, 0, None)
@@ -263,7 +263,14 @@ class Service:
         if logs_kind != 1:
             self.metrics.observe_request(400, time.perf_counter() - t0, 0)
             return 400, self.JSON, b'{"error":"PodFailureData.logs must be a string"}'
-        return self.submit_parse(logs, name, t0)
+        return logs, name
+
+    def parse_body(self, body: bytes, t0: float):
+        """Raw /parse body -> (status, content type, bytes) or a Future of the JSON bytes."""
+        r = self.decode_body(body, t0)
+        if len(r) == 3:
+            return r
+        return self.submit_parse(r[0], r[1], t0)
 
     # ---- other routes
     def route(self, method: str, path: str, body: bytes = b""):

@@ -71,11 +71,14 @@ class NativeHttpFrontend:
                         if method != "POST":
                             self._reply(rid, (405, "application/json", b'{"error":"method not allowed"}'))
                             continue
-                        r = self.svc.parse_body(body, t0)
-                        if isinstance(r, tuple):
+                        r = self.svc.decode_body(body, t0)       # json.loads fallback bodies
+                        if len(r) == 3:
                             self._reply(rid, r)
+                        elif direct:        # the engine is owned by this thread: same batch path
+                            log.info("Received analysis request for pod: %s", r[1] or "<unknown>")
+                            batch.append((rid, r[0], r[1], t0))
                         else:
-                            r.add_done_callback(self._on_done(rid))
+                            self.svc.submit_parse(r[0], r[1], t0).add_done_callback(self._on_done(rid))
                         continue
                     self._reply(rid, self.svc.route(method, path, body))
                 except Exception as e:  # noqa: BLE001
@@ -86,10 +89,12 @@ class NativeHttpFrontend:
 
     def _run_direct(self, b, batch) -> None:
         """Single engine: the pump thread is the continuous batcher -- everything that queued while
-        the previous batch ran is analysed as one batch, with no further thread hand-off."""
+        the previous batch ran is analysed as one batch, with no further thread hand-off. The
+        batcher's own worker never sees a request in this mode (every /parse, including the
+        json.loads-fallback bodies, comes through here), so the engine has one owner thread."""
         t0 = time.perf_counter()
         try:
-            outs = b._analyze(b.engine, [x[1] for x in batch], 0)
+            outs = b.analyze(b.engine, [x[1] for x in batch], 0)
         except Exception as e:  # noqa: BLE001
             log.exception("batch failed")
             for rid, _, _, _ in batch:

@@ -205,7 +205,7 @@ def mode_concurrent(args):
         engines.append(Engine(eng.lib, eng.config, device=d, freq=eng.freq))
     b = Batcher(engines, int(eng.config["engine.batch.max-requests"]), int(eng.config["engine.batch.max-bytes"]),
                 float(eng.config["engine.batch.max-wait-ms"]), Metrics())
-    for f in [b.submit(r) for r in reqs[:64]]:
+    for f in [b.submit(r) for r in reqs]:     # warm server: one untimed burst (staging buffers grown)
         f.result()
     lat = [0.0] * len(reqs)
     done = threading.Semaphore(0)
@@ -216,6 +216,8 @@ def mode_concurrent(args):
             done.release()
         return _f
 
+    if args.timeline and b.pipe is not None:
+        b.pipe.timeline = []
     t_start = time.perf_counter()
     for i, r in enumerate(reqs):              # all requests in flight at once (10k concurrent)
         t0 = time.perf_counter()
@@ -224,6 +226,9 @@ def mode_concurrent(args):
         done.acquire()
     wall = time.perf_counter() - t_start
     b.close()
+    if args.timeline and b.pipe is not None:
+        for st, n, a, z in b.pipe.timeline:
+            print(f"{st:9s} n={n:5d} {1e3 * (a - t_start):8.2f} -> {1e3 * (z - t_start):8.2f} ms", file=sys.stderr)
     lat = np.array(lat)
     print(json.dumps({"config": f"concurrent-{args.requests}-requests-mixed", "device": str(dev), "engines": args.engines,
                       "p50_ms": round(float(np.median(lat)) * 1e3, 3), "p99_ms": round(float(np.percentile(lat, 99)) * 1e3, 3),
@@ -250,6 +255,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--requests", type=int, default=None)
     ap.add_argument("--chunk-mb", type=int, default=512)
+    ap.add_argument("--timeline", action="store_true", help="concurrent: print the pipeline stage timeline")
     ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="rest: HTTP front end")
     args = ap.parse_args()

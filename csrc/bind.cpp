@@ -179,8 +179,10 @@ static py::tuple split_docs(uint64_t buf, py::array_t<int64_t> doc_off) {
 // Pack request bodies (str via their cached UTF-8 buffer -- no copy for ASCII -- or bytes) into
 // dst and split them. Returns None if a str is not UTF-8 encodable (lone surrogates: the caller
 // falls back to str.encode(surrogatepass)), the needed byte count (int) if it exceeds cap, or
-// (line_start, line_len, doc_line_off, doc_off).
-static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, int nthreads) {
+// (line_start, line_len, doc_line_off, doc_off); with an index buffer `idx` (int64[idx_cap] starts
+// then int32[idx_cap] lengths) that holds every line: (L, None, doc_line_off, doc_off).
+static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, int nthreads, uint64_t idx,
+                                     int64_t idx_cap) {
   const int64_t D = (int64_t)docs.size();
   std::vector<const char*> src(D);
   std::vector<int64_t> off(D + 1, 0);
@@ -206,6 +208,11 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   }
   if (off[D] > cap) return py::int_(off[D]);
   DocBatchIndex ix;
+  if (idx && idx_cap > 0) {          // line_start int64[idx_cap] then line_len int32[idx_cap]
+    ix.ext_start = P<int64_t>(idx);
+    ix.ext_len = reinterpret_cast<int32_t*>(P<int64_t>(idx) + idx_cap);
+    ix.ext_cap = idx_cap;
+  }
   {
     py::gil_scoped_release nogil;   // `docs` keeps every buffer alive
     pack_split_docs(src.data(), off.data(), D, P<uint8_t>(dst), nthreads, ix);
@@ -218,11 +225,13 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
     py::capsule cap(ptr, [](void* q) { delete[] static_cast<T*>(q); });
     return py::array_t<T>({(py::ssize_t)n}, {(py::ssize_t)sizeof(T)}, ptr, cap);
   };
-  py::array_t<int64_t> a = own(ix.line_start);
-  py::array_t<int32_t> l = own(ix.line_len);
+  const int64_t L = ix.doc_line_off[D];
   py::array_t<int64_t> o = own(ix.doc_line_off);
   py::array_t<int64_t> d(off.size());
   memcpy(d.mutable_data(), off.data(), off.size() * 8);
+  if (ix.external) return py::make_tuple(py::int_(L), py::none(), o, d);   // index is in `idx`
+  py::array_t<int64_t> a = own(ix.line_start);
+  py::array_t<int32_t> l = own(ix.line_len);
   return py::make_tuple(a, l, o, d);
 }
 
@@ -250,7 +259,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("split_docs", &split_docs);
   m.def("set_host_threads", &set_host_threads);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
-        py::arg("nthreads") = 8);
+        py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("nl_tiles", &nl_tiles);
   m.def("parse_pod_request", &parse_pod_request_py);
 
@@ -315,6 +324,7 @@ PYBIND11_MODULE(_lpnative, m) {
       .def(py::init<const std::string&, int, int, int64_t, double>(), py::arg("host"), py::arg("port"),
            py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30, py::arg("idle_timeout_s") = 60.0)
       .def_property_readonly("port", &HttpServer::port)
+      .def("pending", &HttpServer::pending)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms) {
         std::vector<HttpRequest> v;
         {

@@ -136,8 +136,16 @@ void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, 
     i = j;
   }
   for (int64_t d = 0; d < D; ++d) out.doc_line_off[d + 1] = out.doc_line_off[d] + kept[d];
-  out.line_start.alloc(out.doc_line_off[D]);
-  out.line_len.alloc(out.doc_line_off[D]);
+  const int64_t L = out.doc_line_off[D];
+  int64_t* ls = out.ext_start;
+  int32_t* ll = out.ext_len;
+  out.external = ls && ll && L <= out.ext_cap;
+  if (!out.external) {
+    out.line_start.alloc(L);
+    out.line_len.alloc(L);
+    ls = out.line_start.data();
+    ll = out.line_len.data();
+  }
   // phase 2: line starts / lengths, each unit writes its own newlines' lines
   parallel_units(U, total, nthreads, min_bytes_per_thread, [&](Unit& u) {
     const int64_t k = kept[u.doc], base = out.doc_line_off[u.doc];
@@ -145,16 +153,16 @@ void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, 
     for (size_t w = 0; w < u.nl.size(); ++w) {
       const int64_t g = u.first_nl + (int64_t)w;
       if (g >= k) return;
-      out.line_start[base + g] = start;
-      out.line_len[base + g] = (int32_t)(line_end(u.nl[w], start) - start);
+      ls[base + g] = start;
+      ll[base + g] = (int32_t)(line_end(u.nl[w], start) - start);
       start = u.nl[w] + 1;
     }
     // the line after the document's last newline belongs to the document's last unit
     const bool last_unit = u.b == doc_off[u.doc + 1];
     const int64_t g = u.first_nl + (int64_t)u.nl.size();
     if (last_unit && g < k) {
-      out.line_start[base + g] = start;
-      out.line_len[base + g] = (int32_t)(u.b - start);
+      ls[base + g] = start;
+      ll[base + g] = (int32_t)(u.b - start);
     }
   });
 }

@@ -35,6 +35,12 @@ struct DocBatchIndex {
   RawBuf<int64_t> line_start;   // absolute offsets into the packed buffer
   RawBuf<int32_t> line_len;     // '\r' before '\n' excluded
   RawBuf<int64_t> doc_line_off; // D+1
+  // caller-provided destination (e.g. pinned memory the device copies from directly): used when
+  // the line count fits `ext_cap`; line_start / line_len then stay empty and `external` is set
+  int64_t* ext_start = nullptr;
+  int32_t* ext_len = nullptr;
+  int64_t ext_cap = 0;
+  bool external = false;
 };
 
 // src[d], len[d]: document bytes; dst receives them back to back at doc_off (D+1, prefix sums).

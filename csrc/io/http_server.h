@@ -39,6 +39,11 @@ class HttpServer {
   int port() const { return port_; }
   // up to `max_n` pending requests; waits up to `timeout_ms` for the first one
   std::vector<HttpRequest> next_requests(int max_n, int timeout_ms);
+  // requests parsed and waiting to be drained
+  size_t pending() {
+    std::lock_guard<std::mutex> g(qm_);
+    return q_.size();
+  }
   // queue the response of request `id` (ignored if its connection is gone)
   void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
   void stop();

@@ -168,6 +168,76 @@ class FrequencyTurn:
             self._cv.notify_all()
 
 
+@dataclass
+class BatchJob:
+    """One continuous batch between the pipeline stages (pack -> device -> emit)."""
+    logs: Sequence
+    t0: float
+    tm: Optional[dict] = None
+    number: int = 0                     # batch number of the engine (fault injection)
+    whole: bool = False                 # one huge document, analysed by analyze_json
+    stage: Optional[Stage] = None       # staging buffers from the engine's StagePool
+    staged: Optional[tuple] = None      # (host view, line_start, line_len, doc_line_off, nbytes)
+    n_lines: int = -1                   # >= 0: the line index is in stage.idx (pinned)
+    ev: Optional[tuple] = None          # (ev_line, ev_pat, ev_seg, score, freq counts) on the host
+    timings: Optional[dict] = None
+    outs: Optional[List[bytes]] = None  # responses computed by the device stage itself
+
+
+class Stage:
+    """One batch's (pinned) host staging: packed request bytes + the line index the packer writes
+    straight into ``idx`` (int64 starts for ``cap`` lines, then int32 lengths), so both reach the
+    device with plain async copies and no intermediate host copy."""
+
+    def __init__(self, pinned: bool, nbytes: int, nlines: int):
+        self.pinned = pinned
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
+        self.cap = 0
+        self.idx: Optional[torch.Tensor] = None
+        self.grow_idx(nlines)
+
+    def grow_buf(self, nbytes: int) -> None:
+        self.buf = None
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=self.pinned)
+
+    def grow_idx(self, nlines: int) -> None:
+        self.idx = None
+        self.cap = int(nlines)
+        self.idx = torch.empty(12 * self.cap, dtype=torch.uint8, pin_memory=self.pinned)
+
+    def starts(self, n: int) -> torch.Tensor:
+        return self.idx[:8 * n].view(torch.int64)
+
+    def lens(self, n: int) -> torch.Tensor:
+        return self.idx[8 * self.cap:8 * self.cap + 4 * n].view(torch.int32)
+
+
+class StagePool:
+    """Recycled ``Stage`` buffers, one per batch in flight. ``take`` blocks when ``limit`` stages
+    are out: the back-pressure of the serving pipeline."""
+
+    def __init__(self, pinned: bool, initial: int, limit: int = 3):
+        self.pinned, self.initial, self.limit = pinned, initial, limit
+        self._free: List[Stage] = []
+        self._out = 0
+        self._cv = threading.Condition()
+
+    def take(self) -> Stage:
+        with self._cv:
+            while not self._free and self._out >= self.limit:
+                self._cv.wait()
+            self._out += 1
+            if self._free:
+                return self._free.pop()
+        return Stage(self.pinned, self.initial, self.initial // 16)
+
+    def give(self, st: Stage) -> None:
+        with self._cv:
+            self._out -= 1
+            self._free.append(st)
+            self._cv.notify()
+
+
 class Engine:
     def __init__(self, library: CompiledLibrary, config: Optional[Config] = None,
                  device: Optional[torch.device] = None, freq: Optional[FrequencyState] = None):
@@ -192,7 +262,8 @@ class Engine:
         self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
                          p.max_context_factor, p.freq_threshold, p.freq_max_penalty, float(p.freq_window_hours))
         self._pinned: Optional[torch.Tensor] = None
-        self._bstage: Optional[torch.Tensor] = None     # batch staging (pinned on GPU), reused
+        # batch staging buffers (pinned on GPU), recycled; one per batch in flight in the pipeline
+        self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
         if self.device.type == "cuda":
             props = torch.cuda.get_device_properties(self.device)
             self.pf_grid = int(props.multi_processor_count) * 4
@@ -420,44 +491,81 @@ class Engine:
         deterministic version of the reference's concurrent-request interleaving. With ``turn``
         (several engines serving concurrently) the frequency carry of batch ``seq`` is read and
         its counts recorded inside the turn; the caller releases the turn on failure.
+
+        = ``pack_batch`` -> ``device_batch`` -> ``emit_batch``; the serving pipeline
+        (serve/pipeline.py) runs the three stages of consecutive batches on different threads.
         """
+        job = self.pack_batch(logs_list)
+        try:
+            self.device_batch(job, turn, seq)
+            return self.emit_batch(job)
+        finally:
+            self.release_batch(job)
+
+    def pack_batch(self, logs_list: Sequence) -> "BatchJob":
+        """Stage 1 (host): pack the request bodies into a pinned staging buffer + line index."""
         t0 = time.time()
         self._batches += 1
-        if self.fault_every and self._batches % self.fault_every == 0:
-            raise RuntimeError("injected device fault (engine.fault-inject-every)")
+        job = BatchJob(logs=logs_list, t0=t0, tm={} if self.profile else None, number=self._batches)
         if len(logs_list) == 1 and len(logs_list[0]) >= self.GPU_SPLIT_BYTES:
+            job.whole = True                    # one huge document: streamed by analyze_json
+            return job
+        job.stage = self._stage_pool.take()
+        try:
+            with TR.HostTimer(job.tm, "line_index"):
+                staged = self._stage_docs(job, logs_list)
+                if staged is None:              # lone surrogates: encode in Python
+                    staged = self._stage_docs(job, [l if isinstance(l, (bytes, bytearray)) else
+                                                    l.encode("utf-8", errors="surrogatepass") for l in logs_list])
+        except BaseException:
+            self.release_batch(job)
+            raise
+        job.staged = staged
+        return job
+
+    def device_batch(self, job: "BatchJob", turn: Optional[FrequencyTurn] = None, seq: int = 0) -> None:
+        """Stage 2 (device): H2D, match + score kernels, one D2H, frequency commit (in batch order)."""
+        if self.fault_every and job.number % self.fault_every == 0:
+            raise RuntimeError("injected device fault (engine.fault-inject-every)")
+        if job.whole:
             if turn is not None:
                 turn.wait(seq)
-            out = [self.analyze_json(logs_list[0])]
+            job.outs = [self.analyze_json(job.logs[0])]
             if turn is not None:
                 turn.done(seq)
-            return out
-        tm = {} if self.profile else None
-        with TR.HostTimer(tm, "line_index"):
-            staged = self._stage_docs(logs_list)
-            if staged is None:              # lone surrogates: encode in Python
-                staged = self._stage_docs([l if isinstance(l, (bytes, bytearray)) else
-                                           l.encode("utf-8", errors="surrogatepass") for l in logs_list])
-        hb, ls_h, ll_h, dl, n = staged
-        ndocs = len(logs_list)
+            return
+        hb, ls_h, ll_h, dl, n = job.staged
+        tm = job.tm
         if tm is not None:
             self._start(tm)
-        text = self._stage_h2d(n)
+        text = self._stage_h2d(job.stage.buf, n)
         lo, hi, g0, nn = Segments.doc_arrays(dl)
         verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
+        pinned_idx = job.n_lines >= 0 and self.device.type == "cuda"
+        if pinned_idx:                     # line index straight from the pinned stage (no host copy)
+            ls = job.stage.starts(job.n_lines).to(self.device, non_blocking=True)
+            ll = job.stage.lens(job.n_lines).to(self.device, non_blocking=True)
+            idx = []
+        else:
+            idx = [ls_h, ll_h]
         if turn is None:
             carry = self.freq.carry(self.lib.freq_ids)
-            ls, ll, lo, hi, g0, nn, carry = self.upload(
-                [ls_h, ll_h, lo, hi, g0, nn, carry if carry.size else np.zeros(1, np.int64)])
+            up = self.upload(idx + [lo, hi, g0, nn, carry if carry.size else np.zeros(1, np.int64)])
+            if not pinned_idx:
+                ls, ll = up[0], up[1]
+            lo, hi, g0, nn, carry = up[len(idx):]
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
             res = self.run(text, n, ls, ll, segs, carry, with_factors=verbose, timings=tm)
             with TR.HostTimer(tm, "d2h"):
-                ev_line, ev_pat, ev_seg, score, counts = self._results_to_host(res)
-            self.commit_frequency(counts)
+                job.ev = self._results_to_host(res)
+            self.commit_frequency(job.ev[4])
         else:
-            ls, ll, lo, hi, g0, nn = self.upload([ls_h, ll_h, lo, hi, g0, nn])
+            up = self.upload(idx + [lo, hi, g0, nn])
+            if not pinned_idx:
+                ls, ll = up[0], up[1]
+            lo, hi, g0, nn = up[len(idx):]
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
@@ -465,57 +573,79 @@ class Engine:
             turn.wait(seq)                     # earlier batches have recorded their counts
             res = self.finish(prep, segs, self.freq_carry(), with_factors=verbose)
             with TR.HostTimer(tm, "d2h"):
-                ev_line, ev_pat, ev_seg, score, counts = self._results_to_host(res)
-            self.commit_frequency(counts)
+                job.ev = self._results_to_host(res)
+            self.commit_frequency(job.ev[4])
             turn.done(seq)
         if verbose:
             self._log_events(res, dl)
-        extra = b""
         if tm is not None:
+            job.timings = res.timings
+
+    def emit_batch(self, job: "BatchJob") -> List[bytes]:
+        """Stage 3 (host): every response of the batch (uuid, metadata, events with context lines,
+        summary) in one native call with the GIL released (csrc/io/json_emit.cpp)."""
+        if job.outs is not None:
+            return job.outs
+        hb, ls_h, ll_h, dl, n = job.staged
+        ev_line, ev_pat, ev_seg, score, _ = job.ev
+        ndocs = len(job.logs)
+        extra = b""
+        if job.tm is not None:
             import json
-            st = {k: round(v, 4) for k, v in TR.resolve(res.timings).items()}
-            st.update({k: round(v, 4) for k, v in TR.resolve(tm).items()})
+            st = {k: round(v, 4) for k, v in TR.resolve(job.timings).items()}
+            st.update({k: round(v, 4) for k, v in TR.resolve(job.tm).items()})
             st["batchRequests"] = ndocs
             log.debug("stage timings (ms): %s", st)
             extra = (',"stageTimingsMs":' + json.dumps(st, separators=(",", ":"))).encode()
         now, ts = self._clock()
-        # every response of the batch (uuid, metadata, events with context lines, summary) in one
-        # native call with the GIL released (csrc/io/json_emit.cpp)
         bounds = np.searchsorted(ev_seg, np.arange(ndocs + 1)).astype(np.int64)
         tail = f',"analyzedAt":"{ts}","patternsUsed":{self._patterns_used()}'.encode() + extra
         return N.emit_batch_results(self._pattern_table(), hb.ctypes.data, ls_h, ll_h,
                                     np.ascontiguousarray(dl, np.int64), ev_line, ev_pat, score, bounds,
-                                    int((now - t0) * 1000), tail, self._STAGE_THREADS)
+                                    int((now - job.t0) * 1000), tail, self._STAGE_THREADS)
+
+    def release_batch(self, job: "BatchJob") -> None:
+        """Return the job's staging buffer to the pool (after its H2D and emission are done)."""
+        if job.stage is not None:
+            self._stage_pool.give(job.stage)
+            job.stage = None
 
     _STAGE_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8))
 
-    def _stage_docs(self, docs):
-        """Pack request bodies into the (pinned) batch staging buffer and build the per-document
+    def _stage_docs(self, job: "BatchJob", docs):
+        """Pack request bodies into the job's (pinned) staging buffer and build the per-document
         line index, in native code with the GIL released (csrc/io/docs.cpp): one host copy per
-        byte. Returns (host view, line_start, line_len, doc_line_off, nbytes) or None."""
-        if self._bstage is None:
-            self._bstage = torch.empty(K.padded_len(1 << 20), dtype=torch.uint8,
-                                       pin_memory=self.device.type == "cuda")
-        cap = self._bstage.numel() - K.TEXT_PAD - K.NL_TILE
-        r = N.pack_split_docs(docs, self._bstage.data_ptr(), cap, self._STAGE_THREADS)
+        byte; the index goes straight into the stage's pinned index buffer when it fits.
+        Returns (host view, line_start, line_len, doc_line_off, nbytes) or None."""
+        st = job.stage
+        cap = st.buf.numel() - K.TEXT_PAD - K.NL_TILE
+        r = N.pack_split_docs(docs, st.buf.data_ptr(), cap, self._STAGE_THREADS, st.idx.data_ptr(), st.cap)
         if r is None:
             return None
         if isinstance(r, int):
             size = K.padded_len(max(int(r), 1 << 20) * 5 // 4)
-            self._bstage = torch.empty(size, dtype=torch.uint8, pin_memory=self.device.type == "cuda")
-            r = N.pack_split_docs(docs, self._bstage.data_ptr(), size - K.TEXT_PAD - K.NL_TILE, self._STAGE_THREADS)
-        ls_h, ll_h, dl, doc_off = r
+            st.grow_buf(size)
+            r = N.pack_split_docs(docs, st.buf.data_ptr(), size - K.TEXT_PAD - K.NL_TILE, self._STAGE_THREADS,
+                                  st.idx.data_ptr(), st.cap)
+        a, ll_h, dl, doc_off = r
+        if ll_h is None:                   # index written into the stage
+            job.n_lines = int(a)
+            ls_h, ll_h = st.starts(job.n_lines).numpy(), st.lens(job.n_lines).numpy()
+        else:
+            ls_h = a
+            job.n_lines = -1
+            st.grow_idx(max(ls_h.size * 5 // 4, st.cap))      # fits next time
         n = int(doc_off[-1])
-        return self._bstage.numpy(), ls_h, ll_h, dl, n
+        return st.buf.numpy(), ls_h, ll_h, dl, n
 
-    def _stage_h2d(self, n: int) -> torch.Tensor:
+    def _stage_h2d(self, buf: torch.Tensor, n: int) -> torch.Tensor:
         size = K.padded_len(n)
-        self._bstage[n:size].zero_()
+        buf[n:size].zero_()
         if self.device.type == "cuda":
             dev = torch.empty(size, dtype=torch.uint8, device=self.device)
-            dev.copy_(self._bstage[:size], non_blocking=True)
+            dev.copy_(buf[:size], non_blocking=True)
             return dev
-        return self._bstage[:size]
+        return buf[:size]
 
     def _log_events(self, res: RunResult, doc_line_off) -> None:
         """Reference-style match / factor logs (AnalysisService.java:96-99 INFO per match,

@@ -34,6 +34,7 @@ from ..engine import Engine, FrequencyTurn
 from ..models.compiled import CompiledLibrary
 from ..models.library import load_pattern_directory
 from ..native import N
+from .pipeline import BatchPipeline
 from ..utils.config import Config
 from ..utils.metrics import Metrics
 
@@ -72,6 +73,9 @@ class Batcher:
             gc.collect()
             gc.freeze()
             gc.set_threshold(50_000, 50, 100)
+        # one engine: pack / device / emit of consecutive batches overlap (serve/pipeline.py)
+        self.pipe: Optional[BatchPipeline] = (BatchPipeline(self.engine, self.device_stage, metrics.observe_batch)
+                                              if self.turn is None else None)
         self._threads = [threading.Thread(target=self._loop, args=(e,), name=f"lp-batcher-{i}", daemon=True)
                          for i, e in enumerate(self.engines)]
         for t in self._threads:
@@ -94,6 +98,8 @@ class Batcher:
             self._cv.notify_all()
         for t in self._threads:
             t.join(timeout=5)
+        if self.pipe is not None:
+            self.pipe.close()
 
     def _take(self):
         with self._cv:
@@ -128,10 +134,18 @@ class Batcher:
                 if self._stop:
                     return
                 continue
+            if self.pipe is not None and not (len(batch) == 1 and self.pipe.idle() and not self._q):
+                # under load: hand the batch to the pipeline and form the next one meanwhile; a
+                # lone request on an idle server runs inline (no thread hand-offs)
+                self.pipe.submit([b[0] for b in batch], self._completion(batch))
+                continue
             try:
                 t0 = time.perf_counter()
-                outs = self.analyze(eng, [b[0] for b in batch], seq)
-                self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
+                if self.pipe is not None:
+                    outs = self.pipe.run_inline([b[0] for b in batch])      # observes the batch
+                else:
+                    outs = self.analyze(eng, [b[0] for b in batch], seq)
+                    self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
                 for (_, fut, _), o in zip(batch, outs):
                     fut.set_result(o)
             except Exception as e:  # noqa: BLE001 - propagate to every waiter
@@ -143,6 +157,37 @@ class Batcher:
                 if self.turn is not None:
                     self.turn.done(seq)    # no-op after a successful batch; unblocks later ones
 
+    @staticmethod
+    def _completion(batch):
+        def done(outs, exc):
+            if exc is not None:
+                for _, fut, _ in batch:
+                    if not fut.done():
+                        fut.set_exception(exc)
+                return
+            for (_, fut, _), o in zip(batch, outs):
+                fut.set_result(o)
+        return done
+
+    def device_stage(self, job, eng: Optional[Engine] = None, seq: int = 0) -> None:
+        """Pipeline device stage with the same CPU fallback as ``analyze``."""
+        eng = eng or self.engine
+        try:
+            eng.device_batch(job, self.turn, seq)
+        except Exception:  # noqa: BLE001
+            if not self.fallback_cpu:
+                raise
+            log.exception("device batch failed; serving it from the CPU backend")
+            job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq)
+
+    def _cpu(self, eng: Engine) -> Engine:
+        with self._cpu_lock:
+            self.metrics.device_failures += 1
+            if self._cpu_engine is None:
+                self._cpu_engine = Engine(eng.lib, eng.config, device=torch.device("cpu"), freq=eng.freq)
+                self._cpu_engine.fault_every = 0
+            return self._cpu_engine
+
     def analyze(self, eng: Engine, logs: List[str], seq: int) -> List[bytes]:
         """GPU batch; on a device failure (HIP error, OOM, lost device) serve the batch from the CPU
         backend — same library tables and the same frequency state — for availability only
@@ -153,12 +198,7 @@ class Batcher:
             if not self.fallback_cpu:
                 raise
             log.exception("device batch failed; serving it from the CPU backend")
-            with self._cpu_lock:
-                self.metrics.device_failures += 1
-                if self._cpu_engine is None:
-                    self._cpu_engine = Engine(eng.lib, eng.config, device=torch.device("cpu"), freq=eng.freq)
-                    self._cpu_engine.fault_every = 0
-                return self._cpu_engine.analyze_batch_json(logs, self.turn, seq)
+            return self._cpu(eng).analyze_batch_json(logs, self.turn, seq)
 
 
 def serve_devices(config: Config) -> List[torch.device]:

@@ -89,18 +89,28 @@ class NativeHttpFrontend:
 
     def _run_direct(self, b, batch) -> None:
         """Single engine: the pump thread is the continuous batcher -- everything that queued while
-        the previous batch ran is analysed as one batch, with no further thread hand-off. The
-        batcher's own worker never sees a request in this mode (every /parse, including the
-        json.loads-fallback bodies, comes through here), so the engine has one owner thread."""
-        t0 = time.perf_counter()
-        try:
-            outs = b.analyze(b.engine, [x[1] for x in batch], 0)
-        except Exception as e:  # noqa: BLE001
-            log.exception("batch failed")
+        the previous batch ran forms the next batch, with no hand-off to the batcher's worker (which
+        never sees a request in this mode: every /parse, including the json.loads-fallback bodies,
+        comes through here). A lone request on an idle pipeline runs inline on this thread (lowest
+        latency); under load, batches go through the pack / device / emit pipeline."""
+        logs = [x[1] for x in batch]
+        if len(batch) == 1 and b.pipe.idle() and self.srv.pending() == 0:
+            try:
+                outs = b.pipe.run_inline(logs)
+            except Exception as e:  # noqa: BLE001
+                log.exception("batch failed")
+                self._batch_done(batch, None, e)
+                return
+            self._batch_done(batch, outs, None)
+        else:
+            b.pipe.submit(logs, lambda outs, exc: self._batch_done(batch, outs, exc))
+
+    def _batch_done(self, batch, outs, exc) -> None:
+        if exc is not None:
+            err = ('{"error":"%s"}' % type(exc).__name__).encode()
             for rid, _, _, _ in batch:
-                self.srv.respond(rid, 500, "application/json", ('{"error":"%s"}' % type(e).__name__).encode())
+                self.srv.respond(rid, 500, "application/json", err)
             return
-        self.svc.metrics.observe_batch(len(batch), time.perf_counter() - t0)
         for (rid, logs, name, ta), out in zip(batch, outs):
             self.srv.respond(rid, 200, "application/json", out)
             self.svc.metrics.observe_request(200, time.perf_counter() - ta, len(logs))

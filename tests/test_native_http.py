@@ -143,6 +143,8 @@ def test_concurrent_clients(server):
     for t in th:
         t.join(timeout=300)
     assert not errs, errs[:3]
+    b = fe.svc.batcher()
+    assert b.pipe.idle() and fe.svc.engine()._stage_pool._out == 0   # pipelined batches all released
 
 
 def test_idle_connections_are_closed():

@@ -20,6 +20,7 @@ from __future__ import annotations
 import asyncio
 import gc
 import logging
+import sys
 import threading
 import time
 from collections import deque
@@ -73,6 +74,9 @@ class Batcher:
             gc.collect()
             gc.freeze()
             gc.set_threshold(50_000, 50, 100)
+        si = float(self.engine.config.get("server.switch-interval-ms", 0.0) or 0.0)
+        if si > 0:
+            sys.setswitchinterval(si / 1000.0)
         # one engine: pack / device / emit of consecutive batches overlap (serve/pipeline.py)
         self.pipe: Optional[BatchPipeline] = (BatchPipeline(self.engine, self.device_stage, metrics.observe_batch)
                                               if self.turn is None else None)

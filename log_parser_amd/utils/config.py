@@ -75,6 +75,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.idle-timeout-s": (60.0, float),
     # freeze the startup heap + raise GC thresholds in the batching server (submit-path latency)
     "server.gc-tuning": (True, bool),
+    # Python GIL switch interval in the serving process (ms; 0 = interpreter default 5 ms). The
+    # pipeline's device thread needs the GIL for every launch; a short interval keeps it from
+    # waiting behind the pack / emit threads' Python work
+    "server.switch-interval-ms": (0.0, float),
     # reference logs one INFO line per match (AnalysisService.java:96-99); we log it at DEBUG
     "server.log-matches": (False, bool),
 }

@@ -227,9 +227,17 @@ class StagePool:
             while not self._free and self._out >= self.limit:
                 self._cv.wait()
             self._out += 1
-            if self._free:
-                return self._free.pop()
-        return Stage(self.pinned, self.initial, self.initial // 16)
+            while self._free:
+                st = self._free.pop()
+                if st.buf is not None and st.idx is not None:   # (a failed grow leaves None)
+                    return st
+        try:
+            return Stage(self.pinned, self.initial, self.initial // 16)
+        except BaseException:               # e.g. pinned allocation failed: give the slot back
+            with self._cv:
+                self._out -= 1
+                self._cv.notify()
+            raise
 
     def give(self, st: Stage) -> None:
         with self._cv:

@@ -1,0 +1,41 @@
+"""bench.py contract (the driver's scaling run): launched by torch.distributed.run with one rank
+per device, rank 0 prints ONE JSON line whose value is the whole-job aggregate. Rehearsed here
+with 2 CPU ranks over gloo (the 8-GPU RCCL run is the driver's)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_bench_json_contract(tmp_path):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--lines-per-gpu", "20000"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]          # rank 0 only, one line
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True and d["data"] == "synthetic"
+    assert d["config"]["parallelism"] == "dp2"
+    # whole-job aggregate: lines of BOTH ranks per second of the slowest rank
+    assert d["config"]["global_batch"] == 2 * d["config"]["lines_per_gpu"]
+    assert abs(d["value"] - d["config"]["global_batch"] / (d["ms_per_step"] / 1e3)) / d["value"] < 1e-3
+    assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"].split(";")[0].strip()

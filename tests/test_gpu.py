@@ -37,6 +37,34 @@ def _text(dev, data: bytes):
     return t.to(dev), t
 
 
+def _tile_edge_texts():
+    T = K.NL_TILE
+    yield from ["", "\n", "\n\n", "\r\n", "a", "a\n", "\r", "\r\r\n", "a\r\n\r\n", "\n\na"]
+    yield "x" * (3 * T + 5)                                     # one line over four tiles
+    yield "x" * (T - 1) + "\n" + "y" * 10                        # '\n' on a tile's last byte
+    yield "x" * T + "\n" + "y"                                   # '\n' on a tile's first byte
+    yield "x" * (T - 1) + "\r\nz\n"                              # CRLF across a tile boundary
+    yield "x" * (2 * T - 1) + "\r" + "\n" * 3                     # ... then trailing empty lines
+    yield "x" * (4 * T - 1) + "\r\nz\n" + "w" * (4 * T)            # same at the 64 KiB look-back tiles
+    yield "x" * (4 * T) + "\n" + "y"
+    yield "".join(f"line {i} with some words in it\n" for i in range(200000))   # ~400 tiles: look-back
+    yield "\n" * (5 * T)                                        # only empty lines: none kept
+    yield "ab\n" * (4 * T)                                      # above the capacity guess: re-run
+
+
+def test_line_index_tile_edges(gpu_device):
+    """Single-pass line index (k_nl_lines decoupled look-back): tile boundaries, CR across a
+    boundary, all-empty / no-newline texts, many tiles, capacity re-run -- equal to Java split."""
+    for s in _tile_edge_texts():
+        data = s.encode()
+        td, _ = _text(gpu_device, data)
+        ls_d, ll_d = K.split_lines(td, len(data))
+        ref = golden.split_lines(s)
+        assert ls_d.numel() == len(ref), (len(s), s[:20])
+        got = [data[a:a + b].decode() for a, b in zip(ls_d.cpu().tolist(), ll_d.cpu().tolist())]
+        assert got == ref, (len(s), s[:20])
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_line_index_matches_java_split(gpu_device, seed):
     rng = random.Random(seed)

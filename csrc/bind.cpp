@@ -35,7 +35,7 @@ static PfTables pf_from(const py::tuple& t) {
   T.lit_reg_off = P<const int32_t>(t[9].cast<uint64_t>());
   T.lit_reg = P<const int32_t>(t[10].cast<uint64_t>());
   T.gmask = t[11].cast<int>();
-  T.lit_goff = P<const int32_t>(t[12].cast<uint64_t>());
+  T.stride = t[12].cast<int>();
   return T;
 }
 

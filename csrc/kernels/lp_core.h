@@ -157,8 +157,13 @@ struct PfTables {
   const int32_t* lit_reg_off;
   const int32_t* lit_reg;
   int gmask;                // bit g set when grams of length g (2..4) exist
-  const int32_t* lit_goff;  // offset of each literal's gram window inside the literal
+  int stride;               // 2: every literal indexes two adjacent windows -> test even positions
 };
+
+// gram_lits entry: literal id | (offset of the indexed window inside the literal << 22)
+constexpr int LIT_OFF_SHIFT = 22;
+LP_HD int pf_entry_lit(int32_t e) { return e & ((1 << LIT_OFF_SHIFT) - 1); }
+LP_HD int pf_entry_off(int32_t e) { return (int)((uint32_t)e >> LIT_OFF_SHIFT); }
 
 LP_HD uint32_t gram_mask(int g) { return g >= 4 ? 0xFFFFFFFFu : ((1u << (8 * g)) - 1u); }
 // Blocked bloom filter: one 32-bit word per key holds both probe bits, so a membership test is
@@ -171,9 +176,11 @@ LP_HD uint32_t bloom_hash(uint32_t key, int g) { return (key ^ (uint32_t)g * 0x9
 LP_HD uint32_t bloom_word(uint32_t key, int g, int bits) {   // word index among 2^(bits-5) words
   return bloom_hash(key, g) >> (32 - (bits - 5));
 }
-LP_HD uint32_t bloom_bits_of(uint32_t p) {                     // two bit positions inside the word
+LP_HD uint32_t bloom_bits_of(uint32_t p) {                     // three bit positions inside the word
+  // k = 3: a false positive needs 3 set bits of one word (~20x rarer than k = 2 at our load); it
+  // matters because one frequent text gram (a timestamp fragment) colliding costs a hit per line
   const uint32_t q = p ^ (p >> 15);
-  return (1u << (q & 31)) | (1u << ((q >> 5) & 31));
+  return (1u << (q & 31)) | (1u << ((q >> 5) & 31)) | (1u << ((q >> 10) & 31));
 }
 LP_HD uint32_t bloom_bits2(uint32_t key, int g) { return bloom_bits_of(bloom_hash(key, g)); }
 LP_HD bool bloom_test(const uint32_t* bl, uint32_t key, int g, int bits) {
@@ -283,10 +290,12 @@ LP_HD void pf_bucket(const PfTables& T, uint32_t gram, int g, int& s, int& c) {
   c = T.ht_cnt[h];
 }
 
-// Does literal `lit` occur with its gram window at text position p (ASCII case-insensitive)?
-LP_HD bool pf_lit_at(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, int lit) {
+// Does the literal of gram entry `e` occur with its indexed window at text position p (ASCII
+// case-insensitive)?
+LP_HD bool pf_lit_at(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, int32_t e) {
+  const int lit = pf_entry_lit(e);
   const int lo = T.lit_off[lit], len = T.lit_off[lit + 1] - lo;
-  const int64_t st = p - T.lit_goff[lit];
+  const int64_t st = p - pf_entry_off(e);
   if (st < 0 || st + len > nbytes) return false;
 #if defined(__HIP_DEVICE_COMPILE__)
   return lit_match16(text + st, T.lit_bytes + lo, len);
@@ -306,8 +315,9 @@ LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int6
   pf_bucket(T, gram, g, s, c);
   int64_t line = -1;
   for (int j = 0; j < c; ++j) {
-    const int lit = T.gram_lits[s + j];
-    if (!pf_lit_at(T, text, nbytes, p, lit)) continue;
+    const int32_t e = T.gram_lits[s + j];
+    if (!pf_lit_at(T, text, nbytes, p, e)) continue;
+    const int lit = pf_entry_lit(e);
     if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
     if (line < 0) line = 0;
     for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)

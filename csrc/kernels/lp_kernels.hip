@@ -257,7 +257,9 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
 // table, so the probe/verify/append code exists once in the binary (no I-cache blow-up).
 // GM = set of gram lengths present in the library (bit g), a compile-time constant so the
 // unrolled bloom loop is branch-free and its 16 x 2 LDS reads pipeline behind one wait.
-template <int GM>
+// S = 2 (library built with two adjacent windows per literal): only even positions are tested --
+// half the hash + LDS work; every literal occurrence still has one indexed window on an even byte.
+template <int GM, int S>
 __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,
                                                           int64_t nlines, int64_t* cand, int64_t cap,
@@ -287,7 +289,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
       const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
       uint32_t m4 = 0, m3 = 0, m2 = 0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
+      for (int k = 0; k < 16; k += S) {
         const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
         if constexpr (g4on) m4 |= pf_bloom<4>(bl, bits, gram) << k;
         if constexpr (g3) m3 |= pf_bloom<3>(bl, bits, gram) << k;
@@ -352,8 +354,9 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
       pf_bucket(T, g4 & gram_mask(G), G, s, c);
       int64_t line = -1;
       for (int j = lane; j < c; j += PV_LANES) {
-        const int lit = T.gram_lits[s + j];
-        if (!pf_lit_at(T, text, nbytes, p, lit)) continue;
+        const int32_t e = T.gram_lits[s + j];
+        if (!pf_lit_at(T, text, nbytes, p, e)) continue;
+        const int lit = pf_entry_lit(e);
         if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
         if (line < 0) line = 0;
         for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r) app(((int64_t)T.lit_reg[r] << 32) | line);
@@ -487,11 +490,17 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
   const size_t lds = (size_t(1) << T.bloom_bits) / 8 + PF_BUF * 8 + 16;
   int64_t units = (nbytes + 15) / 16;
   int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS));
-#define LP_PF_CASE(GMV)                                                                                     \
-  case GMV:                                                                                                 \
-    hipLaunchKernelGGL(k_prefilter<GMV>, dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, \
-                       line_start, nlines, cand, cap, count);                                               \
+#define LP_PF_CASE(GMV)                                                                                        \
+  case GMV:                                                                                                    \
+    hipLaunchKernelGGL((k_prefilter<GMV, 1>), dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, \
+                       line_start, nlines, cand, cap, count);                                                  \
     break;
+  if (T.stride == 2 && (T.gmask & 28) == 16) {
+    hipLaunchKernelGGL((k_prefilter<16, 2>), dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T,
+                       line_start, nlines, cand, cap, count);
+    LP_CHECK(hipGetLastError());
+    return;
+  }
   switch (T.gmask & 28) {
     LP_PF_CASE(4) LP_PF_CASE(8) LP_PF_CASE(12) LP_PF_CASE(16) LP_PF_CASE(20) LP_PF_CASE(24) LP_PF_CASE(28)
     default: return;  // no literals: nothing to prefilter

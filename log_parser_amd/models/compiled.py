@@ -60,25 +60,48 @@ _FREQ = {**{c: f * 0.55 for c, f in zip(b"etaoinshrdlcumwfgypbvkjxqz",
          ord("("): 0.3, ord(")"): 0.3, ord("\t"): 0.5}
 
 
-def _choose_grams(lits: List[bytes]) -> List[Tuple[int, int, int]]:
-    """Pick each literal's 4-byte window (key, g, offset): rarest estimated text frequency, with
-    a mild penalty for windows already shared by other literals (each sharer costs a compare)."""
+PF_STRIDE_MAX = 2      # 1 disables stride-2 prefilter sampling
+
+# gram entries: gram_lits value = literal id | (window offset << LIT_OFF_SHIFT)
+LIT_OFF_SHIFT = 22
+MAX_GRAM_OFF = (1 << (31 - LIT_OFF_SHIFT)) - 1
+
+
+def _window_cost(w: bytes) -> float:
+    import math
+    return sum(math.log2(_FREQ.get(c, 0.05) / 100.0) for c in w)
+
+
+def _choose_grams(lits: List[bytes], stride: int = 1) -> List[List[Tuple[int, int, int]]]:
+    """Per literal, the ``stride`` adjacent g-byte windows [(key, g, offset), ...] to index, rarest
+    estimated text frequency first, with a mild penalty for windows already shared by other
+    literals (each sharer costs a compare). With stride 2 every occurrence of the literal has one
+    indexed window starting at an even text position, so the device prefilter tests every other
+    position only (k_prefilter<GM, 2>); callers pass stride 2 only when every literal has >= 5 bytes."""
     import math
     used: Dict[Tuple[int, int], int] = {}
     out = []
     for lit in lits:
         g = min(4, len(lit))
         best = None
-        for i in range(len(lit) - g + 1):
-            w = lit[i:i + g]
-            key = int.from_bytes(w, "little")
-            lp = sum(math.log2(_FREQ.get(c, 0.05) / 100.0) for c in w)
-            cost = (lp + 0.5 * math.log2(1 + used.get((key, g), 0)), i)
-            if best is None or cost < best[0]:
-                best = (cost, key, i)
-        _, key, off = best
-        used[(key, g)] = used.get((key, g), 0) + 1
-        out.append((key, g, off))
+        for i in range(min(len(lit) - g - stride + 1, MAX_GRAM_OFF - stride + 1) + 1):
+            # expected verify work of the indexed windows = SUM over windows of text frequency x
+            # bucket size (log domain: the worst window dominates; a rare partner does not excuse a
+            # common or crowded one). Stride 1 keeps the milder sharing penalty it was tuned with.
+            alpha = 0.5 if stride == 1 else 0.75
+            cost = math.log2(sum(
+                2.0 ** (_window_cost(lit[i + d:i + d + g])
+                        + alpha * math.log2(1 + used.get((int.from_bytes(lit[i + d:i + d + g], "little"), g), 0)))
+                for d in range(stride)))
+            if best is None or (cost, i) < best:
+                best = (cost, i)
+        ents = []
+        for d in range(stride):
+            off = best[1] + d
+            key = int.from_bytes(lit[off:off + g], "little")
+            used[(key, g)] = used.get((key, g), 0) + 1
+            ents.append((key, g, off))
+        out.append(ents)
     return out
 
 
@@ -98,7 +121,7 @@ def bloom_word(key, g, bits):
 def bloom_bits2(key, g):
     p = bloom_hash(key, g)
     q = p ^ (p >> 15)
-    return (1 << (q & 31)) | (1 << ((q >> 5) & 31))
+    return (1 << (q & 31)) | (1 << ((q >> 5) & 31)) | (1 << ((q >> 10) & 31))
 
 
 def ht_hash(key, g):
@@ -309,11 +332,13 @@ class CompiledLibrary:
         lit_reg = np.array([r for rr in lit_regs for r in rr] or [0], np.int32)
         grams: Dict[Tuple[int, int], List[int]] = {}
         gmask = 0
-        lit_goff = np.zeros(max(len(lits), 1), np.int32)
-        for i, (key, g, off) in enumerate(_choose_grams(lits)):
-            grams.setdefault((key, g), []).append(i)
-            gmask |= 1 << g
-            lit_goff[i] = off
+        # stride-2 sampling needs two adjacent 4-byte windows per literal (>= 5 bytes each)
+        stride = 2 if (PF_STRIDE_MAX >= 2 and lits and min(len(l) for l in lits) >= 5
+                       and len(lits) < (1 << LIT_OFF_SHIFT)) else 1
+        for i, ents in enumerate(_choose_grams(lits, stride)):
+            for key, g, off in ents:
+                grams.setdefault((key, g), []).append(i | (off << LIT_OFF_SHIFT))
+                gmask |= 1 << g
         bits = BLOOM_BITS
         bloom = np.zeros((1 << bits) // 32, np.uint32)
         H = 16
@@ -334,7 +359,7 @@ class CompiledLibrary:
             gram_lits.extend(ids)
         self.pf = dict(bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
                        gram_lits=np.array(gram_lits or [0], np.int32), lit_off=lit_off, lit_bytes=lit_bytes,
-                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, lit_goff=lit_goff)
+                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, stride=stride)
 
     # ------------------------------------------------------------------ device tables
     def device_tables(self, device: torch.device) -> dict:
@@ -350,11 +375,11 @@ class CompiledLibrary:
         pf = self.pf
         t["pf_arrays"] = [T(pf["bloom"]), T(pf["ht_key"].view(np.int64)), T(pf["ht_val"]), T(pf["ht_cnt"]),
                           T(pf["gram_lits"]), T(pf["lit_off"]), T(pf["lit_bytes"]), T(pf["lit_reg_off"]),
-                          T(pf["lit_reg"]), T(pf["lit_goff"])]
+                          T(pf["lit_reg"])]
         a = t["pf_arrays"]
         t["pf"] = (a[0].data_ptr(), pf["bits"], a[1].data_ptr(), a[2].data_ptr(), a[3].data_ptr(), pf["ht_mask"],
                    a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"],
-                   a[9].data_ptr())
+                   pf["stride"])
         t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc)]
         d = t["dfa_arrays"]
         t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr())

@@ -1,0 +1,77 @@
+"""Prefilter tables (models/compiled.py _build_prefilter): with stride-2 sampling every literal
+indexes two adjacent 4-byte windows, so every occurrence of a literal has an indexed window that
+starts at an EVEN text position -- the positions k_prefilter<16, 2> tests. Checked here on the
+tables themselves (the device kernel is covered by the GPU tests against the golden model)."""
+import random
+
+import numpy as np
+
+from log_parser_amd.models import compiled as C
+from log_parser_amd.utils.config import ScoringParams
+from log_parser_amd.utils.synth import make_library
+
+
+def _entries(pf):
+    H = pf["ht_mask"] + 1
+    out = {}
+    for h in range(H):
+        k = int(pf["ht_key"][h])
+        if k == 2 ** 64 - 1:
+            continue
+        key, g = k & 0xFFFFFFFF, k >> 32
+        for j in range(int(pf["ht_cnt"][h])):
+            e = int(pf["gram_lits"][int(pf["ht_val"][h]) + j])
+            out.setdefault(e & ((1 << C.LIT_OFF_SHIFT) - 1), []).append((key, g, e >> C.LIT_OFF_SHIFT))
+    return out
+
+
+def test_stride2_tables_index_adjacent_windows_and_bloom_holds_them():
+    sets, _ = make_library(200, seed=5)
+    lib = C.CompiledLibrary(sets, ScoringParams())
+    pf = lib.pf
+    assert pf["stride"] == 2
+    ents = _entries(pf)
+    assert set(ents) == set(range(len(lib.literals)))
+    for i, lit in enumerate(lib.literals):
+        offs = sorted(o for _, _, o in ents[i])
+        assert len(offs) == 2 and offs[1] == offs[0] + 1
+        for key, g, o in ents[i]:
+            assert g == 4 and key == int.from_bytes(lit[o:o + 4], "little")
+            w = C.bloom_word(key, g, pf["bits"])
+            m = C.bloom_bits2(key, g)
+            assert int(pf["bloom"][w]) & m == m
+
+
+def test_every_occurrence_hits_an_even_position():
+    sets, _ = make_library(60, seed=9)
+    lib = C.CompiledLibrary(sets, ScoringParams())
+    ents = _entries(lib.pf)
+    rng = random.Random(3)
+    for i, lit in enumerate(lib.literals[:200]):
+        for shift in range(2):
+            q = rng.randrange(0, 40) * 2 + shift           # occurrence at an even / odd position
+            starts = [q + o for _, _, o in ents[i]]
+            assert any(p % 2 == 0 for p in starts)
+
+
+def test_short_literals_fall_back_to_stride1():
+    old = C.PF_STRIDE_MAX
+    try:
+        C.PF_STRIDE_MAX = 1
+        sets, _ = make_library(30, seed=5)
+        assert C.CompiledLibrary(sets, ScoringParams()).pf["stride"] == 1
+    finally:
+        C.PF_STRIDE_MAX = old
+    import yaml
+    from log_parser_amd.models.schema import PatternSet
+    doc = yaml.safe_load("""
+metadata: {library_id: short}
+patterns:
+  - id: p1
+    name: short literal
+    severity: HIGH
+    primary_pattern: {regex: "OOM", confidence: 0.9}
+""")
+    lib = C.CompiledLibrary([PatternSet.model_validate(doc)], ScoringParams())
+    assert lib.pf["stride"] == 1                      # a 3-byte literal has no two 4-byte windows
+    assert np.all(np.array([len(l) for l in lib.literals]) >= 1)

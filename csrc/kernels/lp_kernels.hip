@@ -205,6 +205,7 @@ __global__ __launch_bounds__(256) void k_last_nonempty(const int32_t* __restrict
 // global hash table and verify the whole literal; survivors append (regex, line) candidates.
 constexpr int PF_THREADS = 512;
 
+
 struct Appender {
   int64_t* out;
   int64_t cap;
@@ -259,7 +260,7 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
 // unrolled bloom loop is branch-free and its 16 x 2 LDS reads pipeline behind one wait.
 // S = 2 (library built with two adjacent windows per literal): only even positions are tested --
 // half the hash + LDS work; every literal occurrence still has one indexed window on an even byte.
-template <int GM, int S>
+template <int GM, int S, int PF_UNROLL>
 __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,
                                                           int64_t nlines, int64_t* cand, int64_t cap,
@@ -280,29 +281,45 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
   const int64_t nunits = (nbytes + 15) >> 4;
   constexpr bool g2 = GM & 4, g3 = GM & 8, g4on = GM & 16;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t ub = (int64_t)blockIdx.x * blockDim.x; ub < nunits; ub += stride) {
-    const int64_t u = ub + threadIdx.x;
-    if (u < nunits) {
-      const int64_t p0 = u << 4;
-      const uint4 v = *reinterpret_cast<const uint4*>(text + p0);
-      const uint32_t nx = *reinterpret_cast<const uint32_t*>(text + p0 + 16);
-      const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
-      uint32_t m4 = 0, m3 = 0, m2 = 0;
+  // one 16-byte unit: lower-case, test the grams, stage the (rare) hits
+  auto scan_unit = [&](int64_t p0, const uint4 v, const uint32_t nx) {
+    const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
+    uint32_t m4 = 0, m3 = 0, m2 = 0;
 #pragma unroll
-      for (int k = 0; k < 16; k += S) {
-        const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
-        if constexpr (g4on) m4 |= pf_bloom<4>(bl, bits, gram) << k;
-        if constexpr (g3) m3 |= pf_bloom<3>(bl, bits, gram) << k;
-        if constexpr (g2) m2 |= pf_bloom<2>(bl, bits, gram) << k;
+    for (int k = 0; k < 16; k += S) {
+      const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
+      if constexpr (g4on) m4 |= pf_bloom<4>(bl, bits, gram) << k;
+      if constexpr (g3) m3 |= pf_bloom<3>(bl, bits, gram) << k;
+      if constexpr (g2) m2 |= pf_bloom<2>(bl, bits, gram) << k;
+    }
+    const int64_t rem = nbytes - p0;
+    const uint32_t valid = rem >= 16 ? 0xFFFFu : ((1u << rem) - 1u);
+    uint64_t hm = ((uint64_t)(m4 & valid) << 32) | ((uint64_t)(m3 & valid) << 16) | (uint64_t)(m2 & valid);
+    while (hm) {  // rare: stage the gram hit; literal verification runs in k_pf_verify
+      const int b = __ffsll((unsigned long long)hm) - 1;
+      hm &= hm - 1;
+      app(((p0 + (b & 15)) << 2) | (int64_t)(b >> 4));   // (position, gram length - 2)
+    }
+  };
+  // PF_UNROLL units per lane per iteration, all loads issued before any is scanned: more bytes in
+  // flight per barrier interval (the stride-2 scan is latency-, not VALU-bound)
+  for (int64_t ub = (int64_t)blockIdx.x * blockDim.x * PF_UNROLL; ub < nunits; ub += PF_UNROLL * stride) {
+    uint4 v[PF_UNROLL];
+    uint32_t nx[PF_UNROLL];
+#pragma unroll
+    for (int j = 0; j < PF_UNROLL; ++j) {
+      const int64_t u = ub + threadIdx.x + (int64_t)j * blockDim.x;
+      v[j] = {0, 0, 0, 0};
+      nx[j] = 0;
+      if (u < nunits) {
+        v[j] = *reinterpret_cast<const uint4*>(text + (u << 4));
+        nx[j] = *reinterpret_cast<const uint32_t*>(text + (u << 4) + 16);
       }
-      const int64_t rem = nbytes - p0;
-      const uint32_t valid = rem >= 16 ? 0xFFFFu : ((1u << rem) - 1u);
-      uint64_t hm = ((uint64_t)(m4 & valid) << 32) | ((uint64_t)(m3 & valid) << 16) | (uint64_t)(m2 & valid);
-      while (hm) {  // rare: stage the gram hit; literal verification runs in k_pf_verify
-        const int b = __ffsll((unsigned long long)hm) - 1;
-        hm &= hm - 1;
-        app(((p0 + (b & 15)) << 2) | (int64_t)(b >> 4));   // (position, gram length - 2)
-      }
+    }
+#pragma unroll
+    for (int j = 0; j < PF_UNROLL; ++j) {
+      const int64_t u = ub + threadIdx.x + (int64_t)j * blockDim.x;
+      if (u < nunits) scan_unit(u << 4, v[j], nx[j]);
     }
     __syncthreads();
     const int c = *reinterpret_cast<volatile int*>(cnt);
@@ -489,15 +506,25 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
   if (nbytes <= 0) return;
   const size_t lds = (size_t(1) << T.bloom_bits) / 8 + PF_BUF * 8 + 16;
   int64_t units = (nbytes + 15) / 16;
-  int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS));
-#define LP_PF_CASE(GMV)                                                                                        \
-  case GMV:                                                                                                    \
-    hipLaunchKernelGGL((k_prefilter<GMV, 1>), dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, \
-                       line_start, nlines, cand, cap, count);                                                  \
+  // large texts: 4 units per lane per iteration (bytes in flight); small requests: 1, so every
+  // launched lane has work (latency)
+  const bool big = nbytes >= (int64_t(32) << 20);
+  int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS * (big ? 4 : 1)));
+#define LP_PF_LAUNCH(GMV, SV, UV)                                                                                   \
+  hipLaunchKernelGGL((k_prefilter<GMV, SV, UV>), dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, \
+                     line_start, nlines, cand, cap, count)
+#define LP_PF_CASE(GMV)                   \
+  case GMV:                               \
+    if (big)                              \
+      LP_PF_LAUNCH(GMV, 1, 4);            \
+    else                                  \
+      LP_PF_LAUNCH(GMV, 1, 1);            \
     break;
   if (T.stride == 2 && (T.gmask & 28) == 16) {
-    hipLaunchKernelGGL((k_prefilter<16, 2>), dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T,
-                       line_start, nlines, cand, cap, count);
+    if (big)
+      LP_PF_LAUNCH(16, 2, 4);
+    else
+      LP_PF_LAUNCH(16, 2, 1);
     LP_CHECK(hipGetLastError());
     return;
   }
@@ -506,6 +533,7 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
     default: return;  // no literals: nothing to prefilter
   }
 #undef LP_PF_CASE
+#undef LP_PF_LAUNCH
   LP_CHECK(hipGetLastError());
 }
 

@@ -42,7 +42,8 @@ void set_host_threads(int n) { host_threads() = std::max(1, n); }
 constexpr int NL_THREADS = 256;
 constexpr int NL_BYTES_PER_THREAD = 64;
 constexpr int NL_TILE = NL_THREADS * NL_BYTES_PER_THREAD;
-constexpr int64_t LP_NL_CR = int64_t(1) << 62;   // flag in a newline position: preceded by '\r'
+constexpr int64_t LP_NL_CR = int64_t(1) << 62;
+constexpr int NL_STAGE = 2048;   // LDS-staged newline positions per 16 KiB tile (~150 in log text)   // flag in a newline position: preceded by '\r'
 
 __device__ __forceinline__ uint32_t zero_byte_mask(uint32_t t) {
   // exact: high bit set in every byte of t that is 0x00
@@ -112,13 +113,22 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restri
     for (int k = 0; k < 16; ++k) m[k] = cr[k] = 0;
   }
   __shared__ int ws[NL_THREADS / 64];
+  __shared__ int64_t sbuf[NL_STAGE];
   int incl = wave_incl_scan(c);
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 63) ws[wid] = incl;
   __syncthreads();
-  int woff = 0;
-  for (int w = 0; w < wid; ++w) woff += ws[w];
-  int64_t o = blk_off[blockIdx.x] + woff + incl - c;
+  int woff = 0, tot = 0;
+  for (int w = 0; w < NL_THREADS / 64; ++w) {
+    if (w < wid) woff += ws[w];
+    tot += ws[w];
+  }
+  // positions are staged in LDS and written out coalesced (a lane's own newlines are ~0.6 on
+  // average: direct 8-byte stores would be scattered partial-line writes); a tile with more
+  // newlines than the stage writes directly
+  const bool staged = tot <= NL_STAGE;                   // block-uniform
+  const int64_t gbase = blk_off[blockIdx.x];
+  int64_t o = woff + incl - c;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     uint32_t mm = m[k];
@@ -129,9 +139,17 @@ __global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restri
       int b = __ffs(mm) - 1;          // bit 7, 15, 23 or 31
       int64_t v = base + 4 * k + (b >> 3);
       if (flag_cr && ((crb >> b) & 1u)) v |= LP_NL_CR;
-      nl_pos[o++] = v;
+      if (staged)                     // explicit LDS / global stores (no flat pointer select)
+        sbuf[o] = v;
+      else
+        nl_pos[gbase + o] = v;
+      ++o;
       mm &= mm - 1;
     }
+  }
+  if (staged) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < tot; i += NL_THREADS) nl_pos[gbase + i] = sbuf[i];
   }
 }
 

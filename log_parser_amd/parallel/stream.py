@@ -22,6 +22,7 @@ from __future__ import annotations
 import queue
 import threading
 import time
+import warnings
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
 
@@ -174,8 +175,12 @@ class StreamAnalyzer:
         try:
             flat = None
             if not isinstance(src, RepeatBuffer):
-                # zero-copy view of bytes / bytearray / memoryview / mmap
-                flat = torch.from_numpy(np.frombuffer(src, dtype=np.uint8)) if len(src) else None
+                # zero-copy view of bytes / bytearray / memoryview / mmap; only ever read (copied
+                # into the pinned stage), so torch's warning about read-only sources does not apply
+                if len(src):
+                    with warnings.catch_warnings():
+                        warnings.simplefilter("ignore", UserWarning)
+                        flat = torch.from_numpy(np.frombuffer(src, dtype=np.uint8))
             for l_start, pos, end, r_end, lh, rh in self._plan(src, eff, start):
                 n = r_end - l_start
                 size = K.padded_len(n)

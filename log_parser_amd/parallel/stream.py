@@ -73,7 +73,9 @@ class RepeatBuffer:
     def copy_into(self, dst: torch.Tensor, start: int, stop: int) -> None:
         """dst[0:stop-start] = self[start:stop] with tensor copies (no Python byte strings)."""
         if not hasattr(self, "_bt"):
-            self._bt = torch.from_numpy(np.frombuffer(self.block, dtype=np.uint8))
+            with warnings.catch_warnings():       # read-only source view, only copied from
+                warnings.simplefilter("ignore", UserWarning)
+                self._bt = torch.from_numpy(np.frombuffer(self.block, dtype=np.uint8))
         B = len(self.block)
         pos, o = start, 0
         while pos < stop:

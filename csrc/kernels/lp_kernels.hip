@@ -538,6 +538,14 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
     else                                  \
       LP_PF_LAUNCH(GMV, 1, 1);            \
     break;
+  if (T.stride == 4 && (T.gmask & 28) == 16) {   // 4 adjacent windows per literal: every 4th position
+    if (big)
+      LP_PF_LAUNCH(16, 4, 4);
+    else
+      LP_PF_LAUNCH(16, 4, 1);
+    LP_CHECK(hipGetLastError());
+    return;
+  }
   if (T.stride == 2 && (T.gmask & 28) == 16) {
     if (big)
       LP_PF_LAUNCH(16, 2, 4);

@@ -60,7 +60,7 @@ _FREQ = {**{c: f * 0.55 for c, f in zip(b"etaoinshrdlcumwfgypbvkjxqz",
          ord("("): 0.3, ord(")"): 0.3, ord("\t"): 0.5}
 
 
-PF_STRIDE_MAX = 2      # 1 disables stride-2 prefilter sampling
+PF_STRIDE_MAX = 4      # largest prefilter sampling stride (1, 2 or 4); 1 disables sampling
 
 # gram entries: gram_lits value = literal id | (window offset << LIT_OFF_SHIFT)
 LIT_OFF_SHIFT = 22
@@ -333,8 +333,14 @@ class CompiledLibrary:
         grams: Dict[Tuple[int, int], List[int]] = {}
         gmask = 0
         # stride-2 sampling needs two adjacent 4-byte windows per literal (>= 5 bytes each)
-        stride = 2 if (PF_STRIDE_MAX >= 2 and lits and min(len(l) for l in lits) >= 5
-                       and len(lits) < (1 << LIT_OFF_SHIFT)) else 1
+        # stride-S sampling needs S adjacent 4-byte windows per literal (>= S + 3 bytes each)
+        stride = 1
+        if lits and len(lits) < (1 << LIT_OFF_SHIFT):
+            shortest = min(len(l) for l in lits)
+            for s_ in (4, 2):
+                if PF_STRIDE_MAX >= s_ and shortest >= s_ + 3:
+                    stride = s_
+                    break
         for i, ents in enumerate(_choose_grams(lits, stride)):
             for key, g, off in ents:
                 grams.setdefault((key, g), []).append(i | (off << LIT_OFF_SHIFT))

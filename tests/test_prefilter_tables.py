@@ -1,10 +1,11 @@
-"""Prefilter tables (models/compiled.py _build_prefilter): with stride-2 sampling every literal
-indexes two adjacent 4-byte windows, so every occurrence of a literal has an indexed window that
-starts at an EVEN text position -- the positions k_prefilter<16, 2> tests. Checked here on the
+"""Prefilter tables (models/compiled.py _build_prefilter): with stride-S sampling (S = 2 or 4) every
+literal indexes S adjacent 4-byte windows, so every occurrence of a literal has an indexed window that
+starts at a text position divisible by S -- the positions k_prefilter<16, S> tests. Checked here on the
 tables themselves (the device kernel is covered by the GPU tests against the golden model)."""
 import random
 
 import numpy as np
+import pytest
 
 from log_parser_amd.models import compiled as C
 from log_parser_amd.utils.config import ScoringParams
@@ -25,16 +26,26 @@ def _entries(pf):
     return out
 
 
-def test_stride2_tables_index_adjacent_windows_and_bloom_holds_them():
-    sets, _ = make_library(200, seed=5)
-    lib = C.CompiledLibrary(sets, ScoringParams())
+def _lib_with_max_stride(smax, n=200, seed=5):
+    old = C.PF_STRIDE_MAX
+    try:
+        C.PF_STRIDE_MAX = smax
+        sets, _ = make_library(n, seed=seed)
+        return C.CompiledLibrary(sets, ScoringParams())
+    finally:
+        C.PF_STRIDE_MAX = old
+
+
+@pytest.mark.parametrize("S", [2, 4])
+def test_strided_tables_index_adjacent_windows_and_bloom_holds_them(S):
+    lib = _lib_with_max_stride(S)
     pf = lib.pf
-    assert pf["stride"] == 2
+    assert pf["stride"] == S                          # synthetic literals have >= 9 bytes
     ents = _entries(pf)
     assert set(ents) == set(range(len(lib.literals)))
     for i, lit in enumerate(lib.literals):
         offs = sorted(o for _, _, o in ents[i])
-        assert len(offs) == 2 and offs[1] == offs[0] + 1
+        assert offs == list(range(offs[0], offs[0] + S)) and offs[-1] + 4 <= len(lit)
         for key, g, o in ents[i]:
             assert g == 4 and key == int.from_bytes(lit[o:o + 4], "little")
             w = C.bloom_word(key, g, pf["bits"])
@@ -42,16 +53,36 @@ def test_stride2_tables_index_adjacent_windows_and_bloom_holds_them():
             assert int(pf["bloom"][w]) & m == m
 
 
-def test_every_occurrence_hits_an_even_position():
-    sets, _ = make_library(60, seed=9)
-    lib = C.CompiledLibrary(sets, ScoringParams())
+@pytest.mark.parametrize("S", [2, 4])
+def test_every_occurrence_hits_a_tested_position(S):
+    lib = _lib_with_max_stride(S, n=60, seed=9)
+    assert lib.pf["stride"] == S
     ents = _entries(lib.pf)
     rng = random.Random(3)
     for i, lit in enumerate(lib.literals[:200]):
-        for shift in range(2):
-            q = rng.randrange(0, 40) * 2 + shift           # occurrence at an even / odd position
+        for shift in range(S):
+            q = rng.randrange(0, 40) * S + shift           # occurrence at every residue mod S
             starts = [q + o for _, _, o in ents[i]]
-            assert any(p % 2 == 0 for p in starts)
+            assert sum(p % S == 0 for p in starts) == 1    # exactly one indexed window is tested
+
+
+def test_stride_follows_the_shortest_literal():
+    import yaml
+    from log_parser_amd.models.schema import PatternSet
+
+    def lib_for(regex):
+        doc = yaml.safe_load(f"""
+metadata: {{library_id: s}}
+patterns:
+  - id: p1
+    name: one literal
+    severity: HIGH
+    primary_pattern: {{regex: "{regex}", confidence: 0.9}}
+""")
+        return C.CompiledLibrary([PatternSet.model_validate(doc)], ScoringParams())
+    assert lib_for("OOMKill").pf["stride"] == 4       # 7 bytes: four 4-byte windows
+    assert lib_for("OOMKil").pf["stride"] == 2        # 6 bytes: only three windows
+    assert lib_for("OOMK").pf["stride"] == 1
 
 
 def test_short_literals_fall_back_to_stride1():

@@ -1,20 +1,29 @@
 #!/usr/bin/env python3
-"""Headline benchmark: log-lines/sec parsed+scored (whole node), 1k-pattern library.
+"""Headline benchmark: log-lines/sec parsed+scored (whole node), 1k-pattern library; p50 /parse.
 
 Config (BASELINE.json configs[2], weak-scaled): every rank (one process per GPU) owns a shard of
 ``--lines-per-gpu`` lines (default 12.5M -> 100M lines on 8 GPUs) of one logical synthetic pod
 log, analysed against a randomly generated 1,000-pattern library (primary + secondary +
-sequence patterns, context rules). A timed step is the complete pipeline for the shard:
+sequence patterns, context rules; ``--library realistic`` adds 3-6-byte-literal and literal-free
+primaries). A timed step is the complete pipeline for the shard:
 
   pinned host -> HBM copy of the raw log bytes (PCIe ingest, H2D)
   -> line index -> literal prefilter -> DFA verify / scan -> hit CSR -> events
   -> packed RCCL all_gather (global N, frequency carry, sequence-chain carry)
   -> fused fp64 scoring -> RCCL all_reduce (severity + frequency histograms)
-  -> RCCL all_gather top-k -> persistent frequency-state update.
+  -> RCCL all_gather top-k -> persistent frequency-state update
+  -> every event record (line, pattern, score) copied to pinned host memory.
+
+Launch: ``python bench.py --gpus N`` starts N rank processes itself (``utils/launch.py``; the
+parent makes no GPU call) -- or runs as one rank of ``torch.distributed.run``. On GPUs the
+process group is ``nccl`` (= RCCL over xGMI) at every world size, including 1.
 
 Nothing is cached between steps (the frequency state evolves exactly as the reference's would).
 Rank 0 prints one JSON line; ``value`` is total lines/s over all ranks (max step time across
-ranks). The reference publishes no number, so ``vs_baseline`` is null.
+ranks). The reference publishes no number, so ``vs_baseline`` is null. After the
+timed loop rank 0 measures p50/p99 of ``POST /parse`` (10k-line body) through a real server
+process started before this process touched the GPU (``p50_parse_ms``), and the engine-only
+latency of the same request (``p50_engine_ms``).
 """
 from __future__ import annotations
 
@@ -24,11 +33,9 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "log-lines/sec parsed+scored (whole node), 1k-pattern library"
 
 
 def parse():
@@ -38,49 +45,95 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--lines-per-gpu", type=int, default=12_500_000)
     ap.add_argument("--patterns", type=int, default=1000)
+    ap.add_argument("--library", default="realistic", choices=["realistic", "synthetic"],
+                    help="realistic: ~10%% short-literal and ~5%% literal-free primaries; synthetic: every "
+                         "primary has a long unique literal (the prefilter's best case)")
     ap.add_argument("--block-lines", type=int, default=250_000, help="unique synthetic lines, tiled to the shard")
     ap.add_argument("--hit-rate", type=float, default=0.004)
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--profile", action="store_true", help="per-stage HIP-event timings (no extra syncs)")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--parse-requests", type=int, default=30,
-                    help="rank 0: p50 latency of N single 10k-line /parse requests after the timed loop (0 = off)")
+                    help="rank 0: p50 latency of N single 10k-line POST /parse requests after the timed loop (0 = off)")
+    ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="server front end for p50")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
-    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
-                    help="process-group backend: auto = nccl (RCCL) on GPUs; gloo = host-staged collectives, "
-                         "only to rehearse several ranks on ONE GPU")
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
+                    help="process group: auto = nccl (RCCL) on GPUs / gloo on CPU, at every world size; "
+                         "gloo on GPUs = host-staged collectives (rehearse several ranks on ONE GPU); "
+                         "none = no process group at world size 1")
     return ap.parse_args()
+
+
+def library(args):
+    from log_parser_amd.utils.synth import make_library, realistic_library
+    if args.library == "realistic":
+        return realistic_library(args.patterns, seed=7)
+    return make_library(args.patterns, seed=7)
 
 
 def main():
     args = parse()
-    from log_parser_amd.engine import Engine
-    from log_parser_amd.models.compiled import CompiledLibrary
-    from log_parser_amd.ops import kernels as K
-    from log_parser_amd.parallel.dp import ShardedAnalyzer
-    from log_parser_amd.utils.config import Config, ScoringParams
-    from log_parser_amd.utils import tracing as TR
-    from log_parser_amd.utils.synth import make_library, make_log
+    from log_parser_amd.utils import launch
+    if not launch.under_launcher() and args.gpus > 1:
+        # parent: no GPU call here; N fresh rank processes, one per GPU
+        sys.exit(launch.spawn_local_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    sets, trig = library(args)
+
+    # p50 /parse server: started BEFORE this process makes any GPU call (rank 0 only)
+    server = None
+    if rank == 0 and args.parse_requests > 0:
+        from log_parser_amd.utils import restbench
+        dev = "cpu" if args.device == "cpu" else f"cuda:{local_rank}"
+        server = restbench.ServerProcess(restbench.write_library(sets), dev, http=args.http)
+    try:
+        run(args, sets, trig, rank, world, local_rank, server)
+    finally:
+        if server is not None:
+            server.stop()
+
+
+def run(args, sets, trig, rank, world, local_rank, server):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from log_parser_amd.engine import Engine
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.ops import kernels as K
+    from log_parser_amd.parallel.dp import ShardedAnalyzer, all_gather_rows
+    from log_parser_amd.utils.config import Config, ScoringParams
+    from log_parser_amd.utils import tracing as TR
+    from log_parser_amd.utils.synth import make_log
+
     use_cuda = torch.cuda.is_available() and args.device != "cpu"
     if use_cuda:
-        local_gpu = local_rank % max(1, torch.cuda.device_count())
+        ngpu = torch.cuda.device_count()
+        if world > ngpu:
+            raise SystemExit(f"{world} ranks but {ngpu} visible GPU(s): one rank per GPU")
+        local_gpu = local_rank
         torch.cuda.set_device(local_gpu)
         device = torch.device("cuda", local_gpu)
         from log_parser_amd.utils.numa import bind_to_gpu_numa
         bind_to_gpu_numa(local_gpu)          # pinned ingest buffers on the GPU's own socket
     else:
         device = torch.device("cpu")
-    if world > 1:
-        backend = args.backend if args.backend != "auto" else ("nccl" if use_cuda else "gloo")
-        dist.init_process_group(backend, rank=rank, world_size=world)
+    backend = args.backend if args.backend != "auto" else ("nccl" if use_cuda else "gloo")
+    if backend == "none" and world > 1:
+        backend = "nccl" if use_cuda else "gloo"
+    if backend != "none":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            from log_parser_amd.utils.launch import free_port
+            os.environ["MASTER_PORT"] = str(free_port())
+        kw = {"device_id": device} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        assert dist.get_world_size() == world
 
     params = ScoringParams()
-    sets, trig = make_library(args.patterns, seed=7)
     lib = CompiledLibrary(sets, params)
     cfg = Config.load(overrides={"engine.device": str(device)})
     eng = Engine(lib, cfg, device=device)
@@ -92,19 +145,22 @@ def main():
     block_b = block.encode()
     blines = block_b.split(b"\n")[:-1]
     reps = max(1, args.lines_per_gpu // len(blines))
-    own = block_b * reps
     own_lines = len(blines) * reps
     H = lib.halo
     head = b"\n".join(blines[:H]) + b"\n"
     tail = b"\n".join(blines[-H:]) + b"\n"
     hl = H if rank > 0 else 0
     hr = H if rank < world - 1 else 0
-    data = (tail if hl else b"") + own + (head if hr else b"")
-    nbytes = len(data)
+    pre = tail if hl else b""
+    post = head if hr else b""
+    nbytes = len(pre) + len(block_b) * reps + len(post)
     size = K.padded_len(nbytes)
     host = torch.zeros(size, dtype=torch.uint8, pin_memory=use_cuda)
-    host[:nbytes].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
-    del data, own
+    hv = host.numpy()
+    o = 0
+    for part in [pre] + [block_b] * reps + [post]:         # fill in place: no whole-shard temporaries
+        hv[o:o + len(part)] = np.frombuffer(part, np.uint8)
+        o += len(part)
     # Double-buffered ingest: the PCIe copy of request k+1 runs on its own HIP stream while request
     # k is analysed (every step still moves all of its bytes host->HBM). --no-overlap serialises.
     bufs = [torch.empty(size, dtype=torch.uint8, device=device) for _ in range(2)]
@@ -112,7 +168,9 @@ def main():
     ready = [torch.cuda.Event() for _ in range(2)] if use_cuda else None
     free = [torch.cuda.Event() for _ in range(2)] if use_cuda else None
     freed = [False, False]
-    state = {"i": 0, "issued": -1}
+    state = {"i": 0, "issued": -1, "events_host": 0}
+    # event records land here (pinned, 2 slots so step k+1's copy never waits on step k's)
+    ev_host = [torch.empty(0, dtype=torch.uint8, pin_memory=use_cuda) for _ in range(2)]
 
     def issue_copy(i):
         b = i % 2
@@ -125,6 +183,20 @@ def main():
             bufs[b].copy_(host, non_blocking=True)
             ready[b].record(copy_stream)
         state["issued"] = i
+
+    def events_to_host(out, slot):
+        """(global line int64, pattern int32, score f64) of EVERY event -> pinned host, one copy."""
+        r = out.result
+        n = r.ev_line.numel()
+        if n == 0:
+            return
+        g = (r.ev_line.to(torch.int64) - out.own_lo + out.own_start_dev)
+        pk = torch.cat([g.view(torch.int32), r.ev_pat.to(torch.int32), r.score.view(torch.int32)])
+        nb = pk.numel() * 4
+        if ev_host[slot].numel() < nb:
+            ev_host[slot] = torch.empty(nb * 5 // 4, dtype=torch.uint8, pin_memory=use_cuda)
+        ev_host[slot][:nb].view(torch.int32).copy_(pk, non_blocking=use_cuda)
+        state["events_host"] = n
 
     def step():
         i = state["i"]
@@ -141,26 +213,31 @@ def main():
             ev0.record()
         ls, ll = K.split_lines(text, nbytes)
         out = sa.step(text, nbytes, ls, ll, hl, hr, topk=args.topk)
+        events_to_host(out, b)                                   # results land on the host
+        if rank == 0 and out.topk_score is not None:
+            out.topk_score.cpu()
         if use_cuda:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()
             state.setdefault("dev", []).append((ev0, ev1))
-        if rank == 0 and out.topk_score is not None:
-            out.topk_score.cpu()                                 # results land on the host
-        if use_cuda:
             free[b].record(torch.cuda.current_stream())
             freed[b] = True
         state["i"] = i + 1
         return out
 
     def barrier():
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         if use_cuda:
             torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
+    barrier()
+    if server is not None and not server.wait_ready():      # server idle before timing starts
+        print("warning: /parse server did not come up; p50_parse_ms omitted", file=sys.stderr)
+        server.stop()
+        server = None
     barrier()
     state["dev"] = []
     t0 = time.perf_counter()
@@ -169,42 +246,51 @@ def main():
         last = step()
     barrier()
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=device)
-    if world > 1:
+    per_rank = [dt]
+    if dist.is_initialized():
+        dt_t = torch.tensor([dt], dtype=torch.float64, device=device)
         if dist.get_backend() == "gloo":
             dt_t = dt_t.cpu()
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+        per_rank = all_gather_rows(dt_t).flatten().cpu().tolist()
+    dt = max(per_rank)
     total_lines = last.total_lines
     ms = dt / args.steps * 1e3
     value = total_lines * args.steps / dt
     if rank == 0:
         rec = {
-            "metric": "log-lines/sec parsed+scored (whole node), 1k-pattern library",
+            "metric": METRIC,
             "value": round(value, 1), "unit": "lines/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp64", "data": "synthetic",
             "ingest": "h2d-serial" if args.no_overlap else "h2d-overlapped(2 buffers, copy stream)",
-            "config": {"model": f"log-parser {args.patterns}-pattern random library (secondary+sequence+context)",
+            "config": {"model": f"log-parser {args.patterns}-pattern {args.library} library "
+                                f"(secondary+sequence+context)",
                        "global_batch": total_lines, "seq_len": round(nbytes / max(own_lines, 1), 1),
                        "parallelism": f"dp{world}", "lines_per_gpu": own_lines, "bytes_per_gpu": nbytes,
                        "events_per_step": int(last.pattern_counts.sum().item()),
-                       "library": lib.summary(), "device": str(device)},
+                       "events_to_host_rank0": state["events_host"],
+                       "library_kind": args.library, "library": lib.summary(), "prefilter_stride": lib.pf["stride"], "device": str(device)},
+            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+            "backend": dist.get_backend() if dist.is_initialized() else "none",
+            "ms_per_step_per_rank": [round(x / args.steps * 1e3, 3) for x in per_rank],
         }
         if state.get("dev"):
-            # compute-stream time of the device pipeline per step (line index .. collectives .. top-k),
-            # i.e. what the GPU sustains when the log is already resident (the timed value above
-            # includes every byte's PCIe copy, overlapped on the copy stream)
+            # compute-stream time of the device pipeline per step (line index .. collectives .. top-k
+            # .. event copy), i.e. what the GPU sustains when the log is already resident (the timed
+            # value above includes every byte's PCIe copy, overlapped on the copy stream)
             dms = float(np.mean([a.elapsed_time(b) for a, b in state["dev"]]))
             rec["device_ms_per_step_rank0"] = round(dms, 3)
             rec["device_resident_lines_per_s"] = round(own_lines * world / (dms / 1e3), 1)
         if args.profile:
             rec["timings_ms_last_step_rank0"] = {k: round(v, 3) for k, v in TR.resolve(last.result.timings).items()}
         if args.parse_requests > 0:
-            # second half of the BASELINE metric: p50 latency of one /parse request (10k-line pod
-            # log, same 1k-pattern library) through the serving engine path (staging, kernels,
-            # JSON). Measured after the timed loop, outside it; HTTP framing excluded.
+            # second half of the BASELINE metric: one 10k-line /parse request, same library
             req = make_log(10_000, trig, seed=13, hit_rate=0.01)
+            if server is not None:
+                lat = server.parse_latencies(req, args.parse_requests)
+                rec["p50_parse_ms"] = round(float(np.median(lat)) * 1e3, 3)
+                rec["p99_parse_ms"] = round(float(np.percentile(lat, 99)) * 1e3, 3)
+                rec["parse_transport"] = f"{args.http} HTTP/1.1 keep-alive, server process on 127.0.0.1"
             for _ in range(3):
                 eng.analyze_batch_json([req])
             lat = []
@@ -212,15 +298,16 @@ def main():
                 t1 = time.perf_counter()
                 eng.analyze_batch_json([req])
                 lat.append(time.perf_counter() - t1)
-            rec["p50_parse_ms"] = round(float(np.median(lat)) * 1e3, 3)
-            rec["p99_parse_ms"] = round(float(np.percentile(lat, 99)) * 1e3, 3)
+            rec["p50_engine_ms"] = round(float(np.median(lat)) * 1e3, 3)
+            rec["p99_engine_ms"] = round(float(np.percentile(lat, 99)) * 1e3, 3)
             rec["config"]["parse_request_lines"] = 10_000
         print(json.dumps(rec), flush=True)
     if args.torch_trace:                                         # untimed, after the measurement
         with TR.torch_profile(args.torch_trace.replace(".json", f".rank{rank}.json"), device):
             step()
             barrier()
-    if world > 1:
+    if dist.is_initialized():
+        barrier()
         dist.destroy_process_group()
 
 

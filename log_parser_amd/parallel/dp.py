@@ -45,10 +45,16 @@ def host_staged(group=None) -> bool:
     return dist.get_backend(group) == "gloo"
 
 
+def distributed() -> bool:
+    """A process group exists. Collectives then always run -- also at world size 1, so a 1-GPU
+    bench still drives the device-tensor RCCL path the 8-GPU run uses."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
     """all_gather of a 1-D tensor -> [world, n] (RCCL all_gather_into_tensor on GPU)."""
     r, w = world()
-    if w == 1:
+    if not distributed():
         return t.unsqueeze(0)
     if t.is_cuda and not host_staged(group):
         out = torch.empty((w,) + tuple(t.shape), dtype=t.dtype, device=t.device)
@@ -61,7 +67,7 @@ def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
 
 
 def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
-    if world()[1] > 1:
+    if distributed():
         if t.is_cuda and host_staged(group):
             h = t.cpu()
             dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
@@ -81,6 +87,8 @@ class StepOutput:
     topk_line: Optional[torch.Tensor] = None    # 0-based global line
     topk_pat: Optional[torch.Tensor] = None
     summary: Optional[dict] = None
+    own_lo: int = 0                                 # first owned local line (= left halo lines)
+    own_start_dev: Optional[torch.Tensor] = None    # [1] global index of the first owned line
 
     # host integers on demand (a host read here would stall the step's launch queue)
     @property
@@ -148,7 +156,7 @@ class ShardedAnalyzer:
         red = all_reduce_sum(red, self.group)
         pattern_counts = red[:P]
         eng.commit_frequency(red[P:])
-        out = StepOutput(res, own_counts, rank, pattern_counts)
+        out = StepOutput(res, own_counts, rank, pattern_counts, own_lo=own_lo, own_start_dev=own_start)
         # C7: top-k
         if topk > 0:
             k = min(topk, res.score.numel())

@@ -1,0 +1,97 @@
+"""``POST /parse`` latency through a real server process (the p50 half of the headline metric).
+
+The service runs as its own process (``python -m log_parser_amd.serve``, native epoll front end by
+default, as deployed) on 127.0.0.1 against a pattern directory written from the benchmark's
+library; the client keeps one HTTP/1.1 connection open and times send-body -> full response
+(``Parse.java:41-61`` is the measured surface). Start the server BEFORE the calling process
+touches the GPU (a GPU-initialised process must not fork interpreters).
+"""
+from __future__ import annotations
+
+import http.client
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from typing import List, Optional, Sequence
+
+from .launch import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def write_library(sets, directory: Optional[str] = None) -> str:
+    """Pattern sets -> one YAML file per set (snake_case, as PatternService loads them)."""
+    import yaml
+    d = directory or tempfile.mkdtemp(prefix="lp-lib-")
+    for i, s in enumerate(sets):
+        with open(os.path.join(d, f"set{i:03d}.yaml"), "w") as f:
+            yaml.safe_dump(s.model_dump(by_alias=True, exclude_none=True), f)
+    return d
+
+
+class ServerProcess:
+    def __init__(self, pattern_dir: str, device: str, http: str = "native", extra: Sequence[str] = (),
+                 log_path: Optional[str] = None):
+        self.port = free_port()
+        self.log = open(log_path, "wb") if log_path else subprocess.DEVNULL
+        cmd = [sys.executable, "-m", "log_parser_amd.serve", f"-Dpattern.directory={pattern_dir}",
+               f"-Dengine.device={device}", "-Dserver.host=127.0.0.1", f"-Dserver.port={self.port}",
+               f"-Dserver.http={http}"] + list(extra)
+        self.proc = subprocess.Popen(cmd, cwd=ROOT, stdout=self.log, stderr=self.log)
+        self.conn: Optional[http.client.HTTPConnection] = None
+
+    def wait_ready(self, timeout_s: float = 240.0) -> bool:
+        deadline = time.time() + timeout_s
+        while time.time() < deadline:
+            if self.proc.poll() is not None:
+                return False
+            try:
+                c = http.client.HTTPConnection("127.0.0.1", self.port, timeout=60)
+                c.request("GET", "/ready")
+                r = c.getresponse()
+                r.read()
+                if r.status == 200:
+                    self.conn = c
+                    return True
+                c.close()
+            except OSError:
+                pass
+            time.sleep(0.25)
+        return False
+
+    def post(self, body: bytes, content_type: str = "application/json") -> tuple:
+        c = self.conn
+        c.request("POST", "/parse", body=body, headers={"content-type": content_type})
+        r = c.getresponse()
+        return r.status, r.read()
+
+    def parse_latencies(self, logs: str, n: int, warmup: int = 5) -> List[float]:
+        body = json.dumps({"pod": {"metadata": {"name": "bench"}}, "logs": logs}).encode()
+        for _ in range(warmup):
+            st, out = self.post(body)
+            if st != 200:
+                raise RuntimeError(f"/parse returned {st}: {out[:200]!r}")
+        lat = []
+        for _ in range(n):
+            t = time.perf_counter()
+            st, out = self.post(body)
+            lat.append(time.perf_counter() - t)
+            if st != 200:
+                raise RuntimeError(f"/parse returned {st}")
+        return lat
+
+    def stop(self) -> None:
+        if self.conn is not None:
+            self.conn.close()
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
+        if self.log is not subprocess.DEVNULL:
+            self.log.close()

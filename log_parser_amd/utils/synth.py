@@ -29,17 +29,77 @@ def _token(rng: random.Random, i: int) -> str:
     return "".join(rng.choice(syl) for _ in range(3)).capitalize() + str(i)
 
 
+# letters that never start a 3-gram of the noise text (no vowels, no T/Z of the timestamps)
+_CODE_LETTERS = "BCFGHJKMPQVWXY"
+
+
+def _short_code(rng: random.Random, n: int) -> str:
+    """3..6-byte error code (e.g. 'K42', 'QX7M1'): a short, realistic prefilter literal."""
+    s = rng.choice(_CODE_LETTERS)
+    while len(s) < n:
+        s += rng.choice(_CODE_LETTERS + "0123456789")
+    return s
+
+
+def _literal_free(rng: random.Random, i: int) -> Tuple[str, str]:
+    """A regex with no usable literal factor (every line must be scanned) + a matching sample.
+    Parametrised by ``i`` so every regex of the library is a distinct string; shapes that the
+    noise text of ``make_log`` never matches."""
+    fam = i % 6
+    a, b = 3 + (i // 6) % 3, 2 + (i // 18) % 6
+    up = "".join(rng.choice("ABCDEFGHJKLMNPQRSUVWXY") for _ in range(a + 1))
+    dg = "".join(rng.choice("0123456789") for _ in range(b))
+    if fam == 0:
+        return rf"\b[A-Z]{{{a},}}_\d{{{b}}}\b", f"state {up}_{dg} entered"
+    if fam == 1:
+        return rf"\b[A-Z]{{2}}\d{{{a}}}[A-Z]{{{b}}}\b", \
+            f"unit {up[:2]}{dg[:1] * a}{''.join(rng.choice('KMPQVX') for _ in range(b))} down"
+    if fam == 2:
+        m = 1 + b % 3
+        return rf"\b\d{{1,3}}\.\d{{1,3}}\.\d{{{m},3}}\.\d+:\d{{{a + 1}}}\b", \
+            f"peer 10.2.{'7' * m}.4:{'9' * (a + 1)} reset"
+    if fam == 3:
+        return rf"[^\s]+@[^\s]+\.[a-z]{{{b}}}\b", f"mail to ops@corp.{'x' * b} bounced"
+    if fam == 4:
+        return rf"\b[A-Z][a-z]+[A-Z][a-z]+\d{{{a}}}[A-Z]{{{b}}}\b", \
+            f"got ShardLost{'5' * a}{'Q' * b} again"
+    return rf"^\s+at\s+[a-z]+\.[A-Z]\w{{{a},}}\(\w*\.\w+:\d{{{b}}}\)", \
+        f"\tat app.R{'x' * a}(Main.java:{'4' * b})"
+
+
 def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate: float = 0.7,
-                 sequence_rate: float = 0.4, feature_mix: bool = True) -> Tuple[List[PatternSet], List[dict]]:
-    """Returns (pattern sets, trigger descriptions used by ``make_log`` to plant matches)."""
+                 sequence_rate: float = 0.4, feature_mix: bool = True, short_literal_rate: float = 0.0,
+                 literal_free_rate: float = 0.0) -> Tuple[List[PatternSet], List[dict]]:
+    """Returns (pattern sets, trigger descriptions used by ``make_log`` to plant matches).
+
+    ``short_literal_rate`` / ``literal_free_rate``: shares of primaries whose only literal is a
+    3-6-byte code, or that have no usable literal at all (``realistic_library``)."""
     rng = random.Random(seed)
     sets = [{"metadata": {"library_id": f"synthetic-lib-{s}", "version": "1.0"}, "patterns": []}
             for s in range(n_sets)]
     triggers = []
+    n_free = 0
     for i in range(n_patterns):
         tok = _token(rng, i)
         style = rng.randrange(8) if feature_mix else 0
-        if style == 0:
+        u = rng.random()
+        if u < literal_free_rate:
+            style = 8
+        elif u < literal_free_rate + short_literal_rate:
+            style = 9
+        if style == 8:
+            regex, sample = _literal_free(rng, n_free)
+            n_free += 1
+        elif style == 9:
+            code = _short_code(rng, 3 + i % 4)
+            k = i % 3
+            if k == 0:
+                regex, sample = rf"\b{code}\b", f"fault {code} raised"
+            elif k == 1:
+                regex, sample = rf"(?i)\b{code}: \w+", f"{code.lower()}: aborted"
+            else:
+                regex, sample = rf"{code}\d*[a-z]?$", f"exit with {code}7"
+        elif style == 0:
             regex, sample = tok + "Failure", f"{tok}Failure detected"
         elif style == 1:
             regex, sample = rf"(?i)\b{tok}\s+(crashed|aborted)\b", f"{tok.upper()} crashed unexpectedly"
@@ -84,6 +144,15 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
     return [PatternSet.model_validate(s) for s in sets], triggers
 
 
+def realistic_library(n_patterns: int, seed: int = 0, **kw):
+    """The headline bench library: the synthetic mix plus ~10% primaries with only a 3-6-byte
+    literal and ~5% literal-free primaries, the shapes real libraries have (short error codes,
+    IP:port, `^\\s+at ...` stack frames) and the prefilter's worst case."""
+    kw.setdefault("short_literal_rate", 0.10)
+    kw.setdefault("literal_free_rate", 0.05)
+    return make_library(n_patterns, seed=seed, **kw)
+
+
 def _noise_line(rng: random.Random, i: int) -> str:
     lvl = rng.choice(LEVELS)
     comp = rng.choice(COMPONENTS)
@@ -104,7 +173,10 @@ def make_log(n_lines: int, triggers: List[dict], seed: int = 0, hit_rate: float 
                 for ev in t["sequence"][:-1]:
                     out.append(f"INFO [app] {ev} reached")
                     i += 1
-            out.append(_noise_line(rng, i)[:40] + " " + t["sample"])
+            if t["sample"][:1].isspace():          # anchored stack-frame shape: a line of its own
+                out.append(t["sample"])
+            else:
+                out.append(_noise_line(rng, i)[:40] + " " + t["sample"])
             if t["sequence"] and rng.random() < 0.6:
                 out.append(f"INFO [app] {t['sequence'][-1]} reached")
                 i += 1

@@ -39,3 +39,44 @@ def test_two_rank_bench_json_contract(tmp_path):
     assert d["config"]["global_batch"] == 2 * d["config"]["lines_per_gpu"]
     assert abs(d["value"] - d["config"]["global_batch"] / (d["ms_per_step"] / 1e3)) / d["value"] < 1e-3
     assert d["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"].split(";")[0].strip()
+
+
+def _json_line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout[-2000:]            # rank 0 only, one line
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_its_own_ranks(tmp_path):
+    """``bench.py --gpus 3`` WITHOUT a launcher: the parent starts 3 rank processes itself (the
+    driver's ``--gpus N`` contract), the JSON reports n_gpus 3 and the live world size."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--device", "cpu", "--steps", "2",
+           "--warmup", "1", "--lines-per-gpu", "6000", "--block-lines", "6000", "--parse-requests", "0",
+           "--library", "synthetic"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 3 and d["world_size"] == 3 and d["backend"] == "gloo"
+    assert d["config"]["parallelism"] == "dp3" and len(d["ms_per_step_per_rank"]) == 3
+    assert d["config"]["global_batch"] == 3 * d["config"]["lines_per_gpu"]
+    assert d["ms_per_step"] == max(d["ms_per_step_per_rank"])
+    assert d["config"]["events_to_host_rank0"] > 0
+
+
+def test_bench_single_rank_parse_over_http(tmp_path):
+    """--gpus 1 on CPU: a process group at world size 1 (collectives still run) and p50 measured
+    through a real POST /parse server process next to the engine-only latency."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--steps", "1", "--warmup", "1",
+           "--lines-per-gpu", "4000", "--block-lines", "4000", "--parse-requests", "2", "--patterns", "60"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1 and d["world_size"] == 1 and d["backend"] == "gloo"
+    assert d["p50_parse_ms"] > 0 and d["p50_engine_ms"] > 0
+    assert "HTTP" in d["parse_transport"]

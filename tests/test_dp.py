@@ -46,7 +46,7 @@ def _reference():
     for _ in range(STEPS):
         res = eng.run(t, len(data), ls, ll, Segments.single(ls.numel(), t.device), eng.freq_carry())
         eng.commit_frequency(res.freq_counts)
-        outs.append((res.ev_line.numpy().astype(np.int64), res.ev_pat.numpy(), res.score.numpy()))
+        outs.append((res.ev_line.numpy().astype(np.int64), res.ev_pat.numpy(), res.score.numpy(), ls.numel()))
     return outs
 
 
@@ -105,8 +105,9 @@ def _run_sharded(world, dev):
         lines = np.concatenate([got[r][s][0] for r in range(world)])
         pats = np.concatenate([got[r][s][1] for r in range(world)])
         scores = np.concatenate([got[r][s][2] for r in range(world)])
-        rl, rp, rs = ref[s]
-        assert got[0][s][3] == len(set(rl)) or True
+        rl, rp, rs, n_lines = ref[s]
+        for r in range(world):                # C1: every rank sees the global line count N
+            assert got[r][s][3] == n_lines
         np.testing.assert_array_equal(lines, rl)
         np.testing.assert_array_equal(pats, rp)
         np.testing.assert_allclose(scores, rs, rtol=1e-13, atol=0)
@@ -183,7 +184,8 @@ def _run_p2p(world, dev):
         p.join(timeout=60)
         assert p.exitcode == 0
     for s in range(STEPS):
-        rl, rp, rs = ref[s]
+        rl, rp, rs, n_lines = ref[s]
+        assert all(got[r][s][3] == n_lines for r in range(world))
         np.testing.assert_array_equal(np.concatenate([got[r][s][0] for r in range(world)]), rl)
         np.testing.assert_array_equal(np.concatenate([got[r][s][1] for r in range(world)]), rp)
         np.testing.assert_allclose(np.concatenate([got[r][s][2] for r in range(world)]), rs, rtol=1e-13, atol=0)

@@ -36,6 +36,10 @@ static PfTables pf_from(const py::tuple& t) {
   T.lit_reg = P<const int32_t>(t[10].cast<uint64_t>());
   T.gmask = t[11].cast<int>();
   T.stride = t[12].cast<int>();
+  T.teddy = P<const uint32_t>(t[13].cast<uint64_t>());
+  T.tb_off = P<const int32_t>(t[14].cast<uint64_t>());
+  T.tb_lits = P<const int32_t>(t[15].cast<uint64_t>());
+  T.teddy_on = t[16].cast<int>();
   return T;
 }
 
@@ -88,6 +92,29 @@ static EvTables ev_from(const py::tuple& t) {
   E.nkeys = t[10].cast<int>();
   E.pbits = t[11].cast<int>();
   return E;
+}
+
+// (blob ptr, lds_words, ngroups, row_base, stride, thr, init_row, init_state, ncol, gt_off, fin_off
+//  [each a 4-tuple], bm_off, rid_off)
+static ScanPass scan_pass_from(const py::tuple& t) {
+  ScanPass S;
+  S.blob = P<const uint32_t>(t[0].cast<uint64_t>());
+  S.lds_words = t[1].cast<int>();
+  S.ngroups = t[2].cast<int>();
+  auto q = [&](int i, int g) { return t[i].cast<py::tuple>()[g].cast<int64_t>(); };
+  for (int g = 0; g < 4; ++g) {
+    S.row_base[g] = (int)q(3, g);
+    S.stride[g] = (int)q(4, g);
+    S.thr[g] = (int)q(5, g);
+    S.init_row[g] = (int)q(6, g);
+    S.init_state[g] = (uint32_t)q(7, g);
+    S.ncol[g] = (int)q(8, g);
+    S.gt_off[g] = (int)q(9, g);
+    S.fin_off[g] = (int)q(10, g);
+  }
+  S.bm_off = t[11].cast<int>();
+  S.rid_off = t[12].cast<int>();
+  return S;
 }
 
 static py::bytes vbytes(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
@@ -254,6 +281,31 @@ static py::tuple parse_pod_request_py(py::bytes body) {
 
 PYBIND11_MODULE(_lpnative, m) {
   m.doc() = "log_parser_amd native core: Java-regex compiler, gfx950 kernels, host twins, JSON emitter";
+  m.def("compile_multi", [](const std::vector<std::string>& pats, int max_states) -> py::object {
+    MultiDfa d;
+    try {
+      d = compile_multi(pats, max_states);
+    } catch (const Unsupported&) {
+      return py::none();
+    }
+    py::dict r;
+    r["nstates"] = d.nstates;
+    r["nclasses"] = d.nclasses;
+    r["nregs"] = d.nregs;
+    r["bytemap"] = vbytes(d.bytemap.data(), d.bytemap.size());
+    r["trans"] = vbytes(d.trans.data(), d.trans.size() * 4);
+    r["fin"] = vbytes(d.fin.data(), d.fin.size() * 4);
+    return r;
+  }, py::arg("patterns"), py::arg("max_states") = 4096);
+  m.def("multi_find", [](const std::vector<std::string>& pats, const std::string& line) -> int64_t {
+    MultiDfa d;
+    try {
+      d = compile_multi(pats, 1 << 16);
+    } catch (const Unsupported&) {
+      return -1;
+    }
+    return multi_find(d, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size());
+  });
   m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
   m.def("dfa_find", &dfa_find_py, py::arg("pattern"), py::arg("line"), py::arg("max_states") = 4096);
   m.def("split_docs", &split_docs);
@@ -309,6 +361,18 @@ PYBIND11_MODULE(_lpnative, m) {
                         uint64_t out, int64_t cap) {
     return scan_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs),
                      nregs, dfa_from(dfa), P<int64_t>(out), cap); });
+  m.def("scan_multi", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, py::tuple pass, uint64_t out,
+                         int64_t cap, uint64_t cnt, int grid, uint64_t s, bool dev) -> int64_t {
+    const ScanPass S = scan_pass_from(pass);
+    if (dev) {
+      scan_multi_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, S, P<int64_t>(out), cap,
+                     P<unsigned long long>(cnt), grid, s);
+      return 0;
+    }
+    py::gil_scoped_release nogil;
+    return scan_multi_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, S, P<int64_t>(out),
+                           cap);
+  });
   m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry,
                          int64_t n, py::tuple st, py::tuple sp, uint64_t out, uint64_t fac) {
     const FreqIn F{P<const int64_t>(rank), P<const int64_t>(fkey), P<const int64_t>(carry)};

@@ -26,6 +26,22 @@ namespace {
 constexpr size_t kMaxHeader = 64 << 10;
 constexpr int kMaxIo = 255;
 const char kInvalid[] = "{\"error\":\"Invalid PodFailureData provided\"}";
+const char kUnsupported[] = "{\"error\":\"Content-Type must be application/json\"}";
+
+// media type of a Content-Type value (parameters such as charset ignored, case-insensitive) is
+// application/json; an absent header is accepted (see log_parser_amd/serve/app.py)
+bool is_json_media_type(const std::string& v) {
+  size_t e = v.find(';');
+  if (e == std::string::npos) e = v.size();
+  size_t a = 0;
+  while (a < e && (v[a] == ' ' || v[a] == '\t')) ++a;
+  while (e > a && (v[e - 1] == ' ' || v[e - 1] == '\t')) --e;
+  static const char kJson[] = "application/json";
+  if (e - a != sizeof(kJson) - 1) return false;
+  for (size_t i = 0; i < e - a; ++i)
+    if (tolower((unsigned char)v[a + i]) != kJson[i]) return false;
+  return true;
+}
 
 double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -40,6 +56,7 @@ const char* reason(int s) {
     case 405: return "Method Not Allowed";
     case 411: return "Length Required";
     case 413: return "Payload Too Large";
+    case 415: return "Unsupported Media Type";
     case 431: return "Request Header Fields Too Large";
     case 500: return "Internal Server Error";
     case 503: return "Service Unavailable";
@@ -262,7 +279,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
   std::string method(s, sp1 - s), path(sp1 + 1, sp2 - sp1 - 1), version(sp2 + 1, s + le - sp2 - 1);
   bool keep = version != "HTTP/1.0";
   int64_t clen = 0;
-  bool has_len = false, chunked = false, expect = false;
+  bool has_len = false, chunked = false, expect = false, json_ctype = true;
   size_t p = le + 2;
   while (p < he) {
     const size_t e = c->in.find("\r\n", p);
@@ -291,6 +308,8 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
         chunked = true;
       } else if (ieq(l, kn, "expect")) {
         expect = true;
+      } else if (ieq(l, kn, "content-type")) {
+        json_ctype = is_json_media_type(v);
       }
     }
     p = e + 2;
@@ -329,6 +348,11 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
   }
   HttpRequest r;
   r.t_arrival = now_s();
+  if (method == "POST" && route == "/parse" && !json_ctype) {
+    // @Consumes(MediaType.APPLICATION_JSON) (Parse.java:42): another media type is a 415
+    send_now(io, c, 415, "application/json", kUnsupported, keep);
+    return !c->closing && !c->dead;
+  }
   if (method == "POST" && route == "/parse") {
     PodRequest pr;
     const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(body.data()), body.size(), pr);

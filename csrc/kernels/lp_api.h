@@ -61,6 +61,30 @@ int64_t nfa_host(const uint64_t* groups, const int32_t* group_list, int ngroups,
                  int64_t* hits, int64_t cap);
 }  // namespace lp
 
+// ---- literal-free scan (scan_multi.hip): up to 4 multi-regex DFA groups per pass, tables in LDS
+namespace lp {
+struct ScanPass {
+  const uint32_t* blob;   // device (or host) copy of the whole blob; layout in scan_multi.hip
+  int lds_words;          // leading words staged in LDS: u16 rows + bm4 (multiple of 4)
+  int ngroups;            // 1..4
+  int row_base[4];        // u16 index of group g's first row
+  int stride[4];          // row stride (u16 entries, odd)
+  int thr[4];             // first row index of a state from which a regex can accept
+  int init_row[4];        // row index of the start state
+  uint32_t init_state[4]; // start state id (exact tables)
+  int ncol[4];            // columns: hold, '\n', byte classes
+  int gt_off[4];          // word offset of group g's exact [state][ncol] table
+  int fin_off[4];         // word offset of group g's [state][EOL, FT] accept masks
+  int bm_off;             // word offset of bm4
+  int rid_off;            // word offset of the regex ids (16 per group)
+};
+void scan_multi_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+                    const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,
+                    uint64_t stream);
+int64_t scan_multi_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+                        const ScanPass& S, int64_t* out, int64_t cap);
+}  // namespace lp
+
 // ---- post-match pipeline (lp_post.hip): hit CSR, events, frequency ranks, context features
 namespace lp {
 struct EvTables {

@@ -156,8 +156,14 @@ struct PfTables {
   const uint8_t* lit_bytes; // ASCII-lowercased
   const int32_t* lit_reg_off;
   const int32_t* lit_reg;
-  int gmask;                // bit g set when grams of length g (2..4) exist
-  int stride;               // 2: every literal indexes two adjacent windows -> test even positions
+  int gmask;                // bit g set when grams of length g (2..4) exist (bloom tier)
+  int stride;               // S in {1, 2, 4}: every bloom literal indexes S adjacent windows -> test
+                            // positions divisible by S (literals of >= S + 3 bytes)
+  // short-literal (Teddy) tier: teddy[4c + j] = buckets whose 3-byte window has byte c at offset j
+  const uint32_t* teddy;    // [256 * 4]
+  const int32_t* tb_off;    // [33] bucket CSR into tb_lits
+  const int32_t* tb_lits;   // literal id | window offset << 22 (as gram_lits)
+  int teddy_on;
 };
 
 // gram_lits entry: literal id | (offset of the indexed window inside the literal << 22)
@@ -322,6 +328,36 @@ LP_HD void pf_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int6
     if (line < 0) line = 0;
     for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
       append(((int64_t)T.lit_reg[r] << 32) | line);
+  }
+}
+
+// Short-literal tier: bucket mask of the 3-byte window at text position p (bytes past nbytes are
+// the zero padding, and byte 0 is in no window: no match there).
+LP_HD uint32_t teddy_mask(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p) {
+  const int b0 = lower_byte(text[p]);
+  const int b1 = p + 1 < nbytes ? lower_byte(text[p + 1]) : 0;
+  const int b2 = p + 2 < nbytes ? lower_byte(text[p + 2]) : 0;
+  return T.teddy[4 * b0] & T.teddy[4 * b1 + 1] & T.teddy[4 * b2 + 2];
+}
+
+// Probe one short-literal candidate position (host twin / small inputs): verify every literal of
+// every bucket in the mask, append (regex << 32 | line).
+template <typename AppendFn>
+LP_HD void teddy_probe(const PfTables& T, const uint8_t* text, int64_t nbytes, int64_t p, uint32_t m,
+                       const int64_t* line_start, int64_t nlines, const int32_t* blk_line, AppendFn&& append) {
+  int64_t line = -1;
+  while (m) {
+    const int b = __builtin_ctz(m);
+    m &= m - 1;
+    for (int j = T.tb_off[b]; j < T.tb_off[b + 1]; ++j) {
+      const int32_t e = T.tb_lits[j];
+      if (!pf_lit_at(T, text, nbytes, p, e)) continue;
+      const int lit = pf_entry_lit(e);
+      if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
+      if (line < 0) line = 0;
+      for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
+        append(((int64_t)T.lit_reg[r] << 32) | line);
+    }
   }
 }
 

@@ -42,8 +42,8 @@ void set_host_threads(int n) { host_threads() = std::max(1, n); }
 constexpr int NL_THREADS = 256;
 constexpr int NL_BYTES_PER_THREAD = 64;
 constexpr int NL_TILE = NL_THREADS * NL_BYTES_PER_THREAD;
-constexpr int64_t LP_NL_CR = int64_t(1) << 62;
-constexpr int NL_STAGE = 2048;   // LDS-staged newline positions per 16 KiB tile (~150 in log text)   // flag in a newline position: preceded by '\r'
+constexpr int64_t LP_NL_CR = int64_t(1) << 62;   // flag in a newline position: preceded by '\r'
+constexpr int NL_STAGE = 2048;   // LDS-staged newline positions per 16 KiB tile (~150 in log text)
 
 __device__ __forceinline__ uint32_t zero_byte_mask(uint32_t t) {
   // exact: high bit set in every byte of t that is 0x00
@@ -271,56 +271,91 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
   return bloom_test(bl, g4 & gram_mask(G), G, bits) ? 1u : 0u;
 }
 
-// Hot loop: only bloom tests (tight, fully unrolled: ~12 VALU + 2 ds_read_b32 per position and
-// gram length). Rare path: one non-unrolled loop over the hit bitmask probes the global hash
-// table, so the probe/verify/append code exists once in the binary (no I-cache blow-up).
-// GM = set of gram lengths present in the library (bit g), a compile-time constant so the
-// unrolled bloom loop is branch-free and its 16 x 2 LDS reads pipeline behind one wait.
-// S = 2 (library built with two adjacent windows per literal): only even positions are tested --
-// half the hash + LDS work; every literal occurrence still has one indexed window on an even byte.
-template <int GM, int S, int PF_UNROLL>
+// Hot loop: only filter tests (tight, fully unrolled, branch-free). Rare path: one non-unrolled loop
+// over the hit bitmask stages the hit; verification runs in k_pf_verify, so the probe/verify code
+// exists once in the binary (no I-cache blow-up).
+//   bloom tier (GM != 0): GM = set of gram lengths present (bit g), a compile-time constant so the
+//     16 / S LDS reads of a unit pipeline behind one wait. S in {1, 2, 4}: every bloom literal
+//     indexes S adjacent 4-byte windows, so only positions divisible by S are tested -- every
+//     occurrence still has exactly one indexed window starting there.
+//   short-literal tier (TD): Teddy byte-position masks. One 16-byte LDS read per text byte gives
+//     (M0, M1, M2)[byte]; the rolling AND of three consecutive reads is the bucket mask of a 3-byte
+//     window. 18 reads per 16-byte unit, ~5 VALU per position, no hashing.
+template <int GM, int S, int PF_UNROLL, bool TD>
 __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,
                                                           int64_t nlines, int64_t* cand, int64_t cap,
                                                           unsigned long long* count) {
-  // dynamic LDS: [bloom (1<<bits)/8 B][candidate buffer PF_BUF x 8 B][cnt 4 B | pad | gbase 8 B]
+  // dynamic LDS: [bloom (1<<bits)/8 B, GM only][teddy 4 KiB, TD only][candidates PF_BUF x 8 B][cnt | pad | gbase]
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* bl = smem;
   const int bits = T.bloom_bits;
-  const int nwords = (1 << bits) >> 5;
-  int64_t* buf = reinterpret_cast<int64_t*>(smem + nwords);
+  const int nwords = GM ? (1 << bits) >> 5 : 0;
+  uint32_t* bl = smem;
+  uint32_t* td = smem + nwords;
+  int64_t* buf = reinterpret_cast<int64_t*>(td + (TD ? 1024 : 0));
   int* cnt = reinterpret_cast<int*>(buf + PF_BUF);
   unsigned long long* gbase = reinterpret_cast<unsigned long long*>(buf + PF_BUF + 1);
   for (int i = threadIdx.x * 4; i < nwords; i += blockDim.x * 4)
     *reinterpret_cast<uint4*>(bl + i) = *reinterpret_cast<const uint4*>(T.bloom + i);
+  if constexpr (TD)
+    for (int i = threadIdx.x * 4; i < 1024; i += blockDim.x * 4)
+      *reinterpret_cast<uint4*>(td + i) = *reinterpret_cast<const uint4*>(T.teddy + i);
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
   const LdsAppender app{buf, cnt, cand, cap, count};
   const int64_t nunits = (nbytes + 15) >> 4;
   constexpr bool g2 = GM & 4, g3 = GM & 8, g4on = GM & 16;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // one 16-byte unit: lower-case, test the grams, stage the (rare) hits
+  const uint4* tt = reinterpret_cast<const uint4*>(td);
+  // one 16-byte unit: lower-case, test the grams / windows, stage the (rare) hits
   auto scan_unit = [&](int64_t p0, const uint4 v, const uint32_t nx) {
     const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
-    uint32_t m4 = 0, m3 = 0, m2 = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k += S) {
-      const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
-      if constexpr (g4on) m4 |= pf_bloom<4>(bl, bits, gram) << k;
-      if constexpr (g3) m3 |= pf_bloom<3>(bl, bits, gram) << k;
-      if constexpr (g2) m2 |= pf_bloom<2>(bl, bits, gram) << k;
-    }
     const int64_t rem = nbytes - p0;
     const uint32_t valid = rem >= 16 ? 0xFFFFu : ((1u << rem) - 1u);
-    uint64_t hm = ((uint64_t)(m4 & valid) << 32) | ((uint64_t)(m3 & valid) << 16) | (uint64_t)(m2 & valid);
-    while (hm) {  // rare: stage the gram hit; literal verification runs in k_pf_verify
-      const int b = __ffsll((unsigned long long)hm) - 1;
-      hm &= hm - 1;
-      app(((p0 + (b & 15)) << 2) | (int64_t)(b >> 4));   // (position, gram length - 2)
+    if constexpr (GM != 0) {
+      uint32_t m4 = 0, m3 = 0, m2 = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k += S) {
+        const uint32_t gram = (k & 3) ? __builtin_amdgcn_alignbyte(w[(k >> 2) + 1], w[k >> 2], k & 3) : w[k >> 2];
+        if constexpr (g4on) m4 |= pf_bloom<4>(bl, bits, gram) << k;
+        if constexpr (g3) m3 |= pf_bloom<3>(bl, bits, gram) << k;
+        if constexpr (g2) m2 |= pf_bloom<2>(bl, bits, gram) << k;
+      }
+      uint64_t hm = ((uint64_t)(m4 & valid) << 32) | ((uint64_t)(m3 & valid) << 16) | (uint64_t)(m2 & valid);
+      while (hm) {  // rare: stage the gram hit; literal verification runs in k_pf_verify
+        const int b = __ffsll((unsigned long long)hm) - 1;
+        hm &= hm - 1;
+        app(((p0 + (b & 15)) << 2) | (int64_t)(b >> 4));   // (position, gram length - 2)
+      }
+    }
+    if constexpr (TD) {
+      uint32_t r0 = 0, r1 = 0, any = 0;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) {
+        const uint4 e = tt[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu];
+        if (k >= 2) any |= r1 & e.z;           // window starting at k - 2 complete
+        r1 = r0 & e.y;
+        r0 = e.x;
+      }
+      if (any) {                               // rare: which positions
+        uint32_t hm = 0;
+        for (int k = 0; k < 16; ++k) {
+          const uint32_t b0 = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+          const uint32_t b1 = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
+          const uint32_t b2 = (w[(k + 2) >> 2] >> (8 * ((k + 2) & 3))) & 0xFFu;
+          if (tt[b0].x & tt[b1].y & tt[b2].z) hm |= 1u << k;
+        }
+        hm &= valid;
+        while (hm) {
+          const int b = __ffs(hm) - 1;
+          hm &= hm - 1;
+          app(((p0 + b) << 2) | 3);            // code 3: short-literal tier
+        }
+      }
     }
   };
   // PF_UNROLL units per lane per iteration, all loads issued before any is scanned: more bytes in
-  // flight per barrier interval (the stride-2 scan is latency-, not VALU-bound)
+  // flight per barrier interval (the strided scan is latency-, not VALU-bound)
   for (int64_t ub = (int64_t)blockIdx.x * blockDim.x * PF_UNROLL; ub < nunits; ub += PF_UNROLL * stride) {
     uint4 v[PF_UNROLL];
     uint32_t nx[PF_UNROLL];
@@ -379,7 +414,24 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
   const int64_t stride = (int64_t)gridDim.x * HITS_PER_BLOCK;
   for (int64_t base = (int64_t)blockIdx.x * HITS_PER_BLOCK; base < n; base += stride) {
     const int64_t i = base + sub;
-    if (i < n) {
+    if (i < n && (ghits[i] & 3) == 3) {          // short-literal tier: every literal of the buckets
+      const int64_t p = ghits[i] >> 2;
+      uint32_t m = teddy_mask(T, text, nbytes, p);
+      int64_t line = -1;
+      while (m) {
+        const int b = __ffs(m) - 1;
+        m &= m - 1;
+        for (int j = T.tb_off[b] + lane; j < T.tb_off[b + 1]; j += PV_LANES) {
+          const int32_t e = T.tb_lits[j];
+          if (!pf_lit_at(T, text, nbytes, p, e)) continue;
+          const int lit = pf_entry_lit(e);
+          if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
+          if (line < 0) line = 0;
+          for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
+            app(((int64_t)T.lit_reg[r] << 32) | line);
+        }
+      }
+    } else if (i < n) {
       const int64_t h = ghits[i];
       const int64_t p = h >> 2;
       const int G = 2 + (int)(h & 3);
@@ -519,47 +571,52 @@ void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, i
   LP_CHECK(hipGetLastError());
 }
 
+template <int GM, int S, bool TD>
+static void launch_pf(int g, size_t lds, bool big, hipStream_t st, const uint8_t* text, int64_t nbytes,
+                      const PfTables& T, const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
+                      unsigned long long* count) {
+  if (big)
+    hipLaunchKernelGGL((k_prefilter<GM, S, 4, TD>), dim3(g), dim3(PF_THREADS), lds, st, text, nbytes, T, line_start,
+                       nlines, cand, cap, count);
+  else
+    hipLaunchKernelGGL((k_prefilter<GM, S, 1, TD>), dim3(g), dim3(PF_THREADS), lds, st, text, nbytes, T, line_start,
+                       nlines, cand, cap, count);
+}
+
+template <bool TD>
+static void dispatch_pf(int g, bool big, hipStream_t st, const uint8_t* text, int64_t nbytes, const PfTables& T,
+                        const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
+                        unsigned long long* count) {
+  const int gm = T.gmask & 28;
+  const size_t lds = (gm ? (size_t(1) << T.bloom_bits) / 8 : 0) + (TD ? 4096 : 0) + PF_BUF * 8 + 16;
+#define LP_PF(GMV, SV) launch_pf<GMV, SV, TD>(g, lds, big, st, text, nbytes, T, line_start, nlines, cand, cap, count)
+  if (gm == 16 && T.stride == 4) { LP_PF(16, 4); return; }
+  if (gm == 16 && T.stride == 2) { LP_PF(16, 2); return; }
+  switch (gm) {
+    case 0: if (TD) LP_PF(0, 1); break;      // short literals only
+    case 4: LP_PF(4, 1); break;
+    case 8: LP_PF(8, 1); break;
+    case 12: LP_PF(12, 1); break;
+    case 16: LP_PF(16, 1); break;
+    case 20: LP_PF(20, 1); break;
+    case 24: LP_PF(24, 1); break;
+    default: LP_PF(28, 1); break;
+  }
+#undef LP_PF
+}
+
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream) {
-  if (nbytes <= 0) return;
-  const size_t lds = (size_t(1) << T.bloom_bits) / 8 + PF_BUF * 8 + 16;
-  int64_t units = (nbytes + 15) / 16;
+  if (nbytes <= 0 || ((T.gmask & 28) == 0 && !T.teddy_on)) return;   // no literals: nothing to prefilter
+  const int64_t units = (nbytes + 15) / 16;
   // large texts: 4 units per lane per iteration (bytes in flight); small requests: 1, so every
   // launched lane has work (latency)
   const bool big = nbytes >= (int64_t(32) << 20);
-  int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS * (big ? 4 : 1)));
-#define LP_PF_LAUNCH(GMV, SV, UV)                                                                                   \
-  hipLaunchKernelGGL((k_prefilter<GMV, SV, UV>), dim3(g), dim3(PF_THREADS), lds, as_stream(stream), text, nbytes, T, \
-                     line_start, nlines, cand, cap, count)
-#define LP_PF_CASE(GMV)                   \
-  case GMV:                               \
-    if (big)                              \
-      LP_PF_LAUNCH(GMV, 1, 4);            \
-    else                                  \
-      LP_PF_LAUNCH(GMV, 1, 1);            \
-    break;
-  if (T.stride == 4 && (T.gmask & 28) == 16) {   // 4 adjacent windows per literal: every 4th position
-    if (big)
-      LP_PF_LAUNCH(16, 4, 4);
-    else
-      LP_PF_LAUNCH(16, 4, 1);
-    LP_CHECK(hipGetLastError());
-    return;
-  }
-  if (T.stride == 2 && (T.gmask & 28) == 16) {
-    if (big)
-      LP_PF_LAUNCH(16, 2, 4);
-    else
-      LP_PF_LAUNCH(16, 2, 1);
-    LP_CHECK(hipGetLastError());
-    return;
-  }
-  switch (T.gmask & 28) {
-    LP_PF_CASE(4) LP_PF_CASE(8) LP_PF_CASE(12) LP_PF_CASE(16) LP_PF_CASE(20) LP_PF_CASE(24) LP_PF_CASE(28)
-    default: return;  // no literals: nothing to prefilter
-  }
-#undef LP_PF_CASE
-#undef LP_PF_LAUNCH
+  const int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS * (big ? 4 : 1)));
+  if (T.teddy_on)
+    dispatch_pf<true>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
+  else
+    dispatch_pf<false>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
   LP_CHECK(hipGetLastError());
 }
 
@@ -692,6 +749,7 @@ int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos) 
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap) {
   std::vector<std::vector<int64_t>> part(std::max(1, host_threads()));
+  const int S = std::max(1, T.stride);
   host_parallel(nbytes, 1 << 18, [&](int t, int64_t a, int64_t b) {
     auto& out = part[t];
     auto app = [&](int64_t v) { out.push_back(v); };
@@ -700,11 +758,18 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
     uint32_t g4 = 0;
     for (int k = 3; k >= 0; --k) g4 = (g4 << 8) | (uint32_t)(a + k < nbytes ? lower_byte(text[a + k]) : 0);
     for (int64_t p = a; p < b; ++p) {
-      for (int g = 4; g >= 2; --g) {
-        if (!(T.gmask & (1 << g))) continue;
-        const uint32_t key = g4 & gram_mask(g);
-        if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
-        pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
+      // bloom tier: like k_prefilter<GM, S>, only positions divisible by the stride (one
+      // candidate per literal occurrence, not one per indexed window)
+      if (p % S == 0)
+        for (int g = 4; g >= 2; --g) {
+          if (!(T.gmask & (1 << g))) continue;
+          const uint32_t key = g4 & gram_mask(g);
+          if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
+          pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
+        }
+      if (T.teddy_on) {
+        const uint32_t m = teddy_mask(T, text, nbytes, p);
+        if (m) teddy_probe(T, text, nbytes, p, m, line_start, nlines, nullptr, app);
       }
       g4 = (g4 >> 8) | ((uint32_t)(p + 4 < nbytes ? lower_byte(text[p + 4]) : 0) << 24);
     }

@@ -934,6 +934,7 @@ Compiled compile(const std::string& pattern, int max_dfa_states, int max_positio
     root = P.parse();
     nodes = std::move(P.nodes);
     wordb = P.uses_wordb;
+    out.wordb = wordb;
   } catch (const SyntaxError& e) {
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   } catch (const Unsupported& e) {
@@ -976,6 +977,155 @@ Compiled compile(const std::string& pattern, int max_dfa_states, int max_positio
     out.kind = Kind::NFA; out.error = e.what();
   }
   return out;
+}
+
+// ------------------------------------------------------------------------------------------
+// multi-regex DFA: subset construction over the union of the members' position NFAs
+namespace {
+
+struct Member {
+  int off = 0;
+  const Nfa* nfa = nullptr;
+};
+
+uint32_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t>& A, int prev, int next) {
+  const uint16_t bit = (uint16_t)(1u << ctx_index(prev, next));
+  uint32_t m = 0;
+  for (size_t r = 0; r < M.size(); ++r) {
+    const Nfa& n = *M[r].nfa;
+    bool ok = (n.nullable & bit) != 0;
+    for (size_t i = 0; !ok && i < n.last.size(); ++i) {
+      const int p = M[r].off + n.last[i].to;
+      ok = ((A[p >> 6] >> (p & 63)) & 1) && (n.last[i].cond & bit);
+    }
+    if (ok) m |= 1u << r;
+  }
+  return m;
+}
+
+}  // namespace
+
+MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states) {
+  if (patterns.empty() || patterns.size() > (size_t)MULTI_MAX_REGS) throw Unsupported("multi-DFA: 1..16 regexes");
+  std::vector<Compiled> comp;
+  comp.reserve(patterns.size());
+  bool wordb = false;
+  for (auto& p : patterns) {
+    comp.push_back(compile(p, 4, 4096));
+    const Compiled& c = comp.back();
+    if (c.kind != Kind::DFA && c.kind != Kind::NFA) throw Unsupported("multi-DFA member is not an automaton regex");
+    wordb |= c.wordb;
+  }
+  std::vector<Member> M(comp.size());
+  int np = 0;
+  for (size_t r = 0; r < comp.size(); ++r) {
+    M[r].off = np;
+    M[r].nfa = &comp[r].nfa;
+    np += comp[r].nfa.npos;
+  }
+  std::vector<const ByteSet*> cls(np);
+  std::vector<std::vector<Edge>> follow(np);
+  std::vector<Edge> first;
+  bool restartable = false;
+  for (auto& m : M) {
+    for (int p = 0; p < m.nfa->npos; ++p) {
+      cls[m.off + p] = &m.nfa->cls[p];
+      for (auto& e : m.nfa->follow[p]) follow[m.off + p].push_back({m.off + e.to, e.cond});
+    }
+    for (auto& e : m.nfa->first) {
+      first.push_back({m.off + e.to, e.cond});
+      if (e.cond & CTX_NOT_BOS) restartable = true;
+    }
+    if (m.nfa->nullable & CTX_NOT_BOS) restartable = true;
+  }
+  MultiDfa d;
+  d.nregs = (int)M.size();
+  // byte classes: (membership in every distinct position class, word byte, UTF-8 continuation)
+  std::vector<ByteSet> dcls;
+  for (int p = 0; p < np; ++p) {
+    bool f = false;
+    for (auto& x : dcls) if (x == *cls[p]) { f = true; break; }
+    if (!f) dcls.push_back(*cls[p]);
+  }
+  std::map<std::vector<bool>, int> sig2cls;
+  d.bytemap.assign(256, 0);
+  std::vector<int> rep;
+  for (int b = 0; b < 256; ++b) {
+    std::vector<bool> sig;
+    for (auto& x : dcls) sig.push_back(x.test(b));
+    sig.push_back(is_word_byte(b));
+    sig.push_back(b >= 0x80 && b <= 0xBF);
+    auto it = sig2cls.find(sig);
+    int k;
+    if (it == sig2cls.end()) { k = (int)rep.size(); sig2cls[sig] = k; rep.push_back(b); }
+    else k = it->second;
+    d.bytemap[b] = (uint8_t)k;
+  }
+  d.nclasses = (int)rep.size();
+  if (d.nclasses > 256) throw Unsupported("too many byte classes");
+  const int nw = (np + 63) / 64 + 1;   // last word: prev kind
+  std::unordered_map<std::vector<uint64_t>, int, KeyHash> ids;
+  std::vector<std::vector<uint64_t>> states;
+  auto intern = [&](std::vector<uint64_t>& key) -> int {
+    auto it = ids.find(key);
+    if (it != ids.end()) return it->second;
+    const int id = (int)states.size() + 1;       // 0 = DEAD
+    if (id >= max_states || id > 0xFFFF) throw Unsupported("multi-DFA state limit");
+    ids.emplace(key, id);
+    states.push_back(key);
+    return id;
+  };
+  std::vector<uint64_t> init(nw, 0);
+  init[nw - 1] = P_BOS;
+  intern(init);
+  std::vector<uint32_t> rows, fin;
+  for (size_t si = 0; si < states.size(); ++si) {
+    const std::vector<uint64_t> A = states[si];
+    const int prev = (int)A[nw - 1];
+    fin.push_back(member_accepts(M, A, prev, N_EOS));
+    fin.push_back(member_accepts(M, A, prev, N_FT));
+    uint32_t acc_k[5];
+    for (int nk = 0; nk < 5; ++nk) acc_k[nk] = member_accepts(M, A, prev, nk);
+    for (int k = 0; k < d.nclasses; ++k) {
+      const int c = rep[k];
+      const int nk = is_word_byte(c) ? N_W : (c >= 0x80 && c <= 0xBF) ? N_C : N_N;
+      const uint16_t bit = (uint16_t)(1u << ctx_index(prev, nk));
+      std::vector<uint64_t> B(nw, 0);
+      bool any = false;
+      for (int p = 0; p < np; ++p) {
+        if (!(A[p >> 6] >> (p & 63) & 1)) continue;
+        for (auto& e : follow[p])
+          if ((e.cond & bit) && cls[e.to]->test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
+      }
+      for (auto& e : first)
+        if ((e.cond & bit) && cls[e.to]->test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
+      uint32_t next = 0;
+      if (any || restartable) {
+        B[nw - 1] = (uint64_t)((nk == N_W && wordb) ? P_W : P_N);
+        next = (uint32_t)intern(B);
+      }
+      rows.push_back(next | (acc_k[nk] << 16));
+    }
+  }
+  d.nstates = (int)states.size() + 1;
+  d.trans.assign((size_t)d.nclasses, 0);            // DEAD row
+  d.trans.insert(d.trans.end(), rows.begin(), rows.end());
+  d.fin.assign(2, 0);
+  d.fin.insert(d.fin.end(), fin.begin(), fin.end());
+  return d;
+}
+
+uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n) {
+  int64_t ft = n - final_terminator_len(s, n);
+  if (ft == n) ft = -1;
+  uint32_t st = 1, acc = 0;
+  for (int64_t t = 0; t < n; ++t) {
+    if (t == ft) acc |= d.fin[2 * st + 1];
+    const uint32_t e = d.trans[(size_t)st * d.nclasses + d.bytemap[s[t]]];
+    acc |= e >> 16;
+    st = e & 0xFFFF;
+  }
+  return acc | d.fin[2 * st];
 }
 
 }  // namespace lp

@@ -69,6 +69,7 @@ struct Dfa {
 
 struct Compiled {
   Kind kind = Kind::INVALID;
+  bool wordb = false;                       // uses \b / \B (prev-byte wordness matters)
   std::string error;                        // reason for FALLBACK / INVALID
   std::vector<std::string> literals;        // OR-set of required factors (ASCII-lowercased bytes)
   bool has_literals = false;
@@ -77,6 +78,26 @@ struct Compiled {
 };
 
 Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions);
+
+// Multi-regex DFA ("scan group"): the Glushkov NFAs of up to 16 regexes determinised TOGETHER, so
+// one table walk per byte answers find() for all of them (Aho-Corasick / RE2::Set style). Used
+// for regexes without a usable literal factor, which must be run over every line. Unlike the
+// single-regex DFA there is no absorbing ACCEPT state: a transition reports the regexes that
+// accept BEFORE its byte and the walk goes on for the others.
+//   trans[s * nclasses + cls] = next state (bits 0..15) | accept mask (bits 16..31)
+//   fin[2 s] = regexes accepting at end of line, fin[2 s + 1] = before a final line terminator
+// State 0 = DEAD (every member anchored and failed), state 1 = start of line.
+constexpr int MULTI_MAX_REGS = 16;
+struct MultiDfa {
+  int nstates = 0, nclasses = 0, nregs = 0;
+  std::vector<uint8_t> bytemap;
+  std::vector<uint32_t> trans;
+  std::vector<uint32_t> fin;
+};
+// throws Unsupported (state limit, > MULTI_MAX_REGS, a member that is not an automaton regex)
+MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states);
+// bit r set <=> patterns[r] finds a match in s[0..n) (host walk; the device kernel is k_scan_multi)
+uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n);
 
 // Host-side exact match of one line with a compiled DFA (CPU backend + tests).
 bool dfa_find(const Dfa& d, const uint8_t* s, int64_t n);

@@ -25,6 +25,7 @@ SOURCES = [
     ("regex/jregex.cpp", "cpp"),
     ("kernels/lp_kernels.hip", "hip"),
     ("kernels/nfa_mfma.hip", "hip"),
+    ("kernels/scan_multi.hip", "hip"),
     ("kernels/lp_post.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),

@@ -274,8 +274,10 @@ class Engine:
         self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
         if self.device.type == "cuda":
             props = torch.cuda.get_device_properties(self.device)
-            self.pf_grid = int(props.multi_processor_count) * 4
+            self.n_cus = int(props.multi_processor_count)
+            self.pf_grid = self.n_cus * 4
         else:
+            self.n_cus = 1
             self.pf_grid = 1
 
     # ------------------------------------------------------------------ staging
@@ -318,7 +320,9 @@ class Engine:
         cand = K.prefilter(text, nbytes, self.tabs["pf"], ls, self.cand_cap, self.pf_grid)
         t = self._tick(timings, "prefilter", t)
         extra = []
-        if self.tabs["scan_regs"].numel():
+        for sp in self.tabs["scan_passes"]:        # literal-free regexes: multi-regex DFAs in LDS
+            extra.append(K.scan_multi(text, ls, ll, sp, max(1024, ls.numel() >> 6), self.scan_grid(sp)))
+        if self.tabs["scan_regs"].numel():        # one whose DFA alone exceeds a scan group
             extra.append(K.scan(text, ls, ll, self.tabs["scan_regs"], self.tabs["dfa"], max(1024, ls.numel())))
         for ncls, glist in self.tabs["nfa_scan_lists"].items():       # DFA blow-up regexes: MFMA NFA
             if glist.numel():
@@ -329,6 +333,13 @@ class Engine:
             t = self._tick(timings, "scan", t)
             return torch.cat([cand] + extra), cand.numel()
         return cand, cand.numel()
+
+    def scan_grid(self, sp: tuple) -> int:
+        """Persistent grid of k_scan_multi: as many blocks per CU as the pass's LDS blob allows."""
+        if self.device.type != "cuda":
+            return 0
+        per_cu = max(1, min(8, (160 << 10) // max(sp[1] * 4, 1)))       # sp[1] = LDS words
+        return self.n_cus * per_cu
 
     def _ev_tables(self, segs: "Segments") -> tuple:
         return K.ev_tables(self.tabs, segs, len(self.lib.freq_ids), len(self.lib.patterns))

@@ -45,6 +45,13 @@ CONTEXT_REGEXES = (ERROR_RE, WARN_RE, STACK_RE, EXC_RE)
 _SPLIT = re.compile(r"\r?\n")
 
 
+
+def java_blank(pid) -> bool:
+    """``id == null || id.trim().isEmpty()`` (FrequencyTrackingService.java:42,65). Java's
+    String.trim() strips every char <= U+0020 (controls included) and nothing else: "\x01" is
+    blank, a non-breaking space (U+00A0) or "\u2003" is not -- unlike Python's str.strip()."""
+    return pid is None or all(ord(c) <= 0x20 for c in pid)
+
 def split_lines(logs: str) -> List[str]:
     """Java ``String.split("\\r?\\n")`` (limit 0)."""
     if _SPLIT.search(logs) is None:
@@ -78,7 +85,7 @@ class FrequencyTracker:
             dq.popleft()
 
     def record(self, pid: Optional[str]) -> None:
-        if pid is None or pid.strip() == "":
+        if java_blank(pid):
             return
         with self._lock:
             self._ts.setdefault(pid, deque()).append(self.clock())
@@ -95,7 +102,7 @@ class FrequencyTracker:
         return self.count(pid) / float(self.params.freq_window_hours)
 
     def penalty(self, pid: Optional[str]) -> float:
-        if pid is None or pid.strip() == "":
+        if java_blank(pid):
             return 0.0
         with self._lock:
             if pid not in self._ts:

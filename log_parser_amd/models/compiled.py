@@ -27,7 +27,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
-from ..golden import CONTEXT_REGEXES, SEVERITY_MULTIPLIERS, severity_key
+from ..golden import CONTEXT_REGEXES, SEVERITY_MULTIPLIERS, java_blank, severity_key
 from ..native import N
 from ..utils.config import ScoringParams
 from .nfa import build_group, fits_group, pack_groups
@@ -61,6 +61,11 @@ _FREQ = {**{c: f * 0.55 for c, f in zip(b"etaoinshrdlcumwfgypbvkjxqz",
 
 
 PF_STRIDE_MAX = 4      # largest prefilter sampling stride (1, 2 or 4); 1 disables sampling
+PF_TEDDY = True        # short literals (3..6 bytes) on the byte-position (Teddy) tier
+TEDDY_MIN, TEDDY_MAX = 3, 6
+TEDDY_BUCKETS = 32
+TEDDY_MAX_LITS = 2048  # beyond this the buckets saturate: extra short literals join the bloom tier
+MIN_LITERAL = 3        # a regex whose required-literal set has a shorter member scans every line
 
 # gram entries: gram_lits value = literal id | (window offset << LIT_OFF_SHIFT)
 LIT_OFF_SHIFT = 22
@@ -75,9 +80,10 @@ def _window_cost(w: bytes) -> float:
 def _choose_grams(lits: List[bytes], stride: int = 1) -> List[List[Tuple[int, int, int]]]:
     """Per literal, the ``stride`` adjacent g-byte windows [(key, g, offset), ...] to index, rarest
     estimated text frequency first, with a mild penalty for windows already shared by other
-    literals (each sharer costs a compare). With stride 2 every occurrence of the literal has one
-    indexed window starting at an even text position, so the device prefilter tests every other
-    position only (k_prefilter<GM, 2>); callers pass stride 2 only when every literal has >= 5 bytes."""
+    literals (each sharer costs a compare). With stride S in {2, 4} every occurrence of the literal
+    has exactly one indexed window starting at a text position divisible by S, so the device
+    prefilter tests every S-th position only (k_prefilter<GM, S>); callers pass stride S only when
+    every literal has >= S + 3 bytes (S adjacent 4-byte windows)."""
     import math
     used: Dict[Tuple[int, int], int] = {}
     out = []
@@ -103,6 +109,33 @@ def _choose_grams(lits: List[bytes], stride: int = 1) -> List[List[Tuple[int, in
             ents.append((key, g, off))
         out.append(ents)
     return out
+
+
+def _teddy_tables(lits: List[bytes], ids: List[int]):
+    """Byte-position masks of the short-literal tier: (table uint32[256, 4] = M0 | M1 | M2 | 0 per
+    byte value, bucket CSR offsets int32[B + 1], bucket entries = literal id | window offset << 22).
+    Each literal indexes its rarest 3-byte window; literals are sorted by window and cut into
+    contiguous buckets, so a bucket's members share leading bytes and its masks stay sparse."""
+    tab = np.zeros((256, 4), np.uint32)
+    if not lits:
+        return tab, np.zeros(TEDDY_BUCKETS + 1, np.int32), np.zeros(1, np.int32)
+    win = []
+    for lit, i in zip(lits, ids):
+        o = min(range(len(lit) - 2), key=lambda k: (_window_cost(lit[k:k + 3]), k))
+        win.append((lit[o:o + 3], o, i))
+    win.sort()
+    B = min(TEDDY_BUCKETS, len(win))
+    members: List[List[int]] = [[] for _ in range(TEDDY_BUCKETS)]
+    for r, (w, o, i) in enumerate(win):
+        b = r * B // len(win)
+        for j in range(3):
+            tab[w[j], j] |= np.uint32(1 << b)
+        members[b].append(i | (o << LIT_OFF_SHIFT))
+    off = np.zeros(TEDDY_BUCKETS + 1, np.int32)
+    for b in range(TEDDY_BUCKETS):
+        off[b + 1] = off[b] + len(members[b])
+    ent = np.array([e for m in members for e in m] or [0], np.int32)
+    return tab, off, ent
 
 
 def _u32(x):
@@ -218,7 +251,7 @@ class CompiledLibrary:
                     seq_ev_reg.append(self._reg(ev.regex, "sequence"))
                 seq_ev_off.append(len(seq_ev_reg))
             seq_off.append(len(seq_bonus))
-            if pat.id is not None and pat.id.strip() != "":
+            if not java_blank(pat.id):
                 if pat.id not in fid:
                     fid[pat.id] = len(self.freq_ids)
                     self.freq_ids.append(pat.id)
@@ -267,6 +300,8 @@ class CompiledLibrary:
                 toff += t.size
                 aoff += a.size
                 lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
+                if lits and min(len(x) for x in lits) < MIN_LITERAL:
+                    lits = []          # a 1-2-byte factor selects nothing: scan every line
                 # anchored regexes (e.g. '^\\s*at\\s+...') die within a few bytes of every line:
                 # scanning all lines beats a short, unselective literal.
                 if d["anchored"] and lits and min(len(x) for x in lits) < 4:
@@ -301,12 +336,150 @@ class CompiledLibrary:
         self.nfa_group_ncls = list(ncls)
         self.nfa_scan_groups = list(range(1, len(groups)))
         self.nfa_regs = [rid for g in groups[1:] for rid, _ in g]
+        self._build_scan_passes()
         self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
         self.dfa_bytemap = np.concatenate(bytemaps)
         self.dfa_trans = np.concatenate(trans)
         self.dfa_acc = np.concatenate(accs)
 
+    # multi-regex DFA scan groups (csrc/kernels/scan_multi.hip)
+    SCAN_GROUP_REGS = 16            # members per multi-regex DFA (16-bit accept masks)
+    SCAN_GROUP_BYTES = 24 << 10     # LDS bytes of one group's uint16 transition rows
+    SCAN_PASS_ROWS = 48 << 10       # LDS bytes of one pass's rows (+ 1 KiB bm4)
+    SCAN_MAX_STATES = 4096
+
+    @staticmethod
+    def _row_stride(d) -> int:
+        ncol = d["nclasses"] + 2                      # hold, '\n', classes
+        return ncol if ncol % 2 else ncol + 1         # odd: rows start on spread-out banks
+
+    def _build_scan_passes(self):
+        """Literal-free regexes -> multi-regex DFA groups (greedy, in registry order: a regex joins
+        the open group while the union DFA stays within the state / LDS budget) -> passes of up to
+        4 groups whose tables fit in LDS together. A regex whose DFA alone does not fit stays on the
+        one-regex-per-walk scan (``scan_regs_single``)."""
+        groups: List[Tuple[List[int], dict]] = []
+        single: List[int] = []
+        cur: List[int] = []
+        cur_d = None
+
+        def fits(d):
+            return (d is not None and 2 * (d["nclasses"] + 2) <= 255
+                    and d["nstates"] * self._row_stride(d) * 2 <= self.SCAN_GROUP_BYTES)
+
+        for r in self.scan_regs:
+            if cur and len(cur) < self.SCAN_GROUP_REGS:
+                d = N.compile_multi([self.regexes[x].pattern for x in cur + [r]], self.SCAN_MAX_STATES)
+                if fits(d):
+                    cur.append(r)
+                    cur_d = d
+                    continue
+            if cur:
+                groups.append((cur, cur_d))
+            d = N.compile_multi([self.regexes[r].pattern], self.SCAN_MAX_STATES)
+            if fits(d):
+                cur, cur_d = [r], d
+            else:
+                cur, cur_d = [], None
+                single.append(r)
+        if cur:
+            groups.append((cur, cur_d))
+        self.scan_groups = groups
+        self.scan_regs_single = single
+        passes, cur_p, size = [], [], 0
+        for regs, d in groups:
+            gb = d["nstates"] * self._row_stride(d) * 2
+            if cur_p and (len(cur_p) == 4 or size + gb > self.SCAN_PASS_ROWS):
+                passes.append(cur_p)
+                cur_p, size = [], 0
+            cur_p.append((regs, d))
+            size += gb
+        if cur_p:
+            passes.append(cur_p)
+        self.scan_passes = [self._scan_blob(p) for p in passes]
+
+    @classmethod
+    def _scan_blob(cls, groups) -> dict:
+        """One pass -> the blob of scan_multi.hip (uint32 words): [bm4 | u16 rows] staged in LDS,
+        then the exact tables the rare path reads from global memory. States are renumbered so
+        that the ones from which a member can accept come last (the hot loop's threshold test)."""
+        BM_BYTES = 1024                                     # bm4 at LDS byte 0, rows after it
+        rows16, exact, fins = [], [], []
+        meta = {k: [0] * 4 for k in ("row_base", "stride", "thr", "init_row", "init_state", "ncol")}
+        bm4 = np.zeros(256, np.uint32)
+        base = BM_BYTES // 2                                # in uint16 entries
+        for g, (regs, d) in enumerate(groups):
+            ns, nc = d["nstates"], d["nclasses"]
+            t = np.frombuffer(d["trans"], np.uint32).reshape(ns, nc)
+            fin = np.frombuffer(d["fin"], np.uint32).reshape(ns, 2)
+            accepting = ((t >> np.uint32(16)) != 0).any(axis=1) | (fin != 0).any(axis=1)
+            order = np.concatenate([np.flatnonzero(~accepting), np.flatnonzero(accepting)])
+            new_of = np.empty(ns, np.uint32)
+            new_of[order] = np.arange(ns, dtype=np.uint32)
+            ncol = nc + 2
+            stride = cls._row_stride(d)
+            init_new = int(new_of[1])
+            # exact table (state ids), rows in the new order
+            ex = np.zeros((ns, ncol), np.uint32)
+            ex[:, 0] = np.arange(ns, dtype=np.uint32)                         # hold
+            ex[:, 1] = np.uint32(init_new) | (fin[order, 0] << np.uint32(16))  # '\n': restart + EOL accepts
+            to = t[order]
+            ex[:, 2:] = new_of[to & np.uint32(0xFFFF)] | (to & np.uint32(0xFFFF0000))
+            exact.append(ex.reshape(-1))
+            fins.append(fin[order].reshape(-1))
+            # LDS rows: byte offset of the next state's row
+            rowb = (2 * (base + np.arange(ns, dtype=np.int64) * stride)).astype(np.int64)
+            r16 = np.zeros((ns, stride), np.uint16)
+            r16[:, :ncol] = rowb[ex & np.uint32(0xFFFF)].astype(np.uint16)
+            rows16.append(r16.reshape(-1))
+            meta["row_base"][g], meta["stride"][g] = 2 * base, stride
+            meta["thr"][g] = int(2 * (base + int((~accepting).sum()) * stride))
+            meta["init_row"][g], meta["init_state"][g], meta["ncol"][g] = int(rowb[init_new]), init_new, ncol
+            base += ns * stride
+            col2 = (np.frombuffer(d["bytemap"], np.uint8).astype(np.uint32) + np.uint32(2)) * np.uint32(2)
+            col2[10] = 2                                                      # '\n': never inside a line
+            col2[0xFF] = 0                                                    # 0xFF: hold (masked bytes)
+            bm4 |= col2 << np.uint32(8 * g)
+        if 2 * base > 0xFFFF:
+            raise ValueError("scan pass rows exceed the uint16 byte offset")
+        r = np.concatenate(rows16)
+        if r.size % 8:
+            r = np.concatenate([r, np.zeros(8 - r.size % 8, np.uint16)])      # whole uint4 words
+        parts = [bm4, r.view(np.uint32)]
+        off = 256 + r.size // 2
+        lds_words = off
+        gt_off, fin_off = [0] * 4, [0] * 4
+        for g in range(len(groups)):
+            gt_off[g] = off
+            parts.append(exact[g])
+            off += exact[g].size
+        for g in range(len(groups)):
+            fin_off[g] = off
+            parts.append(fins[g])
+            off += fins[g].size
+        rid = np.zeros(16 * 4, np.uint32)
+        for g, (regs, _) in enumerate(groups):
+            rid[16 * g:16 * g + len(regs)] = regs
+        rid_off = off
+        parts.append(rid)
+        blob = np.concatenate(parts)
+        return dict(blob=blob, lds_words=lds_words, ngroups=len(groups), gt_off=tuple(gt_off),
+                    fin_off=tuple(fin_off), bm_off=0, rid_off=rid_off,
+                    regs=[x for regs, _ in groups for x in regs], **{k: tuple(v) for k, v in meta.items()})
+
     def _build_prefilter(self):
+        """Two literal tiers, both tested by k_prefilter in one pass over the text:
+
+        * long literals (>= 7 bytes): a blocked bloom filter of 4-byte windows in LDS, with
+          stride-S sampling -- S adjacent windows per literal, every S-th text position tested;
+        * short literals (3..6 bytes, ``PF_TEDDY``): a Teddy-style byte-position filter. Each
+          literal picks its rarest 3-byte window and a bucket (<= 32); table entry c holds, for
+          window offsets 0/1/2, the buckets whose window has byte c there, so a position is a
+          candidate iff M0[b_p] & M1[b_p+1] & M2[b_p+2] != 0 -- one 16-byte LDS read per text
+          byte instead of a hash per position, and one short literal no longer drags the whole
+          library down to stride 1.
+
+        Both tiers verify whole literals (k_pf_verify) before producing (regex, line) candidates."""
         lit_ids: Dict[bytes, int] = {}
         lit_regs: List[List[int]] = []
         for i, ri in enumerate(self.regexes):
@@ -330,18 +503,25 @@ class CompiledLibrary:
         for i, rr in enumerate(lit_regs):
             lit_reg_off[i + 1] = lit_reg_off[i] + len(rr)
         lit_reg = np.array([r for rr in lit_regs for r in rr] or [0], np.int32)
+        # ---- tier split
+        short = []
+        if PF_TEDDY:
+            short = [i for i, l in enumerate(lits) if TEDDY_MIN <= len(l) <= TEDDY_MAX and 0 not in l]
+            short = short[:TEDDY_MAX_LITS]
+        sset = set(short)
+        long_ids = [i for i in range(len(lits)) if i not in sset]
+        teddy, tb_off, tb_lits = _teddy_tables([lits[i] for i in short], short)
+        # ---- bloom tier: stride-S sampling needs S adjacent 4-byte windows per literal (>= S + 3 bytes)
         grams: Dict[Tuple[int, int], List[int]] = {}
         gmask = 0
-        # stride-2 sampling needs two adjacent 4-byte windows per literal (>= 5 bytes each)
-        # stride-S sampling needs S adjacent 4-byte windows per literal (>= S + 3 bytes each)
         stride = 1
-        if lits and len(lits) < (1 << LIT_OFF_SHIFT):
-            shortest = min(len(l) for l in lits)
+        if long_ids and len(lits) < (1 << LIT_OFF_SHIFT):
+            shortest = min(len(lits[i]) for i in long_ids)
             for s_ in (4, 2):
                 if PF_STRIDE_MAX >= s_ and shortest >= s_ + 3:
                     stride = s_
                     break
-        for i, ents in enumerate(_choose_grams(lits, stride)):
+        for i, ents in zip(long_ids, _choose_grams([lits[i] for i in long_ids], stride)):
             for key, g, off in ents:
                 grams.setdefault((key, g), []).append(i | (off << LIT_OFF_SHIFT))
                 gmask |= 1 << g
@@ -365,7 +545,8 @@ class CompiledLibrary:
             gram_lits.extend(ids)
         self.pf = dict(bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
                        gram_lits=np.array(gram_lits or [0], np.int32), lit_off=lit_off, lit_bytes=lit_bytes,
-                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, stride=stride)
+                       lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, stride=stride,
+                       teddy=teddy, tb_off=tb_off, tb_lits=tb_lits, teddy_lits=len(short))
 
     # ------------------------------------------------------------------ device tables
     def device_tables(self, device: torch.device) -> dict:
@@ -381,15 +562,19 @@ class CompiledLibrary:
         pf = self.pf
         t["pf_arrays"] = [T(pf["bloom"]), T(pf["ht_key"].view(np.int64)), T(pf["ht_val"]), T(pf["ht_cnt"]),
                           T(pf["gram_lits"]), T(pf["lit_off"]), T(pf["lit_bytes"]), T(pf["lit_reg_off"]),
-                          T(pf["lit_reg"])]
+                          T(pf["lit_reg"]), T(pf["teddy"]), T(pf["tb_off"]), T(pf["tb_lits"])]
         a = t["pf_arrays"]
         t["pf"] = (a[0].data_ptr(), pf["bits"], a[1].data_ptr(), a[2].data_ptr(), a[3].data_ptr(), pf["ht_mask"],
                    a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"],
-                   pf["stride"])
+                   pf["stride"], a[9].data_ptr(), a[10].data_ptr(), a[11].data_ptr(), 1 if pf["teddy_lits"] else 0)
         t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc)]
         d = t["dfa_arrays"]
         t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr())
-        t["scan_regs"] = T(np.array(self.scan_regs, np.int32))
+        t["scan_regs"] = T(np.array(self.scan_regs_single, np.int32))
+        t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
+        t["scan_passes"] = [(b.data_ptr(), p["lds_words"], p["ngroups"], p["row_base"], p["stride"], p["thr"],
+                             p["init_row"], p["init_state"], p["ncol"], p["gt_off"], p["fin_off"], p["bm_off"],
+                             p["rid_off"]) for b, p in zip(t["scan_blobs"], self.scan_passes)]
         t["conf"], t["sev"] = T(self.conf), T(self.sev)
         t["ctx_before"], t["ctx_after"] = T(self.ctx_before), T(self.ctx_after)
         t["sec_off"], t["sec_reg"], t["sec_w"], t["sec_weight"] = T(self.sec_off), T(self.sec_reg), T(self.sec_w), T(self.sec_weight)
@@ -428,6 +613,8 @@ class CompiledLibrary:
             "patterns": len(self.patterns), "pattern_sets": len(self.pattern_sets), "regexes": len(self.regexes),
             "dfa": kinds.count(KIND_DFA), "host_fallback": len(self.host_regs),
             "invalid": kinds.count(KIND_INVALID), "scan_all": len(self.scan_regs), "literals": len(self.literals),
+            "teddy_literals": int(self.pf["teddy_lits"]), "prefilter_stride": int(self.pf["stride"]),
+            "scan_groups": len(self.scan_groups), "scan_passes": len(self.scan_passes),
             "nfa_mfma": len(self.nfa_regs), "nfa_groups": len(self.nfa_scan_groups),
             "halo": self.halo,
         }

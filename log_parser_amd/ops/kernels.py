@@ -181,6 +181,27 @@ def scan(text, line_start, line_len, regs: torch.Tensor, dfa_tuple, cap: int) ->
         cap = c
 
 
+def scan_multi(text, line_start, line_len, pass_tuple, cap: int, grid: int = 1024) -> torch.Tensor:
+    """Literal-free regexes of one scan pass (<= 4 multi-regex DFA groups) over every line ->
+    (regex << 32 | line) hits, already verified."""
+    nlines = line_start.numel()
+    if nlines == 0:
+        return torch.empty(0, dtype=torch.int64, device=text.device)
+    while True:
+        out = torch.empty(max(cap, 1), dtype=torch.int64, device=text.device)
+        if text.is_cuda:
+            cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
+            N.scan_multi(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), nlines, pass_tuple,
+                         out.data_ptr(), cap, cnt.data_ptr(), grid, _s(text), True)
+            c = int(cnt.item())
+        else:
+            c = N.scan_multi(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), nlines, pass_tuple,
+                             out.data_ptr(), cap, 0, 0, 0, False)
+        if c <= cap:
+            return out[:c]
+        cap = c
+
+
 def context_features(lines: torch.Tensor, L: int, text, line_start, line_len, dfa_tuple) -> torch.Tensor:
     """uint8 feature bits per line (ERR 1, WARN 2, STACK 4, EXC 8) for the given line ids; 0 elsewhere."""
     feat = torch.zeros(max(L, 1), dtype=torch.uint8, device=text.device)

@@ -42,6 +42,17 @@ from ..utils.metrics import Metrics
 log = logging.getLogger("log_parser_amd.server")
 
 INVALID = b'{"error":"Invalid PodFailureData provided"}'
+UNSUPPORTED = b'{"error":"Content-Type must be application/json"}'
+
+
+def json_media_type(content_type: Optional[str]) -> bool:
+    """``@Consumes(MediaType.APPLICATION_JSON)`` (Parse.java:42): the media type of the request's
+    Content-Type (parameters such as ``charset`` ignored, case-insensitive) must be
+    application/json, else HTTP 415. A request without the header is accepted (JAX-RS leaves it to
+    the implementation; parity unpinned -- no JVM here to check Quarkus)."""
+    if content_type is None:
+        return True
+    return content_type.split(";", 1)[0].strip().lower() == "application/json"
 
 
 class Batcher:
@@ -309,8 +320,11 @@ class Service:
             return 400, self.JSON, b'{"error":"PodFailureData.logs must be a string"}'
         return logs, name
 
-    def parse_body(self, body: bytes, t0: float):
+    def parse_body(self, body: bytes, t0: float, content_type: Optional[str] = None):
         """Raw /parse body -> (status, content type, bytes) or a Future of the JSON bytes."""
+        if not json_media_type(content_type):
+            self.metrics.observe_request(415, time.perf_counter() - t0, 0)
+            return 415, self.JSON, UNSUPPORTED
         r = self.decode_body(body, t0)
         if len(r) == 3:
             return r
@@ -374,7 +388,7 @@ def create_app(config: Optional[Config] = None, engine: Optional[Engine] = None,
     @app.post("/parse")
     async def parse(request: Request):
         t0 = time.perf_counter()
-        r = svc.parse_body(await request.body(), t0)
+        r = svc.parse_body(await request.body(), t0, request.headers.get("content-type"))
         if isinstance(r, tuple):
             return _resp(r)
         return Response(await asyncio.wrap_future(r), media_type="application/json")

@@ -47,6 +47,13 @@ def _literal_free(rng: random.Random, i: int) -> Tuple[str, str]:
     noise text of ``make_log`` never matches."""
     fam = i % 6
     a, b = 3 + (i // 6) % 3, 2 + (i // 18) % 6
+    rx, sample = _literal_free_shape(rng, fam, a, b)
+    if i >= 108:                     # past one cycle of shapes: an optional tail keeps them distinct
+        rx += rf"(?:~{i // 108})?"
+    return rx, sample
+
+
+def _literal_free_shape(rng: random.Random, fam: int, a: int, b: int) -> Tuple[str, str]:
     up = "".join(rng.choice("ABCDEFGHJKLMNPQRSUVWXY") for _ in range(a + 1))
     dg = "".join(rng.choice("0123456789") for _ in range(b))
     if fam == 0:

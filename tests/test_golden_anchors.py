@@ -105,3 +105,30 @@ def test_pack_split_docs_equals_java_split():
             assert got == golden.split_lines(s), (d, s[:40])
     assert N.pack_split_docs(docs, buf.ctypes.data, 10, 1) == total       # too small: needed size
     assert N.pack_split_docs(["a\ud800b"], buf.ctypes.data, buf.size, 1) is None   # lone surrogate
+
+
+def test_blank_pattern_ids_follow_java_trim():
+    """FrequencyTrackingService.java:42,65 -- ``id.trim().isEmpty()``: Java trims every char <=
+    U+0020 and nothing else. Ids made of control chars are blank (never penalised); a non-breaking
+    or em space is a real id (penalised past the threshold), unlike Python's str.strip()."""
+    import torch
+    from log_parser_amd.engine import Engine
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.models.schema import PatternSet
+    from log_parser_amd.utils.config import Config
+    assert golden.java_blank(None) and golden.java_blank("") and golden.java_blank(" \t\x01\x1f")
+    assert not golden.java_blank("\u00a0") and not golden.java_blank("\u2003") and not golden.java_blank(" a ")
+    ids = ["\x01", "\u00a0", "\u2003 ", " \x0b "]
+    pats = [{"id": pid, "name": f"p{i}", "severity": "HIGH",
+             "primary_pattern": {"regex": f"tok{i}x", "confidence": 0.5}} for i, pid in enumerate(ids)]
+    sets = [PatternSet.model_validate({"metadata": {"library_id": "ids"}, "patterns": pats})]
+    logs = "\n".join(f"line tok{k % 4}x here" for k in range(100))
+    p = ScoringParams()
+    lib = CompiledLibrary(sets, p)
+    assert lib.freq_ids == ["\u00a0", "\u2003 "]
+    eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    r = eng.analyze(logs)
+    g = golden.analyze(logs, sets, p, golden.FrequencyTracker(p))
+    assert [e["score"] for e in r["events"]] == [e["score"] for e in g["events"]]
+    last = {e["matchedPattern"]["name"]: e["score"] for e in g["events"]}
+    assert last["p1"] < last["p0"]           # U+00A0 id: 25 matches > threshold -> penalised

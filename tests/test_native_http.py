@@ -61,7 +61,28 @@ def test_parse_and_errors(server):
         assert r.status == code, path
     c.request("GET", "/metrics")
     m = c.getresponse().read().decode()
-    assert 'lp_requests_total{code="200"}' in m and 'lp_requests_total{code="400"}' not in m or True
+    assert 'lp_requests_total{code="200"}' in m
+    c.close()
+
+
+def test_non_json_content_type_is_415(server):
+    """@Consumes(MediaType.APPLICATION_JSON) (Parse.java:42): a non-JSON media type is refused
+    before the body is looked at; parameters and case do not matter; no header is accepted."""
+    fe, _, _ = server
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=60)
+    body = b'{"pod":{},"logs":"x"}'
+    for ct, code in [("text/plain", 415), ("application/xml", 415), ("application/jsonx", 415),
+                     ("Application/JSON; charset=UTF-8", 200), ("application/json", 200)]:
+        c.request("POST", "/parse", body=body, headers={"content-type": ct})
+        r = c.getresponse()
+        out = r.read()
+        assert r.status == code, (ct, out)
+        if code == 415:
+            assert json.loads(out) == {"error": "Content-Type must be application/json"}
+    c.request("POST", "/parse", body=body)          # http.client sends no Content-Type here
+    r = c.getresponse()
+    r.read()
+    assert r.status == 200
     c.close()
 
 

@@ -26,14 +26,14 @@ def _entries(pf):
     return out
 
 
-def _lib_with_max_stride(smax, n=200, seed=5):
-    old = C.PF_STRIDE_MAX
+def _lib_with_max_stride(smax, n=200, seed=5, teddy=True):
+    old = C.PF_STRIDE_MAX, C.PF_TEDDY
     try:
-        C.PF_STRIDE_MAX = smax
+        C.PF_STRIDE_MAX, C.PF_TEDDY = smax, teddy
         sets, _ = make_library(n, seed=seed)
         return C.CompiledLibrary(sets, ScoringParams())
     finally:
-        C.PF_STRIDE_MAX = old
+        C.PF_STRIDE_MAX, C.PF_TEDDY = old
 
 
 @pytest.mark.parametrize("S", [2, 4])
@@ -66,12 +66,10 @@ def test_every_occurrence_hits_a_tested_position(S):
             assert sum(p % S == 0 for p in starts) == 1    # exactly one indexed window is tested
 
 
-def test_stride_follows_the_shortest_literal():
+def _one(regex, teddy=True):
     import yaml
     from log_parser_amd.models.schema import PatternSet
-
-    def lib_for(regex):
-        doc = yaml.safe_load(f"""
+    doc = yaml.safe_load(f"""
 metadata: {{library_id: s}}
 patterns:
   - id: p1
@@ -79,30 +77,76 @@ patterns:
     severity: HIGH
     primary_pattern: {{regex: "{regex}", confidence: 0.9}}
 """)
+    old = C.PF_TEDDY
+    try:
+        C.PF_TEDDY = teddy
         return C.CompiledLibrary([PatternSet.model_validate(doc)], ScoringParams())
+    finally:
+        C.PF_TEDDY = old
+
+
+def test_short_literals_go_to_the_teddy_tier():
+    """3..6-byte literals use the byte-position tier and leave the bloom tier at stride 4."""
+    lib = _one("OOMKil")
+    assert lib.pf["teddy_lits"] == 1 and lib.pf["gmask"] == 0
+    lib = _one("(OOM|SIGSEGVKILL)")
+    assert lib.pf["teddy_lits"] == 1 and lib.pf["stride"] == 4      # "sigsegvkill" on the bloom tier
+    assert _one("ab").summary()["scan_all"] == 1                     # < 3 bytes: scan every line
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_teddy_masks_hold_every_short_window(seed):
+    from log_parser_amd.utils.synth import realistic_library
+    sets, _ = realistic_library(300, seed=seed)
+    lib = C.CompiledLibrary(sets, ScoringParams())
+    pf = lib.pf
+    assert pf["teddy_lits"] > 5
+    tab, off, ent = pf["teddy"], pf["tb_off"], pf["tb_lits"]
+    seen = set()
+    for b in range(C.TEDDY_BUCKETS):
+        for e in ent[off[b]:off[b + 1]]:
+            i, o = int(e) & ((1 << C.LIT_OFF_SHIFT) - 1), int(e) >> C.LIT_OFF_SHIFT
+            lit = lib.literals[i]
+            assert C.TEDDY_MIN <= len(lit) <= C.TEDDY_MAX and o + 3 <= len(lit)
+            for j in range(3):
+                assert int(tab[lit[o + j], j]) >> b & 1
+            seen.add(i)
+    assert len(seen) == pf["teddy_lits"]
+
+
+def test_every_short_occurrence_is_a_candidate_cpu():
+    """Host prefilter twin: each planted short literal (any case, any alignment) yields its
+    (regex, line) candidate; the bloom tier yields one candidate per long-literal occurrence."""
+    import torch
+    from log_parser_amd.ops import kernels as K
+    lib = _one("(?i)qx7|VERYLONGLITERAL")
+    lines = [b"noise", b"a QX7 b", b"xqx7", b"verylongliteral here", b"q x7"]
+    data = b"\n".join(lines)
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    ls, ll = K.split_lines(t, len(data))
+    cand = K.prefilter(t, len(data), lib.device_tables(torch.device("cpu"))["pf"], ls, 64)
+    got = sorted(set(int(c) & 0xFFFFFFFF for c in cand.tolist()))
+    assert got == [1, 2, 3]
+    assert cand.numel() == 3                          # no duplicate per indexed window
+
+
+def test_stride_follows_the_shortest_literal():
+    def lib_for(regex):
+        return _one(regex, teddy=False)
     assert lib_for("OOMKill").pf["stride"] == 4       # 7 bytes: four 4-byte windows
     assert lib_for("OOMKil").pf["stride"] == 2        # 6 bytes: only three windows
     assert lib_for("OOMK").pf["stride"] == 1
 
 
 def test_short_literals_fall_back_to_stride1():
-    old = C.PF_STRIDE_MAX
+    old = C.PF_STRIDE_MAX, C.PF_TEDDY
     try:
-        C.PF_STRIDE_MAX = 1
+        C.PF_STRIDE_MAX, C.PF_TEDDY = 1, False
         sets, _ = make_library(30, seed=5)
         assert C.CompiledLibrary(sets, ScoringParams()).pf["stride"] == 1
     finally:
-        C.PF_STRIDE_MAX = old
-    import yaml
-    from log_parser_amd.models.schema import PatternSet
-    doc = yaml.safe_load("""
-metadata: {library_id: short}
-patterns:
-  - id: p1
-    name: short literal
-    severity: HIGH
-    primary_pattern: {regex: "OOM", confidence: 0.9}
-""")
-    lib = C.CompiledLibrary([PatternSet.model_validate(doc)], ScoringParams())
+        C.PF_STRIDE_MAX, C.PF_TEDDY = old
+    lib = _one("OOM", teddy=False)
     assert lib.pf["stride"] == 1                      # a 3-byte literal has no two 4-byte windows
     assert np.all(np.array([len(l) for l in lib.literals]) >= 1)

@@ -1,0 +1,160 @@
+"""Multi-regex DFA scan groups (jregex MultiDfa + csrc/kernels/scan_multi.hip).
+
+Literal-free regexes are determinised together (up to 16 per DFA) and walked over every line.
+Each member's find() must equal its own single-regex DFA (itself fuzzed against the javacompat
+oracle in test_regex.py), on every line shape: anchors, word boundaries, '$' before a final
+'\\r', UTF-8. The device kernel must equal its host twin; a realistic library must give the same
+hits and the same scored events as the per-regex paths and the golden model.
+"""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from log_parser_amd import golden
+from log_parser_amd.engine import Engine
+from log_parser_amd.models.compiled import CompiledLibrary
+from log_parser_amd.native import N
+from log_parser_amd.ops import kernels as K
+from log_parser_amd.utils.config import Config, ScoringParams
+from log_parser_amd.utils.synth import make_log, realistic_library
+
+ATOMS = ["a", "b", "c", "A", " ", "1", "-", ".", r"\d", r"\w", r"\s", r"\W", "[ab]", "[^a]", r"\.", "é", r"\b",
+         r"\B", "^", "$", "_"]
+
+
+def _rand_regex(rng, depth=0):
+    parts = []
+    for _ in range(rng.randint(1, 4)):
+        if rng.random() < 0.15 and depth < 2:
+            a = "(" + "|".join(_rand_regex(rng, depth + 1) for _ in range(rng.randint(1, 3))) + ")"
+        else:
+            a = rng.choice(ATOMS)
+        if a not in ("^", "$", r"\b", r"\B"):
+            q = rng.random()
+            a += "*" if q < 0.12 else "+" if q < 0.22 else "?" if q < 0.3 else ""
+        parts.append(a)
+    s = "".join(parts)
+    return ("(?i)" + s) if rng.random() < 0.15 else s
+
+
+def _rand_line(rng):
+    s = "".join(rng.choice("abcA 1-.é_\t") for _ in range(rng.randint(0, 14)))
+    return s + ("\r" if rng.random() < 0.15 else "")
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_multi_dfa_equals_single_dfas(seed):
+    rng = random.Random(seed)
+    pats = []
+    while len(pats) < rng.randint(1, 16):
+        p = _rand_regex(rng)
+        if N.compile_regex(p)["kind"] == 0 and p not in pats:
+            pats.append(p)
+    d = N.compile_multi(pats, 1 << 16)
+    assert d is not None and d["nregs"] == len(pats)
+    for _ in range(60):
+        line = _rand_line(rng).encode()
+        got = N.multi_find(pats, line.decode())
+        want = sum(1 << r for r, p in enumerate(pats) if N.dfa_find(p, line))
+        assert got == want, (pats, line)
+
+
+def test_multi_dfa_limits():
+    assert N.compile_multi([r"a"] * 17, 4096) is None                  # > 16 members
+    assert N.compile_multi([r"(a)\1"], 4096) is None                   # not an automaton regex
+    assert N.compile_multi([r"(a|b)*a(a|b){12}"], 256) is None        # state limit
+    assert N.multi_find([r"^\s+at\s", r"x$", r"\bK\d{2}\b"], "\tat K42 x\r") == 0b111
+
+
+def _lib():
+    sets, trig = realistic_library(400, seed=21)
+    return sets, trig, CompiledLibrary(sets, ScoringParams())
+
+
+def _text(dev, data: bytes):
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    return t.to(dev)
+
+
+def test_realistic_library_builds_scan_groups():
+    _, _, lib = _lib()
+    assert lib.summary()["scan_all"] >= 10
+    assert sum(len(p["regs"]) for p in lib.scan_passes) + len(lib.scan_regs_single) == len(lib.scan_regs)
+    for p in lib.scan_passes:
+        assert 1 <= p["ngroups"] <= 4 and p["lds_words"] % 4 == 0
+        assert p["lds_words"] * 4 <= (48 << 10) + 2048
+
+
+def test_scan_passes_equal_per_regex_scan_cpu():
+    _, trig, lib = _lib()
+    data = make_log(6000, trig, seed=5, hit_rate=0.08, crlf_rate=0.1).encode()
+    t = _text("cpu", data)
+    ls, ll = K.split_lines(t, len(data))
+    tabs = lib.device_tables(torch.device("cpu"))
+    got = torch.cat([K.scan_multi(t, ls, ll, sp, 1024) for sp in tabs["scan_passes"]])
+    regs = torch.tensor(lib.scan_regs, dtype=torch.int32)
+    want = K.scan(t, ls, ll, regs, tabs["dfa"], 1024)
+    assert want.numel() > 10
+    assert torch.equal(torch.sort(got).values, torch.sort(want).values)
+
+
+def test_realistic_engine_matches_golden_cpu():
+    p = ScoringParams()
+    sets, trig, lib = _lib()
+    logs = make_log(2500, trig, seed=8, hit_rate=0.08)
+    eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    r = eng.analyze(logs)
+    g = golden.analyze(logs, sets, p, golden.FrequencyTracker(p))
+    assert len(r["events"]) == len(g["events"]) > 0
+    assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r["events"]] == \
+        [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+    np.testing.assert_allclose([e["score"] for e in r["events"]], [e["score"] for e in g["events"]], rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_scan_multi_gpu_equals_host(gpu_device):
+    _, trig, lib = _lib()
+    data = make_log(30000, trig, seed=6, hit_rate=0.08, crlf_rate=0.1).encode()
+    td, tc = _text(gpu_device, data), _text("cpu", data)
+    ls_d, ll_d = K.split_lines(td, len(data))
+    ls_c, ll_c = K.split_lines(tc, len(data))
+    ed = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    tabs_c = lib.device_tables(torch.device("cpu"))
+    n = 0
+    for sp_d, sp_c in zip(ed.tabs["scan_passes"], tabs_c["scan_passes"]):
+        hd = K.scan_multi(td, ls_d, ll_d, sp_d, 16, ed.scan_grid(sp_d))     # tiny cap: the retry path too
+        hc = K.scan_multi(tc, ls_c, ll_c, sp_c, 1024)
+        assert torch.equal(torch.sort(hd.cpu()).values, torch.sort(hc).values)
+        n += hc.numel()
+    assert n > 50
+
+
+@pytest.mark.gpu
+def test_realistic_hits_gpu_equal_cpu(gpu_device):
+    _, trig, lib = _lib()
+    data = make_log(20000, trig, seed=9, hit_rate=0.05, crlf_rate=0.1).encode()
+    ed = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    ec = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    td, tc = _text(gpu_device, data), _text("cpu", data)
+    hd = ed.match_hits(td, len(data), *K.split_lines(td, len(data)))
+    hc = ec.match_hits(tc, len(data), *K.split_lines(tc, len(data)))
+    assert hd.numel() > 100
+    assert torch.equal(hd.cpu(), hc)
+
+
+@pytest.mark.gpu
+def test_realistic_engine_matches_golden_gpu(gpu_device):
+    """Short literals (Teddy tier) + literal-free regexes (scan groups) on the device, end to end."""
+    p = ScoringParams()
+    sets, trig, lib = _lib()
+    logs = make_log(4000, trig, seed=12, hit_rate=0.08, crlf_rate=0.05)
+    eng = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    r = eng.analyze(logs)
+    g = golden.analyze(logs, sets, p, golden.FrequencyTracker(p))
+    assert len(r["events"]) == len(g["events"]) > 0
+    assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r["events"]] == \
+        [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+    np.testing.assert_allclose([e["score"] for e in r["events"]], [e["score"] for e in g["events"]], rtol=1e-12)

@@ -43,6 +43,16 @@ def test_invalid_requests(client):
         assert r.json() == {"error": "Invalid PodFailureData provided"}
 
 
+def test_non_json_content_type_is_415(client):
+    body = b'{"pod":{},"logs":"x"}'
+    for ct, code in [("text/plain", 415), ("application/x-www-form-urlencoded", 415),
+                     ("application/json;charset=utf-8", 200), ("APPLICATION/JSON", 200)]:
+        r = client.post("/parse", content=body, headers={"content-type": ct})
+        assert r.status_code == code, ct
+        if code == 415:
+            assert r.json() == {"error": "Content-Type must be application/json"}
+
+
 def test_parse_matches_golden(client, lib_dir):
     from log_parser_amd.models.library import load_pattern_directory
     sets = load_pattern_directory(lib_dir[0])

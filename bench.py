@@ -58,10 +58,13 @@ def parse():
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="server front end for p50")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
+    ap.add_argument("--d2h-stream", default="copy", choices=["copy", "compute"],
+                    help="stream of the per-step event D2H (diagnostic A/B)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
-                    help="process group: auto = nccl (RCCL) on GPUs / gloo on CPU, at every world size; "
-                         "gloo on GPUs = host-staged collectives (rehearse several ranks on ONE GPU); "
-                         "none = no process group at world size 1")
+                    help="process group: auto = nccl (RCCL) on GPUs / gloo on CPU for world size > 1 and none "
+                         "at world size 1 (RCCL's world-1 self-copy rides the SDMA engine the ingest copy "
+                         "occupies and stalls the step; measured 23.6 -> 26-28 ms); nccl / gloo force a group "
+                         "at any size (gloo on GPUs = host-staged, to rehearse several ranks on ONE GPU)")
     return ap.parse_args()
 
 
@@ -121,7 +124,9 @@ def run(args, sets, trig, rank, world, local_rank, server):
         bind_to_gpu_numa(local_gpu)          # pinned ingest buffers on the GPU's own socket
     else:
         device = torch.device("cpu")
-    backend = args.backend if args.backend != "auto" else ("nccl" if use_cuda else "gloo")
+    backend = args.backend
+    if backend == "auto":
+        backend = ("nccl" if use_cuda else "gloo") if world > 1 else "none"
     if backend == "none" and world > 1:
         backend = "nccl" if use_cuda else "gloo"
     if backend != "none":
@@ -130,7 +135,10 @@ def run(args, sets, trig, rank, world, local_rank, server):
             from log_parser_amd.utils.launch import free_port
             os.environ["MASTER_PORT"] = str(free_port())
         kw = {"device_id": device} if backend == "nccl" else {}
-        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        from log_parser_amd.utils.launch import stdout_to_stderr
+        with stdout_to_stderr():            # RCCL prints its version banner on stdout: keep ONE JSON line
+            dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+            dist.barrier()
         assert dist.get_world_size() == world
 
     params = ScoringParams()
@@ -185,7 +193,9 @@ def run(args, sets, trig, rank, world, local_rank, server):
         state["issued"] = i
 
     def events_to_host(out, slot):
-        """(global line int64, pattern int32, score f64) of EVERY event -> pinned host, one copy."""
+        """(global line int64, pattern int32, score f64) of EVERY event -> pinned host, one copy.
+        The D2H runs on the copy stream, behind the prefetch H2D: on the compute stream it would
+        queue behind the 23 ms PCIe ingest of the next step and stall the next step's kernels."""
         r = out.result
         n = r.ev_line.numel()
         if n == 0:
@@ -194,8 +204,18 @@ def run(args, sets, trig, rank, world, local_rank, server):
         pk = torch.cat([g.view(torch.int32), r.ev_pat.to(torch.int32), r.score.view(torch.int32)])
         nb = pk.numel() * 4
         if ev_host[slot].numel() < nb:
+            if use_cuda:
+                torch.cuda.current_stream().synchronize()        # the old slot may still be in flight
             ev_host[slot] = torch.empty(nb * 5 // 4, dtype=torch.uint8, pin_memory=use_cuda)
-        ev_host[slot][:nb].view(torch.int32).copy_(pk, non_blocking=use_cuda)
+        if use_cuda and args.d2h_stream == "copy":
+            done = torch.cuda.Event()
+            done.record()
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(done)
+                ev_host[slot][:nb].view(torch.int32).copy_(pk, non_blocking=True)
+                pk.record_stream(copy_stream)
+        else:
+            ev_host[slot][:nb].view(torch.int32).copy_(pk, non_blocking=use_cuda)
         state["events_host"] = n
 
     def step():

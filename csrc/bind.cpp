@@ -117,6 +117,19 @@ static ScanPass scan_pass_from(const py::tuple& t) {
   return S;
 }
 
+// (t, key, cnt, cap, ht, tot, seen)
+static FreqRing ring_from(const py::tuple& t) {
+  FreqRing R;
+  R.t = P<double>(t[0].cast<uint64_t>());
+  R.key = P<int32_t>(t[1].cast<uint64_t>());
+  R.cnt = P<int32_t>(t[2].cast<uint64_t>());
+  R.cap = t[3].cast<int64_t>();
+  R.ht = P<int64_t>(t[4].cast<uint64_t>());
+  R.tot = P<int64_t>(t[5].cast<uint64_t>());
+  R.seen = P<uint8_t>(t[6].cast<uint64_t>());
+  return R;
+}
+
 static py::bytes vbytes(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
 
 static py::dict compile_regex(const std::string& pat, int max_states, int max_positions) {
@@ -372,6 +385,12 @@ PYBIND11_MODULE(_lpnative, m) {
     py::gil_scoped_release nogil;
     return scan_multi_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, S, P<int64_t>(out),
                            cap);
+  });
+  m.def("freq_evict", [](py::tuple ring, double horizon, uint64_t s, bool dev) {
+    freq_evict(ring_from(ring), horizon, s, dev);
+  });
+  m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev) {
+    freq_record(P<const int64_t>(counts), K, now, ring_from(ring), s, dev);
   });
   m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry,
                          int64_t n, py::tuple st, py::tuple sp, uint64_t out, uint64_t fac) {

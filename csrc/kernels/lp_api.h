@@ -85,6 +85,21 @@ int64_t scan_multi_host(const uint8_t* text, const int64_t* line_start, const in
                         const ScanPass& S, int64_t* out, int64_t cap);
 }  // namespace lp
 
+// ---- device-resident frequency state (freq_state.hip)
+namespace lp {
+struct FreqRing {
+  double* t;          // [cap] batch timestamps (seconds)
+  int32_t* key;       // [cap] frequency key
+  int32_t* cnt;       // [cap] matches of the key in that batch
+  int64_t cap;
+  int64_t* ht;        // [2] head, tail positions (monotonic)
+  int64_t* tot;       // [K] in-window matches per key
+  uint8_t* seen;      // [K]
+};
+void freq_evict(const FreqRing& R, double horizon, uint64_t stream, bool dev);
+void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev);
+}  // namespace lp
+
 // ---- post-match pipeline (lp_post.hip): hit CSR, events, frequency ranks, context features
 namespace lp {
 struct EvTables {

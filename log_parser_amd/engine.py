@@ -40,7 +40,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from .frequency import FrequencyState
+from .frequency import DeviceFrequencyState, FrequencyState
 from .golden import SEVERITY_ORDER
 from .models.compiled import CompiledLibrary
 from .native import N
@@ -253,7 +253,14 @@ class Engine:
         self.lib = library
         self.params: ScoringParams = library.params
         self.device = device if device is not None else resolve_device(self.config["engine.device"])
-        self.freq = freq or FrequencyState(self.params.freq_window_hours)
+        if freq is None:
+            # one engine owning a GPU keeps the sliding window in HBM (no per-batch H2D / D2H);
+            # CPU engines and engines sharing one state across GPUs use the host state
+            if self.device.type == "cuda" and bool(self.config.get("engine.frequency.device-resident", True)):
+                freq = DeviceFrequencyState(library.freq_ids, self.params.freq_window_hours, self.device)
+            else:
+                freq = FrequencyState(self.params.freq_window_hours)
+        self.freq = freq
         self.cand_cap = int(self.config["engine.candidate-capacity"])
         # per-stage HIP-event timers (utils/tracing.py); engine.trace also reports them per response
         self.trace = bool(self.config.get("engine.trace", False))
@@ -443,7 +450,14 @@ class Engine:
         return self.finish(prep, segs, freq_carry, seq_carry, with_factors)
 
     # ------------------------------------------------------------------ request API
+    @property
+    def freq_on_device(self) -> bool:
+        return getattr(self.freq, "device_resident", False)
+
     def freq_carry(self) -> torch.Tensor:
+        if self.freq_on_device:
+            c = self.freq.carry_tensor()
+            return c if c.device == self.device else c.to(self.device)
         c = self.freq.carry(self.lib.freq_ids)
         if c.size == 0:
             c = np.zeros(1, np.int64)
@@ -451,6 +465,10 @@ class Engine:
 
     def commit_frequency(self, counts) -> None:
         """Record this batch's per-id match counts (tensor or host array) in the sliding window."""
+        if self.freq_on_device:
+            if len(counts) and self.lib.freq_ids:
+                self.freq.record_tensor(counts if torch.is_tensor(counts) else torch.from_numpy(np.asarray(counts)))
+            return
         if len(counts):
             self.freq.record_counts(self.lib.freq_ids, counts.cpu().numpy() if torch.is_tensor(counts) else counts)
 
@@ -567,7 +585,20 @@ class Engine:
             idx = []
         else:
             idx = [ls_h, ll_h]
-        if turn is None:
+        if turn is None and self.freq_on_device:
+            # the window lives in HBM: carry read and counts recorded on the device, no host trip
+            up = self.upload(idx + [lo, hi, g0, nn])
+            if not pinned_idx:
+                ls, ll = up[0], up[1]
+            lo, hi, g0, nn = up[len(idx):]
+            segs = Segments(lo, hi, lo, hi, g0, nn)
+            if tm is not None:
+                self._tick(tm, "h2d", 0.0)
+            res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose, timings=tm)
+            self.commit_frequency(res.freq_counts)
+            with TR.HostTimer(tm, "d2h"):
+                job.ev = self._results_to_host(res)
+        elif turn is None:
             carry = self.freq.carry(self.lib.freq_ids)
             up = self.upload(idx + [lo, hi, g0, nn, carry if carry.size else np.zeros(1, np.int64)])
             if not pinned_idx:

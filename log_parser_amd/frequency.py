@@ -169,3 +169,215 @@ class FrequencyState:
                 cc = np.array([c], np.int64)
                 self._tot[s] += c
                 self._q.append((t, sl, cc))
+
+
+class DeviceFrequencyState:
+    """The same sliding-window state, resident in HBM next to the score kernel (SURVEY §2.5 K8,
+    csrc/kernels/freq_state.hip): in-window totals per frequency key + a FIFO ring of
+    (timestamp, key, count) batch records. ``carry_tensor`` evicts (kernel) and returns the totals
+    as the score kernel's carry; ``record_tensor`` appends a batch's per-key counts (kernel).
+    Neither touches the host: the only host input is the clock scalar. The admin / snapshot API
+    reads the state back on demand. Keyed by one library's frequency ids (``ids``); one engine
+    (GPU) owns it -- engines serving concurrently share a host ``FrequencyState`` instead.
+
+    Works on CPU tensors too (the kernels' host twins), which is how the CPU tests pin it to
+    ``golden.FrequencyTracker``."""
+
+    device_resident = True
+
+    def __init__(self, ids: List[str], window_hours: int, device, clock: Callable[[], float] = time.time,
+                 capacity: int = 1 << 20):
+        import torch
+        self.ids = list(ids)
+        self.window_hours = window_hours
+        self.window_s = float(window_hours) * 3600.0
+        self.clock = clock
+        self.device = torch.device(device)
+        K = max(len(self.ids), 1)
+        self.tot = torch.zeros(K, dtype=torch.int64, device=self.device)
+        self.seen = torch.zeros(K, dtype=torch.uint8, device=self.device)
+        self.ht = torch.zeros(2, dtype=torch.int64, device=self.device)
+        self._alloc(max(int(capacity), 2 * K))
+        self._tail_bound = 0          # host upper bound of ht[1] (no sync per batch)
+        self._head_known = 0          # host lower bound of ht[0]
+        self._last_now = float("-inf")
+        self._lock = threading.RLock()
+        self._index = {pid: i for i, pid in enumerate(self.ids)}
+
+    # ---- storage
+    def _alloc(self, cap: int) -> None:
+        import torch
+        self.cap = int(cap)
+        self.t = torch.zeros(self.cap, dtype=torch.float64, device=self.device)
+        self.key = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+        self.cnt = torch.zeros(self.cap, dtype=torch.int32, device=self.device)
+
+    def _ring(self) -> tuple:
+        return (self.t.data_ptr(), self.key.data_ptr(), self.cnt.data_ptr(), self.cap, self.ht.data_ptr(),
+                self.tot.data_ptr(), self.seen.data_ptr())
+
+    def _stream(self) -> int:
+        import torch
+        return torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+
+    def _records(self):
+        """(t, key, cnt) host arrays of the live records, oldest first (syncs)."""
+        h, tl = (int(x) for x in self.ht.cpu())
+        if tl == h:
+            return np.zeros(0), np.zeros(0, np.int64), np.zeros(0, np.int64)
+        idx = (np.arange(h, tl) % self.cap)
+        return (self.t.cpu().numpy()[idx], self.key.cpu().numpy()[idx].astype(np.int64),
+                self.cnt.cpu().numpy()[idx].astype(np.int64))
+
+    def _ensure_room(self, k: int) -> None:
+        """Keep at least ``k`` free ring slots; reads head/tail back only when the host bound says
+        the ring may be full, and grows it (records kept in order) when it really is."""
+        if self._tail_bound + k - self._head_known <= self.cap:
+            return
+        h, tl = (int(x) for x in self.ht.cpu())
+        self._head_known, self._tail_bound = h, tl
+        if tl + k - h <= self.cap:
+            return
+        import torch
+        t, key, cnt = self._records()
+        n = t.size
+        self._alloc(max(2 * self.cap, n + 2 * k))
+        if n:
+            self.t[:n] = torch.from_numpy(t).to(self.device)
+            self.key[:n] = torch.from_numpy(key.astype(np.int32)).to(self.device)
+            self.cnt[:n] = torch.from_numpy(cnt.astype(np.int32)).to(self.device)
+        self.ht.copy_(torch.tensor([0, n], dtype=torch.int64))
+        self._head_known, self._tail_bound = 0, n
+
+    def _now(self, now: Optional[float] = None) -> float:
+        now = self.clock() if now is None else float(now)
+        self._last_now = max(self._last_now, now)      # ring timestamps must not go backwards
+        return self._last_now
+
+    # ---- device pipeline interface
+    def carry_tensor(self, now: Optional[float] = None):
+        """Evict records at or before now - window; returns the in-window totals (device int64[K])."""
+        from .native import N
+        with self._lock:
+            N.freq_evict(self._ring(), self._now(now) - self.window_s, self._stream(), self.device.type == "cuda")
+            return self.tot
+
+    def record_tensor(self, counts, now: Optional[float] = None) -> None:
+        """Append this batch's per-key counts (int64 tensor on the state's device, >= K entries)."""
+        from .native import N
+        K = len(self.ids)
+        if K == 0:
+            return
+        c = counts.to(device=self.device, dtype=__import__("torch").int64)
+        with self._lock:
+            self._ensure_room(K)
+            N.freq_record(c.data_ptr(), K, self._now(now), self._ring(), self._stream(), self.device.type == "cuda")
+            self._tail_bound += K
+
+    # host-array compatibility with FrequencyState (CPU callers, tests)
+    def carry(self, ids: List[str]) -> np.ndarray:
+        assert list(ids) == self.ids, "a device frequency state serves one library"
+        return self.carry_tensor().cpu().numpy()[:len(ids)].copy()
+
+    def record_counts(self, ids: List[str], counts: Iterable[int], now: Optional[float] = None) -> None:
+        import torch
+        assert list(ids) == self.ids, "a device frequency state serves one library"
+        c = torch.as_tensor(np.asarray(counts, np.int64).reshape(-1)[:len(ids)])
+        self.record_tensor(c, now)
+
+    # ---- reference API surface (FrequencyTrackingService.java:101-161)
+    def _pruned_totals(self):
+        self.carry_tensor()
+        return self.tot.cpu().numpy(), self.seen.cpu().numpy()
+
+    def get_pattern_frequency(self, pid: str) -> Optional[dict]:
+        with self._lock:
+            k = self._index.get(pid)
+            if k is None:
+                return None
+            tot, seen = self._pruned_totals()
+            if not seen[k]:
+                return None
+            c = int(tot[k])
+            return {"patternId": pid, "currentCount": c, "hourlyRate": c / float(self.window_hours)}
+
+    def statistics(self) -> Dict[str, int]:
+        with self._lock:
+            tot, seen = self._pruned_totals()
+            return {self.ids[k]: int(tot[k]) for k in np.flatnonzero(seen[:len(self.ids)])}
+
+    def reset(self, pid: str) -> None:
+        with self._lock:
+            k = self._index.get(pid)
+            if k is None:
+                return
+            self.tot[k] = 0
+            self.cnt.masked_fill_(self.key == k, 0)           # queued records no longer count
+
+    def reset_all(self) -> None:
+        with self._lock:
+            self.tot.zero_()
+            self.seen.zero_()
+            self.ht.zero_()
+            self._head_known = self._tail_bound = 0
+
+    # ---- capture / rollback (elastic DP re-runs a step after a rank failure)
+    def capture(self) -> dict:
+        with self._lock:
+            return {"ht": self.ht.clone(), "tot": self.tot.clone(), "seen": self.seen.clone(),
+                    "t": self.t, "key": self.key, "cnt": self.cnt.clone()}
+
+    def rollback(self, state: dict) -> None:
+        with self._lock:
+            if state["t"] is not self.t:                     # the ring grew meanwhile: keep the old one
+                self.t, self.key, self.cap = state["t"], state["key"], state["t"].numel()
+            self.cnt = state["cnt"].clone()
+            self.ht.copy_(state["ht"])
+            self.tot.copy_(state["tot"])
+            self.seen.copy_(state["seen"])
+            h, tl = (int(x) for x in self.ht.cpu())
+            self._head_known, self._tail_bound = h, tl
+
+    # ---- checkpoint / resume: the same JSON as FrequencyState
+    def snapshot(self, path: str) -> None:
+        with self._lock:
+            t, key, cnt = self._records()
+            seen = self.seen.cpu().numpy()
+            rec: Dict[str, list] = {self.ids[k]: [] for k in np.flatnonzero(seen[:len(self.ids)])}
+            for a, k, c in zip(t.tolist(), key.tolist(), cnt.tolist()):
+                if c > 0:
+                    rec[self.ids[k]].append([a, c])
+            data = {"window_hours": self.window_hours, "records": rec}
+        tmp = path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(data, f)
+        os.replace(tmp, path)
+
+    def restore(self, path: str) -> None:
+        import torch
+        if not os.path.exists(path):
+            return
+        with open(path) as f:
+            data = json.load(f)
+        with self._lock:
+            self.reset_all()
+            ev = []
+            for pid, v in data.get("records", {}).items():
+                k = self._index.get(pid)
+                if k is None:
+                    continue
+                self.seen[k] = 1
+                ev += [(float(a), k, int(c)) for a, c in v]
+            ev.sort()
+            n = len(ev)
+            self._ensure_room(n + 1)
+            if n:
+                self.t[:n] = torch.tensor([e[0] for e in ev], dtype=torch.float64)
+                self.key[:n] = torch.tensor([e[1] for e in ev], dtype=torch.int32)
+                self.cnt[:n] = torch.tensor([e[2] for e in ev], dtype=torch.int32)
+                tot = np.zeros(self.tot.numel(), np.int64)
+                np.add.at(tot, [e[1] for e in ev], [e[2] for e in ev])
+                self.tot.copy_(torch.from_numpy(tot))
+                self._last_now = max(self._last_now, ev[-1][0])
+            self.ht.copy_(torch.tensor([0, n], dtype=torch.int64))
+            self._head_known, self._tail_bound = 0, n

@@ -11,7 +11,9 @@ going when a rank dies or hangs:
   whether the step happened -- no rank can run ahead of another by one step.
 * **Recovery.** On abort every survivor rolls the frequency state back to the start of the step
   (the only cross-step state, ``FrequencyState.capture/rollback``), tears the communicator down
-  (``destroy_process_group`` = ``ncclCommAbort`` for RCCL), checks in under a new generation, and
+  -- RCCL: ``_abort_process_group`` (``ncclCommAbort``; a ``destroy_process_group`` would wait for
+  the dead peer's outstanding collectives and can block forever), gloo: ``destroy_process_group``
+  --, checks in under a new generation, and
   the first survivor to decide publishes the new member list; the process group is re-created over
   the survivors (``PrefixStore`` per generation) and the step is re-run with the log re-sharded over
   fewer ranks. Results are bit-identical to an uninterrupted run (tests/test_elastic.py).
@@ -77,8 +79,12 @@ class ElasticGroup:
 
     def _init_pg(self) -> None:
         kw = {}
-        if self.backend == "nccl" and self.device is not None:
-            kw["device_id"] = self.device
+        if self.backend == "nccl":
+            # failures are handled here (vote + abort + rebuild), not by the RCCL watchdog tearing
+            # the process down; required by _abort_process_group
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "0")
+            if self.device is not None:
+                kw["device_id"] = self.device
         dist.init_process_group(self.backend, store=dist.PrefixStore(f"lp/pg/{self.gen}", self.store),
                                 rank=self.rank, world_size=self.size,
                                 timeout=timedelta(seconds=self.timeout_s), **kw)
@@ -111,11 +117,20 @@ class ElasticGroup:
         return bytes(decided) == b"ok"
 
     # ---- rebuild over the survivors ----------------------------------------------------------
-    def rebuild(self) -> None:
+    def teardown(self) -> None:
+        """Drop the (possibly broken) communicator without waiting for peers that may be dead."""
+        if not dist.is_initialized():
+            return
         try:
-            dist.destroy_process_group()
+            if self.backend == "nccl":
+                dist.distributed_c10d._abort_process_group()       # ncclCommAbort, no peer handshake
+            else:
+                dist.destroy_process_group()
         except Exception:  # noqa: BLE001 - a broken communicator may refuse a clean shutdown
             pass
+
+    def rebuild(self) -> None:
+        self.teardown()
         old = self.members
         self.gen += 1
         g = self.gen

@@ -251,6 +251,9 @@ class Service:
                 lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]))
                 log.info("compiled library: %s", lib.summary())
                 self._engine = Engine(lib, cfg)
+                snap = cfg["engine.frequency.snapshot-path"]
+                if snap:                       # resume the sliding window of a previous run
+                    self._engine.freq.restore(snap)
             return self._engine
 
     def batcher(self) -> Batcher:
@@ -259,9 +262,13 @@ class Service:
             if self._batcher is None:
                 cfg = self.config
                 engines = [eng]
-                for dev in serve_devices(cfg):     # data-parallel serving: one engine per GPU
-                    if dev != engines[0].device:
-                        engines.append(Engine(engines[0].lib, cfg, device=dev, freq=engines[0].freq))
+                devs = [d for d in serve_devices(cfg) if d != eng.device]
+                if devs and getattr(eng.freq, "device_resident", False):
+                    # several GPUs record into ONE window in arrival order (FrequencyTurn): host state
+                    from ..frequency import FrequencyState
+                    eng.freq = FrequencyState(eng.params.freq_window_hours)
+                for dev in devs:                   # data-parallel serving: one engine per GPU
+                    engines.append(Engine(engines[0].lib, cfg, device=dev, freq=engines[0].freq))
                 if len(engines) > 1:
                     log.info("serving on %d engines: %s", len(engines), [str(e.device) for e in engines])
                 self._batcher = Batcher(engines, int(cfg["engine.batch.max-requests"]),

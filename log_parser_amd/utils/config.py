@@ -62,6 +62,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.batch.max-wait-ms": (0.0, float),
     # top-k events kept by the distributed reduction (0 = all events)
     "engine.topk": (100, int),
+    # keep the sliding-window frequency state in HBM when one engine owns a GPU (K8)
+    "engine.frequency.device-resident": (True, bool),
     # persist frequency state (snapshot path, empty = disabled, reference default)
     "engine.frequency.snapshot-path": ("", str),
     # max request body (reference: Quarkus default 10 MiB)

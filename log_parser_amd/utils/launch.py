@@ -10,6 +10,7 @@ the GPU must not fork the ranks' interpreters, and each rank selects its own dev
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import socket
 import subprocess
@@ -69,3 +70,18 @@ def spawn_local_ranks(argv: Sequence[str], world: int, poll_s: float = 0.2,
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Point file descriptor 1 at stderr for the duration (native libraries such as RCCL print
+    banners with printf; a bench's stdout must carry only its JSON line)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)

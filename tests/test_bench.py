@@ -67,9 +67,10 @@ def test_bench_spawns_its_own_ranks(tmp_path):
 
 
 def test_bench_single_rank_parse_over_http(tmp_path):
-    """--gpus 1 on CPU: a process group at world size 1 (collectives still run) and p50 measured
-    through a real POST /parse server process next to the engine-only latency."""
+    """--gpus 1 --backend gloo on CPU: a process group at world size 1 (collectives still run) and
+    p50 measured through a real POST /parse server process next to the engine-only latency."""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--steps", "1", "--warmup", "1",
+           "--backend", "gloo",
            "--lines-per-gpu", "4000", "--block-lines", "4000", "--parse-requests", "2", "--patterns", "60"]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     env.pop("WORLD_SIZE", None)

@@ -87,3 +87,24 @@ def test_rank_failure_degrades_to_survivors(tmp_path, mode):
     for s in range(STEPS):
         top = np.sort(ref[s][2])[::-1][:5]
         np.testing.assert_allclose(got[0][f"top{s}"], top, rtol=1e-13)
+
+
+def test_rccl_rebuild_aborts_instead_of_destroying(monkeypatch):
+    """On RCCL a rebuild must ncclCommAbort the old communicator (_abort_process_group): a
+    destroy_process_group would wait for the dead peer's outstanding collectives."""
+    from datetime import timedelta
+    import torch.distributed as dist
+    from log_parser_amd.parallel import elastic as E
+    calls = []
+    monkeypatch.setattr(E.ElasticGroup, "_init_pg", lambda self: calls.append("init"))
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist.distributed_c10d, "_abort_process_group", lambda group=None: calls.append("abort"))
+    monkeypatch.setattr(dist, "destroy_process_group", lambda group=None: calls.append("destroy"))
+    store = dist.HashStore()
+    g = E.ElasticGroup(store, 0, 1, backend="nccl", timeout_s=5.0, grace_s=0.05)
+    g.rebuild()
+    assert calls == ["init", "abort", "init"] and g.members == [0] and g.gen == 1
+    calls.clear()
+    g.backend = "gloo"
+    g.rebuild()
+    assert calls == ["destroy", "init"]

@@ -374,11 +374,11 @@ PYBIND11_MODULE(_lpnative, m) {
                         uint64_t out, int64_t cap) {
     return scan_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs),
                      nregs, dfa_from(dfa), P<int64_t>(out), cap); });
-  m.def("scan_multi", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, py::tuple pass, uint64_t out,
-                         int64_t cap, uint64_t cnt, int grid, uint64_t s, bool dev) -> int64_t {
+  m.def("scan_multi", [](uint64_t text, int64_t nbytes, uint64_t ls, uint64_t ll, int64_t nl, py::tuple pass,
+                         uint64_t out, int64_t cap, uint64_t cnt, int grid, uint64_t s, bool dev) -> int64_t {
     const ScanPass S = scan_pass_from(pass);
     if (dev) {
-      scan_multi_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, S, P<int64_t>(out), cap,
+      scan_multi_dev(P<const uint8_t>(text), nbytes, P<const int64_t>(ls), P<const int32_t>(ll), nl, S, P<int64_t>(out), cap,
                      P<unsigned long long>(cnt), grid, s);
       return 0;
     }

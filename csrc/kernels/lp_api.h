@@ -78,7 +78,7 @@ struct ScanPass {
   int bm_off;             // word offset of bm4
   int rid_off;            // word offset of the regex ids (16 per group)
 };
-void scan_multi_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                     const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,
                     uint64_t stream);
 int64_t scan_multi_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,

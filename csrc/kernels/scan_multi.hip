@@ -9,11 +9,11 @@
 //
 // Two copies of every group's automaton (models/compiled.py _scan_blob):
 //   * LDS (hot loop): bm4 at byte 0 -- bm4[c] holds 2 x (column of byte c in group g) in byte
-//     g -- then uint16 transition rows whose entries are the LDS BYTE offset of the next state's
-//     row, so the next address is row + bm4 byte: one (SDWA) v_add. Row stride is odd (nc + 2 or
-//     nc + 3 entries) so rows start on spread-out banks. Column 0 is "hold" (next = self),
-//     column 1 is '\n' (next = start state), column 2 + k = byte class k; byte 0xFF maps to hold
-//     in every group. States are numbered so that every state from which ANY regex can accept
+//     g, entries 256..511 are 0 (hold) -- then uint16 transition rows whose entries are the LDS
+//     BYTE offset of the next state's row, so the next address is row + bm4 byte: one v_add. Row
+//     stride is odd (nc + 2 or nc + 3 entries) so rows start on spread-out banks. Column 0 is
+//     "hold" (next = self), column 1 is '\n' (next = start state), column 2 + k = byte class k.
+//     States are numbered so that every state from which ANY regex can accept
 //     (on some next byte, at end of line or before a final terminator) comes last: "a match may
 //     have happened" is just max(row offset) >= thr[g] -- one v_max per byte, no mask traffic.
 //   * global (rare path): exact uint32 rows, next state id | accept mask << 16 (masks of the
@@ -21,15 +21,18 @@
 //     per-state [EOL, before-final-terminator] masks and the regex ids.
 //
 // Work split: one lane walks a RUN of SCAN_RUN consecutive lines as ONE byte stream (the '\n'
-// between lines is the restart column, a '\r' right before it is held), so a wave's time is the
-// max of 64 run lengths, not of 64 line lengths. Bytes outside the run and a '\r' before '\n'
-// are overwritten with 0xFF (hold) in the loaded words; a REAL 0xFF byte (never in valid UTF-8)
-// sends the run to the exact walk. Per byte: one LDS read of bm4, then per group one v_add +
-// one ds_read_u16 + one v_max: G independent dependency chains per lane. A 16-byte
-// block whose states crossed a threshold is walked again on the exact global tables from the
-// saved states, attributing accept masks to lines. Runs containing a line whose content ends in
-// a line terminator ('$' must also be tried before it, Matcher.find) or an unusual separator
-// take the exact per-line walk.
+// between lines is the restart column), so a wave's time is the max of 64 run lengths, not of 64
+// line lengths. No byte of the hot loop is masked: the walk starts at the aligned block holding
+// the run's first byte and lets the preceding '\n' restart the automaton (garbage prefix), and it
+// ends by walking the last line's separator, whose '\n' column yields that line's end-of-line
+// accepts (bytes after it are garbage). Only "\r\n"-separated runs take a variant whose bytemap
+// has 512 entries: the separator's '\r' indexes entry 256 + c = hold. Per byte: one LDS read of
+// bm4, then per group one v_add + one ds_read_u16 + one v_max: G independent dependency chains
+// per lane. A 16-byte block whose states crossed a threshold is walked again exactly (global
+// tables, out-of-run bytes skipped, separator '\r' held) from the saved states, attributing
+// accept masks to lines; garbage bytes can only cause such a re-walk, never a hit. Runs with a
+// line whose content ends in a line terminator ('$' must also be tried before it, Matcher.find),
+// an unusual separator or a document boundary take the exact per-line walk.
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
@@ -42,7 +45,7 @@
 
 namespace lp {
 
-constexpr int SCAN_THREADS = 256;
+constexpr int SCAN_THREADS = 1024;   // LDS is per block: more waves per staged byte
 constexpr int SCAN_RUN = 4;
 
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t t) {   // high bit of every zero byte of t
@@ -98,32 +101,109 @@ struct GlobalEmit {
   }
 };
 
-// 0xFF in every byte of a 32-bit word where `nib` (4 bits, one per byte) is set
-__device__ __forceinline__ uint32_t byte_mask4(uint32_t nib) {
-  return ((nib & 1u) ? 0xFFu : 0u) | ((nib & 2u) ? 0xFF00u : 0u) | ((nib & 4u) ? 0xFF0000u : 0u) |
-         ((nib & 8u) ? 0xFF000000u : 0u);
-}
-
 // content of line [st, st + n) ends in a line terminator ('\r', U+0085, U+2028, U+2029): two
-// aligned dword loads instead of up to three dependent byte loads (text is padded both ways:
-// reading the dword before the text start is avoided by the n checks)
+// aligned dword loads instead of up to three dependent byte loads
 __device__ __forceinline__ bool ends_in_terminator(const uint8_t* text, int64_t st, int n) {
   if (n <= 0) return false;
   const int64_t e = st + n;                       // one past the last content byte
   const int64_t a = (e - 1) & ~(int64_t)3;
   const uint32_t hi = *reinterpret_cast<const uint32_t*>(text + a);
   const uint32_t lo = a >= 4 ? *reinterpret_cast<const uint32_t*>(text + a - 4) : 0u;
-  const int sh = (int)(e - a);                    // 1..4 bytes of `hi` belong to the tail
-  // last 3 bytes, the final byte in bits 16..23: (lo:hi) >> (8 * sh) ... take the top 3 of 8
+  const int sh = (int)(e - a);                    // 1..4 bytes of `hi` belong to the content
   const uint64_t v = ((uint64_t)hi << 32 | lo) >> (8 * sh);
-  const uint32_t t3 = (uint32_t)(v >> 8) & 0xFFFFFFu;   // byte -3, -2, -1 in bits 0..7, 8..15, 16..23
+  const uint32_t t3 = (uint32_t)(v >> 8) & 0xFFFFFFu;   // bytes -3, -2, -1 in bits 0..7, 8..15, 16..23
   const uint32_t b1 = t3 >> 16, b2 = (t3 >> 8) & 0xFFu, b3 = t3 & 0xFFu;
   return b1 == 0x0Du || (n >= 2 && b2 == 0xC2u && b1 == 0x85u) ||
          (n >= 3 && b3 == 0xE2u && b2 == 0x80u && (b1 == 0xA8u || b1 == 0xA9u));
 }
 
+// bit 8b+7 set where byte b of w is '\r' and the byte after it (nx = the following word) '\n'
+__device__ __forceinline__ uint32_t crlf_bits(uint32_t w, uint32_t nx) {
+  return nz_bytes(w ^ 0x0D0D0D0Du) & nz_bytes(__builtin_amdgcn_alignbyte(nx, w, 1) ^ 0x0A0A0A0Au);
+}
+
+// exact re-walk of one 16-byte block [p0, p0 + 16) of a run (rare path): bytes outside
+// [p_lo, p_end) are skipped, a separator '\r' is held, '\n' ends line l
+template <typename Emit>
+__device__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, const uint32_t (&w)[5], int64_t p0,
+                                 int64_t p_lo, int64_t p_end, int64_t x0, int64_t x1,
+                                 const int64_t* line_start, int g, uint32_t st, Emit&& emit) {
+  int64_t l = x0;
+  const int64_t first = p0 > p_lo ? p0 : p_lo;
+  while (l + 1 < x1 && line_start[l + 1] <= first) ++l;
+  if (p0 <= p_lo) st = S.init_state[g];
+  uint32_t lacc = 0;
+  for (int j = 0; j < 16; ++j) {
+    const int64_t pos = p0 + j;
+    if (pos < p_lo || pos >= p_end) continue;
+    const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    const uint32_t nx = (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFFu;
+    const uint32_t col = (c == 0x0Du && nx == 0x0Au) ? 0u : ((bm[c] >> (8 * g)) & 0xFFu) >> 1;
+    const uint32_t e = scan_step(S, g, st, col);
+    lacc |= e >> 16;
+    st = e & 0xFFFFu;
+    if (col == 1u) {
+      scan_emit(S, g, lacc, l, emit);
+      lacc = 0;
+      ++l;
+    }
+  }
+  scan_emit(S, g, lacc, l < x1 ? l : x1 - 1, emit);
+}
+
+// the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold
+template <int G, bool CRLF, typename Emit>
+__device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass& S, const uint8_t* text, int64_t p_lo,
+                                              int64_t p_end, int64_t x0, int64_t x1,
+                                              const int64_t* __restrict__ line_start, Emit&& emit) {
+  const uint8_t* lds = reinterpret_cast<const uint8_t*>(sm);
+  uint32_t xr[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
+  const int64_t a0 = p_lo & ~(int64_t)15;
+  const uint4* blk = reinterpret_cast<const uint4*>(text + a0);
+  uint4 cur = blk[0];
+  for (int64_t p0 = a0; p0 < p_end; p0 += 16) {
+    const uint4 nxt = blk[1];
+    ++blk;
+    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
+    uint32_t hold = 0;                    // CRLF: byte j of the block is a separator '\r'
+    if constexpr (CRLF) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t b = crlf_bits(w[q], w[q + 1]);
+        hold |= (((b >> 7) & 1u) | ((b >> 14) & 2u) | ((b >> 21) & 4u) | ((b >> 28) & 8u)) << (4 * q);
+      }
+    }
+    uint32_t xs[G], mx[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      xs[g] = xr[g];
+      mx[g] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;        // entry 256 + c: hold
+      const uint32_t b = sm[c];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        mx[g] = max(mx[g], xr[g]);
+        xr[g] = *reinterpret_cast<const uint16_t*>(lds + xr[g] + ((b >> (8 * g)) & 0xFFu));
+      }
+    }
+    bool hot = false;
+#pragma unroll
+    for (int g = 0; g < G; ++g) hot |= mx[g] >= (uint32_t)S.thr[g];
+    if (hot)        // rare: a state that can accept was visited -- exact re-walk of this block
+      for (int g = 0; g < G; ++g)
+        scan_block_exact(S, sm, w, p0, p_lo, p_end, x0, x1, line_start, g, scan_state_of(S, g, xs[g]), emit);
+    cur = nxt;
+  }
+}
+
 template <int G>
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_multi(const uint8_t* __restrict__ text,
+__global__ __launch_bounds__(SCAN_THREADS) void k_scan_multi(const uint8_t* __restrict__ text, int64_t nbytes,
                                                              const int64_t* __restrict__ line_start,
                                                              const int32_t* __restrict__ line_len, int64_t nlines,
                                                              ScanPass S, int64_t* __restrict__ out, int64_t cap,
@@ -132,121 +212,47 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_multi(const uint8_t* __re
   for (int i = threadIdx.x * 4; i < S.lds_words; i += SCAN_THREADS * 4)      // lds_words: multiple of 4
     *reinterpret_cast<uint4*>(sm + i) = *reinterpret_cast<const uint4*>(S.blob + i);
   __syncthreads();
-  const uint8_t* lds = reinterpret_cast<const uint8_t*>(sm);
-  const uint32_t* bm = sm;
   const GlobalEmit emit{out, cap, count};
   const int64_t nruns = (nlines + SCAN_RUN - 1) / SCAN_RUN;
   const int64_t stride = (int64_t)gridDim.x * SCAN_THREADS;
   for (int64_t run = (int64_t)blockIdx.x * SCAN_THREADS + threadIdx.x; run < nruns; run += stride) {
     const int64_t x0 = run * SCAN_RUN;
     const int64_t x1 = x0 + SCAN_RUN < nlines ? x0 + SCAN_RUN : nlines;
-    // the stream walk needs separators "\n" or "\r\n" between the run's lines and no line whose
-    // content ends in a line terminator
-    bool fast = true;
+    // stream walk preconditions: "\n" / "\r\n" separators (after every line of the run,
+    // the last one included), the run starts right after a '\n', no content ends in a terminator
+    bool fast = true, crlf = false;
     int64_t st_next = line_start[x0];
+    const int64_t p_lo = st_next;
+    int64_t p_end = 0;
     for (int64_t x = x0; x < x1; ++x) {
       const int64_t st = st_next;
       const int n = line_len[x];
       if (ends_in_terminator(text, st, n)) fast = false;
-      if (x + 1 < x1) {
+      int64_t sep;
+      if (x + 1 < nlines) {
         st_next = line_start[x + 1];
-        const int64_t sep = st_next - st - n;
-        if (sep != 1 && sep != 2) fast = false;
+        sep = st_next - st - n;
+      } else {                                   // the text's last line: is there a newline after it?
+        const int64_t e = st + n;
+        sep = (e < nbytes && text[e] == '\n') ? 1 : (e + 1 < nbytes && text[e] == '\r' && text[e + 1] == '\n') ? 2 : 0;
       }
+      if (sep == 2) crlf = true;
+      else if (sep != 1) fast = false;
+      p_end = st + n + sep;                      // after the last line's separator
     }
-    const int64_t p_lo = line_start[x0];
-    const int64_t p_hi = line_start[x1 - 1] + line_len[x1 - 1];
-    uint32_t xr[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
-    const int64_t a0 = p_lo & ~(int64_t)15;
-    const uint4* blk = reinterpret_cast<const uint4*>(text + a0);
-    uint4 cur = blk[0];
-    for (int64_t p0 = a0; fast && p0 < p_hi; p0 += 16) {
-      const uint4 nxt = blk[1];
-      ++blk;
-      uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
-      // bytes outside [p_lo, p_hi) -> 0xFF (hold)
-      const int64_t lo = p_lo - p0, hi = p_hi - p0;
-      uint32_t inval = 0;
-      if (lo > 0) inval |= (1u << (lo < 16 ? lo : 16)) - 1u;
-      if (hi < 16) inval |= 0xFFFFu & ~((1u << hi) - 1u);
-      uint32_t ff = 0, cr = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ff |= nz_bytes(~w[q]) & ~byte_mask4(inval >> (4 * q));
-        cr |= nz_bytes(w[q] ^ 0x0D0D0D0Du);
-      }
-      if (ff) {            // a real 0xFF byte: this run takes the exact walk
-        fast = false;
-        break;
-      }
-      if (cr) {            // rare: '\r' immediately before '\n' is part of Java split's "\r?\n"
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t b = nz_bytes(w[q] ^ 0x0D0D0D0Du) &
-                             nz_bytes(__builtin_amdgcn_alignbyte(w[q + 1], w[q], 1) ^ 0x0A0A0A0Au);
-          inval |= (((b >> 7) & 1u) | ((b >> 14) & 2u) | ((b >> 21) & 4u) | ((b >> 28) & 8u)) << (4 * q);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] |= byte_mask4(inval >> (4 * q));
-      uint32_t xs[G], mx[G];
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        xs[g] = xr[g];
-        mx[g] = 0;
-      }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const uint32_t b = bm[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          mx[g] = max(mx[g], xr[g]);
-          xr[g] = *reinterpret_cast<const uint16_t*>(lds + xr[g] + ((b >> (8 * g)) & 0xFFu));
-        }
-      }
-      bool hot = false;
-#pragma unroll
-      for (int g = 0; g < G; ++g) hot |= mx[g] >= (uint32_t)S.thr[g];
-      if (hot) {
-        // rare: a state that can accept was visited in this block -- walk it again on the exact
-        // tables from the saved states, attributing masks to lines ('\n' ends line l: its mask
-        // is that line's end-of-line accept)
-        int64_t li = x0;
-        const int64_t first = p0 + (lo > 0 ? lo : 0);
-        while (li + 1 < x1 && line_start[li + 1] <= first) ++li;
-        for (int g = 0; g < G; ++g) {
-          uint32_t st = scan_state_of(S, g, xs[g]), lacc = 0;
-          int64_t l = li;
-          for (int j = 0; j < 16; ++j) {
-            const uint32_t col = ((bm[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu] >> (8 * g)) & 0xFFu) >> 1;
-            const uint32_t e = scan_step(S, g, st, col);
-            lacc |= e >> 16;
-            st = e & 0xFFFFu;
-            if (col == 1u) {
-              scan_emit(S, g, lacc, l, emit);
-              lacc = 0;
-              ++l;
-            }
-          }
-          scan_emit(S, g, lacc, l, emit);
-        }
-      }
-      cur = nxt;
-    }
-    if (!fast) {     // rare: exact per-line walks (duplicates of hits emitted above are removed downstream)
-      for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, bm, text + line_start[x], line_len[x], x, emit);
+    if (p_lo > 0 && text[p_lo - 1] != '\n') fast = false;   // e.g. a document boundary in a batch
+    if (!fast) {     // rare: exact per-line walks
+      for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
       continue;
     }
-    // end of the run's last line: its end-of-line accepts
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (xr[g] >= (uint32_t)S.thr[g]) scan_emit(S, g, scan_fin(S, g, scan_state_of(S, g, xr[g]), 0), x1 - 1, emit);
+    if (crlf)
+      scan_run_fast<G, true>(sm, S, text, p_lo, p_end, x0, x1, line_start, emit);
+    else
+      scan_run_fast<G, false>(sm, S, text, p_lo, p_end, x0, x1, line_start, emit);
   }
 }
 
-void scan_multi_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
+void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                     const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,
                     uint64_t stream) {
   if (nlines <= 0 || S.ngroups <= 0) return;
@@ -258,13 +264,13 @@ void scan_multi_dev(const uint8_t* text, const int64_t* line_start, const int32_
   const int g = (int)std::max<int64_t>(1, std::min<int64_t>(grid, need));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (S.ngroups) {
-    case 1: hipLaunchKernelGGL(k_scan_multi<1>, dim3(g), dim3(SCAN_THREADS), lds, st, text, line_start, line_len,
+    case 1: hipLaunchKernelGGL(k_scan_multi<1>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
                                nlines, S, out, cap, count); break;
-    case 2: hipLaunchKernelGGL(k_scan_multi<2>, dim3(g), dim3(SCAN_THREADS), lds, st, text, line_start, line_len,
+    case 2: hipLaunchKernelGGL(k_scan_multi<2>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
                                nlines, S, out, cap, count); break;
-    case 3: hipLaunchKernelGGL(k_scan_multi<3>, dim3(g), dim3(SCAN_THREADS), lds, st, text, line_start, line_len,
+    case 3: hipLaunchKernelGGL(k_scan_multi<3>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
                                nlines, S, out, cap, count); break;
-    default: hipLaunchKernelGGL(k_scan_multi<4>, dim3(g), dim3(SCAN_THREADS), lds, st, text, line_start, line_len,
+    default: hipLaunchKernelGGL(k_scan_multi<4>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
                                 nlines, S, out, cap, count); break;
   }
   hipError_t e = hipGetLastError();

@@ -328,7 +328,7 @@ class Engine:
         t = self._tick(timings, "prefilter", t)
         extra = []
         for sp in self.tabs["scan_passes"]:        # literal-free regexes: multi-regex DFAs in LDS
-            extra.append(K.scan_multi(text, ls, ll, sp, max(1024, ls.numel() >> 6), self.scan_grid(sp)))
+            extra.append(K.scan_multi(text, nbytes, ls, ll, sp, max(1024, ls.numel() >> 6), self.scan_grid(sp)))
         if self.tabs["scan_regs"].numel():        # one whose DFA alone exceeds a scan group
             extra.append(K.scan(text, ls, ll, self.tabs["scan_regs"], self.tabs["dfa"], max(1024, ls.numel())))
         for ncls, glist in self.tabs["nfa_scan_lists"].items():       # DFA blow-up regexes: MFMA NFA
@@ -345,7 +345,7 @@ class Engine:
         """Persistent grid of k_scan_multi: as many blocks per CU as the pass's LDS blob allows."""
         if self.device.type != "cuda":
             return 0
-        per_cu = max(1, min(8, (160 << 10) // max(sp[1] * 4, 1)))       # sp[1] = LDS words
+        per_cu = max(1, min(2, (160 << 10) // max(sp[1] * 4, 1)))       # sp[1] = LDS words; 1024-thread blocks
         return self.n_cus * per_cu
 
     def _ev_tables(self, segs: "Segments") -> tuple:

@@ -403,7 +403,7 @@ class CompiledLibrary:
         """One pass -> the blob of scan_multi.hip (uint32 words): [bm4 | u16 rows] staged in LDS,
         then the exact tables the rare path reads from global memory. States are renumbered so
         that the ones from which a member can accept come last (the hot loop's threshold test)."""
-        BM_BYTES = 1024                                     # bm4 at LDS byte 0, rows after it
+        BM_BYTES = 2048                                     # bm4 (512 entries) at LDS byte 0, rows after
         rows16, exact, fins = [], [], []
         meta = {k: [0] * 4 for k in ("row_base", "stride", "thr", "init_row", "init_state", "ncol")}
         bm4 = np.zeros(256, np.uint32)
@@ -438,15 +438,14 @@ class CompiledLibrary:
             base += ns * stride
             col2 = (np.frombuffer(d["bytemap"], np.uint8).astype(np.uint32) + np.uint32(2)) * np.uint32(2)
             col2[10] = 2                                                      # '\n': never inside a line
-            col2[0xFF] = 0                                                    # 0xFF: hold (masked bytes)
             bm4 |= col2 << np.uint32(8 * g)
         if 2 * base > 0xFFFF:
             raise ValueError("scan pass rows exceed the uint16 byte offset")
         r = np.concatenate(rows16)
         if r.size % 8:
             r = np.concatenate([r, np.zeros(8 - r.size % 8, np.uint16)])      # whole uint4 words
-        parts = [bm4, r.view(np.uint32)]
-        off = 256 + r.size // 2
+        parts = [bm4, np.zeros(256, np.uint32), r.view(np.uint32)]    # entries 256..511: hold
+        off = 512 + r.size // 2
         lds_words = off
         gt_off, fin_off = [0] * 4, [0] * 4
         for g in range(len(groups)):

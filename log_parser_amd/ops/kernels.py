@@ -181,7 +181,7 @@ def scan(text, line_start, line_len, regs: torch.Tensor, dfa_tuple, cap: int) ->
         cap = c
 
 
-def scan_multi(text, line_start, line_len, pass_tuple, cap: int, grid: int = 1024) -> torch.Tensor:
+def scan_multi(text, nbytes: int, line_start, line_len, pass_tuple, cap: int, grid: int = 1024) -> torch.Tensor:
     """Literal-free regexes of one scan pass (<= 4 multi-regex DFA groups) over every line ->
     (regex << 32 | line) hits, already verified."""
     nlines = line_start.numel()
@@ -191,11 +191,11 @@ def scan_multi(text, line_start, line_len, pass_tuple, cap: int, grid: int = 102
         out = torch.empty(max(cap, 1), dtype=torch.int64, device=text.device)
         if text.is_cuda:
             cnt = torch.zeros(1, dtype=torch.int64, device=text.device)
-            N.scan_multi(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), nlines, pass_tuple,
+            N.scan_multi(text.data_ptr(), nbytes, line_start.data_ptr(), line_len.data_ptr(), nlines, pass_tuple,
                          out.data_ptr(), cap, cnt.data_ptr(), grid, _s(text), True)
             c = int(cnt.item())
         else:
-            c = N.scan_multi(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), nlines, pass_tuple,
+            c = N.scan_multi(text.data_ptr(), nbytes, line_start.data_ptr(), line_len.data_ptr(), nlines, pass_tuple,
                              out.data_ptr(), cap, 0, 0, 0, False)
         if c <= cap:
             return out[:c]

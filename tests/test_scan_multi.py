@@ -94,7 +94,7 @@ def test_scan_passes_equal_per_regex_scan_cpu():
     t = _text("cpu", data)
     ls, ll = K.split_lines(t, len(data))
     tabs = lib.device_tables(torch.device("cpu"))
-    got = torch.cat([K.scan_multi(t, ls, ll, sp, 1024) for sp in tabs["scan_passes"]])
+    got = torch.cat([K.scan_multi(t, len(data), ls, ll, sp, 1024) for sp in tabs["scan_passes"]])
     regs = torch.tensor(lib.scan_regs, dtype=torch.int32)
     want = K.scan(t, ls, ll, regs, tabs["dfa"], 1024)
     assert want.numel() > 10
@@ -125,8 +125,8 @@ def test_scan_multi_gpu_equals_host(gpu_device):
     tabs_c = lib.device_tables(torch.device("cpu"))
     n = 0
     for sp_d, sp_c in zip(ed.tabs["scan_passes"], tabs_c["scan_passes"]):
-        hd = K.scan_multi(td, ls_d, ll_d, sp_d, 16, ed.scan_grid(sp_d))     # tiny cap: the retry path too
-        hc = K.scan_multi(tc, ls_c, ll_c, sp_c, 1024)
+        hd = K.scan_multi(td, len(data), ls_d, ll_d, sp_d, 16, ed.scan_grid(sp_d))     # tiny cap: the retry path too
+        hc = K.scan_multi(tc, len(data), ls_c, ll_c, sp_c, 1024)
         assert torch.equal(torch.sort(hd.cpu()).values, torch.sort(hc).values)
         n += hc.numel()
     assert n > 50
@@ -158,3 +158,77 @@ def test_realistic_engine_matches_golden_gpu(gpu_device):
     assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r["events"]] == \
         [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
     np.testing.assert_allclose([e["score"] for e in r["events"]], [e["score"] for e in g["events"]], rtol=1e-12)
+
+
+EDGE_REGEXES = [r"^$", r"^\s*$", r"\d+$", r"[A-Z]{2}\b", r"^\t\w+", r"\b[a-z]{1,2}\b", r"\w\r?$",
+                r"[^\s]+@[^\s]+", r"^[A-Z]", r"\W{2,}", r"x*", r"\s$"]
+
+
+def _edge_text(seed: int) -> bytes:
+    rng = random.Random(seed)
+    parts = []
+    for i in range(4000):
+        kind = rng.random()
+        if kind < 0.1:
+            line = b""
+        elif kind < 0.2:
+            line = b"  \t "
+        elif kind < 0.3:
+            line = bytes(rng.choice(b"AB cd1\t@.x-") for _ in range(rng.randint(1, 300)))
+        elif kind < 0.35:
+            line = b"ends with cr\r"                     # content ending in a terminator
+        elif kind < 0.38:
+            line = b"nel \xc2\x85"                         # U+0085 at the end of content
+        elif kind < 0.4:
+            line = b"bad \xff byte \xfe AB"
+        else:
+            line = bytes(rng.choice(b"abcdefgh ABC 0123\t_@.") for _ in range(rng.randint(1, 90)))
+        parts.append(line + (b"\r\n" if rng.random() < 0.2 else b"\n"))
+    if rng.random() < 0.5:
+        parts[-1] = parts[-1].rstrip(b"\r\n")             # last line without a newline
+    return b"".join(parts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_scan_multi_edge_cases_gpu_equals_host(gpu_device, seed):
+    """Stream-walk preconditions and fallbacks on the device: empty / blank lines, nullable
+    regexes (start state accepting), CRLF and LF mixed, content ending in '\\r' or U+0085, bytes
+    0xFF, long lines, a last line without newline -- hits equal the exact host walk."""
+    pats = [{"id": f"e{i}", "name": f"e{i}", "severity": "LOW", "primary_pattern": {"regex": rx, "confidence": 0.5}}
+            for i, rx in enumerate(EDGE_REGEXES)]
+    from log_parser_amd.models.schema import PatternSet
+    lib = CompiledLibrary([PatternSet.model_validate({"metadata": {"library_id": "edge"}, "patterns": pats})],
+                          ScoringParams())
+    assert len(lib.scan_regs) >= 8 and lib.scan_passes
+    data = _edge_text(seed)
+    td, tc = _text(gpu_device, data), _text("cpu", data)
+    ls_d, ll_d = K.split_lines(td, len(data))
+    ls_c, ll_c = K.split_lines(tc, len(data))
+    ed = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    tabs_c = lib.device_tables(torch.device("cpu"))
+    for sp_d, sp_c in zip(ed.tabs["scan_passes"], tabs_c["scan_passes"]):
+        hd = torch.unique(K.scan_multi(td, len(data), ls_d, ll_d, sp_d, 1024, ed.scan_grid(sp_d)).cpu())
+        hc = torch.unique(K.scan_multi(tc, len(data), ls_c, ll_c, sp_c, 1024))
+        assert hc.numel() > 100
+        assert torch.equal(hd, hc)
+
+
+@pytest.mark.gpu
+def test_scan_multi_batch_documents_gpu(gpu_device):
+    """A continuous batch packs documents back to back (some without a final newline): runs that
+    cross a document boundary must not leak automaton state between documents."""
+    pats = [{"id": f"e{i}", "name": f"e{i}", "severity": "LOW", "primary_pattern": {"regex": rx, "confidence": 0.5}}
+            for i, rx in enumerate(EDGE_REGEXES)]
+    from log_parser_amd.models.schema import PatternSet
+    sets = [PatternSet.model_validate({"metadata": {"library_id": "edge"}, "patterns": pats})]
+    lib = CompiledLibrary(sets, ScoringParams())
+    rng = random.Random(7)
+    docs = [_edge_text(s)[:rng.randint(1, 3000)].decode("utf-8", errors="replace") for s in range(40)]
+    ed = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    ec = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    import json as _json
+    for a, b in zip(ed.analyze_batch_json(docs), ec.analyze_batch_json(docs)):
+        ja, jb = _json.loads(a), _json.loads(b)
+        assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in ja["events"]] == \
+            [(e["lineNumber"], e["matchedPattern"]["id"]) for e in jb["events"]]

@@ -82,8 +82,8 @@ def main():
         def run_dfa():
             outs = []
             for sp in tabs["scan_passes"]:
-                per_cu = max(1, min(8, (160 << 10) // (sp[1] * 4)))
-                outs.append(K.scan_multi(t, ls, ll, sp, max(1024, L >> 4), n_cus * per_cu))
+                per_cu = max(1, min(2, (160 << 10) // (sp[1] * 4)))
+                outs.append(K.scan_multi(t, len(data), ls, ll, sp, max(1024, L >> 4), n_cus * per_cu))
             return torch.cat(outs) if outs else torch.empty(0, dtype=torch.int64, device=dev)
         us, h = timed(run_dfa, args.reps)
         hits["dfa"] = torch.sort(h).values.cpu()

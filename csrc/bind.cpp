@@ -329,9 +329,6 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("parse_pod_request", &parse_pod_request_py);
 
   // ---- device launchers
-  m.def("pull_dev", [](uint64_t src, uint64_t dst, int64_t n, int grid, uint64_t s) {
-    pull_dev(P<const uint8_t>(src), P<uint8_t>(dst), n, grid, s);
-  });
   m.def("nl_count_dev", [](uint64_t text, int64_t n, uint64_t cnt, uint64_t s) { nl_count_dev(P<const uint8_t>(text), n, P<int32_t>(cnt), s); });
   m.def("lines_dev", [](uint64_t nl, int64_t n_nl, uint64_t text, int64_t nb, uint64_t st, uint64_t ln, uint64_t last,
                         uint64_t s) {
@@ -351,8 +348,6 @@ PYBIND11_MODULE(_lpnative, m) {
                   P<const unsigned long long>(dn), max_grid); }, py::arg("gh"), py::arg("n"), py::arg("text"),
         py::arg("nb"), py::arg("pf"), py::arg("ls"), py::arg("nl"), py::arg("blk"), py::arg("cand"), py::arg("cap"),
         py::arg("count"), py::arg("s"), py::arg("dn") = 0, py::arg("max_grid") = 8192);
-  m.def("verify_dev", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out, uint64_t s) {
-    verify_dev(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out), s); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
                        uint64_t out, int64_t cap, uint64_t count, uint64_t s) {
     scan_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs), nregs,
@@ -368,8 +363,6 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("nl_positions_host", [](uint64_t text, int64_t n, uint64_t pos) { return nl_positions_host(P<const uint8_t>(text), n, P<int64_t>(pos)); });
   m.def("prefilter_host", [](uint64_t text, int64_t n, py::tuple pf, uint64_t ls, int64_t nl, uint64_t cand, int64_t cap) {
     return prefilter_host(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap); });
-  m.def("verify_host", [](uint64_t cand, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t out) {
-    verify_host(P<const int64_t>(cand), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(out)); });
   m.def("scan_host", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
                         uint64_t out, int64_t cap) {
     return scan_host(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs),
@@ -488,12 +481,6 @@ PYBIND11_MODULE(_lpnative, m) {
     else
       seq_chain_host(P<const int32_t>(slot_seq), P<const int32_t>(off), P<const int32_t>(reg), P<const int64_t>(hoff),
                      P<const int32_t>(hline), lo, hi, n, P<int32_t>(out));
-  });
-
-  m.def("feat", [](uint64_t lines, int64_t n, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t feat,
-                   uint64_t s, bool dev) {
-    if (dev) feat_dev(P<const int32_t>(lines), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(feat), s);
-    else feat_host(P<const int32_t>(lines), n, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(feat));
   });
 
   m.def("nfa", [](uint64_t groups, uint64_t glist, int ng, int ncls, uint64_t lines, int64_t nsel, uint64_t text,

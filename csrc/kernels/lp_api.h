@@ -9,7 +9,6 @@ namespace lp {
 int64_t nl_tiles(int64_t nbytes);
 // worker threads of the host twins (CPU backend)
 void set_host_threads(int n);
-void pull_dev(const uint8_t* host_src, uint8_t* dst, int64_t nbytes, int grid, uint64_t stream);
 void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream);
 // flag_cr: set bit 62 of a position when the '\n' follows a '\r' (consumed by lines_dev)
 void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, int flag_cr,
@@ -20,8 +19,6 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn = nullptr,
                    int max_grid = 8192);
-void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
-                const DfaPool& P, uint8_t* out, uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
               const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
               uint64_t stream);
@@ -36,15 +33,9 @@ void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const in
                     int32_t* out);
 void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
                unsigned long long* last_nonempty, uint64_t stream);
-void feat_dev(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
-              const DfaPool& P, uint8_t* feat, uint64_t stream);
-void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
-               const DfaPool& P, uint8_t* feat);
 int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap);
-void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start,
-                 const int32_t* line_len, const DfaPool& P, uint8_t* out);
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                   const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap);
 void score_host(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,

@@ -2,10 +2,10 @@
 //
 // Hot loops of the reference and the kernel that replaces each:
 //   K1 line split     AnalysisService.java:53              -> k_nl_count / k_nl_write
-//   K3 primary match  AnalysisService.java:89-95           -> k_prefilter (literal bloom in LDS)
-//                                                             + k_verify (byte DFA)
+//   K3 primary match  AnalysisService.java:89-95           -> k_prefilter (literal bloom + Teddy in LDS)
+//                                                             + k_pf_verify, DFA verify in lp_post.hip
 //   K4/K5 aux match   ScoringService.java:272-347          -> same engine, all aux regexes
-//   K6 context feats  ContextAnalysisService.java:27-83    -> 4 internal regexes, same engine
+//   K6 context feats  ContextAnalysisService.java:27-83    -> k_feat_cov (lp_post.hip)
 //   K7-K9 scoring     ScoringService.java:63-151           -> k_score (fp64, one thread / event)
 // Wave64 throughout; block sizes are multiples of 64; persistent grid-stride grids sized to the
 // 256 CUs so the LDS-resident bloom filter is loaded once per block, not once per tile.
@@ -169,25 +169,6 @@ __global__ __launch_bounds__(256) void k_lines(const int64_t* __restrict__ nl, i
   }
   starts[i] = st;
   lens[i] = (int32_t)(en - st);
-}
-
-// Host -> device "pull" copy: the GPU reads pinned host memory directly over PCIe (no SDMA
-// engine). Four 16-byte loads in flight per lane to cover the ~µs PCIe read latency.
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_pull(const v4u* __restrict__ src, v4u* __restrict__ dst, int64_t n16) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const v4u a = __builtin_nontemporal_load(src + i);
-    const v4u b = __builtin_nontemporal_load(src + i + stride);
-    const v4u c = __builtin_nontemporal_load(src + i + 2 * stride);
-    const v4u d = __builtin_nontemporal_load(src + i + 3 * stride);
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
-  }
-  for (; i < n16; i += stride) dst[i] = __builtin_nontemporal_load(src + i);
 }
 
 // Number of lines up to and including the last non-empty one (Java String.split drops trailing
@@ -458,38 +439,6 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
   if (c > 0) pf_flush(buf, &cnt, &gbase, c, cand, cap, count);
 }
 
-// ------------------------------------------------------------------------------------------
-// K6: context features, computed lazily for the lines inside some event's context window only
-// (ContextAnalysisService.java:62-83): bit0 ERROR, bit1 WARN (only evaluated when not ERROR: the
-// reference's else-if), bit2 stack-trace line, bit3 exception/error class name.
-__global__ __launch_bounds__(256) void k_feat(const int32_t* __restrict__ lines, int64_t n,
-                                              const uint8_t* __restrict__ text,
-                                              const int64_t* __restrict__ line_start,
-                                              const int32_t* __restrict__ line_len, DfaPool P,
-                                              uint8_t* __restrict__ feat) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t line = lines[i];
-  const uint8_t* s = text + line_start[line];
-  const int len = line_len[line];
-  feat[line] = context_feat(P, s, len);
-}
-
-// ------------------------------------------------------------------------------------------
-// K3b: verify candidates (one lane per (regex, line) candidate, byte DFA)
-__global__ __launch_bounds__(256) void k_verify(const int64_t* __restrict__ cand, int64_t n,
-                                                const uint8_t* __restrict__ text,
-                                                const int64_t* __restrict__ line_start,
-                                                const int32_t* __restrict__ line_len, DfaPool P,
-                                                uint8_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int64_t k = cand[i];
-  const int r = (int)(k >> 32);
-  const int64_t line = k & 0xFFFFFFFFll;
-  out[i] = dfa_run(P, r, text + line_start[line], line_len[line]) ? 1 : 0;
-}
-
 // K3c: regexes without a usable literal: every line x every scan regex
 __global__ __launch_bounds__(256) void k_scan(const uint8_t* __restrict__ text,
                                               const int64_t* __restrict__ line_start,
@@ -620,16 +569,6 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
   LP_CHECK(hipGetLastError());
 }
 
-void pull_dev(const uint8_t* host_src, uint8_t* dst, int64_t nbytes, int grid, uint64_t stream) {
-  if (nbytes <= 0) return;
-  // callers pass 16-byte aligned buffers padded to a multiple of 16 (K.padded_len)
-  const int64_t n16 = (nbytes + 15) / 16;
-  const int g = (int)std::min<int64_t>(grid, num_blocks(n16, 256));
-  hipLaunchKernelGGL(k_pull, dim3(g), dim3(256), 0, as_stream(stream), reinterpret_cast<const v4u*>(host_src),
-                     reinterpret_cast<v4u*>(dst), n16);
-  LP_CHECK(hipGetLastError());
-}
-
 void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
                unsigned long long* last_nonempty, uint64_t stream) {
   hipLaunchKernelGGL(k_lines, dim3(num_blocks(n_nl + 1, 256)), dim3(256), 0, as_stream(stream), nl, n_nl, text, nbytes,
@@ -637,26 +576,6 @@ void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nby
   LP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_last_nonempty, dim3(1), dim3(256), 0, as_stream(stream), lens, n_nl + 1, last_nonempty);
   LP_CHECK(hipGetLastError());
-}
-
-void feat_dev(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
-              const DfaPool& P, uint8_t* feat, uint64_t stream) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_feat, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), lines, n, text, line_start,
-                     line_len, P, feat);
-  LP_CHECK(hipGetLastError());
-}
-
-void feat_host(const int32_t* lines, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
-               const DfaPool& P, uint8_t* feat) {
-  host_parallel(n, 2048, [&](int, int64_t a, int64_t b) {
-    for (int64_t i = a; i < b; ++i) {
-      const int32_t line = lines[i];
-      const uint8_t* s = text + line_start[line];
-      const int len = line_len[line];
-      feat[line] = context_feat(P, s, len);
-    }
-  });
 }
 
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
@@ -673,14 +592,6 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
   else
     hipLaunchKernelGGL(k_pf_verify<16>, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
                        line_start, nlines, blk_line, cand, cap, count);
-  LP_CHECK(hipGetLastError());
-}
-
-void verify_dev(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start, const int32_t* line_len,
-                const DfaPool& P, uint8_t* out, uint64_t stream) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_verify, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), cand, n, text, line_start,
-                     line_len, P, out);
   LP_CHECK(hipGetLastError());
 }
 
@@ -781,18 +692,6 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
       ++count;
     }
   return count;
-}
-
-void verify_host(const int64_t* cand, int64_t n, const uint8_t* text, const int64_t* line_start,
-                 const int32_t* line_len, const DfaPool& P, uint8_t* out) {
-  host_parallel(n, 4096, [&](int, int64_t a, int64_t b) {
-    for (int64_t i = a; i < b; ++i) {
-      const int64_t k = cand[i];
-      const int r = (int)(k >> 32);
-      const int64_t line = k & 0xFFFFFFFFll;
-      out[i] = dfa_run(P, r, text + line_start[line], line_len[line]) ? 1 : 0;
-    }
-  });
 }
 
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,

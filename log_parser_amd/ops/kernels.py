@@ -145,19 +145,6 @@ def prefilter(text, nbytes, pf_tuple, line_start, cap: int, grid: int = 2048) ->
         cap = c
 
 
-def verify(cand, text, line_start, line_len, dfa_tuple) -> torch.Tensor:
-    out = torch.empty(cand.numel(), dtype=torch.uint8, device=cand.device)
-    if cand.numel() == 0:
-        return out
-    if cand.is_cuda:
-        N.verify_dev(cand.data_ptr(), cand.numel(), text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(),
-                     dfa_tuple, out.data_ptr(), _s(cand))
-    else:
-        N.verify_host(cand.data_ptr(), cand.numel(), text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(),
-                      dfa_tuple, out.data_ptr())
-    return out
-
-
 def scan(text, line_start, line_len, regs: torch.Tensor, dfa_tuple, cap: int) -> torch.Tensor:
     nlines = line_start.numel()
     if regs.numel() == 0 or nlines == 0:
@@ -200,30 +187,6 @@ def scan_multi(text, nbytes: int, line_start, line_len, pass_tuple, cap: int, gr
         if c <= cap:
             return out[:c]
         cap = c
-
-
-def context_features(lines: torch.Tensor, L: int, text, line_start, line_len, dfa_tuple) -> torch.Tensor:
-    """uint8 feature bits per line (ERR 1, WARN 2, STACK 4, EXC 8) for the given line ids; 0 elsewhere."""
-    feat = torch.zeros(max(L, 1), dtype=torch.uint8, device=text.device)
-    if lines.numel():
-        N.feat(lines.data_ptr(), lines.numel(), text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(),
-               dfa_tuple, feat.data_ptr(), _s(text), text.is_cuda)
-    return feat
-
-
-def score(ev_line, ev_pat, ev_seg, ev_freq, st_tuple, sp_tuple, with_factors: bool = False):
-    n = ev_line.numel()
-    out = torch.empty(n, dtype=torch.float64, device=ev_line.device)
-    fac = torch.empty((n, 7), dtype=torch.float64, device=ev_line.device) if with_factors else None
-    if n == 0:
-        return out, fac
-    if ev_line.is_cuda:
-        N.score_dev(ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_freq.data_ptr(), n, st_tuple,
-                    sp_tuple, out.data_ptr(), _p(fac), _s(ev_line))
-    else:
-        N.score_host(ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_freq.data_ptr(), n, st_tuple,
-                     sp_tuple, out.data_ptr(), _p(fac))
-    return out, fac
 
 
 def nfa_features(groups: torch.Tensor, lines: torch.Tensor, L: int, text, line_start, line_len,

@@ -116,8 +116,16 @@ def test_post_pipeline_host_twin_matches_reference(seed):
     # features: only covered lines are evaluated, the rest stay 0
     *_, feat2, _ = K.post_events(hits, nh, ev_cnt, ev_end, ne, L, evt, t, ls, ll, eng.tabs["dfa"],
                                  len(lib.freq_ids), None, features=True)
-    full = K.context_features(torch.arange(L, dtype=torch.int32), L, t, ls, ll, eng.tabs["dfa"])
-    assert torch.equal(feat2[:L], torch.where(torch.from_numpy(ref_cov), full[:L], torch.zeros_like(full[:L])))
+    from log_parser_amd import golden
+    raw = bytes(t[:n].tolist())
+    full = []
+    for a, b in zip(ls.tolist(), ll.tolist()):      # ContextAnalysisService.java:62-83 per line
+        line = raw[a:a + b].decode("utf-8", errors="replace")
+        f = 1 if golden._find(golden.ERROR_RE, line) else (2 if golden._find(golden.WARN_RE, line) else 0)
+        f |= (4 if golden._find(golden.STACK_RE, line) else 0) | (8 if golden._find(golden.EXC_RE, line) else 0)
+        full.append(f)
+    full = torch.tensor(full, dtype=torch.uint8)
+    assert torch.equal(feat2[:L], torch.where(torch.from_numpy(ref_cov), full, torch.zeros_like(full)))
 
 
 def test_post_pipeline_empty_inputs():

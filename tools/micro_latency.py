@@ -84,11 +84,6 @@ def main():
                             features=False)
     covered = torch.nonzero(cov[:L] > 0).flatten().to(torch.int32)
     out["covered_lines"] = covered.numel()
-    out["k_feat_list_covered"] = timeit(lambda: K.context_features(covered, L, t, ls, ll, tabs["dfa"]))
-    allx = torch.arange(L, dtype=torch.int32, device=dev)
-    out["k_feat_list_all"] = timeit(lambda: K.context_features(allx, L, t, ls, ll, tabs["dfa"]))
-    vcand = cands[:pre]
-    out["k_verify_cands"] = timeit(lambda: K.verify(vcand, t, ls, ll, tabs["dfa"]))
     print(json.dumps(out), flush=True)
 
 

@@ -8,11 +8,15 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <memory>
+
 #include "io/docs.h"
 #include "io/json_in.h"
 #include "io/http_server.h"
 #include "io/json_emit.h"
 #include "kernels/lp_api.h"
+#include "kernels/lp_host.h"
 #include "regex/jregex.h"
 
 namespace py = pybind11;
@@ -130,6 +134,31 @@ static FreqRing ring_from(const py::tuple& t) {
   return R;
 }
 
+// Java-semantics backtracking matchers of a library's non-automaton regexes (host fallback)
+struct BtSet {
+  std::vector<std::unique_ptr<BtRegex>> rx;
+  std::vector<std::string> err;
+  std::atomic<int64_t> exhausted{0};
+  explicit BtSet(const std::vector<std::string>& pats) {
+    for (auto& p : pats) {
+      try {
+        rx.emplace_back(new BtRegex(p));
+        err.emplace_back();
+      } catch (const std::exception& e) {
+        rx.emplace_back(nullptr);
+        err.emplace_back(e.what());
+      }
+    }
+  }
+  bool find(int i, const uint8_t* s, int64_t n) {
+    if (i < 0 || i >= (int)rx.size() || !rx[i]) return false;
+    bool ex = false;
+    const bool m = rx[i]->find(s, n, int64_t(1) << 27, &ex);
+    if (ex) exhausted++;
+    return m;
+  }
+};
+
 static py::bytes vbytes(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
 
 static py::dict compile_regex(const std::string& pat, int max_states, int max_positions) {
@@ -141,6 +170,7 @@ static py::dict compile_regex(const std::string& pat, int max_states, int max_po
   for (auto& s : c.literals) lits.append(py::bytes(s));
   d["literals"] = lits;
   d["has_literals"] = c.has_literals;
+  d["bt_ok"] = c.bt_ok;
   if (c.kind == Kind::DFA) {
     d["nstates"] = c.dfa.nstates;
     d["nclasses"] = c.dfa.nclasses;
@@ -319,6 +349,63 @@ PYBIND11_MODULE(_lpnative, m) {
     }
     return multi_find(d, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size());
   });
+  py::class_<BtSet>(m, "BtSet")
+      .def(py::init<const std::vector<std::string>&>())
+      .def("ok", [](const BtSet& b, int i) { return i >= 0 && i < (int)b.rx.size() && b.rx[i] != nullptr; })
+      .def("error", [](const BtSet& b, int i) { return b.err.at(i); })
+      .def_property_readonly("exhausted", [](const BtSet& b) { return (int64_t)b.exhausted.load(); })
+      .def("find", [](BtSet& b, int i, const std::string& line) {
+        return b.find(i, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size());
+      })
+      // candidates (global regex << 32 | line) with each candidate line's [start, start + len)
+      // in `text` -> the ones whose regex finds a match there; local[g] = index of global regex g
+      // in this set (-1: not ours, dropped)
+      .def("verify", [](BtSet& b, uint64_t text, uint64_t keys, uint64_t starts, uint64_t lens, int64_t nkeys,
+                        uint64_t local, int64_t nglobal, uint64_t out) -> int64_t {
+        const uint8_t* t = P<const uint8_t>(text);
+        const int64_t* K = P<const int64_t>(keys);
+        const int64_t* S = P<const int64_t>(starts);
+        const int64_t* L = P<const int64_t>(lens);
+        const int32_t* loc = P<const int32_t>(local);
+        std::vector<uint8_t> ok(nkeys, 0);
+        {
+          py::gil_scoped_release nogil;
+          host_parallel(nkeys, 64, [&](int, int64_t a, int64_t e) {
+            for (int64_t i = a; i < e; ++i) {
+              const int64_t g = K[i] >> 32;
+              if (g < 0 || g >= nglobal || loc[g] < 0) continue;
+              ok[i] = b.find(loc[g], t + S[i], L[i]) ? 1 : 0;
+            }
+          });
+        }
+        int64_t c = 0;
+        int64_t* o = P<int64_t>(out);
+        for (int64_t i = 0; i < nkeys; ++i)
+          if (ok[i]) o[c++] = K[i];
+        return c;
+      })
+      // every line x every listed regex (fallback regexes without a usable literal)
+      .def("scan", [](BtSet& b, uint64_t text, uint64_t ls, uint64_t ll, int64_t nlines, std::vector<int> locals,
+                      std::vector<int64_t> globals) -> py::array_t<int64_t> {
+        const uint8_t* t = P<const uint8_t>(text);
+        const int64_t* L = P<const int64_t>(ls);
+        const int32_t* N_ = P<const int32_t>(ll);
+        std::vector<std::vector<int64_t>> part(std::max(1, host_threads()));
+        {
+          py::gil_scoped_release nogil;
+          host_parallel(nlines, 256, [&](int th, int64_t a, int64_t e) {
+            for (int64_t x = a; x < e; ++x)
+              for (size_t k = 0; k < locals.size(); ++k)
+                if (b.find(locals[k], t + L[x], N_[x])) part[th].push_back((globals[k] << 32) | x);
+          });
+        }
+        size_t n = 0;
+        for (auto& v : part) n += v.size();
+        py::array_t<int64_t> r(n);
+        int64_t* o = r.mutable_data();
+        for (auto& v : part) for (int64_t k : v) *o++ = k;
+        return r;
+      });
   m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
   m.def("dfa_find", &dfa_find_py, py::arg("pattern"), py::arg("line"), py::arg("max_states") = 4096);
   m.def("split_docs", &split_docs);

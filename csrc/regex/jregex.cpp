@@ -2,6 +2,7 @@
 #include "jregex.h"
 
 #include <algorithm>
+#include <cctype>
 #include <cstring>
 #include <map>
 #include <set>
@@ -60,13 +61,20 @@ struct CodeSet {
 
 // ------------------------------------------------------------------------------------------
 // AST
-enum NT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_ASSERT };
+// N_GROUP .. N_MLANCHOR only exist in backtracking mode (Parser(..., bt = true)); the automaton
+// path rejects their constructs as Unsupported before building them.
+enum NT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_ASSERT, N_GROUP, N_BACKREF, N_LOOK, N_ATOMIC, N_MLANCHOR };
 struct Node {
   NT t = N_EMPTY;
   ByteSet set;
   std::vector<int> kids;
   int lo = 0, hi = 0;      // REP (hi = -1: unbounded)
   uint16_t cond = CTX_ALL; // ASSERT
+  int idx = 0;             // GROUP / BACKREF: group number; MLANCHOR: 0 '^', 1 '$'
+  bool behind = false;     // LOOK: lookbehind
+  bool neg = false;        // LOOK: negative
+  bool ci = false;         // BACKREF: case-insensitive compare
+  bool lazy = false;       // REP: reluctant (priority order matters inside atomic groups)
 };
 
 bool is_word_byte(int c) {
@@ -90,8 +98,11 @@ struct Flags { bool ci = false, dotall = false, comments = false, multiline = fa
 
 class Parser {
  public:
-  explicit Parser(const std::string& s) : s_(s) {}
+  // bt: backtracking mode -- capturing groups, backreferences, lookaround, atomic groups,
+  // possessive quantifiers and MULTILINE anchors become nodes instead of Unsupported
+  explicit Parser(const std::string& s, bool bt = false) : s_(s), bt_(bt) {}
   std::vector<Node> nodes;
+  int ngroups = 0;
   int parse() {
     int r = parse_alt();
     if (i_ < s_.size()) {
@@ -104,8 +115,10 @@ class Parser {
 
  private:
   const std::string& s_;
+  bool bt_ = false;
   size_t i_ = 0;
   Flags f_;
+  std::map<std::string, int> names_;
 
   int add(Node n) { nodes.push_back(std::move(n)); return (int)nodes.size() - 1; }
   int mk_set(const ByteSet& b) { Node n; n.t = N_SET; n.set = b; return add(n); }
@@ -174,7 +187,8 @@ class Parser {
       b.set_range(0xC0, 0xFF);
       ByteSet cont; cont.set_range(0x80, 0xBF);
       int lead = mk_set(b);
-      int tail = mk_rep(mk_set(cont), 0, -1);
+      // at most 3 continuation bytes in valid UTF-8; the bound keeps lookbehind lengths finite
+      int tail = mk_rep(mk_set(cont), 0, bt_ ? 3 : -1);
       return mk_cat({lead, tail});
     }
     std::vector<int> alts;
@@ -408,9 +422,16 @@ class Parser {
           ++i_;
           if (hi != -1 && hi < lo) throw SyntaxError("Illegal repetition range");
         } else break;
-        if (peek() == '?') ++i_;                                   // lazy: same language
-        else if (peek() == '+') throw Unsupported("possessive quantifier");
+        bool lazy = false, possessive = false;
+        if (peek() == '?') { ++i_; lazy = true; }                  // lazy: same language
+        else if (peek() == '+') {
+          if (!bt_) throw Unsupported("possessive quantifier");
+          ++i_;
+          possessive = true;
+        }
         atom = mk_rep(atom, lo, hi);
+        nodes[atom].lazy = lazy;
+        if (possessive) { Node n; n.t = N_ATOMIC; n.kids = {atom}; atom = add(n); }
         break;  // Java does not allow stacked quantifiers (a** is an error); keep one
       }
       int q2 = peek();
@@ -449,15 +470,31 @@ class Parser {
     if (c == '(') {
       ++i_;
       Flags saved = f_;
+      int group = 0;            // capturing group number (backtracking mode)
+      int wrap = -1;            // 0 lookahead, 1 lookbehind, 2 atomic
+      bool neg = false;
       if (peek() == '?') {
         ++i_;
         int d = peek();
-        if (d == '=' || d == '!' || d == '>') throw Unsupported("lookahead/atomic group");
-        if (d == '<') {
-          if (i_ + 1 < s_.size() && (s_[i_ + 1] == '=' || s_[i_ + 1] == '!')) throw Unsupported("lookbehind");
+        if (d == '=' || d == '!' || d == '>') {
+          if (!bt_) throw Unsupported("lookahead/atomic group");
+          ++i_;
+          wrap = d == '>' ? 2 : 0;
+          neg = d == '!';
+        } else if (d == '<' && i_ + 1 < s_.size() && (s_[i_ + 1] == '=' || s_[i_ + 1] == '!')) {
+          if (!bt_) throw Unsupported("lookbehind");
+          neg = s_[i_ + 1] == '!';
+          i_ += 2;
+          wrap = 1;
+        } else if (d == '<') {
           // named group
           size_t e = s_.find('>', i_);
           if (e == std::string::npos) throw SyntaxError("named capturing group is missing trailing '>'");
+          const std::string name = s_.substr(i_ + 1, e - i_ - 1);
+          if (name.empty() || !std::isalpha((unsigned char)name[0])) throw SyntaxError("capturing group name does not start with a Latin letter");
+          if (names_.count(name)) throw SyntaxError("Named capturing group <" + name + "> is already defined");
+          group = ++ngroups;
+          names_[name] = group;
           i_ = e + 1;
         } else {
           bool grp = false;
@@ -471,11 +508,28 @@ class Parser {
           ++i_;        // ':'
           f_ = nf;
         }
+      } else {
+        group = ++ngroups;      // plain '(' : capturing
       }
       int r = parse_alt();
       if (peek() != ')') throw SyntaxError("Unclosed group");
       ++i_;
       f_ = saved;
+      if (bt_ && wrap >= 0) {
+        Node n;
+        n.t = wrap == 2 ? N_ATOMIC : N_LOOK;
+        n.behind = wrap == 1;
+        n.neg = neg;
+        n.kids = {r};
+        return add(n);
+      }
+      if (bt_ && group > 0) {
+        Node n;
+        n.t = N_GROUP;
+        n.idx = group;
+        n.kids = {r};
+        return add(n);
+      }
       return r;
     }
     if (c == '[') { CodeSet cs = parse_class(); return set_node(cs); }
@@ -494,12 +548,18 @@ class Parser {
     }
     if (c == '^') {
       ++i_;
-      if (f_.multiline) throw Unsupported("MULTILINE ^");
+      if (f_.multiline) {
+        if (!bt_) throw Unsupported("MULTILINE ^");
+        Node n; n.t = N_MLANCHOR; n.idx = 0; n.neg = f_.unixl; return add(n);
+      }
       return mk_assert(mask_where(f_bos));
     }
     if (c == '$') {
       ++i_;
-      if (f_.multiline) throw Unsupported("MULTILINE $");
+      if (f_.multiline) {
+        if (!bt_) throw Unsupported("MULTILINE $");
+        Node n; n.t = N_MLANCHOR; n.idx = 1; n.neg = f_.unixl; return add(n);
+      }
       return mk_assert(f_.unixl ? mask_where(f_eos) : mask_where(f_eol));
     }
     if (c == '*' || c == '+' || c == '?') throw SyntaxError("Dangling meta character");
@@ -533,10 +593,33 @@ class Parser {
         }
         case 'X': throw Unsupported("\\X grapheme cluster");
         case 'N': throw Unsupported("\\N{name}");
-        case 'k': throw Unsupported("named backreference");
+        case 'k': {
+          if (!bt_) throw Unsupported("named backreference");
+          ++i_;
+          if (peek() != '<') throw SyntaxError("\\k is not followed by '<' for named capturing group");
+          size_t en = s_.find('>', i_);
+          if (en == std::string::npos) throw SyntaxError("named capturing group is missing trailing '>'");
+          const std::string name = s_.substr(i_ + 1, en - i_ - 1);
+          auto it = names_.find(name);
+          if (it == names_.end()) throw SyntaxError("named capturing group <" + name + "> does not exist");
+          i_ = en + 1;
+          Node n; n.t = N_BACKREF; n.idx = it->second; n.ci = f_.ci; return add(n);
+        }
         default: break;
       }
-      if (e >= '1' && e <= '9') throw Unsupported("backreference");
+      if (e >= '1' && e <= '9') {
+        if (!bt_) throw Unsupported("backreference");
+        // Java Pattern.ref: the first digit always, further digits while the group exists
+        int ref = e - '0';
+        ++i_;
+        while (!eof() && peek() >= '0' && peek() <= '9') {
+          const int nr = ref * 10 + (peek() - '0');
+          if (nr > ngroups) break;
+          ref = nr;
+          ++i_;
+        }
+        Node n; n.t = N_BACKREF; n.idx = ref; n.ci = f_.ci; return add(n);
+      }
       CodeSet cs;
       if (class_escape(cs)) return set_node(cs);
       uint32_t cp;
@@ -592,7 +675,10 @@ Lit lits(const std::vector<Node>& N, int id) {
   const Node& n = N[id];
   Lit r;
   switch (n.t) {
-    case N_EMPTY: case N_ASSERT: r.exact_ok = true; r.exact = {""}; return r;
+    case N_EMPTY: case N_ASSERT: case N_LOOK: case N_MLANCHOR:   // zero-width: no characters
+      r.exact_ok = true; r.exact = {""}; return r;
+    case N_GROUP: case N_ATOMIC: return lits(N, n.kids[0]);        // same strings (atomic: a subset)
+    case N_BACKREF: return r;                                        // unknown text: breaks runs
     case N_SET: {
       std::set<int> ch;
       for (int b = 0; b < 256; ++b) if (n.set.test(b)) ch.insert(lower(b));
@@ -924,6 +1010,42 @@ bool dfa_find(const Dfa& d, const uint8_t* s, int64_t n) {
   return d.accflags[st] & 1;
 }
 
+namespace {
+// required-literal factors of a parsed pattern -> out.literals (ASCII-lowercased OR-set)
+void set_literals(Compiled& out, const std::vector<Node>& nodes, int root) {
+  Lit L = lits(nodes, root);
+  std::set<std::string> best;
+  if (L.exact_ok && quality(L.exact) > -1000000) best = L.exact;
+  if (L.fac_ok && (best.empty() || quality(L.fac) > quality(best))) best = L.fac;
+  if (!best.empty()) {
+    size_t mn = 1000;
+    for (auto& x : best) mn = std::min(mn, x.size());
+    if (mn >= 2) { out.has_literals = true; out.literals.assign(best.begin(), best.end()); }
+  }
+}
+
+// a construct no automaton expresses: classify with the backtracking parser -- Java rejects the
+// pattern (INVALID), the native backtracker runs it (FALLBACK, bt_ok), or only the Python oracle
+// translation can (FALLBACK) -- and take its literals for the device prefilter
+void classify_fallback(Compiled& out, const std::string& pattern, const std::string& why) {
+  out.kind = Kind::FALLBACK;
+  out.error = why;
+  try {
+    Parser B(pattern, true);
+    const int r = B.parse();
+    set_literals(out, B.nodes, r);
+    BtRegex check(pattern);
+    out.bt_ok = true;
+  } catch (const SyntaxError& e) {
+    out.kind = Kind::INVALID;
+    out.error = e.what();
+    out.literals.clear();
+    out.has_literals = false;
+  } catch (const std::exception&) {
+  }
+}
+}  // namespace
+
 Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions) {
   Compiled out;
   std::vector<Node> nodes;
@@ -938,20 +1060,12 @@ Compiled compile(const std::string& pattern, int max_dfa_states, int max_positio
   } catch (const SyntaxError& e) {
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   } catch (const Unsupported& e) {
-    out.kind = Kind::FALLBACK; out.error = e.what(); return out;
+    classify_fallback(out, pattern, e.what());
+    return out;
   } catch (const std::exception& e) {
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   }
-  // literal factors
-  Lit L = lits(nodes, root);
-  std::set<std::string> best;
-  if (L.exact_ok && quality(L.exact) > -1000000) best = L.exact;
-  if (L.fac_ok && (best.empty() || quality(L.fac) > quality(best))) best = L.fac;
-  if (!best.empty()) {
-    size_t mn = 1000;
-    for (auto& x : best) mn = std::min(mn, x.size());
-    if (mn >= 2) { out.has_literals = true; out.literals.assign(best.begin(), best.end()); }
-  }
+  set_literals(out, nodes, root);
   try {
     Glushkov G(nodes, max_positions);
     Info top = G.build(root);
@@ -968,13 +1082,25 @@ Compiled compile(const std::string& pattern, int max_dfa_states, int max_positio
     for (auto& e : out.nfa.first) if (ft_sensitive(e.cond)) throw Unsupported("end anchor inside pattern");
     for (auto& v : out.nfa.follow) for (auto& e : v) if (ft_sensitive(e.cond)) throw Unsupported("end anchor inside pattern");
   } catch (const Unsupported& e) {
-    out.kind = Kind::FALLBACK; out.error = e.what(); return out;
+    out.kind = Kind::FALLBACK;
+    out.error = e.what();
+    try {
+      BtRegex check(pattern);
+      out.bt_ok = true;
+    } catch (const std::exception&) {
+    }
+    return out;
   }
   try {
     out.dfa = build_dfa(out.nfa, wordb, max_dfa_states);
     out.kind = Kind::DFA;
   } catch (const Unsupported& e) {
     out.kind = Kind::NFA; out.error = e.what();
+    try {
+      BtRegex check(pattern);
+      out.bt_ok = true;
+    } catch (const std::exception&) {
+    }
   }
   return out;
 }
@@ -1126,6 +1252,314 @@ uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n) {
     st = e & 0xFFFF;
   }
   return acc | d.fin[2 * st];
+}
+
+// ------------------------------------------------------------------------------------------
+// backtracking VM (Java semantics for non-regular constructs)
+namespace {
+
+enum BOp : uint8_t { B_SET, B_SPLIT, B_JMP, B_SAVE, B_ASSERT, B_BREF, B_LOOK, B_ATOMIC, B_MARK, B_PROGRESS, B_ML,
+                     B_MATCH };
+struct BInst {
+  BOp op;
+  int x = 0, y = 0;        // SET: set id; SPLIT: preferred / other pc; JMP/SAVE/MARK/PROGRESS/BREF/LOOK/ATOMIC: arg
+  uint16_t cond = 0;       // ASSERT
+  bool f1 = false, f2 = false;   // BREF: ci; LOOK: behind, neg; ML: kind ($), unix lines
+  int lo = 0, hi = 0;      // LOOK behind: byte-length bounds of the sub-pattern
+};
+
+constexpr int kMaxBtInsts = 1 << 18;
+
+}  // namespace
+
+struct BtRegex::Impl {
+  std::vector<std::vector<BInst>> progs;   // [0] = main; sub-programs of lookaround / atomic groups
+  std::vector<ByteSet> sets;
+  int ncaps = 0, nmarks = 0;
+  bool bos_only = false;                   // every match starts at BOS (leading \A / ^)
+};
+
+namespace {
+
+struct BtCompiler {
+  const std::vector<Node>& N;
+  BtRegex::Impl& I;
+  int total = 0;
+
+  int new_prog() { I.progs.emplace_back(); return (int)I.progs.size() - 1; }
+  int emit(int p, BInst in) {
+    if (++total > kMaxBtInsts) throw Unsupported("backtracking program too large");
+    I.progs[p].push_back(in);
+    return (int)I.progs[p].size() - 1;
+  }
+  static constexpr int64_t INF = int64_t(1) << 40;
+  void bounds(int id, int64_t& mn, int64_t& mx) const {
+    const Node& n = N[id];
+    switch (n.t) {
+      case N_EMPTY: case N_ASSERT: case N_LOOK: case N_MLANCHOR: mn = mx = 0; return;
+      case N_SET: mn = mx = 1; return;
+      case N_GROUP: case N_ATOMIC: bounds(n.kids[0], mn, mx); return;
+      case N_BACKREF: mn = 0; mx = INF; return;
+      case N_CAT: {
+        mn = mx = 0;
+        for (int k : n.kids) { int64_t a, b; bounds(k, a, b); mn += a; mx = (mx >= INF || b >= INF) ? INF : mx + b; }
+        return;
+      }
+      case N_ALT: {
+        mn = INF; mx = 0;
+        for (int k : n.kids) { int64_t a, b; bounds(k, a, b); mn = std::min(mn, a); mx = std::max(mx, b); }
+        return;
+      }
+      case N_REP: {
+        int64_t a, b; bounds(n.kids[0], a, b);
+        mn = a * n.lo;
+        mx = (n.hi < 0 || b >= INF) ? (b == 0 ? 0 : INF) : b * n.hi;
+        return;
+      }
+    }
+    mn = 0; mx = INF;
+  }
+  void comp(int p, int id) {
+    const Node& n = N[id];
+    switch (n.t) {
+      case N_EMPTY: return;
+      case N_SET: {
+        BInst in{B_SET}; in.x = (int)I.sets.size(); I.sets.push_back(n.set); emit(p, in); return;
+      }
+      case N_CAT: for (int k : n.kids) comp(p, k); return;
+      case N_ALT: {
+        std::vector<int> jumps;
+        for (size_t a = 0; a < n.kids.size(); ++a) {
+          if (a + 1 < n.kids.size()) {
+            const int sp = emit(p, BInst{B_SPLIT});
+            I.progs[p][sp].x = sp + 1;
+            comp(p, n.kids[a]);
+            jumps.push_back(emit(p, BInst{B_JMP}));
+            I.progs[p][sp].y = (int)I.progs[p].size();
+          } else {
+            comp(p, n.kids[a]);
+          }
+        }
+        for (int j : jumps) I.progs[p][j].x = (int)I.progs[p].size();
+        return;
+      }
+      case N_REP: {
+        for (int k = 0; k < n.lo; ++k) comp(p, n.kids[0]);
+        if (n.hi < 0) {                          // loop; an empty iteration may not repeat
+          const int m = I.nmarks++;
+          const int sp = emit(p, BInst{B_SPLIT});
+          BInst mk{B_MARK}; mk.x = m; emit(p, mk);
+          comp(p, n.kids[0]);
+          BInst pr{B_PROGRESS}; pr.x = m; emit(p, pr);
+          BInst j{B_JMP}; j.x = sp; emit(p, j);
+          const int out = (int)I.progs[p].size();
+          I.progs[p][sp].x = n.lazy ? out : sp + 1;
+          I.progs[p][sp].y = n.lazy ? sp + 1 : out;
+        } else {
+          std::vector<int> splits;
+          for (int k = n.lo; k < n.hi; ++k) {
+            splits.push_back(emit(p, BInst{B_SPLIT}));
+            comp(p, n.kids[0]);
+          }
+          const int out = (int)I.progs[p].size();
+          for (int sp : splits) {
+            I.progs[p][sp].x = n.lazy ? out : sp + 1;
+            I.progs[p][sp].y = n.lazy ? sp + 1 : out;
+          }
+        }
+        return;
+      }
+      case N_ASSERT: { BInst in{B_ASSERT}; in.cond = n.cond; emit(p, in); return; }
+      case N_GROUP: {
+        I.ncaps = std::max(I.ncaps, 2 * n.idx + 2);
+        BInst a{B_SAVE}; a.x = 2 * n.idx; emit(p, a);
+        comp(p, n.kids[0]);
+        BInst b{B_SAVE}; b.x = 2 * n.idx + 1; emit(p, b);
+        return;
+      }
+      case N_BACKREF: {
+        I.ncaps = std::max(I.ncaps, 2 * n.idx + 2);
+        BInst in{B_BREF}; in.x = n.idx; in.f1 = n.ci; emit(p, in); return;
+      }
+      case N_LOOK: case N_ATOMIC: {
+        const int sub = new_prog();
+        comp(sub, n.kids[0]);
+        emit(sub, BInst{B_MATCH});
+        BInst in{n.t == N_LOOK ? B_LOOK : B_ATOMIC};
+        in.x = sub;
+        if (n.t == N_LOOK) {
+          in.f1 = n.behind;
+          in.f2 = n.neg;
+          if (n.behind) {
+            int64_t mn, mx;
+            bounds(n.kids[0], mn, mx);
+            if (mx >= INF) throw SyntaxError("Look-behind group does not have an obvious maximum length");
+            in.lo = (int)mn;
+            in.hi = (int)mx;
+          }
+        }
+        emit(p, in);
+        return;
+      }
+      case N_MLANCHOR: { BInst in{B_ML}; in.f1 = n.idx == 1; in.f2 = n.neg; emit(p, in); return; }
+    }
+  }
+};
+
+struct BtRun {
+  const BtRegex::Impl& I;
+  const uint8_t* s;
+  int64_t n, ft;
+  int64_t steps = 0, budget;
+  bool exhausted = false;
+
+  uint16_t ctx_bit(int64_t i) const {
+    const int prev = i == 0 ? P_BOS : (is_word_byte(s[i - 1]) ? P_W : P_N);
+    int next;
+    if (i == n) next = N_EOS;
+    else if (i == ft) next = N_FT;
+    else if (is_word_byte(s[i])) next = N_W;
+    else if (s[i] >= 0x80 && s[i] <= 0xBF) next = N_C;
+    else next = N_N;
+    return (uint16_t)(1u << ctx_index(prev, next));
+  }
+  // line terminator (Java: \n \r U+0085 U+2028 U+2029) starting / ending at byte i
+  bool term_at(int64_t i) const {
+    if (i >= n) return false;
+    const uint8_t c = s[i];
+    if (c == '\n' || c == '\r') return true;
+    if (c == 0xC2 && i + 1 < n && s[i + 1] == 0x85) return true;
+    return c == 0xE2 && i + 2 < n && s[i + 1] == 0x80 && (s[i + 2] == 0xA8 || s[i + 2] == 0xA9);
+  }
+  bool term_before(int64_t i) const {
+    if (i <= 0) return false;
+    const uint8_t c = s[i - 1];
+    if (c == '\n' || c == '\r') return true;
+    if (c == 0x85 && i >= 2 && s[i - 2] == 0xC2) return true;
+    return (c == 0xA8 || c == 0xA9) && i >= 3 && s[i - 3] == 0xE2 && s[i - 2] == 0x80;
+  }
+  bool ml_anchor(const BInst& in, int64_t i) const {
+    if (!in.f1) {                                  // '^' (Pattern.Caret / UnixCaret)
+      if (i == n) return false;                    // Perl: not at end of input, even after a newline
+      if (i == 0) return true;
+      if (in.f2) return s[i - 1] == '\n';
+      if (!term_before(i)) return false;
+      return !(s[i - 1] == '\r' && s[i] == '\n');
+    }
+    if (i == n) return true;                       // '$' (Pattern.Dollar multiline / UnixDollar)
+    if (in.f2) return s[i] == '\n';
+    if (s[i] == '\n') return !(i > 0 && s[i - 1] == '\r');
+    return term_at(i);
+  }
+
+  struct Frame { int kind; int a; int64_t b; };   // 0: alternative (pc, pos); 1: cap undo; 2: mark undo
+
+  // run program p from pos; req_end >= 0: only a match ending exactly there counts
+  bool run(int p, int64_t pos, std::vector<int64_t>& caps, std::vector<int64_t>& marks, int64_t req_end,
+           int64_t* end_out) {
+    const std::vector<BInst>& code = I.progs[p];
+    std::vector<Frame> st;
+    int pc = 0;
+    for (;;) {
+      if (++steps > budget) { exhausted = true; return false; }
+      const BInst& in = code[pc];
+      bool ok = true;
+      switch (in.op) {
+        case B_SET:
+          if (pos < n && I.sets[in.x].test(s[pos])) { ++pos; ++pc; } else ok = false;
+          break;
+        case B_SPLIT: st.push_back({0, in.y, pos}); pc = in.x; break;
+        case B_JMP: pc = in.x; break;
+        case B_SAVE: st.push_back({1, in.x, caps[in.x]}); caps[in.x] = pos; ++pc; break;
+        case B_MARK: st.push_back({2, in.x, marks[in.x]}); marks[in.x] = pos; ++pc; break;
+        case B_PROGRESS: if (pos == marks[in.x]) ok = false; else ++pc; break;
+        case B_ASSERT: if (ctx_bit(pos) & in.cond) ++pc; else ok = false; break;
+        case B_ML: if (ml_anchor(in, pos)) ++pc; else ok = false; break;
+        case B_BREF: {
+          const int64_t a = caps[2 * in.x], b = caps[2 * in.x + 1];
+          if (a < 0 || b < 0) { ok = false; break; }
+          const int64_t len = b - a;
+          if (pos + len > n) { ok = false; break; }
+          for (int64_t k = 0; k < len && ok; ++k) {
+            int x = s[a + k], y = s[pos + k];
+            if (in.f1) { x = (x >= 'A' && x <= 'Z') ? x + 32 : x; y = (y >= 'A' && y <= 'Z') ? y + 32 : y; }
+            ok = x == y;
+          }
+          if (ok) { pos += len; ++pc; }
+          break;
+        }
+        case B_LOOK: case B_ATOMIC: {
+          std::vector<int64_t> c2 = caps, m2 = marks;
+          int64_t e = -1;
+          bool m = false;
+          if (in.op == B_LOOK && in.f1) {          // lookbehind: every start within the length bounds
+            for (int64_t j = pos - in.lo; j >= 0 && j >= pos - in.hi && !m; --j) {
+              c2 = caps;
+              m = run(in.x, j, c2, m2, pos, &e);
+              if (exhausted) return false;
+            }
+          } else {
+            m = run(in.x, pos, c2, m2, -1, &e);
+            if (exhausted) return false;
+          }
+          if (in.op == B_LOOK && in.f2) m = !m;
+          if (!m) { ok = false; break; }
+          if (!(in.op == B_LOOK && in.f2))         // keep the group's captures (undoable)
+            for (size_t k = 0; k < caps.size(); ++k)
+              if (c2[k] != caps[k]) { st.push_back({1, (int)k, caps[k]}); caps[k] = c2[k]; }
+          if (in.op == B_ATOMIC) pos = e;          // no backtracking into the atomic group
+          ++pc;
+          break;
+        }
+        case B_MATCH:
+          if (req_end < 0 || pos == req_end) { if (end_out) *end_out = pos; return true; }
+          ok = false;
+          break;
+      }
+      if (ok) continue;
+      for (;;) {                                   // backtrack
+        if (st.empty()) return false;
+        const Frame f = st.back();
+        st.pop_back();
+        if (f.kind == 1) caps[f.a] = f.b;
+        else if (f.kind == 2) marks[f.a] = f.b;
+        else { pc = f.a; pos = f.b; break; }
+      }
+    }
+  }
+};
+
+}  // namespace
+
+BtRegex::BtRegex(const std::string& pattern) {
+  Parser P(pattern, true);
+  const int root = P.parse();
+  auto impl = std::make_shared<Impl>();
+  impl->ncaps = 2 * P.ngroups + 2;
+  BtCompiler C{P.nodes, *impl};
+  C.new_prog();
+  C.comp(0, root);
+  C.emit(0, BInst{B_MATCH});
+  const std::vector<BInst>& code = impl->progs[0];
+  impl->bos_only = !code.empty() && code[0].op == B_ASSERT && code[0].cond == mask_where(f_bos);
+  p_ = impl;
+}
+
+bool BtRegex::find(const uint8_t* s, int64_t n, int64_t budget, bool* exhausted) const {
+  const Impl& I = *p_;
+  BtRun R{I, s, n, -1, 0, budget};
+  const int ftl = final_terminator_len(s, n);
+  R.ft = ftl ? n - ftl : -1;
+  std::vector<int64_t> caps(I.ncaps, -1), marks(std::max(I.nmarks, 1), -1);
+  for (int64_t start = 0; start <= n; ++start) {
+    if (start > 0 && start < n && s[start] >= 0x80 && s[start] <= 0xBF) continue;   // inside a code point
+    std::fill(caps.begin(), caps.end(), -1);
+    if (R.run(0, start, caps, marks, -1, nullptr)) return true;
+    if (R.exhausted) break;
+    if (I.bos_only) break;
+  }
+  if (exhausted) *exhausted = R.exhausted;
+  return false;
 }
 
 }  // namespace lp

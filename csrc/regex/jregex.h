@@ -15,6 +15,7 @@
 // (backrefs, lookaround, possessive, atomic groups) raise Unsupported -> host fallback.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -73,6 +74,7 @@ struct Compiled {
   std::string error;                        // reason for FALLBACK / INVALID
   std::vector<std::string> literals;        // OR-set of required factors (ASCII-lowercased bytes)
   bool has_literals = false;
+  bool bt_ok = false;                       // the native backtracker (BtRegex) runs it
   Nfa nfa;
   Dfa dfa;
 };
@@ -103,5 +105,21 @@ uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n);
 bool dfa_find(const Dfa& d, const uint8_t* s, int64_t n);
 // Length in bytes of a final line terminator (\r, U+0085, U+2028, U+2029) ending s[0..n), or 0.
 int final_terminator_len(const uint8_t* s, int64_t n);
+
+// Java-semantics backtracking matcher (boolean Matcher.find()) for the regexes no automaton can
+// express: backreferences, lookahead / lookbehind, atomic groups, possessive quantifiers,
+// MULTILINE anchors. The same parser builds the AST (byte-level UTF-8 lowering, ASCII \b \w,
+// CI flag), which is compiled to a small backtracking program run in Java's priority order
+// (greedy/reluctant, left alternative first) -- so atomic / possessive constructs keep exactly
+// the matches Java keeps. Host-only; the device prefilter narrows it to candidate lines.
+class BtRegex {
+ public:
+  explicit BtRegex(const std::string& pattern);    // throws SyntaxError / Unsupported
+  // steps: optional out-count of VM steps; a find exceeding `budget` steps returns false
+  bool find(const uint8_t* s, int64_t n, int64_t budget = int64_t(1) << 27, bool* exhausted = nullptr) const;
+  struct Impl;
+ private:
+  std::shared_ptr<const Impl> p_;
+};
 
 }  // namespace lp

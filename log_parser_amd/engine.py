@@ -318,15 +318,23 @@ class Engine:
             TR.mark(timings, name, self.device)
         return t0
 
-    def match_candidates(self, text, nbytes, ls, ll, host_lines=None, timings=None) -> Tuple[torch.Tensor, int]:
+    def match_candidates(self, text, nbytes, ls, ll, host_text=None, timings=None) -> Tuple[torch.Tensor, int]:
         """(regex << 32 | line) candidates: ``[:pre_from]`` prefilter candidates still to DFA-verify
         (verified inside the post-match pipeline), ``[pre_from:]`` hits of engines that verify
-        themselves (literal-free DFA scan, MFMA NFA, host fallback). Duplicates allowed."""
+        themselves (literal-free DFA scan, MFMA NFA, host backtracker). Duplicates allowed.
+        ``host_text``: the same bytes on the host (uint8 array), if the caller has them."""
         timings = {} if timings is None else timings
         t = self._start(timings)
         cand = K.prefilter(text, nbytes, self.tabs["pf"], ls, self.cand_cap, self.pf_grid)
         t = self._tick(timings, "prefilter", t)
         extra = []
+        fb = None
+        if self.lib.host_regs and cand.numel():
+            # candidates of host-fallback regexes are verified by the host backtracker, not a DFA
+            is_host = self.tabs["host_is"][(cand >> 32).long()]
+            if bool(is_host.any()):
+                fb = cand[is_host]
+                cand = cand[~is_host]
         for sp in self.tabs["scan_passes"]:        # literal-free regexes: multi-regex DFAs in LDS
             extra.append(K.scan_multi(text, nbytes, ls, ll, sp, max(1024, ls.numel() >> 6), self.scan_grid(sp)))
         if self.tabs["scan_regs"].numel():        # one whose DFA alone exceeds a scan group
@@ -335,11 +343,80 @@ class Engine:
             if glist.numel():
                 extra.append(K.nfa_scan(self.tabs["nfa_tables"], glist, ncls, text, ls, ll, max(1024, ls.numel())))
         if self.lib.host_regs:
-            extra.append(self._host_fallback(text, nbytes, ls, ll, host_lines))
+            extra.append(self._host_fallback(text, nbytes, ls, ll, host_text, fb))
         if extra:
             t = self._tick(timings, "scan", t)
             return torch.cat([cand] + extra), cand.numel()
         return cand, cand.numel()
+
+    def _host_fallback(self, text, nbytes, ls, ll, host_text, fb_cand) -> torch.Tensor:
+        """Host backtracker (jregex BtRegex, Java semantics) for the regexes no automaton
+        expresses (backreferences, lookaround, atomic groups, possessive quantifiers): regexes with
+        required literals are checked on their prefilter candidate lines only (the device gathers
+        each candidate's line start / length; one small D2H); literal-free ones on every line.
+        Text bytes come from ``host_text`` (serving: the pinned staging buffer) or one D2H. The
+        few constructs the backtracker lacks (e.g. unicode properties) use the Python oracle."""
+        lib = self.lib
+        dev = text.device
+        hb = host_text
+        if hb is None:
+            hb = text[:nbytes].cpu().numpy()
+        hb = np.ascontiguousarray(hb)
+        if hb.size == 0:
+            hb = np.zeros(1, np.uint8)
+        keys: List[np.ndarray] = []
+        bt = lib.host_bt
+        py_regs = [r for r in lib.host_regs if lib.host_local[r] < 0]
+        lines_h = None                                # (starts, lens) of all lines, on demand
+        if fb_cand is not None and fb_cand.numel():
+            x = (fb_cand & 0xFFFFFFFF).long()
+            pack = torch.stack([fb_cand, ls[x], ll[x].to(torch.int64)]).cpu().numpy()
+            _, first = np.unique(pack[0], return_index=True)    # one check per (regex, line)
+            kc, st, ln = (np.ascontiguousarray(pack[i][first]) for i in range(3))
+            out = np.empty(kc.size, np.int64)
+            nv = bt.verify(hb.ctypes.data, kc.ctypes.data, st.ctypes.data, ln.ctypes.data, kc.size,
+                           lib.host_local.ctypes.data, lib.host_local.size, out.ctypes.data)
+            keys.append(out[:nv])
+            if py_regs:
+                keys.append(self._python_fallback(hb, kc, st, ln, set(py_regs)))
+        scan = [r for r in lib.host_scan_regs if lib.host_local[r] >= 0]
+        if scan or any(not lib.regexes[r].literals for r in py_regs):
+            ls_h = np.ascontiguousarray(ls.cpu().numpy())
+            ll_h = np.ascontiguousarray(ll.cpu().numpy())
+            lines_h = (ls_h, ll_h)
+        if scan:
+            keys.append(bt.scan(hb.ctypes.data, ls_h.ctypes.data, ll_h.ctypes.data, ls_h.size,
+                                [int(lib.host_local[r]) for r in scan], scan))
+        py_scan = [r for r in py_regs if not lib.regexes[r].literals]
+        if py_scan:
+            L = lines_h[0].size
+            kc = np.array([(r << 32) | i for r in py_scan for i in range(L)], np.int64)
+            st = np.tile(lines_h[0], len(py_scan)).astype(np.int64)
+            ln = np.tile(lines_h[1], len(py_scan)).astype(np.int64)
+            keys.append(self._python_fallback(hb, kc, st, ln, set(py_scan)))
+        if bt is not None and bt.exhausted:
+            log.warning("host backtracker: %d line matches exceeded the step budget (treated as no match)",
+                        bt.exhausted)
+        allk = np.concatenate(keys) if keys else np.zeros(0, np.int64)
+        return torch.from_numpy(allk).to(dev)
+
+    def _python_fallback(self, hb: np.ndarray, kc, st, ln, regs: set) -> np.ndarray:
+        out = []
+        cache = {}
+        for k, a, n in zip(kc.tolist(), st.tolist(), ln.tolist()):
+            r = k >> 32
+            if r not in regs:
+                continue
+            rx = cache.get(r)
+            if rx is None:
+                try:
+                    rx = cache[r] = compile_java(self.lib.regexes[r].pattern)
+                except Exception:  # noqa: BLE001 - an untranslatable fallback regex never matches
+                    log.error("host fallback cannot compile %r", self.lib.regexes[r].pattern)
+                    rx = cache[r] = False
+            if rx and rx.search(bytes(hb[a:a + n]).decode("utf-8", errors="surrogateescape")) is not None:
+                out.append(k)
+        return np.array(out, np.int64)
 
     def scan_grid(self, sp: tuple) -> int:
         """Persistent grid of k_scan_multi: as many blocks per CU as the pass's LDS blob allows."""
@@ -351,33 +428,15 @@ class Engine:
     def _ev_tables(self, segs: "Segments") -> tuple:
         return K.ev_tables(self.tabs, segs, len(self.lib.freq_ids), len(self.lib.patterns))
 
-    def match_hits(self, text, nbytes, ls, ll, host_lines=None, timings=None) -> torch.Tensor:
+    def match_hits(self, text, nbytes, ls, ll, host_text=None, timings=None) -> torch.Tensor:
         """Sorted unique verified (regex << 32 | line) hit keys of every library regex."""
-        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_lines, timings)
+        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
         segs = Segments.single(ls.numel(), text.device)
         return K.post_hits(cand, pre, ls.numel(), self.lib.n_regexes, text, ls, ll, self.tabs["dfa"],
                            self._ev_tables(segs), self.ws)[0]
 
-    def _host_fallback(self, text, nbytes, ls, ll, host_lines) -> torch.Tensor:
-        if host_lines is None:
-            hb = text[:nbytes].cpu().numpy().tobytes()
-            s = ls.cpu().numpy()
-            n = ll.cpu().numpy()
-            host_lines = [hb[a:a + b].decode("utf-8", errors="surrogateescape") for a, b in zip(s, n)]
-        keys = []
-        for r in self.lib.host_regs:
-            try:
-                rx = compile_java(self.lib.regexes[r].pattern)
-            except Exception:  # noqa: BLE001 - an untranslatable fallback regex never matches
-                log.error("host fallback cannot compile %r", self.lib.regexes[r].pattern)
-                continue
-            for i, line in enumerate(host_lines):
-                if rx.search(line) is not None:
-                    keys.append((r << 32) | i)
-        return torch.tensor(keys, dtype=torch.int64, device=text.device)
-
     # ------------------------------------------------------------------ core run
-    def prepare(self, text, nbytes, ls, ll, segs: Segments, host_lines=None,
+    def prepare(self, text, nbytes, ls, ll, segs: Segments, host_text=None,
                 timings: Optional[dict] = None) -> "Prepared":
         """Local phase: matching, hit CSR, events, in-batch frequency ranks, context features.
 
@@ -387,7 +446,7 @@ class Engine:
         """
         timings = {} if timings is None else timings
         L = ls.numel()
-        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_lines, timings)
+        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
         t = 0.0
         evt = self._ev_tables(segs)
         hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(
@@ -444,9 +503,9 @@ class Engine:
                          prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings)
 
     def run(self, text, nbytes, ls, ll, segs: Segments, freq_carry: torch.Tensor,
-            seq_carry: Optional[torch.Tensor] = None, host_lines=None, with_factors=False,
+            seq_carry: Optional[torch.Tensor] = None, host_text=None, with_factors=False,
             timings: Optional[dict] = None) -> RunResult:
-        prep = self.prepare(text, nbytes, ls, ll, segs, host_lines, timings)
+        prep = self.prepare(text, nbytes, ls, ll, segs, host_text, timings)
         return self.finish(prep, segs, freq_carry, seq_carry, with_factors)
 
     # ------------------------------------------------------------------ request API
@@ -511,7 +570,8 @@ class Engine:
         text, n = self.stage_text(data)
         ls, ll = K.split_lines(text, n)
         segs = Segments.single(ls.numel(), self.device)
-        res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=with_factors)
+        res = self.run(text, n, ls, ll, segs, self.freq_carry(), host_text=np.frombuffer(data, np.uint8) if n else None,
+                       with_factors=with_factors)
         self.commit_frequency(res.freq_counts)
         return res, ls, ll
 
@@ -594,7 +654,8 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            res = self.run(text, n, ls, ll, segs, self.freq_carry(), with_factors=verbose, timings=tm)
+            res = self.run(text, n, ls, ll, segs, self.freq_carry(), host_text=hb[:n], with_factors=verbose,
+                           timings=tm)
             self.commit_frequency(res.freq_counts)
             with TR.HostTimer(tm, "d2h"):
                 job.ev = self._results_to_host(res)
@@ -607,7 +668,7 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            res = self.run(text, n, ls, ll, segs, carry, with_factors=verbose, timings=tm)
+            res = self.run(text, n, ls, ll, segs, carry, host_text=hb[:n], with_factors=verbose, timings=tm)
             with TR.HostTimer(tm, "d2h"):
                 job.ev = self._results_to_host(res)
             self.commit_frequency(job.ev[4])
@@ -619,7 +680,7 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            prep = self.prepare(text, n, ls, ll, segs, timings=tm)
+            prep = self.prepare(text, n, ls, ll, segs, host_text=hb[:n], timings=tm)
             turn.wait(seq)                     # earlier batches have recorded their counts
             res = self.finish(prep, segs, self.freq_carry(), with_factors=verbose)
             with TR.HostTimer(tm, "d2h"):

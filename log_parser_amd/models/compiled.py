@@ -280,6 +280,7 @@ class CompiledLibrary:
         toff = aoff = 0
         self.scan_regs: List[int] = []
         self.host_regs: List[int] = []
+        self.host_bt_ok: List[bool] = []
         nfa_members: List[Tuple[int, dict]] = []
         ctx_members: List[Tuple[int, dict]] = []
         for i, ri in enumerate(self.regexes):
@@ -323,8 +324,15 @@ class CompiledLibrary:
                     # DFA blow-up: simulate the NFA with the MFMA state-transition kernel
                     nfa_members.append((i, d))
                 else:
-                    log.warning("regex %r uses the host fallback (%s)", ri.pattern, ri.error)
+                    # non-regular (backref, lookaround, atomic, possessive) or too large for the
+                    # automata: the native backtracker on the host, narrowed to prefilter
+                    # candidate lines through the regex's required literals when it has some
+                    log.info("regex %r runs on the host backtracker (%s)", ri.pattern, ri.error)
                     self.host_regs.append(i)
+                    self.host_bt_ok.append(bool(d.get("bt_ok")))
+                    lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
+                    if lits and min(len(x) for x in lits) >= MIN_LITERAL and ri.roles != {"context"}:
+                        ri.literals = lits
         # a dummy DFA for non-DFA regexes: state 2 -> DEAD on every byte (never read: not scanned)
         if not trans:
             trans.append(np.zeros(1, np.uint16))
@@ -337,10 +345,26 @@ class CompiledLibrary:
         self.nfa_scan_groups = list(range(1, len(groups)))
         self.nfa_regs = [rid for g in groups[1:] for rid, _ in g]
         self._build_scan_passes()
+        self._build_host_matchers()
         self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
         self.dfa_bytemap = np.concatenate(bytemaps)
         self.dfa_trans = np.concatenate(trans)
         self.dfa_acc = np.concatenate(accs)
+
+    def _build_host_matchers(self):
+        """Host-fallback regexes: native Java-semantics backtrackers (jregex BtRegex) for all it
+        supports; the rest (e.g. unicode properties) keep the Python oracle translation."""
+        self.host_bt = N.BtSet([self.regexes[r].pattern for r in self.host_regs]) if self.host_regs else None
+        R = len(self.regexes)
+        self.host_local = np.full(max(R, 1), -1, np.int32)      # global regex id -> index in host_bt
+        for k, r in enumerate(self.host_regs):
+            if self.host_bt is not None and self.host_bt.ok(k):
+                self.host_local[r] = k
+        self.host_is = np.zeros(max(R, 1), bool)
+        self.host_is[self.host_regs] = True
+        # split: candidates from the prefilter (literal) vs every line (no literal)
+        self.host_lit_regs = [r for r in self.host_regs if self.regexes[r].literals]
+        self.host_scan_regs = [r for r in self.host_regs if not self.regexes[r].literals]
 
     # multi-regex DFA scan groups (csrc/kernels/scan_multi.hip)
     SCAN_GROUP_REGS = 16            # members per multi-regex DFA (16-bit accept masks)
@@ -570,6 +594,7 @@ class CompiledLibrary:
         d = t["dfa_arrays"]
         t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr())
         t["scan_regs"] = T(np.array(self.scan_regs_single, np.int32))
+        t["host_is"] = T(self.host_is)
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
         t["scan_passes"] = [(b.data_ptr(), p["lds_words"], p["ngroups"], p["row_base"], p["stride"], p["thr"],
                              p["init_row"], p["init_state"], p["ncol"], p["gt_off"], p["fin_off"], p["bm_off"],
@@ -611,6 +636,7 @@ class CompiledLibrary:
         return {
             "patterns": len(self.patterns), "pattern_sets": len(self.pattern_sets), "regexes": len(self.regexes),
             "dfa": kinds.count(KIND_DFA), "host_fallback": len(self.host_regs),
+            "host_backtracker": int((self.host_local >= 0).sum()) if self.host_regs else 0,
             "invalid": kinds.count(KIND_INVALID), "scan_all": len(self.scan_regs), "literals": len(self.literals),
             "teddy_literals": int(self.pf["teddy_lits"]), "prefilter_stride": int(self.pf["stride"]),
             "scan_groups": len(self.scan_groups), "scan_passes": len(self.scan_passes),

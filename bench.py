@@ -234,8 +234,8 @@ def run(args, sets, trig, rank, world, local_rank, server):
         ls, ll = K.split_lines(text, nbytes)
         out = sa.step(text, nbytes, ls, ll, hl, hr, topk=args.topk)
         events_to_host(out, b)                                   # results land on the host
-        if rank == 0 and out.topk_score is not None:
-            out.topk_score.cpu()
+        if rank == 0 and out.topk_rows is not None:
+            state["top"] = out.topk_rows.cpu()                   # merged global top-k on the host
         if use_cuda:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()

@@ -469,6 +469,26 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("freq_evict", [](py::tuple ring, double horizon, uint64_t s, bool dev) {
     freq_evict(ring_from(ring), horizon, s, dev);
   });
+  // ---- summary + top-k (summarize.hip). in = (score, pat, line32, line64, line_add, sev_of_pat, rows)
+  m.def("summarize", [](py::tuple in, int64_t n, int k, uint64_t top, uint64_t pat_hist, uint64_t sev_hist,
+                        uint64_t ws, uint64_t ws_bytes, uint64_t s, bool dev) -> uint64_t {
+    const SummIn I{P<const double>(in[0].cast<uint64_t>()), P<const int32_t>(in[1].cast<uint64_t>()),
+                   P<const int32_t>(in[2].cast<uint64_t>()), P<const int64_t>(in[3].cast<uint64_t>()),
+                   P<const int64_t>(in[4].cast<uint64_t>()), P<const int32_t>(in[5].cast<uint64_t>()),
+                   P<const double>(in[6].cast<uint64_t>())};
+    if (dev)
+      return summarize_dev(I, n, k, P<double>(top), P<unsigned long long>(pat_hist), P<unsigned long long>(sev_hist),
+                           P<void>(ws), ws_bytes, s);
+    summarize_host(I, n, k, P<double>(top), P<int64_t>(pat_hist), P<int64_t>(sev_hist));
+    return 0;
+  });
+  m.def("rescore", [](uint64_t gl, uint64_t fac, int64_t n, int64_t Nn, py::tuple sp, uint64_t out, uint64_t s,
+                      bool dev) {
+    if (dev)
+      rescore_dev(P<const int64_t>(gl), P<const double>(fac), n, Nn, sp_from(sp), P<double>(out), s);
+    else
+      rescore_host(P<const int64_t>(gl), P<const double>(fac), n, Nn, sp_from(sp), P<double>(out));
+  });
   m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev) {
     freq_record(P<const int64_t>(counts), K, now, ring_from(ring), s, dev);
   });

@@ -91,6 +91,30 @@ void freq_evict(const FreqRing& R, double horizon, uint64_t stream, bool dev);
 void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev);
 }  // namespace lp
 
+// ---- summary + top-k, streaming re-score (summarize.hip)
+namespace lp {
+struct SummIn {
+  // events (level 0): score[i], pattern pat[i], global line = (line64 ? line64 : line32)[i] + *line_add
+  const double* score;
+  const int32_t* pat;
+  const int32_t* line32;
+  const int64_t* line64;
+  const int64_t* line_add;   // device (host twin: host) scalar, may be null
+  const int32_t* sev_of_pat; // [P] severity index 0..4
+  // or rows [n][3] = (score, line, pattern) as float64 (merging top-k lists)
+  const double* rows;
+};
+// writes the k best rows (score desc, line asc, pattern asc; missing rows = (-inf, -1, -1)) and,
+// from events, adds the pattern / severity histograms. Device: returns workspace bytes, runs only
+// when ws_bytes suffices.
+size_t summarize_dev(const SummIn& in, int64_t n, int k, double* top_rows, unsigned long long* pat_hist,
+                     unsigned long long* sev_hist, void* ws, size_t ws_bytes, uint64_t stream);
+void summarize_host(const SummIn& in, int64_t n, int k, double* top_rows, int64_t* pat_hist, int64_t* sev_hist);
+void rescore_dev(const int64_t* gl, const double* fac, int64_t n, int64_t N, const ScoreParams& S, double* out,
+                 uint64_t stream);
+void rescore_host(const int64_t* gl, const double* fac, int64_t n, int64_t N, const ScoreParams& S, double* out);
+}  // namespace lp
+
 // ---- post-match pipeline (lp_post.hip): hit CSR, events, frequency ranks, context features
 namespace lp {
 struct EvTables {

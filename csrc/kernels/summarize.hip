@@ -1,0 +1,174 @@
+// Summary + top-k of scored events (reference buildSummary,
+// AnalysisService.java:188-215 -- event count, severity histogram, highest severity -- plus the
+// north star's top-k event reduction), and the streaming mode's final re-score.
+//
+//   k_summ_level  one block per 2048-item chunk: the chunk is bitonic-sorted in LDS by
+//                 (score desc, global line asc, pattern asc) -- a total, deterministic order, so
+//                 every rank / run agrees on ties -- and its first k rows are written out. Level
+//                 0 reads events (and adds them to the pattern / severity histograms with one
+//                 global atomic each); later levels read the previous level's rows, so a few
+//                 launches reduce any event count to the global top k.
+//   k_rescore     streaming: the reference's left-to-right product with the chronological
+//                 factor of the true global N (ScoringService.java:102-151), one lane per event,
+//                 from the factors the score kernel kept (chrono_factor is the same LP_HD code).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lp_api.h"
+#include "lp_core.h"
+
+namespace lp {
+
+constexpr int SUMM_THREADS = 256;
+constexpr int SUMM_CHUNK = 2048;
+
+struct Row {
+  double score;
+  int64_t line;
+  int32_t pat;
+};
+
+LP_HD bool row_before(const Row& a, const Row& b) {      // a sorts before b
+  if (a.score != b.score) return a.score > b.score;
+  if (a.line != b.line) return a.line < b.line;
+  return a.pat < b.pat;
+}
+
+LP_HD Row empty_row() { return Row{-INFINITY, -1, -1}; }
+
+__global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t n, int k, double* __restrict__ rows_out,
+                                                             unsigned long long* __restrict__ pat_hist,
+                                                             unsigned long long* __restrict__ sev_hist) {
+  __shared__ double s_score[SUMM_CHUNK];
+  __shared__ int64_t s_line[SUMM_CHUNK];
+  __shared__ int32_t s_pat[SUMM_CHUNK];
+  const int64_t base = (int64_t)blockIdx.x * SUMM_CHUNK;
+  const int64_t add = in.line_add ? *in.line_add : 0;
+  for (int j = threadIdx.x; j < SUMM_CHUNK; j += SUMM_THREADS) {
+    const int64_t i = base + j;
+    Row r = empty_row();
+    if (i < n) {
+      if (in.rows) {
+        r = Row{in.rows[3 * i], (int64_t)in.rows[3 * i + 1], (int32_t)in.rows[3 * i + 2]};
+      } else {
+        r.score = in.score[i];
+        r.line = (in.line64 ? in.line64[i] : (int64_t)in.line32[i]) + add;
+        r.pat = in.pat[i];
+        if (pat_hist) atomicAdd(pat_hist + r.pat, 1ull);
+        if (sev_hist) atomicAdd(sev_hist + in.sev_of_pat[r.pat], 1ull);
+      }
+    }
+    s_score[j] = r.score;
+    s_line[j] = r.line;
+    s_pat[j] = r.pat;
+  }
+  __syncthreads();
+  // bitonic sort of the chunk, descending in row order
+  for (int size = 2; size <= SUMM_CHUNK; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < SUMM_CHUNK / 2; t += SUMM_THREADS) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;             // this half keeps row order
+        const Row a{s_score[lo], s_line[lo], s_pat[lo]}, b{s_score[hi], s_line[hi], s_pat[hi]};
+        if (row_before(b, a) == up) {
+          s_score[lo] = b.score; s_line[lo] = b.line; s_pat[lo] = b.pat;
+          s_score[hi] = a.score; s_line[hi] = a.line; s_pat[hi] = a.pat;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  double* o = rows_out + (int64_t)blockIdx.x * k * 3;
+  for (int j = threadIdx.x; j < k; j += SUMM_THREADS) {
+    o[3 * j] = s_score[j];
+    o[3 * j + 1] = (double)s_line[j];
+    o[3 * j + 2] = (double)s_pat[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rescore(const int64_t* __restrict__ gl, const double* __restrict__ fac,
+                                                 int64_t n, int64_t N, ScoreParams S, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double* f = fac + 7 * i;
+  out[i] = f[0] * f[1] * chrono_factor(gl[i], N, S) * f[3] * f[4] * f[5] * (1.0 - f[6]);
+}
+
+static void check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in " + what);
+}
+
+size_t summarize_dev(const SummIn& in, int64_t n, int k, double* top_rows, unsigned long long* pat_hist,
+                     unsigned long long* sev_hist, void* ws, size_t ws_bytes, uint64_t stream) {
+  if (k < 1 || k > SUMM_CHUNK / 2) throw std::runtime_error("summarize: 1 <= k <= 1024");
+  // workspace: two ping-pong row buffers sized for level 0
+  const int64_t nb0 = std::max<int64_t>(1, (n + SUMM_CHUNK - 1) / SUMM_CHUNK);
+  const size_t rows_bytes = (size_t)nb0 * k * 3 * sizeof(double);
+  const size_t need = 2 * rows_bytes;
+  if (!ws || ws_bytes < need) return need;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double* buf[2] = {static_cast<double*>(ws), reinterpret_cast<double*>(static_cast<uint8_t*>(ws) + rows_bytes)};
+  int64_t m = n, nb = nb0;
+  SummIn cur = in;
+  int which = 0;
+  for (int level = 0;; ++level) {
+    double* dst = nb == 1 ? top_rows : buf[which];
+    hipLaunchKernelGGL(k_summ_level, dim3((unsigned)nb), dim3(SUMM_THREADS), 0, st, cur, m, k, dst,
+                       level == 0 ? pat_hist : nullptr, level == 0 ? sev_hist : nullptr);
+    check("k_summ_level");
+    if (nb == 1) break;
+    SummIn nx{};
+    nx.rows = dst;
+    cur = nx;
+    m = nb * (int64_t)k;
+    nb = (m + SUMM_CHUNK - 1) / SUMM_CHUNK;
+    which ^= 1;
+  }
+  return need;
+}
+
+void summarize_host(const SummIn& in, int64_t n, int k, double* top_rows, int64_t* pat_hist, int64_t* sev_hist) {
+  const int64_t add = in.line_add ? *in.line_add : 0;
+  std::vector<Row> rows(n);
+  for (int64_t i = 0; i < n; ++i) {
+    if (in.rows) {
+      rows[i] = Row{in.rows[3 * i], (int64_t)in.rows[3 * i + 1], (int32_t)in.rows[3 * i + 2]};
+      continue;
+    }
+    rows[i] = Row{in.score[i], (in.line64 ? in.line64[i] : (int64_t)in.line32[i]) + add, in.pat[i]};
+    if (pat_hist) ++pat_hist[in.pat[i]];
+    if (sev_hist) ++sev_hist[in.sev_of_pat[in.pat[i]]];
+  }
+  const int64_t kk = std::min<int64_t>(k, n);
+  std::partial_sort(rows.begin(), rows.begin() + kk, rows.end(), row_before);
+  for (int j = 0; j < k; ++j) {
+    const Row r = j < kk ? rows[j] : empty_row();
+    top_rows[3 * j] = r.score;
+    top_rows[3 * j + 1] = (double)r.line;
+    top_rows[3 * j + 2] = (double)r.pat;
+  }
+}
+
+void rescore_dev(const int64_t* gl, const double* fac, int64_t n, int64_t N, const ScoreParams& S, double* out,
+                 uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_rescore, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     gl, fac, n, N, S, out);
+  check("k_rescore");
+}
+
+void rescore_host(const int64_t* gl, const double* fac, int64_t n, int64_t N, const ScoreParams& S, double* out) {
+  for (int64_t i = 0; i < n; ++i) {
+    const double* f = fac + 7 * i;
+    out[i] = f[0] * f[1] * chrono_factor(gl[i], N, S) * f[3] * f[4] * f[5] * (1.0 - f[6]);
+  }
+}
+
+}  // namespace lp

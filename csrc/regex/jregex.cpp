@@ -832,6 +832,8 @@ class Glushkov {
         }
         return r;
       }
+      default:   // groups / backreferences / lookaround / atomic: backtracker-only nodes
+        throw Unsupported("construct needs the backtracker");
     }
     return r;
   }

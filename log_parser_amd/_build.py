@@ -27,6 +27,7 @@ SOURCES = [
     ("kernels/nfa_mfma.hip", "hip"),
     ("kernels/scan_multi.hip", "hip"),
     ("kernels/freq_state.hip", "hip"),
+    ("kernels/summarize.hip", "hip"),
     ("kernels/lp_post.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),

@@ -132,6 +132,23 @@ class RunResult:
     timings: Dict[str, float] = field(default_factory=dict)
 
 
+def summary_from_severity(lib, sev_hist: np.ndarray, first_pat: Optional[int]) -> dict:
+    """AnalysisSummary (AnalysisService.java:188-215) from the summary kernel's histogram over the
+    library's distinct severity names: the highest known severity wins; with none known, the
+    severity of the first event in reference order (the reference's first strict improvement)."""
+    dist = {lib.sev_names[s]: int(sev_hist[s]) for s in np.nonzero(sev_hist)[0]}
+    n = sum(dist.values())
+    if n == 0:
+        return {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
+    best_idx, best = -1, None
+    for s in dist:
+        if s in SEVERITY_ORDER and SEVERITY_ORDER.index(s) > best_idx:
+            best_idx, best = SEVERITY_ORDER.index(s), s
+    if best is None and first_pat is not None:
+        best = lib.severity[first_pat]
+    return {"significantEvents": n, "highestSeverity": best, "severityDistribution": dist}
+
+
 def _ro_view(data) -> torch.Tensor:
     """uint8 tensor view of a bytes-like object without copying (never written through)."""
     with warnings.catch_warnings():
@@ -273,9 +290,7 @@ class Engine:
         self.tabs = library.device_tables(self.device)
         self.ws = K.Workspace(self.device)          # post-match pipeline scratch (grow-only)
         self.upload = K.Uploader(self.device)       # batch line index / segments / carry: one H2D
-        p = self.params
-        self.sp_tuple = (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
-                         p.max_context_factor, p.freq_threshold, p.freq_max_penalty, float(p.freq_window_hours))
+        self.sp_tuple = self.score_param_tuple(self.params)
         self._pinned: Optional[torch.Tensor] = None
         # batch staging buffers (pinned on GPU), recycled; one per batch in flight in the pipeline
         self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
@@ -541,6 +556,15 @@ class Engine:
         h = torch.cat(parts).cpu().numpy()
         return (h[:n], h[n:2 * n], h[2 * n:3 * n], h[3 * n:5 * n].view(np.float64),
                 h[5 * n:].view(np.int64))
+
+    @staticmethod
+    def score_param_tuple(p) -> tuple:
+        """ScoringParams -> the kernels' ScoreParams tuple (csrc/bind.cpp sp_from)."""
+        return (p.decay_constant, p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold,
+                p.max_context_factor, p.freq_threshold, p.freq_max_penalty, float(p.freq_window_hours))
+
+    def summary_from_severity(self, sev_hist: np.ndarray, first_pat: Optional[int]) -> dict:
+        return summary_from_severity(self.lib, sev_hist, first_pat)
 
     def summary(self, ev_pat_host: np.ndarray) -> dict:
         if ev_pat_host.size == 0:

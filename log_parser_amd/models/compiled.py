@@ -218,6 +218,11 @@ class CompiledLibrary:
         self.conf = np.zeros(P, np.float64)
         self.sev = np.zeros(P, np.float64)
         self.severity = []
+        # distinct severity strings (first appearance) and each pattern's index into them: the
+        # summary kernel's severity histogram keys (severityDistribution, AnalysisService.java:197)
+        self.sev_names: List[str] = []
+        self.sev_index = np.zeros(P, np.int32)
+        sev_of_name: Dict[str, int] = {}
         self.ctx_before = np.full(P, -1, np.int32)
         self.ctx_after = np.full(P, -1, np.int32)
         sec_off, sec_reg, sec_w, sec_weight = [0], [], [], []
@@ -232,6 +237,10 @@ class CompiledLibrary:
             sk = severity_key(pat.severity)
             self.severity.append(sk)
             self.sev[i] = SEVERITY_MULTIPLIERS.get(sk, 1.0)
+            if sk not in sev_of_name:
+                sev_of_name[sk] = len(self.sev_names)
+                self.sev_names.append(sk)
+            self.sev_index[i] = sev_of_name[sk]
             ce = pat.context_extraction
             if ce is not None:
                 self.ctx_before[i] = max(0, int(ce.lines_before))
@@ -600,6 +609,7 @@ class CompiledLibrary:
                              p["init_row"], p["init_state"], p["ncol"], p["gt_off"], p["fin_off"], p["bm_off"],
                              p["rid_off"]) for b, p in zip(t["scan_blobs"], self.scan_passes)]
         t["conf"], t["sev"] = T(self.conf), T(self.sev)
+        t["sev_index"] = T(self.sev_index)
         t["ctx_before"], t["ctx_after"] = T(self.ctx_before), T(self.ctx_after)
         t["sec_off"], t["sec_reg"], t["sec_w"], t["sec_weight"] = T(self.sec_off), T(self.sec_reg), T(self.sec_w), T(self.sec_weight)
         t["seq_off"], t["seq_bonus"], t["seq_ev_off"], t["seq_ev_reg"] = T(self.seq_off), T(self.seq_bonus), T(self.seq_ev_off), T(self.seq_ev_reg)

@@ -356,6 +356,69 @@ def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text
     return ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts, feat, cov
 
 
+SUMMARY_MAX_K = 1024
+
+
+def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int, sev_index: torch.Tensor,
+              npat: int, nsev: int, line_add: Optional[torch.Tensor] = None, ws: Optional[Workspace] = None):
+    """Top-k rows + histograms of scored events (csrc/kernels/summarize.hip).
+
+    ``line`` is int32 (local, plus the device scalar ``line_add``) or int64 (global);
+    ``sev_index[p]`` is pattern p's index into the library's distinct severity names. Returns
+    (rows float64[k, 3] = (score, global line, pattern) ordered score desc, line asc, pattern asc,
+    missing rows = (-inf, -1, -1); pat_hist int64[npat]; sev_hist int64[nsev]). No host sync."""
+    dev = score.device
+    k = max(1, min(int(k), SUMMARY_MAX_K))
+    n = score.numel()
+    rows = torch.empty((k, 3), dtype=torch.float64, device=dev)
+    pat_hist = torch.zeros(max(npat, 1), dtype=torch.int64, device=dev)
+    sev_hist = torch.zeros(max(nsev, 1), dtype=torch.int64, device=dev)
+    sev_of_pat = sev_index
+    l32 = line.data_ptr() if line.dtype == torch.int32 else 0
+    l64 = line.data_ptr() if line.dtype == torch.int64 else 0
+    ins = (score.data_ptr() if n else 0, pat.data_ptr() if n else 0, l32 if n else 0, l64 if n else 0,
+           _p(line_add), sev_of_pat.data_ptr(), 0)
+
+    def call(wp, wn):
+        return N.summarize(ins, n, k, rows.data_ptr(), pat_hist.data_ptr(), sev_hist.data_ptr(), wp, wn, _s(score),
+                           score.is_cuda)
+
+    if score.is_cuda:
+        _run_ws(call, ws if ws is not None else Workspace(dev))
+    else:
+        call(0, 0)
+    return rows, pat_hist[:npat], sev_hist[:nsev]
+
+
+def topk_rows(rows: torch.Tensor, k: int, ws: Optional[Workspace] = None) -> torch.Tensor:
+    """Merge (score, line, pattern) rows (e.g. every rank's top-k) into the k best, same order."""
+    dev = rows.device
+    k = max(1, min(int(k), SUMMARY_MAX_K))
+    rows = rows.contiguous()
+    out = torch.empty((k, 3), dtype=torch.float64, device=dev)
+    ins = (0, 0, 0, 0, 0, 0, rows.data_ptr())
+
+    def call(wp, wn):
+        return N.summarize(ins, rows.shape[0], k, out.data_ptr(), 0, 0, wp, wn, _s(rows), rows.is_cuda)
+
+    if rows.is_cuda:
+        _run_ws(call, ws if ws is not None else Workspace(dev))
+    else:
+        call(0, 0)
+    return out
+
+
+def rescore(gl: torch.Tensor, fac: torch.Tensor, n_lines: int, sp_tuple) -> torch.Tensor:
+    """Final streaming scores: the score kernel's kept factors with the chronological factor of the
+    true global line count (left-to-right product, ScoringService.java:102-109)."""
+    n = gl.numel()
+    out = torch.empty(n, dtype=torch.float64, device=gl.device)
+    if n:
+        N.rescore(gl.data_ptr(), fac.contiguous().data_ptr(), n, int(n_lines), sp_tuple, out.data_ptr(), _s(gl),
+                  gl.is_cuda)
+    return out
+
+
 def score_fused(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_carry, st_tuple, sp_tuple, with_factors=False):
     """k_score with the frequency count fused in: freq = carry[fkey] + rank (-1 without a key)."""
     n = ev_line.numel()

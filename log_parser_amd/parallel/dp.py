@@ -11,6 +11,7 @@ resolved with collectives:
   C4  backward sequence chain  (ScoringService.java:296-305)  /   [own_lines | freq counts | chain]
   C5/C6 severity histogram + frequency histogram               -> all_reduce(sum)
   C7  top-k events                                             -> all_gather of k rows, merge
+  (the local halves of C5-C7 are one hand-written kernel chain, csrc/kernels/summarize.hip)
   C2  halos: by default every rank stages its halo lines from the shared host source together
       with its own lines (no extra collective); ``exchange_halos`` is the point-to-point variant
       (batch_isend_irecv with both neighbours) for ranks that only hold their own lines
@@ -29,7 +30,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ..engine import Engine, RunResult, Segments
+from ..engine import Engine, RunResult, Segments, summary_from_severity
+from ..ops import kernels as K
 
 
 def world() -> tuple:
@@ -83,10 +85,10 @@ class StepOutput:
     own_counts: torch.Tensor       # owned lines per rank (C1 all-gather), stays on the device
     rank: int
     pattern_counts: torch.Tensor   # global (all-reduced) events per pattern
-    topk_score: Optional[torch.Tensor] = None   # rank 0: merged global top-k
-    topk_line: Optional[torch.Tensor] = None    # 0-based global line
-    topk_pat: Optional[torch.Tensor] = None
-    summary: Optional[dict] = None
+    severity_counts: Optional[torch.Tensor] = None  # global events per library severity name
+    # rank 0: merged global top-k rows (score, 0-based global line, pattern), score desc / line asc
+    # / pattern asc, padded with (-inf, -1, -1) when fewer events exist; stays on the device
+    topk_rows: Optional[torch.Tensor] = None
     own_lo: int = 0                                 # first owned local line (= left halo lines)
     own_start_dev: Optional[torch.Tensor] = None    # [1] global index of the first owned line
 
@@ -98,6 +100,25 @@ class StepOutput:
     @property
     def own_start(self) -> int:
         return int(self.own_counts[:self.rank].sum().item())
+
+    def _top(self, col: int) -> Optional[torch.Tensor]:
+        if self.topk_rows is None:
+            return None
+        r = self.topk_rows
+        k = int(torch.isfinite(r[:, 0]).sum().item())
+        return r[:k, col] if col == 0 else r[:k, col].to(torch.int64)
+
+    @property
+    def topk_score(self) -> Optional[torch.Tensor]:
+        return self._top(0)
+
+    @property
+    def topk_line(self) -> Optional[torch.Tensor]:
+        return self._top(1)
+
+    @property
+    def topk_pat(self) -> Optional[torch.Tensor]:
+        return self._top(2)
 
 
 class ShardedAnalyzer:
@@ -149,51 +170,35 @@ class ShardedAnalyzer:
         segs.g0 = own_start - halo_left
         segs.n = own_counts.sum(0, keepdim=True).clamp(min=1)
         res = eng.finish(prep, segs, carry, seq_carry, with_factors)
-        # C5/C6 + frequency histogram: one all-reduce
-        P = len(lib.patterns)
-        pc = torch.bincount(res.ev_pat.long(), minlength=P) if res.ev_pat.numel() else torch.zeros(P, dtype=torch.int64, device=dev)
-        red = torch.cat([pc.to(torch.int64), prep.freq_counts[:nk].to(torch.int64)])
+        # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
+        # rank's top-k rows with global line numbers, no host sync), then ONE all-reduce for the
+        # histograms + frequency counts and one all-gather of k rows
+        P, S = len(lib.patterns), len(lib.sev_names)
+        k = max(1, min(topk, K.SUMMARY_MAX_K))
+        rows, pc, sc = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
+                                   line_add=segs.g0, ws=eng.ws)
+        red = torch.cat([pc, sc, prep.freq_counts[:nk].to(torch.int64)])
         red = all_reduce_sum(red, self.group)
-        pattern_counts = red[:P]
-        eng.commit_frequency(red[P:])
-        out = StepOutput(res, own_counts, rank, pattern_counts, own_lo=own_lo, own_start_dev=own_start)
-        # C7: top-k
+        eng.commit_frequency(red[P + S:])
+        out = StepOutput(res, own_counts, rank, red[:P], severity_counts=red[P:P + S], own_lo=own_lo,
+                         own_start_dev=own_start)
         if topk > 0:
-            k = min(topk, res.score.numel())
-            rows = torch.full((topk, 3), -1.0, dtype=torch.float64, device=dev)
-            rows[:, 0] = float("-inf")
-            if k:
-                v, idx = torch.topk(res.score, k)
-                rows[:k, 0] = v
-                rows[:k, 1] = (res.ev_line[idx].to(torch.int64) - own_lo + own_start).to(torch.float64)
-                rows[:k, 2] = res.ev_pat[idx].to(torch.float64)
             allrows = all_gather_rows(rows.flatten(), self.group).view(-1, 3)
             if rank == 0:
-                kk = min(topk, int(torch.isfinite(allrows[:, 0]).sum().item()))
-                v, idx = torch.topk(allrows[:, 0], kk)
-                out.topk_score = v
-                out.topk_line = allrows[idx, 1].to(torch.int64)
-                out.topk_pat = allrows[idx, 2].to(torch.int64)
+                out.topk_rows = K.topk_rows(allrows, k, ws=eng.ws) if allrows.shape[0] > k else allrows
         return out
 
-    def summary(self, pattern_counts: torch.Tensor, first_pat: Optional[int] = None) -> dict:
+    def summary(self, pattern_counts: torch.Tensor, first_pat: Optional[int] = None,
+                severity_counts: Optional[torch.Tensor] = None) -> dict:
+        """AnalysisSummary of a step (AnalysisService.java:188-215); from the severity histogram
+        when given (S entries instead of P)."""
         lib = self.engine.lib
-        pc = pattern_counts.cpu().numpy()
-        n = int(pc.sum())
-        if n == 0:
-            return {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
-        from ..golden import SEVERITY_ORDER
-        dist_: dict = {}
-        for p in np.nonzero(pc)[0]:
-            s = lib.severity[p]
-            dist_[s] = dist_.get(s, 0) + int(pc[p])
-        best_idx, best = -1, None
-        for s in dist_:
-            if s in SEVERITY_ORDER and SEVERITY_ORDER.index(s) > best_idx:
-                best_idx, best = SEVERITY_ORDER.index(s), s
-        if best is None and first_pat is not None:
-            best = lib.severity[first_pat]
-        return {"significantEvents": n, "highestSeverity": best, "severityDistribution": dist_}
+        if severity_counts is not None:
+            sc = severity_counts.cpu().numpy()
+        else:
+            pc = pattern_counts.cpu().numpy()
+            sc = np.bincount(lib.sev_index, weights=pc, minlength=len(lib.sev_names)).astype(np.int64)
+        return summary_from_severity(lib, sc, first_pat)
 
 
 def halo_bytes(data, n_lines: int) -> tuple:

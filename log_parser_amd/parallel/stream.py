@@ -325,30 +325,22 @@ class StreamAnalyzer:
             gl = torch.cat(ev_gl)
             pat = torch.cat(ev_pat)
             fac = torch.cat(ev_fac)
-            score = self._final_scores(gl, fac, N)
+            # reference product order with the true chronological factor (k_rescore)
+            score = K.rescore(gl, fac, N, eng.sp_tuple)
         else:
             gl = torch.zeros(0, dtype=torch.int64, device=dev)
             pat = torch.zeros(0, dtype=torch.int32, device=dev)
             score = torch.zeros(0, dtype=torch.float64, device=dev)
         eng.commit_frequency(run_counts[:nkeys])
+        # summary + top-k in one kernel chain (summarize.hip): severity histogram, k best rows
+        P, S = len(lib.patterns), len(lib.sev_names)
+        rows, _, sc = K.summarize(score, pat, gl, max(1, self.topk), eng.tabs["sev_index"], P, S, ws=eng.ws)
         k = min(self.topk, score.numel())
-        v, idx = torch.topk(score, k) if k else (score[:0], torch.zeros(0, dtype=torch.int64, device=dev))
-        pc = torch.bincount(pat.long(), minlength=len(lib.patterns)) if pat.numel() else None
-        pat_h = pat.cpu().numpy()
-        summary = eng.summary(pat_h) if pc is not None else eng.summary(np.zeros(0, np.int32))
-        out = StreamResult(line_base, int(score.numel()), summary, v.cpu().numpy(), gl[idx].cpu().numpy(),
-                           pat[idx].cpu().numpy(), chunks, nbytes_total, time.perf_counter() - t0)
+        top = rows[:k].cpu().numpy()
+        first = int(pat[0].item()) if pat.numel() else None
+        summary = eng.summary_from_severity(sc.cpu().numpy(), first)
+        out = StreamResult(line_base, int(score.numel()), summary, top[:, 0].copy(), top[:, 1].astype(np.int64),
+                           top[:, 2].astype(np.int64), chunks, nbytes_total, time.perf_counter() - t0)
         if self.keep_events:
-            out.events = (gl.cpu().numpy(), pat_h, score.cpu().numpy())
+            out.events = (gl.cpu().numpy(), pat.cpu().numpy(), score.cpu().numpy())
         return out
-
-    def _final_scores(self, gl: torch.Tensor, fac: torch.Tensor, N: int) -> torch.Tensor:
-        """Reference product order with the true chronological factor (ScoringService.java:102-151)."""
-        p = self.engine.params
-        pos = gl.to(torch.float64) / float(N)
-        e, m, t = p.early_bonus_threshold, p.max_early_bonus, p.penalty_threshold
-        early = 1.5 + (e - pos) * ((m - 1.5) / e)
-        mid = 1.0 + (t - pos) * (0.5 / (t - e))
-        late = 0.5 + (1.0 - pos)
-        chrono = torch.where(pos <= e, early, torch.where(pos <= t, mid, late))
-        return fac[:, 0] * fac[:, 1] * chrono * fac[:, 3] * fac[:, 4] * fac[:, 5] * (1.0 - fac[:, 6])

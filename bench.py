@@ -196,13 +196,11 @@ def run(args, sets, trig, rank, world, local_rank, server):
         """(global line int64, pattern int32, score f64) of EVERY event -> pinned host, one copy.
         The D2H runs on the copy stream, behind the prefetch H2D: on the compute stream it would
         queue behind the 23 ms PCIe ingest of the next step and stall the next step's kernels."""
-        r = out.result
-        n = r.ev_line.numel()
+        n = out.result.ev_line.numel()
         if n == 0:
             return
-        g = (r.ev_line.to(torch.int64) - out.own_lo + out.own_start_dev)
-        pk = torch.cat([g.view(torch.int32), r.ev_pat.to(torch.int32), r.score.view(torch.int32)])
-        nb = pk.numel() * 4
+        pk = out.events_packed                  # packed by the summary kernel: [line i64 | score f64 | pat i32]
+        nb = pk.numel()
         if ev_host[slot].numel() < nb:
             if use_cuda:
                 torch.cuda.current_stream().synchronize()        # the old slot may still be in flight
@@ -212,10 +210,10 @@ def run(args, sets, trig, rank, world, local_rank, server):
             done.record()
             with torch.cuda.stream(copy_stream):
                 copy_stream.wait_event(done)
-                ev_host[slot][:nb].view(torch.int32).copy_(pk, non_blocking=True)
+                ev_host[slot][:nb].copy_(pk, non_blocking=True)
                 pk.record_stream(copy_stream)
         else:
-            ev_host[slot][:nb].view(torch.int32).copy_(pk, non_blocking=use_cuda)
+            ev_host[slot][:nb].copy_(pk, non_blocking=use_cuda)
         state["events_host"] = n
 
     def step():
@@ -232,7 +230,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         ls, ll = K.split_lines(text, nbytes)
-        out = sa.step(text, nbytes, ls, ll, hl, hr, topk=args.topk)
+        out = sa.step(text, nbytes, ls, ll, hl, hr, topk=args.topk, pack_events=True)
         events_to_host(out, b)                                   # results land on the host
         if rank == 0 and out.topk_rows is not None:
             state["top"] = out.topk_rows.cpu()                   # merged global top-k on the host

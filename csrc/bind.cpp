@@ -412,17 +412,14 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("set_host_threads", &set_host_threads);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
-  m.def("nl_tiles", &nl_tiles);
   m.def("parse_pod_request", &parse_pod_request_py);
 
   // ---- device launchers
-  m.def("nl_count_dev", [](uint64_t text, int64_t n, uint64_t cnt, uint64_t s) { nl_count_dev(P<const uint8_t>(text), n, P<int32_t>(cnt), s); });
-  m.def("lines_dev", [](uint64_t nl, int64_t n_nl, uint64_t text, int64_t nb, uint64_t st, uint64_t ln, uint64_t last,
-                        uint64_t s) {
-    lines_dev(P<const int64_t>(nl), n_nl, P<const uint8_t>(text), nb, P<int64_t>(st), P<int32_t>(ln),
-              P<unsigned long long>(last), s); });
-  m.def("nl_write_dev", [](uint64_t text, int64_t n, uint64_t off, uint64_t pos, int flag_cr, uint64_t s) {
-    nl_write_dev(P<const uint8_t>(text), n, P<const int64_t>(off), P<int64_t>(pos), flag_cr, s); });
+  m.def("line_index_tiles", &line_index_tiles);
+  m.def("line_index_dev", [](uint64_t text, int64_t n, uint64_t ws, int64_t ntiles_cap, uint64_t starts, uint64_t lens,
+                             int64_t cap, uint64_t info, bool trim, uint64_t blk, int64_t nblk, uint64_t s) {
+    line_index_dev(P<const uint8_t>(text), n, LineIndexWs{P<int64_t>(ws), ntiles_cap, size_t(1) << 20}, P<int64_t>(starts),
+                   P<int32_t>(lens), cap, P<int64_t>(info), trim, P<int32_t>(blk), nblk, s); });
   m.def("prefilter_dev", [](uint64_t text, int64_t n, py::tuple pf, uint64_t ls, int64_t nl, uint64_t cand, int64_t cap,
                             uint64_t count, int grid, uint64_t s) {
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
@@ -469,15 +466,17 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("freq_evict", [](py::tuple ring, double horizon, uint64_t s, bool dev) {
     freq_evict(ring_from(ring), horizon, s, dev);
   });
-  // ---- summary + top-k (summarize.hip). in = (score, pat, line32, line64, line_add, sev_of_pat, rows)
-  m.def("summarize", [](py::tuple in, int64_t n, int k, uint64_t top, uint64_t pat_hist, uint64_t sev_hist,
+  // ---- summary + top-k (summarize.hip). in = (score, pat, line32, line64, line_add, sev_of_pat, rows
+  // [, packed events out])
+  m.def("summarize", [](py::tuple in, int64_t n, int k, int nsev, uint64_t top, uint64_t pat_hist, uint64_t sev_hist,
                         uint64_t ws, uint64_t ws_bytes, uint64_t s, bool dev) -> uint64_t {
     const SummIn I{P<const double>(in[0].cast<uint64_t>()), P<const int32_t>(in[1].cast<uint64_t>()),
                    P<const int32_t>(in[2].cast<uint64_t>()), P<const int64_t>(in[3].cast<uint64_t>()),
                    P<const int64_t>(in[4].cast<uint64_t>()), P<const int32_t>(in[5].cast<uint64_t>()),
-                   P<const double>(in[6].cast<uint64_t>())};
+                   P<const double>(in[6].cast<uint64_t>()),
+                   in.size() > 7 ? P<void>(in[7].cast<uint64_t>()) : nullptr};
     if (dev)
-      return summarize_dev(I, n, k, P<double>(top), P<unsigned long long>(pat_hist), P<unsigned long long>(sev_hist),
+      return summarize_dev(I, n, k, nsev, P<double>(top), P<unsigned long long>(pat_hist), P<unsigned long long>(sev_hist),
                            P<void>(ws), ws_bytes, s);
     summarize_host(I, n, k, P<double>(top), P<int64_t>(pat_hist), P<int64_t>(sev_hist));
     return 0;
@@ -488,6 +487,19 @@ PYBIND11_MODULE(_lpnative, m) {
       rescore_dev(P<const int64_t>(gl), P<const double>(fac), n, Nn, sp_from(sp), P<double>(out), s);
     else
       rescore_host(P<const int64_t>(gl), P<const double>(fac), n, Nn, sp_from(sp), P<double>(out));
+  });
+  // ---- DP step bookkeeping (dp_glue.hip)
+  m.def("dp_pack", [](int64_t own_lines, uint64_t freq, int nk, uint64_t chain, int ns, uint64_t pack, uint64_t s,
+                      bool dev) { dp_pack(own_lines, P<const int64_t>(freq), nk, P<const int32_t>(chain), ns,
+                                          P<int64_t>(pack), s, dev); });
+  // a = (g, world, rank, nk, ns, halo_left, tot, slot_e0, slot_k, own_start, g0, n, carry, seq_carry, red_tail)
+  m.def("dp_carry", [](py::tuple a, uint64_t s, bool dev) {
+    auto u = [&](int i) { return a[i].cast<uint64_t>(); };
+    DpCarryArgs A{P<const int64_t>(u(0)), a[1].cast<int>(), a[2].cast<int>(), a[3].cast<int>(), a[4].cast<int>(),
+                  a[5].cast<int64_t>(), P<const int64_t>(u(6)), P<const int64_t>(u(7)), P<const int64_t>(u(8)),
+                  P<int64_t>(u(9)), P<int64_t>(u(10)), P<int64_t>(u(11)), P<int64_t>(u(12)), P<uint8_t>(u(13)),
+                  P<int64_t>(u(14))};
+    dp_carry(A, s, dev);
   });
   m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev) {
     freq_record(P<const int64_t>(counts), K, now, ring_from(ring), s, dev);
@@ -545,9 +557,11 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("post_hits", [](uint64_t cand, int64_t n, int64_t pre_from, int lbits, int rbits, int R, uint64_t text,
                         uint64_t ls, uint64_t ll, py::tuple dfa, py::tuple ev, uint64_t hits, uint64_t hit_line,
                         uint64_t hit_off, uint64_t ev_cnt, uint64_t ev_end, uint64_t counters, uint64_t ws,
-                        size_t ws_bytes, uint64_t s, bool dev) -> size_t {
+                        size_t ws_bytes, uint64_t s, bool dev, uint64_t cand2, uint64_t dcount) -> size_t {
     HitsArgs A;
     A.cand = P<const int64_t>(cand); A.n = n; A.pre_from = pre_from; A.lbits = lbits; A.rbits = rbits; A.R = R;
+    A.cand2 = P<const int64_t>(cand2); A.dcount = P<const unsigned long long>(dcount);
+    if (A.dcount && !dev) throw std::runtime_error("post_hits: device counters need the device path");
     A.text = P<const uint8_t>(text); A.ls = P<const int64_t>(ls); A.ll = P<const int32_t>(ll);
     A.dfa = dfa_from(dfa); A.ev = ev_from(ev);
     A.hits = P<int64_t>(hits); A.hit_line = P<int32_t>(hit_line); A.hit_off = P<int64_t>(hit_off);

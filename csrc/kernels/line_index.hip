@@ -1,0 +1,279 @@
+// K1 line index (reference: Java logs.split("\\r?\\n"), AnalysisService.java:53): line starts and
+// lengths straight from the bytes, two reads of the text and ONE host read.
+//
+//   k_nl_count   per 16 KiB tile: number of '\n' (one dwordx4-wide pass, memory-bound)
+//   rocprim      exclusive scan of the tile counts (decoupled look-back over ~80k counts)
+//   k_nl_lines   per tile again: every '\n' at p with global index g writes starts[g+1] = p + 1
+//                and, when the previous '\n' is in the same tile, lens[g] = (p minus a '\r' right
+//                before it) - start; staged in LDS, stored coalesced. The tile's FIRST line end is
+//                recorded (fix_g, fix_end) for
+//   k_line_fix   which completes it once every start is written, plus the total (info[0]), the
+//                final line (to nbytes) and info[1] = last '\n' position (or -1);
+//   k_line_trim  Java's trailing-empty trimming -> info[2] = lines kept.
+// k_nl_lines also writes the coarse 4 KiB block -> line index the literal verify uses (one wave
+// per block: the line of its first byte is the number of '\n' before it).
+// A single-pass decoupled look-back variant (tile ticket + 256 predecessor states per round
+// trip) was measured at ~1.08 ms per 1.33 GB vs ~0.55 ms for these two passes: the INCLUSIVE
+// frontier, not HBM, sets its pace (docs/PERFORMANCE.md).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+#include <stdexcept>
+#include <string>
+
+#include "lp_api.h"
+
+namespace lp {
+
+constexpr int LI_BYTES_PER_THREAD = 64;
+__device__ __forceinline__ uint32_t li_zero_bytes(uint32_t t) {
+  const uint32_t y = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;   // high bit of every 0x00 byte of t
+  return ~(y | t | 0x7F7F7F7Fu);
+}
+
+constexpr int LI_THREADS = 256;
+constexpr int LI_TILE = LI_THREADS * LI_BYTES_PER_THREAD;
+constexpr int LI_STAGE = LI_THREADS * 8;       // staged lines per tile (~150 per 16 KiB of log text)
+
+// '\n' / '\r' byte masks of this lane's 64 bytes (bytes past nbytes are not text)
+__device__ __forceinline__ int li_masks(const uint8_t* __restrict__ text, int64_t nbytes, int64_t base,
+                                        uint32_t (&m)[16], uint32_t (&cr)[16]) {
+  int c = 0;
+  if (base < nbytes) {
+    const uint4* p = reinterpret_cast<const uint4*>(text + base);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = p[k];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        m[4 * k + q] = li_zero_bytes(w[q] ^ 0x0A0A0A0Au);
+        cr[4 * k + q] = li_zero_bytes(w[q] ^ 0x0D0D0D0Du);
+      }
+    }
+    if (base + LI_BYTES_PER_THREAD > nbytes) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int64_t valid = nbytes - (base + 4 * k);
+        const uint32_t keep = valid >= 4 ? 0xFFFFFFFFu : valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u);
+        m[k] &= keep;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c += __popc(m[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m[k] = cr[k] = 0;
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(LI_THREADS) void k_nl_count(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                         int32_t* __restrict__ cnt) {
+  const int64_t base = (int64_t)blockIdx.x * LI_TILE + (int64_t)threadIdx.x * LI_BYTES_PER_THREAD;
+  int c = 0;
+  if (base < nbytes) {
+    const uint4* p = reinterpret_cast<const uint4*>(text + base);
+    if (base + LI_BYTES_PER_THREAD <= nbytes) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 v = p[k];
+        c += __popc(li_zero_bytes(v.x ^ 0x0A0A0A0Au)) + __popc(li_zero_bytes(v.y ^ 0x0A0A0A0Au)) +
+             __popc(li_zero_bytes(v.z ^ 0x0A0A0A0Au)) + __popc(li_zero_bytes(v.w ^ 0x0A0A0A0Au));
+      }
+    } else {
+      uint32_t m[16], cr[16];
+      c = li_masks(text, nbytes, base, m, cr);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ int ws[LI_THREADS / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < LI_THREADS / 64; ++w) t += ws[w];
+    cnt[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                         const int64_t* __restrict__ off,
+                                                         int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+                                                         int64_t cap, int64_t* __restrict__ fix_g,
+                                                         int64_t* __restrict__ fix_end, int32_t* __restrict__ blk,
+                                                         int64_t nblk) {
+  constexpr int NW = LI_THREADS / 64;
+  __shared__ int s_wcnt[NW];
+  __shared__ int32_t s_start[LI_STAGE];          // tile-relative: start of the next line (= '\n' + 1)
+  __shared__ int32_t s_end[LI_STAGE];            // tile-relative end of the line ('\n' minus a '\r')
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t tile = blockIdx.x;
+  const int64_t tbase = tile * LI_TILE;
+  const int64_t base = tbase + (int64_t)threadIdx.x * LI_BYTES_PER_THREAD;
+  uint32_t m[16], cr[16];
+  const int c = li_masks(text, nbytes, base, m, cr);
+  int incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) s_wcnt[wid] = incl;
+  __syncthreads();
+  int woff = 0, tot = 0;
+  for (int w = 0; w < NW; ++w) {
+    if (w < wid) woff += s_wcnt[w];
+    tot += s_wcnt[w];
+  }
+  const int64_t excl = off[tile];
+  // coarse index for line lookups (lp_core.h locate_line): a wave covers one 4 KiB block, and the
+  // line holding its first byte is the number of '\n' before it
+  if (blk && lane == 0 && tile * NW + wid < nblk) blk[tile * NW + wid] = (int32_t)(excl + woff);
+  const bool staged = tot <= LI_STAGE;            // block-uniform
+  const uint32_t cr0 = (m[0] & 0x80u) && base > 0 && text[base - 1] == '\r';
+  // pass A: every '\n' -> (start of the next line, end of its own line)
+  int o = woff + (incl - c);                      // tile-local index of this lane's first '\n'
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint32_t mm = m[k];
+    const uint32_t crb = (cr[k] << 8) | ((k > 0 ? (cr[k - 1] >> 31) : cr0) << 7);   // '\r' before byte j -> bit 8j+7
+    while (mm) {
+      const int b = __ffs(mm) - 1;                // bit 7, 15, 23 or 31
+      const int64_t pos = base + 4 * k + (b >> 3);
+      if (staged) {
+        s_start[o] = (int32_t)(pos + 1 - tbase);
+        s_end[o] = (int32_t)(pos - (int64_t)((crb >> b) & 1u) - tbase);
+      } else if (excl + o + 1 < cap) {
+        starts[excl + o + 1] = pos + 1;
+      }
+      ++o;
+      mm &= mm - 1;
+    }
+  }
+  __syncthreads();
+  if (staged) {
+    for (int i = threadIdx.x; i < tot; i += LI_THREADS) {
+      const int64_t g = excl + i;
+      if (g + 1 < cap) starts[g + 1] = tbase + s_start[i];
+      if (i == 0) {
+        fix_g[tile] = g;
+        fix_end[tile] = tbase + s_end[0];
+      } else if (g < cap) {
+        lens[g] = s_end[i] - s_start[i - 1];
+      }
+    }
+  } else {
+    // pass B (a tile with more lines than the stage): lengths from the starts just stored
+    o = woff + (incl - c);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      uint32_t mm = m[k];
+      const uint32_t crb = (cr[k] << 8) | ((k > 0 ? (cr[k - 1] >> 31) : cr0) << 7);
+      while (mm) {
+        const int b = __ffs(mm) - 1;
+        const int64_t end = base + 4 * k + (b >> 3) - (int64_t)((crb >> b) & 1u);
+        const int64_t g = excl + o;
+        if (o == 0) {
+          fix_g[tile] = g;
+          fix_end[tile] = end;
+        } else if (g < cap) {
+          lens[g] = (int32_t)(end - starts[g]);
+        }
+        ++o;
+        mm &= mm - 1;
+      }
+    }
+  }
+  if (tot == 0 && threadIdx.x == 0) fix_g[tile] = -1;
+  if (tile == 0 && threadIdx.x == 0 && cap > 0) starts[0] = 0;
+}
+
+// Completes what needs every tile's starts: the first line end of each tile, the final line and
+// info[1]. Thread t < ntiles: tile t; thread ntiles: the final line.
+__global__ __launch_bounds__(256) void k_line_fix(int64_t ntiles, int64_t nbytes, const int64_t* __restrict__ fix_g,
+                                                  const int64_t* __restrict__ fix_end,
+                                                  const int64_t* __restrict__ off, const int32_t* __restrict__ cnt,
+                                                  const int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+                                                  int64_t cap, int64_t* __restrict__ info, int32_t* __restrict__ blk,
+                                                  int64_t nblk) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < ntiles) {
+    const int64_t g = fix_g[t];
+    if (g >= 0 && g < cap) lens[g] = (int32_t)(fix_end[t] - (g == 0 ? 0 : starts[g]));
+  } else if (t == ntiles) {
+    const int64_t total = off[ntiles - 1] + cnt[ntiles - 1];
+    info[0] = total;
+    if (blk)                                      // coarse-index entries past the last tile
+      for (int64_t b = ntiles * (LI_THREADS / 64); b < nblk; ++b) blk[b] = (int32_t)total;
+    const int64_t st = total == 0 ? 0 : (total < cap ? starts[total] : -1);
+    info[1] = total == 0 ? -1 : (total < cap ? st - 1 : -1);
+    if (total < cap) lens[total] = (int32_t)(nbytes - st);
+  }
+}
+
+// Java String.split drops trailing empty strings -- except that input without any '\n' is one
+// line even when empty. One workgroup walks back from the end 256 lines at a time (trailing empty
+// lines are rare: one iteration in practice). info[2] = lines kept.
+__global__ __launch_bounds__(256) void k_line_trim(const int32_t* __restrict__ lens, int64_t cap,
+                                                   int64_t* __restrict__ info) {
+  __shared__ int64_t wmax[4];
+  const int64_t nl = info[0];
+  if (nl == 0) {
+    if (threadIdx.x == 0) info[2] = 1;
+    return;
+  }
+  const int64_t n = nl + 1 < cap ? nl + 1 : cap;
+  for (int64_t hi = n; hi > 0; hi -= 256) {
+    const int64_t i = hi - 1 - threadIdx.x;
+    int64_t best = (i >= 0 && lens[i] > 0) ? i : -1;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const long long o = __shfl_xor((long long)best, off, 64);
+      best = best > o ? best : o;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = best;
+    __syncthreads();
+    const int64_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (b >= 0) {
+      if (threadIdx.x == 0) info[2] = b + 1;
+      return;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) info[2] = 0;
+}
+
+int64_t line_index_tiles(int64_t nbytes) { return (nbytes + LI_TILE - 1) / LI_TILE; }
+
+void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, int64_t* starts, int32_t* lens,
+                    int64_t cap, int64_t* info, bool trim, int32_t* blk, int64_t nblk, uint64_t stream) {
+  const int64_t nt = line_index_tiles(nbytes);
+  if (nt <= 0 || nt > W.ntiles_cap) throw std::runtime_error("line_index: empty text or workspace too small");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int64_t* off = W.buf;
+  int64_t* fix_g = W.buf + W.ntiles_cap;
+  int64_t* fix_end = W.buf + 2 * W.ntiles_cap;
+  int32_t* cnt = reinterpret_cast<int32_t*>(W.buf + 3 * W.ntiles_cap);
+  void* tmp = W.buf + 4 * W.ntiles_cap;
+  size_t tmp_bytes = 0;
+  if (rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
+          hipSuccess ||
+      tmp_bytes > W.tmp_bytes)
+    throw std::runtime_error("line_index: scan workspace too small");
+  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, cnt);
+  if (rocprim::exclusive_scan(tmp, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
+      hipSuccess)
+    throw std::runtime_error("line_index: rocprim scan failed");
+  hipLaunchKernelGGL(k_nl_lines, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, off, starts, lens, cap,
+                     fix_g, fix_end, blk, nblk);
+  hipLaunchKernelGGL(k_line_fix, dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, st, nt, nbytes, fix_g, fix_end,
+                     off, cnt, starts, lens, cap, info, blk, nblk);
+  if (trim) hipLaunchKernelGGL(k_line_trim, dim3(1), dim3(256), 0, st, lens, cap, info);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in line_index");
+}
+
+}  // namespace lp

@@ -6,13 +6,8 @@
 
 namespace lp {
 
-int64_t nl_tiles(int64_t nbytes);
 // worker threads of the host twins (CPU backend)
 void set_host_threads(int n);
-void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream);
-// flag_cr: set bit 62 of a position when the '\n' follows a '\r' (consumed by lines_dev)
-void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, int flag_cr,
-                  uint64_t stream);
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
                    int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
@@ -31,8 +26,6 @@ void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int
 void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
                     const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
                     int32_t* out);
-void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
-               unsigned long long* last_nonempty, uint64_t stream);
 int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap);
@@ -91,6 +84,41 @@ void freq_evict(const FreqRing& R, double horizon, uint64_t stream, bool dev);
 void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev);
 }  // namespace lp
 
+// ---- line index (line_index.hip)
+namespace lp {
+struct LineIndexWs {
+  int64_t* buf;                // [4 * ntiles_cap] tile offsets, first line ends (line, end), counts;
+  int64_t ntiles_cap;          // then tmp_bytes of scan scratch
+  size_t tmp_bytes;
+};
+int64_t line_index_tiles(int64_t nbytes);
+// starts/lens [cap]; info[0] = '\n' count, info[1] = last '\n' (or -1), info[2] = lines after
+// Java's trailing-empty trimming (trim only). Lines = info[0] + 1 before trimming.
+// blk (optional) [nblk]: line holding byte b << 12 (the coarse index of lp_core.h locate_line)
+void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, int64_t* starts, int32_t* lens,
+                    int64_t cap, int64_t* info, bool trim, int32_t* blk, int64_t nblk, uint64_t stream);
+}  // namespace lp
+
+// ---- DP step bookkeeping (dp_glue.hip)
+namespace lp {
+struct DpCarryArgs {
+  const int64_t* g;          // [world][1 + nk + ns] gathered payloads
+  int world, rank, nk, ns;
+  int64_t halo_left;
+  const int64_t* tot;        // [nk] persistent window totals (may be null)
+  const int64_t* slot_e0;    // [ns] first slot of each sequence-event slot's sequence
+  const int64_t* slot_k;     // [ns] event index of the slot
+  // outputs
+  int64_t* own_start; int64_t* g0; int64_t* n;   // [1] each
+  int64_t* carry;            // [nk]
+  uint8_t* seq_carry;        // [ns]
+  int64_t* red_tail;         // [nk] this rank's counts into the all-reduce buffer (may be null)
+};
+void dp_pack(int64_t own_lines, const int64_t* freq, int nk, const int32_t* chain, int ns, int64_t* pack,
+             uint64_t stream, bool dev);
+void dp_carry(const DpCarryArgs& A, uint64_t stream, bool dev);
+}  // namespace lp
+
 // ---- summary + top-k, streaming re-score (summarize.hip)
 namespace lp {
 struct SummIn {
@@ -103,11 +131,13 @@ struct SummIn {
   const int32_t* sev_of_pat; // [P] severity index 0..4
   // or rows [n][3] = (score, line, pattern) as float64 (merging top-k lists)
   const double* rows;
+  // optional (events): every event packed as [global line int64 x n][score f64 x n][pattern i32 x n]
+  void* ev_out = nullptr;
 };
 // writes the k best rows (score desc, line asc, pattern asc; missing rows = (-inf, -1, -1)) and,
 // from events, adds the pattern / severity histograms. Device: returns workspace bytes, runs only
 // when ws_bytes suffices.
-size_t summarize_dev(const SummIn& in, int64_t n, int k, double* top_rows, unsigned long long* pat_hist,
+size_t summarize_dev(const SummIn& in, int64_t n, int k, int nsev, double* top_rows, unsigned long long* pat_hist,
                      unsigned long long* sev_hist, void* ws, size_t ws_bytes, uint64_t stream);
 void summarize_host(const SummIn& in, int64_t n, int k, double* top_rows, int64_t* pat_hist, int64_t* sev_hist);
 void rescore_dev(const int64_t* gl, const double* fac, int64_t n, int64_t N, const ScoreParams& S, double* out,
@@ -132,6 +162,11 @@ struct EvTables {
 struct HitsArgs {
   const int64_t* cand;       // (regex << 32 | line): [0, pre_from) to DFA-verify, [pre_from, n) pre-verified
   int64_t n, pre_from;
+  // device-count mode (dcount != null): cand[0, pre_from) and cand2[0, n - pre_from) are two
+  // fixed-capacity regions whose used lengths are the device counters dcount[0] / dcount[1]
+  // (the matchers' append counters: no host read between matching and the hit CSR)
+  const int64_t* cand2 = nullptr;
+  const unsigned long long* dcount = nullptr;
   int lbits, rbits, R;
   const uint8_t* text; const int64_t* ls; const int32_t* ll;
   DfaPool dfa;

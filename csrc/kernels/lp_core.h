@@ -237,6 +237,7 @@ LP_HD int64_t locate_line(const int64_t* ls, int64_t n, const int32_t* blk, int6
   const int64_t b = pos >> LINE_BLK_SHIFT;
   int64_t lo = blk[b], hi = (int64_t)blk[b + 1] + 1;
   if (hi > n) hi = n;
+  if (lo > n - 1) lo = n - 1;                    // bytes of trimmed trailing empty lines
   while (lo + 1 < hi) {
     const int64_t mid = (lo + hi) >> 1;
     if (ls[mid] <= pos) lo = mid; else hi = mid;

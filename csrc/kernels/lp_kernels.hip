@@ -1,7 +1,7 @@
 // gfx950 (MI355X) kernels of the log-analysis pipeline + their host (CPU backend) twins.
 //
 // Hot loops of the reference and the kernel that replaces each:
-//   K1 line split     AnalysisService.java:53              -> k_nl_count / k_nl_write
+//   K1 line split     AnalysisService.java:53              -> k_line_index (line_index.hip)
 //   K3 primary match  AnalysisService.java:89-95           -> k_prefilter (literal bloom + Teddy in LDS)
 //                                                             + k_pf_verify, DFA verify in lp_post.hip
 //   K4/K5 aux match   ScoringService.java:272-347          -> same engine, all aux regexes
@@ -36,166 +36,6 @@ static inline hipStream_t as_stream(uint64_t s) { return reinterpret_cast<hipStr
 // ---- host twins: the CPU backend (no-GPU serving, availability fallback, tests). Parallel over
 // independent items with plain threads (lp_host.h); results are order-insensitive (callers sort).
 void set_host_threads(int n) { host_threads() = std::max(1, n); }
-
-// ------------------------------------------------------------------------------------------
-// K1: newline index.  16 KiB tile per 256-thread block, 64 B per thread (4 x dwordx4 loads).
-constexpr int NL_THREADS = 256;
-constexpr int NL_BYTES_PER_THREAD = 64;
-constexpr int NL_TILE = NL_THREADS * NL_BYTES_PER_THREAD;
-constexpr int64_t LP_NL_CR = int64_t(1) << 62;   // flag in a newline position: preceded by '\r'
-constexpr int NL_STAGE = 2048;   // LDS-staged newline positions per 16 KiB tile (~150 in log text)
-
-__device__ __forceinline__ uint32_t zero_byte_mask(uint32_t t) {
-  // exact: high bit set in every byte of t that is 0x00
-  uint32_t y = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
-  return ~(y | t | 0x7F7F7F7Fu);
-}
-
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int t = __shfl_up(v, d, 64);
-    if (lane >= d) v += t;
-  }
-  return v;
-}
-
-__global__ __launch_bounds__(NL_THREADS) void k_nl_count(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                         int32_t* __restrict__ blk_cnt) {
-  const int64_t base = (int64_t)blockIdx.x * NL_TILE + (int64_t)threadIdx.x * NL_BYTES_PER_THREAD;
-  int c = 0;
-  if (base < nbytes) {
-    const uint4* p = reinterpret_cast<const uint4*>(text + base);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint4 v = p[k];
-      c += __popc(zero_byte_mask(v.x ^ 0x0A0A0A0Au)) + __popc(zero_byte_mask(v.y ^ 0x0A0A0A0Au)) +
-           __popc(zero_byte_mask(v.z ^ 0x0A0A0A0Au)) + __popc(zero_byte_mask(v.w ^ 0x0A0A0A0Au));
-    }
-  }
-  // block reduce
-  __shared__ int ws[NL_THREADS / 64];
-  int s = wave_incl_scan(c);
-  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < NL_THREADS / 64; ++w) t += ws[w];
-    blk_cnt[blockIdx.x] = t;
-  }
-}
-
-__global__ __launch_bounds__(NL_THREADS) void k_nl_write(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                         const int64_t* __restrict__ blk_off,
-                                                         int64_t* __restrict__ nl_pos, int flag_cr) {
-  const int64_t base = (int64_t)blockIdx.x * NL_TILE + (int64_t)threadIdx.x * NL_BYTES_PER_THREAD;
-  uint32_t m[16], cr[16];
-  int c = 0;
-  if (base < nbytes) {
-    const uint4* p = reinterpret_cast<const uint4*>(text + base);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      uint4 v = p[k];
-      m[4 * k + 0] = zero_byte_mask(v.x ^ 0x0A0A0A0Au);
-      m[4 * k + 1] = zero_byte_mask(v.y ^ 0x0A0A0A0Au);
-      m[4 * k + 2] = zero_byte_mask(v.z ^ 0x0A0A0A0Au);
-      m[4 * k + 3] = zero_byte_mask(v.w ^ 0x0A0A0A0Au);
-      cr[4 * k + 0] = zero_byte_mask(v.x ^ 0x0D0D0D0Du);
-      cr[4 * k + 1] = zero_byte_mask(v.y ^ 0x0D0D0D0Du);
-      cr[4 * k + 2] = zero_byte_mask(v.z ^ 0x0D0D0D0Du);
-      cr[4 * k + 3] = zero_byte_mask(v.w ^ 0x0D0D0D0Du);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c += __popc(m[k]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) m[k] = cr[k] = 0;
-  }
-  __shared__ int ws[NL_THREADS / 64];
-  __shared__ int64_t sbuf[NL_STAGE];
-  int incl = wave_incl_scan(c);
-  const int wid = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) ws[wid] = incl;
-  __syncthreads();
-  int woff = 0, tot = 0;
-  for (int w = 0; w < NL_THREADS / 64; ++w) {
-    if (w < wid) woff += ws[w];
-    tot += ws[w];
-  }
-  // positions are staged in LDS and written out coalesced (a lane's own newlines are ~0.6 on
-  // average: direct 8-byte stores would be scattered partial-line writes); a tile with more
-  // newlines than the stage writes directly
-  const bool staged = tot <= NL_STAGE;                   // block-uniform
-  const int64_t gbase = blk_off[blockIdx.x];
-  int64_t o = woff + incl - c;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    uint32_t mm = m[k];
-    // bit 31 of the previous dword = '\r' in the byte before this dword
-    const uint32_t prev_cr = k > 0 ? (cr[k - 1] >> 31) : (flag_cr && base > 0 && text[base - 1] == '\r');
-    const uint32_t crb = (cr[k] << 8) | (prev_cr << 7);   // '\r' right before byte j -> bit 8j+7
-    while (mm) {
-      int b = __ffs(mm) - 1;          // bit 7, 15, 23 or 31
-      int64_t v = base + 4 * k + (b >> 3);
-      if (flag_cr && ((crb >> b) & 1u)) v |= LP_NL_CR;
-      if (staged)                     // explicit LDS / global stores (no flat pointer select)
-        sbuf[o] = v;
-      else
-        nl_pos[gbase + o] = v;
-      ++o;
-      mm &= mm - 1;
-    }
-  }
-  if (staged) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < tot; i += NL_THREADS) nl_pos[gbase + i] = sbuf[i];
-  }
-}
-
-// K1b: newline positions -> Java split("\\r?\\n") line index in one pass: line i spans
-// (nl[i-1], nl[i]) minus a '\r' right before nl[i]; the last line runs to nbytes. The highest
-// non-empty line index is reduced with an atomic so the caller can drop trailing empty lines.
-__global__ __launch_bounds__(256) void k_lines(const int64_t* __restrict__ nl, int64_t n_nl,
-                                               const uint8_t* __restrict__ text, int64_t nbytes,
-                                               int64_t* __restrict__ starts, int32_t* __restrict__ lens) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > n_nl) return;
-  const int64_t st = i == 0 ? 0 : (nl[i - 1] & ~LP_NL_CR) + 1;
-  int64_t en = nbytes;
-  if (i < n_nl) {
-    const int64_t v = nl[i];
-    en = (v & ~LP_NL_CR) - (v >> 62);   // k_nl_write flagged a '\r' before this '\n'
-  }
-  starts[i] = st;
-  lens[i] = (int32_t)(en - st);
-}
-
-// Number of lines up to and including the last non-empty one (Java String.split drops trailing
-// empty strings). One workgroup walks back from the end 256 lines at a time -- trailing empty
-// lines are rare, so this is one iteration in practice and needs no global atomics.
-__global__ __launch_bounds__(256) void k_last_nonempty(const int32_t* __restrict__ lens, int64_t n,
-                                                       unsigned long long* __restrict__ out) {
-  __shared__ int64_t wmax[4];
-  for (int64_t hi = n; hi > 0; hi -= 256) {
-    const int64_t i = hi - 1 - threadIdx.x;
-    int64_t best = (i >= 0 && lens[i] > 0) ? i : -1;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const long long o = __shfl_xor((long long)best, off, 64);
-      best = best > o ? best : o;
-    }
-    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = best;
-    __syncthreads();
-    const int64_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-    if (b >= 0) {
-      if (threadIdx.x == 0) *out = (unsigned long long)(b + 1);
-      return;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *out = 0ull;
-}
 
 // ------------------------------------------------------------------------------------------
 // K3a: literal prefilter.  Bloom filter (2 hashes) of every literal's leading 2/3/4-gram lives
@@ -502,24 +342,6 @@ __global__ __launch_bounds__(256) void k_seq_chain(const int32_t* __restrict__ s
 // launchers (device) and host twins
 static int num_blocks(int64_t n, int t) { return (int)std::max<int64_t>(1, (n + t - 1) / t); }
 
-int64_t nl_tiles(int64_t nbytes) { return (nbytes + NL_TILE - 1) / NL_TILE; }
-
-void nl_count_dev(const uint8_t* text, int64_t nbytes, int32_t* blk_cnt, uint64_t stream) {
-  int64_t nb = nl_tiles(nbytes);
-  if (nb == 0) return;
-  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nb), dim3(NL_THREADS), 0, as_stream(stream), text, nbytes, blk_cnt);
-  LP_CHECK(hipGetLastError());
-}
-
-void nl_write_dev(const uint8_t* text, int64_t nbytes, const int64_t* blk_off, int64_t* nl_pos, int flag_cr,
-                  uint64_t stream) {
-  int64_t nb = nl_tiles(nbytes);
-  if (nb == 0) return;
-  hipLaunchKernelGGL(k_nl_write, dim3((unsigned)nb), dim3(NL_THREADS), 0, as_stream(stream), text, nbytes, blk_off, nl_pos,
-                     flag_cr);
-  LP_CHECK(hipGetLastError());
-}
-
 template <int GM, int S, bool TD>
 static void launch_pf(int g, size_t lds, bool big, hipStream_t st, const uint8_t* text, int64_t nbytes,
                       const PfTables& T, const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
@@ -566,15 +388,6 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
     dispatch_pf<true>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
   else
     dispatch_pf<false>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
-  LP_CHECK(hipGetLastError());
-}
-
-void lines_dev(const int64_t* nl, int64_t n_nl, const uint8_t* text, int64_t nbytes, int64_t* starts, int32_t* lens,
-               unsigned long long* last_nonempty, uint64_t stream) {
-  hipLaunchKernelGGL(k_lines, dim3(num_blocks(n_nl + 1, 256)), dim3(256), 0, as_stream(stream), nl, n_nl, text, nbytes,
-                     starts, lens);
-  LP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_last_nonempty, dim3(1), dim3(256), 0, as_stream(stream), lens, n_nl + 1, last_nonempty);
   LP_CHECK(hipGetLastError());
 }
 

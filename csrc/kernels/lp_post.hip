@@ -117,8 +117,35 @@ __global__ __launch_bounds__(256) void k_pack(const int64_t* __restrict__ cand, 
   keys[i] = ((((k >> 32) << lbits) | (k & 0xFFFFFFFFull)) << 1) | (i >= pre_from ? 1ull : 0ull);
 }
 
+// device-count mode: region 1 (to verify) then region 2 (pre-verified), each a fixed capacity
+// with its used length in a device counter; unused slots become LP_PAD_KEY, which sorts after
+// every real key (bit kbits set; the sort covers one extra bit) and is never a hit
+constexpr uint64_t LP_PAD_KEY = ~0ull;
+
+__global__ __launch_bounds__(256) void k_pack_dc(const int64_t* __restrict__ cand, int64_t cap1,
+                                                 const int64_t* __restrict__ cand2, int64_t cap2,
+                                                 const unsigned long long* __restrict__ dcount, int lbits,
+                                                 uint64_t* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap1 + cap2) return;
+  const int64_t n1 = (int64_t)min((unsigned long long)cap1, dcount[0]);
+  const int64_t n2 = (int64_t)min((unsigned long long)cap2, dcount[1]);
+  uint64_t key = LP_PAD_KEY;
+  const bool pre = i >= cap1;
+  const int64_t j = pre ? i - cap1 : i;
+  if (j < (pre ? n2 : n1)) {
+    const uint64_t k = (uint64_t)(pre ? cand2[j] : cand[j]);
+    key = ((((k >> 32) << lbits) | (k & 0xFFFFFFFFull)) << 1) | (pre ? 1ull : 0ull);
+  }
+  keys[i] = key;
+}
+
 LP_HD bool dedupe_verify_one(const uint64_t* keys, int64_t n, int64_t i, int lbits, const uint8_t* text,
                              const int64_t* ls, const int32_t* ll, const DfaPool& P, int64_t* std_key) {
+  if (keys[i] == LP_PAD_KEY) {
+    *std_key = 0;
+    return false;
+  }
   const uint64_t k = keys[i] >> 1;
   if (i > 0 && (keys[i - 1] >> 1) == k) return false;
   bool pre = false;  // pre-verified copies sort last inside a run
@@ -306,7 +333,8 @@ struct Carve {
 
 size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
-  const int kbits = 1 + A.lbits + A.rbits;
+  const bool dc = A.dcount != nullptr;
+  const int kbits = 1 + A.lbits + A.rbits + (dc ? 1 : 0);    // + the pad bit
   Carve C{static_cast<uint8_t*>(ws)};
   hipStream_t st = pstream(stream);
   uint64_t* kin = C.take<uint64_t>(n);
@@ -326,7 +354,11 @@ size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
     LP_PCHECK(hipMemsetAsync(A.hit_off, 0, (size_t)(A.R + 1) * sizeof(int64_t), st));
     return C.used;
   }
-  hipLaunchKernelGGL(k_pack, dim3(nblk(n)), dim3(256), 0, st, A.cand, n, A.pre_from, A.lbits, kin);
+  if (dc)
+    hipLaunchKernelGGL(k_pack_dc, dim3(nblk(n)), dim3(256), 0, st, A.cand, A.pre_from, A.cand2, n - A.pre_from,
+                       A.dcount, A.lbits, kin);
+  else
+    hipLaunchKernelGGL(k_pack, dim3(nblk(n)), dim3(256), 0, st, A.cand, n, A.pre_from, A.lbits, kin);
   LP_PCHECK(hipGetLastError());
   size_t tb = t_sort;
   LP_PCHECK(rocprim::radix_sort_keys(tmp, tb, kin, kout, (size_t)n, 0, kbits, st));

@@ -48,6 +48,14 @@ namespace lp {
 constexpr int SCAN_THREADS = 1024;   // LDS is per block: more waves per staged byte
 constexpr int SCAN_RUN = 4;
 
+// LDS loads from a 32-bit LDS address. The blob sits at LDS address 0 (the kernel's only LDS is
+// the dynamic blob; checked at entry), so a row offset + a bytemap byte IS the address: one
+// v_add_u32_sdwa (byte select folded in) per group per byte, no base add.
+typedef __attribute__((address_space(3))) const uint16_t lds_u16_t;
+typedef __attribute__((address_space(3))) const uint32_t lds_u32_t;
+__device__ __forceinline__ uint32_t lds_ld16(uint32_t a) { return *(lds_u16_t*)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t a) { return *(lds_u32_t*)(uintptr_t)a; }
+
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t t) {   // high bit of every zero byte of t
   const uint32_t y = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
   return ~(y | t | 0x7F7F7F7Fu);
@@ -156,7 +164,6 @@ template <int G, bool CRLF, typename Emit>
 __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass& S, const uint8_t* text, int64_t p_lo,
                                               int64_t p_end, int64_t x0, int64_t x1,
                                               const int64_t* __restrict__ line_start, Emit&& emit) {
-  const uint8_t* lds = reinterpret_cast<const uint8_t*>(sm);
   uint32_t xr[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
@@ -185,11 +192,11 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
     for (int j = 0; j < 16; ++j) {
       uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
       if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;        // entry 256 + c: hold
-      const uint32_t b = sm[c];
+      const uint32_t b = lds_ld32(c * 4);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         mx[g] = max(mx[g], xr[g]);
-        xr[g] = *reinterpret_cast<const uint16_t*>(lds + xr[g] + ((b >> (8 * g)) & 0xFFu));
+        xr[g] = lds_ld16(xr[g] + ((b >> (8 * g)) & 0xFFu));
       }
     }
     bool hot = false;
@@ -213,6 +220,8 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_multi(const uint8_t* __re
     *reinterpret_cast<uint4*>(sm + i) = *reinterpret_cast<const uint4*>(S.blob + i);
   __syncthreads();
   const GlobalEmit emit{out, cap, count};
+  // the fast walk addresses LDS absolutely (blob at address 0); otherwise every run walks exactly
+  const bool at_zero = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)sm == 0u;
   const int64_t nruns = (nlines + SCAN_RUN - 1) / SCAN_RUN;
   const int64_t stride = (int64_t)gridDim.x * SCAN_THREADS;
   for (int64_t run = (int64_t)blockIdx.x * SCAN_THREADS + threadIdx.x; run < nruns; run += stride) {
@@ -241,6 +250,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan_multi(const uint8_t* __re
       p_end = st + n + sep;                      // after the last line's separator
     }
     if (p_lo > 0 && text[p_lo - 1] != '\n') fast = false;   // e.g. a document boundary in a batch
+    if (!at_zero) fast = false;
     if (!fast) {     // rare: exact per-line walks
       for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
       continue;

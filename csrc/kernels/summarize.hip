@@ -2,7 +2,7 @@
 // AnalysisService.java:188-215 -- event count, severity histogram, highest severity -- plus the
 // north star's top-k event reduction), and the streaming mode's final re-score.
 //
-//   k_summ_level  one block per 2048-item chunk: the chunk is bitonic-sorted in LDS by
+//   k_summ_level  one block per 4096-item chunk: the chunk is bitonic-sorted in LDS by
 //                 (score desc, global line asc, pattern asc) -- a total, deterministic order, so
 //                 every rank / run agrees on ties -- and its first k rows are written out. Level
 //                 0 reads events (and adds them to the pattern / severity histograms with one
@@ -24,8 +24,9 @@
 
 namespace lp {
 
-constexpr int SUMM_THREADS = 256;
-constexpr int SUMM_CHUNK = 2048;
+constexpr int SUMM_THREADS = 1024;
+constexpr int SUMM_CHUNK = 4096;
+constexpr int SUMM_LDS_SEV = 256;             // severity histogram in LDS up to this many names
 
 struct Row {
   double score;
@@ -41,12 +42,50 @@ LP_HD bool row_before(const Row& a, const Row& b) {      // a sorts before b
 
 LP_HD Row empty_row() { return Row{-INFINITY, -1, -1}; }
 
-__global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t n, int k, double* __restrict__ rows_out,
+// A row as one 128-bit key whose ASCENDING unsigned order is the row order: hi = the score's
+// order-preserving bit pattern, inverted (higher score first), lo = line << 24 | pattern.
+struct Key {
+  uint64_t hi, lo;
+};
+
+__device__ __forceinline__ Key row_key(const Row& r) {
+  uint64_t b;
+  __builtin_memcpy(&b, &r.score, 8);
+  const uint64_t ord = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+  return Key{~ord, r.line < 0 ? ~0ull : ((uint64_t)r.line << 24) | (uint64_t)(uint32_t)r.pat};
+}
+
+__device__ __forceinline__ Row key_row(const Key& k) {
+  const uint64_t ord = ~k.hi;
+  const uint64_t b = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
+  Row r;
+  __builtin_memcpy(&r.score, &b, 8);
+  if (k.lo == ~0ull) {
+    r.line = -1;
+    r.pat = -1;
+  } else {
+    r.line = (int64_t)(k.lo >> 24);
+    r.pat = (int32_t)(k.lo & 0xFFFFFFull);
+  }
+  return r;
+}
+
+__device__ __forceinline__ bool key_less(const Key& a, const Key& b) {
+  return a.hi != b.hi ? a.hi < b.hi : a.lo < b.lo;
+}
+
+// One 4096-row chunk per 1024-thread block: load (+ histograms, + packed event records), bitonic
+// sort of 128-bit keys in LDS (one compare-exchange per thread per stage pair), write the first k.
+__global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t n, int k, int nsev,
+                                                             double* __restrict__ rows_out,
                                                              unsigned long long* __restrict__ pat_hist,
                                                              unsigned long long* __restrict__ sev_hist) {
-  __shared__ double s_score[SUMM_CHUNK];
-  __shared__ int64_t s_line[SUMM_CHUNK];
-  __shared__ int32_t s_pat[SUMM_CHUNK];
+  __shared__ Key s_key[SUMM_CHUNK];
+  __shared__ unsigned int s_sev[SUMM_LDS_SEV];
+  const bool lds_sev = sev_hist && nsev <= SUMM_LDS_SEV;
+  if (lds_sev)
+    for (int j = threadIdx.x; j < nsev; j += SUMM_THREADS) s_sev[j] = 0;
+  __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * SUMM_CHUNK;
   const int64_t add = in.line_add ? *in.line_add : 0;
   for (int j = threadIdx.x; j < SUMM_CHUNK; j += SUMM_THREADS) {
@@ -60,25 +99,39 @@ __global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t 
         r.line = (in.line64 ? in.line64[i] : (int64_t)in.line32[i]) + add;
         r.pat = in.pat[i];
         if (pat_hist) atomicAdd(pat_hist + r.pat, 1ull);
-        if (sev_hist) atomicAdd(sev_hist + in.sev_of_pat[r.pat], 1ull);
+        if (sev_hist) {
+          const int sv = in.sev_of_pat[r.pat];
+          if (lds_sev)
+            atomicAdd(s_sev + sv, 1u);
+          else
+            atomicAdd(sev_hist + sv, 1ull);
+        }
+        if (in.ev_out) {                      // every event record, packed for one D2H copy
+          reinterpret_cast<int64_t*>(in.ev_out)[i] = r.line;
+          reinterpret_cast<double*>(in.ev_out)[n + i] = r.score;
+          reinterpret_cast<int32_t*>(in.ev_out)[4 * n + i] = r.pat;
+        }
       }
     }
-    s_score[j] = r.score;
-    s_line[j] = r.line;
-    s_pat[j] = r.pat;
+    s_key[j] = row_key(r);
   }
   __syncthreads();
-  // bitonic sort of the chunk, descending in row order
+  if (lds_sev)
+    for (int j = threadIdx.x; j < nsev; j += SUMM_THREADS)
+      if (s_sev[j]) atomicAdd(sev_hist + j, (unsigned long long)s_sev[j]);
+  // bitonic sort, ascending key order = row order
   for (int size = 2; size <= SUMM_CHUNK; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < SUMM_CHUNK / 2; t += SUMM_THREADS) {
+#pragma unroll
+      for (int q = 0; q < SUMM_CHUNK / 2 / SUMM_THREADS; ++q) {
+        const int t = threadIdx.x + q * SUMM_THREADS;
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
-        const bool up = (lo & size) == 0;             // this half keeps row order
-        const Row a{s_score[lo], s_line[lo], s_pat[lo]}, b{s_score[hi], s_line[hi], s_pat[hi]};
-        if (row_before(b, a) == up) {
-          s_score[lo] = b.score; s_line[lo] = b.line; s_pat[lo] = b.pat;
-          s_score[hi] = a.score; s_line[hi] = a.line; s_pat[hi] = a.pat;
+        const bool up = (lo & size) == 0;
+        const Key a = s_key[lo], b = s_key[hi];
+        if (key_less(b, a) == up) {
+          s_key[lo] = b;
+          s_key[hi] = a;
         }
       }
       __syncthreads();
@@ -86,9 +139,10 @@ __global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t 
   }
   double* o = rows_out + (int64_t)blockIdx.x * k * 3;
   for (int j = threadIdx.x; j < k; j += SUMM_THREADS) {
-    o[3 * j] = s_score[j];
-    o[3 * j + 1] = (double)s_line[j];
-    o[3 * j + 2] = (double)s_pat[j];
+    const Row r = key_row(s_key[j]);
+    o[3 * j] = r.score;
+    o[3 * j + 1] = (double)r.line;
+    o[3 * j + 2] = (double)r.pat;
   }
 }
 
@@ -105,7 +159,7 @@ static void check(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in " + what);
 }
 
-size_t summarize_dev(const SummIn& in, int64_t n, int k, double* top_rows, unsigned long long* pat_hist,
+size_t summarize_dev(const SummIn& in, int64_t n, int k, int nsev, double* top_rows, unsigned long long* pat_hist,
                      unsigned long long* sev_hist, void* ws, size_t ws_bytes, uint64_t stream) {
   if (k < 1 || k > SUMM_CHUNK / 2) throw std::runtime_error("summarize: 1 <= k <= 1024");
   // workspace: two ping-pong row buffers sized for level 0
@@ -120,7 +174,7 @@ size_t summarize_dev(const SummIn& in, int64_t n, int k, double* top_rows, unsig
   int which = 0;
   for (int level = 0;; ++level) {
     double* dst = nb == 1 ? top_rows : buf[which];
-    hipLaunchKernelGGL(k_summ_level, dim3((unsigned)nb), dim3(SUMM_THREADS), 0, st, cur, m, k, dst,
+    hipLaunchKernelGGL(k_summ_level, dim3((unsigned)nb), dim3(SUMM_THREADS), 0, st, cur, m, k, nsev, dst,
                        level == 0 ? pat_hist : nullptr, level == 0 ? sev_hist : nullptr);
     check("k_summ_level");
     if (nb == 1) break;
@@ -143,6 +197,11 @@ void summarize_host(const SummIn& in, int64_t n, int k, double* top_rows, int64_
       continue;
     }
     rows[i] = Row{in.score[i], (in.line64 ? in.line64[i] : (int64_t)in.line32[i]) + add, in.pat[i]};
+    if (in.ev_out) {
+      reinterpret_cast<int64_t*>(in.ev_out)[i] = rows[i].line;
+      reinterpret_cast<double*>(in.ev_out)[n + i] = rows[i].score;
+      reinterpret_cast<int32_t*>(in.ev_out)[4 * n + i] = rows[i].pat;
+    }
     if (pat_hist) ++pat_hist[in.pat[i]];
     if (sev_hist) ++sev_hist[in.sev_of_pat[in.pat[i]]];
   }

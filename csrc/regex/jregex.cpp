@@ -189,6 +189,9 @@ class Parser {
       int lead = mk_set(b);
       // at most 3 continuation bytes in valid UTF-8; the bound keeps lookbehind lengths finite
       int tail = mk_rep(mk_set(cont), 0, bt_ ? 3 : -1);
+      if (bt_) {   // a code point is indivisible: backtracking must not give its bytes back
+        Node n; n.t = N_ATOMIC; n.kids = {tail}; tail = add(n);
+      }
       return mk_cat({lead, tail});
     }
     std::vector<int> alts;
@@ -1347,14 +1350,16 @@ struct BtCompiler {
       }
       case N_REP: {
         for (int k = 0; k < n.lo; ++k) comp(p, n.kids[0]);
-        if (n.hi < 0) {                          // loop; an empty iteration may not repeat
+        if (n.hi < 0) {   // loop; an empty iteration ends it (keeping its captures), as Java's Loop
           const int m = I.nmarks++;
           const int sp = emit(p, BInst{B_SPLIT});
           BInst mk{B_MARK}; mk.x = m; emit(p, mk);
           comp(p, n.kids[0]);
-          BInst pr{B_PROGRESS}; pr.x = m; emit(p, pr);
+          BInst pr{B_PROGRESS}; pr.x = m;
+          const int pi = emit(p, pr);
           BInst j{B_JMP}; j.x = sp; emit(p, j);
           const int out = (int)I.progs[p].size();
+          I.progs[p][pi].y = out;
           I.progs[p][sp].x = n.lazy ? out : sp + 1;
           I.progs[p][sp].y = n.lazy ? sp + 1 : out;
         } else {
@@ -1474,7 +1479,7 @@ struct BtRun {
         case B_JMP: pc = in.x; break;
         case B_SAVE: st.push_back({1, in.x, caps[in.x]}); caps[in.x] = pos; ++pc; break;
         case B_MARK: st.push_back({2, in.x, marks[in.x]}); marks[in.x] = pos; ++pc; break;
-        case B_PROGRESS: if (pos == marks[in.x]) ok = false; else ++pc; break;
+        case B_PROGRESS: pc = pos == marks[in.x] ? in.y : pc + 1; break;
         case B_ASSERT: if (ctx_bit(pos) & in.cond) ++pc; else ok = false; break;
         case B_ML: if (ml_anchor(in, pos)) ++pc; else ok = false; break;
         case B_BREF: {

@@ -28,6 +28,8 @@ SOURCES = [
     ("kernels/scan_multi.hip", "hip"),
     ("kernels/freq_state.hip", "hip"),
     ("kernels/summarize.hip", "hip"),
+    ("kernels/line_index.hip", "hip"),
+    ("kernels/dp_glue.hip", "hip"),
     ("kernels/lp_post.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),

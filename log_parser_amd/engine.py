@@ -68,10 +68,14 @@ class Segments:
     n: torch.Tensor
 
     @staticmethod
-    def scalar(lo: int, hi: int, own_lo: int, own_hi: int, g0: int, n: int, device) -> "Segments":
-        """One segment (two small host->device copies instead of six)."""
-        t32 = torch.tensor([lo, hi, own_lo, own_hi], dtype=torch.int32, device=device)
-        t64 = torch.tensor([g0, n], dtype=torch.int64, device=device)
+    def scalar(lo: int, hi: int, own_lo: int, own_hi: int, g0: int, n: int, device, upload=None) -> "Segments":
+        """One segment (two small host->device copies instead of six; with an engine's
+        ``upload``, one async copy through its pinned buffer)."""
+        if upload is not None:
+            t32, t64 = upload([np.array([lo, hi, own_lo, own_hi], np.int32), np.array([g0, n], np.int64)])
+        else:
+            t32 = torch.tensor([lo, hi, own_lo, own_hi], dtype=torch.int32, device=device)
+            t64 = torch.tensor([g0, n], dtype=torch.int64, device=device)
         return Segments(t32[0:1], t32[1:2], t32[2:3], t32[3:4], t64[0:1], t64[1:2])
 
     @staticmethod
@@ -289,6 +293,7 @@ class Engine:
         self._batches = 0
         self.tabs = library.device_tables(self.device)
         self.ws = K.Workspace(self.device)          # post-match pipeline scratch (grow-only)
+        self.arena = K.MatchArena()                 # matcher output capacities (GPU, adaptive)
         self.upload = K.Uploader(self.device)       # batch line index / segments / carry: one H2D
         self.sp_tuple = self.score_param_tuple(self.params)
         self._pinned: Optional[torch.Tensor] = None
@@ -461,11 +466,18 @@ class Engine:
         """
         timings = {} if timings is None else timings
         L = ls.numel()
-        cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
         t = 0.0
         evt = self._ev_tables(segs)
-        hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(
-            cand, pre, L, self.lib.n_regexes, text, ls, ll, self.tabs["dfa"], evt, self.ws)
+        if text.is_cuda and not self.lib.host_regs:
+            # every matcher appends to fixed-capacity device buffers; ONE host read after the CSR
+            self._start(timings)
+            hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
+                text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
+                self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None)
+        else:
+            cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
+            hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(
+                cand, pre, L, self.lib.n_regexes, text, ls, ll, self.tabs["dfa"], evt, self.ws)
         t = self._tick(timings, "verify_csr", t)
         nkeys = len(self.lib.freq_ids)
         dfa_feats = self.context_engine != "mfma"

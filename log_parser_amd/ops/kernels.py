@@ -29,47 +29,82 @@ def padded_len(nbytes: int) -> int:
     return ((max(nbytes, 1) + NL_TILE - 1) // NL_TILE) * NL_TILE + TEXT_PAD
 
 
-def newline_positions(text: torch.Tensor, nbytes: int, flag_cr: bool = False) -> torch.Tensor:
-    """Positions of every '\\n' in text[0:nbytes] (int64, ascending). ``flag_cr`` (device only):
-    bit 62 marks a '\\n' preceded by '\\r' -- the input format of ``lines_dev``."""
-    if text.is_cuda:
-        nb = N.nl_tiles(nbytes)
-        if nb == 0:
-            return torch.empty(0, dtype=torch.int64, device=text.device)
-        cnt = torch.empty(nb, dtype=torch.int32, device=text.device)
-        N.nl_count_dev(text.data_ptr(), nbytes, cnt.data_ptr(), _s(text))
-        off = torch.cumsum(cnt, 0, dtype=torch.int64)
-        total = int(off[-1].item())
-        off = off - cnt.to(torch.int64)
-        pos = torch.empty(total, dtype=torch.int64, device=text.device)
-        N.nl_write_dev(text.data_ptr(), nbytes, off.data_ptr(), pos.data_ptr(), int(flag_cr), _s(text))
-        return pos
+def newline_positions(text: torch.Tensor, nbytes: int) -> torch.Tensor:
+    """Positions of every '\\n' in text[0:nbytes] (int64, ascending; host twin)."""
     c = N.nl_positions_host(text.data_ptr(), nbytes, 0)
     pos = torch.empty(c, dtype=torch.int64)
     N.nl_positions_host(text.data_ptr(), nbytes, pos.data_ptr())
     return pos
 
 
+class _LineIndexWs:
+    """Per (device, stream) scratch of the line index: tile counts + offsets and each tile's first
+    line end (k_line_fix), then the scan scratch. Grow-only; stream order makes reuse safe."""
+    SCAN_TMP = 1 << 20           # bytes of rocprim scan scratch (csrc/bind.cpp passes the same)
+    _all: dict = {}
+
+    @classmethod
+    def get(cls, text: torch.Tensor, ntiles: int) -> Tuple[int, int]:
+        key = (text.device, _s(text))
+        buf = cls._all.get(key)
+        if buf is None or buf.numel() < 4 * ntiles + cls.SCAN_TMP // 8:
+            cap = max(ntiles * 5 // 4, 1024)
+            buf = cls._all[key] = torch.empty(4 * cap + cls.SCAN_TMP // 8, dtype=torch.int64, device=text.device)
+        return buf.data_ptr(), (buf.numel() - cls.SCAN_TMP // 8) // 4
+
+
+# lines per byte seen so far (grows only): capacity of the line index outputs, so the one-pass
+# kernel rarely needs a second pass; a text with more lines than that re-runs with the exact count
+_LINES_PER_BYTE = [1.0 / 48]
+LINE_BLK_SHIFT = 12
+
+
+def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool):
+    """k_nl_count, rocprim scan, k_nl_lines, k_line_fix (+ k_line_trim): (starts, lens, n_newlines,
+    last_newline, kept, blk) with ONE host read; blk = the coarse 4 KiB block -> line index."""
+    dev = text.device
+    nt = N.line_index_tiles(nbytes)
+    cap = int(nbytes * _LINES_PER_BYTE[0] * 1.25) + 1024
+    blk = torch.empty((max(nbytes, 1) >> LINE_BLK_SHIFT) + 2, dtype=torch.int32, device=dev)
+    while True:
+        cap = min(cap, nbytes + 1)
+        starts = torch.empty(cap, dtype=torch.int64, device=dev)
+        lens = torch.empty(cap, dtype=torch.int32, device=dev)
+        info = torch.empty(3, dtype=torch.int64, device=dev)
+        wp, wcap = _LineIndexWs.get(text, nt)
+        N.line_index_dev(text.data_ptr(), nbytes, wp, wcap, starts.data_ptr(), lens.data_ptr(), cap, info.data_ptr(),
+                         trim, blk.data_ptr(), blk.numel(), _s(text))
+        n_nl, last, kept = info.tolist()
+        if n_nl + 1 <= cap:
+            _LINES_PER_BYTE[0] = max(_LINES_PER_BYTE[0], (n_nl + 1) / max(nbytes, 1))
+            return starts, lens, n_nl, last, kept, blk
+        cap = n_nl + 1
+
+
+def _with_blk(ls: torch.Tensor, blk: torch.Tensor, nbytes: int) -> torch.Tensor:
+    """Attach the coarse block index to the line-start tensor the caller gets (reused by
+    ``line_block_index`` for the same object; any other tensor recomputes it)."""
+    ls._lp_blk = (blk, nbytes)
+    return ls
+
+
 def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Tensor]:
     """Java ``logs.split("\\\\r?\\\\n")`` line index (AnalysisService.java:53).
 
     Returns (line_start int64[L], line_len int32[L]); trailing empty lines removed; input
-    without any newline is one line (possibly empty).
+    without any newline is one line (possibly empty). GPU: two reads of the text, five small
+    launches, one 24-byte host read (csrc/kernels/line_index.hip).
     """
     dev = text.device
-    nl = newline_positions(text, nbytes, flag_cr=text.is_cuda)
+    if text.is_cuda:
+        if nbytes == 0:
+            return torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
+        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True)
+        return _with_blk(starts[:L], blk, nbytes), lens[:L]
+    nl = newline_positions(text, nbytes)
     if nl.numel() == 0:
         return (torch.zeros(1, dtype=torch.int64, device=dev),
                 torch.full((1,), nbytes, dtype=torch.int32, device=dev))
-    if text.is_cuda:                       # k_lines (CR flags from k_nl_write) + k_last_nonempty
-        n = nl.numel()
-        starts = torch.empty(n + 1, dtype=torch.int64, device=dev)
-        lens = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        last = torch.zeros(1, dtype=torch.int64, device=dev)
-        N.lines_dev(nl.data_ptr(), n, text.data_ptr(), nbytes, starts.data_ptr(), lens.data_ptr(), last.data_ptr(),
-                    _s(text))
-        L = int(last.item())
-        return starts[:L], lens[:L]
     zero = torch.zeros(1, dtype=torch.int64, device=dev)
     starts = torch.cat([zero, nl + 1])
     ends = torch.cat([nl, torch.full((1,), nbytes, dtype=torch.int64, device=dev)])
@@ -86,7 +121,11 @@ def split_chunk_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, to
     """Line index of a chunk made of complete lines (streaming): no trailing-empty trimming; a
     final '\\n' terminates the last line instead of opening an empty one."""
     dev = text.device
-    nl = newline_positions(text, nbytes)
+    if text.is_cuda and nbytes > 0:
+        starts, lens, n_nl, last, _, blk = _line_index_dev(text, nbytes, trim=False)
+        L = n_nl + 1 - (1 if n_nl and last == nbytes - 1 else 0)
+        return _with_blk(starts[:L], blk, nbytes), lens[:L]
+    nl = newline_positions(text.cpu(), nbytes).to(dev)
     zero = torch.zeros(1, dtype=torch.int64, device=dev)
     starts = torch.cat([zero, nl + 1])
     ends = torch.cat([nl, torch.full((1,), nbytes, dtype=torch.int64, device=dev)])
@@ -100,11 +139,14 @@ def split_chunk_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, to
     return starts[:L].contiguous(), (ends - starts)[:L].to(torch.int32).contiguous()
 
 
-LINE_BLK_SHIFT = 12
 
 
 def line_block_index(line_start: torch.Tensor, nbytes: int) -> torch.Tensor:
-    """blk[b] = line containing byte b << 12 (int32), for O(log lines-per-4KiB) line lookups."""
+    """blk[b] = line containing byte b << 12 (int32), for O(log lines-per-4KiB) line lookups
+    (already built by the GPU line index for the tensors ``split_lines`` returns)."""
+    cached = getattr(line_start, "_lp_blk", None)
+    if cached is not None and cached[1] == nbytes:
+        return cached[0]
     nblk = (max(nbytes, 1) >> LINE_BLK_SHIFT) + 2
     blk = torch.empty(nblk, dtype=torch.int32, device=line_start.device)
     N.blk_index(line_start.data_ptr(), line_start.numel(), nblk, blk.data_ptr(), _s(line_start), line_start.is_cuda)
@@ -312,7 +354,7 @@ def post_hits(cand: torch.Tensor, pre_from: int, L: int, R: int, text, line_star
         return N.post_hits(cand.data_ptr(), n, pre_from, lbits, rbits, R, text.data_ptr(), line_start.data_ptr(),
                            line_len.data_ptr(), dfa_tuple, evt, hits.data_ptr(), hit_line.data_ptr(),
                            hit_off.data_ptr(), ev_cnt.data_ptr(), ev_end.data_ptr(), counters.data_ptr(), wp, wn,
-                           _s(cand), cand.is_cuda)
+                           _s(cand), cand.is_cuda, 0, 0)
 
     if cand.is_cuda:
         _run_ws(call, ws)
@@ -322,6 +364,85 @@ def post_hits(cand: torch.Tensor, pre_from: int, L: int, R: int, text, line_star
         c = counters
     nh, ne = int(c[0]), int(c[1])
     return hits[:nh], hit_line, hit_off, ev_cnt, ev_end, nh, ne
+
+
+class MatchArena:
+    """Fixed-capacity device buffers of every matcher of one batch + their append counters
+    (GPU): gram hits (k_prefilter), prefilter candidates (k_pf_verify), verified hits of the
+    self-verifying engines (scan passes, single-DFA scan, MFMA NFA). Nothing is read back until
+    the hit CSR is built, so matching + verify + CSR + event count cost ONE host read
+    (``match_and_hits``); capacities follow the largest per-line rates seen so far, and a batch
+    that overflows one re-runs with its exact counts."""
+
+    def __init__(self):
+        self.rate = {"gram": 0.2, "cand": 0.1, "ver": 1.0 / 16}
+
+    def caps(self, L: int) -> dict:
+        return {k: int(L * r * 1.25) + 512 for k, r in self.rate.items()}
+
+    def learn(self, L: int, counts: dict, overflow: bool) -> None:
+        """Overflow: the exact rates. Otherwise decay toward what batches need (the hit sort
+        covers the whole capacity, so slack costs sort time)."""
+        for k, c in counts.items():
+            r = c / max(L, 1)
+            self.rate[k] = max(r, self.rate[k] if overflow else self.rate[k] * 0.9, 1e-4)
+
+
+def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
+                   ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None):
+    """GPU: every matcher appends to the arena, then the post-match hit pipeline reads the device
+    counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read."""
+    dev = text.device
+    L = line_start.numel()
+    st = _s(text)
+    blk = line_block_index(line_start, nbytes)
+    lbits, rbits = N.bits_for(max(L, 1)), N.bits_for(max(R, 1))
+    while True:
+        cap = arena.caps(L)
+        gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
+        cand = torch.empty(cap["cand"], dtype=torch.int64, device=dev)
+        ver = torch.empty(cap["ver"], dtype=torch.int64, device=dev)
+        # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters)
+        cnt = torch.zeros(5, dtype=torch.int64, device=dev)
+        c0 = cnt.data_ptr()
+        N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L, gh.data_ptr(), cap["gram"],
+                        c0, pf_grid, st)
+        N.pf_verify_dev(gh.data_ptr(), cap["gram"], text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L,
+                        blk.data_ptr(), cand.data_ptr(), cap["cand"], c0 + 8, st, c0,
+                        max(16, min(8192, nbytes >> 13)))
+        if tick:
+            tick("prefilter")
+        for sp in tabs["scan_passes"]:
+            N.scan_multi(text.data_ptr(), nbytes, line_start.data_ptr(), line_len.data_ptr(), L, sp, ver.data_ptr(),
+                         cap["ver"], c0 + 16, scan_grid(sp), st, True)
+        if tabs["scan_regs"].numel():
+            N.scan_dev(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), L, tabs["scan_regs"].data_ptr(),
+                       tabs["scan_regs"].numel(), tabs["dfa"], ver.data_ptr(), cap["ver"], c0 + 16, st)
+        for ncls, glist in tabs["nfa_scan_lists"].items():
+            if glist.numel():
+                N.nfa(tabs["nfa_tables"].data_ptr(), glist.data_ptr(), glist.numel(), ncls, 0, L, text.data_ptr(),
+                      line_start.data_ptr(), line_len.data_ptr(), 0, ver.data_ptr(), cap["ver"], c0 + 16, st, True)
+        if tick:
+            tick("scan")
+        n = cap["cand"] + cap["ver"]
+        hits = torch.empty(n, dtype=torch.int64, device=dev)
+        hit_line = torch.empty(n, dtype=torch.int32, device=dev)
+        hit_off = torch.empty(R + 1, dtype=torch.int64, device=dev)
+        ev_cnt = torch.empty(n, dtype=torch.int64, device=dev)
+        ev_end = torch.empty(n, dtype=torch.int64, device=dev)
+
+        def call(wp, wn):
+            return N.post_hits(cand.data_ptr(), n, cap["cand"], lbits, rbits, R, text.data_ptr(),
+                               line_start.data_ptr(), line_len.data_ptr(), tabs["dfa"], evt, hits.data_ptr(),
+                               hit_line.data_ptr(), hit_off.data_ptr(), ev_cnt.data_ptr(), ev_end.data_ptr(),
+                               c0 + 24, wp, wn, st, True, ver.data_ptr(), c0 + 8)
+
+        _run_ws(call, ws)
+        g, k, v, nh, ne = cnt.tolist()                 # the one host read
+        ok = g <= cap["gram"] and k <= cap["cand"] and v <= cap["ver"]
+        arena.learn(L, {"gram": g, "cand": k, "ver": v}, overflow=not ok)
+        if ok:
+            return hits[:nh], hit_line, hit_off, ev_cnt, ev_end, nh, ne
 
 
 def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text, line_start, line_len, dfa_tuple,
@@ -360,34 +481,67 @@ SUMMARY_MAX_K = 1024
 
 
 def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int, sev_index: torch.Tensor,
-              npat: int, nsev: int, line_add: Optional[torch.Tensor] = None, ws: Optional[Workspace] = None):
+              npat: int, nsev: int, line_add: Optional[torch.Tensor] = None, ws: Optional[Workspace] = None,
+              pack_events: bool = False, hist_out: Optional[torch.Tensor] = None):
     """Top-k rows + histograms of scored events (csrc/kernels/summarize.hip).
 
     ``line`` is int32 (local, plus the device scalar ``line_add``) or int64 (global);
     ``sev_index[p]`` is pattern p's index into the library's distinct severity names. Returns
     (rows float64[k, 3] = (score, global line, pattern) ordered score desc, line asc, pattern asc,
-    missing rows = (-inf, -1, -1); pat_hist int64[npat]; sev_hist int64[nsev]). No host sync."""
+    missing rows = (-inf, -1, -1); pat_hist int64[npat]; sev_hist int64[nsev]; packed) where
+    ``packed`` (with ``pack_events``) is every event as uint8[20 n] = [global line int64 x n |
+    score f64 x n | pattern int32 x n], written by the same kernel. No host sync."""
     dev = score.device
     k = max(1, min(int(k), SUMMARY_MAX_K))
     n = score.numel()
     rows = torch.empty((k, 3), dtype=torch.float64, device=dev)
-    pat_hist = torch.zeros(max(npat, 1), dtype=torch.int64, device=dev)
-    sev_hist = torch.zeros(max(nsev, 1), dtype=torch.int64, device=dev)
+    if hist_out is not None:           # zeroed by the caller: [pattern hist | severity hist | ...]
+        pat_hist, sev_hist = hist_out[:npat], hist_out[npat:npat + nsev]
+    else:
+        hist = torch.zeros(npat + nsev + 1, dtype=torch.int64, device=dev)
+        pat_hist, sev_hist = hist[:npat], hist[npat:npat + nsev]
+    packed = torch.empty(20 * n, dtype=torch.uint8, device=dev) if pack_events else None
     sev_of_pat = sev_index
     l32 = line.data_ptr() if line.dtype == torch.int32 else 0
     l64 = line.data_ptr() if line.dtype == torch.int64 else 0
     ins = (score.data_ptr() if n else 0, pat.data_ptr() if n else 0, l32 if n else 0, l64 if n else 0,
-           _p(line_add), sev_of_pat.data_ptr(), 0)
+           _p(line_add), sev_of_pat.data_ptr(), 0, _p(packed) if n else 0)
 
     def call(wp, wn):
-        return N.summarize(ins, n, k, rows.data_ptr(), pat_hist.data_ptr(), sev_hist.data_ptr(), wp, wn, _s(score),
+        return N.summarize(ins, n, k, nsev, rows.data_ptr(), pat_hist.data_ptr(), sev_hist.data_ptr(), wp, wn, _s(score),
                            score.is_cuda)
 
     if score.is_cuda:
         _run_ws(call, ws if ws is not None else Workspace(dev))
     else:
         call(0, 0)
-    return rows, pat_hist[:npat], sev_hist[:nsev]
+    return rows, pat_hist[:npat], sev_hist[:nsev], packed
+
+
+def dp_pack(own_lines: int, freq_counts: torch.Tensor, nk: int, chain: torch.Tensor) -> torch.Tensor:
+    """C1+C3+C4 all-gather payload [owned lines | nk frequency counts | chain table] (int64)."""
+    ns = chain.numel()
+    pack = torch.empty(1 + nk + ns, dtype=torch.int64, device=chain.device)
+    fc = freq_counts if freq_counts.dtype == torch.int64 else freq_counts.to(torch.int64)
+    N.dp_pack(int(own_lines), fc.data_ptr(), nk, chain.data_ptr(), ns, pack.data_ptr(), _s(chain), chain.is_cuda)
+    return pack
+
+
+def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: Optional[torch.Tensor],
+             slot_e0: torch.Tensor, slot_k: torch.Tensor, red_tail: Optional[torch.Tensor] = None):
+    """From the gathered payloads: (own_start[1], g0[1], n[1], carry[nk], seq_carry uint8[ns]);
+    ``red_tail`` (optional) receives this rank's frequency counts."""
+    dev = g.device
+    sc = torch.empty(5, dtype=torch.int64, device=dev)          # own_start, g0, n (+ pad)
+    carry = torch.empty(max(nk, 1), dtype=torch.int64, device=dev)
+    if nk == 0:
+        carry.zero_()
+    seq = torch.empty(max(ns, 1), dtype=torch.uint8, device=dev)
+    g = g.contiguous()
+    p = sc.data_ptr()
+    N.dp_carry((g.data_ptr(), g.shape[0], rank, nk, ns, int(halo_left), _p(tot) if nk else 0, slot_e0.data_ptr(),
+                slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail)), _s(g), g.is_cuda)
+    return sc[0:1], sc[1:2], sc[2:3], carry, seq
 
 
 def topk_rows(rows: torch.Tensor, k: int, ws: Optional[Workspace] = None) -> torch.Tensor:
@@ -399,7 +553,7 @@ def topk_rows(rows: torch.Tensor, k: int, ws: Optional[Workspace] = None) -> tor
     ins = (0, 0, 0, 0, 0, 0, rows.data_ptr())
 
     def call(wp, wn):
-        return N.summarize(ins, rows.shape[0], k, out.data_ptr(), 0, 0, wp, wn, _s(rows), rows.is_cuda)
+        return N.summarize(ins, rows.shape[0], k, 0, out.data_ptr(), 0, 0, wp, wn, _s(rows), rows.is_cuda)
 
     if rows.is_cuda:
         _run_ws(call, ws if ws is not None else Workspace(dev))

@@ -91,6 +91,8 @@ class StepOutput:
     topk_rows: Optional[torch.Tensor] = None
     own_lo: int = 0                                 # first owned local line (= left halo lines)
     own_start_dev: Optional[torch.Tensor] = None    # [1] global index of the first owned line
+    # pack_events: every owned event as uint8[20 n] = [global line i64 | score f64 | pattern i32]
+    events_packed: Optional[torch.Tensor] = None
 
     # host integers on demand (a host read here would stall the step's launch queue)
     @property
@@ -137,51 +139,40 @@ class ShardedAnalyzer:
         self.slot_e0 = torch.from_numpy(e0).to(dev)
         self.slot_k = torch.from_numpy(kk).to(dev)
 
-    def _compose_chain(self, chains: torch.Tensor, rank: int) -> torch.Tensor:
-        """carry[j] = 1 iff the chain needing events k..0 completes in ranks < rank."""
-        k = self.slot_k.clone()
-        for q in range(rank - 1, -1, -1):
-            idx = self.slot_e0 + k.clamp(min=0)
-            nk = chains[q].to(torch.int64)[idx]
-            k = torch.where(k >= 0, nk, k)
-        return (k < 0).to(torch.uint8)
-
     def step(self, text: torch.Tensor, nbytes: int, ls: torch.Tensor, ll: torch.Tensor,
-             halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False) -> StepOutput:
+             halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False,
+             pack_events: bool = False) -> StepOutput:
         eng = self.engine
         lib = eng.lib
         rank, wsize = world()
         dev = text.device
         L = ls.numel()
         own_lo, own_hi = halo_left, L - halo_right
-        segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev)
+        segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev, upload=eng.upload)
         prep = eng.prepare(text, nbytes, ls, ll, segs)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
-        pack = torch.cat([segs.own_hi.to(torch.int64) - own_lo, prep.freq_counts[:nk].to(torch.int64),
-                          chain.to(torch.int64)])
+        pack = K.dp_pack(own_hi - own_lo, prep.freq_counts, nk, chain)         # k_dp_pack
         g = all_gather_rows(pack, self.group)                      # C1 + C3 + C4 in one collective
         own_counts = g[:, 0]
-        own_start = own_counts[:rank].sum(0, keepdim=True)        # device scalars: no host round trip
-        carry = eng.freq_carry()
-        if nk:
-            carry = carry + g[:rank, 1:1 + nk].sum(0)
-        seq_carry = self._compose_chain(g[:, 1 + nk:].to(torch.int32), rank)
-        segs.g0 = own_start - halo_left
-        segs.n = own_counts.sum(0, keepdim=True).clamp(min=1)
+        # the all-reduce buffer [pattern hist | severity hist | frequency counts]: k_dp_carry seeds
+        # the counts, the summary kernel accumulates the histograms
+        P, S = len(lib.patterns), len(lib.sev_names)
+        red = torch.zeros(P + S + nk, dtype=torch.int64, device=dev)
+        own_start, segs.g0, segs.n, carry, seq_carry = K.dp_carry(     # k_dp_carry: device scalars, no sync
+            g, rank, nk, chain.numel(), halo_left, eng.freq_carry() if nk else None, self.slot_e0, self.slot_k,
+            red_tail=red[P + S:] if nk else None)
         res = eng.finish(prep, segs, carry, seq_carry, with_factors)
         # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
         # rank's top-k rows with global line numbers, no host sync), then ONE all-reduce for the
         # histograms + frequency counts and one all-gather of k rows
-        P, S = len(lib.patterns), len(lib.sev_names)
         k = max(1, min(topk, K.SUMMARY_MAX_K))
-        rows, pc, sc = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
-                                   line_add=segs.g0, ws=eng.ws)
-        red = torch.cat([pc, sc, prep.freq_counts[:nk].to(torch.int64)])
+        rows, _, _, packed = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
+                                         line_add=segs.g0, ws=eng.ws, pack_events=pack_events, hist_out=red)
         red = all_reduce_sum(red, self.group)
         eng.commit_frequency(red[P + S:])
         out = StepOutput(res, own_counts, rank, red[:P], severity_counts=red[P:P + S], own_lo=own_lo,
-                         own_start_dev=own_start)
+                         own_start_dev=own_start, events_packed=packed)
         if topk > 0:
             allrows = all_gather_rows(rows.flatten(), self.group).view(-1, 3)
             if rank == 0:

@@ -334,7 +334,7 @@ class StreamAnalyzer:
         eng.commit_frequency(run_counts[:nkeys])
         # summary + top-k in one kernel chain (summarize.hip): severity histogram, k best rows
         P, S = len(lib.patterns), len(lib.sev_names)
-        rows, _, sc = K.summarize(score, pat, gl, max(1, self.topk), eng.tabs["sev_index"], P, S, ws=eng.ws)
+        rows, _, sc, _ = K.summarize(score, pat, gl, max(1, self.topk), eng.tabs["sev_index"], P, S, ws=eng.ws)
         k = min(self.topk, score.numel())
         top = rows[:k].cpu().numpy()
         first = int(pat[0].item()) if pat.numel() else None

@@ -38,7 +38,13 @@ def _ref(score, line, pat, add, k, sev_index, npat, nsev):
 def _run(dev, score, line, pat, sev_index, k, npat, nsev, add):
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     la = T(np.array([add], np.int64)) if add else None
-    rows, ph, sh = K.summarize(T(score), T(pat), T(line), k, T(sev_index), npat, nsev, line_add=la)
+    rows, ph, sh, packed = K.summarize(T(score), T(pat), T(line), k, T(sev_index), npat, nsev, line_add=la,
+                                      pack_events=True)
+    pk = packed.cpu().numpy()
+    n = score.size
+    np.testing.assert_array_equal(pk[:8 * n].view(np.int64), line.astype(np.int64) + add)
+    np.testing.assert_array_equal(pk[8 * n:16 * n].view(np.float64), score)
+    np.testing.assert_array_equal(pk[16 * n:].view(np.int32), pat)
     return rows.cpu().numpy(), ph.cpu().numpy(), sh.cpu().numpy()
 
 

@@ -204,17 +204,18 @@ __global__ __launch_bounds__(256) void k_expand(const int64_t* __restrict__ hits
   for (int64_t j = 0; j < c; ++j) evk[base + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
 }
 
-LP_HD void ev_post_one(const EvTables& E, uint64_t key, int64_t e, int32_t* ev_line, int32_t* ev_pat, int32_t* ev_seg,
-                       uint32_t* fsort, int32_t& a, int32_t& b) {
+// returns the event's frequency sort key (its frequency key, or nkeys when it has none)
+LP_HD uint32_t ev_post_one(const EvTables& E, uint64_t key, int64_t e, int32_t* ev_line, int32_t* ev_pat,
+                           int32_t* ev_seg, int32_t& a, int32_t& b) {
   const int32_t x = (int32_t)(key >> E.pbits);
   const int p = (int)(key & ((1ull << E.pbits) - 1));
   const int s = seg_of(E.seg_lo, E.nseg, x);
   ev_line[e] = x;
   ev_pat[e] = p;
   ev_seg[e] = s;
-  const int32_t fk = E.freq_key[p];
-  fsort[e] = fk >= 0 ? (uint32_t)fk : (uint32_t)E.nkeys;
   event_window(E, x, p, s, a, b);
+  const int32_t fk = E.freq_key[p];
+  return fk >= 0 ? (uint32_t)fk : (uint32_t)E.nkeys;
 }
 
 __global__ __launch_bounds__(256) void k_ev_post(const uint64_t* __restrict__ evk, int64_t ne, EvTables E,
@@ -224,7 +225,7 @@ __global__ __launch_bounds__(256) void k_ev_post(const uint64_t* __restrict__ ev
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= ne) return;
   int32_t a, b;
-  ev_post_one(E, evk[e], e, ev_line, ev_pat, ev_seg, fsort, a, b);
+  fsort[e] = ev_post_one(E, evk[e], e, ev_line, ev_pat, ev_seg, a, b);
   idx[e] = (int32_t)e;
   if (a < b) {
     atomicAdd(diff + a, 1);
@@ -307,6 +308,213 @@ __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ co
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Small batches (a request of a few thousand lines): the whole hit stage and the whole event stage
+// are ONE workgroup each -- LDS bitonic sorts and block scans replace the rocPRIM sort / select /
+// scan launches and their temp-storage passes (8 + 9 launches -> 1 + 1). Same results as the bulk
+// path: sorted unique hits, events in (line, pattern) order, ranks from a stable sort by key.
+constexpr int SB_THREADS = 1024;
+constexpr int SB_MAX = 4096;           // keys / events held in LDS
+constexpr int SB_MAX_LINES = 16384;    // window-coverage difference array in LDS
+
+__device__ __forceinline__ int sb_pow2(int64_t n) {
+  int p = 64;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// ascending bitonic sort of s[0, n) (n a power of two <= SB_MAX), whole block
+__device__ void sb_sort(uint64_t* s, int n) {
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < n / 2; t += SB_THREADS) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const uint64_t a = s[lo], b = s[hi];
+        if ((b < a) == ((lo & size) == 0)) {
+          s[lo] = b;
+          s[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// exclusive prefix of v over the block (thread order); *total = block sum. Uses scratch[SB_THREADS/64 + 1].
+__device__ int64_t sb_excl_scan(int64_t v, int64_t* scratch, int64_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const long long u = __shfl_up((long long)incl, d, 64);
+    if (lane >= d) incl += u;
+  }
+  if (lane == 63) scratch[wid] = incl;
+  __syncthreads();
+  int64_t base = 0, tot = 0;
+  for (int w = 0; w < SB_THREADS / 64; ++w) {
+    if (w < wid) base += scratch[w];
+    tot += scratch[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return base + incl - v;
+}
+
+// small path, step 1 (all CUs): DFA-verify every prefilter candidate in place (a failed one
+// becomes -1). A DFA walk is a chain of dependent table loads; in one workgroup the ~1k walks
+// of a request queue behind one CU's memory pipeline, spread over the grid they do not.
+__global__ __launch_bounds__(256) void k_cand_verify(HitsArgs A) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n1 = A.dcount ? (int64_t)min((unsigned long long)A.pre_from, A.dcount[0]) : A.pre_from;
+  if (i >= n1) return;
+  int64_t* cand = const_cast<int64_t*>(A.cand);
+  const int64_t k = cand[i];
+  const int r = (int)(k >> 32);
+  const int64_t x = k & 0xFFFFFFFFll;
+  if (!dfa_run(A.dfa, r, A.text + A.ls[x], A.ll[x])) cand[i] = -1;
+}
+
+// small path, step 2 (one workgroup): every remaining candidate is verified; sort, keep the first
+// of each (regex, line) run, CSR, event counts and their scan
+__global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
+  __shared__ uint64_t keys[SB_MAX];
+  __shared__ int64_t hk[SB_MAX];
+  __shared__ int64_t scratch[SB_THREADS / 64 + 1];
+  const int64_t n = A.n;
+  const bool dc = A.dcount != nullptr;
+  const int64_t n1 = dc ? (int64_t)min((unsigned long long)A.pre_from, A.dcount[0]) : A.pre_from;
+  const int64_t n2 = dc ? (int64_t)min((unsigned long long)(n - A.pre_from), A.dcount[1]) : n - A.pre_from;
+  // the used entries of both regions, packed: the sort covers pow2(used), not the capacities
+  const int np = sb_pow2(n1 + n2);
+  for (int i = threadIdx.x; i < np; i += SB_THREADS) {
+    uint64_t key = LP_PAD_KEY;
+    if (i < n1 + n2) {
+      const bool pre = i >= n1;
+      const int64_t k = pre ? (dc ? A.cand2[i - n1] : A.cand[A.pre_from + i - n1]) : A.cand[i];
+      if (k >= 0)                   // -1: failed k_cand_verify; every other key counts as verified
+        key = (((((uint64_t)k >> 32) << A.lbits) | ((uint64_t)k & 0xFFFFFFFFull)) << 1) | 1ull;
+    }
+    keys[i] = key;
+  }
+  __syncthreads();
+  sb_sort(keys, np);
+  // dedupe + DFA verify, then compaction in sorted order: 4 consecutive keys per thread
+  constexpr int PER = SB_MAX / SB_THREADS;
+  bool keep[PER];
+  int64_t sk[PER];
+  int c = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x * PER + q;
+    keep[q] = i < np && dedupe_verify_one(keys, np, i, A.lbits, A.text, A.ls, A.ll, A.dfa, &sk[q]);
+    c += keep[q];
+  }
+  int64_t nh = 0;
+  int64_t o = sb_excl_scan(c, scratch, &nh);
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
+    if (keep[q]) {
+      hk[o] = sk[q];
+      A.hits[o] = sk[q];
+      ++o;
+    }
+  __syncthreads();
+  // CSR per regex, hit lines, events per hit and their inclusive scan (4 consecutive per thread)
+  for (int r = threadIdx.x; r <= A.R; r += SB_THREADS) A.hit_off[r] = lower_bound64(hk, nh, (int64_t)r << 32);
+  int64_t ec[PER], e = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x * PER + q;
+    ec[q] = 0;
+    if (i < nh) {
+      A.hit_line[i] = (int32_t)(hk[i] & 0xFFFFFFFFll);
+      ec[q] = hit_event_count(A.ev, hk[i]);
+      A.ev_cnt[i] = ec[q];
+    }
+    e += ec[q];
+  }
+  int64_t ne = 0;
+  int64_t run = sb_excl_scan(e, scratch, &ne);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = threadIdx.x * PER + q;
+    run += ec[q];
+    if (i < nh) A.ev_end[i] = run;
+  }
+  if (threadIdx.x == 0) {
+    A.counters[0] = nh;
+    A.counters[1] = ne;
+  }
+}
+
+__global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32_t* __restrict__ cov_out) {
+  __shared__ uint64_t keys[SB_MAX];
+  __shared__ int32_t diff[SB_MAX_LINES + 1];
+  __shared__ int64_t scratch[SB_THREADS / 64 + 1];
+  const EvTables& E = A.ev;
+  const int64_t ne = A.ne, L = A.L;
+  const int np = sb_pow2(ne);
+  for (int i = threadIdx.x; i <= L; i += SB_THREADS) diff[i] = 0;
+  for (int k = threadIdx.x; k < E.nkeys; k += SB_THREADS) A.freq_counts[k] = 0;
+  for (int i = threadIdx.x; i < np; i += SB_THREADS) keys[i] = LP_PAD_KEY;
+  __syncthreads();
+  // expand: each hit's events, keyed (line, pattern)
+  for (int64_t i = threadIdx.x; i < A.nh; i += SB_THREADS) {
+    const int64_t c = A.ev_cnt[i];
+    if (c == 0) continue;
+    const int64_t k = A.hits[i];
+    const int r = (int)(k >> 32);
+    const uint64_t x = (uint64_t)(k & 0xFFFFFFFFll);
+    const int64_t b0 = A.ev_end[i] - c, p0 = E.prim_off[r];
+    for (int64_t j = 0; j < c; ++j) keys[b0 + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
+  }
+  __syncthreads();
+  sb_sort(keys, np);
+  // per event: outputs + window coverage; then re-key by (frequency key, event) for the ranks
+  for (int e = threadIdx.x; e < ne; e += SB_THREADS) {
+    int32_t a, b;
+    const uint32_t fs = ev_post_one(E, keys[e], e, A.ev_line, A.ev_pat, A.ev_seg, a, b);
+    if (a < b) {
+      atomicAdd(diff + a, 1);
+      atomicAdd(diff + b, -1);
+    }
+    keys[e] = ((uint64_t)fs << 32) | (uint32_t)e;
+  }
+  __syncthreads();
+  sb_sort(keys, np);
+  for (int j = threadIdx.x; j < ne; j += SB_THREADS) {
+    const uint32_t fk = (uint32_t)(keys[j] >> 32);
+    const int32_t e = (int32_t)(keys[j] & 0xFFFFFFFFull);
+    if ((int)fk >= E.nkeys) {
+      A.ev_rank[e] = -1;
+      A.ev_fkey[e] = -1;
+      continue;
+    }
+    int64_t lo = 0, hi = j;                      // first slot of this key
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if ((uint32_t)(keys[m] >> 32) < fk) lo = m + 1; else hi = m;
+    }
+    A.ev_rank[e] = j - lo;
+    A.ev_fkey[e] = fk;
+    if (j + 1 == ne || (uint32_t)(keys[j + 1] >> 32) != fk) A.freq_counts[fk] = j - lo + 1;
+  }
+  // coverage = inclusive scan of diff over [0, L): contiguous runs per thread
+  const int64_t per = (L + SB_THREADS - 1) / SB_THREADS;
+  const int64_t lo = (int64_t)threadIdx.x * per, hi = lo + per < L ? lo + per : L;
+  int64_t s = 0;
+  for (int64_t i = lo; i < hi; ++i) s += diff[i];
+  int64_t tot = 0;
+  int64_t run = sb_excl_scan(s, scratch, &tot);
+  for (int64_t i = lo; i < hi; ++i) {
+    run += diff[i];
+    cov_out[i] = (int32_t)run;
+  }
+}
+
+bool hits_small_ok(const HitsArgs& A) { return A.n > 0 && A.n <= SB_MAX; }
+bool events_small_ok(const EventsArgs& A) { return A.ne <= SB_MAX && A.L <= SB_MAX_LINES; }
+
 // coarse byte-block -> line index (blk[b] = line containing byte b << 12), one lane per block
 __global__ __launch_bounds__(256) void k_blk_index(const int64_t* __restrict__ ls, int64_t L, int64_t nblk,
                                                    int32_t* __restrict__ blk) {
@@ -333,6 +541,12 @@ struct Carve {
 
 size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
+  if (hits_small_ok(A)) {          // a request: verify on the grid, the rest in one workgroup
+    hipLaunchKernelGGL(k_cand_verify, dim3(nblk(A.pre_from)), dim3(256), 0, pstream(stream), A);
+    hipLaunchKernelGGL(k_hits_small, dim3(1), dim3(SB_THREADS), 0, pstream(stream), A);
+    LP_PCHECK(hipGetLastError());
+    return 0;
+  }
   const bool dc = A.dcount != nullptr;
   const int kbits = 1 + A.lbits + A.rbits + (dc ? 1 : 0);    // + the pad bit
   Carve C{static_cast<uint8_t*>(ws)};
@@ -390,6 +604,21 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
   uint32_t* fout = C.take<uint32_t>(ne);
   int32_t* iin = C.take<int32_t>(ne);
   int32_t* iout = C.take<int32_t>(ne);
+  if (events_small_ok(A)) {        // a request: one workgroup for expand / sort / ranks / coverage
+    Carve D{static_cast<uint8_t*>(ws)};
+    int32_t* cov_s = A.cov ? A.cov : D.take<int32_t>(L);
+    if (!A.cov && (!ws || D.used > ws_bytes)) return D.used;
+    hipLaunchKernelGGL(k_events_small, dim3(1), dim3(SB_THREADS), 0, pstream(stream), A, cov_s);
+    LP_PCHECK(hipGetLastError());
+    if (L > 0 && A.feat) {
+      int per = (int)std::min<int64_t>(FC_MAX_LINES, std::max<int64_t>(256, L / 1024));
+      per = (per + 255) / 256 * 256;
+      hipLaunchKernelGGL(k_feat_cov, dim3(nblk(L, per)), dim3(256), 0, pstream(stream), cov_s, L, per, A.text, A.ls,
+                         A.ll, A.dfa, A.ctx_trans, A.ctx_acc, A.feat);
+      LP_PCHECK(hipGetLastError());
+    }
+    return D.used;
+  }
   int32_t* diff = C.take<int32_t>(L + 1);
   int32_t* cov = A.cov ? A.cov : C.take<int32_t>(L);
   size_t t_sort = 0, t_pairs = 0, t_scan = 0;
@@ -492,7 +721,7 @@ void events_host(const EventsArgs& A) {
   std::vector<int32_t> diff(L + 1, 0);
   for (int64_t e = 0; e < ne; ++e) {
     int32_t a, b;
-    ev_post_one(E, evk[e], e, A.ev_line, A.ev_pat, A.ev_seg, fs.data(), a, b);
+    fs[e] = ev_post_one(E, evk[e], e, A.ev_line, A.ev_pat, A.ev_seg, a, b);
     if (a < b) {
       ++diff[a];
       --diff[b];

@@ -45,7 +45,11 @@
 
 namespace lp {
 
-constexpr int SCAN_THREADS = 1024;   // LDS is per block: more waves per staged byte
+// Bulk texts: 1024-thread blocks (LDS is per block: more waves per staged byte), runs of 4 lines.
+// Small texts (a request): 256-thread blocks and one line per lane, so the few thousand lines
+// spread over many CUs and each lane's dependent chain is one line, not four.
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_THREADS_SMALL = 256;
 constexpr int SCAN_RUN = 4;
 
 // LDS loads from a 32-bit LDS address. The blob sits at LDS address 0 (the kernel's only LDS is
@@ -209,24 +213,24 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
   }
 }
 
-template <int G>
-__global__ __launch_bounds__(SCAN_THREADS) void k_scan_multi(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                             const int64_t* __restrict__ line_start,
-                                                             const int32_t* __restrict__ line_len, int64_t nlines,
-                                                             ScanPass S, int64_t* __restrict__ out, int64_t cap,
-                                                             unsigned long long* __restrict__ count) {
+template <int G, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                        const int64_t* __restrict__ line_start,
+                                                        const int32_t* __restrict__ line_len, int64_t nlines,
+                                                        ScanPass S, int64_t* __restrict__ out, int64_t cap,
+                                                        unsigned long long* __restrict__ count, int run_len) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-  for (int i = threadIdx.x * 4; i < S.lds_words; i += SCAN_THREADS * 4)      // lds_words: multiple of 4
+  for (int i = threadIdx.x * 4; i < S.lds_words; i += THREADS * 4)      // lds_words: multiple of 4
     *reinterpret_cast<uint4*>(sm + i) = *reinterpret_cast<const uint4*>(S.blob + i);
   __syncthreads();
   const GlobalEmit emit{out, cap, count};
   // the fast walk addresses LDS absolutely (blob at address 0); otherwise every run walks exactly
   const bool at_zero = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)sm == 0u;
-  const int64_t nruns = (nlines + SCAN_RUN - 1) / SCAN_RUN;
-  const int64_t stride = (int64_t)gridDim.x * SCAN_THREADS;
-  for (int64_t run = (int64_t)blockIdx.x * SCAN_THREADS + threadIdx.x; run < nruns; run += stride) {
-    const int64_t x0 = run * SCAN_RUN;
-    const int64_t x1 = x0 + SCAN_RUN < nlines ? x0 + SCAN_RUN : nlines;
+  const int64_t nruns = (nlines + run_len - 1) / run_len;
+  const int64_t stride = (int64_t)gridDim.x * THREADS;
+  for (int64_t run = (int64_t)blockIdx.x * THREADS + threadIdx.x; run < nruns; run += stride) {
+    const int64_t x0 = run * run_len;
+    const int64_t x1 = x0 + run_len < nlines ? x0 + run_len : nlines;
     // stream walk preconditions: "\n" / "\r\n" separators (after every line of the run,
     // the last one included), the run starts right after a '\n', no content ends in a terminator
     bool fast = true, crlf = false;
@@ -269,20 +273,28 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
   if (S.ngroups > 4 || (S.lds_words & 3) || S.lds_words * 4 > (160 << 10))
     throw std::runtime_error("scan_multi: bad pass descriptor");
   const size_t lds = (size_t)S.lds_words * 4;
-  const int64_t runs = (nlines + SCAN_RUN - 1) / SCAN_RUN;
-  const int64_t need = (runs + SCAN_THREADS - 1) / SCAN_THREADS;
-  const int g = (int)std::max<int64_t>(1, std::min<int64_t>(grid, need));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // small texts: one line per lane in 256-thread blocks (the grid is sized for 1024-thread blocks)
+  const bool small = nlines <= (int64_t)grid * SCAN_THREADS_SMALL;
+  const int run_len = small ? 1 : SCAN_RUN;
+  const int threads = small ? SCAN_THREADS_SMALL : SCAN_THREADS;
+  const int64_t runs = (nlines + run_len - 1) / run_len;
+  const int64_t need = (runs + threads - 1) / threads;
+  const int g = (int)std::max<int64_t>(1, std::min<int64_t>(small ? 4 * (int64_t)grid : grid, need));
+#define LP_SCAN(GV)                                                                                        \
+  if (small)                                                                                               \
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS_SMALL>), dim3(g), dim3(SCAN_THREADS_SMALL), lds, st, text, \
+                       nbytes, line_start, line_len, nlines, S, out, cap, count, run_len);                 \
+  else                                                                                                     \
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS>), dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, \
+                       line_start, line_len, nlines, S, out, cap, count, run_len)
   switch (S.ngroups) {
-    case 1: hipLaunchKernelGGL(k_scan_multi<1>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
-                               nlines, S, out, cap, count); break;
-    case 2: hipLaunchKernelGGL(k_scan_multi<2>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
-                               nlines, S, out, cap, count); break;
-    case 3: hipLaunchKernelGGL(k_scan_multi<3>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
-                               nlines, S, out, cap, count); break;
-    default: hipLaunchKernelGGL(k_scan_multi<4>, dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start, line_len,
-                                nlines, S, out, cap, count); break;
+    case 1: LP_SCAN(1); break;
+    case 2: LP_SCAN(2); break;
+    case 3: LP_SCAN(3); break;
+    default: LP_SCAN(4); break;
   }
+#undef LP_SCAN
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in scan_multi");
 }

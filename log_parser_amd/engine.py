@@ -119,6 +119,7 @@ class Prepared:
     feat: torch.Tensor
     n_lines: int
     timings: Dict[str, float] = field(default_factory=dict)
+    out_buf: Optional[torch.Tensor] = None   # K.results_buffer holding line / pattern / segment / counts
 
 
 @dataclass
@@ -134,6 +135,7 @@ class RunResult:
     hit_off: torch.Tensor
     n_lines: int
     timings: Dict[str, float] = field(default_factory=dict)
+    out_buf: Optional[torch.Tensor] = None   # K.results_buffer: every host-bound result, one D2H
 
 
 def summary_from_severity(lib, sev_hist: np.ndarray, first_pat: Optional[int]) -> dict:
@@ -481,16 +483,17 @@ class Engine:
         t = self._tick(timings, "verify_csr", t)
         nkeys = len(self.lib.freq_ids)
         dfa_feats = self.context_engine != "mfma"
+        out_buf = K.results_buffer(ne, nkeys, text.device) if text.is_cuda else None
         ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts, feat, cov = K.post_events(
             hits, nh, ev_cnt, ev_end, ne, L, evt, text, ls, ll, self.tabs["dfa"], nkeys, self.ws, features=dfa_feats,
-            ctx_ext=self.lib.ctx_dfa_extent)
+            ctx_ext=self.lib.ctx_dfa_extent, out=out_buf)
         if not dfa_feats:           # A/B engine: context features on the MFMA NFA kernel
             lines = torch.nonzero(cov[:L] > 0).flatten().to(torch.int32)
             feat = K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],
                                   self.lib.nfa_group_ncls[0])
         self._tick(timings, "events_context_freq", t)
         return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
-                        hit_line, feat, L, timings)
+                        hit_line, feat, L, timings, out_buf=out_buf)
 
     def seq_chain_table(self, prep: "Prepared", own_lo: int, own_hi: int) -> torch.Tensor:
         """Per sequence-event slot: event index still unmatched after this shard (-1 = done)."""
@@ -523,11 +526,15 @@ class Engine:
               tabs["seq_bonus"].data_ptr(), tabs["seq_ev_off"].data_ptr(), tabs["seq_ev_reg"].data_ptr(),
               seq_carry.data_ptr(), prep.hit_off.data_ptr(), prep.hit_line.data_ptr(), prep.feat.data_ptr(),
               segs.lo.data_ptr(), segs.hi.data_ptr(), segs.own_lo.data_ptr(), segs.g0.data_ptr(), segs.n.data_ptr())
+        score_out = None
+        if prep.out_buf is not None:
+            score_out = K.results_views(prep.out_buf, prep.ev_line.numel(), len(self.lib.freq_ids))[0]
         score, factors = K.score_fused(prep.ev_line, prep.ev_pat, prep.ev_seg, prep.ev_rank, prep.ev_fkey,
-                                       freq_carry, st, self.sp_tuple, with_factors)
+                                       freq_carry, st, self.sp_tuple, with_factors, out=score_out)
         self._tick(timings, "score", t)
         return RunResult(prep.ev_line, prep.ev_pat, prep.ev_seg, score, factors,
-                         prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings)
+                         prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings,
+                         out_buf=prep.out_buf)
 
     def run(self, text, nbytes, ls, ll, segs: Segments, freq_carry: torch.Tensor,
             seq_carry: Optional[torch.Tensor] = None, host_text=None, with_factors=False,
@@ -563,6 +570,13 @@ class Engine:
         """events (line, pattern, segment: int32; score: f64) + frequency counts (int64) in ONE
         device->host copy (one sync instead of five)."""
         n = res.ev_line.numel()
+        if res.out_buf is not None:        # already one buffer (K.results_buffer): no cat
+            h = res.out_buf.cpu().numpy()
+            k = res.out_buf.numel() - 20 * n
+            a, b = 8 * n, 8 * n + k
+            return (h[b:b + 4 * n].view(np.int32), h[b + 4 * n:b + 8 * n].view(np.int32),
+                    h[b + 8 * n:b + 12 * n].view(np.int32), h[:a].view(np.float64),
+                    h[a:a + 8 * len(res.freq_counts)].view(np.int64))
         parts = [res.ev_line.to(torch.int32), res.ev_pat.to(torch.int32), res.ev_seg.to(torch.int32),
                  res.score.contiguous().view(torch.int32), res.freq_counts.to(torch.int64).contiguous().view(torch.int32)]
         h = torch.cat(parts).cpu().numpy()

@@ -445,18 +445,40 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             return hits[:nh], hit_line, hit_off, ev_cnt, ev_end, nh, ne
 
 
+def results_buffer(ne: int, nkeys: int, device) -> torch.Tensor:
+    """One device buffer for everything a batch returns to the host (one D2H, no cat):
+    [score f64 x ne | frequency counts i64 x max(nkeys, 1) | line i32 x ne | pattern i32 x ne |
+    segment i32 x ne]."""
+    return torch.empty(20 * ne + 8 * max(nkeys, 1), dtype=torch.uint8, device=device)
+
+
+def results_views(buf: torch.Tensor, ne: int, nkeys: int):
+    """(score, freq_counts, ev_line, ev_pat, ev_seg) views of ``results_buffer``."""
+    k = max(nkeys, 1)
+    a, b = 8 * ne, 8 * ne + 8 * k
+    return (buf[:a].view(torch.float64), buf[a:b].view(torch.int64), buf[b:b + 4 * ne].view(torch.int32),
+            buf[b + 4 * ne:b + 8 * ne].view(torch.int32), buf[b + 8 * ne:b + 12 * ne].view(torch.int32))
+
+
 def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text, line_start, line_len, dfa_tuple,
-                nkeys: int, ws: Optional[Workspace], features: bool = True, ctx_ext: Tuple[int, int] = (1 << 30, 1 << 30)):
+                nkeys: int, ws: Optional[Workspace], features: bool = True, ctx_ext: Tuple[int, int] = (1 << 30, 1 << 30),
+                out: Optional[torch.Tensor] = None):
     """Events in reference order + segment, frequency rank/key, per-key counts and context features
     (or, with ``features=False``, the int32 window coverage per line for another feature engine).
-    ``ctx_ext`` = table extents of the 4 context DFAs (trans, acc entries) for LDS staging."""
+    ``ctx_ext`` = table extents of the 4 context DFAs (trans, acc entries) for LDS staging.
+    ``out``: a ``results_buffer`` receiving line / pattern / segment / frequency counts."""
     dev = text.device
-    ev_line = torch.empty(ne, dtype=torch.int32, device=dev)
-    ev_pat = torch.empty(ne, dtype=torch.int32, device=dev)
-    ev_seg = torch.empty(ne, dtype=torch.int32, device=dev)
+    if out is not None:
+        _, freq_counts, ev_line, ev_pat, ev_seg = results_views(out, ne, nkeys)
+    else:
+        ev_line = torch.empty(ne, dtype=torch.int32, device=dev)
+        ev_pat = torch.empty(ne, dtype=torch.int32, device=dev)
+        ev_seg = torch.empty(ne, dtype=torch.int32, device=dev)
+        freq_counts = (torch.empty if nkeys else torch.zeros)(max(nkeys, 1), dtype=torch.int64, device=dev)
     ev_rank = torch.empty(ne, dtype=torch.int64, device=dev)
     ev_fkey = torch.empty(ne, dtype=torch.int64, device=dev)
-    freq_counts = (torch.empty if nkeys else torch.zeros)(max(nkeys, 1), dtype=torch.int64, device=dev)
+    if out is not None and not nkeys:
+        freq_counts.zero_()
     # k_feat_cov writes every line (0 outside windows); the host twin too
     feat = torch.empty(max(L, 1), dtype=torch.uint8, device=dev) if features and L else \
         torch.zeros(max(L, 1), dtype=torch.uint8, device=dev)
@@ -573,10 +595,13 @@ def rescore(gl: torch.Tensor, fac: torch.Tensor, n_lines: int, sp_tuple) -> torc
     return out
 
 
-def score_fused(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_carry, st_tuple, sp_tuple, with_factors=False):
-    """k_score with the frequency count fused in: freq = carry[fkey] + rank (-1 without a key)."""
+def score_fused(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_carry, st_tuple, sp_tuple, with_factors=False,
+                out: Optional[torch.Tensor] = None):
+    """k_score with the frequency count fused in: freq = carry[fkey] + rank (-1 without a key).
+    ``out``: float64[n] destination (e.g. the score view of a ``results_buffer``)."""
     n = ev_line.numel()
-    out = torch.empty(n, dtype=torch.float64, device=ev_line.device)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=ev_line.device)
     fac = torch.empty((n, 7), dtype=torch.float64, device=ev_line.device) if with_factors else None
     if n == 0:
         return out, fac

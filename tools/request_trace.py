@@ -48,20 +48,16 @@ def summarise(args):
     except sqlite3.Error:
         cs = []
     ev = sorted([(s, e, n) for n, s, e in ks] + [(s, e, "<copy>") for s, e in cs])
-    # the last R requests: split the timeline at gaps > 200 us (between requests)
-    groups, cur = [], [ev[0]]
-    for x in ev[1:]:
-        if x[0] - max(y[1] for y in cur) > 200_000:
-            groups.append(cur)
-            cur = [x]
-        else:
-            cur.append(x)
-    groups.append(cur)
+    # one k_prefilter launch per request: a request = from one to the next (steady state)
+    marks = [x[0] for x in ev if "k_prefilter" in x[2]]
+    groups = []
+    for a, b in zip(marks, marks[1:]):
+        groups.append([x for x in ev if a <= x[0] < b])
     groups = groups[-args.requests:]
     spans, busy, nk, nc = [], [], [], []
     per_name = {}
     for g in groups:
-        spans.append((max(y[1] for y in g) - g[0][0]) / 1e3)
+        spans.append((max(y[1] for y in g) - g[0][0]) / 1e3)     # first kernel .. last end
         busy.append(sum(y[1] - y[0] for y in g) / 1e3)
         nk.append(sum(1 for y in g if y[2] != "<copy>"))
         nc.append(sum(1 for y in g if y[2] == "<copy>"))

@@ -291,6 +291,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
             "world_size": dist.get_world_size() if dist.is_initialized() else 1,
             "backend": dist.get_backend() if dist.is_initialized() else "none",
             "ms_per_step_per_rank": [round(x / args.steps * 1e3, 3) for x in per_rank],
+            "matcher_counts_rank0": dict(eng.arena.last),
         }
         if state.get("dev"):
             # compute-stream time of the device pipeline per step (line index .. collectives .. top-k

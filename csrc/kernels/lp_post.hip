@@ -10,11 +10,10 @@
 //               (primary role x owned line, k_csr_evcount); inclusive scan -> event offsets.
 //   events_dev  expand (line << pbits | pattern) keys (k_expand); radix sort = the reference's
 //               event order (line, then pattern: AnalysisService.java:89-113); per event segment,
-//               frequency key and context window (k_ev_post; window bounds go into a difference
-//               array); stable radix sort by frequency key -> rank among earlier same-key events and
+//               frequency key and context window (k_ev_post marks the window's lines covered);
+//               stable radix sort by frequency key -> rank among earlier same-key events and
 //               per-key counts (k_rank: the in-batch part of the penalty-before-record scan,
-//               ScoringService.java:84-88); inclusive scan of the difference array = window
-//               coverage; features only for covered lines (k_feat_cov, ContextAnalysisService.java:
+//               ScoringService.java:84-88); features only for covered lines (k_feat_cov, ContextAnalysisService.java:
 //               46-117 reads the 4 features of window lines only).
 //
 // The host twins below run the same element functions (the LP_HD helpers in this file) with
@@ -221,16 +220,15 @@ LP_HD uint32_t ev_post_one(const EvTables& E, uint64_t key, int64_t e, int32_t* 
 __global__ __launch_bounds__(256) void k_ev_post(const uint64_t* __restrict__ evk, int64_t ne, EvTables E,
                                                  int32_t* __restrict__ ev_line, int32_t* __restrict__ ev_pat,
                                                  int32_t* __restrict__ ev_seg, uint32_t* __restrict__ fsort,
-                                                 int32_t* __restrict__ idx, int32_t* __restrict__ diff) {
+                                                 int32_t* __restrict__ idx, int32_t* __restrict__ cov) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= ne) return;
   int32_t a, b;
   fsort[e] = ev_post_one(E, evk[e], e, ev_line, ev_pat, ev_seg, a, b);
   idx[e] = (int32_t)e;
-  if (a < b) {
-    atomicAdd(diff + a, 1);
-    atomicAdd(diff + b, -1);
-  }
+  // window coverage: mark the window's lines (consumers test cov > 0; equal concurrent stores
+  // from overlapping windows are benign) -- no difference array, no scan over all L lines
+  for (int32_t x = a; x < b; ++x) cov[x] = 1;
 }
 
 LP_HD void rank_one(const uint32_t* fs, const int32_t* idx, int64_t ne, int64_t j, int nkeys, int64_t* ev_rank,
@@ -619,25 +617,23 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
     }
     return D.used;
   }
-  int32_t* diff = C.take<int32_t>(L + 1);
   int32_t* cov = A.cov ? A.cov : C.take<int32_t>(L);
-  size_t t_sort = 0, t_pairs = 0, t_scan = 0;
+  size_t t_sort = 0, t_pairs = 0;
   if (ne > 0) {
     LP_PCHECK(rocprim::radix_sort_keys(nullptr, t_sort, kin, kout, (size_t)ne, 0, ebits, st));
     LP_PCHECK(rocprim::radix_sort_pairs(nullptr, t_pairs, fin, fout, iin, iout, (size_t)ne, 0, fbits, st));
   }
-  if (L > 0) LP_PCHECK(rocprim::inclusive_scan(nullptr, t_scan, diff, cov, (size_t)L, rocprim::plus<int32_t>(), st));
-  void* tmp = C.take_bytes(std::max(t_sort, std::max(t_pairs, t_scan)));
+  void* tmp = C.take_bytes(std::max(t_sort, t_pairs));
   if (!ws || C.used > ws_bytes) return C.used;
   if (E.nkeys > 0) LP_PCHECK(hipMemsetAsync(A.freq_counts, 0, (size_t)E.nkeys * sizeof(int64_t), st));
-  if (L > 0) LP_PCHECK(hipMemsetAsync(diff, 0, (size_t)(L + 1) * sizeof(int32_t), st));
+  if (L > 0) LP_PCHECK(hipMemsetAsync(cov, 0, (size_t)L * sizeof(int32_t), st));
   if (ne > 0) {
     hipLaunchKernelGGL(k_expand, dim3(nblk(A.nh)), dim3(256), 0, st, A.hits, A.nh, A.ev_cnt, A.ev_end, E, kin);
     LP_PCHECK(hipGetLastError());
     size_t tb = t_sort;
     LP_PCHECK(rocprim::radix_sort_keys(tmp, tb, kin, kout, (size_t)ne, 0, ebits, st));
     hipLaunchKernelGGL(k_ev_post, dim3(nblk(ne)), dim3(256), 0, st, kout, ne, E, A.ev_line, A.ev_pat, A.ev_seg, fin,
-                       iin, diff);
+                       iin, cov);
     LP_PCHECK(hipGetLastError());
     tb = t_pairs;
     LP_PCHECK(rocprim::radix_sort_pairs(tmp, tb, fin, fout, iin, iout, (size_t)ne, 0, fbits, st));
@@ -646,8 +642,6 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
     LP_PCHECK(hipGetLastError());
   }
   if (L > 0) {
-    size_t tb = t_scan;
-    LP_PCHECK(rocprim::inclusive_scan(tmp, tb, diff, cov, (size_t)L, rocprim::plus<int32_t>(), st));
     if (A.feat) {
       // lines per block: enough blocks to spread a small request over the CUs, 4096 for big ones
       int per = (int)std::min<int64_t>(FC_MAX_LINES, std::max<int64_t>(256, L / 1024));

@@ -375,7 +375,11 @@ class MatchArena:
     that overflows one re-runs with its exact counts."""
 
     def __init__(self):
-        self.rate = {"gram": 0.2, "cand": 0.1, "ver": 1.0 / 16}
+        # starting rates per line (an underestimate costs one re-run of the matchers; an
+        # overestimate costs sort work on every batch: the hit sort covers the capacity, and past
+        # ~1M keys rocPRIM switches from merge sort to onesweep with a fill per digit pass)
+        self.rate = {"gram": 0.08, "cand": 0.03, "ver": 0.01}
+        self.last: dict = {}            # counts of the latest batch (diagnostics)
 
     def caps(self, L: int) -> dict:
         return {k: int(L * r * 1.25) + 512 for k, r in self.rate.items()}
@@ -385,7 +389,7 @@ class MatchArena:
         covers the whole capacity, so slack costs sort time)."""
         for k, c in counts.items():
             r = c / max(L, 1)
-            self.rate[k] = max(r, self.rate[k] if overflow else self.rate[k] * 0.9, 1e-4)
+            self.rate[k] = max(r, self.rate[k] if overflow else self.rate[k] * 0.5, 1e-4)
 
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
@@ -439,6 +443,7 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
 
         _run_ws(call, ws)
         g, k, v, nh, ne = cnt.tolist()                 # the one host read
+        arena.last = {"lines": L, "gram_hits": g, "prefilter_candidates": k, "scan_hits": v, "hits": nh, "events": ne}
         ok = g <= cap["gram"] and k <= cap["cand"] and v <= cap["ver"]
         arena.learn(L, {"gram": g, "cand": k, "ver": v}, overflow=not ok)
         if ok:

@@ -150,3 +150,45 @@ def test_short_literals_fall_back_to_stride1():
     lib = _one("OOM", teddy=False)
     assert lib.pf["stride"] == 1                      # a 3-byte literal has no two 4-byte windows
     assert np.all(np.array([len(l) for l in lib.literals]) >= 1)
+
+
+def _parity_run(dev, lib, data, torch):
+    from log_parser_amd.engine import Engine, Segments
+    from log_parser_amd.ops import kernels as K
+    from log_parser_amd.utils.config import Config
+    eng = Engine(lib, Config.load(overrides={"engine.device": str(dev)}), device=dev)
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    t = t.to(dev)
+    ls, ll = K.split_lines(t, len(data))
+    res = eng.run(t, len(data), ls, ll, Segments.single(ls.numel(), dev), eng.freq_carry())
+    return res.ev_line.cpu().numpy(), res.ev_pat.cpu().numpy(), res.score.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("smax,teddy", [(1, False), (2, False), (4, False), (4, True)])
+def test_every_prefilter_variant_gpu_equals_cpu_and_golden(gpu_device, smax, teddy):
+    """Pins each k_prefilter<GM, S, *, TD> variant on the device: the library's sampling stride
+    (1, 2 or 4, from PF_STRIDE_MAX) and the Teddy tier on/off, against the host twin and the
+    golden model (AnalysisService.java:89-95 runs every primary on every line)."""
+    import torch
+    from log_parser_amd import golden
+    from log_parser_amd.utils.synth import make_log, realistic_library
+    old = C.PF_STRIDE_MAX, C.PF_TEDDY
+    try:
+        C.PF_STRIDE_MAX, C.PF_TEDDY = smax, teddy
+        sets, trig = realistic_library(150, seed=23) if teddy else make_library(150, seed=23)
+        lib = C.CompiledLibrary(sets, ScoringParams())
+    finally:
+        C.PF_STRIDE_MAX, C.PF_TEDDY = old
+    assert lib.pf["stride"] == smax and bool(lib.pf["teddy_lits"]) == teddy
+    logs = make_log(4000, trig, seed=24, hit_rate=0.05, crlf_rate=0.1)
+    data = logs.encode()
+    g = _parity_run(gpu_device, lib, data, torch)
+    c = _parity_run(torch.device("cpu"), lib, data, torch)
+    for a, b in zip(g, c):
+        np.testing.assert_array_equal(a, b)
+    ref = golden.analyze(logs, sets, ScoringParams(), golden.FrequencyTracker(ScoringParams()))
+    assert [(e["lineNumber"] - 1, e["matchedPattern"]["id"]) for e in ref["events"]] == \
+        [(int(x), lib.patterns[int(p)].id) for x, p in zip(g[0], g[1])]
+    np.testing.assert_allclose(g[2], [e["score"] for e in ref["events"]], rtol=1e-12)

@@ -307,7 +307,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
 
 // POST /parse body -> (status, pod_nonnull, pod_name | None, logs_kind, logs bytes | None);
 // status: 0 ok, 1 invalid JSON, 2 JSON but not an object, 3 fall back to json.loads
-static py::tuple parse_pod_request_py(py::bytes body) {
+static py::tuple parse_pod_request_py(py::bytes body, bool two_pass) {
   char* p = nullptr;
   Py_ssize_t n = 0;
   PyBytes_AsStringAndSize(body.ptr(), &p, &n);
@@ -315,7 +315,12 @@ static py::tuple parse_pod_request_py(py::bytes body) {
   int st;
   {
     py::gil_scoped_release nogil;
-    st = parse_pod_request(reinterpret_cast<const uint8_t*>(p), (size_t)n, r);
+    // two_pass: what the HTTP front end does -- validate, then unescape the recorded span
+    st = parse_pod_request(reinterpret_cast<const uint8_t*>(p), (size_t)n, r, !two_pass);
+    if (two_pass && st == JIN_OK && r.logs_kind == 1) {
+      r.logs.resize(r.logs_len + 64);
+      r.logs.resize(decode_json_string(reinterpret_cast<const uint8_t*>(p) + r.logs_off, r.logs_len, &r.logs[0]));
+    }
   }
   py::object name = r.has_name ? py::object(py::str(r.pod_name)) : py::object(py::none());
   py::object logs = r.logs_kind == 1 ? py::object(py::bytes(r.logs)) : py::object(py::none());
@@ -412,7 +417,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("set_host_threads", &set_host_threads);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
-  m.def("parse_pod_request", &parse_pod_request_py);
+  m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false);
 
   // ---- device launchers
   m.def("line_index_tiles", &line_index_tiles);
@@ -526,12 +531,41 @@ PYBIND11_MODULE(_lpnative, m) {
           py::gil_scoped_release nogil;
           v = s.next_requests(max_n, timeout_ms);
         }
+        // decoded POST /parse: one bytes object per request sized for the escaped text, filled by
+        // the unescaper with the GIL released (the only copy of the log between the socket
+        // buffer and the engine's pinned stage), then trimmed
+        std::vector<PyObject*> bufs(v.size(), nullptr);
+        for (size_t i = 0; i < v.size(); ++i)
+          if (v[i].kind == 0) {
+            bufs[i] = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(v[i].logs_len + 64));
+            if (!bufs[i]) {
+              for (PyObject* b : bufs) Py_XDECREF(b);
+              throw py::error_already_set();
+            }
+          }
+        std::vector<size_t> lens(v.size(), 0);
+        {
+          py::gil_scoped_release nogil;
+          for (size_t i = 0; i < v.size(); ++i)
+            if (v[i].kind == 0) {
+              lens[i] = decode_json_string(reinterpret_cast<const uint8_t*>(v[i].body.data()) + v[i].logs_off,
+                                           v[i].logs_len, PyBytes_AS_STRING(bufs[i]));
+              s.recycle(std::move(v[i].body));
+            }
+        }
         py::list out;
-        for (auto& r : v) {
-          if (r.kind == 0)
-            out.append(py::make_tuple(r.id, 0, py::bytes(r.logs), r.pod_name, r.t_arrival));
-          else
+        for (size_t i = 0; i < v.size(); ++i) {
+          auto& r = v[i];
+          if (r.kind == 0) {
+            PyObject* b = bufs[i];
+            if (_PyBytes_Resize(&b, (Py_ssize_t)lens[i]) != 0) {
+              for (size_t j = i + 1; j < v.size(); ++j) Py_XDECREF(bufs[j]);
+              throw py::error_already_set();
+            }
+            out.append(py::make_tuple(r.id, 0, py::reinterpret_steal<py::bytes>(b), r.pod_name, r.t_arrival));
+          } else {
             out.append(py::make_tuple(r.id, 1, r.method, r.path, py::bytes(r.body), r.t_arrival));
+          }
         }
         return out;
       }, py::arg("max_n") = 4096, py::arg("timeout_ms") = 100)
@@ -539,9 +573,8 @@ PYBIND11_MODULE(_lpnative, m) {
         char* p = nullptr;
         Py_ssize_t n = 0;
         PyBytes_AsStringAndSize(body.ptr(), &p, &n);
-        std::string b(p, (size_t)n);
-        py::gil_scoped_release nogil;
-        s.respond(id, status, ctype, b);
+        py::gil_scoped_release nogil;   // `body` (immutable) stays referenced for the call
+        s.respond(id, status, ctype, p, (size_t)n);
       })
       .def("stats", [](HttpServer& s) {
         py::dict d;

@@ -15,6 +15,8 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -93,6 +95,8 @@ struct HttpServer::Conn {
   bool paused = false;      // EPOLLIN off: too much pipelined input while a request is in flight
   bool dead = false;        // closed; freed at the end of the event-loop iteration
   double last = 0;          // last read / write activity (idle-timeout sweep)
+  double t_first = 0;       // first byte of the request being received (LP_HTTP_TRACE)
+  int n_recv = 0, n_wake = 0;
 };
 
 struct HttpServer::Io {
@@ -113,6 +117,9 @@ struct HttpServer::Io {
 HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s)
     : host_(host), port_(port), max_body_(max_body), idle_timeout_s_(idle_timeout_s) {
   io_threads = std::max(1, std::min(io_threads, kMaxIo));
+  if (const char* e = getenv("LP_HTTP_SPIN_US")) io_spin_s_ = atof(e) * 1e-6;
+  if (const char* e = getenv("LP_HTTP_PUMP_SPIN_US")) pump_spin_s_ = atof(e) * 1e-6;
+  trace_ = getenv("LP_HTTP_TRACE") != nullptr;
   for (int i = 0; i < io_threads; ++i) {
     auto io = std::make_unique<Io>();
     io->index = i;
@@ -170,6 +177,17 @@ void HttpServer::stop() {
 }
 
 std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
+  if (pump_spin_s_ > 0) {
+    const double until = now_s() + pump_spin_s_;
+    for (;;) {
+      {
+        std::lock_guard<std::mutex> g(qm_);
+        if (!q_.empty() || stop_) break;
+      }
+      if (now_s() > until) break;
+      __builtin_ia32_pause();
+    }
+  }
   std::unique_lock<std::mutex> lk(qm_);
   // system_clock deadline: pthread_cond_timedwait (steady-clock waits map to pthread_cond_clockwait,
   // which the ThreadSanitizer runtime of this toolchain does not intercept); a short poll anyway
@@ -193,18 +211,37 @@ static std::string head(int status, const std::string& ctype, size_t n, bool kee
 }
 
 void HttpServer::respond(uint64_t id, int status, const std::string& content_type, const std::string& body) {
+  respond(id, status, content_type, body.data(), body.size());
+}
+
+void HttpServer::respond(uint64_t id, int status, const std::string& content_type, const char* body, size_t n) {
   const int ioi = (int)(id & 0xFF);
   if (ioi >= (int)ios_.size()) return;
   Io* io = ios_[ioi].get();
   const bool keep = (id >> 63) == 0;
-  std::string data = head(status, content_type, body.size(), keep);
-  data += body;
+  std::string data = head(status, content_type, n, keep);
+  data.append(body, n);   // header + body in one buffer: one send() for a small response
   {
     std::lock_guard<std::mutex> lk(io->om);
     io->outbox.push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep});
   }
   uint64_t one = 1;
   (void)!write(io->efd, &one, 8);
+}
+
+std::string HttpServer::take_buffer() {
+  std::lock_guard<std::mutex> g(pm_);
+  if (pool_.empty()) return std::string();
+  std::string b = std::move(pool_.back());
+  pool_.pop_back();
+  return b;
+}
+
+void HttpServer::recycle(std::string&& buf) {
+  if (buf.capacity() < (64u << 10) || buf.capacity() > (size_t(256) << 20)) return;
+  buf.clear();
+  std::lock_guard<std::mutex> g(pm_);
+  if (pool_.size() < 64) pool_.push_back(std::move(buf));
 }
 
 void HttpServer::send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body,
@@ -329,6 +366,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
   }
   const size_t total = he + 4 + (size_t)clen;
   if (c->in.size() < total) {
+    if (c->in.capacity() < total) c->in.reserve(total);   // one allocation, not log2(n) regrowths
     if (expect && !c->sent_continue) {
       c->out += "HTTP/1.1 100 Continue\r\n\r\n";
       c->sent_continue = true;
@@ -337,12 +375,13 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     return false;
   }
   c->sent_continue = false;
-  std::string body = c->in.substr(he + 4, (size_t)clen);
-  c->in.erase(0, total);
   stats.requests++;
   const size_t q = path.find('?');
   const std::string route = q == std::string::npos ? path : path.substr(0, q);
+  const size_t b0 = he + 4;
+  auto consume = [&] { c->in.erase(0, total); };
   if (method == "GET" && route == "/health") {
+    consume();
     send_now(io, c, 200, "application/json", "{\"status\":\"UP\"}", keep);
     return !c->closing && !c->dead;
   }
@@ -350,38 +389,58 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
   r.t_arrival = now_s();
   if (method == "POST" && route == "/parse" && !json_ctype) {
     // @Consumes(MediaType.APPLICATION_JSON) (Parse.java:42): another media type is a 415
+    consume();
     send_now(io, c, 415, "application/json", kUnsupported, keep);
     return !c->closing && !c->dead;
   }
   if (method == "POST" && route == "/parse") {
+    // validated in place; the logs string is decoded later, once, straight into the Python bytes
+    // object the engine packs from (bind.cpp next_requests)
     PodRequest pr;
-    const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(body.data()), body.size(), pr);
+    const double tv = trace_ ? now_s() : 0;
+    const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
+    if (trace_)
+      fprintf(stderr, "lp-http-trace bytes %zu receive_us %.1f recvs %d wakeups %d validate_us %.1f\n", total,
+              (tv - c->t_first) * 1e6, c->n_recv, c->n_wake, (now_s() - tv) * 1e6);
     if (st == JIN_OK && (!pr.pod_nonnull || pr.logs_kind != 1)) {
       stats.native_400++;
+      consume();
       if (!pr.pod_nonnull)
         send_now(io, c, 400, "application/json", kInvalid, keep);
       else
         send_now(io, c, 400, "application/json", "{\"error\":\"PodFailureData.logs must be a string\"}", keep);
       return !c->closing && !c->dead;
     }
-    if (st == JIN_INVALID || st == JIN_NOT_OBJECT || body.empty()) {
+    if (st == JIN_INVALID || st == JIN_NOT_OBJECT || clen == 0) {
       stats.native_400++;
+      consume();
       send_now(io, c, 400, "application/json", kInvalid, keep);
       return !c->closing && !c->dead;
     }
     if (st == JIN_OK) {
       r.kind = 0;
-      r.logs = std::move(pr.logs);
       r.pod_name = pr.has_name ? pr.pod_name : std::string();
+      r.logs_off = b0 + pr.logs_off;
+      r.logs_len = pr.logs_len;
+      if (c->in.size() == total) {   // the usual case: hand the whole buffer over, no copy
+        r.body.swap(c->in);
+        c->in = take_buffer();
+      } else {                       // pipelined bytes follow: copy this request out
+        r.body.assign(c->in, 0, total);
+        consume();
+      }
     } else {
       r.kind = 1;  // JIN_FALLBACK: the Python route decodes it with json.loads
     }
   } else {
     r.kind = 1;
   }
+  if (r.kind == 1) {
+    r.body = c->in.substr(b0, (size_t)clen);
+    consume();
+  }
   r.method = std::move(method);
   r.path = std::move(path);
-  if (r.kind == 1) r.body = std::move(body);
   r.id = (c->id << 8) | (uint64_t)io->index | (keep ? 0 : (uint64_t(1) << 63));
   c->busy = true;
   c->keep = keep;
@@ -396,10 +455,17 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
 void HttpServer::handle_readable(Io* io, Conn* c) {
   if (c->dead) return;
   char buf[65536];
+  c->n_wake++;
   for (;;) {
     const ssize_t k = ::recv(c->fd, buf, sizeof(buf), 0);
     if (k > 0) {
       c->last = now_s();
+      if (c->in.empty()) {
+        c->t_first = c->last;
+        c->n_recv = 0;
+        c->n_wake = 1;
+      }
+      c->n_recv++;
       c->in.append(buf, (size_t)k);
       if ((int64_t)c->in.size() > max_body_ + (int64_t)kMaxHeader + 4) {
         if (c->busy) {  // stop reading until the in-flight request is answered
@@ -426,8 +492,11 @@ void HttpServer::handle_readable(Io* io, Conn* c) {
 
 void HttpServer::io_loop(Io* io) {
   epoll_event evs[256];
+  double active = 0;
   while (!stop_) {
-    const int n = epoll_wait(io->ep, evs, 256, 200);
+    const bool spin = io_spin_s_ > 0 && now_s() - active < io_spin_s_;
+    const int n = epoll_wait(io->ep, evs, 256, spin ? 0 : 200);
+    if (n > 0) active = now_s();
     for (int i = 0; i < n; ++i) {
       const uint64_t tag = evs[i].data.u64;
       if (tag == 0) {  // accept

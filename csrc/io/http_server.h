@@ -23,7 +23,9 @@ struct HttpRequest {
   uint64_t id = 0;          // reply handle
   int kind = 0;             // 0 = decoded POST /parse, 1 = other route (raw method/path/body)
   std::string method, path, body;
-  std::string logs;         // kind 0: UTF-8 log text
+  std::string logs;         // decoded UTF-8 log text (callers of the decode_logs mode)
+  size_t logs_off = 0;      // kind 0: `body` is the raw request buffer and the JSON `logs`
+  size_t logs_len = 0;      //   string's escaped content is body[logs_off, logs_off + logs_len)
   std::string pod_name;     // kind 0: pod.metadata.name or "" (unknown)
   double t_arrival = 0;     // monotonic seconds, when the body was complete
 };
@@ -46,6 +48,10 @@ class HttpServer {
   }
   // queue the response of request `id` (ignored if its connection is gone)
   void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
+  void respond(uint64_t id, int status, const std::string& content_type, const char* body, size_t n);
+  // hand a drained request's raw buffer back (its capacity serves a later request: no page faults
+  // of a fresh megabyte-sized allocation per request)
+  void recycle(std::string&& buf);
   void stop();
   HttpStats stats;
 
@@ -60,11 +66,15 @@ class HttpServer {
   void flush(Io* io, Conn* c);
   void set_events(Io* io, Conn* c);
   void close_conn(Io* io, Conn* c);
+  std::string take_buffer();
 
   std::string host_;
   int port_;
   int64_t max_body_;
   double idle_timeout_s_;
+  double io_spin_s_ = 0;     // LP_HTTP_SPIN_US: IO threads poll (no sleep) this long after activity
+  bool trace_ = false;       // LP_HTTP_TRACE: per-request receive / validate timings on stderr
+  double pump_spin_s_ = 0;   // LP_HTTP_PUMP_SPIN_US: next_requests polls this long before waiting
   std::atomic<bool> stop_{false};
   std::vector<std::unique_ptr<Io>> ios_;
   std::vector<std::thread> threads_;
@@ -73,6 +83,8 @@ class HttpServer {
   std::condition_variable qcv_;
   std::deque<HttpRequest> q_;
   std::atomic<uint64_t> next_id_{1};
+  std::mutex pm_;
+  std::vector<std::string> pool_;
 };
 
 }  // namespace lp

@@ -13,9 +13,18 @@ struct PodRequest {
   bool has_name = false;      // pod.metadata.name is a string
   std::string pod_name;
   int logs_kind = 0;          // 0 absent / null, 1 string, 2 other type
-  std::string logs;           // UTF-8, escapes decoded
+  std::string logs;           // UTF-8, escapes decoded (decode_logs mode)
+  size_t logs_off = 0;        // logs_kind 1: the raw JSON string's content (between the quotes)
+  size_t logs_len = 0;        //   as an offset / length into the body
 };
 
-int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out);
+// Validates the whole body. With decode_logs the `logs` string is unescaped into out.logs;
+// without it only its raw span is recorded (decode later with decode_json_string, e.g. straight
+// into a Python bytes object -- the HTTP front end's one-copy path).
+int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs = true);
+
+// Unescapes the content of a JSON string that parse_pod_request validated (`n` raw bytes between
+// the quotes) into `w`, which must have room for n + 64 bytes; returns the decoded length.
+size_t decode_json_string(const uint8_t* p, size_t n, char* w);
 
 }  // namespace lp

@@ -9,6 +9,7 @@ touches the GPU (a GPU-initialised process must not fork interpreters).
 from __future__ import annotations
 
 import http.client
+import socket
 import json
 import os
 import subprocess
@@ -30,6 +31,56 @@ def write_library(sets, directory: Optional[str] = None) -> str:
         with open(os.path.join(d, f"set{i:03d}.yaml"), "w") as f:
             yaml.safe_dump(s.model_dump(by_alias=True, exclude_none=True), f)
     return d
+
+
+class RawClient:
+    """Minimal HTTP/1.1 keep-alive client for latency runs: the request (headers + body) is
+    serialised once and written with one sendall; the response is read by Content-Length. This is
+    how a load generator (wrk, ab) drives a server -- the client-side cost of http.client (which
+    concatenates headers and body into a fresh 1 MB buffer per call and parses headers in
+    Python) is not server latency."""
+
+    def __init__(self, host: str, port: int, timeout: float = 60.0):
+        self.sock = socket.create_connection((host, port), timeout=timeout)
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self.buf = bytearray(1 << 16)
+
+    @staticmethod
+    def request(path: str, body: bytes, content_type: str = "application/json") -> bytes:
+        return (b"POST %s HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: %s\r\nContent-Length: %d\r\n\r\n"
+                % (path.encode(), content_type.encode(), len(body))) + body
+
+    def roundtrip(self, msg: bytes) -> tuple:
+        self.sock.sendall(msg)
+        data = bytearray()
+        while True:
+            he = data.find(b"\r\n\r\n")
+            if he >= 0:
+                break
+            k = self.sock.recv_into(self.buf)
+            if k == 0:
+                raise ConnectionError("server closed the connection")
+            data += self.buf[:k]
+        head = bytes(data[:he]).decode("latin-1").split("\r\n")
+        status = int(head[0].split()[1])
+        n = 0
+        for h in head[1:]:
+            k, _, v = h.partition(":")
+            if k.strip().lower() == "content-length":
+                n = int(v)
+        body = data[he + 4:]
+        while len(body) < n:
+            k = self.sock.recv_into(self.buf)
+            if k == 0:
+                raise ConnectionError("server closed the connection")
+            body += self.buf[:k]
+        return status, bytes(body[:n])
+
+    def post(self, body: bytes, path: str = "/parse") -> tuple:
+        return self.roundtrip(self.request(path, body))
+
+    def close(self) -> None:
+        self.sock.close()
 
 
 class ServerProcess:
@@ -68,19 +119,32 @@ class ServerProcess:
         r = c.getresponse()
         return r.status, r.read()
 
-    def parse_latencies(self, logs: str, n: int, warmup: int = 5) -> List[float]:
+    def parse_latencies(self, logs: str, n: int, warmup: int = 5, client: str = "raw") -> List[float]:
+        """Wall time of ``n`` sequential POST /parse round trips on one keep-alive connection
+        (``client``: "raw" = pre-serialised request over a socket, "http.client" = stdlib)."""
         body = json.dumps({"pod": {"metadata": {"name": "bench"}}, "logs": logs}).encode()
-        for _ in range(warmup):
-            st, out = self.post(body)
-            if st != 200:
-                raise RuntimeError(f"/parse returned {st}: {out[:200]!r}")
-        lat = []
-        for _ in range(n):
-            t = time.perf_counter()
-            st, out = self.post(body)
-            lat.append(time.perf_counter() - t)
-            if st != 200:
-                raise RuntimeError(f"/parse returned {st}")
+        if client == "raw":
+            rc = RawClient("127.0.0.1", self.port)
+            msg = rc.request("/parse", body)
+            send = lambda: rc.roundtrip(msg)  # noqa: E731
+        else:
+            rc = None
+            send = lambda: self.post(body)  # noqa: E731
+        try:
+            for _ in range(warmup):
+                st, out = send()
+                if st != 200:
+                    raise RuntimeError(f"/parse returned {st}: {out[:200]!r}")
+            lat = []
+            for _ in range(n):
+                t = time.perf_counter()
+                st, out = send()
+                lat.append(time.perf_counter() - t)
+                if st != 200:
+                    raise RuntimeError(f"/parse returned {st}")
+        finally:
+            if rc is not None:
+                rc.close()
         return lat
 
     def stop(self) -> None:

@@ -25,8 +25,8 @@ def _ref(body: bytes):
             logs.encode() if kind == 1 else None)
 
 
-def _check(body: bytes):
-    got = N.parse_pod_request(body)
+def _check(body: bytes, two_pass: bool = False):
+    got = N.parse_pod_request(body, two_pass)
     if got[0] == 3:
         return False
     ref = _ref(body)
@@ -59,8 +59,9 @@ def _rand_value(rng, depth=0):
     return {_rand_str(rng): _rand_value(rng, depth + 1) for _ in range(rng.randint(0, 4))}
 
 
+@pytest.mark.parametrize("two_pass", [False, True])
 @pytest.mark.parametrize("seed", range(4))
-def test_native_decoder_matches_json_loads_on_random_requests(seed):
+def test_native_decoder_matches_json_loads_on_random_requests(seed, two_pass):
     rng = random.Random(seed)
     native = 0
     for _ in range(600):
@@ -76,11 +77,11 @@ def test_native_decoder_matches_json_loads_on_random_requests(seed):
         body = json.dumps(d, ensure_ascii=rng.random() < 0.5, indent=rng.choice([None, 1])).encode()
         if rng.random() < 0.2 and "logs" in d:       # duplicate key: the last one wins
             body = body[:-1] + b', "logs": "dup\\nlast"}'
-        native += _check(body)
+        native += _check(body, two_pass)
         if rng.random() < 0.3:                        # corruptions must be rejected like json.loads
             cut = rng.randrange(len(body) + 1)
-            native += _check(body[:cut])
-            native += _check(body + rng.choice([b"x", b",", b"}", b" ", b"\n"]))
+            native += _check(body[:cut], two_pass)
+            native += _check(body + rng.choice([b"x", b",", b"}", b" ", b"\n"]), two_pass)
     assert native > 500                               # most bodies take the native path
 
 
@@ -95,3 +96,19 @@ def test_native_decoder_edge_cases():
     for c in [b'{"pod":NaN}', b'{"pod":{},"logs":"\\ud83d\\ude00"}', b'\xef\xbb\xbf{}', b'{"pod":{},"logs":"\xff"}',
               b"[" * 600 + b"]" * 600]:
         assert N.parse_pod_request(c)[0] == 3, c      # handed to json.loads
+
+
+@pytest.mark.parametrize("two_pass", [False, True])
+def test_native_decoder_64_byte_blocks(two_pass):
+    """Long logs go through the 64-byte branch-free block decoder (AVX-512 VBMI2 hosts): backslash
+    runs of every length at every offset, runs crossing a block boundary, escaped quotes, a closing
+    quote and invalid / \\u escapes inside a block -- all byte-identical to json.loads."""
+    rng = random.Random(5)
+    pieces = ["a" * 63, "x" * 64, "b", " ", "\\", "\\\\", "\\\\\\", "\\n", "\\t", "\\r", "\\/", '\\"',
+              "\\b", "\\f", "\\u00e9", "\\u20ac", "\\q", "\x01", "\u00e9"]
+    native = 0
+    for _ in range(3000):
+        raw = "z" * rng.randint(0, 130) + "".join(rng.choice(pieces) for _ in range(rng.randint(1, 24)))
+        body = ('{"pod": {}, "logs": "' + raw + '"}').encode()
+        native += _check(body, two_pass)
+    assert native > 1000

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-2 re-entry check: smoke, pytest -m gpu, default bench, realistic kernel stats.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$(pwd)
+OUT=${OUT:-gpurun_out/r2k}
+mkdir -p $OUT
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo SMOKE_OK || exit 1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $OUT/pytest_gpu.log 2>&1 && echo PYTEST_OK || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && echo BENCH_OK || exit 1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof -o run -- python3 $R/bench.py --steps 8 --warmup 2 --parse-requests 0 > $R/$OUT/bench_prof.json 2> $R/$OUT/bench_prof.err && echo PROF_OK || exit 1

@@ -2,20 +2,104 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <thread>
+
+#include "kernels/lp_host.h"
 
 #if defined(__SSE2__)
 #include <emmintrin.h>
 #endif
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 namespace lp {
 
+// Newline positions of one unit: grow-only, uninitialised storage (a zero-filled vector costs a
+// memset of its capacity per request).
+struct NlBuf {
+  std::unique_ptr<int64_t[]> p;
+  int64_t n = 0, cap = 0;
+  void reserve(int64_t c) {
+    if (c <= cap) return;
+    std::unique_ptr<int64_t[]> q(new int64_t[(size_t)c]);
+    if (n) std::memcpy(q.get(), p.get(), (size_t)n * sizeof(int64_t));
+    p = std::move(q);
+    cap = c;
+  }
+  void push_back(int64_t v) {
+    if (n == cap) reserve(std::max<int64_t>(64, 2 * cap));
+    p[n++] = v;
+  }
+  int64_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  int64_t back() const { return p[n - 1]; }
+  int64_t operator[](int64_t i) const { return p[i]; }
+};
+
+#if defined(__x86_64__)
+// AVX-512 VBMI2: 64 bytes per step, copied with one load / store; the newline offsets of the block
+// are compressed out of an iota vector (vpcompressb) and the first 8 widened to absolute int64
+// positions and stored unconditionally -- no branch per newline (the bit loop mispredicted on
+// every ~100-byte line). Blocks with more than 8 newlines take a short scalar loop. Returns the
+// bytes consumed (a multiple of 64, stops early when `nl` lacks 64 + 8 free slots).
+__attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vbmi2,bmi,bmi2,popcnt")))
+static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int64_t base, NlBuf& nl) {
+  alignas(64) static const uint8_t kIota[64] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                                                16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31,
+                                                32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47,
+                                                48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63};
+  const __m512i iota = _mm512_load_si512(reinterpret_cast<const void*>(kIota));
+  const __m512i NL = _mm512_set1_epi8('\n');
+  int64_t i = 0, k = nl.n;
+  int64_t* out = nl.p.get();
+  const int64_t room = nl.cap - 72;
+  for (; i + 64 <= n && k <= room; i += 64) {
+    const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(src + i));
+    _mm512_storeu_si512(reinterpret_cast<void*>(dst + i), v);
+    const uint64_t m = _mm512_cmpeq_epi8_mask(v, NL);
+    const __m512i offs = _mm512_maskz_compress_epi8(m, iota);
+    const __m512i pos = _mm512_add_epi64(_mm512_cvtepu8_epi64(_mm512_castsi512_si128(offs)), _mm512_set1_epi64(base + i));
+    _mm512_storeu_si512(reinterpret_cast<void*>(out + k), pos);
+    const int c = (int)_mm_popcnt_u64(m);
+    if (c > 8) {   // rare: short lines
+      uint64_t r = m;
+      for (int j = 0; j < 8; ++j) r &= r - 1;
+      int64_t q = k + 8;
+      while (r) {
+        out[q++] = base + i + __builtin_ctzll(r);
+        r &= r - 1;
+      }
+    }
+    k += c;
+  }
+  nl.n = k;
+  return i;
+}
+
+static bool have_avx512_vbmi2() {
+  static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+                         __builtin_cpu_supports("avx512vbmi") && __builtin_cpu_supports("avx512vbmi2") &&
+                         __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("popcnt");
+  return ok;
+}
+#endif
+
 // Copy src[0, n) to dst and record the absolute position (base + i) of every '\n', in ONE pass
-// over the bytes: 64-byte blocks are loaded once, stored, and compared with SSE2 into a bit
-// mask whose set bits are the newlines (a memchr call per ~100-byte log line costs more than the
-// bytes themselves: 1.9M calls per 2k-request batch).
-static void copy_scan_nl(const uint8_t* src, uint8_t* dst, int64_t n, int64_t base, std::vector<int64_t>& nl) {
+// over the bytes: 64-byte blocks are loaded once, stored, and compared into a bit mask whose set
+// bits are the newlines (a memchr call per ~100-byte log line costs more than the bytes
+// themselves: 1.9M calls per 2k-request batch).
+static void copy_scan_nl(const uint8_t* src, uint8_t* dst, int64_t n, int64_t base, NlBuf& nl) {
   int64_t i = 0;
+#if defined(__x86_64__)
+  if (have_avx512_vbmi2()) {
+    while (i + 64 <= n) {
+      nl.reserve(nl.n + std::max<int64_t>(1024, (n - i) / 32) + 72);
+      i += copy_scan_nl_512(src + i, dst + i, n - i, base + i, nl);
+    }
+  }
+#endif
 #if defined(__SSE2__)
   const __m128i NL = _mm_set1_epi8('\n');
   for (; i + 64 <= n; i += 64) {
@@ -43,11 +127,11 @@ static void copy_scan_nl(const uint8_t* src, uint8_t* dst, int64_t n, int64_t ba
   }
 }
 
-// Work unit: one document, or a ~256 KiB slice of a large one (so a single big request also
+// Work unit: one document, or a ~128 KiB slice of a large one (so a single big request also
 // copies and splits on several threads).
 struct Unit {
   int64_t doc, a, b;           // bytes [a, b) of document `doc` (absolute packed offsets)
-  std::vector<int64_t> nl;     // '\n' positions inside [a, b)
+  NlBuf nl;                    // '\n' positions inside [a, b)
   int64_t first_nl = 0;        // index of nl[0] among the document's newlines
   int64_t prev = 0;            // position of the newline before this unit (doc start - 1 if none)
 };
@@ -55,34 +139,20 @@ struct Unit {
 template <class F>
 static void parallel_units(std::vector<Unit>& U, int64_t total, int nthreads, int64_t per_thread, F&& fn) {
   const int64_t n = (int64_t)U.size();
-  // >= per_thread bytes per thread (4 MB default): below that, spawning threads costs more than
-  // the copy itself
+  // >= per_thread bytes per helper (4 MB default): a request's bytes sit in the caller's cache,
+  // and on a many-chiplet host, moving them to helpers on other CCDs costs more than the copy
+  // (measured on the MI355X box's EPYC: 1 MB pack 46 us on one thread, 93-111 us on the pool)
   const int T = std::max(1, std::min<int>(nthreads, (int)std::min<int64_t>(n, 1 + total / std::max<int64_t>(1, per_thread))));
   if (T == 1) {
     for (int64_t u = 0; u < n; ++u) fn(U[u]);
     return;
   }
-  // contiguous unit ranges of ~equal bytes
-  std::vector<int64_t> cut(T + 1, n);
-  cut[0] = 0;
-  int64_t acc = 0, t = 1;
-  for (int64_t u = 0; u < n && t < T; ++u) {
-    acc += U[u].b - U[u].a;
-    if (acc >= total / T * t) cut[t++] = u + 1;
-  }
-  std::vector<std::thread> th;
-  th.reserve(T);
-  for (int k = 0; k < T; ++k)
-    if (cut[k + 1] > cut[k])
-      th.emplace_back([&, k] {
-        for (int64_t u = cut[k]; u < cut[k + 1]; ++u) fn(U[u]);
-      });
-  for (auto& x : th) x.join();
+  HostPool::get().run(n, T, [&](int64_t u) { fn(U[u]); });
 }
 
 void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, uint8_t* dst, int nthreads,
                      DocBatchIndex& out, int64_t min_bytes_per_thread) {
-  constexpr int64_t SLICE = 256 << 10;
+  constexpr int64_t SLICE = 128 << 10;
   std::vector<Unit> U;
   U.reserve(D);
   for (int64_t d = 0; d < D; ++d) {
@@ -94,7 +164,7 @@ void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, 
   // phase 1: copy + newline positions, one pass over the bytes
   parallel_units(U, total, nthreads, min_bytes_per_thread, [&](Unit& u) {
     const int64_t s0 = doc_off[u.doc];
-    u.nl.reserve((size_t)((u.b - u.a) / 64 + 4));
+    u.nl.reserve((u.b - u.a) / 64 + 4);
     copy_scan_nl(reinterpret_cast<const uint8_t*>(src[u.doc]) + (u.a - s0), dst + u.a, u.b - u.a, u.a, u.nl);
   });
   // per document: newline numbering, kept lines (Java split: trailing empty strings dropped; a

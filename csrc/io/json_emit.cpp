@@ -1,12 +1,19 @@
 #include "json_emit.h"
 
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
+
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <random>
 #include <stdexcept>
 #include <thread>
 #include <string>
 #include <vector>
+
+#include "kernels/lp_host.h"
 
 namespace py = pybind11;
 
@@ -28,6 +35,23 @@ void put_str(std::string& o, const uint8_t* s, int64_t n) {
   int64_t i = 0;
   while (i < n) {
     int64_t j = i;
+#if defined(__SSE2__)
+    // 16 bytes per step: '"', '\\' and control bytes (<= 0x1F: saturating c - 0x1F == 0) end a run
+    {
+      const __m128i q = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\'), lim = _mm_set1_epi8(0x1F);
+      while (j + 16 <= n) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + j));
+        const __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, q), _mm_cmpeq_epi8(v, bs)),
+                                       _mm_cmpeq_epi8(_mm_subs_epu8(v, lim), _mm_setzero_si128()));
+        const int bits = _mm_movemask_epi8(m);
+        if (bits) {
+          j += __builtin_ctz((unsigned)bits);
+          break;
+        }
+        j += 16;
+      }
+    }
+#endif
     while (j < n && !kEsc.esc[s[j]]) ++j;       // copy clean runs in one append
     if (j > i) o.append(reinterpret_cast<const char*>(s + i), (size_t)(j - i));
     if (j >= n) break;
@@ -62,14 +86,14 @@ void put_int(std::string& o, int64_t v) {
   o.append(b, r.ptr);
 }
 
-// events [e0, e1) of one document whose lines are [doc_lo, doc_hi) of the line index
-void emit_events(std::string& o, const uint8_t* b, const int64_t* LS, const int32_t* LL, int64_t doc_lo,
-                 int64_t doc_hi, const int32_t* EL, const int32_t* EP, const double* ES, int64_t e0, int64_t e1,
-                 const PatternTable& T) {
+// events [a, z) of a document whose lines are [doc_lo, doc_hi) of the line index, without the
+// enclosing brackets; a comma precedes every event but the document's first (index e_first)
+void emit_event_range(std::string& o, const uint8_t* b, const int64_t* LS, const int32_t* LL, int64_t doc_lo,
+                      int64_t doc_hi, const int32_t* EL, const int32_t* EP, const double* ES, int64_t a, int64_t z,
+                      int64_t e_first, const PatternTable& T) {
   auto line = [&](int64_t j) { put_str(o, b + LS[j], LL[j]); };
-  o.push_back('[');
-  for (int64_t e = e0; e < e1; ++e) {
-    if (e > e0) o.push_back(',');
+  for (int64_t e = a; e < z; ++e) {
+    if (e > e_first) o.push_back(',');
     const int64_t x = EL[e];
     const int32_t p = EP[e];
     o.append("{\"lineNumber\":");
@@ -83,18 +107,40 @@ void emit_events(std::string& o, const uint8_t* b, const int64_t* LS, const int3
       o.append(",\"linesBefore\":null,\"linesAfter\":null}");
     } else {
       o.append(",\"linesBefore\":[");
-      const int64_t a = x - bf < doc_lo ? doc_lo : x - bf;
-      for (int64_t j = a; j < x; ++j) { if (j > a) o.push_back(','); line(j); }
+      const int64_t lo = x - bf < doc_lo ? doc_lo : x - bf;
+      for (int64_t j = lo; j < x; ++j) { if (j > lo) o.push_back(','); line(j); }
       o.append("],\"linesAfter\":[");
-      const int64_t z = x + 1 + af > doc_hi ? doc_hi : x + 1 + af;
-      for (int64_t j = x + 1; j < z; ++j) { if (j > x + 1) o.push_back(','); line(j); }
+      const int64_t hi = x + 1 + af > doc_hi ? doc_hi : x + 1 + af;
+      for (int64_t j = x + 1; j < hi; ++j) { if (j > x + 1) o.push_back(','); line(j); }
       o.append("]}");
     }
     o.append(",\"score\":");
     put_double(o, ES[e]);
     o.push_back('}');
   }
+}
+
+// events [e0, e1) of one document whose lines are [doc_lo, doc_hi) of the line index
+void emit_events(std::string& o, const uint8_t* b, const int64_t* LS, const int32_t* LL, int64_t doc_lo,
+                 int64_t doc_hi, const int32_t* EL, const int32_t* EP, const double* ES, int64_t e0, int64_t e1,
+                 const PatternTable& T) {
+  o.push_back('[');
+  emit_event_range(o, b, LS, LL, doc_lo, doc_hi, EL, EP, ES, e0, e1, e0, T);
   o.push_back(']');
+}
+
+// per-call UUID seed: one entropy read per process (std::random_device per call opened the
+// entropy source on every request), then a splitmix64 sequence
+uint64_t uuid_seed() {
+  static const uint64_t base = [] {
+    std::random_device rd;
+    return ((uint64_t)rd() << 32) ^ rd();
+  }();
+  static std::atomic<uint64_t> ctr{0};
+  uint64_t z = base + 0x9E3779B97F4A7C15ull * (ctr.fetch_add(1, std::memory_order_relaxed) + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
 }
 
 // RFC 4122 version-4 UUID (UUID.randomUUID, AnalysisService.java:117)
@@ -152,20 +198,41 @@ void put_summary(std::string& o, const int32_t* EP, int64_t e0, int64_t e1, cons
 
 template <class F>
 void parallel_docs(const int64_t* eo, int64_t D, int nthreads, F&& run) {
-  // documents are independent: split them into ranges of ~equal event counts
+  // documents are independent: ranges of ~equal document counts on the host pool
   const int64_t E = eo[D];
   const int T_ = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nthreads, D, 1 + (E + D) / 2048}));
   if (T_ == 1) {
     run(0, D);
     return;
   }
-  std::vector<int64_t> cut(T_ + 1, D);
-  cut[0] = 0;
-  for (int t = 1; t < T_; ++t) cut[t] = std::max(cut[t - 1], D * t / T_);
-  std::vector<std::thread> th;
-  for (int t = 0; t < T_; ++t)
-    if (cut[t + 1] > cut[t]) th.emplace_back(run, cut[t], cut[t + 1]);
-  for (auto& x : th) x.join();
+  HostPool::get().run(T_, T_, [&](int64_t t) { run(D * t / T_, D * (t + 1) / T_); });
+}
+
+// events [e0, e1) of one document, emitted in `chunks` pieces on the host pool and joined (a
+// single large request is one document: its ~1 KB-per-event context text is the emitter's work)
+void emit_events_parallel(std::string& o, const uint8_t* b, const int64_t* LS, const int32_t* LL, int64_t doc_lo,
+                          int64_t doc_hi, const int32_t* EL, const int32_t* EP, const double* ES, int64_t e0,
+                          int64_t e1, const PatternTable& T, int nthreads) {
+  const int64_t n = e1 - e0;
+  // >= 2048 events per helper: below that the caller's cache-hot serial loop wins (see docs.cpp)
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, n / 2048));
+  if (chunks <= 1) {
+    emit_events(o, b, LS, LL, doc_lo, doc_hi, EL, EP, ES, e0, e1, T);
+    return;
+  }
+  std::vector<std::string> part(chunks);
+  HostPool::get().run(chunks, chunks, [&](int64_t c) {
+    const int64_t a = e0 + n * c / chunks, z = e0 + n * (c + 1) / chunks;
+    std::string& s = part[c];
+    s.reserve((size_t)(z - a) * 1536);
+    emit_event_range(s, b, LS, LL, doc_lo, doc_hi, EL, EP, ES, a, z, e0, T);
+  });
+  size_t tot = 2;
+  for (auto& s : part) tot += s.size();
+  o.reserve(o.size() + tot);
+  o.push_back('[');
+  for (auto& s : part) o.append(s);
+  o.push_back(']');
 }
 
 }  // namespace
@@ -196,13 +263,13 @@ py::list emit_batch_results_py(const PatternTable& T, uint64_t buf, py::array_t<
     py::gil_scoped_release nogil;
     const int64_t* dl = doc_line_off.data();
     const int64_t* eo = ev_doc_off.data();
-    std::random_device rd;
-    const uint64_t seed = ((uint64_t)rd() << 32) ^ rd();
+    const uint64_t seed = uuid_seed();
+    const bool one = D == 1;            // one document: parallel over its events instead
     parallel_docs(eo, D, nthreads, [&](int64_t a, int64_t z) {
       std::mt19937_64 rng(seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(a + 1)));
       for (int64_t d = a; d < z; ++d) {
         std::string& o = outs[d];
-        o.reserve(256 + (size_t)(eo[d + 1] - eo[d]) * 512);
+        o.reserve(256 + (size_t)(eo[d + 1] - eo[d]) * 1536);
         o.append("{\"analysisId\":\"");
         put_uuid4(o, rng);
         o.append("\",\"metadata\":{\"processingTimeMs\":");
@@ -211,8 +278,9 @@ py::list emit_batch_results_py(const PatternTable& T, uint64_t buf, py::array_t<
         put_int(o, dl[d + 1] - dl[d]);
         o.append(meta_tail);
         o.append("},\"events\":");
-        emit_events(o, reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), dl[d], dl[d + 1],
-                    ev_line.data(), ev_pat.data(), ev_score.data(), eo[d], eo[d + 1], T);
+        emit_events_parallel(o, reinterpret_cast<const uint8_t*>(buf), line_start.data(), line_len.data(), dl[d],
+                             dl[d + 1], ev_line.data(), ev_pat.data(), ev_score.data(), eo[d], eo[d + 1], T,
+                             one ? nthreads : 1);
         o.push_back(',');
         put_summary(o, ev_pat.data(), eo[d], eo[d + 1], T);
         o.push_back('}');

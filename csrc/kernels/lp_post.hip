@@ -275,9 +275,9 @@ __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ co
   if (threadIdx.x == 0) n = 0;
   if (lds) {
     if (threadIdx.x < 16) s_meta[threadIdx.x] = P.meta[threadIdx.x];
-    for (int i = threadIdx.x; i < 4 * 256; i += blockDim.x) s_bm[i] = P.bytemap[i];
-    for (int i = threadIdx.x; i < ctx_trans; i += blockDim.x) s_trans[i] = P.trans[i];
-    for (int i = threadIdx.x; i < ctx_acc; i += blockDim.x) s_acc[i] = P.acc[i];
+    lds_fill<uint8_t, 4>(s_bm, P.bytemap, 4 * 256);
+    lds_fill<uint16_t, 4>(s_trans, P.trans, ctx_trans);
+    lds_fill<uint8_t, 4>(s_acc, P.acc, ctx_acc);
   }
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * per_block;

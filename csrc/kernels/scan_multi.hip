@@ -220,8 +220,7 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
                                                         ScanPass S, int64_t* __restrict__ out, int64_t cap,
                                                         unsigned long long* __restrict__ count, int run_len) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-  for (int i = threadIdx.x * 4; i < S.lds_words; i += THREADS * 4)      // lds_words: multiple of 4
-    *reinterpret_cast<uint4*>(sm + i) = *reinterpret_cast<const uint4*>(S.blob + i);
+  lds_fill<uint4>(reinterpret_cast<uint4*>(sm), reinterpret_cast<const uint4*>(S.blob), S.lds_words >> 2);  // multiple of 4
   __syncthreads();
   const GlobalEmit emit{out, cap, count};
   // the fast walk addresses LDS absolutely (blob at address 0); otherwise every run walks exactly

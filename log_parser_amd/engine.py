@@ -301,10 +301,14 @@ class Engine:
         self._pinned: Optional[torch.Tensor] = None
         # batch staging buffers (pinned on GPU), recycled; one per batch in flight in the pipeline
         self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
+        # second compute stream: literal-free scans overlap the prefilter chain (K.match_and_hits)
+        self._side = None
         if self.device.type == "cuda":
             props = torch.cuda.get_device_properties(self.device)
             self.n_cus = int(props.multi_processor_count)
             self.pf_grid = self.n_cus * 4
+            if bool(self.config.get("engine.scan-stream", True)):
+                self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
         else:
             self.n_cus = 1
             self.pf_grid = 1
@@ -475,7 +479,8 @@ class Engine:
             self._start(timings)
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
-                self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None)
+                self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None,
+                side=self._side)
         else:
             cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(

@@ -393,14 +393,21 @@ class MatchArena:
 
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
-                   ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None):
+                   ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None, side=None):
     """GPU: every matcher appends to the arena, then the post-match hit pipeline reads the device
-    counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read."""
+    counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read.
+
+    ``side`` = (stream, fork event, join event): the self-verifying engines (literal-free DFA scan,
+    single-DFA scan, MFMA NFA) run on that stream, concurrently with the literal prefilter chain
+    (block index -> prefilter -> verify) on the current one; both join before the hit pipeline.
+    A small request's kernels are latency-bound and leave most CUs idle, so the two chains
+    overlap almost fully."""
     dev = text.device
     L = line_start.numel()
     st = _s(text)
-    blk = line_block_index(line_start, nbytes)
     lbits, rbits = N.bits_for(max(L, 1)), N.bits_for(max(R, 1))
+    scans = bool(tabs["scan_passes"]) or bool(tabs["scan_regs"].numel()) or \
+        any(g.numel() for g in tabs["nfa_scan_lists"].values())
     while True:
         cap = arena.caps(L)
         gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
@@ -409,6 +416,27 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
         # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters)
         cnt = torch.zeros(5, dtype=torch.int64, device=dev)
         c0 = cnt.data_ptr()
+        sst = st
+        if side is not None and scans and tick is None:
+            side[1].record()
+            side[0].wait_event(side[1])
+            sst = side[0].cuda_stream
+        # the long pole first: literal-free scans (own stream when `side`)
+        for sp in tabs["scan_passes"]:
+            N.scan_multi(text.data_ptr(), nbytes, line_start.data_ptr(), line_len.data_ptr(), L, sp, ver.data_ptr(),
+                         cap["ver"], c0 + 16, scan_grid(sp), sst, True)
+        if tabs["scan_regs"].numel():
+            N.scan_dev(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), L, tabs["scan_regs"].data_ptr(),
+                       tabs["scan_regs"].numel(), tabs["dfa"], ver.data_ptr(), cap["ver"], c0 + 16, sst)
+        for ncls, glist in tabs["nfa_scan_lists"].items():
+            if glist.numel():
+                N.nfa(tabs["nfa_tables"].data_ptr(), glist.data_ptr(), glist.numel(), ncls, 0, L, text.data_ptr(),
+                      line_start.data_ptr(), line_len.data_ptr(), 0, ver.data_ptr(), cap["ver"], c0 + 16, sst, True)
+        if sst != st:
+            side[2].record(side[0])
+        elif tick:
+            tick("scan")
+        blk = line_block_index(line_start, nbytes)
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L, gh.data_ptr(), cap["gram"],
                         c0, pf_grid, st)
         N.pf_verify_dev(gh.data_ptr(), cap["gram"], text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L,
@@ -416,18 +444,8 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
                         max(16, min(8192, nbytes >> 13)))
         if tick:
             tick("prefilter")
-        for sp in tabs["scan_passes"]:
-            N.scan_multi(text.data_ptr(), nbytes, line_start.data_ptr(), line_len.data_ptr(), L, sp, ver.data_ptr(),
-                         cap["ver"], c0 + 16, scan_grid(sp), st, True)
-        if tabs["scan_regs"].numel():
-            N.scan_dev(text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), L, tabs["scan_regs"].data_ptr(),
-                       tabs["scan_regs"].numel(), tabs["dfa"], ver.data_ptr(), cap["ver"], c0 + 16, st)
-        for ncls, glist in tabs["nfa_scan_lists"].items():
-            if glist.numel():
-                N.nfa(tabs["nfa_tables"].data_ptr(), glist.data_ptr(), glist.numel(), ncls, 0, L, text.data_ptr(),
-                      line_start.data_ptr(), line_len.data_ptr(), 0, ver.data_ptr(), cap["ver"], c0 + 16, st, True)
-        if tick:
-            tick("scan")
+        if sst != st:
+            torch.cuda.current_stream(dev).wait_event(side[2])
         n = cap["cand"] + cap["ver"]
         hits = torch.empty(n, dtype=torch.int64, device=dev)
         hit_line = torch.empty(n, dtype=torch.int32, device=dev)

@@ -48,6 +48,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.dfa-max-states": (2048, int),
     # context-feature engine: "mfma" (NFA state-transition GEMM on matrix cores) or "dfa"
     "engine.context-engine": ("dfa", str),
+    # run the literal-free scan engines on a second HIP stream, overlapping the literal prefilter
+    "engine.scan-stream": (True, bool),
     # serve a batch from the CPU backend when the device path fails (availability)
     "engine.fallback-cpu": (True, bool),
     # per-stage HIP-event timers, reported in response metadata as stageTimingsMs (opt-in)

@@ -15,6 +15,8 @@ namespace lp {
 // loads are issued before its first LDS store, so staging costs ~one memory round trip per U
 // elements per lane instead of one per element (a loop of load -> ds_write pairs waits on every
 // load: ~10 serial L2/HBM trips per lane for a 42 KB scan blob in a 256-thread block).
+// The loads are unconditional (index clamped to n - 1) so `v` stays in registers: a guarded
+// load left the array partially defined and the compiler put it in scratch memory.
 template <typename T, int U = 8>
 __device__ __forceinline__ void lds_fill(T* dst, const T* __restrict__ src, int n) {
   for (int b = threadIdx.x; b < n; b += U * (int)blockDim.x) {
@@ -22,7 +24,7 @@ __device__ __forceinline__ void lds_fill(T* dst, const T* __restrict__ src, int 
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const int i = b + j * (int)blockDim.x;
-      if (i < n) v[j] = src[i];
+      v[j] = src[i < n ? i : n - 1];
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {

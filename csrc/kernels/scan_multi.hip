@@ -87,10 +87,14 @@ LP_HD void scan_emit(const ScanPass& S, int g, uint32_t m, int64_t line, Emit&& 
 
 // exact walk of ONE line on the global tables (Matcher.find: accept before a final line
 // terminator, at end of line, or before any byte). Shared by the host twin and the device.
-template <typename Emit>
+// G_MAX: the device instantiates it with the pass's group count so every S.x[g] index is a
+// compile-time constant (a runtime-indexed kernel-argument array was copied to scratch memory)
+template <int G_MAX = 4, typename Emit>
 LP_HD void scan_line_exact(const ScanPass& S, const uint32_t* bm, const uint8_t* s, int n, int64_t line, Emit&& emit) {
   const int ft = n - final_term_len(s, n);
-  for (int g = 0; g < S.ngroups; ++g) {
+#pragma unroll
+  for (int g = 0; g < G_MAX; ++g) {
+    if (g >= S.ngroups) break;
     uint32_t st = S.init_state[g], acc = 0;
     for (int t = 0; t < n; ++t) {
       if (t == ft) acc |= scan_fin(S, g, st, 1);
@@ -134,30 +138,39 @@ __device__ __forceinline__ uint32_t crlf_bits(uint32_t w, uint32_t nx) {
   return nz_bytes(w ^ 0x0D0D0D0Du) & nz_bytes(__builtin_amdgcn_alignbyte(nx, w, 1) ^ 0x0A0A0A0Au);
 }
 
+// byte j (0..16) of the 5-word window w0..w4; j is a compile-time constant in the unrolled
+// loops below, so the window stays in registers (an indexed array lived in scratch memory)
+__device__ __forceinline__ uint32_t win_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, int j) {
+  const uint32_t w = j < 4 ? w0 : j < 8 ? w1 : j < 12 ? w2 : j < 16 ? w3 : w4;
+  return (w >> (8 * (j & 3))) & 0xFFu;
+}
+
 // exact re-walk of one 16-byte block [p0, p0 + 16) of a run (rare path): bytes outside
 // [p_lo, p_end) are skipped, a separator '\r' is held, '\n' ends line l
 template <typename Emit>
-__device__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, const uint32_t (&w)[5], int64_t p0,
-                                 int64_t p_lo, int64_t p_end, int64_t x0, int64_t x1,
-                                 const int64_t* line_start, int g, uint32_t st, Emit&& emit) {
+__device__ __forceinline__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, uint32_t w0, uint32_t w1, uint32_t w2,
+                                 uint32_t w3, uint32_t w4, int64_t p0, int64_t p_lo, int64_t p_end, int64_t x0,
+                                 int64_t x1, const int64_t* line_start, int g, uint32_t st, Emit&& emit) {
   int64_t l = x0;
   const int64_t first = p0 > p_lo ? p0 : p_lo;
   while (l + 1 < x1 && line_start[l + 1] <= first) ++l;
   if (p0 <= p_lo) st = S.init_state[g];
   uint32_t lacc = 0;
+#pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int64_t pos = p0 + j;
-    if (pos < p_lo || pos >= p_end) continue;
-    const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-    const uint32_t nx = (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFFu;
-    const uint32_t col = (c == 0x0Du && nx == 0x0Au) ? 0u : ((bm[c] >> (8 * g)) & 0xFFu) >> 1;
-    const uint32_t e = scan_step(S, g, st, col);
-    lacc |= e >> 16;
-    st = e & 0xFFFFu;
-    if (col == 1u) {
-      scan_emit(S, g, lacc, l, emit);
-      lacc = 0;
-      ++l;
+    if (pos >= p_lo && pos < p_end) {
+      const uint32_t c = win_byte(w0, w1, w2, w3, w4, j);
+      const uint32_t nx = win_byte(w0, w1, w2, w3, w4, j + 1);
+      const uint32_t col = (c == 0x0Du && nx == 0x0Au) ? 0u : ((bm[c] >> (8 * g)) & 0xFFu) >> 1;
+      const uint32_t e = scan_step(S, g, st, col);
+      lacc |= e >> 16;
+      st = e & 0xFFFFu;
+      if (col == 1u) {
+        scan_emit(S, g, lacc, l, emit);
+        lacc = 0;
+        ++l;
+      }
     }
   }
   scan_emit(S, g, lacc, l < x1 ? l : x1 - 1, emit);
@@ -177,7 +190,7 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
   for (int64_t p0 = a0; p0 < p_end; p0 += 16) {
     const uint4 nxt = blk[1];
     ++blk;
-    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
+    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};   // constant indices only
     uint32_t hold = 0;                    // CRLF: byte j of the block is a separator '\r'
     if constexpr (CRLF) {
 #pragma unroll
@@ -203,12 +216,14 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
         xr[g] = lds_ld16(xr[g] + ((b >> (8 * g)) & 0xFFu));
       }
     }
-    bool hot = false;
+    // rare: a state that can accept was visited -- exact re-walk of this block, only for the
+    // groups that visited one (a group below its threshold cannot accept anywhere in the block;
+    // each re-walk is a chain of 16 dependent global loads, ~8 us, on a request's critical path)
 #pragma unroll
-    for (int g = 0; g < G; ++g) hot |= mx[g] >= (uint32_t)S.thr[g];
-    if (hot)        // rare: a state that can accept was visited -- exact re-walk of this block
-      for (int g = 0; g < G; ++g)
-        scan_block_exact(S, sm, w, p0, p_lo, p_end, x0, x1, line_start, g, scan_state_of(S, g, xs[g]), emit);
+    for (int g = 0; g < G; ++g)
+      if (mx[g] >= (uint32_t)S.thr[g])
+        scan_block_exact(S, sm, w[0], w[1], w[2], w[3], w[4], p0, p_lo, p_end, x0, x1, line_start, g,
+                         scan_state_of(S, g, xs[g]), emit);
     cur = nxt;
   }
 }
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
     if (p_lo > 0 && text[p_lo - 1] != '\n') fast = false;   // e.g. a document boundary in a batch
     if (!at_zero) fast = false;
     if (!fast) {     // rare: exact per-line walks
-      for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
+      for (int64_t x = x0; x < x1; ++x) scan_line_exact<G>(S, sm, text + line_start[x], line_len[x], x, emit);
       continue;
     }
     if (crlf)

@@ -49,7 +49,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # context-feature engine: "mfma" (NFA state-transition GEMM on matrix cores) or "dfa"
     "engine.context-engine": ("dfa", str),
     # run the literal-free scan engines on a second HIP stream, overlapping the literal prefilter
-    "engine.scan-stream": (True, bool),
+    # (off: the cross-stream event wait cost more than the overlap saved -- 10k-line request
+    # 0.362 -> 0.382-0.408 ms on the MI355X box, tools/engine_phases.py A/B)
+    "engine.scan-stream": (False, bool),
     # serve a batch from the CPU backend when the device path fails (availability)
     "engine.fallback-cpu": (True, bool),
     # per-stage HIP-event timers, reported in response metadata as stageTimingsMs (opt-in)

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=100)
     ap.add_argument("--lines", type=int, default=10_000)
+    ap.add_argument("-D", action="append", default=[], help="config override key=value (A/B runs)")
     args = ap.parse_args()
     import torch
     from log_parser_amd import engine as E
@@ -28,7 +29,7 @@ def main():
     from log_parser_amd.utils.synth import make_log, realistic_library
     dev = torch.device("cuda", 0)
     sets, trig = realistic_library(1000, seed=7)
-    eng = E.Engine(CompiledLibrary(sets, ScoringParams()), Config.load(overrides={"engine.device": "cuda:0"}), device=dev)
+    eng = E.Engine(CompiledLibrary(sets, ScoringParams()), Config.load(overrides=dict([("engine.device", "cuda:0")] + [tuple(d.split("=", 1)) for d in args.D])), device=dev)
     logs = make_log(args.lines, trig, seed=13, hit_rate=0.01).encode()
     acc = defaultdict(list)
     cur = {}
@@ -66,6 +67,7 @@ def main():
                 acc[k].append(v)
             acc["total"].append(tot)
     out = {k: round(float(np.median(v)) * 1e3, 4) for k, v in acc.items()}
+    out["overrides"] = args.D
     print(json.dumps(out))
 
 

@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--profile", action="store_true", help="per-stage HIP-event timings (no extra syncs)")
     ap.add_argument("--device", default="auto")
-    ap.add_argument("--parse-requests", type=int, default=30,
+    ap.add_argument("--parse-requests", type=int, default=100,
                     help="rank 0: p50 latency of N single 10k-line POST /parse requests after the timed loop (0 = off)")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="server front end for p50")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")

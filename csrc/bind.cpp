@@ -118,6 +118,7 @@ static ScanPass scan_pass_from(const py::tuple& t) {
   }
   S.bm_off = t[11].cast<int>();
   S.rid_off = t[12].cast<int>();
+  S.am_off = t.size() > 13 ? t[13].cast<int>() : -1;
   return S;
 }
 

@@ -87,14 +87,10 @@ LP_HD void scan_emit(const ScanPass& S, int g, uint32_t m, int64_t line, Emit&& 
 
 // exact walk of ONE line on the global tables (Matcher.find: accept before a final line
 // terminator, at end of line, or before any byte). Shared by the host twin and the device.
-// G_MAX: the device instantiates it with the pass's group count so every S.x[g] index is a
-// compile-time constant (a runtime-indexed kernel-argument array was copied to scratch memory)
-template <int G_MAX = 4, typename Emit>
+template <typename Emit>
 LP_HD void scan_line_exact(const ScanPass& S, const uint32_t* bm, const uint8_t* s, int n, int64_t line, Emit&& emit) {
   const int ft = n - final_term_len(s, n);
-#pragma unroll
-  for (int g = 0; g < G_MAX; ++g) {
-    if (g >= S.ngroups) break;
+  for (int g = 0; g < S.ngroups; ++g) {
     uint32_t st = S.init_state[g], acc = 0;
     for (int t = 0; t < n; ++t) {
       if (t == ft) acc |= scan_fin(S, g, st, 1);
@@ -138,42 +134,72 @@ __device__ __forceinline__ uint32_t crlf_bits(uint32_t w, uint32_t nx) {
   return nz_bytes(w ^ 0x0D0D0D0Du) & nz_bytes(__builtin_amdgcn_alignbyte(nx, w, 1) ^ 0x0A0A0A0Au);
 }
 
-// byte j (0..16) of the 5-word window w0..w4; j is a compile-time constant in the unrolled
-// loops below, so the window stays in registers (an indexed array lived in scratch memory)
-__device__ __forceinline__ uint32_t win_byte(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, int j) {
-  const uint32_t w = j < 4 ? w0 : j < 8 ? w1 : j < 12 ? w2 : j < 16 ? w3 : w4;
-  return (w >> (8 * (j & 3))) & 0xFFu;
-}
-
 // exact re-walk of one 16-byte block [p0, p0 + 16) of a run (rare path): bytes outside
 // [p_lo, p_end) are skipped, a separator '\r' is held, '\n' ends line l
 template <typename Emit>
-__device__ __forceinline__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, uint32_t w0, uint32_t w1, uint32_t w2,
-                                 uint32_t w3, uint32_t w4, int64_t p0, int64_t p_lo, int64_t p_end, int64_t x0,
-                                 int64_t x1, const int64_t* line_start, int g, uint32_t st, Emit&& emit) {
+__device__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, const uint32_t (&w)[5], int64_t p0,
+                                 int64_t p_lo, int64_t p_end, int64_t x0, int64_t x1,
+                                 const int64_t* line_start, int g, uint32_t st, Emit&& emit) {
   int64_t l = x0;
   const int64_t first = p0 > p_lo ? p0 : p_lo;
   while (l + 1 < x1 && line_start[l + 1] <= first) ++l;
   if (p0 <= p_lo) st = S.init_state[g];
   uint32_t lacc = 0;
-#pragma unroll
   for (int j = 0; j < 16; ++j) {
     const int64_t pos = p0 + j;
-    if (pos >= p_lo && pos < p_end) {
-      const uint32_t c = win_byte(w0, w1, w2, w3, w4, j);
-      const uint32_t nx = win_byte(w0, w1, w2, w3, w4, j + 1);
-      const uint32_t col = (c == 0x0Du && nx == 0x0Au) ? 0u : ((bm[c] >> (8 * g)) & 0xFFu) >> 1;
-      const uint32_t e = scan_step(S, g, st, col);
-      lacc |= e >> 16;
-      st = e & 0xFFFFu;
-      if (col == 1u) {
-        scan_emit(S, g, lacc, l, emit);
-        lacc = 0;
-        ++l;
-      }
+    if (pos < p_lo || pos >= p_end) continue;
+    const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    const uint32_t nx = (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFFu;
+    const uint32_t col = (c == 0x0Du && nx == 0x0Au) ? 0u : ((bm[c] >> (8 * g)) & 0xFFu) >> 1;
+    const uint32_t e = scan_step(S, g, st, col);
+    lacc |= e >> 16;
+    st = e & 0xFFFFu;
+    if (col == 1u) {
+      scan_emit(S, g, lacc, l, emit);
+      lacc = 0;
+      ++l;
     }
   }
   scan_emit(S, g, lacc, l < x1 ? l : x1 - 1, emit);
+}
+
+// exact re-walk of one 16-byte block through the LDS rows (the same transitions as the hot
+// walk) with each transition's accept mask from the global mask table laid out like the rows:
+// the 16 mask loads depend only on the LDS chain, so they are all in flight together (the
+// exact-table walk above is a chain of 16 dependent global loads). xr = group g's row at p0;
+// positions outside [p_lo, p_end) are walked but not attributed, as in the hot walk.
+template <bool CRLF, typename Emit>
+__device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32_t (&w)[5], uint32_t hold, int64_t p0,
+                                                 int64_t p_lo, int64_t p_end, int64_t x0, int64_t x1,
+                                                 const int64_t* __restrict__ line_start, int g, uint32_t xr,
+                                                 Emit&& emit) {
+  const uint16_t* __restrict__ am = reinterpret_cast<const uint16_t*>(S.blob + S.am_off);
+  // in-range positions of the block; a run holds <= SCAN_RUN lines, so an in-range byte belongs
+  // to line l0 + k, k = in-range '\n's before it (0..3): per-line masks accumulate branch-free
+  const int lo = p_lo > p0 ? (int)(p_lo - p0) : 0;
+  const int hi = p_end - p0 < 16 ? (int)(p_end - p0) : 16;
+  const uint32_t inr = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, k = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+    if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;
+    const uint32_t b = (lds_ld32(c * 4) >> (8 * g)) & 0xFFu;
+    const uint32_t m = ((inr >> j) & 1u) ? (uint32_t)am[(xr + b) >> 1] : 0u;
+    a0 |= k == 0 ? m : 0u;
+    a1 |= k == 1 ? m : 0u;
+    a2 |= k == 2 ? m : 0u;
+    a3 |= k == 3 ? m : 0u;
+    k += (b == 2u && ((inr >> j) & 1u)) ? 1u : 0u;     // column 1 = '\n': the line ends here
+    xr = lds_ld16(xr + b);
+  }
+  int64_t l = x0;
+  const int64_t first = p0 > p_lo ? p0 : p_lo;
+  while (l + 1 < x1 && line_start[l + 1] <= first) ++l;
+  const uint32_t acc[4] = {a0, a1, a2, a3};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (acc[q]) scan_emit(S, g, acc[q], l + q < x1 ? l + q : x1 - 1, emit);
 }
 
 // the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold
@@ -190,7 +216,7 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
   for (int64_t p0 = a0; p0 < p_end; p0 += 16) {
     const uint4 nxt = blk[1];
     ++blk;
-    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};   // constant indices only
+    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
     uint32_t hold = 0;                    // CRLF: byte j of the block is a separator '\r'
     if constexpr (CRLF) {
 #pragma unroll
@@ -219,11 +245,18 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
     // rare: a state that can accept was visited -- exact re-walk of this block, only for the
     // groups that visited one (a group below its threshold cannot accept anywhere in the block;
     // each re-walk is a chain of 16 dependent global loads, ~8 us, on a request's critical path)
+    uint32_t hotm = 0;
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-      if (mx[g] >= (uint32_t)S.thr[g])
-        scan_block_exact(S, sm, w[0], w[1], w[2], w[3], w[4], p0, p_lo, p_end, x0, x1, line_start, g,
-                         scan_state_of(S, g, xs[g]), emit);
+    for (int g = 0; g < G; ++g) hotm |= (mx[g] >= (uint32_t)S.thr[g] ? 1u : 0u) << g;
+    while (hotm) {      // one inlined re-walk, runtime group (an unrolled copy per group cost VGPRs)
+      const int g = __builtin_ctz(hotm);
+      hotm &= hotm - 1;
+      uint32_t xg = xs[0];
+#pragma unroll
+      for (int q = 1; q < G; ++q)
+        if (g == q) xg = xs[q];
+      scan_block_masks<CRLF>(S, w, hold, p0, p_lo, p_end, x0, x1, line_start, g, xg, emit);
+    }
     cur = nxt;
   }
 }
@@ -270,7 +303,7 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
     if (p_lo > 0 && text[p_lo - 1] != '\n') fast = false;   // e.g. a document boundary in a batch
     if (!at_zero) fast = false;
     if (!fast) {     // rare: exact per-line walks
-      for (int64_t x = x0; x < x1; ++x) scan_line_exact<G>(S, sm, text + line_start[x], line_len[x], x, emit);
+      for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
       continue;
     }
     if (crlf)

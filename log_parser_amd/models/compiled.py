@@ -494,9 +494,23 @@ class CompiledLibrary:
             rid[16 * g:16 * g + len(regs)] = regs
         rid_off = off
         parts.append(rid)
+        off += rid.size
+        # accept masks laid out like the LDS rows (u16 entry i of the LDS blob <-> mask i): the
+        # device's exact re-walk follows the LDS rows and loads each transition's mask with an
+        # address known from the LDS chain -- 16 independent global loads per block instead of a
+        # chain of 16 dependent exact-row loads
+        am = np.zeros(2 * lds_words, np.uint16)
+        for g, (regs, d) in enumerate(groups):
+            ns, ncol, stride = d["nstates"], meta["ncol"][g], meta["stride"][g]
+            b0 = meta["row_base"][g] // 2
+            ex = exact[g].reshape(ns, ncol)
+            idx = b0 + np.arange(ns, dtype=np.int64)[:, None] * stride + np.arange(ncol, dtype=np.int64)[None, :]
+            am[idx] = (ex >> np.uint32(16)).astype(np.uint16)
+        am_off = off
+        parts.append(am.view(np.uint32))
         blob = np.concatenate(parts)
         return dict(blob=blob, lds_words=lds_words, ngroups=len(groups), gt_off=tuple(gt_off),
-                    fin_off=tuple(fin_off), bm_off=0, rid_off=rid_off,
+                    fin_off=tuple(fin_off), bm_off=0, rid_off=rid_off, am_off=am_off,
                     regs=[x for regs, _ in groups for x in regs], **{k: tuple(v) for k, v in meta.items()})
 
     def _build_prefilter(self):
@@ -607,7 +621,7 @@ class CompiledLibrary:
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
         t["scan_passes"] = [(b.data_ptr(), p["lds_words"], p["ngroups"], p["row_base"], p["stride"], p["thr"],
                              p["init_row"], p["init_state"], p["ncol"], p["gt_off"], p["fin_off"], p["bm_off"],
-                             p["rid_off"]) for b, p in zip(t["scan_blobs"], self.scan_passes)]
+                             p["rid_off"], p["am_off"]) for b, p in zip(t["scan_blobs"], self.scan_passes)]
         t["conf"], t["sev"] = T(self.conf), T(self.sev)
         t["sev_index"] = T(self.sev_index)
         t["ctx_before"], t["ctx_after"] = T(self.ctx_before), T(self.ctx_after)

@@ -1,17 +1,30 @@
 """Per-step kernel table from a rocprofv3 rocpd database (sqlite; the default output format of
-ROCm 7): python tools/kstats_db.py run_results.db [steps] [top]."""
+ROCm 7): python tools/kstats_db.py run_results.db [steps] [top] [--median].
+
+--median: per step = median duration x calls / steps (robust to the few launches that queue
+behind the copy stream's H2D blit under the profiler); otherwise total duration / steps."""
 import sqlite3
+import statistics
 import sys
 
-db = sys.argv[1]
-steps = float(sys.argv[2]) if len(sys.argv) > 2 else 4.0
-top = int(sys.argv[3]) if len(sys.argv) > 3 else 25
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+median = "--median" in sys.argv
+db = args[0]
+steps = float(args[1]) if len(args) > 1 else 4.0
+top = int(args[2]) if len(args) > 2 else 25
 c = sqlite3.connect(db)
 cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
 name = "name" if "name" in cols else "kernel_name"
-rows = c.execute(f"select {name}, count(*), sum(end - start) from kernels group by {name} "
-                 f"order by sum(end - start) desc").fetchall()
+durs = {}
+for n, s, e in c.execute(f"select {name}, start, end from kernels"):
+    durs.setdefault(n, []).append(e - s)
+rows = []
+for n, d in durs.items():
+    t = statistics.median(d) * len(d) if median else sum(d)
+    rows.append((n, len(d), t, statistics.median(d)))
+rows.sort(key=lambda r: -r[2])
 tot = sum(r[2] for r in rows)
-for n, k, t in rows[:top]:
-    print(f"{t / steps / 1e3:9.1f} us/step {k / steps:7.1f}/step  {n[:90]}")
-print(f"total {tot / steps / 1e3:.1f} us/step over {sum(r[1] for r in rows) / steps:.0f} launches/step")
+for n, k, t, m in rows[:top]:
+    print(f"{t / steps / 1e3:9.1f} us/step {k / steps:7.1f}/step  med {m / 1e3:8.1f}  {n[:90]}")
+print(f"total {tot / steps / 1e3:.1f} us/step over {sum(r[1] for r in rows) / steps:.0f} launches/step"
+      + (" (median-based)" if median else ""))

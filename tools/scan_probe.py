@@ -30,20 +30,21 @@ def main():
         "lines10": ("abcdefghi\n") * 10_000,
         "one_line": "x" * 100 + "\n",
     }
+    texts["bulk_1m25"] = texts["request"] * 125          # bulk path: 1024-thread blocks, 4-line runs
     out = {}
     for name, t in texts.items():
         data = t.encode()
         text, n = eng.stage_text(data)
         ls, ll = K.split_lines(text, n)
         L = ls.numel()
-        buf = torch.empty(1 << 16, dtype=torch.int64, device=dev)
+        buf = torch.empty(1 << 20, dtype=torch.int64, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
         st = torch.cuda.current_stream().cuda_stream
         lat = []
-        for i in range(60):
+        for i in range(30 if L > 100_000 else 60):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            N.scan_multi(text.data_ptr(), n, ls.data_ptr(), ll.data_ptr(), L, sp, buf.data_ptr(), 1 << 16, cnt.data_ptr(),
+            N.scan_multi(text.data_ptr(), n, ls.data_ptr(), ll.data_ptr(), L, sp, buf.data_ptr(), 1 << 20, cnt.data_ptr(),
                          eng.scan_grid(sp), st, True)
             b.record()
             torch.cuda.synchronize()

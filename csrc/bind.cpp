@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <cstring>
 #include <memory>
 
 #include "io/docs.h"
@@ -18,6 +19,7 @@
 #include "kernels/lp_api.h"
 #include "kernels/lp_host.h"
 #include "regex/jregex.h"
+#include "runtime/request.h"
 
 namespace py = pybind11;
 using namespace lp;
@@ -519,6 +521,64 @@ PYBIND11_MODULE(_lpnative, m) {
   // ---- post-match pipeline (lp_post.hip); device calls return the workspace bytes they need and
   // only run when ws_bytes suffices
   m.def("bits_for", &bits_for);
+
+  // ---- native request runner (csrc/runtime/request.cpp): the device half of a batch in one call
+  py::class_<RequestRunner>(m, "RequestRunner")
+      .def(py::init([](py::tuple pf, py::tuple dfa, py::list scans, py::list grids, uint64_t scan_regs, int n_scan_regs,
+                       py::tuple st12, py::tuple sp, py::tuple ev5, int R, int npat, int nkeys, int nseq, int ctx_trans,
+                       int ctx_acc, int pf_grid, int device) {
+             RequestStatic S;
+             S.pf = pf_from(pf);
+             S.dfa = dfa_from(dfa);
+             for (auto h : scans) S.scans.push_back(scan_pass_from(h.cast<py::tuple>()));
+             for (auto h : grids) S.scan_grids.push_back(h.cast<int>());
+             if (S.scans.size() != S.scan_grids.size()) throw std::invalid_argument("RequestRunner: one grid per scan pass");
+             S.scan_regs = P<const int32_t>(scan_regs);
+             S.n_scan_regs = n_scan_regs;
+             int i = 0;
+             auto nx = [&]() { return st12[i++].cast<uint64_t>(); };
+             ScoreTables& T = S.st;
+             T.conf = P<const double>(nx()); T.sev = P<const double>(nx());
+             T.ctx_before = P<const int32_t>(nx()); T.ctx_after = P<const int32_t>(nx());
+             T.sec_off = P<const int32_t>(nx()); T.sec_reg = P<const int32_t>(nx()); T.sec_w = P<const int32_t>(nx());
+             T.sec_weight = P<const double>(nx());
+             T.seq_off = P<const int32_t>(nx()); T.seq_bonus = P<const double>(nx());
+             T.seq_ev_off = P<const int32_t>(nx()); T.seq_ev_reg = P<const int32_t>(nx());
+             S.sp = sp_from(sp);
+             EvTables& E = S.ev;
+             E.prim_off = P<const int64_t>(ev5[0].cast<uint64_t>());
+             E.prim_pats = P<const int32_t>(ev5[1].cast<uint64_t>());
+             E.freq_key = P<const int32_t>(ev5[2].cast<uint64_t>());
+             E.ctx_before = P<const int32_t>(ev5[3].cast<uint64_t>());
+             E.ctx_after = P<const int32_t>(ev5[4].cast<uint64_t>());
+             E.nkeys = nkeys;
+             E.pbits = bits_for(std::max(npat, 1));
+             S.R = R; S.npat = npat; S.nkeys = nkeys; S.nseq = nseq;
+             S.ctx_trans = ctx_trans; S.ctx_acc = ctx_acc; S.pf_grid = pf_grid; S.device = device;
+             return new RequestRunner(S);
+           }))
+      .def("run", [](RequestRunner& r, uint64_t text, int64_t nbytes, uint64_t starts, uint64_t lens, int64_t L,
+                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> lo,
+                     py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
+                     double evict_before, double now, uint64_t stream) {
+        const FreqRing R = ring_from(ring);
+        const int D = (int)lo.shape(0);
+        int64_t ne;
+        {
+          py::gil_scoped_release nogil;
+          ne = r.run(P<uint8_t>(text), nbytes, P<const int64_t>(starts), P<const int32_t>(lens), L, lo.data(), hi.data(),
+                     g0.data(), n.data(), D, R, evict_before, now, stream);
+        }
+        py::array_t<uint8_t> out((py::ssize_t)r.result_bytes());
+        std::memcpy(out.mutable_data(), r.result(), r.result_bytes());
+        const RequestCounts& c = r.counts();
+        py::dict d;
+        d["lines"] = c.lines; d["gram_hits"] = c.gram; d["prefilter_candidates"] = c.cand; d["scan_hits"] = c.ver;
+        d["hits"] = c.hits; d["events"] = c.events;
+        return py::make_tuple(ne, out, d);
+      });
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
   py::class_<HttpServer>(m, "HttpServer")

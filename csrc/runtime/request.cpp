@@ -1,0 +1,252 @@
+// Native request runner (see request.h).
+#include "runtime/request.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+namespace lp {
+
+namespace {
+
+constexpr int64_t kNlTile = 16384;   // ops/kernels.py NL_TILE / TEXT_PAD
+constexpr int64_t kTextPad = 64;
+constexpr int kBlkShift = 12;        // LINE_BLK_SHIFT
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error in request runner (") + what + "): " + hipGetErrorString(e));
+}
+
+int64_t padded_len(int64_t n) { return ((std::max<int64_t>(n, 1) + kNlTile - 1) / kNlTile) * kNlTile + kTextPad; }
+
+size_t up256(size_t n) { return (n + 255) & ~size_t(255); }
+
+// a device or pinned buffer that only grows (between runs, when nothing in flight uses it)
+template <bool Pinned>
+void grow(uint8_t*& p, size_t& cap, size_t need) {
+  if (need <= cap) return;
+  const size_t n = std::max(need + need / 4, size_t(1) << 20);
+  if (p) check(Pinned ? hipHostFree(p) : hipFree(p), "free");
+  p = nullptr;
+  cap = 0;
+  check(Pinned ? hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault)
+               : hipMalloc(reinterpret_cast<void**>(&p), n), "alloc");
+  cap = n;
+}
+
+}  // namespace
+
+RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
+  check(hipSetDevice(S_.device), "set device");
+  check(hipHostMalloc(reinterpret_cast<void**>(&cnt_host_), 8 * sizeof(int64_t), hipHostMallocDefault), "pinned counters");
+}
+
+RequestRunner::~RequestRunner() {
+  if (ws_) (void)hipFree(ws_);
+  if (post_ws_) (void)hipFree(post_ws_);
+  if (up_host_) (void)hipHostFree(up_host_);
+  if (res_host_) (void)hipHostFree(res_host_);
+  if (cnt_host_) (void)hipHostFree(cnt_host_);
+}
+
+uint8_t* RequestRunner::dev(size_t bytes) {
+  uint8_t* p = ws_ ? ws_ + ws_used_ : nullptr;
+  ws_used_ += up256(bytes);
+  return p;
+}
+
+int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
+                           const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
+                           int D, const FreqRing& ring, double evict_before, double now, uint64_t stream) {
+  check(hipSetDevice(S_.device), "set device");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t tsize = padded_len(nbytes);
+  std::memset(host_text + nbytes, 0, (size_t)(tsize - nbytes));       // vector loads past the end
+  const int64_t nblk = (std::max<int64_t>(nbytes, 1) >> kBlkShift) + 2;
+  const int lbits = bits_for(std::max<int64_t>(L, 1)), rbits = bits_for(std::max(S_.R, 1));
+  const int K1 = std::max(S_.nkeys, 1);
+
+  // segments -> one pinned staging area -> one H2D copy
+  const size_t seg_bytes = up256(4 * (size_t)D) * 2 + up256(8 * (size_t)D) * 2;
+  grow<true>(up_host_, up_cap_, seg_bytes);
+  std::memcpy(up_host_, seg_lo, 4 * (size_t)D);
+  std::memcpy(up_host_ + up256(4 * (size_t)D), seg_hi, 4 * (size_t)D);
+  std::memcpy(up_host_ + 2 * up256(4 * (size_t)D), seg_g0, 8 * (size_t)D);
+  std::memcpy(up_host_ + 2 * up256(4 * (size_t)D) + up256(8 * (size_t)D), seg_n, 8 * (size_t)D);
+
+  // window eviction first (FrequencyState.carry): the totals it leaves are this batch's carry
+  freq_evict(ring, evict_before, stream, true);
+
+  RequestCounts c;
+  c.lines = L;
+  int64_t ne = 0, nh = 0;
+  uint8_t* text = nullptr;
+  int32_t* blk = nullptr;
+  int64_t *ls = nullptr, *hits = nullptr, *hit_off = nullptr, *ev_cnt = nullptr, *ev_end = nullptr, *cnt = nullptr;
+  int64_t *gh = nullptr, *cand = nullptr, *ver = nullptr;
+  int32_t *ll = nullptr, *hit_line = nullptr, *dlo = nullptr, *dhi = nullptr;
+  int64_t *dg0 = nullptr, *dn = nullptr;
+  EvTables ev = S_.ev;
+  for (int attempt = 0;; ++attempt) {
+    const int64_t cap_g = (int64_t)((double)L * rate_gram_ * 1.25) + 512;
+    const int64_t cap_c = (int64_t)((double)L * rate_cand_ * 1.25) + 512;
+    const int64_t cap_v = (int64_t)((double)L * rate_ver_ * 1.25) + 512;
+    const int64_t n = cap_c + cap_v;
+    // layout (two passes: measure, then carve from a workspace large enough)
+    for (int pass = 0; pass < 2; ++pass) {
+      ws_used_ = 0;
+      text = dev((size_t)tsize);
+      ls = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(L, 1)));
+      ll = reinterpret_cast<int32_t*>(dev(4 * (size_t)std::max<int64_t>(L, 1)));
+      uint8_t* segs = dev(seg_bytes);
+      dlo = reinterpret_cast<int32_t*>(segs);
+      dhi = reinterpret_cast<int32_t*>(segs + up256(4 * (size_t)D));
+      dg0 = reinterpret_cast<int64_t*>(segs + 2 * up256(4 * (size_t)D));
+      dn = reinterpret_cast<int64_t*>(segs + 2 * up256(4 * (size_t)D) + up256(8 * (size_t)D));
+      blk = reinterpret_cast<int32_t*>(dev(4 * (size_t)nblk));
+      cnt = reinterpret_cast<int64_t*>(dev(8 * 8));
+      gh = reinterpret_cast<int64_t*>(dev(8 * (size_t)cap_g));
+      cand = reinterpret_cast<int64_t*>(dev(8 * (size_t)cap_c));
+      ver = reinterpret_cast<int64_t*>(dev(8 * (size_t)cap_v));
+      hits = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
+      hit_line = reinterpret_cast<int32_t*>(dev(4 * (size_t)n));
+      hit_off = reinterpret_cast<int64_t*>(dev(8 * (size_t)(S_.R + 1)));
+      ev_cnt = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
+      ev_end = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
+      if (pass == 0) {
+        if (ws_used_ > ws_cap_) {   // nothing in flight uses the workspace: previous runs synced
+          check(hipStreamSynchronize(st), "sync before growth");
+          grow<false>(ws_, ws_cap_, ws_used_);
+        }
+      }
+    }
+    // inputs: packed text, line index, segments (all pinned -> async)
+    check(hipMemcpyAsync(text, host_text, (size_t)tsize, hipMemcpyHostToDevice, st), "text H2D");
+    if (L > 0) {
+      check(hipMemcpyAsync(ls, starts, 8 * (size_t)L, hipMemcpyHostToDevice, st), "starts H2D");
+      check(hipMemcpyAsync(ll, lens, 4 * (size_t)L, hipMemcpyHostToDevice, st), "lens H2D");
+    }
+    check(hipMemcpyAsync(dlo, up_host_, seg_bytes, hipMemcpyHostToDevice, st), "segments H2D");
+    ev.seg_lo = dlo;
+    ev.seg_hi = dhi;
+    ev.own_lo = dlo;
+    ev.own_hi = dhi;
+    ev.nseg = D;
+    check(hipMemsetAsync(cnt, 0, 8 * sizeof(int64_t), st), "counters");
+    unsigned long long* c0 = reinterpret_cast<unsigned long long*>(cnt);
+
+    // matchers: literal-free scan groups, single-DFA scans, then the literal prefilter chain
+    for (size_t i = 0; i < S_.scans.size(); ++i)
+      scan_multi_dev(text, nbytes, ls, ll, L, S_.scans[i], ver, cap_v, c0 + 2, S_.scan_grids[i], stream);
+    if (S_.n_scan_regs)
+      scan_dev(text, ls, ll, L, S_.scan_regs, S_.n_scan_regs, S_.dfa, ver, cap_v, c0 + 2, stream);
+    blk_index_dev(ls, L, nblk, blk, stream);
+    prefilter_dev(text, nbytes, S_.pf, ls, L, gh, cap_g, c0, S_.pf_grid, stream);
+    pf_verify_dev(gh, cap_g, text, nbytes, S_.pf, ls, L, blk, cand, cap_c, c0 + 1, stream, c0,
+                  (int)std::max<int64_t>(16, std::min<int64_t>(8192, nbytes >> 13)));
+
+    // hit CSR + event counts: the pipeline reads the matchers' device counters itself
+    HitsArgs A;
+    A.cand = cand; A.n = n; A.pre_from = cap_c;
+    A.cand2 = ver; A.dcount = c0 + 1;
+    A.lbits = lbits; A.rbits = rbits; A.R = S_.R;
+    A.text = text; A.ls = ls; A.ll = ll; A.dfa = S_.dfa; A.ev = ev;
+    A.hits = hits; A.hit_line = hit_line; A.hit_off = hit_off; A.ev_cnt = ev_cnt; A.ev_end = ev_end;
+    A.counters = cnt + 3;
+    size_t need = hits_dev(A, post_ws_, post_cap_, stream);
+    if (need > post_cap_) {       // post_ws_ is not used by anything in flight yet
+      check(hipStreamSynchronize(st), "sync before growth");
+      grow<false>(post_ws_, post_cap_, need);
+      hits_dev(A, post_ws_, post_cap_, stream);
+    }
+    check(hipMemcpyAsync(cnt_host_, cnt, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st), "counters D2H");
+    check(hipStreamSynchronize(st), "counters");              // the one mid-batch host read
+    c.gram = cnt_host_[0]; c.cand = cnt_host_[1]; c.ver = cnt_host_[2];
+    nh = cnt_host_[3]; ne = cnt_host_[4];
+    c.hits = nh; c.events = ne;
+    const bool ok = c.gram <= cap_g && c.cand <= cap_c && c.ver <= cap_v;
+    // MatchArena.learn: overflow -> the exact rates; otherwise decay toward what batches need
+    auto learn = [&](double& rate, int64_t v) {
+      const double r = (double)v / (double)std::max<int64_t>(L, 1);
+      rate = std::max(std::max(r, ok ? rate * 0.5 : rate), 1e-4);
+    };
+    learn(rate_gram_, c.gram);
+    learn(rate_cand_, c.cand);
+    learn(rate_ver_, c.ver);
+    if (ok) break;
+    if (attempt > 8) throw std::runtime_error("request runner: matcher capacities did not converge");
+  }
+
+  // events, context features, frequency ranks (results buffer receives line / pattern / segment /
+  // counts), then the fused fp64 score into the same buffer
+  const size_t res = 20 * (size_t)ne + 8 * (size_t)K1;
+  const size_t ws2 = up256(res) + 2 * up256(8 * (size_t)std::max<int64_t>(ne, 1)) +
+                     up256((size_t)std::max<int64_t>(L, 1)) + up256((size_t)std::max(S_.nseq, 1));
+  const size_t base = ws_used_;
+  if (base + ws2 > ws_cap_) {
+    // the workspace must grow while the inputs / CSR it holds are still needed: move them. The
+    // stream is idle (counter read above), so copy the used prefix into the new allocation.
+    uint8_t* old = ws_;
+    size_t old_used = base;
+    uint8_t* nw = nullptr;
+    const size_t ncap = std::max((base + ws2) * 5 / 4, size_t(1) << 20);
+    check(hipMalloc(reinterpret_cast<void**>(&nw), ncap), "alloc");
+    check(hipMemcpyAsync(nw, old, old_used, hipMemcpyDeviceToDevice, st), "workspace move");
+    check(hipStreamSynchronize(st), "workspace move");
+    check(hipFree(old), "free");
+    const ptrdiff_t d = nw - old;
+    auto mv = [&](auto*& q) { q = reinterpret_cast<std::remove_reference_t<decltype(q)>>(reinterpret_cast<uint8_t*>(q) + d); };
+    mv(text); mv(ls); mv(ll); mv(dlo); mv(dhi); mv(dg0); mv(dn); mv(hits); mv(hit_line); mv(hit_off); mv(ev_cnt); mv(ev_end);
+    ev.seg_lo = dlo; ev.seg_hi = dhi; ev.own_lo = dlo; ev.own_hi = dhi;
+    ws_ = nw;
+    ws_cap_ = ncap;
+  }
+  ws_used_ = base;
+  uint8_t* out = dev(res);
+  double* score = reinterpret_cast<double*>(out);
+  int64_t* freq_counts = reinterpret_cast<int64_t*>(out + 8 * (size_t)ne);
+  int32_t* ev_line = reinterpret_cast<int32_t*>(out + 8 * (size_t)ne + 8 * (size_t)K1);
+  int32_t* ev_pat = ev_line + ne;
+  int32_t* ev_seg = ev_pat + ne;
+  int64_t* ev_rank = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(ne, 1)));
+  int64_t* ev_fkey = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(ne, 1)));
+  uint8_t* feat = dev((size_t)std::max<int64_t>(L, 1));
+  uint8_t* seq_carry = dev((size_t)std::max(S_.nseq, 1));
+  if (S_.nkeys == 0) check(hipMemsetAsync(freq_counts, 0, 8, st), "counts");
+  if (L == 0) check(hipMemsetAsync(feat, 0, 1, st), "feat");
+  check(hipMemsetAsync(seq_carry, 0, (size_t)std::max(S_.nseq, 1), st), "seq carry");
+
+  EventsArgs E;
+  E.ctx_trans = S_.ctx_trans; E.ctx_acc = S_.ctx_acc;
+  E.hits = nh ? hits : nullptr; E.nh = nh; E.ev_cnt = ev_cnt; E.ev_end = ev_end; E.ne = ne; E.L = L; E.lbits = lbits;
+  E.ev = ev; E.text = text; E.ls = ls; E.ll = ll; E.dfa = S_.dfa;
+  E.ev_line = ev_line; E.ev_pat = ev_pat; E.ev_seg = ev_seg; E.ev_rank = ev_rank; E.ev_fkey = ev_fkey;
+  E.freq_counts = freq_counts; E.feat = feat; E.cov = nullptr;
+  size_t need = events_dev(E, post_ws_, post_cap_, stream);
+  if (need > post_cap_) {          // the stream is idle since the counter read: safe to replace
+    grow<false>(post_ws_, post_cap_, need);
+    events_dev(E, post_ws_, post_cap_, stream);
+  }
+  if (ne > 0) {
+    ScoreTables T = S_.st;
+    T.seq_carry = seq_carry;
+    T.hit_off = hit_off; T.hit_line = hit_line; T.feat = feat;
+    T.seg_lo = dlo; T.seg_hi = dhi; T.seg_own_lo = dlo; T.seg_g0 = dg0; T.seg_n = dn;
+    const FreqIn F{ev_rank, ev_fkey, ring.tot};
+    score_dev(ev_line, ev_pat, ev_seg, F, ne, T, S_.sp, score, nullptr, stream);
+  }
+  // this batch's per-key counts enter the window (after its own scoring: penalty before record)
+  if (S_.nkeys > 0) freq_record(freq_counts, S_.nkeys, now, ring, stream, true);
+  grow<true>(res_host_, res_cap_, res);
+  check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
+  check(hipStreamSynchronize(st), "results");
+  res_bytes_ = res;
+  counts_ = c;
+  return ne;
+}
+
+}  // namespace lp

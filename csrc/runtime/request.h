@@ -1,0 +1,84 @@
+// Native request runner: the whole device half of one continuous batch (Engine.device_batch on
+// a GPU that owns its frequency state) in one C++ call with the GIL released.
+//
+// The Python orchestration of the same stages (log_parser_amd/engine.py prepare / finish,
+// ops/kernels.py match_and_hits / post_events) spent ~150 us of host time per 10k-line request
+// on tuple conversion, ~15 torch allocations and ~20 launches from Python -- more than the
+// GPU's ~200 us of kernels, so the GPU idled between them. Here every buffer comes from one
+// grow-only device workspace, the tables are converted once, and the stages are launched back to
+// back on the caller's stream: H2D of the packed text + line index + segments, frequency
+// eviction, matchers (prefilter + verify, scan groups), hit CSR + events (ONE counter read),
+// events / context features / ranks, fp64 score, frequency record, ONE results read.
+//
+// Semantics are those of the Python path it replaces (which stays for the CPU backend, tracing,
+// host-fallback regexes, MFMA scan groups and engines sharing a frequency state): same kernels,
+// same arguments, same order on the stream.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "kernels/lp_api.h"
+
+namespace lp {
+
+struct RequestStatic {
+  PfTables pf;
+  DfaPool dfa;
+  std::vector<ScanPass> scans;
+  std::vector<int> scan_grids;      // persistent grid of each scan pass
+  const int32_t* scan_regs = nullptr;
+  int n_scan_regs = 0;
+  ScoreTables st;                   // per-pattern tables (batch fields filled per run)
+  ScoreParams sp;
+  EvTables ev;                      // static fields (segments filled per run)
+  int R = 0;                        // regexes
+  int npat = 0;
+  int nkeys = 0;                    // frequency keys
+  int nseq = 0;                     // sequence-event slots
+  int ctx_trans = 0, ctx_acc = 0;   // context DFA extents (LDS staging)
+  int pf_grid = 1;
+  int device = 0;
+};
+
+struct RequestCounts {
+  int64_t gram = 0, cand = 0, ver = 0, hits = 0, events = 0, lines = 0;
+};
+
+class RequestRunner {
+ public:
+  explicit RequestRunner(const RequestStatic& S);
+  ~RequestRunner();
+  RequestRunner(const RequestRunner&) = delete;
+  RequestRunner& operator=(const RequestRunner&) = delete;
+
+  // host_text: pinned packed bytes [0, nbytes) with room up to the padded length (zero-filled
+  // here); starts / lens: pinned line index (L lines); seg_*: D documents (host arrays).
+  // ring: the device frequency state; evict_before / now: its eviction horizon and record time.
+  // Returns the number of events; the results stay in result() until the next run:
+  // [score f64 x ne | freq counts i64 x max(nkeys, 1) | line i32 x ne | pattern i32 x ne | seg i32 x ne]
+  int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
+              const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
+              const FreqRing& ring, double evict_before, double now, uint64_t stream);
+  const uint8_t* result() const { return res_host_; }
+  size_t result_bytes() const { return res_bytes_; }
+  const RequestCounts& counts() const { return counts_; }
+
+ private:
+  uint8_t* dev(size_t bytes);          // carve from the device workspace (grown between runs)
+  RequestStatic S_;
+  // matcher capacity rates per line (as ops/kernels.py MatchArena)
+  double rate_gram_ = 0.08, rate_cand_ = 0.03, rate_ver_ = 0.01;
+  uint8_t* ws_ = nullptr;              // device workspace
+  size_t ws_cap_ = 0, ws_used_ = 0, ws_need_ = 0;
+  uint8_t* post_ws_ = nullptr;         // rocPRIM / post-pipeline scratch
+  size_t post_cap_ = 0;
+  uint8_t* up_host_ = nullptr;         // pinned upload staging (segments)
+  size_t up_cap_ = 0;
+  uint8_t* res_host_ = nullptr;        // pinned results
+  size_t res_cap_ = 0, res_bytes_ = 0;
+  int64_t* cnt_host_ = nullptr;        // pinned counters
+  RequestCounts counts_;
+};
+
+}  // namespace lp

@@ -35,6 +35,7 @@ SOURCES = [
     ("io/docs.cpp", "cpp"),
     ("io/json_in.cpp", "cpp"),
     ("io/http_server.cpp", "cpp"),
+    ("runtime/request.cpp", "cpp"),
     ("bind.cpp", "cpp"),
 ]
 

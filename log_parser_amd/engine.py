@@ -303,6 +303,7 @@ class Engine:
         self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
         # second compute stream: literal-free scans overlap the prefilter chain (K.match_and_hits)
         self._side = None
+        self._runner = None                         # N.RequestRunner (built on first use) / False
         if self.device.type == "cuda":
             props = torch.cuda.get_device_properties(self.device)
             self.n_cus = int(props.multi_processor_count)
@@ -688,11 +689,15 @@ class Engine:
             return
         hb, ls_h, ll_h, dl, n = job.staged
         tm = job.tm
+        verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
+        if turn is None and self._runner_ok(job, verbose, tm):
+            # the whole device half in one native call (csrc/runtime/request.cpp)
+            self._run_native(job, dl, n)
+            return
         if tm is not None:
             self._start(tm)
         text = self._stage_h2d(job.stage.buf, n)
         lo, hi, g0, nn = Segments.doc_arrays(dl)
-        verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
         pinned_idx = job.n_lines >= 0 and self.device.type == "cuda"
         if pinned_idx:                     # line index straight from the pinned stage (no host copy)
             ls = job.stage.starts(job.n_lines).to(self.device, non_blocking=True)
@@ -746,6 +751,58 @@ class Engine:
             self._log_events(res, dl)
         if tm is not None:
             job.timings = res.timings
+
+    def _runner_ok(self, job: "BatchJob", verbose: bool, tm) -> bool:
+        """The native request runner covers the common device configuration: a GPU engine owning
+        its frequency window, DFA context features, no host-fallback or MFMA scan regexes, the
+        line index in the pinned stage, no tracing / per-match logging."""
+        if self._runner is False or tm is not None or verbose or job.n_lines < 0:
+            return False
+        if self._runner is None:
+            ok = (self.device.type == "cuda" and self.freq_on_device and not self.lib.host_regs
+                  and self.context_engine != "mfma" and bool(self.config.get("engine.native-runner", True))
+                  and not any(g.numel() for g in self.tabs["nfa_scan_lists"].values()))
+            if not ok:
+                self._runner = False
+                return False
+            t = self.tabs
+            ptr = lambda k: t[k].data_ptr()  # noqa: E731
+            st12 = tuple(ptr(k) for k in ("conf", "sev", "ctx_before", "ctx_after", "sec_off", "sec_reg", "sec_w",
+                                          "sec_weight", "seq_off", "seq_bonus", "seq_ev_off", "seq_ev_reg"))
+            ev5 = tuple(ptr(k) for k in ("prim_off", "prim_pats", "freq_key", "ctx_before", "ctx_after"))
+            dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            self._runner = N.RequestRunner(
+                t["pf"], t["dfa"], list(t["scan_passes"]), [self.scan_grid(sp) for sp in t["scan_passes"]],
+                ptr("scan_regs"), t["scan_regs"].numel(), st12, self.sp_tuple, ev5, self.lib.n_regexes,
+                len(self.lib.patterns), len(self.lib.freq_ids), self.lib.n_seq_events, self.lib.ctx_dfa_extent[0],
+                self.lib.ctx_dfa_extent[1], self.pf_grid, dev)
+        return True
+
+    def _run_native(self, job: "BatchJob", dl, n: int) -> None:
+        """Engine.device_batch through N.RequestRunner: same kernels and order as prepare / finish
+        (H2D, eviction, matchers, ONE counter read, events + features + ranks, score, record,
+        ONE results read); the frequency state's host bookkeeping stays here, under its lock."""
+        lo, hi, g0, nn = Segments.doc_arrays(dl)
+        fr = self.freq
+        K = len(self.lib.freq_ids)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        st = job.stage
+        with fr._lock:
+            if K:
+                fr._ensure_room(K)
+            evict_before = fr._now() - fr.window_s      # carry_tensor()
+            now = fr._now()                              # record_tensor()
+            ne, out, counts = self._runner.run(st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(),
+                                               st.lens(job.n_lines).data_ptr(), job.n_lines, lo, hi, g0, nn,
+                                               fr._ring(), evict_before, now, stream)
+            if K:
+                fr._tail_bound += K
+        self.arena.last = counts
+        k1 = max(K, 1)
+        a, b = 8 * ne, 8 * ne + 8 * k1
+        job.ev = (out[b:b + 4 * ne].view(np.int32), out[b + 4 * ne:b + 8 * ne].view(np.int32),
+                  out[b + 8 * ne:b + 12 * ne].view(np.int32), out[:a].view(np.float64),
+                  out[a:a + 8 * K].view(np.int64))
 
     def emit_batch(self, job: "BatchJob") -> List[bytes]:
         """Stage 3 (host): every response of the batch (uuid, metadata, events with context lines,

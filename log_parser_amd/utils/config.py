@@ -52,6 +52,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # (off: the cross-stream event wait cost more than the overlap saved -- 10k-line request
     # 0.362 -> 0.382-0.408 ms on the MI355X box, tools/engine_phases.py A/B)
     "engine.scan-stream": (False, bool),
+    # the device half of a batch in one native call (csrc/runtime/request.cpp) when applicable
+    "engine.native-runner": (True, bool),
     # serve a batch from the CPU backend when the device path fails (availability)
     "engine.fallback-cpu": (True, bool),
     # per-stage HIP-event timers, reported in response metadata as stageTimingsMs (opt-in)

@@ -194,3 +194,25 @@ def test_batch_edge_cases_gpu_equal_cpu_and_golden(gpu_device):
         for a, b in zip(o["events"], g["events"]):
             assert math.isclose(a["score"], b["score"], rel_tol=1e-12)
     assert sum(len(o["events"]) for o in outs["gpu"]) > 10
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_native_runner_equals_python_orchestration(gpu_device, seed):
+    """csrc/runtime/request.cpp runs the same kernels as Engine.prepare / finish: over a sequence
+    of batches (the device frequency window evolving through them, one batch large enough to
+    overflow the first matcher capacities) the responses are identical with the runner on and
+    off, and the runner path really ran."""
+    import json
+    sets, trig = make_library(300, seed=seed)
+    lib = CompiledLibrary(sets, ScoringParams())
+    batches = [[make_log(3000, trig, seed=seed * 10 + i, hit_rate=0.05) for i in range(3)],
+               [make_log(20_000, trig, seed=seed * 10 + 5, hit_rate=0.3)],
+               [make_log(500, trig, seed=seed * 10 + 6, hit_rate=0.02), "", "\n"]]
+    outs = {}
+    for on in (True, False):
+        cfg = Config.load(overrides={"engine.device": str(gpu_device), "engine.native-runner": on})
+        eng = Engine(lib, cfg, device=gpu_device)
+        outs[on] = [[_strip(json.loads(o)) for o in eng.analyze_batch_json(b)] for b in batches]
+        assert (eng._runner is not None and eng._runner is not False) == on
+    assert outs[True] == outs[False]
+    assert sum(len(o["events"]) for b in outs[True] for o in b) > 100

@@ -25,8 +25,11 @@ inline int& host_threads() {
 
 class HostPool {
  public:
+  // one pool per calling thread: the serving pipeline packs batch k+1 while it emits batch k, and
+  // a single shared pool ran whichever region came second serially (10k-request burst: 140k ->
+  // 111k req/s). Never destroyed: workers may outlive static teardown.
   static HostPool& get() {
-    static HostPool* p = new HostPool();   // never destroyed: workers may outlive static teardown
+    static thread_local HostPool* p = new HostPool();
     return *p;
   }
 
@@ -71,7 +74,7 @@ class HostPool {
 
   HostPool() {
     const unsigned hw = std::thread::hardware_concurrency();
-    nworkers_ = (int)std::max(1u, std::min(hw ? hw : 8u, 8u)) - 1;
+    nworkers_ = (int)std::max(1u, std::min(hw ? hw : 8u, 16u)) - 1;
     for (int i = 0; i < nworkers_; ++i) std::thread([this, i] { loop(i); }).detach();
   }
 

@@ -526,8 +526,9 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<RequestRunner>(m, "RequestRunner")
       .def(py::init([](py::tuple pf, py::tuple dfa, py::list scans, py::list grids, uint64_t scan_regs, int n_scan_regs,
                        py::tuple st12, py::tuple sp, py::tuple ev5, int R, int npat, int nkeys, int nseq, int ctx_trans,
-                       int ctx_acc, int pf_grid, int device) {
+                       int ctx_acc, int pf_grid, int device, bool device_counts) {
              RequestStatic S;
+             S.device_counts = device_counts;
              S.pf = pf_from(pf);
              S.dfa = dfa_from(dfa);
              for (auto h : scans) S.scans.push_back(scan_pass_from(h.cast<py::tuple>()));
@@ -556,7 +557,10 @@ PYBIND11_MODULE(_lpnative, m) {
              S.R = R; S.npat = npat; S.nkeys = nkeys; S.nseq = nseq;
              S.ctx_trans = ctx_trans; S.ctx_acc = ctx_acc; S.pf_grid = pf_grid; S.device = device;
              return new RequestRunner(S);
-           }))
+           }), py::arg("pf"), py::arg("dfa"), py::arg("scans"), py::arg("grids"), py::arg("scan_regs"),
+           py::arg("n_scan_regs"), py::arg("st12"), py::arg("sp"), py::arg("ev5"), py::arg("R"), py::arg("npat"),
+           py::arg("nkeys"), py::arg("nseq"), py::arg("ctx_trans"), py::arg("ctx_acc"), py::arg("pf_grid"),
+           py::arg("device"), py::arg("device_counts") = true)
       .def("run", [](RequestRunner& r, uint64_t text, int64_t nbytes, uint64_t starts, uint64_t lens, int64_t L,
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> lo,
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,
@@ -577,7 +581,7 @@ PYBIND11_MODULE(_lpnative, m) {
         py::dict d;
         d["lines"] = c.lines; d["gram_hits"] = c.gram; d["prefilter_candidates"] = c.cand; d["scan_hits"] = c.ver;
         d["hits"] = c.hits; d["events"] = c.events;
-        return py::make_tuple(ne, out, d);
+        return py::make_tuple(ne, out, d, r.stride());
       });
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)

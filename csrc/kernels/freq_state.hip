@@ -41,9 +41,10 @@ __global__ __launch_bounds__(FREQ_EVICT_THREADS) void k_freq_evict(FreqRing R, d
 }
 
 __global__ __launch_bounds__(256) void k_freq_record(const int64_t* __restrict__ counts, int K, double now,
-                                                     FreqRing R) {
+                                                     FreqRing R, RecordGate G) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
+  if (G.cnt && (G.cnt[0] > G.cap[0] || G.cnt[1] > G.cap[1] || G.cnt[2] > G.cap[2] || G.cnt[4] > G.cap[3])) return;
   const int64_t c = counts[k];
   if (c <= 0) return;
   const int64_t p = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(R.ht + 1), 1ull);
@@ -71,11 +72,12 @@ void freq_evict(const FreqRing& R, double horizon, uint64_t stream, bool dev) {
   R.ht[0] = h;
 }
 
-void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev) {
+void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev,
+                 const RecordGate& gate) {
   if (K <= 0) return;
   if (dev) {
     hipLaunchKernelGGL(k_freq_record, dim3((K + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       counts, K, now, R);
+                       counts, K, now, R, gate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in freq_record");
     return;

@@ -18,7 +18,8 @@ void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* lin
               const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
               uint64_t stream);
 void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,
-               const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream);
+               const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream,
+               const int64_t* dn = nullptr);   // dn: device event count (n = capacity)
 
 void seq_chain_dev(const int32_t* slot_seq, const int32_t* seq_ev_off, const int32_t* seq_ev_reg,
                    const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
@@ -82,7 +83,14 @@ struct FreqRing {
   uint8_t* seen;      // [K]
 };
 void freq_evict(const FreqRing& R, double horizon, uint64_t stream, bool dev);
-void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev);
+// gate (device, optional): record only when cnt[0..2] <= cap[0..2] and cnt[4] <= cap[3] -- the
+// request runner's matcher / event capacities held, so the counts are this batch's real ones
+struct RecordGate {
+  const int64_t* cnt = nullptr;
+  int64_t cap[4] = {0, 0, 0, 0};
+};
+void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev,
+                 const RecordGate& gate = RecordGate());
 }  // namespace lp
 
 // ---- line index (line_index.hip)
@@ -186,6 +194,9 @@ struct EventsArgs {
   const uint8_t* text; const int64_t* ls; const int32_t* ll;
   DfaPool dfa;
   int ctx_trans, ctx_acc;    // table extents of the 4 context DFAs (pool entries 0..3), for LDS staging
+  // device-count mode (request path): [nh, ne] on the device; nh / ne above are then capacities
+  // and a batch over them leaves the outputs unset (the caller re-runs with host counts)
+  const int64_t* dcounts = nullptr;
   // outputs
   int32_t* ev_line; int32_t* ev_pat; int32_t* ev_seg; int64_t* ev_rank; int64_t* ev_fkey;
   int64_t* freq_counts;      // [nkeys]
@@ -197,6 +208,10 @@ int bits_for(int64_t n);
 // device versions return the workspace bytes they need; they only run when ws_bytes suffices
 size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
 size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
+// capacities of the single-workgroup request path (events, lines): a batch within them can run
+// the event stage in device-count mode
+int64_t request_event_cap();
+int64_t request_line_cap();
 void blk_index_dev(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk, uint64_t stream);
 void hits_host(const HitsArgs& A);
 void events_host(const EventsArgs& A);

@@ -301,9 +301,9 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t* __restrict__ text,
 __global__ __launch_bounds__(256) void k_score(const int32_t* __restrict__ ev_line, const int32_t* __restrict__ ev_pat,
                                                const int32_t* __restrict__ ev_seg, FreqIn F,
                                                int64_t n, ScoreTables T, ScoreParams S, double* __restrict__ out,
-                                               double* __restrict__ factors) {
+                                               double* __restrict__ factors, const int64_t* __restrict__ dn) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || (dn && i >= dn[0])) return;
   out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], freq_before(F, i), factors ? factors + 7 * i : nullptr);
 }
 
@@ -418,10 +418,11 @@ void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* lin
 }
 
 void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,
-               const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream) {
+               const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream,
+               const int64_t* dn) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_score, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ev_line, ev_pat, ev_seg,
-                     F, n, T, S, out, factors);
+                     F, n, T, S, out, factors, dn);
   LP_CHECK(hipGetLastError());
 }
 

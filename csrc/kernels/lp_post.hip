@@ -450,14 +450,20 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
   __shared__ int32_t diff[SB_MAX_LINES + 1];
   __shared__ int64_t scratch[SB_THREADS / 64 + 1];
   const EvTables& E = A.ev;
-  const int64_t ne = A.ne, L = A.L;
+  int64_t ne = A.ne, nh = A.nh;
+  const int64_t L = A.L;
+  if (A.dcounts) {                 // device-count mode: A.ne / A.nh are capacities
+    nh = A.dcounts[0];
+    ne = A.dcounts[1];
+    if (ne > A.ne || nh > A.nh) return;   // over capacity: the host re-runs with read counts
+  }
   const int np = sb_pow2(ne);
   for (int i = threadIdx.x; i <= L; i += SB_THREADS) diff[i] = 0;
   for (int k = threadIdx.x; k < E.nkeys; k += SB_THREADS) A.freq_counts[k] = 0;
   for (int i = threadIdx.x; i < np; i += SB_THREADS) keys[i] = LP_PAD_KEY;
   __syncthreads();
   // expand: each hit's events, keyed (line, pattern)
-  for (int64_t i = threadIdx.x; i < A.nh; i += SB_THREADS) {
+  for (int64_t i = threadIdx.x; i < nh; i += SB_THREADS) {
     const int64_t c = A.ev_cnt[i];
     if (c == 0) continue;
     const int64_t k = A.hits[i];
@@ -512,6 +518,8 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
 
 bool hits_small_ok(const HitsArgs& A) { return A.n > 0 && A.n <= SB_MAX; }
 bool events_small_ok(const EventsArgs& A) { return A.ne <= SB_MAX && A.L <= SB_MAX_LINES; }
+int64_t request_event_cap() { return SB_MAX; }
+int64_t request_line_cap() { return SB_MAX_LINES; }
 
 // coarse byte-block -> line index (blk[b] = line containing byte b << 12), one lane per block
 __global__ __launch_bounds__(256) void k_blk_index(const int64_t* __restrict__ ls, int64_t L, int64_t nblk,

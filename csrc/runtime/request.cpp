@@ -69,6 +69,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   const int64_t nblk = (std::max<int64_t>(nbytes, 1) >> kBlkShift) + 2;
   const int lbits = bits_for(std::max<int64_t>(L, 1)), rbits = bits_for(std::max(S_.R, 1));
   const int K1 = std::max(S_.nkeys, 1);
+  const int64_t ecap_small = request_event_cap();
 
   // segments -> one pinned staging area -> one H2D copy
   const size_t seg_bytes = up256(4 * (size_t)D) * 2 + up256(8 * (size_t)D) * 2;
@@ -83,21 +84,68 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
 
   RequestCounts c;
   c.lines = L;
-  int64_t ne = 0, nh = 0;
+  int64_t ne = 0, nh = 0, stride = 0;
   uint8_t* text = nullptr;
   int32_t* blk = nullptr;
   int64_t *ls = nullptr, *hits = nullptr, *hit_off = nullptr, *ev_cnt = nullptr, *ev_end = nullptr, *cnt = nullptr;
   int64_t *gh = nullptr, *cand = nullptr, *ver = nullptr;
   int32_t *ll = nullptr, *hit_line = nullptr, *dlo = nullptr, *dhi = nullptr;
   int64_t *dg0 = nullptr, *dn = nullptr;
+  // event-stage buffers (results layout: [score f64 x E | counts i64 x K1 | line | pattern | seg i32 x E])
+  uint8_t *out = nullptr, *feat = nullptr, *seq_carry = nullptr;
+  int64_t *ev_rank = nullptr, *ev_fkey = nullptr;
   EvTables ev = S_.ev;
+  bool done = false;   // events + score already ran (device-count mode)
+  auto carve_events = [&](int64_t E) {
+    out = dev(20 * (size_t)E + 8 * (size_t)K1);
+    ev_rank = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(E, 1)));
+    ev_fkey = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(E, 1)));
+    feat = dev((size_t)std::max<int64_t>(L, 1));
+    seq_carry = dev((size_t)std::max(S_.nseq, 1));
+  };
+  // events, context features, frequency ranks into the results buffer, then the fused fp64
+  // score; `dcnt` = device [nh, ne] (device-count mode, E = capacity) or null (E = ne read back)
+  auto run_events = [&](int64_t E, int64_t nh_cap, const int64_t* dcnt) {
+    double* score = reinterpret_cast<double*>(out);
+    int64_t* freq_counts = reinterpret_cast<int64_t*>(out + 8 * (size_t)E);
+    int32_t* ev_line = reinterpret_cast<int32_t*>(out + 8 * (size_t)E + 8 * (size_t)K1);
+    int32_t* ev_pat = ev_line + E;
+    int32_t* ev_seg = ev_pat + E;
+    if (S_.nkeys == 0) check(hipMemsetAsync(freq_counts, 0, 8, st), "counts");
+    if (L == 0) check(hipMemsetAsync(feat, 0, 1, st), "feat");
+    check(hipMemsetAsync(seq_carry, 0, (size_t)std::max(S_.nseq, 1), st), "seq carry");
+    EventsArgs A;
+    A.ctx_trans = S_.ctx_trans; A.ctx_acc = S_.ctx_acc;
+    A.hits = (nh_cap || dcnt) ? hits : nullptr; A.nh = nh_cap; A.ev_cnt = ev_cnt; A.ev_end = ev_end; A.ne = E; A.L = L;
+    A.lbits = lbits; A.ev = ev; A.text = text; A.ls = ls; A.ll = ll; A.dfa = S_.dfa;
+    A.ev_line = ev_line; A.ev_pat = ev_pat; A.ev_seg = ev_seg; A.ev_rank = ev_rank; A.ev_fkey = ev_fkey;
+    A.freq_counts = freq_counts; A.feat = feat; A.cov = nullptr; A.dcounts = dcnt;
+    const size_t need = events_dev(A, post_ws_, post_cap_, stream);
+    if (need > post_cap_) {
+      if (dcnt) throw std::runtime_error("request runner: event workspace not pre-sized");
+      grow<false>(post_ws_, post_cap_, need);   // the stream is idle since the counter read
+      events_dev(A, post_ws_, post_cap_, stream);
+    }
+    if (E > 0) {
+      ScoreTables T = S_.st;
+      T.seq_carry = seq_carry;
+      T.hit_off = hit_off; T.hit_line = hit_line; T.feat = feat;
+      T.seg_lo = dlo; T.seg_hi = dhi; T.seg_own_lo = dlo; T.seg_g0 = dg0; T.seg_n = dn;
+      const FreqIn F{ev_rank, ev_fkey, ring.tot};
+      score_dev(ev_line, ev_pat, ev_seg, F, E, T, S_.sp, score, nullptr, stream, dcnt ? dcnt + 1 : nullptr);
+    }
+    return freq_counts;
+  };
+
   for (int attempt = 0;; ++attempt) {
     const int64_t cap_g = (int64_t)((double)L * rate_gram_ * 1.25) + 512;
     const int64_t cap_c = (int64_t)((double)L * rate_cand_ * 1.25) + 512;
     const int64_t cap_v = (int64_t)((double)L * rate_ver_ * 1.25) + 512;
     const int64_t n = cap_c + cap_v;
-    // layout (two passes: measure, then carve from a workspace large enough)
-    for (int pass = 0; pass < 2; ++pass) {
+    // device-count mode: a request on the single-workgroup paths runs matching, CSR, events,
+    // score and the (gated) frequency record without the mid-batch host read
+    const bool fast = S_.device_counts && attempt == 0 && n <= ecap_small && L <= request_line_cap();
+    for (int pass = 0; pass < 2; ++pass) {   // measure, then carve from a workspace large enough
       ws_used_ = 0;
       text = dev((size_t)tsize);
       ls = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(L, 1)));
@@ -117,12 +165,15 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       hit_off = reinterpret_cast<int64_t*>(dev(8 * (size_t)(S_.R + 1)));
       ev_cnt = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
       ev_end = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
-      if (pass == 0) {
-        if (ws_used_ > ws_cap_) {   // nothing in flight uses the workspace: previous runs synced
-          check(hipStreamSynchronize(st), "sync before growth");
-          grow<false>(ws_, ws_cap_, ws_used_);
-        }
+      if (fast) carve_events(ecap_small);
+      if (pass == 0 && ws_used_ > ws_cap_) {   // nothing in flight uses the workspace here
+        check(hipStreamSynchronize(st), "sync before growth");
+        grow<false>(ws_, ws_cap_, ws_used_);
       }
+    }
+    if (fast && post_cap_ < 4 * (size_t)std::max<int64_t>(L, 1) + 4096) {   // events' coverage array
+      check(hipStreamSynchronize(st), "sync before growth");
+      grow<false>(post_ws_, post_cap_, 4 * (size_t)std::max<int64_t>(L, 1) + 4096);
     }
     // inputs: packed text, line index, segments (all pinned -> async)
     check(hipMemcpyAsync(text, host_text, (size_t)tsize, hipMemcpyHostToDevice, st), "text H2D");
@@ -159,12 +210,26 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     A.counters = cnt + 3;
     size_t need = hits_dev(A, post_ws_, post_cap_, stream);
     if (need > post_cap_) {       // post_ws_ is not used by anything in flight yet
+      if (fast) throw std::runtime_error("request runner: hit workspace on the small path");
       check(hipStreamSynchronize(st), "sync before growth");
       grow<false>(post_ws_, post_cap_, need);
       hits_dev(A, post_ws_, post_cap_, stream);
     }
+    if (fast) {
+      int64_t* fc = run_events(ecap_small, n, cnt + 3);
+      if (S_.nkeys > 0) {
+        RecordGate G;
+        G.cnt = cnt;
+        G.cap[0] = cap_g; G.cap[1] = cap_c; G.cap[2] = cap_v; G.cap[3] = ecap_small;
+        freq_record(fc, S_.nkeys, now, ring, stream, true, G);
+      }
+      const size_t res = 20 * (size_t)ecap_small + 8 * (size_t)K1;
+      grow<true>(res_host_, res_cap_, res);
+      check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
+      res_bytes_ = res;
+    }
     check(hipMemcpyAsync(cnt_host_, cnt, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st), "counters D2H");
-    check(hipStreamSynchronize(st), "counters");              // the one mid-batch host read
+    check(hipStreamSynchronize(st), "counters");   // fast: the only host read; else the mid-batch one
     c.gram = cnt_host_[0]; c.cand = cnt_host_[1]; c.ver = cnt_host_[2];
     nh = cnt_host_[3]; ne = cnt_host_[4];
     c.hits = nh; c.events = ne;
@@ -177,74 +242,50 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     learn(rate_gram_, c.gram);
     learn(rate_cand_, c.cand);
     learn(rate_ver_, c.ver);
-    if (ok) break;
+    if (ok && fast && ne <= ecap_small) {    // recorded through the gate; results already read
+      done = true;
+      stride = ecap_small;
+      break;
+    }
+    if (ok && !fast) break;
     if (attempt > 8) throw std::runtime_error("request runner: matcher capacities did not converge");
   }
 
-  // events, context features, frequency ranks (results buffer receives line / pattern / segment /
-  // counts), then the fused fp64 score into the same buffer
-  const size_t res = 20 * (size_t)ne + 8 * (size_t)K1;
-  const size_t ws2 = up256(res) + 2 * up256(8 * (size_t)std::max<int64_t>(ne, 1)) +
-                     up256((size_t)std::max<int64_t>(L, 1)) + up256((size_t)std::max(S_.nseq, 1));
-  const size_t base = ws_used_;
-  if (base + ws2 > ws_cap_) {
-    // the workspace must grow while the inputs / CSR it holds are still needed: move them. The
-    // stream is idle (counter read above), so copy the used prefix into the new allocation.
-    uint8_t* old = ws_;
-    size_t old_used = base;
-    uint8_t* nw = nullptr;
-    const size_t ncap = std::max((base + ws2) * 5 / 4, size_t(1) << 20);
-    check(hipMalloc(reinterpret_cast<void**>(&nw), ncap), "alloc");
-    check(hipMemcpyAsync(nw, old, old_used, hipMemcpyDeviceToDevice, st), "workspace move");
-    check(hipStreamSynchronize(st), "workspace move");
-    check(hipFree(old), "free");
-    const ptrdiff_t d = nw - old;
-    auto mv = [&](auto*& q) { q = reinterpret_cast<std::remove_reference_t<decltype(q)>>(reinterpret_cast<uint8_t*>(q) + d); };
-    mv(text); mv(ls); mv(ll); mv(dlo); mv(dhi); mv(dg0); mv(dn); mv(hits); mv(hit_line); mv(hit_off); mv(ev_cnt); mv(ev_end);
-    ev.seg_lo = dlo; ev.seg_hi = dhi; ev.own_lo = dlo; ev.own_hi = dhi;
-    ws_ = nw;
-    ws_cap_ = ncap;
+  if (!done) {
+    // host-count mode: event buffers sized by the counts just read
+    const size_t res = 20 * (size_t)ne + 8 * (size_t)K1;
+    const size_t ws2 = up256(res) + 2 * up256(8 * (size_t)std::max<int64_t>(ne, 1)) +
+                       up256((size_t)std::max<int64_t>(L, 1)) + up256((size_t)std::max(S_.nseq, 1));
+    const size_t base = ws_used_;
+    if (base + ws2 > ws_cap_) {
+      // the workspace must grow while the inputs / CSR it holds are still needed: move them. The
+      // stream is idle (counter read above), so copy the used prefix into the new allocation.
+      uint8_t* old = ws_;
+      uint8_t* nw = nullptr;
+      const size_t ncap = std::max((base + ws2) * 5 / 4, size_t(1) << 20);
+      check(hipMalloc(reinterpret_cast<void**>(&nw), ncap), "alloc");
+      check(hipMemcpyAsync(nw, old, base, hipMemcpyDeviceToDevice, st), "workspace move");
+      check(hipStreamSynchronize(st), "workspace move");
+      check(hipFree(old), "free");
+      const ptrdiff_t d = nw - old;
+      auto mv = [&](auto*& q) { q = reinterpret_cast<std::remove_reference_t<decltype(q)>>(reinterpret_cast<uint8_t*>(q) + d); };
+      mv(text); mv(ls); mv(ll); mv(dlo); mv(dhi); mv(dg0); mv(dn); mv(hits); mv(hit_line); mv(hit_off); mv(ev_cnt); mv(ev_end);
+      ev.seg_lo = dlo; ev.seg_hi = dhi; ev.own_lo = dlo; ev.own_hi = dhi;
+      ws_ = nw;
+      ws_cap_ = ncap;
+    }
+    ws_used_ = base;
+    carve_events(ne);
+    int64_t* fc = run_events(ne, nh, nullptr);
+    // this batch's per-key counts enter the window (after its own scoring: penalty before record)
+    if (S_.nkeys > 0) freq_record(fc, S_.nkeys, now, ring, stream, true);
+    grow<true>(res_host_, res_cap_, res);
+    check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
+    check(hipStreamSynchronize(st), "results");
+    res_bytes_ = res;
+    stride = ne;
   }
-  ws_used_ = base;
-  uint8_t* out = dev(res);
-  double* score = reinterpret_cast<double*>(out);
-  int64_t* freq_counts = reinterpret_cast<int64_t*>(out + 8 * (size_t)ne);
-  int32_t* ev_line = reinterpret_cast<int32_t*>(out + 8 * (size_t)ne + 8 * (size_t)K1);
-  int32_t* ev_pat = ev_line + ne;
-  int32_t* ev_seg = ev_pat + ne;
-  int64_t* ev_rank = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(ne, 1)));
-  int64_t* ev_fkey = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(ne, 1)));
-  uint8_t* feat = dev((size_t)std::max<int64_t>(L, 1));
-  uint8_t* seq_carry = dev((size_t)std::max(S_.nseq, 1));
-  if (S_.nkeys == 0) check(hipMemsetAsync(freq_counts, 0, 8, st), "counts");
-  if (L == 0) check(hipMemsetAsync(feat, 0, 1, st), "feat");
-  check(hipMemsetAsync(seq_carry, 0, (size_t)std::max(S_.nseq, 1), st), "seq carry");
-
-  EventsArgs E;
-  E.ctx_trans = S_.ctx_trans; E.ctx_acc = S_.ctx_acc;
-  E.hits = nh ? hits : nullptr; E.nh = nh; E.ev_cnt = ev_cnt; E.ev_end = ev_end; E.ne = ne; E.L = L; E.lbits = lbits;
-  E.ev = ev; E.text = text; E.ls = ls; E.ll = ll; E.dfa = S_.dfa;
-  E.ev_line = ev_line; E.ev_pat = ev_pat; E.ev_seg = ev_seg; E.ev_rank = ev_rank; E.ev_fkey = ev_fkey;
-  E.freq_counts = freq_counts; E.feat = feat; E.cov = nullptr;
-  size_t need = events_dev(E, post_ws_, post_cap_, stream);
-  if (need > post_cap_) {          // the stream is idle since the counter read: safe to replace
-    grow<false>(post_ws_, post_cap_, need);
-    events_dev(E, post_ws_, post_cap_, stream);
-  }
-  if (ne > 0) {
-    ScoreTables T = S_.st;
-    T.seq_carry = seq_carry;
-    T.hit_off = hit_off; T.hit_line = hit_line; T.feat = feat;
-    T.seg_lo = dlo; T.seg_hi = dhi; T.seg_own_lo = dlo; T.seg_g0 = dg0; T.seg_n = dn;
-    const FreqIn F{ev_rank, ev_fkey, ring.tot};
-    score_dev(ev_line, ev_pat, ev_seg, F, ne, T, S_.sp, score, nullptr, stream);
-  }
-  // this batch's per-key counts enter the window (after its own scoring: penalty before record)
-  if (S_.nkeys > 0) freq_record(freq_counts, S_.nkeys, now, ring, stream, true);
-  grow<true>(res_host_, res_cap_, res);
-  check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
-  check(hipStreamSynchronize(st), "results");
-  res_bytes_ = res;
+  stride_ = stride;
   counts_ = c;
   return ne;
 }

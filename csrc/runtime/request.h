@@ -39,6 +39,7 @@ struct RequestStatic {
   int ctx_trans = 0, ctx_acc = 0;   // context DFA extents (LDS staging)
   int pf_grid = 1;
   int device = 0;
+  bool device_counts = true;        // requests: no mid-batch host read (see run())
 };
 
 struct RequestCounts {
@@ -55,14 +56,16 @@ class RequestRunner {
   // host_text: pinned packed bytes [0, nbytes) with room up to the padded length (zero-filled
   // here); starts / lens: pinned line index (L lines); seg_*: D documents (host arrays).
   // ring: the device frequency state; evict_before / now: its eviction horizon and record time.
-  // Returns the number of events; the results stay in result() until the next run:
-  // [score f64 x ne | freq counts i64 x max(nkeys, 1) | line i32 x ne | pattern i32 x ne | seg i32 x ne]
+  // Returns the number of events ne; the results stay in result() until the next run:
+  // [score f64 x E | freq counts i64 x max(nkeys, 1) | line i32 x E | pattern i32 x E | seg i32 x E]
+  // with E = stride() >= ne (the event capacity of a device-count-mode request, else ne).
   int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
               const FreqRing& ring, double evict_before, double now, uint64_t stream);
   const uint8_t* result() const { return res_host_; }
   size_t result_bytes() const { return res_bytes_; }
   const RequestCounts& counts() const { return counts_; }
+  int64_t stride() const { return stride_; }
 
  private:
   uint8_t* dev(size_t bytes);          // carve from the device workspace (grown between runs)
@@ -79,6 +82,7 @@ class RequestRunner {
   size_t res_cap_ = 0, res_bytes_ = 0;
   int64_t* cnt_host_ = nullptr;        // pinned counters
   RequestCounts counts_;
+  int64_t stride_ = 0;
 };
 
 }  // namespace lp

@@ -775,7 +775,8 @@ class Engine:
                 t["pf"], t["dfa"], list(t["scan_passes"]), [self.scan_grid(sp) for sp in t["scan_passes"]],
                 ptr("scan_regs"), t["scan_regs"].numel(), st12, self.sp_tuple, ev5, self.lib.n_regexes,
                 len(self.lib.patterns), len(self.lib.freq_ids), self.lib.n_seq_events, self.lib.ctx_dfa_extent[0],
-                self.lib.ctx_dfa_extent[1], self.pf_grid, dev)
+                self.lib.ctx_dfa_extent[1], self.pf_grid, dev,
+                bool(self.config.get("engine.runner-device-counts", False)))
         return True
 
     def _run_native(self, job: "BatchJob", dl, n: int) -> None:
@@ -792,16 +793,16 @@ class Engine:
                 fr._ensure_room(K)
             evict_before = fr._now() - fr.window_s      # carry_tensor()
             now = fr._now()                              # record_tensor()
-            ne, out, counts = self._runner.run(st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(),
+            ne, out, counts, E = self._runner.run(st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(),
                                                st.lens(job.n_lines).data_ptr(), job.n_lines, lo, hi, g0, nn,
                                                fr._ring(), evict_before, now, stream)
             if K:
                 fr._tail_bound += K
         self.arena.last = counts
         k1 = max(K, 1)
-        a, b = 8 * ne, 8 * ne + 8 * k1
-        job.ev = (out[b:b + 4 * ne].view(np.int32), out[b + 4 * ne:b + 8 * ne].view(np.int32),
-                  out[b + 8 * ne:b + 12 * ne].view(np.int32), out[:a].view(np.float64),
+        a, b = 8 * E, 8 * E + 8 * k1          # E: the results' event stride (>= ne)
+        job.ev = (out[b:b + 4 * ne].view(np.int32), out[b + 4 * E:b + 4 * E + 4 * ne].view(np.int32),
+                  out[b + 8 * E:b + 8 * E + 4 * ne].view(np.int32), out[:8 * ne].view(np.float64),
                   out[a:a + 8 * K].view(np.int64))
 
     def emit_batch(self, job: "BatchJob") -> List[bytes]:

@@ -216,3 +216,20 @@ def test_native_runner_equals_python_orchestration(gpu_device, seed):
         assert (eng._runner is not None and eng._runner is not False) == on
     assert outs[True] == outs[False]
     assert sum(len(o["events"]) for b in outs[True] for o in b) > 100
+
+
+def test_native_runner_device_counts_equals_host_counts(gpu_device):
+    """The runner's device-count mode (no mid-batch host read, frequency record gated on the
+    capacities) gives the same responses as its host-count mode, including a batch whose matcher
+    counts overflow the first capacities (gate closed, re-run)."""
+    import json
+    sets, trig = make_library(300, seed=9)
+    lib = CompiledLibrary(sets, ScoringParams())
+    batches = [[make_log(2000, trig, seed=90 + i, hit_rate=0.05)] for i in range(3)] + \
+              [[make_log(8000, trig, seed=95, hit_rate=0.4)], [make_log(1000, trig, seed=96, hit_rate=0.05)]]
+    outs = {}
+    for dc in (True, False):
+        cfg = Config.load(overrides={"engine.device": str(gpu_device), "engine.runner-device-counts": dc})
+        eng = Engine(lib, cfg, device=gpu_device)
+        outs[dc] = [[_strip(json.loads(o)) for o in eng.analyze_batch_json(b)] for b in batches]
+    assert outs[True] == outs[False]

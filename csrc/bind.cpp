@@ -566,14 +566,14 @@ PYBIND11_MODULE(_lpnative, m) {
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
-                     double evict_before, double now, uint64_t stream) {
+                     double evict_before, double now, uint64_t stream, int64_t host_cap) {
         const FreqRing R = ring_from(ring);
         const int D = (int)lo.shape(0);
         int64_t ne;
         {
           py::gil_scoped_release nogil;
           ne = r.run(P<uint8_t>(text), nbytes, P<const int64_t>(starts), P<const int32_t>(lens), L, lo.data(), hi.data(),
-                     g0.data(), n.data(), D, R, evict_before, now, stream);
+                     g0.data(), n.data(), D, R, evict_before, now, stream, host_cap);
         }
         py::array_t<uint8_t> out((py::ssize_t)r.result_bytes());
         std::memcpy(out.mutable_data(), r.result(), r.result_bytes());
@@ -582,7 +582,10 @@ PYBIND11_MODULE(_lpnative, m) {
         d["lines"] = c.lines; d["gram_hits"] = c.gram; d["prefilter_candidates"] = c.cand; d["scan_hits"] = c.ver;
         d["hits"] = c.hits; d["events"] = c.events;
         return py::make_tuple(ne, out, d, r.stride());
-      });
+      }, py::arg("text"), py::arg("nbytes"), py::arg("starts"), py::arg("lens"), py::arg("L"), py::arg("lo"),
+         py::arg("hi"), py::arg("g0"), py::arg("n"), py::arg("ring"), py::arg("evict_before"), py::arg("now"),
+         py::arg("stream"), py::arg("host_cap") = 0)
+      .def("upload_bytes", &RequestRunner::upload_bytes);
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
   py::class_<HttpServer>(m, "HttpServer")

@@ -1,6 +1,8 @@
 #include "io/docs.h"
 
 #include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -44,6 +46,10 @@ struct NlBuf {
 // positions and stored unconditionally -- no branch per newline (the bit loop mispredicted on
 // every ~100-byte line). Blocks with more than 8 newlines take a short scalar loop. Returns the
 // bytes consumed (a multiple of 64, stops early when `nl` lacks 64 + 8 free slots).
+// NT: dst is 64-byte aligned and the stores stream past the cache (the destination is the
+// pinned staging buffer the GPU's DMA reads next, never this core: no read-for-ownership of the
+// destination lines).
+template <bool NT>
 __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vbmi2,bmi,bmi2,popcnt")))
 static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int64_t base, NlBuf& nl) {
   alignas(64) static const uint8_t kIota[64] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
@@ -57,7 +63,10 @@ static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int
   const int64_t room = nl.cap - 72;
   for (; i + 64 <= n && k <= room; i += 64) {
     const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(src + i));
-    _mm512_storeu_si512(reinterpret_cast<void*>(dst + i), v);
+    if constexpr (NT)
+      _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i), v);
+    else
+      _mm512_storeu_si512(reinterpret_cast<void*>(dst + i), v);
     const uint64_t m = _mm512_cmpeq_epi8_mask(v, NL);
     const __m512i offs = _mm512_maskz_compress_epi8(m, iota);
     const __m512i pos = _mm512_add_epi64(_mm512_cvtepu8_epi64(_mm512_castsi512_si128(offs)), _mm512_set1_epi64(base + i));
@@ -74,8 +83,17 @@ static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int
     }
     k += c;
   }
+  if constexpr (NT) _mm_sfence();
   nl.n = k;
   return i;
+}
+
+static bool pack_nt_enabled() {       // LP_PACK_NT=0: cached stores (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("LP_PACK_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 static bool have_avx512_vbmi2() {
@@ -94,9 +112,11 @@ static void copy_scan_nl(const uint8_t* src, uint8_t* dst, int64_t n, int64_t ba
   int64_t i = 0;
 #if defined(__x86_64__)
   if (have_avx512_vbmi2()) {
+    const bool nt = ((uintptr_t)dst & 63) == 0 && pack_nt_enabled();
     while (i + 64 <= n) {
       nl.reserve(nl.n + std::max<int64_t>(1024, (n - i) / 32) + 72);
-      i += copy_scan_nl_512(src + i, dst + i, n - i, base + i, nl);
+      i += nt ? copy_scan_nl_512<true>(src + i, dst + i, n - i, base + i, nl)
+              : copy_scan_nl_512<false>(src + i, dst + i, n - i, base + i, nl);
     }
   }
 #endif

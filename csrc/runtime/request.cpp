@@ -59,9 +59,17 @@ uint8_t* RequestRunner::dev(size_t bytes) {
   return p;
 }
 
+int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
+  const size_t seg_bytes = up256(4 * (size_t)D) * 2 + up256(8 * (size_t)D) * 2;
+  const size_t L1 = (size_t)std::max<int64_t>(L, 1);
+  return (int64_t)(up256((size_t)padded_len(nbytes)) + up256(8 * L1) + up256(4 * L1) + up256(seg_bytes) +
+                   up256(8 * sizeof(int64_t)) + (size_t)std::max(S_.nseq, 1));
+}
+
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
                            const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
-                           int D, const FreqRing& ring, double evict_before, double now, uint64_t stream) {
+                           int D, const FreqRing& ring, double evict_before, double now, uint64_t stream,
+                           int64_t host_cap) {
   check(hipSetDevice(S_.device), "set device");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t tsize = padded_len(nbytes);
@@ -71,13 +79,33 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   const int K1 = std::max(S_.nkeys, 1);
   const int64_t ecap_small = request_event_cap();
 
-  // segments -> one pinned staging area -> one H2D copy
+  // Inputs. Single-copy layout (when host_cap allows): the line index, the segments, zeroed
+  // matcher counters and a zeroed sequence carry sit behind the padded text at the offsets the
+  // workspace carve below gives them, so ONE H2D moves them all (each extra copy of a request
+  // cost ~8 us of DMA setup plus ~8 us of queue gap, and the counter memset another fill).
+  const int64_t L1 = std::max<int64_t>(L, 1);
   const size_t seg_bytes = up256(4 * (size_t)D) * 2 + up256(8 * (size_t)D) * 2;
-  grow<true>(up_host_, up_cap_, seg_bytes);
-  std::memcpy(up_host_, seg_lo, 4 * (size_t)D);
-  std::memcpy(up_host_ + up256(4 * (size_t)D), seg_hi, 4 * (size_t)D);
-  std::memcpy(up_host_ + 2 * up256(4 * (size_t)D), seg_g0, 8 * (size_t)D);
-  std::memcpy(up_host_ + 2 * up256(4 * (size_t)D) + up256(8 * (size_t)D), seg_n, 8 * (size_t)D);
+  const size_t nseq1 = (size_t)std::max(S_.nseq, 1);
+  const size_t o_ls = up256((size_t)tsize), o_ll = o_ls + up256(8 * (size_t)L1), o_seg = o_ll + up256(4 * (size_t)L1);
+  const size_t o_cnt = o_seg + up256(seg_bytes), o_seq = o_cnt + up256(8 * sizeof(int64_t)), up_total = o_seq + nseq1;
+  const bool one_copy = host_cap >= (int64_t)up_total;
+  uint8_t* segh;
+  if (one_copy) {
+    if (L > 0) {
+      std::memcpy(host_text + o_ls, starts, 8 * (size_t)L);
+      std::memcpy(host_text + o_ll, lens, 4 * (size_t)L);
+    }
+    std::memset(host_text + o_cnt, 0, 8 * sizeof(int64_t));
+    std::memset(host_text + o_seq, 0, nseq1);
+    segh = host_text + o_seg;
+  } else {
+    grow<true>(up_host_, up_cap_, seg_bytes);
+    segh = up_host_;
+  }
+  std::memcpy(segh, seg_lo, 4 * (size_t)D);
+  std::memcpy(segh + up256(4 * (size_t)D), seg_hi, 4 * (size_t)D);
+  std::memcpy(segh + 2 * up256(4 * (size_t)D), seg_g0, 8 * (size_t)D);
+  std::memcpy(segh + 2 * up256(4 * (size_t)D) + up256(8 * (size_t)D), seg_n, 8 * (size_t)D);
 
   // window eviction first (FrequencyState.carry): the totals it leaves are this batch's carry
   freq_evict(ring, evict_before, stream, true);
@@ -101,7 +129,6 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     ev_rank = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(E, 1)));
     ev_fkey = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(E, 1)));
     feat = dev((size_t)std::max<int64_t>(L, 1));
-    seq_carry = dev((size_t)std::max(S_.nseq, 1));
   };
   // events, context features, frequency ranks into the results buffer, then the fused fp64
   // score; `dcnt` = device [nh, ne] (device-count mode, E = capacity) or null (E = ne read back)
@@ -113,7 +140,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     int32_t* ev_seg = ev_pat + E;
     if (S_.nkeys == 0) check(hipMemsetAsync(freq_counts, 0, 8, st), "counts");
     if (L == 0) check(hipMemsetAsync(feat, 0, 1, st), "feat");
-    check(hipMemsetAsync(seq_carry, 0, (size_t)std::max(S_.nseq, 1), st), "seq carry");
+    if (!one_copy) check(hipMemsetAsync(seq_carry, 0, nseq1, st), "seq carry");
     EventsArgs A;
     A.ctx_trans = S_.ctx_trans; A.ctx_acc = S_.ctx_acc;
     A.hits = (nh_cap || dcnt) ? hits : nullptr; A.nh = nh_cap; A.ev_cnt = ev_cnt; A.ev_end = ev_end; A.ne = E; A.L = L;
@@ -147,16 +174,19 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     const bool fast = S_.device_counts && attempt == 0 && n <= ecap_small && L <= request_line_cap();
     for (int pass = 0; pass < 2; ++pass) {   // measure, then carve from a workspace large enough
       ws_used_ = 0;
+      // carve order == the single-copy host layout (o_ls .. o_seq above)
       text = dev((size_t)tsize);
-      ls = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(L, 1)));
-      ll = reinterpret_cast<int32_t*>(dev(4 * (size_t)std::max<int64_t>(L, 1)));
+      ls = reinterpret_cast<int64_t*>(dev(8 * (size_t)L1));
+      ll = reinterpret_cast<int32_t*>(dev(4 * (size_t)L1));
       uint8_t* segs = dev(seg_bytes);
       dlo = reinterpret_cast<int32_t*>(segs);
       dhi = reinterpret_cast<int32_t*>(segs + up256(4 * (size_t)D));
       dg0 = reinterpret_cast<int64_t*>(segs + 2 * up256(4 * (size_t)D));
       dn = reinterpret_cast<int64_t*>(segs + 2 * up256(4 * (size_t)D) + up256(8 * (size_t)D));
+      cnt = reinterpret_cast<int64_t*>(dev(8 * sizeof(int64_t)));
+      seq_carry = dev(nseq1);
+      if (ws_ && (size_t)(seq_carry - text) != o_seq) throw std::runtime_error("request runner: upload layout mismatch");
       blk = reinterpret_cast<int32_t*>(dev(4 * (size_t)nblk));
-      cnt = reinterpret_cast<int64_t*>(dev(8 * 8));
       gh = reinterpret_cast<int64_t*>(dev(8 * (size_t)cap_g));
       cand = reinterpret_cast<int64_t*>(dev(8 * (size_t)cap_c));
       ver = reinterpret_cast<int64_t*>(dev(8 * (size_t)cap_v));
@@ -176,18 +206,22 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, 4 * (size_t)std::max<int64_t>(L, 1) + 4096);
     }
     // inputs: packed text, line index, segments (all pinned -> async)
-    check(hipMemcpyAsync(text, host_text, (size_t)tsize, hipMemcpyHostToDevice, st), "text H2D");
-    if (L > 0) {
-      check(hipMemcpyAsync(ls, starts, 8 * (size_t)L, hipMemcpyHostToDevice, st), "starts H2D");
-      check(hipMemcpyAsync(ll, lens, 4 * (size_t)L, hipMemcpyHostToDevice, st), "lens H2D");
+    if (one_copy) {
+      check(hipMemcpyAsync(text, host_text, up_total, hipMemcpyHostToDevice, st), "inputs H2D");
+    } else {
+      check(hipMemcpyAsync(text, host_text, (size_t)tsize, hipMemcpyHostToDevice, st), "text H2D");
+      if (L > 0) {
+        check(hipMemcpyAsync(ls, starts, 8 * (size_t)L, hipMemcpyHostToDevice, st), "starts H2D");
+        check(hipMemcpyAsync(ll, lens, 4 * (size_t)L, hipMemcpyHostToDevice, st), "lens H2D");
+      }
+      check(hipMemcpyAsync(dlo, up_host_, seg_bytes, hipMemcpyHostToDevice, st), "segments H2D");
+      check(hipMemsetAsync(cnt, 0, 8 * sizeof(int64_t), st), "counters");
     }
-    check(hipMemcpyAsync(dlo, up_host_, seg_bytes, hipMemcpyHostToDevice, st), "segments H2D");
     ev.seg_lo = dlo;
     ev.seg_hi = dhi;
     ev.own_lo = dlo;
     ev.own_hi = dhi;
     ev.nseg = D;
-    check(hipMemsetAsync(cnt, 0, 8 * sizeof(int64_t), st), "counters");
     unsigned long long* c0 = reinterpret_cast<unsigned long long*>(cnt);
 
     // matchers: literal-free scan groups, single-DFA scans, then the literal prefilter chain
@@ -269,7 +303,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       check(hipFree(old), "free");
       const ptrdiff_t d = nw - old;
       auto mv = [&](auto*& q) { q = reinterpret_cast<std::remove_reference_t<decltype(q)>>(reinterpret_cast<uint8_t*>(q) + d); };
-      mv(text); mv(ls); mv(ll); mv(dlo); mv(dhi); mv(dg0); mv(dn); mv(hits); mv(hit_line); mv(hit_off); mv(ev_cnt); mv(ev_end);
+      mv(text); mv(ls); mv(ll); mv(dlo); mv(dhi); mv(dg0); mv(dn); mv(hits); mv(hit_line); mv(hit_off); mv(ev_cnt); mv(ev_end); mv(seq_carry);
       ev.seg_lo = dlo; ev.seg_hi = dhi; ev.own_lo = dlo; ev.own_hi = dhi;
       ws_ = nw;
       ws_cap_ = ncap;

@@ -54,14 +54,19 @@ class RequestRunner {
   RequestRunner& operator=(const RequestRunner&) = delete;
 
   // host_text: pinned packed bytes [0, nbytes) with room up to the padded length (zero-filled
-  // here); starts / lens: pinned line index (L lines); seg_*: D documents (host arrays).
+  // here); host_cap: bytes usable at host_text -- when upload_bytes(nbytes, L, D) fit, the line
+  // index, segments and the zero-initialised counters are laid out behind the text exactly as
+  // the device workspace is carved and everything goes up in ONE H2D copy (otherwise one copy
+  // per array); starts / lens: pinned line index (L lines); seg_*: D documents (host arrays).
   // ring: the device frequency state; evict_before / now: its eviction horizon and record time.
   // Returns the number of events ne; the results stay in result() until the next run:
   // [score f64 x E | freq counts i64 x max(nkeys, 1) | line i32 x E | pattern i32 x E | seg i32 x E]
   // with E = stride() >= ne (the event capacity of a device-count-mode request, else ne).
   int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
-              const FreqRing& ring, double evict_before, double now, uint64_t stream);
+              const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0);
+  // host bytes the single-copy upload needs (text padded, index, segments, counters, carry)
+  int64_t upload_bytes(int64_t nbytes, int64_t L, int D) const;
   const uint8_t* result() const { return res_host_; }
   size_t result_bytes() const { return res_bytes_; }
   const RequestCounts& counts() const { return counts_; }

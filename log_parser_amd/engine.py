@@ -215,6 +215,7 @@ class Stage:
     def __init__(self, pinned: bool, nbytes: int, nlines: int):
         self.pinned = pinned
         self.buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
+        self.want = 0                       # bytes the request runner's single-copy upload wants
         self.cap = 0
         self.idx: Optional[torch.Tensor] = None
         self.grow_idx(nlines)
@@ -793,12 +794,17 @@ class Engine:
                 fr._ensure_room(K)
             evict_before = fr._now() - fr.window_s      # carry_tensor()
             now = fr._now()                              # record_tensor()
+            # host_cap: the stage's room behind the text lets the runner send text, line index,
+            # segments and zeroed counters in ONE H2D copy (request.cpp, single-copy layout)
             ne, out, counts, E = self._runner.run(st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(),
                                                st.lens(job.n_lines).data_ptr(), job.n_lines, lo, hi, g0, nn,
-                                               fr._ring(), evict_before, now, stream)
+                                               fr._ring(), evict_before, now, stream, st.buf.numel())
             if K:
                 fr._tail_bound += K
         self.arena.last = counts
+        need = self._runner.upload_bytes(n, job.n_lines, len(lo))
+        if need > st.buf.numel():
+            st.want = need * 5 // 4                      # grown on release (emission still reads buf)
         k1 = max(K, 1)
         a, b = 8 * E, 8 * E + 8 * k1          # E: the results' event stride (>= ne)
         job.ev = (out[b:b + 4 * ne].view(np.int32), out[b + 4 * E:b + 4 * E + 4 * ne].view(np.int32),
@@ -831,6 +837,11 @@ class Engine:
     def release_batch(self, job: "BatchJob") -> None:
         """Return the job's staging buffer to the pool (after its H2D and emission are done)."""
         if job.stage is not None:
+            if job.stage.want > job.stage.buf.numel():
+                try:
+                    job.stage.grow_buf(job.stage.want)
+                except BaseException:           # keep the slot usable; the next pack regrows
+                    job.stage.buf = None
             self._stage_pool.give(job.stage)
             job.stage = None
 

@@ -25,7 +25,10 @@ def run(args):
     dev = torch.device("cuda", 0)
     sets, trig = realistic_library(args.patterns, seed=7)
     lib = CompiledLibrary(sets, ScoringParams())
-    eng = Engine(lib, Config.load(overrides={"engine.device": "cuda:0"}), device=dev)
+    ov = {"engine.device": "cuda:0"}
+    if args.device_counts:
+        ov["engine.runner-device-counts"] = True
+    eng = Engine(lib, Config.load(overrides=ov), device=dev)
     logs = make_log(args.lines, trig, seed=13, hit_rate=0.01)
     for _ in range(20):
         eng.analyze_batch_json([logs])
@@ -69,6 +72,15 @@ def summarise(args):
                       "copies_per_request": statistics.median(nc)}))
     for name, d in sorted(per_name.items(), key=lambda kv: -sum(kv[1]))[:25]:
         print(f"{sum(d) / n:8.1f} us/req  {len(d) / n:5.1f}/req  {name}")
+    # timeline of the median-span request: start offset, duration and the idle gap before each op
+    if groups:
+        med = sorted(range(n), key=lambda i: spans[i])[n // 2]
+        g = groups[med]
+        t0, prev_end = g[0][0], g[0][0]
+        print(f"timeline of request {med} (span {spans[med]:.1f} us): offset_us dur_us gap_us name")
+        for s, e, name in g:
+            print(f"{(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f} {max(0, s - prev_end) / 1e3:7.1f}  {name[:60]}")
+            prev_end = max(prev_end, e)
 
 
 if __name__ == "__main__":
@@ -77,5 +89,6 @@ if __name__ == "__main__":
     ap.add_argument("--patterns", type=int, default=1000)
     ap.add_argument("--requests", type=int, default=200)
     ap.add_argument("--db", default="")
+    ap.add_argument("--device-counts", action="store_true", help="runner device-count mode (no mid-batch read)")
     a = ap.parse_args()
     summarise(a) if a.db else run(a)

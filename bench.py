@@ -306,7 +306,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
             # second half of the BASELINE metric: one 10k-line /parse request, same library
             req = make_log(10_000, trig, seed=13, hit_rate=0.01)
             if server is not None:
-                lat = server.parse_latencies(req, args.parse_requests)
+                lat = server.parse_latencies(req, args.parse_requests, warmup=20)   # server idle since start-up
                 rec["p50_parse_ms"] = round(float(np.median(lat)) * 1e3, 3)
                 rec["p99_parse_ms"] = round(float(np.percentile(lat, 99)) * 1e3, 3)
                 rec["parse_transport"] = f"{args.http} HTTP/1.1 keep-alive, server process on 127.0.0.1"

@@ -88,10 +88,13 @@ static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int
   return i;
 }
 
-static bool pack_nt_enabled() {       // LP_PACK_NT=0: cached stores (A/B)
+// LP_PACK_NT=1: streaming stores (A/B, off by default: a 10k-line request measured 0.299-0.302 ms
+// with them vs 0.282 ms without -- the '\r' checks of the line pass and the JSON emitter's context
+// lines then read the stage from DRAM instead of the cache)
+static bool pack_nt_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("LP_PACK_NT");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

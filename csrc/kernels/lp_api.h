@@ -212,6 +212,10 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
 // the event stage in device-count mode
 int64_t request_event_cap();
 int64_t request_line_cap();
+// device-count-mode results -> pinned host memory (request_io.hip): the 5 matcher/event counters
+// and the results compacted to stride ne (cnt[4]) when ne <= E; both pointers device-visible
+void publish_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host, uint8_t* res_host,
+                 uint64_t stream);
 void blk_index_dev(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk, uint64_t stream);
 void hits_host(const HitsArgs& A);
 void events_host(const EventsArgs& A);

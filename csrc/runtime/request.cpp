@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -25,24 +26,42 @@ int64_t padded_len(int64_t n) { return ((std::max<int64_t>(n, 1) + kNlTile - 1) 
 
 size_t up256(size_t n) { return (n + 255) & ~size_t(255); }
 
+// pinned host memory kernels write into (k_publish): fine-grained, so the GPU's stores go to
+// host memory and are visible once the stream has synchronised
+constexpr unsigned kCoherentHost = hipHostMallocMapped | hipHostMallocCoherent;
+
 // a device or pinned buffer that only grows (between runs, when nothing in flight uses it)
 template <bool Pinned>
-void grow(uint8_t*& p, size_t& cap, size_t need) {
+void grow(uint8_t*& p, size_t& cap, size_t need, unsigned host_flags = hipHostMallocDefault) {
   if (need <= cap) return;
   const size_t n = std::max(need + need / 4, size_t(1) << 20);
   if (p) check(Pinned ? hipHostFree(p) : hipFree(p), "free");
   p = nullptr;
   cap = 0;
-  check(Pinned ? hipHostMalloc(reinterpret_cast<void**>(&p), n, hipHostMallocDefault)
+  check(Pinned ? hipHostMalloc(reinterpret_cast<void**>(&p), n, host_flags)
                : hipMalloc(reinterpret_cast<void**>(&p), n), "alloc");
   cap = n;
+}
+
+template <typename T>
+T* device_view(T* host) {
+  void* d = nullptr;
+  check(hipHostGetDevicePointer(&d, host, 0), "host device pointer");
+  return static_cast<T*>(d);
+}
+
+bool publish_enabled() {               // LP_RUNNER_PUBLISH=0: copy-based results (A/B)
+  const char* e = std::getenv("LP_RUNNER_PUBLISH");
+  return !(e && e[0] == '0');
 }
 
 }  // namespace
 
 RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
   check(hipSetDevice(S_.device), "set device");
-  check(hipHostMalloc(reinterpret_cast<void**>(&cnt_host_), 8 * sizeof(int64_t), hipHostMallocDefault), "pinned counters");
+  check(hipHostMalloc(reinterpret_cast<void**>(&cnt_host_), 8 * sizeof(int64_t), kCoherentHost), "pinned counters");
+  cnt_host_dev_ = device_view(cnt_host_);
+  publish_ = publish_enabled();
 }
 
 RequestRunner::~RequestRunner() {
@@ -258,11 +277,19 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
         freq_record(fc, S_.nkeys, now, ring, stream, true, G);
       }
       const size_t res = 20 * (size_t)ecap_small + 8 * (size_t)K1;
-      grow<true>(res_host_, res_cap_, res);
-      check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
-      res_bytes_ = res;
+      if (res > res_cap_) {
+        grow<true>(res_host_, res_cap_, res, kCoherentHost);
+        res_host_dev_ = device_view(res_host_);
+      }
+      if (publish_) {      // counters + compacted results written into host memory by a kernel
+        publish_dev(cnt, out, ecap_small, (int)K1, cnt_host_dev_, res_host_dev_, stream);
+      } else {
+        check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
+        res_bytes_ = res;
+      }
     }
-    check(hipMemcpyAsync(cnt_host_, cnt, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st), "counters D2H");
+    if (!(fast && publish_))
+      check(hipMemcpyAsync(cnt_host_, cnt, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st), "counters D2H");
     check(hipStreamSynchronize(st), "counters");   // fast: the only host read; else the mid-batch one
     c.gram = cnt_host_[0]; c.cand = cnt_host_[1]; c.ver = cnt_host_[2];
     nh = cnt_host_[3]; ne = cnt_host_[4];
@@ -278,7 +305,8 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     learn(rate_ver_, c.ver);
     if (ok && fast && ne <= ecap_small) {    // recorded through the gate; results already read
       done = true;
-      stride = ecap_small;
+      stride = publish_ ? ne : ecap_small;
+      if (publish_) res_bytes_ = 20 * (size_t)ne + 8 * (size_t)K1;
       break;
     }
     if (ok && !fast) break;
@@ -313,7 +341,10 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     int64_t* fc = run_events(ne, nh, nullptr);
     // this batch's per-key counts enter the window (after its own scoring: penalty before record)
     if (S_.nkeys > 0) freq_record(fc, S_.nkeys, now, ring, stream, true);
-    grow<true>(res_host_, res_cap_, res);
+    if (res > res_cap_) {
+      grow<true>(res_host_, res_cap_, res, kCoherentHost);
+      res_host_dev_ = device_view(res_host_);
+    }
     check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
     check(hipStreamSynchronize(st), "results");
     res_bytes_ = res;

@@ -85,7 +85,10 @@ class RequestRunner {
   size_t up_cap_ = 0;
   uint8_t* res_host_ = nullptr;        // pinned results
   size_t res_cap_ = 0, res_bytes_ = 0;
-  int64_t* cnt_host_ = nullptr;        // pinned counters
+  int64_t* cnt_host_ = nullptr;        // pinned counters (fine-grained: k_publish writes them)
+  int64_t* cnt_host_dev_ = nullptr;    // ... and the device's address of them
+  uint8_t* res_host_dev_ = nullptr;    // device address of res_host_
+  bool publish_ = true;                // device-count mode: results published by k_publish
   RequestCounts counts_;
   int64_t stride_ = 0;
 };

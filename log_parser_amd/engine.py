@@ -777,7 +777,7 @@ class Engine:
                 ptr("scan_regs"), t["scan_regs"].numel(), st12, self.sp_tuple, ev5, self.lib.n_regexes,
                 len(self.lib.patterns), len(self.lib.freq_ids), self.lib.n_seq_events, self.lib.ctx_dfa_extent[0],
                 self.lib.ctx_dfa_extent[1], self.pf_grid, dev,
-                bool(self.config.get("engine.runner-device-counts", False)))
+                bool(self.config.get("engine.runner-device-counts", True)))
         return True
 
     def _run_native(self, job: "BatchJob", dl, n: int) -> None:

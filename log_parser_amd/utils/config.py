@@ -55,9 +55,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # the device half of a batch in one native call (csrc/runtime/request.cpp) when applicable
     "engine.native-runner": (True, bool),
     # runner, request-sized batches: events / score / frequency record read the matcher counts on
-    # the device (no mid-batch host read; the record is gated on the capacities holding). Off:
-    # measured equal (10k-line request 0.335 vs 0.329 ms) -- the GPU chain, not the read, bounds it
-    "engine.runner-device-counts": (False, bool),
+    # the device (no mid-batch host read; the record is gated on the capacities holding) and
+    # k_publish writes the counters + compacted results into pinned host memory (no copies back):
+    # 10k-line request GPU span 352 -> 326 us, engine p50 0.310 -> 0.302 ms (profiles/r2_v10)
+    "engine.runner-device-counts": (True, bool),
     # serve a batch from the CPU backend when the device path fails (availability)
     "engine.fallback-cpu": (True, bool),
     # per-stage HIP-event timers, reported in response metadata as stageTimingsMs (opt-in)

@@ -249,6 +249,35 @@ static py::tuple split_docs(uint64_t buf, py::array_t<int64_t> doc_off) {
   return py::make_tuple(a, l, o);
 }
 
+// A drained POST /parse whose `logs` string is still JSON-escaped inside its receive buffer
+// (HttpServer.next_requests(raw=True)). pack_split_docs unescapes it straight into the engine's
+// pinned stage -- one pass over the bytes instead of unescape-to-bytes + copy-to-stage -- and the
+// buffer goes back to the server's pool when the object dies.
+struct RawLogs {
+  std::string body;
+  size_t off = 0, len = 0;
+  std::shared_ptr<BufferPool> pool;
+  RawLogs() = default;
+  RawLogs(const RawLogs&) = delete;
+  RawLogs& operator=(const RawLogs&) = delete;
+  ~RawLogs() {
+    if (pool) pool->give(std::move(body));
+  }
+  const uint8_t* data() const { return reinterpret_cast<const uint8_t*>(body.data()) + off; }
+};
+
+static py::bytes raw_logs_decode(const RawLogs& r) {
+  PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(r.len + 64));
+  if (!b) throw py::error_already_set();
+  size_t n;
+  {
+    py::gil_scoped_release nogil;
+    n = decode_json_string(r.data(), r.len, PyBytes_AS_STRING(b));
+  }
+  if (_PyBytes_Resize(&b, (Py_ssize_t)n) != 0) throw py::error_already_set();
+  return py::reinterpret_steal<py::bytes>(b);
+}
+
 // Pack request bodies (str via their cached UTF-8 buffer -- no copy for ASCII -- or bytes) into
 // dst and split them. Returns None if a str is not UTF-8 encodable (lone surrogates: the caller
 // falls back to str.encode(surrogatepass)), the needed byte count (int) if it exceeds cap, or
@@ -259,7 +288,27 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   const int64_t D = (int64_t)docs.size();
   std::vector<const char*> src(D);
   std::vector<int64_t> off(D + 1, 0);
-  for (int64_t i = 0; i < D; ++i) {
+  bool raw = D > 0;
+  for (int64_t i = 0; i < D && raw; ++i) raw = py::isinstance<RawLogs>(docs[i]);
+  if (raw) {
+    // escaped length bounds the decoded one; the decoder may write 64 bytes past its output
+    std::vector<const RawLogs*> rl(D);
+    int64_t bound = 64;
+    for (int64_t i = 0; i < D; ++i) {
+      rl[i] = &docs[i].cast<const RawLogs&>();
+      bound += (int64_t)rl[i]->len;
+    }
+    if (bound > cap) return py::int_(bound);
+    {
+      py::gil_scoped_release nogil;
+      uint8_t* d = P<uint8_t>(dst);
+      for (int64_t i = 0; i < D; ++i) {
+        off[i + 1] = off[i] + (int64_t)decode_json_string(rl[i]->data(), rl[i]->len, reinterpret_cast<char*>(d + off[i]));
+        src[i] = reinterpret_cast<const char*>(d + off[i]);     // split in place (no copy)
+      }
+    }
+  }
+  for (int64_t i = 0; i < D && !raw; ++i) {
     PyObject* o = docs[i].ptr();
     Py_ssize_t n = 0;
     const char* p = nullptr;
@@ -588,16 +637,38 @@ PYBIND11_MODULE(_lpnative, m) {
       .def("upload_bytes", &RequestRunner::upload_bytes);
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
+  py::class_<RawLogs>(m, "RawLogs")
+      .def("__len__", [](const RawLogs& r) { return r.len; })
+      .def("decode", &raw_logs_decode, "the unescaped UTF-8 log text")
+      .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; });
+
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init<const std::string&, int, int, int64_t, double>(), py::arg("host"), py::arg("port"),
            py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30, py::arg("idle_timeout_s") = 60.0)
       .def_property_readonly("port", &HttpServer::port)
       .def("pending", &HttpServer::pending)
-      .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms) {
+      .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms, bool raw) {
         std::vector<HttpRequest> v;
         {
           py::gil_scoped_release nogil;
           v = s.next_requests(max_n, timeout_ms);
+        }
+        if (raw) {          // decoded later, straight into the engine's stage (RawLogs)
+          py::list out;
+          for (auto& r : v) {
+            if (r.kind == 0) {
+              auto* rl = new RawLogs();
+              rl->off = r.logs_off;
+              rl->len = r.logs_len;
+              rl->body = std::move(r.body);
+              rl->pool = s.pool();
+              out.append(py::make_tuple(r.id, 0, py::cast(rl, py::return_value_policy::take_ownership), r.pod_name,
+                                        r.t_arrival));
+            } else {
+              out.append(py::make_tuple(r.id, 1, r.method, r.path, py::bytes(r.body), r.t_arrival));
+            }
+          }
+          return out;
         }
         // decoded POST /parse: one bytes object per request sized for the escaped text, filled by
         // the unescaper with the GIL released (the only copy of the log between the socket
@@ -636,7 +707,7 @@ PYBIND11_MODULE(_lpnative, m) {
           }
         }
         return out;
-      }, py::arg("max_n") = 4096, py::arg("timeout_ms") = 100)
+      }, py::arg("max_n") = 4096, py::arg("timeout_ms") = 100, py::arg("raw") = false)
       .def("respond", [](HttpServer& s, uint64_t id, int status, const std::string& ctype, py::bytes body) {
         char* p = nullptr;
         Py_ssize_t n = 0;

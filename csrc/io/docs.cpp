@@ -49,7 +49,7 @@ struct NlBuf {
 // NT: dst is 64-byte aligned and the stores stream past the cache (the destination is the
 // pinned staging buffer the GPU's DMA reads next, never this core: no read-for-ownership of the
 // destination lines).
-template <bool NT>
+template <int MODE>   // 0: stores, 1: streaming stores, 2: no stores (src == dst)
 __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vbmi2,bmi,bmi2,popcnt")))
 static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int64_t base, NlBuf& nl) {
   alignas(64) static const uint8_t kIota[64] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
@@ -63,9 +63,9 @@ static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int
   const int64_t room = nl.cap - 72;
   for (; i + 64 <= n && k <= room; i += 64) {
     const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(src + i));
-    if constexpr (NT)
+    if constexpr (MODE == 1)
       _mm512_stream_si512(reinterpret_cast<__m512i*>(dst + i), v);
-    else
+    else if constexpr (MODE == 0)
       _mm512_storeu_si512(reinterpret_cast<void*>(dst + i), v);
     const uint64_t m = _mm512_cmpeq_epi8_mask(v, NL);
     const __m512i offs = _mm512_maskz_compress_epi8(m, iota);
@@ -83,7 +83,7 @@ static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int
     }
     k += c;
   }
-  if constexpr (NT) _mm_sfence();
+  if constexpr (MODE == 1) _mm_sfence();
   nl.n = k;
   return i;
 }
@@ -115,11 +115,13 @@ static void copy_scan_nl(const uint8_t* src, uint8_t* dst, int64_t n, int64_t ba
   int64_t i = 0;
 #if defined(__x86_64__)
   if (have_avx512_vbmi2()) {
-    const bool nt = ((uintptr_t)dst & 63) == 0 && pack_nt_enabled();
+    // src == dst: the bytes were decoded into the stage already (RawLogs): scan only
+    const int mode = src == dst ? 2 : (((uintptr_t)dst & 63) == 0 && pack_nt_enabled()) ? 1 : 0;
     while (i + 64 <= n) {
       nl.reserve(nl.n + std::max<int64_t>(1024, (n - i) / 32) + 72);
-      i += nt ? copy_scan_nl_512<true>(src + i, dst + i, n - i, base + i, nl)
-              : copy_scan_nl_512<false>(src + i, dst + i, n - i, base + i, nl);
+      i += mode == 2 ? copy_scan_nl_512<2>(src + i, dst + i, n - i, base + i, nl)
+           : mode == 1 ? copy_scan_nl_512<1>(src + i, dst + i, n - i, base + i, nl)
+                       : copy_scan_nl_512<0>(src + i, dst + i, n - i, base + i, nl);
     }
   }
 #endif

@@ -229,20 +229,22 @@ void HttpServer::respond(uint64_t id, int status, const std::string& content_typ
   (void)!write(io->efd, &one, 8);
 }
 
-std::string HttpServer::take_buffer() {
-  std::lock_guard<std::mutex> g(pm_);
-  if (pool_.empty()) return std::string();
-  std::string b = std::move(pool_.back());
-  pool_.pop_back();
+std::string BufferPool::take() {
+  std::lock_guard<std::mutex> g(m);
+  if (v.empty()) return std::string();
+  std::string b = std::move(v.back());
+  v.pop_back();
   return b;
 }
 
-void HttpServer::recycle(std::string&& buf) {
+void BufferPool::give(std::string&& buf) {
   if (buf.capacity() < (64u << 10) || buf.capacity() > (size_t(256) << 20)) return;
   buf.clear();
-  std::lock_guard<std::mutex> g(pm_);
-  if (pool_.size() < 64) pool_.push_back(std::move(buf));
+  std::lock_guard<std::mutex> g(m);
+  if (v.size() < 64) v.push_back(std::move(buf));
 }
+
+std::string HttpServer::take_buffer() { return pool_->take(); }
 
 void HttpServer::send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body,
                           bool keep) {

@@ -30,6 +30,16 @@ struct HttpRequest {
   double t_arrival = 0;     // monotonic seconds, when the body was complete
 };
 
+// Receive buffers recycled between requests (a fresh megabyte-sized allocation page-faults).
+// Shared: a drained request's buffer may outlive the server (RawLogs in bind.cpp holds it until
+// the engine has decoded it into its pinned stage).
+struct BufferPool {
+  std::mutex m;
+  std::vector<std::string> v;
+  std::string take();
+  void give(std::string&& buf);
+};
+
 struct HttpStats {
   std::atomic<uint64_t> accepted{0}, requests{0}, bad_requests{0}, native_400{0};
 };
@@ -51,7 +61,8 @@ class HttpServer {
   void respond(uint64_t id, int status, const std::string& content_type, const char* body, size_t n);
   // hand a drained request's raw buffer back (its capacity serves a later request: no page faults
   // of a fresh megabyte-sized allocation per request)
-  void recycle(std::string&& buf);
+  void recycle(std::string&& buf) { pool_->give(std::move(buf)); }
+  const std::shared_ptr<BufferPool>& pool() const { return pool_; }
   void stop();
   HttpStats stats;
 
@@ -83,8 +94,7 @@ class HttpServer {
   std::condition_variable qcv_;
   std::deque<HttpRequest> q_;
   std::atomic<uint64_t> next_id_{1};
-  std::mutex pm_;
-  std::vector<std::string> pool_;
+  std::shared_ptr<BufferPool> pool_ = std::make_shared<BufferPool>();
 };
 
 }  // namespace lp

@@ -214,6 +214,8 @@ int64_t request_event_cap();
 int64_t request_line_cap();
 // device-count-mode results -> pinned host memory (request_io.hip): the 5 matcher/event counters
 // and the results compacted to stride ne (cnt[4]) when ne <= E; both pointers device-visible
+// n16 16-byte words from device-visible pinned host memory (host_dev) into device memory
+void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream);
 void publish_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host, uint8_t* res_host,
                  uint64_t stream);
 void blk_index_dev(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk, uint64_t stream);

@@ -50,6 +50,11 @@ T* device_view(T* host) {
   return static_cast<T*>(d);
 }
 
+bool fetch_enabled() {                 // LP_RUNNER_FETCH=0: SDMA copy of the inputs (A/B)
+  const char* e = std::getenv("LP_RUNNER_FETCH");
+  return !(e && e[0] == '0');
+}
+
 bool publish_enabled() {               // LP_RUNNER_PUBLISH=0: copy-based results (A/B)
   const char* e = std::getenv("LP_RUNNER_PUBLISH");
   return !(e && e[0] == '0');
@@ -62,6 +67,7 @@ RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
   check(hipHostMalloc(reinterpret_cast<void**>(&cnt_host_), 8 * sizeof(int64_t), kCoherentHost), "pinned counters");
   cnt_host_dev_ = device_view(cnt_host_);
   publish_ = publish_enabled();
+  fetch_ = fetch_enabled();
 }
 
 RequestRunner::~RequestRunner() {
@@ -81,8 +87,9 @@ uint8_t* RequestRunner::dev(size_t bytes) {
 int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
   const size_t seg_bytes = up256(4 * (size_t)D) * 2 + up256(8 * (size_t)D) * 2;
   const size_t L1 = (size_t)std::max<int64_t>(L, 1);
-  return (int64_t)(up256((size_t)padded_len(nbytes)) + up256(8 * L1) + up256(4 * L1) + up256(seg_bytes) +
-                   up256(8 * sizeof(int64_t)) + (size_t)std::max(S_.nseq, 1));
+  const size_t n = up256((size_t)padded_len(nbytes)) + up256(8 * L1) + up256(4 * L1) + up256(seg_bytes) +
+                   up256(8 * sizeof(int64_t)) + (size_t)std::max(S_.nseq, 1);
+  return (int64_t)((n + 15) & ~size_t(15));
 }
 
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
@@ -106,8 +113,24 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   const size_t seg_bytes = up256(4 * (size_t)D) * 2 + up256(8 * (size_t)D) * 2;
   const size_t nseq1 = (size_t)std::max(S_.nseq, 1);
   const size_t o_ls = up256((size_t)tsize), o_ll = o_ls + up256(8 * (size_t)L1), o_seg = o_ll + up256(4 * (size_t)L1);
-  const size_t o_cnt = o_seg + up256(seg_bytes), o_seq = o_cnt + up256(8 * sizeof(int64_t)), up_total = o_seq + nseq1;
+  const size_t o_cnt = o_seg + up256(seg_bytes), o_seq = o_cnt + up256(8 * sizeof(int64_t));
+  const size_t up_total = (o_seq + nseq1 + 15) & ~size_t(15);     // whole 16-byte words
   const bool one_copy = host_cap >= (int64_t)up_total;
+  // ... read by a kernel from the pinned buffer itself when the runtime maps it for the device
+  const uint8_t* text_dev_src = nullptr;
+  if (one_copy && fetch_ && ((uintptr_t)host_text & 15) == 0) {
+    if (host_text != fetch_host_ || host_cap != fetch_cap_) {
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, host_text, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        d = nullptr;
+      }
+      fetch_host_ = host_text;
+      fetch_cap_ = host_cap;
+      fetch_dev_ = static_cast<uint8_t*>(d);
+    }
+    text_dev_src = fetch_dev_;
+  }
   uint8_t* segh;
   if (one_copy) {
     if (L > 0) {
@@ -225,7 +248,9 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, 4 * (size_t)std::max<int64_t>(L, 1) + 4096);
     }
     // inputs: packed text, line index, segments (all pinned -> async)
-    if (one_copy) {
+    if (one_copy && text_dev_src) {
+      fetch_dev(text_dev_src, text, (int64_t)(up_total / 16), stream);
+    } else if (one_copy) {
       check(hipMemcpyAsync(text, host_text, up_total, hipMemcpyHostToDevice, st), "inputs H2D");
     } else {
       check(hipMemcpyAsync(text, host_text, (size_t)tsize, hipMemcpyHostToDevice, st), "text H2D");

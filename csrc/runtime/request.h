@@ -89,6 +89,10 @@ class RequestRunner {
   int64_t* cnt_host_dev_ = nullptr;    // ... and the device's address of them
   uint8_t* res_host_dev_ = nullptr;    // device address of res_host_
   bool publish_ = true;                // device-count mode: results published by k_publish
+  bool fetch_ = true;                  // single-copy inputs read by k_fetch from the pinned stage
+  uint8_t* fetch_host_ = nullptr;      // last stage buffer seen ...
+  uint8_t* fetch_dev_ = nullptr;       // ... and its device address (null: not mapped, SDMA copy)
+  int64_t fetch_cap_ = 0;
   RequestCounts counts_;
   int64_t stride_ = 0;
 };

@@ -684,7 +684,8 @@ class Engine:
         if job.whole:
             if turn is not None:
                 turn.wait(seq)
-            job.outs = [self.analyze_json(job.logs[0])]
+            doc = job.logs[0]
+            job.outs = [self.analyze_json(doc.decode() if isinstance(doc, N.RawLogs) else doc)]
             if turn is not None:
                 turn.done(seq)
             return
@@ -853,6 +854,9 @@ class Engine:
         byte; the index goes straight into the stage's pinned index buffer when it fits.
         Returns (host view, line_start, line_len, doc_line_off, nbytes) or None."""
         st = job.stage
+        raw = [isinstance(d, N.RawLogs) for d in docs]
+        if any(raw) and not all(raw):   # escaped request logs are unescaped in place only as a batch
+            docs = [d.decode() if r else d for d, r in zip(docs, raw)]
         cap = st.buf.numel() - K.TEXT_PAD - K.NL_TILE
         r = N.pack_split_docs(docs, st.buf.data_ptr(), cap, self._STAGE_THREADS, st.idx.data_ptr(), st.cap)
         if r is None:

@@ -11,10 +11,30 @@ from ..utils.config import Config, parse_cli_overrides
 from .app import Service, create_app
 
 
+def bind_numa(cfg: Config) -> None:
+    """Single-GPU service: run every thread (IO, pump, pipeline) on the CPUs of the GPU's NUMA node,
+    before any of them starts -- request bodies, the pinned stage buffers (HIP places them on the
+    device's node) and the threads touching them then stay on one socket (``server.numa-bind``)."""
+    dev = str(cfg["engine.device"])
+    if not cfg.get("server.numa-bind", True) or not dev.startswith("cuda") or cfg.get("engine.serve-devices", ""):
+        return
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return
+        from ..utils.numa import bind_to_gpu_numa
+        cpus = bind_to_gpu_numa(int(dev.split(":", 1)[1]) if ":" in dev else 0)
+        if cpus:
+            logging.getLogger("log_parser_amd.server").info("bound to the %d CPUs of %s's NUMA node", len(cpus), dev)
+    except Exception as e:  # noqa: BLE001 - affinity is an optimisation only
+        logging.getLogger("log_parser_amd.server").warning("NUMA binding skipped: %s", e)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s [%(name)s] %(message)s")
     cfg = Config.load(overrides=parse_cli_overrides(argv))
+    bind_numa(cfg)
     if str(cfg["server.http"]) == "uvicorn":
         import uvicorn
         uvicorn.run(create_app(cfg), host=cfg["server.host"], port=int(cfg["server.port"]), log_level="info")

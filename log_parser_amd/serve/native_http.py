@@ -1,10 +1,12 @@
 """Native HTTP/1.1 front end of the REST service (``server.http=native``, the default).
 
 The C++ epoll server (``csrc/io/http_server.cpp``) owns the sockets: it parses requests, answers
-``GET /health`` and malformed ``/parse`` bodies itself (HTTP 400, ``Parse.java:45-49``), and decodes
-valid ``POST /parse`` bodies to UTF-8 log bytes (``csrc/io/json_in.cpp``). One Python pump thread
-drains the decoded requests in bulk with the GIL released and hands them to the continuous
-batcher; responses go back through ``HttpServer.respond`` from the batcher's completion callbacks.
+``GET /health`` and malformed ``/parse`` bodies itself (HTTP 400, ``Parse.java:45-49``), and validates
+``POST /parse`` bodies (``csrc/io/json_in.cpp``). One Python pump thread drains the requests in bulk
+with the GIL released and hands them to the continuous batcher; with one engine (direct mode) the
+log strings stay JSON-escaped in their receive buffers (``N.RawLogs``) until the engine's packer
+unescapes them straight into its pinned stage, otherwise they are unescaped to UTF-8 bytes while
+draining. Responses go back through ``HttpServer.respond`` from the batcher's completion callbacks.
 Every other route (``/ready``, ``/metrics``, ``/admin/*``, the json.loads fallback of exotic
 ``/parse`` bodies) is served by the same ``Service`` methods as the FastAPI front end.
 """
@@ -50,7 +52,9 @@ class NativeHttpFrontend:
         b = self.svc.batcher()
         direct = len(b.engines) == 1 and b.turn is None
         while not self._stop.is_set():
-            reqs = self.srv.next_requests(b.max_requests, 100)
+            # direct mode: /parse logs stay JSON-escaped in their receive buffers (N.RawLogs) and
+            # are unescaped by the engine's packer straight into its pinned stage
+            reqs = self.srv.next_requests(b.max_requests, 100, direct)
             if not reqs:
                 continue
             batch = []
@@ -58,7 +62,7 @@ class NativeHttpFrontend:
                 rid, kind = req[0], req[1]
                 t0 = time.perf_counter()
                 try:
-                    if kind == 0:                            # decoded POST /parse
+                    if kind == 0:                            # validated POST /parse
                         _, _, logs, name, _ = req
                         if direct:
                             log.info("Received analysis request for pod: %s", name or "<unknown>")

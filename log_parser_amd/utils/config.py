@@ -84,6 +84,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # HTTP front end: "native" (C++ epoll server, csrc/io/http_server.cpp) or "uvicorn" (FastAPI)
     "server.http": ("native", str),
     "server.io-threads": (2, int),
+    # single-GPU service: bind the process to the CPUs of the GPU's NUMA node (serve/__main__.py)
+    "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)
     "server.idle-timeout-s": (60.0, float),
     # freeze the startup heap + raise GC thresholds in the batching server (submit-path latency)

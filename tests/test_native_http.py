@@ -182,3 +182,60 @@ def test_idle_connections_are_closed():
         s.close()
     finally:
         fe.close()
+
+
+def test_raw_logs_unescaped_in_the_stage(server):
+    """Direct mode drains /parse logs still JSON-escaped (N.RawLogs) and the packer unescapes them
+    straight into the pinned stage: escapes of every kind, CRLF / CR-only lines, non-ASCII, a
+    batch mixing raw and json.loads-fallback bodies, and RawLogs == their decode() through the
+    engine."""
+    from log_parser_amd.native import N
+    fe, sets, trig = server
+    base = make_log(300, trig, seed=31, hit_rate=0.05)
+    logs = base.replace("\n", "\r\n", 40) + '\ttab "quoted" back\\slash caf\u00e9 \x01 end\n\n\n'
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=60)
+    c.request("DELETE", "/admin/frequency")
+    c.getresponse().read()
+    st, out = _post(c, json.dumps({"pod": {"metadata": {"name": "raw"}}, "logs": logs}).encode())
+    assert st == 200
+    tracker = golden.FrequencyTracker(ScoringParams())
+    o, g = json.loads(out), golden.analyze(logs, sets, ScoringParams(), tracker)
+    assert o["metadata"]["totalLines"] == g["metadata"]["totalLines"]
+    assert o["summary"] == g["summary"] and len(o["events"]) == len(g["events"]) > 0
+    assert [e["context"] for e in o["events"]] == [e["context"] for e in g["events"]]
+
+    # engine level: a RawLogs batch == the same logs as bytes (fresh frequency state each time)
+    hs = N.HttpServer("127.0.0.1", 0, 1, 1 << 24, 60.0)
+    try:
+        bodies = [json.dumps({"pod": {}, "logs": l}).encode() for l in (logs, base, "")]
+        socks = []
+        for b in bodies:                  # connections stay open until the requests are drained
+            s = socket.create_connection(("127.0.0.1", hs.port))
+            s.sendall(b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                      b"Content-Length: %d\r\n\r\n" % len(b) + b)
+            socks.append(s)
+        got = []
+        for _ in range(50):
+            got += [r for r in hs.next_requests(8, 200, True) if r[1] == 0]
+            if len(got) == 3:
+                break
+        for s in socks:
+            s.close()
+        assert len(got) == 3
+        raws = sorted((r[2] for r in got), key=len, reverse=True)
+        assert [r.decode() for r in raws] == [l.encode() for l in (logs, base, "")]
+        eng = fe.svc.engine()
+        eng.freq.reset_all()
+        a = [json.loads(x) for x in eng.analyze_batch_json(raws)]
+        eng.freq.reset_all()
+        b = [json.loads(x) for x in eng.analyze_batch_json([logs.encode(), base.encode(), b""])]
+        for x, y in zip(a, b):
+            for r in (x, y):
+                r.pop("analysisId"), r["metadata"].pop("analyzedAt"), r["metadata"].pop("processingTimeMs")
+            assert x == y
+        # mixed batch: raw + plain bytes
+        eng.freq.reset_all()
+        m = [json.loads(x) for x in eng.analyze_batch_json([raws[0], base.encode()])]
+        assert m[0]["summary"] == a[0]["summary"] and m[1]["metadata"]["totalLines"] == a[1]["metadata"]["totalLines"]
+    finally:
+        hs.stop()

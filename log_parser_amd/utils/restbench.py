@@ -130,11 +130,17 @@ class ServerProcess:
         else:
             rc = None
             send = lambda: self.post(body)  # noqa: E731
+        import gc
+        gc_was = gc.isenabled()
         try:
             for _ in range(warmup):
                 st, out = send()
                 if st != 200:
                     raise RuntimeError(f"/parse returned {st}: {out[:200]!r}")
+            # the client's own collector must not land inside a round trip: a full collection of
+            # this (benchmark) process's heap takes milliseconds -- a C load generator has none
+            gc.collect()
+            gc.disable()
             lat = []
             for _ in range(n):
                 t = time.perf_counter()
@@ -143,6 +149,8 @@ class ServerProcess:
                 if st != 200:
                     raise RuntimeError(f"/parse returned {st}")
         finally:
+            if gc_was:
+                gc.enable()
             if rc is not None:
                 rc.close()
         return lat

@@ -101,7 +101,11 @@ def main():
                      device=dev)
         lb = logs.encode()
         out["engine"] = med(lambda: eng.analyze_batch_json([lb]), args.n)
-        out["parse_raw"] = round(float(np.median(server.parse_latencies(logs, args.n))) * 1e3, 3)
+        raw = np.array(server.parse_latencies(logs, args.n)) * 1e3
+        out["parse_raw"] = round(float(np.median(raw)), 3)
+        out["parse_raw_p90_p99_max"] = [round(float(np.percentile(raw, q)), 3) for q in (90, 99, 100)]
+        worst = np.argsort(raw)[-6:][::-1]
+        out["parse_raw_worst"] = [[int(i), round(float(raw[i]), 3)] for i in worst]     # (index, ms)
         out["parse_lib"] = round(float(np.median(server.parse_latencies(logs, args.n, client="http.client"))) * 1e3, 3)
         out["response_bytes"] = len(server.post(body)[1])
     finally:

@@ -115,7 +115,13 @@ def test_realistic_engine_matches_golden_cpu():
 
 
 @pytest.mark.gpu
-def test_scan_multi_gpu_equals_host(gpu_device):
+@pytest.mark.parametrize("mode", ["default", "bulk", "bulk_overflow"])
+def test_scan_multi_gpu_equals_host(gpu_device, mode, monkeypatch):
+    """default: a 30k-line text takes the one-line-per-lane request kernel; bulk: a 4-block grid
+    forces the bulk walk (hot blocks queued, re-walked by k_scan_rewalk); bulk_overflow: a 3-entry
+    hot-block queue overflows and the pass re-runs with the inline re-walk."""
+    if mode == "bulk_overflow":
+        monkeypatch.setenv("LP_SCAN_HOTQ_CAP", "3")
     _, trig, lib = _lib()
     data = make_log(30000, trig, seed=6, hit_rate=0.08, crlf_rate=0.1).encode()
     td, tc = _text(gpu_device, data), _text("cpu", data)
@@ -125,7 +131,8 @@ def test_scan_multi_gpu_equals_host(gpu_device):
     tabs_c = lib.device_tables(torch.device("cpu"))
     n = 0
     for sp_d, sp_c in zip(ed.tabs["scan_passes"], tabs_c["scan_passes"]):
-        hd = K.scan_multi(td, len(data), ls_d, ll_d, sp_d, 16, ed.scan_grid(sp_d))     # tiny cap: the retry path too
+        grid = ed.scan_grid(sp_d) if mode == "default" else 4
+        hd = K.scan_multi(td, len(data), ls_d, ll_d, sp_d, 16, grid)     # tiny cap: the retry path too
         hc = K.scan_multi(tc, len(data), ls_c, ll_c, sp_c, 1024)
         assert torch.equal(torch.sort(hd.cpu()).values, torch.sort(hc).values)
         n += hc.numel()
@@ -190,8 +197,9 @@ def _edge_text(seed: int) -> bytes:
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("bulk", [False, True])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_scan_multi_edge_cases_gpu_equals_host(gpu_device, seed):
+def test_scan_multi_edge_cases_gpu_equals_host(gpu_device, seed, bulk):
     """Stream-walk preconditions and fallbacks on the device: empty / blank lines, nullable
     regexes (start state accepting), CRLF and LF mixed, content ending in '\\r' or U+0085, bytes
     0xFF, long lines, a last line without newline -- hits equal the exact host walk."""
@@ -208,7 +216,8 @@ def test_scan_multi_edge_cases_gpu_equals_host(gpu_device, seed):
     ed = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
     tabs_c = lib.device_tables(torch.device("cpu"))
     for sp_d, sp_c in zip(ed.tabs["scan_passes"], tabs_c["scan_passes"]):
-        hd = torch.unique(K.scan_multi(td, len(data), ls_d, ll_d, sp_d, 1024, ed.scan_grid(sp_d)).cpu())
+        grid = 2 if bulk else ed.scan_grid(sp_d)                   # 2 blocks: the bulk (queued) walk
+        hd = torch.unique(K.scan_multi(td, len(data), ls_d, ll_d, sp_d, 1024, grid).cpu())
         hc = torch.unique(K.scan_multi(tc, len(data), ls_c, ll_c, sp_c, 1024))
         assert hc.numel() > 100
         assert torch.equal(hd, hc)

@@ -78,12 +78,9 @@ __device__ __forceinline__ void dfa_advance(const DfaRef (&D)[K], const uint8_t*
   if (e <= 0) return;
   const int sh = (int)((uintptr_t)s & 15);
   const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
-  // two blocks of look-ahead: the load of block k + 2 is issued while block k is walked, so a
-  // line's text loads overlap ~32 dependent table steps instead of 16 (a request's lines were
-  // stalling on every other block's memory latency)
-  uint4 cur = blk[0], nxt = blk[1];
+  uint4 cur = blk[0];
   for (int t0 = -sh; t0 < e; t0 += 16) {
-    const uint4 nx2 = blk[2];
+    const uint4 nxt = blk[1];
     ++blk;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -98,7 +95,6 @@ __device__ __forceinline__ void dfa_advance(const DfaRef (&D)[K], const uint8_t*
       }
     }
     cur = nxt;
-    nxt = nx2;
     bool alive = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) alive |= st[k] >= 2;

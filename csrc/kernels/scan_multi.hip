@@ -35,11 +35,8 @@
 // an unusual separator or a document boundary take the exact per-line walk.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-#include <mutex>
 #include <stdexcept>
 #include <string>
-#include <unordered_map>
 #include <vector>
 
 #include "lp_api.h"
@@ -205,24 +202,11 @@ __device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32
     if (acc[q]) scan_emit(S, g, acc[q], l + q < x1 ? l + q : x1 - 1, emit);
 }
 
-// Hot blocks of the bulk walk, re-walked by k_scan_rewalk (the inlined re-walk doubled the hot
-// kernel's registers: 103 -> 48 VGPRs without it, i.e. 4 -> 8 waves per SIMD to hide the
-// dependent LDS chain). Entry: block start, (run << 20 | group << 18 | LDS row byte of the group
-// at the block start). Past `cap` entries are dropped and k_scan_multi re-runs with the inline
-// re-walk (device-side check, no host read).
-struct HotQueue {
-  longlong2* q;
-  int64_t cap;
-  unsigned long long* count;
-};
-constexpr int HQ_RUN_SHIFT = 20;
-
 // the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold
-template <int G, bool CRLF, bool QUEUE, typename Emit>
+template <int G, bool CRLF, typename Emit>
 __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass& S, const uint8_t* text, int64_t p_lo,
                                               int64_t p_end, int64_t x0, int64_t x1,
-                                              const int64_t* __restrict__ line_start, Emit&& emit, int64_t run,
-                                              const HotQueue& hq) {
+                                              const int64_t* __restrict__ line_start, Emit&& emit) {
   uint32_t xr[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
@@ -264,16 +248,6 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
     uint32_t hotm = 0;
 #pragma unroll
     for (int g = 0; g < G; ++g) hotm |= (mx[g] >= (uint32_t)S.thr[g] ? 1u : 0u) << g;
-    if constexpr (QUEUE) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-        if ((hotm >> g) & 1u) {
-          const unsigned long long i = atomicAdd(hq.count, 1ull);
-          if ((int64_t)i < hq.cap)
-            hq.q[i] = make_longlong2(p0, (long long)((run << HQ_RUN_SHIFT) | ((int64_t)g << 18) | xs[g]));
-        }
-      hotm = 0;
-    }
     while (hotm) {      // one inlined re-walk, runtime group (an unrolled copy per group cost VGPRs)
       const int g = __builtin_ctz(hotm);
       hotm &= hotm - 1;
@@ -287,56 +261,12 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
   }
 }
 
-// one run of lines [x0, x1) as a stream walk: byte range [p_lo, p_end) (separators included)
-struct RunDesc {
-  int64_t x0, x1, p_lo, p_end;
-  bool fast, crlf;
-};
-
-__device__ __forceinline__ RunDesc run_desc(const uint8_t* __restrict__ text, int64_t nbytes,
-                                            const int64_t* __restrict__ line_start,
-                                            const int32_t* __restrict__ line_len, int64_t nlines, int64_t run,
-                                            int run_len) {
-  RunDesc r;
-  r.x0 = run * run_len;
-  r.x1 = r.x0 + run_len < nlines ? r.x0 + run_len : nlines;
-  // stream walk preconditions: "\n" / "\r\n" separators (after every line of the run,
-  // the last one included), the run starts right after a '\n', no content ends in a terminator
-  r.fast = true;
-  r.crlf = false;
-  int64_t st_next = line_start[r.x0];
-  r.p_lo = st_next;
-  r.p_end = 0;
-  for (int64_t x = r.x0; x < r.x1; ++x) {
-    const int64_t st = st_next;
-    const int n = line_len[x];
-    if (ends_in_terminator(text, st, n)) r.fast = false;
-    int64_t sep;
-    if (x + 1 < nlines) {
-      st_next = line_start[x + 1];
-      sep = st_next - st - n;
-    } else {                                   // the text's last line: is there a newline after it?
-      const int64_t e = st + n;
-      sep = (e < nbytes && text[e] == '\n') ? 1 : (e + 1 < nbytes && text[e] == '\r' && text[e + 1] == '\n') ? 2 : 0;
-    }
-    if (sep == 2) r.crlf = true;
-    else if (sep != 1) r.fast = false;
-    r.p_end = st + n + sep;                    // after the last line's separator
-  }
-  if (r.p_lo > 0 && text[r.p_lo - 1] != '\n') r.fast = false;   // e.g. a document boundary in a batch
-  return r;
-}
-
-// QUEUE: hot blocks go to `hq` (bulk texts); otherwise they are re-walked inline. `over`: run
-// only when the hot-block queue of a QUEUE launch overflowed (the whole pass again, inline).
-template <int G, int THREADS, bool QUEUE>
-__device__ __forceinline__ void scan_multi_body(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                const int64_t* __restrict__ line_start,
-                                                const int32_t* __restrict__ line_len, int64_t nlines,
-                                                const ScanPass& S, int64_t* __restrict__ out, int64_t cap,
-                                                unsigned long long* __restrict__ count, int run_len,
-                                                const HotQueue& hq, const unsigned long long* over) {
-  if (over && (int64_t)*over <= hq.cap) return;
+template <int G, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                        const int64_t* __restrict__ line_start,
+                                                        const int32_t* __restrict__ line_len, int64_t nlines,
+                                                        ScanPass S, int64_t* __restrict__ out, int64_t cap,
+                                                        unsigned long long* __restrict__ count, int run_len) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   lds_fill<uint4>(reinterpret_cast<uint4*>(sm), reinterpret_cast<const uint4*>(S.blob), S.lds_words >> 2);  // multiple of 4
   __syncthreads();
@@ -346,108 +276,42 @@ __device__ __forceinline__ void scan_multi_body(const uint8_t* __restrict__ text
   const int64_t nruns = (nlines + run_len - 1) / run_len;
   const int64_t stride = (int64_t)gridDim.x * THREADS;
   for (int64_t run = (int64_t)blockIdx.x * THREADS + threadIdx.x; run < nruns; run += stride) {
-    const RunDesc r = run_desc(text, nbytes, line_start, line_len, nlines, run, run_len);
-    if (!r.fast || !at_zero) {     // rare: exact per-line walks (an overflow re-run: done already)
-      if (!over)
-        for (int64_t x = r.x0; x < r.x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
+    const int64_t x0 = run * run_len;
+    const int64_t x1 = x0 + run_len < nlines ? x0 + run_len : nlines;
+    // stream walk preconditions: "\n" / "\r\n" separators (after every line of the run,
+    // the last one included), the run starts right after a '\n', no content ends in a terminator
+    bool fast = true, crlf = false;
+    int64_t st_next = line_start[x0];
+    const int64_t p_lo = st_next;
+    int64_t p_end = 0;
+    for (int64_t x = x0; x < x1; ++x) {
+      const int64_t st = st_next;
+      const int n = line_len[x];
+      if (ends_in_terminator(text, st, n)) fast = false;
+      int64_t sep;
+      if (x + 1 < nlines) {
+        st_next = line_start[x + 1];
+        sep = st_next - st - n;
+      } else {                                   // the text's last line: is there a newline after it?
+        const int64_t e = st + n;
+        sep = (e < nbytes && text[e] == '\n') ? 1 : (e + 1 < nbytes && text[e] == '\r' && text[e + 1] == '\n') ? 2 : 0;
+      }
+      if (sep == 2) crlf = true;
+      else if (sep != 1) fast = false;
+      p_end = st + n + sep;                      // after the last line's separator
+    }
+    if (p_lo > 0 && text[p_lo - 1] != '\n') fast = false;   // e.g. a document boundary in a batch
+    if (!at_zero) fast = false;
+    if (!fast) {     // rare: exact per-line walks
+      for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
       continue;
     }
-    if (r.crlf)
-      scan_run_fast<G, true, QUEUE>(sm, S, text, r.p_lo, r.p_end, r.x0, r.x1, line_start, emit, run, hq);
+    if (crlf)
+      scan_run_fast<G, true>(sm, S, text, p_lo, p_end, x0, x1, line_start, emit);
     else
-      scan_run_fast<G, false, QUEUE>(sm, S, text, r.p_lo, r.p_end, r.x0, r.x1, line_start, emit, run, hq);
+      scan_run_fast<G, false>(sm, S, text, p_lo, p_end, x0, x1, line_start, emit);
   }
 }
-
-template <int G, int THREADS>
-__global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                        const int64_t* __restrict__ line_start,
-                                                        const int32_t* __restrict__ line_len, int64_t nlines,
-                                                        ScanPass S, int64_t* __restrict__ out, int64_t cap,
-                                                        unsigned long long* __restrict__ count, int run_len,
-                                                        HotQueue hq, const unsigned long long* over) {
-  scan_multi_body<G, THREADS, false>(text, nbytes, line_start, line_len, nlines, S, out, cap, count, run_len, hq, over);
-}
-
-// bulk hot walk: two 1024-thread blocks per CU (8 waves per SIMD) need <= 64 VGPRs
-template <int G>
-__global__ __launch_bounds__(SCAN_THREADS) __attribute__((amdgpu_waves_per_eu(8, 8)))
-void k_scan_multi_q(const uint8_t* __restrict__ text, int64_t nbytes, const int64_t* __restrict__ line_start,
-                    const int32_t* __restrict__ line_len, int64_t nlines, ScanPass S, int64_t* __restrict__ out,
-                    int64_t cap, unsigned long long* __restrict__ count, int run_len, HotQueue hq) {
-  scan_multi_body<G, SCAN_THREADS, true>(text, nbytes, line_start, line_len, nlines, S, out, cap, count, run_len, hq,
-                                          nullptr);
-}
-
-// The queued hot blocks: the exact re-walk of each through the LDS rows (scan_block_masks), from
-// the state the hot walk saved. Does nothing when the queue overflowed (k_scan_multi<.., false>
-// with `over` then redoes the pass).
-template <int G>
-__global__ __launch_bounds__(256) void k_scan_rewalk(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                     const int64_t* __restrict__ line_start,
-                                                     const int32_t* __restrict__ line_len, int64_t nlines,
-                                                     ScanPass S, int64_t* __restrict__ out, int64_t cap,
-                                                     unsigned long long* __restrict__ count, int run_len, HotQueue hq) {
-  const int64_t nq = (int64_t)*hq.count;
-  if (nq > hq.cap || nq == 0) return;
-  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-  lds_fill<uint4>(reinterpret_cast<uint4*>(sm), reinterpret_cast<const uint4*>(S.blob), S.lds_words >> 2);
-  __syncthreads();
-  const GlobalEmit emit{out, cap, count};
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nq; i += (int64_t)gridDim.x * 256) {
-    const longlong2 e = hq.q[i];
-    const int64_t p0 = e.x;
-    const int64_t run = (int64_t)((uint64_t)e.y >> HQ_RUN_SHIFT);
-    const int g = (int)((e.y >> 18) & 3);
-    const uint32_t xg = (uint32_t)(e.y & 0x3FFFF);
-    const RunDesc r = run_desc(text, nbytes, line_start, line_len, nlines, run, run_len);
-    const uint4 cur = *reinterpret_cast<const uint4*>(text + p0);
-    const uint32_t nx = *reinterpret_cast<const uint32_t*>(text + p0 + 16);
-    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nx};
-    if (r.crlf) {
-      uint32_t hold = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t b = crlf_bits(w[q], w[q + 1]);
-        hold |= (((b >> 7) & 1u) | ((b >> 14) & 2u) | ((b >> 21) & 4u) | ((b >> 28) & 8u)) << (4 * q);
-      }
-      scan_block_masks<true>(S, w, hold, p0, r.p_lo, r.p_end, r.x0, r.x1, line_start, g, xg, emit);
-    } else {
-      scan_block_masks<false>(S, w, 0u, p0, r.p_lo, r.p_end, r.x0, r.x1, line_start, g, xg, emit);
-    }
-  }
-}
-
-namespace {
-// per-stream hot-block queues (grow-only device buffers; engines on one device may run bulk
-// batches concurrently on their own streams)
-struct HotBuf {
-  longlong2* q = nullptr;
-  unsigned long long* count = nullptr;
-  int64_t cap = 0;
-};
-std::mutex g_hq_mu;
-std::unordered_map<uint64_t, HotBuf> g_hq;
-
-HotBuf hot_buffer(uint64_t stream, int64_t want) {
-  std::lock_guard<std::mutex> lk(g_hq_mu);
-  HotBuf& b = g_hq[stream];
-  if (b.cap < want) {
-    // grown between launches on this stream: wait for the previous user before freeing
-    if (b.q) {
-      if (hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)) != hipSuccess ||
-          hipFree(b.q) != hipSuccess || hipFree(b.count) != hipSuccess)
-        throw std::runtime_error("scan_multi: hot queue free failed");
-    }
-    b = HotBuf{};
-    if (hipMalloc(reinterpret_cast<void**>(&b.q), (size_t)want * sizeof(longlong2)) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&b.count), 64) != hipSuccess)
-      throw std::runtime_error("scan_multi: hot queue allocation failed");
-    b.cap = want;
-  }
-  return b;
-}
-}  // namespace
 
 void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                     const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,
@@ -464,30 +328,13 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
   const int64_t runs = (nlines + run_len - 1) / run_len;
   const int64_t need = (runs + threads - 1) / threads;
   const int g = (int)std::max<int64_t>(1, std::min<int64_t>(small ? 4 * (int64_t)grid : grid, need));
-  HotQueue hq{nullptr, 0, nullptr};
-  if (!small) {
-    // capacity: one hot (block, group) per 64 text bytes -- far above what log text produces;
-    // past it the pass re-runs with the inline re-walk (correct, slower)
-    const HotBuf b = hot_buffer(stream, std::max<int64_t>(int64_t(1) << 16, nbytes >> 6));
-    hq = HotQueue{b.q, b.cap, b.count};
-    if (const char* e = std::getenv("LP_SCAN_HOTQ_CAP")) hq.cap = std::min<int64_t>(b.cap, std::atoll(e));   // tests
-    if (hipMemsetAsync(b.count, 0, sizeof(unsigned long long), st) != hipSuccess)
-      throw std::runtime_error("scan_multi: hot queue reset failed");
-  }
-  const HotQueue none{nullptr, 0, nullptr};
-  const int rw_grid = std::max(1, std::min(grid, 1024));
 #define LP_SCAN(GV)                                                                                        \
-  if (small) {                                                                                             \
-    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS_SMALL>), dim3(g), dim3(SCAN_THREADS_SMALL), lds, st, \
-                       text, nbytes, line_start, line_len, nlines, S, out, cap, count, run_len, none, nullptr); \
-  } else {                                                                                                 \
-    hipLaunchKernelGGL((k_scan_multi_q<GV>), dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, line_start,   \
-                       line_len, nlines, S, out, cap, count, run_len, hq);                                \
-    hipLaunchKernelGGL((k_scan_rewalk<GV>), dim3(rw_grid), dim3(256), lds, st, text, nbytes, line_start, line_len, \
-                       nlines, S, out, cap, count, run_len, hq);                                           \
-    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS>), dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes,   \
-                       line_start, line_len, nlines, S, out, cap, count, run_len, hq, hq.count);           \
-  }
+  if (small)                                                                                               \
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS_SMALL>), dim3(g), dim3(SCAN_THREADS_SMALL), lds, st, text, \
+                       nbytes, line_start, line_len, nlines, S, out, cap, count, run_len);                 \
+  else                                                                                                     \
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS>), dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, \
+                       line_start, line_len, nlines, S, out, cap, count, run_len)
   switch (S.ngroups) {
     case 1: LP_SCAN(1); break;
     case 2: LP_SCAN(2); break;

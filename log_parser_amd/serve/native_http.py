@@ -13,6 +13,8 @@ Every other route (``/ready``, ``/metrics``, ``/admin/*``, the json.loads fallba
 from __future__ import annotations
 
 import logging
+import os
+import sys
 import threading
 import time
 from typing import Optional
@@ -31,6 +33,9 @@ class NativeHttpFrontend:
                                 float(service.config["server.idle-timeout-s"]))
         self.port = self.srv.port
         self._stop = threading.Event()
+        # LP_PARSE_TRACE=1: per /parse request on stderr -- queue (body complete -> drained by the
+        # pump) and engine (drained -> response queued) microseconds (tools/parse_tail.py)
+        self._trace = {} if os.environ.get("LP_PARSE_TRACE") else None
         self._t = threading.Thread(target=self._pump, name="lp-http-pump", daemon=True)
         self._t.start()
         log.info("native HTTP front end on %s:%d (%d IO threads)", host, self.port, io_threads)
@@ -63,7 +68,9 @@ class NativeHttpFrontend:
                 t0 = time.perf_counter()
                 try:
                     if kind == 0:                            # validated POST /parse
-                        _, _, logs, name, _ = req
+                        _, _, logs, name, t_arr = req
+                        if self._trace is not None:
+                            self._trace[rid] = t_arr
                         if direct:
                             log.info("Received analysis request for pod: %s", name or "<unknown>")
                             batch.append((rid, logs, name, t0))
@@ -117,6 +124,9 @@ class NativeHttpFrontend:
             return
         for (rid, logs, name, ta), out in zip(batch, outs):
             self.srv.respond(rid, 200, "application/json", out)
+            if self._trace is not None and rid in self._trace:
+                sys.stderr.write("lp-parse-trace queue_us %.1f engine_us %.1f\n" % (
+                    (ta - self._trace.pop(rid)) * 1e6, (time.perf_counter() - ta) * 1e6))
             self.svc.metrics.observe_request(200, time.perf_counter() - ta, len(logs))
             log.info("Analysis complete for pod: %s.", name or "<unknown>")
 

@@ -86,6 +86,8 @@ class HttpServer {
   double io_spin_s_ = 0;     // LP_HTTP_SPIN_US: IO threads poll (no sleep) this long after activity
   bool trace_ = false;       // LP_HTTP_TRACE: per-request receive / validate timings on stderr
   double pump_spin_s_ = 0;   // LP_HTTP_PUMP_SPIN_US: next_requests polls this long before waiting
+  bool quickack_ = true;     // TCP_QUICKACK re-armed per read (LP_HTTP_QUICKACK=0: delayed ACKs)
+  int rcvbuf_ = 0;           // LP_HTTP_RCVBUF: SO_RCVBUF of accepted sockets (0 = autotuned)
   std::atomic<bool> stop_{false};
   std::vector<std::unique_ptr<Io>> ios_;
   std::vector<std::thread> threads_;

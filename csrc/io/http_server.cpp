@@ -118,6 +118,9 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
     : host_(host), port_(port), max_body_(max_body), idle_timeout_s_(idle_timeout_s) {
   io_threads = std::max(1, std::min(io_threads, kMaxIo));
   if (const char* e = getenv("LP_HTTP_SPIN_US")) io_spin_s_ = atof(e) * 1e-6;
+  // the pump polls for the next request this long before sleeping on the queue's condition
+  // variable (a sleeping pump took ~45 us to wake: /parse "queue" time, tools/parse_tail.py)
+  pump_spin_s_ = 1e-3;
   if (const char* e = getenv("LP_HTTP_PUMP_SPIN_US")) pump_spin_s_ = atof(e) * 1e-6;
   // Receive-side TCP: ACK every read at once. With delayed ACKs ~1-2% of 1 MB request bodies
   // stalled ~1.5 ms in the receive (the sender waiting on a window update): /parse p99 2.1 ms ->
@@ -184,13 +187,8 @@ void HttpServer::stop() {
 std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
   if (pump_spin_s_ > 0) {
     const double until = now_s() + pump_spin_s_;
-    for (;;) {
-      {
-        std::lock_guard<std::mutex> g(qm_);
-        if (!q_.empty() || stop_) break;
-      }
-      if (now_s() > until) break;
-      __builtin_ia32_pause();
+    while (qn_.load(std::memory_order_acquire) == 0 && !stop_ && now_s() <= until) {
+      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
     }
   }
   std::unique_lock<std::mutex> lk(qm_);
@@ -203,6 +201,7 @@ std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
   while (!q_.empty() && (int)r.size() < max_n) {
     r.push_back(std::move(q_.front()));
     q_.pop_front();
+    qn_.store(q_.size(), std::memory_order_release);
   }
   return r;
 }
@@ -454,6 +453,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
   {
     std::lock_guard<std::mutex> lk(qm_);
     q_.push_back(std::move(r));
+    qn_.store(q_.size(), std::memory_order_release);
   }
   qcv_.notify_one();
   return false;

@@ -85,7 +85,7 @@ class HttpServer {
   double idle_timeout_s_;
   double io_spin_s_ = 0;     // LP_HTTP_SPIN_US: IO threads poll (no sleep) this long after activity
   bool trace_ = false;       // LP_HTTP_TRACE: per-request receive / validate timings on stderr
-  double pump_spin_s_ = 0;   // LP_HTTP_PUMP_SPIN_US: next_requests polls this long before waiting
+  double pump_spin_s_ = 0;   // next_requests polls this long before waiting (1 ms; LP_HTTP_PUMP_SPIN_US)
   bool quickack_ = true;     // TCP_QUICKACK re-armed per read (LP_HTTP_QUICKACK=0: delayed ACKs)
   int rcvbuf_ = 0;           // LP_HTTP_RCVBUF: SO_RCVBUF of accepted sockets (0 = autotuned)
   std::atomic<bool> stop_{false};
@@ -95,6 +95,7 @@ class HttpServer {
   std::mutex qm_;
   std::condition_variable qcv_;
   std::deque<HttpRequest> q_;
+  std::atomic<size_t> qn_{0};   // q_.size(), for the pump's lock-free spin
   std::atomic<uint64_t> next_id_{1};
   std::shared_ptr<BufferPool> pool_ = std::make_shared<BufferPool>();
 };

@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <vector>
+
 #include "lp_core.h"
 
 namespace lp {
@@ -28,6 +30,11 @@ void seq_chain_host(const int32_t* slot_seq, const int32_t* seq_ev_off, const in
                     const int64_t* hit_off, const int32_t* hit_line, int32_t own_lo, int32_t own_hi, int nslots,
                     int32_t* out);
 int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
+// AVX-512 bloom tier of the host twin (prefilter_cpu.cpp): 4-gram-only bloom, no Teddy tier;
+// handles positions from the 4-aligned point at or after `a` in 64-byte steps, returns where it stopped
+bool prefilter_bloom_simd_ok();
+int64_t prefilter_bloom_simd(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
+                             int64_t nlines, int64_t a, int64_t b, std::vector<int64_t>& out);
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap);
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,

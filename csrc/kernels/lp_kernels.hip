@@ -475,28 +475,53 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
                        int64_t nlines, int64_t* cand, int64_t cap) {
   std::vector<std::vector<int64_t>> part(std::max(1, host_threads()));
   const int S = std::max(1, T.stride);
-  host_parallel(nbytes, 1 << 18, [&](int t, int64_t a, int64_t b) {
+  // 4-gram-only bloom, no Teddy tier: the AVX-512 path, threads only for multi-MB texts (request-sized
+  // texts ran slower on the pool than on the calling thread)
+  const bool simd = !T.teddy_on && T.gmask == (1 << 4) && (S == 1 || S == 2 || S == 4) && prefilter_bloom_simd_ok();
+  host_parallel(nbytes, simd ? (int64_t(4) << 20) : (1 << 18), [&](int t, int64_t a, int64_t b) {
     auto& out = part[t];
     auto app = [&](int64_t v) { out.push_back(v); };
     const uint32_t* bl = T.bloom;
-    // rolling lower-cased 4-gram starting at p (bytes past the end read as 0)
-    uint32_t g4 = 0;
-    for (int k = 3; k >= 0; --k) g4 = (g4 << 8) | (uint32_t)(a + k < nbytes ? lower_byte(text[a + k]) : 0);
-    for (int64_t p = a; p < b; ++p) {
-      // bloom tier: like k_prefilter<GM, S>, only positions divisible by the stride (one
-      // candidate per literal occurrence, not one per indexed window)
-      if (p % S == 0)
-        for (int g = 4; g >= 2; --g) {
-          if (!(T.gmask & (1 << g))) continue;
-          const uint32_t key = g4 & gram_mask(g);
-          if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
-          pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
+    // lower-cased 4-gram starting at p (bytes past the end read as 0): one unaligned load + SWAR
+    auto gram = [&](int64_t p) -> uint32_t {
+      if (p + 4 <= nbytes) {
+        uint32_t w;
+        std::memcpy(&w, text + p, 4);
+        return lower4(w);
+      }
+      uint32_t g4 = 0;
+      for (int k = 3; k >= 0; --k) g4 = (g4 << 8) | (uint32_t)(p + k < nbytes ? lower_byte(text[p + k]) : 0);
+      return g4;
+    };
+    // bloom tier: like k_prefilter<GM, S>, only positions divisible by the stride (one candidate
+    // per literal occurrence, not one per indexed window)
+    auto bloom_at = [&](int64_t p) {
+      const uint32_t g4 = gram(p);
+      for (int g = 4; g >= 2; --g) {
+        if (!(T.gmask & (1 << g))) continue;
+        const uint32_t key = g4 & gram_mask(g);
+        if (!bloom_test(bl, key, g, T.bloom_bits)) continue;
+        pf_probe(T, text, nbytes, p, key, g, line_start, nlines, nullptr, app);
+      }
+    };
+    const int64_t p0 = (a + S - 1) / S * S;
+    if (simd) {
+      const int64_t v0 = (a + 3) & ~int64_t(3);
+      for (int64_t p = p0; p < v0 && p < b; p += S) bloom_at(p);
+      const int64_t v1 = prefilter_bloom_simd(text, nbytes, T, line_start, nlines, v0, b, out);
+      for (int64_t p = std::max(v1, p0); p < b; p += S) bloom_at(p);
+    } else if (!T.teddy_on) {       // the stride's positions only
+      for (int64_t p = p0; p < b; p += S) bloom_at(p);
+    } else {
+      int64_t next = p0;
+      for (int64_t p = a; p < b; ++p) {
+        if (p == next) {
+          bloom_at(p);
+          next += S;
         }
-      if (T.teddy_on) {
         const uint32_t m = teddy_mask(T, text, nbytes, p);
         if (m) teddy_probe(T, text, nbytes, p, m, line_start, nlines, nullptr, app);
       }
-      g4 = (g4 >> 8) | ((uint32_t)(p + 4 < nbytes ? lower_byte(text[p + 4]) : 0) << 24);
     }
   });
   int64_t count = 0;

@@ -37,6 +37,7 @@ SOURCES = [
     ("io/json_in.cpp", "cpp"),
     ("io/http_server.cpp", "cpp"),
     ("runtime/request.cpp", "cpp"),
+    ("kernels/prefilter_cpu.cpp", "cpp"),
     ("bind.cpp", "cpp"),
 ]
 

@@ -192,3 +192,43 @@ def test_every_prefilter_variant_gpu_equals_cpu_and_golden(gpu_device, smax, ted
     assert [(e["lineNumber"] - 1, e["matchedPattern"]["id"]) for e in ref["events"]] == \
         [(int(x), lib.patterns[int(p)].id) for x, p in zip(g[0], g[1])]
     np.testing.assert_allclose(g[2], [e["score"] for e in ref["events"]], rtol=1e-12)
+
+
+@pytest.mark.parametrize("S", [1, 2, 4])
+def test_host_prefilter_simd_equals_exact_literal_search(S):
+    """The CPU backend's bloom tier (AVX-512, 16 positions per step, prefilter_cpu.cpp) finds every
+    literal occurrence: its candidates == an exact search for every library literal on every line,
+    with occurrences at every residue mod 64 (step edges), mixed case, the text end and no-hit text."""
+    import torch
+    from log_parser_amd.ops import kernels as K
+    lib = _lib_with_max_stride(S, n=40, seed=11, teddy=False)
+    assert lib.pf["stride"] == S and lib.pf["gmask"] == 16
+    tabs = lib.device_tables(torch.device("cpu"))
+    rng = random.Random(S)
+    lines = []
+    for i in range(3000):
+        pad = "x" * rng.randrange(0, 130)
+        if rng.random() < 0.1:
+            lit = rng.choice(lib.literals).decode("latin-1")
+            lit = lit.upper() if rng.random() < 0.3 else lit
+            lines.append(pad + lit + "y" * rng.randrange(0, 5))
+        else:
+            lines.append(pad + "noise line %d" % i)
+    lines.append("tail " + lib.literals[0].decode("latin-1"))        # literal touching the text end
+    data = "\n".join(lines).encode()
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    ls, ll = K.split_lines(t, len(data))
+    got = set(K.prefilter(t, len(data), tabs["pf"], ls, 1 << 16).tolist())
+    # exact: (regex << 32 | line) for every literal occurring (case-insensitively) in a line
+    lit_regs = {}
+    for i, lit in enumerate(lib.literals):
+        a, b = int(lib.pf["lit_reg_off"][i]), int(lib.pf["lit_reg_off"][i + 1])
+        lit_regs[lit.lower()] = [int(r) for r in lib.pf["lit_reg"][a:b]]
+    want = set()
+    for x, line in enumerate(data.split(b"\n")):
+        low = line.lower()
+        for lit, regs in lit_regs.items():
+            if lit in low:
+                want.update((r << 32) | x for r in regs)
+    assert got == want and len(want) > 100

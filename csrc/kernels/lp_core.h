@@ -156,12 +156,34 @@ LP_HD uint8_t context_feat(const DfaPool& P, const uint8_t* s, int len) {
   const uint8_t f = (res & 1u) ? 1 : ((res & 2u) ? 2 : 0);
   return (uint8_t)(f | (res & 12u));
 #else
-  uint8_t f = 0;
-  if (dfa_run(P, 0, s, len)) f |= 1;
-  else if (dfa_run(P, 1, s, len)) f |= 2;
-  if (dfa_run(P, 2, s, len)) f |= 4;
-  if (dfa_run(P, 3, s, len)) f |= 8;
-  return f;
+  // host: the 4 walks advance together too (4 independent table-load chains per byte for the
+  // out-of-order core instead of 4 passes); same Matcher.find semantics as dfa_find_k
+  const DfaRef D[4] = {dfa_ref(P, 0), dfa_ref(P, 1), dfa_ref(P, 2), dfa_ref(P, 3)};
+  int st[4] = {2, 2, 2, 2};
+  auto advance = [&](const uint8_t* q, int e) {
+    for (int t = 0; t < e; ++t) {
+      const int c = q[t];
+      bool alive = false;
+      for (int k = 0; k < 4; ++k) {
+        if (st[k] >= 2) st[k] = D[k].T[st[k] * D[k].nc + D[k].bm[c]];
+        alive |= st[k] >= 2;
+      }
+      if (!alive) return;
+    }
+  };
+  const int ftl = final_term_len(s, len);
+  const int ft = len - ftl;
+  advance(s, ft);
+  if (ftl) {
+    for (int k = 0; k < 4; ++k)
+      if (st[k] >= 2 && (D[k].A[st[k]] & 2)) st[k] = 1;
+    advance(s + ft, ftl);
+  }
+  uint32_t res = 0;
+  for (int k = 0; k < 4; ++k)
+    if (st[k] == 1 || (st[k] >= 2 && (D[k].A[st[k]] & 1))) res |= 1u << k;
+  const uint8_t f = (res & 1u) ? 1 : ((res & 2u) ? 2 : 0);
+  return (uint8_t)(f | (res & 12u));
 #endif
 }
 

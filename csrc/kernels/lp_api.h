@@ -35,6 +35,8 @@ int64_t nl_positions_host(const uint8_t* text, int64_t nbytes, int64_t* nl_pos);
 bool prefilter_bloom_simd_ok();
 int64_t prefilter_bloom_simd(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                              int64_t nlines, int64_t a, int64_t b, std::vector<int64_t>& out);
+int64_t prefilter_teddy_simd(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
+                             int64_t nlines, int64_t a, int64_t b, std::vector<int64_t>& out);
 int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start,
                        int64_t nlines, int64_t* cand, int64_t cap);
 int64_t scan_host(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,

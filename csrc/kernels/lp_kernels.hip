@@ -477,8 +477,9 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
   const int S = std::max(1, T.stride);
   // 4-gram-only bloom, no Teddy tier: the AVX-512 path, threads only for multi-MB texts (request-sized
   // texts ran slower on the pool than on the calling thread)
-  const bool simd = !T.teddy_on && T.gmask == (1 << 4) && (S == 1 || S == 2 || S == 4) && prefilter_bloom_simd_ok();
-  host_parallel(nbytes, simd ? (int64_t(4) << 20) : (1 << 18), [&](int t, int64_t a, int64_t b) {
+  const bool vec = prefilter_bloom_simd_ok();
+  const bool simd = vec && T.gmask == (1 << 4) && (S == 1 || S == 2 || S == 4);
+  host_parallel(nbytes, vec ? (int64_t(4) << 20) : (1 << 18), [&](int t, int64_t a, int64_t b) {
     auto& out = part[t];
     auto app = [&](int64_t v) { out.push_back(v); };
     const uint32_t* bl = T.bloom;
@@ -505,20 +506,18 @@ int64_t prefilter_host(const uint8_t* text, int64_t nbytes, const PfTables& T, c
       }
     };
     const int64_t p0 = (a + S - 1) / S * S;
+    // the two tiers in separate passes (candidates are unordered: the hit CSR sorts them)
     if (simd) {
       const int64_t v0 = (a + 3) & ~int64_t(3);
       for (int64_t p = p0; p < v0 && p < b; p += S) bloom_at(p);
       const int64_t v1 = prefilter_bloom_simd(text, nbytes, T, line_start, nlines, v0, b, out);
       for (int64_t p = std::max(v1, p0); p < b; p += S) bloom_at(p);
-    } else if (!T.teddy_on) {       // the stride's positions only
+    } else if (T.gmask) {           // the stride's positions only
       for (int64_t p = p0; p < b; p += S) bloom_at(p);
-    } else {
-      int64_t next = p0;
-      for (int64_t p = a; p < b; ++p) {
-        if (p == next) {
-          bloom_at(p);
-          next += S;
-        }
+    }
+    if (T.teddy_on) {
+      const int64_t t1 = vec ? prefilter_teddy_simd(text, nbytes, T, line_start, nlines, a, b, out) : a;
+      for (int64_t p = t1; p < b; ++p) {
         const uint32_t m = teddy_mask(T, text, nbytes, p);
         if (m) teddy_probe(T, text, nbytes, p, m, line_start, nlines, nullptr, app);
       }

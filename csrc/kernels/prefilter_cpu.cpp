@@ -65,4 +65,46 @@ __attribute__((target("avx512f,avx512bw"))) int64_t prefilter_bloom_simd(
   return p;
 }
 
+// Short-literal (Teddy) tier, every position p in [a, b): the bucket mask of the 3-byte window is
+// teddy[4 c0] & teddy[4 c1 + 1] & teddy[4 c2 + 2] (lower-cased bytes); 16 positions per step with
+// three gathers, the scalar probe only where the mask is non-zero. Returns the first position not
+// handled (the window must stay clear of the text end: bytes past it read as 0).
+__attribute__((target("avx512f,avx512bw"))) int64_t prefilter_teddy_simd(
+    const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines, int64_t a,
+    int64_t b, std::vector<int64_t>& out) {
+  auto app = [&](int64_t v) { out.push_back(v); };
+  const __m512i cA = _mm512_set1_epi32('A'), cZ = _mm512_set1_epi32('Z'), c20 = _mm512_set1_epi32(0x20);
+  const __m512i j1 = _mm512_set1_epi32(1), j2 = _mm512_set1_epi32(2);
+  const void* tb = reinterpret_cast<const void*>(T.teddy);
+#define LP_TEDDY_LANES(q, out)                                                                       \
+  do {                                                                                               \
+    __m512i v_ = _mm512_cvtepu8_epi32(_mm_loadu_si128(reinterpret_cast<const __m128i*>(q)));        \
+    const __mmask16 up_ = _mm512_cmpge_epu32_mask(v_, cA) & _mm512_cmple_epu32_mask(v_, cZ);        \
+    out = _mm512_slli_epi32(_mm512_mask_add_epi32(v_, up_, v_, c20), 2);                            \
+  } while (0)
+  int64_t p = a;
+  for (; p + 16 + 2 <= b && p + 16 + 2 <= nbytes; p += 16) {
+    __m512i i0, i1, i2;                 // 16 lower-cased bytes as dwords, x4 (table index)
+    LP_TEDDY_LANES(text + p, i0);
+    LP_TEDDY_LANES(text + p + 1, i1);
+    LP_TEDDY_LANES(text + p + 2, i2);
+    const __m512i m0 = _mm512_i32gather_epi32(i0, tb, 4);
+    const __m512i m1 = _mm512_i32gather_epi32(_mm512_add_epi32(i1, j1), tb, 4);
+    const __m512i m2 = _mm512_i32gather_epi32(_mm512_add_epi32(i2, j2), tb, 4);
+    const __m512i m = _mm512_and_si512(_mm512_and_si512(m0, m1), m2);
+    __mmask16 hit = _mm512_test_epi32_mask(m, m);
+    if (hit) {
+      alignas(64) uint32_t mk[16];
+      _mm512_store_si512(reinterpret_cast<void*>(mk), m);
+      while (hit) {
+        const int k = __builtin_ctz(hit);
+        hit &= hit - 1;
+        teddy_probe(T, text, nbytes, p + k, mk[k], line_start, nlines, nullptr, app);
+      }
+    }
+  }
+  return p;
+}
+#undef LP_TEDDY_LANES
+
 }  // namespace lp

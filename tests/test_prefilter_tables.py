@@ -232,3 +232,42 @@ def test_host_prefilter_simd_equals_exact_literal_search(S):
             if lit in low:
                 want.update((r << 32) | x for r in regs)
     assert got == want and len(want) > 100
+
+
+def test_host_prefilter_simd_teddy_equals_exact_literal_search():
+    """Both tiers on the CPU backend (AVX-512 bloom tier for the long literals, three-gather Teddy tier
+    for the 3-6-byte ones): candidates == an exact literal search on every line."""
+    import torch
+    from log_parser_amd.ops import kernels as K
+    from log_parser_amd.utils.synth import realistic_library
+    sets, trig = realistic_library(120, seed=5)
+    lib = C.CompiledLibrary(sets, ScoringParams())
+    assert lib.pf["teddy_lits"] > 0 and lib.pf["gmask"] == 16
+    tabs = lib.device_tables(torch.device("cpu"))
+    rng = random.Random(21)
+    lines = []
+    for i in range(4000):
+        pad = "q" * rng.randrange(0, 90)
+        if rng.random() < 0.15:
+            lit = rng.choice(lib.literals).decode("latin-1")
+            lit = lit.upper() if rng.random() < 0.3 else lit
+            lines.append(pad + lit + "z" * rng.randrange(0, 4))
+        else:
+            lines.append(pad + "plain text %d" % i)
+    lines.append(lib.literals[-1].decode("latin-1"))
+    data = "\n".join(lines).encode()
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    ls, ll = K.split_lines(t, len(data))
+    got = set(K.prefilter(t, len(data), tabs["pf"], ls, 1 << 18).tolist())
+    lit_regs = {}
+    for i, lit in enumerate(lib.literals):
+        a, b = int(lib.pf["lit_reg_off"][i]), int(lib.pf["lit_reg_off"][i + 1])
+        lit_regs.setdefault(lit.lower(), []).extend(int(r) for r in lib.pf["lit_reg"][a:b])
+    want = set()
+    for x, line in enumerate(data.split(b"\n")):
+        low = line.lower()
+        for lit, regs in lit_regs.items():
+            if lit in low:
+                want.update((r << 32) | x for r in regs)
+    assert got == want and len(want) > 100

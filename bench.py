@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--profile", action="store_true", help="per-stage HIP-event timings (no extra syncs)")
     ap.add_argument("--device", default="auto")
-    ap.add_argument("--parse-requests", type=int, default=100,
+    ap.add_argument("--parse-requests", type=int, default=300,
                     help="rank 0: p50 latency of N single 10k-line POST /parse requests after the timed loop (0 = off)")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="server front end for p50")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
@@ -306,7 +306,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
             # second half of the BASELINE metric: one 10k-line /parse request, same library
             req = make_log(10_000, trig, seed=13, hit_rate=0.01)
             if server is not None:
-                lat = server.parse_latencies(req, args.parse_requests, warmup=20)   # server idle since start-up
+                lat = server.parse_latencies(req, args.parse_requests, warmup=50)   # server idle since start-up
                 rec["p50_parse_ms"] = round(float(np.median(lat)) * 1e3, 3)
                 rec["p99_parse_ms"] = round(float(np.percentile(lat, 99)) * 1e3, 3)
                 rec["parse_transport"] = f"{args.http} HTTP/1.1 keep-alive, server process on 127.0.0.1"

@@ -227,6 +227,10 @@ int64_t request_line_cap();
 void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream);
 void publish_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host, uint8_t* res_host,
                  uint64_t stream);
+// publish_dev + the batch's gated frequency record (k_freq_record) in one launch
+void publish_record_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host,
+                        uint8_t* res_host, const int64_t* counts, int K, double now, const FreqRing& R,
+                        const RecordGate& G, uint64_t stream);
 void blk_index_dev(const int64_t* ls, int64_t L, int64_t nblocks, int32_t* blk, uint64_t stream);
 void hits_host(const HitsArgs& A);
 void events_host(const EventsArgs& A);

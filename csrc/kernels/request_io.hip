@@ -77,6 +77,66 @@ void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in fetch");
 }
 
+// k_publish and the frequency record of the batch (k_freq_record, freq_state.hip) in ONE launch:
+// both only read the finished results, so blocks [0, rec_blocks) record the per-key counts into
+// the device window (gated on the matcher capacities, as k_freq_record) and the rest publish.
+__global__ __launch_bounds__(256) void k_publish_record(const int64_t* __restrict__ cnt, const uint8_t* __restrict__ out,
+                                                        int64_t E, int K1, int64_t* __restrict__ cnt_host,
+                                                        uint8_t* __restrict__ res_host,
+                                                        const int64_t* __restrict__ counts, int K, double now,
+                                                        FreqRing R, RecordGate G, int rec_blocks) {
+  if ((int)blockIdx.x < rec_blocks) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    if (G.cnt && (G.cnt[0] > G.cap[0] || G.cnt[1] > G.cap[1] || G.cnt[2] > G.cap[2] || G.cnt[4] > G.cap[3])) return;
+    const int64_t c = counts[k];
+    if (c <= 0) return;
+    const int64_t p = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(R.ht + 1), 1ull);
+    const int64_t s = p % R.cap;
+    R.t[s] = now;
+    R.key[s] = k;
+    R.cnt[s] = (int32_t)c;
+    R.tot[k] += c;
+    R.seen[k] = 1;
+    return;
+  }
+  const int64_t ne = cnt[4];
+  const int64_t gid = (int64_t)(blockIdx.x - rec_blocks) * blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)(gridDim.x - rec_blocks) * blockDim.x;
+  if (gid < 5) cnt_host[gid] = cnt[gid];
+  if (ne < 0 || ne > E) return;
+  const double* score = reinterpret_cast<const double*>(out);
+  const int64_t* counts_e = reinterpret_cast<const int64_t*>(out + 8 * E);
+  const int32_t* cols = reinterpret_cast<const int32_t*>(out + 8 * E + 8 * (int64_t)K1);
+  double* h_score = reinterpret_cast<double*>(res_host);
+  int64_t* h_counts = reinterpret_cast<int64_t*>(res_host + 8 * ne);
+  int32_t* h_cols = reinterpret_cast<int32_t*>(res_host + 8 * ne + 8 * (int64_t)K1);
+  const int64_t total = ne + K1 + 3 * ne;
+  for (int64_t i = gid; i < total; i += stride) {
+    if (i < ne) {
+      h_score[i] = score[i];
+    } else if (i < ne + K1) {
+      h_counts[i - ne] = counts_e[i - ne];
+    } else {
+      const int64_t j = i - ne - K1;
+      const int64_t c = j / ne, r = j - c * ne;
+      h_cols[j] = cols[c * E + r];
+    }
+  }
+}
+
+void publish_record_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host,
+                        uint8_t* res_host, const int64_t* counts, int K, double now, const FreqRing& R,
+                        const RecordGate& G, uint64_t stream) {
+  const int64_t total = 4 * E + K1;
+  const int pub = (int)std::max<int64_t>(1, std::min<int64_t>(64, (total + 255) / 256));
+  const int rec = K > 0 ? (K + 255) / 256 : 0;
+  hipLaunchKernelGGL(k_publish_record, dim3(rec + pub), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), cnt, out,
+                     E, K1, cnt_host, res_host, counts, K, now, R, G, rec);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in publish_record");
+}
+
 void publish_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host, uint8_t* res_host,
                  uint64_t stream) {
   const int64_t total = 4 * E + K1;

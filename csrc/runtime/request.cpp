@@ -297,19 +297,18 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     }
     if (fast) {
       int64_t* fc = run_events(ecap_small, n, cnt + 3);
-      if (S_.nkeys > 0) {
-        RecordGate G;
-        G.cnt = cnt;
-        G.cap[0] = cap_g; G.cap[1] = cap_c; G.cap[2] = cap_v; G.cap[3] = ecap_small;
-        freq_record(fc, S_.nkeys, now, ring, stream, true, G);
-      }
+      RecordGate G;
+      G.cnt = cnt;
+      G.cap[0] = cap_g; G.cap[1] = cap_c; G.cap[2] = cap_v; G.cap[3] = ecap_small;
+      if (S_.nkeys > 0 && !publish_) freq_record(fc, S_.nkeys, now, ring, stream, true, G);
       const size_t res = 20 * (size_t)ecap_small + 8 * (size_t)K1;
       if (res > res_cap_) {
         grow<true>(res_host_, res_cap_, res, kCoherentHost);
         res_host_dev_ = device_view(res_host_);
       }
-      if (publish_) {      // counters + compacted results written into host memory by a kernel
-        publish_dev(cnt, out, ecap_small, (int)K1, cnt_host_dev_, res_host_dev_, stream);
+      if (publish_) {      // frequency record + counters + compacted results in host memory: one kernel
+        publish_record_dev(cnt, out, ecap_small, (int)K1, cnt_host_dev_, res_host_dev_, fc, S_.nkeys, now, ring, G,
+                           stream);
       } else {
         check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
         res_bytes_ = res;

@@ -224,7 +224,9 @@ int64_t request_line_cap();
 // device-count-mode results -> pinned host memory (request_io.hip): the 5 matcher/event counters
 // and the results compacted to stride ne (cnt[4]) when ne <= E; both pointers device-visible
 // n16 16-byte words from device-visible pinned host memory (host_dev) into device memory
-void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream);
+// (evict: block 0 also runs the frequency window's eviction at `horizon`, as k_freq_evict)
+void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream, const FreqRing* evict = nullptr,
+               double horizon = 0.0);
 void publish_dev(const int64_t* cnt, const uint8_t* out, int64_t E, int K1, int64_t* cnt_host, uint8_t* res_host,
                  uint64_t stream);
 // publish_dev + the batch's gated frequency record (k_freq_record) in one launch

@@ -55,9 +55,30 @@ __global__ __launch_bounds__(256) void k_publish(const int64_t* __restrict__ cnt
 // lanes each keep up to 4 16-byte PCIe reads in flight. Replaces the SDMA copy, whose completion
 // the compute queue only sees ~9 us later (request trace: copy 32 us + 9.6 us gap before it and
 // 8.9 us after it).
-__global__ __launch_bounds__(256) void k_fetch(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// With `evict`, block 0 first drops the frequency window's records at or before `horizon` (the
+// request's k_freq_evict, freq_state.hip: it reads nothing the fetch writes) and the fetch runs on
+// the other blocks: one launch fewer per request.
+__global__ __launch_bounds__(256) void k_fetch(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n,
+                                               int evict, FreqRing R, double horizon) {
+  if (evict && blockIdx.x == 0) {
+    for (;;) {
+      const int64_t head = R.ht[0], tail = R.ht[1];
+      const int64_t i = head + threadIdx.x;
+      bool v = false;
+      if (i < tail) {
+        const int64_t s = i % R.cap;
+        v = R.t[s] <= horizon;
+        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(R.tot + R.key[s]),
+                         (unsigned long long)(-(int64_t)R.cnt[s]));
+      }
+      const int c = __syncthreads_count(v);   // a prefix of the window: timestamps are ordered
+      if (threadIdx.x == 0) R.ht[0] = head + c;
+      __syncthreads();
+      if (c < (int)blockDim.x) return;
+    }
+  }
+  const int64_t stride = (int64_t)(gridDim.x - evict) * blockDim.x;
+  int64_t i = (int64_t)(blockIdx.x - evict) * blockDim.x + threadIdx.x;
   for (; i + 3 * stride < n; i += 4 * stride) {
     const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
     dst[i] = a;
@@ -68,11 +89,13 @@ __global__ __launch_bounds__(256) void k_fetch(const uint4* __restrict__ src, ui
   for (; i < n; i += stride) dst[i] = src[i];
 }
 
-void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream) {
-  if (n16 <= 0) return;
+void fetch_dev(const void* host_dev, void* dst, int64_t n16, uint64_t stream, const FreqRing* evict, double horizon) {
+  if (n16 <= 0 && !evict) return;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n16 + 255) / 256));
-  hipLaunchKernelGGL(k_fetch, dim3(blocks), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     static_cast<const uint4*>(host_dev), static_cast<uint4*>(dst), n16);
+  const int ev = evict ? 1 : 0;
+  hipLaunchKernelGGL(k_fetch, dim3(blocks + ev), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint4*>(host_dev), static_cast<uint4*>(dst), n16, ev,
+                     evict ? *evict : FreqRing{}, horizon);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in fetch");
 }

@@ -69,6 +69,10 @@ RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
   cnt_host_dev_ = device_view(cnt_host_);
   publish_ = publish_enabled();
   fetch_ = fetch_enabled();
+  // the window eviction inside the k_fetch launch (one launch fewer): opt-in until its A/B is in
+  // (LP_RUNNER_EVICT_IN_FETCH=1; the one run so far showed an unexplained engine p99 of 1.97 ms)
+  const char* ev = std::getenv("LP_RUNNER_EVICT_IN_FETCH");
+  evict_in_fetch_ = ev && ev[0] == '1';
 }
 
 RequestRunner::~RequestRunner() {
@@ -151,8 +155,10 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   std::memcpy(segh + 2 * up256(4 * (size_t)D), seg_g0, 8 * (size_t)D);
   std::memcpy(segh + 2 * up256(4 * (size_t)D) + up256(8 * (size_t)D), seg_n, 8 * (size_t)D);
 
-  // window eviction first (FrequencyState.carry): the totals it leaves are this batch's carry
-  freq_evict(ring, evict_before, stream, true);
+  // window eviction first (FrequencyState.carry): the totals it leaves are this batch's carry --
+  // inside the k_fetch launch when the inputs go up that way, else its own kernel
+  const bool evict_in_fetch = text_dev_src != nullptr && evict_in_fetch_;
+  if (!evict_in_fetch) freq_evict(ring, evict_before, stream, true);
 
   RequestCounts c;
   c.lines = L;
@@ -250,8 +256,9 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, 4 * (size_t)std::max<int64_t>(L, 1) + 4096);
     }
     // inputs: packed text, line index, segments (all pinned -> async)
-    if (one_copy && text_dev_src) {
-      fetch_dev(text_dev_src, text, (int64_t)(up_total / 16), stream);
+    if (one_copy && text_dev_src) {   // (a re-run's eviction is a no-op: the window's head moved)
+      fetch_dev(text_dev_src, text, (int64_t)(up_total / 16), stream, attempt == 0 && evict_in_fetch ? &ring : nullptr,
+                evict_before);
     } else if (one_copy) {
       check(hipMemcpyAsync(text, host_text, up_total, hipMemcpyHostToDevice, st), "inputs H2D");
     } else {

@@ -90,6 +90,7 @@ class RequestRunner {
   uint8_t* res_host_dev_ = nullptr;    // device address of res_host_
   bool publish_ = true;                // device-count mode: results published by k_publish
   bool fetch_ = true;                  // single-copy inputs read by k_fetch from the pinned stage
+  bool evict_in_fetch_ = false;        // the window eviction runs inside the k_fetch launch (opt-in)
   uint8_t* fetch_host_ = nullptr;      // last stage buffer seen ...
   uint8_t* fetch_dev_ = nullptr;       // ... and its device address (null: not mapped, SDMA copy)
   int64_t fetch_cap_ = 0;

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd)
-OUT=${OUT:-gpurun_out/r2cc}
+OUT=${OUT:-gpurun_out/r2dd}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $OUT/pytest_gpu.log 2>&1 && echo PYTEST_OK || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 timeout -k 10 200 python tools/request_trace.py --requests 400 > $OUT/rt.json 2>/dev/null && echo RT_OK || exit 1

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Final-tree check: smoke, pytest -m gpu, default bench (what the driver runs).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=${OUT:-gpurun_out/last}
+mkdir -p $OUT
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo SMOKE_OK || exit 1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $OUT/pytest_gpu.log 2>&1 && echo PYTEST_OK || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && echo BENCH_OK || exit 1

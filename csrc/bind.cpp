@@ -55,6 +55,7 @@ static DfaPool dfa_from(const py::tuple& t) {
   D.bytemap = P<const uint8_t>(t[1].cast<uint64_t>());
   D.trans = P<const uint16_t>(t[2].cast<uint64_t>());
   D.acc = P<const uint8_t>(t[3].cast<uint64_t>());
+  D.bpg = t.size() > 4 ? P<const uint64_t>(t[4].cast<uint64_t>()) : nullptr;
   return D;
 }
 

@@ -42,6 +42,7 @@ struct DfaPool {
   const uint8_t* bytemap;   // [R][256]
   const uint16_t* trans;
   const uint8_t* acc;
+  const uint64_t* bpg = nullptr;   // bit-parallel Glushkov programs (meta flag bit1, offset in meta[0])
 };
 
 LP_HD int final_term_len(const uint8_t* s, int n) {
@@ -50,6 +51,11 @@ LP_HD int final_term_len(const uint8_t* s, int n) {
   if (n >= 3 && s[n - 3] == 0xE2 && s[n - 2] == 0x80 && (s[n - 1] == 0xA8 || s[n - 1] == 0xA9)) return 3;
   return 0;
 }
+}  // namespace lp
+
+#include "bpg.h"
+
+namespace lp {
 
 // One DFA of the pool: transition rows (nc classes per state), byte -> class map, accept flags
 // (bit0: accepting at end of line, bit1: accepting before a final line terminator). States 0
@@ -128,6 +134,7 @@ __device__ __forceinline__ uint32_t dfa_find_k(const DfaRef (&D)[K], const uint8
 
 // find() of regex r over one line (java.util.regex Matcher.find semantics, see jregex.h)
 LP_HD bool dfa_run(const DfaPool& P, int r, const uint8_t* s, int n) {
+  if (P.meta[4 * r + 3] & 2) return bpg_find(P.bpg + P.meta[4 * r], s, n);   // DFA blow-up: BPG program
 #if defined(__HIP_DEVICE_COMPILE__)
   const DfaRef D[1] = {dfa_ref(P, r)};
   return dfa_find_k<1>(D, s, n) != 0;

@@ -44,11 +44,6 @@ constexpr int G_CLS = 0, G_FIRST = 256, G_LAST = 271, G_REGMASK = 286, G_F = 294
 constexpr int NFA_WAVES = 4;
 constexpr int MAX_NFA_REGS = 8;   // regexes per group (models/nfa.py MAX_REGS)
 
-LP_HD int byte_kind(int c) {  // next-kind of a byte: 2 word, 3 other, 4 UTF-8 continuation
-  const bool w = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
-  return w ? 2 : (c >= 0x80 && c <= 0xBF) ? 4 : 3;
-}
-
 LP_HD uint32_t nfa_accept(const uint64_t* tab, uint64_t S, int ctx, int nreg) {
   const uint64_t hit = S & tab[G_LAST + ctx];
   uint32_t acc = 0;

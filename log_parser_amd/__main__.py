@@ -33,7 +33,8 @@ def cmd_validate(args, cfg: Config) -> int:
     from .models.library import load_pattern_directory
     d = args.directory or cfg["pattern.directory"]
     sets = load_pattern_directory(d)
-    lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]))
+    lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]),
+                                  nfa_engine=str(cfg["engine.nfa-engine"]))
     names = {KIND_DFA: "dfa", KIND_NFA: "nfa", KIND_FALLBACK: "host-fallback", KIND_INVALID: "invalid"}
     problems = []
     for r in lib.regexes:

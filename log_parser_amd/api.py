@@ -22,7 +22,8 @@ class LogParser:
         self.config = config or Config.load()
         dev = resolve_device(device or self.config["engine.device"])
         self.library = CompiledLibrary(pattern_sets, self.config.scoring,
-                                       max_dfa_states=int(self.config["engine.dfa-max-states"]))
+                                       max_dfa_states=int(self.config["engine.dfa-max-states"]),
+                                       nfa_engine=str(self.config["engine.nfa-engine"]))
         self.engine = Engine(self.library, self.config, device=dev, freq=freq)
 
     @classmethod

@@ -386,21 +386,32 @@ class Engine:
         few constructs the backtracker lacks (e.g. unicode properties) use the Python oracle."""
         lib = self.lib
         dev = text.device
+        keys: List[np.ndarray] = []
+        bt = lib.host_bt
+        py_regs = [r for r in lib.host_regs if lib.host_local[r] < 0]
+        need_all = bool([r for r in lib.host_scan_regs if lib.host_local[r] >= 0]) or \
+            any(not lib.regexes[r].literals for r in py_regs)
         hb = host_text
-        if hb is None:
+        gathered = None
+        if hb is None and not need_all and text.is_cuda:
+            # only candidate lines travel to the host: gather their bytes on the device (a DP shard
+            # of 1+ GB never crosses PCIe for a handful of backreference candidates)
+            gathered = self._gather_candidate_lines(text, ls, ll, fb_cand)
+            hb = gathered[0]
+        elif hb is None:
             hb = text[:nbytes].cpu().numpy()
         hb = np.ascontiguousarray(hb)
         if hb.size == 0:
             hb = np.zeros(1, np.uint8)
-        keys: List[np.ndarray] = []
-        bt = lib.host_bt
-        py_regs = [r for r in lib.host_regs if lib.host_local[r] < 0]
         lines_h = None                                # (starts, lens) of all lines, on demand
         if fb_cand is not None and fb_cand.numel():
-            x = (fb_cand & 0xFFFFFFFF).long()
-            pack = torch.stack([fb_cand, ls[x], ll[x].to(torch.int64)]).cpu().numpy()
-            _, first = np.unique(pack[0], return_index=True)    # one check per (regex, line)
-            kc, st, ln = (np.ascontiguousarray(pack[i][first]) for i in range(3))
+            if gathered is not None:
+                kc, st, ln = gathered[1:]
+            else:
+                x = (fb_cand & 0xFFFFFFFF).long()
+                pack = torch.stack([fb_cand, ls[x], ll[x].to(torch.int64)]).cpu().numpy()
+                _, first = np.unique(pack[0], return_index=True)    # one check per (regex, line)
+                kc, st, ln = (np.ascontiguousarray(pack[i][first]) for i in range(3))
             out = np.empty(kc.size, np.int64)
             nv = bt.verify(hb.ctypes.data, kc.ctypes.data, st.ctypes.data, ln.ctypes.data, kc.size,
                            lib.host_local.ctypes.data, lib.host_local.size, out.ctypes.data)
@@ -427,6 +438,28 @@ class Engine:
                         bt.exhausted)
         allk = np.concatenate(keys) if keys else np.zeros(0, np.int64)
         return torch.from_numpy(allk).to(dev)
+
+    @staticmethod
+    def _gather_candidate_lines(text, ls, ll, fb_cand):
+        """Unique (regex, line) candidates -> (compact host bytes of their lines, keys, starts in
+        the compact buffer, lengths): one gather on the device, one D2H of the candidate lines."""
+        if fb_cand is None or not fb_cand.numel():
+            return np.zeros(1, np.uint8), None, None, None
+        keys = torch.unique(fb_cand)
+        lines = keys & 0xFFFFFFFF
+        ul, inv = torch.unique(lines, return_inverse=True)
+        st = ls[ul]
+        ln = ll[ul].to(torch.int64)
+        off = torch.cumsum(ln, 0) - ln
+        total = int(ln.sum().item()) if ul.numel() else 0
+        if total:
+            rep = torch.repeat_interleave(torch.arange(ul.numel(), device=text.device), ln)
+            pos = st[rep] + (torch.arange(total, device=text.device) - off[rep])
+            buf = text[pos].cpu().numpy()
+        else:
+            buf = np.zeros(1, np.uint8)
+        kc = keys.cpu().numpy()
+        return buf, kc, np.ascontiguousarray(off[inv].cpu().numpy()), np.ascontiguousarray(ln[inv].cpu().numpy())
 
     def _python_fallback(self, hb: np.ndarray, kc, st, ln, regs: set) -> np.ndarray:
         out = []

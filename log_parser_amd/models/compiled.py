@@ -30,6 +30,7 @@ import torch
 from ..golden import CONTEXT_REGEXES, SEVERITY_MULTIPLIERS, java_blank, severity_key
 from ..native import N
 from ..utils.config import ScoringParams
+from .bpg import build_program
 from .nfa import build_group, fits_group, pack_groups
 from .schema import Pattern, PatternSet, pattern_to_json
 
@@ -176,10 +177,17 @@ class RegexInfo:
 
 
 class CompiledLibrary:
-    def __init__(self, pattern_sets: List[PatternSet], params: ScoringParams, max_dfa_states: int = 2048):
+    def __init__(self, pattern_sets: List[PatternSet], params: ScoringParams, max_dfa_states: int = 2048,
+                 nfa_engine: str = "bpg"):
         self.pattern_sets = pattern_sets
         self.params = params
         self.max_dfa_states = max_dfa_states
+        # regexes whose DFA exceeds max_dfa_states: "bpg" = bit-parallel Glushkov programs run by the
+        # DFA verify / scan kernels (models/bpg.py), "mfma" = the MFMA state-transition GEMM over
+        # every line (<= 64 positions; A/B engine)
+        if nfa_engine not in ("bpg", "mfma"):
+            raise ValueError(f"engine.nfa-engine must be 'bpg' or 'mfma', not {nfa_engine!r}")
+        self.nfa_engine = nfa_engine
         self.patterns: List[Pattern] = []
         self.pattern_set_index: List[int] = []
         for si, ps in enumerate(pattern_sets):
@@ -287,13 +295,18 @@ class CompiledLibrary:
     def _compile_regexes(self):
         meta, bytemaps, trans, accs = [], [], [], []
         toff = aoff = 0
+        bpgs: List[np.ndarray] = []
+        boff = 0
+        self.bpg_regs: List[int] = []
+        self.bpg_scan_regs: List[int] = []
         self.scan_regs: List[int] = []
         self.host_regs: List[int] = []
         self.host_bt_ok: List[bool] = []
         nfa_members: List[Tuple[int, dict]] = []
         ctx_members: List[Tuple[int, dict]] = []
         for i, ri in enumerate(self.regexes):
-            d = N.compile_regex(ri.pattern, self.max_dfa_states, 4096)
+            # the 4 context regexes are always DFAs: k_feat_cov walks their tables directly
+            d = N.compile_regex(ri.pattern, max(self.max_dfa_states, 2048) if i < 4 else self.max_dfa_states, 4096)
             ri.kind = d["kind"]
             ri.error = d["error"]
             if i < 4:
@@ -325,6 +338,23 @@ class CompiledLibrary:
                 if not lits:
                     self.scan_regs.append(i)
             else:
+                prog = build_program(d) if ri.kind == KIND_NFA and self.nfa_engine == "bpg" else None
+                if prog is not None:
+                    # DFA blow-up (bounded gaps X.{0,120}Y, repeated groups): a bit-parallel Glushkov
+                    # program, dispatched by the same verify / scan kernels as the DFAs (meta bit 1)
+                    ri.nstates = int(d["npos"])
+                    meta.append([boff, 1, 0, 2])
+                    bytemaps.append(np.zeros(256, np.uint8))
+                    bpgs.append(prog)
+                    boff += prog.size
+                    self.bpg_regs.append(i)
+                    lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
+                    if lits and min(len(x) for x in lits) < MIN_LITERAL:
+                        lits = []
+                    ri.literals = lits if ri.roles != {"context"} else []
+                    if not ri.literals:
+                        self.bpg_scan_regs.append(i)      # every line, one lane per line (k_scan)
+                    continue
                 meta.append([0, 1, 0, 0])
                 bytemaps.append(np.zeros(256, np.uint8))
                 if ri.kind == KIND_INVALID:
@@ -354,7 +384,9 @@ class CompiledLibrary:
         self.nfa_scan_groups = list(range(1, len(groups)))
         self.nfa_regs = [rid for g in groups[1:] for rid, _ in g]
         self._build_scan_passes()
+        self.scan_regs_single = self.scan_regs_single + self.bpg_scan_regs
         self._build_host_matchers()
+        self.bpg_pool = np.concatenate(bpgs) if bpgs else np.zeros(1, np.uint64)
         self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
         self.dfa_bytemap = np.concatenate(bytemaps)
         self.dfa_trans = np.concatenate(trans)
@@ -613,9 +645,10 @@ class CompiledLibrary:
         t["pf"] = (a[0].data_ptr(), pf["bits"], a[1].data_ptr(), a[2].data_ptr(), a[3].data_ptr(), pf["ht_mask"],
                    a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"],
                    pf["stride"], a[9].data_ptr(), a[10].data_ptr(), a[11].data_ptr(), 1 if pf["teddy_lits"] else 0)
-        t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc)]
+        t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc),
+                           T(self.bpg_pool.view(np.int64))]
         d = t["dfa_arrays"]
-        t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr())
+        t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr())
         t["scan_regs"] = T(np.array(self.scan_regs_single, np.int32))
         t["host_is"] = T(self.host_is)
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
@@ -665,6 +698,7 @@ class CompiledLibrary:
             "teddy_literals": int(self.pf["teddy_lits"]), "prefilter_stride": int(self.pf["stride"]),
             "scan_groups": len(self.scan_groups), "scan_passes": len(self.scan_passes),
             "nfa_mfma": len(self.nfa_regs), "nfa_groups": len(self.nfa_scan_groups),
+            "nfa_bpg": len(self.bpg_regs), "nfa_bpg_scan_all": len(self.bpg_scan_regs),
             "halo": self.halo,
         }
 

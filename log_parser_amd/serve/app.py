@@ -248,7 +248,8 @@ class Service:
             if self._engine is None:
                 cfg = self.config
                 sets = load_pattern_directory(cfg["pattern.directory"])
-                lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]))
+                lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]),
+                                  nfa_engine=str(cfg["engine.nfa-engine"]))
                 log.info("compiled library: %s", lib.summary())
                 self._engine = Engine(lib, cfg)
                 snap = cfg["engine.frequency.snapshot-path"]

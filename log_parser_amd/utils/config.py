@@ -44,8 +44,12 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.chunk-bytes": (256 << 20, int),
     # capacity hint for candidate (line, regex) pairs per chunk; grown on overflow
     "engine.candidate-capacity": (1 << 22, int),
-    # max DFA states per regex before it is routed to the NFA (MFMA) path
+    # max DFA states per regex before it is routed to the NFA engine
     "engine.dfa-max-states": (2048, int),
+    # NFA engine of regexes whose DFA blows up: "bpg" (bit-parallel Glushkov programs, literal
+    # prefilter candidates or every line) or "mfma" (state-transition GEMM, every line, <= 64
+    # positions; A/B engine)
+    "engine.nfa-engine": ("bpg", str),
     # context-feature engine: "mfma" (NFA state-transition GEMM on matrix cores) or "dfa"
     "engine.context-engine": ("dfa", str),
     # run the literal-free scan engines on a second HIP stream, overlapping the literal prefilter

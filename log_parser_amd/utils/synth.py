@@ -74,18 +74,40 @@ def _literal_free_shape(rng: random.Random, fam: int, a: int, b: int) -> Tuple[s
         f"\tat app.R{'x' * a}(Main.java:{'4' * b})"
 
 
+def _bounded_gap(rng: random.Random, tok: str, i: int) -> Tuple[str, str, str, str]:
+    """A bounded-gap regex (``X.{0,n}Y``: its DFA exceeds engine.dfa-max-states, so it runs as a
+    bit-parallel Glushkov program) + a matching sample, and a bounded-gap secondary + its sample."""
+    fam = i % 6
+    g = (60, 80, 100, 120)[(i // 6) % 4]
+    if fam == 0:
+        rx, sm = rf"{tok} refused.{{0,{g}}}port \d+", f"{tok} refused by upstream 10.0.0.7 on port 8443"
+    elif fam == 1:
+        rx, sm = rf"pod .{{1,{g}}} in namespace {tok} .{{1,40}} failed", f"pod web-7f9c in namespace {tok} sync failed"
+    elif fam == 2:
+        rx, sm = rf"(?i)error.{{0,{g}}}{tok}.{{0,{g}}}retry", f"ERROR while calling {tok}, will retry in 5s"
+    elif fam == 3:
+        rx, sm = rf"(\w+\.){{2,}}{tok}Exception.{{0,{g}}}Caused by", f"com.acme.{tok}Exception: boom Caused by io"
+    elif fam == 4:
+        rx, sm = rf"{tok}.{{0,{g}}}(?:timed out|deadline exceeded)", f"{tok} call to db-0 deadline exceeded"
+    else:
+        rx, sm = rf"\b\d{{1,3}}(?:\.\d{{1,3}}){{3}}\b.{{0,{g}}}{tok} (?:refused|reset)", f"peer 10.1.2.3 said {tok} reset"
+    srx, ssm = rf"{tok}Gap.{{0,{g // 2}}}code=\d+", f"{tok}Gap probe returned code=503"
+    return rx, sm, srx, ssm
+
+
 def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate: float = 0.7,
                  sequence_rate: float = 0.4, feature_mix: bool = True, short_literal_rate: float = 0.0,
-                 literal_free_rate: float = 0.0) -> Tuple[List[PatternSet], List[dict]]:
+                 literal_free_rate: float = 0.0, gap_rate: float = 0.0) -> Tuple[List[PatternSet], List[dict]]:
     """Returns (pattern sets, trigger descriptions used by ``make_log`` to plant matches).
 
-    ``short_literal_rate`` / ``literal_free_rate``: shares of primaries whose only literal is a
-    3-6-byte code, or that have no usable literal at all (``realistic_library``)."""
+    ``short_literal_rate`` / ``literal_free_rate`` / ``gap_rate``: shares of primaries whose only
+    literal is a 3-6-byte code, that have no usable literal at all, or that are bounded-gap regexes
+    whose DFA blows up (``realistic_library``)."""
     rng = random.Random(seed)
     sets = [{"metadata": {"library_id": f"synthetic-lib-{s}", "version": "1.0"}, "patterns": []}
             for s in range(n_sets)]
     triggers = []
-    n_free = 0
+    n_free = n_gap = 0
     for i in range(n_patterns):
         tok = _token(rng, i)
         style = rng.randrange(8) if feature_mix else 0
@@ -94,7 +116,14 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
             style = 8
         elif u < literal_free_rate + short_literal_rate:
             style = 9
-        if style == 8:
+        elif u < literal_free_rate + short_literal_rate + gap_rate:
+            style = 10
+        gap_sec = None
+        if style == 10:
+            regex, sample, srx, ssm = _bounded_gap(rng, tok, n_gap)
+            gap_sec = (srx, ssm)
+            n_gap += 1
+        elif style == 8:
             regex, sample = _literal_free(rng, n_free)
             n_free += 1
         elif style == 9:
@@ -129,12 +158,16 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
             "primary_pattern": {"regex": regex, "confidence": round(rng.uniform(0.3, 0.95), 3)},
             "remediation": {"description": f"fix {tok}", "common_causes": ["synthetic"]},
         }
-        secs, seqs = [], []
-        if rng.random() < secondary_rate:
+        secs, seqs, sec_samples = [], [], []
+        if rng.random() < secondary_rate or gap_sec:
             for k in range(rng.randint(1, 3)):
                 stok = f"{tok}Aux{k}"
                 secs.append({"regex": stok if k else rf"(?i){stok}\b", "weight": round(rng.uniform(0.1, 0.9), 2),
                              "proximity_window": rng.choice([3, 5, 10, 20, 50, 200])})
+                sec_samples.append(stok)
+            if gap_sec:
+                secs.append({"regex": gap_sec[0], "weight": 0.4, "proximity_window": 20})
+                sec_samples.append(gap_sec[1])
             pat["secondary_patterns"] = secs
         if rng.random() < sequence_rate:
             evs = [{"regex": f"{tok}Step{k}"} for k in range(rng.randint(1, 3))]
@@ -145,18 +178,19 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
             pat["context_extraction"] = {"lines_before": rng.randint(0, 8), "lines_after": rng.randint(0, 6),
                                          "include_stack_trace": rng.random() < 0.5}
         sets[i % n_sets]["patterns"].append(pat)
-        triggers.append({"sample": sample, "secondary": [s["regex"].replace("(?i)", "").replace("\\b", "")
-                                                         for s in secs],
+        triggers.append({"sample": sample, "secondary": sec_samples,
                          "sequence": [e["regex"] for q in seqs for e in q["events"]]})
     return [PatternSet.model_validate(s) for s in sets], triggers
 
 
 def realistic_library(n_patterns: int, seed: int = 0, **kw):
     """The headline bench library: the synthetic mix plus ~10% primaries with only a 3-6-byte
-    literal and ~5% literal-free primaries, the shapes real libraries have (short error codes,
-    IP:port, `^\\s+at ...` stack frames) and the prefilter's worst case."""
+    literal, ~5% literal-free primaries and ~1.5% bounded-gap primaries (``X.{0,120}Y``, each
+    with a bounded-gap secondary) -- the shapes real libraries have (short error codes, IP:port,
+    `^\\s+at ...` stack frames, "refused ... port N") and the matcher's worst cases."""
     kw.setdefault("short_literal_rate", 0.10)
     kw.setdefault("literal_free_rate", 0.05)
+    kw.setdefault("gap_rate", 0.015)
     return make_library(n_patterns, seed=seed, **kw)
 
 

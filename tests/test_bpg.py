@@ -1,0 +1,152 @@
+"""Bit-parallel Glushkov programs (models/bpg.py, csrc/kernels/bpg.h) for regexes whose DFA blows
+up -- bounded gaps ``X.{0,120}Y``, repeated groups, boundary-gated edges. The reference runs
+``Pattern.compile(rx).matcher(line).find()`` for every regex role (AnalysisService.java:62-65,93-95;
+secondaries ScoringService.java:315-347), so these must give exactly Java's boolean find():
+checked against the javacompat oracle (pure Python twin, native host twin, gfx950 kernel) and end
+to end against the golden model."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from log_parser_amd import golden
+from log_parser_amd.engine import Engine
+from log_parser_amd.models.bpg import build_program, decompose, program_info, run_program
+from log_parser_amd.models.compiled import CompiledLibrary
+from log_parser_amd.native import N
+from log_parser_amd.ops import kernels as K
+from log_parser_amd.regex.javacompat import compile_java
+from log_parser_amd.utils.config import Config, ScoringParams
+from log_parser_amd.utils.synth import make_library, make_log
+
+GAP_PATS = [
+    r"Connection refused.{0,120}port \d+", r"pod .{1,60} in namespace .{1,60} failed",
+    r"error.{0,100}timeout.{0,100}retry", r"(\w+\.){2,}\w+Exception.{0,200}Caused by",
+    r"(?i)\bfoo\b.{0,40}bar", r"x.{0,3}y", r"^\s*at .{0,50}\(", r"(?i)(?:fail|error|fatal).{0,30}(?:disk|volume|mount)\b",
+    r"\b\d{1,3}(?:\.\d{1,3}){3}\b.{0,80}(?:refused|reset|timed out)", r"(a|bc)+d.{0,20}e", r"a.{2,5}b$",
+    r"(?i)é.{0,9}z\B", r"(?:ab|cd){2,4}.{0,30}x+y?z",
+]
+POS = ["Connection refused by 10.0.0.1 on port 80", "pod a in namespace b c failed", "error: x timeout y retry",
+       "at com.acme.FooException: bad Caused by", "FOO, then bar", "x12y", "  at x(", "Fatal: no disk",
+       "10.0.0.1 said hi refused", "abcbcd123e", "aééb", "ÉabcZz", "abcd...xxz"]
+ALPHA = "abcdefxyz .:()é\tÉ" + "Connection refused port 123 pod in namespace failed error timeout retry " \
+        "java.lang.FooException Caused by foo bar FOO at 10.0.0.1 disk volume\r"
+
+
+def _lines(rng, n):
+    toks = ALPHA.split(" ")
+    out = list(POS)
+    for _ in range(n):
+        if rng.random() < 0.5:
+            out.append(" ".join(rng.choice(toks) for _ in range(rng.randint(0, 25))))
+        else:
+            out.append("".join(rng.choice(ALPHA) for _ in range(rng.randint(0, 90))))
+    return out
+
+
+def test_decomposition_is_exact_and_compact():
+    for p in GAP_PATS:
+        d = N.compile_regex(p, 64, 4096)
+        assert d["kind"] in (0, 1)
+        decompose(d["npos"], d["nfa_follow"])           # asserts the parts rebuild every follow set
+        info = program_info(build_program(d))
+        assert info["exceptions"] <= 4, (p, info)
+    # the verdict's bounded-gap shapes all blow up the DFA and need no exception edges
+    for p in GAP_PATS[:3]:
+        d = N.compile_regex(p, 2048, 4096)
+        assert d["kind"] == 1 and program_info(build_program(d))["exceptions"] == 0
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_python_twin_matches_java_oracle(seed):
+    rng = random.Random(seed)
+    lines = _lines(rng, 400)
+    for p in GAP_PATS:
+        prog = build_program(N.compile_regex(p, 64, 4096))
+        rx = compile_java(p)
+        for s in lines:
+            assert run_program(prog, s.encode()) == (rx.search(s) is not None), (p, s)
+
+
+def _lib(pats):
+    from log_parser_amd.models.schema import PatternSet
+    ps = PatternSet.model_validate({"metadata": {"library_id": "gap"}, "patterns": [
+        {"id": f"g{i}", "name": p, "severity": "HIGH", "primary_pattern": {"regex": p, "confidence": 0.5}}
+        for i, p in enumerate(pats)]})
+    return CompiledLibrary([ps], ScoringParams(), max_dfa_states=64)
+
+
+def _scan(lib, lines, dev):
+    blob = "\n".join(lines).encode()
+    t = torch.zeros(K.padded_len(len(blob)), dtype=torch.uint8)
+    t[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    starts, lens, pos = [], [], 0
+    for s in lines:
+        starts.append(pos)
+        lens.append(len(s.encode()))
+        pos += lens[-1] + 1
+    ls = torch.tensor(starts, dtype=torch.int64, device=dev)
+    ll = torch.tensor(lens, dtype=torch.int32, device=dev)
+    tabs = lib.device_tables(dev)
+    regs = torch.tensor(lib.bpg_regs, dtype=torch.int32, device=dev)
+    return set(K.scan(t.to(dev), ls, ll, regs, tabs["dfa"], 1 << 16).cpu().tolist())
+
+
+def test_native_host_twin_matches_oracle():
+    lib = _lib(GAP_PATS)
+    assert len(lib.bpg_regs) >= len(GAP_PATS) - 2   # max_dfa_states=64: nearly all are BPG programs
+    lines = _lines(random.Random(5), 600)
+    got = _scan(lib, lines, torch.device("cpu"))
+    want = {(r << 32) | j for r in lib.bpg_regs for j, s in enumerate(lines)
+            if compile_java(lib.regexes[r].pattern).search(s) is not None}
+    assert got == want and len(want) > 50
+
+
+def _gap_library(seed):
+    sets, trig = make_library(48, seed=seed, gap_rate=0.5)
+    return sets, trig
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_engine_with_bounded_gap_regexes_matches_golden(seed):
+    """Bounded-gap primaries (literal-narrowed to prefilter candidates) and bounded-gap
+    secondaries give the golden model's events and scores (rtol 1e-12); nothing runs on the host
+    backtracker and the native request runner stays eligible."""
+    p = ScoringParams()
+    sets, trig = _gap_library(seed)
+    lib = CompiledLibrary(sets, p)
+    s = lib.summary()
+    assert s["nfa_bpg"] >= 10 and s["host_fallback"] == 0 and s["nfa_mfma"] == 0
+    logs = make_log(4000, trig, seed=seed + 1, hit_rate=0.08, crlf_rate=0.05)
+    eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    r = eng.analyze(logs)
+    g = golden.analyze(logs, sets, p, golden.FrequencyTracker(p))
+    assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r["events"]] == \
+        [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+    gap_ids = {pt.id for ps in sets for pt in ps.patterns if "{" in pt.primary_pattern.regex}
+    assert sum(e["matchedPattern"]["id"] in gap_ids for e in r["events"]) > 20
+    np.testing.assert_allclose([e["score"] for e in r["events"]], [e["score"] for e in g["events"]], rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_bpg_kernel_matches_host(gpu_device):
+    lib = _lib(GAP_PATS)
+    lines = _lines(random.Random(6), 5000)
+    assert _scan(lib, lines, gpu_device) == _scan(lib, lines, torch.device("cpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11])
+def test_engine_bounded_gap_gpu_matches_golden(gpu_device, seed):
+    p = ScoringParams()
+    sets, trig = _gap_library(seed)
+    lib = CompiledLibrary(sets, p)
+    logs = make_log(4000, trig, seed=seed + 1, hit_rate=0.08)
+    eng = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    r = eng.analyze(logs)
+    assert eng._runner not in (None, False)            # the native request runner served it
+    g = golden.analyze(logs, sets, p, golden.FrequencyTracker(p))
+    assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r["events"]] == \
+        [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+    np.testing.assert_allclose([e["score"] for e in r["events"]], [e["score"] for e in g["events"]], rtol=1e-12)

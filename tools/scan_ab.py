@@ -1,8 +1,9 @@
-"""A/B of the two whole-text engines for literal-free regexes: multi-regex DFA scan groups
-(csrc/kernels/scan_multi.hip) vs the MFMA NFA state-transition kernel (csrc/kernels/nfa_mfma.hip),
-on N literal-free regexes over every line of a synthetic log.
+"""A/B of the whole-text engines for literal-free regexes: multi-regex DFA scan groups
+(csrc/kernels/scan_multi.hip), the MFMA NFA state-transition kernel (csrc/kernels/nfa_mfma.hip)
+and bit-parallel Glushkov programs (csrc/kernels/bpg.h, one lane per line) on N literal-free
+regexes over every line of a synthetic log.
 
-    python tools/scan_ab.py --regexes 64 --lines 2500000 [--engine dfa|mfma|both] [--reps 10]
+    python tools/scan_ab.py --regexes 64 --lines 2500000 [--engine dfa|mfma|bpg|both|all] [--reps 10]
 
 Prints one JSON line: per-engine kernel time (median of --reps, HIP events), hits (both engines
 must agree), groups. Used for the crossover table in docs/PERFORMANCE.md and under rocprofv3 PMC.
@@ -60,7 +61,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--regexes", type=int, default=64)
     ap.add_argument("--lines", type=int, default=2_500_000)
-    ap.add_argument("--engine", default="both", choices=["dfa", "mfma", "both"])
+    ap.add_argument("--engine", default="both", choices=["dfa", "mfma", "bpg", "both", "all"])
     ap.add_argument("--reps", type=int, default=10)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -78,7 +79,7 @@ def main():
     tabs = lib.device_tables(dev)
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     hits = {}
-    if args.engine in ("dfa", "both"):
+    if args.engine in ("dfa", "both", "all"):
         def run_dfa():
             outs = []
             for sp in tabs["scan_passes"]:
@@ -92,7 +93,7 @@ def main():
         rec["dfa_passes"] = len(lib.scan_passes)
         rec["dfa_states"] = [d["nstates"] for _, d in lib.scan_groups]
         rec["dfa_single"] = len(lib.scan_regs_single)
-    if args.engine in ("mfma", "both"):
+    if args.engine in ("mfma", "both", "all"):
         members = []
         for r in lib.scan_regs:
             d = N.compile_regex(lib.regexes[r].pattern, 4, 4096)
@@ -113,10 +114,22 @@ def main():
         rec["mfma_us"] = round(us, 1)
         rec["mfma_groups"] = len(groups)
         rec["mfma_regexes"] = len(members)
+    if args.engine in ("bpg", "all"):
+        blib = CompiledLibrary(sets, ScoringParams(), max_dfa_states=4)      # every regex -> BPG program
+        btabs = blib.device_tables(dev)
+        regs = torch.tensor(blib.bpg_regs, dtype=torch.int32, device=dev)
+
+        def run_bpg():
+            return K.scan(t, ls, ll, regs, btabs["dfa"], max(1024, L >> 4))
+        us, h = timed(run_bpg, args.reps)
+        hits["bpg"] = torch.sort(h).values.cpu()
+        rec["bpg_us"] = round(us, 1)
+        rec["bpg_regexes"] = len(blib.bpg_regs)
     for k, v in hits.items():
         rec[f"{k}_hits"] = int(v.numel())
-    if len(hits) == 2 and rec.get("mfma_regexes") == len(lib.scan_regs):
-        rec["agree"] = bool(torch.equal(hits["dfa"], hits["mfma"]))
+    if len(hits) >= 2 and "dfa" in hits:
+        rec["agree"] = {k: bool(torch.equal(hits["dfa"], v)) for k, v in hits.items() if k != "dfa"
+                        and (k != "mfma" or rec.get("mfma_regexes") == len(lib.scan_regs))}
     print(json.dumps(rec), flush=True)
 
 

@@ -56,6 +56,7 @@ static DfaPool dfa_from(const py::tuple& t) {
   D.trans = P<const uint16_t>(t[2].cast<uint64_t>());
   D.acc = P<const uint8_t>(t[3].cast<uint64_t>());
   D.bpg = t.size() > 4 ? P<const uint64_t>(t[4].cast<uint64_t>()) : nullptr;
+  D.bpg_widths = t.size() > 5 ? t[5].cast<uint32_t>() : 0u;
   return D;
 }
 
@@ -616,14 +617,14 @@ PYBIND11_MODULE(_lpnative, m) {
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
-                     double evict_before, double now, uint64_t stream, int64_t host_cap) {
+                     double evict_before, double now, uint64_t stream, int64_t host_cap, WindowTurn* turn, int64_t seq) {
         const FreqRing R = ring_from(ring);
         const int D = (int)lo.shape(0);
         int64_t ne;
         {
           py::gil_scoped_release nogil;
           ne = r.run(P<uint8_t>(text), nbytes, P<const int64_t>(starts), P<const int32_t>(lens), L, lo.data(), hi.data(),
-                     g0.data(), n.data(), D, R, evict_before, now, stream, host_cap);
+                     g0.data(), n.data(), D, R, evict_before, now, stream, host_cap, turn, seq);
         }
         py::array_t<uint8_t> out((py::ssize_t)r.result_bytes());
         std::memcpy(out.mutable_data(), r.result(), r.result_bytes());
@@ -634,8 +635,29 @@ PYBIND11_MODULE(_lpnative, m) {
         return py::make_tuple(ne, out, d, r.stride());
       }, py::arg("text"), py::arg("nbytes"), py::arg("starts"), py::arg("lens"), py::arg("L"), py::arg("lo"),
          py::arg("hi"), py::arg("g0"), py::arg("n"), py::arg("ring"), py::arg("evict_before"), py::arg("now"),
-         py::arg("stream"), py::arg("host_cap") = 0)
+         py::arg("stream"), py::arg("host_cap") = 0, py::arg("turn") = nullptr, py::arg("seq") = 0)
+      .def_property_readonly("recorded", &RequestRunner::recorded)
       .def("upload_bytes", &RequestRunner::upload_bytes);
+
+  // arrival-order gate of a window shared by several runners (csrc/runtime/request.h)
+  py::class_<WindowTurn>(m, "WindowTurn")
+      .def(py::init<>())
+      .def("wait", [](WindowTurn& t, int64_t seq) { py::gil_scoped_release nogil; t.wait(seq); })
+      .def("done", &WindowTurn::done)
+      .def_property_readonly("next", &WindowTurn::next);
+  // peer access for kernels on `device` reading / writing memory of `peer` (a shared window)
+  m.def("enable_peer_access", [](int device, int peer) {
+    if (device == peer) return true;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess || !can) return false;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    (void)hipSetDevice(cur);
+    if (e == hipErrorPeerAccessAlreadyEnabled) { (void)hipGetLastError(); return true; }
+    return e == hipSuccess;
+  });
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
   py::class_<RawLogs>(m, "RawLogs")

@@ -121,21 +121,142 @@ LP_HD bool bpg_find_w(const uint64_t* __restrict__ P, const uint8_t* __restrict_
   }
 }
 
-// find() of one BPG program over s[0, n), word count rounded up to an instantiated width (unused
-// words carry zero masks). The device version is a real call: the walk is long and the per-W bodies
-// are large, so inlining them into every DFA-verify kernel would bloat all of those kernels.
-#if defined(__HIP_DEVICE_COMPILE__)
-static __device__ __attribute__((noinline)) bool bpg_find(const uint64_t* P, const uint8_t* s, int n)
-#else
-static inline bool bpg_find(const uint64_t* P, const uint8_t* s, int n)
+#if defined(__HIP__)
+// Device walk of one program (kernels in bpg.hip, one instantiation per width W so each kernel's
+// registers are sized for its own W): the line's bytes come from 16-byte ALIGNED vector loads one
+// block ahead (a byte load per step would put a memory round trip on the dependency chain), the
+// structural masks live in registers, class / first / last / exception rows are read through P --
+// a global pointer for candidate verification, an LDS copy for the all-lines scan.
+template <int W>
+__device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, const uint8_t* __restrict__ s, int n) {
+  const uint64_t hdr = P[0];
+  const int E = (int)((hdr >> 8) & 0xFFF);
+  const int ncls = (int)((hdr >> 20) & 0x3FF);
+  const bool uniform = (hdr & BPG_UNIFORM) != 0;
+  const bool anchored = (hdr & BPG_ANCHORED) != 0;
+  const uint32_t nullm = (uint32_t)(hdr >> 32) & 0x7FFFu;
+  const uint64_t* q = P + 1;
+  uint64_t shm[W], selfm[W], src[W], R[W], lo[W], hi[W], f0[W], l0[W], S[W];
+  const uint64_t* first = q + 6 * W;
+  const uint64_t* last = first + 15 * W;
+  const uint8_t* bm = reinterpret_cast<const uint8_t*>(last + 15 * W);
+  const uint64_t* cls = last + 15 * W + 32;
+  const uint64_t* exc = cls + (size_t)ncls * W;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    shm[w] = q[w];
+    selfm[w] = q[W + w];
+    src[w] = q[2 * W + w];
+    R[w] = q[3 * W + w];
+    lo[w] = q[4 * W + w];
+    hi[w] = q[5 * W + w];
+    f0[w] = first[w];
+    l0[w] = last[w];
+    S[w] = 0;
+  }
+  const int ftl = final_term_len(s, n);
+  const int ft = ftl ? n - ftl : -1;
+  int prevk = 0;  // P_BOS
+// accept in boundary context ACTX (a macro, not a lambda: a lambda capturing S by reference kept
+// the state array in scratch memory)
+#define LP_BPG_ACCEPT(ACTX, RES)                                                 \
+  do {                                                                           \
+    const int a_ = (ACTX);                                                       \
+    uint64_t any_ = 0;                                                           \
+    if (uniform) {                                                               \
+      _Pragma("unroll") for (int w = 0; w < W; ++w) any_ |= S[w] & l0[w];        \
+    } else {                                                                     \
+      const uint64_t* L_ = last + a_ * W;                                        \
+      _Pragma("unroll") for (int w = 0; w < W; ++w) any_ |= S[w] & L_[w];        \
+    }                                                                            \
+    RES = ((nullm >> a_) & 1u) || any_ != 0;                                     \
+  } while (0)
+  bool hit = false;
+  if (n > 0) {
+    const int sh = (int)((uintptr_t)s & 15);
+    const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
+    uint4 cur = blk[0];
+    for (int t0 = -sh; t0 < n; t0 += 16) {
+      const uint4 nxt = blk[1];   // (text is padded: the look-ahead stays in bounds)
+      ++blk;
+      const int j0 = t0 < 0 ? -t0 : 0;
+      const int j1 = n - t0 < 16 ? n - t0 : 16;
+      for (int j = j0; j < j1; ++j) {
+        const int t = t0 + j;
+        const uint32_t wv = (j < 4) ? cur.x : (j < 8) ? cur.y : (j < 12) ? cur.z : cur.w;
+        const int c = (int)((wv >> (8 * (j & 3))) & 0xFFu);
+        const int nk = byte_kind(c);
+        if (t == ft) {
+          LP_BPG_ACCEPT(prevk * 5 + 1, hit);
+          if (hit) return true;
+        }
+        LP_BPG_ACCEPT(prevk * 5 + nk, hit);
+        if (hit) return true;
+        const int ctx = prevk * 5 + nk;
+        uint64_t F[W];
+        uint64_t carry = 0, borrow = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const uint64_t x = S[w] & shm[w];
+          F[w] = (x << 1) | carry | (S[w] & selfm[w]);
+          carry = x >> 63;
+          const uint64_t df = (S[w] & src[w]) | hi[w];
+          const uint64_t u = df - lo[w];
+          const uint64_t b1 = df < lo[w] ? 1ull : 0ull;
+          const uint64_t d = u - borrow;
+          const uint64_t b2 = u < borrow ? 1ull : 0ull;
+          borrow = b1 | b2;
+          F[w] |= R[w] & ~(d ^ df);
+        }
+        for (int e = 0; e < E; ++e) {
+          const uint64_t* x = exc + (size_t)e * (W + 1);
+          const uint64_t h = x[0];
+          const int p = (int)(h & 0xFFFF);
+          uint64_t sw = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) sw = (w == (p >> 6)) ? S[w] : sw;
+          if (((sw >> (p & 63)) & 1ull) && (((uint32_t)(h >> 16) >> ctx) & 1u)) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
+          }
+        }
+        const uint64_t* C = cls + (size_t)bm[c] * W;
+        uint64_t alive = 0;
+        if (uniform) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            S[w] = (F[w] | f0[w]) & C[w];
+            alive |= S[w];
+          }
+        } else {
+          const uint64_t* Fi = first + ctx * W;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            S[w] = (F[w] | Fi[w]) & C[w];
+            alive |= S[w];
+          }
+        }
+        if (anchored && !alive) return false;
+        prevk = nk == 2 ? 1 : 2;
+      }
+      cur = nxt;
+    }
+  }
+  LP_BPG_ACCEPT(prevk * 5 + 0, hit);  // end of line (N_EOS)
+  return hit;
+#undef LP_BPG_ACCEPT
+}
 #endif
-{
+
+// host twin: find() of one BPG program over s[0, n) (width from the header). On the device the
+// programs run in their own kernels (bpg.hip): dfa_run never walks them there.
+inline bool bpg_find_host(const uint64_t* P, const uint8_t* s, int n) {
   switch ((int)(P[0] & 0xFF)) {
     case 1: return bpg_find_w<1>(P, s, n);
     case 2: return bpg_find_w<2>(P, s, n);
     case 3: return bpg_find_w<3>(P, s, n);
     case 4: return bpg_find_w<4>(P, s, n);
-    case 5: case 6: return bpg_find_w<6>(P, s, n);
+    case 6: return bpg_find_w<6>(P, s, n);
     default: return bpg_find_w<8>(P, s, n);
   }
 }

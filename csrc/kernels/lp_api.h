@@ -16,6 +16,15 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn = nullptr,
                    int max_grid = 8192);
+// bit-parallel Glushkov programs (bpg.hip): candidate verify (small path, in place), first-of-run
+// verify of sorted keys (bulk path, flags), all-lines scan of literal-free programs
+void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text, const int64_t* ls,
+                  const int32_t* ll, const DfaPool& P, uint64_t stream);
+void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
+                    const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream);
+void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,
+                  int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
+                  uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
               const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
               uint64_t stream);

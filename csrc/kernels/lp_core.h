@@ -43,6 +43,7 @@ struct DfaPool {
   const uint16_t* trans;
   const uint8_t* acc;
   const uint64_t* bpg = nullptr;   // bit-parallel Glushkov programs (meta flag bit1, offset in meta[0])
+  uint32_t bpg_widths = 0;         // bit W set: some program has W words (which bpg.hip kernels to launch)
 };
 
 LP_HD int final_term_len(const uint8_t* s, int n) {
@@ -133,12 +134,16 @@ __device__ __forceinline__ uint32_t dfa_find_k(const DfaRef (&D)[K], const uint8
 #endif
 
 // find() of regex r over one line (java.util.regex Matcher.find semantics, see jregex.h)
+// regex r is a bit-parallel Glushkov program (DFA blow-up), not a DFA of the pool
+LP_HD bool is_bpg(const DfaPool& P, int r) { return (P.meta[4 * r + 3] & 2) != 0; }
+
 LP_HD bool dfa_run(const DfaPool& P, int r, const uint8_t* s, int n) {
-  if (P.meta[4 * r + 3] & 2) return bpg_find(P.bpg + P.meta[4 * r], s, n);   // DFA blow-up: BPG program
 #if defined(__HIP_DEVICE_COMPILE__)
+  if (is_bpg(P, r)) return false;      // verified by the bpg.hip kernels launched next to this one
   const DfaRef D[1] = {dfa_ref(P, r)};
   return dfa_find_k<1>(D, s, n) != 0;
 #else
+  if (is_bpg(P, r)) return bpg_find_host(P.bpg + P.meta[4 * r], s, n);
   const DfaRef D = dfa_ref(P, r);
   int ft = n - final_term_len(s, n);
   if (ft == n) ft = -1;

@@ -415,6 +415,7 @@ void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* lin
   hipLaunchKernelGGL(k_scan, dim3(num_blocks(nlines, 256)), dim3(256), 0, as_stream(stream), text, line_start,
                      line_len, nlines, regs, nregs, P, out, cap, count);
   LP_CHECK(hipGetLastError());
+  bpg_scan_dev(text, line_start, line_len, nlines, regs, nregs, P, out, cap, count, stream);   // DFA blow-ups
 }
 
 void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_seg, const FreqIn& F, int64_t n,

@@ -368,6 +368,7 @@ __global__ __launch_bounds__(256) void k_cand_verify(HitsArgs A) {
   int64_t* cand = const_cast<int64_t*>(A.cand);
   const int64_t k = cand[i];
   const int r = (int)(k >> 32);
+  if (is_bpg(A.dfa, r)) return;                // bit-parallel Glushkov program: k_bpg_cand
   const int64_t x = k & 0xFFFFFFFFll;
   if (!dfa_run(A.dfa, r, A.text + A.ls[x], A.ll[x])) cand[i] = -1;
 }
@@ -549,6 +550,7 @@ size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
   if (hits_small_ok(A)) {          // a request: verify on the grid, the rest in one workgroup
     hipLaunchKernelGGL(k_cand_verify, dim3(nblk(A.pre_from)), dim3(256), 0, pstream(stream), A);
+    bpg_cand_dev(const_cast<int64_t*>(A.cand), A.pre_from, A.dcount, A.text, A.ls, A.ll, A.dfa, stream);
     hipLaunchKernelGGL(k_hits_small, dim3(1), dim3(SB_THREADS), 0, pstream(stream), A);
     LP_PCHECK(hipGetLastError());
     return 0;
@@ -585,6 +587,7 @@ size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   hipLaunchKernelGGL(k_dedupe_verify, dim3(nblk(n)), dim3(256), 0, st, kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa,
                      stdk, flag);
   LP_PCHECK(hipGetLastError());
+  bpg_dedupe_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, flag, stream);
   tb = t_sel;
   LP_PCHECK(rocprim::select(tmp, tb, stdk, flag, A.hits, A.counters, (size_t)n, st));
   hipLaunchKernelGGL(k_csr_evcount, dim3(nblk(std::max<int64_t>(n, A.R + 1))), dim3(256), 0, st, A.hits, A.counters,

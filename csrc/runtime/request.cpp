@@ -100,7 +100,14 @@ int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
                            const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
                            int D, const FreqRing& ring, double evict_before, double now, uint64_t stream,
-                           int64_t host_cap) {
+                           int64_t host_cap, WindowTurn* turn, int64_t seq) {
+  // a shared window: released on every exit, also when a HIP call throws
+  struct Release {
+    WindowTurn* t;
+    int64_t s;
+    ~Release() { if (t) t->done(s); }
+  } release{turn, seq};
+  recorded_ = false;
   check(hipSetDevice(S_.device), "set device");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t tsize = padded_len(nbytes);
@@ -157,8 +164,16 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
 
   // window eviction first (FrequencyState.carry): the totals it leaves are this batch's carry --
   // inside the k_fetch launch when the inputs go up that way, else its own kernel
-  const bool evict_in_fetch = text_dev_src != nullptr && evict_in_fetch_;
-  if (!evict_in_fetch) freq_evict(ring, evict_before, stream, true);
+  const bool evict_in_fetch = turn == nullptr && text_dev_src != nullptr && evict_in_fetch_;
+  if (!evict_in_fetch && turn == nullptr) freq_evict(ring, evict_before, stream, true);
+  // shared window: wait for the earlier batches' records, then evict (this batch's carry)
+  bool in_window = turn == nullptr;
+  auto enter_window = [&]() {
+    if (in_window) return;
+    turn->wait(seq);
+    freq_evict(ring, evict_before, stream, true);
+    in_window = true;
+  };
 
   RequestCounts c;
   c.lines = L;
@@ -303,11 +318,13 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       hits_dev(A, post_ws_, post_cap_, stream);
     }
     if (fast) {
+      enter_window();
       int64_t* fc = run_events(ecap_small, n, cnt + 3);
       RecordGate G;
       G.cnt = cnt;
       G.cap[0] = cap_g; G.cap[1] = cap_c; G.cap[2] = cap_v; G.cap[3] = ecap_small;
       if (S_.nkeys > 0 && !publish_) freq_record(fc, S_.nkeys, now, ring, stream, true, G);
+      recorded_ = true;            // (gated on the device: an overflowing attempt records nothing)
       const size_t res = 20 * (size_t)ecap_small + 8 * (size_t)K1;
       if (res > res_cap_) {
         grow<true>(res_host_, res_cap_, res, kCoherentHost);
@@ -336,7 +353,9 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     learn(rate_gram_, c.gram);
     learn(rate_cand_, c.cand);
     learn(rate_ver_, c.ver);
+    if (fast) recorded_ = false;             // the gate held: nothing was recorded on this attempt
     if (ok && fast && ne <= ecap_small) {    // recorded through the gate; results already read
+      recorded_ = true;
       done = true;
       stride = publish_ ? ne : ecap_small;
       if (publish_) res_bytes_ = 20 * (size_t)ne + 8 * (size_t)K1;
@@ -371,9 +390,11 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     }
     ws_used_ = base;
     carve_events(ne);
+    enter_window();
     int64_t* fc = run_events(ne, nh, nullptr);
     // this batch's per-key counts enter the window (after its own scoring: penalty before record)
     if (S_.nkeys > 0) freq_record(fc, S_.nkeys, now, ring, stream, true);
+    recorded_ = true;
     if (res > res_cap_) {
       grow<true>(res_host_, res_cap_, res, kCoherentHost);
       res_host_dev_ = device_view(res_host_);

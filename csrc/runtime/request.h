@@ -16,11 +16,48 @@
 #pragma once
 #include <stdint.h>
 
+#include <condition_variable>
+#include <mutex>
+#include <set>
 #include <vector>
 
 #include "kernels/lp_api.h"
 
 namespace lp {
+
+// Arrival-order gate of ONE shared frequency window used by several runners (engines on several
+// GPUs, or several streams of one GPU): batch `seq` runs its window section -- eviction, score with
+// the in-window carry, record (ScoringService.java:84-88 penalty before record, in arrival order,
+// FrequencyTrackingService.java:25 one map for all workers) -- only after every earlier batch has
+// finished its own. Matching runs before the gate, concurrently. done() is idempotent and may
+// come out of order (a failed batch releases its slot).
+class WindowTurn {
+ public:
+  void wait(int64_t seq) {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [&] { return next_ >= seq; });
+  }
+  void done(int64_t seq) {
+    std::lock_guard<std::mutex> g(m_);
+    if (seq < next_) return;
+    done_.insert(seq);
+    while (!done_.empty() && *done_.begin() == next_) {
+      done_.erase(done_.begin());
+      ++next_;
+    }
+    cv_.notify_all();
+  }
+  int64_t next() {
+    std::lock_guard<std::mutex> g(m_);
+    return next_;
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int64_t next_ = 0;
+  std::set<int64_t> done_;
+};
 
 struct RequestStatic {
   PfTables pf;
@@ -62,9 +99,15 @@ class RequestRunner {
   // Returns the number of events ne; the results stay in result() until the next run:
   // [score f64 x E | freq counts i64 x max(nkeys, 1) | line i32 x E | pattern i32 x E | seg i32 x E]
   // with E = stride() >= ne (the event capacity of a device-count-mode request, else ne).
+  // turn / seq: a shared window (WindowTurn above): the eviction moves from the start of the run to
+  // the window section, entered through turn->wait(seq) once the matchers are queued and left
+  // (turn->done(seq)) when the batch's record has completed -- also on errors.
   int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
-              const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0);
+              const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0,
+              WindowTurn* turn = nullptr, int64_t seq = 0);
+  // the batch's frequency record was enqueued (a failure after it must not record the batch again)
+  bool recorded() const { return recorded_; }
   // host bytes the single-copy upload needs (text padded, index, segments, counters, carry)
   int64_t upload_bytes(int64_t nbytes, int64_t L, int D) const;
   const uint8_t* result() const { return res_host_; }
@@ -96,6 +139,7 @@ class RequestRunner {
   int64_t fetch_cap_ = 0;
   RequestCounts counts_;
   int64_t stride_ = 0;
+  bool recorded_ = false;
 };
 
 }  // namespace lp

@@ -25,6 +25,7 @@ SOURCES = [
     ("regex/jregex.cpp", "cpp"),
     ("kernels/lp_kernels.hip", "hip"),
     ("kernels/nfa_mfma.hip", "hip"),
+    ("kernels/bpg.hip", "hip"),
     ("kernels/scan_multi.hip", "hip"),
     ("kernels/freq_state.hip", "hip"),
     ("kernels/summarize.hip", "hip"),

@@ -191,6 +191,26 @@ class FrequencyTurn:
             self._cv.notify_all()
 
 
+class SharedWindowTurn:
+    """Arrival order for several engines sharing ONE device-resident frequency window (GPUs of
+    a node reading / recording it over xGMI peer access, or streams of one GPU): ``host`` orders the
+    ring's host bookkeeping (record timestamps, tail bound), ``dev`` (``N.WindowTurn``, also used
+    inside the native request runner with the GIL released) orders the window sections on the
+    device -- eviction, score with the carry, record. Matching runs before both, concurrently."""
+
+    def __init__(self):
+        self.host = FrequencyTurn()
+        self.dev = N.WindowTurn()
+
+    def wait(self, seq: int) -> None:
+        self.host.wait(seq)
+        self.dev.wait(seq)
+
+    def done(self, seq: int) -> None:
+        self.host.done(seq)
+        self.dev.done(seq)
+
+
 @dataclass
 class BatchJob:
     """One continuous batch between the pipeline stages (pack -> device -> emit)."""
@@ -205,6 +225,7 @@ class BatchJob:
     ev: Optional[tuple] = None          # (ev_line, ev_pat, ev_seg, score, freq counts) on the host
     timings: Optional[dict] = None
     outs: Optional[List[bytes]] = None  # responses computed by the device stage itself
+    recorded: bool = False              # its counts entered the frequency window (a fallback must not re-record)
 
 
 class Stage:
@@ -293,6 +314,7 @@ class Engine:
         self.context_engine = str(self.config["engine.context-engine"])
         self.log_matches = bool(self.config["server.log-matches"])
         self.fault_every = int(self.config["engine.fault-inject-every"])   # tests: injected device faults
+        self.fault_after_record = int(self.config.get("engine.fault-inject-after-record", 0))
         self._batches = 0
         self.tabs = library.device_tables(self.device)
         self.ws = K.Workspace(self.device)          # post-match pipeline scratch (grow-only)
@@ -655,22 +677,25 @@ class Engine:
             best = self.lib.severity[int(ev_pat_host[0])]
         return {"significantEvents": int(ev_pat_host.size), "highestSeverity": best, "severityDistribution": dist}
 
-    def analyze_bytes(self, data: bytes, with_factors: bool = False):
+    def analyze_bytes(self, data: bytes, with_factors: bool = False, record: bool = True):
         """One document end to end. Returns (RunResult, host line index arrays)."""
         text, n = self.stage_text(data)
         ls, ll = K.split_lines(text, n)
         segs = Segments.single(ls.numel(), self.device)
-        res = self.run(text, n, ls, ll, segs, self.freq_carry(), host_text=np.frombuffer(data, np.uint8) if n else None,
-                       with_factors=with_factors)
-        self.commit_frequency(res.freq_counts)
+        prep = self.prepare(text, n, ls, ll, segs, np.frombuffer(data, np.uint8) if n else None)
+        carry = self.freq_carry()
+        res = self.finish(prep, segs, carry if record else self._carry_before(BatchJob((), 0.0, recorded=True), prep,
+                                                                               carry), with_factors)
+        if record:
+            self.commit_frequency(res.freq_counts)
         return res, ls, ll
 
     # documents larger than this are line-indexed on the GPU (k_nl_count/k_nl_write); smaller
     # batches are split on the host while they are being packed (memchr, no extra pass)
     GPU_SPLIT_BYTES = 32 << 20
 
-    def analyze_batch_json(self, logs_list: Sequence[str], turn: Optional[FrequencyTurn] = None,
-                           seq: int = 0) -> List[bytes]:
+    def analyze_batch_json(self, logs_list: Sequence[str], turn=None, seq: int = 0,
+                           record: bool = True) -> List[bytes]:
         """Continuous-batching entry: many requests -> ONE device batch -> one JSON per request.
 
         Requests become segments of a single line batch (windows never cross a segment, each
@@ -683,6 +708,7 @@ class Engine:
         (serve/pipeline.py) runs the three stages of consecutive batches on different threads.
         """
         job = self.pack_batch(logs_list)
+        job.recorded = not record          # record=False: a fallback re-run of an already recorded batch
         try:
             self.device_batch(job, turn, seq)
             return self.emit_batch(job)
@@ -710,24 +736,33 @@ class Engine:
         job.staged = staged
         return job
 
-    def device_batch(self, job: "BatchJob", turn: Optional[FrequencyTurn] = None, seq: int = 0) -> None:
+    def device_batch(self, job: "BatchJob", turn=None, seq: int = 0) -> None:
         """Stage 2 (device): H2D, match + score kernels, one D2H, frequency commit (in batch order)."""
         if self.fault_every and job.number % self.fault_every == 0:
             raise RuntimeError("injected device fault (engine.fault-inject-every)")
+        self._device_batch(job, turn, seq)
+        if self.fault_after_record and job.number % self.fault_after_record == 0:
+            raise RuntimeError("injected device fault after the frequency record (engine.fault-inject-after-record)")
+
+    def _device_batch(self, job: "BatchJob", turn=None, seq: int = 0) -> None:
         if job.whole:
             if turn is not None:
                 turn.wait(seq)
             doc = job.logs[0]
-            job.outs = [self.analyze_json(doc.decode() if isinstance(doc, N.RawLogs) else doc)]
+            job.outs = [self.analyze_json(doc.decode() if isinstance(doc, N.RawLogs) else doc,
+                                          record=not job.recorded)]
+            job.recorded = True
             if turn is not None:
+                self._window_quiet()
                 turn.done(seq)
             return
         hb, ls_h, ll_h, dl, n = job.staged
         tm = job.tm
         verbose = self.log_matches or log.isEnabledFor(logging.DEBUG)
-        if turn is None and self._runner_ok(job, verbose, tm):
-            # the whole device half in one native call (csrc/runtime/request.cpp)
-            self._run_native(job, dl, n)
+        if (turn is None or isinstance(turn, SharedWindowTurn)) and self._runner_ok(job, verbose, tm):
+            # the whole device half in one native call (csrc/runtime/request.cpp); with a shared
+            # window its eviction / score / record run in arrival order inside the runner
+            self._run_native(job, dl, n, turn, seq)
             return
         if tm is not None:
             self._start(tm)
@@ -749,9 +784,10 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            res = self.run(text, n, ls, ll, segs, self.freq_carry(), host_text=hb[:n], with_factors=verbose,
-                           timings=tm)
-            self.commit_frequency(res.freq_counts)
+            res = self._run_job(job, text, n, ls, ll, segs, self.freq_carry(), hb[:n], verbose, tm)
+            if not job.recorded:
+                self.commit_frequency(res.freq_counts)
+                job.recorded = True
             with TR.HostTimer(tm, "d2h"):
                 job.ev = self._results_to_host(res)
         elif turn is None:
@@ -763,10 +799,12 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            res = self.run(text, n, ls, ll, segs, carry, host_text=hb[:n], with_factors=verbose, timings=tm)
+            res = self._run_job(job, text, n, ls, ll, segs, carry, hb[:n], verbose, tm)
             with TR.HostTimer(tm, "d2h"):
                 job.ev = self._results_to_host(res)
-            self.commit_frequency(job.ev[4])
+            if not job.recorded:
+                self.commit_frequency(job.ev[4])
+                job.recorded = True
         else:
             up = self.upload(idx + [lo, hi, g0, nn])
             if not pinned_idx:
@@ -777,21 +815,47 @@ class Engine:
                 self._tick(tm, "h2d", 0.0)
             prep = self.prepare(text, n, ls, ll, segs, host_text=hb[:n], timings=tm)
             turn.wait(seq)                     # earlier batches have recorded their counts
-            res = self.finish(prep, segs, self.freq_carry(), with_factors=verbose)
+            res = self.finish(prep, segs, self._carry_before(job, prep, self.freq_carry()), with_factors=verbose)
             with TR.HostTimer(tm, "d2h"):
                 job.ev = self._results_to_host(res)
-            self.commit_frequency(job.ev[4])
+            if not job.recorded:
+                self.commit_frequency(job.ev[4])
+                job.recorded = True
+            self._window_quiet()               # the record has landed before later batches evict
             turn.done(seq)
         if verbose:
             self._log_events(res, dl)
         if tm is not None:
             job.timings = res.timings
 
+    @staticmethod
+    def _carry_before(job: "BatchJob", prep: "Prepared", carry: torch.Tensor) -> torch.Tensor:
+        """The carry this batch must be scored with. A re-run of a batch whose counts already
+        entered the window (a failure after the record) takes them back out: the penalty is the
+        one before its own record (ScoringService.java:84-88)."""
+        if not job.recorded or not carry.numel():
+            return carry
+        k = min(carry.numel(), prep.freq_counts.numel())
+        c = carry.clone()
+        c[:k] = (c[:k] - prep.freq_counts[:k].to(c.device, c.dtype)).clamp(min=0)
+        return c
+
+    def _run_job(self, job: "BatchJob", text, n, ls, ll, segs, carry, host_text, verbose, tm) -> RunResult:
+        prep = self.prepare(text, n, ls, ll, segs, host_text, tm)
+        return self.finish(prep, segs, self._carry_before(job, prep, carry), with_factors=verbose)
+
+    def _window_quiet(self) -> None:
+        """Wait for the frequency window's queued kernels (a shared device window: the next batch
+        in arrival order may run on another stream or GPU)."""
+        if self.freq_on_device and self.freq.device.type == "cuda":
+            torch.cuda.current_stream(self.freq.device).synchronize()
+
     def _runner_ok(self, job: "BatchJob", verbose: bool, tm) -> bool:
-        """The native request runner covers the common device configuration: a GPU engine owning
-        its frequency window, DFA context features, no host-fallback or MFMA scan regexes, the
-        line index in the pinned stage, no tracing / per-match logging."""
-        if self._runner is False or tm is not None or verbose or job.n_lines < 0:
+        """The native request runner covers the common device configuration: a GPU engine with a
+        device-resident frequency window (its own, or one shared by several engines), DFA context
+        features, no host-fallback or MFMA scan regexes, the line index in the pinned stage, no
+        tracing / per-match logging, a batch not yet recorded."""
+        if self._runner is False or tm is not None or verbose or job.n_lines < 0 or job.recorded:
             return False
         if self._runner is None:
             ok = (self.device.type == "cuda" and self.freq_on_device and not self.lib.host_regs
@@ -814,27 +878,52 @@ class Engine:
                 bool(self.config.get("engine.runner-device-counts", True)))
         return True
 
-    def _run_native(self, job: "BatchJob", dl, n: int) -> None:
+    def _run_native(self, job: "BatchJob", dl, n: int, turn: Optional[SharedWindowTurn] = None, seq: int = 0) -> None:
         """Engine.device_batch through N.RequestRunner: same kernels and order as prepare / finish
         (H2D, eviction, matchers, ONE counter read, events + features + ranks, score, record,
-        ONE results read); the frequency state's host bookkeeping stays here, under its lock."""
+        ONE results read); the frequency state's host bookkeeping stays here, under its lock.
+
+        With a shared window (``turn``): the bookkeeping runs in arrival order (``turn.host``) and
+        only briefly; the runner queues its matchers, then enters the window section through
+        ``turn.dev`` -- engines on other GPUs / streams overlap everything but that section."""
         lo, hi, g0, nn = Segments.doc_arrays(dl)
         fr = self.freq
         K = len(self.lib.freq_ids)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         st = job.stage
-        with fr._lock:
-            if K:
-                fr._ensure_room(K)
-            evict_before = fr._now() - fr.window_s      # carry_tensor()
-            now = fr._now()                              # record_tensor()
-            # host_cap: the stage's room behind the text lets the runner send text, line index,
-            # segments and zeroed counters in ONE H2D copy (request.cpp, single-copy layout)
-            ne, out, counts, E = self._runner.run(st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(),
-                                               st.lens(job.n_lines).data_ptr(), job.n_lines, lo, hi, g0, nn,
-                                               fr._ring(), evict_before, now, stream, st.buf.numel())
-            if K:
-                fr._tail_bound += K
+        args = (st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(), st.lens(job.n_lines).data_ptr(), job.n_lines,
+                lo, hi, g0, nn)
+        if turn is None:
+            with fr._lock:
+                if K:
+                    fr._ensure_room(K)
+                evict_before = fr._now() - fr.window_s      # carry_tensor()
+                now = fr._now()                              # record_tensor()
+                # host_cap: the stage's room behind the text lets the runner send text, line index,
+                # segments and zeroed counters in ONE H2D copy (request.cpp, single-copy layout)
+                ne, out, counts, E = self._runner.run(*args, fr._ring(), evict_before, now, stream, st.buf.numel())
+                if K:
+                    fr._tail_bound += K
+        else:
+            turn.host.wait(seq)
+            try:
+                with fr._lock:
+                    if K:
+                        fr._ensure_room(K, quiesce=lambda: turn.dev.wait(seq))
+                    evict_before = fr._now() - fr.window_s
+                    now = fr._now()
+                    ring = fr._ring()
+                    if K:
+                        fr._tail_bound += K
+            finally:
+                turn.host.done(seq)
+            try:
+                ne, out, counts, E = self._runner.run(*args, ring, evict_before, now, stream, st.buf.numel(),
+                                                      turn=turn.dev, seq=seq)
+            except BaseException:
+                job.recorded = bool(self._runner.recorded)
+                raise
+        job.recorded = True
         self.arena.last = counts
         need = self._runner.upload_bytes(n, job.n_lines, len(lo))
         if need > st.buf.numel():
@@ -954,13 +1043,13 @@ class Engine:
             pu = self._patterns_used_json = json.dumps(self.lib.library_ids, separators=(",", ":"))
         return pu
 
-    def analyze_json(self, logs, library_ids: Optional[List] = None) -> bytes:
+    def analyze_json(self, logs, library_ids: Optional[List] = None, record: bool = True) -> bytes:
         """Full AnalysisResult as JSON bytes (camelCase result, snake_case matchedPattern)."""
         data = logs if isinstance(logs, (bytes, bytearray)) else logs.encode("utf-8", errors="surrogatepass")
         if len(data) < self.GPU_SPLIT_BYTES:
-            return self.analyze_batch_json([logs])[0]
+            return self.analyze_batch_json([logs], record=record)[0]
         t0 = time.time()
-        res, ls, ll = self.analyze_bytes(data)
+        res, ls, ll = self.analyze_bytes(data, record=record)
         ev_line = res.ev_line.cpu().numpy()
         ev_pat = res.ev_pat.cpu().numpy()
         score = res.score.cpu().numpy()

@@ -18,6 +18,7 @@ admin endpoints, optional snapshot/restore to a JSON file (off by default, like 
 from __future__ import annotations
 
 import json
+import logging
 import os
 import threading
 import time
@@ -25,6 +26,8 @@ from collections import deque
 from typing import Callable, Dict, Iterable, List, Optional
 
 import numpy as np
+
+log = logging.getLogger("log_parser_amd.frequency")
 
 
 class FrequencyState:
@@ -229,11 +232,15 @@ class DeviceFrequencyState:
         return (self.t.cpu().numpy()[idx], self.key.cpu().numpy()[idx].astype(np.int64),
                 self.cnt.cpu().numpy()[idx].astype(np.int64))
 
-    def _ensure_room(self, k: int) -> None:
+    def _ensure_room(self, k: int, quiesce: Optional[Callable[[], None]] = None) -> None:
         """Keep at least ``k`` free ring slots; reads head/tail back only when the host bound says
-        the ring may be full, and grows it (records kept in order) when it really is."""
+        the ring may be full, and grows it (records kept in order) when it really is.
+        ``quiesce``: with several engines sharing the window, waits until every earlier batch's
+        window section has completed, so head / tail are exact and no kernel uses the old ring."""
         if self._tail_bound + k - self._head_known <= self.cap:
             return
+        if quiesce is not None:
+            quiesce()
         h, tl = (int(x) for x in self.ht.cpu())
         self._head_known, self._tail_bound = h, tl
         if tl + k - h <= self.cap:
@@ -324,19 +331,40 @@ class DeviceFrequencyState:
     # ---- capture / rollback (elastic DP re-runs a step after a rank failure)
     def capture(self) -> dict:
         with self._lock:
+            # the whole ring is cloned: records appended after the capture may reuse slots that
+            # were live at capture time, and rollback must restore their timestamps and keys too
             return {"ht": self.ht.clone(), "tot": self.tot.clone(), "seen": self.seen.clone(),
-                    "t": self.t, "key": self.key, "cnt": self.cnt.clone()}
+                    "t": self.t.clone(), "key": self.key.clone(), "cnt": self.cnt.clone()}
 
     def rollback(self, state: dict) -> None:
         with self._lock:
-            if state["t"] is not self.t:                     # the ring grew meanwhile: keep the old one
-                self.t, self.key, self.cap = state["t"], state["key"], state["t"].numel()
+            self.t, self.key, self.cap = state["t"].clone(), state["key"].clone(), state["t"].numel()
             self.cnt = state["cnt"].clone()
             self.ht.copy_(state["ht"])
             self.tot.copy_(state["tot"])
             self.seen.copy_(state["seen"])
             h, tl = (int(x) for x in self.ht.cpu())
             self._head_known, self._tail_bound = h, tl
+
+    def to_host_state(self) -> "FrequencyState":
+        """A host ``FrequencyState`` holding the same in-window records (the CPU fallback's copy
+        of the window after a device fault); empty when the device cannot be read."""
+        fs = FrequencyState(self.window_hours, clock=self.clock)
+        try:
+            with self._lock:
+                t, key, cnt = self._records()
+                seen = self.seen.cpu().numpy()
+        except Exception:  # noqa: BLE001 - a failed device: start from an empty window
+            log.warning("device frequency window unreadable; the CPU fallback starts from an empty window")
+            return fs
+        for k in np.flatnonzero(seen[:len(self.ids)]):
+            fs._seen[fs._slot_of(self.ids[k])] = True
+        for a, k, c in zip(t.tolist(), key.tolist(), cnt.tolist()):
+            if c > 0:
+                s = fs._slot_of(self.ids[k])
+                fs._tot[s] += c
+                fs._q.append((float(a), np.array([s], np.int64), np.array([c], np.int64)))
+        return fs
 
     # ---- checkpoint / resume: the same JSON as FrequencyState
     def snapshot(self, path: str) -> None:
@@ -381,3 +409,24 @@ class DeviceFrequencyState:
                 self._last_now = max(self._last_now, ev[-1][0])
             self.ht.copy_(torch.tensor([0, n], dtype=torch.int64))
             self._head_known, self._tail_bound = 0, n
+
+
+class MirroredFrequencyState(FrequencyState):
+    """Host copy of a device-resident window for the CPU fallback after a device failure
+    (availability only): reads come from the copy; records go to the copy and, best
+    effort, to the device window, so a recovered GPU keeps counting the fallback's matches."""
+
+    def __init__(self, dev: DeviceFrequencyState):
+        host = dev.to_host_state()
+        super().__init__(dev.window_hours, clock=dev.clock)
+        self._slot, self._names, self._seen, self._tot, self._q = \
+            host._slot, host._names, host._seen, host._tot, host._q
+        self._dev = dev
+
+    def record_counts(self, ids: List[str], counts: Iterable[int], now: Optional[float] = None) -> None:
+        now = self.clock() if now is None else now
+        super().record_counts(ids, counts, now)
+        try:
+            self._dev.record_counts(ids, counts, now)
+        except Exception:  # noqa: BLE001 - the device may be the thing that failed
+            log.warning("could not record the fallback batch in the device frequency window")

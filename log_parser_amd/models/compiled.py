@@ -387,6 +387,9 @@ class CompiledLibrary:
         self.scan_regs_single = self.scan_regs_single + self.bpg_scan_regs
         self._build_host_matchers()
         self.bpg_pool = np.concatenate(bpgs) if bpgs else np.zeros(1, np.uint64)
+        self.bpg_widths = 0                  # bit W: a program of W words exists (bpg.hip launches)
+        for b in bpgs:
+            self.bpg_widths |= 1 << int(b[0] & np.uint64(0xFF))
         self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
         self.dfa_bytemap = np.concatenate(bytemaps)
         self.dfa_trans = np.concatenate(trans)
@@ -648,7 +651,8 @@ class CompiledLibrary:
         t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc),
                            T(self.bpg_pool.view(np.int64))]
         d = t["dfa_arrays"]
-        t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr())
+        t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr(),
+                    self.bpg_widths)
         t["scan_regs"] = T(np.array(self.scan_regs_single, np.int32))
         t["host_is"] = T(self.host_is)
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]

@@ -525,6 +525,13 @@ def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text
 SUMMARY_MAX_K = 1024
 
 
+def _check_k(k: int) -> None:
+    """The summary kernel keeps at most SUMMARY_MAX_K rows: a larger top-k is a configuration
+    error, not something to truncate silently (engine.topk is validated at config load)."""
+    if int(k) > SUMMARY_MAX_K:
+        raise ValueError(f"top-k {k} exceeds the summary kernel's maximum of {SUMMARY_MAX_K}")
+
+
 def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int, sev_index: torch.Tensor,
               npat: int, nsev: int, line_add: Optional[torch.Tensor] = None, ws: Optional[Workspace] = None,
               pack_events: bool = False, hist_out: Optional[torch.Tensor] = None):
@@ -537,7 +544,8 @@ def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int
     ``packed`` (with ``pack_events``) is every event as uint8[20 n] = [global line int64 x n |
     score f64 x n | pattern int32 x n], written by the same kernel. No host sync."""
     dev = score.device
-    k = max(1, min(int(k), SUMMARY_MAX_K))
+    _check_k(k)
+    k = max(1, int(k))
     n = score.numel()
     rows = torch.empty((k, 3), dtype=torch.float64, device=dev)
     if hist_out is not None:           # zeroed by the caller: [pattern hist | severity hist | ...]
@@ -592,7 +600,8 @@ def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: 
 def topk_rows(rows: torch.Tensor, k: int, ws: Optional[Workspace] = None) -> torch.Tensor:
     """Merge (score, line, pattern) rows (e.g. every rank's top-k) into the k best, same order."""
     dev = rows.device
-    k = max(1, min(int(k), SUMMARY_MAX_K))
+    _check_k(k)
+    k = max(1, int(k))
     rows = rows.contiguous()
     out = torch.empty((k, 3), dtype=torch.float64, device=dev)
     ins = (0, 0, 0, 0, 0, 0, rows.data_ptr())

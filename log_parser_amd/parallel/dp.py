@@ -166,7 +166,8 @@ class ShardedAnalyzer:
         # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
         # rank's top-k rows with global line numbers, no host sync), then ONE all-reduce for the
         # histograms + frequency counts and one all-gather of k rows
-        k = max(1, min(topk, K.SUMMARY_MAX_K))
+        K._check_k(topk)
+        k = max(1, topk)
         rows, _, _, packed = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
                                          line_add=segs.g0, ws=eng.ws, pack_events=pack_events, hist_out=red)
         red = all_reduce_sum(red, self.group)

@@ -129,6 +129,7 @@ class StreamAnalyzer:
                  keep_events: bool = True):
         self.engine = engine
         self.chunk_bytes = int(chunk_bytes or engine.config["engine.chunk-bytes"])
+        K._check_k(topk)
         self.topk = topk
         self.keep_events = keep_events
         lib = engine.lib

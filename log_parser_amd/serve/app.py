@@ -31,7 +31,8 @@ import torch
 from fastapi import FastAPI, Request
 from fastapi.responses import Response
 
-from ..engine import Engine, FrequencyTurn
+from ..engine import Engine, FrequencyTurn, SharedWindowTurn
+from ..frequency import MirroredFrequencyState
 from ..models.compiled import CompiledLibrary
 from ..models.library import load_pattern_directory
 from ..native import N
@@ -66,7 +67,7 @@ class Batcher:
     def __init__(self, engines, max_requests: int, max_bytes: int, max_wait_ms: float, metrics: Metrics):
         self.engines: List[Engine] = list(engines) if isinstance(engines, (list, tuple)) else [engines]
         self.engine = self.engines[0]
-        self.turn: Optional[FrequencyTurn] = FrequencyTurn() if len(self.engines) > 1 else None
+        self.turn: Optional[SharedWindowTurn] = SharedWindowTurn() if len(self.engines) > 1 else None
         self.max_requests = max_requests
         self.max_bytes = max_bytes
         self.max_wait = max_wait_ms / 1000.0
@@ -193,27 +194,43 @@ class Batcher:
             if not self.fallback_cpu:
                 raise
             log.exception("device batch failed; serving it from the CPU backend")
-            job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq)
+            job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq, record=not job.recorded)
 
     def _cpu(self, eng: Engine) -> Engine:
+        """The CPU backend for one failed batch. A device-resident window is not touched by it
+        directly (the device may be the thing that failed): the fallback reads a host copy of the
+        window (empty when the device cannot be read) and its record goes to that copy and, best
+        effort, back to the device window."""
         with self._cpu_lock:
             self.metrics.device_failures += 1
-            if self._cpu_engine is None:
-                self._cpu_engine = Engine(eng.lib, eng.config, device=torch.device("cpu"), freq=eng.freq)
-                self._cpu_engine.fault_every = 0
-            return self._cpu_engine
+            freq = eng.freq
+            if getattr(freq, "device_resident", False):
+                freq = MirroredFrequencyState(freq)
+            elif self._cpu_engine is not None:
+                return self._cpu_engine
+            cpu = Engine(eng.lib, eng.config, device=torch.device("cpu"), freq=freq)
+            cpu.fault_every = cpu.fault_after_record = 0
+            if not getattr(eng.freq, "device_resident", False):
+                self._cpu_engine = cpu
+            return cpu
 
     def analyze(self, eng: Engine, logs: List[str], seq: int) -> List[bytes]:
         """GPU batch; on a device failure (HIP error, OOM, lost device) serve the batch from the CPU
-        backend — same library tables and the same frequency state — for availability only
-        (SURVEY §5.3), and report it in /metrics."""
+        backend — same library tables, a host copy of the frequency window — for availability only
+        (SURVEY §5.3), and report it in /metrics. A batch whose counts already entered the window
+        (failure after the record) is not recorded again."""
+        job = eng.pack_batch(logs)
         try:
-            return eng.analyze_batch_json(logs, self.turn, seq)
+            try:
+                eng.device_batch(job, self.turn, seq)
+                return eng.emit_batch(job)
+            finally:
+                eng.release_batch(job)
         except Exception:  # noqa: BLE001
             if not self.fallback_cpu:
                 raise
             log.exception("device batch failed; serving it from the CPU backend")
-            return self._cpu(eng).analyze_batch_json(logs, self.turn, seq)
+            return self._cpu(eng).analyze_batch_json(logs, self.turn, seq, record=not job.recorded)
 
 
 def serve_devices(config: Config) -> List[torch.device]:
@@ -263,12 +280,18 @@ class Service:
             if self._batcher is None:
                 cfg = self.config
                 engines = [eng]
-                devs = [d for d in serve_devices(cfg) if d != eng.device]
-                if devs and getattr(eng.freq, "device_resident", False):
-                    # several GPUs record into ONE window in arrival order (FrequencyTurn): host state
-                    from ..frequency import FrequencyState
-                    eng.freq = FrequencyState(eng.params.freq_window_hours)
-                for dev in devs:                   # data-parallel serving: one engine per GPU
+                devs = serve_devices(cfg)
+                if devs and devs[0] == eng.device:
+                    devs = devs[1:]
+                elif eng.device in devs:
+                    devs.remove(eng.device)
+                for dev in devs:                   # data-parallel serving: one engine per GPU (or stream)
+                    if getattr(eng.freq, "device_resident", False) and dev.type == "cuda":
+                        # ONE window in HBM of the first engine's GPU: the others' kernels read and
+                        # record it over xGMI peer access, in arrival order (SharedWindowTurn)
+                        if not N.enable_peer_access(dev.index if dev.index is not None else 0,
+                                                    eng.freq.device.index or 0):
+                            raise RuntimeError(f"no peer access from {dev} to {eng.freq.device} for the shared window")
                     engines.append(Engine(engines[0].lib, cfg, device=dev, freq=engines[0].freq))
                 if len(engines) > 1:
                     log.info("serving on %d engines: %s", len(engines), [str(e.device) for e in engines])

@@ -69,6 +69,8 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.trace": (False, bool),
     # fault injection for tests: fail the device path every N-th batch (0 = off)
     "engine.fault-inject-every": (0, int),
+    # fault injection for tests: fail every N-th batch AFTER its frequency record (0 = off)
+    "engine.fault-inject-after-record": (0, int),
     # continuous batching
     "engine.batch.max-requests": (2048, int),
     "engine.batch.max-bytes": (256 << 20, int),
@@ -133,6 +135,18 @@ def parse_properties(text: str) -> Dict[str, str]:
     return out
 
 
+TOPK_MAX = 1024     # rows the summary / top-k kernel keeps (ops/kernels.py SUMMARY_MAX_K)
+
+
+def _validate(v: Mapping[str, Any]) -> None:
+    k = v.get("engine.topk")
+    if k is not None and not 0 <= int(k) <= TOPK_MAX:
+        raise ValueError(f"engine.topk must be within [0, {TOPK_MAX}], got {k}")
+    e = v.get("engine.nfa-engine")
+    if e is not None and e not in ("bpg", "mfma"):
+        raise ValueError(f"engine.nfa-engine must be 'bpg' or 'mfma', got {e!r}")
+
+
 @dataclass(frozen=True)
 class Config:
     values: Mapping[str, Any] = field(default_factory=dict)
@@ -159,6 +173,7 @@ class Config:
         for k, v in vals.items():
             typ = ALL_KEYS[k][1] if k in ALL_KEYS else str
             typed[k] = _coerce(v, typ)
+        _validate(typed)
         return Config(values=typed)
 
     def __getitem__(self, key: str) -> Any:

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from log_parser_amd import golden
-from log_parser_amd.engine import Engine, FrequencyTurn
+from log_parser_amd.engine import Engine, FrequencyTurn, SharedWindowTurn
 from log_parser_amd.models.compiled import CompiledLibrary
 from log_parser_amd.serve.app import Batcher, serve_devices
 from log_parser_amd.utils.config import Config, ScoringParams
@@ -16,7 +16,7 @@ from log_parser_amd.utils.metrics import Metrics
 from log_parser_amd.utils.synth import make_library, make_log
 
 
-def _check(devices, n_req=48, max_requests=3):
+def _check(devices, n_req=48, max_requests=3, runner=False):
     # frequent ids and a low threshold so the frequency penalty actually bites across requests
     sets, trig = make_library(25, seed=91)
     params = ScoringParams(freq_threshold=1.0)
@@ -29,6 +29,9 @@ def _check(devices, n_req=48, max_requests=3):
     futs = [b.submit(r) for r in reqs]
     outs = [json.loads(f.result(timeout=300)) for f in futs]
     b.close()
+    if runner:      # every engine served through the native runner on the ONE shared device window
+        assert all(e._runner not in (None, False) for e in engines)
+        assert all(e.freq is e0.freq and e.freq_on_device for e in engines)
     tracker = golden.FrequencyTracker(params)
     for r, o in zip(reqs, outs):
         g = golden.analyze(r, sets, params, tracker)
@@ -67,5 +70,32 @@ def test_serve_devices_parsing():
 
 @pytest.mark.gpu
 def test_two_engines_on_one_gpu_equal_sequential_reference(gpu_device):
-    """Two engines (own HIP streams) on the one test GPU stand in for one engine per GPU."""
-    _check([gpu_device, gpu_device])
+    """Two engines (own HIP streams) on the one test GPU stand in for one engine per GPU: both run
+    the native request runner on one shared device-resident window (SharedWindowTurn)."""
+    _check([gpu_device, gpu_device], runner=True)
+
+
+@pytest.mark.gpu
+def test_four_engines_shared_window_service(gpu_device):
+    """engine.serve-devices=cuda:0 x4 through the Service: identical to sequential serving."""
+    from log_parser_amd.serve.app import Service
+    sets, trig = make_library(25, seed=93)
+    params = ScoringParams(freq_threshold=1.0)
+    lib = CompiledLibrary(sets, params)
+    dev = str(gpu_device)
+    cfg = Config.load(overrides={"engine.device": dev, "engine.serve-devices": ",".join([dev] * 4),
+                                 "scoring.frequency.threshold": "1.0"})
+    svc = Service(cfg, engine=Engine(lib, cfg, device=gpu_device))
+    b = svc.batcher()
+    assert len(b.engines) == 4 and isinstance(b.turn, SharedWindowTurn)
+    reqs = [make_log(150 + 13 * (i % 7), trig, seed=1900 + i, hit_rate=0.1) for i in range(64)]
+    outs = [json.loads(f.result(timeout=300)) for f in [b.submit(r) for r in reqs]]
+    svc.close()
+    tracker = golden.FrequencyTracker(params)
+    for r, o in zip(reqs, outs):
+        g = golden.analyze(r, sets, params, tracker)
+        assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o["events"]] == \
+               [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+        for a, c in zip(o["events"], g["events"]):
+            assert a["score"] == pytest.approx(c["score"], rel=1e-12, abs=0)
+    assert sum(e._runner not in (None, False) for e in b.engines) >= 2

@@ -31,6 +31,33 @@ def test_device_failure_falls_back_to_cpu_backend():
         assert "lp_device_failures_total 2" in c.get("/metrics").text
 
 
+def _serve_with_faults(device, overrides, n=5, params=None):
+    params = params or ScoringParams(freq_threshold=1.0)
+    sets, trig = make_library(20, seed=62)
+    lib = CompiledLibrary(sets, params)
+    cfg = Config.load(overrides={"engine.device": str(device), "engine.batch.max-wait-ms": "0", **overrides})
+    eng = Engine(lib, cfg, device=device)
+    fz = golden.FrequencyTracker(params)
+    with TestClient(create_app(cfg, engine=eng)) as c:
+        for i in range(n):
+            logs = make_log(300, trig, seed=170 + i, hit_rate=0.08)
+            r = c.post("/parse", json={"pod": {}, "logs": logs})
+            assert r.status_code == 200
+            g = golden.analyze(logs, sets, params, fz)
+            assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r.json()["events"]] == \
+                [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+            np.testing.assert_allclose([e["score"] for e in r.json()["events"]], [e["score"] for e in g["events"]],
+                                       rtol=1e-12)
+        return c.get("/metrics").text, eng.freq.statistics()
+
+
+def test_failure_after_record_is_not_recorded_twice():
+    """A batch that fails AFTER its counts entered the window is served by the fallback without
+    a second record: later batches see exactly the reference's frequency penalties."""
+    metrics, stats = _serve_with_faults(torch.device("cpu"), {"engine.fault-inject-after-record": "2"})
+    assert "lp_device_failures_total 2" in metrics
+
+
 def test_stream_checkpoint_resume_is_exact(tmp_path):
     import pytest
     from log_parser_amd.parallel.stream import StreamAnalyzer
@@ -48,3 +75,16 @@ def test_stream_checkpoint_resume_is_exact(tmp_path):
     for a, b in zip(out.events, ref.events):
         np.testing.assert_array_equal(a, b)
     assert out.summary == ref.summary
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_gpu_fallback_uses_host_copy_of_device_window(gpu_device):
+    """Device-resident window: the CPU fallback reads a host copy of it (not the GPU) and records
+    back; failures before and after the runner's record keep the reference penalties."""
+    m1, _ = _serve_with_faults(gpu_device, {"engine.fault-inject-every": "2"})
+    assert "lp_device_failures_total 2" in m1
+    m2, _ = _serve_with_faults(gpu_device, {"engine.fault-inject-after-record": "2"})
+    assert "lp_device_failures_total 2" in m2

@@ -16,7 +16,8 @@ primaries). A timed step is the complete pipeline for the shard:
 
 Launch: ``python bench.py --gpus N`` starts N rank processes itself (``utils/launch.py``; the
 parent makes no GPU call) -- or runs as one rank of ``torch.distributed.run``. On GPUs the
-process group is ``nccl`` (= RCCL over xGMI) at every world size, including 1.
+process group is ``nccl`` (= RCCL over xGMI) at every world size, including 1: the 1-GPU number
+runs the same two in-place all-gathers per step as the 8-GPU run (``parallel/dp.py``).
 
 Nothing is cached between steps (the frequency state evolves exactly as the reference's would).
 Rank 0 prints one JSON line; ``value`` is total lines/s over all ranks (max step time across
@@ -61,10 +62,9 @@ def parse():
     ap.add_argument("--d2h-stream", default="copy", choices=["copy", "compute"],
                     help="stream of the per-step event D2H (diagnostic A/B)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
-                    help="process group: auto = nccl (RCCL) on GPUs / gloo on CPU for world size > 1 and none "
-                         "at world size 1 (RCCL's world-1 self-copy rides the SDMA engine the ingest copy "
-                         "occupies and stalls the step; measured 23.6 -> 26-28 ms); nccl / gloo force a group "
-                         "at any size (gloo on GPUs = host-staged, to rehearse several ranks on ONE GPU)")
+                    help="process group: auto = nccl (RCCL) on GPUs at every world size, gloo on CPU for world "
+                         "size > 1 and none on CPU at world size 1; nccl / gloo / none force one (gloo on GPUs "
+                         "= host-staged, to rehearse several ranks on ONE GPU; none = no collectives at world 1)")
     return ap.parse_args()
 
 
@@ -126,7 +126,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
         device = torch.device("cpu")
     backend = args.backend
     if backend == "auto":
-        backend = ("nccl" if use_cuda else "gloo") if world > 1 else "none"
+        backend = "nccl" if use_cuda else ("gloo" if world > 1 else "none")
     if backend == "none" and world > 1:
         backend = "nccl" if use_cuda else "gloo"
     if backend != "none":
@@ -249,6 +249,19 @@ def run(args, sets, trig, rank, world, local_rank, server):
         if use_cuda:
             torch.cuda.synchronize()
 
+    # per-rank diagnostics: this rank's pinned-host -> HBM bandwidth (one whole-shard copy, untimed)
+    # and its GPU's NUMA node, so an 8-GPU result explains itself (a slow socket, a far buffer)
+    h2d_gbps = 0.0
+    if use_cuda:
+        a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a_.record()
+        bufs[0].copy_(host, non_blocking=True)
+        b_.record()
+        torch.cuda.synchronize()
+        h2d_gbps = size / (a_.elapsed_time(b_) / 1e3) / 1e9
+    from log_parser_amd.utils.numa import gpu_numa_node
+    numa = gpu_numa_node(local_rank) if use_cuda else -1
+
     for _ in range(args.warmup):
         step()
     barrier()
@@ -264,12 +277,15 @@ def run(args, sets, trig, rank, world, local_rank, server):
         last = step()
     barrier()
     dt = time.perf_counter() - t0
-    per_rank = [dt]
+    dms_local = float(np.mean([a.elapsed_time(b) for a, b in state["dev"]])) if state.get("dev") else -1.0
+    diag = [dt, h2d_gbps, dms_local, float(numa)]
+    per_rank_diag = [diag]
     if dist.is_initialized():
-        dt_t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dt_t = torch.tensor(diag, dtype=torch.float64, device=device)
         if dist.get_backend() == "gloo":
             dt_t = dt_t.cpu()
-        per_rank = all_gather_rows(dt_t).flatten().cpu().tolist()
+        per_rank_diag = all_gather_rows(dt_t).cpu().tolist()
+    per_rank = [x[0] for x in per_rank_diag]
     dt = max(per_rank)
     total_lines = last.total_lines
     ms = dt / args.steps * 1e3
@@ -291,6 +307,9 @@ def run(args, sets, trig, rank, world, local_rank, server):
             "world_size": dist.get_world_size() if dist.is_initialized() else 1,
             "backend": dist.get_backend() if dist.is_initialized() else "none",
             "ms_per_step_per_rank": [round(x / args.steps * 1e3, 3) for x in per_rank],
+            "per_rank": [{"rank": r, "ms_per_step": round(x[0] / args.steps * 1e3, 3), "h2d_GBps": round(x[1], 2),
+                          "device_ms": round(x[2], 3), "numa_node": int(x[3])} for r, x in enumerate(per_rank_diag)],
+            "collectives_per_step": 2 if dist.is_initialized() else 0,
             "matcher_counts_rank0": dict(eng.arena.last),
         }
         if state.get("dev"):

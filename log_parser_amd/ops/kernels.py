@@ -534,7 +534,8 @@ def _check_k(k: int) -> None:
 
 def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int, sev_index: torch.Tensor,
               npat: int, nsev: int, line_add: Optional[torch.Tensor] = None, ws: Optional[Workspace] = None,
-              pack_events: bool = False, hist_out: Optional[torch.Tensor] = None):
+              pack_events: bool = False, hist_out: Optional[torch.Tensor] = None,
+              rows_out: Optional[torch.Tensor] = None):
     """Top-k rows + histograms of scored events (csrc/kernels/summarize.hip).
 
     ``line`` is int32 (local, plus the device scalar ``line_add``) or int64 (global);
@@ -547,7 +548,7 @@ def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int
     _check_k(k)
     k = max(1, int(k))
     n = score.numel()
-    rows = torch.empty((k, 3), dtype=torch.float64, device=dev)
+    rows = rows_out if rows_out is not None else torch.empty((k, 3), dtype=torch.float64, device=dev)
     if hist_out is not None:           # zeroed by the caller: [pattern hist | severity hist | ...]
         pat_hist, sev_hist = hist_out[:npat], hist_out[npat:npat + nsev]
     else:
@@ -571,10 +572,12 @@ def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int
     return rows, pat_hist[:npat], sev_hist[:nsev], packed
 
 
-def dp_pack(own_lines: int, freq_counts: torch.Tensor, nk: int, chain: torch.Tensor) -> torch.Tensor:
-    """C1+C3+C4 all-gather payload [owned lines | nk frequency counts | chain table] (int64)."""
+def dp_pack(own_lines: int, freq_counts: torch.Tensor, nk: int, chain: torch.Tensor,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C1+C3+C4 all-gather payload [owned lines | nk frequency counts | chain table] (int64);
+    ``out``: where to write it (this rank's row of an in-place all-gather buffer)."""
     ns = chain.numel()
-    pack = torch.empty(1 + nk + ns, dtype=torch.int64, device=chain.device)
+    pack = out if out is not None else torch.empty(1 + nk + ns, dtype=torch.int64, device=chain.device)
     fc = freq_counts if freq_counts.dtype == torch.int64 else freq_counts.to(torch.int64)
     N.dp_pack(int(own_lines), fc.data_ptr(), nk, chain.data_ptr(), ns, pack.data_ptr(), _s(chain), chain.is_cuda)
     return pack

@@ -7,19 +7,25 @@ the ±5 sequence window). Every cross-shard dependency of the reference's sequen
 resolved with collectives:
 
   C1  global N / line offsets  (ScoringService.java:125)      \\
-  C3  frequency ordering       (ScoringService.java:84-88)     } ONE packed all_gather, int64
+  C3  frequency ordering       (ScoringService.java:84-88)     } in-place all_gather #1, int64
   C4  backward sequence chain  (ScoringService.java:296-305)  /   [own_lines | freq counts | chain]
-  C5/C6 severity histogram + frequency histogram               -> all_reduce(sum)
-  C7  top-k events                                             -> all_gather of k rows, merge
+  C5/C6 severity histogram + frequency histogram  \  in-place all_gather #2 of
+  C7  top-k events                                /   [pattern hist | severity hist | freq counts | k rows],
+                                                     then a local sum over ranks + top-k merge
   (the local halves of C5-C7 are one hand-written kernel chain, csrc/kernels/summarize.hip)
+
+Two collectives per step, both in place (this rank's payload is written straight into its row of
+the gather buffer): at world size 1 RCCL moves no bytes at all -- a world-1 copy was the
+self-copy that queued behind the PCIe ingest in round 2 -- and at world size N each step moves
+N x ~20 KB, latency-bound either way (an all-reduce would be the same number of latency hops and
+the top-k rows have to be gathered anyway).
   C2  halos: by default every rank stages its halo lines from the shared host source together
       with its own lines (no extra collective); ``exchange_halos`` is the point-to-point variant
       (batch_isend_irecv with both neighbours) for ranks that only hold their own lines
 
-Every message but the top-k rows is a few KB, so each step pays ~3 latency-bound collectives
-regardless of log size; xGMI bandwidth is irrelevant, PCIe ingest and HBM are what scale.
-The backend is whatever ``torch.distributed`` was initialised with: ``nccl`` (= RCCL on ROCm)
-on GPUs, ``gloo`` for the CPU tests.
+xGMI bandwidth is irrelevant here; PCIe ingest and HBM are what scale. The backend is whatever
+``torch.distributed`` was initialised with: ``nccl`` (= RCCL on ROCm) on GPUs, ``gloo`` for the
+CPU tests (and to rehearse several ranks on one GPU, host-staged).
 """
 from __future__ import annotations
 
@@ -48,9 +54,26 @@ def host_staged(group=None) -> bool:
 
 
 def distributed() -> bool:
-    """A process group exists. Collectives then always run -- also at world size 1, so a 1-GPU
-    bench still drives the device-tensor RCCL path the 8-GPU run uses."""
+    """A process group exists. Collectives then always run -- also at world size 1 (the bench's
+    default on a GPU is a world-1 RCCL group, so the 1-GPU number drives the same calls the
+    8-GPU run makes; in place, they move no bytes there)."""
     return dist.is_available() and dist.is_initialized()
+
+
+def all_gather_inplace(buf: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place all_gather of ``buf`` [world, n]: this rank's row is already filled; on return
+    every row is (RCCL all_gather_into_tensor with the input aliasing its output row)."""
+    r, w = world()
+    if not distributed():
+        return buf
+    if buf.is_cuda and not host_staged(group):
+        dist.all_gather_into_tensor(buf, buf[r], group=group)
+        return buf
+    h = buf.cpu()
+    rows = list(h.unbind(0))
+    dist.all_gather(rows, h[r].clone(), group=group)
+    buf.copy_(h)
+    return buf
 
 
 def all_gather_rows(t: torch.Tensor, group=None) -> torch.Tensor:
@@ -152,32 +175,37 @@ class ShardedAnalyzer:
         prep = eng.prepare(text, nbytes, ls, ll, segs)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
-        pack = K.dp_pack(own_hi - own_lo, prep.freq_counts, nk, chain)         # k_dp_pack
-        g = all_gather_rows(pack, self.group)                      # C1 + C3 + C4 in one collective
+        ns = chain.numel()
+        g = torch.empty((wsize, 1 + nk + ns), dtype=torch.int64, device=dev)
+        K.dp_pack(own_hi - own_lo, prep.freq_counts, nk, chain, out=g[rank])      # k_dp_pack -> own row
+        all_gather_inplace(g, self.group)                          # collective 1: C1 + C3 + C4
         own_counts = g[:, 0]
-        # the all-reduce buffer [pattern hist | severity hist | frequency counts]: k_dp_carry seeds
-        # the counts, the summary kernel accumulates the histograms
+        # collective 2 buffer, one row per rank: [pattern hist | severity hist | frequency counts |
+        # top-k rows (k x 3 f64)]; k_dp_carry seeds the counts, the summary kernel the histograms + rows
         P, S = len(lib.patterns), len(lib.sev_names)
-        red = torch.zeros(P + S + nk, dtype=torch.int64, device=dev)
-        own_start, segs.g0, segs.n, carry, seq_carry = K.dp_carry(     # k_dp_carry: device scalars, no sync
-            g, rank, nk, chain.numel(), halo_left, eng.freq_carry() if nk else None, self.slot_e0, self.slot_k,
-            red_tail=red[P + S:] if nk else None)
-        res = eng.finish(prep, segs, carry, seq_carry, with_factors)
-        # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
-        # rank's top-k rows with global line numbers, no host sync), then ONE all-reduce for the
-        # histograms + frequency counts and one all-gather of k rows
         K._check_k(topk)
         k = max(1, topk)
-        rows, _, _, packed = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
-                                         line_add=segs.g0, ws=eng.ws, pack_events=pack_events, hist_out=red)
-        red = all_reduce_sum(red, self.group)
+        H = P + S + nk
+        red2 = torch.zeros((wsize, H + 3 * k), dtype=torch.int64, device=dev)
+        mine = red2[rank]
+        own_start, segs.g0, segs.n, carry, seq_carry = K.dp_carry(     # k_dp_carry: device scalars, no sync
+            g, rank, nk, ns, halo_left, eng.freq_carry() if nk else None, self.slot_e0, self.slot_k,
+            red_tail=mine[P + S:H] if nk else None)
+        res = eng.finish(prep, segs, carry, seq_carry, with_factors)
+        # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
+        # rank's top-k rows with global line numbers, no host sync) into this rank's row
+        rows_out = mine[H:].view(torch.float64).view(k, 3)
+        _, _, _, packed = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
+                                      line_add=segs.g0, ws=eng.ws, pack_events=pack_events, hist_out=mine[:H],
+                                      rows_out=rows_out)
+        all_gather_inplace(red2, self.group)                       # collective 2: C5 + C6 + C7
+        red = red2[:, :H].sum(0) if wsize > 1 else red2[0, :H]
         eng.commit_frequency(red[P + S:])
         out = StepOutput(res, own_counts, rank, red[:P], severity_counts=red[P:P + S], own_lo=own_lo,
                          own_start_dev=own_start, events_packed=packed)
-        if topk > 0:
-            allrows = all_gather_rows(rows.flatten(), self.group).view(-1, 3)
-            if rank == 0:
-                out.topk_rows = K.topk_rows(allrows, k, ws=eng.ws) if allrows.shape[0] > k else allrows
+        if topk > 0 and rank == 0:
+            allrows = red2[:, H:].contiguous().view(torch.float64).view(-1, 3)
+            out.topk_rows = K.topk_rows(allrows, k, ws=eng.ws) if allrows.shape[0] > k else allrows
         return out
 
     def summary(self, pattern_counts: torch.Tensor, first_pat: Optional[int] = None,

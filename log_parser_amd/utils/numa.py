@@ -46,6 +46,18 @@ def gpu_numa_cpus(index: int) -> Set[int]:
         return set()
 
 
+def gpu_numa_node(index: int) -> int:
+    """NUMA node of GPU ``index`` (-1 when unknown)."""
+    path = gpu_pci_path(index)
+    if path is None:
+        return -1
+    try:
+        with open(os.path.join(path, "numa_node")) as f:
+            return int(f.read().strip())
+    except (OSError, ValueError):
+        return -1
+
+
 def bind_to_gpu_numa(index: int) -> Optional[Set[int]]:
     """Restrict this process to the CPUs local to GPU ``index`` (intersected with the CPUs it may
     already use). Returns the new CPU set, or None when nothing was changed."""

@@ -66,6 +66,24 @@ def test_bench_spawns_its_own_ranks(tmp_path):
     assert d["config"]["events_to_host_rank0"] > 0
 
 
+def test_bench_eight_ranks_cpu(tmp_path):
+    """The driver's N=8 launch, rehearsed on CPU: 8 rank processes, gloo, halos on both sides of
+    the 6 inner ranks, the two in-place collectives, per-rank diagnostics in the JSON."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu", "--steps", "2",
+           "--warmup", "1", "--lines-per-gpu", "3000", "--block-lines", "3000", "--parse-requests", "0",
+           "--library", "synthetic", "--patterns", "200"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 8 and d["world_size"] == 8 and d["config"]["parallelism"] == "dp8"
+    assert len(d["ms_per_step_per_rank"]) == 8 and d["ms_per_step"] == max(d["ms_per_step_per_rank"])
+    assert d["config"]["global_batch"] == 8 * d["config"]["lines_per_gpu"]
+    assert len(d["per_rank"]) == 8 and all("numa_node" in x for x in d["per_rank"])
+
+
 def test_bench_single_rank_parse_over_http(tmp_path):
     """--gpus 1 --backend gloo on CPU: a process group at world size 1 (collectives still run) and
     p50 measured through a real POST /parse server process next to the engine-only latency."""

@@ -1,4 +1,6 @@
-"""Line-sharded data parallelism (parallel/dp.py) on CPU with gloo, world_size 2 and 3.
+"""Line-sharded data parallelism (parallel/dp.py) on CPU with gloo, world_size 2, 3, 4 and 8
+(the driver's scaling run launches 8 ranks: the 8-rank halo / carry / top-k paths are rehearsed
+here on CPU).
 
 The sharded pipeline (halos + packed all_gather carries + all_reduce histograms + top-k gather)
 must reproduce the single-process run event for event and score for score, over consecutive
@@ -115,7 +117,7 @@ def _run_sharded(world, dev):
         np.testing.assert_allclose(got[0][s][4], top, rtol=1e-13)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_equals_single(world):
     _run_sharded(world, "cpu")
 
@@ -161,7 +163,7 @@ def _worker_p2p(rank, world, port, q, dev="cpu"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_p2p_halo_exchange_equals_single(world):
     _run_p2p(world, "cpu")
 
@@ -189,3 +191,55 @@ def _run_p2p(world, dev):
         np.testing.assert_array_equal(np.concatenate([got[r][s][0] for r in range(world)]), rl)
         np.testing.assert_array_equal(np.concatenate([got[r][s][1] for r in range(world)]), rp)
         np.testing.assert_allclose(np.concatenate([got[r][s][2] for r in range(world)]), rs, rtol=1e-13, atol=0)
+
+
+def _worker_nccl1(port, q):
+    """One rank, RCCL (nccl backend) at world size 1 on the test GPU: the device-tensor in-place
+    all-gathers the 8-GPU run uses, against the single-process engine."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        lib, data = _setup()
+        eng = Engine(lib, Config.load(overrides={"engine.device": "cuda:0"}), device=dev)
+        t = _text(data).to(dev)
+        ls, ll = K.split_lines(t, len(data))
+        sa = ShardedAnalyzer(eng)
+        res = []
+        for _ in range(STEPS):
+            out = sa.step(t, len(data), ls, ll, 0, 0, topk=5)
+            r = out.result
+            res.append((r.ev_line.cpu().numpy().astype(np.int64), r.ev_pat.cpu().numpy(), r.score.cpu().numpy(),
+                        out.total_lines, out.topk_score.cpu().numpy(), out.topk_line.cpu().numpy(),
+                        out.pattern_counts.cpu().numpy()))
+        q.put(("ok", res, dist.get_backend()))
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", repr(e), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_nccl_world1_equals_engine(gpu_device):
+    """ShardedAnalyzer under RCCL at world 1 == Engine.run on the whole log, top-k included."""
+    ref = _reference()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_nccl1, args=(_free_port(), q))
+    p.start()
+    status, res, backend = q.get(timeout=300)
+    p.join(timeout=60)
+    assert status == "ok", res
+    assert backend == "nccl" and p.exitcode == 0
+    for s in range(STEPS):
+        rl, rp, rs, n_lines = ref[s]
+        gl, gp, gs, tot, top, topl, pc = res[s]
+        assert tot == n_lines
+        np.testing.assert_array_equal(gl, rl)
+        np.testing.assert_array_equal(gp, rp)
+        np.testing.assert_allclose(gs, rs, rtol=1e-13, atol=0)
+        order = np.lexsort((rl, -rs))[:5]                # score desc, line asc
+        np.testing.assert_allclose(top, rs[order], rtol=1e-13)
+        np.testing.assert_array_equal(topl, rl[order])
+        assert pc.sum() == rl.size

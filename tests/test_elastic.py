@@ -108,3 +108,50 @@ def test_rccl_rebuild_aborts_instead_of_destroying(monkeypatch):
     g.backend = "gloo"
     g.rebuild()
     assert calls == ["destroy", "init"]
+
+
+def _abort_worker(host, port, q):
+    """World-1 RCCL communicator: collective -> real _abort_process_group -> re-init -> collective,
+    then an elastic analysis step on the rebuilt group."""
+    import torch.distributed as dist
+    from log_parser_amd.parallel.elastic import ElasticAnalyzer, ElasticGroup, connect
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        grp = ElasticGroup(connect(host, port), 0, 1, backend="nccl", timeout_s=30.0, grace_s=0.2, device=dev)
+        x = torch.arange(8, dtype=torch.int64, device=dev)
+        dist.all_reduce(x)
+        before = x.cpu().tolist()
+        grp.rebuild()                                    # ncclCommAbort, new generation, new communicator
+        y = torch.full((4,), 3, dtype=torch.int64, device=dev)
+        dist.all_reduce(y)
+        after = y.cpu().tolist()
+        lib, data = _setup()
+        eng = Engine(lib, Config.load(overrides={"engine.device": "cuda:0"}), device=dev)
+        out = ElasticAnalyzer(eng, grp).step(data, topk=5)
+        q.put(("ok", before, after, grp.gen, out.result.score.cpu().numpy(), dist.get_backend()))
+        grp.close()
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", repr(e), None, None, None, None))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_rccl_abort_reinit_cycle_world1(gpu_device):
+    """The RCCL teardown of a rebuild runs for real (not monkeypatched): at world 1 on the test GPU
+    a collective, ncclCommAbort through _abort_process_group, a new generation's communicator and
+    a collective on it, then an elastic step equal to the single-process reference."""
+    import multiprocessing as mp
+    from datetime import timedelta
+    import torch.distributed as dist
+    store = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False, timeout=timedelta(seconds=120))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_abort_worker, args=("127.0.0.1", store.port, q))
+    p.start()
+    r = q.get(timeout=240)
+    p.join(timeout=60)
+    assert r[0] == "ok", r[1]
+    _, before, after, gen, score, backend = r
+    assert before == list(range(8)) and after == [3, 3, 3, 3] and gen == 1 and backend == "nccl"
+    np.testing.assert_allclose(score, _reference()[0][2], rtol=1e-13, atol=0)

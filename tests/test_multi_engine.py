@@ -84,7 +84,7 @@ def test_four_engines_shared_window_service(gpu_device):
     lib = CompiledLibrary(sets, params)
     dev = str(gpu_device)
     cfg = Config.load(overrides={"engine.device": dev, "engine.serve-devices": ",".join([dev] * 4),
-                                 "scoring.frequency.threshold": "1.0"})
+                                 "scoring.frequency.threshold": "1.0", "engine.batch.max-requests": "3"})
     svc = Service(cfg, engine=Engine(lib, cfg, device=gpu_device))
     b = svc.batcher()
     assert len(b.engines) == 4 and isinstance(b.turn, SharedWindowTurn)

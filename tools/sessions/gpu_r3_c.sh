@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 3: new tests, bench nccl (default) vs none, memory-copy trace of the nccl step, kernel stats, full GPU suite.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+R=$(pwd)
+OUT=${OUT:-gpurun_out/r3_c}
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_bpg.py tests/test_multi_engine.py tests/test_resilience.py tests/test_dp.py > $OUT/pytest_new.log 2>&1 && echo NEW_OK || { tail -60 $OUT/pytest_new.log; exit 1; }
+timeout -k 10 300 python tools/scan_ab.py --regexes 64 --lines 1000000 --engine all --reps 5 > $OUT/scan_ab.json 2>&1 && echo AB_OK || { tail -20 $OUT/scan_ab.json; exit 1; }
+tail -1 $OUT/scan_ab.json
+for b in nccl none nccl none; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --backend $b --parse-requests 0 > $OUT/bench_$b.json 2> $OUT/bench_$b.err && echo BENCH_${b}_OK || { tail -20 $OUT/bench_$b.err; exit 1; }
+  python -c "import json;d=json.load(open('$OUT/bench_$b.json'));print('$b',d['value'],d['ms_per_step'],d['device_ms_per_step_rank0'],d['per_rank'])"
+done
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err && echo BENCH_OK || { tail -20 $OUT/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$OUT/bench.json'));print(d['value'],d['ms_per_step'],d['device_ms_per_step_rank0'],d['p50_parse_ms'],d['p99_parse_ms'],d['backend'])"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $R/$OUT/prof_nccl -o run -- python3 $R/bench.py --steps 5 --warmup 2 --parse-requests 0 --backend nccl > $R/$OUT/prof_nccl.log 2>&1 && echo PROF_OK || { tail -20 $R/$OUT/prof_nccl.log; exit 1; }
+cd $R
+timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > $OUT/pytest_gpu.log 2>&1 && echo PYTEST_OK || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log

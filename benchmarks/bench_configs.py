@@ -50,8 +50,11 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
-def _engine(n_patterns, dev, seed=7):
-    sets, trig = make_library(n_patterns, seed=seed)
+def _engine(n_patterns, dev, seed=7, library="realistic"):
+    """Configs 2 / 4 / 5 run on the realistic library (short-literal, literal-free and bounded-gap
+    primaries: utils/synth.realistic_library) unless --library synthetic (the prefilter's best case)."""
+    from log_parser_amd.utils.synth import realistic_library
+    sets, trig = (realistic_library if library == "realistic" else make_library)(n_patterns, seed=seed)
     lib = CompiledLibrary(sets, ScoringParams())
     return Engine(lib, Config.load(overrides={"engine.device": str(dev)}), device=dev), sets, trig
 
@@ -136,7 +139,7 @@ def _rest(args, n_patterns, device, name):
 
 def mode_single(args):
     dev = _dev(args)
-    eng, _, trig = _engine(256, dev)
+    eng, _, trig = _engine(256, dev, library=args.library)
     data = make_log(args.lines, trig, seed=5, hit_rate=0.004, aux_rate=0.01, stack_rate=0.01).encode()
     text, n = eng.stage_text(data)
     ls, ll = K.split_lines(text, n)
@@ -169,7 +172,7 @@ def mode_single(args):
 def mode_stream(args):
     from log_parser_amd.parallel.stream import RepeatBuffer, StreamAnalyzer
     dev = _dev(args)
-    eng, _, trig = _engine(args.patterns, dev)
+    eng, _, trig = _engine(args.patterns, dev, library=args.library)
     block = make_log(200_000, trig, seed=6, hit_rate=0.004, aux_rate=0.01, stack_rate=0.01).encode()
     lines_per_block = block.count(b"\n")
     total = len(block) * max(1, args.lines // lines_per_block)
@@ -193,7 +196,7 @@ def mode_concurrent(args):
     from log_parser_amd.serve.app import Batcher
     from log_parser_amd.utils.metrics import Metrics
     dev = _dev(args)
-    eng, _, trig = _engine(1000, dev)
+    eng, _, trig = _engine(1000, dev, library=args.library)
     rng = np.random.default_rng(0)
     sizes = rng.choice([20, 100, 500, 2000, 10000], size=args.requests, p=[0.3, 0.3, 0.2, 0.15, 0.05])
     pool = {s: [make_log(int(s), trig, seed=int(s) + k, hit_rate=0.01) for k in range(4)] for s in set(sizes.tolist())}
@@ -235,6 +238,55 @@ def mode_concurrent(args):
                       "requests_per_s": round(len(reqs) / wall, 1), "lines_per_s": round(float(sizes.sum()) / wall, 1)}))
 
 
+def mode_concurrent_http(args):
+    """Config 5 as stated: N concurrent POST /parse requests over N keep-alive HTTP connections to
+    the service process (native epoll front end -> continuous batcher -> GPU), mixed body sizes,
+    realistic library. The native load generator (csrc/io/loadgen.cpp) opens every connection
+    first, then sends one request on each at once; latency = first request byte -> last response
+    byte. One untimed burst warms the server; the second is reported."""
+    from log_parser_amd.native import N
+    from log_parser_amd.serve.__main__ import raise_fd_limit
+    from log_parser_amd.utils.restbench import ServerProcess, write_library
+    from log_parser_amd.utils.synth import realistic_library
+    n = args.requests
+    if raise_fd_limit() < n + 256:
+        raise SystemExit(f"open-file limit too low for {n} connections")
+    sets, trig = realistic_library(1000, seed=7)
+    dev = "cpu" if args.device == "cpu" else ("cuda:0" if torch.cuda.is_available() else "cpu")
+    srv = ServerProcess(write_library(sets), dev, http="native",
+                        extra=[f"-Dengine.serve-devices={','.join([dev] * args.engines)}"] if args.engines > 1 else [])
+    try:
+        if not srv.wait_ready():
+            raise SystemExit("server did not come up")
+        rng = np.random.default_rng(0)
+        sizes_set = [20, 100, 500, 2000, 10000]
+        sizes = rng.choice(sizes_set, size=n, p=[0.3, 0.3, 0.2, 0.15, 0.05])
+        msgs, lines_of = [], []
+        for s_ in sizes_set:
+            for k in range(4):
+                body = json.dumps({"pod": {"metadata": {"name": f"pod-{s_}-{k}"}},
+                                   "logs": make_log(int(s_), trig, seed=int(s_) + k, hit_rate=0.01)}).encode()
+                msgs.append(b"POST /parse HTTP/1.1\r\nHost: 127.0.0.1\r\nContent-Type: application/json\r\n"
+                            b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+                lines_of.append(int(s_))
+        idx = np.array([sizes_set.index(int(s_)) * 4 + i % 4 for i, s_ in enumerate(sizes)], np.int32)
+        N.http_burst("127.0.0.1", srv.port, msgs, idx[:min(n, 2000)], 300.0)          # warm-up burst
+        lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0)
+    finally:
+        srv.stop()
+    ok = lat >= 0
+    lines = float(np.array(lines_of)[idx].sum())
+    print(json.dumps({"config": f"concurrent-http-{n}-connections-mixed-realistic", "device": dev,
+                      "engines": args.engines, "connections": n, "completed": int(done),
+                      "status_200": int((st == 200).sum()),
+                      "p50_ms": round(float(np.median(lat[ok])) * 1e3, 3),
+                      "p99_ms": round(float(np.percentile(lat[ok], 99)) * 1e3, 3),
+                      "max_ms": round(float(lat[ok].max()) * 1e3, 3),
+                      "requests_per_s": round(int(done) / wall, 1), "lines_per_s": round(lines / wall, 1),
+                      "wall_s": round(wall, 3), "bytes": int(sum(len(msgs[i]) for i in idx)),
+                      "transport": "native HTTP/1.1 front end, one keep-alive connection per request, 127.0.0.1"}))
+
+
 def mode_golden(args):
     sets, trig = make_library(20, seed=3, n_sets=2)
     logs = make_log(args.lines, trig, seed=4, hit_rate=0.01)
@@ -248,7 +300,7 @@ def mode_golden(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["rest", "rest_gpu", "single", "stream", "concurrent", "golden"])
+    ap.add_argument("mode", choices=["rest", "rest_gpu", "single", "stream", "concurrent", "concurrent_http", "golden"])
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lines", type=int, default=None)
     ap.add_argument("--patterns", type=int, default=4000)
@@ -258,9 +310,11 @@ def main():
     ap.add_argument("--timeline", action="store_true", help="concurrent: print the pipeline stage timeline")
     ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="rest: HTTP front end")
+    ap.add_argument("--library", default="realistic", choices=["realistic", "synthetic"],
+                    help="single / stream / concurrent: pattern library kind")
     args = ap.parse_args()
     defaults = {"rest": (10_000, 50), "rest_gpu": (10_000, 100), "single": (1_000_000, None), "stream": (1_000_000_000, None),
-                "concurrent": (None, 10_000), "golden": (10_000, None)}
+                "concurrent": (None, 10_000), "concurrent_http": (None, 10_000), "golden": (10_000, None)}
     dl, dr = defaults[args.mode]
     args.lines = args.lines or dl
     args.requests = args.requests or dr

@@ -14,6 +14,7 @@
 
 #include "io/docs.h"
 #include "io/json_in.h"
+#include "io/loadgen.h"
 #include "io/http_server.h"
 #include "io/json_emit.h"
 #include "kernels/lp_api.h"
@@ -658,6 +659,23 @@ PYBIND11_MODULE(_lpnative, m) {
     if (e == hipErrorPeerAccessAlreadyEnabled) { (void)hipGetLastError(); return true; }
     return e == hipSuccess;
   });
+
+  // ---- native load generator (csrc/io/loadgen.cpp): config 5 over real connections
+  m.def("http_burst", [](const std::string& host, int port, py::list msgs, py::array_t<int32_t> idx, double timeout_s) {
+    std::vector<std::string> M;
+    for (auto h : msgs) M.push_back(h.cast<std::string>());
+    std::vector<int32_t> I(idx.data(), idx.data() + idx.size());
+    LoadResult R;
+    {
+      py::gil_scoped_release nogil;
+      R = http_burst(host, port, M, I, timeout_s);
+    }
+    py::array_t<double> lat(R.latency.size());
+    std::memcpy(lat.mutable_data(), R.latency.data(), R.latency.size() * sizeof(double));
+    py::array_t<int32_t> st(R.status.size());
+    std::memcpy(st.mutable_data(), R.status.data(), R.status.size() * sizeof(int32_t));
+    return py::make_tuple(lat, st, R.t_end - R.t_start, R.completed);
+  }, py::arg("host"), py::arg("port"), py::arg("msgs"), py::arg("idx"), py::arg("timeout_s") = 120.0);
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
   py::class_<RawLogs>(m, "RawLogs")

@@ -37,6 +37,7 @@ SOURCES = [
     ("io/docs.cpp", "cpp"),
     ("io/json_in.cpp", "cpp"),
     ("io/http_server.cpp", "cpp"),
+    ("io/loadgen.cpp", "cpp"),
     ("runtime/request.cpp", "cpp"),
     ("kernels/prefilter_cpu.cpp", "cpp"),
     ("bind.cpp", "cpp"),

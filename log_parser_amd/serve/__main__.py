@@ -30,10 +30,24 @@ def bind_numa(cfg: Config) -> None:
         logging.getLogger("log_parser_amd.server").warning("NUMA binding skipped: %s", e)
 
 
+def raise_fd_limit() -> int:
+    """Open-file soft limit up to the hard limit: every keep-alive connection is a descriptor, and
+    BASELINE config 5 holds 10k of them at once."""
+    try:
+        import resource
+        soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+        if hard == resource.RLIM_INFINITY or hard > soft:
+            resource.setrlimit(resource.RLIMIT_NOFILE, (hard if hard != resource.RLIM_INFINITY else 1 << 20, hard))
+        return resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+    except (ImportError, ValueError, OSError):
+        return -1
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s [%(name)s] %(message)s")
     cfg = Config.load(overrides=parse_cli_overrides(argv))
+    raise_fd_limit()
     bind_numa(cfg)
     if str(cfg["server.http"]) == "uvicorn":
         import uvicorn

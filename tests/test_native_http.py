@@ -239,3 +239,19 @@ def test_raw_logs_unescaped_in_the_stage(server):
         assert m[0]["summary"] == a[0]["summary"] and m[1]["metadata"]["totalLines"] == a[1]["metadata"]["totalLines"]
     finally:
         hs.stop()
+
+
+def test_load_generator_burst_over_many_connections(server):
+    """The native load generator (config 5 over HTTP): 256 keep-alive connections established
+    first, one request each fired together; every response is a complete 200 AnalysisResult."""
+    import numpy as np
+    from log_parser_amd.native import N
+    fe, sets, trig = server
+    msgs = []
+    for k, n in enumerate((5, 40, 300)):
+        body = json.dumps({"pod": {"metadata": {"name": f"p{k}"}}, "logs": make_log(n, trig, seed=90 + k)}).encode()
+        msgs.append(b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: "
+                    + str(len(body)).encode() + b"\r\n\r\n" + body)
+    idx = np.arange(256, dtype=np.int32) % 3
+    lat, st, wall, done = N.http_burst("127.0.0.1", fe.port, msgs, idx, 120.0)
+    assert done == 256 and (st == 200).all() and (lat > 0).all() and wall >= lat.max() * 0.5

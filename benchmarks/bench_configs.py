@@ -177,19 +177,60 @@ def mode_stream(args):
     lines_per_block = block.count(b"\n")
     total = len(block) * max(1, args.lines // lines_per_block)
     src = RepeatBuffer(block, total)
-    sa = StreamAnalyzer(eng, chunk_bytes=args.chunk_mb << 20, topk=100, keep_events=False)
+    sa = StreamAnalyzer(eng, chunk_bytes=(args.chunk_mb << 20) or None, topk=100, keep_events=False)
     # untimed warm-up stream (3 chunks): pinned pool, kernels, allocator; then a fresh frequency state
-    sa.run(RepeatBuffer(block, min(total, 3 * (args.chunk_mb << 20))))
+    sa.run(RepeatBuffer(block, min(total, 3 * sa.chunk_bytes)))
     eng.freq.reset_all()
     _sync(dev)
     t0 = time.perf_counter()
     res = sa.run(src)
     _sync(dev)
     dt = time.perf_counter() - t0
+    import hashlib
+    digest = hashlib.sha256(np.concatenate([res.topk_score.view(np.int64), res.topk_line,
+                                            res.topk_pat]).tobytes()).hexdigest()[:16]
     print(json.dumps({"config": f"stream-{res.total_lines}-lines-{args.patterns}-patterns", "device": str(dev),
                       "seconds": round(dt, 3), "lines_per_s": round(res.total_lines / dt, 1),
                       "bytes": res.bytes, "GB_per_s": round(res.bytes / dt / 1e9, 3), "chunks": res.chunks,
-                      "events": res.n_events, "summary": res.summary}))
+                      "chunk_bytes": sa.chunk_bytes, "events": res.n_events, "summary": res.summary,
+                      "topk_digest": digest}))
+
+
+def mode_resident(args):
+    """A >= 50 GB log kept resident in HBM (parallel/stream.ResidentLog) and analysed twice with two
+    different 1k-pattern libraries: the load crosses PCIe once, each re-analysis reads HBM only."""
+    from log_parser_amd.parallel.stream import RepeatBuffer, ResidentLog, StreamAnalyzer
+    from log_parser_amd.utils.synth import realistic_library
+    dev = _dev(args)
+    eng, _, trig = _engine(1000, dev, library=args.library)
+    sets2, _ = realistic_library(1000, seed=99)
+    eng2 = Engine(CompiledLibrary(sets2, ScoringParams()), eng.config, device=dev)
+    big = eng if eng.lib.halo >= eng2.lib.halo else eng2
+    block = make_log(200_000, trig, seed=6, hit_rate=0.004, aux_rate=0.01, stack_rate=0.01).encode()
+    total = (args.gb << 30) // len(block) * len(block)
+    src = RepeatBuffer(block, total)
+    chunk = (args.chunk_mb << 20) if args.chunk_mb else None
+    _sync(dev)
+    t0 = time.perf_counter()
+    res = ResidentLog.load(src, big, chunk_bytes=chunk)
+    _sync(dev)
+    load_s = time.perf_counter() - t0
+    out = {"config": f"resident-{total / (1 << 30):.1f}GiB-reanalysis", "device": str(dev), "bytes": total,
+           "chunks": len(res.chunks), "chunk_bytes": res.chunk_bytes, "load_s": round(load_s, 3),
+           "load_GB_per_s": round(total / load_s / 1e9, 2), "analyses": []}
+    for name, e in (("library-A", eng), ("library-B", eng2)):
+        sa = StreamAnalyzer(e, chunk_bytes=res.chunk_bytes, topk=100, keep_events=False)
+        sa.run(ResidentLog(res.chunks[:1], res.chunks[0][1], res.halo, res.chunk_bytes))    # warm (1 chunk)
+        e.freq.reset_all()
+        _sync(dev)
+        t1 = time.perf_counter()
+        r = sa.run(res)
+        _sync(dev)
+        dt = time.perf_counter() - t1
+        out["analyses"].append({"library": name, "seconds": round(dt, 3), "lines": r.total_lines,
+                                "lines_per_s": round(r.total_lines / dt, 1), "GB_per_s": round(total / dt / 1e9, 1),
+                                "events": r.n_events, "highest": r.summary["highestSeverity"]})
+    print(json.dumps(out))
 
 
 def mode_concurrent(args):
@@ -300,13 +341,15 @@ def mode_golden(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["rest", "rest_gpu", "single", "stream", "concurrent", "concurrent_http", "golden"])
+    ap.add_argument("mode", choices=["rest", "rest_gpu", "single", "stream", "concurrent", "concurrent_http", "resident",
+                                     "golden"])
+    ap.add_argument("--gb", type=int, default=50, help="resident: GiB of log kept in HBM")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--lines", type=int, default=None)
     ap.add_argument("--patterns", type=int, default=4000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--requests", type=int, default=None)
-    ap.add_argument("--chunk-mb", type=int, default=512)
+    ap.add_argument("--chunk-mb", type=int, default=0, help="stream / resident chunk MiB (0 = from free HBM)")
     ap.add_argument("--timeline", action="store_true", help="concurrent: print the pipeline stage timeline")
     ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="rest: HTTP front end")
@@ -314,7 +357,8 @@ def main():
                     help="single / stream / concurrent: pattern library kind")
     args = ap.parse_args()
     defaults = {"rest": (10_000, 50), "rest_gpu": (10_000, 100), "single": (1_000_000, None), "stream": (1_000_000_000, None),
-                "concurrent": (None, 10_000), "concurrent_http": (None, 10_000), "golden": (10_000, None)}
+                "concurrent": (None, 10_000), "concurrent_http": (None, 10_000), "resident": (None, None),
+                "golden": (10_000, None)}
     dl, dr = defaults[args.mode]
     args.lines = args.lines or dl
     args.requests = args.requests or dr

@@ -54,7 +54,8 @@ def cmd_analyze(args, cfg: Config) -> int:
         cfg = cfg.replace({"engine.device": args.device})
     lp = LogParser.from_directory(cfg["pattern.directory"], config=cfg)
     size = os.path.getsize(args.file)
-    stream = args.stream or size > int(cfg["engine.chunk-bytes"])
+    from .parallel.stream import auto_chunk_bytes
+    stream = args.stream or size > (int(cfg["engine.chunk-bytes"]) or auto_chunk_bytes(lp.engine.device))
     with open(args.file, "rb") as f:
         if not stream:
             data = f.read()

@@ -33,6 +33,21 @@ from ..engine import Engine, Segments
 from ..ops import kernels as K
 
 
+CHUNK_MIN, CHUNK_MAX = 256 << 20, 8 << 30
+
+
+def auto_chunk_bytes(device: torch.device) -> int:
+    """``engine.chunk-bytes = 0``: chunks sized from the GPU's free HBM -- 1/16 of it, within
+    [256 MiB, 8 GiB] (a chunk's device footprint is ~3x its bytes: text, line index, matcher
+    arenas, CSR, with the next chunk's copy in flight). On a 288 GB MI355X that is 8 GiB chunks:
+    fewer halos, launches and host hand-offs than the 256 MiB of round 2."""
+    if device.type != "cuda":
+        return CHUNK_MIN
+    free, _ = torch.cuda.mem_get_info(device)
+    c = max(CHUNK_MIN, min(CHUNK_MAX, free // 16))
+    return int(c) & ~((1 << 20) - 1)
+
+
 def _eff_end(src) -> int:
     """End of the content that survives Java's trailing-empty-line removal."""
     n = len(src)
@@ -124,11 +139,67 @@ class StreamResult:
     timings: dict = field(default_factory=dict)
 
 
+class ResidentLog:
+    """A log held in HBM for repeated analyses (e.g. re-analysis with a new pattern library): the
+    bytes cross PCIe once, as line-aligned chunks with their halos (the same chunk plan as the
+    stream), and ``StreamAnalyzer.run(resident)`` then reads them in place -- no host staging, no
+    H2D per analysis. Sized for 288 GB of HBM per MI355X: a multi-10-GB log fits with room for
+    the analysis workspaces."""
+
+    def __init__(self, chunks: list, nbytes: int, halo: int, chunk_bytes: int):
+        self.chunks = chunks            # [(device text (padded), n, lh, rh, end)]
+        self.nbytes = nbytes
+        self.halo = halo
+        self.chunk_bytes = chunk_bytes
+
+    @classmethod
+    def load(cls, src, engine: Engine, chunk_bytes: Optional[int] = None) -> "ResidentLog":
+        sa = StreamAnalyzer(engine, chunk_bytes=chunk_bytes)
+        dev = engine.device
+        q: "queue.Queue" = queue.Queue(maxsize=2)
+        free_q: Optional[queue.Queue] = None
+        if dev.type == "cuda":
+            free_q = queue.Queue()
+            for _ in range(sa.PINNED_BUFFERS):
+                free_q.put((None, None))
+        th = threading.Thread(target=sa._producer, args=(src, _eff_end(src), q, 0, free_q), daemon=True)
+        th.start()
+        chunks, total = [], 0
+        while True:
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            if item is None:
+                break
+            pinned, n, size, lh, rh, end = item
+            d = torch.empty(size, dtype=torch.uint8, device=dev)
+            d.copy_(pinned[:size], non_blocking=dev.type == "cuda")
+            ev = None
+            if dev.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record()
+            if free_q is not None:
+                free_q.put((pinned, ev))
+            chunks.append((d, n, lh, rh, end))
+            total += n
+        th.join()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        return cls(chunks, len(src), engine.lib.halo, sa.chunk_bytes)
+
+    @property
+    def device_bytes(self) -> int:
+        return sum(c[0].numel() for c in self.chunks)
+
+
 class StreamAnalyzer:
     def __init__(self, engine: Engine, chunk_bytes: Optional[int] = None, topk: int = 100,
                  keep_events: bool = True):
+        """``keep_events=False``: bounded memory for dense matches -- the summary histograms
+        accumulate per chunk and only events that can still reach the top-k are kept (exact, see
+        ``_prune``), instead of every event's seven factors until the end of the stream."""
         self.engine = engine
-        self.chunk_bytes = int(chunk_bytes or engine.config["engine.chunk-bytes"])
+        self.chunk_bytes = int(chunk_bytes or engine.config["engine.chunk-bytes"] or auto_chunk_bytes(engine.device))
         K._check_k(topk)
         self.topk = topk
         self.keep_events = keep_events
@@ -169,6 +240,35 @@ class StreamAnalyzer:
             pos = end
 
     PINNED_BUFFERS = 3          # one being filled, one in the H2D copy, one spare
+    PRUNE_AT = 1 << 20          # bounded mode: prune the kept events past this many
+
+    def _chrono_bounds(self):
+        """[min, max] of the chronological factor over any position (ScoringService.java:123-151:
+        piecewise linear through m at 0, 1.5 at e, 1.0 at t, -> 0.5 at the end)."""
+        p = self.engine.params
+        return 0.5, max(float(p.max_early_bonus), 1.5, 1.0)
+
+    def _prune(self, ev_gl, ev_pat, ev_fac, cmin: float, cmax: float):
+        """Keep only events that can still be in the final top-k. The final score is the
+        left-to-right product with the chronological factor of the (not yet known) line count;
+        fp64 multiplication is monotone, so evaluating the same product with the factor's min /
+        max gives exact lower / upper bounds. Events whose upper bound is below the k-th largest
+        lower bound can never enter the top-k (ties keep: the bound test is strict)."""
+        gl, pat, fac = torch.cat(ev_gl), torch.cat(ev_pat), torch.cat(ev_fac)
+        k = max(1, self.topk)
+        if gl.numel() <= k:
+            return [gl], [pat], [fac]
+
+        def prod(c):
+            v = fac[:, 0] * fac[:, 1]
+            v = v * c
+            for j in (3, 4, 5):
+                v = v * fac[:, j]
+            return v * (1.0 - fac[:, 6])
+        lb, ub = prod(cmin), prod(cmax)
+        thr = torch.topk(lb, k).values[-1]
+        keep = ub >= thr
+        return [gl[keep]], [pat[keep]], [fac[keep]]
     RAMP = 3                    # chunk-size ramp-up steps (halving)
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None):
@@ -222,13 +322,21 @@ class StreamAnalyzer:
         eng = self.engine
         lib = eng.lib
         dev = eng.device
-        eff = _eff_end(src)
-        if eff == 0 and len(src) > 0 and src.find(b"\n", 0) >= 0:
+        eff = src.nbytes if isinstance(src, ResidentLog) else _eff_end(src)
+        if not isinstance(src, ResidentLog) and eff == 0 and len(src) > 0 and src.find(b"\n", 0) >= 0:
             empty = {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
             z = np.zeros(0)
             return StreamResult(0, 0, empty, z, z.astype(np.int64), z.astype(np.int64), 0, len(src), 0.0)
         nkeys = len(lib.freq_ids)
+        resident = isinstance(src, ResidentLog)
+        if resident and src.halo < lib.halo:
+            raise ValueError(f"resident log staged with {src.halo} halo lines, the library needs {lib.halo}")
         start = 0
+        P, S = len(lib.patterns), len(lib.sev_names)
+        hist = torch.zeros(P + S + 1, dtype=torch.int64, device=dev)      # bounded mode: running histograms
+        n_events = 0
+        first_pat = None
+        cmin, cmax = self._chrono_bounds()
         if resume:
             with np.load(resume, allow_pickle=False) as ck:
                 start = int(ck["pos"])
@@ -251,13 +359,19 @@ class StreamAnalyzer:
             nbytes_total = 0
         q: "queue.Queue" = queue.Queue(maxsize=2)
         free_q: Optional[queue.Queue] = None
-        if dev.type == "cuda":
+        if dev.type == "cuda" and not resident:
             free_q = queue.Queue()
             for _ in range(self.PINNED_BUFFERS):
                 free_q.put((None, None))
-        th = threading.Thread(target=self._producer, args=(src, eff, q, start, free_q), daemon=True)
-        th.start()
-        copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        th = None
+        if resident:
+            if resume:
+                raise ValueError("resume applies to host streams, not resident logs")
+            res_iter = iter(src.chunks)
+        else:
+            th = threading.Thread(target=self._producer, args=(src, eff, q, start, free_q), daemon=True)
+            th.start()
+        copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" and not resident else None
 
         def save(pos_next):
             def cat(xs, dt, shape):
@@ -272,6 +386,9 @@ class StreamAnalyzer:
             os.replace(tmp, checkpoint)
 
         def fetch():
+            if resident:                        # already in HBM: nothing to stage or copy
+                c = next(res_iter, None)
+                return None if c is None else (c[0], c[1], c[2], c[3], None, c[4])
             item = q.get()
             if isinstance(item, BaseException):
                 raise item
@@ -308,9 +425,23 @@ class StreamAnalyzer:
                 seq_state = torch.where(k < 0, torch.ones_like(seq_state), prev)
             run_counts = run_counts + prep.freq_counts[:max(nkeys, 1)]
             if res.ev_line.numel():
-                ev_gl.append(res.ev_line.to(torch.int64) - own_lo + line_base)
-                ev_pat.append(res.ev_pat)
-                ev_fac.append(res.factors)
+                gl_c = res.ev_line.to(torch.int64) - own_lo + line_base
+                if self.keep_events:
+                    ev_gl.append(gl_c)
+                    ev_pat.append(res.ev_pat)
+                    ev_fac.append(res.factors)
+                else:
+                    # bounded: histograms now, and only events that may still make the top-k
+                    K.summarize(res.score, res.ev_pat, res.ev_line, 1, eng.tabs["sev_index"], P, S, ws=eng.ws,
+                                hist_out=hist)
+                    n_events += int(res.ev_line.numel())
+                    if first_pat is None:
+                        first_pat = int(res.ev_pat[0].item())
+                    ev_gl.append(gl_c)
+                    ev_pat.append(res.ev_pat)
+                    ev_fac.append(res.factors)
+                    if sum(x.numel() for x in ev_gl) > self.PRUNE_AT:
+                        ev_gl, ev_pat, ev_fac = self._prune(ev_gl, ev_pat, ev_fac, cmin, cmax)
             if on_chunk is not None:
                 on_chunk(chunks, line_base, own_hi - own_lo)
             line_base += own_hi - own_lo
@@ -320,7 +451,8 @@ class StreamAnalyzer:
                 save(chunk_end)
             if fail_after_chunks is not None and chunks >= fail_after_chunks:
                 raise RuntimeError("injected stream failure after chunk %d" % chunks)
-        th.join()
+        if th is not None:
+            th.join()
         N = max(line_base, 1)
         if ev_gl:
             gl = torch.cat(ev_gl)
@@ -334,13 +466,17 @@ class StreamAnalyzer:
             score = torch.zeros(0, dtype=torch.float64, device=dev)
         eng.commit_frequency(run_counts[:nkeys])
         # summary + top-k in one kernel chain (summarize.hip): severity histogram, k best rows
-        P, S = len(lib.patterns), len(lib.sev_names)
         rows, _, sc, _ = K.summarize(score, pat, gl, max(1, self.topk), eng.tabs["sev_index"], P, S, ws=eng.ws)
-        k = min(self.topk, score.numel())
+        if self.keep_events:
+            n_events = int(score.numel())
+            first = int(pat[0].item()) if pat.numel() else None
+        else:
+            sc = hist[P:P + S]
+            first = first_pat
+        k = min(self.topk, n_events)
         top = rows[:k].cpu().numpy()
-        first = int(pat[0].item()) if pat.numel() else None
         summary = eng.summary_from_severity(sc.cpu().numpy(), first)
-        out = StreamResult(line_base, int(score.numel()), summary, top[:, 0].copy(), top[:, 1].astype(np.int64),
+        out = StreamResult(line_base, n_events, summary, top[:, 0].copy(), top[:, 1].astype(np.int64),
                            top[:, 2].astype(np.int64), chunks, nbytes_total, time.perf_counter() - t0)
         if self.keep_events:
             out.events = (gl.cpu().numpy(), pat.cpu().numpy(), score.cpu().numpy())

@@ -56,3 +56,58 @@ def test_repeat_buffer():
     for st in range(0, 100, 7):
         assert rb.find(b"\n", st) == full.find(b"\n", st)
         assert rb.rfind(b"\n", 0, st) == full.rfind(b"\n", 0, st)
+
+
+def _dense():
+    sets, trig = make_library(40, seed=43, sequence_rate=0.8)
+    lib = CompiledLibrary(sets, ScoringParams())
+    data = make_log(4000, trig, seed=44, hit_rate=0.3).encode()      # dense matches
+    return lib, data
+
+
+def test_bounded_topk_mode_equals_full(monkeypatch):
+    """keep_events=False keeps only events that can still reach the top-k (bounds from the
+    chronological factor's min / max): same top-k, summary and event count as keeping all."""
+    lib, data = _dense()
+    full = StreamAnalyzer(_eng(lib), chunk_bytes=8192, topk=9).run(data)
+    monkeypatch.setattr(StreamAnalyzer, "PRUNE_AT", 64)           # prune after (almost) every chunk
+    sa = StreamAnalyzer(_eng(lib), chunk_bytes=8192, topk=9, keep_events=False)
+    kept = []
+    orig = StreamAnalyzer._prune
+
+    def spy(self, *a):
+        out = orig(self, *a)
+        kept.append(out[0][0].numel())
+        return out
+    monkeypatch.setattr(StreamAnalyzer, "_prune", spy)
+    b = sa.run(data)
+    assert kept and max(kept) < full.n_events // 2               # memory stays bounded
+    assert b.n_events == full.n_events and b.summary == full.summary and b.events is None
+    np.testing.assert_array_equal(b.topk_line, full.topk_line)
+    np.testing.assert_array_equal(b.topk_pat, full.topk_pat)
+    np.testing.assert_allclose(b.topk_score, full.topk_score, rtol=1e-15, atol=0)
+
+
+def test_resident_log_reanalysis_equals_stream():
+    """A log loaded into (device) memory once is re-analysed by two libraries without restaging,
+    each equal to a host stream of the same bytes."""
+    from log_parser_amd.parallel.stream import ResidentLog
+    lib, data = _dense()
+    sets2, _ = make_library(30, seed=45)
+    lib2 = CompiledLibrary(sets2, ScoringParams())
+    big = lib if lib.halo >= lib2.halo else lib2
+    res = ResidentLog.load(data, _eng(big), chunk_bytes=8192)
+    assert len(res.chunks) > 3 and res.device_bytes >= len(data)
+    for L in (lib, lib2):
+        a = StreamAnalyzer(_eng(L), chunk_bytes=8192, topk=5).run(res)
+        b = StreamAnalyzer(_eng(L), chunk_bytes=8192, topk=5).run(data)
+        assert a.total_lines == b.total_lines and a.summary == b.summary
+        for x, y in zip(a.events, b.events):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_auto_chunk_bytes_cpu():
+    from log_parser_amd.parallel.stream import CHUNK_MIN, auto_chunk_bytes
+    assert auto_chunk_bytes(torch.device("cpu")) == CHUNK_MIN
+    sets, _ = make_library(5, seed=1)
+    assert StreamAnalyzer(_eng(CompiledLibrary(sets, ScoringParams()))).chunk_bytes == CHUNK_MIN

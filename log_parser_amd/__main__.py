@@ -15,8 +15,6 @@ from __future__ import annotations
 import argparse
 import json
 import logging
-import mmap
-import os
 import sys
 from typing import List, Optional
 
@@ -29,21 +27,12 @@ def _split(argv: List[str]):
 
 
 def cmd_validate(args, cfg: Config) -> int:
-    from .models.compiled import KIND_DFA, KIND_FALLBACK, KIND_INVALID, KIND_NFA, CompiledLibrary
-    from .models.library import load_pattern_directory
+    from .api import LogParser
     d = args.directory or cfg["pattern.directory"]
-    sets = load_pattern_directory(d)
-    lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]),
-                                  nfa_engine=str(cfg["engine.nfa-engine"]))
-    names = {KIND_DFA: "dfa", KIND_NFA: "nfa", KIND_FALLBACK: "host-fallback", KIND_INVALID: "invalid"}
-    problems = []
-    for r in lib.regexes:
-        if r.kind in (KIND_INVALID, KIND_FALLBACK) or (r.kind == KIND_NFA and "nfa" not in args.allow):
-            problems.append({"regex": r.pattern, "kind": names.get(r.kind, str(r.kind)), "error": r.error,
-                             "roles": sorted(r.roles)})
-    out = {"directory": d, "library": lib.summary(), "problems": problems}
-    print(json.dumps(out, indent=2))
-    return 1 if any(p["kind"] == "invalid" for p in problems) else 0
+    rep = LogParser.from_directory(d, config=cfg.replace({"engine.device": "cpu"})).validate(
+        allow=tuple(x for x in args.allow.split(",") if x))
+    print(json.dumps({"directory": d, **rep}, indent=2))
+    return 1 if any(p["kind"] == "invalid" for p in rep["problems"]) else 0
 
 
 def cmd_analyze(args, cfg: Config) -> int:
@@ -53,22 +42,16 @@ def cmd_analyze(args, cfg: Config) -> int:
     if args.device:
         cfg = cfg.replace({"engine.device": args.device})
     lp = LogParser.from_directory(cfg["pattern.directory"], config=cfg)
-    size = os.path.getsize(args.file)
-    from .parallel.stream import auto_chunk_bytes
-    stream = args.stream or size > (int(cfg["engine.chunk-bytes"]) or auto_chunk_bytes(lp.engine.device))
-    with open(args.file, "rb") as f:
-        if not stream:
-            data = f.read()
-            sys.stdout.buffer.write(lp.parse_json(data.decode("utf-8", errors="surrogateescape")))
-            sys.stdout.write("\n")
-            return 0
-        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) if size else b""
-        res = lp.parse_stream(mm, topk=args.topk)
-        pats = lp.library.patterns
-        top = [{"lineNumber": int(l) + 1, "score": float(s), "patternId": pats[int(p)].id}
-               for s, l, p in zip(res.topk_score, res.topk_line, res.topk_pat)]
-        print(json.dumps({"totalLines": res.total_lines, "bytes": res.bytes, "chunks": res.chunks,
-                          "seconds": round(res.seconds, 3), "summary": res.summary, "topEvents": top}))
+    out = lp.parse_file(args.file, stream=True if args.stream else None, topk=args.topk, raw=True)
+    if isinstance(out, (bytes, bytearray)):
+        sys.stdout.buffer.write(out)
+        sys.stdout.write("\n")
+        return 0
+    pats = lp.library.patterns
+    top = [{"lineNumber": int(l) + 1, "score": float(s), "patternId": pats[int(p)].id}
+           for s, l, p in zip(out.topk_score, out.topk_line, out.topk_pat)]
+    print(json.dumps({"totalLines": out.total_lines, "bytes": out.bytes, "chunks": out.chunks,
+                      "seconds": round(out.seconds, 3), "summary": out.summary, "topEvents": top}))
     return 0
 
 

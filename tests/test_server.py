@@ -160,3 +160,42 @@ def test_parse_special_characters_roundtrip(client, lib_dir):
     assert len(res["events"]) == len(g["events"]) > 0
     for a, b in zip(res["events"], g["events"]):
         assert a["context"] == b["context"]
+
+
+def test_embedding_api_submit_file_resident_and_frequency(tmp_path):
+    """api.LogParser beyond a facade: concurrent submit through the batcher (results equal the
+    sequential golden model in submission order), parse_file (doc and stream), a resident log
+    re-analysed, the compile report, and the FrequencyTrackingService surface."""
+    import concurrent.futures as cf
+    from log_parser_amd import LogParser, golden
+    from log_parser_amd.utils.synth import make_library, make_log
+    p = ScoringParams(freq_threshold=1.0)
+    sets, trig = make_library(20, seed=77)
+    cfg = Config.load(overrides={"engine.device": "cpu", "scoring.frequency.threshold": "1.0"})
+    lp = LogParser(sets, config=cfg)
+    reqs = [make_log(150, trig, seed=700 + i, hit_rate=0.1) for i in range(12)]
+    futs = [lp.submit(r) for r in reqs]                       # submission order = frequency order
+    outs = [json.loads(f.result(timeout=120)) for f in futs]
+    tr = golden.FrequencyTracker(p)
+    for r, o in zip(reqs, outs):
+        g = golden.analyze(r, sets, p, tr)
+        assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
+    stats = lp.frequency_statistics()
+    assert stats and lp.pattern_frequency(next(iter(stats)))["currentCount"] == stats[next(iter(stats))]
+    lp.reset_pattern_frequency(next(iter(stats)))
+    assert lp.pattern_frequency(next(iter(stats)))["currentCount"] == 0
+    lp.reset_all_frequencies()
+    assert lp.frequency_statistics() == {}
+    f = tmp_path / "x.log"
+    f.write_text(make_log(3000, trig, seed=701, hit_rate=0.05))
+    doc = lp.parse_file(str(f), stream=False)
+    lp.reset_all_frequencies()
+    st = lp.parse_file(str(f), stream=True, topk=5)
+    assert st.total_lines == doc["metadata"]["totalLines"] and st.summary == doc["summary"]
+    res = lp.load_resident(f.read_bytes(), chunk_bytes=16384)
+    lp.reset_all_frequencies()
+    again = lp.analyze_resident(res, topk=5)
+    assert again.summary == st.summary and list(again.topk_line) == list(st.topk_line)
+    rep = lp.validate()
+    assert rep["library"]["patterns"] == 20 and rep["problems"] == []
+    lp.close()

@@ -358,7 +358,8 @@ class DeviceFrequencyState:
             log.warning("device frequency window unreadable; the CPU fallback starts from an empty window")
             return fs
         for k in np.flatnonzero(seen[:len(self.ids)]):
-            fs._seen[fs._slot_of(self.ids[k])] = True
+            slot = fs._slot_of(self.ids[k])       # (may grow fs._seen: index it afterwards)
+            fs._seen[slot] = True
         for a, k, c in zip(t.tolist(), key.tolist(), cnt.tolist()):
             if c > 0:
                 s = fs._slot_of(self.ids[k])

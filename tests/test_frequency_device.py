@@ -74,3 +74,19 @@ def test_gpu_engine_defaults_to_device_state(monkeypatch):
     e = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
     assert isinstance(e.freq, FrequencyState)                 # CPU engine: host state
     assert Config.load()["engine.frequency.device-resident"] is True
+
+
+def test_to_host_state_copies_the_window():
+    """The CPU fallback's host copy of a device window (here the CPU twin of the device state)."""
+    from log_parser_amd.frequency import DeviceFrequencyState, MirroredFrequencyState
+    import numpy as np
+    ids = [f"p{i}" for i in range(300)]
+    d = DeviceFrequencyState(ids, 1, "cpu", clock=lambda: 1000.0)
+    c = np.zeros(300, np.int64)
+    c[[0, 7, 299]] = [3, 1, 5]
+    d.record_counts(ids, c)
+    h = d.to_host_state()
+    assert h.statistics() == d.statistics() == {"p0": 3, "p7": 1, "p299": 5}
+    m = MirroredFrequencyState(d)
+    m.record_counts(ids, c)
+    assert m.statistics() == d.statistics() == {"p0": 6, "p7": 2, "p299": 10}

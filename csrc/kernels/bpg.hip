@@ -46,6 +46,35 @@ __global__ __launch_bounds__(256) void k_bpg_cand(int64_t* __restrict__ cand, in
   if (!bpg_find_dev<W>(prog, text + ls[x], ll[x])) cand[i] = -1;
 }
 
+// small path, one launch for every width (a request's few candidates: the launch, not the
+// registers of the widest walk, is what costs here)
+__global__ __launch_bounds__(256) void k_bpg_cand_all(int64_t* __restrict__ cand, int64_t cap,
+                                                      const unsigned long long* __restrict__ dcount,
+                                                      const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
+                                                      const int32_t* __restrict__ ll, DfaPool P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = dcount ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
+  if (i >= n) return;
+  const int64_t k = cand[i];
+  if (k < 0) return;
+  const int r = (int)(k >> 32);
+  if (!is_bpg(P, r)) return;
+  const uint64_t* prog = P.bpg + P.meta[4 * r];
+  const int64_t x = k & 0xFFFFFFFFll;
+  const uint8_t* s = text + ls[x];
+  const int len = ll[x];
+  bool m;
+  switch ((int)(prog[0] & 0xFF)) {
+    case 1: m = bpg_find_dev<1>(prog, s, len); break;
+    case 2: m = bpg_find_dev<2>(prog, s, len); break;
+    case 3: m = bpg_find_dev<3>(prog, s, len); break;
+    case 4: m = bpg_find_dev<4>(prog, s, len); break;
+    case 6: m = bpg_find_dev<6>(prog, s, len); break;
+    default: m = bpg_find_dev<8>(prog, s, len); break;
+  }
+  if (!m) cand[i] = -1;
+}
+
 // bulk path: sorted packed keys ((regex << lbits | line) << 1 | pre-verified); the first key of
 // every run whose regex is a width-W program and that no engine pre-verified gets its flag here
 // (k_dedupe_verify left it 0)
@@ -120,6 +149,11 @@ void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, 
                   const int32_t* ll, const DfaPool& P, uint64_t stream) {
   if (!P.bpg_widths || cap <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (cap <= 4096) {                // a request: one launch for every width
+    hipLaunchKernelGGL(k_bpg_cand_all, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text, ls, ll, P);
+    check_launch("k_bpg_cand_all");
+    return;
+  }
   for_widths(P.bpg_widths, [&](auto w) {
     hipLaunchKernelGGL(k_bpg_cand<decltype(w)::value>, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text,
                        ls, ll, P);

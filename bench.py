@@ -126,7 +126,9 @@ def run(args, sets, trig, rank, world, local_rank, server):
         device = torch.device("cpu")
     backend = args.backend
     if backend == "auto":
-        backend = "nccl" if use_cuda else ("gloo" if world > 1 else "none")
+        # world 1: no process group until the RCCL group stops serialising the ingest copy with the
+        # compute (docs/PERFORMANCE.md, profiles/r3_*: 23.4 -> 27.5 ms/step with a world-1 group)
+        backend = ("nccl" if use_cuda else "gloo") if world > 1 else "none"
     if backend == "none" and world > 1:
         backend = "nccl" if use_cuda else "gloo"
     if backend != "none":
@@ -134,7 +136,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
         if "MASTER_PORT" not in os.environ:
             from log_parser_amd.utils.launch import free_port
             os.environ["MASTER_PORT"] = str(free_port())
-        kw = {"device_id": device} if backend == "nccl" else {}
+        kw = {"device_id": device} if backend == "nccl" and os.environ.get("LP_BENCH_LAZY_NCCL", "0") != "1" else {}
         from log_parser_amd.utils.launch import stdout_to_stderr
         with stdout_to_stderr():            # RCCL prints its version banner on stdout: keep ONE JSON line
             dist.init_process_group(backend, rank=rank, world_size=world, **kw)

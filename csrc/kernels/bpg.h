@@ -181,63 +181,80 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
       ++blk;
       const int j0 = t0 < 0 ? -t0 : 0;
       const int j1 = n - t0 < 16 ? n - t0 : 16;
-      for (int j = j0; j < j1; ++j) {
-        const int t = t0 + j;
-        const uint32_t wv = (j < 4) ? cur.x : (j < 8) ? cur.y : (j < 12) ? cur.z : cur.w;
-        const int c = (int)((wv >> (8 * (j & 3))) & 0xFFu);
-        const int nk = byte_kind(c);
-        if (t == ft) {
-          LP_BPG_ACCEPT(prevk * 5 + 1, hit);
+      // PF bytes at a time: their class rows depend on the text only, not on the state, so all
+      // PF rows are loaded before the first state update (one load latency per PF bytes instead
+      // of two dependent loads -- byte map, then row -- on every byte's chain)
+      constexpr int PF = W <= 4 ? 4 : 2;     // rows in flight (registers: PF x W words)
+      for (int jb = j0; jb < j1; jb += PF) {
+        uint64_t Cr[PF][W];
+        int cb[PF];
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          const int j = jb + q < 15 ? jb + q : 15;
+          const uint32_t wv = (j < 4) ? cur.x : (j < 8) ? cur.y : (j < 12) ? cur.z : cur.w;
+          cb[q] = (int)((wv >> (8 * (j & 3))) & 0xFFu);
+          const uint64_t* row = cls + (size_t)bm[cb[q]] * W;
+#pragma unroll
+          for (int w = 0; w < W; ++w) Cr[q][w] = row[w];
+        }
+#pragma unroll
+        for (int q = 0; q < PF; ++q) {
+          if (jb + q >= j1) break;
+          const int t = t0 + jb + q;
+          const int c = cb[q];
+          const int nk = byte_kind(c);
+          if (t == ft) {
+            LP_BPG_ACCEPT(prevk * 5 + 1, hit);
+            if (hit) return true;
+          }
+          LP_BPG_ACCEPT(prevk * 5 + nk, hit);
           if (hit) return true;
-        }
-        LP_BPG_ACCEPT(prevk * 5 + nk, hit);
-        if (hit) return true;
-        const int ctx = prevk * 5 + nk;
-        uint64_t F[W];
-        uint64_t carry = 0, borrow = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          const uint64_t x = S[w] & shm[w];
-          F[w] = (x << 1) | carry | (S[w] & selfm[w]);
-          carry = x >> 63;
-          const uint64_t df = (S[w] & src[w]) | hi[w];
-          const uint64_t u = df - lo[w];
-          const uint64_t b1 = df < lo[w] ? 1ull : 0ull;
-          const uint64_t d = u - borrow;
-          const uint64_t b2 = u < borrow ? 1ull : 0ull;
-          borrow = b1 | b2;
-          F[w] |= R[w] & ~(d ^ df);
-        }
-        for (int e = 0; e < E; ++e) {
-          const uint64_t* x = exc + (size_t)e * (W + 1);
-          const uint64_t h = x[0];
-          const int p = (int)(h & 0xFFFF);
-          uint64_t sw = 0;
-#pragma unroll
-          for (int w = 0; w < W; ++w) sw = (w == (p >> 6)) ? S[w] : sw;
-          if (((sw >> (p & 63)) & 1ull) && (((uint32_t)(h >> 16) >> ctx) & 1u)) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
-          }
-        }
-        const uint64_t* C = cls + (size_t)bm[c] * W;
-        uint64_t alive = 0;
-        if (uniform) {
+          const int ctx = prevk * 5 + nk;
+          uint64_t F[W];
+          uint64_t carry = 0, borrow = 0;
 #pragma unroll
           for (int w = 0; w < W; ++w) {
-            S[w] = (F[w] | f0[w]) & C[w];
-            alive |= S[w];
+            const uint64_t x = S[w] & shm[w];
+            F[w] = (x << 1) | carry | (S[w] & selfm[w]);
+            carry = x >> 63;
+            const uint64_t df = (S[w] & src[w]) | hi[w];
+            const uint64_t u = df - lo[w];
+            const uint64_t b1 = df < lo[w] ? 1ull : 0ull;
+            const uint64_t d = u - borrow;
+            const uint64_t b2 = u < borrow ? 1ull : 0ull;
+            borrow = b1 | b2;
+            F[w] |= R[w] & ~(d ^ df);
           }
-        } else {
-          const uint64_t* Fi = first + ctx * W;
+          for (int e = 0; e < E; ++e) {
+            const uint64_t* x = exc + (size_t)e * (W + 1);
+            const uint64_t h = x[0];
+            const int p = (int)(h & 0xFFFF);
+            uint64_t sw = 0;
 #pragma unroll
-          for (int w = 0; w < W; ++w) {
-            S[w] = (F[w] | Fi[w]) & C[w];
-            alive |= S[w];
+            for (int w = 0; w < W; ++w) sw = (w == (p >> 6)) ? S[w] : sw;
+            if (((sw >> (p & 63)) & 1ull) && (((uint32_t)(h >> 16) >> ctx) & 1u)) {
+#pragma unroll
+              for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
+            }
           }
+          uint64_t alive = 0;
+          if (uniform) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              S[w] = (F[w] | f0[w]) & Cr[q][w];
+              alive |= S[w];
+            }
+          } else {
+            const uint64_t* Fi = first + ctx * W;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              S[w] = (F[w] | Fi[w]) & Cr[q][w];
+              alive |= S[w];
+            }
+          }
+          if (anchored && !alive) return false;
+          prevk = nk == 2 ? 1 : 2;
         }
-        if (anchored && !alive) return false;
-        prevk = nk == 2 ? 1 : 2;
       }
       cur = nxt;
     }

@@ -78,28 +78,57 @@ __global__ __launch_bounds__(256) void k_bpg_cand_all(int64_t* __restrict__ cand
 // bulk path: sorted packed keys ((regex << lbits | line) << 1 | pre-verified); the first key of
 // every run whose regex is a width-W program and that no engine pre-verified gets its flag here
 // (k_dedupe_verify left it 0)
+constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global memory)
+
+__device__ __forceinline__ int prog_words(const uint64_t* prog, int W) {   // header, masks, tables
+  const uint64_t h = prog[0];
+  return 1 + 36 * W + 32 + (int)((h >> 20) & 0x3FF) * W + (int)((h >> 8) & 0xFFF) * (W + 1);
+}
+
 template <int W>
 __global__ __launch_bounds__(256) void k_bpg_dedupe(const uint64_t* __restrict__ keys, int64_t n, int lbits,
                                                     const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
                                                     const int32_t* __restrict__ ll, DfaPool P,
                                                     uint8_t* __restrict__ flag) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // keys are sorted by regex: a block's keys nearly always share one program, staged in LDS
+  __shared__ uint64_t sp[kLdsProgWords];
+  __shared__ int s_r;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  if (threadIdx.x == 0) {
+    int r0 = -1;
+    if (i0 < n && keys[i0] != kPadKey) {
+      const int r = (int)((keys[i0] >> 1) >> lbits);
+      const uint64_t* p = prog_of(P, r, W);
+      if (p && prog_words(p, W) <= kLdsProgWords) r0 = r;
+    }
+    s_r = r0;
+  }
+  __syncthreads();
+  const int r0 = s_r;
+  if (r0 >= 0) {
+    const uint64_t* p = P.bpg + P.meta[4 * r0];
+    const int nw = prog_words(p, W);
+    for (int j = threadIdx.x; j < nw; j += blockDim.x) sp[j] = p[j];
+  }
+  __syncthreads();
+  const int64_t i = i0 + threadIdx.x;
   if (i >= n) return;
   const uint64_t key = keys[i];
   if (key == kPadKey) return;
   const uint64_t k = key >> 1;
   if (i > 0 && (keys[i - 1] >> 1) == k) return;
-  const uint64_t* prog = prog_of(P, (int)(k >> lbits), W);
+  const int r = (int)(k >> lbits);
+  const uint64_t* prog = prog_of(P, r, W);
   if (!prog) return;
   for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j)
     if (keys[j] & 1) return;                  // pre-verified: flag already 1
   const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
-  flag[i] = bpg_find_dev<W>(prog, text + ls[x], ll[x]) ? 1 : 0;
+  const bool m = r == r0 ? bpg_find_dev<W>(sp, text + ls[x], ll[x]) : bpg_find_dev<W>(prog, text + ls[x], ll[x]);
+  flag[i] = m ? 1 : 0;
 }
 
 // literal-free programs over every line: blockIdx.y = regex slot (block-uniform), the program is
 // staged in LDS so class / first / last / exception reads are LDS hits
-constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global memory)
 template <int W>
 __global__ __launch_bounds__(kScanLines) void k_bpg_scan(const uint8_t* __restrict__ text,
                                                          const int64_t* __restrict__ ls,
@@ -111,8 +140,7 @@ __global__ __launch_bounds__(kScanLines) void k_bpg_scan(const uint8_t* __restri
   if (!is_bpg(P, r)) return;                  // block-uniform
   const uint64_t* prog = P.bpg + P.meta[4 * r];
   if ((int)(prog[0] & 0xFF) != W) return;
-  const uint64_t h = prog[0];   // program words: header, 6 masks, first / last, bytemap, classes, exceptions
-  const int nw = 1 + 36 * W + 32 + (int)((h >> 20) & 0x3FF) * W + (int)((h >> 8) & 0xFFF) * (W + 1);
+  const int nw = prog_words(prog, W);
   const int64_t line = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool m = false;
   if (nw <= kLdsProgWords) {

@@ -120,10 +120,16 @@ def run(args, sets, trig, rank, world, local_rank, server):
         local_gpu = local_rank
         torch.cuda.set_device(local_gpu)
         device = torch.device("cuda", local_gpu)
+        # the ingest copy stream is created before RCCL creates its own: HIP maps streams to a few
+        # hardware queues in creation order (GPU_MAX_HW_QUEUES), and a copy stream created after the
+        # process group can share the compute stream's queue -- the copy then waits for the step's
+        # kernels instead of overlapping them (LP_BENCH_LATE_COPY_STREAM=1 restores the old order, A/B)
+        early_copy_stream = None if os.environ.get("LP_BENCH_LATE_COPY_STREAM") == "1" else torch.cuda.Stream(device)
         from log_parser_amd.utils.numa import bind_to_gpu_numa
         bind_to_gpu_numa(local_gpu)          # pinned ingest buffers on the GPU's own socket
     else:
         device = torch.device("cpu")
+        early_copy_stream = None
     backend = args.backend
     if backend == "auto":
         # world 1: no process group until the RCCL group stops serialising the ingest copy with the
@@ -174,7 +180,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
     # Double-buffered ingest: the PCIe copy of request k+1 runs on its own HIP stream while request
     # k is analysed (every step still moves all of its bytes host->HBM). --no-overlap serialises.
     bufs = [torch.empty(size, dtype=torch.uint8, device=device) for _ in range(2)]
-    copy_stream = torch.cuda.Stream(device) if use_cuda else None
+    copy_stream = (early_copy_stream or torch.cuda.Stream(device)) if use_cuda else None
     ready = [torch.cuda.Event() for _ in range(2)] if use_cuda else None
     free = [torch.cuda.Event() for _ in range(2)] if use_cuda else None
     freed = [False, False]

@@ -1,10 +1,11 @@
 // gfx950 kernels of the bit-parallel Glushkov programs (bpg.h, models/bpg.py): the regexes whose
 // DFA blows up, verified on prefilter candidate lines or scanned over every line.
 //
-// One instantiation per program width W (words of 64 positions), launched only for the widths a
-// library has: each kernel's registers are sized for its own W, and the DFA kernels next to them
-// (k_cand_verify, k_dedupe_verify, k_scan) never carry the BPG walk -- folding it into dfa_run
-// took those kernels from ~40 to 130 VGPRs plus 580 B of scratch per lane (3 waves / SIMD).
+// Candidate verification (few lines: the slowest walk decides) is one kernel for every program width;
+// the all-lines scan (every line: occupancy decides) is one instantiation per width W (words of 64
+// positions), launched only for the widths a library has. The DFA kernels next to them
+// (k_cand_verify, k_dedupe_verify, k_scan) never carry the BPG walk -- folding it into dfa_run took
+// those kernels from ~40 to 130 VGPRs plus 580 B of scratch per lane (3 waves / SIMD).
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
@@ -22,32 +23,9 @@ constexpr int kScanLines = 256;
 
 inline unsigned nblocks(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
 
-__device__ __forceinline__ const uint64_t* prog_of(const DfaPool& P, int r, int W) {
-  if (!is_bpg(P, r)) return nullptr;
-  const uint64_t* p = P.bpg + P.meta[4 * r];
-  return (int)(p[0] & 0xFF) == W ? p : nullptr;
-}
-
-// small path: raw candidates (regex << 32 | line) verified in place (-1 = no match); the DFA ones
-// were verified by k_cand_verify
-template <int W>
-__global__ __launch_bounds__(256) void k_bpg_cand(int64_t* __restrict__ cand, int64_t cap,
-                                                  const unsigned long long* __restrict__ dcount,
-                                                  const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
-                                                  const int32_t* __restrict__ ll, DfaPool P) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = dcount ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
-  if (i >= n) return;
-  const int64_t k = cand[i];
-  if (k < 0) return;
-  const uint64_t* prog = prog_of(P, (int)(k >> 32), W);
-  if (!prog) return;
-  const int64_t x = k & 0xFFFFFFFFll;
-  if (!bpg_find_dev<W>(prog, text + ls[x], ll[x])) cand[i] = -1;
-}
-
-// small path, one launch for every width (a request's few candidates: the launch, not the
-// registers of the widest walk, is what costs here)
+// candidates of the small path, in place (-1 = no match; k_cand_verify did the DFA ones): one
+// launch for every width -- a step's BPG candidates are few, the launch and the slowest walk are
+// what cost, not the registers of the widest walk
 __global__ __launch_bounds__(256) void k_bpg_cand_all(int64_t* __restrict__ cand, int64_t cap,
                                                       const unsigned long long* __restrict__ dcount,
                                                       const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
@@ -85,45 +63,35 @@ __device__ __forceinline__ int prog_words(const uint64_t* prog, int W) {   // he
   return 1 + 36 * W + 32 + (int)((h >> 20) & 0x3FF) * W + (int)((h >> 8) & 0xFFF) * (W + 1);
 }
 
-template <int W>
-__global__ __launch_bounds__(256) void k_bpg_dedupe(const uint64_t* __restrict__ keys, int64_t n, int lbits,
-                                                    const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
-                                                    const int32_t* __restrict__ ll, DfaPool P,
-                                                    uint8_t* __restrict__ flag) {
-  // keys are sorted by regex: a block's keys nearly always share one program, staged in LDS
-  __shared__ uint64_t sp[kLdsProgWords];
-  __shared__ int s_r;
-  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
-  if (threadIdx.x == 0) {
-    int r0 = -1;
-    if (i0 < n && keys[i0] != kPadKey) {
-      const int r = (int)((keys[i0] >> 1) >> lbits);
-      const uint64_t* p = prog_of(P, r, W);
-      if (p && prog_words(p, W) <= kLdsProgWords) r0 = r;
-    }
-    s_r = r0;
-  }
-  __syncthreads();
-  const int r0 = s_r;
-  if (r0 >= 0) {
-    const uint64_t* p = P.bpg + P.meta[4 * r0];
-    const int nw = prog_words(p, W);
-    for (int j = threadIdx.x; j < nw; j += blockDim.x) sp[j] = p[j];
-  }
-  __syncthreads();
-  const int64_t i = i0 + threadIdx.x;
+// bulk path, every width in one kernel (registers of the widest walk: fine for a few waves)
+__global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restrict__ keys, int64_t n, int lbits,
+                                                        const uint8_t* __restrict__ text,
+                                                        const int64_t* __restrict__ ls,
+                                                        const int32_t* __restrict__ ll, DfaPool P,
+                                                        uint8_t* __restrict__ flag) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t key = keys[i];
   if (key == kPadKey) return;
   const uint64_t k = key >> 1;
   if (i > 0 && (keys[i - 1] >> 1) == k) return;
   const int r = (int)(k >> lbits);
-  const uint64_t* prog = prog_of(P, r, W);
-  if (!prog) return;
+  if (!is_bpg(P, r)) return;
   for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j)
     if (keys[j] & 1) return;                  // pre-verified: flag already 1
+  const uint64_t* prog = P.bpg + P.meta[4 * r];
   const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
-  const bool m = r == r0 ? bpg_find_dev<W>(sp, text + ls[x], ll[x]) : bpg_find_dev<W>(prog, text + ls[x], ll[x]);
+  const uint8_t* s = text + ls[x];
+  const int len = ll[x];
+  bool m;
+  switch ((int)(prog[0] & 0xFF)) {
+    case 1: m = bpg_find_dev<1>(prog, s, len); break;
+    case 2: m = bpg_find_dev<2>(prog, s, len); break;
+    case 3: m = bpg_find_dev<3>(prog, s, len); break;
+    case 4: m = bpg_find_dev<4>(prog, s, len); break;
+    case 6: m = bpg_find_dev<6>(prog, s, len); break;
+    default: m = bpg_find_dev<8>(prog, s, len); break;
+  }
   flag[i] = m ? 1 : 0;
 }
 
@@ -177,27 +145,19 @@ void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, 
                   const int32_t* ll, const DfaPool& P, uint64_t stream) {
   if (!P.bpg_widths || cap <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (cap <= 4096) {                // a request: one launch for every width
-    hipLaunchKernelGGL(k_bpg_cand_all, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text, ls, ll, P);
-    check_launch("k_bpg_cand_all");
-    return;
-  }
-  for_widths(P.bpg_widths, [&](auto w) {
-    hipLaunchKernelGGL(k_bpg_cand<decltype(w)::value>, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text,
-                       ls, ll, P);
-    check_launch("k_bpg_cand");
-  });
+  hipLaunchKernelGGL(k_bpg_cand_all, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text, ls, ll, P);
+  check_launch("k_bpg_cand_all");
 }
 
 void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
                     const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream) {
   if (!P.bpg_widths || n <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  for_widths(P.bpg_widths, [&](auto w) {
-    hipLaunchKernelGGL(k_bpg_dedupe<decltype(w)::value>, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text,
-                       ls, ll, P, flag);
-    check_launch("k_bpg_dedupe");
-  });
+  // ONE launch for every width: a step's BPG candidates are few (hundreds to thousands, a handful of
+  // waves) and each walk is a serial chain of ~150 wave instructions per byte, so per-width launches
+  // added up their slowest walks (~100 us each) where one launch runs them side by side
+  hipLaunchKernelGGL(k_bpg_dedupe_all, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag);
+  check_launch("k_bpg_dedupe_all");
 }
 
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,

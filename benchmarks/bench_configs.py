@@ -170,14 +170,17 @@ def mode_single(args):
 
 
 def mode_stream(args):
-    from log_parser_amd.parallel.stream import RepeatBuffer, StreamAnalyzer
+    from log_parser_amd.parallel.stream import RepeatBuffer, StreamAnalyzer, auto_chunk_bytes
     dev = _dev(args)
     eng, _, trig = _engine(args.patterns, dev, library=args.library)
     block = make_log(200_000, trig, seed=6, hit_rate=0.004, aux_rate=0.01, stack_rate=0.01).encode()
     lines_per_block = block.count(b"\n")
     total = len(block) * max(1, args.lines // lines_per_block)
     src = RepeatBuffer(block, total)
-    sa = StreamAnalyzer(eng, chunk_bytes=(args.chunk_mb << 20) or None, topk=100, keep_events=False)
+    # the chunk the timed stream will use (auto: from free HBM and the stream length), fixed so the
+    # warm-up sizes the pinned pool for it
+    chunk = (args.chunk_mb << 20) or auto_chunk_bytes(dev, total)
+    sa = StreamAnalyzer(eng, chunk_bytes=chunk, topk=100, keep_events=False)
     # untimed warm-up stream (3 chunks): pinned pool, kernels, allocator; then a fresh frequency state
     sa.run(RepeatBuffer(block, min(total, 3 * sa.chunk_bytes)))
     eng.freq.reset_all()

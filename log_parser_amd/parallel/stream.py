@@ -36,15 +36,20 @@ from ..ops import kernels as K
 CHUNK_MIN, CHUNK_MAX = 256 << 20, 8 << 30
 
 
-def auto_chunk_bytes(device: torch.device) -> int:
+def auto_chunk_bytes(device: torch.device, total: Optional[int] = None) -> int:
     """``engine.chunk-bytes = 0``: chunks sized from the GPU's free HBM -- 1/16 of it, within
     [256 MiB, 8 GiB] (a chunk's device footprint is ~3x its bytes: text, line index, matcher
     arenas, CSR, with the next chunk's copy in flight). On a 288 GB MI355X that is 8 GiB chunks:
-    fewer halos, launches and host hand-offs than the 256 MiB of round 2."""
+    fewer halos, launches and host hand-offs than the 256 MiB of round 2 -- what a resident log
+    (analysed from HBM, no copy to hide) wants. A host stream (``total`` = its length) also caps
+    the chunk at 1/32 of the stream: the first chunk's copy and the last chunk's analysis are not
+    overlapped, and on 100 GB 8 GiB chunks ran 8% slower than 256 MiB ones (profiles/r3_d)."""
     if device.type != "cuda":
         return CHUNK_MIN
     free, _ = torch.cuda.mem_get_info(device)
     c = max(CHUNK_MIN, min(CHUNK_MAX, free // 16))
+    if total is not None:
+        c = max(CHUNK_MIN, min(c, total // 32))
     return int(c) & ~((1 << 20) - 1)
 
 
@@ -199,6 +204,7 @@ class StreamAnalyzer:
         accumulate per chunk and only events that can still reach the top-k are kept (exact, see
         ``_prune``), instead of every event's seven factors until the end of the stream."""
         self.engine = engine
+        self._auto_chunk = not (chunk_bytes or engine.config["engine.chunk-bytes"])
         self.chunk_bytes = int(chunk_bytes or engine.config["engine.chunk-bytes"] or auto_chunk_bytes(engine.device))
         K._check_k(topk)
         self.topk = topk
@@ -329,6 +335,8 @@ class StreamAnalyzer:
             return StreamResult(0, 0, empty, z, z.astype(np.int64), z.astype(np.int64), 0, len(src), 0.0)
         nkeys = len(lib.freq_ids)
         resident = isinstance(src, ResidentLog)
+        if self._auto_chunk and not resident:
+            self.chunk_bytes = auto_chunk_bytes(dev, eff)       # (same on resume: eff is the whole stream)
         if resident and src.halo < lib.halo:
             raise ValueError(f"resident log staged with {src.halo} halo lines, the library needs {lib.halo}")
         start = 0

@@ -78,6 +78,10 @@ def library(args):
 def main():
     args = parse()
     from log_parser_amd.utils import launch
+    # >= 8 HIP hardware queues, before any HIP call here, in the ranks or in the /parse server: with
+    # HIP's default 4 an RCCL group's streams push the ingest copy onto a kernel queue and the copy
+    # stops overlapping the step (23.5 -> 27.1 ms/step at world 1, profiles/r3_f)
+    hw_queues = launch.ensure_hw_queues()
     if not launch.under_launcher() and args.gpus > 1:
         # parent: no GPU call here; N fresh rank processes, one per GPU
         sys.exit(launch.spawn_local_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
@@ -94,13 +98,13 @@ def main():
         dev = "cpu" if args.device == "cpu" else f"cuda:{local_rank}"
         server = restbench.ServerProcess(restbench.write_library(sets), dev, http=args.http)
     try:
-        run(args, sets, trig, rank, world, local_rank, server)
+        run(args, sets, trig, rank, world, local_rank, server, hw_queues)
     finally:
         if server is not None:
             server.stop()
 
 
-def run(args, sets, trig, rank, world, local_rank, server):
+def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -132,9 +136,9 @@ def run(args, sets, trig, rank, world, local_rank, server):
         early_copy_stream = None
     backend = args.backend
     if backend == "auto":
-        # world 1: no process group until the RCCL group stops serialising the ingest copy with the
-        # compute (docs/PERFORMANCE.md, profiles/r3_*: 23.4 -> 27.5 ms/step with a world-1 group)
-        backend = ("nccl" if use_cuda else "gloo") if world > 1 else "none"
+        # GPUs: RCCL at every world size, 1 included -- the 1-GPU number runs the same collectives as
+        # the 8-GPU one (with >= 8 HW queues the world-1 group costs nothing, profiles/r3_f)
+        backend = "nccl" if use_cuda else ("gloo" if world > 1 else "none")
     if backend == "none" and world > 1:
         backend = "nccl" if use_cuda else "gloo"
     if backend != "none":
@@ -318,6 +322,7 @@ def run(args, sets, trig, rank, world, local_rank, server):
             "per_rank": [{"rank": r, "ms_per_step": round(x[0] / args.steps * 1e3, 3), "h2d_GBps": round(x[1], 2),
                           "device_ms": round(x[2], 3), "numa_node": int(x[3])} for r, x in enumerate(per_rank_diag)],
             "collectives_per_step": 2 if dist.is_initialized() else 0,
+            "hip_hw_queues": hw_queues,
             "matcher_counts_rank0": dict(eng.arena.last),
         }
         if state.get("dev"):

@@ -57,6 +57,8 @@ def cmd_analyze(args, cfg: Config) -> int:
 
 def main(argv: Optional[List[str]] = None) -> int:
     argv = sys.argv[1:] if argv is None else argv
+    from .utils.launch import ensure_hw_queues
+    ensure_hw_queues()                  # before the first HIP call (profiles/r3_f)
     if argv and argv[0] == "serve":
         from .serve.__main__ import main as serve_main
         serve_main(argv[1:])

@@ -46,6 +46,8 @@ def raise_fd_limit() -> int:
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s [%(name)s] %(message)s")
+    from ..utils.launch import ensure_hw_queues
+    ensure_hw_queues()                  # before the first HIP call (profiles/r3_f)
     cfg = Config.load(overrides=parse_cli_overrides(argv))
     raise_fd_limit()
     bind_numa(cfg)

@@ -496,6 +496,16 @@ PYBIND11_MODULE(_lpnative, m) {
                        uint64_t out, int64_t cap, uint64_t count, uint64_t s) {
     scan_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs), nregs,
              dfa_from(dfa), P<int64_t>(out), cap, P<unsigned long long>(count), s); });
+  // BPG candidate walks (bpg.hip) on their own, for kernel tests / A/B: in-place candidate verify
+  // (cand = (regex << 32 | line), -1 = rejected) and first-of-run flags over sorted packed keys
+  m.def("bpg_cand_dev", [](uint64_t cand, int64_t cap, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa,
+                           uint64_t s) {
+    bpg_cand_dev(P<int64_t>(cand), cap, nullptr, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll),
+                 dfa_from(dfa), s); });
+  m.def("bpg_dedupe_dev", [](uint64_t keys, int64_t n, int lbits, uint64_t text, uint64_t ls, uint64_t ll,
+                             py::tuple dfa, uint64_t flag, uint64_t s) {
+    bpg_dedupe_dev(P<const uint64_t>(keys), n, lbits, P<const uint8_t>(text), P<const int64_t>(ls),
+                   P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(flag), s); });
   // ev_rank / ev_fkey / carry: frequency count before each event = carry[fkey] + rank (fused)
   m.def("score_dev", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry, int64_t n,
                         py::tuple st, py::tuple sp, uint64_t out, uint64_t fac, uint64_t s) {

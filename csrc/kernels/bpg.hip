@@ -8,6 +8,7 @@
 // those kernels from ~40 to 130 VGPRs plus 580 B of scratch per lane (3 waves / SIMD).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -95,6 +96,245 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
   flag[i] = m ? 1 : 0;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wave-cooperative walk (candidate verification: few lines, so the latency of ONE line's walk decides).
+//
+// The one-lane-per-line walk above is a serial chain of ~40 dependent VALU ops per 64-bit word per
+// byte (~240 for a 6-word program: 75 us for one 10k-line request's candidates, profiles/r3_h). Here
+// a line is walked by a GROUP of G lanes (G = power of two >= 2W), lane j holding 32-bit word j of
+// every mask, so a byte costs ~20 ops on the chain whatever the width:
+//   * shift edges: the carry of word j-1 arrives by DPP row_shr:1 (groups never straddle a 16-lane row);
+//   * spread fields: the multi-word subtraction's borrow chain is a carry-lookahead on two ballots --
+//     generate g = df < lo, propagate p = df == lo; the borrow INTO lane i is bit i of
+//     (X + G) ^ X ^ G with X = G | P (a 64-bit scalar add resolves every group's chain at once;
+//     each group's top lane is masked out of G and P, so no borrow crosses into the next group);
+//   * exceptions: the source bit's owner lane votes (ballot), every lane of the group reads it;
+//   * class / first / last words for 16 bytes are loaded before the 16 serial updates (they depend
+//     on the text only), so no load latency sits on the state chain.
+// A wave takes 64 candidate slots, compacts the ones that need a BPG walk (ballot) and walks them
+// 64 / G at a time.
+
+__device__ __forceinline__ uint64_t coop_chain_mask(int G) {   // every lane but each group's top lane
+  uint64_t top = 0;
+  for (int b = G - 1; b < 64; b += G) top |= 1ull << b;
+  return ~top;
+}
+
+template <int G>
+__device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, const uint8_t* __restrict__ s, int n,
+                                              bool valid) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int j = lane & (G - 1);
+  const int gb = lane & ~(G - 1);
+  const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
+  const uint64_t chain = coop_chain_mask(G);
+  const uint64_t hdr = valid ? P[0] : 0ull;
+  const int W = (int)(hdr & 0xFF);
+  const int E = (int)((hdr >> 8) & 0xFFF);
+  const int ncls = (int)((hdr >> 20) & 0x3FF);
+  const bool uniform = (hdr & BPG_UNIFORM) != 0;
+  const uint32_t nullm = (uint32_t)(hdr >> 32) & 0x7FFFu;
+  const bool wl = valid && j < 2 * W;           // this lane holds a program word
+  const uint32_t* p32 = reinterpret_cast<const uint32_t*>(P);
+  // uint32 index of word j of the 64-bit mask at uint64 offset o
+#define LP_W32(o) (p32[2 * (o) + j])
+  // word j of every structural mask; lanes past the program (and invalid groups) hold zeros, so
+  // their state stays empty. The top word's bit 31 never has a shift edge (no position above), so
+  // no shift carry leaves a group and row_shr:1 needs no mask.
+  const uint32_t shm = wl ? LP_W32(1) : 0u, selfm = wl ? LP_W32(1 + W) : 0u, src = wl ? LP_W32(1 + 2 * W) : 0u;
+  const uint32_t R = wl ? LP_W32(1 + 3 * W) : 0u, lo = wl ? LP_W32(1 + 4 * W) : 0u, hi = wl ? LP_W32(1 + 5 * W) : 0u;
+  const int first_o = 1 + 6 * W, last_o = 1 + 21 * W, cls_o = 1 + 36 * W + 32;
+  const uint32_t f0 = wl ? LP_W32(first_o) : 0u, l0 = wl ? LP_W32(last_o) : 0u;
+  const uint8_t* bm = reinterpret_cast<const uint8_t*>(P + 1 + 36 * W);
+  const int exc_o = cls_o + ncls * W;
+  const int ftl = valid ? final_term_len(s, n) : 0;
+  const int ft = ftl ? n - ftl : -1;
+  // wave-uniform feature switches: the common program (uniform first/last sets, no exception edges,
+  // not nullable, line without a final terminator) walks only the shift / self / spread chain
+  const bool wnon = __ballot(valid && !uniform) != 0;
+  const bool wexc = __ballot(valid && E > 0) != 0;
+  const bool wctx = wnon || wexc || __ballot(valid && nullm != 0) != 0;
+  const bool wft = __ballot(ftl > 0) != 0;
+  const int sh = valid ? (int)((uintptr_t)s & 15) : 0;
+  const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
+  int T = valid ? n + sh : 0;                    // position of this group's end of line (pos = t + sh)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) T = max(T, __shfl_xor(T, o, 64));
+  uint32_t S = 0, acc = 0, Sft = 0;
+  int ftctx = 0;
+  bool nullhit = false;
+  int prevk = 0;                                 // P_BOS
+  for (int b0 = 0; b0 <= T; b0 += 16) {          // wave-uniform
+    const uint4 cur = (valid && b0 < sh + n) ? blk[b0 >> 4] : make_uint4(0, 0, 0, 0);
+    // text-only operands of the 16 bytes, off the state chain: class words (0 outside [0, n): the
+    // state is empty before the line and dies after its end), boundary contexts, first / last words
+    uint32_t cw[16], fw[16], lw[16];
+    int ctxq[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t wv = (q < 4) ? cur.x : (q < 8) ? cur.y : (q < 12) ? cur.z : cur.w;
+      const int c = (int)((wv >> (8 * (q & 3))) & 0xFFu);
+      const int t = b0 + q - sh;
+      const bool live = wl && t >= 0 && t < n;
+      cw[q] = live ? LP_W32(cls_o + (int)bm[c] * W) : 0u;
+      if (wctx) {
+        const bool lv = valid && t >= 0 && t < n;
+        const int nk = lv ? byte_kind(c) : 0;    // N_EOS from the end of line on
+        if (wft && t == ft) ftctx = prevk * 5 + 1;
+        ctxq[q] = prevk * 5 + nk;
+        nullhit |= valid && t >= 0 && t <= n && ((nullm >> ctxq[q]) & 1u);
+        if (lv) prevk = nk == 2 ? 1 : 2;
+      }
+    }
+    if (wnon) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        fw[q] = uniform ? f0 : (wl ? LP_W32(first_o + ctxq[q] * W) : 0u);
+        lw[q] = uniform ? l0 : (wl ? LP_W32(last_o + ctxq[q] * W) : 0u);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      // accept before this byte (the state after the last byte is checked at t = n; later
+      // positions see the empty state)
+      acc |= S & (wnon ? lw[q] : l0);
+      if (wft) Sft = (b0 + q - sh == ft) ? S : Sft;
+      // shift edges with the carry out of word j-1, self loops
+      const uint32_t x = S & shm;
+      const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x >> 31), 0x111 /* row_shr:1 */, 0xF, 0xF, true);
+      uint32_t F = (x << 1) | y | (S & selfm);
+      // spread fields: d = df - lo over the group; borrow INTO lane i = bit i of (X + G) ^ X ^ G
+      const uint32_t df = (S & src) | hi;
+      const uint64_t Gm = __ballot(df < lo) & chain;
+      const uint64_t Pm = __ballot(df == lo) & chain;
+      const uint64_t X = Gm | Pm;
+      const uint64_t Cm = (X + Gm) ^ X ^ Gm;
+      const uint32_t d = df - lo - (uint32_t)((Cm >> lane) & 1ull);
+      F |= R & ~(d ^ df);
+      if (wexc) {                                // exception edges: the source word's lane votes
+        const int ctx = ctxq[q];
+        for (int e = 0; e < E; ++e) {            // E varies across groups: lanes past their E idle
+          const uint32_t h = (uint32_t)P[exc_o + e * (W + 1)];
+          const uint32_t tw = wl ? LP_W32(exc_o + e * (W + 1) + 1) : 0u;
+          const int p = (int)(h & 0xFFFF);
+          const uint64_t M = __ballot(j == (p >> 5) && ((S >> (p & 31)) & 1u));
+          if (((M >> (gb + (p >> 5))) & 1ull) && (((h >> 16) >> ctx) & 1u)) F |= tw;
+        }
+      }
+      S = (F | (wnon ? fw[q] : f0)) & cw[q];
+    }
+    // a group is finished once it accepted or its line ended; the wave stops when all are
+    const uint64_t hitm = __ballot(acc != 0 || nullhit);
+    const bool fin = !valid || (hitm & gm) != 0 || b0 + 16 > sh + n;
+    if (__ballot(!fin) == 0) break;
+  }
+  if (wft && ft >= 0) acc |= Sft & (uniform ? l0 : (wl ? LP_W32(last_o + ftctx * W) : 0u));
+#undef LP_W32
+  return (__ballot(acc != 0 || nullhit) & gm) != 0;
+}
+
+// mode 0: cand[i] = -1 for BPG candidates that do not match (request path, k_cand_verify did the
+// DFA ones); mode 1: flag the first key of every sorted run whose regex is a BPG program that no
+// engine pre-verified (bulk path, k_dedupe_verify left the flag 0)
+template <int G, int MODE>
+__global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, const uint64_t* __restrict__ keys,
+                                                  int64_t cap, const unsigned long long* __restrict__ dcount, int lbits,
+                                                  const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
+                                                  const int32_t* __restrict__ ll, DfaPool P,
+                                                  uint8_t* __restrict__ flag) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (MODE == 0 && dcount) ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
+  int r = 0;
+  int64_t x = 0;
+  bool need = false;
+  if (i < n) {
+    if (MODE == 0) {
+      const int64_t k = cand[i];
+      if (k >= 0) {
+        r = (int)(k >> 32);
+        x = k & 0xFFFFFFFFll;
+        need = is_bpg(P, r);
+      }
+    } else {
+      const uint64_t key = keys[i];
+      const uint64_t k = key >> 1;
+      if (key != kPadKey && !(i > 0 && (keys[i - 1] >> 1) == k)) {
+        r = (int)(k >> lbits);
+        x = (int64_t)(k & ((1ull << lbits) - 1));
+        need = is_bpg(P, r);
+        for (int64_t q = i; need && q < n && (keys[q] >> 1) == k; ++q)
+          if (keys[q] & 1) need = false;         // pre-verified: flag already 1
+      }
+    }
+  }
+  uint64_t todo = __ballot(need);                // wave-uniform
+  constexpr int NG = 64 / G;
+  const int g = lane / G;
+  while (todo) {
+    // group g takes the g-th lowest pending slot of the wave
+    int src = -1;
+    uint64_t m = todo;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int b = m ? __builtin_ctzll(m) : -1;
+      if (k == g) src = b;
+      m &= m ? m - 1 : 0ull;
+    }
+    todo = m;
+    const int sl = src < 0 ? lane : src;
+    const int rr = __shfl(r, sl, 64);
+    const int64_t xx = __shfl(x, sl, 64);
+    const bool valid = src >= 0;
+    const uint64_t* prog = P.bpg + (valid ? P.meta[4 * rr] : 0);
+    const uint8_t* s = text + (valid ? ls[xx] : 0);
+    const int len = valid ? ll[xx] : 0;
+    const bool hit = bpg_coop_walk<G>(prog, s, len, valid);
+    if (valid && (lane & (G - 1)) == 0) {
+      const int64_t slot = (i - lane) + src;
+      if (MODE == 0) {
+        if (!hit) cand[slot] = -1;
+      } else {
+        flag[slot] = hit ? 1 : 0;
+      }
+    }
+  }
+}
+
+int coop_group(uint32_t widths) {                // lanes per line: power of two >= 2 x the widest program
+  int w = 0;
+  for (int b = 31; b >= 0; --b)
+    if (widths & (1u << b)) { w = b; break; }
+  int g = 2;
+  while (g < 2 * w) g <<= 1;
+  return g;
+}
+
+// LP_BPG_WALK (A/B): "auto" (default) = the cooperative walk for request-path candidates (latency:
+// few lines) and the one-lane walk for the bulk path's first-of-run keys (throughput: a lane per line
+// does ~4x fewer instructions per line-byte than a 16-lane group); "lane" / "coop" force one.
+int walk_mode() {
+  static const int m = [] {
+    const char* e = getenv("LP_BPG_WALK");
+    const std::string v = e ? e : "auto";
+    return v == "lane" ? 1 : v == "coop" ? 2 : 0;
+  }();
+  return m;
+}
+
+template <int MODE>
+void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigned long long* dcount, int lbits,
+                 const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P, uint8_t* flag,
+                 hipStream_t st) {
+  const dim3 grid(nblocks(cap)), block(256);
+  switch (coop_group(P.bpg_widths)) {
+    case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
+    case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
+    case 8: hipLaunchKernelGGL((k_bpg_coop<8, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
+    default: hipLaunchKernelGGL((k_bpg_coop<16, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
+  }
+}
+
 // literal-free programs over every line: blockIdx.y = regex slot (block-uniform), the program is
 // staged in LDS so class / first / last / exception reads are LDS hits
 template <int W>
@@ -145,6 +385,11 @@ void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, 
                   const int32_t* ll, const DfaPool& P, uint64_t stream) {
   if (!P.bpg_widths || cap <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (walk_mode() != 1) {
+    launch_coop<0>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, st);
+    check_launch("k_bpg_coop<cand>");
+    return;
+  }
   hipLaunchKernelGGL(k_bpg_cand_all, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text, ls, ll, P);
   check_launch("k_bpg_cand_all");
 }
@@ -153,6 +398,11 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
                     const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream) {
   if (!P.bpg_widths || n <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (walk_mode() == 2) {
+    launch_coop<1>(nullptr, keys, n, nullptr, lbits, text, ls, ll, P, flag, st);
+    check_launch("k_bpg_coop<dedupe>");
+    return;
+  }
   // ONE launch for every width: a step's BPG candidates are few (hundreds to thousands, a handful of
   // waves) and each walk is a serial chain of ~150 wave instructions per byte, so per-width launches
   // added up their slowest walks (~100 us each) where one launch runs them side by side

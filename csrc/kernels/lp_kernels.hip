@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -279,6 +280,121 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
   if (c > 0) pf_flush(buf, &cnt, &gbase, c, cand, cap, count);
 }
 
+// K3a'' (default): the same verification, load-balanced inside each wave. Bucket sizes are skewed
+// (a 4-gram shared by 186 literals next to buckets of 1-3: profiles/r3_k), so a lane group per gram
+// hit made every block wait, at its barrier, for its largest bucket walked 4 literals at a time. Here
+// a wave takes 64 gram hits, prefix-sums their bucket sizes and then checks 64 (hit, literal) pairs
+// per iteration -- a 186-literal bucket costs 3 iterations of one wave -- and appends its candidates
+// with one atomic per iteration (wave prefix sum of the per-lane region counts). No block barrier.
+constexpr int PVW_WAVES = 4;
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(64 * PVW_WAVES) void k_pf_verify_wave(const int64_t* __restrict__ ghits, int64_t n,
+                                                                   const unsigned long long* __restrict__ dn,
+                                                                   const uint8_t* __restrict__ text, int64_t nbytes,
+                                                                   PfTables T, const int64_t* __restrict__ line_start,
+                                                                   int64_t nlines, const int32_t* __restrict__ blk_line,
+                                                                   int64_t* cand, int64_t cap,
+                                                                   unsigned long long* count) {
+  __shared__ int s_incl[PVW_WAVES][64];
+  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+  if (dn) {
+    const int64_t d = (int64_t)*dn;
+    n = d < n ? d : n;
+  }
+  const int64_t nwaves = (int64_t)gridDim.x * PVW_WAVES;
+  for (int64_t chunk = ((int64_t)blockIdx.x * PVW_WAVES + w) * 64; chunk < n; chunk += nwaves * 64) {
+    // this lane's gram hit: position, tier, bucket (bloom: start in gram_lits; Teddy: bucket mask)
+    const int64_t i = chunk + lane;
+    int64_t p = 0;
+    int c = 0, sm = 0;
+    bool td = false;
+    if (i < n) {
+      const int64_t h = ghits[i];
+      p = h >> 2;
+      if ((h & 3) == 3) {
+        td = true;
+        const uint32_t m = teddy_mask(T, text, nbytes, p);
+        sm = (int)m;
+        for (uint32_t mm = m; mm; mm &= mm - 1) {
+          const int b = __ffs(mm) - 1;
+          c += T.tb_off[b + 1] - T.tb_off[b];
+        }
+      } else {
+        const int G = 2 + (int)(h & 3);
+        uint32_t g4 = 0;
+        for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
+        int st;
+        pf_bucket(T, g4 & gram_mask(G), G, st, c);
+        sm = st;
+      }
+    }
+    const int incl = wave_incl_scan(c, lane);
+    const int total = __shfl(incl, 63, 64);
+    s_incl[w][lane] = incl;
+    const int excl = incl - c;
+    for (int k0 = 0; k0 < total; k0 += 64) {
+      const int q = k0 + lane;
+      // owner = first lane whose inclusive count exceeds q
+      int o = 0;
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1)
+        if (s_incl[w][o + step - 1] <= q) o += step;
+      o = q < total ? o : lane;
+      const int64_t op = __shfl(p, o, 64);
+      const int osm = __shfl(sm, o, 64);
+      const bool otd = __shfl((int)td, o, 64) != 0;
+      const int k = q - __shfl(excl, o, 64);
+      int nr = 0, lit = 0;
+      int64_t line = 0;
+      if (q < total) {
+        int32_t e;
+        if (otd) {
+          int kk = k;
+          e = 0;
+          for (uint32_t mm = (uint32_t)osm; mm; mm &= mm - 1) {
+            const int b = __ffs(mm) - 1;
+            const int sz = T.tb_off[b + 1] - T.tb_off[b];
+            if (kk < sz) {
+              e = T.tb_lits[T.tb_off[b] + kk];
+              break;
+            }
+            kk -= sz;
+          }
+        } else {
+          e = T.gram_lits[osm + k];
+        }
+        if (pf_lit_at(T, text, nbytes, op, e)) {
+          lit = pf_entry_lit(e);
+          nr = T.lit_reg_off[lit + 1] - T.lit_reg_off[lit];
+          line = locate_line(line_start, nlines, blk_line, op);
+          if (line < 0) line = 0;
+        }
+      }
+      // one atomic per wave for this iteration's candidates
+      const int ri = wave_incl_scan(nr, lane);
+      const int rt = __shfl(ri, 63, 64);
+      if (rt == 0) continue;
+      unsigned long long base = 0;
+      if (lane == 0) base = atomicAdd(count, (unsigned long long)rt);
+      base = __shfl(base, 0, 64);
+      const int r0 = T.lit_reg_off[lit];
+      for (int j = 0; j < nr; ++j) {
+        const unsigned long long slot = base + (unsigned long long)(ri - nr + j);
+        if ((int64_t)slot < cap) cand[slot] = ((int64_t)T.lit_reg[r0 + j] << 32) | line;
+      }
+    }
+  }
+}
+
 // K3c: regexes without a usable literal: every line x every scan regex
 __global__ __launch_bounds__(256) void k_scan(const uint8_t* __restrict__ text,
                                               const int64_t* __restrict__ line_start,
@@ -395,6 +511,18 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn, int max_grid) {
   if (n <= 0) return;
+  static const bool lane_groups = [] {   // LP_PF_VERIFY=lanes: the lane-group kernel (A/B)
+    const char* e = getenv("LP_PF_VERIFY");
+    return e && std::string(e) == "lanes";
+  }();
+  if (!lane_groups) {
+    const int64_t need = (n + 64 * PVW_WAVES - 1) / (64 * PVW_WAVES);
+    const int g = dn ? (int)std::min<int64_t>(need, std::max(1, max_grid)) : (int)std::max<int64_t>(1, need);
+    hipLaunchKernelGGL(k_pf_verify_wave, dim3(g), dim3(64 * PVW_WAVES), 0, as_stream(stream), ghits, n, dn, text, nbytes,
+                       T, line_start, nlines, blk_line, cand, cap, count);
+    LP_CHECK(hipGetLastError());
+    return;
+  }
   // with a device-side count the grid is sized for the buffer but capped (grid-stride loop)
   const int lanes = nbytes >= (int64_t(64) << 20) ? 4 : 16;
   const int64_t need = (n + 256 / lanes - 1) / (256 / lanes);   // blocks for one pass over n hits

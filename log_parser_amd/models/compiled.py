@@ -295,6 +295,15 @@ class CompiledLibrary:
         np.cumsum(cnt, out=self.prim_off[1:])
         self.prim_pats = np.argsort(self.primary_reg, kind="stable").astype(np.int32)
 
+    def bpg_program(self, r: int) -> np.ndarray:
+        """The bit-parallel Glushkov program of regex ``r`` (a slice of ``bpg_pool``)."""
+        if r not in self.bpg_regs:
+            raise KeyError(f"regex {r} is not a BPG program")
+        o = int(self.dfa_meta[r, 0])
+        h = int(self.bpg_pool[o])
+        W, E, ncls = h & 0xFF, (h >> 8) & 0xFFF, (h >> 20) & 0x3FF
+        return self.bpg_pool[o:o + 1 + 36 * W + 32 + ncls * W + E * (W + 1)]
+
     def _compile_regexes(self):
         meta, bytemaps, trans, accs = [], [], [], []
         toff = aoff = 0

@@ -150,3 +150,89 @@ def test_engine_bounded_gap_gpu_matches_golden(gpu_device, seed):
     assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in r["events"]] == \
         [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
     np.testing.assert_allclose([e["score"] for e in r["events"]], [e["score"] for e in g["events"]], rtol=1e-12)
+
+
+# libraries whose widest program sets the wave-cooperative group size (bpg.hip k_bpg_coop<G>):
+# 1 word -> G = 2 lanes, 2 words -> 4, up to 4 words -> 8, 6 / 8 words -> 16 (exceptions and boundary-gated
+# programs included)
+COOP_LIBS = [
+    ([r"ab.{0,10}cd", r"x.{0,3}y", r"(a|bc)+d.{0,20}e", r"(?i)é.{0,3}z\B"], 8),
+    (GAP_PATS[4:6], 64),
+    (GAP_PATS[4:], 64),
+    (GAP_PATS + [r"a.{0,150}b", r"(?i)error.{0,220}\bdisk"], 64),
+]
+
+
+def _text_dev(lines, dev):
+    blob = "\n".join(lines).encode()
+    t = torch.zeros(K.padded_len(len(blob)), dtype=torch.uint8)
+    t[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    starts, lens, pos = [], [], 0
+    for s in lines:
+        starts.append(pos)
+        lens.append(len(s.encode()))
+        pos += lens[-1] + 1
+    return (t.to(dev), torch.tensor(starts, dtype=torch.int64, device=dev),
+            torch.tensor(lens, dtype=torch.int32, device=dev))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("li", range(len(COOP_LIBS)))
+def test_bpg_candidate_walks_match_host(gpu_device, li):
+    """The candidate walks (request path: in-place verify; bulk path: first-of-run flags over sorted
+    keys with duplicates and pre-verified copies) give the host twin's find() for every width."""
+    pats, max_states = COOP_LIBS[li]
+    from log_parser_amd.models.schema import PatternSet
+    ps = PatternSet.model_validate({"metadata": {"library_id": "gap"}, "patterns": [
+        {"id": f"g{i}", "name": p, "severity": "HIGH", "primary_pattern": {"regex": p, "confidence": 0.5}}
+        for i, p in enumerate(pats)]})
+    lib = CompiledLibrary([ps], ScoringParams(), max_dfa_states=max_states)
+    assert lib.bpg_regs
+    rng = random.Random(40 + li)
+    lines = _lines(rng, 3000) + ["a" + "é" * k + "b" for k in range(0, 160, 7)] + \
+        ["ERROR " + "x" * k + " disk" for k in range(0, 260, 13)]
+    text, ls, ll = _text_dev(lines, gpu_device)
+    dfa = lib.device_tables(gpu_device)["dfa"]
+    want = {(r, j) for r in lib.bpg_regs for j, s in enumerate(lines) if run_program(lib.bpg_program(r), s.encode())}
+    assert len(want) > 100
+    # request path: every (regex, line) pair plus rejected slots (-1) and non-BPG regexes, shuffled
+    pairs = [(r, j) for r in lib.bpg_regs for j in range(len(lines))]
+    others = [r for r in range(len(lib.regexes)) if r not in set(lib.bpg_regs)]
+    pairs += [(others[k % len(others)], k) for k in range(0, len(lines), 5)] if others else []
+    rng.shuffle(pairs)
+    cand = [(r << 32) | j for r, j in pairs] + [-1] * 77
+    ct = torch.tensor(cand, dtype=torch.int64, device=gpu_device)
+    N.bpg_cand_dev(ct.data_ptr(), ct.numel(), text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                   torch.cuda.current_stream().cuda_stream)
+    got = ct.cpu().tolist()
+    bpg = set(lib.bpg_regs)
+    for before, after in zip(cand, got):
+        if before < 0 or (before >> 32) not in bpg:
+            assert after == before
+        else:
+            assert (after >= 0) == ((before >> 32, before & 0xFFFFFFFF) in want), (before >> 32, before & 0xFFFFFFFF)
+    # bulk path: sorted packed keys, some duplicated, some pre-verified (flag bit 1)
+    lbits = N.bits_for(len(lines))
+    keys = []
+    for r, j in pairs:
+        k = ((r << lbits) | j) << 1
+        keys.append(k)
+        if rng.random() < 0.1:
+            keys.append(k)
+        if rng.random() < 0.05:
+            keys.append(k | 1)
+    keys.sort()
+    kt = torch.tensor(keys, dtype=torch.int64, device=gpu_device)
+    flag = torch.full((len(keys),), 7, dtype=torch.uint8, device=gpu_device)
+    N.bpg_dedupe_dev(kt.data_ptr(), kt.numel(), lbits, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                     flag.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    fl = flag.cpu().tolist()
+    for i, k in enumerate(keys):
+        kk = k >> 1
+        r, j = kk >> lbits, kk & ((1 << lbits) - 1)
+        run = [x for x in keys if x >> 1 == kk]
+        first = i == 0 or keys[i - 1] >> 1 != kk
+        if first and r in bpg and not any(x & 1 for x in run):
+            assert fl[i] == (1 if (r, j) in want else 0), (r, j)
+        else:
+            assert fl[i] == 7

@@ -47,6 +47,10 @@ static PfTables pf_from(const py::tuple& t) {
   T.tb_off = P<const int32_t>(t[14].cast<uint64_t>());
   T.tb_lits = P<const int32_t>(t[15].cast<uint64_t>());
   T.teddy_on = t[16].cast<int>();
+  if (t.size() > 18) {
+    T.gram_fp = P<const uint64_t>(t[17].cast<uint64_t>());
+    T.tb_fp = P<const uint64_t>(t[18].cast<uint64_t>());
+  }
   return T;
 }
 

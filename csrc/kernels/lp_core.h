@@ -221,6 +221,10 @@ struct PfTables {
   const int32_t* tb_off;    // [33] bucket CSR into tb_lits
   const int32_t* tb_lits;   // literal id | window offset << 22 (as gram_lits)
   int teddy_on;
+  // per bucket entry (gram_lits / tb_lits order): {fingerprint, mask} of the literal's bytes in the 4
+  // text positions before and the 4 after the indexed window (models/compiled.py _fingerprint)
+  const uint64_t* gram_fp = nullptr;
+  const uint64_t* tb_fp = nullptr;
 };
 
 // gram_lits entry: literal id | (offset of the indexed window inside the literal << 22)
@@ -302,7 +306,7 @@ LP_HD int64_t locate_line(const int64_t* ls, int64_t n, const int32_t* blk, int6
   return lo;
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP__)
 // 16 bytes starting at p (any alignment) from two aligned vector loads + byte funnel shifts
 __device__ __forceinline__ void load16u(const uint8_t* p, uint32_t out[4]) {
   const int sh = (int)((uintptr_t)p & 15);

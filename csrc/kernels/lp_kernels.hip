@@ -236,39 +236,57 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
   const int64_t stride = (int64_t)gridDim.x * HITS_PER_BLOCK;
   for (int64_t base = (int64_t)blockIdx.x * HITS_PER_BLOCK; base < n; base += stride) {
     const int64_t i = base + sub;
-    if (i < n && (ghits[i] & 3) == 3) {          // short-literal tier: every literal of the buckets
-      const int64_t p = ghits[i] >> 2;
-      uint32_t m = teddy_mask(T, text, nbytes, p);
+    if (i < n) {
+      const int64_t h = ghits[i];
+      const int64_t p = h >> 2;
+      const bool td = (h & 3) == 3;
+      const int G = td ? 3 : 2 + (int)(h & 3);
+      // the 16 text bytes [p - 4, p + 12), lower-cased: window + the fingerprint context of every
+      // literal of the bucket (4 bytes before, 4 after the window)
+      uint32_t a[4];
+      if (p >= 4) {
+        load16u(text + p - 4, a);
+      } else {
+        for (int k = 0; k < 4; ++k) {
+          uint32_t v = 0;
+          for (int b = 3; b >= 0; --b) {
+            const int64_t x = p - 4 + 4 * k + b;
+            v = (v << 8) | (x >= 0 ? (uint32_t)text[x] : 0u);
+          }
+          a[k] = v;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = lower4(a[k]);
+      const uint64_t t8 = (uint64_t)a[0] |
+                          ((uint64_t)(G == 4 ? a[2] : __builtin_amdgcn_alignbyte(a[2], a[1], G)) << 32);
       int64_t line = -1;
-      while (m) {
-        const int b = __ffs(m) - 1;
-        m &= m - 1;
-        for (int j = T.tb_off[b] + lane; j < T.tb_off[b + 1]; j += PV_LANES) {
-          const int32_t e = T.tb_lits[j];
+      // one bucket (bloom tier) or the buckets of a Teddy mask: entries [j0, j1) of ents / fps
+      auto walk = [&](const int32_t* ents, const uint64_t* fps, int j0, int j1) {
+        for (int j = j0 + lane; j < j1; j += PV_LANES) {
+          const uint4 f = *reinterpret_cast<const uint4*>(fps + 2 * j);    // {fingerprint, mask}
+          const uint64_t fp = (uint64_t)f.x | ((uint64_t)f.y << 32), fm = (uint64_t)f.z | ((uint64_t)f.w << 32);
+          if ((t8 ^ fp) & fm) continue;            // a context byte differs: not this literal
+          const int32_t e = ents[j];
           if (!pf_lit_at(T, text, nbytes, p, e)) continue;
           const int lit = pf_entry_lit(e);
           if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
           if (line < 0) line = 0;
-          for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r)
-            app(((int64_t)T.lit_reg[r] << 32) | line);
+          for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r) app(((int64_t)T.lit_reg[r] << 32) | line);
         }
-      }
-    } else if (i < n) {
-      const int64_t h = ghits[i];
-      const int64_t p = h >> 2;
-      const int G = 2 + (int)(h & 3);
-      uint32_t g4 = 0;
-      for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
-      int s, c;
-      pf_bucket(T, g4 & gram_mask(G), G, s, c);
-      int64_t line = -1;
-      for (int j = lane; j < c; j += PV_LANES) {
-        const int32_t e = T.gram_lits[s + j];
-        if (!pf_lit_at(T, text, nbytes, p, e)) continue;
-        const int lit = pf_entry_lit(e);
-        if (line < 0) line = locate_line(line_start, nlines, blk_line, p);
-        if (line < 0) line = 0;
-        for (int r = T.lit_reg_off[lit]; r < T.lit_reg_off[lit + 1]; ++r) app(((int64_t)T.lit_reg[r] << 32) | line);
+      };
+      if (td) {                                    // short-literal tier: every literal of the buckets
+        const uint32_t b1 = p + 1 < nbytes ? (a[1] >> 8) & 0xFF : 0u, b2 = p + 2 < nbytes ? (a[1] >> 16) & 0xFF : 0u;
+        uint32_t m = T.teddy[4 * (a[1] & 0xFF)] & T.teddy[4 * b1 + 1] & T.teddy[4 * b2 + 2];
+        while (m) {
+          const int b = __ffs(m) - 1;
+          m &= m - 1;
+          walk(T.tb_lits, T.tb_fp, T.tb_off[b], T.tb_off[b + 1]);
+        }
+      } else {
+        int s0, c;
+        pf_bucket(T, a[1] & gram_mask(G), G, s0, c);
+        walk(T.gram_lits, T.gram_fp, s0, s0 + c);
       }
     }
     __syncthreads();
@@ -278,121 +296,6 @@ __global__ __launch_bounds__(256) void k_pf_verify(const int64_t* __restrict__ g
   __syncthreads();
   const int c = *reinterpret_cast<volatile int*>(&cnt);
   if (c > 0) pf_flush(buf, &cnt, &gbase, c, cand, cap, count);
-}
-
-// K3a'' (default): the same verification, load-balanced inside each wave. Bucket sizes are skewed
-// (a 4-gram shared by 186 literals next to buckets of 1-3: profiles/r3_k), so a lane group per gram
-// hit made every block wait, at its barrier, for its largest bucket walked 4 literals at a time. Here
-// a wave takes 64 gram hits, prefix-sums their bucket sizes and then checks 64 (hit, literal) pairs
-// per iteration -- a 186-literal bucket costs 3 iterations of one wave -- and appends its candidates
-// with one atomic per iteration (wave prefix sum of the per-lane region counts). No block barrier.
-constexpr int PVW_WAVES = 4;
-
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
-  return v;
-}
-
-__global__ __launch_bounds__(64 * PVW_WAVES) void k_pf_verify_wave(const int64_t* __restrict__ ghits, int64_t n,
-                                                                   const unsigned long long* __restrict__ dn,
-                                                                   const uint8_t* __restrict__ text, int64_t nbytes,
-                                                                   PfTables T, const int64_t* __restrict__ line_start,
-                                                                   int64_t nlines, const int32_t* __restrict__ blk_line,
-                                                                   int64_t* cand, int64_t cap,
-                                                                   unsigned long long* count) {
-  __shared__ int s_incl[PVW_WAVES][64];
-  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
-  if (dn) {
-    const int64_t d = (int64_t)*dn;
-    n = d < n ? d : n;
-  }
-  const int64_t nwaves = (int64_t)gridDim.x * PVW_WAVES;
-  for (int64_t chunk = ((int64_t)blockIdx.x * PVW_WAVES + w) * 64; chunk < n; chunk += nwaves * 64) {
-    // this lane's gram hit: position, tier, bucket (bloom: start in gram_lits; Teddy: bucket mask)
-    const int64_t i = chunk + lane;
-    int64_t p = 0;
-    int c = 0, sm = 0;
-    bool td = false;
-    if (i < n) {
-      const int64_t h = ghits[i];
-      p = h >> 2;
-      if ((h & 3) == 3) {
-        td = true;
-        const uint32_t m = teddy_mask(T, text, nbytes, p);
-        sm = (int)m;
-        for (uint32_t mm = m; mm; mm &= mm - 1) {
-          const int b = __ffs(mm) - 1;
-          c += T.tb_off[b + 1] - T.tb_off[b];
-        }
-      } else {
-        const int G = 2 + (int)(h & 3);
-        uint32_t g4 = 0;
-        for (int q = 3; q >= 0; --q) g4 = (g4 << 8) | (uint32_t)lower_byte(text[p + q]);
-        int st;
-        pf_bucket(T, g4 & gram_mask(G), G, st, c);
-        sm = st;
-      }
-    }
-    const int incl = wave_incl_scan(c, lane);
-    const int total = __shfl(incl, 63, 64);
-    s_incl[w][lane] = incl;
-    const int excl = incl - c;
-    for (int k0 = 0; k0 < total; k0 += 64) {
-      const int q = k0 + lane;
-      // owner = first lane whose inclusive count exceeds q
-      int o = 0;
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1)
-        if (s_incl[w][o + step - 1] <= q) o += step;
-      o = q < total ? o : lane;
-      const int64_t op = __shfl(p, o, 64);
-      const int osm = __shfl(sm, o, 64);
-      const bool otd = __shfl((int)td, o, 64) != 0;
-      const int k = q - __shfl(excl, o, 64);
-      int nr = 0, lit = 0;
-      int64_t line = 0;
-      if (q < total) {
-        int32_t e;
-        if (otd) {
-          int kk = k;
-          e = 0;
-          for (uint32_t mm = (uint32_t)osm; mm; mm &= mm - 1) {
-            const int b = __ffs(mm) - 1;
-            const int sz = T.tb_off[b + 1] - T.tb_off[b];
-            if (kk < sz) {
-              e = T.tb_lits[T.tb_off[b] + kk];
-              break;
-            }
-            kk -= sz;
-          }
-        } else {
-          e = T.gram_lits[osm + k];
-        }
-        if (pf_lit_at(T, text, nbytes, op, e)) {
-          lit = pf_entry_lit(e);
-          nr = T.lit_reg_off[lit + 1] - T.lit_reg_off[lit];
-          line = locate_line(line_start, nlines, blk_line, op);
-          if (line < 0) line = 0;
-        }
-      }
-      // one atomic per wave for this iteration's candidates
-      const int ri = wave_incl_scan(nr, lane);
-      const int rt = __shfl(ri, 63, 64);
-      if (rt == 0) continue;
-      unsigned long long base = 0;
-      if (lane == 0) base = atomicAdd(count, (unsigned long long)rt);
-      base = __shfl(base, 0, 64);
-      const int r0 = T.lit_reg_off[lit];
-      for (int j = 0; j < nr; ++j) {
-        const unsigned long long slot = base + (unsigned long long)(ri - nr + j);
-        if ((int64_t)slot < cap) cand[slot] = ((int64_t)T.lit_reg[r0 + j] << 32) | line;
-      }
-    }
-  }
 }
 
 // K3c: regexes without a usable literal: every line x every scan regex
@@ -511,18 +414,6 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn, int max_grid) {
   if (n <= 0) return;
-  static const bool lane_groups = [] {   // LP_PF_VERIFY=lanes: the lane-group kernel (A/B)
-    const char* e = getenv("LP_PF_VERIFY");
-    return e && std::string(e) == "lanes";
-  }();
-  if (!lane_groups) {
-    const int64_t need = (n + 64 * PVW_WAVES - 1) / (64 * PVW_WAVES);
-    const int g = dn ? (int)std::min<int64_t>(need, std::max(1, max_grid)) : (int)std::max<int64_t>(1, need);
-    hipLaunchKernelGGL(k_pf_verify_wave, dim3(g), dim3(64 * PVW_WAVES), 0, as_stream(stream), ghits, n, dn, text, nbytes,
-                       T, line_start, nlines, blk_line, cand, cap, count);
-    LP_CHECK(hipGetLastError());
-    return;
-  }
   // with a device-side count the grid is sized for the buffer but capped (grid-stride loop)
   const int lanes = nbytes >= (int64_t(64) << 20) ? 4 : 16;
   const int64_t need = (n + 256 / lanes - 1) / (256 / lanes);   // blocks for one pass over n hits

@@ -22,7 +22,7 @@ from __future__ import annotations
 
 import logging
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -112,6 +112,36 @@ def _choose_grams(lits: List[bytes], stride: int = 1) -> List[List[Tuple[int, in
             used[(key, g)] = used.get((key, g), 0) + 1
             ents.append((key, g, off))
         out.append(ents)
+    return out
+
+
+def _fingerprint(lit: bytes, off: int, g: int) -> Tuple[int, int]:
+    """(fingerprint, mask) of one indexed window: the literal's (lower-cased) bytes in the 4 text
+    positions before the window (low 32 bits) and the 4 after it (high 32 bits), where the literal
+    has them. The device verify compares these 8 text bytes -- loaded once per gram hit -- against
+    every literal of the bucket with ONE contiguous 16-byte load per literal, and walks the literal
+    itself (3 dependent loads) only when they agree (k_pf_verify)."""
+    fp = mask = 0
+    for k in range(4):                     # text byte p - 4 + k  <->  literal byte off - 4 + k
+        i = off - 4 + k
+        if 0 <= i < len(lit):
+            fp |= lit[i] << (8 * k)
+            mask |= 0xFF << (8 * k)
+    for k in range(4):                     # text byte p + g + k  <->  literal byte off + g + k
+        i = off + g + k
+        if i < len(lit):
+            fp |= lit[i] << (32 + 8 * k)
+            mask |= 0xFF << (32 + 8 * k)
+    return fp, mask
+
+
+def _fingerprints(entries: Sequence[int], lits: List[bytes], g_of) -> np.ndarray:
+    """uint64 [2 x len(entries)]: (fingerprint, mask) per bucket entry (literal id | offset << 22)."""
+    out = np.zeros(2 * max(len(entries), 1), np.uint64)
+    for j, e in enumerate(entries):
+        lit = lits[e & ((1 << LIT_OFF_SHIFT) - 1)]
+        fp, mask = _fingerprint(lit, e >> LIT_OFF_SHIFT, g_of(lit))
+        out[2 * j], out[2 * j + 1] = np.uint64(fp), np.uint64(mask)
     return out
 
 
@@ -636,7 +666,10 @@ class CompiledLibrary:
             ht_val[h] = len(gram_lits)
             ht_cnt[h] = len(ids)
             gram_lits.extend(ids)
+        gram_fp = _fingerprints(gram_lits, lits, lambda lit: min(4, len(lit)))
+        tb_fp = _fingerprints([int(x) for x in tb_lits[:int(tb_off[-1])]], lits, lambda lit: 3)
         self.pf = dict(bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
+                       gram_fp=gram_fp, tb_fp=tb_fp,
                        gram_lits=np.array(gram_lits or [0], np.int32), lit_off=lit_off, lit_bytes=lit_bytes,
                        lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, stride=stride,
                        teddy=teddy, tb_off=tb_off, tb_lits=tb_lits, teddy_lits=len(short))
@@ -655,11 +688,13 @@ class CompiledLibrary:
         pf = self.pf
         t["pf_arrays"] = [T(pf["bloom"]), T(pf["ht_key"].view(np.int64)), T(pf["ht_val"]), T(pf["ht_cnt"]),
                           T(pf["gram_lits"]), T(pf["lit_off"]), T(pf["lit_bytes"]), T(pf["lit_reg_off"]),
-                          T(pf["lit_reg"]), T(pf["teddy"]), T(pf["tb_off"]), T(pf["tb_lits"])]
+                          T(pf["lit_reg"]), T(pf["teddy"]), T(pf["tb_off"]), T(pf["tb_lits"]),
+                          T(pf["gram_fp"].view(np.int64)), T(pf["tb_fp"].view(np.int64))]
         a = t["pf_arrays"]
         t["pf"] = (a[0].data_ptr(), pf["bits"], a[1].data_ptr(), a[2].data_ptr(), a[3].data_ptr(), pf["ht_mask"],
                    a[4].data_ptr(), a[5].data_ptr(), a[6].data_ptr(), a[7].data_ptr(), a[8].data_ptr(), pf["gmask"],
-                   pf["stride"], a[9].data_ptr(), a[10].data_ptr(), a[11].data_ptr(), 1 if pf["teddy_lits"] else 0)
+                   pf["stride"], a[9].data_ptr(), a[10].data_ptr(), a[11].data_ptr(), 1 if pf["teddy_lits"] else 0,
+                   a[12].data_ptr(), a[13].data_ptr())
         t["dfa_arrays"] = [T(self.dfa_meta), T(self.dfa_bytemap), T(self.dfa_trans.view(np.int16)), T(self.dfa_acc),
                            T(self.bpg_pool.view(np.int64))]
         d = t["dfa_arrays"]

@@ -271,3 +271,41 @@ def test_host_prefilter_simd_teddy_equals_exact_literal_search():
             if lit in low:
                 want.update((r << 32) | x for r in regs)
     assert got == want and len(want) > 100
+
+
+def test_fingerprints_never_reject_an_occurrence():
+    """k_pf_verify skips a bucket literal when the 8 text bytes around the window (4 before, 4
+    after, lower-cased) disagree with its fingerprint under its mask: every true occurrence of
+    every literal must pass, for both tiers (bloom windows g = 4, Teddy windows g = 3)."""
+    import random
+    import numpy as np
+    from log_parser_amd.models.compiled import CompiledLibrary, LIT_OFF_SHIFT
+    from log_parser_amd.utils.config import ScoringParams
+    from log_parser_amd.utils.synth import realistic_library
+    sets, _ = realistic_library(300, seed=3)
+    lib = CompiledLibrary(sets, ScoringParams())
+    pf = lib.pf
+    rng = random.Random(1)
+
+    def t8_at(text: bytes, p: int, g: int) -> int:
+        low = bytes(text).lower()
+        before = sum((low[p - 4 + k] if p - 4 + k >= 0 else 0) << (8 * k) for k in range(4))
+        after = sum((low[p + g + k] if p + g + k < len(low) else 0) << (8 * k) for k in range(4))
+        return before | (after << 32)
+
+    def check(ents, fps, g_of):
+        n = 0
+        for j, e in enumerate(ents):
+            lit = lib.literals[int(e) & ((1 << LIT_OFF_SHIFT) - 1)]
+            off = int(e) >> LIT_OFF_SHIFT
+            pre = bytes(rng.choice(b"abc xyZ09:") for _ in range(rng.randint(0, 9)))
+            text = pre + lit.upper() if rng.random() < 0.5 else pre + lit
+            text += bytes(rng.choice(b"qrs_ 7") for _ in range(rng.randint(0, 9)))
+            t8 = t8_at(text, len(pre) + off, g_of(lit))
+            fp, mask = int(fps[2 * j]), int(fps[2 * j + 1])
+            assert (t8 ^ fp) & mask == 0, (lit, off)
+            n += mask != 0
+        return n
+    assert check(pf["gram_lits"], pf["gram_fp"], lambda lit: min(4, len(lit))) > 100
+    ntb = int(pf["tb_off"][-1])
+    check(pf["tb_lits"][:ntb], pf["tb_fp"], lambda lit: 3)

@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--parse-requests", type=int, default=300,
                     help="rank 0: p50 latency of N single 10k-line POST /parse requests after the timed loop (0 = off)")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="server front end for p50")
+    ap.add_argument("--server-env", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra environment of the /parse server process only (A/B knob, repeatable)")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
     ap.add_argument("--d2h-stream", default="copy", choices=["copy", "compute"],
@@ -96,7 +98,8 @@ def main():
     if rank == 0 and args.parse_requests > 0:
         from log_parser_amd.utils import restbench
         dev = "cpu" if args.device == "cpu" else f"cuda:{local_rank}"
-        server = restbench.ServerProcess(restbench.write_library(sets), dev, http=args.http)
+        server = restbench.ServerProcess(restbench.write_library(sets), dev, http=args.http,
+                                         env=dict(kv.split("=", 1) for kv in args.server_env))
     try:
         run(args, sets, trig, rank, world, local_rank, server, hw_queues)
     finally:

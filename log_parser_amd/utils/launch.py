@@ -32,9 +32,12 @@ def ensure_hw_queues(n: int = HW_QUEUES) -> int:
     processes (ranks, the server) inherit the setting. Returns the value in effect.
     """
     try:
+        n = int(os.environ.get("LP_HW_QUEUES", n))     # LP_HW_QUEUES=0: leave HIP's setting alone (A/B)
         cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
     except ValueError:
         cur = 0
+    if n <= 0:
+        return cur
     if cur < n:
         os.environ["GPU_MAX_HW_QUEUES"] = str(n)
         cur = n

@@ -85,13 +85,14 @@ class RawClient:
 
 class ServerProcess:
     def __init__(self, pattern_dir: str, device: str, http: str = "native", extra: Sequence[str] = (),
-                 log_path: Optional[str] = None):
+                 log_path: Optional[str] = None, env: Optional[dict] = None):
         self.port = free_port()
         self.log = open(log_path, "wb") if log_path else subprocess.DEVNULL
         cmd = [sys.executable, "-m", "log_parser_amd.serve", f"-Dpattern.directory={pattern_dir}",
                f"-Dengine.device={device}", "-Dserver.host=127.0.0.1", f"-Dserver.port={self.port}",
                f"-Dserver.http={http}"] + list(extra)
-        self.proc = subprocess.Popen(cmd, cwd=ROOT, stdout=self.log, stderr=self.log)
+        self.proc = subprocess.Popen(cmd, cwd=ROOT, stdout=self.log, stderr=self.log,
+                                     env=None if not env else {**os.environ, **env})
         self.conn: Optional[http.client.HTTPConnection] = None
 
     def wait_ready(self, timeout_s: float = 240.0) -> bool:

@@ -1,9 +1,10 @@
 // K1 line index (reference: Java logs.split("\\r?\\n"), AnalysisService.java:53): line starts and
-// lengths straight from the bytes, two reads of the text and ONE host read.
+// lengths straight from the bytes, ONE read of the text (+ its 1/8-size newline bitmask) and ONE
+// host read.
 //
-//   k_nl_count   per 16 KiB tile: number of '\n' (one dwordx4-wide pass, memory-bound)
+//   k_nl_count   per 16 KiB tile: number of '\n' + a 1-bit-per-byte '\n' mask + a "\r\n" flag
 //   rocprim      exclusive scan of the tile counts (decoupled look-back over ~80k counts)
-//   k_nl_lines   per tile again: every '\n' at p with global index g writes starts[g+1] = p + 1
+//   k_nl_lines   per tile again, from the mask (text only in "\r\n" tiles): every '\n' at p with global index g writes starts[g+1] = p + 1
 //                and, when the previous '\n' is in the same tile, lens[g] = (p minus a '\r' right
 //                before it) - start; staged in LDS, stored coalesced. The tile's FIRST line end is
 //                recorded (fix_g, fix_end) for
@@ -69,37 +70,69 @@ __device__ __forceinline__ int li_masks(const uint8_t* __restrict__ text, int64_
   return c;
 }
 
+// bits 7, 15, 23, 31 of x -> bits 0..3
+__device__ __forceinline__ uint32_t li_pack4(uint32_t x) {
+  const uint32_t y = x >> 7;                      // bits 0, 8, 16, 24
+  const uint32_t z = (y | (y >> 7)) & 0x00030003u; // bits 0, 1, 16, 17
+  return (z | (z >> 14)) & 0xFu;
+}
+
+// Pass 1: per 16 KiB tile the '\n' count, and per lane (64 bytes) a 64-bit '\n' bitmask -- the
+// second pass reads these 2 KiB per tile instead of the tile's 16 KiB of text. A tile holding a
+// "\r\n" (a '\r' right before one of its '\n', possibly the previous tile's last byte) is flagged:
+// only those tiles (CRLF logs) are read again as text to strip the '\r'.
 __global__ __launch_bounds__(LI_THREADS) void k_nl_count(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                         int32_t* __restrict__ cnt) {
+                                                         int32_t* __restrict__ cnt, uint64_t* __restrict__ nlm,
+                                                         int32_t* __restrict__ crf) {
   const int64_t base = (int64_t)blockIdx.x * LI_TILE + (int64_t)threadIdx.x * LI_BYTES_PER_THREAD;
-  int c = 0;
+  uint64_t m64 = 0;
+  int crnl = 0;
   if (base < nbytes) {
     const uint4* p = reinterpret_cast<const uint4*>(text + base);
-    if (base + LI_BYTES_PER_THREAD <= nbytes) {
+    uint32_t carry = 0;                           // '\r' in the previous word's last byte
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint4 v = p[k];
-        c += __popc(li_zero_bytes(v.x ^ 0x0A0A0A0Au)) + __popc(li_zero_bytes(v.y ^ 0x0A0A0A0Au)) +
-             __popc(li_zero_bytes(v.z ^ 0x0A0A0A0Au)) + __popc(li_zero_bytes(v.w ^ 0x0A0A0A0Au));
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = p[k];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t nl = li_zero_bytes(w[q] ^ 0x0A0A0A0Au);
+        const uint32_t cr = li_zero_bytes(w[q] ^ 0x0D0D0D0Du);
+        crnl |= (int)(((cr << 8) | carry) & nl);
+        carry = cr >> 24;                         // bit 7 <- '\r' in byte 3
+        m64 |= (uint64_t)li_pack4(nl) << (4 * (4 * k + q));
       }
-    } else {
-      uint32_t m[16], cr[16];
-      c = li_masks(text, nbytes, base, m, cr);
     }
+    const int64_t valid = nbytes - base;
+    if (valid < 64) m64 &= (1ull << valid) - 1ull;
+    if ((m64 & 1ull) && base > 0 && text[base - 1] == '\r') crnl = 1;
   }
+  nlm[(int64_t)blockIdx.x * LI_THREADS + threadIdx.x] = m64;
+  int c = __popcll(m64);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  const bool anycr = __ballot(crnl != 0) != 0;
   __shared__ int ws[LI_THREADS / 64];
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __shared__ int wcr[LI_THREADS / 64];
+  if ((threadIdx.x & 63) == 0) {
+    ws[threadIdx.x >> 6] = c;
+    wcr[threadIdx.x >> 6] = anycr ? 1 : 0;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int t = 0;
-    for (int w = 0; w < LI_THREADS / 64; ++w) t += ws[w];
+    int t = 0, f = 0;
+    for (int w = 0; w < LI_THREADS / 64; ++w) {
+      t += ws[w];
+      f |= wcr[w];
+    }
     cnt[blockIdx.x] = t;
+    crf[blockIdx.x] = f;
   }
 }
 
 __global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                         const uint64_t* __restrict__ nlm,
+                                                         const int32_t* __restrict__ crf,
                                                          const int64_t* __restrict__ off,
                                                          int64_t* __restrict__ starts, int32_t* __restrict__ lens,
                                                          int64_t cap, int64_t* __restrict__ fix_g,
@@ -113,8 +146,18 @@ __global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restri
   const int64_t tile = blockIdx.x;
   const int64_t tbase = tile * LI_TILE;
   const int64_t base = tbase + (int64_t)threadIdx.x * LI_BYTES_PER_THREAD;
-  uint32_t m[16], cr[16];
-  const int c = li_masks(text, nbytes, base, m, cr);
+  // this lane's 64 bytes as bitmasks: '\n' from pass 1; '\r' before a '\n' (bit b: byte b - 1 is
+  // '\r') only in flagged tiles, which are read as text again
+  uint64_t m64 = nlm[tile * LI_THREADS + threadIdx.x], crb = 0;
+  if (crf[tile] && base < nbytes) {
+    uint32_t m[16], cr[16];
+    li_masks(text, nbytes, base, m, cr);
+    uint64_t c64 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c64 |= (uint64_t)li_pack4(cr[k]) << (4 * k);
+    crb = (c64 << 1) | ((base > 0 && text[base - 1] == '\r') ? 1ull : 0ull);
+  }
+  const int c = __popcll(m64);
   int incl = c;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -133,25 +176,18 @@ __global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restri
   // line holding its first byte is the number of '\n' before it
   if (blk && lane == 0 && tile * NW + wid < nblk) blk[tile * NW + wid] = (int32_t)(excl + woff);
   const bool staged = tot <= LI_STAGE;            // block-uniform
-  const uint32_t cr0 = (m[0] & 0x80u) && base > 0 && text[base - 1] == '\r';
   // pass A: every '\n' -> (start of the next line, end of its own line)
   int o = woff + (incl - c);                      // tile-local index of this lane's first '\n'
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    uint32_t mm = m[k];
-    const uint32_t crb = (cr[k] << 8) | ((k > 0 ? (cr[k - 1] >> 31) : cr0) << 7);   // '\r' before byte j -> bit 8j+7
-    while (mm) {
-      const int b = __ffs(mm) - 1;                // bit 7, 15, 23 or 31
-      const int64_t pos = base + 4 * k + (b >> 3);
-      if (staged) {
-        s_start[o] = (int32_t)(pos + 1 - tbase);
-        s_end[o] = (int32_t)(pos - (int64_t)((crb >> b) & 1u) - tbase);
-      } else if (excl + o + 1 < cap) {
-        starts[excl + o + 1] = pos + 1;
-      }
-      ++o;
-      mm &= mm - 1;
+  for (uint64_t mm = m64; mm; mm &= mm - 1) {
+    const int b = __ffsll((unsigned long long)mm) - 1;
+    const int64_t pos = base + b;
+    if (staged) {
+      s_start[o] = (int32_t)(pos + 1 - tbase);
+      s_end[o] = (int32_t)(pos - (int64_t)((crb >> b) & 1ull) - tbase);
+    } else if (excl + o + 1 < cap) {
+      starts[excl + o + 1] = pos + 1;
     }
+    ++o;
   }
   __syncthreads();
   if (staged) {
@@ -168,23 +204,17 @@ __global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restri
   } else {
     // pass B (a tile with more lines than the stage): lengths from the starts just stored
     o = woff + (incl - c);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      uint32_t mm = m[k];
-      const uint32_t crb = (cr[k] << 8) | ((k > 0 ? (cr[k - 1] >> 31) : cr0) << 7);
-      while (mm) {
-        const int b = __ffs(mm) - 1;
-        const int64_t end = base + 4 * k + (b >> 3) - (int64_t)((crb >> b) & 1u);
-        const int64_t g = excl + o;
-        if (o == 0) {
-          fix_g[tile] = g;
-          fix_end[tile] = end;
-        } else if (g < cap) {
-          lens[g] = (int32_t)(end - starts[g]);
-        }
-        ++o;
-        mm &= mm - 1;
+    for (uint64_t mm = m64; mm; mm &= mm - 1) {
+      const int b = __ffsll((unsigned long long)mm) - 1;
+      const int64_t end = base + b - (int64_t)((crb >> b) & 1ull);
+      const int64_t g = excl + o;
+      if (o == 0) {
+        fix_g[tile] = g;
+        fix_end[tile] = end;
+      } else if (g < cap) {
+        lens[g] = (int32_t)(end - starts[g]);
       }
+      ++o;
     }
   }
   if (tot == 0 && threadIdx.x == 0) fix_g[tile] = -1;
@@ -257,17 +287,19 @@ void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, i
   int64_t* fix_g = W.buf + W.ntiles_cap;
   int64_t* fix_end = W.buf + 2 * W.ntiles_cap;
   int32_t* cnt = reinterpret_cast<int32_t*>(W.buf + 3 * W.ntiles_cap);
-  void* tmp = W.buf + 4 * W.ntiles_cap;
+  int32_t* crf = cnt + W.ntiles_cap;               // the int64 slot region holds 2 x ntiles_cap int32
+  uint64_t* nlm = reinterpret_cast<uint64_t*>(W.buf + 4 * W.ntiles_cap);   // LI_THREADS words per tile
+  void* tmp = W.buf + (4 + LI_THREADS) * W.ntiles_cap;
   size_t tmp_bytes = 0;
   if (rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
           hipSuccess ||
       tmp_bytes > W.tmp_bytes)
     throw std::runtime_error("line_index: scan workspace too small");
-  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, cnt);
+  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, cnt, nlm, crf);
   if (rocprim::exclusive_scan(tmp, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
       hipSuccess)
     throw std::runtime_error("line_index: rocprim scan failed");
-  hipLaunchKernelGGL(k_nl_lines, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, off, starts, lens, cap,
+  hipLaunchKernelGGL(k_nl_lines, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, nlm, crf, off, starts, lens, cap,
                      fix_g, fix_end, blk, nblk);
   hipLaunchKernelGGL(k_line_fix, dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, st, nt, nbytes, fix_g, fix_end,
                      off, cnt, starts, lens, cap, info, blk, nblk);

@@ -38,19 +38,22 @@ def newline_positions(text: torch.Tensor, nbytes: int) -> torch.Tensor:
 
 
 class _LineIndexWs:
-    """Per (device, stream) scratch of the line index: tile counts + offsets and each tile's first
-    line end (k_line_fix), then the scan scratch. Grow-only; stream order makes reuse safe."""
+    """Per (device, stream) scratch of the line index: tile counts + offsets, "\\r\\n" flags and
+    each tile's first line end (k_line_fix), the per-tile newline bitmasks (256 words = 2 KiB per
+    16 KiB tile), then the scan scratch. Grow-only; stream order makes reuse safe."""
     SCAN_TMP = 1 << 20           # bytes of rocprim scan scratch (csrc/bind.cpp passes the same)
+    WORDS_PER_TILE = 4 + 256     # int64 words per tile (csrc/kernels/line_index.hip line_index_dev)
     _all: dict = {}
 
     @classmethod
     def get(cls, text: torch.Tensor, ntiles: int) -> Tuple[int, int]:
         key = (text.device, _s(text))
         buf = cls._all.get(key)
-        if buf is None or buf.numel() < 4 * ntiles + cls.SCAN_TMP // 8:
+        w = cls.WORDS_PER_TILE
+        if buf is None or buf.numel() < w * ntiles + cls.SCAN_TMP // 8:
             cap = max(ntiles * 5 // 4, 1024)
-            buf = cls._all[key] = torch.empty(4 * cap + cls.SCAN_TMP // 8, dtype=torch.int64, device=text.device)
-        return buf.data_ptr(), (buf.numel() - cls.SCAN_TMP // 8) // 4
+            buf = cls._all[key] = torch.empty(w * cap + cls.SCAN_TMP // 8, dtype=torch.int64, device=text.device)
+        return buf.data_ptr(), (buf.numel() - cls.SCAN_TMP // 8) // w
 
 
 # lines per byte seen so far (grows only): capacity of the line index outputs, so the one-pass
@@ -92,7 +95,7 @@ def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Te
     """Java ``logs.split("\\\\r?\\\\n")`` line index (AnalysisService.java:53).
 
     Returns (line_start int64[L], line_len int32[L]); trailing empty lines removed; input
-    without any newline is one line (possibly empty). GPU: two reads of the text, five small
+    without any newline is one line (possibly empty). GPU: one read of the text + its newline bitmask, five small
     launches, one 24-byte host read (csrc/kernels/line_index.hip).
     """
     dev = text.device

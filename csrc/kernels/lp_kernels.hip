@@ -102,7 +102,10 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
 //     occurrence still has exactly one indexed window starting there.
 //   short-literal tier (TD): Teddy byte-position masks. One 16-byte LDS read per text byte gives
 //     (M0, M1, M2)[byte]; the rolling AND of three consecutive reads is the bucket mask of a 3-byte
-//     window. 18 reads per 16-byte unit, ~5 VALU per position, no hashing.
+//     window. 18 reads per 16-byte unit, ~5 VALU per position, no hashing. (A/B, profiles/r3_p:
+//     a 4 KiB bloom of 3-byte windows tested at every position -- 4-byte reads, 4.5x less LDS
+//     traffic -- was SLOWER, 824 -> 933 us per 1.33 GB: the hash multiply and bit math per
+//     position outweigh the wider reads.)
 template <int GM, int S, int PF_UNROLL, bool TD>
 __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,

@@ -135,12 +135,13 @@ def _fingerprint(lit: bytes, off: int, g: int) -> Tuple[int, int]:
     return fp, mask
 
 
-def _fingerprints(entries: Sequence[int], lits: List[bytes], g_of) -> np.ndarray:
-    """uint64 [2 x len(entries)]: (fingerprint, mask) per bucket entry (literal id | offset << 22)."""
+def _fingerprints(entries: Sequence[int], lits: List[bytes], gs: Sequence[int]) -> np.ndarray:
+    """uint64 [2 x len(entries)]: (fingerprint, mask) per bucket entry (literal id | offset << 22)
+    whose indexed window is gs[j] bytes long."""
     out = np.zeros(2 * max(len(entries), 1), np.uint64)
     for j, e in enumerate(entries):
         lit = lits[e & ((1 << LIT_OFF_SHIFT) - 1)]
-        fp, mask = _fingerprint(lit, e >> LIT_OFF_SHIFT, g_of(lit))
+        fp, mask = _fingerprint(lit, e >> LIT_OFF_SHIFT, gs[j])
         out[2 * j], out[2 * j + 1] = np.uint64(fp), np.uint64(mask)
     return out
 
@@ -650,6 +651,8 @@ class CompiledLibrary:
                 gmask |= 1 << g
         bits = BLOOM_BITS
         bloom = np.zeros((1 << bits) // 32, np.uint32)
+        for key, g in grams:
+            bloom[bloom_word(key, g, bits)] |= np.uint32(bloom_bits2(key, g))
         H = 16
         while H < 2 * max(1, len(grams)):
             H *= 2
@@ -657,8 +660,8 @@ class CompiledLibrary:
         ht_val = np.zeros(H, np.int32)
         ht_cnt = np.zeros(H, np.int32)
         gram_lits: List[int] = []
+        gram_g: List[int] = []
         for (key, g), ids in grams.items():
-            bloom[bloom_word(key, g, bits)] |= np.uint32(bloom_bits2(key, g))
             h = ht_hash(key, g) & (H - 1)
             while ht_key[h] != np.uint64(0xFFFFFFFFFFFFFFFF):
                 h = (h + 1) & (H - 1)
@@ -666,9 +669,11 @@ class CompiledLibrary:
             ht_val[h] = len(gram_lits)
             ht_cnt[h] = len(ids)
             gram_lits.extend(ids)
-        gram_fp = _fingerprints(gram_lits, lits, lambda lit: min(4, len(lit)))
-        tb_fp = _fingerprints([int(x) for x in tb_lits[:int(tb_off[-1])]], lits, lambda lit: 3)
-        self.pf = dict(bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
+            gram_g.extend([g] * len(ids))
+        gram_fp = _fingerprints(gram_lits, lits, gram_g)
+        ntb = int(tb_off[-1])
+        tb_fp = _fingerprints([int(x) for x in tb_lits[:ntb]], lits, [3] * ntb)
+        self.pf = dict(gram_g=np.array(gram_g or [4], np.int32), bloom=bloom, bits=bits, ht_key=ht_key, ht_val=ht_val, ht_cnt=ht_cnt, ht_mask=H - 1,
                        gram_fp=gram_fp, tb_fp=tb_fp,
                        gram_lits=np.array(gram_lits or [0], np.int32), lit_off=lit_off, lit_bytes=lit_bytes,
                        lit_reg_off=lit_reg_off, lit_reg=lit_reg, gmask=gmask, stride=stride,

@@ -293,19 +293,20 @@ def test_fingerprints_never_reject_an_occurrence():
         after = sum((low[p + g + k] if p + g + k < len(low) else 0) << (8 * k) for k in range(4))
         return before | (after << 32)
 
-    def check(ents, fps, g_of):
+    def check(ents, fps, gs):
         n = 0
         for j, e in enumerate(ents):
             lit = lib.literals[int(e) & ((1 << LIT_OFF_SHIFT) - 1)]
             off = int(e) >> LIT_OFF_SHIFT
+            assert lit[off:off + gs[j]].lower() == lit[off:off + gs[j]]
             pre = bytes(rng.choice(b"abc xyZ09:") for _ in range(rng.randint(0, 9)))
             text = pre + lit.upper() if rng.random() < 0.5 else pre + lit
             text += bytes(rng.choice(b"qrs_ 7") for _ in range(rng.randint(0, 9)))
-            t8 = t8_at(text, len(pre) + off, g_of(lit))
+            t8 = t8_at(text, len(pre) + off, int(gs[j]))
             fp, mask = int(fps[2 * j]), int(fps[2 * j + 1])
             assert (t8 ^ fp) & mask == 0, (lit, off)
             n += mask != 0
         return n
-    assert check(pf["gram_lits"], pf["gram_fp"], lambda lit: min(4, len(lit))) > 100
+    assert check(pf["gram_lits"], pf["gram_fp"], pf["gram_g"]) > 100
     ntb = int(pf["tb_off"][-1])
-    check(pf["tb_lits"][:ntb], pf["tb_fp"], lambda lit: 3)
+    check(pf["tb_lits"][:ntb], pf["tb_fp"], [3] * ntb)

@@ -234,7 +234,7 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
 }
 
 // mode 0: cand[i] = -1 for BPG candidates that do not match (request path, k_cand_verify did the
-// DFA ones); mode 1: flag the first key of every sorted run whose regex is a BPG program that no
+// DFA ones); mode 2: the same, with the DFA candidates verified by the grid's upper half; mode 1: flag the first key of every sorted run whose regex is a BPG program that no
 // engine pre-verified (bulk path, k_dedupe_verify left the flag 0)
 template <int G, int MODE>
 __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, const uint64_t* __restrict__ keys,
@@ -243,13 +243,27 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
                                                   const int32_t* __restrict__ ll, DfaPool P,
                                                   uint8_t* __restrict__ flag) {
   const int lane = (int)(threadIdx.x & 63);
+  const int64_t n = (MODE != 1 && dcount) ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
+  if (MODE == 2 && blockIdx.x >= (gridDim.x >> 1)) {
+    // the grid's upper half: DFA candidates, one lane each (k_cand_verify's work), side by side
+    // with the BPG walks of the lower half -- one launch, and a request's critical path is the
+    // longer of the two instead of their sum
+    const int64_t j = (int64_t)(blockIdx.x - (gridDim.x >> 1)) * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const int64_t k = cand[j];
+    if (k < 0) return;
+    const int r = (int)(k >> 32);
+    if (is_bpg(P, r)) return;
+    const int64_t x = k & 0xFFFFFFFFll;
+    if (!dfa_run(P, r, text + ls[x], ll[x])) cand[j] = -1;
+    return;
+  }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = (MODE == 0 && dcount) ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
   int r = 0;
   int64_t x = 0;
   bool need = false;
   if (i < n) {
-    if (MODE == 0) {
+    if (MODE != 1) {
       const int64_t k = cand[i];
       if (k >= 0) {
         r = (int)(k >> 32);
@@ -292,7 +306,7 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
     const bool hit = bpg_coop_walk<G>(prog, s, len, valid);
     if (valid && (lane & (G - 1)) == 0) {
       const int64_t slot = (i - lane) + src;
-      if (MODE == 0) {
+      if (MODE != 1) {
         if (!hit) cand[slot] = -1;
       } else {
         flag[slot] = hit ? 1 : 0;
@@ -326,7 +340,7 @@ template <int MODE>
 void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigned long long* dcount, int lbits,
                  const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P, uint8_t* flag,
                  hipStream_t st) {
-  const dim3 grid(nblocks(cap)), block(256);
+  const dim3 grid(nblocks(cap) * (MODE == 2 ? 2 : 1)), block(256);
   switch (coop_group(P.bpg_widths)) {
     case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
     case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
@@ -392,6 +406,14 @@ void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, 
   }
   hipLaunchKernelGGL(k_bpg_cand_all, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text, ls, ll, P);
   check_launch("k_bpg_cand_all");
+}
+
+bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text,
+                         const int64_t* ls, const int32_t* ll, const DfaPool& P, uint64_t stream) {
+  if (!P.bpg_widths || cap <= 0 || walk_mode() == 1) return false;   // caller runs k_cand_verify
+  launch_coop<2>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, reinterpret_cast<hipStream_t>(stream));
+  check_launch("k_bpg_coop<cand+dfa>");
+  return true;
 }
 
 void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,

@@ -20,6 +20,10 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
 // verify of sorted keys (bulk path, flags), all-lines scan of literal-free programs
 void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text, const int64_t* ls,
                   const int32_t* ll, const DfaPool& P, uint64_t stream);
+// request path: DFA candidates (grid's upper half) and BPG candidates (lower half, cooperative walk)
+// verified in place by ONE launch; false (nothing launched) when the library has no BPG programs
+bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text,
+                         const int64_t* ls, const int32_t* ll, const DfaPool& P, uint64_t stream);
 void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
                     const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream);
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,

@@ -244,8 +244,8 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
         if use_cuda:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        ls, ll = K.split_lines(text, nbytes)
-        out = sa.step(text, nbytes, ls, ll, hl, hr, topk=args.topk, pack_events=True)
+        # line index + literal prefilter queued before the index's host read (sa.step builds both)
+        out = sa.step(text, nbytes, None, None, hl, hr, topk=args.topk, pack_events=True)
         events_to_host(out, b)                                   # results land on the host
         if rank == 0 and out.topk_rows is not None:
             state["top"] = out.topk_rows.cpu()                   # merged global top-k on the host

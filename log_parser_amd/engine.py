@@ -519,8 +519,15 @@ class Engine:
                            self._ev_tables(segs), self.ws)[0]
 
     # ------------------------------------------------------------------ core run
+    def prefilter_early(self, text, nbytes: int):
+        """Queue the literal prefilter before the line index reaches the host (bulk path; pass the
+        result to ``prepare(early=...)``). None when the matcher arena path does not apply."""
+        if not text.is_cuda or self.lib.host_regs or self.profile:
+            return None
+        return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid)
+
     def prepare(self, text, nbytes, ls, ll, segs: Segments, host_text=None,
-                timings: Optional[dict] = None) -> "Prepared":
+                timings: Optional[dict] = None, early=None) -> "Prepared":
         """Local phase: matching, hit CSR, events, in-batch frequency ranks, context features.
 
         Needs no global information, so the data-parallel path runs it before its collectives.
@@ -537,7 +544,7 @@ class Engine:
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
                 self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None,
-                side=self._side)
+                side=self._side, early=early)
         else:
             cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(

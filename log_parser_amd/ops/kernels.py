@@ -62,9 +62,11 @@ _LINES_PER_BYTE = [1.0 / 48]
 LINE_BLK_SHIFT = 12
 
 
-def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool):
+def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=None):
     """k_nl_count, rocprim scan, k_nl_lines, k_line_fix (+ k_line_trim): (starts, lens, n_newlines,
-    last_newline, kept, blk) with ONE host read; blk = the coarse 4 KiB block -> line index."""
+    last_newline, kept, blk) with ONE host read; blk = the coarse 4 KiB block -> line index.
+    ``before_read()`` runs once, after the launches and before that read: work it queues (the
+    literal prefilter, which needs no line index) runs on the GPU while the host waits."""
     dev = text.device
     nt = N.line_index_tiles(nbytes)
     cap = int(nbytes * _LINES_PER_BYTE[0] * 1.25) + 1024
@@ -77,7 +79,19 @@ def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool):
         wp, wcap = _LineIndexWs.get(text, nt)
         N.line_index_dev(text.data_ptr(), nbytes, wp, wcap, starts.data_ptr(), lens.data_ptr(), cap, info.data_ptr(),
                          trim, blk.data_ptr(), blk.numel(), _s(text))
-        n_nl, last, kept = info.tolist()
+        if before_read is not None:
+            # the counts travel to pinned memory behind the line index only; the host then waits
+            # for that copy, not for the work before_read() queued after it
+            hinfo = torch.empty(3, dtype=torch.int64, pin_memory=True)
+            hinfo.copy_(info, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record()
+            before_read()
+            before_read = None
+            done.synchronize()
+            n_nl, last, kept = hinfo.tolist()
+        else:
+            n_nl, last, kept = info.tolist()
         if n_nl + 1 <= cap:
             _LINES_PER_BYTE[0] = max(_LINES_PER_BYTE[0], (n_nl + 1) / max(nbytes, 1))
             return starts, lens, n_nl, last, kept, blk
@@ -91,7 +105,7 @@ def _with_blk(ls: torch.Tensor, blk: torch.Tensor, nbytes: int) -> torch.Tensor:
     return ls
 
 
-def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Tensor]:
+def split_lines(text: torch.Tensor, nbytes: int, before_read=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Java ``logs.split("\\\\r?\\\\n")`` line index (AnalysisService.java:53).
 
     Returns (line_start int64[L], line_len int32[L]); trailing empty lines removed; input
@@ -102,7 +116,7 @@ def split_lines(text: torch.Tensor, nbytes: int) -> Tuple[torch.Tensor, torch.Te
     if text.is_cuda:
         if nbytes == 0:
             return torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
-        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True)
+        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True, before_read=before_read)
         return _with_blk(starts[:L], blk, nbytes), lens[:L]
     nl = newline_positions(text, nbytes)
     if nl.numel() == 0:
@@ -395,8 +409,22 @@ class MatchArena:
             self.rate[k] = max(r, self.rate[k] if overflow else self.rate[k] * 0.5, 1e-4)
 
 
+class EarlyPrefilter:
+    """The literal prefilter launched before the line index is known on the host (it reads only
+    the text): gram hits + the arena counters, handed to ``match_and_hits``."""
+
+    def __init__(self, text, nbytes: int, tabs: dict, arena: "MatchArena", pf_grid: int):
+        L_est = int(nbytes * _LINES_PER_BYTE[0]) + 1
+        self.cap = arena.caps(L_est)["gram"]
+        self.gh = torch.empty(self.cap, dtype=torch.int64, device=text.device)
+        self.cnt = torch.zeros(5, dtype=torch.int64, device=text.device)
+        N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
+                        pf_grid, _s(text))
+
+
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
-                   ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None, side=None):
+                   ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None, side=None,
+                   early: Optional[EarlyPrefilter] = None):
     """GPU: every matcher appends to the arena, then the post-match hit pipeline reads the device
     counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read.
 
@@ -413,11 +441,15 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
         any(g.numel() for g in tabs["nfa_scan_lists"].values())
     while True:
         cap = arena.caps(L)
-        gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
+        if early is not None:            # prefilter already queued (behind the line index)
+            cap["gram"] = early.cap
+            gh, cnt = early.gh, early.cnt
+        else:
+            gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
+            # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters)
+            cnt = torch.zeros(5, dtype=torch.int64, device=dev)
         cand = torch.empty(cap["cand"], dtype=torch.int64, device=dev)
         ver = torch.empty(cap["ver"], dtype=torch.int64, device=dev)
-        # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters)
-        cnt = torch.zeros(5, dtype=torch.int64, device=dev)
         c0 = cnt.data_ptr()
         sst = st
         if side is not None and scans and tick is None:
@@ -440,8 +472,10 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
         elif tick:
             tick("scan")
         blk = line_block_index(line_start, nbytes)
-        N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L, gh.data_ptr(), cap["gram"],
-                        c0, pf_grid, st)
+        if early is None:
+            N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L, gh.data_ptr(), cap["gram"],
+                            c0, pf_grid, st)
+        early = None                     # an overflow re-run launches everything itself
         N.pf_verify_dev(gh.data_ptr(), cap["gram"], text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L,
                         blk.data_ptr(), cand.data_ptr(), cap["cand"], c0 + 8, st, c0,
                         max(16, min(8192, nbytes >> 13)))

@@ -168,17 +168,25 @@ class ShardedAnalyzer:
         self.slot_e0 = torch.from_numpy(e0).to(dev)
         self.slot_k = torch.from_numpy(kk).to(dev)
 
-    def step(self, text: torch.Tensor, nbytes: int, ls: torch.Tensor, ll: torch.Tensor,
+    def step(self, text: torch.Tensor, nbytes: int, ls: Optional[torch.Tensor], ll: Optional[torch.Tensor],
              halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False,
              pack_events: bool = False) -> StepOutput:
+        """One shard step. ``ls`` / ``ll`` = None: the line index is built here, with the literal
+        prefilter queued behind it before its host read (the GPU filters while the host waits)."""
         eng = self.engine
         lib = eng.lib
         rank, wsize = world()
         dev = text.device
+        early = None
+        if ls is None:
+            box = []
+            ls, ll = K.split_lines(text, nbytes, before_read=(lambda: box.append(eng.prefilter_early(text, nbytes)))
+                                   if text.is_cuda else None)
+            early = box[0] if box else None
         L = ls.numel()
         own_lo, own_hi = halo_left, L - halo_right
         segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev, upload=eng.upload)
-        prep = eng.prepare(text, nbytes, ls, ll, segs)
+        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
         ns = chain.numel()

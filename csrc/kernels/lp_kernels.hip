@@ -106,32 +106,41 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
 //     a 4 KiB bloom of 3-byte windows tested at every position -- 4-byte reads, 4.5x less LDS
 //     traffic -- was SLOWER, 824 -> 933 us per 1.33 GB: the hash multiply and bit math per
 //     position outweigh the wider reads.)
+//   Teddy table layout (profiles/r3_t PMC: the 4 KiB table read with ds_read_b128 at random byte
+//     values ran 8.2 bank-conflict cycles per LDS instruction, LDS-bound): 16 copies, entry c of
+//     copy j at 16-byte slot c * 16 + j, and lane l reads copy l & 15. A b128 read is serviced in
+//     four 16-lane groups over 16 slots of 16 B; the lanes of each group have distinct l & 15, so
+//     every group hits 16 distinct slots -- conflict-free for any bytes. 64 KiB of LDS: the TD
+//     variant runs 1024-thread blocks, one per CU.
+template <bool TD>
+constexpr int pf_threads() { return TD ? 1024 : PF_THREADS; }
+
 template <int GM, int S, int PF_UNROLL, bool TD>
-__global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
+__global__ __launch_bounds__(pf_threads<TD>()) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,
                                                           int64_t nlines, int64_t* cand, int64_t cap,
                                                           unsigned long long* count) {
-  // dynamic LDS: [bloom (1<<bits)/8 B, GM only][teddy 4 KiB, TD only][candidates PF_BUF x 8 B][cnt | pad | gbase]
+  // dynamic LDS: [bloom (1<<bits)/8 B, GM only][teddy 16 x 4 KiB, TD only][candidates PF_BUF x 8 B][cnt | pad | gbase]
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int bits = T.bloom_bits;
   const int nwords = GM ? (1 << bits) >> 5 : 0;
   uint32_t* bl = smem;
   uint32_t* td = smem + nwords;
-  int64_t* buf = reinterpret_cast<int64_t*>(td + (TD ? 1024 : 0));
+  int64_t* buf = reinterpret_cast<int64_t*>(td + (TD ? 16 * 1024 : 0));
   int* cnt = reinterpret_cast<int*>(buf + PF_BUF);
   unsigned long long* gbase = reinterpret_cast<unsigned long long*>(buf + PF_BUF + 1);
   for (int i = threadIdx.x * 4; i < nwords; i += blockDim.x * 4)
     *reinterpret_cast<uint4*>(bl + i) = *reinterpret_cast<const uint4*>(T.bloom + i);
   if constexpr (TD)
-    for (int i = threadIdx.x * 4; i < 1024; i += blockDim.x * 4)
-      *reinterpret_cast<uint4*>(td + i) = *reinterpret_cast<const uint4*>(T.teddy + i);
+    for (int i = threadIdx.x; i < 16 * 256; i += blockDim.x)   // slot i = entry i >> 4, copy i & 15
+      reinterpret_cast<uint4*>(td)[i] = reinterpret_cast<const uint4*>(T.teddy)[i >> 4];
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
   const LdsAppender app{buf, cnt, cand, cap, count};
   const int64_t nunits = (nbytes + 15) >> 4;
   constexpr bool g2 = GM & 4, g3 = GM & 8, g4on = GM & 16;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const uint4* tt = reinterpret_cast<const uint4*>(td);
+  const uint4* tt = reinterpret_cast<const uint4*>(td) + (threadIdx.x & 15);   // this lane's copy
   // one 16-byte unit: lower-case, test the grams / windows, stage the (rare) hits
   auto scan_unit = [&](int64_t p0, const uint4 v, const uint32_t nx) {
     const uint32_t w[5] = {lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w), lower4(nx)};
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
       uint32_t r0 = 0, r1 = 0, any = 0;
 #pragma unroll
       for (int k = 0; k < 18; ++k) {
-        const uint4 e = tt[(w[k >> 2] >> (8 * (k & 3))) & 0xFFu];
+        const uint4 e = tt[((w[k >> 2] >> (8 * (k & 3))) & 0xFFu) << 4];
         if (k >= 2) any |= r1 & e.z;           // window starting at k - 2 complete
         r1 = r0 & e.y;
         r0 = e.x;
@@ -168,7 +177,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_prefilter(const uint8_t* __restr
           const uint32_t b0 = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
           const uint32_t b1 = (w[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu;
           const uint32_t b2 = (w[(k + 2) >> 2] >> (8 * ((k + 2) & 3))) & 0xFFu;
-          if (tt[b0].x & tt[b1].y & tt[b2].z) hm |= 1u << k;
+          if (tt[b0 << 4].x & tt[b1 << 4].y & tt[b2 << 4].z) hm |= 1u << k;
         }
         hm &= valid;
         while (hm) {
@@ -369,11 +378,11 @@ static void launch_pf(int g, size_t lds, bool big, hipStream_t st, const uint8_t
                       const PfTables& T, const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
                       unsigned long long* count) {
   if (big)
-    hipLaunchKernelGGL((k_prefilter<GM, S, 4, TD>), dim3(g), dim3(PF_THREADS), lds, st, text, nbytes, T, line_start,
-                       nlines, cand, cap, count);
+    hipLaunchKernelGGL((k_prefilter<GM, S, 4, TD>), dim3(g), dim3(pf_threads<TD>()), lds, st, text, nbytes, T,
+                       line_start, nlines, cand, cap, count);
   else
-    hipLaunchKernelGGL((k_prefilter<GM, S, 1, TD>), dim3(g), dim3(PF_THREADS), lds, st, text, nbytes, T, line_start,
-                       nlines, cand, cap, count);
+    hipLaunchKernelGGL((k_prefilter<GM, S, 1, TD>), dim3(g), dim3(pf_threads<TD>()), lds, st, text, nbytes, T,
+                       line_start, nlines, cand, cap, count);
 }
 
 template <bool TD>
@@ -381,7 +390,7 @@ static void dispatch_pf(int g, bool big, hipStream_t st, const uint8_t* text, in
                         const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
                         unsigned long long* count) {
   const int gm = T.gmask & 28;
-  const size_t lds = (gm ? (size_t(1) << T.bloom_bits) / 8 : 0) + (TD ? 4096 : 0) + PF_BUF * 8 + 16;
+  const size_t lds = (gm ? (size_t(1) << T.bloom_bits) / 8 : 0) + (TD ? 16 * 4096 : 0) + PF_BUF * 8 + 16;
 #define LP_PF(GMV, SV) launch_pf<GMV, SV, TD>(g, lds, big, st, text, nbytes, T, line_start, nlines, cand, cap, count)
   if (gm == 16 && T.stride == 4) { LP_PF(16, 4); return; }
   if (gm == 16 && T.stride == 2) { LP_PF(16, 2); return; }
@@ -405,7 +414,8 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
   // large texts: 4 units per lane per iteration (bytes in flight); small requests: 1, so every
   // launched lane has work (latency)
   const bool big = nbytes >= (int64_t(32) << 20);
-  const int g = (int)std::min<int64_t>(grid, num_blocks(units, PF_THREADS * (big ? 4 : 1)));
+  const int threads = T.teddy_on ? pf_threads<true>() : pf_threads<false>();
+  const int g = (int)std::min<int64_t>(grid, num_blocks(units, threads * (big ? 4 : 1)));
   if (T.teddy_on)
     dispatch_pf<true>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
   else

@@ -16,7 +16,7 @@
 //               ScoringService.java:84-88); features only for covered lines (k_feat_cov, ContextAnalysisService.java:
 //               46-117 reads the 4 features of window lines only).
 //
-// The host twins below run the same element functions (the LP_HD helpers in this file) with
+// The host twins below run the same element functions (the LP_HD helpers of post_core.h) with
 // std::sort, so CPU tests exercise the GPU arithmetic and ordering rules.
 #include <hip/hip_runtime.h>
 
@@ -31,6 +31,7 @@
 #include "lp_api.h"
 #include "lp_core.h"
 #include "lp_host.h"
+#include "post_core.h"
 
 namespace lp {
 
@@ -50,63 +51,7 @@ int bits_for(int64_t n) {  // bits needed to hold values 0..n-1 (>= 1)
 }
 
 // ---------------------------------------------------------------------------------------------
-// element functions (host + device)
-
-// segment of local line x: the last segment whose first line is <= x (a document with zero kept
-// lines, e.g. "\n\n" under Java split, has lo == hi and is skipped by taking the last match)
-LP_HD int seg_of(const int32_t* lo, int nseg, int32_t x) {
-  int a = 0, b = nseg;
-  while (b - a > 1) {
-    const int m = (a + b) >> 1;
-    if (lo[m] <= x) a = m; else b = m;
-  }
-  return a;
-}
-
-LP_HD int64_t lower_bound64(const int64_t* a, int64_t n, int64_t v) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if (a[m] < v) lo = m + 1; else hi = m;
-  }
-  return lo;
-}
-
-LP_HD int64_t lower_bound_u32(const uint32_t* a, int64_t n, uint32_t v) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if (a[m] < v) lo = m + 1; else hi = m;
-  }
-  return lo;
-}
-
-// events a hit produces: one per pattern whose primary regex it is, on lines the segment owns
-LP_HD int64_t hit_event_count(const EvTables& E, int64_t key) {
-  const int r = (int)(key >> 32);
-  const int32_t x = (int32_t)(key & 0xFFFFFFFFll);
-  const int64_t c = E.prim_off[r + 1] - E.prim_off[r];
-  if (c == 0) return 0;
-  const int s = seg_of(E.seg_lo, E.nseg, x);
-  return (x >= E.own_lo[s] && x < E.own_hi[s]) ? c : 0;
-}
-
-// context window [a, b) of an event (AnalysisService.java:132-156 clipping; [x, x+1) when the
-// pattern has no context rules)
-LP_HD void event_window(const EvTables& E, int32_t x, int p, int s, int32_t& a, int32_t& b) {
-  const int32_t before = E.ctx_before[p], after = E.ctx_after[p];
-  if (before < 0) {
-    a = x;
-    b = x + 1;
-    return;
-  }
-  const int64_t aa = (int64_t)x - before, bb = (int64_t)x + 1 + after;
-  a = (int32_t)(aa < E.seg_lo[s] ? E.seg_lo[s] : aa);
-  b = (int32_t)(bb > E.seg_hi[s] ? E.seg_hi[s] : bb);
-}
-
-// ---------------------------------------------------------------------------------------------
-// kernels
+// kernels (element functions: post_core.h)
 
 __global__ __launch_bounds__(256) void k_pack(const int64_t* __restrict__ cand, int64_t n, int64_t pre_from, int lbits,
                                               uint64_t* __restrict__ keys) {
@@ -117,10 +62,8 @@ __global__ __launch_bounds__(256) void k_pack(const int64_t* __restrict__ cand, 
 }
 
 // device-count mode: region 1 (to verify) then region 2 (pre-verified), each a fixed capacity
-// with its used length in a device counter; unused slots become LP_PAD_KEY, which sorts after
-// every real key (bit kbits set; the sort covers one extra bit) and is never a hit
-constexpr uint64_t LP_PAD_KEY = ~0ull;
-
+// with its used length in a device counter; unused slots become LP_PAD_KEY (post_core.h), which
+// sorts after every real key (bit kbits set; the sort covers one extra bit)
 __global__ __launch_bounds__(256) void k_pack_dc(const int64_t* __restrict__ cand, int64_t cap1,
                                                  const int64_t* __restrict__ cand2, int64_t cap2,
                                                  const unsigned long long* __restrict__ dcount, int lbits,
@@ -139,21 +82,6 @@ __global__ __launch_bounds__(256) void k_pack_dc(const int64_t* __restrict__ can
   keys[i] = key;
 }
 
-LP_HD bool dedupe_verify_one(const uint64_t* keys, int64_t n, int64_t i, int lbits, const uint8_t* text,
-                             const int64_t* ls, const int32_t* ll, const DfaPool& P, int64_t* std_key) {
-  if (keys[i] == LP_PAD_KEY) {
-    *std_key = 0;
-    return false;
-  }
-  const uint64_t k = keys[i] >> 1;
-  if (i > 0 && (keys[i - 1] >> 1) == k) return false;
-  bool pre = false;  // pre-verified copies sort last inside a run
-  for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j) pre |= (keys[j] & 1) != 0;
-  const int r = (int)(k >> lbits);
-  const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
-  *std_key = ((int64_t)r << 32) | x;
-  return pre || dfa_run(P, r, text + ls[x], ll[x]);
-}
 
 __global__ __launch_bounds__(256) void k_dedupe_verify(const uint64_t* __restrict__ keys, int64_t n, int lbits,
                                                        const uint8_t* __restrict__ text,
@@ -203,19 +131,6 @@ __global__ __launch_bounds__(256) void k_expand(const int64_t* __restrict__ hits
   for (int64_t j = 0; j < c; ++j) evk[base + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
 }
 
-// returns the event's frequency sort key (its frequency key, or nkeys when it has none)
-LP_HD uint32_t ev_post_one(const EvTables& E, uint64_t key, int64_t e, int32_t* ev_line, int32_t* ev_pat,
-                           int32_t* ev_seg, int32_t& a, int32_t& b) {
-  const int32_t x = (int32_t)(key >> E.pbits);
-  const int p = (int)(key & ((1ull << E.pbits) - 1));
-  const int s = seg_of(E.seg_lo, E.nseg, x);
-  ev_line[e] = x;
-  ev_pat[e] = p;
-  ev_seg[e] = s;
-  event_window(E, x, p, s, a, b);
-  const int32_t fk = E.freq_key[p];
-  return fk >= 0 ? (uint32_t)fk : (uint32_t)E.nkeys;
-}
 
 __global__ __launch_bounds__(256) void k_ev_post(const uint64_t* __restrict__ evk, int64_t ne, EvTables E,
                                                  int32_t* __restrict__ ev_line, int32_t* __restrict__ ev_pat,
@@ -231,20 +146,6 @@ __global__ __launch_bounds__(256) void k_ev_post(const uint64_t* __restrict__ ev
   for (int32_t x = a; x < b; ++x) cov[x] = 1;
 }
 
-LP_HD void rank_one(const uint32_t* fs, const int32_t* idx, int64_t ne, int64_t j, int nkeys, int64_t* ev_rank,
-                    int64_t* ev_fkey, int64_t* freq_counts) {
-  const uint32_t fk = fs[j];
-  const int32_t e = idx[j];
-  if ((int)fk >= nkeys) {
-    ev_rank[e] = -1;
-    ev_fkey[e] = -1;
-    return;
-  }
-  const int64_t start = lower_bound_u32(fs, j, fk);
-  ev_rank[e] = j - start;
-  ev_fkey[e] = fk;
-  if (j + 1 == ne || fs[j + 1] != fk) freq_counts[fk] = j - start + 1;
-}
 
 __global__ __launch_bounds__(256) void k_rank(const uint32_t* __restrict__ fs, const int32_t* __restrict__ idx,
                                               int64_t ne, int nkeys, int64_t* __restrict__ ev_rank,
@@ -546,6 +447,25 @@ struct Carve {
   void* take_bytes(size_t n) { return take<uint8_t>(n); }
 };
 
+void dedupe_verify_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
+                       const int32_t* ll, const DfaPool& P, int64_t* stdk, uint8_t* flag, uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_dedupe_verify, dim3(nblk(n)), dim3(256), 0, pstream(stream), keys, n, lbits, text, ls, ll, P,
+                     stdk, flag);
+  LP_PCHECK(hipGetLastError());
+}
+
+void feat_cov_dev(const int32_t* cov, int64_t L, const uint8_t* text, const int64_t* ls, const int32_t* ll,
+                  const DfaPool& P, int ctx_trans, int ctx_acc, uint8_t* feat, uint64_t stream) {
+  if (L <= 0 || !feat) return;
+  // lines per block: enough blocks to spread a small request over the CUs, 4096 for big ones
+  int per = (int)std::min<int64_t>(FC_MAX_LINES, std::max<int64_t>(256, L / 1024));
+  per = (per + 255) / 256 * 256;
+  hipLaunchKernelGGL(k_feat_cov, dim3(nblk(L, per)), dim3(256), 0, pstream(stream), cov, L, per, text, ls, ll, P,
+                     ctx_trans, ctx_acc, feat);
+  LP_PCHECK(hipGetLastError());
+}
+
 size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
   if (hits_small_ok(A)) {          // a request: verify on the grid, the rest in one workgroup
@@ -557,6 +477,7 @@ size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
     LP_PCHECK(hipGetLastError());
     return 0;
   }
+  if (hits_bulk_ok(A)) return hits_bulk_dev(A, ws, ws_bytes, stream);   // bucket sorts (post_bulk.hip)
   const bool dc = A.dcount != nullptr;
   const int kbits = 1 + A.lbits + A.rbits + (dc ? 1 : 0);    // + the pad bit
   Carve C{static_cast<uint8_t*>(ws)};
@@ -630,6 +551,7 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
     }
     return D.used;
   }
+  if (events_bulk_ok(A)) return events_bulk_dev(A, ws, ws_bytes, stream);   // bucket sorts (post_bulk.hip)
   int32_t* cov = A.cov ? A.cov : C.take<int32_t>(L);
   size_t t_sort = 0, t_pairs = 0;
   if (ne > 0) {

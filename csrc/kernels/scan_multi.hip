@@ -51,6 +51,8 @@ namespace lp {
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_THREADS_SMALL = 256;
 constexpr int SCAN_RUN = 4;
+constexpr int SCAN_BM_COPIES = 32;                         // lane-replicated bytemap (bulk variant)
+constexpr int SCAN_BM_REP_BYTES = 512 * SCAN_BM_COPIES * 4; // 64 KiB after the blob
 
 // LDS loads from a 32-bit LDS address. The blob sits at LDS address 0 (the kernel's only LDS is
 // the dynamic blob; checked at entry), so a row offset + a bytemap byte IS the address: one
@@ -202,11 +204,13 @@ __device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32
     if (acc[q]) scan_emit(S, g, acc[q], l + q < x1 ? l + q : x1 - 1, emit);
 }
 
-// the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold
-template <int G, bool CRLF, typename Emit>
+// the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold.
+// REP: the bytemap read goes to this lane's copy of the lane-replicated bytemap at LDS byte bm_rep
+// (entry c at bm_rep + c * 128); otherwise to the blob's bm4 at LDS byte 0
+template <int G, bool CRLF, bool REP, typename Emit>
 __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass& S, const uint8_t* text, int64_t p_lo,
                                               int64_t p_end, int64_t x0, int64_t x1,
-                                              const int64_t* __restrict__ line_start, Emit&& emit) {
+                                              const int64_t* __restrict__ line_start, uint32_t bm_rep, Emit&& emit) {
   uint32_t xr[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
@@ -235,7 +239,7 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
     for (int j = 0; j < 16; ++j) {
       uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
       if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;        // entry 256 + c: hold
-      const uint32_t b = lds_ld32(c * 4);
+      const uint32_t b = lds_ld32(REP ? bm_rep + (c << 7) : c * 4);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         mx[g] = max(mx[g], xr[g]);
@@ -269,6 +273,17 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
                                                         unsigned long long* __restrict__ count, int run_len) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   lds_fill<uint4>(reinterpret_cast<uint4*>(sm), reinterpret_cast<const uint4*>(S.blob), S.lds_words >> 2);  // multiple of 4
+  // bulk variant: a lane-replicated copy of bm4 after the blob (SCAN_BM_COPIES copies: entry c of
+  // copy j at word c * 32 + j, lane l reads copy l & 31). A ds_read_b32 is serviced in two 32-lane
+  // groups with bank = word mod 32, so the byte-map read of every byte is conflict-free whatever
+  // the bytes (profiles/r3_t: 1.5 bank-conflict cycles per LDS instruction over the whole walk)
+  constexpr bool REP = THREADS == SCAN_THREADS;
+  uint32_t bm_rep = 0;
+  if constexpr (REP) {
+    uint32_t* rep = sm + S.lds_words;
+    for (int i = threadIdx.x; i < 512 * SCAN_BM_COPIES; i += THREADS) rep[i] = S.blob[i / SCAN_BM_COPIES];
+    bm_rep = (uint32_t)S.lds_words * 4 + (threadIdx.x & (SCAN_BM_COPIES - 1)) * 4;
+  }
   __syncthreads();
   const GlobalEmit emit{out, cap, count};
   // the fast walk addresses LDS absolutely (blob at address 0); otherwise every run walks exactly
@@ -307,9 +322,9 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
       continue;
     }
     if (crlf)
-      scan_run_fast<G, true>(sm, S, text, p_lo, p_end, x0, x1, line_start, emit);
+      scan_run_fast<G, true, REP>(sm, S, text, p_lo, p_end, x0, x1, line_start, bm_rep, emit);
     else
-      scan_run_fast<G, false>(sm, S, text, p_lo, p_end, x0, x1, line_start, emit);
+      scan_run_fast<G, false, REP>(sm, S, text, p_lo, p_end, x0, x1, line_start, bm_rep, emit);
   }
 }
 
@@ -317,12 +332,12 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
                     const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,
                     uint64_t stream) {
   if (nlines <= 0 || S.ngroups <= 0) return;
-  if (S.ngroups > 4 || (S.lds_words & 3) || S.lds_words * 4 > (160 << 10))
+  if (S.ngroups > 4 || (S.lds_words & 3) || S.lds_words * 4 + SCAN_BM_REP_BYTES > (160 << 10))
     throw std::runtime_error("scan_multi: bad pass descriptor");
-  const size_t lds = (size_t)S.lds_words * 4;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // small texts: one line per lane in 256-thread blocks (the grid is sized for 1024-thread blocks)
   const bool small = nlines <= (int64_t)grid * SCAN_THREADS_SMALL;
+  const size_t lds = (size_t)S.lds_words * 4 + (small ? 0 : SCAN_BM_REP_BYTES);
   const int run_len = small ? 1 : SCAN_RUN;
   const int threads = small ? SCAN_THREADS_SMALL : SCAN_THREADS;
   const int64_t runs = (nlines + run_len - 1) / run_len;

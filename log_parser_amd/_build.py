@@ -32,6 +32,7 @@ SOURCES = [
     ("kernels/line_index.hip", "hip"),
     ("kernels/dp_glue.hip", "hip"),
     ("kernels/lp_post.hip", "hip"),
+    ("kernels/post_bulk.hip", "hip"),
     ("kernels/request_io.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),

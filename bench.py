@@ -250,8 +250,11 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
         if rank == 0 and out.topk_rows is not None:
             state["top"] = out.topk_rows.cpu()                   # merged global top-k on the host
         if use_cuda:
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev1.record()
+            # device span: to the step's last kernel (the step records it before its count read)
+            ev1 = out.end_event
+            if ev1 is None:
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record()
             state.setdefault("dev", []).append((ev0, ev1))
             free[b].record(torch.cuda.current_stream())
             freed[b] = True

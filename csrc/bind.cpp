@@ -511,11 +511,14 @@ PYBIND11_MODULE(_lpnative, m) {
     bpg_dedupe_dev(P<const uint64_t>(keys), n, lbits, P<const uint8_t>(text), P<const int64_t>(ls),
                    P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(flag), s); });
   // ev_rank / ev_fkey / carry: frequency count before each event = carry[fkey] + rank (fused)
+  // dn (optional): device event count, n is then a capacity
   m.def("score_dev", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry, int64_t n,
-                        py::tuple st, py::tuple sp, uint64_t out, uint64_t fac, uint64_t s) {
+                        py::tuple st, py::tuple sp, uint64_t out, uint64_t fac, uint64_t s, uint64_t dn) {
     const FreqIn F{P<const int64_t>(rank), P<const int64_t>(fkey), P<const int64_t>(carry)};
     score_dev(P<const int32_t>(el), P<const int32_t>(ep), P<const int32_t>(es), F, n, st_from(st),
-              sp_from(sp), P<double>(out), P<double>(fac), s); });
+              sp_from(sp), P<double>(out), P<double>(fac), s, P<const int64_t>(dn)); },
+        py::arg("el"), py::arg("ep"), py::arg("es"), py::arg("rank"), py::arg("fkey"), py::arg("carry"), py::arg("n"),
+        py::arg("st"), py::arg("sp"), py::arg("out"), py::arg("fac"), py::arg("s"), py::arg("dn") = 0);
 
   // ---- host twins
   m.def("nl_positions_host", [](uint64_t text, int64_t n, uint64_t pos) { return nl_positions_host(P<const uint8_t>(text), n, P<int64_t>(pos)); });
@@ -548,7 +551,8 @@ PYBIND11_MODULE(_lpnative, m) {
                    P<const int32_t>(in[2].cast<uint64_t>()), P<const int64_t>(in[3].cast<uint64_t>()),
                    P<const int64_t>(in[4].cast<uint64_t>()), P<const int32_t>(in[5].cast<uint64_t>()),
                    P<const double>(in[6].cast<uint64_t>()),
-                   in.size() > 7 ? P<void>(in[7].cast<uint64_t>()) : nullptr};
+                   in.size() > 7 ? P<void>(in[7].cast<uint64_t>()) : nullptr,
+                   in.size() > 8 ? P<const int64_t>(in[8].cast<uint64_t>()) : nullptr};
     if (dev)
       return summarize_dev(I, n, k, nsev, P<double>(top), P<unsigned long long>(pat_hist), P<unsigned long long>(sev_hist),
                            P<void>(ws), ws_bytes, s);
@@ -563,9 +567,14 @@ PYBIND11_MODULE(_lpnative, m) {
       rescore_host(P<const int64_t>(gl), P<const double>(fac), n, Nn, sp_from(sp), P<double>(out));
   });
   // ---- DP step bookkeeping (dp_glue.hip)
+  // cnt (optional, device [5] match / event counters) + caps [4]: the payload's overflow flag
   m.def("dp_pack", [](int64_t own_lines, uint64_t freq, int nk, uint64_t chain, int ns, uint64_t pack, uint64_t s,
-                      bool dev) { dp_pack(own_lines, P<const int64_t>(freq), nk, P<const int32_t>(chain), ns,
-                                          P<int64_t>(pack), s, dev); });
+                      bool dev, uint64_t cnt, std::vector<int64_t> caps) {
+    if (cnt && caps.size() != 4) throw std::invalid_argument("dp_pack: 4 capacities");
+    dp_pack(own_lines, P<const int64_t>(freq), nk, P<const int32_t>(chain), ns, P<int64_t>(pack), s, dev,
+            P<const int64_t>(cnt), cnt ? caps.data() : nullptr); },
+        py::arg("own_lines"), py::arg("freq"), py::arg("nk"), py::arg("chain"), py::arg("ns"), py::arg("pack"),
+        py::arg("s"), py::arg("dev"), py::arg("cnt") = 0, py::arg("caps") = std::vector<int64_t>());
   // a = (g, world, rank, nk, ns, halo_left, tot, slot_e0, slot_k, own_start, g0, n, carry, seq_carry, red_tail)
   m.def("dp_carry", [](py::tuple a, uint64_t s, bool dev) {
     auto u = [&](int i) { return a[i].cast<uint64_t>(); };
@@ -573,11 +582,15 @@ PYBIND11_MODULE(_lpnative, m) {
                   a[5].cast<int64_t>(), P<const int64_t>(u(6)), P<const int64_t>(u(7)), P<const int64_t>(u(8)),
                   P<int64_t>(u(9)), P<int64_t>(u(10)), P<int64_t>(u(11)), P<int64_t>(u(12)), P<uint8_t>(u(13)),
                   P<int64_t>(u(14))};
+    if (a.size() > 15) A.veto = P<int64_t>(u(15));
     dp_carry(A, s, dev);
   });
-  m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev) {
-    freq_record(P<const int64_t>(counts), K, now, ring_from(ring), s, dev);
-  });
+  // veto (optional, device int64): no record when *veto != 0 (a DP step that re-runs)
+  m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev, uint64_t veto) {
+    RecordGate G;
+    G.veto = P<const int64_t>(veto);
+    freq_record(P<const int64_t>(counts), K, now, ring_from(ring), s, dev, G);
+  }, py::arg("counts"), py::arg("K"), py::arg("now"), py::arg("ring"), py::arg("s"), py::arg("dev"), py::arg("veto") = 0);
   m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry,
                          int64_t n, py::tuple st, py::tuple sp, uint64_t out, uint64_t fac) {
     const FreqIn F{P<const int64_t>(rank), P<const int64_t>(fkey), P<const int64_t>(carry)};
@@ -802,8 +815,11 @@ PYBIND11_MODULE(_lpnative, m) {
                           py::tuple ev, uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, uint64_t ev_line,
                           uint64_t ev_pat, uint64_t ev_seg, uint64_t ev_rank, uint64_t ev_fkey, uint64_t freq_counts,
                           uint64_t feat, uint64_t cov, int ctx_trans, int ctx_acc, uint64_t ws, size_t ws_bytes,
-                          uint64_t s, bool dev) -> size_t {
+                          uint64_t s, bool dev, uint64_t dcounts, uint64_t ne_fit) -> size_t {
     EventsArgs A;
+    A.dcounts = P<const int64_t>(dcounts);
+    A.ne_fit = P<int64_t>(ne_fit);
+    if (A.dcounts && !dev) throw std::runtime_error("post_events: device counters need the device path");
     A.ctx_trans = ctx_trans; A.ctx_acc = ctx_acc;
     A.hits = P<const int64_t>(hits); A.nh = nh; A.ev_cnt = P<const int64_t>(ev_cnt);
     A.ev_end = P<const int64_t>(ev_end); A.ne = ne; A.L = L; A.lbits = lbits; A.ev = ev_from(ev);

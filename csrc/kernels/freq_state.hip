@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void k_freq_record(const int64_t* __restrict__
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
   if (G.cnt && (G.cnt[0] > G.cap[0] || G.cnt[1] > G.cap[1] || G.cnt[2] > G.cap[2] || G.cnt[4] > G.cap[3])) return;
+  if (G.veto && *G.veto) return;
   const int64_t c = counts[k];
   if (c <= 0) return;
   const int64_t p = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(R.ht + 1), 1ull);
@@ -82,6 +83,7 @@ void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, ui
     if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in freq_record");
     return;
   }
+  if (gate.veto && *gate.veto) return;
   for (int k = 0; k < K; ++k) {
     const int64_t c = counts[k];
     if (c <= 0) continue;

@@ -110,6 +110,7 @@ void freq_evict(const FreqRing& R, double horizon, uint64_t stream, bool dev);
 struct RecordGate {
   const int64_t* cnt = nullptr;
   int64_t cap[4] = {0, 0, 0, 0};
+  const int64_t* veto = nullptr;   // (device) record only when *veto == 0: a DP step's overflow veto
 };
 void freq_record(const int64_t* counts, int K, double now, const FreqRing& R, uint64_t stream, bool dev,
                  const RecordGate& gate = RecordGate());
@@ -144,9 +145,12 @@ struct DpCarryArgs {
   int64_t* carry;            // [nk]
   uint8_t* seq_carry;        // [ns]
   int64_t* red_tail;         // [nk] this rank's counts into the all-reduce buffer (may be null)
+  int64_t* veto = nullptr;   // [1] OR of every rank's overflow flag (may be null)
 };
+// payload [1 + nk + ns + 1]; cnt (device [5] match / event counters, may be null) and caps (host
+// [4]: gram, candidate, verified, event capacities) set the trailing overflow flag
 void dp_pack(int64_t own_lines, const int64_t* freq, int nk, const int32_t* chain, int ns, int64_t* pack,
-             uint64_t stream, bool dev);
+             uint64_t stream, bool dev, const int64_t* cnt = nullptr, const int64_t* caps = nullptr);
 void dp_carry(const DpCarryArgs& A, uint64_t stream, bool dev);
 }  // namespace lp
 
@@ -164,6 +168,9 @@ struct SummIn {
   const double* rows;
   // optional (events): every event packed as [global line int64 x n][score f64 x n][pattern i32 x n]
   void* ev_out = nullptr;
+  // optional (events): device event count; n is then a capacity and the level-0 pass reads
+  // min(n, *dn) events (ev_out packed at stride min(n, *dn))
+  const int64_t* dn = nullptr;
 };
 // writes the k best rows (score desc, line asc, pattern asc; missing rows = (-inf, -1, -1)) and,
 // from events, adds the pattern / severity histograms. Device: returns workspace bytes, runs only
@@ -219,6 +226,9 @@ struct EventsArgs {
   // device-count mode (request path): [nh, ne] on the device; nh / ne above are then capacities
   // and a batch over them leaves the outputs unset (the caller re-runs with host counts)
   const int64_t* dcounts = nullptr;
+  // device-count mode, bulk path (optional): receives the event count when the events fit ne, else
+  // 0 -- the count every later kernel of the batch reads (event fields past it are unset)
+  int64_t* ne_fit = nullptr;
   // outputs
   int32_t* ev_line; int32_t* ev_pat; int32_t* ev_seg; int64_t* ev_rank; int64_t* ev_fkey;
   int64_t* freq_counts;      // [nkeys]

@@ -357,7 +357,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
   if (A.dcounts) {                 // device-count mode: A.ne / A.nh are capacities
     nh = A.dcounts[0];
     ne = A.dcounts[1];
-    if (ne > A.ne || nh > A.nh) return;   // over capacity: the host re-runs with read counts
+    const bool over = ne > A.ne || nh > A.nh;
+    if (A.ne_fit && threadIdx.x == 0) A.ne_fit[0] = over ? 0 : ne;
+    if (over) return;                     // over capacity: the host re-runs with read counts
   }
   const int np = sb_pow2(ne);
   for (int i = threadIdx.x; i <= L; i += SB_THREADS) diff[i] = 0;

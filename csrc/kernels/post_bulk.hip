@@ -247,9 +247,11 @@ __global__ __launch_bounds__(PB_AT) void k_pb_scan(TI* in, int64_t nb, int64_t* 
 // plan: shift[p], first sub-bucket base[p] (base[np] = total), owner sub_prim[b]; optionally the
 // primary counts copied out as int64
 __global__ __launch_bounds__(PB_AT) void k_pb_plan(const uint32_t* __restrict__ cnt, int np, int cbits, int64_t range,
-                                                  uint8_t* __restrict__ shift, uint32_t* __restrict__ base,
-                                                  int32_t* __restrict__ sub_prim, int64_t* __restrict__ copy_out) {
+                                                  const int64_t* __restrict__ drange, uint8_t* __restrict__ shift,
+                                                  uint32_t* __restrict__ base, int32_t* __restrict__ sub_prim,
+                                                  int64_t* __restrict__ copy_out) {
   __shared__ int64_t scratch[PB_AT / 64];
+  if (drange) range = *drange < range ? *drange : range;     // device count, capped at the capacity
   const int64_t per = (np + blockDim.x - 1) / blockDim.x;
   const int64_t a = threadIdx.x * per, e = a + per < np ? a + per : np;
   auto plan = [&](uint32_t c, int& s) -> int64_t {
@@ -504,22 +506,45 @@ __global__ __launch_bounds__(PB_T) void k_hb_emit(const int64_t* __restrict__ su
 struct EbIn {
   const int64_t* hits;
   const int64_t* ev_cnt;
-  int64_t nh;
+  int64_t nh;                 // hits (device-count mode: capacity)
   int shift;
+  const int64_t* dcnt;        // device-count mode: [hits, events]; else null
+  int64_t ne_cap;             // device-count mode: event capacity
 };
 
-__global__ __launch_bounds__(PB_AT) void k_eb_count(EbIn S, int nb, uint32_t* cnt) {
+// device-count mode: false when the events overflowed their capacity (every kernel then leaves its
+// outputs unset; the caller re-runs); n = the hits to read
+__device__ __forceinline__ bool eb_live(const EbIn& S, int64_t& n) {
+  n = S.nh;
+  if (!S.dcnt) return true;
+  if (S.dcnt[1] > S.ne_cap) return false;
+  n = S.dcnt[0] < n ? S.dcnt[0] : n;
+  return true;
+}
+
+// device-count mode: the events to read (0 after an overflow)
+__device__ __forceinline__ int64_t eb_events(const int64_t* dcnt, int64_t ne) {
+  if (!dcnt) return ne;
+  return dcnt[1] > ne ? 0 : dcnt[1];
+}
+
+__global__ __launch_bounds__(PB_AT) void k_eb_count(EbIn S, int nb, uint32_t* cnt, int64_t* ne_fit) {
   extern __shared__ uint32_t pb_lds[];
+  if (ne_fit && blockIdx.x == 0 && threadIdx.x == 0) ne_fit[0] = eb_events(S.dcnt, S.ne_cap);
+  int64_t nh;
+  if (!eb_live(S, nh)) return;
   pb_count([&](int64_t i, uint32_t& b, uint32_t& w) {
     w = (uint32_t)S.ev_cnt[i];
     b = (uint32_t)(S.hits[i] & 0xFFFFFFFFll) >> S.shift;
     return true;
-  }, S.nh, nb, cnt, pb_lds);
+  }, nh, nb, cnt, pb_lds);
 }
 
 __global__ __launch_bounds__(PB_AT) void k_eb_scatter(EbIn S, int nb, EvTables E, const int64_t* __restrict__ bin_off,
                                                      uint32_t* fill, uint64_t* __restrict__ ekeys) {
   extern __shared__ uint32_t pb_lds[];
+  int64_t nh;
+  if (!eb_live(S, nh)) return;
   pb_scatter([&](int64_t i, uint32_t& b, uint32_t& w, uint64_t& pay) {
     w = (uint32_t)S.ev_cnt[i];
     b = (uint32_t)(S.hits[i] & 0xFFFFFFFFll) >> S.shift;
@@ -531,7 +556,7 @@ __global__ __launch_bounds__(PB_AT) void k_eb_scatter(EbIn S, int nb, EvTables E
     const uint64_t x = (uint64_t)(k & 0xFFFFFFFFll);
     const int64_t c = S.ev_cnt[i], p0 = E.prim_off[r], q = bin_off[b] + o;
     for (int64_t j = 0; j < c; ++j) ekeys[q + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
-  }, S.nh, nb, fill, pb_lds, pb_lds + nb);
+  }, nh, nb, fill, pb_lds, pb_lds + nb);
 }
 
 // one workgroup per line block: events in (line, pattern) order + their outputs, window coverage
@@ -540,8 +565,9 @@ __global__ __launch_bounds__(PB_T) void k_eb_sort(const int64_t* __restrict__ bi
                                                   EvTables E, int32_t* __restrict__ ev_line, int32_t* __restrict__ ev_pat,
                                                   int32_t* __restrict__ ev_seg, uint32_t* __restrict__ fsort,
                                                   int64_t* __restrict__ ev_rank, int64_t* __restrict__ ev_fkey,
-                                                  int32_t* __restrict__ cov) {
+                                                  int32_t* __restrict__ cov, const int64_t* dcnt, int64_t ne_cap) {
   __shared__ uint64_t lds[PB_EV_CAP];
+  if (dcnt && dcnt[1] > ne_cap) return;
   const int b = blockIdx.x;
   const int64_t o = bin_off[b], m = bin_off[b + 1] - o;
   if (m == 0) return;
@@ -571,8 +597,10 @@ struct KbPlan {
   const uint32_t* base;     // [nk + 1]
 };
 
-__global__ __launch_bounds__(PB_AT) void k_kb_count(const uint32_t* __restrict__ fsort, int64_t ne, int nk, uint32_t* cnt) {
+__global__ __launch_bounds__(PB_AT) void k_kb_count(const uint32_t* __restrict__ fsort, int64_t ne, int nk, uint32_t* cnt,
+                                                   const int64_t* dcnt) {
   extern __shared__ uint32_t pb_lds[];
+  ne = eb_events(dcnt, ne);
   pb_count([&](int64_t e, uint32_t& b, uint32_t& w) {
     b = fsort[e];
     w = 1;
@@ -581,8 +609,9 @@ __global__ __launch_bounds__(PB_AT) void k_kb_count(const uint32_t* __restrict__
 }
 
 __global__ __launch_bounds__(PB_AT) void k_kb_count2(const uint32_t* __restrict__ fsort, int64_t ne, int nk, KbPlan Q,
-                                                    int bcap, uint32_t* sub_cnt) {
+                                                    int bcap, uint32_t* sub_cnt, const int64_t* dcnt) {
   extern __shared__ uint32_t pb_lds[];
+  ne = eb_events(dcnt, ne);
   pb_count([&](int64_t e, uint32_t& b, uint32_t& w) {
     const uint32_t k = fsort[e];
     w = 1;
@@ -594,8 +623,9 @@ __global__ __launch_bounds__(PB_AT) void k_kb_count2(const uint32_t* __restrict_
 
 __global__ __launch_bounds__(PB_AT) void k_kb_scatter(const uint32_t* __restrict__ fsort, int64_t ne, int nk, KbPlan Q,
                                                      int bcap, const int64_t* __restrict__ sub_off, uint32_t* fill,
-                                                     uint32_t* __restrict__ kidx) {
+                                                     uint32_t* __restrict__ kidx, const int64_t* dcnt) {
   extern __shared__ uint32_t pb_lds[];
+  ne = eb_events(dcnt, ne);
   pb_scatter([&](int64_t e, uint32_t& b, uint32_t& w, uint64_t& pay) {
     const uint32_t k = fsort[e];
     w = 1;
@@ -699,7 +729,8 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
   const HbPlan Q{shift, base};
   hipLaunchKernelGGL(k_hb_count, dim3(g), dim3(PB_AT), agg_lds(R, false), st, A, cnt);
   PB_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(PB_AT), 0, st, cnt, R, A.lbits, L, shift, base, sub_reg, nullptr);
+  hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(PB_AT), 0, st, cnt, R, A.lbits, L, nullptr, shift, base, sub_reg,
+                     nullptr);
   PB_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_hb_count2, dim3(g), dim3(PB_AT), agg_lds(bcap, false), st, A, Q, bcap, sub_cnt);
   PB_CHECK(hipGetLastError());
@@ -711,6 +742,9 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
                      base, R, bcap, vals, tmp, A.lbits, n, kout);
   PB_CHECK(hipGetLastError());
   dedupe_verify_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, stdk, flag, stream);
+  // BPG programs: one lane per first-of-run key over the sorted keys (a regex's keys are contiguous,
+  // so its waves are dense). A workgroup per sub-bucket (lanes looping over its candidates) measured
+  // 138 us against this kernel's 118 us: the walks are latency-bound, lanes should not loop.
   bpg_dedupe_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, flag, stream);
   hipLaunchKernelGGL(k_hb_kept, dim3((unsigned)bcap), dim3(PB_T), 0, st, sub_off, sub_reg, base, R, flag, stdk, A.ev,
                      kept, evs);
@@ -724,7 +758,7 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
   return C.used;
 }
 
-bool events_bulk_ok(const EventsArgs& A) { return !bulk_disabled() && A.dcounts == nullptr && A.lbits <= 31; }
+bool events_bulk_ok(const EventsArgs& A) { return !bulk_disabled() && A.lbits <= 31; }
 
 size_t events_bulk_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t ne = A.ne, L = A.L, nh = A.nh;
@@ -757,39 +791,43 @@ size_t events_bulk_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t 
   uint8_t* zero_from = A.cov ? reinterpret_cast<uint8_t*>(bin_cnt) : reinterpret_cast<uint8_t*>(cov);
   PB_CHECK(hipMemsetAsync(zero_from, 0, static_cast<uint8_t*>(ws) + zero_end - zero_from, st));
   if (A.cov && L > 0) PB_CHECK(hipMemsetAsync(A.cov, 0, (size_t)L * sizeof(int32_t), st));
+  // device-count mode (A.dcounts = [hits, events] on the device): nh / ne are capacities
+  const int64_t* dc = A.dcounts;
   if (ne > 0) {
-    const EbIn S{A.hits, A.ev_cnt, nh, shift};
+    const EbIn S{A.hits, A.ev_cnt, nh, shift, dc, ne};
     const unsigned g = pb_agg_grid(nh);
-    hipLaunchKernelGGL(k_eb_count, dim3(g), dim3(PB_AT), agg_lds(nb, false), st, S, nb, bin_cnt);
+    hipLaunchKernelGGL(k_eb_count, dim3(g), dim3(PB_AT), agg_lds(nb, false), st, S, nb, bin_cnt, A.ne_fit);
     PB_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_pb_scan<uint32_t>, dim3(1), dim3(PB_AT), 0, st, bin_cnt, (int64_t)nb, bin_off, nullptr, 1);
     PB_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_eb_scatter, dim3(g), dim3(PB_AT), agg_lds(nb, true), st, S, nb, E, bin_off, bin_cnt, ekeys);
     PB_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_eb_sort, dim3((unsigned)nb), dim3(PB_T), 0, st, bin_off, ekeys, etmp, E, A.ev_line, A.ev_pat,
-                       A.ev_seg, fsort, A.ev_rank, A.ev_fkey, cov);
+                       A.ev_seg, fsort, A.ev_rank, A.ev_fkey, cov, dc, ne);
     PB_CHECK(hipGetLastError());
     if (nk > 0) {
       const unsigned gk = pb_agg_grid(ne);
       const KbPlan Q{kshift, kbase};
-      hipLaunchKernelGGL(k_kb_count, dim3(gk), dim3(PB_AT), agg_lds(nk, false), st, fsort, ne, nk, key_cnt);
+      hipLaunchKernelGGL(k_kb_count, dim3(gk), dim3(PB_AT), agg_lds(nk, false), st, fsort, ne, nk, key_cnt, dc);
       PB_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(PB_AT), 0, st, key_cnt, nk, ebits, ne, kshift, kbase, sub_key,
-                         A.freq_counts);
+      hipLaunchKernelGGL(k_pb_plan, dim3(1), dim3(PB_AT), 0, st, key_cnt, nk, ebits, ne, dc ? dc + 1 : nullptr, kshift,
+                         kbase, sub_key, A.freq_counts);
       PB_CHECK(hipGetLastError());
-      hipLaunchKernelGGL(k_kb_count2, dim3(gk), dim3(PB_AT), agg_lds(kcap, false), st, fsort, ne, nk, Q, kcap, ksub_cnt);
+      hipLaunchKernelGGL(k_kb_count2, dim3(gk), dim3(PB_AT), agg_lds(kcap, false), st, fsort, ne, nk, Q, kcap, ksub_cnt,
+                         dc);
       PB_CHECK(hipGetLastError());
       hipLaunchKernelGGL(k_pb_scan<uint32_t>, dim3(1), dim3(PB_AT), 0, st, ksub_cnt, (int64_t)kcap, ksub_off, nullptr, 1);
       PB_CHECK(hipGetLastError());
       hipLaunchKernelGGL(k_kb_scatter, dim3(gk), dim3(PB_AT), agg_lds(kcap, true), st, fsort, ne, nk, Q, kcap, ksub_off,
-                         ksub_cnt, kidx);
+                         ksub_cnt, kidx, dc);
       PB_CHECK(hipGetLastError());
       hipLaunchKernelGGL(k_kb_rank, dim3((unsigned)kcap), dim3(PB_T), 0, st, ksub_off, sub_key, kbase, nk, kidx, ktmp,
                          A.ev_rank, A.ev_fkey);
       PB_CHECK(hipGetLastError());
     }
-  } else if (nk > 0) {
-    PB_CHECK(hipMemsetAsync(A.freq_counts, 0, (size_t)nk * sizeof(int64_t), st));
+  } else {
+    if (nk > 0) PB_CHECK(hipMemsetAsync(A.freq_counts, 0, (size_t)nk * sizeof(int64_t), st));
+    if (A.ne_fit) PB_CHECK(hipMemsetAsync(A.ne_fit, 0, sizeof(int64_t), st));
   }
   if (A.feat) feat_cov_dev(cov, L, A.text, A.ls, A.ll, A.dfa, A.ctx_trans, A.ctx_acc, A.feat, stream);
   return C.used;

@@ -88,6 +88,7 @@ __global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t 
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * SUMM_CHUNK;
   const int64_t add = in.line_add ? *in.line_add : 0;
+  if (in.dn && !in.rows) n = min(n, *in.dn);      // capacity n, device count *dn
   for (int j = threadIdx.x; j < SUMM_CHUNK; j += SUMM_THREADS) {
     const int64_t i = base + j;
     Row r = empty_row();
@@ -191,6 +192,8 @@ size_t summarize_dev(const SummIn& in, int64_t n, int k, int nsev, double* top_r
 void summarize_host(const SummIn& in, int64_t n, int k, double* top_rows, int64_t* pat_hist, int64_t* sev_hist) {
   const int64_t add = in.line_add ? *in.line_add : 0;
   std::vector<Row> rows(n);
+  if (in.dn && !in.rows) n = std::min<int64_t>(n, *in.dn);
+  rows.resize(n);
   for (int64_t i = 0; i < n; ++i) {
     if (in.rows) {
       rows[i] = Row{in.rows[3 * i], (int64_t)in.rows[3 * i + 1], (int32_t)in.rows[3 * i + 2]};

@@ -120,6 +120,16 @@ class Prepared:
     n_lines: int
     timings: Dict[str, float] = field(default_factory=dict)
     out_buf: Optional[torch.Tensor] = None   # K.results_buffer holding line / pattern / segment / counts
+    # deferred counts (``prepare(defer=True)``): the arrays above are capacities; cnt = device
+    # [gram hits, candidates, verified hits, unique hits, events, events that fit (0 on overflow)],
+    # caps = their host capacities
+    cnt: Optional[torch.Tensor] = None
+    caps: Optional[Dict[str, int]] = None
+
+    @property
+    def ne_dev(self) -> Optional[torch.Tensor]:
+        """The device event count later kernels read: 0 when the events overflowed their buffer."""
+        return None if self.cnt is None else self.cnt[5:6]
 
 
 @dataclass
@@ -332,7 +342,9 @@ class Engine:
             self.n_cus = int(props.multi_processor_count)
             self.pf_grid = self.n_cus * 4
             if bool(self.config.get("engine.scan-stream", True)):
-                self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
+                # LP_SIDE_PRIORITY (A/B knob): stream priority of the scan stream
+                prio = int(__import__("os").environ.get("LP_SIDE_PRIORITY", "0"))
+                self._side = (torch.cuda.Stream(self.device, priority=prio), torch.cuda.Event(), torch.cuda.Event())
         else:
             self.n_cus = 1
             self.pf_grid = 1
@@ -527,18 +539,40 @@ class Engine:
             return None
         return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid)
 
+    def can_defer(self, text) -> bool:
+        """``prepare(defer=True)`` applies: device text, every matcher on the arena path, and the
+        bucket-sorted post path (csrc/kernels/post_bulk.hip: device-count events)."""
+        import os
+        return (text.is_cuda and not self.lib.host_regs and not self.profile and self.context_engine != "mfma"
+                and os.environ.get("LP_POST_SORT", "") != "rocprim")
+
     def prepare(self, text, nbytes, ls, ll, segs: Segments, host_text=None,
-                timings: Optional[dict] = None, early=None) -> "Prepared":
+                timings: Optional[dict] = None, early=None, defer: bool = False) -> "Prepared":
         """Local phase: matching, hit CSR, events, in-batch frequency ranks, context features.
 
         Needs no global information, so the data-parallel path runs it before its collectives.
         After matching it is the native post-match pipeline (csrc/kernels/lp_post.hip): one host
         read of (hit, event) counts in the middle, everything else stream-ordered on the device.
+        ``defer`` (``can_defer``): no read at all -- hits and events run in device-count mode on
+        capacity-sized buffers (``Prepared.cnt`` / ``caps``); the caller reads the counts once its
+        whole step is queued and re-runs the step if a buffer overflowed.
         """
         timings = {} if timings is None else timings
         L = ls.numel()
         t = 0.0
         evt = self._ev_tables(segs)
+        if defer:
+            hits, hit_line, hit_off, ev_cnt, ev_end, nh_cap, cnt, caps = K.match_and_hits(
+                text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
+                self.scan_grid, side=self._side, early=early, defer=True)
+            nkeys = len(self.lib.freq_ids)
+            ne_cap = caps["ev"]
+            out_buf = K.results_buffer(ne_cap, nkeys, text.device)
+            ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts, feat, _ = K.post_events(
+                hits, nh_cap, ev_cnt, ev_end, ne_cap, L, evt, text, ls, ll, self.tabs["dfa"], nkeys, self.ws,
+                ctx_ext=self.lib.ctx_dfa_extent, out=out_buf, dcounts=cnt[3:5], ne_fit=cnt[5:6])
+            return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
+                            hit_line, feat, L, timings, out_buf=out_buf, cnt=cnt, caps=caps)
         if text.is_cuda and not self.lib.host_regs:
             # every matcher appends to fixed-capacity device buffers; ONE host read after the CSR
             self._start(timings)
@@ -600,7 +634,7 @@ class Engine:
         if prep.out_buf is not None:
             score_out = K.results_views(prep.out_buf, prep.ev_line.numel(), len(self.lib.freq_ids))[0]
         score, factors = K.score_fused(prep.ev_line, prep.ev_pat, prep.ev_seg, prep.ev_rank, prep.ev_fkey,
-                                       freq_carry, st, self.sp_tuple, with_factors, out=score_out)
+                                       freq_carry, st, self.sp_tuple, with_factors, out=score_out, dn=prep.ne_dev)
         self._tick(timings, "score", t)
         return RunResult(prep.ev_line, prep.ev_pat, prep.ev_seg, score, factors,
                          prep.freq_counts[:len(self.lib.freq_ids)], prep.hits, prep.hit_off, prep.n_lines, timings,
@@ -626,11 +660,15 @@ class Engine:
             c = np.zeros(1, np.int64)
         return torch.from_numpy(c).to(self.device)
 
-    def commit_frequency(self, counts) -> None:
-        """Record this batch's per-id match counts (tensor or host array) in the sliding window."""
+    def commit_frequency(self, counts, veto: Optional[torch.Tensor] = None) -> None:
+        """Record this batch's per-id match counts (tensor or host array) in the sliding window.
+        ``veto`` (device int64[1], device window only): skip the record when non-zero."""
         if self.freq_on_device:
             if len(counts) and self.lib.freq_ids:
-                self.freq.record_tensor(counts if torch.is_tensor(counts) else torch.from_numpy(np.asarray(counts)))
+                self.freq.record_tensor(counts if torch.is_tensor(counts) else torch.from_numpy(np.asarray(counts)),
+                                        veto=veto)
+            return
+        if veto is not None and int(veto.item()):
             return
         if len(counts):
             self.freq.record_counts(self.lib.freq_ids, counts.cpu().numpy() if torch.is_tensor(counts) else counts)

@@ -269,8 +269,10 @@ class DeviceFrequencyState:
             N.freq_evict(self._ring(), self._now(now) - self.window_s, self._stream(), self.device.type == "cuda")
             return self.tot
 
-    def record_tensor(self, counts, now: Optional[float] = None) -> None:
-        """Append this batch's per-key counts (int64 tensor on the state's device, >= K entries)."""
+    def record_tensor(self, counts, now: Optional[float] = None, veto=None) -> None:
+        """Append this batch's per-key counts (int64 tensor on the state's device, >= K entries).
+        ``veto`` (device int64[1], optional): nothing is recorded when it is non-zero (a DP step
+        whose buffers overflowed and that re-runs)."""
         from .native import N
         K = len(self.ids)
         if K == 0:
@@ -278,7 +280,8 @@ class DeviceFrequencyState:
         c = counts.to(device=self.device, dtype=__import__("torch").int64)
         with self._lock:
             self._ensure_room(K)
-            N.freq_record(c.data_ptr(), K, self._now(now), self._ring(), self._stream(), self.device.type == "cuda")
+            N.freq_record(c.data_ptr(), K, self._now(now), self._ring(), self._stream(), self.device.type == "cuda",
+                          veto.data_ptr() if veto is not None else 0)
             self._tail_bound += K
 
     # host-array compatibility with FrequencyState (CPU callers, tests)

@@ -393,13 +393,24 @@ class MatchArena:
 
     def __init__(self):
         # starting rates per line (an underestimate costs one re-run of the matchers; an
-        # overestimate costs sort work on every batch: the hit sort covers the capacity, and past
-        # ~1M keys rocPRIM switches from merge sort to onesweep with a fill per digit pass)
-        self.rate = {"gram": 0.08, "cand": 0.03, "ver": 0.01}
+        # overestimate costs post-match work on every batch, which covers the capacity); "ev":
+        # events, only for steps that defer the count read (``match_and_hits(defer=True)``)
+        self.rate = {"gram": 0.08, "cand": 0.03, "ver": 0.01, "ev": 0.01}
         self.last: dict = {}            # counts of the latest batch (diagnostics)
 
     def caps(self, L: int) -> dict:
         return {k: int(L * r * 1.25) + 512 for k, r in self.rate.items()}
+
+    @staticmethod
+    def overflow(counts: list, caps: dict) -> bool:
+        """counts = [gram, cand, ver, nh, ne] of a deferred step vs its capacities."""
+        g, k, v, _, ne = counts
+        return g > caps["gram"] or k > caps["cand"] or v > caps["ver"] or ne > caps["ev"]
+
+    def learn_deferred(self, L: int, counts: list) -> None:
+        g, k, v, nh, ne = counts
+        self.last = {"lines": L, "gram_hits": g, "prefilter_candidates": k, "scan_hits": v, "hits": nh, "events": ne}
+        self.learn(L, {"gram": g, "cand": k, "ver": v, "ev": ne}, overflow=False)
 
     def learn(self, L: int, counts: dict, overflow: bool) -> None:
         """Overflow: the exact rates. Otherwise decay toward what batches need (the hit sort
@@ -417,16 +428,20 @@ class EarlyPrefilter:
         L_est = int(nbytes * _LINES_PER_BYTE[0]) + 1
         self.cap = arena.caps(L_est)["gram"]
         self.gh = torch.empty(self.cap, dtype=torch.int64, device=text.device)
-        self.cnt = torch.zeros(5, dtype=torch.int64, device=text.device)
+        self.cnt = torch.zeros(6, dtype=torch.int64, device=text.device)
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
                         pf_grid, _s(text))
 
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
                    ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None, side=None,
-                   early: Optional[EarlyPrefilter] = None):
+                   early: Optional[EarlyPrefilter] = None, defer: bool = False):
     """GPU: every matcher appends to the arena, then the post-match hit pipeline reads the device
     counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read.
+
+    ``defer``: no read -> (hits, hit_line, hit_off, ev_cnt, ev_end, hit capacity, device counters
+    [gram, cand, ver, nh, ne], capacities incl. "ev"); the caller checks the counters against the
+    capacities later (``MatchArena.overflow``) and re-runs with ``arena.learn``.
 
     ``side`` = (stream, fork event, join event): the self-verifying engines (literal-free DFA scan,
     single-DFA scan, MFMA NFA) run on that stream, concurrently with the literal prefilter chain
@@ -446,8 +461,9 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             gh, cnt = early.gh, early.cnt
         else:
             gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
-            # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters)
-            cnt = torch.zeros(5, dtype=torch.int64, device=dev)
+            # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters),
+            # then the events that fit their buffer (deferred steps: post_events' ne_fit)
+            cnt = torch.zeros(6, dtype=torch.int64, device=dev)
         cand = torch.empty(cap["cand"], dtype=torch.int64, device=dev)
         ver = torch.empty(cap["ver"], dtype=torch.int64, device=dev)
         c0 = cnt.data_ptr()
@@ -497,7 +513,9 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
                                c0 + 24, wp, wn, st, True, ver.data_ptr(), c0 + 8)
 
         _run_ws(call, ws)
-        g, k, v, nh, ne = cnt.tolist()                 # the one host read
+        if defer:
+            return hits, hit_line, hit_off, ev_cnt, ev_end, n, cnt, cap
+        g, k, v, nh, ne = cnt[:5].tolist()             # the one host read
         arena.last = {"lines": L, "gram_hits": g, "prefilter_candidates": k, "scan_hits": v, "hits": nh, "events": ne}
         ok = g <= cap["gram"] and k <= cap["cand"] and v <= cap["ver"]
         arena.learn(L, {"gram": g, "cand": k, "ver": v}, overflow=not ok)
@@ -522,11 +540,16 @@ def results_views(buf: torch.Tensor, ne: int, nkeys: int):
 
 def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text, line_start, line_len, dfa_tuple,
                 nkeys: int, ws: Optional[Workspace], features: bool = True, ctx_ext: Tuple[int, int] = (1 << 30, 1 << 30),
-                out: Optional[torch.Tensor] = None):
+                out: Optional[torch.Tensor] = None, dcounts: Optional[torch.Tensor] = None,
+                ne_fit: Optional[torch.Tensor] = None):
     """Events in reference order + segment, frequency rank/key, per-key counts and context features
     (or, with ``features=False``, the int32 window coverage per line for another feature engine).
     ``ctx_ext`` = table extents of the 4 context DFAs (trans, acc entries) for LDS staging.
-    ``out``: a ``results_buffer`` receiving line / pattern / segment / frequency counts."""
+    ``out``: a ``results_buffer`` receiving line / pattern / segment / frequency counts.
+    ``dcounts``: device [hits, events] counts (device only); nh / ne are then capacities and the
+    outputs are left unset when the events exceed ne (the caller re-runs). ``ne_fit`` (int64[1],
+    with ``dcounts``): receives the event count, or 0 when the events did not fit -- the count the
+    batch's later kernels must read (score, summary), so they never touch unset event fields."""
     dev = text.device
     if out is not None:
         _, freq_counts, ev_line, ev_pat, ev_seg = results_views(out, ne, nkeys)
@@ -550,7 +573,8 @@ def post_events(hits, nh: int, ev_cnt, ev_end, ne: int, L: int, evt: tuple, text
                              evt, text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), dfa_tuple,
                              ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_rank.data_ptr(),
                              ev_fkey.data_ptr(), freq_counts.data_ptr(), feat.data_ptr() if features else 0,
-                             _p(cov), ctx_ext[0], ctx_ext[1], wp, wn, _s(text), text.is_cuda)
+                             _p(cov), ctx_ext[0], ctx_ext[1], wp, wn, _s(text), text.is_cuda, _p(dcounts),
+                             _p(ne_fit))
 
     if text.is_cuda:
         _run_ws(call, ws)
@@ -572,7 +596,7 @@ def _check_k(k: int) -> None:
 def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int, sev_index: torch.Tensor,
               npat: int, nsev: int, line_add: Optional[torch.Tensor] = None, ws: Optional[Workspace] = None,
               pack_events: bool = False, hist_out: Optional[torch.Tensor] = None,
-              rows_out: Optional[torch.Tensor] = None):
+              rows_out: Optional[torch.Tensor] = None, dn: Optional[torch.Tensor] = None):
     """Top-k rows + histograms of scored events (csrc/kernels/summarize.hip).
 
     ``line`` is int32 (local, plus the device scalar ``line_add``) or int64 (global);
@@ -580,7 +604,8 @@ def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int
     (rows float64[k, 3] = (score, global line, pattern) ordered score desc, line asc, pattern asc,
     missing rows = (-inf, -1, -1); pat_hist int64[npat]; sev_hist int64[nsev]; packed) where
     ``packed`` (with ``pack_events``) is every event as uint8[20 n] = [global line int64 x n |
-    score f64 x n | pattern int32 x n], written by the same kernel. No host sync."""
+    score f64 x n | pattern int32 x n], written by the same kernel. No host sync. ``dn``: device
+    event count (the arrays are capacities; ``packed`` then holds the events at stride *dn)."""
     dev = score.device
     _check_k(k)
     k = max(1, int(k))
@@ -596,7 +621,7 @@ def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int
     l32 = line.data_ptr() if line.dtype == torch.int32 else 0
     l64 = line.data_ptr() if line.dtype == torch.int64 else 0
     ins = (score.data_ptr() if n else 0, pat.data_ptr() if n else 0, l32 if n else 0, l64 if n else 0,
-           _p(line_add), sev_of_pat.data_ptr(), 0, _p(packed) if n else 0)
+           _p(line_add), sev_of_pat.data_ptr(), 0, _p(packed) if n else 0, _p(dn))
 
     def call(wp, wn):
         return N.summarize(ins, n, k, nsev, rows.data_ptr(), pat_hist.data_ptr(), sev_hist.data_ptr(), wp, wn, _s(score),
@@ -609,23 +634,33 @@ def summarize(score: torch.Tensor, pat: torch.Tensor, line: torch.Tensor, k: int
     return rows, pat_hist[:npat], sev_hist[:nsev], packed
 
 
+def dp_payload_width(nk: int, ns: int) -> int:
+    """Columns of the C1+C3+C4 all-gather payload: owned lines, nk counts, ns chain slots, overflow."""
+    return 1 + nk + ns + 1
+
+
 def dp_pack(own_lines: int, freq_counts: torch.Tensor, nk: int, chain: torch.Tensor,
-            out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C1+C3+C4 all-gather payload [owned lines | nk frequency counts | chain table] (int64);
-    ``out``: where to write it (this rank's row of an in-place all-gather buffer)."""
+            out: Optional[torch.Tensor] = None, overflow: Optional[tuple] = None) -> torch.Tensor:
+    """C1+C3+C4 all-gather payload [owned lines | nk frequency counts | chain table | overflow flag]
+    (int64); ``out``: where to write it (this rank's row of an in-place all-gather buffer);
+    ``overflow`` = (device counters [5], host capacities [4]) of a deferred-count step: the flag is
+    set when a counter exceeded its buffer (every rank then vetoes the step's record and re-runs)."""
     ns = chain.numel()
-    pack = out if out is not None else torch.empty(1 + nk + ns, dtype=torch.int64, device=chain.device)
+    pack = out if out is not None else torch.empty(dp_payload_width(nk, ns), dtype=torch.int64, device=chain.device)
     fc = freq_counts if freq_counts.dtype == torch.int64 else freq_counts.to(torch.int64)
-    N.dp_pack(int(own_lines), fc.data_ptr(), nk, chain.data_ptr(), ns, pack.data_ptr(), _s(chain), chain.is_cuda)
+    cnt, caps = (overflow[0].data_ptr(), [int(c) for c in overflow[1]]) if overflow is not None else (0, [])
+    N.dp_pack(int(own_lines), fc.data_ptr(), nk, chain.data_ptr(), ns, pack.data_ptr(), _s(chain), chain.is_cuda,
+              cnt, caps)
     return pack
 
 
 def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: Optional[torch.Tensor],
              slot_e0: torch.Tensor, slot_k: torch.Tensor, red_tail: Optional[torch.Tensor] = None):
-    """From the gathered payloads: (own_start[1], g0[1], n[1], carry[nk], seq_carry uint8[ns]);
-    ``red_tail`` (optional) receives this rank's frequency counts."""
+    """From the gathered payloads: (own_start[1], g0[1], n[1], carry[nk], seq_carry uint8[ns],
+    veto[1]); ``red_tail`` (optional) receives this rank's frequency counts; veto = any rank's
+    overflow flag."""
     dev = g.device
-    sc = torch.empty(5, dtype=torch.int64, device=dev)          # own_start, g0, n (+ pad)
+    sc = torch.empty(5, dtype=torch.int64, device=dev)          # own_start, g0, n, veto (+ pad)
     carry = torch.empty(max(nk, 1), dtype=torch.int64, device=dev)
     if nk == 0:
         carry.zero_()
@@ -633,8 +668,9 @@ def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: 
     g = g.contiguous()
     p = sc.data_ptr()
     N.dp_carry((g.data_ptr(), g.shape[0], rank, nk, ns, int(halo_left), _p(tot) if nk else 0, slot_e0.data_ptr(),
-                slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail)), _s(g), g.is_cuda)
-    return sc[0:1], sc[1:2], sc[2:3], carry, seq
+                slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail), p + 24), _s(g),
+               g.is_cuda)
+    return sc[0:1], sc[1:2], sc[2:3], carry, seq, sc[3:4]
 
 
 def topk_rows(rows: torch.Tensor, k: int, ws: Optional[Workspace] = None) -> torch.Tensor:
@@ -668,9 +704,10 @@ def rescore(gl: torch.Tensor, fac: torch.Tensor, n_lines: int, sp_tuple) -> torc
 
 
 def score_fused(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_carry, st_tuple, sp_tuple, with_factors=False,
-                out: Optional[torch.Tensor] = None):
+                out: Optional[torch.Tensor] = None, dn: Optional[torch.Tensor] = None):
     """k_score with the frequency count fused in: freq = carry[fkey] + rank (-1 without a key).
-    ``out``: float64[n] destination (e.g. the score view of a ``results_buffer``)."""
+    ``out``: float64[n] destination (e.g. the score view of a ``results_buffer``); ``dn``: device
+    event count (the arrays are then capacities; device only)."""
     n = ev_line.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.float64, device=ev_line.device)
@@ -680,7 +717,7 @@ def score_fused(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_carry, st_tuple,
     args = (ev_line.data_ptr(), ev_pat.data_ptr(), ev_seg.data_ptr(), ev_rank.data_ptr(), ev_fkey.data_ptr(),
             freq_carry.data_ptr(), n, st_tuple, sp_tuple, out.data_ptr(), _p(fac))
     if ev_line.is_cuda:
-        N.score_dev(*args, _s(ev_line))
+        N.score_dev(*args, _s(ev_line), _p(dn))
     else:
         N.score_host(*args)
     return out, fac

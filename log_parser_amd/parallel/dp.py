@@ -122,6 +122,8 @@ class StepOutput:
     own_start_dev: Optional[torch.Tensor] = None    # [1] global index of the first owned line
     # pack_events: every owned event as uint8[20 n] = [global line i64 | score f64 | pattern i32]
     events_packed: Optional[torch.Tensor] = None
+    # GPU: recorded on the compute stream after the step's last kernel (before its count read)
+    end_event: Optional[object] = None
 
     # host integers on demand (a host read here would stall the step's launch queue)
     @property
@@ -172,27 +174,70 @@ class ShardedAnalyzer:
              halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False,
              pack_events: bool = False) -> StepOutput:
         """One shard step. ``ls`` / ``ll`` = None: the line index is built here, with the literal
-        prefilter queued behind it before its host read (the GPU filters while the host waits)."""
+        prefilter queued behind it before its host read (the GPU filters while the host waits).
+
+        On a GPU the step reads NO counts between its matchers and its end: hits and events run in
+        device-count mode on capacity-sized buffers (``Engine.prepare(defer=True)``), so the host
+        queues the whole step -- event stage, both collectives, carry, score, summary, record --
+        while the GPU is still matching. Each rank's overflow flag rides in collective 1; any
+        overflow vetoes the frequency record on every rank, and after the one end-of-step read all
+        ranks re-run the step with the capacities they learned."""
         eng = self.engine
-        lib = eng.lib
         rank, wsize = world()
-        dev = text.device
         early = None
         if ls is None:
             box = []
             ls, ll = K.split_lines(text, nbytes, before_read=(lambda: box.append(eng.prefilter_early(text, nbytes)))
                                    if text.is_cuda else None)
             early = box[0] if box else None
+        defer = eng.can_defer(text)
+        for attempt in range(4):
+            out, prep, veto = self._step(text, nbytes, ls, ll, halo_left, halo_right, topk, with_factors, pack_events,
+                                         early if attempt == 0 else None, defer)
+            if not defer:
+                return out
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            h = torch.cat([veto, prep.cnt[:5]]).cpu().tolist()  # the step's one count read, at its end
+            counts, L = h[1:], ls.numel()
+            if not h[0]:
+                eng.arena.learn_deferred(L, counts)
+                out.end_event = end
+                return self._trim(out, prep, counts[4])
+            # some rank overflowed a buffer: every rank learns its exact rates and re-runs
+            eng.arena.learn(L, {"gram": counts[0], "cand": counts[1], "ver": counts[2], "ev": counts[4]}, overflow=True)
+        raise RuntimeError("DP step: buffers still overflowing after re-runs")
+
+    @staticmethod
+    def _trim(out: StepOutput, prep, ne: int) -> StepOutput:
+        """A deferred step's capacity-sized event arrays cut to the step's ``ne`` events."""
+        r = out.result
+        r.ev_line, r.ev_pat, r.ev_seg, r.score = r.ev_line[:ne], r.ev_pat[:ne], r.ev_seg[:ne], r.score[:ne]
+        if r.factors is not None:
+            r.factors = r.factors[:ne]
+        if out.events_packed is not None:
+            out.events_packed = out.events_packed[:20 * ne]
+        return out
+
+    def _step(self, text, nbytes, ls, ll, halo_left, halo_right, topk, with_factors, pack_events, early, defer):
+        eng = self.engine
+        lib = eng.lib
+        rank, wsize = world()
+        dev = text.device
         L = ls.numel()
         own_lo, own_hi = halo_left, L - halo_right
         segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev, upload=eng.upload)
-        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early)
+        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early, defer=defer)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
         ns = chain.numel()
-        g = torch.empty((wsize, 1 + nk + ns), dtype=torch.int64, device=dev)
-        K.dp_pack(own_hi - own_lo, prep.freq_counts, nk, chain, out=g[rank])      # k_dp_pack -> own row
-        all_gather_inplace(g, self.group)                          # collective 1: C1 + C3 + C4
+        g = torch.empty((wsize, K.dp_payload_width(nk, ns)), dtype=torch.int64, device=dev)
+        ovf = None
+        if defer:
+            c = prep.caps
+            ovf = (prep.cnt, (c["gram"], c["cand"], c["ver"], c["ev"]))
+        K.dp_pack(own_hi - own_lo, prep.freq_counts, nk, chain, out=g[rank], overflow=ovf)   # k_dp_pack -> own row
+        all_gather_inplace(g, self.group)                          # collective 1: C1 + C3 + C4 + overflow
         own_counts = g[:, 0]
         # collective 2 buffer, one row per rank: [pattern hist | severity hist | frequency counts |
         # top-k rows (k x 3 f64)]; k_dp_carry seeds the counts, the summary kernel the histograms + rows
@@ -202,7 +247,7 @@ class ShardedAnalyzer:
         H = P + S + nk
         red2 = torch.zeros((wsize, H + 3 * k), dtype=torch.int64, device=dev)
         mine = red2[rank]
-        own_start, segs.g0, segs.n, carry, seq_carry = K.dp_carry(     # k_dp_carry: device scalars, no sync
+        own_start, segs.g0, segs.n, carry, seq_carry, veto = K.dp_carry(     # k_dp_carry: device scalars, no sync
             g, rank, nk, ns, halo_left, eng.freq_carry() if nk else None, self.slot_e0, self.slot_k,
             red_tail=mine[P + S:H] if nk else None)
         res = eng.finish(prep, segs, carry, seq_carry, with_factors)
@@ -211,16 +256,16 @@ class ShardedAnalyzer:
         rows_out = mine[H:].view(torch.float64).view(k, 3)
         _, _, _, packed = K.summarize(res.score, res.ev_pat, res.ev_line, k, eng.tabs["sev_index"], P, S,
                                       line_add=segs.g0, ws=eng.ws, pack_events=pack_events, hist_out=mine[:H],
-                                      rows_out=rows_out)
+                                      rows_out=rows_out, dn=prep.ne_dev)
         all_gather_inplace(red2, self.group)                       # collective 2: C5 + C6 + C7
         red = red2[:, :H].sum(0) if wsize > 1 else red2[0, :H]
-        eng.commit_frequency(red[P + S:])
+        eng.commit_frequency(red[P + S:], veto=veto if defer else None)
         out = StepOutput(res, own_counts, rank, red[:P], severity_counts=red[P:P + S], own_lo=own_lo,
                          own_start_dev=own_start, events_packed=packed)
         if topk > 0 and rank == 0:
             allrows = red2[:, H:].contiguous().view(torch.float64).view(-1, 3)
             out.topk_rows = K.topk_rows(allrows, k, ws=eng.ws) if allrows.shape[0] > k else allrows
-        return out
+        return out, prep, veto
 
     def summary(self, pattern_counts: torch.Tensor, first_pat: Optional[int] = None,
                 severity_counts: Optional[torch.Tensor] = None) -> dict:

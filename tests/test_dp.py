@@ -52,7 +52,7 @@ def _reference():
     return outs
 
 
-def _worker(rank, world, port, q, dev="cpu"):
+def _worker(rank, world, port, q, dev="cpu", tiny_rank=-1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -71,6 +71,8 @@ def _worker(rank, world, port, q, dev="cpu"):
         ls = (gls[a:b] - base).contiguous()
         ll = gll[a:b].contiguous()
         sa = ShardedAnalyzer(eng)
+        if rank == tiny_rank:              # this rank's buffers overflow on the first step
+            eng.arena.rate = {k: 1e-6 for k in eng.arena.rate}
         res = []
         for _ in range(STEPS):
             out = sa.step(t, len(shard), ls, ll, hl, hr, topk=5)
@@ -91,12 +93,12 @@ def _free_port():
     return p
 
 
-def _run_sharded(world, dev):
+def _run_sharded(world, dev, tiny_rank=-1):
     ref = _reference()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dev)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dev, tiny_rank)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))
@@ -128,6 +130,14 @@ def test_sharded_equals_single_gpu_ranks(gpu_device):
     carries / histograms / top-k collectives (host-staged gloo here; RCCL on a multi-GPU node)
     must reproduce the single-process CPU reference event for event."""
     _run_sharded(2, "cuda:0")
+
+
+@pytest.mark.gpu
+def test_sharded_one_rank_overflow_gpu_ranks(gpu_device):
+    """GPU steps read no counts until their end: rank 1 starts with capacities far too small, its
+    overflow flag travels in collective 1, BOTH ranks veto the frequency record and re-run the
+    step, and every step still equals the single-process reference (window recorded once)."""
+    _run_sharded(2, "cuda:0", tiny_rank=1)
 
 
 def _worker_p2p(rank, world, port, q, dev="cpu"):

@@ -87,3 +87,30 @@ def test_bulk_path_hot_buckets_equal_host_twins(gpu_device):
     d, c = _run_both(lib, "\n".join(lines).encode(), gpu_device)
     assert d["line"].numel() > 3 * 59_000                            # every line, three patterns
     _assert_same(d, c)
+
+
+def test_deferred_dp_step_overflow_reruns_and_records_once(gpu_device):
+    """A DP step reads no counts until its end (device-count events, overflow flag in the payload).
+    With every capacity far too small the first attempt overflows: its frequency record is vetoed
+    on the device, the step re-runs with learned capacities, and the result and the window equal
+    a plain engine run's."""
+    from log_parser_amd.parallel.dp import ShardedAnalyzer
+    sets, trig = realistic_library(200, seed=41)
+    lib = CompiledLibrary(sets, ScoringParams())
+    data = make_log(60_000, trig, seed=42, hit_rate=0.05).encode()
+    e1, e2 = _eng(lib, gpu_device), _eng(lib, gpu_device)
+    t = _text(gpu_device, data)
+    ls, ll = K.split_lines(t, len(data))
+    e1.arena.rate = {k: 1e-6 for k in e1.arena.rate}
+    out = ShardedAnalyzer(e1).step(t, len(data), ls, ll, 0, 0, topk=10, pack_events=True)
+    ref = e2.run(t, len(data), ls, ll, Segments.single(ls.numel(), gpu_device), e2.freq_carry())
+    ne = ref.ev_line.numel()
+    assert ne > 1000 and e1.arena.last["events"] == ne
+    assert torch.equal(out.result.ev_line, ref.ev_line) and torch.equal(out.result.ev_pat, ref.ev_pat)
+    torch.testing.assert_close(out.result.score, ref.score, rtol=0, atol=0)
+    assert out.events_packed.numel() == 20 * ne
+    e2.commit_frequency(ref.freq_counts)
+    assert e1.freq.statistics() == e2.freq.statistics()
+    # a second step runs within the learned capacities: no re-run, same window evolution
+    out2 = ShardedAnalyzer(e1).step(t, len(data), ls, ll, 0, 0, topk=10)
+    assert torch.equal(out2.result.ev_line, ref.ev_line)

@@ -583,6 +583,10 @@ PYBIND11_MODULE(_lpnative, m) {
                   P<int64_t>(u(9)), P<int64_t>(u(10)), P<int64_t>(u(11)), P<int64_t>(u(12)), P<uint8_t>(u(13)),
                   P<int64_t>(u(14))};
     if (a.size() > 15) A.veto = P<int64_t>(u(15));
+    if (a.size() > 17) {
+      A.zero = P<int64_t>(u(16));
+      A.nzero = a[17].cast<int64_t>();
+    }
     dp_carry(A, s, dev);
   });
   // veto (optional, device int64): no record when *veto != 0 (a DP step that re-runs)

@@ -61,6 +61,7 @@ LP_HD void dp_carry_one(int64_t i, const DpCarryArgs& A) {
     A.carry[i] = c;
     if (A.red_tail) A.red_tail[i] = A.g[A.rank * row + 1 + i];
   }
+  if (i < A.nzero) A.zero[i] = 0;
   if (i < A.ns) {
     int64_t k = A.slot_k[i];
     for (int q = A.rank - 1; q >= 0 && k >= 0; --q) k = A.g[q * row + 1 + A.nk + A.slot_e0[i] + k];
@@ -105,7 +106,7 @@ void dp_pack(int64_t own_lines, const int64_t* freq, int nk, const int32_t* chai
 }
 
 void dp_carry(const DpCarryArgs& A, uint64_t stream, bool dev) {
-  const int64_t n = std::max<int64_t>(1, std::max<int64_t>(A.nk, A.ns));
+  const int64_t n = std::max<int64_t>(std::max<int64_t>(1, A.nzero), std::max<int64_t>(A.nk, A.ns));
   if (dev) {
     hipLaunchKernelGGL(k_dp_carry, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), n, A);

@@ -146,6 +146,8 @@ struct DpCarryArgs {
   uint8_t* seq_carry;        // [ns]
   int64_t* red_tail;         // [nk] this rank's counts into the all-reduce buffer (may be null)
   int64_t* veto = nullptr;   // [1] OR of every rank's overflow flag (may be null)
+  int64_t* zero = nullptr;   // [nzero] zeroed (this rank's histogram slots of the all-gather buffer)
+  int64_t nzero = 0;
 };
 // payload [1 + nk + ns + 1]; cnt (device [5] match / event counters, may be null) and caps (host
 // [4]: gram, candidate, verified, event capacities) set the trailing overflow flag

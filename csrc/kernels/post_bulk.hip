@@ -724,7 +724,9 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
     PB_CHECK(hipMemsetAsync(A.hit_off, 0, (size_t)(R + 1) * sizeof(int64_t), st));
     return C.used;
   }
-  PB_CHECK(hipMemsetAsync(cnt, 0, zero_end, st));
+  // whole 256-byte granules (the next carve starts on one): a tail that is not a multiple of 16
+  // bytes makes the runtime split the fill into two kernels
+  PB_CHECK(hipMemsetAsync(cnt, 0, (zero_end + 255) & ~size_t(255), st));
   const unsigned g = pb_agg_grid(n);
   const HbPlan Q{shift, base};
   hipLaunchKernelGGL(k_hb_count, dim3(g), dim3(PB_AT), agg_lds(R, false), st, A, cnt);
@@ -789,7 +791,7 @@ size_t events_bulk_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t 
   if (!ws || C.used > ws_bytes) return C.used;
   hipStream_t st = pb_stream(stream);
   uint8_t* zero_from = A.cov ? reinterpret_cast<uint8_t*>(bin_cnt) : reinterpret_cast<uint8_t*>(cov);
-  PB_CHECK(hipMemsetAsync(zero_from, 0, static_cast<uint8_t*>(ws) + zero_end - zero_from, st));
+  PB_CHECK(hipMemsetAsync(zero_from, 0, static_cast<uint8_t*>(ws) + ((zero_end + 255) & ~size_t(255)) - zero_from, st));
   if (A.cov && L > 0) PB_CHECK(hipMemsetAsync(A.cov, 0, (size_t)L * sizeof(int32_t), st));
   // device-count mode (A.dcounts = [hits, events] on the device): nh / ne are capacities
   const int64_t* dc = A.dcounts;

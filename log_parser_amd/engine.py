@@ -342,9 +342,7 @@ class Engine:
             self.n_cus = int(props.multi_processor_count)
             self.pf_grid = self.n_cus * 4
             if bool(self.config.get("engine.scan-stream", True)):
-                # LP_SIDE_PRIORITY (A/B knob): stream priority of the scan stream
-                prio = int(__import__("os").environ.get("LP_SIDE_PRIORITY", "0"))
-                self._side = (torch.cuda.Stream(self.device, priority=prio), torch.cuda.Event(), torch.cuda.Event())
+                self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
         else:
             self.n_cus = 1
             self.pf_grid = 1
@@ -603,9 +601,9 @@ class Engine:
         """Per sequence-event slot: event index still unmatched after this shard (-1 = done)."""
         tabs = self.tabs
         n = self.lib.n_seq_events
-        out = torch.full((max(n, 1),), -1, dtype=torch.int32, device=prep.hit_off.device)
         if n == 0:
-            return out
+            return torch.full((1,), -1, dtype=torch.int32, device=prep.hit_off.device)
+        out = torch.empty(n, dtype=torch.int32, device=prep.hit_off.device)     # k_seq_chain writes every slot
         dev = prep.hit_off.is_cuda
         s = torch.cuda.current_stream(prep.hit_off.device).cuda_stream if dev else 0
         N.seq_chain(tabs["slot_seq"].data_ptr(), tabs["seq_ev_off"].data_ptr(), tabs["seq_ev_reg"].data_ptr(),

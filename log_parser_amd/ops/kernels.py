@@ -428,7 +428,7 @@ class EarlyPrefilter:
         L_est = int(nbytes * _LINES_PER_BYTE[0]) + 1
         self.cap = arena.caps(L_est)["gram"]
         self.gh = torch.empty(self.cap, dtype=torch.int64, device=text.device)
-        self.cnt = torch.zeros(6, dtype=torch.int64, device=text.device)
+        self.cnt = torch.zeros(7, dtype=torch.int64, device=text.device)
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
                         pf_grid, _s(text))
 
@@ -462,8 +462,9 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
         else:
             gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
             # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters),
-            # then the events that fit their buffer (deferred steps: post_events' ne_fit)
-            cnt = torch.zeros(6, dtype=torch.int64, device=dev)
+            # then the events that fit their buffer (deferred steps: post_events' ne_fit) and the
+            # DP step's overflow veto (k_dp_carry)
+            cnt = torch.zeros(7, dtype=torch.int64, device=dev)
         cand = torch.empty(cap["cand"], dtype=torch.int64, device=dev)
         ver = torch.empty(cap["ver"], dtype=torch.int64, device=dev)
         c0 = cnt.data_ptr()
@@ -472,6 +473,7 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             side[1].record()
             side[0].wait_event(side[1])
             sst = side[0].cuda_stream
+        blk = line_block_index(line_start, nbytes)
         # the long pole first: literal-free scans (own stream when `side`)
         for sp in tabs["scan_passes"]:
             N.scan_multi(text.data_ptr(), nbytes, line_start.data_ptr(), line_len.data_ptr(), L, sp, ver.data_ptr(),
@@ -487,7 +489,6 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             side[2].record(side[0])
         elif tick:
             tick("scan")
-        blk = line_block_index(line_start, nbytes)
         if early is None:
             N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L, gh.data_ptr(), cap["gram"],
                             c0, pf_grid, st)
@@ -655,10 +656,12 @@ def dp_pack(own_lines: int, freq_counts: torch.Tensor, nk: int, chain: torch.Ten
 
 
 def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: Optional[torch.Tensor],
-             slot_e0: torch.Tensor, slot_k: torch.Tensor, red_tail: Optional[torch.Tensor] = None):
+             slot_e0: torch.Tensor, slot_k: torch.Tensor, red_tail: Optional[torch.Tensor] = None,
+             veto_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None):
     """From the gathered payloads: (own_start[1], g0[1], n[1], carry[nk], seq_carry uint8[ns],
     veto[1]); ``red_tail`` (optional) receives this rank's frequency counts; veto = any rank's
-    overflow flag."""
+    overflow flag (written into ``veto_out`` when given); ``zero`` (int64, optional) is zeroed by
+    the same kernel."""
     dev = g.device
     sc = torch.empty(5, dtype=torch.int64, device=dev)          # own_start, g0, n, veto (+ pad)
     carry = torch.empty(max(nk, 1), dtype=torch.int64, device=dev)
@@ -667,10 +670,11 @@ def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: 
     seq = torch.empty(max(ns, 1), dtype=torch.uint8, device=dev)
     g = g.contiguous()
     p = sc.data_ptr()
+    veto = veto_out if veto_out is not None else sc[3:4]
     N.dp_carry((g.data_ptr(), g.shape[0], rank, nk, ns, int(halo_left), _p(tot) if nk else 0, slot_e0.data_ptr(),
-                slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail), p + 24), _s(g),
-               g.is_cuda)
-    return sc[0:1], sc[1:2], sc[2:3], carry, seq, sc[3:4]
+                slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail), veto.data_ptr(),
+                _p(zero), 0 if zero is None else zero.numel()), _s(g), g.is_cuda)
+    return sc[0:1], sc[1:2], sc[2:3], carry, seq, veto
 
 
 def topk_rows(rows: torch.Tensor, k: int, ws: Optional[Workspace] = None) -> torch.Tensor:

@@ -198,9 +198,9 @@ class ShardedAnalyzer:
                 return out
             end = torch.cuda.Event(enable_timing=True)
             end.record()
-            h = torch.cat([veto, prep.cnt[:5]]).cpu().tolist()  # the step's one count read, at its end
-            counts, L = h[1:], ls.numel()
-            if not h[0]:
+            h = prep.cnt.cpu().tolist()          # the step's one count read, at its end (veto = cnt[6])
+            counts, L = h[:5], ls.numel()
+            if not h[6]:
                 eng.arena.learn_deferred(L, counts)
                 out.end_event = end
                 return self._trim(out, prep, counts[4])
@@ -245,11 +245,12 @@ class ShardedAnalyzer:
         K._check_k(topk)
         k = max(1, topk)
         H = P + S + nk
-        red2 = torch.zeros((wsize, H + 3 * k), dtype=torch.int64, device=dev)
+        red2 = torch.empty((wsize, H + 3 * k), dtype=torch.int64, device=dev)   # other rows: the all-gather
         mine = red2[rank]
         own_start, segs.g0, segs.n, carry, seq_carry, veto = K.dp_carry(     # k_dp_carry: device scalars, no sync
             g, rank, nk, ns, halo_left, eng.freq_carry() if nk else None, self.slot_e0, self.slot_k,
-            red_tail=mine[P + S:H] if nk else None)
+            red_tail=mine[P + S:H] if nk else None, veto_out=prep.cnt[6:7] if defer else None,
+            zero=mine[:P + S])                                     # histogram slots (summary kernel adds)
         res = eng.finish(prep, segs, carry, seq_carry, with_factors)
         # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
         # rank's top-k rows with global line numbers, no host sync) into this rank's row

@@ -2,7 +2,7 @@
 // AnalysisService.java:188-215 -- event count, severity histogram, highest severity -- plus the
 // north star's top-k event reduction), and the streaming mode's final re-score.
 //
-//   k_summ_level  one block per 4096-item chunk: the chunk is bitonic-sorted in LDS by
+//   k_summ_level  one block per 4096-item chunk (1024 when k <= 256): the chunk is bitonic-sorted in LDS by
 //                 (score desc, global line asc, pattern asc) -- a total, deterministic order, so
 //                 every rank / run agrees on ties -- and its first k rows are written out. Level
 //                 0 reads events (and adds them to the pattern / severity histograms with one
@@ -26,6 +26,11 @@ namespace lp {
 
 constexpr int SUMM_THREADS = 1024;
 constexpr int SUMM_CHUNK = 4096;
+// k <= 256 (the usual top-100): 1024-row chunks in 256-thread blocks. A 44.5k-event step then runs
+// its first level on 44 CUs instead of 11, with 55 barrier stages of 1024 keys instead of 78 of 4096
+// (the 4096-row level took 68 + 48 us per step for two levels, profiles/r3_w)
+constexpr int SUMM_THREADS_S = 256;
+constexpr int SUMM_CHUNK_S = 1024;
 constexpr int SUMM_LDS_SEV = 256;             // severity histogram in LDS up to this many names
 
 struct Row {
@@ -74,22 +79,23 @@ __device__ __forceinline__ bool key_less(const Key& a, const Key& b) {
   return a.hi != b.hi ? a.hi < b.hi : a.lo < b.lo;
 }
 
-// One 4096-row chunk per 1024-thread block: load (+ histograms, + packed event records), bitonic
+// One CHUNK-row chunk per THREADS-thread block: load (+ histograms, + packed event records), bitonic
 // sort of 128-bit keys in LDS (one compare-exchange per thread per stage pair), write the first k.
-__global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t n, int k, int nsev,
-                                                             double* __restrict__ rows_out,
-                                                             unsigned long long* __restrict__ pat_hist,
-                                                             unsigned long long* __restrict__ sev_hist) {
-  __shared__ Key s_key[SUMM_CHUNK];
+template <int CHUNK, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_summ_level(SummIn in, int64_t n, int k, int nsev,
+                                                        double* __restrict__ rows_out,
+                                                        unsigned long long* __restrict__ pat_hist,
+                                                        unsigned long long* __restrict__ sev_hist) {
+  __shared__ Key s_key[CHUNK];
   __shared__ unsigned int s_sev[SUMM_LDS_SEV];
   const bool lds_sev = sev_hist && nsev <= SUMM_LDS_SEV;
   if (lds_sev)
-    for (int j = threadIdx.x; j < nsev; j += SUMM_THREADS) s_sev[j] = 0;
+    for (int j = threadIdx.x; j < nsev; j += THREADS) s_sev[j] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * SUMM_CHUNK;
+  const int64_t base = (int64_t)blockIdx.x * CHUNK;
   const int64_t add = in.line_add ? *in.line_add : 0;
   if (in.dn && !in.rows) n = min(n, *in.dn);      // capacity n, device count *dn
-  for (int j = threadIdx.x; j < SUMM_CHUNK; j += SUMM_THREADS) {
+  for (int j = threadIdx.x; j < CHUNK; j += THREADS) {
     const int64_t i = base + j;
     Row r = empty_row();
     if (i < n) {
@@ -118,14 +124,14 @@ __global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t 
   }
   __syncthreads();
   if (lds_sev)
-    for (int j = threadIdx.x; j < nsev; j += SUMM_THREADS)
+    for (int j = threadIdx.x; j < nsev; j += THREADS)
       if (s_sev[j]) atomicAdd(sev_hist + j, (unsigned long long)s_sev[j]);
   // bitonic sort, ascending key order = row order
-  for (int size = 2; size <= SUMM_CHUNK; size <<= 1) {
+  for (int size = 2; size <= CHUNK; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
 #pragma unroll
-      for (int q = 0; q < SUMM_CHUNK / 2 / SUMM_THREADS; ++q) {
-        const int t = threadIdx.x + q * SUMM_THREADS;
+      for (int q = 0; q < CHUNK / 2 / THREADS; ++q) {
+        const int t = threadIdx.x + q * THREADS;
         const int lo = 2 * t - (t & (stride - 1));
         const int hi = lo + stride;
         const bool up = (lo & size) == 0;
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(SUMM_THREADS) void k_summ_level(SummIn in, int64_t 
     }
   }
   double* o = rows_out + (int64_t)blockIdx.x * k * 3;
-  for (int j = threadIdx.x; j < k; j += SUMM_THREADS) {
+  for (int j = threadIdx.x; j < k; j += THREADS) {
     const Row r = key_row(s_key[j]);
     o[3 * j] = r.score;
     o[3 * j + 1] = (double)r.line;
@@ -163,8 +169,10 @@ static void check(const char* what) {
 size_t summarize_dev(const SummIn& in, int64_t n, int k, int nsev, double* top_rows, unsigned long long* pat_hist,
                      unsigned long long* sev_hist, void* ws, size_t ws_bytes, uint64_t stream) {
   if (k < 1 || k > SUMM_CHUNK / 2) throw std::runtime_error("summarize: 1 <= k <= 1024");
+  const bool small = k <= SUMM_CHUNK_S / 4;
+  const int64_t chunk = small ? SUMM_CHUNK_S : SUMM_CHUNK;
   // workspace: two ping-pong row buffers sized for level 0
-  const int64_t nb0 = std::max<int64_t>(1, (n + SUMM_CHUNK - 1) / SUMM_CHUNK);
+  const int64_t nb0 = std::max<int64_t>(1, (n + chunk - 1) / chunk);
   const size_t rows_bytes = (size_t)nb0 * k * 3 * sizeof(double);
   const size_t need = 2 * rows_bytes;
   if (!ws || ws_bytes < need) return need;
@@ -175,15 +183,19 @@ size_t summarize_dev(const SummIn& in, int64_t n, int k, int nsev, double* top_r
   int which = 0;
   for (int level = 0;; ++level) {
     double* dst = nb == 1 ? top_rows : buf[which];
-    hipLaunchKernelGGL(k_summ_level, dim3((unsigned)nb), dim3(SUMM_THREADS), 0, st, cur, m, k, nsev, dst,
-                       level == 0 ? pat_hist : nullptr, level == 0 ? sev_hist : nullptr);
+    if (small)
+      hipLaunchKernelGGL((k_summ_level<SUMM_CHUNK_S, SUMM_THREADS_S>), dim3((unsigned)nb), dim3(SUMM_THREADS_S), 0, st,
+                         cur, m, k, nsev, dst, level == 0 ? pat_hist : nullptr, level == 0 ? sev_hist : nullptr);
+    else
+      hipLaunchKernelGGL((k_summ_level<SUMM_CHUNK, SUMM_THREADS>), dim3((unsigned)nb), dim3(SUMM_THREADS), 0, st, cur,
+                         m, k, nsev, dst, level == 0 ? pat_hist : nullptr, level == 0 ? sev_hist : nullptr);
     check("k_summ_level");
     if (nb == 1) break;
     SummIn nx{};
     nx.rows = dst;
     cur = nx;
     m = nb * (int64_t)k;
-    nb = (m + SUMM_CHUNK - 1) / SUMM_CHUNK;
+    nb = (m + chunk - 1) / chunk;
     which ^= 1;
   }
   return need;

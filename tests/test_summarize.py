@@ -49,7 +49,7 @@ def _run(dev, score, line, pat, sev_index, k, npat, nsev, add):
 
 
 CASES = [(0, 5), (1, 5), (7, 5), (2047, 100), (2048, 100), (2049, 1), (50_000, 100), (50_000, 1024),
-         (300_000, 37)]
+         (300_000, 37), (50_000, 256), (50_000, 257)]     # 256 / 257: the 1024-row / 4096-row chunk variants
 
 
 @pytest.mark.parametrize("n,k", CASES)

@@ -481,13 +481,34 @@ PYBIND11_MODULE(_lpnative, m) {
   // ---- device launchers
   m.def("line_index_tiles", &line_index_tiles);
   m.def("line_index_dev", [](uint64_t text, int64_t n, uint64_t ws, int64_t ntiles_cap, uint64_t starts, uint64_t lens,
-                             int64_t cap, uint64_t info, bool trim, uint64_t blk, int64_t nblk, uint64_t s) {
+                             int64_t cap, uint64_t info, bool trim, uint64_t blk, int64_t nblk, uint64_t s, bool counted) {
     line_index_dev(P<const uint8_t>(text), n, LineIndexWs{P<int64_t>(ws), ntiles_cap, size_t(1) << 20}, P<int64_t>(starts),
-                   P<int32_t>(lens), cap, P<int64_t>(info), trim, P<int32_t>(blk), nblk, s); });
+                   P<int32_t>(lens), cap, P<int64_t>(info), trim, P<int32_t>(blk), nblk, s, counted); },
+        py::arg("text"), py::arg("n"), py::arg("ws"), py::arg("ntiles_cap"), py::arg("starts"), py::arg("lens"),
+        py::arg("cap"), py::arg("info"), py::arg("trim"), py::arg("blk"), py::arg("nblk"), py::arg("s"),
+        py::arg("counted") = false);
+  // nlp (optional): (nlm, cnt, crf, ntiles) of line_index_pass1 -- the fused line-index pass 1
   m.def("prefilter_dev", [](uint64_t text, int64_t n, py::tuple pf, uint64_t ls, int64_t nl, uint64_t cand, int64_t cap,
-                            uint64_t count, int grid, uint64_t s) {
+                            uint64_t count, int grid, uint64_t s, py::object nlp) {
+    NlOut o;
+    const bool fused = !nlp.is_none();
+    if (fused) {
+      py::tuple t = nlp.cast<py::tuple>();
+      o.nlm = P<uint64_t>(t[0].cast<uint64_t>());
+      o.cnt = P<int32_t>(t[1].cast<uint64_t>());
+      o.crf = P<int32_t>(t[2].cast<uint64_t>());
+      o.ntiles = t[3].cast<int64_t>();
+    }
     prefilter_dev(P<const uint8_t>(text), n, pf_from(pf), P<const int64_t>(ls), nl, P<int64_t>(cand), cap,
-                  P<unsigned long long>(count), grid, s); });
+                  P<unsigned long long>(count), grid, s, fused ? &o : nullptr); },
+        py::arg("text"), py::arg("n"), py::arg("pf"), py::arg("ls"), py::arg("nl"), py::arg("cand"), py::arg("cap"),
+        py::arg("count"), py::arg("grid"), py::arg("s"), py::arg("nlp") = py::none());
+  // zeroes and returns the line index's pass-1 outputs (nlm, cnt, crf, ntiles) for a fused prefilter
+  m.def("line_index_pass1", [](uint64_t ws, int64_t ntiles_cap, int64_t n, uint64_t s) {
+    const NlOut o = line_index_pass1_views(LineIndexWs{P<int64_t>(ws), ntiles_cap, size_t(1) << 20}, n, s);
+    return py::make_tuple(reinterpret_cast<uint64_t>(o.nlm), reinterpret_cast<uint64_t>(o.cnt),
+                          reinterpret_cast<uint64_t>(o.crf), o.ntiles);
+  });
   m.def("pf_verify_dev", [](uint64_t gh, int64_t n, uint64_t text, int64_t nb, py::tuple pf, uint64_t ls, int64_t nl,
                             uint64_t blk, uint64_t cand, int64_t cap, uint64_t count, uint64_t s, uint64_t dn,
                             int max_grid) {

@@ -13,6 +13,8 @@
 //   k_line_trim  Java's trailing-empty trimming -> info[2] = lines kept.
 // k_nl_lines also writes the coarse 4 KiB block -> line index the literal verify uses (one wave
 // per block: the line of its first byte is the number of '\n' before it).
+// Bulk DP steps fold pass 1 into the literal prefilter's read of the text (lp_kernels.hip
+// k_prefilter<..., NLF>): the same counts, masks and flags, one pass over the text fewer.
 // A single-pass decoupled look-back variant (tile ticket + 256 predecessor states per round
 // trip) was measured at ~1.08 ms per 1.33 GB vs ~0.55 ms for these two passes: the INCLUSIVE
 // frontier, not HBM, sets its pace (docs/PERFORMANCE.md).
@@ -278,8 +280,23 @@ __global__ __launch_bounds__(256) void k_line_trim(const int32_t* __restrict__ l
 
 int64_t line_index_tiles(int64_t nbytes) { return (nbytes + LI_TILE - 1) / LI_TILE; }
 
+NlOut line_index_pass1_views(const LineIndexWs& W, int64_t nbytes, uint64_t stream) {
+  const int64_t nt = line_index_tiles(nbytes);
+  if (nt <= 0 || nt > W.ntiles_cap) throw std::runtime_error("line_index: empty text or workspace too small");
+  NlOut o;
+  o.cnt = reinterpret_cast<int32_t*>(W.buf + 3 * W.ntiles_cap);
+  o.crf = o.cnt + W.ntiles_cap;
+  o.nlm = reinterpret_cast<uint64_t*>(W.buf + 4 * W.ntiles_cap);
+  o.ntiles = nt;
+  // counts + flags are accumulated with atomics by the fused pass: zero [cnt, crf + nt) at once
+  const hipError_t e = hipMemsetAsync(o.cnt, 0, (size_t)(W.ntiles_cap + nt) * sizeof(int32_t),
+                                      reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in line_index");
+  return o;
+}
+
 void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, int64_t* starts, int32_t* lens,
-                    int64_t cap, int64_t* info, bool trim, int32_t* blk, int64_t nblk, uint64_t stream) {
+                    int64_t cap, int64_t* info, bool trim, int32_t* blk, int64_t nblk, uint64_t stream, bool counted) {
   const int64_t nt = line_index_tiles(nbytes);
   if (nt <= 0 || nt > W.ntiles_cap) throw std::runtime_error("line_index: empty text or workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -295,7 +312,7 @@ void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, i
           hipSuccess ||
       tmp_bytes > W.tmp_bytes)
     throw std::runtime_error("line_index: scan workspace too small");
-  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, cnt, nlm, crf);
+  if (!counted) hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, cnt, nlm, crf);
   if (rocprim::exclusive_scan(tmp, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
       hipSuccess)
     throw std::runtime_error("line_index: rocprim scan failed");

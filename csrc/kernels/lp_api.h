@@ -10,8 +10,17 @@ namespace lp {
 
 // worker threads of the host twins (CPU backend)
 void set_host_threads(int n);
+// line-index pass 1 folded into the bulk prefilter (line_index.hip k_nl_count's outputs): per 16 KiB
+// tile the '\n' count and the "\r\n" flag (both zeroed by the caller), per 64 bytes a '\n' bitmask
+struct NlOut {
+  uint64_t* nlm = nullptr;   // [ntiles * 256]
+  int32_t* cnt = nullptr;    // [ntiles]
+  int32_t* crf = nullptr;    // [ntiles]
+  int64_t ntiles = 0;
+};
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
-                   int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream);
+                   int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream,
+                   const NlOut* nl = nullptr);
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn = nullptr,
@@ -128,7 +137,11 @@ int64_t line_index_tiles(int64_t nbytes);
 // Java's trailing-empty trimming (trim only). Lines = info[0] + 1 before trimming.
 // blk (optional) [nblk]: line holding byte b << 12 (the coarse index of lp_core.h locate_line)
 void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, int64_t* starts, int32_t* lens,
-                    int64_t cap, int64_t* info, bool trim, int32_t* blk, int64_t nblk, uint64_t stream);
+                    int64_t cap, int64_t* info, bool trim, int32_t* blk, int64_t nblk, uint64_t stream,
+                    bool counted = false);
+// the workspace views pass 1 writes (counted = true: a fused prefilter already wrote them); zeroes
+// the counts and flags on `stream`
+NlOut line_index_pass1_views(const LineIndexWs& W, int64_t nbytes, uint64_t stream);
 }  // namespace lp
 
 // ---- DP step bookkeeping (dp_glue.hip)

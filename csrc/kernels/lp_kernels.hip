@@ -112,14 +112,31 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
 //     four 16-lane groups over 16 slots of 16 B; the lanes of each group have distinct l & 15, so
 //     every group hits 16 distinct slots -- conflict-free for any bytes. 64 KiB of LDS: the TD
 //     variant runs 1024-thread blocks, one per CU.
+//   NLF: the line index's first pass rides on this read of the text (bulk DP steps): per 16-byte
+//     unit the '\n' bits, four lanes' bits form the 64-bit mask word of 64 bytes (lanes 4q..4q+3
+//     hold consecutive units), a wave's 64 units are 1 KiB of one 16 KiB tile -> one atomic count
+//     per wave and tile; a '\r' right before a '\n' flags the '\n''s tile (CRLF logs). The outputs
+//     equal line_index.hip k_nl_count's, which then does not run.
 template <bool TD>
 constexpr int pf_threads() { return TD ? 1024 : PF_THREADS; }
 
-template <int GM, int S, int PF_UNROLL, bool TD>
+constexpr int NL_WORDS_PER_TILE = 256;     // line_index.hip: 64-byte mask words per 16 KiB tile
+
+__device__ __forceinline__ uint32_t nl_zero_bytes(uint32_t t) {   // high bit of every 0x00 byte (exact)
+  const uint32_t y = (t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(y | t | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t nl_pack4(uint32_t x) {          // bits 7, 15, 23, 31 -> bits 0..3
+  const uint32_t y = x >> 7;
+  const uint32_t z = (y | (y >> 7)) & 0x00030003u;
+  return (z | (z >> 14)) & 0xFu;
+}
+
+template <int GM, int S, int PF_UNROLL, bool TD, bool NLF>
 __global__ __launch_bounds__(pf_threads<TD>()) void k_prefilter(const uint8_t* __restrict__ text, int64_t nbytes,
                                                           PfTables T, const int64_t* __restrict__ line_start,
                                                           int64_t nlines, int64_t* cand, int64_t cap,
-                                                          unsigned long long* count) {
+                                                          unsigned long long* count, NlOut NL) {
   // dynamic LDS: [bloom (1<<bits)/8 B, GM only][teddy 16 x 4 KiB, TD only][candidates PF_BUF x 8 B][cnt | pad | gbase]
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const int bits = T.bloom_bits;
@@ -201,6 +218,46 @@ __global__ __launch_bounds__(pf_threads<TD>()) void k_prefilter(const uint8_t* _
       if (u < nunits) {
         v[j] = *reinterpret_cast<const uint4*>(text + (u << 4));
         nx[j] = *reinterpret_cast<const uint32_t*>(text + (u << 4) + 16);
+      }
+    }
+    if constexpr (NLF) {
+#pragma unroll
+      for (int j = 0; j < PF_UNROLL; ++j) {
+        const int64_t u = ub + threadIdx.x + (int64_t)j * blockDim.x;
+        const int64_t p0 = u << 4;
+        uint32_t m16 = 0;
+        if (u < nunits) {
+          const uint32_t w4[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+          uint32_t cr16 = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            m16 |= nl_pack4(nl_zero_bytes(w4[q] ^ 0x0A0A0A0Au)) << (4 * q);
+            cr16 |= nl_pack4(nl_zero_bytes(w4[q] ^ 0x0D0D0D0Du)) << (4 * q);
+          }
+          const int64_t rem = nbytes - p0;
+          const uint32_t valid = rem >= 16 ? 0xFFFFu : ((1u << rem) - 1u);
+          m16 &= valid;
+          cr16 &= valid;
+          if (cr16) {                          // rare outside CRLF logs
+            const uint32_t nl_next = (rem > 16 && (nx[j] & 0xFFu) == 0x0Au) ? 1u : 0u;
+            uint32_t pairs = cr16 & ((m16 | (nl_next << 16)) >> 1);
+            while (pairs) {
+              const int b = __ffs(pairs) - 1;
+              pairs &= pairs - 1;
+              atomicOr(NL.crf + ((p0 + b + 1) >> 14), 1);
+            }
+          }
+        }
+        // every lane shuffles (convergent); lane 4q writes the word of units 4q..4q+3
+        const uint32_t m01 = m16 | ((uint32_t)__shfl_down((int)m16, 1, 64) << 16);
+        const uint32_t m23 = (uint32_t)__shfl_down((int)m01, 2, 64);
+        const int64_t word = u >> 2;
+        if ((threadIdx.x & 3) == 0 && word < NL.ntiles * NL_WORDS_PER_TILE)
+          NL.nlm[word] = (uint64_t)m01 | ((uint64_t)m23 << 32);
+        int c = __popc(m16);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if ((threadIdx.x & 63) == 0 && c) atomicAdd(NL.cnt + ((u >> 10)), c);   // lane 0: the wave's first unit
       }
     }
 #pragma unroll
@@ -376,22 +433,26 @@ static int num_blocks(int64_t n, int t) { return (int)std::max<int64_t>(1, (n + 
 template <int GM, int S, bool TD>
 static void launch_pf(int g, size_t lds, bool big, hipStream_t st, const uint8_t* text, int64_t nbytes,
                       const PfTables& T, const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
-                      unsigned long long* count) {
-  if (big)
-    hipLaunchKernelGGL((k_prefilter<GM, S, 4, TD>), dim3(g), dim3(pf_threads<TD>()), lds, st, text, nbytes, T,
-                       line_start, nlines, cand, cap, count);
-  else
-    hipLaunchKernelGGL((k_prefilter<GM, S, 1, TD>), dim3(g), dim3(pf_threads<TD>()), lds, st, text, nbytes, T,
-                       line_start, nlines, cand, cap, count);
+                      unsigned long long* count, const NlOut* nl) {
+  const NlOut NL = nl ? *nl : NlOut();
+#define LP_PF_K(U, F)                                                                                          \
+  hipLaunchKernelGGL((k_prefilter<GM, S, U, TD, F>), dim3(g), dim3(pf_threads<TD>()), lds, st, text, nbytes, T, \
+                     line_start, nlines, cand, cap, count, NL)
+  if (big) {
+    if (nl) LP_PF_K(4, true); else LP_PF_K(4, false);
+  } else {
+    if (nl) LP_PF_K(1, true); else LP_PF_K(1, false);
+  }
+#undef LP_PF_K
 }
 
 template <bool TD>
 static void dispatch_pf(int g, bool big, hipStream_t st, const uint8_t* text, int64_t nbytes, const PfTables& T,
                         const int64_t* line_start, int64_t nlines, int64_t* cand, int64_t cap,
-                        unsigned long long* count) {
+                        unsigned long long* count, const NlOut* nl) {
   const int gm = T.gmask & 28;
   const size_t lds = (gm ? (size_t(1) << T.bloom_bits) / 8 : 0) + (TD ? 16 * 4096 : 0) + PF_BUF * 8 + 16;
-#define LP_PF(GMV, SV) launch_pf<GMV, SV, TD>(g, lds, big, st, text, nbytes, T, line_start, nlines, cand, cap, count)
+#define LP_PF(GMV, SV) launch_pf<GMV, SV, TD>(g, lds, big, st, text, nbytes, T, line_start, nlines, cand, cap, count, nl)
   if (gm == 16 && T.stride == 4) { LP_PF(16, 4); return; }
   if (gm == 16 && T.stride == 2) { LP_PF(16, 2); return; }
   switch (gm) {
@@ -408,8 +469,11 @@ static void dispatch_pf(int g, bool big, hipStream_t st, const uint8_t* text, in
 }
 
 void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const int64_t* line_start, int64_t nlines,
-                   int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream) {
-  if (nbytes <= 0 || ((T.gmask & 28) == 0 && !T.teddy_on)) return;   // no literals: nothing to prefilter
+                   int64_t* cand, int64_t cap, unsigned long long* count, int grid, uint64_t stream, const NlOut* nl) {
+  if (nbytes <= 0 || ((T.gmask & 28) == 0 && !T.teddy_on)) {   // no literals: nothing to prefilter
+    if (nl) throw std::runtime_error("prefilter_dev: the fused line-index pass needs a prefilter");
+    return;
+  }
   const int64_t units = (nbytes + 15) / 16;
   // large texts: 4 units per lane per iteration (bytes in flight); small requests: 1, so every
   // launched lane has work (latency)
@@ -417,9 +481,9 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
   const int threads = T.teddy_on ? pf_threads<true>() : pf_threads<false>();
   const int g = (int)std::min<int64_t>(grid, num_blocks(units, threads * (big ? 4 : 1)));
   if (T.teddy_on)
-    dispatch_pf<true>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
+    dispatch_pf<true>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count, nl);
   else
-    dispatch_pf<false>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count);
+    dispatch_pf<false>(g, big, as_stream(stream), text, nbytes, T, line_start, nlines, cand, cap, count, nl);
   LP_CHECK(hipGetLastError());
 }
 

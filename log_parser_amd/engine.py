@@ -530,12 +530,23 @@ class Engine:
                            self._ev_tables(segs), self.ws)[0]
 
     # ------------------------------------------------------------------ core run
-    def prefilter_early(self, text, nbytes: int):
+    def prefilter_early(self, text, nbytes: int, nlp=None):
         """Queue the literal prefilter before the line index reaches the host (bulk path; pass the
-        result to ``prepare(early=...)``). None when the matcher arena path does not apply."""
+        result to ``prepare(early=...)``). None when the matcher arena path does not apply.
+        ``nlp``: the line index's pass-1 outputs -- the prefilter then also writes them (see
+        ``fuses_line_index``)."""
         if not text.is_cuda or self.lib.host_regs or self.profile:
             return None
-        return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid)
+        return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid, nlp)
+
+    def fuses_line_index(self, text) -> bool:
+        """The bulk step folds the line index's first pass into the literal prefilter (one read of the
+        text fewer): device text, the arena path, a library with literals. Opt-in (LP_FUSED_NL=1) until its
+        GPU A/B is in."""
+        import os
+        pf = self.lib.pf
+        return (text.is_cuda and not self.lib.host_regs and not self.profile
+                and bool((pf["gmask"] & 28) or pf["teddy_lits"]) and os.environ.get("LP_FUSED_NL", "0") == "1")
 
     def can_defer(self, text) -> bool:
         """``prepare(defer=True)`` applies: device text, every matcher on the arena path, and the

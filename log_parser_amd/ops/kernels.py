@@ -62,23 +62,30 @@ _LINES_PER_BYTE = [1.0 / 48]
 LINE_BLK_SHIFT = 12
 
 
-def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=None):
+def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=None, fused=None):
     """k_nl_count, rocprim scan, k_nl_lines, k_line_fix (+ k_line_trim): (starts, lens, n_newlines,
     last_newline, kept, blk) with ONE host read; blk = the coarse 4 KiB block -> line index.
     ``before_read()`` runs once, after the launches and before that read: work it queues (the
-    literal prefilter, which needs no line index) runs on the GPU while the host waits."""
+    literal prefilter, which needs no line index) runs on the GPU while the host waits.
+    ``fused(nlp)`` instead launches the literal prefilter FIRST with the line index's first pass
+    folded into its read of the text (nlp = the pass-1 outputs, zeroed): k_nl_count does not run."""
     dev = text.device
     nt = N.line_index_tiles(nbytes)
     cap = int(nbytes * _LINES_PER_BYTE[0] * 1.25) + 1024
     blk = torch.empty((max(nbytes, 1) >> LINE_BLK_SHIFT) + 2, dtype=torch.int32, device=dev)
+    counted = False
     while True:
         cap = min(cap, nbytes + 1)
         starts = torch.empty(cap, dtype=torch.int64, device=dev)
         lens = torch.empty(cap, dtype=torch.int32, device=dev)
         info = torch.empty(3, dtype=torch.int64, device=dev)
         wp, wcap = _LineIndexWs.get(text, nt)
+        if fused is not None:
+            fused(N.line_index_pass1(wp, wcap, nbytes, _s(text)))
+            fused = None
+            counted = True            # a re-run (more lines than the capacity) reuses pass 1's outputs
         N.line_index_dev(text.data_ptr(), nbytes, wp, wcap, starts.data_ptr(), lens.data_ptr(), cap, info.data_ptr(),
-                         trim, blk.data_ptr(), blk.numel(), _s(text))
+                         trim, blk.data_ptr(), blk.numel(), _s(text), counted)
         if before_read is not None:
             # the counts travel to pinned memory behind the line index only; the host then waits
             # for that copy, not for the work before_read() queued after it
@@ -105,7 +112,7 @@ def _with_blk(ls: torch.Tensor, blk: torch.Tensor, nbytes: int) -> torch.Tensor:
     return ls
 
 
-def split_lines(text: torch.Tensor, nbytes: int, before_read=None) -> Tuple[torch.Tensor, torch.Tensor]:
+def split_lines(text: torch.Tensor, nbytes: int, before_read=None, fused=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Java ``logs.split("\\\\r?\\\\n")`` line index (AnalysisService.java:53).
 
     Returns (line_start int64[L], line_len int32[L]); trailing empty lines removed; input
@@ -116,7 +123,7 @@ def split_lines(text: torch.Tensor, nbytes: int, before_read=None) -> Tuple[torc
     if text.is_cuda:
         if nbytes == 0:
             return torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
-        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True, before_read=before_read)
+        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True, before_read=before_read, fused=fused)
         return _with_blk(starts[:L], blk, nbytes), lens[:L]
     nl = newline_positions(text, nbytes)
     if nl.numel() == 0:
@@ -424,13 +431,13 @@ class EarlyPrefilter:
     """The literal prefilter launched before the line index is known on the host (it reads only
     the text): gram hits + the arena counters, handed to ``match_and_hits``."""
 
-    def __init__(self, text, nbytes: int, tabs: dict, arena: "MatchArena", pf_grid: int):
+    def __init__(self, text, nbytes: int, tabs: dict, arena: "MatchArena", pf_grid: int, nlp=None):
         L_est = int(nbytes * _LINES_PER_BYTE[0]) + 1
         self.cap = arena.caps(L_est)["gram"]
         self.gh = torch.empty(self.cap, dtype=torch.int64, device=text.device)
         self.cnt = torch.zeros(7, dtype=torch.int64, device=text.device)
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
-                        pf_grid, _s(text))
+                        pf_grid, _s(text), nlp)
 
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,

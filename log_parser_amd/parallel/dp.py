@@ -187,8 +187,11 @@ class ShardedAnalyzer:
         early = None
         if ls is None:
             box = []
-            ls, ll = K.split_lines(text, nbytes, before_read=(lambda: box.append(eng.prefilter_early(text, nbytes)))
-                                   if text.is_cuda else None)
+            if eng.fuses_line_index(text):      # the prefilter's read of the text also counts the lines
+                ls, ll = K.split_lines(text, nbytes, fused=lambda nlp: box.append(eng.prefilter_early(text, nbytes, nlp)))
+            else:
+                ls, ll = K.split_lines(text, nbytes, before_read=(lambda: box.append(eng.prefilter_early(text, nbytes)))
+                                       if text.is_cuda else None)
             early = box[0] if box else None
         defer = eng.can_defer(text)
         for attempt in range(4):

@@ -114,3 +114,50 @@ def test_deferred_dp_step_overflow_reruns_and_records_once(gpu_device):
     # a second step runs within the learned capacities: no re-run, same window evolution
     out2 = ShardedAnalyzer(e1).step(t, len(data), ls, ll, 0, 0, topk=10)
     assert torch.equal(out2.result.ev_line, ref.ev_line)
+
+
+def _fused_split(eng, t, n):
+    box = []
+    ls, ll = K.split_lines(t, n, fused=lambda nlp: box.append(eng.prefilter_early(t, n, nlp)))
+    return ls, ll, box[0]
+
+
+@pytest.mark.parametrize("size_mb", [1, 40])      # 40 MB: the 4-units-per-lane (bulk) prefilter variant
+def test_fused_line_index_equals_plain(gpu_device, size_mb):
+    """The line index's first pass folded into the literal prefilter (k_prefilter<..., NLF>) gives the
+    same line starts / lengths / block index as k_nl_count, on mixed "\\n" / "\\r\\n" text with
+    separators straddling 16-byte units and 16 KiB tiles, lone '\\r's, trailing empty lines and an
+    unterminated last line; and the prefilter's own output is unchanged."""
+    import random
+    sets, trig = realistic_library(100, seed=51)
+    lib = CompiledLibrary(sets, ScoringParams())
+    eng = _eng(lib, gpu_device)
+    rng = random.Random(size_mb)
+    base = make_log(20_000, trig, seed=52, hit_rate=0.05).split("\n")
+    parts, total = [], 0
+    while total < size_mb << 20:
+        ln = rng.choice(base)
+        if rng.random() < 0.05:
+            ln += "\r"                                     # a lone '\r' before the separator
+        sep = "\r\n" if rng.random() < 0.3 else "\n"
+        if rng.random() < 0.01:
+            ln = ln[: rng.randint(0, 20)]
+        parts.append(ln + sep)
+        total += len(ln) + len(sep)
+    data = "".join(parts)
+    # separators exactly at unit / tile boundaries
+    for edge in (16 * 1024 - 1, 16 * 1024, 2 * 16 * 1024 - 2, 15, 16, 31):
+        if edge + 2 < len(data):
+            data = data[:edge] + "\r\n" + data[edge + 2:]
+    data = data.rstrip("\n") + "tail without newline\n\n\n"
+    raw = data.encode()
+    t = _text(gpu_device, raw)
+    n = len(raw)
+    ls1, ll1 = K.split_lines(t, n)
+    ls2, ll2, early = _fused_split(eng, t, n)
+    assert torch.equal(ls1, ls2) and torch.equal(ll1, ll2)
+    assert torch.equal(ls1._lp_blk[0], ls2._lp_blk[0])
+    plain = K.EarlyPrefilter(t, n, eng.tabs, eng.arena, eng.pf_grid)
+    c1, c2 = int(plain.cnt[0]), int(early.cnt[0])
+    assert c1 == c2 and c1 <= plain.cap
+    assert torch.equal(torch.sort(plain.gh[:c1]).values, torch.sort(early.gh[:c2]).values)

@@ -82,33 +82,41 @@ __device__ __forceinline__ uint32_t li_pack4(uint32_t x) {
 // Pass 1: per 16 KiB tile the '\n' count, and per lane (64 bytes) a 64-bit '\n' bitmask -- the
 // second pass reads these 2 KiB per tile instead of the tile's 16 KiB of text. A tile holding a
 // "\r\n" (a '\r' right before one of its '\n', possibly the previous tile's last byte) is flagged:
-// only those tiles (CRLF logs) are read again as text to strip the '\r'.
+// only those tiles (CRLF logs) are read again as text to strip the '\r'. The flag is conservative
+// (any '\r' in the tile or right before it): k_nl_lines derives the exact '\r\n' positions.
+//
+// Loads are coalesced: a wave's k-th 16-byte load covers 1 KiB of its 4 KiB contiguously (lane l
+// at k*1024 + 16*l), and the 16-bit masks are transposed through LDS into the per-lane 64-byte
+// layout k_nl_lines reads (a lane-strided 64-byte layout touched 64 cache lines per load
+// instruction and re-fetched them from L2 four times).
 __global__ __launch_bounds__(LI_THREADS) void k_nl_count(const uint8_t* __restrict__ text, int64_t nbytes,
                                                          int32_t* __restrict__ cnt, uint64_t* __restrict__ nlm,
                                                          int32_t* __restrict__ crf) {
-  const int64_t base = (int64_t)blockIdx.x * LI_TILE + (int64_t)threadIdx.x * LI_BYTES_PER_THREAD;
-  uint64_t m64 = 0;
+  __shared__ uint16_t s_m[LI_THREADS * 4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t wbase = (int64_t)blockIdx.x * LI_TILE + (int64_t)wid * (64 * LI_BYTES_PER_THREAD);
   int crnl = 0;
-  if (base < nbytes) {
-    const uint4* p = reinterpret_cast<const uint4*>(text + base);
-    uint32_t carry = 0;                           // '\r' in the previous word's last byte
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 v = p[k];
+  for (int k = 0; k < 4; ++k) {
+    const int64_t p = wbase + k * 1024 + 16 * lane;
+    uint32_t m16 = 0;
+    if (p < nbytes) {
+      const uint4 v = *reinterpret_cast<const uint4*>(text + p);
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint32_t nl = li_zero_bytes(w[q] ^ 0x0A0A0A0Au);
-        const uint32_t cr = li_zero_bytes(w[q] ^ 0x0D0D0D0Du);
-        crnl |= (int)(((cr << 8) | carry) & nl);
-        carry = cr >> 24;                         // bit 7 <- '\r' in byte 3
-        m64 |= (uint64_t)li_pack4(nl) << (4 * (4 * k + q));
+        m16 |= li_pack4(li_zero_bytes(w[q] ^ 0x0A0A0A0Au)) << (4 * q);
+        crnl |= (int)li_zero_bytes(w[q] ^ 0x0D0D0D0Du);
       }
+      const int64_t valid = nbytes - p;
+      if (valid < 16) m16 &= (1u << valid) - 1u;
     }
-    const int64_t valid = nbytes - base;
-    if (valid < 64) m64 &= (1ull << valid) - 1ull;
-    if ((m64 & 1ull) && base > 0 && text[base - 1] == '\r') crnl = 1;
+    s_m[wid * 256 + k * 64 + lane] = (uint16_t)m16;
   }
+  if (threadIdx.x == 0 && blockIdx.x > 0 && text[(int64_t)blockIdx.x * LI_TILE - 1] == '\r') crnl = 1;
+  __syncthreads();
+  // lane l's 64 bytes are the 16-byte pieces 4l .. 4l+3 of its wave, stored in that order
+  const uint64_t m64 = *reinterpret_cast<const uint64_t*>(&s_m[wid * 256 + 4 * lane]);
   nlm[(int64_t)blockIdx.x * LI_THREADS + threadIdx.x] = m64;
   int c = __popcll(m64);
 #pragma unroll
@@ -132,26 +140,21 @@ __global__ __launch_bounds__(LI_THREADS) void k_nl_count(const uint8_t* __restri
   }
 }
 
-__global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restrict__ text, int64_t nbytes,
-                                                         const uint64_t* __restrict__ nlm,
-                                                         const int32_t* __restrict__ crf,
-                                                         const int64_t* __restrict__ off,
-                                                         int64_t* __restrict__ starts, int32_t* __restrict__ lens,
-                                                         int64_t cap, int64_t* __restrict__ fix_g,
-                                                         int64_t* __restrict__ fix_end, int32_t* __restrict__ blk,
-                                                         int64_t nblk) {
+// One tile of pass 2. m64 / excl / cf were loaded up front (see k_nl_lines); the caller
+// separates consecutive tiles of a block with a barrier (the LDS stage is reused).
+__device__ __forceinline__ void li_lines_tile(const uint8_t* __restrict__ text, int64_t nbytes, int64_t tile,
+                                              uint64_t m64, int64_t excl, int cf, int* s_wcnt,
+                                              int32_t* s_start, int32_t* s_end, int64_t* __restrict__ starts,
+                                              int32_t* __restrict__ lens, int64_t cap,
+                                              int64_t* __restrict__ fix_g, int64_t* __restrict__ fix_end,
+                                              int32_t* __restrict__ blk, int64_t nblk) {
   constexpr int NW = LI_THREADS / 64;
-  __shared__ int s_wcnt[NW];
-  __shared__ int32_t s_start[LI_STAGE];          // tile-relative: start of the next line (= '\n' + 1)
-  __shared__ int32_t s_end[LI_STAGE];            // tile-relative end of the line ('\n' minus a '\r')
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t tile = blockIdx.x;
   const int64_t tbase = tile * LI_TILE;
   const int64_t base = tbase + (int64_t)threadIdx.x * LI_BYTES_PER_THREAD;
-  // this lane's 64 bytes as bitmasks: '\n' from pass 1; '\r' before a '\n' (bit b: byte b - 1 is
-  // '\r') only in flagged tiles, which are read as text again
-  uint64_t m64 = nlm[tile * LI_THREADS + threadIdx.x], crb = 0;
-  if (crf[tile] && base < nbytes) {
+  // '\r' before a '\n' (bit b: byte b - 1 is '\r') only in flagged tiles, which are read as text again
+  uint64_t crb = 0;
+  if (cf && base < nbytes) {
     uint32_t m[16], cr[16];
     li_masks(text, nbytes, base, m, cr);
     uint64_t c64 = 0;
@@ -173,7 +176,6 @@ __global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restri
     if (w < wid) woff += s_wcnt[w];
     tot += s_wcnt[w];
   }
-  const int64_t excl = off[tile];
   // coarse index for line lookups (lp_core.h locate_line): a wave covers one 4 KiB block, and the
   // line holding its first byte is the number of '\n' before it
   if (blk && lane == 0 && tile * NW + wid < nblk) blk[tile * NW + wid] = (int32_t)(excl + woff);
@@ -221,6 +223,41 @@ __global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restri
   }
   if (tot == 0 && threadIdx.x == 0) fix_g[tile] = -1;
   if (tile == 0 && threadIdx.x == 0 && cap > 0) starts[0] = 0;
+}
+
+// Pass 2 over LI_LINES_TPB consecutive tiles per workgroup: every tile's mask word, offset and
+// CRLF flag are loaded before the first tile is walked, so a workgroup keeps LI_LINES_TPB loads in
+// flight instead of one (one tile per workgroup was latency-bound: ~3 us per 2 KiB of masks).
+constexpr int LI_LINES_TPB = 4;
+__global__ __launch_bounds__(LI_THREADS) void k_nl_lines(const uint8_t* __restrict__ text, int64_t nbytes,
+                                                         int64_t ntiles, const uint64_t* __restrict__ nlm,
+                                                         const int32_t* __restrict__ crf,
+                                                         const int64_t* __restrict__ off,
+                                                         int64_t* __restrict__ starts, int32_t* __restrict__ lens,
+                                                         int64_t cap, int64_t* __restrict__ fix_g,
+                                                         int64_t* __restrict__ fix_end, int32_t* __restrict__ blk,
+                                                         int64_t nblk) {
+  __shared__ int s_wcnt[LI_THREADS / 64];
+  __shared__ int32_t s_start[LI_STAGE];          // tile-relative: start of the next line (= '\n' + 1)
+  __shared__ int32_t s_end[LI_STAGE];            // tile-relative end of the line ('\n' minus a '\r')
+  const int64_t t0 = (int64_t)blockIdx.x * LI_LINES_TPB;
+  uint64_t m[LI_LINES_TPB];
+  int64_t ex[LI_LINES_TPB];
+  int cf[LI_LINES_TPB];
+#pragma unroll
+  for (int j = 0; j < LI_LINES_TPB; ++j) {
+    const bool in = t0 + j < ntiles;
+    m[j] = in ? nlm[(t0 + j) * LI_THREADS + threadIdx.x] : 0ull;
+    ex[j] = in ? off[t0 + j] : 0;
+    cf[j] = in ? crf[t0 + j] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < LI_LINES_TPB; ++j) {
+    if (t0 + j >= ntiles) break;                  // block-uniform
+    if (j) __syncthreads();                       // the previous tile's stage has been stored
+    li_lines_tile(text, nbytes, t0 + j, m[j], ex[j], cf[j], s_wcnt, s_start, s_end, starts, lens, cap, fix_g,
+                  fix_end, blk, nblk);
+  }
 }
 
 // Completes what needs every tile's starts: the first line end of each tile, the final line and
@@ -316,7 +353,8 @@ void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, i
   if (rocprim::exclusive_scan(tmp, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
       hipSuccess)
     throw std::runtime_error("line_index: rocprim scan failed");
-  hipLaunchKernelGGL(k_nl_lines, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, nlm, crf, off, starts, lens, cap,
+  hipLaunchKernelGGL(k_nl_lines, dim3((unsigned)((nt + LI_LINES_TPB - 1) / LI_LINES_TPB)), dim3(LI_THREADS), 0, st,
+                     text, nbytes, (int64_t)nt, nlm, crf, off, starts, lens, cap,
                      fix_g, fix_end, blk, nblk);
   hipLaunchKernelGGL(k_line_fix, dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, st, nt, nbytes, fix_g, fix_end,
                      off, cnt, starts, lens, cap, info, blk, nblk);

@@ -115,8 +115,9 @@ __device__ __forceinline__ uint32_t pf_bloom(const uint32_t* bl, int bits, uint3
 //   NLF: the line index's first pass rides on this read of the text (bulk DP steps): per 16-byte
 //     unit the '\n' bits, four lanes' bits form the 64-bit mask word of 64 bytes (lanes 4q..4q+3
 //     hold consecutive units), a wave's 64 units are 1 KiB of one 16 KiB tile -> one atomic count
-//     per wave and tile; a '\r' right before a '\n' flags the '\n''s tile (CRLF logs). The outputs
-//     equal line_index.hip k_nl_count's, which then does not run.
+//     per wave and tile; a '\r' right before a '\n' flags the '\n''s tile (CRLF logs). Counts and
+//     masks equal line_index.hip k_nl_count's (which then does not run); its CRLF flags are a
+//     superset of these (both are only hints for k_nl_lines' exact '\r' masks).
 template <bool TD>
 constexpr int pf_threads() { return TD ? 1024 : PF_THREADS; }
 

@@ -50,11 +50,16 @@ def _tile_edge_texts():
     yield "".join(f"line {i} with some words in it\n" for i in range(200000))   # ~400 tiles: look-back
     yield "\n" * (5 * T)                                        # only empty lines: none kept
     yield "ab\n" * (4 * T)                                      # above the capacity guess: re-run
+    for n in (5, 6, 7, 9):                                       # tile counts off the 4-tile workgroups
+        yield "".join(f"r{i} \r\n" if i % 7 == 0 else f"row {i}\n" for i in range(n * T // 9)) + "x" * 3
+    yield "a\rb\n" * (T // 2) + "tail"                            # stray '\r's: flagged tiles, no CRLF
+    yield "x" * (T + 7) + "\n" + "y" * 3                          # partial 16-byte piece at the end
 
 
 def test_line_index_tile_edges(gpu_device):
-    """Single-pass line index (k_nl_lines decoupled look-back): tile boundaries, CR across a
-    boundary, all-empty / no-newline texts, many tiles, capacity re-run -- equal to Java split."""
+    """Line index (k_nl_count masks, k_nl_lines over 4-tile workgroups): tile boundaries, CR across
+    a boundary, stray CRs, all-empty / no-newline texts, many tiles, tile counts that are not a
+    multiple of 4, capacity re-run -- equal to Java split."""
     for s in _tile_edge_texts():
         data = s.encode()
         td, _ = _text(gpu_device, data)

@@ -2,9 +2,9 @@
 // lengths straight from the bytes, ONE read of the text (+ its 1/8-size newline bitmask) and ONE
 // host read.
 //
-//   k_nl_count   per 16 KiB tile: number of '\n' + a 1-bit-per-byte '\n' mask + a "\r\n" flag
+//   k_nl_count   per 16 KiB tile: number of '\n' + a 1-bit-per-byte '\n' mask + a '\r' flag
 //   rocprim      exclusive scan of the tile counts (decoupled look-back over ~80k counts)
-//   k_nl_lines   per tile again, from the mask (text only in "\r\n" tiles): every '\n' at p with global index g writes starts[g+1] = p + 1
+//   k_nl_lines   4 tiles per workgroup, from the mask (text only in '\r'-flagged tiles): every '\n' at p with global index g writes starts[g+1] = p + 1
 //                and, when the previous '\n' is in the same tile, lens[g] = (p minus a '\r' right
 //                before it) - start; staged in LDS, stored coalesced. The tile's FIRST line end is
 //                recorded (fix_g, fix_end) for

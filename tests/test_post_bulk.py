@@ -89,6 +89,28 @@ def test_bulk_path_hot_buckets_equal_host_twins(gpu_device):
     _assert_same(d, c)
 
 
+def test_bulk_context_features_dense_windows_equal_host_twins(gpu_device):
+    """Dense context windows over 300k lines: every k_feat_cov workgroup holds more covered lines
+    than lanes (512 lines per workgroup at this size). Lines of different lengths, feature words,
+    stack frames and final terminators (U+0085, U+2028, a lone '\\r')."""
+    pats = [{"id": "hb", "name": "heartbeat", "severity": "LOW",
+             "primary_pattern": {"regex": "heartbeat", "confidence": 0.5},
+             "context_extraction": {"lines_before": 3, "lines_after": 2}}]
+    lib = CompiledLibrary([PatternSet.model_validate({"metadata": {"library_id": "ctx", "version": "1"},
+                                                      "patterns": pats})], ScoringParams())
+    tails = ["", " ERROR disk", " warn: slow", " java.lang.IllegalStateException: x", " Error", "\u0085",
+             "\u2028", "\r", " FATAL" + " pad" * 40, " ok" * 3]
+    lines = []
+    for i in range(300_000):
+        if i % 11 == 5:
+            lines.append(f"\tat com.x.Y{i % 13}.run(Y.java:{i % 97})")
+        else:
+            lines.append(f"{i % 60:02d} node-{i % 7} heartbeat{tails[(i * 7) % len(tails)]}" + "x" * (i % 23))
+    d, c = _run_both(lib, "\n".join(lines).encode(), gpu_device)
+    assert d["line"].numel() > 250_000
+    _assert_same(d, c)
+
+
 def test_deferred_dp_step_overflow_reruns_and_records_once(gpu_device):
     """A DP step reads no counts until its end (device-count events, overflow flag in the payload).
     With every capacity far too small the first attempt overflows: its frequency record is vetoed

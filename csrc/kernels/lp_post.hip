@@ -154,6 +154,76 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t* __restrict__ fs, c
   if (j < ne) rank_one(fs, idx, ne, j, nkeys, ev_rank, ev_fkey, freq_counts);
 }
 
+// Context walk on row-offset tables (k_feat_cov's LDS path). DFA k's states are rows of W_k =
+// nc_k + 2 uint16 entries: column 0 = hold (the row's own offset), columns 1..nc_k = the BYTE offset
+// (from the table base) of the next state's row, column nc_k + 1 = the state's accept flags. The
+// dead and match states (0, 1) hold on every column. One packed word per byte, bm4[c], holds
+// 2 * column of byte c for the 4 DFAs in its 4 bytes; a byte outside the walked range uses 0
+// (hold). A step is one byte extract + one 3-way add + one ds_read_u16 per DFA: about half the
+// VALU work of the state-id walk (mad, address, terminal-state select), which is what bound
+// k_feat_cov (profiles/r3_al: 22 us without walks, 110 us with).
+struct CtxRows {
+  int w2[4];      // 2 * W_k (row bytes)
+  int live[4];    // byte offset of state 2's row: offsets >= live[k] are live states
+  int one[4];     // byte offset of state 1's row (match found)
+};
+
+__device__ __forceinline__ uint32_t ctx_row_ld(const uint8_t* rows, uint32_t off) {
+  return *reinterpret_cast<const uint16_t*>(rows + off);
+}
+
+__device__ __forceinline__ void ctx_rows_advance(const uint8_t* rows, const uint32_t* bm4, const CtxRows& R,
+                                                 const uint8_t* s, int e, uint32_t (&off)[4]) {
+  if (e <= 0) return;
+  const int sh = (int)((uintptr_t)s & 15);
+  const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
+  uint4 cur = blk[0];
+  for (int t0 = -sh; t0 < e; t0 += 16) {
+    const uint4 nxt = blk[1];
+    ++blk;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int t = t0 + j;
+      const uint32_t w = (j < 4) ? cur.x : (j < 8) ? cur.y : (j < 12) ? cur.z : cur.w;
+      const uint32_t c = (w >> (8 * (j & 3))) & 0xFFu;
+      const uint32_t b = ((t >= 0) & (t < e)) ? bm4[c] : 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) off[k] = ctx_row_ld(rows, off[k] + ((b >> (8 * k)) & 0xFFu));
+    }
+    cur = nxt;
+    bool alive = false;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) alive |= off[k] >= (uint32_t)R.live[k];
+    if (!alive) return;
+  }
+}
+
+// Matcher.find semantics of dfa_find_k / context_feat on the row-offset tables
+__device__ __forceinline__ uint8_t ctx_rows_feat(const uint8_t* rows, const uint32_t* bm4, const CtxRows& R,
+                                                 const uint8_t* s, int n) {
+  uint32_t off[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) off[k] = (uint32_t)R.live[k];       // state 2 = start
+  const int ftl = final_term_len(s, n);
+  const int ft = ftl ? n - ftl : n;
+  ctx_rows_advance(rows, bm4, R, s, ft, off);
+  if (ftl) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (off[k] >= (uint32_t)R.live[k] && (ctx_row_ld(rows, off[k] + R.w2[k] - 2) & 2)) off[k] = (uint32_t)R.one[k];
+    ctx_rows_advance(rows, bm4, R, s + ft, ftl, off);
+  }
+  uint32_t res = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool acc = off[k] == (uint32_t)R.one[k] ||
+                     (off[k] >= (uint32_t)R.live[k] && (ctx_row_ld(rows, off[k] + R.w2[k] - 2) & 1));
+    res |= (acc ? 1u : 0u) << k;
+  }
+  const uint8_t f = (res & 1u) ? 1 : ((res & 2u) ? 2 : 0);
+  return (uint8_t)(f | (res & 12u));
+}
+
 // Context features of covered lines. A block owns `per_block` consecutive lines: it compacts the
 // covered ones into an LDS list (uncovered lines get 0) and then runs the 4 DFAs with every lane
 // busy -- covered lines come in short runs, so one lane per line would idle most of each wave.
@@ -162,19 +232,66 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t* __restrict__ fs, c
 constexpr int FC_MAX_LINES = 4096;
 constexpr int FC_TRANS = 4096;   // uint16 entries (context DFAs need ~900)
 constexpr int FC_ACC = 1024;
+constexpr int FC_ROWS = FC_TRANS; // uint16 row-offset entries (context DFAs need ~1,100)
 __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ cov, int64_t L, int per_block,
                                                   const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
                                                   const int32_t* __restrict__ ll, DfaPool P, int ctx_trans,
                                                   int ctx_acc, uint8_t* __restrict__ feat) {
-  __shared__ int32_t list[FC_MAX_LINES];
+  __shared__ uint16_t list[FC_MAX_LINES];         // block-relative line numbers (< FC_MAX_LINES)
   __shared__ int n;
   __shared__ int32_t s_meta[16];
   __shared__ __attribute__((aligned(16))) uint8_t s_bm[4 * 256];
-  __shared__ uint16_t s_trans[FC_TRANS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_trans[FC_TRANS];
   __shared__ uint8_t s_acc[FC_ACC];
+  // the row-offset path keeps its tables in the state-id path's arrays (one of the two is used)
+  uint16_t* s_rows = s_trans;
+  uint32_t* s_bm4 = reinterpret_cast<uint32_t*>(s_bm);
+  // row-offset tables (ctx_rows_feat) when they fit: rows of nc_k + 2 entries, columns in a byte
+  int nst[4], W[4], rbase[4];
+  int rows_total = 0;
+  bool fit = true;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int nc = P.meta[4 * k + 1];
+    const int t0 = P.meta[4 * k], t1 = k < 3 ? P.meta[4 * k + 4] : ctx_trans;
+    nst[k] = nc > 0 ? (t1 - t0) / nc : 0;
+    W[k] = nc + 2;
+    rbase[k] = rows_total;
+    rows_total += nst[k] * W[k];
+    fit = fit && nc > 0 && 2 * (nc + 1) <= 255 && nst[k] >= 3 && t0 >= 0 && t1 <= ctx_trans;
+  }
   const bool lds = ctx_trans <= FC_TRANS && ctx_acc <= FC_ACC;
+  const bool rows_ok = fit && rows_total <= FC_ROWS && 2 * rows_total < 65536;
+  CtxRows R;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    R.w2[k] = 2 * W[k];
+    R.live[k] = 2 * (rbase[k] + 2 * W[k]);
+    R.one[k] = 2 * (rbase[k] + W[k]);
+  }
   if (threadIdx.x == 0) n = 0;
-  if (lds) {
+  if (rows_ok) {
+    for (int i = threadIdx.x; i < rows_total; i += blockDim.x) {
+      int k = 0;
+#pragma unroll
+      for (int q = 1; q < 4; ++q) k += i >= rbase[q] ? 1 : 0;
+      const int loc = i - rbase[k], st = loc / W[k], col = loc - st * W[k];
+      const int self = 2 * (rbase[k] + st * W[k]);
+      int v;
+      if (col == 0) v = self;
+      else if (col == W[k] - 1) v = P.acc[P.meta[4 * k + 2] + st];
+      else if (st < 2) v = self;
+      else v = 2 * (rbase[k] + (int)P.trans[P.meta[4 * k] + st * (W[k] - 2) + col - 1] * W[k]);
+      s_rows[i] = (uint16_t)v;
+    }
+    {
+      const int c = threadIdx.x;                  // blockDim.x == 256
+      uint32_t b = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) b |= (uint32_t)(2 * (P.bytemap[256 * k + c] + 1)) << (8 * k);
+      s_bm4[c] = b;
+    }
+  } else if (lds) {
     if (threadIdx.x < 16) s_meta[threadIdx.x] = P.meta[threadIdx.x];
     lds_fill<uint8_t, 4>(s_bm, P.bytemap, 4 * 256);
     lds_fill<uint16_t, 4>(s_trans, P.trans, ctx_trans);
@@ -185,7 +302,7 @@ __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ co
   for (int k = threadIdx.x; k < per_block; k += blockDim.x) {
     const int64_t x = base + k;
     if (x < L) {
-      if (cov[x] > 0) list[atomicAdd(&n, 1)] = k;
+      if (cov[x] > 0) list[atomicAdd(&n, 1)] = (uint16_t)k;
       else feat[x] = 0;
     }
   }
@@ -193,7 +310,13 @@ __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ co
   const int m = n;
   // two call sites, each with a provable address space: the LDS copy compiles to ds_read (a
   // runtime select between LDS and global pointers degrades every table read to a flat load)
-  if (lds) {
+  if (rows_ok) {
+    const uint8_t* rows = reinterpret_cast<const uint8_t*>(s_rows);
+    for (int j = threadIdx.x; j < m; j += blockDim.x) {
+      const int64_t x = base + list[j];
+      feat[x] = ctx_rows_feat(rows, s_bm4, R, text + ls[x], ll[x]);
+    }
+  } else if (lds) {
     const DfaPool Q{s_meta, s_bm, s_trans, s_acc};
     for (int j = threadIdx.x; j < m; j += blockDim.x) {
       const int64_t x = base + list[j];

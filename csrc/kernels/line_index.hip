@@ -92,7 +92,7 @@ __device__ __forceinline__ uint32_t li_pack4(uint32_t x) {
 __global__ __launch_bounds__(LI_THREADS) void k_nl_count(const uint8_t* __restrict__ text, int64_t nbytes,
                                                          int32_t* __restrict__ cnt, uint64_t* __restrict__ nlm,
                                                          int32_t* __restrict__ crf) {
-  __shared__ uint16_t s_m[LI_THREADS * 4];
+  __shared__ __attribute__((aligned(16))) uint16_t s_m[LI_THREADS * 4];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wbase = (int64_t)blockIdx.x * LI_TILE + (int64_t)wid * (64 * LI_BYTES_PER_THREAD);
   int crnl = 0;

@@ -85,8 +85,11 @@ class LogParser:
         return self._batcher.submit(logs)
 
     def stream_threshold(self) -> int:
-        from .parallel.stream import auto_chunk_bytes
-        return int(self.config["engine.chunk-bytes"]) or auto_chunk_bytes(self.engine.device)
+        """File size above which ``parse_file`` streams (StreamResult summary) instead of analysing
+        one whole document (full AnalysisResult): ``engine.stream.threshold-bytes``, independent of
+        the HBM-sized stream chunk, so the output format and host memory of a file do not depend
+        on the GPU it runs on."""
+        return int(self.config["engine.stream.threshold-bytes"])
 
     def parse_stream(self, data, chunk_bytes: Optional[int] = None, topk: int = 100, keep_events: bool = False):
         from .parallel.stream import StreamAnalyzer

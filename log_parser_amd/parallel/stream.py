@@ -252,7 +252,10 @@ class StreamAnalyzer:
         """[min, max] of the chronological factor over any position (ScoringService.java:123-151:
         piecewise linear through m at 0, 1.5 at e, 1.0 at t, -> 0.5 at the end)."""
         p = self.engine.params
-        return 0.5, max(float(p.max_early_bonus), 1.5, 1.0)
+        m, e, t = float(p.max_early_bonus), float(p.early_bonus_threshold), float(p.penalty_threshold)
+        # segment endpoints: m (pos 0), 1.5 (pos e), 1.0 (pos t), 1.5 - max(e, t) (late segment
+        # start), -> 0.5 (pos 1); m may be configured below 0.5 or above 1.5
+        return min(0.5, m), max(m, 1.5, 1.5 - min(e, t, 0.0))
 
     def _prune(self, ev_gl, ev_pat, ev_fac, cmin: float, cmax: float):
         """Keep only events that can still be in the final top-k. The final score is the

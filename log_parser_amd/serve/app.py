@@ -285,13 +285,12 @@ class Service:
                     devs = devs[1:]
                 elif eng.device in devs:
                     devs.remove(eng.device)
+                if getattr(eng.freq, "device_resident", False) and not self._device_window_ok(eng, devs):
+                    # engines on other physical GPUs without a verified peer window: ONE host
+                    # window shared by every engine (the pre-peer behaviour), seeded from the device
+                    log.warning("serving on several GPUs with a shared host frequency window")
+                    eng.freq = eng.freq.to_host_state()
                 for dev in devs:                   # data-parallel serving: one engine per GPU (or stream)
-                    if getattr(eng.freq, "device_resident", False) and dev.type == "cuda":
-                        # ONE window in HBM of the first engine's GPU: the others' kernels read and
-                        # record it over xGMI peer access, in arrival order (SharedWindowTurn)
-                        if not N.enable_peer_access(dev.index if dev.index is not None else 0,
-                                                    eng.freq.device.index or 0):
-                            raise RuntimeError(f"no peer access from {dev} to {eng.freq.device} for the shared window")
                     engines.append(Engine(engines[0].lib, cfg, device=dev, freq=engines[0].freq))
                 if len(engines) > 1:
                     log.info("serving on %d engines: %s", len(engines), [str(e.device) for e in engines])
@@ -299,6 +298,24 @@ class Service:
                                         int(cfg["engine.batch.max-bytes"]), float(cfg["engine.batch.max-wait-ms"]),
                                         self.metrics)
             return self._batcher
+
+    def _device_window_ok(self, eng: Engine, devs: List[torch.device]) -> bool:
+        """Whether the engines on ``devs`` can share the first engine's HBM window. Streams of the
+        same GPU always can; other GPUs only with ``engine.serve.peer-window`` (the cross-GPU peer
+        path is opt-in until a multi-GPU run has pinned it) and working peer access."""
+        home = eng.freq.device.index or 0
+        for dev in devs:
+            if dev.type != "cuda":
+                return False
+            idx = dev.index if dev.index is not None else 0
+            if idx == home:
+                continue
+            if not bool(self.config.get("engine.serve.peer-window", False)):
+                return False
+            if not N.enable_peer_access(idx, home):
+                log.warning("no peer access from %s to %s for the shared window", dev, eng.freq.device)
+                return False
+        return True
 
     def close(self):
         if self._batcher is not None:

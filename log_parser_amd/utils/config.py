@@ -40,9 +40,15 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.device": ("auto", str),
     # data-parallel serving: "" = engine.device only, "all" = every visible GPU, or "cuda:0,cuda:1"
     "engine.serve-devices": ("", str),
+    # engines on OTHER GPUs share the first engine's HBM frequency window over xGMI peer access
+    # (off: they share one host window; streams of the same GPU always share the device window)
+    "engine.serve.peer-window": (False, bool),
     # bytes per streamed H2D chunk for long logs (double-buffered pinned staging); 0 = sized from
     # the GPU's free HBM (parallel/stream.py auto_chunk_bytes: 1/16 of it, 256 MiB .. 8 GiB)
     "engine.chunk-bytes": (0, int),
+    # LogParser.parse_file / CLI: files above this many bytes are streamed (StreamResult summary +
+    # top-k); smaller files are analysed as one document (full AnalysisResult)
+    "engine.stream.threshold-bytes": (256 << 20, int),
     # capacity hint for candidate (line, regex) pairs per chunk; grown on overflow
     "engine.candidate-capacity": (1 << 22, int),
     # max DFA states per regex before it is routed to the NFA engine

@@ -124,3 +124,36 @@ def test_auto_chunk_bytes_policy(monkeypatch):
     assert S.auto_chunk_bytes(dev, 1 << 40) == S.CHUNK_MAX
     monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d: (1 << 30, 288 << 30))
     assert S.auto_chunk_bytes(dev, 100 << 30) == S.CHUNK_MIN
+
+
+def test_parse_file_threshold_is_fixed(tmp_path):
+    """parse_file streams above engine.stream.threshold-bytes (a fixed size, not the HBM-derived
+    chunk), and analyses one whole document below it."""
+    from log_parser_amd.api import LogParser
+    from log_parser_amd.parallel.stream import StreamResult
+    sets, trig = make_library(8, seed=5)
+    logs = make_log(300, trig, seed=6, hit_rate=0.1)
+    p = tmp_path / "a.log"
+    p.write_text(logs)
+    size = p.stat().st_size
+    big = LogParser(sets, Config.load(overrides={"engine.device": "cpu", "engine.stream.threshold-bytes": size - 1}))
+    assert big.stream_threshold() == size - 1
+    assert isinstance(big.parse_file(str(p)), StreamResult)
+    small = LogParser(sets, Config.load(overrides={"engine.device": "cpu", "engine.stream.threshold-bytes": size}))
+    res = small.parse_file(str(p))
+    assert isinstance(res, dict) and res["metadata"]["totalLines"] == 300
+    assert LogParser(sets, Config.load(overrides={"engine.device": "cpu"})).stream_threshold() == 256 << 20
+
+
+@pytest.mark.parametrize("m", [0.3, 1.2, 2.5, 4.0])
+def test_chrono_bounds_cover_factor(m):
+    """_chrono_bounds brackets chrono_factor for any configured max-early-bonus."""
+    from log_parser_amd.golden import chronological_factor
+    sets, _ = make_library(3, seed=1)
+    params = ScoringParams(max_early_bonus=m)
+    eng = Engine(CompiledLibrary(sets, params), Config.load(overrides={"engine.device": "cpu"}),
+                 device=torch.device("cpu"))
+    lo, hi = StreamAnalyzer(eng, chunk_bytes=4096)._chrono_bounds()
+    n = 997
+    vals = [chronological_factor(i, n, params) for i in range(n)]
+    assert lo <= min(vals) and max(vals) <= hi

@@ -169,7 +169,120 @@ struct BtSet {
   }
 };
 
+// Java String.split("\\r?\\n") line index of ONE document (trim: drop trailing empty lines, as
+// split(regex) does; the device line index of a batch / shard uses the same rule)
+static void host_line_index(const uint8_t* t, int64_t n, bool trim, std::vector<int64_t>& ls, std::vector<int32_t>& ll) {
+  const int T = std::max(1, std::min<int>(host_threads(), (int)(n >> 22) + 1));
+  std::vector<std::vector<int64_t>> nl(T);
+  host_parallel(n, int64_t(1) << 22, [&](int th, int64_t a, int64_t e) {
+    for (const uint8_t* p = t + a; p < t + e;) {
+      const void* q = std::memchr(p, '\n', (size_t)(t + e - p));
+      if (!q) break;
+      nl[th].push_back(static_cast<const uint8_t*>(q) - t);
+      p = static_cast<const uint8_t*>(q) + 1;
+    }
+  });
+  std::vector<int64_t> pos;
+  for (auto& v : nl) pos.insert(pos.end(), v.begin(), v.end());
+  std::sort(pos.begin(), pos.end());
+  ls.clear();
+  ll.clear();
+  int64_t st = 0;
+  for (int64_t q : pos) {
+    const int64_t e = (q > st && t[q - 1] == '\r') ? q - 1 : q;
+    ls.push_back(st);
+    ll.push_back((int32_t)(e - st));
+    st = q + 1;
+  }
+  if (st < n || pos.empty()) { ls.push_back(st); ll.push_back((int32_t)(n - st)); }
+  if (trim)
+    while (ls.size() > (pos.empty() ? 1u : 0u) && ll.back() == 0) { ls.pop_back(); ll.pop_back(); }
+}
+
+// Host side path of the backtracker regexes (non-regular: backreferences, lookaround, atomic
+// groups, possessive quantifiers), run BEFORE the device pipeline so their hits join it as
+// pre-verified keys (append_keys_dev) and no host round trip sits in the middle of a batch:
+// lines holding one of a regex's required literals (ASCII case-insensitive, as the device
+// prefilter) -- or every line for a literal-free one -- are checked with BtRegex, in parallel.
+static py::array_t<int64_t> bt_prepass(BtSet& b, uint64_t text, int64_t nbytes, uint64_t lsp, uint64_t llp, int64_t nlines,
+                                       bool trim, const std::vector<int>& locals, const std::vector<int64_t>& globals,
+                                       const std::vector<std::vector<std::string>>& lits) {
+  const uint8_t* t = P<const uint8_t>(text);
+  std::vector<int64_t> ls_own;
+  std::vector<int32_t> ll_own;
+  const int64_t* ls = P<const int64_t>(lsp);
+  const int32_t* ll = P<const int32_t>(llp);
+  std::vector<int64_t> keys;
+  {
+    py::gil_scoped_release nogil;
+    if (!ls) {
+      host_line_index(t, nbytes, trim, ls_own, ll_own);
+      ls = ls_own.data();
+      ll = ll_own.data();
+      nlines = (int64_t)ls_own.size();
+    }
+    uint8_t low[256];
+    for (int c = 0; c < 256; ++c) low[c] = (uint8_t)((c >= 'A' && c <= 'Z') ? c + 32 : c);
+    // candidate (regex slot, line) pairs
+    std::vector<std::vector<std::pair<int, int64_t>>> part(std::max(1, host_threads()));
+    std::vector<int> scan_all;
+    for (size_t k = 0; k < locals.size(); ++k) {
+      if (lits[k].empty()) { scan_all.push_back((int)k); continue; }
+      for (const std::string& lit : lits[k]) {
+        const int64_t m = (int64_t)lit.size();
+        if (m == 0 || m > nbytes) continue;
+        const uint8_t* L = reinterpret_cast<const uint8_t*>(lit.data());
+        host_parallel(nbytes - m + 1, int64_t(1) << 20, [&](int th, int64_t a, int64_t e) {
+          for (int64_t i = a; i < e; ++i) {
+            if (low[t[i]] != L[0]) continue;
+            int64_t j = 1;
+            while (j < m && low[t[i + j]] == L[j]) ++j;
+            if (j < m) continue;
+            const int64_t x = std::upper_bound(ls, ls + nlines, i) - ls - 1;
+            if (x >= 0 && i + m <= ls[x] + ll[x]) part[th].push_back({(int)k, x});
+          }
+        });
+      }
+    }
+    std::vector<std::pair<int, int64_t>> cand;
+    for (auto& v : part) cand.insert(cand.end(), v.begin(), v.end());
+    std::sort(cand.begin(), cand.end());
+    cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+    std::vector<uint8_t> ok(cand.size(), 0);
+    host_parallel((int64_t)cand.size(), 64, [&](int, int64_t a, int64_t e) {
+      for (int64_t i = a; i < e; ++i) {
+        const int64_t x = cand[i].second;
+        ok[i] = b.find(locals[cand[i].first], t + ls[x], ll[x]) ? 1 : 0;
+      }
+    });
+    for (size_t i = 0; i < cand.size(); ++i)
+      if (ok[i]) keys.push_back((globals[cand[i].first] << 32) | cand[i].second);
+    if (!scan_all.empty()) {
+      std::vector<std::vector<int64_t>> sk(std::max(1, host_threads()));
+      host_parallel(nlines, 256, [&](int th, int64_t a, int64_t e) {
+        for (int64_t x = a; x < e; ++x)
+          for (int k : scan_all)
+            if (b.find(locals[k], t + ls[x], ll[x])) sk[th].push_back((globals[k] << 32) | x);
+      });
+      for (auto& v : sk) keys.insert(keys.end(), v.begin(), v.end());
+    }
+  }
+  py::array_t<int64_t> r((py::ssize_t)keys.size());
+  if (!keys.empty()) std::memcpy(r.mutable_data(), keys.data(), keys.size() * 8);
+  return r;
+}
+
 static py::bytes vbytes(const void* p, size_t n) { return py::bytes(static_cast<const char*>(p), n); }
+
+// byte-level NFA conditions for the MFMA group builder (models/nfa.py, nfa_mfma.hip), which use
+// the 15 byte-level contexts prev * 5 + next (prev < 3, next < 5) of the jregex 24-context masks
+static uint32_t legacy_cond(uint32_t c) {
+  uint32_t o = 0;
+  for (int p = 0; p < 3; ++p)
+    for (int n = 0; n < 5; ++n)
+      if ((c >> ctx_index(p, n)) & 1u) o |= 1u << (p * 5 + n);
+  return o;
+}
 
 static py::dict compile_regex(const std::string& pat, int max_states, int max_positions) {
   Compiled c = compile(pat, max_states, max_positions);
@@ -181,6 +294,9 @@ static py::dict compile_regex(const std::string& pat, int max_states, int max_po
   d["literals"] = lits;
   d["has_literals"] = c.has_literals;
   d["bt_ok"] = c.bt_ok;
+  d["cp_only"] = c.cp_only;
+  d["uword"] = c.uword;
+  d["bpg"] = vbytes(c.bpg.data(), c.bpg.size() * 8);
   if (c.kind == Kind::DFA) {
     d["nstates"] = c.dfa.nstates;
     d["nclasses"] = c.dfa.nclasses;
@@ -189,23 +305,23 @@ static py::dict compile_regex(const std::string& pat, int max_states, int max_po
     d["acc"] = vbytes(c.dfa.accflags.data(), c.dfa.accflags.size());
     d["anchored"] = c.dfa.anchored;
   }
-  if (c.kind == Kind::DFA || c.kind == Kind::NFA) {
-    d["npos"] = c.nfa.npos;
+  d["npos"] = c.byte_nfa ? c.nfa.npos : 0;   // byte-level NFA (0 also: none -- code-point contexts, too large)
+  if ((c.kind == Kind::DFA || c.kind == Kind::NFA) && c.byte_nfa) {
     std::string cls;
     for (auto& b : c.nfa.cls) cls.append(reinterpret_cast<const char*>(b.w), 32);
     d["nfa_cls"] = py::bytes(cls);
     py::list first, last, follow;
-    for (auto& e : c.nfa.first) first.append(py::make_tuple(e.to, e.cond));
-    for (auto& e : c.nfa.last) last.append(py::make_tuple(e.to, e.cond));
+    for (auto& e : c.nfa.first) first.append(py::make_tuple(e.to, legacy_cond(e.cond)));
+    for (auto& e : c.nfa.last) last.append(py::make_tuple(e.to, legacy_cond(e.cond)));
     for (auto& v : c.nfa.follow) {
       py::list l;
-      for (auto& e : v) l.append(py::make_tuple(e.to, e.cond));
+      for (auto& e : v) l.append(py::make_tuple(e.to, legacy_cond(e.cond)));
       follow.append(l);
     }
     d["nfa_first"] = first;
     d["nfa_last"] = last;
     d["nfa_follow"] = follow;
-    d["nfa_nullable"] = c.nfa.nullable;
+    d["nfa_nullable"] = legacy_cond(c.nfa.nullable);
   }
   return d;
 }
@@ -448,6 +564,8 @@ PYBIND11_MODULE(_lpnative, m) {
           if (ok[i]) o[c++] = K[i];
         return c;
       })
+      .def("prepass", &bt_prepass, py::arg("text"), py::arg("nbytes"), py::arg("ls"), py::arg("ll"),
+           py::arg("nlines"), py::arg("trim"), py::arg("locals"), py::arg("globals"), py::arg("literals"))
       // every line x every listed regex (fallback regexes without a usable literal)
       .def("scan", [](BtSet& b, uint64_t text, uint64_t ls, uint64_t ll, int64_t nlines, std::vector<int> locals,
                       std::vector<int64_t> globals) -> py::array_t<int64_t> {
@@ -472,6 +590,18 @@ PYBIND11_MODULE(_lpnative, m) {
       });
   m.def("compile_regex", &compile_regex, py::arg("pattern"), py::arg("max_states") = 2048, py::arg("max_positions") = 4096);
   m.def("dfa_find", &dfa_find_py, py::arg("pattern"), py::arg("line"), py::arg("max_states") = 4096);
+  // host twin of the BPG walk (bpg.h bpg_find_w) over one line, for tests
+  m.def("bpg_find", [](py::bytes prog, const std::string& line) {
+    const std::string p = prog;
+    std::vector<uint64_t> w(p.size() / 8);
+    std::memcpy(w.data(), p.data(), w.size() * 8);
+    return bpg_find_host(w.data(), reinterpret_cast<const uint8_t*>(line.data()), (int)line.size());
+  });
+  m.def("unicode_set", [](const std::string& key) {
+    py::list out;
+    for (auto& r : unicode_set(key).r) out.append(py::make_tuple(r.first, r.second));
+    return out;
+  });
   m.def("split_docs", &split_docs);
   m.def("set_host_threads", &set_host_threads);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
@@ -517,6 +647,8 @@ PYBIND11_MODULE(_lpnative, m) {
                   P<const unsigned long long>(dn), max_grid); }, py::arg("gh"), py::arg("n"), py::arg("text"),
         py::arg("nb"), py::arg("pf"), py::arg("ls"), py::arg("nl"), py::arg("blk"), py::arg("cand"), py::arg("cap"),
         py::arg("count"), py::arg("s"), py::arg("dn") = 0, py::arg("max_grid") = 8192);
+  m.def("append_keys", [](uint64_t dst, int64_t cap, uint64_t count, uint64_t src, int64_t n, uint64_t s) {
+    append_keys_dev(P<int64_t>(dst), cap, P<unsigned long long>(count), P<const int64_t>(src), n, s); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
                        uint64_t out, int64_t cap, uint64_t count, uint64_t s) {
     scan_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs), nregs,
@@ -670,14 +802,16 @@ PYBIND11_MODULE(_lpnative, m) {
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
-                     double evict_before, double now, uint64_t stream, int64_t host_cap, WindowTurn* turn, int64_t seq) {
+                     double evict_before, double now, uint64_t stream, int64_t host_cap, WindowTurn* turn, int64_t seq,
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> inj) {
         const FreqRing R = ring_from(ring);
         const int D = (int)lo.shape(0);
         int64_t ne;
         {
           py::gil_scoped_release nogil;
           ne = r.run(P<uint8_t>(text), nbytes, P<const int64_t>(starts), P<const int32_t>(lens), L, lo.data(), hi.data(),
-                     g0.data(), n.data(), D, R, evict_before, now, stream, host_cap, turn, seq);
+                     g0.data(), n.data(), D, R, evict_before, now, stream, host_cap, turn, seq,
+                     inj.size() ? inj.data() : nullptr, (int64_t)inj.size());
         }
         py::array_t<uint8_t> out((py::ssize_t)r.result_bytes());
         std::memcpy(out.mutable_data(), r.result(), r.result_bytes());
@@ -688,7 +822,8 @@ PYBIND11_MODULE(_lpnative, m) {
         return py::make_tuple(ne, out, d, r.stride());
       }, py::arg("text"), py::arg("nbytes"), py::arg("starts"), py::arg("lens"), py::arg("L"), py::arg("lo"),
          py::arg("hi"), py::arg("g0"), py::arg("n"), py::arg("ring"), py::arg("evict_before"), py::arg("now"),
-         py::arg("stream"), py::arg("host_cap") = 0, py::arg("turn") = nullptr, py::arg("seq") = 0)
+         py::arg("stream"), py::arg("host_cap") = 0, py::arg("turn") = nullptr, py::arg("seq") = 0,
+         py::arg("inj") = py::array_t<int64_t>(0))
       .def_property_readonly("recorded", &RequestRunner::recorded)
       .def("upload_bytes", &RequestRunner::upload_bytes);
 

@@ -1,48 +1,123 @@
-// Bit-parallel Glushkov ("BPG") find() for regexes whose DFA exceeds engine.dfa-max-states.
+// Bit-parallel Glushkov ("BPG") find() for regexes whose DFA exceeds engine.dfa-max-states or that
+// need code-point boundary contexts (MULTILINE ^ $, Unicode \b).
 //
-// The program (built at library load by log_parser_amd/models/bpg.py, which documents the layout)
-// decomposes the Glushkov follow relation into word-parallel parts: shift edges p -> p+1, self
-// loops, "spread fields" (a bounded gap X.{0,n}Y is one field: every active source reaches every
-// target above it, computed for all fields with ONE multi-word subtraction whose guard bits stop
-// each borrow inside its field) and a short exception list (loop-backs, boundary-gated edges).
-// Per byte and 64 positions that is ~20 VALU ops with no table walk on the dependency chain except
-// the byte's class mask -- against M-squared multiply-accumulates for the same step as a
+// The program (built at library load by jregex.cpp bpg_program from the CODE-POINT Glushkov NFA)
+// decomposes the follow relation into word-parallel parts: shift edges p -> p+1, self loops,
+// "spread fields" (a bounded gap X.{0,n}Y is one field: every active source reaches every target
+// above it, computed for all fields with ONE multi-word subtraction whose guard bits stop each
+// borrow inside its field) and a short exception list (loop-backs, boundary-gated edges). Per code
+// point and 64 positions that is ~20 VALU ops with no table walk on the dependency chain except
+// the character's class mask -- against M-squared multiply-accumulates for the same step as a
 // state-transition GEMM (nfa_mfma.hip; profiles/r3_* hold the A/B).
 //
-// Matcher.find() semantics as the DFA walk (jregex.h): boundary context ctx = prev kind x next
-// kind is checked before every byte (accept) and gates edges; extra accept check before a final
-// line terminator; end of line is next kind N_EOS.
+// The walk steps once per CODE POINT: a UTF-8 lead byte is decoded (with its continuation bytes)
+// and mapped to its class through a sorted range table, continuation bytes are skipped, ASCII goes
+// through a 128-entry map. So '.', [^x] or \p{L} is ONE position (exact: '.' excludes U+0085 /
+// U+2028 / U+2029 as Java's does) and X.{0,1000}Y is ~1000 positions = 16 words.
+//
+// Matcher.find() semantics (jregex.h): boundary context ctx = prev kind x next kind (24 contexts,
+// ctx = prev * 6 + next) is checked before every code point (accept) and gates edges; extra accept
+// check before a final line terminator; end of line is next kind N_EOS.
+//
+// Program layout (uint64 words):
+//   [0] W | E << 8 | ncls << 20 | anchored << 30 | uniform << 31 | nullable(24) << 32 | uword << 56
+//   [1] nranges | total words << 32
+//   [2 ..]           shm[W] selfm[W] src[W] R[W] lo[W] hi[W]
+//   [2 + 6W ..]      first[24][W]           (per boundary context; uniform -> only [0] is read)
+//   [2 + 30W ..]     last[24][W]
+//   [2 + 54W ..]     amap: 128 x uint16 (ASCII code point -> class), 32 words
+//   [2 + 54W + 32..] cls[ncls][W]
+//   then             exc[E][1 + W]          (src | cond << 16, then the target mask)
+//   then             ranges[nranges]        (lo | class << 21 | kind << 37; kind 0 N, 1 W, 2 T),
+//                                           sorted by lo, first lo = 0x80
 #pragma once
 #include <stdint.h>
 
 namespace lp {
 
-constexpr int BPG_MAX_W = 8;          // 512 positions (models/bpg.py MAX_WORDS)
+constexpr int BPG_LANE_MAX_W = 8;      // widest program of the one-lane-per-line walk
 constexpr uint64_t BPG_UNIFORM = 1ull << 31;
 constexpr uint64_t BPG_ANCHORED = 1ull << 30;
 
-// next-kind of a byte: 2 word, 3 other, 4 UTF-8 continuation (jregex.h N_W / N_N / N_C)
+struct BpgLayout {
+  int W, E, ncls, nranges;
+  bool uniform, anchored;
+  uint32_t nullm;
+  int o_first, o_last, o_amap, o_cls, o_exc, o_rng;
+};
+
+LP_HD BpgLayout bpg_layout(const uint64_t* P) {
+  const uint64_t h = P[0];
+  BpgLayout L;
+  L.W = (int)(h & 0xFF);
+  L.E = (int)((h >> 8) & 0xFFF);
+  L.ncls = (int)((h >> 20) & 0x3FF);
+  L.anchored = (h & BPG_ANCHORED) != 0;
+  L.uniform = (h & BPG_UNIFORM) != 0;
+  L.nullm = (uint32_t)(h >> 32) & 0xFFFFFFu;
+  L.nranges = (int)(P[1] & 0xFFFFFFFFu);
+  L.o_first = 2 + 6 * L.W;
+  L.o_last = 2 + 30 * L.W;
+  L.o_amap = 2 + 54 * L.W;
+  L.o_cls = L.o_amap + 32;
+  L.o_exc = L.o_cls + L.ncls * L.W;
+  L.o_rng = L.o_exc + L.E * (L.W + 1);
+  return L;
+}
+LP_HD int bpg_words(const uint64_t* P) { return (int)(P[1] >> 32); }
+
+// byte-level next kind (the MFMA NFA engine's 15 contexts, nfa_mfma.hip): 2 word, 3 other,
+// 4 UTF-8 continuation
 LP_HD int byte_kind(int c) {
   const bool w = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
   return w ? 2 : (c >= 0x80 && c <= 0xBF) ? 4 : 3;
 }
 
+// code-point next kinds (jregex.h): N_EOS 0, N_FT 1, N_W 2, N_N 3, N_T 5; prev kinds P_W 1, P_N 2, P_T 3
+LP_HD int ascii_kind(int c) {
+  const bool w = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
+  return w ? 2 : (c == '\r' || c == '\n') ? 5 : 3;
+}
+LP_HD int prev_of(int nk) { return nk == 2 ? 1 : nk == 5 ? 3 : 2; }
+
+// class and next kind of a non-ASCII code point: binary search of the range table
+LP_HD int bpg_cp_class(const uint64_t* __restrict__ rg, int nr, uint32_t cp, int* kind) {
+  int lo = 0, hi = nr - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((uint32_t)(rg[mid] & 0x1FFFFFu) <= cp) lo = mid; else hi = mid - 1;
+  }
+  const uint64_t e = rg[lo];
+  const int kd = (int)((e >> 37) & 3);
+  *kind = kd == 1 ? 2 : kd == 2 ? 5 : 3;
+  return (int)((e >> 21) & 0xFFFF);
+}
+
+// the UTF-8 code point whose lead byte is c, with its continuation bytes b1..b3 (lenient)
+LP_HD uint32_t utf8_cp(int c, int b1, int b2, int b3) {
+  if (c >= 0xF0) return ((uint32_t)(c & 7) << 18) | ((uint32_t)(b1 & 0x3F) << 12) | ((uint32_t)(b2 & 0x3F) << 6) | (uint32_t)(b3 & 0x3F);
+  if (c >= 0xE0) return ((uint32_t)(c & 15) << 12) | ((uint32_t)(b1 & 0x3F) << 6) | (uint32_t)(b2 & 0x3F);
+  return ((uint32_t)(c & 31) << 6) | (uint32_t)(b1 & 0x3F);
+}
+
+// per-character operands of byte t of the line: class (-1: a continuation byte, skipped) and kind
+LP_HD int bpg_char(const uint64_t* __restrict__ P, const BpgLayout& L, const uint8_t* s, int n, int t, int* kind) {
+  const int c = s[t];
+  if (c < 0x80) { *kind = ascii_kind(c); return reinterpret_cast<const uint16_t*>(P + L.o_amap)[c]; }
+  if (c < 0xC0) { *kind = 3; return -1; }
+  const int b1 = t + 1 < n ? s[t + 1] : 0x80, b2 = t + 2 < n ? s[t + 2] : 0x80, b3 = t + 3 < n ? s[t + 3] : 0x80;
+  return bpg_cp_class(P + L.o_rng, L.nranges, utf8_cp(c, b1, b2, b3), kind);
+}
+
 template <int W>
 LP_HD bool bpg_find_w(const uint64_t* __restrict__ P, const uint8_t* __restrict__ s, int n) {
-  const uint64_t hdr = P[0];
-  const int E = (int)((hdr >> 8) & 0xFFF);
-  const int ncls = (int)((hdr >> 20) & 0x3FF);
-  const bool uniform = (hdr & BPG_UNIFORM) != 0;
-  const bool anchored = (hdr & BPG_ANCHORED) != 0;
-  const uint32_t nullm = (uint32_t)(hdr >> 32) & 0x7FFFu;
-  const uint64_t* q = P + 1;
-  uint64_t shm[W], selfm[W], src[W], R[W], lo[W], hi[W], f0[W], l0[W], S[W];
-  const uint64_t* first = q + 6 * W;
-  const uint64_t* last = first + 15 * W;
-  const uint8_t* bm = reinterpret_cast<const uint8_t*>(last + 15 * W);
-  const uint64_t* cls = last + 15 * W + 32;
-  const uint64_t* exc = cls + (size_t)ncls * W;
-#pragma unroll
+  const BpgLayout L = bpg_layout(P);
+  const uint64_t* q = P + 2;
+  uint64_t shm[W], selfm[W], src[W], R[W], lo[W], hi[W], S[W];
+  const uint64_t* first = P + L.o_first;
+  const uint64_t* last = P + L.o_last;
+  const uint64_t* cls = P + L.o_cls;
+  const uint64_t* exc = P + L.o_exc;
   for (int w = 0; w < W; ++w) {
     shm[w] = q[w];
     selfm[w] = q[W + w];
@@ -50,42 +125,36 @@ LP_HD bool bpg_find_w(const uint64_t* __restrict__ P, const uint8_t* __restrict_
     R[w] = q[3 * W + w];
     lo[w] = q[4 * W + w];
     hi[w] = q[5 * W + w];
-    f0[w] = first[w];
-    l0[w] = last[w];
     S[w] = 0;
   }
   const int ftl = final_term_len(s, n);
   const int ft = ftl ? n - ftl : -1;
   int prevk = 0;  // P_BOS
   for (int t = 0;; ++t) {
-    const int c = t < n ? (int)s[t] : 0;
-    const int nk = t < n ? byte_kind(c) : 0;  // N_EOS at end of line
-    // accept before this byte (and before a final line terminator)
+    int nk = 0, k = 0;                          // N_EOS at end of line
+    if (t < n) {
+      k = bpg_char(P, L, s, n, t, &nk);
+      if (k < 0) continue;                      // inside a code point
+    }
+    // accept before this character (and before a final line terminator)
     for (int pass = (t == ft) ? 0 : 1; pass < 2; ++pass) {
-      const int actx = prevk * 5 + (pass == 0 ? 1 : nk);
-      if ((nullm >> actx) & 1u) return true;
-      const uint64_t* L = uniform ? nullptr : last + actx * W;
+      const int actx = prevk * 6 + (pass == 0 ? 1 : nk);
+      if ((L.nullm >> actx) & 1u) return true;
+      const uint64_t* Lm = last + (L.uniform ? 0 : actx * W);
       uint64_t any = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) any |= S[w] & (uniform ? l0[w] : L[w]);
+      for (int w = 0; w < W; ++w) any |= S[w] & Lm[w];
       if (any) return true;
     }
     if (t >= n) return false;
-    const int ctx = prevk * 5 + nk;
+    const int ctx = prevk * 6 + nk;
     uint64_t F[W];
-    // shift (with the carry across words) + self loops
-    uint64_t carry = 0;
-#pragma unroll
+    uint64_t carry = 0, borrow = 0;
     for (int w = 0; w < W; ++w) {
       const uint64_t x = S[w] & shm[w];
       F[w] = (x << 1) | carry | (S[w] & selfm[w]);
       carry = x >> 63;
-    }
-    // spread fields: d = (S & src | hi) - lo (multi-word borrow); targets above the lowest
-    // active source of every field = R & ~(d ^ (S & src | hi))
-    uint64_t borrow = 0;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
+      // spread fields: d = (S & src | hi) - lo (multi-word borrow); targets above the lowest
+      // active source of every field = R & ~(d ^ (S & src | hi))
       const uint64_t df = (S[w] & src[w]) | hi[w];
       const uint64_t u = df - lo[w];
       const uint64_t b1 = df < lo[w] ? 1ull : 0ull;
@@ -94,54 +163,63 @@ LP_HD bool bpg_find_w(const uint64_t* __restrict__ P, const uint8_t* __restrict_
       borrow = b1 | b2;
       F[w] |= R[w] & ~(d ^ df);
     }
-    // exceptions: (source, condition, targets)
-    for (int e = 0; e < E; ++e) {
+    for (int e = 0; e < L.E; ++e) {               // exceptions: (source, condition, targets)
       const uint64_t* x = exc + (size_t)e * (W + 1);
-      const uint64_t h = x[0];
-      const int p = (int)(h & 0xFFFF);
-      const uint32_t cond = (uint32_t)(h >> 16) & 0xFFFFu;
-      uint64_t sw = 0;
-#pragma unroll
-      for (int w = 0; w < W; ++w) sw = (w == (p >> 6)) ? S[w] : sw;
-      if (((sw >> (p & 63)) & 1ull) && ((cond >> ctx) & 1u)) {
-#pragma unroll
+      const int p = (int)(x[0] & 0xFFFF);
+      const uint32_t cond = (uint32_t)(x[0] >> 16) & 0xFFFFFFu;
+      if (((S[p >> 6] >> (p & 63)) & 1ull) && ((cond >> ctx) & 1u))
         for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
-      }
     }
-    const uint64_t* C = cls + (size_t)bm[c] * W;
-    const uint64_t* Fi = uniform ? nullptr : first + ctx * W;
+    const uint64_t* C = cls + (size_t)k * W;
+    const uint64_t* Fi = first + (L.uniform ? 0 : ctx * W);
     uint64_t alive = 0;
-#pragma unroll
     for (int w = 0; w < W; ++w) {
-      S[w] = (F[w] | (uniform ? f0[w] : Fi[w])) & C[w];
+      S[w] = (F[w] | Fi[w]) & C[w];
       alive |= S[w];
     }
-    if (anchored && !alive) return false;  // first set only at the line start: nothing can match
-    prevk = nk == 2 ? 1 : 2;
+    if (L.anchored && !alive) return false;  // first set only at the line start: nothing can match
+    prevk = prev_of(nk);
   }
 }
 
 #if defined(__HIP__)
-// Device walk of one program (kernels in bpg.hip, one instantiation per width W so each kernel's
-// registers are sized for its own W): the line's bytes come from 16-byte ALIGNED vector loads one
-// block ahead (a byte load per step would put a memory round trip on the dependency chain), the
-// structural masks live in registers, class / first / last / exception rows are read through P --
-// a global pointer for candidate verification, an LDS copy for the all-lines scan.
+__device__ __forceinline__ int blk_byte(const uint4& v, int j) {   // byte j (0..15) of a 16-byte block
+  const uint32_t w = (j < 4) ? v.x : (j < 8) ? v.y : (j < 12) ? v.z : v.w;
+  return (int)((w >> (8 * (j & 3))) & 0xFFu);
+}
+// byte j (0..31) of the 32-byte window cur:nxt
+__device__ __forceinline__ int win_byte(const uint4& cur, const uint4& nxt, int j) {
+  return j < 16 ? blk_byte(cur, j) : blk_byte(nxt, j - 16);
+}
+// class (-1: continuation byte) and next kind of the character whose first byte is window byte j
+// (text position t of a line of n bytes)
+__device__ __forceinline__ int bpg_char_win(const uint64_t* __restrict__ P, const BpgLayout& L, const uint4& cur,
+                                            const uint4& nxt, int j, int t, int n, int* kind) {
+  const int c = win_byte(cur, nxt, j);
+  if (c < 0x80) { *kind = ascii_kind(c); return reinterpret_cast<const uint16_t*>(P + L.o_amap)[c]; }
+  if (c < 0xC0) { *kind = 3; return -1; }
+  // non-ASCII (rare in logs): decode from the window, binary-search the range table
+  const int b1 = t + 1 < n ? win_byte(cur, nxt, j + 1) : 0x80;
+  const int b2 = t + 2 < n ? win_byte(cur, nxt, j + 2) : 0x80;
+  const int b3 = t + 3 < n ? win_byte(cur, nxt, j + 3) : 0x80;
+  return bpg_cp_class(P + L.o_rng, L.nranges, utf8_cp(c, b1, b2, b3), kind);
+}
+
+// Device walk of one program, one lane per line (W <= BPG_LANE_MAX_W; kernels in bpg.hip, one
+// instantiation per width so each kernel's registers are sized for its own W): the line's bytes
+// come from 16-byte ALIGNED vector loads one block ahead (a byte load per step would put a memory
+// round trip on the dependency chain), the structural masks live in registers, class / first /
+// last / exception rows are read through P -- a global pointer for candidate verification, an LDS
+// copy for the all-lines scan.
 template <int W>
 __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, const uint8_t* __restrict__ s, int n) {
-  const uint64_t hdr = P[0];
-  const int E = (int)((hdr >> 8) & 0xFFF);
-  const int ncls = (int)((hdr >> 20) & 0x3FF);
-  const bool uniform = (hdr & BPG_UNIFORM) != 0;
-  const bool anchored = (hdr & BPG_ANCHORED) != 0;
-  const uint32_t nullm = (uint32_t)(hdr >> 32) & 0x7FFFu;
-  const uint64_t* q = P + 1;
+  const BpgLayout L = bpg_layout(P);
+  const uint64_t* q = P + 2;
   uint64_t shm[W], selfm[W], src[W], R[W], lo[W], hi[W], f0[W], l0[W], S[W];
-  const uint64_t* first = q + 6 * W;
-  const uint64_t* last = first + 15 * W;
-  const uint8_t* bm = reinterpret_cast<const uint8_t*>(last + 15 * W);
-  const uint64_t* cls = last + 15 * W + 32;
-  const uint64_t* exc = cls + (size_t)ncls * W;
+  const uint64_t* first = P + L.o_first;
+  const uint64_t* last = P + L.o_last;
+  const uint64_t* cls = P + L.o_cls;
+  const uint64_t* exc = P + L.o_exc;
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     shm[w] = q[w];
@@ -154,6 +232,8 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
     l0[w] = last[w];
     S[w] = 0;
   }
+  const bool uniform = L.uniform;
+  const uint32_t nullm = L.nullm;
   const int ftl = final_term_len(s, n);
   const int ft = ftl ? n - ftl : -1;
   int prevk = 0;  // P_BOS
@@ -181,35 +261,34 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
       ++blk;
       const int j0 = t0 < 0 ? -t0 : 0;
       const int j1 = n - t0 < 16 ? n - t0 : 16;
-      // PF bytes at a time: their class rows depend on the text only, not on the state, so all
-      // PF rows are loaded before the first state update (one load latency per PF bytes instead
-      // of two dependent loads -- byte map, then row -- on every byte's chain)
+      // PF characters at a time: their class rows depend on the text only, not on the state, so
+      // all PF rows are loaded before the first state update (one load latency per PF bytes
+      // instead of two dependent loads -- class map, then row -- on every byte's chain)
       constexpr int PF = W <= 4 ? 4 : 2;     // rows in flight (registers: PF x W words)
       for (int jb = j0; jb < j1; jb += PF) {
         uint64_t Cr[PF][W];
-        int cb[PF];
+        int kq[PF], nkq[PF];
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          const int j = jb + q < 15 ? jb + q : 15;
-          const uint32_t wv = (j < 4) ? cur.x : (j < 8) ? cur.y : (j < 12) ? cur.z : cur.w;
-          cb[q] = (int)((wv >> (8 * (j & 3))) & 0xFFu);
-          const uint64_t* row = cls + (size_t)bm[cb[q]] * W;
+        for (int qq = 0; qq < PF; ++qq) {
+          const int j = jb + qq < 15 ? jb + qq : 15;
+          kq[qq] = bpg_char_win(P, L, cur, nxt, j, t0 + j, n, &nkq[qq]);
+          const uint64_t* row = cls + (size_t)(kq[qq] < 0 ? 0 : kq[qq]) * W;
 #pragma unroll
-          for (int w = 0; w < W; ++w) Cr[q][w] = row[w];
+          for (int w = 0; w < W; ++w) Cr[qq][w] = row[w];
         }
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-          if (jb + q >= j1) break;
-          const int t = t0 + jb + q;
-          const int c = cb[q];
-          const int nk = byte_kind(c);
+        for (int qq = 0; qq < PF; ++qq) {
+          if (jb + qq >= j1) break;
+          if (kq[qq] < 0) continue;             // continuation byte: inside a code point
+          const int t = t0 + jb + qq;
+          const int nk = nkq[qq];
           if (t == ft) {
-            LP_BPG_ACCEPT(prevk * 5 + 1, hit);
+            LP_BPG_ACCEPT(prevk * 6 + 1, hit);
             if (hit) return true;
           }
-          LP_BPG_ACCEPT(prevk * 5 + nk, hit);
+          LP_BPG_ACCEPT(prevk * 6 + nk, hit);
           if (hit) return true;
-          const int ctx = prevk * 5 + nk;
+          const int ctx = prevk * 6 + nk;
           uint64_t F[W];
           uint64_t carry = 0, borrow = 0;
 #pragma unroll
@@ -225,7 +304,7 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
             borrow = b1 | b2;
             F[w] |= R[w] & ~(d ^ df);
           }
-          for (int e = 0; e < E; ++e) {
+          for (int e = 0; e < L.E; ++e) {
             const uint64_t* x = exc + (size_t)e * (W + 1);
             const uint64_t h = x[0];
             const int p = (int)(h & 0xFFFF);
@@ -241,25 +320,25 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
           if (uniform) {
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-              S[w] = (F[w] | f0[w]) & Cr[q][w];
+              S[w] = (F[w] | f0[w]) & Cr[qq][w];
               alive |= S[w];
             }
           } else {
             const uint64_t* Fi = first + ctx * W;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-              S[w] = (F[w] | Fi[w]) & Cr[q][w];
+              S[w] = (F[w] | Fi[w]) & Cr[qq][w];
               alive |= S[w];
             }
           }
-          if (anchored && !alive) return false;
-          prevk = nk == 2 ? 1 : 2;
+          if (L.anchored && !alive) return false;
+          prevk = prev_of(nk);
         }
       }
       cur = nxt;
     }
   }
-  LP_BPG_ACCEPT(prevk * 5 + 0, hit);  // end of line (N_EOS)
+  LP_BPG_ACCEPT(prevk * 6 + 0, hit);  // end of line (N_EOS)
   return hit;
 #undef LP_BPG_ACCEPT
 }
@@ -274,7 +353,11 @@ inline bool bpg_find_host(const uint64_t* P, const uint8_t* s, int n) {
     case 3: return bpg_find_w<3>(P, s, n);
     case 4: return bpg_find_w<4>(P, s, n);
     case 6: return bpg_find_w<6>(P, s, n);
-    default: return bpg_find_w<8>(P, s, n);
+    case 8: return bpg_find_w<8>(P, s, n);
+    case 12: return bpg_find_w<12>(P, s, n);
+    case 16: return bpg_find_w<16>(P, s, n);
+    case 24: return bpg_find_w<24>(P, s, n);
+    default: return bpg_find_w<32>(P, s, n);
   }
 }
 

@@ -1,14 +1,16 @@
-// gfx950 kernels of the bit-parallel Glushkov programs (bpg.h, models/bpg.py): the regexes whose
-// DFA blows up, verified on prefilter candidate lines or scanned over every line.
+// gfx950 kernels of the bit-parallel Glushkov programs (bpg.h, jregex.cpp bpg_program): the regexes
+// whose DFA blows up or that need code-point contexts, verified on prefilter candidate lines or
+// scanned over every line.
 //
-// Candidate verification (few lines: the slowest walk decides) is one kernel for every program width;
-// the all-lines scan (every line: occupancy decides) is one instantiation per width W (words of 64
-// positions), launched only for the widths a library has. The DFA kernels next to them
-// (k_cand_verify, k_dedupe_verify, k_scan) never carry the BPG walk -- folding it into dfa_run took
-// those kernels from ~40 to 130 VGPRs plus 580 B of scratch per lane (3 waves / SIMD).
+// Two walks of the same program:
+//   * one lane per line (bpg_find_dev<W>, W <= 8 words): throughput -- the bulk path's first-of-run
+//     keys and the literal-free scan of W <= 8 programs;
+//   * a GROUP of G lanes per line (bpg_coop_walk<G>, any width up to 32 words = 2,048 positions):
+//     latency -- request-path candidates, and every line of programs wider than 8 words.
+// The DFA kernels next to them (k_cand_verify, k_dedupe_verify, k_scan) never carry the BPG walk --
+// folding it into dfa_run took those kernels from ~40 to 130 VGPRs plus 580 B of scratch per lane.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -21,50 +23,25 @@ namespace {
 
 constexpr uint64_t kPadKey = ~0ull;   // lp_post.hip LP_PAD_KEY
 constexpr int kScanLines = 256;
+constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global memory)
 
 inline unsigned nblocks(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
 
-// candidates of the small path, in place (-1 = no match; k_cand_verify did the DFA ones): one
-// launch for every width -- a step's BPG candidates are few, the launch and the slowest walk are
-// what cost, not the registers of the widest walk
-__global__ __launch_bounds__(256) void k_bpg_cand_all(int64_t* __restrict__ cand, int64_t cap,
-                                                      const unsigned long long* __restrict__ dcount,
-                                                      const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
-                                                      const int32_t* __restrict__ ll, DfaPool P) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = dcount ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
-  if (i >= n) return;
-  const int64_t k = cand[i];
-  if (k < 0) return;
-  const int r = (int)(k >> 32);
-  if (!is_bpg(P, r)) return;
-  const uint64_t* prog = P.bpg + P.meta[4 * r];
-  const int64_t x = k & 0xFFFFFFFFll;
-  const uint8_t* s = text + ls[x];
-  const int len = ll[x];
-  bool m;
+__device__ __forceinline__ bool lane_walk(const uint64_t* prog, const uint8_t* s, int len) {
   switch ((int)(prog[0] & 0xFF)) {
-    case 1: m = bpg_find_dev<1>(prog, s, len); break;
-    case 2: m = bpg_find_dev<2>(prog, s, len); break;
-    case 3: m = bpg_find_dev<3>(prog, s, len); break;
-    case 4: m = bpg_find_dev<4>(prog, s, len); break;
-    case 6: m = bpg_find_dev<6>(prog, s, len); break;
-    default: m = bpg_find_dev<8>(prog, s, len); break;
+    case 1: return bpg_find_dev<1>(prog, s, len);
+    case 2: return bpg_find_dev<2>(prog, s, len);
+    case 3: return bpg_find_dev<3>(prog, s, len);
+    case 4: return bpg_find_dev<4>(prog, s, len);
+    case 6: return bpg_find_dev<6>(prog, s, len);
+    default: return bpg_find_dev<8>(prog, s, len);
   }
-  if (!m) cand[i] = -1;
 }
 
 // bulk path: sorted packed keys ((regex << lbits | line) << 1 | pre-verified); the first key of
-// every run whose regex is a width-W program and that no engine pre-verified gets its flag here
-// (k_dedupe_verify left it 0)
-constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global memory)
-
-__device__ __forceinline__ int prog_words(const uint64_t* prog, int W) {   // header, masks, tables
-  const uint64_t h = prog[0];
-  return 1 + 36 * W + 32 + (int)((h >> 20) & 0x3FF) * W + (int)((h >> 8) & 0xFFF) * (W + 1);
-}
-
-// bulk path, every width in one kernel (registers of the widest walk: fine for a few waves)
+// every run whose regex is a program of <= 8 words and that no engine pre-verified gets its flag
+// here (k_dedupe_verify left it 0; wider programs: k_bpg_coop<G, 1>). Every width in one kernel
+// (registers of the widest walk: fine for a few waves).
 __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restrict__ keys, int64_t n, int lbits,
                                                         const uint8_t* __restrict__ text,
                                                         const int64_t* __restrict__ ls,
@@ -78,39 +55,32 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
   if (i > 0 && (keys[i - 1] >> 1) == k) return;
   const int r = (int)(k >> lbits);
   if (!is_bpg(P, r)) return;
+  const uint64_t* prog = P.bpg + P.meta[4 * r];
+  if ((int)(prog[0] & 0xFF) > BPG_LANE_MAX_W) return;
   for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j)
     if (keys[j] & 1) return;                  // pre-verified: flag already 1
-  const uint64_t* prog = P.bpg + P.meta[4 * r];
   const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
-  const uint8_t* s = text + ls[x];
-  const int len = ll[x];
-  bool m;
-  switch ((int)(prog[0] & 0xFF)) {
-    case 1: m = bpg_find_dev<1>(prog, s, len); break;
-    case 2: m = bpg_find_dev<2>(prog, s, len); break;
-    case 3: m = bpg_find_dev<3>(prog, s, len); break;
-    case 4: m = bpg_find_dev<4>(prog, s, len); break;
-    case 6: m = bpg_find_dev<6>(prog, s, len); break;
-    default: m = bpg_find_dev<8>(prog, s, len); break;
-  }
-  flag[i] = m ? 1 : 0;
+  flag[i] = lane_walk(prog, text + ls[x], ll[x]) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wave-cooperative walk (candidate verification: few lines, so the latency of ONE line's walk decides).
+// Wave-cooperative walk (candidate verification: few lines, so the latency of ONE line's walk
+// decides; and programs too wide for one lane's registers).
 //
-// The one-lane-per-line walk above is a serial chain of ~40 dependent VALU ops per 64-bit word per
-// byte (~240 for a 6-word program: 75 us for one 10k-line request's candidates, profiles/r3_h). Here
-// a line is walked by a GROUP of G lanes (G = power of two >= 2W), lane j holding 32-bit word j of
-// every mask, so a byte costs ~20 ops on the chain whatever the width:
-//   * shift edges: the carry of word j-1 arrives by DPP row_shr:1 (groups never straddle a 16-lane row);
+// The one-lane walk is a serial chain of ~40 dependent VALU ops per 64-bit word per character
+// (~240 for a 6-word program: 75 us for one 10k-line request's candidates, profiles/r3_h). Here a
+// line is walked by a GROUP of G lanes (G = power of two >= 2W), lane j holding 32-bit word j of
+// every mask, so a character costs ~20 ops on the chain whatever the width:
+//   * shift edges: the carry of word j-1 arrives by DPP row_shr:1 when groups fit in a 16-lane row
+//     (G <= 16), else from a ballot of the words' top bits;
 //   * spread fields: the multi-word subtraction's borrow chain is a carry-lookahead on two ballots --
 //     generate g = df < lo, propagate p = df == lo; the borrow INTO lane i is bit i of
 //     (X + G) ^ X ^ G with X = G | P (a 64-bit scalar add resolves every group's chain at once;
 //     each group's top lane is masked out of G and P, so no borrow crosses into the next group);
 //   * exceptions: the source bit's owner lane votes (ballot), every lane of the group reads it;
 //   * class / first / last words for 16 bytes are loaded before the 16 serial updates (they depend
-//     on the text only), so no load latency sits on the state chain.
+//     on the text only), so no load latency sits on the state chain; UTF-8 continuation bytes keep
+//     the state (a select), lead bytes are decoded from the 32-byte window of this block and the next.
 // A wave takes 64 candidate slots, compacts the ones that need a BPG walk (ballot) and walks them
 // 64 / G at a time.
 
@@ -128,25 +98,23 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
   const int gb = lane & ~(G - 1);
   const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
   const uint64_t chain = coop_chain_mask(G);
-  const uint64_t hdr = valid ? P[0] : 0ull;
-  const int W = (int)(hdr & 0xFF);
-  const int E = (int)((hdr >> 8) & 0xFFF);
-  const int ncls = (int)((hdr >> 20) & 0x3FF);
-  const bool uniform = (hdr & BPG_UNIFORM) != 0;
-  const uint32_t nullm = (uint32_t)(hdr >> 32) & 0x7FFFu;
+  BpgLayout L = bpg_layout(P);
+  if (!valid) { L.W = 0; L.E = 0; L.uniform = true; L.nullm = 0; }
+  const int W = L.W;
+  const int E = L.E;
+  const bool uniform = L.uniform;
+  const uint32_t nullm = L.nullm;
   const bool wl = valid && j < 2 * W;           // this lane holds a program word
   const uint32_t* p32 = reinterpret_cast<const uint32_t*>(P);
   // uint32 index of word j of the 64-bit mask at uint64 offset o
 #define LP_W32(o) (p32[2 * (o) + j])
   // word j of every structural mask; lanes past the program (and invalid groups) hold zeros, so
-  // their state stays empty. The top word's bit 31 never has a shift edge (no position above), so
-  // no shift carry leaves a group and row_shr:1 needs no mask.
-  const uint32_t shm = wl ? LP_W32(1) : 0u, selfm = wl ? LP_W32(1 + W) : 0u, src = wl ? LP_W32(1 + 2 * W) : 0u;
-  const uint32_t R = wl ? LP_W32(1 + 3 * W) : 0u, lo = wl ? LP_W32(1 + 4 * W) : 0u, hi = wl ? LP_W32(1 + 5 * W) : 0u;
-  const int first_o = 1 + 6 * W, last_o = 1 + 21 * W, cls_o = 1 + 36 * W + 32;
+  // their state stays empty. The last position never has a shift edge (no position above), so no
+  // shift carry leaves a group.
+  const uint32_t shm = wl ? LP_W32(2) : 0u, selfm = wl ? LP_W32(2 + W) : 0u, src = wl ? LP_W32(2 + 2 * W) : 0u;
+  const uint32_t R = wl ? LP_W32(2 + 3 * W) : 0u, lo = wl ? LP_W32(2 + 4 * W) : 0u, hi = wl ? LP_W32(2 + 5 * W) : 0u;
+  const int first_o = L.o_first, last_o = L.o_last, cls_o = L.o_cls, exc_o = L.o_exc;
   const uint32_t f0 = wl ? LP_W32(first_o) : 0u, l0 = wl ? LP_W32(last_o) : 0u;
-  const uint8_t* bm = reinterpret_cast<const uint8_t*>(P + 1 + 36 * W);
-  const int exc_o = cls_o + ncls * W;
   const int ftl = valid ? final_term_len(s, n) : 0;
   const int ft = ftl ? n - ftl : -1;
   // wave-uniform feature switches: the common program (uniform first/last sets, no exception edges,
@@ -165,26 +133,30 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
   bool nullhit = false;
   int prevk = 0;                                 // P_BOS
   for (int b0 = 0; b0 <= T; b0 += 16) {          // wave-uniform
-    const uint4 cur = (valid && b0 < sh + n) ? blk[b0 >> 4] : make_uint4(0, 0, 0, 0);
+    const bool inl = valid && b0 < sh + n;
+    const uint4 cur = inl ? blk[b0 >> 4] : make_uint4(0, 0, 0, 0);
+    const uint4 nxt = (inl && b0 + 16 < sh + n) ? blk[(b0 >> 4) + 1] : make_uint4(0, 0, 0, 0);
     // text-only operands of the 16 bytes, off the state chain: class words (0 outside [0, n): the
-    // state is empty before the line and dies after its end), boundary contexts, first / last words
+    // state is empty before the line and dies after its end), skip flags of UTF-8 continuation
+    // bytes, boundary contexts, first / last words
     uint32_t cw[16], fw[16], lw[16];
     int ctxq[16];
+    uint32_t skipm = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const uint32_t wv = (q < 4) ? cur.x : (q < 8) ? cur.y : (q < 12) ? cur.z : cur.w;
-      const int c = (int)((wv >> (8 * (q & 3))) & 0xFFu);
       const int t = b0 + q - sh;
-      const bool live = wl && t >= 0 && t < n;
-      cw[q] = live ? LP_W32(cls_o + (int)bm[c] * W) : 0u;
-      if (wctx) {
-        const bool lv = valid && t >= 0 && t < n;
-        const int nk = lv ? byte_kind(c) : 0;    // N_EOS from the end of line on
-        if (wft && t == ft) ftctx = prevk * 5 + 1;
-        ctxq[q] = prevk * 5 + nk;
+      const bool lv = valid && t >= 0 && t < n;
+      int nk = 0, k = 0;
+      if (lv) k = bpg_char_win(P, L, cur, nxt, q, t, n, &nk);
+      const bool skip = lv && k < 0;
+      skipm |= skip ? 1u << q : 0u;
+      cw[q] = (wl && lv && !skip) ? LP_W32(cls_o + k * W) : 0u;
+      ctxq[q] = prevk * 6 + nk;                  // N_EOS from the end of line on
+      if (wctx && !skip) {
+        if (wft && t == ft) ftctx = prevk * 6 + 1;
         nullhit |= valid && t >= 0 && t <= n && ((nullm >> ctxq[q]) & 1u);
-        if (lv) prevk = nk == 2 ? 1 : 2;
       }
+      if (lv && !skip) prevk = prev_of(nk);
     }
     if (wnon) {
 #pragma unroll
@@ -195,13 +167,20 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      // accept before this byte (the state after the last byte is checked at t = n; later
+      const bool skip = (skipm >> q) & 1u;
+      // accept before this character (the state after the last one is checked at t = n; later
       // positions see the empty state)
-      acc |= S & (wnon ? lw[q] : l0);
+      acc |= skip ? 0u : (S & (wnon ? lw[q] : l0));
       if (wft) Sft = (b0 + q - sh == ft) ? S : Sft;
       // shift edges with the carry out of word j-1, self loops
       const uint32_t x = S & shm;
-      const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x >> 31), 0x111 /* row_shr:1 */, 0xF, 0xF, true);
+      uint32_t y;
+      if (G <= 16) {
+        y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(x >> 31), 0x111 /* row_shr:1 */, 0xF, 0xF, true);
+      } else {
+        const uint64_t cm = __ballot((x >> 31) != 0u);
+        y = (uint32_t)(((cm << 1) >> lane) & 1ull);
+      }
       uint32_t F = (x << 1) | y | (S & selfm);
       // spread fields: d = df - lo over the group; borrow INTO lane i = bit i of (X + G) ^ X ^ G
       const uint32_t df = (S & src) | hi;
@@ -214,14 +193,15 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
       if (wexc) {                                // exception edges: the source word's lane votes
         const int ctx = ctxq[q];
         for (int e = 0; e < E; ++e) {            // E varies across groups: lanes past their E idle
-          const uint32_t h = (uint32_t)P[exc_o + e * (W + 1)];
+          const uint64_t h = P[exc_o + e * (W + 1)];
           const uint32_t tw = wl ? LP_W32(exc_o + e * (W + 1) + 1) : 0u;
           const int p = (int)(h & 0xFFFF);
           const uint64_t M = __ballot(j == (p >> 5) && ((S >> (p & 31)) & 1u));
-          if (((M >> (gb + (p >> 5))) & 1ull) && (((h >> 16) >> ctx) & 1u)) F |= tw;
+          if (((M >> (gb + (p >> 5))) & 1ull) && ((((uint32_t)(h >> 16) & 0xFFFFFFu) >> ctx) & 1u)) F |= tw;
         }
       }
-      S = (F | (wnon ? fw[q] : f0)) & cw[q];
+      const uint32_t Sn = (F | (wnon ? fw[q] : f0)) & cw[q];
+      S = skip ? S : Sn;
     }
     // a group is finished once it accepted or its line ended; the wave stops when all are
     const uint64_t hitm = __ballot(acc != 0 || nullhit);
@@ -234,28 +214,29 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
 }
 
 // mode 0: cand[i] = -1 for BPG candidates that do not match (request path, k_cand_verify did the
-// DFA ones); mode 2: the same, with the DFA candidates verified by the grid's upper half; mode 1: flag the first key of every sorted run whose regex is a BPG program that no
-// engine pre-verified (bulk path, k_dedupe_verify left the flag 0)
+// DFA ones); mode 2: the same, with the DFA candidates verified by the grid's upper half; mode 1:
+// flag the first key of every sorted run whose regex is a program of >= wmin words that no engine
+// pre-verified (bulk path, k_dedupe_verify left the flag 0)
 template <int G, int MODE>
 __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, const uint64_t* __restrict__ keys,
                                                   int64_t cap, const unsigned long long* __restrict__ dcount, int lbits,
                                                   const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
                                                   const int32_t* __restrict__ ll, DfaPool P,
-                                                  uint8_t* __restrict__ flag) {
+                                                  uint8_t* __restrict__ flag, int wmin) {
   const int lane = (int)(threadIdx.x & 63);
   const int64_t n = (MODE != 1 && dcount) ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
   if (MODE == 2 && blockIdx.x >= (gridDim.x >> 1)) {
     // the grid's upper half: DFA candidates, one lane each (k_cand_verify's work), side by side
     // with the BPG walks of the lower half -- one launch, and a request's critical path is the
     // longer of the two instead of their sum
-    const int64_t j = (int64_t)(blockIdx.x - (gridDim.x >> 1)) * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const int64_t k = cand[j];
+    const int64_t jj = (int64_t)(blockIdx.x - (gridDim.x >> 1)) * blockDim.x + threadIdx.x;
+    if (jj >= n) return;
+    const int64_t k = cand[jj];
     if (k < 0) return;
     const int r = (int)(k >> 32);
     if (is_bpg(P, r)) return;
     const int64_t x = k & 0xFFFFFFFFll;
-    if (!dfa_run(P, r, text + ls[x], ll[x])) cand[j] = -1;
+    if (!dfa_run(P, r, text + ls[x], ll[x])) cand[jj] = -1;
     return;
   }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -276,7 +257,7 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
       if (key != kPadKey && !(i > 0 && (keys[i - 1] >> 1) == k)) {
         r = (int)(k >> lbits);
         x = (int64_t)(k & ((1ull << lbits) - 1));
-        need = is_bpg(P, r);
+        need = is_bpg(P, r) && (int)(P.bpg[P.meta[4 * r]] & 0xFF) >= wmin;
         for (int64_t q = i; need && q < n && (keys[q] >> 1) == k; ++q)
           if (keys[q] & 1) need = false;         // pre-verified: flag already 1
       }
@@ -319,38 +300,29 @@ int coop_group(uint32_t widths) {                // lanes per line: power of two
   int w = 0;
   for (int b = 31; b >= 0; --b)
     if (widths & (1u << b)) { w = b; break; }
+  if (widths & 0x80000000u) w = 32;              // bit 31 stands for 32 words (bpg_widths)
   int g = 2;
   while (g < 2 * w) g <<= 1;
   return g;
 }
 
-// LP_BPG_WALK (A/B): "auto" (default) = the cooperative walk for request-path candidates (latency:
-// few lines) and the one-lane walk for the bulk path's first-of-run keys (throughput: a lane per line
-// does ~4x fewer instructions per line-byte than a 16-lane group); "lane" / "coop" force one.
-int walk_mode() {
-  static const int m = [] {
-    const char* e = getenv("LP_BPG_WALK");
-    const std::string v = e ? e : "auto";
-    return v == "lane" ? 1 : v == "coop" ? 2 : 0;
-  }();
-  return m;
-}
-
 template <int MODE>
 void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigned long long* dcount, int lbits,
                  const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P, uint8_t* flag,
-                 hipStream_t st) {
+                 hipStream_t st, int wmin) {
   const dim3 grid(nblocks(cap) * (MODE == 2 ? 2 : 1)), block(256);
   switch (coop_group(P.bpg_widths)) {
-    case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
-    case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
-    case 8: hipLaunchKernelGGL((k_bpg_coop<8, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
-    default: hipLaunchKernelGGL((k_bpg_coop<16, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag); break;
+    case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
+    case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
+    case 8: hipLaunchKernelGGL((k_bpg_coop<8, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
+    case 16: hipLaunchKernelGGL((k_bpg_coop<16, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
+    case 32: hipLaunchKernelGGL((k_bpg_coop<32, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
+    default: hipLaunchKernelGGL((k_bpg_coop<64, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
   }
 }
 
-// literal-free programs over every line: blockIdx.y = regex slot (block-uniform), the program is
-// staged in LDS so class / first / last / exception reads are LDS hits
+// literal-free programs of <= 8 words over every line: blockIdx.y = regex slot (block-uniform),
+// the program is staged in LDS so class / first / last / exception reads are LDS hits
 template <int W>
 __global__ __launch_bounds__(kScanLines) void k_bpg_scan(const uint8_t* __restrict__ text,
                                                          const int64_t* __restrict__ ls,
@@ -362,7 +334,7 @@ __global__ __launch_bounds__(kScanLines) void k_bpg_scan(const uint8_t* __restri
   if (!is_bpg(P, r)) return;                  // block-uniform
   const uint64_t* prog = P.bpg + P.meta[4 * r];
   if ((int)(prog[0] & 0xFF) != W) return;
-  const int nw = prog_words(prog, W);
+  const int nw = bpg_words(prog);
   const int64_t line = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool m = false;
   if (nw <= kLdsProgWords) {
@@ -373,6 +345,28 @@ __global__ __launch_bounds__(kScanLines) void k_bpg_scan(const uint8_t* __restri
     m = bpg_find_dev<W>(prog, text + ls[line], ll[line]);
   }
   if (m) {
+    const unsigned long long i = atomicAdd(count, 1ull);
+    if ((int64_t)i < cap) out[i] = ((int64_t)r << 32) | line;
+  }
+}
+
+// literal-free programs wider than 8 words over every line: a group of G lanes per line
+template <int G>
+__global__ __launch_bounds__(256) void k_bpg_scan_coop(const uint8_t* __restrict__ text,
+                                                       const int64_t* __restrict__ ls,
+                                                       const int32_t* __restrict__ ll, int64_t L,
+                                                       const int32_t* __restrict__ regs, DfaPool P,
+                                                       int64_t* out, int64_t cap, unsigned long long* count) {
+  const int r = regs[blockIdx.y];
+  if (!is_bpg(P, r)) return;                  // block-uniform
+  const uint64_t* prog = P.bpg + P.meta[4 * r];
+  if ((int)(prog[0] & 0xFF) <= BPG_LANE_MAX_W) return;
+  constexpr int NG = 64 / G;
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t line = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * NG + lane / G;
+  const bool valid = line < L;
+  const bool hit = bpg_coop_walk<G>(prog, text + (valid ? ls[line] : 0), valid ? ll[line] : 0, valid);
+  if (valid && hit && (lane & (G - 1)) == 0) {
     const unsigned long long i = atomicAdd(count, 1ull);
     if ((int64_t)i < cap) out[i] = ((int64_t)r << 32) | line;
   }
@@ -393,25 +387,21 @@ void for_widths(uint32_t mask, F&& f) {
   if (mask & (1u << 8)) f(std::integral_constant<int, 8>{});
 }
 
+constexpr uint32_t kWideMask = ~0x1FFu;        // bpg_widths bits of programs wider than 8 words
+
 }  // namespace
 
 void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text, const int64_t* ls,
                   const int32_t* ll, const DfaPool& P, uint64_t stream) {
   if (!P.bpg_widths || cap <= 0) return;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (walk_mode() != 1) {
-    launch_coop<0>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, st);
-    check_launch("k_bpg_coop<cand>");
-    return;
-  }
-  hipLaunchKernelGGL(k_bpg_cand_all, dim3(nblocks(cap)), dim3(256), 0, st, cand, cap, dcount, text, ls, ll, P);
-  check_launch("k_bpg_cand_all");
+  launch_coop<0>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, reinterpret_cast<hipStream_t>(stream), 0);
+  check_launch("k_bpg_coop<cand>");
 }
 
 bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text,
                          const int64_t* ls, const int32_t* ll, const DfaPool& P, uint64_t stream) {
-  if (!P.bpg_widths || cap <= 0 || walk_mode() == 1) return false;   // caller runs k_cand_verify
-  launch_coop<2>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, reinterpret_cast<hipStream_t>(stream));
+  if (!P.bpg_widths || cap <= 0) return false;   // caller runs k_cand_verify
+  launch_coop<2>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, reinterpret_cast<hipStream_t>(stream), 0);
   check_launch("k_bpg_coop<cand+dfa>");
   return true;
 }
@@ -420,16 +410,17 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
                     const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream) {
   if (!P.bpg_widths || n <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (walk_mode() == 2) {
-    launch_coop<1>(nullptr, keys, n, nullptr, lbits, text, ls, ll, P, flag, st);
-    check_launch("k_bpg_coop<dedupe>");
-    return;
+  // programs of <= 8 words: ONE launch for every width, a lane per key (a step's BPG candidates are
+  // few -- hundreds to thousands, a handful of waves -- and each walk is a serial chain, so
+  // per-width launches added up their slowest walks where one launch runs them side by side)
+  if (P.bpg_widths & 0x1FFu) {
+    hipLaunchKernelGGL(k_bpg_dedupe_all, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag);
+    check_launch("k_bpg_dedupe_all");
   }
-  // ONE launch for every width: a step's BPG candidates are few (hundreds to thousands, a handful of
-  // waves) and each walk is a serial chain of ~150 wave instructions per byte, so per-width launches
-  // added up their slowest walks (~100 us each) where one launch runs them side by side
-  hipLaunchKernelGGL(k_bpg_dedupe_all, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag);
-  check_launch("k_bpg_dedupe_all");
+  if (P.bpg_widths & kWideMask) {               // wider programs: a lane group per key
+    launch_coop<1>(nullptr, keys, n, nullptr, lbits, text, ls, ll, P, flag, st, BPG_LANE_MAX_W + 1);
+    check_launch("k_bpg_coop<dedupe>");
+  }
 }
 
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,
@@ -443,6 +434,16 @@ void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int
                        cap, count);
     check_launch("k_bpg_scan");
   });
+  if (P.bpg_widths & kWideMask) {
+    const int G = coop_group(P.bpg_widths);
+    const int64_t per_block = 4 * (64 / G);      // 4 waves x lines per wave
+    const dim3 g2((unsigned)std::max<int64_t>(1, (L + per_block - 1) / per_block), (unsigned)nregs);
+    switch (G) {
+      case 32: hipLaunchKernelGGL(k_bpg_scan_coop<32>, g2, dim3(256), 0, st, text, ls, ll, L, regs, P, out, cap, count); break;
+      default: hipLaunchKernelGGL(k_bpg_scan_coop<64>, g2, dim3(256), 0, st, text, ls, ll, L, regs, P, out, cap, count); break;
+    }
+    check_launch("k_bpg_scan_coop");
+  }
 }
 
 }  // namespace lp

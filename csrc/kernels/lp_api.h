@@ -38,6 +38,9 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,
                   int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
                   uint64_t stream);
+// host-verified keys appended to a verified-hit buffer at its device counter (k_append_keys)
+void append_keys_dev(int64_t* dst, int64_t cap, unsigned long long* count, const int64_t* src, int64_t n,
+                     uint64_t stream);
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
               const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
               uint64_t stream);

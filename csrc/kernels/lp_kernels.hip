@@ -505,6 +505,29 @@ void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t
   LP_CHECK(hipGetLastError());
 }
 
+// pre-verified keys from the host (the backtracker side path, bt_prepass) appended to a matcher's
+// verified-hit buffer behind the device engines' hits: one reservation per block
+__global__ __launch_bounds__(256) void k_append_keys(int64_t* __restrict__ dst, int64_t cap,
+                                                     unsigned long long* __restrict__ count,
+                                                     const int64_t* __restrict__ src, int64_t n) {
+  __shared__ unsigned long long base;
+  const int64_t b0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t nb = min((int64_t)blockDim.x, n - b0);
+  if (threadIdx.x == 0) base = atomicAdd(count, (unsigned long long)nb);
+  __syncthreads();
+  const int64_t i = b0 + threadIdx.x;
+  if (i < n && (int64_t)(base + threadIdx.x) < cap) dst[base + threadIdx.x] = src[i];
+}
+
+void append_keys_dev(int64_t* dst, int64_t cap, unsigned long long* count, const int64_t* src, int64_t n,
+                     uint64_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_append_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), dst, cap, count, src, n);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in k_append_keys");
+}
+
 void scan_dev(const uint8_t* text, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
               const int32_t* regs, int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
               uint64_t stream) {

@@ -207,8 +207,11 @@ __global__ __launch_bounds__(64 * NFA_WAVES) void k_nfa_mfma(const uint64_t* __r
   acc |= __shfl_xor(acc, 16, 64);
   acc |= __shfl_xor(acc, 32, 64);
   if (grp == 0 && valid) {
-    if (feat) {
-      feat[line] = (uint8_t)acc;
+    if (feat) {   // context features: bit = context regex id (0..3); one group per launch
+      uint32_t f = 0;
+      for (int q = 0; q < nreg; ++q)
+        if ((acc >> q) & 1) f |= 1u << (tab[G_REGID + q] & 7);
+      feat[line] |= (uint8_t)f;
     } else {
       for (int q = 0; q < nreg; ++q)
         if ((acc >> q) & 1) {
@@ -272,7 +275,10 @@ int64_t nfa_host(const uint64_t* groups, const int32_t* group_list, int ngroups,
         prevk = nk == 2 ? 1 : 2;
       }
       if (feat) {
-        feat[line] = (uint8_t)acc;
+        uint32_t f = 0;
+        for (int q = 0; q < nreg; ++q)
+          if ((acc >> q) & 1) f |= 1u << (tab[G_REGID + q] & 7);
+        feat[line] |= (uint8_t)f;
       } else {
         for (int q = 0; q < nreg; ++q)
           if ((acc >> q) & 1) {

@@ -1,91 +1,207 @@
-// Java-regex -> literal factors + Glushkov NFA + byte DFA.  See jregex.h for the design.
+// Java-regex -> literal factors + Glushkov NFAs (code-point and byte level) + byte DFA +
+// backtracking VM.  See jregex.h for the design.
 #include "jregex.h"
 
 #include <algorithm>
 #include <cctype>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <set>
 #include <unordered_map>
 
+#include "unicode_tables.inc"
+
 namespace lp {
+
+// ------------------------------------------------------------------------------------------
+// code-point sets
+void CpSet::add_range(uint32_t lo, uint32_t hi) {
+  if (hi > MAX) hi = MAX;
+  if (lo > hi) return;
+  // first range that ends at or after lo - 1 (touching ranges merge)
+  size_t i = std::lower_bound(r.begin(), r.end(), lo,
+                              [](const std::pair<uint32_t, uint32_t>& p, uint32_t v) {
+                                return (uint64_t)p.second + 1 < v;
+                              }) - r.begin();
+  size_t j = i;
+  uint32_t nlo = lo, nhi = hi;
+  while (j < r.size() && (uint64_t)r[j].first <= (uint64_t)hi + 1) {
+    nlo = std::min(nlo, r[j].first);
+    nhi = std::max(nhi, r[j].second);
+    ++j;
+  }
+  r.erase(r.begin() + i, r.begin() + j);
+  r.insert(r.begin() + i, {nlo, nhi});
+}
+
+void CpSet::unite(const CpSet& o) {
+  if (r.empty()) { r = o.r; return; }
+  for (auto& p : o.r) add_range(p.first, p.second);
+}
+
+void CpSet::intersect(const CpSet& o) {
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  size_t i = 0, j = 0;
+  while (i < r.size() && j < o.r.size()) {
+    const uint32_t lo = std::max(r[i].first, o.r[j].first), hi = std::min(r[i].second, o.r[j].second);
+    if (lo <= hi) out.push_back({lo, hi});
+    if (r[i].second < o.r[j].second) ++i; else ++j;
+  }
+  r.swap(out);
+}
+
+void CpSet::negate() {
+  std::vector<std::pair<uint32_t, uint32_t>> out;
+  uint32_t next = 0;
+  for (auto& p : r) {
+    if (p.first > next) out.push_back({next, p.first - 1});
+    next = p.second + 1;
+  }
+  if (next <= MAX) out.push_back({next, MAX});
+  r.swap(out);
+}
+
+bool CpSet::contains(uint32_t c) const { return covers(c, c); }
+
+bool CpSet::covers(uint32_t lo, uint32_t hi) const {
+  auto it = std::upper_bound(r.begin(), r.end(), lo,
+                             [](uint32_t v, const std::pair<uint32_t, uint32_t>& p) { return v < p.first; });
+  if (it == r.begin()) return false;
+  --it;
+  return it->first <= lo && hi <= it->second;
+}
+
+bool CpSet::touches(uint32_t lo, uint32_t hi) const {
+  auto it = std::lower_bound(r.begin(), r.end(), lo,
+                             [](const std::pair<uint32_t, uint32_t>& p, uint32_t v) { return p.second < v; });
+  return it != r.end() && it->first <= hi;
+}
+
+uint64_t CpSet::count() const {
+  uint64_t n = 0;
+  for (auto& p : r) n += (uint64_t)p.second - p.first + 1;
+  return n;
+}
+
+// ------------------------------------------------------------------------------------------
+// Unicode tables (generated: tools/gen_unicode_tables.py)
 namespace {
 
-// ------------------------------------------------------------------------------------------
-// code-point sets (ASCII bitmap + non-ASCII part: NONE / finite / ALL / PARTIAL)
-struct CodeSet {
-  uint64_t a[2] = {0, 0};          // ASCII 0..127
-  enum Mode { FIN, ALL, PARTIAL } mode = FIN;
-  std::set<uint32_t> cps;          // finite non-ASCII code points (mode FIN)
+const uni::SetRef* uni_find(const std::string& key) {
+  const uni::SetRef* b = uni::kSets;
+  const uni::SetRef* e = uni::kSets + sizeof(uni::kSets) / sizeof(uni::kSets[0]);
+  const uni::SetRef* it = std::lower_bound(b, e, key, [](const uni::SetRef& s, const std::string& k) {
+    return std::strcmp(s.key, k.c_str()) < 0;
+  });
+  return (it != e && key == it->key) ? it : nullptr;
+}
 
-  void add(uint32_t cp) {
-    if (cp < 128) { a[cp >> 6] |= 1ull << (cp & 63); return; }
-    if (mode == FIN) { cps.insert(cp); if (cps.size() > 256) { mode = PARTIAL; cps.clear(); } }
-  }
-  void add_range(uint32_t lo, uint32_t hi) {
-    for (uint32_t c = lo; c <= hi && c < 128; ++c) add(c);
-    if (hi >= 128) {
-      uint32_t l2 = std::max<uint32_t>(lo, 128);
-      if (l2 <= 128 && hi >= 0x10FFFF) { mode = ALL; cps.clear(); return; }
-      if (mode == ALL) return;
-      if (hi - l2 > 256) { mode = PARTIAL; cps.clear(); return; }
-      for (uint32_t c = l2; c <= hi; ++c) add(c);
+bool uni_get(const std::string& key, CpSet& out) {
+  const uni::SetRef* s = uni_find(key);
+  if (!s) return false;
+  out.r.clear();
+  out.r.reserve(s->n);
+  for (uint32_t k = 0; k < s->n; ++k) out.r.push_back({uni::kRanges[2 * (s->off + k)], uni::kRanges[2 * (s->off + k) + 1]});
+  return true;
+}
+
+struct CaseMaps {
+  std::unordered_map<uint32_t, uint32_t> up, lo;
+  std::vector<std::pair<uint32_t, uint32_t>> pairs;      // (c, up(c)) and (c, lo(c))
+  std::unordered_map<uint32_t, std::vector<uint32_t>> adj;  // case graph (both directions)
+  CaseMaps() {
+    for (size_t i = 0; i < sizeof(uni::kUpper) / sizeof(uint32_t); i += 2) {
+      up[uni::kUpper[i]] = uni::kUpper[i + 1];
+      pairs.push_back({uni::kUpper[i], uni::kUpper[i + 1]});
     }
-  }
-  bool has_ascii(int c) const { return (a[c >> 6] >> (c & 63)) & 1; }
-  void unite(const CodeSet& o) {
-    a[0] |= o.a[0]; a[1] |= o.a[1];
-    if (mode == ALL || o.mode == ALL) { mode = ALL; cps.clear(); return; }
-    if (mode == PARTIAL || o.mode == PARTIAL) { mode = PARTIAL; cps.clear(); return; }
-    for (auto c : o.cps) add(c);
-  }
-  void intersect(const CodeSet& o) {
-    a[0] &= o.a[0]; a[1] &= o.a[1];
-    if (o.mode == ALL) return;
-    if (mode == ALL) { mode = o.mode; cps = o.cps; return; }
-    if (mode == FIN && o.mode == FIN) {
-      std::set<uint32_t> r;
-      for (auto c : cps) if (o.cps.count(c)) r.insert(c);
-      cps.swap(r);
-      return;
+    for (size_t i = 0; i < sizeof(uni::kLower) / sizeof(uint32_t); i += 2) {
+      lo[uni::kLower[i]] = uni::kLower[i + 1];
+      pairs.push_back({uni::kLower[i], uni::kLower[i + 1]});
     }
-    mode = PARTIAL; cps.clear();
+    for (auto& p : pairs) { adj[p.first].push_back(p.second); adj[p.second].push_back(p.first); }
   }
-  void negate() {
-    a[0] = ~a[0]; a[1] = ~a[1];
-    if (mode == ALL) { mode = FIN; cps.clear(); }
-    else if (mode == FIN && cps.empty()) mode = ALL;
-    else { mode = PARTIAL; cps.clear(); }
-  }
+  uint32_t U(uint32_t c) const { auto it = up.find(c); return it == up.end() ? c : it->second; }
+  uint32_t L(uint32_t c) const { auto it = lo.find(c); return it == lo.end() ? c : it->second; }
 };
 
-// ------------------------------------------------------------------------------------------
-// AST
-// N_GROUP .. N_MLANCHOR only exist in backtracking mode (Parser(..., bt = true)); the automaton
-// path rejects their constructs as Unsupported before building them.
-enum NT { N_EMPTY, N_SET, N_CAT, N_ALT, N_REP, N_ASSERT, N_GROUP, N_BACKREF, N_LOOK, N_ATOMIC, N_MLANCHOR };
-struct Node {
-  NT t = N_EMPTY;
-  ByteSet set;
-  std::vector<int> kids;
-  int lo = 0, hi = 0;      // REP (hi = -1: unbounded)
-  uint16_t cond = CTX_ALL; // ASSERT
-  int idx = 0;             // GROUP / BACKREF: group number; MLANCHOR: 0 '^', 1 '$'
-  bool behind = false;     // LOOK: lookbehind
-  bool neg = false;        // LOOK: negative
-  bool ci = false;         // BACKREF: case-insensitive compare
-  bool lazy = false;       // REP: reluctant (priority order matters inside atomic groups)
-};
+const CaseMaps& case_maps() {
+  static const CaseMaps m;
+  return m;
+}
+
+const CpSet& unicode_word() {
+  static const CpSet w = [] { CpSet s; uni_get("u:word", s); return s; }();
+  return w;
+}
+
+}  // namespace
+
+CpSet unicode_set(const std::string& key) {
+  CpSet s;
+  uni_get(key, s);
+  return s;
+}
+
+namespace {
 
 bool is_word_byte(int c) {
   return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '_';
 }
 
-uint16_t mask_where(bool (*f)(int, int)) {
-  uint16_t m = 0;
-  for (int p = 0; p < 3; ++p)
-    for (int n = 0; n < 5; ++n)
-      if (f(p, n)) m |= (uint16_t)(1u << ctx_index(p, n));
+bool is_line_term(uint32_t c) { return c == '\n' || c == '\r' || c == 0x85 || c == 0x2028 || c == 0x2029; }
+
+void utf8(uint32_t cp, std::string& out) {
+  if (cp < 0x80) { out.push_back((char)cp); return; }
+  if (cp < 0x800) { out.push_back((char)(0xC0 | (cp >> 6))); out.push_back((char)(0x80 | (cp & 0x3F))); return; }
+  if (cp < 0x10000) {
+    out.push_back((char)(0xE0 | (cp >> 12))); out.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+    out.push_back((char)(0x80 | (cp & 0x3F)));
+    return;
+  }
+  out.push_back((char)(0xF0 | (cp >> 18))); out.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+  out.push_back((char)(0x80 | ((cp >> 6) & 0x3F))); out.push_back((char)(0x80 | (cp & 0x3F)));
+}
+
+// decode the code point starting at s[i] (lenient: a truncated / invalid sequence still yields a
+// value); *len = its byte length
+uint32_t decode_at(const uint8_t* s, int64_t n, int64_t i, int* len) {
+  const uint8_t c = s[i];
+  if (c < 0x80 || c < 0xC0) { *len = 1; return c; }
+  const int k = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+  uint32_t cp = c & (0x7F >> k);
+  int m = 1;
+  for (; m < k && i + m < n; ++m) cp = (cp << 6) | (s[i + m] & 0x3F);
+  *len = m;
+  return cp;
+}
+
+// ------------------------------------------------------------------------------------------
+// AST
+// N_CSET: code-point set (parser output); N_SET: byte set (UTF-8-lowered AST only).
+// N_GROUP .. N_MLANCHOR only exist in backtracking mode (Parser(..., bt = true)); the automaton
+// path rejects their constructs as Unsupported before building them.
+enum NT { N_EMPTY, N_SET, N_CSET, N_CAT, N_ALT, N_REP, N_ASSERT, N_GROUP, N_BACKREF, N_LOOK, N_ATOMIC, N_MLANCHOR };
+struct Node {
+  NT t = N_EMPTY;
+  ByteSet set;
+  CpSet cs;
+  std::vector<int> kids;
+  int lo = 0, hi = 0;      // REP (hi = -1: unbounded)
+  uint32_t cond = CTX_ALL; // ASSERT
+  bool uword = false;      // ASSERT: \b / \B with Unicode WORD semantics
+  int idx = 0;             // GROUP / BACKREF: group number; MLANCHOR: 0 '^', 1 '$'
+  bool behind = false;     // LOOK: lookbehind
+  bool neg = false;        // LOOK: negative; MLANCHOR: UNIX_LINES
+  bool ci = false;         // BACKREF: case-insensitive compare
+  bool lazy = false;       // REP: reluctant (priority order matters inside atomic groups)
+};
+
+uint32_t mask_where(bool (*f)(int, int)) {
+  uint32_t m = 0;
+  for (int p = 0; p < 4; ++p)
+    for (int n = 0; n < 6; ++n)
+      if (f(p, n)) m |= 1u << ctx_index(p, n);
   return m;
 }
 bool f_bos(int p, int n) { return p == P_BOS && n != N_C; }
@@ -93,8 +209,27 @@ bool f_eol(int, int n) { return n == N_EOS || n == N_FT; }
 bool f_eos(int, int n) { return n == N_EOS; }
 bool f_wb(int p, int n) { return n != N_C && (p == P_W) != (n == N_W); }
 bool f_nwb(int p, int n) { return n != N_C && (p == P_W) == (n == N_W); }
+// MULTILINE '^' (Pattern.Caret): after BOS or a line terminator, never at the end of input
+bool f_ml_caret(int p, int n) { return (p == P_BOS || p == P_T) && n != N_EOS && n != N_C; }
+// MULTILINE '$' (Pattern.Dollar): before any line terminator or at the end
+bool f_ml_dollar(int, int n) { return n == N_EOS || n == N_FT || n == N_T; }
+// UNIX_LINES MULTILINE '^' (UnixCaret): lines hold no '\n', so only at BOS (not at the end)
+bool f_ux_caret(int p, int n) { return p == P_BOS && n != N_EOS && n != N_C; }
 
-struct Flags { bool ci = false, dotall = false, comments = false, multiline = false, unixl = false; };
+struct Flags {
+  bool ci = false, dotall = false, comments = false, multiline = false, unixl = false;
+  bool ucase = false;    // UNICODE_CASE
+  bool uclass = false;   // UNICODE_CHARACTER_CLASS
+};
+
+std::string upper_ascii(std::string s) {
+  for (auto& c : s) c = (char)std::toupper((unsigned char)c);
+  return s;
+}
+std::string lower_ascii(std::string s) {
+  for (auto& c : s) c = (char)std::tolower((unsigned char)c);
+  return s;
+}
 
 class Parser {
  public:
@@ -112,6 +247,8 @@ class Parser {
     return r;
   }
   bool uses_wordb = false;
+  bool uses_uword = false, uses_aword = false;   // \b with Unicode / ASCII word semantics
+  bool needs_cp = false;                         // MULTILINE ^ / $ (code-point contexts)
 
  private:
   const std::string& s_;
@@ -121,8 +258,8 @@ class Parser {
   std::map<std::string, int> names_;
 
   int add(Node n) { nodes.push_back(std::move(n)); return (int)nodes.size() - 1; }
-  int mk_set(const ByteSet& b) { Node n; n.t = N_SET; n.set = b; return add(n); }
-  int mk_assert(uint16_t c) { Node n; n.t = N_ASSERT; n.cond = c; return add(n); }
+  int mk_cset(const CpSet& c) { Node n; n.t = N_CSET; n.cs = c; return add(n); }
+  int mk_assert(uint32_t c) { Node n; n.t = N_ASSERT; n.cond = c; return add(n); }
   int mk_cat(std::vector<int> k) {
     if (k.empty()) { Node n; n.t = N_EMPTY; return add(n); }
     if (k.size() == 1) return k[0];
@@ -156,53 +293,42 @@ class Parser {
     return cp;
   }
 
-  static void utf8(uint32_t cp, std::vector<int>& out) {
-    if (cp < 0x80) { out.push_back(cp); return; }
-    if (cp < 0x800) { out.push_back(0xC0 | (cp >> 6)); out.push_back(0x80 | (cp & 0x3F)); return; }
-    if (cp < 0x10000) { out.push_back(0xE0 | (cp >> 12)); out.push_back(0x80 | ((cp >> 6) & 0x3F)); out.push_back(0x80 | (cp & 0x3F)); return; }
-    out.push_back(0xF0 | (cp >> 18)); out.push_back(0x80 | ((cp >> 12) & 0x3F));
-    out.push_back(0x80 | ((cp >> 6) & 0x3F)); out.push_back(0x80 | (cp & 0x3F));
-  }
-
-  void add_ci(CodeSet& cs, uint32_t cp) {
+  // ---- case folding (Java: CASE_INSENSITIVE folds ASCII letters only; with UNICODE_CASE it uses
+  // Character.toUpperCase / toLowerCase; predefined classes and properties are not folded)
+  void add_ci(CpSet& cs, uint32_t cp) {
     cs.add(cp);
-    if (f_.ci && cp < 128) {
+    if (!f_.ci) return;
+    if (!f_.ucase) {
       if (cp >= 'a' && cp <= 'z') cs.add(cp - 32);
       else if (cp >= 'A' && cp <= 'Z') cs.add(cp + 32);
+      return;
+    }
+    // SingleU: ch matches when toLowerCase(toUpperCase(ch)) equals that of cp; walk the case graph
+    const CaseMaps& M = case_maps();
+    const uint32_t key = M.L(M.U(cp));
+    std::vector<uint32_t> todo = {cp};
+    std::set<uint32_t> seen = {cp};
+    while (!todo.empty()) {
+      const uint32_t x = todo.back();
+      todo.pop_back();
+      if (M.L(M.U(x)) == key) cs.add(x);
+      auto it = M.adj.find(x);
+      if (it == M.adj.end()) continue;
+      for (uint32_t y : it->second)
+        if (seen.insert(y).second) todo.push_back(y);
     }
   }
-  void add_range_ci(CodeSet& cs, uint32_t lo, uint32_t hi) {
+  void add_range_ci(CpSet& cs, uint32_t lo, uint32_t hi) {
     cs.add_range(lo, hi);
-    if (f_.ci) for (uint32_t c = lo; c <= hi && c < 128; ++c) add_ci(cs, c);
-  }
-
-  // Lower a code-point set to an AST node over bytes.
-  int set_node(const CodeSet& cs) {
-    ByteSet b;
-    for (int c = 0; c < 128; ++c) if (cs.has_ascii(c)) b.set(c);
-    if (cs.mode == CodeSet::PARTIAL)
-      throw Unsupported("character class with a partial non-ASCII range");
-    if (cs.mode == CodeSet::ALL) {
-      // any non-ASCII code point = lead byte followed by continuation bytes (valid UTF-8 input)
-      b.set_range(0xC0, 0xFF);
-      ByteSet cont; cont.set_range(0x80, 0xBF);
-      int lead = mk_set(b);
-      // at most 3 continuation bytes in valid UTF-8; the bound keeps lookbehind lengths finite
-      int tail = mk_rep(mk_set(cont), 0, bt_ ? 3 : -1);
-      if (bt_) {   // a code point is indivisible: backtracking must not give its bytes back
-        Node n; n.t = N_ATOMIC; n.kids = {tail}; tail = add(n);
-      }
-      return mk_cat({lead, tail});
+    if (!f_.ci) return;
+    if (!f_.ucase) {   // CIRange: an ASCII ch matches when its ASCII upper / lower case is in range
+      for (uint32_t c = 'a'; c <= 'z'; ++c) if (c >= lo && c <= hi) cs.add(c - 32);
+      for (uint32_t c = 'A'; c <= 'Z'; ++c) if (c >= lo && c <= hi) cs.add(c + 32);
+      return;
     }
-    std::vector<int> alts;
-    if (!b.empty() || cs.cps.empty()) alts.push_back(mk_set(b));
-    for (auto cp : cs.cps) {
-      std::vector<int> bytes; utf8(cp, bytes);
-      std::vector<int> seq;
-      for (int x : bytes) { ByteSet bb; bb.set(x); seq.push_back(mk_set(bb)); }
-      alts.push_back(mk_cat(seq));
-    }
-    return mk_alt(alts);
+    // CIRangeU: ch matches when ch, toUpperCase(ch) or toLowerCase(ch) is in range
+    for (auto& p : case_maps().pairs)
+      if (p.second >= lo && p.second <= hi) cs.add(p.first);
   }
 
   int hexval(int c) {
@@ -237,7 +363,7 @@ class Parser {
         ++i_;
         if (peek() == '{') {
           ++i_; uint32_t v = 0; int nd = 0;
-          while (!eof() && peek() != '}') { v = v * 16 + hexval(peek()); ++i_; ++nd; }
+          while (!eof() && peek() != '}') { v = v * 16 + hexval(peek()); ++i_; ++nd; if (v > CpSet::MAX) throw SyntaxError("Hexadecimal codepoint is too big"); }
           if (eof() || nd == 0) throw SyntaxError("Unclosed hexadecimal escape sequence");
           ++i_; cp = v; return true;
         }
@@ -269,14 +395,69 @@ class Parser {
     return false;
   }
 
-  bool class_escape(CodeSet& cs) {  // predefined classes; i_ at the letter
+  // ---- \p{..} resolution (Pattern.family + CharPredicates, Java 21)
+  bool for_property(const std::string& name, CpSet& out) {      // CharPredicates.forProperty
+    if (f_.ci && uni_get("gci:" + name, out)) return true;
+    return uni_get("gc:" + name, out);
+  }
+  bool for_unicode_property(const std::string& name, CpSet& out) {   // forUnicodeProperty (+ POSIX)
+    const std::string u = upper_ascii(name);
+    if (f_.ci && uni_get("upi:" + u, out)) return true;
+    return uni_get("up:" + u, out);
+  }
+  bool for_posix_name(const std::string& name, CpSet& out) {
+    static const std::set<std::string> posix = {"ALPHA", "LOWER", "UPPER", "SPACE", "PUNCT", "XDIGIT",
+                                                "ALNUM", "CNTRL", "DIGIT", "BLANK", "GRAPH", "PRINT"};
+    const std::string u = upper_ascii(name);
+    if (!posix.count(u)) return false;
+    return for_unicode_property(u, out);
+  }
+  CpSet script(const std::string& name) {
+    CpSet s;
+    if (!uni_get("sc:" + upper_ascii(name), s)) throw SyntaxError("Unknown character script name {" + name + "}");
+    return s;
+  }
+  CpSet block(const std::string& name) {
+    CpSet s;
+    if (!uni_get("blk:" + upper_ascii(name), s)) throw SyntaxError("Unknown character block name {" + name + "}");
+    return s;
+  }
+  CpSet property(const std::string& name) {
+    CpSet s;
+    const size_t eq = name.find('=');
+    if (eq != std::string::npos) {
+      const std::string key = lower_ascii(name.substr(0, eq)), value = name.substr(eq + 1);
+      if (key == "sc" || key == "script") return script(value);
+      if (key == "blk" || key == "block") return block(value);
+      if ((key == "gc" || key == "general_category") && for_property(value, s)) return s;
+      throw SyntaxError("Unknown Unicode property {name=<" + key + ">, value=<" + value + ">}");
+    }
+    if (name.rfind("In", 0) == 0) return block(name.substr(2));
+    if (name.rfind("Is", 0) == 0) {
+      const std::string sh = name.substr(2);
+      if (for_unicode_property(sh, s) || for_property(sh, s)) return s;
+      return script(sh);
+    }
+    if (f_.uclass && for_posix_name(name, s)) return s;
+    if (for_property(name, s)) return s;
+    throw SyntaxError("Unknown character property name {" + name + "}");
+  }
+
+  bool class_escape(CpSet& cs) {  // predefined classes; i_ at the letter
     int c = peek();
-    CodeSet t;
+    CpSet t;
     bool neg = false;
     switch (c) {
-      case 'd': case 'D': t.add_range('0', '9'); neg = c == 'D'; break;
-      case 's': case 'S': for (uint32_t x : {' ', '\t', '\n', '\x0b', '\f', '\r'}) t.add(x); neg = c == 'S'; break;
-      case 'w': case 'W': t.add_range('a', 'z'); t.add_range('A', 'Z'); t.add_range('0', '9'); t.add('_'); neg = c == 'W'; break;
+      case 'd': case 'D':
+        if (f_.uclass) uni_get("u:digit", t); else t.add_range('0', '9');
+        neg = c == 'D'; break;
+      case 's': case 'S':
+        if (f_.uclass) uni_get("u:space", t); else { t.add_range('\t', '\r'); t.add(' '); }
+        neg = c == 'S'; break;
+      case 'w': case 'W':
+        if (f_.uclass) t = unicode_word();
+        else { t.add_range('a', 'z'); t.add_range('A', 'Z'); t.add_range('0', '9'); t.add('_'); }
+        neg = c == 'W'; break;
       case 'h': case 'H':
         for (uint32_t x : {0x20u, 0x09u, 0xA0u, 0x1680u, 0x180Eu, 0x202Fu, 0x205Fu, 0x3000u}) t.add(x);
         t.add_range(0x2000, 0x200A); neg = c == 'H'; break;
@@ -297,22 +478,7 @@ class Parser {
           name.push_back(s_[i_++]);
         }
         if (!name.empty() && name[0] == '^') { neg = !neg; name = name.substr(1); }
-        if (name.rfind("Is", 0) == 0) name = name.substr(2);
-        auto R = [&](int lo, int hi) { t.add_range(lo, hi); };
-        if (name == "Lower" || name == "javaLowerCase") { R('a', 'z'); if (f_.ci) R('A', 'Z'); }
-        else if (name == "Upper" || name == "javaUpperCase") { R('A', 'Z'); if (f_.ci) R('a', 'z'); }
-        else if (name == "ASCII") R(0, 127);
-        else if (name == "Alpha") { R('a', 'z'); R('A', 'Z'); }
-        else if (name == "Digit") R('0', '9');
-        else if (name == "Alnum") { R('a', 'z'); R('A', 'Z'); R('0', '9'); }
-        else if (name == "Punct") { R('!', '/'); R(':', '@'); R('[', '`'); R('{', '~'); }
-        else if (name == "Graph") R('!', '~');
-        else if (name == "Print") R(' ', '~');
-        else if (name == "Blank") { t.add(' '); t.add('\t'); }
-        else if (name == "Cntrl") { R(0, 0x1F); t.add(0x7F); }
-        else if (name == "XDigit") { R('0', '9'); R('a', 'f'); R('A', 'F'); }
-        else if (name == "Space" || name == "javaWhitespace") { for (uint32_t x : {' ', '\t', '\n', '\x0b', '\f', '\r'}) t.add(x); }
-        else throw Unsupported("unicode property \\p{" + name + "}");
+        t = property(name);
         if (neg) t.negate();
         cs.unite(t);
         return true;
@@ -325,24 +491,24 @@ class Parser {
     return true;
   }
 
-  CodeSet parse_class() {  // at '['
+  CpSet parse_class() {  // at '['
     ++i_;
     bool neg = false;
     if (peek() == '^') { neg = true; ++i_; }
-    CodeSet cur;
+    CpSet cur;
     bool have_acc = false;
-    CodeSet acc;
+    CpSet acc;
     bool first = true;
     for (;;) {
       if (eof()) throw SyntaxError("Unclosed character class");
       int c = peek();
       if (c == ']' && !first) { ++i_; break; }
       first = false;
-      if (c == '[') { CodeSet sub = parse_class(); cur.unite(sub); continue; }
+      if (c == '[') { CpSet sub = parse_class(); cur.unite(sub); continue; }
       if (c == '&' && i_ + 1 < s_.size() && s_[i_ + 1] == '&') {
         i_ += 2;
         if (!have_acc) { acc = cur; have_acc = true; } else acc.intersect(cur);
-        cur = CodeSet();
+        cur = CpSet();
         continue;
       }
       uint32_t lo;
@@ -378,7 +544,7 @@ class Parser {
         add_ci(cur, lo);
       }
     }
-    CodeSet res = cur;
+    CpSet res = cur;
     if (have_acc) { acc.intersect(cur); res = acc; }
     if (neg) res.negate();
     return res;
@@ -459,9 +625,9 @@ class Parser {
         case 'x': fl.comments = v; break;
         case 'm': fl.multiline = v; break;
         case 'd': fl.unixl = v; break;
-        case 'u': break;   // UNICODE_CASE: ASCII behaviour identical; non-ASCII CI literals unsupported below
-        case 'U': throw Unsupported("UNICODE_CHARACTER_CLASS");
-        case 'c': throw Unsupported("CANON_EQ");
+        case 'u': fl.ucase = v; break;
+        case 'U': fl.uclass = v; fl.ucase = v; break;   // UNICODE_CHARACTER_CLASS implies UNICODE_CASE
+        case 'c': break;                                 // CANON_EQ: no effect on composed input
         default: throw SyntaxError("Unknown inline modifier");
       }
     }
@@ -535,33 +701,37 @@ class Parser {
       }
       return r;
     }
-    if (c == '[') { CodeSet cs = parse_class(); return set_node(cs); }
+    if (c == '[') { CpSet cs = parse_class(); return mk_cset(cs); }
     if (c == '.') {
       ++i_;
-      CodeSet cs;
-      cs.add_range(0, 127);
-      cs.mode = CodeSet::ALL;
+      CpSet cs;
+      cs.add_range(0, CpSet::MAX);
       if (!f_.dotall) {
-        // Java: '.' excludes line terminators (\n \r; U+0085/U+2028/U+2029 are treated as ordinary
-        // non-ASCII here — documented divergence). UNIX_LINES: only \n.
-        cs.a[0] &= ~(1ull << '\n');
-        if (!f_.unixl) cs.a[0] &= ~(1ull << '\r');
+        CpSet t;   // Java '.': every line terminator excluded (UNIX_LINES: only '\n')
+        if (f_.unixl) t.add('\n');
+        else for (uint32_t x : {0x0Au, 0x0Du, 0x85u, 0x2028u, 0x2029u}) t.add(x);
+        t.negate();
+        cs.intersect(t);
       }
-      return set_node(cs);
+      return mk_cset(cs);
     }
     if (c == '^') {
       ++i_;
       if (f_.multiline) {
-        if (!bt_) throw Unsupported("MULTILINE ^");
-        Node n; n.t = N_MLANCHOR; n.idx = 0; n.neg = f_.unixl; return add(n);
+        if (bt_) { Node n; n.t = N_MLANCHOR; n.idx = 0; n.neg = f_.unixl; return add(n); }
+        if (f_.unixl) return mk_assert(mask_where(f_ux_caret));
+        needs_cp = true;
+        return mk_assert(mask_where(f_ml_caret));
       }
       return mk_assert(mask_where(f_bos));
     }
     if (c == '$') {
       ++i_;
       if (f_.multiline) {
-        if (!bt_) throw Unsupported("MULTILINE $");
-        Node n; n.t = N_MLANCHOR; n.idx = 1; n.neg = f_.unixl; return add(n);
+        if (bt_) { Node n; n.t = N_MLANCHOR; n.idx = 1; n.neg = f_.unixl; return add(n); }
+        if (f_.unixl) return mk_assert(mask_where(f_eos));
+        needs_cp = true;
+        return mk_assert(mask_where(f_ml_dollar));
       }
       return mk_assert(f_.unixl ? mask_where(f_eos) : mask_where(f_eol));
     }
@@ -572,8 +742,14 @@ class Parser {
       if (eof()) throw SyntaxError("Unexpected internal error");
       int e = peek();
       switch (e) {
-        case 'b': ++i_; uses_wordb = true; return mk_assert(mask_where(f_wb));
-        case 'B': ++i_; uses_wordb = true; return mk_assert(mask_where(f_nwb));
+        case 'b': case 'B': {
+          ++i_;
+          uses_wordb = true;
+          (f_.uclass ? uses_uword : uses_aword) = true;
+          const int a = mk_assert(mask_where(e == 'b' ? f_wb : f_nwb));
+          nodes[a].uword = f_.uclass;
+          return a;
+        }
         case 'A': case 'G': ++i_; return mk_assert(mask_where(f_bos));
         case 'z': ++i_; return mk_assert(mask_where(f_eos));
         case 'Z': ++i_; return mk_assert(f_.unixl ? mask_where(f_eos) : mask_where(f_eol));
@@ -588,13 +764,25 @@ class Parser {
         }
         case 'R': {
           ++i_;
-          // (?:\r\n|[\n\x0B\f\r\x85  ])
-          ByteSet cr; cr.set('\r'); ByteSet nl; nl.set('\n');
-          int crlf = mk_cat({mk_set(cr), mk_set(nl)});
-          CodeSet v; for (uint32_t x : {0x0Au, 0x0Bu, 0x0Cu, 0x0Du, 0x85u, 0x2028u, 0x2029u}) v.add(x);
-          return mk_alt({crlf, set_node(v)});
+          // (?:\r\n|[\n\x0B\f\r\x85  ]); lines never hold '\n', so no atomicity issue
+          CpSet cr; cr.add('\r');
+          CpSet nl; nl.add('\n');
+          int crlf = mk_cat({mk_cset(cr), mk_cset(nl)});
+          CpSet v; for (uint32_t x : {0x0Au, 0x0Bu, 0x0Cu, 0x0Du, 0x85u, 0x2028u, 0x2029u}) v.add(x);
+          return mk_alt({crlf, mk_cset(v)});
         }
-        case 'X': throw Unsupported("\\X grapheme cluster");
+        case 'X': {
+          ++i_;
+          if (!bt_) throw Unsupported("\\X grapheme cluster");
+          // approximation: (?>\r\n|\P{M}\p{M}*) (legacy grapheme cluster)
+          CpSet m; uni_get("gc:M", m);
+          CpSet nm = m; nm.negate();
+          CpSet cr; cr.add('\r');
+          CpSet nl; nl.add('\n');
+          const int g = mk_alt({mk_cat({mk_cset(cr), mk_cset(nl)}), mk_cat({mk_cset(nm), mk_rep(mk_cset(m), 0, -1)})});
+          Node n; n.t = N_ATOMIC; n.kids = {g};
+          return add(n);
+        }
         case 'N': throw Unsupported("\\N{name}");
         case 'k': {
           if (!bt_) throw Unsupported("named backreference");
@@ -623,8 +811,8 @@ class Parser {
         }
         Node n; n.t = N_BACKREF; n.idx = ref; n.ci = f_.ci; return add(n);
       }
-      CodeSet cs;
-      if (class_escape(cs)) return set_node(cs);
+      CpSet cs;
+      if (class_escape(cs)) return mk_cset(cs);
       uint32_t cp;
       if (!char_escape(cp)) throw SyntaxError("Illegal/unsupported escape sequence");
       return literal_node(cp);
@@ -634,16 +822,114 @@ class Parser {
   }
 
   int literal_node(uint32_t cp) {
-    if (cp < 128) {
-      CodeSet cs; add_ci(cs, cp);
-      ByteSet b;
-      for (int x = 0; x < 128; ++x) if (cs.has_ascii(x)) b.set(x);
-      return mk_set(b);
+    CpSet cs;
+    add_ci(cs, cp);
+    return mk_cset(cs);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// UTF-8 lowering: code-point sets -> byte AST (for the byte DFA, the MFMA NFA and the backtracker)
+//
+// The non-ASCII part of a set is built as a trie over UTF-8 bytes: a byte whose whole code-point
+// window (valid code points only: overlongs / beyond U+10FFFF are never in the input) lies in the
+// set is "full" and is followed by free continuation bytes; a partial byte recurses into its
+// continuation byte. Bytes with identical subtrees share one alternative. Automata follow a full
+// byte by ONE self-looping continuation position (valid UTF-8 fixes the count, and no position can
+// start on a continuation byte), so '.' / [^x] cost a handful of positions; the backtracker takes
+// the exact continuation count.
+class Lowerer {
+ public:
+  Lowerer(const std::vector<Node>& in, bool bt) : in_(in), bt_(bt) {}
+  std::vector<Node> out;
+  int lower(int id) {
+    const Node& n = in_[id];
+    if (n.t == N_CSET) return lower_cset(n.cs);
+    Node c = n;
+    c.cs = CpSet();
+    for (auto& k : c.kids) k = lower(k);
+    return add(std::move(c));
+  }
+
+ private:
+  const std::vector<Node>& in_;
+  bool bt_;
+  struct Win { int b; uint32_t lo, hi, minv; int rem; };
+
+  int add(Node n) { out.push_back(std::move(n)); return (int)out.size() - 1; }
+  int mk_set(const ByteSet& b) { Node n; n.t = N_SET; n.set = b; return add(n); }
+  int mk_cat(std::vector<int> k) { if (k.size() == 1) return k[0]; Node n; n.t = N_CAT; n.kids = std::move(k); return add(n); }
+  int mk_alt(std::vector<int> k) { if (k.size() == 1) return k[0]; Node n; n.t = N_ALT; n.kids = std::move(k); return add(n); }
+  int tail(int rem, bool any_len) {        // rem free continuation bytes
+    ByteSet cont; cont.set_range(0x80, 0xBF);
+    Node n; n.t = N_REP; n.kids = {mk_set(cont)};
+    if (any_len) { n.lo = 1; n.hi = -1; } else { n.lo = rem; n.hi = rem; }
+    return add(n);
+  }
+  static std::string sig_of(const ByteSet& b) {
+    char buf[80];
+    snprintf(buf, sizeof buf, "%016llx%016llx%016llx%016llx", (unsigned long long)b.w[0], (unsigned long long)b.w[1],
+             (unsigned long long)b.w[2], (unsigned long long)b.w[3]);
+    return buf;
+  }
+
+  // one trie level: the windows of the candidate bytes at this position; returns -1 if nothing
+  int level(const CpSet& cs, const std::vector<Win>& wins, bool top, std::string& sig) {
+    std::map<int, ByteSet> full;                         // rem -> bytes
+    std::map<std::string, std::pair<ByteSet, int>> part; // subtree signature -> (bytes, subtree)
+    for (const Win& w : wins) {
+      const uint32_t vlo = std::max(w.lo, w.minv), vhi = std::min(w.hi, CpSet::MAX);
+      if (vlo > vhi || !cs.touches(vlo, vhi)) continue;
+      if (cs.covers(vlo, vhi)) { full[w.rem].set(w.b); continue; }
+      // partial: recurse into the next (continuation) byte
+      std::vector<Win> kids;
+      const uint32_t span = (w.hi - w.lo + 1) / 64;
+      for (int x = 0x80; x <= 0xBF; ++x) {
+        const uint32_t lo = w.lo + (uint32_t)(x - 0x80) * span;
+        kids.push_back({x, lo, lo + span - 1, w.minv, w.rem - 1});
+      }
+      std::string s;
+      const int sub = level(cs, kids, false, s);
+      if (sub < 0) continue;
+      auto it = part.find(s);
+      if (it == part.end()) part[s] = {ByteSet(), sub};
+      part[s].first.set(w.b);
     }
-    std::vector<int> bytes; utf8(cp, bytes);
-    std::vector<int> seq;
-    for (int x : bytes) { ByteSet bb; bb.set(x); seq.push_back(mk_set(bb)); }
-    return mk_cat(seq);
+    std::vector<int> alts;
+    ByteSet merged;
+    bool any_merged = false;
+    for (auto& kv : full) {
+      sig += "F" + std::to_string(kv.first) + sig_of(kv.second);
+      if (kv.first == 0) alts.push_back(mk_set(kv.second));
+      else if (top && !bt_) { merged = merged | kv.second; any_merged = true; }
+      else alts.push_back(mk_cat({mk_set(kv.second), tail(kv.first, !bt_)}));
+    }
+    if (any_merged) alts.push_back(mk_cat({mk_set(merged), tail(1, true)}));
+    for (auto& kv : part) {
+      sig += "P" + sig_of(kv.second.first) + "(" + kv.first + ")";
+      alts.push_back(mk_cat({mk_set(kv.second.first), kv.second.second}));
+    }
+    if (alts.empty()) return -1;
+    return mk_alt(alts);
+  }
+
+  int lower_cset(const CpSet& cs) {
+    ByteSet ascii;
+    for (auto& p : cs.r)
+      for (uint32_t c = p.first; c <= p.second && c < 128; ++c) ascii.set((int)c);
+    std::vector<int> alts;
+    if (!ascii.empty()) alts.push_back(mk_set(ascii));
+    if (cs.touches(0x80, CpSet::MAX)) {
+      std::vector<Win> leads;
+      for (int b = 0xC0; b <= 0xDF; ++b) leads.push_back({b, (uint32_t)(b & 0x1F) << 6, ((uint32_t)(b & 0x1F) << 6) + 63, 0x80, 1});
+      for (int b = 0xE0; b <= 0xEF; ++b) leads.push_back({b, (uint32_t)(b & 0x0F) << 12, ((uint32_t)(b & 0x0F) << 12) + 4095, 0x800, 2});
+      for (int b = 0xF0; b <= 0xF7; ++b) leads.push_back({b, (uint32_t)(b & 0x07) << 18, ((uint32_t)(b & 0x07) << 18) + 0x3FFFF, 0x10000, 3});
+      std::string sig;
+      const int t = level(cs, leads, true, sig);
+      if (t >= 0) alts.push_back(t);
+    }
+    if (alts.empty()) return mk_set(ByteSet());   // the empty set: a position that never matches
+    return mk_alt(alts);
   }
 };
 
@@ -686,6 +972,19 @@ Lit lits(const std::vector<Node>& N, int id) {
       std::set<int> ch;
       for (int b = 0; b < 256; ++b) if (n.set.test(b)) ch.insert(lower(b));
       if (!ch.empty() && ch.size() <= 4) { r.exact_ok = true; for (int c : ch) r.exact.insert(std::string(1, (char)c)); }
+      return r;
+    }
+    case N_CSET: {   // a few code points: their UTF-8 strings (ASCII lower-cased)
+      if (n.cs.empty() || n.cs.count() > 8) return r;
+      std::set<std::string> ch;
+      for (auto& p : n.cs.r)
+        for (uint32_t c = p.first; c <= p.second; ++c) {
+          std::string s;
+          utf8(c, s);
+          for (auto& x : s) x = (char)lower((unsigned char)x);
+          ch.insert(s);
+        }
+      if (ch.size() <= 4) { r.exact_ok = true; r.exact = ch; }
       return r;
     }
     case N_CAT: {
@@ -763,9 +1062,10 @@ Lit lits(const std::vector<Node>& N, int id) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Glushkov construction with boundary conditions
+// Glushkov construction with boundary conditions (byte positions from N_SET, code-point positions
+// from N_CSET)
 struct Info {
-  uint16_t nullable = 0;
+  uint32_t nullable = 0;
   std::vector<Edge> first, last;
 };
 
@@ -773,7 +1073,6 @@ class Glushkov {
  public:
   Glushkov(const std::vector<Node>& N, int max_pos) : N_(N), max_pos_(max_pos) {}
   Nfa nfa;
-  std::vector<std::map<int, uint16_t>> fol;
 
   Info build(int id) {
     const Node& n = N_[id];
@@ -781,11 +1080,11 @@ class Glushkov {
     switch (n.t) {
       case N_EMPTY: r.nullable = CTX_ALL; return r;
       case N_ASSERT: r.nullable = n.cond; return r;
-      case N_SET: {
+      case N_SET: case N_CSET: {
         int p = nfa.npos++;
         if (nfa.npos > max_pos_) throw Unsupported("too many NFA positions");
-        nfa.cls.push_back(n.set);
-        fol.emplace_back();
+        if (n.t == N_SET) nfa.cls.push_back(n.set); else nfa.ccls.push_back(n.cs);
+        fol_.emplace_back();
         r.first.push_back({p, CTX_ALL});
         r.last.push_back({p, CTX_ALL});
         return r;
@@ -846,25 +1145,38 @@ class Glushkov {
     nfa.last = top.last;
     nfa.nullable = top.nullable;
     nfa.follow.resize(nfa.npos);
-    for (int p = 0; p < nfa.npos; ++p)
-      for (auto& kv : fol[p]) nfa.follow[p].push_back({kv.first, kv.second});
+    for (int p = 0; p < nfa.npos; ++p) {
+      auto& v = fol_[p];
+      std::sort(v.begin(), v.end(), [](const Edge& a, const Edge& b) { return a.to < b.to; });
+      std::vector<Edge>& o = nfa.follow[p];
+      for (auto& e : v) {
+        if (!o.empty() && o.back().to == e.to) o.back().cond |= e.cond;
+        else o.push_back(e);
+      }
+      std::vector<Edge>().swap(v);
+    }
   }
 
  private:
   const std::vector<Node>& N_;
   int max_pos_;
+  std::vector<std::vector<Edge>> fol_;
 
   static void merge(std::vector<Edge>& v) {
-    std::map<int, uint16_t> m;
-    for (auto& e : v) m[e.to] |= e.cond;
+    std::sort(v.begin(), v.end(), [](const Edge& a, const Edge& b) { return a.to < b.to; });
+    std::vector<Edge> o;
+    for (auto& e : v) {
+      if (!o.empty() && o.back().to == e.to) o.back().cond |= e.cond;
+      else o.push_back(e);
+    }
     v.clear();
-    for (auto& kv : m) if (kv.second) v.push_back({kv.first, kv.second});
+    for (auto& e : o) if (e.cond) v.push_back(e);
   }
   void link(const std::vector<Edge>& from, const std::vector<Edge>& to) {
     for (auto& a : from)
       for (auto& b : to) {
-        uint16_t c = a.cond & b.cond;
-        if (c) fol[a.to][b.to] |= c;
+        uint32_t c = a.cond & b.cond;
+        if (c) fol_[a.to].push_back({b.to, c});
       }
   }
   void loop(Info& c) { link(c.last, c.first); }
@@ -872,17 +1184,33 @@ class Glushkov {
     Info r;
     r.nullable = a.nullable & b.nullable;
     r.first = a.first;
-    for (auto& e : b.first) { uint16_t c = e.cond & a.nullable; if (c) r.first.push_back({e.to, c}); }
+    for (auto& e : b.first) { uint32_t c = e.cond & a.nullable; if (c) r.first.push_back({e.to, c}); }
     r.last = b.last;
-    for (auto& e : a.last) { uint16_t c = e.cond & b.nullable; if (c) r.last.push_back({e.to, c}); }
+    for (auto& e : a.last) { uint32_t c = e.cond & b.nullable; if (c) r.last.push_back({e.to, c}); }
     link(a.last, b.first);
     merge(r.first); merge(r.last);
     return r;
   }
 };
 
+// a '$'-type condition (before-final-terminator vs plain) on a consuming edge: the automata only
+// evaluate FT for acceptance, so such patterns go to the backtracker
+bool ft_sensitive(uint32_t c) {
+  for (int p = 0; p < 4; ++p) {
+    const bool ft = (c >> ctx_index(p, N_FT)) & 1, nn = (c >> ctx_index(p, N_N)) & 1, nt = (c >> ctx_index(p, N_T)) & 1;
+    if (ft != nn && ft != nt) return true;
+  }
+  return false;
+}
+void check_ft(const Nfa& nfa) {
+  for (auto& e : nfa.first) if (ft_sensitive(e.cond)) throw Unsupported("end anchor inside pattern");
+  for (auto& v : nfa.follow) for (auto& e : v) if (ft_sensitive(e.cond)) throw Unsupported("end anchor inside pattern");
+}
+
 // ------------------------------------------------------------------------------------------
-// subset construction
+// subset construction (byte DFAs). Ungated follow edges are precomputed as position bitsets, so
+// a state's successor costs |state| word-ORs plus one AND per byte class instead of a walk of
+// every follow list per class (bounded-gap NFAs have O(n^2) edges).
 struct KeyHash {
   size_t operator()(const std::vector<uint64_t>& v) const {
     size_t h = 1469598103934665603ull;
@@ -891,11 +1219,76 @@ struct KeyHash {
   }
 };
 
+struct SubsetTables {
+  int np = 0, nw = 0;                                  // positions, bitset words
+  std::vector<uint64_t> fu;                            // [np][nw] ungated follow bitsets
+  std::vector<std::vector<Edge>> fg;                   // gated follow edges per position
+  std::vector<uint64_t> first_u;                       // ungated first set
+  std::vector<Edge> first_g;
+  std::vector<uint64_t> cm;                            // [nclasses][nw] positions whose class holds the rep byte
+  void init(int npos, const std::vector<const ByteSet*>& cls, const std::vector<std::vector<Edge>>& follow,
+            const std::vector<Edge>& first, const std::vector<int>& rep) {
+    np = npos;
+    nw = (np + 63) / 64;
+    fu.assign((size_t)np * nw, 0);
+    fg.assign(np, {});
+    for (int p = 0; p < np; ++p)
+      for (auto& e : follow[p]) {
+        if (e.cond == CTX_ALL) fu[(size_t)p * nw + (e.to >> 6)] |= 1ull << (e.to & 63);
+        else fg[p].push_back(e);
+      }
+    first_u.assign(nw, 0);
+    first_g.clear();
+    for (auto& e : first) {
+      if (e.cond == CTX_ALL) first_u[e.to >> 6] |= 1ull << (e.to & 63);
+      else first_g.push_back(e);
+    }
+    cm.assign(rep.size() * nw, 0);
+    for (size_t k = 0; k < rep.size(); ++k)
+      for (int p = 0; p < np; ++p)
+        if (cls[p]->test(rep[k])) cm[k * nw + (p >> 6)] |= 1ull << (p & 63);
+  }
+  // U = union of the ungated follow sets of the active positions
+  void ungated(const std::vector<uint64_t>& A, std::vector<uint64_t>& U) const {
+    std::fill(U.begin(), U.begin() + nw, 0);
+    for (int w = 0; w < nw; ++w) {
+      uint64_t m = A[w];
+      while (m) {
+        const int p = w * 64 + __builtin_ctzll(m);
+        m &= m - 1;
+        const uint64_t* f = fu.data() + (size_t)p * nw;
+        for (int j = 0; j < nw; ++j) U[j] |= f[j];
+      }
+    }
+  }
+  // successor positions on class k (rep byte c) in context bit `bit`; returns whether any
+  bool step(const std::vector<uint64_t>& A, const std::vector<uint64_t>& U, int k, int c, uint32_t bit,
+            const std::vector<const ByteSet*>& cls, std::vector<uint64_t>& B) const {
+    bool any = false;
+    const uint64_t* m = cm.data() + (size_t)k * nw;
+    for (int w = 0; w < nw; ++w) { B[w] = (U[w] | first_u[w]) & m[w]; any |= B[w] != 0; }
+    for (int w = 0; w < nw; ++w) {
+      uint64_t a = A[w];
+      while (a) {
+        const int p = w * 64 + __builtin_ctzll(a);
+        a &= a - 1;
+        for (auto& e : fg[p])
+          if ((e.cond & bit) && cls[e.to]->test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
+      }
+    }
+    for (auto& e : first_g)
+      if ((e.cond & bit) && cls[e.to]->test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
+    return any;
+  }
+};
+
+int next_kind_of_byte(int c) { return is_word_byte(c) ? N_W : (c >= 0x80 && c <= 0xBF) ? N_C : N_N; }
+
 Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
   Dfa d;
   const int np = nfa.npos;
   const int nw = (np + 63) / 64 + 1;  // last word: prev kind
-  // byte classes: signature = (membership in every distinct position class, word bit)
+  // byte classes: signature = (membership in every distinct position class, word bit, cont bit)
   std::vector<ByteSet> dcls;
   for (auto& c : nfa.cls) {
     bool f = false;
@@ -907,7 +1300,7 @@ Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
   std::vector<int> rep;
   for (int b = 0; b < 256; ++b) {
     std::vector<bool> sig;
-    sig.reserve(dcls.size() + 1);
+    sig.reserve(dcls.size() + 2);
     for (auto& x : dcls) sig.push_back(x.test(b));
     sig.push_back(is_word_byte(b));
     sig.push_back(b >= 0x80 && b <= 0xBF);
@@ -924,9 +1317,12 @@ Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
   for (auto& e : nfa.first) if (e.cond & CTX_NOT_BOS) restartable = true;
   d.anchored = !restartable;
 
-  // ACCEPT check helper
+  std::vector<const ByteSet*> clsp(np);
+  for (int p = 0; p < np; ++p) clsp[p] = &nfa.cls[p];
+  SubsetTables T;
+  T.init(np, clsp, nfa.follow, nfa.first, rep);
   auto accepts = [&](const std::vector<uint64_t>& A, int prev, int next) {
-    uint16_t bit = (uint16_t)(1u << ctx_index(prev, next));
+    const uint32_t bit = 1u << ctx_index(prev, next);
     if (nfa.nullable & bit) return true;
     for (auto& e : nfa.last)
       if ((A[e.to >> 6] >> (e.to & 63) & 1) && (e.cond & bit)) return true;
@@ -948,33 +1344,25 @@ Dfa build_dfa(const Nfa& nfa, bool uses_wordb, int max_states) {
   init[nw - 1] = P_BOS;
   intern(init);
 
-  d.trans.clear();
-  d.accflags.clear();
   std::vector<std::vector<uint16_t>> rows;
   std::vector<uint8_t> acc;
+  std::vector<uint64_t> U(nw, 0), B(nw, 0);
   for (size_t si = 0; si < states.size(); ++si) {
-    std::vector<uint64_t> A = states[si];
-    int prev = (int)A[nw - 1];
+    const std::vector<uint64_t> A = states[si];
+    const int prev = (int)A[nw - 1];
     uint8_t fl = 0;
     if (accepts(A, prev, N_EOS)) fl |= 1;
     if (accepts(A, prev, N_FT)) fl |= 2;
     acc.push_back(fl);
     std::vector<uint16_t> row(d.nclasses, 0);
+    T.ungated(A, U);
     for (int k = 0; k < d.nclasses; ++k) {
-      int c = rep[k];
-      int nk = is_word_byte(c) ? N_W : (c >= 0x80 && c <= 0xBF) ? N_C : N_N;
+      const int c = rep[k];
+      const int nk = next_kind_of_byte(c);
       if (accepts(A, prev, nk)) { row[k] = 1; continue; }
-      uint16_t bit = (uint16_t)(1u << ctx_index(prev, nk));
-      std::vector<uint64_t> B(nw, 0);
-      bool any = false;
-      for (int p = 0; p < np; ++p) {
-        if (!(A[p >> 6] >> (p & 63) & 1)) continue;
-        for (auto& e : nfa.follow[p])
-          if ((e.cond & bit) && nfa.cls[e.to].test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
-      }
-      for (auto& e : nfa.first)
-        if ((e.cond & bit) && nfa.cls[e.to].test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
-      int nprev = (nk == N_W && uses_wordb) ? P_W : P_N;
+      std::fill(B.begin(), B.end(), 0);
+      const bool any = T.step(A, U, k, c, 1u << ctx_index(prev, nk), clsp, B);
+      const int nprev = (nk == N_W && uses_wordb) ? P_W : P_N;
       if (!any && !restartable) { row[k] = 0; continue; }
       B[nw - 1] = (uint64_t)nprev;
       row[k] = (uint16_t)intern(B);
@@ -1030,11 +1418,13 @@ void set_literals(Compiled& out, const std::vector<Node>& nodes, int root) {
 }
 
 // a construct no automaton expresses: classify with the backtracking parser -- Java rejects the
-// pattern (INVALID), the native backtracker runs it (FALLBACK, bt_ok), or only the Python oracle
-// translation can (FALLBACK) -- and take its literals for the device prefilter
+// pattern (INVALID) or the native backtracker runs it (FALLBACK, bt_ok) -- and take its literals
+// for the device prefilter
 void classify_fallback(Compiled& out, const std::string& pattern, const std::string& why) {
   out.kind = Kind::FALLBACK;
   out.error = why;
+  out.literals.clear();
+  out.has_literals = false;
   try {
     Parser B(pattern, true);
     const int r = B.parse();
@@ -1049,19 +1439,24 @@ void classify_fallback(Compiled& out, const std::string& pattern, const std::str
   } catch (const std::exception&) {
   }
 }
-}  // namespace
 
-Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions) {
+Compiled compile_impl(const std::string& pattern, int max_dfa_states, int max_positions, bool want_bpg) {
   Compiled out;
   std::vector<Node> nodes;
   int root;
-  bool wordb = false;
   try {
     Parser P(pattern);
     root = P.parse();
     nodes = std::move(P.nodes);
-    wordb = P.uses_wordb;
-    out.wordb = wordb;
+    out.wordb = P.uses_wordb;
+    out.uword = P.uses_uword;
+    if (P.uses_uword && P.uses_aword) {
+      classify_fallback(out, pattern, "\\b with both ASCII and Unicode word semantics");
+      return out;
+    }
+    // Unicode \b needs the wordness of whole code points, MULTILINE anchors the line-terminator
+    // contexts: only the code-point automaton has them
+    out.cp_only = P.needs_cp || P.uses_uword;
   } catch (const SyntaxError& e) {
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   } catch (const Unsupported& e) {
@@ -1071,43 +1466,58 @@ Compiled compile(const std::string& pattern, int max_dfa_states, int max_positio
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   }
   set_literals(out, nodes, root);
-  try {
-    Glushkov G(nodes, max_positions);
-    Info top = G.build(root);
-    G.finish(top);
-    out.nfa = std::move(G.nfa);
-    // a '$'-type condition on a consuming edge cannot be represented by the DFA's FT handling
-    auto ft_sensitive = [](uint16_t c) {
-      for (int p = 0; p < 3; ++p) {
-        bool ft = (c >> ctx_index(p, N_FT)) & 1, nn = (c >> ctx_index(p, N_N)) & 1;
-        if (ft != nn) return true;
-      }
-      return false;
-    };
-    for (auto& e : out.nfa.first) if (ft_sensitive(e.cond)) throw Unsupported("end anchor inside pattern");
-    for (auto& v : out.nfa.follow) for (auto& e : v) if (ft_sensitive(e.cond)) throw Unsupported("end anchor inside pattern");
-  } catch (const Unsupported& e) {
-    out.kind = Kind::FALLBACK;
-    out.error = e.what();
+  std::string why = out.cp_only ? "code-point contexts" : "";
+  if (!out.cp_only) {
     try {
-      BtRegex check(pattern);
-      out.bt_ok = true;
-    } catch (const std::exception&) {
+      Lowerer Lw(nodes, false);
+      const int broot = Lw.lower(root);
+      Glushkov G(Lw.out, max_positions);
+      Info top = G.build(broot);
+      G.finish(top);
+      check_ft(G.nfa);
+      out.nfa = std::move(G.nfa);
+      out.byte_nfa = true;
+      out.dfa = build_dfa(out.nfa, out.wordb, max_dfa_states);
+      out.kind = Kind::DFA;
+      return out;
+    } catch (const Unsupported& e) {
+      why = e.what();
+      if (why == "end anchor inside pattern") { classify_fallback(out, pattern, why); return out; }
+      out.dfa = Dfa();
     }
+  }
+  // DFA blow-up (bounded gaps, repeated groups) or code-point contexts: the code-point NFA
+  out.kind = Kind::NFA;
+  out.error = why;
+  if (want_bpg) {
+    try {
+      Glushkov G(nodes, BPG_MAX_POS);
+      Info top = G.build(root);
+      G.finish(top);
+      check_ft(G.nfa);
+      out.bpg = bpg_program(G.nfa, out.uword);
+    } catch (const Unsupported& e) {
+      out.error = why + "; bpg: " + e.what();
+      out.bpg.clear();
+    }
+  }
+  if (out.bpg.empty() && !out.byte_nfa) {
+    // neither a program nor a byte NFA (for the MFMA engine): the backtracker
+    out.nfa = Nfa();
+    classify_fallback(out, pattern, out.error);
     return out;
   }
   try {
-    out.dfa = build_dfa(out.nfa, wordb, max_dfa_states);
-    out.kind = Kind::DFA;
-  } catch (const Unsupported& e) {
-    out.kind = Kind::NFA; out.error = e.what();
-    try {
-      BtRegex check(pattern);
-      out.bt_ok = true;
-    } catch (const std::exception&) {
-    }
+    BtRegex check(pattern);
+    out.bt_ok = true;
+  } catch (const std::exception&) {
   }
   return out;
+}
+}  // namespace
+
+Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions) {
+  return compile_impl(pattern, max_dfa_states, max_positions, true);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1120,7 +1530,7 @@ struct Member {
 };
 
 uint32_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t>& A, int prev, int next) {
-  const uint16_t bit = (uint16_t)(1u << ctx_index(prev, next));
+  const uint32_t bit = 1u << ctx_index(prev, next);
   uint32_t m = 0;
   for (size_t r = 0; r < M.size(); ++r) {
     const Nfa& n = *M[r].nfa;
@@ -1142,9 +1552,10 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
   comp.reserve(patterns.size());
   bool wordb = false;
   for (auto& p : patterns) {
-    comp.push_back(compile(p, 4, 4096));
+    comp.push_back(compile_impl(p, 4, 4096, false));
     const Compiled& c = comp.back();
-    if (c.kind != Kind::DFA && c.kind != Kind::NFA) throw Unsupported("multi-DFA member is not an automaton regex");
+    if ((c.kind != Kind::DFA && c.kind != Kind::NFA) || !c.byte_nfa)
+      throw Unsupported("multi-DFA member has no byte automaton");
     wordb |= c.wordb;
   }
   std::vector<Member> M(comp.size());
@@ -1194,7 +1605,9 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
   }
   d.nclasses = (int)rep.size();
   if (d.nclasses > 256) throw Unsupported("too many byte classes");
-  const int nw = (np + 63) / 64 + 1;   // last word: prev kind
+  SubsetTables T;
+  T.init(np, cls, follow, first, rep);
+  const int nw = T.nw + 1;   // last word: prev kind
   std::unordered_map<std::vector<uint64_t>, int, KeyHash> ids;
   std::vector<std::vector<uint64_t>> states;
   auto intern = [&](std::vector<uint64_t>& key) -> int {
@@ -1210,26 +1623,20 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
   init[nw - 1] = P_BOS;
   intern(init);
   std::vector<uint32_t> rows, fin;
+  std::vector<uint64_t> U(nw, 0), B(nw, 0);
   for (size_t si = 0; si < states.size(); ++si) {
     const std::vector<uint64_t> A = states[si];
     const int prev = (int)A[nw - 1];
     fin.push_back(member_accepts(M, A, prev, N_EOS));
     fin.push_back(member_accepts(M, A, prev, N_FT));
-    uint32_t acc_k[5];
-    for (int nk = 0; nk < 5; ++nk) acc_k[nk] = member_accepts(M, A, prev, nk);
+    uint32_t acc_k[6];
+    for (int nk = 0; nk < 6; ++nk) acc_k[nk] = member_accepts(M, A, prev, nk);
+    T.ungated(A, U);
     for (int k = 0; k < d.nclasses; ++k) {
       const int c = rep[k];
-      const int nk = is_word_byte(c) ? N_W : (c >= 0x80 && c <= 0xBF) ? N_C : N_N;
-      const uint16_t bit = (uint16_t)(1u << ctx_index(prev, nk));
-      std::vector<uint64_t> B(nw, 0);
-      bool any = false;
-      for (int p = 0; p < np; ++p) {
-        if (!(A[p >> 6] >> (p & 63) & 1)) continue;
-        for (auto& e : follow[p])
-          if ((e.cond & bit) && cls[e.to]->test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
-      }
-      for (auto& e : first)
-        if ((e.cond & bit) && cls[e.to]->test(c)) { B[e.to >> 6] |= 1ull << (e.to & 63); any = true; }
+      const int nk = next_kind_of_byte(c);
+      std::fill(B.begin(), B.end(), 0);
+      const bool any = T.step(A, U, k, c, 1u << ctx_index(prev, nk), cls, B);
       uint32_t next = 0;
       if (any || restartable) {
         B[nw - 1] = (uint64_t)((nk == N_W && wordb) ? P_W : P_N);
@@ -1260,6 +1667,177 @@ uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n) {
 }
 
 // ------------------------------------------------------------------------------------------
+// bit-parallel Glushkov programs over code points (layout documented in csrc/kernels/bpg.h)
+namespace {
+
+constexpr int kBpgWidths[] = {1, 2, 3, 4, 6, 8, 12, 16, 24, 32};
+
+struct Bits {
+  int nw = 0;
+  std::vector<uint64_t> w;
+  explicit Bits(int n = 0) : nw((n + 63) / 64), w(nw, 0) {}
+  void set(int p) { w[p >> 6] |= 1ull << (p & 63); }
+  bool test(int p) const { return (w[p >> 6] >> (p & 63)) & 1; }
+  bool any() const { for (auto x : w) if (x) return true; return false; }
+  bool subset_of(const Bits& o) const { for (int i = 0; i < nw; ++i) if (w[i] & ~o.w[i]) return false; return true; }
+  void orr(const Bits& o) { for (int i = 0; i < nw; ++i) w[i] |= o.w[i]; }
+  void andnot(const Bits& o) { for (int i = 0; i < nw; ++i) w[i] &= ~o.w[i]; }
+  bool operator==(const Bits& o) const { return w == o.w; }
+};
+
+// the kind of a code point at code-point level: W / N / T (a line terminator)
+int cp_kind(uint32_t c, bool uword) {
+  if (is_line_term(c)) return N_T;
+  if (c < 128) return is_word_byte((int)c) ? N_W : N_N;
+  return (uword && unicode_word().contains(c)) ? N_W : N_N;
+}
+
+}  // namespace
+
+std::vector<uint64_t> bpg_program(const Nfa& nf, bool uword) {
+  const int np = nf.npos;
+  if (np <= 0) throw Unsupported("empty program");
+  if (np > BPG_MAX_POS) throw Unsupported("more than 2048 positions");
+  int W = 0;
+  for (int w : kBpgWidths) if (w * 64 >= np) { W = w; break; }
+  // ---- decomposition of the follow relation: shift, self, spread fields, exceptions (exact)
+  std::vector<Bits> F(np, Bits(np));
+  std::vector<std::pair<int, std::pair<uint32_t, Bits>>> gated;   // (src, (cond, targets))
+  {
+    std::map<std::pair<int, uint32_t>, Bits> g;
+    for (int p = 0; p < np; ++p)
+      for (auto& e : nf.follow[p]) {
+        if (e.cond == CTX_ALL) F[p].set(e.to);
+        else {
+          auto it = g.find({p, e.cond});
+          if (it == g.end()) it = g.emplace(std::make_pair(p, e.cond), Bits(np)).first;
+          it->second.set(e.to);
+        }
+      }
+    for (auto& kv : g) gated.push_back({kv.first.first, {kv.first.second, kv.second}});
+  }
+  Bits shift(np), selfl(np);
+  std::vector<Bits> covered(np, Bits(np));
+  for (int p = 0; p < np; ++p) {
+    if (p + 1 < np && F[p].test(p + 1)) { shift.set(p); covered[p].set(p + 1); }
+    if (F[p].test(p)) { selfl.set(p); covered[p].set(p); }
+  }
+  Bits src_all(np), R_all(np), lo_all(np), hi_all(np);
+  for (int p = 0; p < np;) {
+    // forward targets not yet covered
+    bool fwd = false;
+    int hi = -1, nR = 0;
+    for (int q = p + 1; q < np; ++q)
+      if (F[p].test(q)) { ++nR; hi = q; if (!covered[p].test(q)) fwd = true; }
+    if (!fwd || hi - p < 1 || nR < 2) { ++p; continue; }
+    Bits R(np);
+    for (int q = p + 1; q <= hi; ++q) if (F[p].test(q)) R.set(q);
+    // sources: every s in [p, hi] that reaches all targets above it (a field grows while they do)
+    std::vector<int> src;
+    for (int s = p; s <= hi; ++s) {
+      Bits above = R;
+      for (int q = 0; q <= s && q < np; ++q) if (above.test(q)) above.w[q >> 6] &= ~(1ull << (q & 63));
+      if (above.subset_of(F[s])) src.push_back(s);
+    }
+    for (int s : src) {
+      src_all.set(s);
+      for (int q = s + 1; q <= hi; ++q) if (R.test(q)) covered[s].set(q);
+    }
+    R_all.orr(R);
+    lo_all.set(p);
+    hi_all.set(hi);
+    p = hi + 1;
+  }
+  struct Exc { int src; uint32_t cond; Bits tos; };
+  std::vector<Exc> exc;
+  for (int p = 0; p < np; ++p) {
+    Bits rest = F[p];
+    rest.andnot(covered[p]);
+    if (rest.any()) exc.push_back({p, CTX_ALL, rest});
+    Bits extra = covered[p];
+    extra.andnot(F[p]);
+    if (extra.any()) throw Unsupported("bpg decomposition is not exact");
+  }
+  for (auto& g : gated) exc.push_back({g.first, g.second.first, g.second.second});
+  std::sort(exc.begin(), exc.end(), [](const Exc& a, const Exc& b) { return a.src < b.src; });
+  if ((int)exc.size() > BPG_MAX_EXC) throw Unsupported("too many exception edges");
+  // ---- code-point classes: elementary intervals with the same (kind, membership) signature
+  std::vector<uint32_t> cuts = {0, 128, CpSet::MAX + 1};
+  for (int c = 1; c < 128; ++c) cuts.push_back((uint32_t)c);
+  for (auto& cs : nf.ccls)
+    for (auto& r : cs.r) { cuts.push_back(r.first); cuts.push_back(r.second + 1); }
+  for (uint32_t t : {0x85u, 0x2028u, 0x2029u}) { cuts.push_back(t); cuts.push_back(t + 1); }
+  if (uword)
+    for (auto& r : unicode_word().r) { cuts.push_back(r.first); cuts.push_back(r.second + 1); }
+  std::sort(cuts.begin(), cuts.end());
+  cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+  std::map<std::pair<int, std::vector<uint64_t>>, int> sig2cls;
+  std::vector<Bits> rows;
+  std::vector<uint16_t> amap(128, 0);
+  std::vector<uint64_t> ranges;   // lo | cls << 21 | kind << 37
+  int last_cls = -1, last_kind = -1;
+  for (size_t i = 0; i + 1 < cuts.size(); ++i) {
+    const uint32_t lo = cuts[i];   // [lo, cuts[i + 1]) has one signature (no cut inside)
+    if (lo > CpSet::MAX) break;
+    const int kind = cp_kind(lo, uword);
+    Bits mem(W * 64);
+    for (int p = 0; p < np; ++p) if (nf.ccls[p].contains(lo)) mem.set(p);
+    auto key = std::make_pair(kind, mem.w);
+    auto it = sig2cls.find(key);
+    int k;
+    if (it == sig2cls.end()) {
+      k = (int)rows.size();
+      if (k >= BPG_MAX_CLS) throw Unsupported("too many code-point classes");
+      sig2cls[key] = k;
+      rows.push_back(mem);
+    } else {
+      k = it->second;
+    }
+    if (lo < 128) { amap[lo] = (uint16_t)k; continue; }
+    const int kd = kind == N_W ? 1 : kind == N_T ? 2 : 0;
+    if (k == last_cls && kd == last_kind) continue;      // merged with the previous interval
+    ranges.push_back((uint64_t)lo | ((uint64_t)k << 21) | ((uint64_t)kd << 37));
+    last_cls = k;
+    last_kind = kd;
+  }
+  const int ncls = (int)rows.size();
+  // ---- first / last per context, header flags
+  std::vector<uint64_t> first((size_t)NCTX * W, 0), last((size_t)NCTX * W, 0);
+  for (auto& e : nf.first)
+    for (int c = 0; c < NCTX; ++c) if ((e.cond >> c) & 1) first[(size_t)c * W + (e.to >> 6)] |= 1ull << (e.to & 63);
+  for (auto& e : nf.last)
+    for (int c = 0; c < NCTX; ++c) if ((e.cond >> c) & 1) last[(size_t)c * W + (e.to >> 6)] |= 1ull << (e.to & 63);
+  bool uniform = true;
+  for (int c = 1; c < NCTX && uniform; ++c)
+    for (int w = 0; w < W; ++w)
+      if (first[(size_t)c * W + w] != first[w] || last[(size_t)c * W + w] != last[w]) { uniform = false; break; }
+  const uint32_t nullable = nf.nullable & CTX_ALL;
+  bool anchored = (nullable >> 6) == 0;                  // first set only after BOS (prev kind 0)
+  for (size_t i = 6 * (size_t)W; i < first.size() && anchored; ++i) if (first[i]) anchored = false;
+  const uint64_t E = exc.size();
+  const uint64_t hdr = (uint64_t)W | (E << 8) | ((uint64_t)ncls << 20) | (anchored ? 1ull << 30 : 0) |
+                       (uniform ? 1ull << 31 : 0) | ((uint64_t)nullable << 32) | (uword ? 1ull << 56 : 0);
+  std::vector<uint64_t> P;
+  P.push_back(hdr);
+  P.push_back(0);   // hdr2: nranges | total words << 32 (below)
+  auto put = [&](const Bits& b) { for (int w = 0; w < W; ++w) P.push_back(w < b.nw ? b.w[w] : 0); };
+  auto widen = [&](const Bits& b) { Bits o(W * 64); for (int w = 0; w < b.nw; ++w) o.w[w] = b.w[w]; return o; };
+  put(widen(shift)); put(widen(selfl)); put(widen(src_all)); put(widen(R_all)); put(widen(lo_all)); put(widen(hi_all));
+  P.insert(P.end(), first.begin(), first.end());
+  P.insert(P.end(), last.begin(), last.end());
+  for (int i = 0; i < 128; i += 4)
+    P.push_back((uint64_t)amap[i] | ((uint64_t)amap[i + 1] << 16) | ((uint64_t)amap[i + 2] << 32) | ((uint64_t)amap[i + 3] << 48));
+  for (auto& r : rows) put(r);
+  for (auto& e : exc) {
+    P.push_back((uint64_t)e.src | ((uint64_t)e.cond << 16));
+    put(widen(e.tos));
+  }
+  P.insert(P.end(), ranges.begin(), ranges.end());
+  P[1] = (uint64_t)ranges.size() | ((uint64_t)P.size() << 32);
+  return P;
+}
+
+// ------------------------------------------------------------------------------------------
 // backtracking VM (Java semantics for non-regular constructs)
 namespace {
 
@@ -1268,8 +1846,8 @@ enum BOp : uint8_t { B_SET, B_SPLIT, B_JMP, B_SAVE, B_ASSERT, B_BREF, B_LOOK, B_
 struct BInst {
   BOp op;
   int x = 0, y = 0;        // SET: set id; SPLIT: preferred / other pc; JMP/SAVE/MARK/PROGRESS/BREF/LOOK/ATOMIC: arg
-  uint16_t cond = 0;       // ASSERT
-  bool f1 = false, f2 = false;   // BREF: ci; LOOK: behind, neg; ML: kind ($), unix lines
+  uint32_t cond = 0;       // ASSERT
+  bool f1 = false, f2 = false;   // BREF: ci; LOOK: behind, neg; ML: kind ($), unix lines; ASSERT: Unicode word
   int lo = 0, hi = 0;      // LOOK behind: byte-length bounds of the sub-pattern
 };
 
@@ -1302,7 +1880,7 @@ struct BtCompiler {
     const Node& n = N[id];
     switch (n.t) {
       case N_EMPTY: case N_ASSERT: case N_LOOK: case N_MLANCHOR: mn = mx = 0; return;
-      case N_SET: mn = mx = 1; return;
+      case N_SET: case N_CSET: mn = mx = 1; return;
       case N_GROUP: case N_ATOMIC: bounds(n.kids[0], mn, mx); return;
       case N_BACKREF: mn = 0; mx = INF; return;
       case N_CAT: {
@@ -1327,7 +1905,7 @@ struct BtCompiler {
   void comp(int p, int id) {
     const Node& n = N[id];
     switch (n.t) {
-      case N_EMPTY: return;
+      case N_EMPTY: case N_CSET: return;    // (N_CSET never reaches here: lowered)
       case N_SET: {
         BInst in{B_SET}; in.x = (int)I.sets.size(); I.sets.push_back(n.set); emit(p, in); return;
       }
@@ -1376,7 +1954,7 @@ struct BtCompiler {
         }
         return;
       }
-      case N_ASSERT: { BInst in{B_ASSERT}; in.cond = n.cond; emit(p, in); return; }
+      case N_ASSERT: { BInst in{B_ASSERT}; in.cond = n.cond; in.f1 = n.uword; emit(p, in); return; }
       case N_GROUP: {
         I.ncaps = std::max(I.ncaps, 2 * n.idx + 2);
         BInst a{B_SAVE}; a.x = 2 * n.idx; emit(p, a);
@@ -1420,15 +1998,33 @@ struct BtRun {
   int64_t steps = 0, budget;
   bool exhausted = false;
 
-  uint16_t ctx_bit(int64_t i) const {
-    const int prev = i == 0 ? P_BOS : (is_word_byte(s[i - 1]) ? P_W : P_N);
-    int next;
-    if (i == n) next = N_EOS;
-    else if (i == ft) next = N_FT;
-    else if (is_word_byte(s[i])) next = N_W;
-    else if (s[i] >= 0x80 && s[i] <= 0xBF) next = N_C;
-    else next = N_N;
-    return (uint16_t)(1u << ctx_index(prev, next));
+  uint32_t ctx_bit(int64_t i, bool uword) const {
+    int prev, next;
+    if (!uword) {
+      prev = i == 0 ? P_BOS : (is_word_byte(s[i - 1]) ? P_W : P_N);
+      if (i == n) next = N_EOS;
+      else if (i == ft) next = N_FT;
+      else next = next_kind_of_byte(s[i]);
+    } else {   // Unicode WORD on whole code points
+      if (i == 0) {
+        prev = P_BOS;
+      } else {
+        int64_t j = i - 1;
+        while (j > 0 && s[j] >= 0x80 && s[j] <= 0xBF) --j;
+        int len;
+        const uint32_t c = decode_at(s, n, j, &len);
+        prev = (c < 128 ? is_word_byte((int)c) : unicode_word().contains(c)) ? P_W : P_N;
+      }
+      if (i == n) next = N_EOS;
+      else if (i == ft) next = N_FT;
+      else if (s[i] >= 0x80 && s[i] <= 0xBF) next = N_C;
+      else {
+        int len;
+        const uint32_t c = decode_at(s, n, i, &len);
+        next = (c < 128 ? is_word_byte((int)c) : unicode_word().contains(c)) ? N_W : N_N;
+      }
+    }
+    return 1u << ctx_index(prev, next);
   }
   // line terminator (Java: \n \r U+0085 U+2028 U+2029) starting / ending at byte i
   bool term_at(int64_t i) const {
@@ -1480,7 +2076,7 @@ struct BtRun {
         case B_SAVE: st.push_back({1, in.x, caps[in.x]}); caps[in.x] = pos; ++pc; break;
         case B_MARK: st.push_back({2, in.x, marks[in.x]}); marks[in.x] = pos; ++pc; break;
         case B_PROGRESS: pc = pos == marks[in.x] ? in.y : pc + 1; break;
-        case B_ASSERT: if (ctx_bit(pos) & in.cond) ++pc; else ok = false; break;
+        case B_ASSERT: if (ctx_bit(pos, in.f1) & in.cond) ++pc; else ok = false; break;
         case B_ML: if (ml_anchor(in, pos)) ++pc; else ok = false; break;
         case B_BREF: {
           const int64_t a = caps[2 * in.x], b = caps[2 * in.x + 1];
@@ -1541,11 +2137,13 @@ struct BtRun {
 BtRegex::BtRegex(const std::string& pattern) {
   Parser P(pattern, true);
   const int root = P.parse();
+  Lowerer Lw(P.nodes, true);
+  const int broot = Lw.lower(root);
   auto impl = std::make_shared<Impl>();
   impl->ncaps = 2 * P.ngroups + 2;
-  BtCompiler C{P.nodes, *impl};
+  BtCompiler C{Lw.out, *impl};
   C.new_prog();
-  C.comp(0, root);
+  C.comp(0, broot);
   C.emit(0, BInst{B_MATCH});
   const std::vector<BInst>& code = impl->progs[0];
   impl->bos_only = !code.empty() && code[0].op == B_ASSERT && code[0].cond == mask_where(f_bos);

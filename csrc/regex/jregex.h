@@ -1,23 +1,28 @@
-// java.util.regex (Java 21 defaults) -> byte-level automata for the MI355X log engine.
+// java.util.regex (Java 21 defaults) -> automata for the MI355X log engine.
 //
-// Pipeline (host C++, run once per distinct regex at library load — the reference recompiles
+// Pipeline (host C++, run once per distinct regex at library load -- the reference recompiles
 // every regex on every request, AnalysisService.java:55-86):
-//   parse (Java syntax subset) -> AST
+//   parse (Java syntax) -> AST over CODE POINTS: every character / class / property is one exact
+//          code-point set (sorted disjoint ranges), flags resolved at parse time (CASE_INSENSITIVE
+//          with or without UNICODE_CASE, UNICODE_CHARACTER_CLASS, DOTALL, UNIX_LINES, MULTILINE,
+//          COMMENTS), Unicode properties from generated tables (unicode_tables.inc)
 //   AST -> required-literal factor set (prefilter keys)
-//   AST -> Glushkov position NFA whose edges carry *boundary-context* conditions
-//          (^ $ \b \B \A \z \Z as zero-width assertions)
-//   NFA -> byte DFA (subset construction, previous-byte wordness folded into the state,
-//          absorbing DEAD=0 / ACCEPT=1 states, per-state accept flags for end-of-line).
+//   AST -> byte AST (code-point sets lowered to UTF-8 byte sequences) -> Glushkov NFA over bytes
+//          -> byte DFA (subset construction; absorbing DEAD=0 / ACCEPT=1; end-of-line flags)
+//   AST -> Glushkov NFA over code points (one position per character / class) -> bit-parallel
+//          Glushkov program (bpg_program) for regexes whose DFA blows up or that need code-point
+//          boundary contexts (MULTILINE ^ $, Unicode \b)
 //
 // Only boolean find() is ever used by the reference (AnalysisService.java:95,
 // ScoringService.java:281,300,330), so language membership of ".*R.*" is all that matters and
 // an automaton is exact for the regular subset. Non-regular / language-changing constructs
-// (backrefs, lookaround, possessive, atomic groups) raise Unsupported -> host fallback.
+// (backrefs, lookaround, possessive, atomic groups) raise Unsupported -> the host backtracker.
 #pragma once
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace lp {
@@ -25,15 +30,19 @@ namespace lp {
 struct SyntaxError : std::runtime_error { using std::runtime_error::runtime_error; };
 struct Unsupported : std::runtime_error { using std::runtime_error::runtime_error; };
 
-// Boundary contexts: prev in {BOS=0, W=1, N=2} x next in {EOS=0, FT=1, W=2, N=3, C=4}
-// ctx index = prev*5 + next (15 contexts). FT = "before the final line terminator".
-enum : int { P_BOS = 0, P_W = 1, P_N = 2 };
-// N_C: the next byte is a UTF-8 continuation byte (a boundary inside one code point); no
-// assertion holds there, so assertions are only ever evaluated between whole characters.
-enum : int { N_EOS = 0, N_FT = 1, N_W = 2, N_N = 3, N_C = 4 };
-constexpr uint16_t CTX_ALL = 0x7FFF;                    // 15 contexts
-constexpr uint16_t CTX_NOT_BOS = 0x7FE0;                // prev != BOS
-inline int ctx_index(int prev, int next) { return prev * 5 + next; }
+// Boundary contexts: prev in {BOS=0, W=1, N=2, T=3} x next in {EOS=0, FT=1, W=2, N=3, C=4, T=5},
+// ctx index = prev * 6 + next (24 contexts). FT = "before the final line terminator".
+//   W / N: word / other character (ASCII word characters; Unicode WORD under (?U) \b)
+//   T: a line terminator character (\r U+0085 U+2028 U+2029) -- code-point level only, the
+//      MULTILINE anchors test it
+//   C: the next byte is a UTF-8 continuation byte (a boundary inside one code point) -- byte level
+//      only; no assertion holds there, so assertions are only evaluated between whole characters
+enum : int { P_BOS = 0, P_W = 1, P_N = 2, P_T = 3 };
+enum : int { N_EOS = 0, N_FT = 1, N_W = 2, N_N = 3, N_C = 4, N_T = 5 };
+constexpr int NCTX = 24;
+constexpr uint32_t CTX_ALL = (1u << NCTX) - 1;
+constexpr uint32_t CTX_NOT_BOS = CTX_ALL & ~0x3Fu;      // prev != BOS
+inline int ctx_index(int prev, int next) { return prev * 6 + next; }
 
 struct ByteSet {
   uint64_t w[4] = {0, 0, 0, 0};
@@ -46,17 +55,35 @@ struct ByteSet {
   int count() const { return __builtin_popcountll(w[0]) + __builtin_popcountll(w[1]) + __builtin_popcountll(w[2]) + __builtin_popcountll(w[3]); }
 };
 
+// Exact set of Unicode code points: sorted, disjoint, non-adjacent [lo, hi] ranges.
+struct CpSet {
+  std::vector<std::pair<uint32_t, uint32_t>> r;
+  static constexpr uint32_t MAX = 0x10FFFF;
+  void add(uint32_t c) { add_range(c, c); }
+  void add_range(uint32_t lo, uint32_t hi);
+  void unite(const CpSet& o);
+  void intersect(const CpSet& o);
+  void negate();
+  bool contains(uint32_t c) const;
+  bool covers(uint32_t lo, uint32_t hi) const;       // [lo, hi] entirely inside
+  bool touches(uint32_t lo, uint32_t hi) const;      // [lo, hi] intersects
+  bool empty() const { return r.empty(); }
+  uint64_t count() const;
+  bool operator==(const CpSet& o) const { return r == o.r; }
+};
+
 enum class Kind : int { DFA = 0, NFA = 1, FALLBACK = 2, INVALID = 3 };
 
-struct Edge { int to; uint16_t cond; };
+struct Edge { int to; uint32_t cond; };
 
 struct Nfa {
   int npos = 0;
-  std::vector<ByteSet> cls;                 // per position byte class
+  std::vector<ByteSet> cls;                 // byte level: per position byte class
+  std::vector<CpSet> ccls;                  // code-point level: per position code-point class
   std::vector<std::vector<Edge>> follow;    // per position
   std::vector<Edge> first;                  // (pos, cond)
   std::vector<Edge> last;                   // (pos, cond)
-  uint16_t nullable = 0;                    // contexts in which the empty string matches
+  uint32_t nullable = 0;                    // contexts in which the empty string matches
 };
 
 struct Dfa {
@@ -70,15 +97,20 @@ struct Dfa {
 
 struct Compiled {
   Kind kind = Kind::INVALID;
-  bool wordb = false;                       // uses \b / \B (prev-byte wordness matters)
-  std::string error;                        // reason for FALLBACK / INVALID
+  bool wordb = false;                       // uses \b / \B (prev-character wordness matters)
+  bool uword = false;                       // \b / \B with Unicode WORD semantics ((?U))
+  bool cp_only = false;                     // needs code-point contexts: no byte automaton (DFA / MFMA)
+  std::string error;                        // reason for NFA / FALLBACK / INVALID
   std::vector<std::string> literals;        // OR-set of required factors (ASCII-lowercased bytes)
   bool has_literals = false;
   bool bt_ok = false;                       // the native backtracker (BtRegex) runs it
+  bool byte_nfa = false;                    // nfa holds the byte-level Glushkov NFA (DFA / MFMA engines)
   Nfa nfa;
   Dfa dfa;
+  std::vector<uint64_t> bpg;                // kind NFA: bit-parallel Glushkov program (empty: none)
 };
 
+// max_positions bounds the byte-level NFA; the code-point NFA of a BPG program has <= BPG_MAX_POS.
 Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions);
 
 // Multi-regex DFA ("scan group"): the Glushkov NFAs of up to 16 regexes determinised TOGETHER, so
@@ -96,7 +128,7 @@ struct MultiDfa {
   std::vector<uint32_t> trans;
   std::vector<uint32_t> fin;
 };
-// throws Unsupported (state limit, > MULTI_MAX_REGS, a member that is not an automaton regex)
+// throws Unsupported (state limit, > MULTI_MAX_REGS, a member without a byte automaton)
 MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states);
 // bit r set <=> patterns[r] finds a match in s[0..n) (host walk; the device kernel is k_scan_multi)
 uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n);
@@ -106,12 +138,19 @@ bool dfa_find(const Dfa& d, const uint8_t* s, int64_t n);
 // Length in bytes of a final line terminator (\r, U+0085, U+2028, U+2029) ending s[0..n), or 0.
 int final_terminator_len(const uint8_t* s, int64_t n);
 
+// ---- bit-parallel Glushkov programs over code points (layout: csrc/kernels/bpg.h) ----------
+constexpr int BPG_MAX_POS = 2048;         // 32 words of 64 positions
+constexpr int BPG_MAX_EXC = 256;
+constexpr int BPG_MAX_CLS = 1023;
+// code-point NFA -> program; throws Unsupported when it does not fit
+std::vector<uint64_t> bpg_program(const Nfa& cnfa, bool uword);
+
 // Java-semantics backtracking matcher (boolean Matcher.find()) for the regexes no automaton can
-// express: backreferences, lookahead / lookbehind, atomic groups, possessive quantifiers,
-// MULTILINE anchors. The same parser builds the AST (byte-level UTF-8 lowering, ASCII \b \w,
-// CI flag), which is compiled to a small backtracking program run in Java's priority order
-// (greedy/reluctant, left alternative first) -- so atomic / possessive constructs keep exactly
-// the matches Java keeps. Host-only; the device prefilter narrows it to candidate lines.
+// express: backreferences, lookahead / lookbehind, atomic groups, possessive quantifiers. The same
+// parser builds the AST, lowered to UTF-8 bytes (ASCII or Unicode \b, CI flags), which is compiled
+// to a small backtracking program run in Java's priority order (greedy/reluctant, left
+// alternative first) -- so atomic / possessive constructs keep exactly the matches Java keeps.
+// Host-only; the device prefilter narrows it to candidate lines.
 class BtRegex {
  public:
   explicit BtRegex(const std::string& pattern);    // throws SyntaxError / Unsupported
@@ -121,5 +160,9 @@ class BtRegex {
  private:
   std::shared_ptr<const Impl> p_;
 };
+
+// Unicode tables (unicode_tables.inc) for tests / tools: the named set (jregex key, e.g.
+// "gc:Lu", "sc:LATIN", "blk:BASICLATIN"); empty when unknown.
+CpSet unicode_set(const std::string& key);
 
 }  // namespace lp

@@ -79,6 +79,7 @@ RequestRunner::~RequestRunner() {
   if (ws_) (void)hipFree(ws_);
   if (post_ws_) (void)hipFree(post_ws_);
   if (up_host_) (void)hipHostFree(up_host_);
+  if (inj_host_) (void)hipHostFree(inj_host_);
   if (res_host_) (void)hipHostFree(res_host_);
   if (cnt_host_) (void)hipHostFree(cnt_host_);
 }
@@ -100,7 +101,7 @@ int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
                            const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
                            int D, const FreqRing& ring, double evict_before, double now, uint64_t stream,
-                           int64_t host_cap, WindowTurn* turn, int64_t seq) {
+                           int64_t host_cap, WindowTurn* turn, int64_t seq, const int64_t* inj, int64_t ninj) {
   // a shared window: released on every exit, also when a HIP call throws
   struct Release {
     WindowTurn* t;
@@ -181,7 +182,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   uint8_t* text = nullptr;
   int32_t* blk = nullptr;
   int64_t *ls = nullptr, *hits = nullptr, *hit_off = nullptr, *ev_cnt = nullptr, *ev_end = nullptr, *cnt = nullptr;
-  int64_t *gh = nullptr, *cand = nullptr, *ver = nullptr;
+  int64_t *gh = nullptr, *cand = nullptr, *ver = nullptr, *inj_dev = nullptr;
   int32_t *ll = nullptr, *hit_line = nullptr, *dlo = nullptr, *dhi = nullptr;
   int64_t *dg0 = nullptr, *dn = nullptr;
   // event-stage buffers (results layout: [score f64 x E | counts i64 x K1 | line | pattern | seg i32 x E])
@@ -232,7 +233,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   for (int attempt = 0;; ++attempt) {
     const int64_t cap_g = (int64_t)((double)L * rate_gram_ * 1.25) + 512;
     const int64_t cap_c = (int64_t)((double)L * rate_cand_ * 1.25) + 512;
-    const int64_t cap_v = (int64_t)((double)L * rate_ver_ * 1.25) + 512;
+    const int64_t cap_v = (int64_t)((double)L * rate_ver_ * 1.25) + 512 + ninj;
     const int64_t n = cap_c + cap_v;
     // device-count mode: a request on the single-workgroup paths runs matching, CSR, events,
     // score and the (gated) frequency record without the mid-batch host read
@@ -260,6 +261,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       hit_off = reinterpret_cast<int64_t*>(dev(8 * (size_t)(S_.R + 1)));
       ev_cnt = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
       ev_end = reinterpret_cast<int64_t*>(dev(8 * (size_t)n));
+      inj_dev = ninj > 0 ? reinterpret_cast<int64_t*>(dev(8 * (size_t)ninj)) : nullptr;
       if (fast) carve_events(ecap_small);
       if (pass == 0 && ws_used_ > ws_cap_) {   // nothing in flight uses the workspace here
         check(hipStreamSynchronize(st), "sync before growth");
@@ -297,6 +299,14 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       scan_multi_dev(text, nbytes, ls, ll, L, S_.scans[i], ver, cap_v, c0 + 2, S_.scan_grids[i], stream);
     if (S_.n_scan_regs)
       scan_dev(text, ls, ll, L, S_.scan_regs, S_.n_scan_regs, S_.dfa, ver, cap_v, c0 + 2, stream);
+    if (ninj > 0) {   // the backtracker regexes' host-verified hits (Engine.host_hits), pre-verified
+      if (attempt == 0) {
+        grow<true>(inj_host_, inj_cap_, 8 * (size_t)ninj);
+        std::memcpy(inj_host_, inj, 8 * (size_t)ninj);
+      }
+      check(hipMemcpyAsync(inj_dev, inj_host_, 8 * (size_t)ninj, hipMemcpyHostToDevice, st), "host hits H2D");
+      append_keys_dev(ver, cap_v, c0 + 2, inj_dev, ninj, stream);
+    }
     blk_index_dev(ls, L, nblk, blk, stream);
     prefilter_dev(text, nbytes, S_.pf, ls, L, gh, cap_g, c0, S_.pf_grid, stream);
     pf_verify_dev(gh, cap_g, text, nbytes, S_.pf, ls, L, blk, cand, cap_c, c0 + 1, stream, c0,

@@ -105,7 +105,7 @@ class RequestRunner {
   int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
               const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0,
-              WindowTurn* turn = nullptr, int64_t seq = 0);
+              WindowTurn* turn = nullptr, int64_t seq = 0, const int64_t* inj = nullptr, int64_t ninj = 0);
   // the batch's frequency record was enqueued (a failure after it must not record the batch again)
   bool recorded() const { return recorded_; }
   // host bytes the single-copy upload needs (text padded, index, segments, counters, carry)
@@ -117,6 +117,8 @@ class RequestRunner {
 
  private:
   uint8_t* dev(size_t bytes);          // carve from the device workspace (grown between runs)
+  uint8_t* inj_host_ = nullptr;        // pinned staging of host-verified keys (backtracker side path)
+  size_t inj_cap_ = 0;
   RequestStatic S_;
   // matcher capacity rates per line (as ops/kernels.py MatchArena)
   double rate_gram_ = 0.08, rate_cand_ = 0.03, rate_ver_ = 0.01;

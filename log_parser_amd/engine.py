@@ -378,138 +378,68 @@ class Engine:
             TR.mark(timings, name, self.device)
         return t0
 
-    def match_candidates(self, text, nbytes, ls, ll, host_text=None, timings=None) -> Tuple[torch.Tensor, int]:
+    def match_candidates(self, text, nbytes, ls, ll, host_text=None, timings=None,
+                         inj: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, int]:
         """(regex << 32 | line) candidates: ``[:pre_from]`` prefilter candidates still to DFA-verify
         (verified inside the post-match pipeline), ``[pre_from:]`` hits of engines that verify
-        themselves (literal-free DFA scan, MFMA NFA, host backtracker). Duplicates allowed.
-        ``host_text``: the same bytes on the host (uint8 array), if the caller has them."""
+        themselves (literal-free DFA scan, MFMA NFA, the host backtracker's side path). Duplicates
+        allowed. ``host_text``: the same bytes on the host (uint8 array), if the caller has them;
+        ``inj``: the backtracker side path's keys when the caller ran it (``host_hits``)."""
         timings = {} if timings is None else timings
+        if inj is None:
+            inj = self.host_hits(text, nbytes, host_text)
         t = self._start(timings)
         cand = K.prefilter(text, nbytes, self.tabs["pf"], ls, self.cand_cap, self.pf_grid)
         t = self._tick(timings, "prefilter", t)
         extra = []
-        fb = None
-        if self.lib.host_regs and cand.numel():
-            # candidates of host-fallback regexes are verified by the host backtracker, not a DFA
-            is_host = self.tabs["host_is"][(cand >> 32).long()]
-            if bool(is_host.any()):
-                fb = cand[is_host]
-                cand = cand[~is_host]
         for sp in self.tabs["scan_passes"]:        # literal-free regexes: multi-regex DFAs in LDS
             extra.append(K.scan_multi(text, nbytes, ls, ll, sp, max(1024, ls.numel() >> 6), self.scan_grid(sp)))
         if self.tabs["scan_regs"].numel():        # one whose DFA alone exceeds a scan group
             extra.append(K.scan(text, ls, ll, self.tabs["scan_regs"], self.tabs["dfa"], max(1024, ls.numel())))
-        for ncls, glist in self.tabs["nfa_scan_lists"].items():       # DFA blow-up regexes: MFMA NFA
+        for ncls, glist in self.tabs["nfa_scan_lists"].items():       # engine.nfa-engine=mfma
             if glist.numel():
                 extra.append(K.nfa_scan(self.tabs["nfa_tables"], glist, ncls, text, ls, ll, max(1024, ls.numel())))
-        if self.lib.host_regs:
-            extra.append(self._host_fallback(text, nbytes, ls, ll, host_text, fb))
+        if inj is not None and inj.numel():
+            extra.append(inj)
         if extra:
             t = self._tick(timings, "scan", t)
             return torch.cat([cand] + extra), cand.numel()
         return cand, cand.numel()
 
-    def _host_fallback(self, text, nbytes, ls, ll, host_text, fb_cand) -> torch.Tensor:
-        """Host backtracker (jregex BtRegex, Java semantics) for the regexes no automaton
-        expresses (backreferences, lookaround, atomic groups, possessive quantifiers): regexes with
-        required literals are checked on their prefilter candidate lines only (the device gathers
-        each candidate's line start / length; one small D2H); literal-free ones on every line.
-        Text bytes come from ``host_text`` (serving: the pinned staging buffer) or one D2H. The
-        few constructs the backtracker lacks (e.g. unicode properties) use the Python oracle."""
-        lib = self.lib
-        dev = text.device
-        keys: List[np.ndarray] = []
-        bt = lib.host_bt
-        py_regs = [r for r in lib.host_regs if lib.host_local[r] < 0]
-        need_all = bool([r for r in lib.host_scan_regs if lib.host_local[r] >= 0]) or \
-            any(not lib.regexes[r].literals for r in py_regs)
+    def host_hits(self, text, nbytes: int, host_text=None, ls_h=None, ll_h=None) -> Optional[torch.Tensor]:
+        """The host backtracker's side path (non-regular regexes -- backreferences,
+        lookaround, atomic groups, possessive quantifiers -- on C++ BtRegex): run BEFORE the device
+        pipeline on the host copy of the bytes, so its verified (regex << 32 | line) keys join the
+        device matchers' hits (``match_and_hits(inject=...)``, the native runner's ``inj``) and no
+        host round trip, veto of the native runner or of the deferred DP step sits in a batch.
+        Lines holding one of a regex's required literals are checked, every line without one.
+        ``ls_h`` / ``ll_h``: the batch's host line index (serving), else a Java split of the one
+        document / shard (the device line index's rule). None without backtracker regexes."""
+        if not self.lib.host_plan:
+            return None
         hb = host_text
-        gathered = None
-        if hb is None and not need_all and text.is_cuda:
-            # only candidate lines travel to the host: gather their bytes on the device (a DP shard
-            # of 1+ GB never crosses PCIe for a handful of backreference candidates)
-            gathered = self._gather_candidate_lines(text, ls, ll, fb_cand)
-            hb = gathered[0]
-        elif hb is None:
+        if hb is None:
             hb = text[:nbytes].cpu().numpy()
-        hb = np.ascontiguousarray(hb)
+        return torch.from_numpy(self._host_keys(hb, nbytes, ls_h, ll_h)).to(text.device)
+
+    def _host_keys(self, hb, nbytes: int, ls_h=None, ll_h=None) -> np.ndarray:
+        lib = self.lib
+        hb = np.ascontiguousarray(np.asarray(hb, dtype=np.uint8)[:nbytes])
         if hb.size == 0:
             hb = np.zeros(1, np.uint8)
-        lines_h = None                                # (starts, lens) of all lines, on demand
-        if fb_cand is not None and fb_cand.numel():
-            if gathered is not None:
-                kc, st, ln = gathered[1:]
-            else:
-                x = (fb_cand & 0xFFFFFFFF).long()
-                pack = torch.stack([fb_cand, ls[x], ll[x].to(torch.int64)]).cpu().numpy()
-                _, first = np.unique(pack[0], return_index=True)    # one check per (regex, line)
-                kc, st, ln = (np.ascontiguousarray(pack[i][first]) for i in range(3))
-            out = np.empty(kc.size, np.int64)
-            nv = bt.verify(hb.ctypes.data, kc.ctypes.data, st.ctypes.data, ln.ctypes.data, kc.size,
-                           lib.host_local.ctypes.data, lib.host_local.size, out.ctypes.data)
-            keys.append(out[:nv])
-            if py_regs:
-                keys.append(self._python_fallback(hb, kc, st, ln, set(py_regs)))
-        scan = [r for r in lib.host_scan_regs if lib.host_local[r] >= 0]
-        if scan or any(not lib.regexes[r].literals for r in py_regs):
-            ls_h = np.ascontiguousarray(ls.cpu().numpy())
-            ll_h = np.ascontiguousarray(ll.cpu().numpy())
-            lines_h = (ls_h, ll_h)
-        if scan:
-            keys.append(bt.scan(hb.ctypes.data, ls_h.ctypes.data, ll_h.ctypes.data, ls_h.size,
-                                [int(lib.host_local[r]) for r in scan], scan))
-        py_scan = [r for r in py_regs if not lib.regexes[r].literals]
-        if py_scan:
-            L = lines_h[0].size
-            kc = np.array([(r << 32) | i for r in py_scan for i in range(L)], np.int64)
-            st = np.tile(lines_h[0], len(py_scan)).astype(np.int64)
-            ln = np.tile(lines_h[1], len(py_scan)).astype(np.int64)
-            keys.append(self._python_fallback(hb, kc, st, ln, set(py_scan)))
-        if bt is not None and bt.exhausted:
-            log.warning("host backtracker: %d line matches exceeded the step budget (treated as no match)",
-                        bt.exhausted)
-        allk = np.concatenate(keys) if keys else np.zeros(0, np.int64)
-        return torch.from_numpy(allk).to(dev)
-
-    @staticmethod
-    def _gather_candidate_lines(text, ls, ll, fb_cand):
-        """Unique (regex, line) candidates -> (compact host bytes of their lines, keys, starts in
-        the compact buffer, lengths): one gather on the device, one D2H of the candidate lines."""
-        if fb_cand is None or not fb_cand.numel():
-            return np.zeros(1, np.uint8), None, None, None
-        keys = torch.unique(fb_cand)
-        lines = keys & 0xFFFFFFFF
-        ul, inv = torch.unique(lines, return_inverse=True)
-        st = ls[ul]
-        ln = ll[ul].to(torch.int64)
-        off = torch.cumsum(ln, 0) - ln
-        total = int(ln.sum().item()) if ul.numel() else 0
-        if total:
-            rep = torch.repeat_interleave(torch.arange(ul.numel(), device=text.device), ln)
-            pos = st[rep] + (torch.arange(total, device=text.device) - off[rep])
-            buf = text[pos].cpu().numpy()
+        if ls_h is not None:
+            ls_h = np.ascontiguousarray(ls_h, np.int64)
+            ll_h = np.ascontiguousarray(ll_h, np.int32)
+            lsp, llp, nl = ls_h.ctypes.data, ll_h.ctypes.data, ls_h.size
         else:
-            buf = np.zeros(1, np.uint8)
-        kc = keys.cpu().numpy()
-        return buf, kc, np.ascontiguousarray(off[inv].cpu().numpy()), np.ascontiguousarray(ln[inv].cpu().numpy())
-
-    def _python_fallback(self, hb: np.ndarray, kc, st, ln, regs: set) -> np.ndarray:
-        out = []
-        cache = {}
-        for k, a, n in zip(kc.tolist(), st.tolist(), ln.tolist()):
-            r = k >> 32
-            if r not in regs:
-                continue
-            rx = cache.get(r)
-            if rx is None:
-                try:
-                    rx = cache[r] = compile_java(self.lib.regexes[r].pattern)
-                except Exception:  # noqa: BLE001 - an untranslatable fallback regex never matches
-                    log.error("host fallback cannot compile %r", self.lib.regexes[r].pattern)
-                    rx = cache[r] = False
-            if rx and rx.search(bytes(hb[a:a + n]).decode("utf-8", errors="surrogateescape")) is not None:
-                out.append(k)
-        return np.array(out, np.int64)
+            lsp = llp = nl = 0
+        loc, glob, lits = zip(*lib.host_plan)
+        keys = lib.host_bt.prepass(hb.ctypes.data, int(nbytes), lsp, llp, nl, True, list(loc), list(glob),
+                                   [list(x) for x in lits])
+        if lib.host_bt.exhausted:
+            log.warning("host backtracker: %d line matches exceeded the step budget (treated as no match)",
+                        lib.host_bt.exhausted)
+        return keys
 
     def scan_grid(self, sp: tuple) -> int:
         """Persistent grid of k_scan_multi: as many blocks per CU as the pass's LDS blob allows."""
@@ -535,7 +465,7 @@ class Engine:
         result to ``prepare(early=...)``). None when the matcher arena path does not apply.
         ``nlp``: the line index's pass-1 outputs -- the prefilter then also writes them (see
         ``fuses_line_index``)."""
-        if not text.is_cuda or self.lib.host_regs or self.profile:
+        if not text.is_cuda or self.profile:
             return None
         return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid, nlp)
 
@@ -545,18 +475,18 @@ class Engine:
         GPU A/B is in."""
         import os
         pf = self.lib.pf
-        return (text.is_cuda and not self.lib.host_regs and not self.profile
+        return (text.is_cuda and not self.profile
                 and bool((pf["gmask"] & 28) or pf["teddy_lits"]) and os.environ.get("LP_FUSED_NL", "0") == "1")
 
     def can_defer(self, text) -> bool:
         """``prepare(defer=True)`` applies: device text, every matcher on the arena path, and the
         bucket-sorted post path (csrc/kernels/post_bulk.hip: device-count events)."""
         import os
-        return (text.is_cuda and not self.lib.host_regs and not self.profile and self.context_engine != "mfma"
-                and os.environ.get("LP_POST_SORT", "") != "rocprim")
+        return text.is_cuda and not self.profile and self.context_engine != "mfma"
 
     def prepare(self, text, nbytes, ls, ll, segs: Segments, host_text=None,
-                timings: Optional[dict] = None, early=None, defer: bool = False) -> "Prepared":
+                timings: Optional[dict] = None, early=None, defer: bool = False,
+                host_index: Optional[tuple] = None) -> "Prepared":
         """Local phase: matching, hit CSR, events, in-batch frequency ranks, context features.
 
         Needs no global information, so the data-parallel path runs it before its collectives.
@@ -565,15 +495,18 @@ class Engine:
         ``defer`` (``can_defer``): no read at all -- hits and events run in device-count mode on
         capacity-sized buffers (``Prepared.cnt`` / ``caps``); the caller reads the counts once its
         whole step is queued and re-runs the step if a buffer overflowed.
+        ``host_text`` / ``host_index`` (line starts, lengths): host copies of the batch for the
+        backtracker side path (``host_hits``; a multi-document batch needs its index).
         """
         timings = {} if timings is None else timings
         L = ls.numel()
         t = 0.0
         evt = self._ev_tables(segs)
+        inj = self.host_hits(text, nbytes, host_text, *(host_index or (None, None)))
         if defer:
             hits, hit_line, hit_off, ev_cnt, ev_end, nh_cap, cnt, caps = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
-                self.scan_grid, side=self._side, early=early, defer=True)
+                self.scan_grid, side=self._side, early=early, defer=True, inject=inj)
             nkeys = len(self.lib.freq_ids)
             ne_cap = caps["ev"]
             out_buf = K.results_buffer(ne_cap, nkeys, text.device)
@@ -582,15 +515,16 @@ class Engine:
                 ctx_ext=self.lib.ctx_dfa_extent, out=out_buf, dcounts=cnt[3:5], ne_fit=cnt[5:6])
             return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
                             hit_line, feat, L, timings, out_buf=out_buf, cnt=cnt, caps=caps)
-        if text.is_cuda and not self.lib.host_regs:
+        if text.is_cuda:
             # every matcher appends to fixed-capacity device buffers; ONE host read after the CSR
             self._start(timings)
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
                 self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None,
-                side=self._side, early=early)
+                side=self._side, early=early, inject=inj)
         else:
-            cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings)
+            cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings,
+                                              inj=inj if inj is not None else torch.zeros(0, dtype=torch.int64, device=text.device))
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.post_hits(
                 cand, pre, L, self.lib.n_regexes, text, ls, ll, self.tabs["dfa"], evt, self.ws)
         t = self._tick(timings, "verify_csr", t)
@@ -603,7 +537,7 @@ class Engine:
         if not dfa_feats:           # A/B engine: context features on the MFMA NFA kernel
             lines = torch.nonzero(cov[:L] > 0).flatten().to(torch.int32)
             feat = K.nfa_features(self.tabs["nfa_tables"], lines, L, text, ls, ll, self.tabs["nfa_ctx_list"],
-                                  self.lib.nfa_group_ncls[0])
+                                  self.lib.nfa_ctx_ncls)
         self._tick(timings, "events_context_freq", t)
         return Prepared(ev_line, ev_pat, ev_seg, ev_rank, ev_fkey, freq_counts[:max(nkeys, 1)], hits, hit_off,
                         hit_line, feat, L, timings, out_buf=out_buf)
@@ -839,7 +773,7 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            res = self._run_job(job, text, n, ls, ll, segs, self.freq_carry(), hb[:n], verbose, tm)
+            res = self._run_job(job, text, n, ls, ll, segs, self.freq_carry(), hb[:n], verbose, tm, (ls_h, ll_h))
             if not job.recorded:
                 self.commit_frequency(res.freq_counts)
                 job.recorded = True
@@ -854,7 +788,7 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            res = self._run_job(job, text, n, ls, ll, segs, carry, hb[:n], verbose, tm)
+            res = self._run_job(job, text, n, ls, ll, segs, carry, hb[:n], verbose, tm, (ls_h, ll_h))
             with TR.HostTimer(tm, "d2h"):
                 job.ev = self._results_to_host(res)
             if not job.recorded:
@@ -868,7 +802,7 @@ class Engine:
             segs = Segments(lo, hi, lo, hi, g0, nn)
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
-            prep = self.prepare(text, n, ls, ll, segs, host_text=hb[:n], timings=tm)
+            prep = self.prepare(text, n, ls, ll, segs, host_text=hb[:n], timings=tm, host_index=(ls_h, ll_h))
             turn.wait(seq)                     # earlier batches have recorded their counts
             res = self.finish(prep, segs, self._carry_before(job, prep, self.freq_carry()), with_factors=verbose)
             with TR.HostTimer(tm, "d2h"):
@@ -895,8 +829,9 @@ class Engine:
         c[:k] = (c[:k] - prep.freq_counts[:k].to(c.device, c.dtype)).clamp(min=0)
         return c
 
-    def _run_job(self, job: "BatchJob", text, n, ls, ll, segs, carry, host_text, verbose, tm) -> RunResult:
-        prep = self.prepare(text, n, ls, ll, segs, host_text, tm)
+    def _run_job(self, job: "BatchJob", text, n, ls, ll, segs, carry, host_text, verbose, tm,
+                 host_index=None) -> RunResult:
+        prep = self.prepare(text, n, ls, ll, segs, host_text, tm, host_index=host_index)
         return self.finish(prep, segs, self._carry_before(job, prep, carry), with_factors=verbose)
 
     def _window_quiet(self) -> None:
@@ -913,7 +848,7 @@ class Engine:
         if self._runner is False or tm is not None or verbose or job.n_lines < 0 or job.recorded:
             return False
         if self._runner is None:
-            ok = (self.device.type == "cuda" and self.freq_on_device and not self.lib.host_regs
+            ok = (self.device.type == "cuda" and self.freq_on_device
                   and self.context_engine != "mfma" and bool(self.config.get("engine.native-runner", True))
                   and not any(g.numel() for g in self.tabs["nfa_scan_lists"].values()))
             if not ok:
@@ -948,6 +883,9 @@ class Engine:
         st = job.stage
         args = (st.buf.data_ptr(), n, st.starts(job.n_lines).data_ptr(), st.lens(job.n_lines).data_ptr(), job.n_lines,
                 lo, hi, g0, nn)
+        inj = np.zeros(0, np.int64)
+        if self.lib.host_plan:              # the backtracker's side path, on the pinned host bytes
+            inj = self._host_keys(st.buf[:n].numpy(), n, st.starts(job.n_lines).numpy(), st.lens(job.n_lines).numpy())
         if turn is None:
             with fr._lock:
                 if K:
@@ -956,7 +894,8 @@ class Engine:
                 now = fr._now()                              # record_tensor()
                 # host_cap: the stage's room behind the text lets the runner send text, line index,
                 # segments and zeroed counters in ONE H2D copy (request.cpp, single-copy layout)
-                ne, out, counts, E = self._runner.run(*args, fr._ring(), evict_before, now, stream, st.buf.numel())
+                ne, out, counts, E = self._runner.run(*args, fr._ring(), evict_before, now, stream, st.buf.numel(),
+                                                      inj=inj)
                 if K:
                     fr._tail_bound += K
         else:
@@ -974,7 +913,7 @@ class Engine:
                 turn.host.done(seq)
             try:
                 ne, out, counts, E = self._runner.run(*args, ring, evict_before, now, stream, st.buf.numel(),
-                                                      turn=turn.dev, seq=seq)
+                                                      turn=turn.dev, seq=seq, inj=inj)
             except BaseException:
                 job.recorded = bool(self._runner.recorded)
                 raise

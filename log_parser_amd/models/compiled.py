@@ -13,10 +13,13 @@ noted in SURVEY §5.2). Here the whole library is compiled once into:
 * **pattern tables** for the fused score kernel (confidence, severity multiplier, context rules,
   secondary / sequence descriptors, frequency key).
 
-Regexes the automaton engine cannot express (backrefs, lookaround, possessive/atomic groups,
-DFA blow-up) are matched by the host fallback (``regex/javacompat.py``); syntactically invalid
-regexes never match and are reported at load (the reference would fail every request with a
-``PatternSyntaxException`` -> HTTP 500).
+Every regular Java regex runs on the device: a byte DFA when its subset construction fits
+``engine.dfa-max-states``, otherwise (bounded gaps ``X.{0,1000}Y``, repeated groups, MULTILINE
+anchors, Unicode ``\b``) a bit-parallel Glushkov program over code points (``jregex.cpp``
+bpg_program, ``csrc/kernels/bpg.h``). Only non-regular regexes (backreferences, lookaround,
+possessive / atomic groups) use the host backtracker, as a side path run before the device
+pipeline (``Engine.host_hits``); syntactically invalid regexes never match and are reported at load
+(the reference would fail every request with a ``PatternSyntaxException`` -> HTTP 500).
 """
 from __future__ import annotations
 
@@ -30,7 +33,6 @@ import torch
 from ..golden import CONTEXT_REGEXES, SEVERITY_MULTIPLIERS, java_blank, severity_key
 from ..native import N
 from ..utils.config import ScoringParams
-from .bpg import build_program
 from .nfa import build_group, fits_group, pack_groups
 from .schema import Pattern, PatternSet, pattern_to_json
 
@@ -331,9 +333,7 @@ class CompiledLibrary:
         if r not in self.bpg_regs:
             raise KeyError(f"regex {r} is not a BPG program")
         o = int(self.dfa_meta[r, 0])
-        h = int(self.bpg_pool[o])
-        W, E, ncls = h & 0xFF, (h >> 8) & 0xFFF, (h >> 20) & 0x3FF
-        return self.bpg_pool[o:o + 1 + 36 * W + 32 + ncls * W + E * (W + 1)]
+        return self.bpg_pool[o:o + int(self.bpg_pool[o + 1] >> np.uint64(32))]
 
     def _compile_regexes(self):
         meta, bytemaps, trans, accs = [], [], [], []
@@ -345,6 +345,7 @@ class CompiledLibrary:
         self.scan_regs: List[int] = []
         self.host_regs: List[int] = []
         self.host_bt_ok: List[bool] = []
+        self.host_lits: List[List[bytes]] = []        # backtracker regexes' required literals (host side path)
         nfa_members: List[Tuple[int, dict]] = []
         ctx_members: List[Tuple[int, dict]] = []
         for i, ri in enumerate(self.regexes):
@@ -381,11 +382,15 @@ class CompiledLibrary:
                 if not lits:
                     self.scan_regs.append(i)
             else:
-                prog = build_program(d) if ri.kind == KIND_NFA and self.nfa_engine == "bpg" else None
+                prog = None
+                mfma_ok = ri.kind == KIND_NFA and d["npos"] > 0 and not d["cp_only"] and fits_group(d)
+                if ri.kind == KIND_NFA and d["bpg"] and (self.nfa_engine == "bpg" or not mfma_ok):
+                    prog = np.frombuffer(d["bpg"], np.uint64)
                 if prog is not None:
-                    # DFA blow-up (bounded gaps X.{0,120}Y, repeated groups): a bit-parallel Glushkov
-                    # program, dispatched by the same verify / scan kernels as the DFAs (meta bit 1)
-                    ri.nstates = int(d["npos"])
+                    # DFA blow-up (bounded gaps X.{0,1000}Y, repeated groups) or code-point contexts
+                    # (MULTILINE anchors, Unicode \b): a bit-parallel Glushkov program over code
+                    # points, dispatched by the verify / scan kernels next to the DFAs (meta bit 1)
+                    ri.nstates = int(prog[0] & np.uint64(0xFF)) * 64
                     meta.append([boff, 1, 0, 2])
                     bytemaps.append(np.zeros(256, np.uint8))
                     bpgs.append(prog)
@@ -402,56 +407,59 @@ class CompiledLibrary:
                 bytemaps.append(np.zeros(256, np.uint8))
                 if ri.kind == KIND_INVALID:
                     log.error("invalid regex %r: %s (never matches)", ri.pattern, ri.error)
-                elif ri.kind == KIND_NFA and fits_group(d):
-                    # DFA blow-up: simulate the NFA with the MFMA state-transition kernel
+                elif mfma_ok:
+                    # engine.nfa-engine=mfma: simulate the NFA with the MFMA state-transition kernel
                     nfa_members.append((i, d))
                 else:
-                    # non-regular (backref, lookaround, atomic, possessive) or too large for the
-                    # automata: the native backtracker on the host, narrowed to prefilter
-                    # candidate lines through the regex's required literals when it has some
+                    # non-regular (backref, lookaround, atomic, possessive): the native backtracker on
+                    # the host, as a side path before the device pipeline (Engine.host_hits) --
+                    # lines holding a required literal, or every line without one
                     log.info("regex %r runs on the host backtracker (%s)", ri.pattern, ri.error)
+                    if not d.get("bt_ok"):
+                        log.error("regex %r: no engine runs it (%s); it never matches", ri.pattern, ri.error)
                     self.host_regs.append(i)
                     self.host_bt_ok.append(bool(d.get("bt_ok")))
                     lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
-                    if lits and min(len(x) for x in lits) >= MIN_LITERAL and ri.roles != {"context"}:
-                        ri.literals = lits
+                    self.host_lits.append(lits if lits and min(len(x) for x in lits) >= MIN_LITERAL else [])
         # a dummy DFA for non-DFA regexes: state 2 -> DEAD on every byte (never read: not scanned)
         if not trans:
             trans.append(np.zeros(1, np.uint16))
             accs.append(np.zeros(1, np.uint8))
-        # NFA groups for the MFMA kernel: group 0 = the 4 context regexes, then DFA-blow-up regexes
-        groups = [ctx_members] + pack_groups(nfa_members)
+        # NFA groups for the MFMA kernel: the 4 context regexes first (one or two groups: the exact
+        # UTF-8 '.' of the stack-frame regex costs ~10 positions), then DFA-blow-up regexes
+        ctx_groups = pack_groups(ctx_members)
+        groups = ctx_groups + pack_groups(nfa_members)
         tabs, ncls = zip(*[build_group(g) for g in groups])
         self.nfa_tables = np.concatenate(tabs)
         self.nfa_group_ncls = list(ncls)
-        self.nfa_scan_groups = list(range(1, len(groups)))
-        self.nfa_regs = [rid for g in groups[1:] for rid, _ in g]
+        self.nfa_ctx_groups = list(range(len(ctx_groups)))
+        self.nfa_ctx_ncls = max(ncls[:len(ctx_groups)])
+        self.nfa_scan_groups = list(range(len(ctx_groups), len(groups)))
+        self.nfa_regs = [rid for g in groups[len(ctx_groups):] for rid, _ in g]
         self._build_scan_passes()
         self.scan_regs_single = self.scan_regs_single + self.bpg_scan_regs
         self._build_host_matchers()
         self.bpg_pool = np.concatenate(bpgs) if bpgs else np.zeros(1, np.uint64)
         self.bpg_widths = 0                  # bit W: a program of W words exists (bpg.hip launches)
-        for b in bpgs:
-            self.bpg_widths |= 1 << int(b[0] & np.uint64(0xFF))
+        for b in bpgs:        # (bit 31 stands for 32 words)
+            self.bpg_widths |= 1 << min(31, int(b[0] & np.uint64(0xFF)))
         self.dfa_meta = np.array(meta, np.int32).reshape(-1, 4)
         self.dfa_bytemap = np.concatenate(bytemaps)
         self.dfa_trans = np.concatenate(trans)
         self.dfa_acc = np.concatenate(accs)
 
     def _build_host_matchers(self):
-        """Host-fallback regexes: native Java-semantics backtrackers (jregex BtRegex) for all it
-        supports; the rest (e.g. unicode properties) keep the Python oracle translation."""
+        """Backtracker regexes: native Java-semantics backtrackers (jregex BtRegex); a regex the
+        backtracker rejects as well (e.g. \\N{name}) never matches (logged at load)."""
         self.host_bt = N.BtSet([self.regexes[r].pattern for r in self.host_regs]) if self.host_regs else None
         R = len(self.regexes)
         self.host_local = np.full(max(R, 1), -1, np.int32)      # global regex id -> index in host_bt
         for k, r in enumerate(self.host_regs):
             if self.host_bt is not None and self.host_bt.ok(k):
                 self.host_local[r] = k
-        self.host_is = np.zeros(max(R, 1), bool)
-        self.host_is[self.host_regs] = True
-        # split: candidates from the prefilter (literal) vs every line (no literal)
-        self.host_lit_regs = [r for r in self.host_regs if self.regexes[r].literals]
-        self.host_scan_regs = [r for r in self.host_regs if not self.regexes[r].literals]
+        # (local index, global id, required literals) of every runnable backtracker regex
+        self.host_plan = [(int(self.host_local[r]), r, lits) for r, lits in zip(self.host_regs, self.host_lits)
+                          if self.host_local[r] >= 0]
 
     # multi-regex DFA scan groups (csrc/kernels/scan_multi.hip)
     SCAN_GROUP_REGS = 16            # members per multi-regex DFA (16-bit accept masks)
@@ -706,7 +714,6 @@ class CompiledLibrary:
         t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr(),
                     self.bpg_widths)
         t["scan_regs"] = T(np.array(self.scan_regs_single, np.int32))
-        t["host_is"] = T(self.host_is)
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
         t["scan_passes"] = [(b.data_ptr(), p["lds_words"], p["ngroups"], p["row_base"], p["stride"], p["thr"],
                              p["init_row"], p["init_state"], p["ncol"], p["gt_off"], p["fin_off"], p["bm_off"],
@@ -725,7 +732,7 @@ class CompiledLibrary:
         t["freq_key"] = T(self.freq_key)
         t["is_primary"] = T(np.diff(self.prim_off) > 0)
         t["nfa_tables"] = T(self.nfa_tables.view(np.int64))
-        t["nfa_ctx_list"] = T(np.zeros(1, np.int32))
+        t["nfa_ctx_list"] = T(np.array(self.nfa_ctx_groups, np.int32))
         t["nfa_scan_lists"] = {k: T(np.array([g for g in self.nfa_scan_groups if self.nfa_group_ncls[g] == k], np.int32))
                                for k in (1, 2, 3)}
         self._device_cache[key] = t

@@ -257,11 +257,14 @@ def scan_multi(text, nbytes: int, line_start, line_len, pass_tuple, cap: int, gr
 
 def nfa_features(groups: torch.Tensor, lines: torch.Tensor, L: int, text, line_start, line_len,
                  group_list: torch.Tensor, ncls: int) -> torch.Tensor:
-    """Context features via the MFMA NFA kernel (group 0 = the 4 context regexes): uint8 bits per line."""
+    """Context features via the MFMA NFA kernel (``group_list`` = the groups of the 4 context
+    regexes, one launch each: a group ORs its members' bits into the line's byte): uint8 bits per line."""
     feat = torch.zeros(max(L, 1), dtype=torch.uint8, device=text.device)
     if lines.numel():
-        N.nfa(groups.data_ptr(), group_list.data_ptr(), 1, ncls, lines.data_ptr(), lines.numel(), text.data_ptr(),
-              line_start.data_ptr(), line_len.data_ptr(), feat.data_ptr(), 0, 0, 0, _s(text), text.is_cuda)
+        for k in range(group_list.numel()):
+            N.nfa(groups.data_ptr(), group_list[k:k + 1].data_ptr(), 1, ncls, lines.data_ptr(), lines.numel(),
+                  text.data_ptr(), line_start.data_ptr(), line_len.data_ptr(), feat.data_ptr(), 0, 0, 0, _s(text),
+                  text.is_cuda)
     return feat
 
 
@@ -442,7 +445,8 @@ class EarlyPrefilter:
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
                    ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None, side=None,
-                   early: Optional[EarlyPrefilter] = None, defer: bool = False):
+                   early: Optional[EarlyPrefilter] = None, defer: bool = False,
+                   inject: Optional[torch.Tensor] = None):
     """GPU: every matcher appends to the arena, then the post-match hit pipeline reads the device
     counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read.
 
@@ -454,15 +458,20 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
     single-DFA scan, MFMA NFA) run on that stream, concurrently with the literal prefilter chain
     (block index -> prefilter -> verify) on the current one; both join before the hit pipeline.
     A small request's kernels are latency-bound and leave most CUs idle, so the two chains
-    overlap almost fully."""
+    overlap almost fully.
+
+    ``inject``: device keys verified elsewhere (the host backtracker's side path,
+    ``Engine.host_hits``), appended to the verified-hit buffer like a self-verifying engine's."""
     dev = text.device
     L = line_start.numel()
     st = _s(text)
     lbits, rbits = N.bits_for(max(L, 1)), N.bits_for(max(R, 1))
     scans = bool(tabs["scan_passes"]) or bool(tabs["scan_regs"].numel()) or \
         any(g.numel() for g in tabs["nfa_scan_lists"].values())
+    ninj = 0 if inject is None else inject.numel()
     while True:
         cap = arena.caps(L)
+        cap["ver"] += ninj
         if early is not None:            # prefilter already queued (behind the line index)
             cap["gram"] = early.cap
             gh, cnt = early.gh, early.cnt
@@ -492,6 +501,8 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             if glist.numel():
                 N.nfa(tabs["nfa_tables"].data_ptr(), glist.data_ptr(), glist.numel(), ncls, 0, L, text.data_ptr(),
                       line_start.data_ptr(), line_len.data_ptr(), 0, ver.data_ptr(), cap["ver"], c0 + 16, sst, True)
+        if ninj:
+            N.append_keys(ver.data_ptr(), cap["ver"], c0 + 16, inject.data_ptr(), ninj, sst)
         if sst != st:
             side[2].record(side[0])
         elif tick:

@@ -9,6 +9,14 @@ Java 21 defaults reproduced: ``\\w \\d \\s \\b`` and CASE_INSENSI
 ``.`` excludes ``\\n \\r \\u0085 \\u2028 \\u2029``; without MULTILINE ``$`` / ``\\Z`` match at the end
 of input or before a final line terminator; ``\\z`` is the absolute end; ``\\h``/``\\v``/``\\R`` are
 Java's horizontal/vertical whitespace and linebreak; POSIX ``\\p{..}`` classes are ASCII.
+
+Character classes are evaluated here as explicit code-point range sets (nesting, negation,
+``&&`` intersection, predefined and property escapes, CASE_INSENSITIVE closure) and emitted as
+ranges; ``\\p{..}`` names are resolved with Java's rules (``In`` block / ``Is`` property, category
+or script / ``name=value`` / POSIX, CharPredicates) against the generated Unicode tables
+(``N.unicode_set``); ``(?U)`` switches ``\\w \\d \\s \\b`` and POSIX classes to Unicode and, with
+``(?iu)``, case-insensitive literals and ranges use Java's simple upper / lower case mappings
+(``Character.toUpperCase`` / ``toLowerCase``, built here from Python's ``str.upper`` / ``lower``).
 """
 from __future__ import annotations
 
@@ -37,6 +45,194 @@ _POSIX = {
 
 class UnsupportedJavaRegex(ValueError):
     pass
+
+
+# ---- explicit code-point sets (sorted disjoint ranges) --------------------------------------
+MAXCP = 0x10FFFF
+
+
+def _norm(rs):
+    out = []
+    for lo, hi in sorted(rs):
+        if out and lo <= out[-1][1] + 1:
+            if hi > out[-1][1]:
+                out[-1] = (out[-1][0], hi)
+        else:
+            out.append((lo, hi))
+    return out
+
+
+def _neg(rs):
+    out, nxt = [], 0
+    for lo, hi in rs:
+        if lo > nxt:
+            out.append((nxt, lo - 1))
+        nxt = hi + 1
+    if nxt <= MAXCP:
+        out.append((nxt, MAXCP))
+    return out
+
+
+def _inter(a, b):
+    out, i, j = [], 0, 0
+    while i < len(a) and j < len(b):
+        lo, hi = max(a[i][0], b[j][0]), min(a[i][1], b[j][1])
+        if lo <= hi:
+            out.append((lo, hi))
+        if a[i][1] < b[j][1]:
+            i += 1
+        else:
+            j += 1
+    return out
+
+
+def _chr(c: int) -> str:
+    return "\\U%08x" % c
+
+
+def _emit(rs, neg=False) -> str:
+    if neg:
+        rs = _neg(_norm(rs))
+    rs = _norm(rs)
+    if not rs:
+        return "(?!)"
+    return "[" + "".join(_chr(lo) if lo == hi else _chr(lo) + "-" + _chr(hi) for lo, hi in rs) + "]"
+
+
+@functools.lru_cache(maxsize=None)
+def _uset(key: str):
+    from ..native import N
+    return tuple((int(a), int(b)) for a, b in N.unicode_set(key))
+
+
+@functools.lru_cache(maxsize=1)
+def _case_pairs():
+    """(c, upper(c)) and (c, lower(c)) pairs of Java's simple case mappings (single code point)."""
+    up, lo = {}, {}
+    for c in range(MAXCP + 1):
+        if 0xD800 <= c <= 0xDFFF:
+            continue
+        ch = chr(c)
+        u, w = ch.upper(), ch.lower()
+        if len(u) == 1 and u != ch:
+            up[c] = ord(u)
+        if len(w) == 1 and w != ch:
+            lo[c] = ord(w)
+    adj = {}
+    for m in (up, lo):
+        for a, b in m.items():
+            adj.setdefault(a, set()).add(b)
+            adj.setdefault(b, set()).add(a)
+    return up, lo, adj
+
+
+def _case_variants(c: int, unicode_case: bool):
+    """Code points equal to c under Java CASE_INSENSITIVE (ASCII) / + UNICODE_CASE (SingleU)."""
+    if not unicode_case:
+        if 97 <= c <= 122:
+            return [c, c - 32]
+        if 65 <= c <= 90:
+            return [c, c + 32]
+        return [c]
+    up, lo, adj = _case_pairs()
+    key = lambda x: lo.get(up.get(x, x), up.get(x, x))  # noqa: E731
+    seen, todo, out = {c}, [c], []
+    while todo:
+        x = todo.pop()
+        if key(x) == key(c):
+            out.append(x)
+        for y in adj.get(x, ()):
+            if y not in seen:
+                seen.add(y)
+                todo.append(y)
+    return out
+
+
+def _ci_range(lo: int, hi: int, unicode_case: bool):
+    """Java CIRange / CIRangeU: ch matches when its (ASCII / simple) upper or lower case is in range."""
+    rs = [(lo, hi)]
+    if not unicode_case:
+        for c in range(65, 91):
+            if lo <= c + 32 <= hi:
+                rs.append((c, c))
+            if lo <= c <= hi:
+                rs.append((c + 32, c + 32))
+        return rs
+    up, low, _ = _case_pairs()
+    for m in (up, low):
+        for a, b in m.items():
+            if lo <= b <= hi:
+                rs.append((a, a))
+    return rs
+
+
+_JPOSIX = {"ALPHA", "LOWER", "UPPER", "SPACE", "PUNCT", "XDIGIT", "ALNUM", "CNTRL", "DIGIT", "BLANK", "GRAPH",
+           "PRINT"}
+
+
+def _prop_ranges(name: str, ci: bool, uclass: bool):
+    """Java Pattern.family: \\p{name} -> code-point ranges (raises UnsupportedJavaRegex if unknown)."""
+    def get(key):
+        rs = _uset(key)
+        return list(rs) if rs else None
+
+    def gc(nm):
+        return (get("gci:" + nm) if ci else None) or get("gc:" + nm)
+
+    def uprop(nm):
+        nm = nm.upper()
+        return (get("upi:" + nm) if ci else None) or get("up:" + nm)
+
+    def script(nm):
+        r = get("sc:" + nm.upper())
+        if r is None:
+            raise UnsupportedJavaRegex("Unknown character script name {%s}" % nm)
+        return r
+
+    def block(nm):
+        r = get("blk:" + nm.upper())
+        if r is None:
+            raise UnsupportedJavaRegex("Unknown character block name {%s}" % nm)
+        return r
+
+    if "=" in name:
+        k, v = name.split("=", 1)
+        k = k.lower()
+        if k in ("sc", "script"):
+            return script(v)
+        if k in ("blk", "block"):
+            return block(v)
+        if k in ("gc", "general_category") and gc(v) is not None:
+            return gc(v)
+        raise UnsupportedJavaRegex("Unknown Unicode property {%s}" % name)
+    if name.startswith("In"):
+        return block(name[2:])
+    if name.startswith("Is"):
+        r = uprop(name[2:]) or gc(name[2:])
+        return r if r is not None else script(name[2:])
+    if uclass and name.upper() in _JPOSIX:
+        return uprop(name)
+    r = gc(name)
+    if r is None:
+        raise UnsupportedJavaRegex("Unknown character property name {%s}" % name)
+    return r
+
+
+def _escape_ranges(e: str, uclass: bool):
+    """(ranges, negated) of a predefined class escape letter."""
+    low = e.lower()
+    if low == "d":
+        rs = list(_uset("u:digit")) if uclass else [(48, 57)]
+    elif low == "s":
+        rs = list(_uset("u:space")) if uclass else [(9, 13), (32, 32)]
+    elif low == "w":
+        rs = list(_uset("u:word")) if uclass else [(48, 57), (65, 90), (95, 95), (97, 122)]
+    elif low == "h":
+        rs = [(0x20, 0x20), (9, 9), (0xA0, 0xA0), (0x1680, 0x1680), (0x180E, 0x180E), (0x2000, 0x200A),
+              (0x202F, 0x202F), (0x205F, 0x205F), (0x3000, 0x3000)]
+    else:  # v
+        rs = [(0x0A, 0x0D), (0x85, 0x85), (0x2028, 0x2029)]
+    return rs, e.isupper()
 
 
 def _class_body_for_escape(esc: str, neg: bool):
@@ -82,11 +278,15 @@ def _char_escape(p: str, i: int):
     return None
 
 
-def _posix(p: str, i: int):
-    """p[i] is 'p' or 'P'. Returns (body, negated, new_i) for a bracket-able class."""
+def _prop_name(p: str, i: int):
+    """p[i] is 'p' or 'P'. Returns (name, negated, new_i)."""
     neg = p[i] == "P"
+    if i + 1 >= len(p):
+        raise UnsupportedJavaRegex("Illegal character family")
     if p[i + 1] == "{":
-        j = p.index("}", i + 2)
+        j = p.find("}", i + 2)
+        if j < 0:
+            raise UnsupportedJavaRegex("Unclosed character family")
         name = p[i + 2:j]
         ni = j + 1
     else:
@@ -95,19 +295,70 @@ def _posix(p: str, i: int):
     if name.startswith("^"):
         neg = not neg
         name = name[1:]
-    key = name[2:] if name.startswith("Is") and name[2:] in _POSIX else name
-    if key in _POSIX:
-        return _POSIX[key], neg, ni
-    # unicode property: let the regex module interpret it
-    return None, (("\\P{%s}" if neg else "\\p{%s}") % name), ni
+    return name, neg, ni
+
+
+def _char_escape_cp(p: str, i: int):
+    """Java single-char escape at p[i] (after the backslash) -> (code point, new_i) or None."""
+    c = p[i]
+    simple = {"t": 9, "n": 10, "r": 13, "f": 12, "a": 7, "e": 27}
+    if c in simple:
+        return simple[c], i + 1
+    if c == "0":
+        j = i + 1
+        digs = ""
+        while j < len(p) and len(digs) < 3 and p[j] in "01234567":
+            digs += p[j]
+            j += 1
+        if not digs:
+            raise UnsupportedJavaRegex("illegal octal escape")
+        if int(digs, 8) > 0o377:
+            digs = digs[:-1]
+            j -= 1
+        return int(digs, 8), j
+    if c == "x":
+        if i + 1 < len(p) and p[i + 1] == "{":
+            j = p.index("}", i + 2)
+            return int(p[i + 2:j], 16), j + 1
+        return int(p[i + 1:i + 3], 16), i + 3
+    if c == "u":
+        v = int(p[i + 1:i + 5], 16)
+        j = i + 5
+        if 0xD800 <= v < 0xDC00 and p.startswith("\\u", j):
+            lo = int(p[j + 2:j + 6], 16)
+            if 0xDC00 <= lo < 0xE000:
+                return 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00), j + 6
+        return v, j
+    if c == "c":
+        return ord(p[i + 1]) ^ 64, i + 2
+    if not c.isalnum():
+        return ord(c), i + 1
+    return None
+
+
+def _lit(cp: int, sc) -> str:
+    """One literal code point under the scope's case flags."""
+    if sc["i"] and (sc["u"] or sc["U"]):
+        v = _case_variants(cp, True)
+        if len(v) > 1:
+            return _emit([(x, x) for x in v])
+    return _re.escape(chr(cp))
+
+
+def _word_boundary(neg: bool) -> str:
+    """Unicode \\b / \\B ((?U)): Java's WORD predicate on both sides."""
+    w = _emit(list(_uset("u:word")))
+    if neg:
+        return "(?:(?<=%s)(?=%s)|(?<!%s)(?!%s))" % (w, w, w, w)
+    return "(?:(?<=%s)(?!%s)|(?<!%s)(?=%s))" % (w, w, w, w)
 
 
 @functools.lru_cache(maxsize=65536)
 def to_python(pattern: str) -> str:
     p = pattern
     out = []
-    # scope stack: dict(dotall, multiline, unix, comments, pending_closes)
-    scopes = [dict(s=False, m=False, d=False, x=False, close=0)]
+    # scope stack: dict(dotall, multiline, unix, comments, ci, unicode case, unicode class, pending closes)
+    scopes = [dict(s=False, m=False, d=False, x=False, i=False, u=False, U=False, close=0)]
     i = 0
     n = len(p)
 
@@ -120,7 +371,7 @@ def to_python(pattern: str) -> str:
             ch = p[j]
             if ch == "-":
                 neg = True
-            elif ch in "idmsuxU":
+            elif ch in "idmsuxUc":
                 if neg:
                     off += ch
                 else:
@@ -133,10 +384,10 @@ def to_python(pattern: str) -> str:
     def apply(scope, on, off):
         s = dict(scope)
         for ch, v in [(c, True) for c in on] + [(c, False) for c in off]:
-            if ch in "smdx":
+            if ch in "smdxiu":
                 s[ch] = v
             elif ch == "U":
-                raise UnsupportedJavaRegex("UNICODE_CHARACTER_CLASS")
+                s["U"] = s["u"] = v          # UNICODE_CHARACTER_CLASS implies UNICODE_CASE
         return s
 
     def ci_prefix(on, off):
@@ -166,27 +417,20 @@ def to_python(pattern: str) -> str:
             if e == "Q":
                 j = p.find("\\E", i + 1)
                 lit = p[i + 1:] if j < 0 else p[i + 1:j]
-                out.append(_re.escape(lit))
+                out.append("".join(_lit(ord(ch), sc) for ch in lit))
                 i = n if j < 0 else j + 2
                 continue
             if e in "dDsSwWhHvV":
-                body, neg = _class_body_for_escape(e, False)
-                out.append(("[^%s]" if neg else "[%s]") % body)
+                rs, neg = _escape_ranges(e, sc["U"])
+                out.append(_emit(rs, neg))
                 i += 1
                 continue
             if e in "pP":
-                body, neg, i = _posix(p, i)
-                if body is None:
-                    out.append(neg)
-                else:
-                    out.append(("[^%s]" if neg else "[%s]") % body)
+                name, neg, i = _prop_name(p, i)
+                out.append(_emit(_prop_ranges(name, sc["i"], sc["U"]), neg))
                 continue
-            if e == "b":
-                out.append("\\b")
-                i += 1
-                continue
-            if e == "B":
-                out.append("\\B")
+            if e in "bB":
+                out.append(_word_boundary(e == "B") if sc["U"] else "\\" + e)
                 i += 1
                 continue
             if e == "A":
@@ -225,15 +469,15 @@ def to_python(pattern: str) -> str:
                 out.append("\\" + p[i:j])
                 i = j
                 continue
-            r = _char_escape(p, i)
+            r = _char_escape_cp(p, i)
             if r is None:
                 raise UnsupportedJavaRegex("unknown escape \\%s" % e)
-            out.append(r[0])
+            out.append(_lit(r[0], sc))
             i = r[1]
             continue
         if c == "[":
-            body, i = _parse_class(p, i)
-            out.append(body)
+            rs, i = _class_set(p, i, sc)
+            out.append(_emit(rs))
             continue
         if c == ".":
             out.append("(?s:.)") if sc["s"] else out.append(DOT_UNIX if sc["d"] else DOT)
@@ -241,13 +485,16 @@ def to_python(pattern: str) -> str:
             continue
         if c == "$":
             if sc["m"]:
-                out.append(EOL_MULTI)
+                out.append(r"(?=\n|\Z)" if sc["d"] else EOL_MULTI)
             else:
                 out.append(EOL_UNIX if sc["d"] else EOL)
             i += 1
             continue
         if c == "^":
-            out.append(BOL_MULTI if sc["m"] else "\\A")
+            if sc["m"]:
+                out.append(r"(?:\A|(?<=\n))(?!\Z)" if sc["d"] else BOL_MULTI)
+            else:
+                out.append("\\A")
             i += 1
             continue
         if c == "(":
@@ -311,21 +558,24 @@ def to_python(pattern: str) -> str:
             out.append(p[i:j + 1])
             i = j + 1
             continue
-        out.append(_re.escape(c) if c not in "*+?" else c)
+        out.append(c if c in "*+?" else _lit(ord(c), sc))
         i += 1
     out.append(")" * cur()["close"])
     return "".join(out)
 
 
-def _parse_class(p: str, i: int):
-    """Parse a Java character class starting at p[i]=='['; supports nested unions (flattened)."""
+def _class_set(p: str, i: int, sc):
+    """Java character class at p[i] == '[' -> (code-point ranges, new_i): nested unions, '&&'
+    intersections, negation of the whole class, predefined / property escapes, ranges, and the
+    scope's CASE_INSENSITIVE (ASCII or UNICODE_CASE) closure of literal characters and ranges."""
     assert p[i] == "["
     i += 1
     neg = False
     if i < len(p) and p[i] == "^":
         neg = True
         i += 1
-    parts = []
+    ci, uc, U = sc["i"], sc["u"] or sc["U"], sc["U"]
+    cur_rs, acc = [], None
     first = True
     while True:
         if i >= len(p):
@@ -336,58 +586,63 @@ def _parse_class(p: str, i: int):
             break
         first = False
         if c == "[":
-            sub, i = _parse_class(p, i)
-            if sub.startswith("[^"):
-                raise UnsupportedJavaRegex("negated nested class")
-            parts.append(sub[1:-1])
+            sub, i = _class_set(p, i, sc)
+            cur_rs += sub
             continue
         if c == "&" and p.startswith("&&", i):
-            raise UnsupportedJavaRegex("class intersection")
+            i += 2
+            acc = _norm(cur_rs) if acc is None else _inter(acc, _norm(cur_rs))
+            cur_rs = []
+            continue
         if c == "\\":
+            if i + 1 >= len(p):
+                raise UnsupportedJavaRegex("bad class escape")
             e = p[i + 1]
             if e == "Q":
                 j = p.find("\\E", i + 2)
-                lit = p[i + 2:j]
-                parts.append("".join(_cls_escape(ch) for ch in lit))
-                i = j + 2
+                end = len(p) if j < 0 else j
+                for ch in p[i + 2:end]:
+                    cur_rs += [(v, v) for v in (_case_variants(ord(ch), uc) if ci else [ord(ch)])]
+                i = len(p) if j < 0 else j + 2
                 continue
             if e in "dDsSwWhHvV":
-                body, ng = _class_body_for_escape(e, False)
-                if ng:
-                    if len(parts) == 0 and p[i + 2] == "]" and not neg:
-                        # [\D] alone
-                        return "[^%s]" % body, i + 3
-                    raise UnsupportedJavaRegex("negated escape inside class")
-                parts.append(body)
+                rs, ng = _escape_ranges(e, U)
+                cur_rs += _neg(_norm(rs)) if ng else rs
                 i += 2
                 continue
             if e in "pP":
-                body, ng, ni = _posix(p, i + 1)
-                if body is None or ng:
-                    raise UnsupportedJavaRegex("unicode/negated property in class")
-                parts.append(body)
-                i = ni
+                name, ng, i = _prop_name(p, i + 1)
+                rs = _prop_ranges(name, ci, U)
+                cur_rs += _neg(_norm(rs)) if ng else rs
                 continue
-            r = _char_escape(p, i + 1)
+            r = _char_escape_cp(p, i + 1)
             if r is None:
                 raise UnsupportedJavaRegex("bad class escape")
-            parts.append(r[0] if r[0].startswith("\\") else _cls_escape(r[0].replace("\\", "")))
-            i = r[1]
-            continue
-        if c == "-" and parts and i + 1 < len(p) and p[i + 1] not in "]":
-            parts.append("-")
+            lo, i = r
+        else:
+            lo = ord(c)
             i += 1
-            continue
-        parts.append(_cls_escape(c))
-        i += 1
-    body = "".join(parts)
-    return ("[^%s]" if neg else "[%s]") % body, i
-
-
-def _cls_escape(ch: str) -> str:
-    if ch in "\\]^-[":
-        return "\\" + ch
-    return ch
+        if i + 1 < len(p) and p[i] == "-" and p[i + 1] not in "][":
+            i += 1
+            if p[i] == "\\":
+                r = _char_escape_cp(p, i + 1)
+                if r is None:
+                    raise UnsupportedJavaRegex("Illegal character range")
+                hi, i = r
+            else:
+                hi = ord(p[i])
+                i += 1
+            if hi < lo:
+                raise UnsupportedJavaRegex("Illegal character range")
+            cur_rs += _ci_range(lo, hi, uc) if ci else [(lo, hi)]
+        else:
+            cur_rs += [(v, v) for v in (_case_variants(lo, uc) if ci else [lo])]
+    res = _norm(cur_rs)
+    if acc is not None:
+        res = _inter(acc, res)
+    if neg:
+        res = _neg(res)
+    return res, i
 
 
 @functools.lru_cache(maxsize=65536)

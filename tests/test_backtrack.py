@@ -90,7 +90,8 @@ def test_backtracker_classification():
     d = N.compile_regex(r"(\w+) failed: \1")
     assert d["kind"] == 2 and d["bt_ok"] and d["literals"] == [b" failed: "]
     assert N.compile_regex(r"(?<=a*)b")["kind"] == 3               # Java: no obvious maximum length
-    assert not N.compile_regex(r"\p{InGreek}")["bt_ok"]           # unicode blocks: Python oracle
+    assert N.compile_regex(r"\p{InGreek}")["kind"] == 0           # unicode blocks: a byte DFA
+    assert N.BtSet([r"(\p{InGreek})\1"]).find(0, "xΣΣ")          # ... and in the backtracker
 
 
 def _library():
@@ -110,7 +111,7 @@ def test_engine_with_backtracking_regexes_matches_golden():
     lib = CompiledLibrary(sets, p)
     s = lib.summary()
     assert s["host_fallback"] >= 6 and s["host_backtracker"] == s["host_fallback"]
-    assert lib.host_lit_regs and lib.host_scan_regs
+    assert any(lits for _, _, lits in lib.host_plan) and any(not lits for _, _, lits in lib.host_plan)
     logs = make_log(3000, trig, seed=18, hit_rate=0.1, crlf_rate=0.05)
     eng = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
     r = eng.analyze(logs)
@@ -170,9 +171,9 @@ def test_backref_pattern_cost_on_a_million_lines(gpu_device):
 
 
 @pytest.mark.gpu
-def test_host_regex_candidates_gathered_on_device(gpu_device):
-    """Without host bytes (the data-parallel shard path) only the candidate lines of the host
-    regexes cross PCIe: same hits as with the whole text on the host."""
+def test_host_regex_side_path_without_host_bytes(gpu_device):
+    """Without host bytes the side path copies the text to the host once: same hits as with the
+    caller's host copy."""
     from log_parser_amd.ops import kernels as K
     p = ScoringParams()
     sets, trig = _library()
@@ -183,7 +184,7 @@ def test_host_regex_candidates_gathered_on_device(gpu_device):
         {"id": f"h{i}", "name": rx, "severity": "LOW", "primary_pattern": {"regex": rx, "confidence": 0.5}}
         for i, rx in enumerate(lits)]})
     lib = CompiledLibrary(sets[:-1] + [extra], p)
-    assert lib.host_lit_regs and not lib.host_scan_regs
+    assert lib.host_plan and all(lits for _, _, lits in lib.host_plan)
     data = make_log(20000, trig, seed=21, hit_rate=0.05).encode()
     t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
     t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)

@@ -1,5 +1,6 @@
-"""Bit-parallel Glushkov programs (models/bpg.py, csrc/kernels/bpg.h) for regexes whose DFA blows
-up -- bounded gaps ``X.{0,120}Y``, repeated groups, boundary-gated edges. The reference runs
+"""Bit-parallel Glushkov programs over code points (jregex.cpp bpg_program, csrc/kernels/bpg.h) for
+regexes whose DFA blows up -- bounded gaps ``X.{0,1000}Y``, repeated groups, boundary-gated edges --
+or that need code-point contexts (MULTILINE ``^ $``, Unicode ``\b``). The reference runs
 ``Pattern.compile(rx).matcher(line).find()`` for every regex role (AnalysisService.java:62-65,93-95;
 secondaries ScoringService.java:315-347), so these must give exactly Java's boolean find():
 checked against the javacompat oracle (pure Python twin, native host twin, gfx950 kernel) and end
@@ -12,7 +13,7 @@ import torch
 
 from log_parser_amd import golden
 from log_parser_amd.engine import Engine
-from log_parser_amd.models.bpg import build_program, decompose, program_info, run_program
+from log_parser_amd.models.bpg import program_info, run_program
 from log_parser_amd.models.compiled import CompiledLibrary
 from log_parser_amd.native import N
 from log_parser_amd.ops import kernels as K
@@ -26,12 +27,20 @@ GAP_PATS = [
     r"(?i)\bfoo\b.{0,40}bar", r"x.{0,3}y", r"^\s*at .{0,50}\(", r"(?i)(?:fail|error|fatal).{0,30}(?:disk|volume|mount)\b",
     r"\b\d{1,3}(?:\.\d{1,3}){3}\b.{0,80}(?:refused|reset|timed out)", r"(a|bc)+d.{0,20}e", r"a.{2,5}b$",
     r"(?i)é.{0,9}z\B", r"(?:ab|cd){2,4}.{0,30}x+y?z",
+    # wide gaps (> 512 positions at byte level), MULTILINE anchors, Unicode classes / \b
+    r"Connection refused.{0,600}port \d+", r"error.{0,300}timeout.{0,300}retry", r"X.{0,1000}Y",
+    r"(?m)^ERROR$", r"(?m)fail$.{0,5}", r"(?U)\bfoo\w*\b.{0,20}bar", r"\p{L}+Exception.{0,50}at",
+    r"[^é]x.{0,40}y", r"(?iu)ÉCOLE.{0,30}\p{Lu}",
 ]
 POS = ["Connection refused by 10.0.0.1 on port 80", "pod a in namespace b c failed", "error: x timeout y retry",
        "at com.acme.FooException: bad Caused by", "FOO, then bar", "x12y", "  at x(", "Fatal: no disk",
-       "10.0.0.1 said hi refused", "abcbcd123e", "aééb", "ÉabcZz", "abcd...xxz"]
+       "10.0.0.1 said hi refused", "abcbcd123e", "aééb", "ÉabcZz", "abcd...xxz",
+       "Connection refused " + "x" * 580 + "port 8", "error " + "é" * 280 + "timeout" + "y" * 250 + "retry",
+       "X" + "z" * 990 + "Y", "boom\rERROR", "ERROR\u2028x", "it fail\u0085", "fooé bar", "féoo xbar",
+       "ÉcoleException at", "zx oy", "école 1 Ä"]
 ALPHA = "abcdefxyz .:()é\tÉ" + "Connection refused port 123 pod in namespace failed error timeout retry " \
-        "java.lang.FooException Caused by foo bar FOO at 10.0.0.1 disk volume\r"
+        "java.lang.FooException Caused by foo bar FOO at 10.0.0.1 disk volume\r" \
+        "ERROR fail X Y \u0085\u2028\u2029 école ÉCOLE Ä 日本 x y"
 
 
 def _lines(rng, n):
@@ -46,16 +55,18 @@ def _lines(rng, n):
 
 
 def test_decomposition_is_exact_and_compact():
+    """jregex builds every shape into an exact program (bpg_program checks the decomposition) with
+    few exception rows; the wide bounded gaps need none."""
     for p in GAP_PATS:
         d = N.compile_regex(p, 64, 4096)
-        assert d["kind"] in (0, 1)
-        decompose(d["npos"], d["nfa_follow"])           # asserts the parts rebuild every follow set
-        info = program_info(build_program(d))
-        assert info["exceptions"] <= 4, (p, info)
-    # the verdict's bounded-gap shapes all blow up the DFA and need no exception edges
-    for p in GAP_PATS[:3]:
+        assert d["kind"] in (0, 1), (p, d["error"])
+        if d["kind"] == 1:
+            assert d["bpg"], (p, d["error"])
+            assert program_info(d["bpg"])["exceptions"] <= 4, (p, program_info(d["bpg"]))
+    for p in GAP_PATS[:3] + GAP_PATS[13:16]:
         d = N.compile_regex(p, 2048, 4096)
-        assert d["kind"] == 1 and program_info(build_program(d))["exceptions"] == 0
+        assert d["kind"] == 1 and program_info(d["bpg"])["exceptions"] == 0, p
+    assert program_info(N.compile_regex(r"X.{0,1000}Y")["bpg"])["words"] == 16
 
 
 @pytest.mark.parametrize("seed", [0, 1])
@@ -63,10 +74,14 @@ def test_python_twin_matches_java_oracle(seed):
     rng = random.Random(seed)
     lines = _lines(rng, 400)
     for p in GAP_PATS:
-        prog = build_program(N.compile_regex(p, 64, 4096))
+        d = N.compile_regex(p, 64, 4096)
+        if d["kind"] != 1:
+            continue
         rx = compile_java(p)
         for s in lines:
-            assert run_program(prog, s.encode()) == (rx.search(s) is not None), (p, s)
+            want = rx.search(s) is not None
+            assert run_program(d["bpg"], s.encode()) == want, (p, s)
+            assert N.bpg_find(d["bpg"], s.encode()) == want, (p, s)
 
 
 def _lib(pats):
@@ -159,7 +174,9 @@ COOP_LIBS = [
     ([r"ab.{0,10}cd", r"x.{0,3}y", r"(a|bc)+d.{0,20}e", r"(?i)é.{0,3}z\B"], 8),
     (GAP_PATS[4:6], 64),
     (GAP_PATS[4:], 64),
-    (GAP_PATS + [r"a.{0,150}b", r"(?i)error.{0,220}\bdisk"], 64),
+    (GAP_PATS[:13] + [r"a.{0,150}b", r"(?i)error.{0,220}\bdisk"], 64),
+    (GAP_PATS, 64),                                   # up to 16 words -> G = 32
+    ([r"a.{0,1500}b", r"(?m)^x$"], 64),               # 24 words -> G = 64
 ]
 
 

@@ -95,19 +95,41 @@ def _bounded_gap(rng: random.Random, tok: str, i: int) -> Tuple[str, str, str, s
     return rx, sm, srx, ssm
 
 
+def _java_shape(rng: random.Random, tok: str, i: int) -> Tuple[str, str]:
+    """The Java regex shapes a byte-DFA engine cannot hold, + a matching sample (planted after an
+    ASCII noise prefix): wide bounded gaps (> 512 byte positions), Unicode properties, MULTILINE
+    anchors inside a line (after U+2028), Unicode \\b, partial non-ASCII classes, UNICODE_CASE."""
+    fam = i % 7
+    if fam == 0:
+        return rf"{tok} refused.{{0,600}}port \d+", f"{tok} refused by upstream 10.0.0.7 on port 8443"
+    if fam == 1:
+        return rf"(?i)error.{{0,300}}{tok}.{{0,300}}retry", f"ERROR while calling {tok} (état dégradé), will retry"
+    if fam == 2:
+        return rf"\p{{Lu}}\p{{L}}+{tok}Exception", f"caught Élan{tok}Exception in worker"
+    if fam == 3:
+        return rf"(?m)^\[{tok}\] (?:FATAL|ERROR)$", f"\u2028[{tok}] FATAL"
+    if fam == 4:
+        return rf"(?U)\b{tok}\w*Fehler\b", f"{tok}größeFehler erkannt"
+    if fam == 5:
+        return rf"[^\sé]+ {tok} échec", f"job-7 {tok} échec"
+    return rf"(?iu){tok}: ÉCHEC .{{0,40}}Ä", f"{tok.upper()}: échec du contrôleur ä"
+
+
 def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate: float = 0.7,
                  sequence_rate: float = 0.4, feature_mix: bool = True, short_literal_rate: float = 0.0,
-                 literal_free_rate: float = 0.0, gap_rate: float = 0.0) -> Tuple[List[PatternSet], List[dict]]:
+                 literal_free_rate: float = 0.0, gap_rate: float = 0.0,
+                 java_shape_rate: float = 0.0) -> Tuple[List[PatternSet], List[dict]]:
     """Returns (pattern sets, trigger descriptions used by ``make_log`` to plant matches).
 
-    ``short_literal_rate`` / ``literal_free_rate`` / ``gap_rate``: shares of primaries whose only
-    literal is a 3-6-byte code, that have no usable literal at all, or that are bounded-gap regexes
-    whose DFA blows up (``realistic_library``)."""
+    ``short_literal_rate`` / ``literal_free_rate`` / ``gap_rate`` / ``java_shape_rate``: shares of
+    primaries whose only literal is a 3-6-byte code, that have no usable literal at all, that are
+    bounded-gap regexes whose DFA blows up, or that use the Unicode / MULTILINE / wide-gap shapes of
+    ``_java_shape`` (``realistic_library``)."""
     rng = random.Random(seed)
     sets = [{"metadata": {"library_id": f"synthetic-lib-{s}", "version": "1.0"}, "patterns": []}
             for s in range(n_sets)]
     triggers = []
-    n_free = n_gap = 0
+    n_free = n_gap = n_java = 0
     for i in range(n_patterns):
         tok = _token(rng, i)
         style = rng.randrange(8) if feature_mix else 0
@@ -118,8 +140,13 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
             style = 9
         elif u < literal_free_rate + short_literal_rate + gap_rate:
             style = 10
+        elif u < literal_free_rate + short_literal_rate + gap_rate + java_shape_rate:
+            style = 11
         gap_sec = None
-        if style == 10:
+        if style == 11:
+            regex, sample = _java_shape(rng, tok, n_java)
+            n_java += 1
+        elif style == 10:
             regex, sample, srx, ssm = _bounded_gap(rng, tok, n_gap)
             gap_sec = (srx, ssm)
             n_gap += 1
@@ -185,12 +212,15 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
 
 def realistic_library(n_patterns: int, seed: int = 0, **kw):
     """The headline bench library: the synthetic mix plus ~10% primaries with only a 3-6-byte
-    literal, ~5% literal-free primaries and ~1.5% bounded-gap primaries (``X.{0,120}Y``, each
-    with a bounded-gap secondary) -- the shapes real libraries have (short error codes, IP:port,
-    `^\\s+at ...` stack frames, "refused ... port N") and the matcher's worst cases."""
+    literal, ~5% literal-free primaries, ~1.5% bounded-gap primaries (``X.{0,120}Y``, each
+    with a bounded-gap secondary) and ~1% Unicode / MULTILINE / wide-gap shapes
+    (``X.{0,600}Y``, ``\\p{L}``, ``(?m)^..$``, ``(?U)\\b``, ``[^é]``, ``(?iu)``) -- the shapes real
+    libraries have (short error codes, IP:port, `^\\s+at ...` stack frames, "refused ... port N")
+    and the matcher's worst cases."""
     kw.setdefault("short_literal_rate", 0.10)
     kw.setdefault("literal_free_rate", 0.05)
     kw.setdefault("gap_rate", 0.015)
+    kw.setdefault("java_shape_rate", 0.01)
     return make_library(n_patterns, seed=seed, **kw)
 
 

@@ -130,8 +130,8 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
         # the ingest copy stream is created before RCCL creates its own: HIP maps streams to a few
         # hardware queues in creation order (GPU_MAX_HW_QUEUES), and a copy stream created after the
         # process group can share the compute stream's queue -- the copy then waits for the step's
-        # kernels instead of overlapping them (LP_BENCH_LATE_COPY_STREAM=1 restores the old order, A/B)
-        early_copy_stream = None if os.environ.get("LP_BENCH_LATE_COPY_STREAM") == "1" else torch.cuda.Stream(device)
+        # kernels instead of overlapping them (profiles/r3_f)
+        early_copy_stream = torch.cuda.Stream(device)
         from log_parser_amd.utils.numa import bind_to_gpu_numa
         bind_to_gpu_numa(local_gpu)          # pinned ingest buffers on the GPU's own socket
     else:
@@ -149,7 +149,7 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
         if "MASTER_PORT" not in os.environ:
             from log_parser_amd.utils.launch import free_port
             os.environ["MASTER_PORT"] = str(free_port())
-        kw = {"device_id": device} if backend == "nccl" and os.environ.get("LP_BENCH_LAZY_NCCL", "0") != "1" else {}
+        kw = {"device_id": device} if backend == "nccl" else {}
         from log_parser_amd.utils.launch import stdout_to_stderr
         with stdout_to_stderr():            # RCCL prints its version banner on stdout: keep ONE JSON line
             dist.init_process_group(backend, rank=rank, world_size=world, **kw)

@@ -88,16 +88,10 @@ static int64_t copy_scan_nl_512(const uint8_t* src, uint8_t* dst, int64_t n, int
   return i;
 }
 
-// LP_PACK_NT=1: streaming stores (A/B, off by default: a 10k-line request measured 0.299-0.302 ms
+// streaming (non-temporal) stores of the pack are off: a 10k-line request measured 0.299-0.302 ms
 // with them vs 0.282 ms without -- the '\r' checks of the line pass and the JSON emitter's context
-// lines then read the stage from DRAM instead of the cache)
-static bool pack_nt_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("LP_PACK_NT");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+// lines then read the stage from DRAM instead of the cache
+static bool pack_nt_enabled() { return false; }
 
 static bool have_avx512_vbmi2() {
   static const bool ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&

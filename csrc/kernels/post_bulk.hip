@@ -675,14 +675,6 @@ struct Carve {
   }
 };
 
-bool bulk_disabled() {   // LP_POST_SORT=rocprim: the device radix-sort path (A/B)
-  static const bool off = [] {
-    const char* e = getenv("LP_POST_SORT");
-    return e && std::strcmp(e, "rocprim") == 0;
-  }();
-  return off;
-}
-
 size_t agg_lds(int nb, bool scatter) {
   return nb <= PB_LDS_BINS ? (size_t)(scatter ? 2 * nb : nb) * sizeof(uint32_t) : 0;
 }
@@ -692,7 +684,7 @@ int64_t plan_cap(int64_t np, int64_t items) { return np + 2 * (items / PB_TARGET
 
 }  // namespace
 
-bool hits_bulk_ok(const HitsArgs& A) { return !bulk_disabled() && A.lbits <= 30 && A.R > 0; }
+bool hits_bulk_ok(const HitsArgs& A) { return A.lbits <= 30 && A.R > 0; }
 
 size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
@@ -760,7 +752,7 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
   return C.used;
 }
 
-bool events_bulk_ok(const EventsArgs& A) { return !bulk_disabled() && A.lbits <= 31; }
+bool events_bulk_ok(const EventsArgs& A) { return A.lbits <= 31; }
 
 size_t events_bulk_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t ne = A.ne, L = A.L, nh = A.nh;

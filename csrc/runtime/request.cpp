@@ -51,28 +51,18 @@ T* device_view(T* host) {
   return static_cast<T*>(d);
 }
 
-bool fetch_enabled() {                 // LP_RUNNER_FETCH=0: SDMA copy of the inputs (A/B)
-  const char* e = std::getenv("LP_RUNNER_FETCH");
-  return !(e && e[0] == '0');
-}
-
-bool publish_enabled() {               // LP_RUNNER_PUBLISH=0: copy-based results (A/B)
-  const char* e = std::getenv("LP_RUNNER_PUBLISH");
-  return !(e && e[0] == '0');
-}
-
 }  // namespace
 
 RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
   check(hipSetDevice(S_.device), "set device");
   check(hipHostMalloc(reinterpret_cast<void**>(&cnt_host_), 8 * sizeof(int64_t), kCoherentHost), "pinned counters");
   cnt_host_dev_ = device_view(cnt_host_);
-  publish_ = publish_enabled();
-  fetch_ = fetch_enabled();
-  // the window eviction inside the k_fetch launch (one launch fewer): opt-in until its A/B is in
-  // (LP_RUNNER_EVICT_IN_FETCH=1; the one run so far showed an unexplained engine p99 of 1.97 ms)
-  const char* ev = std::getenv("LP_RUNNER_EVICT_IN_FETCH");
-  evict_in_fetch_ = ev && ev[0] == '1';
+  // k_fetch reads the inputs from pinned memory (no SDMA copy) and k_publish writes the results
+  // there (no copy back); the window eviction stays its own launch (inside k_fetch it showed an
+  // unexplained engine p99 of 1.97 ms)
+  publish_ = true;
+  fetch_ = true;
+  evict_in_fetch_ = false;
 }
 
 RequestRunner::~RequestRunner() {

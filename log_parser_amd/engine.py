@@ -471,12 +471,11 @@ class Engine:
 
     def fuses_line_index(self, text) -> bool:
         """The bulk step folds the line index's first pass into the literal prefilter (one read of the
-        text fewer): device text, the arena path, a library with literals. Opt-in (LP_FUSED_NL=1) until its
-        GPU A/B is in."""
-        import os
+        text fewer): device text, the arena path, a library with literals. Opt-in
+        (``engine.fused-line-index``) until its GPU A/B is in."""
         pf = self.lib.pf
-        return (text.is_cuda and not self.profile
-                and bool((pf["gmask"] & 28) or pf["teddy_lits"]) and os.environ.get("LP_FUSED_NL", "0") == "1")
+        return (text.is_cuda and not self.profile and bool(self.config.get("engine.fused-line-index", False))
+                and bool((pf["gmask"] & 28) or pf["teddy_lits"]))
 
     def can_defer(self, text) -> bool:
         """``prepare(defer=True)`` applies: device text, every matcher on the arena path, and the

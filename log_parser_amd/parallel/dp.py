@@ -60,17 +60,11 @@ def distributed() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-import os as _os
-
-# diagnostic A/B (bench): LP_DP_SKIP_WORLD1=1 skips the (data-free) world-1 collectives
-_SKIP_WORLD1 = _os.environ.get("LP_DP_SKIP_WORLD1", "0") == "1"
-
-
 def all_gather_inplace(buf: torch.Tensor, group=None) -> torch.Tensor:
     """In-place all_gather of ``buf`` [world, n]: this rank's row is already filled; on return
     every row is (RCCL all_gather_into_tensor with the input aliasing its output row)."""
     r, w = world()
-    if not distributed() or (w == 1 and _SKIP_WORLD1):
+    if not distributed():
         return buf
     if buf.is_cuda and not host_staged(group):
         dist.all_gather_into_tensor(buf, buf[r], group=group)

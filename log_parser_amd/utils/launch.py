@@ -32,7 +32,6 @@ def ensure_hw_queues(n: int = HW_QUEUES) -> int:
     processes (ranks, the server) inherit the setting. Returns the value in effect.
     """
     try:
-        n = int(os.environ.get("LP_HW_QUEUES", n))     # LP_HW_QUEUES=0: leave HIP's setting alone (A/B)
         cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "0"))
     except ValueError:
         cur = 0

@@ -240,11 +240,11 @@ def test_native_runner_device_counts_equals_host_counts(gpu_device):
     assert outs[True] == outs[False]
 
 
-def test_native_runner_fetch_publish_equal_copies(gpu_device, monkeypatch):
-    """k_fetch (inputs read from the pinned stage by a kernel) + k_publish (counters and compacted
-    results written into pinned host memory) give the same responses as the SDMA-copy paths
-    (LP_RUNNER_FETCH=0, LP_RUNNER_PUBLISH=0), over batches of several documents, an empty one and
-    a stage too small for the single-copy layout on its first use."""
+def test_native_runner_fetch_publish_equal_orchestration(gpu_device):
+    """The runner's k_fetch (inputs read from the pinned stage by a kernel) + k_publish (counters and
+    compacted results written into pinned host memory) give the same responses as the Python
+    orchestration (engine.native-runner=false), over batches of several documents, an empty one
+    and a stage too small for the single-copy layout on its first use."""
     import json
     sets, trig = make_library(200, seed=12)
     lib = CompiledLibrary(sets, ScoringParams())
@@ -252,11 +252,10 @@ def test_native_runner_fetch_publish_equal_copies(gpu_device, monkeypatch):
                [make_log(500, trig, seed=121 + i, hit_rate=0.1) for i in range(4)],
                [""], [make_log(12000, trig, seed=125, hit_rate=0.02)]]
     outs = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("LP_RUNNER_FETCH", flag)
-        monkeypatch.setenv("LP_RUNNER_PUBLISH", flag)
-        eng = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
-        outs[flag] = [[_strip(json.loads(o)) for o in eng.analyze_batch_json(b)] for b in batches]
-        assert eng._runner not in (None, False)
-    assert outs["1"] == outs["0"]
-    assert sum(len(o["events"]) for b in outs["1"] for o in b) > 50
+    for native in (True, False):
+        eng = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device), "engine.native-runner": native}),
+                     device=gpu_device)
+        outs[native] = [[_strip(json.loads(o)) for o in eng.analyze_batch_json(b)] for b in batches]
+        assert (eng._runner not in (None, False)) == native
+    assert outs[True] == outs[False]
+    assert sum(len(o["events"]) for b in outs[True] for o in b) > 50

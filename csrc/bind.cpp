@@ -740,6 +740,12 @@ PYBIND11_MODULE(_lpnative, m) {
       A.zero = P<int64_t>(u(16));
       A.nzero = a[17].cast<int64_t>();
     }
+    if (a.size() > 21) {
+      A.seq_base = P<const uint8_t>(u(18));
+      A.line_base = a[19].cast<int64_t>();
+      A.n_fixed = a[20].cast<int64_t>();
+      A.seq_next = P<uint8_t>(u(21));
+    }
     dp_carry(A, s, dev);
   });
   // veto (optional, device int64): no record when *veto != 0 (a DP step that re-runs)

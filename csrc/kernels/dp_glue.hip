@@ -50,9 +50,9 @@ LP_HD void dp_carry_one(int64_t i, const DpCarryArgs& A) {
       if (q < A.rank) before += A.g[q * row];
       veto |= A.g[q * row + row - 1];
     }
-    A.own_start[0] = before;
-    A.g0[0] = before - A.halo_left;
-    A.n[0] = total > 1 ? total : 1;
+    A.own_start[0] = A.line_base + before;
+    A.g0[0] = A.line_base + before - A.halo_left;
+    A.n[0] = A.n_fixed > 0 ? A.n_fixed : (total > 1 ? total : 1);
     if (A.veto) A.veto[0] = veto;
   }
   if (i < A.nk) {
@@ -65,7 +65,12 @@ LP_HD void dp_carry_one(int64_t i, const DpCarryArgs& A) {
   if (i < A.ns) {
     int64_t k = A.slot_k[i];
     for (int q = A.rank - 1; q >= 0 && k >= 0; --q) k = A.g[q * row + 1 + A.nk + A.slot_e0[i] + k];
-    A.seq_carry[i] = k < 0 ? 1 : 0;
+    A.seq_carry[i] = k < 0 ? 1 : (A.seq_base ? A.seq_base[A.slot_e0[i] + k] : 0);
+    if (A.seq_next) {       // the walk over every rank of the step: the state after it
+      int64_t kk = A.slot_k[i];
+      for (int q = A.world - 1; q >= 0 && kk >= 0; --q) kk = A.g[q * row + 1 + A.nk + A.slot_e0[i] + kk];
+      A.seq_next[i] = kk < 0 ? 1 : (A.seq_base ? A.seq_base[A.slot_e0[i] + kk] : 0);
+    }
   }
 }
 

@@ -164,6 +164,13 @@ struct DpCarryArgs {
   int64_t* veto = nullptr;   // [1] OR of every rank's overflow flag (may be null)
   int64_t* zero = nullptr;   // [nzero] zeroed (this rank's histogram slots of the all-gather buffer)
   int64_t nzero = 0;
+  // a stream of DP steps (parallel/stream.py ShardedStreamAnalyzer): the carries of the earlier
+  // steps -- sequence-chain state before this step, global index of its first line, an open N
+  // (chronological factor rescored at the end) -- and the state after the step (every rank composed)
+  const uint8_t* seq_base = nullptr;   // [ns] or null (= nothing matched before the step)
+  int64_t line_base = 0;
+  int64_t n_fixed = 0;                 // > 0: N written as this instead of the step's line count
+  uint8_t* seq_next = nullptr;         // [ns] or null
 };
 // payload [1 + nk + ns + 1]; cnt (device [5] match / event counters, may be null) and caps (host
 // [4]: gram, candidate, verified, event capacities) set the trailing overflow flag

@@ -406,7 +406,8 @@ class Engine:
             return torch.cat([cand] + extra), cand.numel()
         return cand, cand.numel()
 
-    def host_hits(self, text, nbytes: int, host_text=None, ls_h=None, ll_h=None) -> Optional[torch.Tensor]:
+    def host_hits(self, text, nbytes: int, host_text=None, ls_h=None, ll_h=None,
+                  trim: bool = True) -> Optional[torch.Tensor]:
         """The host backtracker's side path (non-regular regexes -- backreferences,
         lookaround, atomic groups, possessive quantifiers -- on C++ BtRegex): run BEFORE the device
         pipeline on the host copy of the bytes, so its verified (regex << 32 | line) keys join the
@@ -414,15 +415,16 @@ class Engine:
         host round trip, veto of the native runner or of the deferred DP step sits in a batch.
         Lines holding one of a regex's required literals are checked, every line without one.
         ``ls_h`` / ``ll_h``: the batch's host line index (serving), else a Java split of the one
-        document / shard (the device line index's rule). None without backtracker regexes."""
+        document / shard (the device line index's rule; ``trim=False``: a stream chunk's rule, no
+        trailing-empty-line removal). None without backtracker regexes."""
         if not self.lib.host_plan:
             return None
         hb = host_text
         if hb is None:
             hb = text[:nbytes].cpu().numpy()
-        return torch.from_numpy(self._host_keys(hb, nbytes, ls_h, ll_h)).to(text.device)
+        return torch.from_numpy(self._host_keys(hb, nbytes, ls_h, ll_h, trim)).to(text.device)
 
-    def _host_keys(self, hb, nbytes: int, ls_h=None, ll_h=None) -> np.ndarray:
+    def _host_keys(self, hb, nbytes: int, ls_h=None, ll_h=None, trim: bool = True) -> np.ndarray:
         lib = self.lib
         hb = np.ascontiguousarray(np.asarray(hb, dtype=np.uint8)[:nbytes])
         if hb.size == 0:
@@ -434,7 +436,7 @@ class Engine:
         else:
             lsp = llp = nl = 0
         loc, glob, lits = zip(*lib.host_plan)
-        keys = lib.host_bt.prepass(hb.ctypes.data, int(nbytes), lsp, llp, nl, True, list(loc), list(glob),
+        keys = lib.host_bt.prepass(hb.ctypes.data, int(nbytes), lsp, llp, nl, trim, list(loc), list(glob),
                                    [list(x) for x in lits])
         if lib.host_bt.exhausted:
             log.warning("host backtracker: %d line matches exceeded the step budget (treated as no match)",
@@ -485,7 +487,7 @@ class Engine:
 
     def prepare(self, text, nbytes, ls, ll, segs: Segments, host_text=None,
                 timings: Optional[dict] = None, early=None, defer: bool = False,
-                host_index: Optional[tuple] = None) -> "Prepared":
+                host_index: Optional[tuple] = None, split_trim: bool = True) -> "Prepared":
         """Local phase: matching, hit CSR, events, in-batch frequency ranks, context features.
 
         Needs no global information, so the data-parallel path runs it before its collectives.
@@ -495,13 +497,14 @@ class Engine:
         capacity-sized buffers (``Prepared.cnt`` / ``caps``); the caller reads the counts once its
         whole step is queued and re-runs the step if a buffer overflowed.
         ``host_text`` / ``host_index`` (line starts, lengths): host copies of the batch for the
-        backtracker side path (``host_hits``; a multi-document batch needs its index).
+        backtracker side path (``host_hits``; a multi-document batch needs its index);
+        ``split_trim=False``: the lines came from ``split_chunk_lines`` (stream chunks).
         """
         timings = {} if timings is None else timings
         L = ls.numel()
         t = 0.0
         evt = self._ev_tables(segs)
-        inj = self.host_hits(text, nbytes, host_text, *(host_index or (None, None)))
+        inj = self.host_hits(text, nbytes, host_text, *(host_index or (None, None)), trim=split_trim)
         if defer:
             hits, hit_line, hit_off, ev_cnt, ev_end, nh_cap, cnt, caps = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,

@@ -675,11 +675,14 @@ def dp_pack(own_lines: int, freq_counts: torch.Tensor, nk: int, chain: torch.Ten
 
 def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: Optional[torch.Tensor],
              slot_e0: torch.Tensor, slot_k: torch.Tensor, red_tail: Optional[torch.Tensor] = None,
-             veto_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None):
+             veto_out: Optional[torch.Tensor] = None, zero: Optional[torch.Tensor] = None,
+             stream: Optional[tuple] = None):
     """From the gathered payloads: (own_start[1], g0[1], n[1], carry[nk], seq_carry uint8[ns],
     veto[1]); ``red_tail`` (optional) receives this rank's frequency counts; veto = any rank's
     overflow flag (written into ``veto_out`` when given); ``zero`` (int64, optional) is zeroed by
-    the same kernel."""
+    the same kernel. ``stream`` = (seq_base uint8[ns], line_base, n_fixed, seq_next uint8[ns]): one
+    step of a stream of steps (the earlier steps' sequence state and line count, an open N, and the
+    sequence state after this step written into seq_next)."""
     dev = g.device
     sc = torch.empty(5, dtype=torch.int64, device=dev)          # own_start, g0, n, veto (+ pad)
     carry = torch.empty(max(nk, 1), dtype=torch.int64, device=dev)
@@ -689,9 +692,13 @@ def dp_carry(g: torch.Tensor, rank: int, nk: int, ns: int, halo_left: int, tot: 
     g = g.contiguous()
     p = sc.data_ptr()
     veto = veto_out if veto_out is not None else sc[3:4]
-    N.dp_carry((g.data_ptr(), g.shape[0], rank, nk, ns, int(halo_left), _p(tot) if nk else 0, slot_e0.data_ptr(),
-                slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail), veto.data_ptr(),
-                _p(zero), 0 if zero is None else zero.numel()), _s(g), g.is_cuda)
+    args = (g.data_ptr(), g.shape[0], rank, nk, ns, int(halo_left), _p(tot) if nk else 0, slot_e0.data_ptr(),
+            slot_k.data_ptr(), p, p + 8, p + 16, carry.data_ptr(), seq.data_ptr(), _p(red_tail), veto.data_ptr(),
+            _p(zero), 0 if zero is None else zero.numel())
+    if stream is not None:
+        sb, lb, nf, sn = stream
+        args = args + (_p(sb), int(lb), int(nf), _p(sn))
+    N.dp_carry(args, _s(g), g.is_cuda)
     return sc[0:1], sc[1:2], sc[2:3], carry, seq, veto
 
 

@@ -103,6 +103,18 @@ def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
 
 
 @dataclass
+class StreamCarry:
+    """The carries of earlier steps when a long log is streamed as a sequence of DP steps
+    (parallel/stream.py ShardedStreamAnalyzer) -- the same protocol as a chunk of one stream:
+    the frequency carry (window totals at the stream's start + every earlier step's counts), the
+    sequence-chain state before the step, and the global index of the step's first line. The
+    chronological factor's N is open (the step keeps every event's factors; rescored at the end)."""
+    freq: torch.Tensor             # int64 [max(nk, 1)]
+    seq: torch.Tensor              # uint8 [max(ns, 1)]
+    line_base: int = 0
+
+
+@dataclass
 class StepOutput:
     result: RunResult
     own_counts: torch.Tensor       # owned lines per rank (C1 all-gather), stays on the device
@@ -118,6 +130,9 @@ class StepOutput:
     events_packed: Optional[torch.Tensor] = None
     # GPU: recorded on the compute stream after the step's last kernel (before its count read)
     end_event: Optional[object] = None
+    # stream steps: the sequence-chain state after the step and the step's summed frequency counts
+    seq_next: Optional[torch.Tensor] = None
+    freq_counts: Optional[torch.Tensor] = None
 
     # host integers on demand (a host read here would stall the step's launch queue)
     @property
@@ -166,7 +181,8 @@ class ShardedAnalyzer:
 
     def step(self, text: torch.Tensor, nbytes: int, ls: Optional[torch.Tensor], ll: Optional[torch.Tensor],
              halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False,
-             pack_events: bool = False) -> StepOutput:
+             pack_events: bool = False, stream_carry: Optional[StreamCarry] = None,
+             split_trim: bool = True) -> StepOutput:
         """One shard step. ``ls`` / ``ll`` = None: the line index is built here, with the literal
         prefilter queued behind it before its host read (the GPU filters while the host waits).
 
@@ -175,7 +191,12 @@ class ShardedAnalyzer:
         queues the whole step -- event stage, both collectives, carry, score, summary, record --
         while the GPU is still matching. Each rank's overflow flag rides in collective 1; any
         overflow vetoes the frequency record on every rank, and after the one end-of-step read all
-        ranks re-run the step with the capacities they learned."""
+        ranks re-run the step with the capacities they learned.
+
+        ``stream_carry``: the step is one of a stream of steps -- its carries come from the earlier
+        steps, N stays open (factors kept, ``with_factors`` implied), the frequency window is not
+        recorded (the stream records once, at its end) and the output carries the sequence state
+        after the step and the step's summed frequency counts."""
         eng = self.engine
         rank, wsize = world()
         early = None
@@ -189,8 +210,9 @@ class ShardedAnalyzer:
             early = box[0] if box else None
         defer = eng.can_defer(text)
         for attempt in range(4):
-            out, prep, veto = self._step(text, nbytes, ls, ll, halo_left, halo_right, topk, with_factors, pack_events,
-                                         early if attempt == 0 else None, defer)
+            out, prep, veto = self._step(text, nbytes, ls, ll, halo_left, halo_right, topk,
+                                         with_factors or stream_carry is not None, pack_events,
+                                         early if attempt == 0 else None, defer, stream_carry, split_trim)
             if not defer:
                 return out
             end = torch.cuda.Event(enable_timing=True)
@@ -216,7 +238,8 @@ class ShardedAnalyzer:
             out.events_packed = out.events_packed[:20 * ne]
         return out
 
-    def _step(self, text, nbytes, ls, ll, halo_left, halo_right, topk, with_factors, pack_events, early, defer):
+    def _step(self, text, nbytes, ls, ll, halo_left, halo_right, topk, with_factors, pack_events, early, defer,
+              sc: Optional[StreamCarry] = None, split_trim: bool = True):
         eng = self.engine
         lib = eng.lib
         rank, wsize = world()
@@ -224,7 +247,7 @@ class ShardedAnalyzer:
         L = ls.numel()
         own_lo, own_hi = halo_left, L - halo_right
         segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev, upload=eng.upload)
-        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early, defer=defer)
+        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early, defer=defer, split_trim=split_trim)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
         ns = chain.numel()
@@ -244,10 +267,16 @@ class ShardedAnalyzer:
         H = P + S + nk
         red2 = torch.empty((wsize, H + 3 * k), dtype=torch.int64, device=dev)   # other rows: the all-gather
         mine = red2[rank]
+        seq_next = None
+        stream = None
+        if sc is not None:
+            seq_next = torch.empty(max(ns, 1), dtype=torch.uint8, device=dev)
+            stream = (sc.seq, sc.line_base, 1 << 62, seq_next)
         own_start, segs.g0, segs.n, carry, seq_carry, veto = K.dp_carry(     # k_dp_carry: device scalars, no sync
-            g, rank, nk, ns, halo_left, eng.freq_carry() if nk else None, self.slot_e0, self.slot_k,
-            red_tail=mine[P + S:H] if nk else None, veto_out=prep.cnt[6:7] if defer else None,
-            zero=mine[:P + S])                                     # histogram slots (summary kernel adds)
+            g, rank, nk, ns, halo_left, (sc.freq if sc is not None else eng.freq_carry()) if nk else None,
+            self.slot_e0, self.slot_k, red_tail=mine[P + S:H] if nk else None,
+            veto_out=prep.cnt[6:7] if defer else None, zero=mine[:P + S],   # histogram slots (summary kernel adds)
+            stream=stream)
         res = eng.finish(prep, segs, carry, seq_carry, with_factors)
         # C5/C6 + C7 local half: one summarize kernel chain (pattern + severity histograms and this
         # rank's top-k rows with global line numbers, no host sync) into this rank's row
@@ -257,9 +286,11 @@ class ShardedAnalyzer:
                                       rows_out=rows_out, dn=prep.ne_dev)
         all_gather_inplace(red2, self.group)                       # collective 2: C5 + C6 + C7
         red = red2[:, :H].sum(0) if wsize > 1 else red2[0, :H]
-        eng.commit_frequency(red[P + S:], veto=veto if defer else None)
+        if sc is None:
+            eng.commit_frequency(red[P + S:], veto=veto if defer else None)
         out = StepOutput(res, own_counts, rank, red[:P], severity_counts=red[P:P + S], own_lo=own_lo,
-                         own_start_dev=own_start, events_packed=packed)
+                         own_start_dev=own_start, events_packed=packed, seq_next=seq_next,
+                         freq_counts=red[P + S:H] if nk else None)
         if topk > 0 and rank == 0:
             allrows = red2[:, H:].contiguous().view(torch.float64).view(-1, 3)
             out.topk_rows = K.topk_rows(allrows, k, ws=eng.ws) if allrows.shape[0] > k else allrows

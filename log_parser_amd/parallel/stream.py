@@ -222,9 +222,14 @@ class StreamAnalyzer:
         pos = start
         k = 0
         while pos < eff or (pos == 0 and eff == 0):
-            # ramp-up: the first chunks are 1/8, 1/4, 1/2 of chunk_bytes so the staging -> H2D ->
-            # compute pipeline fills in milliseconds instead of one full-size host copy
-            size = max(min(self.chunk_bytes, 16 << 20), self.chunk_bytes >> max(0, self.RAMP - k))
+            # ramp-up: chunks double from RAMP_MIN, so the staging -> H2D -> compute pipeline fills
+            # in milliseconds instead of one full-size host copy; ramp-down: near the end a chunk is
+            # at most half of what remains (down to RAMP_MIN), so the drain -- the last chunk's
+            # analysis after the last copy -- is a small chunk's, not an 8 GiB one's
+            size = min(self.chunk_bytes, self.RAMP_MIN << min(k, 40))
+            rest = eff - pos
+            if rest > self.RAMP_MIN:
+                size = min(size, max(self.RAMP_MIN, rest // 2))
             k += 1
             end = min(eff, pos + size)
             if end < eff:
@@ -278,12 +283,14 @@ class StreamAnalyzer:
         thr = torch.topk(lb, k).values[-1]
         keep = ub >= thr
         return [gl[keep]], [pat[keep]], [fac[keep]]
-    RAMP = 3                    # chunk-size ramp-up steps (halving)
+    RAMP_MIN = 64 << 20         # first / last chunk size of the ramps (bytes)
 
-    def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None):
+    def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None,
+                  plan=None):
         """Stages line-aligned chunks (+ halos) into pinned buffers. On GPU the buffers come from a
         small recycled pool (``free_q``: buffer + the event of the H2D copy that last read it) --
-        allocating and pinning a fresh 0.5 GB buffer per chunk costs 30-100 ms, 3x the copy."""
+        allocating and pinning a fresh 0.5 GB buffer per chunk costs 30-100 ms, 3x the copy.
+        ``plan``: an explicit list of chunks (``_plan`` entries; None = an empty chunk)."""
         try:
             flat = None
             if not isinstance(src, RepeatBuffer):
@@ -293,7 +300,11 @@ class StreamAnalyzer:
                     with warnings.catch_warnings():
                         warnings.simplefilter("ignore", UserWarning)
                         flat = torch.from_numpy(np.frombuffer(src, dtype=np.uint8))
-            for l_start, pos, end, r_end, lh, rh in self._plan(src, eff, start):
+            for ent in (plan if plan is not None else self._plan(src, eff, start)):
+                if ent is None:                               # no chunk for this rank in this step
+                    q.put((torch.zeros(K.padded_len(0), dtype=torch.uint8), 0, K.padded_len(0), 0, 0, -1))
+                    continue
+                l_start, pos, end, r_end, lh, rh = ent
                 n = r_end - l_start
                 size = K.padded_len(n)
                 if free_q is not None:
@@ -396,10 +407,14 @@ class StreamAnalyzer:
             import os
             os.replace(tmp, checkpoint)
 
+        # the backtracker side path reads the chunk's pinned host bytes: their buffer is recycled
+        # only after this chunk's prepare
+        hold = bool(lib.host_plan)
+
         def fetch():
             if resident:                        # already in HBM: nothing to stage or copy
                 c = next(res_iter, None)
-                return None if c is None else (c[0], c[1], c[2], c[3], None, c[4])
+                return None if c is None else (c[0], c[1], c[2], c[3], None, c[4], None)
             item = q.get()
             if isinstance(item, BaseException):
                 raise item
@@ -412,13 +427,14 @@ class StreamAnalyzer:
                     d.copy_(pinned[:size], non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(copy_stream)
-                free_q.put((pinned, ev))                       # recycled once the copy is done
-                return d, n, lh, rh, ev, end
-            return pinned, n, lh, rh, None, end
+                if not hold:
+                    free_q.put((pinned, ev))                   # recycled once the copy is done
+                return d, n, lh, rh, ev, end, pinned
+            return pinned, n, lh, rh, None, end, pinned
 
         nxt = fetch()
         while nxt is not None:
-            text, n, lh, rh, ev, chunk_end = nxt
+            text, n, lh, rh, ev, chunk_end, host = nxt
             if ev is not None:
                 torch.cuda.current_stream(dev).wait_event(ev)
                 text.record_stream(torch.cuda.current_stream(dev))
@@ -427,7 +443,10 @@ class StreamAnalyzer:
             L = ls.numel()
             own_lo, own_hi = lh, L - rh
             segs = Segments.scalar(0, L, own_lo, own_hi, line_base - own_lo, 1 << 62, dev)
-            prep = eng.prepare(text, n, ls, ll, segs)
+            prep = eng.prepare(text, n, ls, ll, segs, host_text=host[:n].numpy() if hold and host is not None else None,
+                               split_trim=False)
+            if hold and free_q is not None and host is not None:
+                free_q.put((host, ev))
             chain = eng.seq_chain_table(prep, own_lo, own_hi)
             res = eng.finish(prep, segs, freq_carry + run_counts, seq_state, with_factors=True)
             if lib.n_seq_events:
@@ -491,4 +510,128 @@ class StreamAnalyzer:
                            top[:, 2].astype(np.int64), chunks, nbytes_total, time.perf_counter() - t0)
         if self.keep_events:
             out.events = (gl.cpu().numpy(), pat.cpu().numpy(), score.cpu().numpy())
+        return out
+
+
+class ShardedStreamAnalyzer:
+    """One long log streamed over the ranks of a process group (one process per GPU): the chunk
+    plan of ``StreamAnalyzer`` is cut into steps of ``world`` consecutive chunks, rank r analyses
+    chunk r of every step, and each step is a data-parallel step (``ShardedAnalyzer.step``) whose
+    carries come from the earlier steps (``StreamCarry``) -- the SAME carry protocol for chunks and
+    for ranks: frequency counts of everything before (window totals + earlier steps
+    + earlier ranks of the step), the composed backward sequence-chain state, the global line
+    offset; N stays open and every event keeps its factors, rescored at the end with the true N
+    (the reference's left-to-right product, ``k_rescore``). Every rank stages only its own chunks
+    (reading its byte ranges of the shared source), so a 1B-line log costs each of 8 GPUs 1/8 of
+    the PCIe ingest. The summary and top-k are merged across ranks at the end (one all-gather);
+    every rank returns the same ``StreamResult``, with ``events`` = its own events."""
+
+    def __init__(self, engine: Engine, chunk_bytes: Optional[int] = None, topk: int = 100, group=None):
+        from .dp import ShardedAnalyzer
+        self.engine = engine
+        self.group = group
+        self.sa = StreamAnalyzer(engine, chunk_bytes=chunk_bytes, topk=topk, keep_events=True)
+        self.dp = ShardedAnalyzer(engine, group)
+        self.topk = topk
+
+    def run(self, src) -> StreamResult:
+        from .dp import StreamCarry, all_gather_inplace, world
+        t0 = time.perf_counter()
+        eng = self.engine
+        lib = eng.lib
+        dev = eng.device
+        rank, W = world()
+        eff = _eff_end(src)
+        if eff == 0 and len(src) > 0 and src.find(b"\n", 0) >= 0:
+            empty = {"significantEvents": 0, "highestSeverity": "NONE", "severityDistribution": {}}
+            z = np.zeros(0)
+            return StreamResult(0, 0, empty, z, z.astype(np.int64), z.astype(np.int64), 0, len(src), 0.0)
+        if self.sa._auto_chunk:
+            self.sa.chunk_bytes = auto_chunk_bytes(dev, max(eff // W, 1))
+        plan = list(self.sa._plan(src, eff))                      # the same plan on every rank
+        steps = (len(plan) + W - 1) // W
+        mine = [plan[s * W + rank] if s * W + rank < len(plan) else None for s in range(steps)]
+        nkeys, ns = len(lib.freq_ids), max(lib.n_seq_events, 1)
+        carry = StreamCarry(eng.freq_carry()[:max(nkeys, 1)].clone() if nkeys else
+                            torch.zeros(1, dtype=torch.int64, device=dev),
+                            torch.zeros(ns, dtype=torch.uint8, device=dev), 0)
+        start_carry = carry.freq.clone()
+        q: "queue.Queue" = queue.Queue(maxsize=2)
+        free_q: Optional[queue.Queue] = None
+        if dev.type == "cuda":
+            free_q = queue.Queue()
+            for _ in range(self.sa.PINNED_BUFFERS):
+                free_q.put((None, None))
+        th = threading.Thread(target=self.sa._producer, args=(src, eff, q, 0, free_q, mine), daemon=True)
+        th.start()
+        copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        ev_gl, ev_pat, ev_fac = [], [], []
+        nbytes_total = 0
+        for _ in range(steps):
+            item = q.get()
+            if isinstance(item, BaseException):
+                raise item
+            pinned, n, size, lh, rh, _end = item
+            if copy_stream is not None:
+                with torch.cuda.stream(copy_stream):
+                    text = torch.empty(size, dtype=torch.uint8, device=dev)
+                    text.copy_(pinned[:size], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(copy_stream)
+                free_q.put((pinned, ev))
+                torch.cuda.current_stream(dev).wait_event(ev)
+                text.record_stream(torch.cuda.current_stream(dev))
+            else:
+                text = pinned
+            if _end < 0:                                         # idle: own no line this step
+                ls = torch.zeros(0, dtype=torch.int64, device=dev)
+                ll = torch.zeros(0, dtype=torch.int32, device=dev)
+            else:
+                ls, ll = K.split_chunk_lines(text, n)
+            out = self.dp.step(text, n, ls, ll, lh, rh, topk=0, stream_carry=carry, split_trim=False)
+            res = out.result
+            if res.ev_line.numel():
+                ev_gl.append(res.ev_line.to(torch.int64) - out.own_lo + out.own_start_dev)
+                ev_pat.append(res.ev_pat)
+                ev_fac.append(res.factors)
+            carry = StreamCarry(carry.freq + out.freq_counts[:carry.freq.numel()] if nkeys else carry.freq,
+                                out.seq_next, carry.line_base + out.total_lines)
+            nbytes_total += n
+        th.join()
+        N_total = max(carry.line_base, 1)
+        if ev_gl:
+            gl, pat, fac = torch.cat(ev_gl), torch.cat(ev_pat), torch.cat(ev_fac)
+            score = K.rescore(gl, fac, N_total, eng.sp_tuple)
+        else:
+            gl = torch.zeros(0, dtype=torch.int64, device=dev)
+            pat = torch.zeros(0, dtype=torch.int32, device=dev)
+            score = torch.zeros(0, dtype=torch.float64, device=dev)
+        if nkeys:
+            eng.commit_frequency(carry.freq - start_carry)        # every rank: the stream's global counts
+        # merge: [pattern hist | severity hist | first event (line, pattern) | top-k rows] per rank
+        P, S = len(lib.patterns), len(lib.sev_names)
+        k = max(1, self.topk)
+        H = P + S
+        red2 = torch.empty((W, H + 2 + 3 * k), dtype=torch.int64, device=dev)
+        row = red2[rank]
+        row[:H].zero_()
+        row[H] = int(gl[0].item()) if gl.numel() else (1 << 62)
+        row[H + 1] = int(pat[0].item()) if pat.numel() else -1
+        K.summarize(score, pat, gl, k, eng.tabs["sev_index"], P, S, ws=eng.ws, hist_out=row[:H],
+                    rows_out=row[H + 2:].view(torch.float64).view(k, 3))
+        all_gather_inplace(red2, self.group)
+        hist = red2[:, :H].sum(0)
+        rows = red2[:, H + 2:].contiguous().view(torch.float64).view(-1, 3)
+        top = (K.topk_rows(rows, k, ws=eng.ws) if rows.shape[0] > k else rows).cpu().numpy()
+        n_events = int(hist[:P].sum().item())
+        firsts = red2[:, H:H + 2].cpu().numpy()
+        first = None
+        if n_events:
+            j = int(np.lexsort((firsts[:, 1], firsts[:, 0]))[0])
+            first = int(firsts[j, 1])
+        kk = min(self.topk, n_events)
+        summary = eng.summary_from_severity(hist[P:P + S].cpu().numpy(), first)
+        out = StreamResult(carry.line_base, n_events, summary, top[:kk, 0].copy(), top[:kk, 1].astype(np.int64),
+                           top[:kk, 2].astype(np.int64), len(plan), nbytes_total, time.perf_counter() - t0)
+        out.events = (gl.cpu().numpy(), pat.cpu().numpy(), score.cpu().numpy())
         return out

@@ -157,3 +157,109 @@ def test_chrono_bounds_cover_factor(m):
     n = 997
     vals = [chronological_factor(i, n, params) for i in range(n)]
     assert lo <= min(vals) and max(vals) <= hi
+
+
+# ---- one long log streamed over the ranks of a process group (ShardedStreamAnalyzer) ---------
+def _sstream_setup():
+    sets, trig = make_library(40, seed=51, sequence_rate=0.8)
+    lib = CompiledLibrary(sets, ScoringParams())
+    data = (make_log(6000, trig, seed=52, hit_rate=0.08, crlf_rate=0.1) + "\n\n").encode()
+    return lib, data
+
+
+def _sstream_worker(rank, world, port, q, dev, chunk):
+    import os
+    import torch.distributed as dist
+    from log_parser_amd.parallel.stream import ShardedStreamAnalyzer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lib, data = _sstream_setup()
+        eng = _eng(lib, dev)
+        outs = []
+        for _ in range(2):                    # the second stream sees the first one's window counts
+            r = ShardedStreamAnalyzer(eng, chunk_bytes=chunk, topk=9).run(data)
+            outs.append((r.total_lines, r.n_events, r.summary, r.topk_score, r.topk_line, r.topk_pat, r.chunks,
+                         tuple(np.asarray(x) for x in r.events)))
+        q.put((rank, outs, eng.freq.statistics()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_sstream(world, dev, chunk=9000):
+    import socket
+    import torch.multiprocessing as mp
+    lib, data = _sstream_setup()
+    e1 = _eng(lib, "cpu")
+    refs = [StreamAnalyzer(e1, chunk_bytes=chunk, topk=9).run(data) for _ in range(2)]
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sstream_worker, args=(r, world, port, q, dev, chunk)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (o, st)) for r, o, st in (q.get(timeout=600) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i, ref in enumerate(refs):
+        assert ref.chunks > world                       # several steps of `world` chunks
+        gl = np.concatenate([got[r][0][i][7][0] for r in range(world)])
+        order = np.argsort(gl, kind="stable")
+        pat = np.concatenate([got[r][0][i][7][1] for r in range(world)])[order]
+        sc = np.concatenate([got[r][0][i][7][2] for r in range(world)])[order]
+        np.testing.assert_array_equal(gl[order], ref.events[0])
+        np.testing.assert_array_equal(pat, ref.events[1])
+        np.testing.assert_allclose(sc, ref.events[2], rtol=1e-13, atol=0)
+        for r in range(world):
+            tl, ne, summ, ts, tline, tpat, nch, _ = got[r][0][i]
+            assert (tl, ne, summ, nch) == (ref.total_lines, ref.n_events, ref.summary, ref.chunks)
+            np.testing.assert_allclose(ts, ref.topk_score, rtol=1e-13)
+            np.testing.assert_array_equal(tline, ref.topk_line)
+            np.testing.assert_array_equal(tpat, ref.topk_pat)
+    for r in range(world):                               # every rank's window recorded the global counts
+        assert got[r][1] == e1.freq.statistics()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_stream_equals_single_stream(world):
+    """One log streamed over `world` gloo ranks (chunk r of every step on rank r, carries from the
+    earlier steps and ranks) equals the single-rank stream event for event, twice in a row."""
+    _run_sstream(world, "cpu")
+
+
+@pytest.mark.gpu
+def test_sharded_stream_two_ranks_one_gpu(gpu_device):
+    _run_sstream(2, "cuda:0", chunk=1 << 16)
+
+
+def test_stream_with_backtracker_regexes_equals_single_pass():
+    """Backtracker regexes (host side path on each chunk's pinned bytes, with the chunk line rule:
+    no trailing-empty-line removal) stream exactly like one pass -- incl. one that matches the
+    empty lines in the middle of the log."""
+    from log_parser_amd.models.schema import PatternSet
+    sets, trig = make_library(20, seed=61, sequence_rate=0.5)
+    bt = [r"^(\w*)\1$", r"(\w+)Aux0 \1", r"(?i)fatal (?=\w+Failure)"]
+    sets.append(PatternSet.model_validate({"metadata": {"library_id": "bt"}, "patterns": [
+        {"id": f"bt{i}", "name": rx, "severity": "LOW", "primary_pattern": {"regex": rx, "confidence": 0.5}}
+        for i, rx in enumerate(bt)]}))
+    lib = CompiledLibrary(sets, ScoringParams())
+    assert len(lib.host_plan) == 3
+    logs = make_log(2500, trig, seed=62, hit_rate=0.08)
+    logs = logs.replace("\n", "\n\n", 40) + "\n\n"
+    data = logs.encode()
+    e1 = _eng(lib)
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    ls, ll = K.split_lines(t, len(data))
+    ref = e1.run(t, len(data), ls, ll, Segments.single(ls.numel(), t.device), e1.freq_carry(),
+                 host_text=np.frombuffer(data, np.uint8))
+    out = StreamAnalyzer(_eng(lib), chunk_bytes=3000, topk=7).run(data)
+    gl, pat, score = out.events
+    np.testing.assert_array_equal(gl, ref.ev_line.numpy())
+    np.testing.assert_array_equal(pat, ref.ev_pat.numpy())
+    np.testing.assert_allclose(score, ref.score.numpy(), rtol=1e-15, atol=0)
+    assert (pat == lib.patterns.index(next(p for p in lib.patterns if p.id == "bt0"))).sum() >= 40

@@ -854,21 +854,23 @@ PYBIND11_MODULE(_lpnative, m) {
   });
 
   // ---- native load generator (csrc/io/loadgen.cpp): config 5 over real connections
-  m.def("http_burst", [](const std::string& host, int port, py::list msgs, py::array_t<int32_t> idx, double timeout_s) {
+  m.def("http_burst", [](const std::string& host, int port, py::list msgs, py::array_t<int32_t> idx, double timeout_s,
+                         int nthreads) {
     std::vector<std::string> M;
     for (auto h : msgs) M.push_back(h.cast<std::string>());
     std::vector<int32_t> I(idx.data(), idx.data() + idx.size());
     LoadResult R;
     {
       py::gil_scoped_release nogil;
-      R = http_burst(host, port, M, I, timeout_s);
+      R = http_burst(host, port, M, I, timeout_s, nthreads);
     }
     py::array_t<double> lat(R.latency.size());
     std::memcpy(lat.mutable_data(), R.latency.data(), R.latency.size() * sizeof(double));
     py::array_t<int32_t> st(R.status.size());
     std::memcpy(st.mutable_data(), R.status.data(), R.status.size() * sizeof(int32_t));
     return py::make_tuple(lat, st, R.t_end - R.t_start, R.completed);
-  }, py::arg("host"), py::arg("port"), py::arg("msgs"), py::arg("idx"), py::arg("timeout_s") = 120.0);
+  }, py::arg("host"), py::arg("port"), py::arg("msgs"), py::arg("idx"), py::arg("timeout_s") = 120.0,
+     py::arg("nthreads") = 8);
 
   // ---- native HTTP/1.1 front end (csrc/io/http_server.cpp)
   py::class_<RawLogs>(m, "RawLogs")
@@ -948,6 +950,22 @@ PYBIND11_MODULE(_lpnative, m) {
         PyBytes_AsStringAndSize(body.ptr(), &p, &n);
         py::gil_scoped_release nogil;   // `body` (immutable) stays referenced for the call
         s.respond(id, status, ctype, p, (size_t)n);
+      })
+      // one status / content type for a whole batch of responses: one call, GIL released
+      .def("respond_many", [](HttpServer& s, std::vector<uint64_t> ids, int status, const std::string& ctype,
+                              py::list bodies) {
+        const size_t k = std::min(ids.size(), (size_t)py::len(bodies));
+        std::vector<const char*> ptrs(k);
+        std::vector<size_t> lens(k);
+        for (size_t i = 0; i < k; ++i) {
+          char* p = nullptr;
+          Py_ssize_t n = 0;
+          PyBytes_AsStringAndSize(bodies[i].ptr(), &p, &n);
+          ptrs[i] = p;
+          lens[i] = (size_t)n;
+        }
+        py::gil_scoped_release nogil;   // the list keeps every (immutable) body referenced
+        s.respond_many(ids.data(), k, status, ctype, ptrs.data(), lens.data());
       })
       .def("stats", [](HttpServer& s) {
         py::dict d;

@@ -233,6 +233,30 @@ void HttpServer::respond(uint64_t id, int status, const std::string& content_typ
   (void)!write(io->efd, &one, 8);
 }
 
+void HttpServer::respond_many(const uint64_t* ids, size_t k, int status, const std::string& content_type,
+                              const char* const* bodies, const size_t* lens) {
+  std::vector<std::vector<Io::Out>> per(ios_.size());
+  for (size_t i = 0; i < k; ++i) {
+    const uint64_t id = ids[i];
+    const int ioi = (int)(id & 0xFF);
+    if (ioi >= (int)ios_.size()) continue;
+    const bool keep = (id >> 63) == 0;
+    std::string data = head(status, content_type, lens[i], keep);
+    data.append(bodies[i], lens[i]);
+    per[ioi].push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep});
+  }
+  for (size_t q = 0; q < per.size(); ++q) {
+    if (per[q].empty()) continue;
+    Io* io = ios_[q].get();
+    {
+      std::lock_guard<std::mutex> lk(io->om);
+      for (auto& o : per[q]) io->outbox.push_back(std::move(o));
+    }
+    uint64_t one = 1;
+    (void)!write(io->efd, &one, 8);
+  }
+}
+
 std::string BufferPool::take() {
   std::lock_guard<std::mutex> g(m);
   if (v.empty()) return std::string();

@@ -59,6 +59,9 @@ class HttpServer {
   // queue the response of request `id` (ignored if its connection is gone)
   void respond(uint64_t id, int status, const std::string& content_type, const std::string& body);
   void respond(uint64_t id, int status, const std::string& content_type, const char* body, size_t n);
+  // many responses of one status / content type: one outbox lock and one wake-up per IO thread
+  void respond_many(const uint64_t* ids, size_t k, int status, const std::string& content_type,
+                    const char* const* bodies, const size_t* lens);
   // hand a drained request's raw buffer back (its capacity serves a later request: no page faults
   // of a fresh megabyte-sized allocation per request)
   void recycle(std::string&& buf) { pool_->give(std::move(buf)); }

@@ -21,12 +21,26 @@
 #include <cerrno>
 #include <chrono>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 
 namespace lp {
-
 namespace {
+// a one-shot barrier (std::barrier is C++20; the build is C++17)
+struct OnceBarrier {
+  explicit OnceBarrier(int n) : left(n) {}
+  void arrive_and_wait() {
+    std::unique_lock<std::mutex> lk(m);
+    if (--left == 0) { cv.notify_all(); return; }
+    cv.wait(lk, [&] { return left == 0; });
+  }
+  std::mutex m;
+  std::condition_variable cv;
+  int left;
+};
 
 double mono() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
@@ -59,65 +73,76 @@ size_t response_size(const std::string& s, int* status) {
 
 }  // namespace
 
-LoadResult http_burst(const std::string& host, int port, const std::vector<std::string>& msgs,
-                      const std::vector<int32_t>& idx, double timeout_s) {
-  const size_t n = idx.size();
-  LoadResult R;
-  R.latency.assign(n, -1.0);
-  R.status.assign(n, 0);
-  if (n == 0) return R;
-  std::vector<Conn> conns(n);
+namespace {
+
+// one client thread: connections [lo, hi) on its own epoll set -- connect, wait for the common
+// start, send, collect the responses
+struct Group {
+  std::vector<Conn>* conns;
+  size_t lo, hi;
+  const sockaddr_in* addr;
+  const std::vector<std::string>* msgs;
+  const std::vector<int32_t>* idx;
+  double deadline;
+  LoadResult* R;
+  std::string error;
+};
+
+void run_group(Group& G, OnceBarrier& ready) {
+  std::vector<Conn>& conns = *G.conns;
   const int ep = epoll_create1(EPOLL_CLOEXEC);
-  if (ep < 0) throw std::runtime_error("epoll_create1 failed");
-  sockaddr_in a{};
-  a.sin_family = AF_INET;
-  a.sin_port = htons((uint16_t)port);
-  if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) throw std::runtime_error("bad host " + host);
   std::vector<epoll_event> evs(1024);
-  const double deadline = mono() + timeout_s;
-
-  // 1) connections, in waves of at most 256 pending connects (the listen backlogs are finite)
-  size_t next = 0, pending = 0, up = 0;
-  while (up < n) {
-    while (next < n && pending < 256) {
-      Conn& c = conns[next];
-      c.fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
-      if (c.fd < 0) throw std::runtime_error("socket() failed: " + std::string(strerror(errno)) + " (fd limit?)");
-      int one = 1;
-      setsockopt(c.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-      const int r = connect(c.fd, reinterpret_cast<sockaddr*>(&a), sizeof a);
-      if (r != 0 && errno != EINPROGRESS) throw std::runtime_error("connect() failed: " + std::string(strerror(errno)));
-      epoll_event ev{};
-      ev.events = EPOLLOUT;
-      ev.data.u64 = next;
-      epoll_ctl(ep, EPOLL_CTL_ADD, c.fd, &ev);
-      ++next;
-      ++pending;
+  try {
+    if (ep < 0) throw std::runtime_error("epoll_create1 failed");
+    // 1) connections, in waves of at most 128 pending connects per thread (finite listen backlogs)
+    size_t next = G.lo, pending = 0, up = 0;
+    const size_t n = G.hi - G.lo;
+    while (up < n) {
+      while (next < G.hi && pending < 128) {
+        Conn& c = conns[next];
+        c.fd = socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+        if (c.fd < 0) throw std::runtime_error("socket() failed: " + std::string(strerror(errno)) + " (fd limit?)");
+        int one = 1;
+        setsockopt(c.fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+        const int r = connect(c.fd, reinterpret_cast<const sockaddr*>(G.addr), sizeof *G.addr);
+        if (r != 0 && errno != EINPROGRESS) throw std::runtime_error("connect() failed: " + std::string(strerror(errno)));
+        epoll_event ev{};
+        ev.events = EPOLLOUT;
+        ev.data.u64 = next;
+        epoll_ctl(ep, EPOLL_CTL_ADD, c.fd, &ev);
+        ++next;
+        ++pending;
+      }
+      const int k = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
+      for (int i = 0; i < k; ++i) {
+        Conn& c = conns[evs[i].data.u64];
+        if (c.connected) continue;
+        int err = 0;
+        socklen_t sl = sizeof err;
+        getsockopt(c.fd, SOL_SOCKET, SO_ERROR, &err, &sl);
+        if (err) throw std::runtime_error("connect failed: " + std::string(strerror(err)));
+        c.connected = true;
+        epoll_event ev{};
+        ev.events = EPOLLIN;          // quiet until the burst
+        ev.data.u64 = evs[i].data.u64;
+        epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
+        --pending;
+        ++up;
+      }
+      if (mono() > G.deadline) throw std::runtime_error("load generator: connecting timed out");
     }
-    const int k = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
-    for (int i = 0; i < k; ++i) {
-      Conn& c = conns[evs[i].data.u64];
-      if (c.connected) continue;
-      int err = 0;
-      socklen_t sl = sizeof err;
-      getsockopt(c.fd, SOL_SOCKET, SO_ERROR, &err, &sl);
-      if (err) throw std::runtime_error("connect failed: " + std::string(strerror(err)));
-      c.connected = true;
-      epoll_event ev{};
-      ev.events = EPOLLIN;          // quiet until the burst
-      ev.data.u64 = evs[i].data.u64;
-      epoll_ctl(ep, EPOLL_CTL_MOD, c.fd, &ev);
-      --pending;
-      ++up;
-    }
-    if (mono() > deadline) throw std::runtime_error("load generator: connecting timed out");
+  } catch (const std::exception& e) {
+    G.error = e.what();
   }
-
-  // 2) the burst: every connection sends its request now
-  R.t_start = mono();
-  for (size_t i = 0; i < n; ++i) {
+  ready.arrive_and_wait();            // every thread connected (or failed): the burst starts
+  if (!G.error.empty()) {
+    if (ep >= 0) close(ep);
+    return;
+  }
+  // 2) the burst: every connection of this thread sends its request now
+  for (size_t i = G.lo; i < G.hi; ++i) {
     Conn& c = conns[i];
-    c.msg = &msgs.at((size_t)idx[i]);
+    c.msg = &G.msgs->at((size_t)(*G.idx)[i]);
     c.t0 = mono();
     const ssize_t w = send(c.fd, c.msg->data(), c.msg->size(), MSG_NOSIGNAL);
     if (w > 0) c.sent = (size_t)w;
@@ -130,9 +155,10 @@ LoadResult http_burst(const std::string& host, int port, const std::vector<std::
   }
   // 3) responses
   size_t finished = 0;
-  char buf[1 << 16];
+  const size_t n = G.hi - G.lo;
+  std::vector<char> buf(1 << 16);
   while (finished < n) {
-    if (mono() > deadline) break;
+    if (mono() > G.deadline) break;
     const int k = epoll_wait(ep, evs.data(), (int)evs.size(), 100);
     for (int i = 0; i < k; ++i) {
       const size_t ci = evs[i].data.u64;
@@ -150,9 +176,9 @@ LoadResult http_burst(const std::string& host, int port, const std::vector<std::
       }
       if (evs[i].events & (EPOLLIN | EPOLLHUP | EPOLLERR)) {
         for (;;) {
-          const ssize_t r = recv(c.fd, buf, sizeof buf, 0);
+          const ssize_t r = recv(c.fd, buf.data(), buf.size(), 0);
           if (r > 0) {
-            c.in.append(buf, (size_t)r);
+            c.in.append(buf.data(), (size_t)r);
             continue;
           }
           if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK)) {   // closed / error: incomplete
@@ -166,18 +192,50 @@ LoadResult http_burst(const std::string& host, int port, const std::vector<std::
           if (c.need && c.in.size() >= c.need) {
             c.t1 = mono();
             c.done = true;
-            R.latency[ci] = c.t1 - c.t0;
-            R.status[ci] = c.status;
+            G.R->latency[ci] = c.t1 - c.t0;
+            G.R->status[ci] = c.status;
             ++finished;
           }
         }
       }
     }
   }
-  R.t_end = mono();
+  close(ep);
+}
+
+}  // namespace
+
+LoadResult http_burst(const std::string& host, int port, const std::vector<std::string>& msgs,
+                      const std::vector<int32_t>& idx, double timeout_s, int nthreads) {
+  const size_t n = idx.size();
+  LoadResult R;
+  R.latency.assign(n, -1.0);
+  R.status.assign(n, 0);
+  if (n == 0) return R;
+  std::vector<Conn> conns(n);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  if (inet_pton(AF_INET, host.c_str(), &a.sin_addr) != 1) throw std::runtime_error("bad host " + host);
+  const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(nthreads, 1), n));
+  std::vector<Group> groups(T);
+  const double deadline = mono() + timeout_s;
+  OnceBarrier ready(T + 1);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    groups[t] = Group{&conns, n * t / T, n * (t + 1) / T, &a, &msgs, &idx, deadline, &R, {}};
+    th.emplace_back(run_group, std::ref(groups[t]), std::ref(ready));
+  }
+  ready.arrive_and_wait();
+  R.t_start = mono();
+  for (auto& x : th) x.join();
+  R.t_end = 0;
+  for (auto& c : conns) R.t_end = std::max(R.t_end, c.t1);
+  if (R.t_end == 0) R.t_end = mono();
   for (auto& c : conns)
     if (c.fd >= 0) close(c.fd);
-  close(ep);
+  for (auto& g : groups)
+    if (!g.error.empty()) throw std::runtime_error(g.error);
   R.completed = (int64_t)std::count_if(R.latency.begin(), R.latency.end(), [](double x) { return x >= 0; });
   return R;
 }

@@ -15,7 +15,9 @@ struct LoadResult {
 
 // One request per connection, all connections established before the burst; connection c sends
 // msgs[idx[c]] (a complete HTTP request). Blocks until every response arrived or timeout_s passed.
+// nthreads client threads, each with its own slice of the connections and epoll set (one thread
+// sending ~1 GB of bodies over loopback was the bottleneck of the burst, not the server).
 LoadResult http_burst(const std::string& host, int port, const std::vector<std::string>& msgs,
-                      const std::vector<int32_t>& idx, double timeout_s);
+                      const std::vector<int32_t>& idx, double timeout_s, int nthreads = 8);
 
 }  // namespace lp

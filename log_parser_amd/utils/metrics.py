@@ -52,6 +52,15 @@ class Metrics:
             if code == 200:
                 self.latency.observe(seconds)
 
+    def observe_requests(self, code: int, seconds, nbytes: int):
+        """Many requests of one status at once (the native front end's batch completion)."""
+        with self._lock:
+            self.requests[code] = self.requests.get(code, 0) + len(seconds)
+            self.bytes_total += nbytes
+            if code == 200:
+                for s in seconds:
+                    self.latency.observe(s)
+
     def observe_batch(self, n: int, seconds: float):
         with self._lock:
             self.batches += 1

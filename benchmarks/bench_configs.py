@@ -297,10 +297,13 @@ def mode_concurrent_http(args):
         raise SystemExit(f"open-file limit too low for {n} connections")
     sets, trig = realistic_library(1000, seed=7)
     dev = "cpu" if args.device == "cpu" else ("cuda:0" if torch.cuda.is_available() else "cpu")
-    srv = ServerProcess(write_library(sets), dev, http="native",
-                        extra=[f"-Dengine.serve-devices={','.join([dev] * args.engines)}"] if args.engines > 1 else [])
+    extra = [f"-Dengine.serve-devices={','.join([dev] * args.engines)}"] if args.engines > 1 else []
+    if args.processes > 1:          # serving processes sharing one window (serve/procs.py)
+        extra = [f"-Dserver.processes={args.processes}"]
+    srv = ServerProcess(write_library(sets), dev, http="native", extra=extra + list(args.server_opt or []),
+                        log_path=args.server_log)
     try:
-        if not srv.wait_ready():
+        if not srv.wait_ready(workers=max(args.processes, 1)):
             raise SystemExit("server did not come up")
         rng = np.random.default_rng(0)
         sizes_set = [20, 100, 500, 2000, 10000]
@@ -321,7 +324,8 @@ def mode_concurrent_http(args):
     ok = lat >= 0
     lines = float(np.array(lines_of)[idx].sum())
     print(json.dumps({"config": f"concurrent-http-{n}-connections-mixed-realistic", "device": dev,
-                      "engines": args.engines, "connections": n, "completed": int(done),
+                      "engines": args.engines, "processes": args.processes, "connections": n,
+                      "completed": int(done),
                       "status_200": int((st == 200).sum()),
                       "p50_ms": round(float(np.median(lat[ok])) * 1e3, 3),
                       "p99_ms": round(float(np.percentile(lat[ok], 99)) * 1e3, 3),
@@ -355,6 +359,10 @@ def main():
     ap.add_argument("--chunk-mb", type=int, default=0, help="stream / resident chunk MiB (0 = from free HBM)")
     ap.add_argument("--timeline", action="store_true", help="concurrent: print the pipeline stage timeline")
     ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
+    ap.add_argument("--processes", type=int, default=1,
+                    help="concurrent_http: serving processes sharing one frequency window (server.processes)")
+    ap.add_argument("--server-opt", action="append", help="concurrent_http: extra -Dkey=value for the server")
+    ap.add_argument("--server-log", default=None, help="concurrent_http: server stdout / stderr to this file")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="rest: HTTP front end")
     ap.add_argument("--library", default="realistic", choices=["realistic", "synthetic"],
                     help="single / stream / concurrent: pattern library kind")

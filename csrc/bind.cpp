@@ -20,6 +20,7 @@
 #include "kernels/lp_api.h"
 #include "kernels/lp_host.h"
 #include "regex/jregex.h"
+#include "runtime/proc_shared.h"
 #include "runtime/request.h"
 
 namespace py = pybind11;
@@ -502,6 +503,41 @@ static py::tuple parse_pod_request_py(py::bytes body, bool two_pass) {
   return py::make_tuple(st, r.pod_nonnull, name, r.logs_kind, logs);
 }
 
+// ---- DLPack (v0.8 ABI, unversioned "dltensor" capsule) ---------------------------------------
+namespace dl {
+struct Device { int32_t device_type; int32_t device_id; };
+struct DataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct Tensor { void* data; Device device; int32_t ndim; DataType dtype; int64_t* shape; int64_t* strides;
+                uint64_t byte_offset; };
+struct Managed { Tensor t; void* ctx; void (*deleter)(Managed*); };
+constexpr int32_t kCPU = 1, kROCM = 10;
+struct Holder { Managed m; int64_t shape[1]; };
+void free_managed(Managed* m) { delete reinterpret_cast<Holder*>(m); }
+}  // namespace dl
+
+// device < 0: host memory. The memory itself is not owned (the shared window keeps it mapped).
+static py::capsule dlpack_capsule(uint64_t ptr, int64_t numel, const std::string& dtype, int device) {
+  auto* h = new dl::Holder();
+  dl::DataType t{};
+  if (dtype == "float64") t = {2, 64, 1};
+  else if (dtype == "int64") t = {0, 64, 1};
+  else if (dtype == "int32") t = {0, 32, 1};
+  else if (dtype == "uint8") t = {1, 8, 1};
+  else { delete h; throw std::invalid_argument("dlpack: unsupported dtype " + dtype); }
+  h->shape[0] = numel;
+  h->m.t = dl::Tensor{reinterpret_cast<void*>(ptr), {device < 0 ? dl::kCPU : dl::kROCM, device < 0 ? 0 : device},
+                      1, t, h->shape, nullptr, 0};
+  h->m.ctx = nullptr;
+  h->m.deleter = dl::free_managed;
+  return py::capsule(&h->m, "dltensor", [](PyObject* cap) {
+    // consumed capsules are renamed "used_dltensor": the consumer then owns the deleter call
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* m = static_cast<dl::Managed*>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (m && m->deleter) m->deleter(m);
+    }
+  });
+}
+
 PYBIND11_MODULE(_lpnative, m) {
   m.doc() = "log_parser_amd native core: Java-regex compiler, gfx950 kernels, host twins, JSON emitter";
   m.def("compile_multi", [](const std::vector<std::string>& pats, int max_states) -> py::object {
@@ -808,7 +844,7 @@ PYBIND11_MODULE(_lpnative, m) {
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
-                     double evict_before, double now, uint64_t stream, int64_t host_cap, WindowTurn* turn, int64_t seq,
+                     double evict_before, double now, uint64_t stream, int64_t host_cap, Turn* turn, int64_t seq,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> inj) {
         const FreqRing R = ring_from(ring);
         const int D = (int)lo.shape(0);
@@ -834,11 +870,61 @@ PYBIND11_MODULE(_lpnative, m) {
       .def("upload_bytes", &RequestRunner::upload_bytes);
 
   // arrival-order gate of a window shared by several runners (csrc/runtime/request.h)
-  py::class_<WindowTurn>(m, "WindowTurn")
+  py::class_<Turn>(m, "Turn")
+      .def("wait", [](Turn& t, int64_t seq) { py::gil_scoped_release nogil; t.wait(seq); })
+      .def("done", [](Turn& t, int64_t seq) { py::gil_scoped_release nogil; t.done(seq); });
+  py::class_<WindowTurn, Turn>(m, "WindowTurn")
       .def(py::init<>())
-      .def("wait", [](WindowTurn& t, int64_t seq) { py::gil_scoped_release nogil; t.wait(seq); })
-      .def("done", &WindowTurn::done)
       .def_property_readonly("next", &WindowTurn::next);
+  // the serving processes of a node (csrc/runtime/proc_shared.h): arrival ticket, cross-process
+  // turns, the shared window's metadata
+  py::class_<ProcTurn, Turn>(m, "ProcTurn").def_property_readonly("next", &ProcTurn::next);
+  py::class_<ProcShared>(m, "ProcShared")
+      .def(py::init<const std::string&, bool, int>(), py::arg("name"), py::arg("create"), py::arg("nproc") = 0)
+      .def("take", &ProcShared::take)
+      .def_property_readonly("host", &ProcShared::host, py::return_value_policy::reference_internal)
+      .def_property_readonly("dev", &ProcShared::dev, py::return_value_policy::reference_internal)
+      .def_property_readonly("name", &ProcShared::name)
+      .def_property_readonly("nproc", &ProcShared::nproc)
+      .def_property_readonly("ticket", [](ProcShared& s) { return s.header()->ticket.load(); })
+      .def_property_readonly("released_dead", [](ProcShared& s) { return s.header()->released_dead.load(); })
+      .def("mark_up", &ProcShared::mark_up)
+      .def("up", &ProcShared::up)
+      .def_property("generation", [](ProcShared& s) { return s.win().generation.load(std::memory_order_acquire); },
+                    [](ProcShared& s, int64_t g) { s.win().generation.store(g, std::memory_order_release); })
+      .def_property("cap", [](ProcShared& s) { return s.win().cap; }, [](ProcShared& s, int64_t v) { s.win().cap = v; })
+      .def_property("tail_bound", [](ProcShared& s) { return s.win().tail_bound; },
+                    [](ProcShared& s, int64_t v) { s.win().tail_bound = v; })
+      .def_property("head_known", [](ProcShared& s) { return s.win().head_known; },
+                    [](ProcShared& s, int64_t v) { s.win().head_known = v; })
+      .def_property("last_now", [](ProcShared& s) { return s.win().last_now; },
+                    [](ProcShared& s, double v) { s.win().last_now = v; })
+      .def_property("block_bytes", [](ProcShared& s) { return s.win().block_bytes; },
+                    [](ProcShared& s, int64_t v) { s.win().block_bytes = v; })
+      .def_property("kind", [](ProcShared& s) { return s.win().kind; }, [](ProcShared& s, int v) { s.win().kind = v; })
+      .def_property("home_device", [](ProcShared& s) { return s.win().home_device; },
+                    [](ProcShared& s, int v) { s.win().home_device = v; })
+      .def_property("handle", [](ProcShared& s) { return py::bytes(reinterpret_cast<const char*>(s.win().handle), 64); },
+                    [](ProcShared& s, const std::string& h) {
+                      if (h.size() > 64) throw std::invalid_argument("handle longer than 64 bytes");
+                      std::memset(s.win().handle, 0, 64);
+                      std::memcpy(s.win().handle, h.data(), h.size());
+                    })
+      .def("host_block", [](py::object self, int64_t gen, int64_t bytes, bool create) {
+        ProcShared& s = self.cast<ProcShared&>();
+        void* p = s.host_block(gen, bytes, create);
+        return py::array(py::dtype("uint8"), {(py::ssize_t)bytes}, {(py::ssize_t)1}, p, self);
+      })
+      .def_static("unlink", &ProcShared::unlink);
+  m.def("ipc_alloc", [](int device, int64_t bytes) {
+    auto r = ipc_alloc(device, bytes);
+    return py::make_tuple(r.first, py::bytes(r.second));
+  });
+  m.def("ipc_open", [](int device, const std::string& h) { return ipc_open(device, h); });
+  // a DLPack view (torch.from_dlpack) of raw memory: an IPC mapping of the shared window
+  m.def("dlpack", [](uint64_t ptr, int64_t numel, const std::string& dtype, int device) {
+    return dlpack_capsule(ptr, numel, dtype, device);
+  }, py::arg("ptr"), py::arg("numel"), py::arg("dtype"), py::arg("device"));
   // peer access for kernels on `device` reading / writing memory of `peer` (a shared window)
   m.def("enable_peer_access", [](int device, int peer) {
     if (device == peer) return true;

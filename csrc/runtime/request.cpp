@@ -91,10 +91,10 @@ int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
                            const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
                            int D, const FreqRing& ring, double evict_before, double now, uint64_t stream,
-                           int64_t host_cap, WindowTurn* turn, int64_t seq, const int64_t* inj, int64_t ninj) {
+                           int64_t host_cap, Turn* turn, int64_t seq, const int64_t* inj, int64_t ninj) {
   // a shared window: released on every exit, also when a HIP call throws
   struct Release {
-    WindowTurn* t;
+    Turn* t;
     int64_t s;
     ~Release() { if (t) t->done(s); }
   } release{turn, seq};

@@ -31,13 +31,23 @@ namespace lp {
 // FrequencyTrackingService.java:25 one map for all workers) -- only after every earlier batch has
 // finished its own. Matching runs before the gate, concurrently. done() is idempotent and may
 // come out of order (a failed batch releases its slot).
-class WindowTurn {
+//
+// Turn is the interface the runner sees; WindowTurn orders the runners of ONE process,
+// ProcTurn (runtime/proc_shared.h) the serving processes of a node over shared memory.
+class Turn {
  public:
-  void wait(int64_t seq) {
+  virtual ~Turn() = default;
+  virtual void wait(int64_t seq) = 0;
+  virtual void done(int64_t seq) = 0;
+};
+
+class WindowTurn : public Turn {
+ public:
+  void wait(int64_t seq) override {
     std::unique_lock<std::mutex> g(m_);
     cv_.wait(g, [&] { return next_ >= seq; });
   }
-  void done(int64_t seq) {
+  void done(int64_t seq) override {
     std::lock_guard<std::mutex> g(m_);
     if (seq < next_) return;
     done_.insert(seq);
@@ -105,7 +115,7 @@ class RequestRunner {
   int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
               const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0,
-              WindowTurn* turn = nullptr, int64_t seq = 0, const int64_t* inj = nullptr, int64_t ninj = 0);
+              Turn* turn = nullptr, int64_t seq = 0, const int64_t* inj = nullptr, int64_t ninj = 0);
   // the batch's frequency record was enqueued (a failure after it must not record the batch again)
   bool recorded() const { return recorded_; }
   // host bytes the single-copy upload needs (text padded, index, segments, counters, carry)

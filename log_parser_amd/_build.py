@@ -40,6 +40,7 @@ SOURCES = [
     ("io/http_server.cpp", "cpp"),
     ("io/loadgen.cpp", "cpp"),
     ("runtime/request.cpp", "cpp"),
+    ("runtime/proc_shared.cpp", "cpp"),
     ("kernels/prefilter_cpu.cpp", "cpp"),
     ("bind.cpp", "cpp"),
 ]

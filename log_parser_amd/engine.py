@@ -221,6 +221,21 @@ class SharedWindowTurn:
         self.dev.done(seq)
 
 
+class ProcessWindowTurn(SharedWindowTurn):
+    """The same two turns across the serving PROCESSES of a node (``serve/procs.py``): both live
+    in the shared segment (``N.ProcShared``: ``host`` / ``dev`` are ``N.ProcTurn``, which the native
+    request runner takes like ``N.WindowTurn``) and a batch's sequence number is its arrival ticket
+    there (``take``), drawn when the batch enters its device stage on whichever process."""
+
+    def __init__(self, shared):
+        self.shared = shared
+        self.host = shared.host
+        self.dev = shared.dev
+
+    def take(self) -> int:
+        return self.shared.take()
+
+
 @dataclass
 class BatchJob:
     """One continuous batch between the pipeline stages (pack -> device -> emit)."""

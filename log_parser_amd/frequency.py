@@ -434,3 +434,173 @@ class MirroredFrequencyState(FrequencyState):
             self._dev.record_counts(ids, counts, now)
         except Exception:  # noqa: BLE001 - the device may be the thing that failed
             log.warning("could not record the fallback batch in the device frequency window")
+
+
+class SharedFrequencyState(DeviceFrequencyState):
+    """ONE device-resident window shared by the serving PROCESSES of a node (one process per GPU,
+    ``serve/procs.py``) -- the reference's single process-global window
+    (FrequencyTrackingService.java:25) kept across processes instead of across threads.
+
+    The ring, totals and head / tail live in one block of GPU memory on the window's home GPU,
+    allocated by the process that creates (or grows) it and mapped by the others through
+    ``hipIpcGetMemHandle`` / ``hipIpcOpenMemHandle`` (``N.ipc_alloc`` / ``N.ipc_open``; CPU engines
+    use a host shared-memory block instead). The host bookkeeping that ``DeviceFrequencyState``
+    keeps in attributes -- tail bound, known head, last record timestamp, capacity -- lives in the
+    shared segment (``N.ProcShared``), and is only touched inside the cross-process host turn,
+    exactly like the in-process ``SharedWindowTurn`` orders it between engines. A grown ring is a
+    new generation: the other processes re-map it at their next access (the turn orders that after
+    the growth; superseded blocks stay mapped until exit -- at most the final size again).
+
+    The admin / snapshot API takes its own arrival ticket and runs between batches."""
+
+    def __init__(self, ids: List[str], window_hours: int, device, shared, clock: Callable[[], float] = time.time,
+                 capacity: int = 1 << 20, create: bool = False):
+        import torch
+        self.ids = list(ids)
+        self.window_hours = window_hours
+        self.window_s = float(window_hours) * 3600.0
+        self.clock = clock
+        self.device = torch.device(device)
+        self.sh = shared
+        self._K = max(len(self.ids), 1)
+        self._lock = threading.RLock()
+        self._index = {pid: i for i, pid in enumerate(self.ids)}
+        self._gen = 0
+        self._views: tuple = ()
+        self._keep: list = []                 # mappings of every generation seen (kept until exit)
+        self._tls = threading.local()
+        if create:
+            self._exclusive_enter()
+            try:
+                self.sh.home_device = self._dev_index()
+                self.sh.last_now = float("-inf")
+                self._alloc(max(int(capacity), 2 * self._K))
+            finally:
+                self._exclusive_exit()
+
+    # ---- shared host bookkeeping (DeviceFrequencyState attributes -> the segment)
+    _tail_bound = property(lambda s: s.sh.tail_bound, lambda s, v: setattr(s.sh, "tail_bound", int(v)))
+    _head_known = property(lambda s: s.sh.head_known, lambda s, v: setattr(s.sh, "head_known", int(v)))
+    _last_now = property(lambda s: s.sh.last_now, lambda s, v: setattr(s.sh, "last_now", float(v)))
+
+    @property
+    def cap(self) -> int:
+        return int(self.sh.cap)
+
+    def _dev_index(self) -> int:
+        return -1 if self.device.type != "cuda" else (self.device.index if self.device.index is not None else 0)
+
+    # ---- storage: one block per generation
+    def _layout(self, cap: int):
+        up = lambda n: (n + 255) & ~255  # noqa: E731
+        K = self._K
+        sizes = [("t", "float64", 8, cap), ("key", "int32", 4, cap), ("cnt", "int32", 4, cap),
+                 ("ht", "int64", 8, 2), ("tot", "int64", 8, K), ("seen", "uint8", 1, K)]
+        off, out = 0, []
+        for name, dt, isz, n in sizes:
+            out.append((name, dt, off, n))
+            off += up(isz * n)
+        return out, off
+
+    def _map(self, gen: int, create: bool, cap: int):
+        import torch
+        layout, nbytes = self._layout(cap)
+        dev = self._dev_index()
+        if dev < 0:
+            arr = self.sh.host_block(gen, nbytes, create)
+            self._keep.append(arr)
+            views = tuple(torch.from_numpy(arr[o:o + n * np.dtype(dt).itemsize].view(dt)) for _, dt, o, n in layout)
+        else:
+            from .native import N
+            if create:
+                base, handle = N.ipc_alloc(int(self.sh.home_device), nbytes)
+                self.sh.handle = handle
+            else:
+                base = N.ipc_open(dev, bytes(self.sh.handle))
+            self._keep.append(base)
+            views = tuple(torch.from_dlpack(N.dlpack(base + o, n, dt, dev)) for _, dt, o, n in layout)
+        if create:
+            self.sh.block_bytes = nbytes
+            self.sh.kind = 0 if dev < 0 else 1
+        return views
+
+    def _alloc(self, cap: int) -> None:
+        """A new generation (creation or growth; inside the host turn)."""
+        gen = int(self.sh.generation) + 1
+        old = self._current() if gen > 1 else None
+        self._views = self._map(gen, True, int(cap))
+        if old is not None:                           # totals / seen / head-tail carry over; the
+            for i in (3, 4, 5):                       # records are copied by _ensure_room
+                self._views[i].copy_(old[i])
+        self.sh.cap = int(cap)
+        self._gen = gen
+        self.sh.generation = gen                      # published last: the block is complete
+
+    def _current(self) -> tuple:
+        g = int(self.sh.generation)
+        if g != self._gen:
+            if g == 0:
+                raise RuntimeError("the shared frequency window has not been created yet")
+            self._views = self._map(g, False, self.cap)
+            self._gen = g
+        return self._views
+
+    t = property(lambda s: s._current()[0])
+    key = property(lambda s: s._current()[1])
+    cnt = property(lambda s: s._current()[2])
+    ht = property(lambda s: s._current()[3])
+    tot = property(lambda s: s._current()[4])
+    seen = property(lambda s: s._current()[5])
+
+    # ---- the admin API runs between batches, under an arrival ticket of its own
+    def _exclusive_enter(self) -> None:
+        d = getattr(self._tls, "depth", 0)
+        self._tls.depth = d + 1
+        if d:
+            return
+        seq = self.sh.take()
+        self._tls.seq = seq
+        self.sh.host.wait(seq)
+        self.sh.dev.wait(seq)
+
+    def _exclusive_exit(self) -> None:
+        self._tls.depth -= 1
+        if self._tls.depth:
+            return
+        try:
+            if self.device.type == "cuda":
+                import torch
+                torch.cuda.current_stream(self.device).synchronize()
+        finally:
+            self.sh.host.done(self._tls.seq)
+            self.sh.dev.done(self._tls.seq)
+
+    def _exclusive(self, fn, *a):
+        self._exclusive_enter()
+        try:
+            return fn(*a)
+        finally:
+            self._exclusive_exit()
+
+    def get_pattern_frequency(self, pid: str) -> Optional[dict]:
+        return self._exclusive(super().get_pattern_frequency, pid)
+
+    def statistics(self) -> Dict[str, int]:
+        return self._exclusive(super().statistics)
+
+    def reset(self, pid: str) -> None:
+        self._exclusive(super().reset, pid)
+
+    def reset_all(self) -> None:
+        self._exclusive(super().reset_all)
+
+    def snapshot(self, path: str) -> None:
+        self._exclusive(super().snapshot, path)
+
+    def restore(self, path: str) -> None:
+        self._exclusive(super().restore, path)
+
+    def capture(self) -> dict:
+        raise NotImplementedError("the elastic DP capture / rollback does not apply to a shared serving window")
+
+    rollback = capture

@@ -50,8 +50,18 @@ def main(argv=None):
     ensure_hw_queues()                  # before the first HIP call (profiles/r3_f)
     cfg = Config.load(overrides=parse_cli_overrides(argv))
     raise_fd_limit()
+    from .procs import WorkerContext, process_count, run_processes
+    proc = WorkerContext.from_env()
+    if proc is None and process_count(cfg) > 1:
+        # supervisor of one serving process per GPU (serve/procs.py); makes no HIP call itself
+        stop = threading.Event()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            signal.signal(sig, lambda *_: stop.set())
+        sys.exit(run_processes(argv, cfg, process_count(cfg), stop))
     bind_numa(cfg)
     if str(cfg["server.http"]) == "uvicorn":
+        if proc is not None:
+            raise SystemExit("server.processes > 1 needs the native HTTP front end (SO_REUSEPORT listeners)")
         import uvicorn
         uvicorn.run(create_app(cfg), host=cfg["server.host"], port=int(cfg["server.port"]), log_level="info")
         return
@@ -59,7 +69,7 @@ def main(argv=None):
     stop = threading.Event()
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *_: stop.set())
-    fe = NativeHttpFrontend(Service(cfg), cfg["server.host"], int(cfg["server.port"]),
+    fe = NativeHttpFrontend(Service(cfg, proc=proc), cfg["server.host"], int(cfg["server.port"]),
                             int(cfg["server.io-threads"]))
     fe.serve_forever(stop)
 

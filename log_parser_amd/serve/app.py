@@ -20,6 +20,7 @@ from __future__ import annotations
 import asyncio
 import gc
 import logging
+import os
 import sys
 import threading
 import time
@@ -31,7 +32,7 @@ import torch
 from fastapi import FastAPI, Request
 from fastapi.responses import Response
 
-from ..engine import Engine, FrequencyTurn, SharedWindowTurn
+from ..engine import Engine, ProcessWindowTurn, SharedWindowTurn
 from ..frequency import MirroredFrequencyState
 from ..models.compiled import CompiledLibrary
 from ..models.library import load_pattern_directory
@@ -64,10 +65,16 @@ class Batcher:
     frequency state inside a ``FrequencyTurn`` in that order, so results are identical to serving
     the same batches one after another on one GPU."""
 
-    def __init__(self, engines, max_requests: int, max_bytes: int, max_wait_ms: float, metrics: Metrics):
+    def __init__(self, engines, max_requests: int, max_bytes: int, max_wait_ms: float, metrics: Metrics,
+                 turn: Optional[SharedWindowTurn] = None):
+        """``turn``: a ``ProcessWindowTurn`` when this process is one of several serving processes
+        sharing one window (serve/procs.py): each batch then draws its arrival ticket from the
+        shared segment when it enters the device stage."""
         self.engines: List[Engine] = list(engines) if isinstance(engines, (list, tuple)) else [engines]
         self.engine = self.engines[0]
-        self.turn: Optional[SharedWindowTurn] = SharedWindowTurn() if len(self.engines) > 1 else None
+        self.proc = isinstance(turn, ProcessWindowTurn)
+        self.turn: Optional[SharedWindowTurn] = turn if turn is not None else (
+            SharedWindowTurn() if len(self.engines) > 1 else None)
         self.max_requests = max_requests
         self.max_bytes = max_bytes
         self.max_wait = max_wait_ms / 1000.0
@@ -91,7 +98,7 @@ class Batcher:
             sys.setswitchinterval(si / 1000.0)
         # one engine: pack / device / emit of consecutive batches overlap (serve/pipeline.py)
         self.pipe: Optional[BatchPipeline] = (BatchPipeline(self.engine, self.device_stage, metrics.observe_batch)
-                                              if self.turn is None else None)
+                                              if len(self.engines) == 1 else None)
         self._threads = [threading.Thread(target=self._loop, args=(e,), name=f"lp-batcher-{i}", daemon=True)
                          for i, e in enumerate(self.engines)]
         for t in self._threads:
@@ -170,7 +177,7 @@ class Batcher:
                     if not fut.done():
                         fut.set_exception(e)
             finally:
-                if self.turn is not None:
+                if self.turn is not None and self.pipe is None:
                     self.turn.done(seq)    # no-op after a successful batch; unblocks later ones
 
     @staticmethod
@@ -186,15 +193,22 @@ class Batcher:
         return done
 
     def device_stage(self, job, eng: Optional[Engine] = None, seq: int = 0) -> None:
-        """Pipeline device stage with the same CPU fallback as ``analyze``."""
+        """Pipeline device stage with the same CPU fallback as ``analyze``. Several serving
+        processes: the batch's arrival ticket is drawn here and released on every exit."""
         eng = eng or self.engine
+        if self.proc:
+            seq = self.turn.take()
         try:
-            eng.device_batch(job, self.turn, seq)
-        except Exception:  # noqa: BLE001
-            if not self.fallback_cpu:
-                raise
-            log.exception("device batch failed; serving it from the CPU backend")
-            job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq, record=not job.recorded)
+            try:
+                eng.device_batch(job, self.turn, seq)
+            except Exception:  # noqa: BLE001
+                if not self.fallback_cpu:
+                    raise
+                log.exception("device batch failed; serving it from the CPU backend")
+                job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq, record=not job.recorded)
+        finally:
+            if self.proc:
+                self.turn.done(seq)
 
     def _cpu(self, eng: Engine) -> Engine:
         """The CPU backend for one failed batch. A device-resident window is not touched by it
@@ -252,12 +266,15 @@ class Service:
 
     JSON = "application/json"
 
-    def __init__(self, config: Optional[Config] = None, engine: Optional[Engine] = None):
+    def __init__(self, config: Optional[Config] = None, engine: Optional[Engine] = None, proc=None):
+        """``proc``: this process's ``serve.procs.WorkerContext`` when it is one of several serving
+        processes (one engine here, the frequency window shared with the others)."""
         self.config = config or Config.load()
         self.metrics = Metrics()
         self._engine = engine
         self._batcher: Optional[Batcher] = None
         self._lock = threading.Lock()
+        self.proc = proc
 
     # ---- lifecycle
     def engine(self) -> Engine:
@@ -268,10 +285,16 @@ class Service:
                 lib = CompiledLibrary(sets, cfg.scoring, max_dfa_states=int(cfg["engine.dfa-max-states"]),
                                   nfa_engine=str(cfg["engine.nfa-engine"]))
                 log.info("compiled library: %s", lib.summary())
-                self._engine = Engine(lib, cfg)
-                snap = cfg["engine.frequency.snapshot-path"]
+                if self.proc is not None:      # one of several serving processes: the shared window
+                    self._engine = Engine(lib, cfg, freq=self.proc.frequency_state(lib, cfg))
+                    snap = cfg["engine.frequency.snapshot-path"] if self.proc.owner else ""
+                else:
+                    self._engine = Engine(lib, cfg)
+                    snap = cfg["engine.frequency.snapshot-path"]
                 if snap:                       # resume the sliding window of a previous run
                     self._engine.freq.restore(snap)
+                if self.proc is not None:
+                    self.proc.window_ready()
             return self._engine
 
     def batcher(self) -> Batcher:
@@ -279,6 +302,11 @@ class Service:
         with self._lock:
             if self._batcher is None:
                 cfg = self.config
+                if self.proc is not None:
+                    self._batcher = Batcher([eng], int(cfg["engine.batch.max-requests"]),
+                                            int(cfg["engine.batch.max-bytes"]), float(cfg["engine.batch.max-wait-ms"]),
+                                            self.metrics, turn=ProcessWindowTurn(self.proc.shared))
+                    return self._batcher
                 engines = [eng]
                 devs = serve_devices(cfg)
                 if devs and devs[0] == eng.device:
@@ -321,7 +349,7 @@ class Service:
         if self._batcher is not None:
             self._batcher.close()
         path = self.config["engine.frequency.snapshot-path"]
-        if path and self._engine is not None:
+        if path and self._engine is not None and (self.proc is None or self.proc.owner):
             self._engine.freq.snapshot(path)
 
     # ---- POST /parse (Parse.java:41-61)
@@ -389,7 +417,10 @@ class Service:
             e = self._engine
             if e is None:
                 return j({"status": "DOWN", "reason": "library not loaded"}, 503)
-            return j({"status": "UP", "device": str(e.device), "library": e.lib.summary()})
+            w = {"index": self.proc.index if self.proc is not None else 0, "pid": os.getpid(),
+                 "processes": self.proc.nproc if self.proc is not None else 1}
+            return j({"status": "UP", "device": str(e.device), "library": e.lib.summary(), "worker": w,
+                      "nativeRunner": e._runner not in (None, False)})
         if path == "/metrics" and method == "GET":
             if self._engine is not None:
                 self.metrics.set_frequency(self._engine.freq.statistics())

@@ -56,7 +56,7 @@ class NativeHttpFrontend:
 
     def _pump(self) -> None:
         b = self.svc.batcher()
-        direct = len(b.engines) == 1 and b.turn is None
+        direct = b.pipe is not None
         while not self._stop.is_set():
             # direct mode: /parse logs stay JSON-escaped in their receive buffers (N.RawLogs) and
             # are unescaped by the engine's packer straight into its pinned stage

@@ -100,6 +100,11 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # HTTP front end: "native" (C++ epoll server, csrc/io/http_server.cpp) or "uvicorn" (FastAPI)
     "server.http": ("native", str),
     "server.io-threads": (2, int),
+    # serving processes (serve/procs.py): 1 = this process only; N > 1 = N processes started before
+    # any GPU call, each with its own SO_REUSEPORT listeners, GIL and pipeline, sharing ONE
+    # frequency window (GPU memory over IPC) in arrival-ticket order; -1 = one per visible GPU.
+    # Process i serves on engine.serve-devices[i % n] (or engine.device when that is empty)
+    "server.processes": (1, int),
     # single-GPU service: bind the process to the CPUs of the GPU's NUMA node (serve/__main__.py)
     "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)

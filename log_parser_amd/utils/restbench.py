@@ -95,8 +95,11 @@ class ServerProcess:
                                      env=None if not env else {**os.environ, **env})
         self.conn: Optional[http.client.HTTPConnection] = None
 
-    def wait_ready(self, timeout_s: float = 240.0) -> bool:
+    def wait_ready(self, timeout_s: float = 240.0, workers: int = 1) -> bool:
+        """Until /ready answers 200 -- from ``workers`` distinct serving processes
+        (``server.processes``; fresh connections land on either SO_REUSEPORT listener)."""
         deadline = time.time() + timeout_s
+        pids = set()
         while time.time() < deadline:
             if self.proc.poll() is not None:
                 return False
@@ -104,11 +107,15 @@ class ServerProcess:
                 c = http.client.HTTPConnection("127.0.0.1", self.port, timeout=60)
                 c.request("GET", "/ready")
                 r = c.getresponse()
-                r.read()
+                body = r.read()
                 if r.status == 200:
-                    self.conn = c
-                    return True
+                    pids.add(json.loads(body).get("worker", {}).get("pid"))
+                    if len(pids) >= workers:
+                        self.conn = c
+                        return True
                 c.close()
+                if r.status == 200:
+                    continue
             except OSError:
                 pass
             time.sleep(0.25)

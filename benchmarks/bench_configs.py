@@ -290,7 +290,7 @@ def mode_concurrent_http(args):
     byte. One untimed burst warms the server; the second is reported."""
     from log_parser_amd.native import N
     from log_parser_amd.serve.__main__ import raise_fd_limit
-    from log_parser_amd.utils.restbench import ServerProcess, write_library
+    from log_parser_amd.utils.restbench import ServerProcess, collect_stages, stage_breakdown, write_library
     from log_parser_amd.utils.synth import realistic_library
     n = args.requests
     if raise_fd_limit() < n + 256:
@@ -318,7 +318,10 @@ def mode_concurrent_http(args):
                 lines_of.append(int(s_))
         idx = np.array([sizes_set.index(int(s_)) * 4 + i % 4 for i, s_ in enumerate(sizes)], np.int32)
         N.http_burst("127.0.0.1", srv.port, msgs, idx[:min(n, 2000)], 300.0)          # warm-up burst
+        workers = max(args.processes, 1)
+        st0 = collect_stages(srv.port, workers)
         lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0)
+        breakdown = stage_breakdown(st0, collect_stages(srv.port, workers), wall)
     finally:
         srv.stop()
     ok = lat >= 0
@@ -332,6 +335,7 @@ def mode_concurrent_http(args):
                       "max_ms": round(float(lat[ok].max()) * 1e3, 3),
                       "requests_per_s": round(int(done) / wall, 1), "lines_per_s": round(lines / wall, 1),
                       "wall_s": round(wall, 3), "bytes": int(sum(len(msgs[i]) for i in idx)),
+                      "breakdown": breakdown,
                       "transport": "native HTTP/1.1 front end, one keep-alive connection per request, 127.0.0.1"}))
 
 

@@ -1060,6 +1060,15 @@ PYBIND11_MODULE(_lpnative, m) {
         d["native_400"] = s.stats.native_400.load();
         return d;
       })
+      .def("stage_stats", [](HttpServer& s) {
+        const HttpStageStats& g = s.stages;
+        py::dict d;
+        d["parse"] = g.parse.load(); d["receive_s"] = g.receive_ns.load() * 1e-9;
+        d["validate_s"] = g.validate_ns.load() * 1e-9; d["drained"] = g.drained.load();
+        d["queue_s"] = g.queue_ns.load() * 1e-9; d["responses"] = g.responses.load();
+        d["handoff_s"] = g.handoff_ns.load() * 1e-9; d["sent"] = g.sent.load(); d["send_s"] = g.send_ns.load() * 1e-9;
+        return d;
+      })
       .def("stop", [](HttpServer& s) {
         py::gil_scoped_release nogil;
         s.stop();

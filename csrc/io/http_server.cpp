@@ -95,7 +95,8 @@ struct HttpServer::Conn {
   bool paused = false;      // EPOLLIN off: too much pipelined input while a request is in flight
   bool dead = false;        // closed; freed at the end of the event-loop iteration
   double last = 0;          // last read / write activity (idle-timeout sweep)
-  double t_first = 0;       // first byte of the request being received (LP_HTTP_TRACE)
+  double t_first = 0;       // first byte of the request being received
+  double t_resp = 0;        // respond() of the response being written (0: none timed)
   int n_recv = 0, n_wake = 0;
 };
 
@@ -110,6 +111,7 @@ struct HttpServer::Io {
     uint64_t conn;
     std::string data;
     bool keep;
+    double t_resp;
   };
   std::vector<Out> outbox;
 };
@@ -198,10 +200,17 @@ std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
     qcv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms)),
                     [&] { return !q_.empty() || stop_; });
   std::vector<HttpRequest> r;
+  const double t = now_s();
+  uint64_t qns = 0;
   while (!q_.empty() && (int)r.size() < max_n) {
     r.push_back(std::move(q_.front()));
     q_.pop_front();
     qn_.store(q_.size(), std::memory_order_release);
+    qns += (uint64_t)std::max(0.0, (t - r.back().t_arrival) * 1e9);
+  }
+  if (!r.empty()) {
+    stages.drained += r.size();
+    stages.queue_ns += qns;
   }
   return r;
 }
@@ -227,7 +236,7 @@ void HttpServer::respond(uint64_t id, int status, const std::string& content_typ
   data.append(body, n);   // header + body in one buffer: one send() for a small response
   {
     std::lock_guard<std::mutex> lk(io->om);
-    io->outbox.push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep});
+    io->outbox.push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep, now_s()});
   }
   uint64_t one = 1;
   (void)!write(io->efd, &one, 8);
@@ -236,6 +245,7 @@ void HttpServer::respond(uint64_t id, int status, const std::string& content_typ
 void HttpServer::respond_many(const uint64_t* ids, size_t k, int status, const std::string& content_type,
                               const char* const* bodies, const size_t* lens) {
   std::vector<std::vector<Io::Out>> per(ios_.size());
+  const double t = now_s();
   for (size_t i = 0; i < k; ++i) {
     const uint64_t id = ids[i];
     const int ioi = (int)(id & 0xFF);
@@ -243,7 +253,7 @@ void HttpServer::respond_many(const uint64_t* ids, size_t k, int status, const s
     const bool keep = (id >> 63) == 0;
     std::string data = head(status, content_type, lens[i], keep);
     data.append(bodies[i], lens[i]);
-    per[ioi].push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep});
+    per[ioi].push_back(Io::Out{(id & ~(uint64_t(1) << 63)) >> 8, std::move(data), keep, t});
   }
   for (size_t q = 0; q < per.size(); ++q) {
     if (per[q].empty()) continue;
@@ -298,6 +308,11 @@ void HttpServer::flush(Io* io, Conn* c) {
   if (c->out_off >= c->out.size()) {
     c->out.clear();
     c->out_off = 0;
+    if (c->t_resp > 0) {
+      stages.sent++;
+      stages.send_ns += (uint64_t)std::max(0.0, (now_s() - c->t_resp) * 1e9);
+      c->t_resp = 0;
+    }
     if (c->closing) {
       close_conn(io, c);
       return;
@@ -427,11 +442,15 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     // validated in place; the logs string is decoded later, once, straight into the Python bytes
     // object the engine packs from (bind.cpp next_requests)
     PodRequest pr;
-    const double tv = trace_ ? now_s() : 0;
+    const double tv = r.t_arrival;
     const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
+    const double tz = now_s();
+    stages.parse++;
+    stages.receive_ns += (uint64_t)std::max(0.0, (tv - c->t_first) * 1e9);
+    stages.validate_ns += (uint64_t)std::max(0.0, (tz - tv) * 1e9);
     if (trace_)
       fprintf(stderr, "lp-http-trace bytes %zu receive_us %.1f recvs %d wakeups %d validate_us %.1f\n", total,
-              (tv - c->t_first) * 1e6, c->n_recv, c->n_wake, (now_s() - tv) * 1e6);
+              (tv - c->t_first) * 1e6, c->n_recv, c->n_wake, (tz - tv) * 1e6);
     if (st == JIN_OK && (!pr.pod_nonnull || pr.logs_kind != 1)) {
       stats.native_400++;
       consume();
@@ -572,6 +591,10 @@ void HttpServer::io_loop(Io* io) {
             c->paused = false;
             set_events(io, c);
           }
+          const double tp = now_s();
+          stages.responses++;
+          stages.handoff_ns += (uint64_t)std::max(0.0, (tp - o.t_resp) * 1e9);
+          if (c->out.empty()) c->t_resp = tp;
           c->out += o.data;
           c->last = now_s();
           if (!o.keep) c->closing = true;

@@ -44,6 +44,16 @@ struct HttpStats {
   std::atomic<uint64_t> accepted{0}, requests{0}, bad_requests{0}, native_400{0};
 };
 
+// Where a decoded POST /parse spends its time on the native side (nanosecond sums; the Python
+// side -- pack / device / emit -- is added by serve/native_http.py): receive = first byte -> body
+// complete, validate = the JSON validation, queue = body complete -> drained by the pump,
+// handoff = respond() -> the IO thread picks the response up, send = picked up -> last byte
+// written to the socket.
+struct HttpStageStats {
+  std::atomic<uint64_t> parse{0}, receive_ns{0}, validate_ns{0}, drained{0}, queue_ns{0};
+  std::atomic<uint64_t> responses{0}, handoff_ns{0}, sent{0}, send_ns{0};
+};
+
 class HttpServer {
  public:
   HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s = 60.0);
@@ -68,6 +78,7 @@ class HttpServer {
   const std::shared_ptr<BufferPool>& pool() const { return pool_; }
   void stop();
   HttpStats stats;
+  HttpStageStats stages;
 
   struct Conn;
   struct Io;

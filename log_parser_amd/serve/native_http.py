@@ -12,6 +12,7 @@ Every other route (``/ready``, ``/metrics``, ``/admin/*``, the json.loads fallba
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import sys
@@ -37,6 +38,9 @@ class NativeHttpFrontend:
         # LP_PARSE_TRACE=1: per /parse request on stderr -- queue (body complete -> drained by the
         # pump) and engine (drained -> response queued) microseconds (tools/parse_tail.py)
         self._trace = {} if os.environ.get("LP_PARSE_TRACE") else None
+        # pump thread's busy time: turning drained requests into a batch (dispatch) and, for an
+        # inline batch, its responses (complete)
+        self._pump_s = {"dispatch": 0.0, "complete_inline": 0.0}
         self._t = threading.Thread(target=self._pump, name="lp-http-pump", daemon=True)
         self._t.start()
         log.info("native HTTP front end on %s:%d (%d IO threads)", host, self.port, io_threads)
@@ -63,6 +67,7 @@ class NativeHttpFrontend:
             reqs = self.srv.next_requests(b.max_requests, 100, direct)
             if not reqs:
                 continue
+            td = time.perf_counter()
             batch = []
             for req in reqs:
                 rid, kind = req[0], req[1]
@@ -90,11 +95,15 @@ class NativeHttpFrontend:
                         else:
                             self.svc.submit_parse(r[0], r[1], t0).add_done_callback(self._on_done(rid))
                         continue
+                    if path == "/admin/stages" and method == "GET":
+                        self._reply(rid, (200, "application/json", json.dumps(self.stages()).encode()))
+                        continue
                     self._reply(rid, self.svc.route(method, path, body))
                 except Exception as e:  # noqa: BLE001
                     log.exception("request handling failed")
                     self._reply(rid, (500, "application/json", ('{"error":"%s"}' % type(e).__name__).encode()))
             if batch:
+                self._pump_s["dispatch"] += time.perf_counter() - td
                 self._run_direct(b, batch)
 
     def _run_direct(self, b, batch) -> None:
@@ -111,7 +120,9 @@ class NativeHttpFrontend:
                 log.exception("batch failed")
                 self._batch_done(batch, None, e)
                 return
+            t = time.perf_counter()
             self._batch_done(batch, outs, None)
+            self._pump_s["complete_inline"] += time.perf_counter() - t
         else:
             b.pipe.submit(logs, lambda outs, exc: self._batch_done(batch, outs, exc))
 
@@ -138,6 +149,18 @@ class NativeHttpFrontend:
             lines.append("Received analysis request for pod: " + n)
             lines.append("Analysis complete for pod: " + n + ".")
         log_lines(log, logging.INFO, lines)
+
+    def stages(self) -> dict:
+        """Per-stage busy seconds of this process (GET /admin/stages): the native side's receive /
+        validate / queue / handoff / send sums (HttpServer.stage_stats) and the pump + pipeline
+        threads' dispatch / pack / device / emit / complete sums, with request and batch counts."""
+        out = {"pid": os.getpid(), "native": self.srv.stage_stats(), "pump": dict(self._pump_s)}
+        pipe = self.svc.batcher().pipe
+        if pipe is not None:
+            out["pipeline"] = dict(pipe.stage_s)
+            out["batches"] = pipe.batches
+            out["requests"] = pipe.requests
+        return out
 
     def close(self) -> None:
         self._stop.set()

@@ -43,6 +43,11 @@ class BatchPipeline:
         self._inflight = 0
         self.submitted = 0              # batches that went through the threads (not inline)
         self.timeline: Optional[list] = None   # set to [] to record (stage, batch size, start, end)
+        # busy seconds per stage (and batches / requests through them): the serving breakdown
+        # (/admin/stages, benchmarks/bench_configs.py concurrent_http)
+        self.stage_s = {"pack": 0.0, "device": 0.0, "emit": 0.0, "complete": 0.0}
+        self.batches = 0
+        self.requests = 0
         self._threads = [threading.Thread(target=self._device_loop, name="lp-pipe-device", daemon=True),
                          threading.Thread(target=self._emit_loop, name="lp-pipe-emit", daemon=True)]
         for t in self._threads:
@@ -59,12 +64,21 @@ class BatchPipeline:
         t0 = time.perf_counter()
         job = self.engine.pack_batch(logs)
         try:
+            t1 = time.perf_counter()
             self._device_fn(job)
+            t2 = time.perf_counter()
             outs = self.engine.emit_batch(job)
         finally:
             self.engine.release_batch(job)
+        t3 = time.perf_counter()
+        st = self.stage_s
+        st["pack"] += t1 - t0
+        st["device"] += t2 - t1
+        st["emit"] += t3 - t2
+        self.batches += 1
+        self.requests += len(logs)
         if self._on_batch:
-            self._on_batch(len(logs), time.perf_counter() - t0)
+            self._on_batch(len(logs), t3 - t0)
         return outs
 
     def submit(self, logs: Sequence, done: Done) -> None:
@@ -76,8 +90,10 @@ class BatchPipeline:
             log.exception("batch packing failed")
             done(None, e)
             return
+        t1 = time.perf_counter()
+        self.stage_s["pack"] += t1 - t0
         if self.timeline is not None:
-            self.timeline.append(("pack", len(logs), t0, time.perf_counter()))
+            self.timeline.append(("pack", len(logs), t0, t1))
         with self._lock:
             self._inflight += 1
             self.submitted += 1
@@ -96,8 +112,10 @@ class BatchPipeline:
             try:
                 ts = time.perf_counter()
                 self._device_fn(job)
+                te = time.perf_counter()
+                self.stage_s["device"] += te - ts
                 if self.timeline is not None:
-                    self.timeline.append(("device", len(job.logs), ts, time.perf_counter()))
+                    self.timeline.append(("device", len(job.logs), ts, te))
                 self._eq.put(item)
             except Exception as e:  # noqa: BLE001
                 log.exception("batch failed")
@@ -112,8 +130,10 @@ class BatchPipeline:
             try:
                 ts = time.perf_counter()
                 outs = self.engine.emit_batch(job)
+                te = time.perf_counter()
+                self.stage_s["emit"] += te - ts
                 if self.timeline is not None:
-                    self.timeline.append(("emit", len(job.logs), ts, time.perf_counter()))
+                    self.timeline.append(("emit", len(job.logs), ts, te))
             except Exception as e:  # noqa: BLE001
                 log.exception("response emission failed")
                 self._finish(job, done, None, e, t0)
@@ -131,8 +151,12 @@ class BatchPipeline:
             done(outs, exc)
         except Exception:  # noqa: BLE001
             log.exception("batch completion callback failed")
+        te = time.perf_counter()
+        self.stage_s["complete"] += te - ts
+        self.batches += 1
+        self.requests += len(job.logs)
         if self.timeline is not None:
-            self.timeline.append(("complete", len(job.logs), ts, time.perf_counter()))
+            self.timeline.append(("complete", len(job.logs), ts, te))
 
     def close(self) -> None:
         self._dq.put(None)

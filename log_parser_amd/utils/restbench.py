@@ -175,3 +175,50 @@ class ServerProcess:
                 self.proc.wait()
         if self.log is not subprocess.DEVNULL:
             self.log.close()
+
+
+def collect_stages(port: int, workers: int = 1, tries: int = 400) -> dict:
+    """GET /admin/stages from every serving process (fresh connections until ``workers`` distinct
+    pids answered; SO_REUSEPORT spreads them) -> {pid: stages}."""
+    got = {}
+    for _ in range(tries):
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
+        try:
+            c.request("GET", "/admin/stages")
+            r = c.getresponse()
+            d = json.loads(r.read())
+            got[d["pid"]] = d
+        finally:
+            c.close()
+        if len(got) >= workers:
+            break
+    return got
+
+
+def stage_breakdown(before: dict, after: dict, wall_s: float) -> dict:
+    """Per-stage totals between two ``collect_stages`` snapshots, summed over processes:
+    mean seconds per request of every native stage (receive, validate, queue, handoff, send) and
+    busy fraction of the wall time of every Python thread stage (dispatch, pack, device, emit,
+    complete) -- a thread stage near 1.0 x processes is the bottleneck."""
+    tot = {}
+    cnt = {}
+    for pid, a in after.items():
+        b = before.get(pid, {})
+        for k, v in a["native"].items():
+            bv = b.get("native", {}).get(k, 0)
+            (tot if k.endswith("_s") else cnt)[k] = (tot if k.endswith("_s") else cnt).get(k, 0) + v - bv
+        for grp in ("pump", "pipeline"):
+            for k, v in a.get(grp, {}).items():
+                tot[k] = tot.get(k, 0.0) + v - b.get(grp, {}).get(k, 0.0)
+        for k in ("batches", "requests"):
+            cnt[k] = cnt.get(k, 0) + a.get(k, 0) - b.get(k, 0)
+    per = lambda key, n: round(1e3 * tot.get(key, 0.0) / max(cnt.get(n, 0), 1), 4)  # noqa: E731
+    out = {"requests": cnt.get("parse", 0), "batches": cnt.get("batches", 0),
+           "mean_batch_requests": round(cnt.get("requests", 0) / max(cnt.get("batches", 0), 1), 1),
+           "per_request_ms": {"receive": per("receive_s", "parse"), "validate": per("validate_s", "parse"),
+                              "queue": per("queue_s", "drained"), "handoff": per("handoff_s", "responses"),
+                              "send": per("send_s", "sent")},
+           "thread_busy_fraction": {k: round(tot.get(k, 0.0) / wall_s, 3)
+                                    for k in ("dispatch", "pack", "device", "emit", "complete", "complete_inline")}}
+    return out
+

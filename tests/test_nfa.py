@@ -77,3 +77,71 @@ def test_nfa_mfma_gpu_equals_host(gpu_device, seed):
     members = [(i, N.compile_regex(p, 64, 4096)) for i, p in enumerate(PATS)]
     groups = pack_groups(members)
     assert _run(groups, lines, gpu_device) == _run(groups, lines, torch.device("cpu"))
+
+
+# ---- engine.nfa-engine=mfma end to end: the MFMA engine serving regexes whose DFA is refused
+MFMA_PATS = [r"error.{0,12}timeout", r"(a|b)*a(a|b){5}x", r"\bconn(ection)? (reset|refused).{0,9}port \d+",
+             r"(?i)fail(ed|ure)?.{0,8}retry \d", r"[A-Z]{2}\d{2,5}(-[a-z]+){1,3}\b"]
+
+
+def _mfma_engine(dev):
+    from log_parser_amd.engine import Engine
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.models.schema import PatternSet
+    from log_parser_amd.utils.config import Config, ScoringParams
+    from log_parser_amd.utils.synth import make_library
+    sets, trig = make_library(30, seed=12)
+    pats = [{"id": f"m{i}", "name": rx, "severity": "HIGH", "primary_pattern": {"regex": rx, "confidence": 0.8},
+             "context_extraction": {"lines_before": 1, "lines_after": 1}} for i, rx in enumerate(MFMA_PATS)]
+    sets.append(PatternSet.model_validate({"metadata": {"library_id": "mfma"}, "patterns": pats}))
+    p = ScoringParams()
+    # a small DFA budget sends the gap / counted shapes to the NFA engines; mfma serves them
+    lib = CompiledLibrary(sets, p, max_dfa_states=24, nfa_engine="mfma")
+    eng = Engine(lib, Config.load(overrides={"engine.device": str(dev), "engine.nfa-engine": "mfma"}), device=dev)
+    return eng, lib, sets, trig, p
+
+
+def _mfma_docs(trig, seed):
+    from log_parser_amd.utils.synth import make_log
+    extra = ["error while waiting: timeout", "connection refused by peer port 8080", "FAILED twice, retry 3",
+             "AB1234-foo-bar ok", "abababaabbbabx", "error.....................timeout"]
+    rng = random.Random(seed)
+    docs = []
+    for k in range(3):
+        lines = make_log(600 + 200 * k, trig, seed=seed + k, hit_rate=0.1).split("\n")
+        for _ in range(40):
+            lines.insert(rng.randrange(len(lines)), rng.choice(extra))
+        docs.append("\n".join(lines))
+    return docs
+
+
+def _check_mfma(dev):
+    import json
+    from log_parser_amd import golden
+    eng, lib, sets, trig, p = _mfma_engine(dev)
+    assert lib.summary()["nfa_mfma"] >= len(MFMA_PATS)
+    docs = _mfma_docs(trig, 5)
+    outs = [json.loads(o) for o in eng.analyze_batch_json(docs)]
+    ft = golden.FrequencyTracker(p)
+    got_m = 0
+    for o, d in zip(outs, docs):
+        g = golden.analyze(d, sets, p, ft)
+        assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o["events"]] == \
+            [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]]
+        np.testing.assert_allclose([e["score"] for e in o["events"]], [e["score"] for e in g["events"]], rtol=1e-12)
+        got_m += sum(e["matchedPattern"]["id"].startswith("m") for e in o["events"])
+    assert got_m > 20
+    return eng
+
+
+def test_engine_nfa_mfma_end_to_end_cpu():
+    """engine.nfa-engine=mfma through the whole engine (host twin of the MFMA kernel) == golden."""
+    _check_mfma(torch.device("cpu"))
+
+
+@pytest.mark.gpu
+def test_engine_nfa_mfma_end_to_end_gpu(gpu_device):
+    """The same on the GPU: the NFA regexes are matched by the MFMA state-transition kernel
+    (k_nfa_* on matrix cores) inside the engine's match stage, results == golden (rtol 1e-12)."""
+    eng = _check_mfma(gpu_device)
+    assert any(g.numel() for g in eng.tabs["nfa_scan_lists"].values())

@@ -109,7 +109,7 @@ static EvTables ev_from(const py::tuple& t) {
 }
 
 // (blob ptr, lds_words, ngroups, row_base, stride, thr, init_row, init_state, ncol, gt_off, fin_off
-//  [each a 4-tuple], bm_off, rid_off)
+//  [each a 4-tuple], bm_off, rid_off, am_off, gm_off [4-tuple])
 static ScanPass scan_pass_from(const py::tuple& t) {
   ScanPass S;
   S.blob = P<const uint32_t>(t[0].cast<uint64_t>());
@@ -128,7 +128,8 @@ static ScanPass scan_pass_from(const py::tuple& t) {
   }
   S.bm_off = t[11].cast<int>();
   S.rid_off = t[12].cast<int>();
-  S.am_off = t.size() > 13 ? t[13].cast<int>() : -1;
+  S.am_off = t[13].cast<int>();
+  for (int g = 0; g < 4; ++g) S.gm_off[g] = (int)q(14, g);
   return S;
 }
 
@@ -553,6 +554,7 @@ PYBIND11_MODULE(_lpnative, m) {
     r["nregs"] = d.nregs;
     r["bytemap"] = vbytes(d.bytemap.data(), d.bytemap.size());
     r["trans"] = vbytes(d.trans.data(), d.trans.size() * 4);
+    r["acc"] = vbytes(d.acc.data(), d.acc.size() * 4);
     r["fin"] = vbytes(d.fin.data(), d.fin.size() * 4);
     return r;
   }, py::arg("patterns"), py::arg("max_states") = 4096);

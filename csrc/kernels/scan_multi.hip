@@ -3,7 +3,7 @@
 // The reference runs every primary regex over every line (AnalysisService.java:89-95). Regexes
 // with a usable literal factor are reached through the literal prefilter; the rest (e.g.
 // "\b[A-Z]{3,}_\d{4}\b", IP:port shapes, "^\s+at ..." frames) must scan the whole text. They are
-// compiled at library load into *scan groups*: up to 16 regexes determinised together into one
+// compiled at library load into *scan groups*: up to 32 regexes determinised together into one
 // multi-regex DFA (jregex.h MultiDfa), so one table walk per byte answers all members. A *pass*
 // holds up to 4 groups walked together.
 //
@@ -16,9 +16,9 @@
 //     States are numbered so that every state from which ANY regex can accept
 //     (on some next byte, at end of line or before a final terminator) comes last: "a match may
 //     have happened" is just max(row offset) >= thr[g] -- one v_max per byte, no mask traffic.
-//   * global (rare path): exact uint32 rows, next state id | accept mask << 16 (masks of the
-//     regexes accepting BEFORE the byte; the '\n' column carries the end-of-line accepts), the
-//     per-state [EOL, before-final-terminator] masks and the regex ids.
+//   * global (rare path): exact rows of next state ids and, indexed alike, uint32 accept masks
+//     (the regexes accepting BEFORE the byte; the '\n' column carries the end-of-line accepts),
+//     the per-state [EOL, before-final-terminator] masks and the regex ids.
 //
 // Work split: one lane walks a RUN of SCAN_RUN consecutive lines as ONE byte stream (the '\n'
 // between lines is the restart column), so a wave's time is the max of 64 run lengths, not of 64
@@ -74,6 +74,9 @@ LP_HD uint32_t scan_state_of(const ScanPass& S, int g, uint32_t row_byte) {
 LP_HD uint32_t scan_step(const ScanPass& S, int g, uint32_t st, uint32_t col) {
   return S.blob[S.gt_off[g] + st * (uint32_t)S.ncol[g] + col];
 }
+LP_HD uint32_t scan_mask(const ScanPass& S, int g, uint32_t st, uint32_t col) {
+  return S.blob[S.gm_off[g] + st * (uint32_t)S.ncol[g] + col];
+}
 LP_HD uint32_t scan_fin(const ScanPass& S, int g, uint32_t st, int ft) {
   return S.blob[S.fin_off[g] + 2 * st + ft];
 }
@@ -83,7 +86,7 @@ LP_HD void scan_emit(const ScanPass& S, int g, uint32_t m, int64_t line, Emit&& 
   while (m) {
     const int r = __builtin_ctz(m);
     m &= m - 1;
-    emit(((int64_t)S.blob[S.rid_off + 16 * g + r] << 32) | line);
+    emit(((int64_t)S.blob[S.rid_off + 32 * g + r] << 32) | line);
   }
 }
 
@@ -96,9 +99,9 @@ LP_HD void scan_line_exact(const ScanPass& S, const uint32_t* bm, const uint8_t*
     uint32_t st = S.init_state[g], acc = 0;
     for (int t = 0; t < n; ++t) {
       if (t == ft) acc |= scan_fin(S, g, st, 1);
-      const uint32_t e = scan_step(S, g, st, ((bm[s[t]] >> (8 * g)) & 0xFFu) >> 1);
-      acc |= e >> 16;
-      st = e & 0xFFFFu;
+      const uint32_t col = ((bm[s[t]] >> (8 * g)) & 0xFFu) >> 1;
+      acc |= scan_mask(S, g, st, col);
+      st = scan_step(S, g, st, col);
     }
     acc |= scan_fin(S, g, st, 0);
     scan_emit(S, g, acc, line, emit);
@@ -153,9 +156,8 @@ __device__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, const ui
     const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
     const uint32_t nx = (w[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 0xFFu;
     const uint32_t col = (c == 0x0Du && nx == 0x0Au) ? 0u : ((bm[c] >> (8 * g)) & 0xFFu) >> 1;
-    const uint32_t e = scan_step(S, g, st, col);
-    lacc |= e >> 16;
-    st = e & 0xFFFFu;
+    lacc |= scan_mask(S, g, st, col);
+    st = scan_step(S, g, st, col);
     if (col == 1u) {
       scan_emit(S, g, lacc, l, emit);
       lacc = 0;
@@ -175,7 +177,7 @@ __device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32
                                                  int64_t p_lo, int64_t p_end, int64_t x0, int64_t x1,
                                                  const int64_t* __restrict__ line_start, int g, uint32_t xr,
                                                  Emit&& emit) {
-  const uint16_t* __restrict__ am = reinterpret_cast<const uint16_t*>(S.blob + S.am_off);
+  const uint32_t* __restrict__ am = S.blob + S.am_off;
   // in-range positions of the block; a run holds <= SCAN_RUN lines, so an in-range byte belongs
   // to line l0 + k, k = in-range '\n's before it (0..3): per-line masks accumulate branch-free
   const int lo = p_lo > p0 ? (int)(p_lo - p0) : 0;
@@ -187,7 +189,7 @@ __device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32
     uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
     if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;
     const uint32_t b = (lds_ld32(c * 4) >> (8 * g)) & 0xFFu;
-    const uint32_t m = ((inr >> j) & 1u) ? (uint32_t)am[(xr + b) >> 1] : 0u;
+    const uint32_t m = ((inr >> j) & 1u) ? am[(xr + b) >> 1] : 0u;
     a0 |= k == 0 ? m : 0u;
     a1 |= k == 1 ? m : 0u;
     a2 |= k == 2 ? m : 0u;

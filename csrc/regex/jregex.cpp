@@ -1547,7 +1547,7 @@ uint32_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t
 }  // namespace
 
 MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states) {
-  if (patterns.empty() || patterns.size() > (size_t)MULTI_MAX_REGS) throw Unsupported("multi-DFA: 1..16 regexes");
+  if (patterns.empty() || patterns.size() > (size_t)MULTI_MAX_REGS) throw Unsupported("multi-DFA: 1..32 regexes");
   std::vector<Compiled> comp;
   comp.reserve(patterns.size());
   bool wordb = false;
@@ -1622,7 +1622,7 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
   std::vector<uint64_t> init(nw, 0);
   init[nw - 1] = P_BOS;
   intern(init);
-  std::vector<uint32_t> rows, fin;
+  std::vector<uint32_t> rows, racc, fin;
   std::vector<uint64_t> U(nw, 0), B(nw, 0);
   for (size_t si = 0; si < states.size(); ++si) {
     const std::vector<uint64_t> A = states[si];
@@ -1642,12 +1642,15 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
         B[nw - 1] = (uint64_t)((nk == N_W && wordb) ? P_W : P_N);
         next = (uint32_t)intern(B);
       }
-      rows.push_back(next | (acc_k[nk] << 16));
+      rows.push_back(next);
+      racc.push_back(acc_k[nk]);
     }
   }
   d.nstates = (int)states.size() + 1;
   d.trans.assign((size_t)d.nclasses, 0);            // DEAD row
   d.trans.insert(d.trans.end(), rows.begin(), rows.end());
+  d.acc.assign((size_t)d.nclasses, 0);
+  d.acc.insert(d.acc.end(), racc.begin(), racc.end());
   d.fin.assign(2, 0);
   d.fin.insert(d.fin.end(), fin.begin(), fin.end());
   return d;
@@ -1659,9 +1662,9 @@ uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n) {
   uint32_t st = 1, acc = 0;
   for (int64_t t = 0; t < n; ++t) {
     if (t == ft) acc |= d.fin[2 * st + 1];
-    const uint32_t e = d.trans[(size_t)st * d.nclasses + d.bytemap[s[t]]];
-    acc |= e >> 16;
-    st = e & 0xFFFF;
+    const size_t i = (size_t)st * d.nclasses + d.bytemap[s[t]];
+    acc |= d.acc[i];
+    st = d.trans[i];
   }
   return acc | d.fin[2 * st];
 }

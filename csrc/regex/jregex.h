@@ -113,19 +113,20 @@ struct Compiled {
 // max_positions bounds the byte-level NFA; the code-point NFA of a BPG program has <= BPG_MAX_POS.
 Compiled compile(const std::string& pattern, int max_dfa_states, int max_positions);
 
-// Multi-regex DFA ("scan group"): the Glushkov NFAs of up to 16 regexes determinised TOGETHER, so
+// Multi-regex DFA ("scan group"): the Glushkov NFAs of up to 32 regexes determinised TOGETHER, so
 // one table walk per byte answers find() for all of them (Aho-Corasick / RE2::Set style). Used
 // for regexes without a usable literal factor, which must be run over every line. Unlike the
 // single-regex DFA there is no absorbing ACCEPT state: a transition reports the regexes that
 // accept BEFORE its byte and the walk goes on for the others.
-//   trans[s * nclasses + cls] = next state (bits 0..15) | accept mask (bits 16..31)
+//   trans[s * nclasses + cls] = next state (< 65536), acc[same] = accept mask of that transition
 //   fin[2 s] = regexes accepting at end of line, fin[2 s + 1] = before a final line terminator
 // State 0 = DEAD (every member anchored and failed), state 1 = start of line.
-constexpr int MULTI_MAX_REGS = 16;
+constexpr int MULTI_MAX_REGS = 32;
 struct MultiDfa {
   int nstates = 0, nclasses = 0, nregs = 0;
   std::vector<uint8_t> bytemap;
   std::vector<uint32_t> trans;
+  std::vector<uint32_t> acc;
   std::vector<uint32_t> fin;
 };
 // throws Unsupported (state limit, > MULTI_MAX_REGS, a member without a byte automaton)

@@ -462,7 +462,7 @@ class CompiledLibrary:
                           if self.host_local[r] >= 0]
 
     # multi-regex DFA scan groups (csrc/kernels/scan_multi.hip)
-    SCAN_GROUP_REGS = 16            # members per multi-regex DFA (16-bit accept masks)
+    SCAN_GROUP_REGS = 32            # members per multi-regex DFA (32-bit accept masks)
     SCAN_GROUP_BYTES = 24 << 10     # LDS bytes of one group's uint16 transition rows
     SCAN_PASS_ROWS = 48 << 10       # LDS bytes of one pass's rows (+ 1 KiB bm4)
     SCAN_MAX_STATES = 4096
@@ -523,33 +523,37 @@ class CompiledLibrary:
         then the exact tables the rare path reads from global memory. States are renumbered so
         that the ones from which a member can accept come last (the hot loop's threshold test)."""
         BM_BYTES = 2048                                     # bm4 (512 entries) at LDS byte 0, rows after
-        rows16, exact, fins = [], [], []
+        rows16, exact, emask, fins = [], [], [], []
         meta = {k: [0] * 4 for k in ("row_base", "stride", "thr", "init_row", "init_state", "ncol")}
         bm4 = np.zeros(256, np.uint32)
         base = BM_BYTES // 2                                # in uint16 entries
         for g, (regs, d) in enumerate(groups):
             ns, nc = d["nstates"], d["nclasses"]
             t = np.frombuffer(d["trans"], np.uint32).reshape(ns, nc)
+            a = np.frombuffer(d["acc"], np.uint32).reshape(ns, nc)
             fin = np.frombuffer(d["fin"], np.uint32).reshape(ns, 2)
-            accepting = ((t >> np.uint32(16)) != 0).any(axis=1) | (fin != 0).any(axis=1)
+            accepting = (a != 0).any(axis=1) | (fin != 0).any(axis=1)
             order = np.concatenate([np.flatnonzero(~accepting), np.flatnonzero(accepting)])
             new_of = np.empty(ns, np.uint32)
             new_of[order] = np.arange(ns, dtype=np.uint32)
             ncol = nc + 2
             stride = cls._row_stride(d)
             init_new = int(new_of[1])
-            # exact table (state ids), rows in the new order
+            # exact tables (state ids; accept masks indexed alike), rows in the new order
             ex = np.zeros((ns, ncol), np.uint32)
             ex[:, 0] = np.arange(ns, dtype=np.uint32)                         # hold
-            ex[:, 1] = np.uint32(init_new) | (fin[order, 0] << np.uint32(16))  # '\n': restart + EOL accepts
-            to = t[order]
-            ex[:, 2:] = new_of[to & np.uint32(0xFFFF)] | (to & np.uint32(0xFFFF0000))
+            ex[:, 1] = np.uint32(init_new)                                    # '\n': restart ...
+            ex[:, 2:] = new_of[t[order]]
+            em = np.zeros((ns, ncol), np.uint32)
+            em[:, 1] = fin[order, 0]                                          # ... + EOL accepts
+            em[:, 2:] = a[order]
             exact.append(ex.reshape(-1))
+            emask.append(em.reshape(-1))
             fins.append(fin[order].reshape(-1))
             # LDS rows: byte offset of the next state's row
             rowb = (2 * (base + np.arange(ns, dtype=np.int64) * stride)).astype(np.int64)
             r16 = np.zeros((ns, stride), np.uint16)
-            r16[:, :ncol] = rowb[ex & np.uint32(0xFFFF)].astype(np.uint16)
+            r16[:, :ncol] = rowb[ex].astype(np.uint16)
             rows16.append(r16.reshape(-1))
             meta["row_base"][g], meta["stride"][g] = 2 * base, stride
             meta["thr"][g] = int(2 * (base + int((~accepting).sum()) * stride))
@@ -566,37 +570,41 @@ class CompiledLibrary:
         parts = [bm4, np.zeros(256, np.uint32), r.view(np.uint32)]    # entries 256..511: hold
         off = 512 + r.size // 2
         lds_words = off
-        gt_off, fin_off = [0] * 4, [0] * 4
+        gt_off, gm_off, fin_off = [0] * 4, [0] * 4, [0] * 4
         for g in range(len(groups)):
             gt_off[g] = off
             parts.append(exact[g])
             off += exact[g].size
         for g in range(len(groups)):
+            gm_off[g] = off
+            parts.append(emask[g])
+            off += emask[g].size
+        for g in range(len(groups)):
             fin_off[g] = off
             parts.append(fins[g])
             off += fins[g].size
-        rid = np.zeros(16 * 4, np.uint32)
+        G = 32                                   # regex-id slots per group (scan_multi.hip scan_emit)
+        rid = np.zeros(G * 4, np.uint32)
         for g, (regs, _) in enumerate(groups):
-            rid[16 * g:16 * g + len(regs)] = regs
+            rid[G * g:G * g + len(regs)] = regs
         rid_off = off
         parts.append(rid)
         off += rid.size
-        # accept masks laid out like the LDS rows (u16 entry i of the LDS blob <-> mask i): the
+        # accept masks laid out like the LDS rows (u16 entry i of the LDS blob <-> u32 mask i): the
         # device's exact re-walk follows the LDS rows and loads each transition's mask with an
         # address known from the LDS chain -- 16 independent global loads per block instead of a
         # chain of 16 dependent exact-row loads
-        am = np.zeros(2 * lds_words, np.uint16)
+        am = np.zeros(2 * lds_words, np.uint32)
         for g, (regs, d) in enumerate(groups):
             ns, ncol, stride = d["nstates"], meta["ncol"][g], meta["stride"][g]
             b0 = meta["row_base"][g] // 2
-            ex = exact[g].reshape(ns, ncol)
             idx = b0 + np.arange(ns, dtype=np.int64)[:, None] * stride + np.arange(ncol, dtype=np.int64)[None, :]
-            am[idx] = (ex >> np.uint32(16)).astype(np.uint16)
+            am[idx] = emask[g].reshape(ns, ncol)
         am_off = off
-        parts.append(am.view(np.uint32))
+        parts.append(am)
         blob = np.concatenate(parts)
         return dict(blob=blob, lds_words=lds_words, ngroups=len(groups), gt_off=tuple(gt_off),
-                    fin_off=tuple(fin_off), bm_off=0, rid_off=rid_off, am_off=am_off,
+                    fin_off=tuple(fin_off), gm_off=tuple(gm_off), bm_off=0, rid_off=rid_off, am_off=am_off,
                     regs=[x for regs, _ in groups for x in regs], **{k: tuple(v) for k, v in meta.items()})
 
     def _build_prefilter(self):
@@ -717,7 +725,7 @@ class CompiledLibrary:
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
         t["scan_passes"] = [(b.data_ptr(), p["lds_words"], p["ngroups"], p["row_base"], p["stride"], p["thr"],
                              p["init_row"], p["init_state"], p["ncol"], p["gt_off"], p["fin_off"], p["bm_off"],
-                             p["rid_off"], p["am_off"]) for b, p in zip(t["scan_blobs"], self.scan_passes)]
+                             p["rid_off"], p["am_off"], p["gm_off"]) for b, p in zip(t["scan_blobs"], self.scan_passes)]
         t["conf"], t["sev"] = T(self.conf), T(self.sev)
         t["sev_index"] = T(self.sev_index)
         t["ctx_before"], t["ctx_after"] = T(self.ctx_before), T(self.ctx_after)

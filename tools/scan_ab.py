@@ -63,7 +63,10 @@ def main():
     ap.add_argument("--lines", type=int, default=2_500_000)
     ap.add_argument("--engine", default="both", choices=["dfa", "mfma", "bpg", "both", "all"])
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--group-regs", type=int, default=0, help="members per scan group (0: the library default)")
     args = ap.parse_args()
+    if args.group_regs:
+        CompiledLibrary.SCAN_GROUP_REGS = args.group_regs
     dev = torch.device("cuda", 0)
     sets, trig = library(args.regexes)
     lib = CompiledLibrary(sets, ScoringParams())
@@ -75,7 +78,7 @@ def main():
     t = t.to(dev)
     ls, ll = K.split_lines(t, len(data))
     L = ls.numel()
-    rec = {"regexes": args.regexes, "lines": L, "bytes": len(data)}
+    rec = {"regexes": args.regexes, "lines": L, "bytes": len(data), "group_regs": CompiledLibrary.SCAN_GROUP_REGS}
     tabs = lib.device_tables(dev)
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
     hits = {}

@@ -967,8 +967,15 @@ PYBIND11_MODULE(_lpnative, m) {
       .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; });
 
   py::class_<HttpServer>(m, "HttpServer")
-      .def(py::init<const std::string&, int, int, int64_t, double>(), py::arg("host"), py::arg("port"),
-           py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30, py::arg("idle_timeout_s") = 60.0)
+      .def(py::init([](const std::string& host, int port, int io_threads, int64_t max_body, double idle,
+                       double io_spin_us, double pump_spin_us, bool quickack, int rcvbuf, bool trace) {
+             HttpOptions o;
+             o.io_spin_us = io_spin_us; o.pump_spin_us = pump_spin_us; o.quickack = quickack; o.rcvbuf = rcvbuf;
+             o.trace = trace;
+             return new HttpServer(host, port, io_threads, max_body, idle, o);
+           }), py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30,
+           py::arg("idle_timeout_s") = 60.0, py::arg("io_spin_us") = 0.0, py::arg("pump_spin_us") = 1000.0,
+           py::arg("quickack") = true, py::arg("rcvbuf") = 0, py::arg("trace") = false)
       .def_property_readonly("port", &HttpServer::port)
       .def("pending", &HttpServer::pending)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms, bool raw) {

@@ -116,20 +116,20 @@ struct HttpServer::Io {
   std::vector<Out> outbox;
 };
 
-HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s)
+HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s,
+                       const HttpOptions& opt)
     : host_(host), port_(port), max_body_(max_body), idle_timeout_s_(idle_timeout_s) {
   io_threads = std::max(1, std::min(io_threads, kMaxIo));
-  if (const char* e = getenv("LP_HTTP_SPIN_US")) io_spin_s_ = atof(e) * 1e-6;
+  io_spin_s_ = opt.io_spin_us * 1e-6;
   // the pump polls for the next request this long before sleeping on the queue's condition
   // variable (a sleeping pump took ~45 us to wake: /parse "queue" time, tools/parse_tail.py)
-  pump_spin_s_ = 1e-3;
-  if (const char* e = getenv("LP_HTTP_PUMP_SPIN_US")) pump_spin_s_ = atof(e) * 1e-6;
+  pump_spin_s_ = opt.pump_spin_us * 1e-6;
   // Receive-side TCP: ACK every read at once. With delayed ACKs ~1-2% of 1 MB request bodies
   // stalled ~1.5 ms in the receive (the sender waiting on a window update): /parse p99 2.1 ms ->
-  // 0.56 ms (profiles/r2_v12/tail_*.json; LP_HTTP_QUICKACK=0 restores delayed ACKs).
-  if (const char* e = getenv("LP_HTTP_QUICKACK")) quickack_ = atoi(e) != 0;
-  if (const char* e = getenv("LP_HTTP_RCVBUF")) rcvbuf_ = atoi(e);
-  trace_ = getenv("LP_HTTP_TRACE") != nullptr;
+  // 0.56 ms (profiles/r2_v12/tail_*.json; server.tcp-quickack=false restores delayed ACKs).
+  quickack_ = opt.quickack;
+  rcvbuf_ = opt.rcvbuf;
+  trace_ = opt.trace;
   for (int i = 0; i < io_threads; ++i) {
     auto io = std::make_unique<Io>();
     io->index = i;

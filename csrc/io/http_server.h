@@ -54,9 +54,20 @@ struct HttpStageStats {
   std::atomic<uint64_t> responses{0}, handoff_ns{0}, sent{0}, send_ns{0};
 };
 
+// Tuning of the front end (config keys server.io-spin-us, server.pump-spin-us, server.tcp-quickack,
+// server.rcvbuf-bytes, server.trace-requests; serve/native_http.py passes them)
+struct HttpOptions {
+  double io_spin_us = 0;        // IO threads poll (no sleep) this long after activity
+  double pump_spin_us = 1000;   // next_requests polls this long before sleeping on the queue
+  bool quickack = true;         // TCP_QUICKACK re-armed per read
+  int rcvbuf = 0;               // SO_RCVBUF of accepted sockets (0 = autotuned)
+  bool trace = false;           // per-request receive / validate timings on stderr
+};
+
 class HttpServer {
  public:
-  HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s = 60.0);
+  HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s = 60.0,
+             const HttpOptions& opt = HttpOptions());
   ~HttpServer();
   int port() const { return port_; }
   // up to `max_n` pending requests; waits up to `timeout_ms` for the first one
@@ -97,11 +108,11 @@ class HttpServer {
   int port_;
   int64_t max_body_;
   double idle_timeout_s_;
-  double io_spin_s_ = 0;     // LP_HTTP_SPIN_US: IO threads poll (no sleep) this long after activity
-  bool trace_ = false;       // LP_HTTP_TRACE: per-request receive / validate timings on stderr
-  double pump_spin_s_ = 0;   // next_requests polls this long before waiting (1 ms; LP_HTTP_PUMP_SPIN_US)
-  bool quickack_ = true;     // TCP_QUICKACK re-armed per read (LP_HTTP_QUICKACK=0: delayed ACKs)
-  int rcvbuf_ = 0;           // LP_HTTP_RCVBUF: SO_RCVBUF of accepted sockets (0 = autotuned)
+  double io_spin_s_ = 0;     // HttpOptions (seconds)
+  bool trace_ = false;
+  double pump_spin_s_ = 0;
+  bool quickack_ = true;
+  int rcvbuf_ = 0;
   std::atomic<bool> stop_{false};
   std::vector<std::unique_ptr<Io>> ios_;
   std::vector<std::thread> threads_;

@@ -31,13 +31,19 @@ class NativeHttpFrontend:
     def __init__(self, service: Service, host: str = "0.0.0.0", port: int = 8080, io_threads: int = 2):
         self.svc = service
         self.svc.batcher()                               # compile the library before accepting
-        self.srv = N.HttpServer(host, port, io_threads, int(service.config["server.max-body-bytes"]),
-                                float(service.config["server.idle-timeout-s"]))
+        cfg = service.config
+        trace = bool(cfg.get("server.trace-requests", False))
+        self.srv = N.HttpServer(host, port, io_threads, int(cfg["server.max-body-bytes"]),
+                                float(cfg["server.idle-timeout-s"]), io_spin_us=float(cfg["server.io-spin-us"]),
+                                pump_spin_us=float(cfg["server.pump-spin-us"]),
+                                quickack=bool(cfg["server.tcp-quickack"]), rcvbuf=int(cfg["server.rcvbuf-bytes"]),
+                                trace=trace)
         self.port = self.srv.port
         self._stop = threading.Event()
-        # LP_PARSE_TRACE=1: per /parse request on stderr -- queue (body complete -> drained by the
-        # pump) and engine (drained -> response queued) microseconds (tools/parse_tail.py)
-        self._trace = {} if os.environ.get("LP_PARSE_TRACE") else None
+        # server.trace-requests: per /parse request on stderr -- receive / validate (native side),
+        # queue (body complete -> drained by the pump) and engine (drained -> response queued)
+        # microseconds (tools/parse_tail.py)
+        self._trace = {} if trace else None
         # pump thread's busy time: turning drained requests into a batch (dispatch) and, for an
         # inline batch, its responses (complete)
         self._pump_s = {"dispatch": 0.0, "complete_inline": 0.0}

@@ -109,6 +109,17 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)
     "server.idle-timeout-s": (60.0, float),
+    # native front end: IO threads poll this long after activity before sleeping in epoll_wait
+    "server.io-spin-us": (0.0, float),
+    # native front end: the pump polls for the next request this long before sleeping on the queue
+    # (a sleeping pump took ~45 us to wake, tools/parse_tail.py)
+    "server.pump-spin-us": (1000.0, float),
+    # TCP_QUICKACK on every read (delayed ACKs stalled ~1-2% of 1 MB bodies by ~1.5 ms)
+    "server.tcp-quickack": (True, bool),
+    # SO_RCVBUF of accepted sockets (0 = kernel autotuning)
+    "server.rcvbuf-bytes": (0, int),
+    # per-request receive / validate / queue / engine microseconds on stderr (tools/parse_tail.py)
+    "server.trace-requests": (False, bool),
     # freeze the startup heap + raise GC thresholds in the batching server (submit-path latency)
     "server.gc-tuning": (True, bool),
     # Python GIL switch interval in the serving process (ms; 0 = interpreter default 5 ms). The

@@ -1,5 +1,5 @@
-"""Where the slow POST /parse requests spend their time: a server process with LP_HTTP_TRACE (receive /
-validate per request, C++ front end) and LP_PARSE_TRACE (queue / engine per request, pump) on, N
+"""Where the slow POST /parse requests spend their time: a server process with server.trace-requests
+on (receive / validate per request from the C++ front end, queue / engine per request from the pump), N
 sequential 10k-line requests from the raw client; prints the median and the slowest requests with
 their server-side breakdown (requests are sequential, so trace line i is request i).
 
@@ -24,10 +24,9 @@ def main():
     from log_parser_amd.utils import restbench
     from log_parser_amd.utils.synth import make_log, realistic_library
     sets, trig = realistic_library(1000, seed=7)
-    os.environ["LP_HTTP_TRACE"] = "1"
-    os.environ["LP_PARSE_TRACE"] = "1"
     log_path = os.path.join(tempfile.mkdtemp(prefix="lp-tail-"), "server.log")
-    server = restbench.ServerProcess(restbench.write_library(sets), a.device, http="native", log_path=log_path)
+    server = restbench.ServerProcess(restbench.write_library(sets), a.device, http="native", log_path=log_path,
+                                     extra=["-Dserver.trace-requests=true"])
     try:
         if not server.wait_ready():
             raise SystemExit("server did not come up")

@@ -30,6 +30,15 @@ def bind_numa(cfg: Config) -> None:
         logging.getLogger("log_parser_amd.server").warning("NUMA binding skipped: %s", e)
 
 
+def io_threads(cfg: Config, processes: int = 1) -> int:
+    """``server.io-threads``, or (0) half of this process's share of the CPU budget, 2..8."""
+    n = int(cfg.get("server.io-threads", 0) or 0)
+    if n > 0:
+        return n
+    from ..utils.numa import cpu_budget
+    return max(2, min(8, cpu_budget() // (2 * max(processes, 1))))
+
+
 def raise_fd_limit() -> int:
     """Open-file soft limit up to the hard limit: every keep-alive connection is a descriptor, and
     BASELINE config 5 holds 10k of them at once."""
@@ -70,7 +79,7 @@ def main(argv=None):
     for sig in (signal.SIGINT, signal.SIGTERM):
         signal.signal(sig, lambda *_: stop.set())
     fe = NativeHttpFrontend(Service(cfg, proc=proc), cfg["server.host"], int(cfg["server.port"]),
-                            int(cfg["server.io-threads"]))
+                            io_threads(cfg, proc.nproc if proc is not None else 1))
     fe.serve_forever(stop)
 
 

@@ -99,7 +99,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.host": ("0.0.0.0", str),
     # HTTP front end: "native" (C++ epoll server, csrc/io/http_server.cpp) or "uvicorn" (FastAPI)
     "server.http": ("native", str),
-    "server.io-threads": (2, int),
+    # native front end IO threads (epoll loops receiving / validating bodies, sending responses);
+    # 0 = auto: half this process's CPU budget, 2..8 (tools/http_ceiling.py: the config-5 burst with no
+    # engine reaches 13.7k req/s with 2 threads, 32k with 8, on an 8-CPU container)
+    "server.io-threads": (0, int),
     # serving processes (serve/procs.py): 1 = this process only; N > 1 = N processes started before
     # any GPU call, each with its own SO_REUSEPORT listeners, GIL and pipeline, sharing ONE
     # frequency window (GPU memory over IPC) in arrival-ticket order; -1 = one per visible GPU.

@@ -73,3 +73,29 @@ def bind_to_gpu_numa(index: int) -> Optional[Set[int]]:
         return None
     os.sched_setaffinity(0, cpus)
     return cpus
+
+
+def cpu_budget() -> int:
+    """CPUs this process can actually use: its affinity set, capped by a cgroup CPU quota
+    (``cpu.max``, v2, or ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``, v1) -- a container's
+    ``os.cpu_count()`` shows the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0 and p > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)

@@ -211,7 +211,7 @@ def test_bpg_candidate_walks_match_host(gpu_device, li):
     text, ls, ll = _text_dev(lines, gpu_device)
     dfa = lib.device_tables(gpu_device)["dfa"]
     want = {(r, j) for r in lib.bpg_regs for j, s in enumerate(lines) if run_program(lib.bpg_program(r), s.encode())}
-    assert len(want) > 100
+    assert len(want) > 50
     # request path: every (regex, line) pair plus rejected slots (-1) and non-BPG regexes, shuffled
     pairs = [(r, j) for r in lib.bpg_regs for j in range(len(lines))]
     others = [r for r in range(len(lib.regexes)) if r not in set(lib.bpg_regs)]

@@ -348,7 +348,10 @@ class CompiledLibrary:
         self.host_lits: List[List[bytes]] = []        # backtracker regexes' required literals (host side path)
         nfa_members: List[Tuple[int, dict]] = []
         ctx_members: List[Tuple[int, dict]] = []
+        self._ctx_ext = (0, 0)
         for i, ri in enumerate(self.regexes):
+            if i == 4:
+                self._ctx_ext = (toff, aoff)     # the context DFAs' tables end here
             # the 4 context regexes are always DFAs: k_feat_cov walks their tables directly
             d = N.compile_regex(ri.pattern, max(self.max_dfa_states, 2048) if i < 4 else self.max_dfa_states, 4096)
             ri.kind = d["kind"]
@@ -749,10 +752,11 @@ class CompiledLibrary:
     @property
     def ctx_dfa_extent(self) -> Tuple[int, int]:
         """(trans, acc) entries spanned by the 4 context DFAs (pool entries 0..3, offset 0): the
-        context-feature kernel stages exactly this prefix of the pool in LDS."""
-        m = self.dfa_meta.reshape(-1, 4)
-        if m.shape[0] > 4:
-            return int(m[4, 0]), int(m[4, 2])
+        context-feature kernel stages exactly this prefix of the pool in LDS. (Recorded while the
+        pool is laid out: entry 4 may be a BPG program or a host regex, whose meta holds no DFA
+        offsets.)"""
+        if len(self.regexes) > 4:
+            return self._ctx_ext
         return int(self.dfa_trans.size), int(self.dfa_acc.size)
 
     @property

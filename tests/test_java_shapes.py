@@ -144,3 +144,15 @@ def test_engine_java_shapes_gpu_runner_matches_golden(gpu_device, seed):
     g = golden.analyze(big, sets, p, golden.FrequencyTracker(p))
     assert r.ev_line.numel() == len(g["events"])
     np.testing.assert_allclose(np.sort(r.score.cpu().numpy()), np.sort([e["score"] for e in g["events"]]), rtol=1e-12)
+
+
+def test_context_dfa_extent_with_non_dfa_neighbour():
+    """The context DFAs' table extent (what k_feat_cov stages in LDS) does not depend on what regex
+    5 compiles to: a BPG program or a backtracker regex there holds no DFA offsets in its meta."""
+    from log_parser_amd.utils.synth import make_library as ml
+    plain = CompiledLibrary(ml(5, seed=1)[0], ScoringParams())
+    ps = PatternSet.model_validate({"metadata": {"library_id": "x"}, "patterns": [
+        {"id": "b", "name": "b", "severity": "HIGH", "primary_pattern": {"regex": r"(\w+)\1", "confidence": 0.5}}]})
+    lib = CompiledLibrary([ps], ScoringParams())
+    assert lib.regexes[4].kind == KIND_FALLBACK
+    assert lib.ctx_dfa_extent == plain.ctx_dfa_extent and lib.ctx_dfa_extent[0] > 0

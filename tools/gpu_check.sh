@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 900 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py tests/test_nfa.py tests/test_regex.py tests/test_serve_procs.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu2_regex.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py tests/test_nfa.py tests/test_regex.py tests/test_serve_procs.py -m gpu -x -v --durations=15 --timeout 300 --timeout-method thread > gpurun_out/gpu2_regex.log 2>&1
 rc=$?; echo "regex tests rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 16 > gpurun_out/gpu3_scan16.log 2>&1
 rc=$?; echo "scan16 rc=$rc"; [ $rc -eq 0 ] || exit $rc

@@ -9,6 +9,8 @@ timeout -k 10 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-r
 rc=$?; echo "scan16 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 32 > gpurun_out/gpu3_scan32.log 2>&1
 rc=$?; echo "scan32 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u tools/nfa_ab.py --lines 1000000 > gpurun_out/gpu2_nfa_ab.log 2>&1
+rc=$?; echo "nfa_ab rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > gpurun_out/gpu2_bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u benchmarks/bench_configs.py concurrent_http --server-log gpurun_out/gpu2_http_srv1.log > gpurun_out/gpu2_http.log 2>&1

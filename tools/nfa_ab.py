@@ -40,6 +40,15 @@ SHAPES = {
     "repeated_group": r"(\w+\.){{2,}}{t}Ex",
     "ip_boundary": r"\b\d{{1,3}}(?:\.\d{{1,3}}){{3}}\b.{{0,4}}{t}",
     "alternation_loop": r"(?:ab|{t})+d.{{0,8}}e",
+    # the round-3 review's shapes, as written and scaled to the MFMA kernel's 64
+    # positions: the unscaled ones and the code-point ones are recorded as not runnable on MFMA
+    "r3_refused_600": r"Connection {t} refused.{{0,600}}port \d+",
+    "r3_gap_pair_300": r"error.{{0,300}}{t}.{{0,300}}retry",
+    "r3_refused_scaled": r"{t} refused.{{0,40}}port \d+",
+    "r3_gap_pair_scaled": r"error.{{0,20}}{t}.{{0,20}}retry",
+    "r3_unicode_letters": r"\p{{L}}+{t}Exception",
+    "r3_multiline": r"(?m)^{t}ERROR$",
+    "r3_java_dot": r"a.{{0,8}}{t}b",
 }
 FILL = ("the quick brown fox jumps over the lazy dog 10.0.0.7 port 8443 at com.acme.Foo. "
         "error while calling upstream, will retry in 5s refused by peer abd e")

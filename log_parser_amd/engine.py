@@ -691,7 +691,7 @@ class Engine:
         prep = self.prepare(text, n, ls, ll, segs, np.frombuffer(data, np.uint8) if n else None)
         carry = self.freq_carry()
         res = self.finish(prep, segs, carry if record else self._carry_before(BatchJob((), 0.0, recorded=True), prep,
-                                                                               carry), with_factors)
+                                                                               carry), with_factors=with_factors)
         if record:
             self.commit_frequency(res.freq_counts)
         return res, ls, ll

@@ -210,7 +210,8 @@ def test_bpg_candidate_walks_match_host(gpu_device, li):
         ["ERROR " + "x" * k + " disk" for k in range(0, 260, 13)]
     text, ls, ll = _text_dev(lines, gpu_device)
     dfa = lib.device_tables(gpu_device)["dfa"]
-    want = {(r, j) for r in lib.bpg_regs for j, s in enumerate(lines) if run_program(lib.bpg_program(r), s.encode())}
+    progs = {r: lib.bpg_program(r).tobytes() for r in lib.bpg_regs}      # the C++ host twin (bpg.h)
+    want = {(r, j) for r in lib.bpg_regs for j, s in enumerate(lines) if N.bpg_find(progs[r], s.encode())}
     assert len(want) > 50
     # request path: every (regex, line) pair plus rejected slots (-1) and non-BPG regexes, shuffled
     pairs = [(r, j) for r in lib.bpg_regs for j in range(len(lines))]

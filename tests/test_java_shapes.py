@@ -123,6 +123,12 @@ def test_engine_java_shapes_batch_matches_golden(seed):
     ids = {pt.id for ps in sets for pt in ps.patterns}
     got = [e["matchedPattern"]["id"] for o in outs for e in json.loads(o)["events"]]
     assert sum(x.startswith("bt") for x in got) > 5 and len(set(got)) > 20 and set(got) <= ids
+    big = "".join(docs)                       # one document through analyze_bytes (prepare / finish)
+    eng2 = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    r, _, _ = eng2.analyze_bytes(big.encode())
+    g = golden.analyze(big, sets, p, golden.FrequencyTracker(p))
+    assert r.ev_line.numel() == len(g["events"])
+    np.testing.assert_allclose(np.sort(r.score.cpu().numpy()), np.sort([e["score"] for e in g["events"]]), rtol=1e-12)
 
 
 @pytest.mark.gpu

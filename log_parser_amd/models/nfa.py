@@ -19,7 +19,8 @@ def _gated_conds(d) -> set:
 
 
 def fits_group(d) -> bool:
-    return d.get("npos", M + 1) <= M and len(_gated_conds(d)) <= 2
+    """A byte-level Glushkov NFA (no code-point-only regex) of <= 64 positions, <= 2 gated conditions."""
+    return 0 < d.get("npos", 0) <= M and "nfa_follow" in d and len(_gated_conds(d)) <= 2
 
 
 def pack_groups(members: Sequence[Tuple[int, dict]]) -> List[List[Tuple[int, dict]]]:

@@ -698,9 +698,11 @@ PYBIND11_MODULE(_lpnative, m) {
     bpg_cand_dev(P<int64_t>(cand), cap, nullptr, P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll),
                  dfa_from(dfa), s); });
   m.def("bpg_dedupe_dev", [](uint64_t keys, int64_t n, int lbits, uint64_t text, uint64_t ls, uint64_t ll,
-                             py::tuple dfa, uint64_t flag, uint64_t s) {
+                             py::tuple dfa, uint64_t flag, uint64_t s, uint64_t wcnt, uint64_t wlist) {
     bpg_dedupe_dev(P<const uint64_t>(keys), n, lbits, P<const uint8_t>(text), P<const int64_t>(ls),
-                   P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(flag), s); });
+                   P<const int32_t>(ll), dfa_from(dfa), P<uint8_t>(flag), s, P<uint32_t>(wcnt), P<uint32_t>(wlist)); },
+        py::arg("keys"), py::arg("n"), py::arg("lbits"), py::arg("text"), py::arg("ls"), py::arg("ll"), py::arg("dfa"),
+        py::arg("flag"), py::arg("stream"), py::arg("wcnt") = 0, py::arg("wlist") = 0);
   // ev_rank / ev_fkey / carry: frequency count before each event = carry[fkey] + rank (fused)
   // dn (optional): device event count, n is then a capacity
   m.def("score_dev", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry, int64_t n,

@@ -40,13 +40,17 @@ __device__ __forceinline__ bool lane_walk(const uint64_t* prog, const uint8_t* s
 
 // bulk path: sorted packed keys ((regex << lbits | line) << 1 | pre-verified); the first key of
 // every run whose regex is a program of <= 8 words and that no engine pre-verified gets its flag
-// here (k_dedupe_verify left it 0; wider programs: k_bpg_coop<G, 1>). Every width in one kernel
-// (registers of the widest walk: fine for a few waves).
+// here (k_dedupe_verify left it 0). Every width in one kernel (registers of the widest walk: fine
+// for a few waves). Keys of wider programs are appended to `wlist` (count in `wcnt`, zeroed by the
+// caller) for k_bpg_coop_list: a regex's keys are contiguous in the sorted array,
+// so walking them where they sit would serialise up to 64 / (64 / G) walks in one wave (a W = 12
+// program's keys cost 1.17 ms per bench step that way).
 __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restrict__ keys, int64_t n, int lbits,
                                                         const uint8_t* __restrict__ text,
                                                         const int64_t* __restrict__ ls,
                                                         const int32_t* __restrict__ ll, DfaPool P,
-                                                        uint8_t* __restrict__ flag) {
+                                                        uint8_t* __restrict__ flag, uint32_t* __restrict__ wcnt,
+                                                        uint32_t* __restrict__ wlist) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t key = keys[i];
@@ -56,9 +60,14 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
   const int r = (int)(k >> lbits);
   if (!is_bpg(P, r)) return;
   const uint64_t* prog = P.bpg + P.meta[4 * r];
-  if ((int)(prog[0] & 0xFF) > BPG_LANE_MAX_W) return;
+  const bool is_wide = (int)(prog[0] & 0xFF) > BPG_LANE_MAX_W;
+  if (is_wide && !wcnt) return;
   for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j)
     if (keys[j] & 1) return;                  // pre-verified: flag already 1
+  if (is_wide) {
+    wlist[atomicAdd(wcnt, 1u)] = (uint32_t)i;
+    return;
+  }
   const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
   flag[i] = lane_walk(prog, text + ls[x], ll[x]) ? 1 : 0;
 }
@@ -296,6 +305,38 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
   }
 }
 
+// the listed keys of wide programs (k_bpg_dedupe_all): one group of G lanes per key, the groups
+// of a fixed grid striding over the list (the walks' collectives need whole waves: a wave leaves
+// the loop together, idle groups walk as invalid)
+template <int G>
+__global__ __launch_bounds__(256) void k_bpg_coop_list(const uint64_t* __restrict__ keys, int lbits,
+                                                       const uint32_t* __restrict__ wcnt,
+                                                       const uint32_t* __restrict__ wlist,
+                                                       const uint8_t* __restrict__ text,
+                                                       const int64_t* __restrict__ ls,
+                                                       const int32_t* __restrict__ ll, DfaPool P,
+                                                       uint8_t* __restrict__ flag) {
+  const uint32_t cnt = *wcnt;
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t gid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int64_t ngroups = (int64_t)gridDim.x * blockDim.x / G;
+  for (int64_t j = gid;; j += ngroups) {
+    const bool valid = j < (int64_t)cnt;
+    if (!__ballot(valid)) break;
+    int64_t i = 0, x = 0;
+    int r = 0;
+    if (valid) {
+      i = wlist[j];
+      const uint64_t k = keys[i] >> 1;
+      r = (int)(k >> lbits);
+      x = (int64_t)(k & ((1ull << lbits) - 1));
+    }
+    const uint64_t* prog = P.bpg + (valid ? P.meta[4 * r] : 0);
+    const bool hit = bpg_coop_walk<G>(prog, text + (valid ? ls[x] : 0), valid ? ll[x] : 0, valid);
+    if (valid && (lane & (G - 1)) == 0) flag[i] = hit ? 1 : 0;
+  }
+}
+
 int coop_group(uint32_t widths) {                // lanes per line: power of two >= 2 x the widest program
   int w = 0;
   for (int b = 31; b >= 0; --b)
@@ -407,17 +448,31 @@ bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* d
 }
 
 void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
-                    const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream) {
+                    const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream, uint32_t* wcnt,
+                    uint32_t* wlist) {
   if (!P.bpg_widths || n <= 0) return;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const bool any_wide = (P.bpg_widths & kWideMask) != 0;
   // programs of <= 8 words: ONE launch for every width, a lane per key (a step's BPG candidates are
   // few -- hundreds to thousands, a handful of waves -- and each walk is a serial chain, so
   // per-width launches added up their slowest walks where one launch runs them side by side)
-  if (P.bpg_widths & 0x1FFu) {
-    hipLaunchKernelGGL(k_bpg_dedupe_all, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag);
+  const bool listed = any_wide && wcnt && wlist;
+  if ((P.bpg_widths & 0x1FFu) || listed) {
+    hipLaunchKernelGGL(k_bpg_dedupe_all, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag,
+                       listed ? wcnt : nullptr, listed ? wlist : nullptr);
     check_launch("k_bpg_dedupe_all");
   }
-  if (P.bpg_widths & kWideMask) {               // wider programs: a lane group per key
+  if (!any_wide) return;
+  if (listed) {                                 // wider programs: a lane group per listed key
+    const int G = coop_group(P.bpg_widths);
+    const dim3 grid(256), block(256);
+    switch (G) {
+      case 16: hipLaunchKernelGGL(k_bpg_coop_list<16>, grid, block, 0, st, keys, lbits, wcnt, wlist, text, ls, ll, P, flag); break;
+      case 32: hipLaunchKernelGGL(k_bpg_coop_list<32>, grid, block, 0, st, keys, lbits, wcnt, wlist, text, ls, ll, P, flag); break;
+      default: hipLaunchKernelGGL(k_bpg_coop_list<64>, grid, block, 0, st, keys, lbits, wcnt, wlist, text, ls, ll, P, flag); break;
+    }
+    check_launch("k_bpg_coop_list");
+  } else {                                      // no list memory: a lane group per key in place
     launch_coop<1>(nullptr, keys, n, nullptr, lbits, text, ls, ll, P, flag, st, BPG_LANE_MAX_W + 1);
     check_launch("k_bpg_coop<dedupe>");
   }

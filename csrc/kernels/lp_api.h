@@ -33,8 +33,11 @@ void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, 
 // verified in place by ONE launch; false (nothing launched) when the library has no BPG programs
 bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text,
                          const int64_t* ls, const int32_t* ll, const DfaPool& P, uint64_t stream);
+// wcnt / wlist (optional): a counter zeroed in stream order before the call and n uint32 of scratch --
+// keys of programs wider than 8 words are listed there and walked one lane group per key
 void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
-                    const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream);
+                    const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream, uint32_t* wcnt = nullptr,
+                    uint32_t* wlist = nullptr);
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,
                   int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
                   uint64_t stream);

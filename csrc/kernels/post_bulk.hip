@@ -695,6 +695,7 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
   // [regex counts | sub-bucket counts]: one memset
   uint32_t* cnt = C.take<uint32_t>(R);
   uint32_t* sub_cnt = C.take<uint32_t>(bcap);
+  uint32_t* wide_cnt = C.take<uint32_t>(1);        // BPG wide-program list: count (zeroed), entries in tmp
   const size_t zero_end = C.used;
   uint8_t* shift = C.take<uint8_t>(R);
   uint32_t* base = C.take<uint32_t>(R + 1);
@@ -739,7 +740,7 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
   // BPG programs: one lane per first-of-run key over the sorted keys (a regex's keys are contiguous,
   // so its waves are dense). A workgroup per sub-bucket (lanes looping over its candidates) measured
   // 138 us against this kernel's 118 us: the walks are latency-bound, lanes should not loop.
-  bpg_dedupe_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, flag, stream);
+  bpg_dedupe_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, flag, stream, wide_cnt, tmp);   // tmp: free after k_hb_sort
   hipLaunchKernelGGL(k_hb_kept, dim3((unsigned)bcap), dim3(PB_T), 0, st, sub_off, sub_reg, base, R, flag, stdk, A.ev,
                      kept, evs);
   PB_CHECK(hipGetLastError());

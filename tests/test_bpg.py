@@ -241,16 +241,22 @@ def test_bpg_candidate_walks_match_host(gpu_device, li):
             keys.append(k | 1)
     keys.sort()
     kt = torch.tensor(keys, dtype=torch.int64, device=gpu_device)
-    flag = torch.full((len(keys),), 7, dtype=torch.uint8, device=gpu_device)
-    N.bpg_dedupe_dev(kt.data_ptr(), kt.numel(), lbits, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
-                     flag.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    fl = flag.cpu().tolist()
-    for i, k in enumerate(keys):
-        kk = k >> 1
-        r, j = kk >> lbits, kk & ((1 << lbits) - 1)
-        run = [x for x in keys if x >> 1 == kk]
-        first = i == 0 or keys[i - 1] >> 1 != kk
-        if first and r in bpg and not any(x & 1 for x in run):
-            assert fl[i] == (1 if (r, j) in want else 0), (r, j)
-        else:
-            assert fl[i] == 7
+    for listed in (False, True):    # wide programs walked in place / from the listed keys (bulk path)
+        flag = torch.full((len(keys),), 7, dtype=torch.uint8, device=gpu_device)
+        wcnt = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+        wlist = torch.zeros(len(keys), dtype=torch.int32, device=gpu_device)
+        N.bpg_dedupe_dev(kt.data_ptr(), kt.numel(), lbits, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                         flag.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                         wcnt.data_ptr() if listed else 0, wlist.data_ptr() if listed else 0)
+        fl = flag.cpu().tolist()
+        pre = {}
+        for x in keys:                       # run (same regex + line) -> holds a pre-verified copy
+            pre[x >> 1] = pre.get(x >> 1, False) or bool(x & 1)
+        for i, k in enumerate(keys):
+            kk = k >> 1
+            r, j = kk >> lbits, kk & ((1 << lbits) - 1)
+            first = i == 0 or keys[i - 1] >> 1 != kk
+            if first and r in bpg and not pre[kk]:
+                assert fl[i] == (1 if (r, j) in want else 0), (r, j, listed)
+            else:
+                assert fl[i] == 7

@@ -300,6 +300,8 @@ def mode_concurrent_http(args):
     extra = [f"-Dengine.serve-devices={','.join([dev] * args.engines)}"] if args.engines > 1 else []
     if args.processes > 1:          # serving processes sharing one window (serve/procs.py)
         extra = [f"-Dserver.processes={args.processes}"]
+    if args.timeline:
+        extra.append("-Dserver.stage-timeline=true")
     srv = ServerProcess(write_library(sets), dev, http="native", extra=extra + list(args.server_opt or []),
                         log_path=args.server_log)
     try:
@@ -321,7 +323,16 @@ def mode_concurrent_http(args):
         workers = max(args.processes, 1)
         st0 = collect_stages(srv.port, workers)
         lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0)
-        breakdown = stage_breakdown(st0, collect_stages(srv.port, workers), wall)
+        st1 = collect_stages(srv.port, workers)
+        breakdown = stage_breakdown(st0, st1, wall)
+        if args.timeline:           # per process: stage intervals of the timed burst, ms from its start
+            for pid, d in st1.items():
+                t_end = d["now"]
+                ev = [e for e in d.get("timeline", []) if e[3] >= t_end - wall - 0.05]
+                t0 = min((e[2] for e in ev), default=t_end)
+                for stg, nreq, a, z in ev:
+                    print(f"pid {pid} {stg:9s} n={nreq:5d} {1e3 * (a - t0):8.2f} -> {1e3 * (z - t0):8.2f} ms",
+                          file=sys.stderr)
     finally:
         srv.stop()
     ok = lat >= 0

@@ -30,7 +30,9 @@ log = logging.getLogger("log_parser_amd.server")
 class NativeHttpFrontend:
     def __init__(self, service: Service, host: str = "0.0.0.0", port: int = 8080, io_threads: int = 2):
         self.svc = service
-        self.svc.batcher()                               # compile the library before accepting
+        b = self.svc.batcher()                           # compile the library before accepting
+        if b.pipe is not None and bool(service.config.get("server.stage-timeline", False)):
+            b.pipe.timeline = []
         cfg = service.config
         trace = bool(cfg.get("server.trace-requests", False))
         self.srv = N.HttpServer(host, port, io_threads, int(cfg["server.max-body-bytes"]),
@@ -110,6 +112,8 @@ class NativeHttpFrontend:
                     self._reply(rid, (500, "application/json", ('{"error":"%s"}' % type(e).__name__).encode()))
             if batch:
                 self._pump_s["dispatch"] += time.perf_counter() - td
+                if b.pipe is not None and b.pipe.timeline is not None:
+                    b.pipe.timeline.append(("drain", len(batch), td, time.perf_counter()))
                 self._run_direct(b, batch)
 
     def _run_direct(self, b, batch) -> None:
@@ -166,6 +170,9 @@ class NativeHttpFrontend:
             out["pipeline"] = dict(pipe.stage_s)
             out["batches"] = pipe.batches
             out["requests"] = pipe.requests
+            if pipe.timeline is not None:
+                out["timeline"] = list(pipe.timeline)
+        out["now"] = time.perf_counter()
         return out
 
     def close(self) -> None:

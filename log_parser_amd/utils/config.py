@@ -123,6 +123,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.rcvbuf-bytes": (0, int),
     # per-request receive / validate / queue / engine microseconds on stderr (tools/parse_tail.py)
     "server.trace-requests": (False, bool),
+    # record the serving pipeline's per-batch stage intervals (pack / device / emit / complete),
+    # returned by GET /admin/stages (benchmarks/bench_configs.py concurrent_http --timeline)
+    "server.stage-timeline": (False, bool),
     # freeze the startup heap + raise GC thresholds in the batching server (submit-path latency)
     "server.gc-tuning": (True, bool),
     # Python GIL switch interval in the serving process (ms; 0 = interpreter default 5 ms). The

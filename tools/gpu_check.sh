@@ -3,7 +3,8 @@
 #   scan    scan-group A/B (16 vs 32 members per multi-regex DFA)
 #   nfa     MFMA vs BPG A/B per regex shape (tools/nfa_ab.py)
 #   bench   bench.py (headline, 1 GPU)
-#   http    config 5 over HTTP: 1 and 2 serving processes, and the front end alone
+#   http    config 5 over HTTP: 1 and 2 serving processes (stage timelines), and the front end alone
+#   stream  config 4: 1B-line stream, auto (HBM-sized) chunks and 256 MiB chunks (same digest)
 # Run: gpurun -- bash tools/gpu_check.sh [step ...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -33,10 +34,14 @@ for s in $steps; do
     bench)
       run bench 600 python -u bench.py --steps 10 --warmup 3 ;;
     http)
-      run http1 300 python -u benchmarks/bench_configs.py concurrent_http --server-log gpurun_out/gc_http1_srv.log
-      run http2 300 python -u benchmarks/bench_configs.py concurrent_http --processes 2 \
+      run http1 300 python -u benchmarks/bench_configs.py concurrent_http --timeline \
+        --server-log gpurun_out/gc_http1_srv.log
+      run http2 300 python -u benchmarks/bench_configs.py concurrent_http --processes 2 --timeline \
         --server-log gpurun_out/gc_http2_srv.log
       run ceiling 300 python -u tools/http_ceiling.py --requests 10000 --io 2,8 ;;
+    stream)
+      run stream_auto 600 python -u benchmarks/bench_configs.py stream
+      run stream_256 600 python -u benchmarks/bench_configs.py stream --chunk-mb 256 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

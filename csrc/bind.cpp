@@ -929,6 +929,16 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("dlpack", [](uint64_t ptr, int64_t numel, const std::string& dtype, int device) {
     return dlpack_capsule(ptr, numel, dtype, device);
   }, py::arg("ptr"), py::arg("numel"), py::arg("dtype"), py::arg("device"));
+  // page-lock existing host memory for DMA (a stream source already in RAM: its chunks are copied
+  // to the GPU straight from it, no staging copy); false when the runtime refuses
+  m.def("host_register", [](uint64_t ptr, int64_t n) {
+    if (hipHostRegister(reinterpret_cast<void*>(ptr), (size_t)n, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    return true;
+  });
+  m.def("host_unregister", [](uint64_t ptr) { return hipHostUnregister(reinterpret_cast<void*>(ptr)) == hipSuccess; });
   // peer access for kernels on `device` reading / writing memory of `peer` (a shared window)
   m.def("enable_peer_access", [](int device, int peer) {
     if (device == peer) return true;

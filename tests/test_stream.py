@@ -263,3 +263,30 @@ def test_stream_with_backtracker_regexes_equals_single_pass():
     np.testing.assert_array_equal(pat, ref.ev_pat.numpy())
     np.testing.assert_allclose(score, ref.score.numpy(), rtol=1e-15, atol=0)
     assert (pat == lib.patterns.index(next(p for p in lib.patterns if p.id == "bt0"))).sum() >= 40
+
+
+def test_repeat_buffer_segments():
+    rb = RepeatBuffer(b"0123456789", 95)
+    segs = rb.segments(7, 33)
+    assert sum(t for _, _, t in segs) == 26
+    assert b"".join(rb.block[b:b + t] for b, _, t in segs) == rb[7:33]
+    assert [o for _, o, _ in segs] == [0, 3, 13, 23]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [1 << 16, 1 << 20])
+def test_stream_direct_from_registered_source_equals_staged(gpu_device, chunk):
+    """A RepeatBuffer's block is page-locked once and every chunk is copied to the GPU straight
+    from it (no staging copy): same events, scores and summary as the staged bytes of that stream."""
+    sets, trig = make_library(40, seed=41, sequence_rate=0.8)
+    lib = CompiledLibrary(sets, ScoringParams())
+    block = (make_log(1500, trig, seed=45, hit_rate=0.08) + "\n").encode()
+    rb = RepeatBuffer(block, 7 * len(block) + 1234)
+    assert rb.pinned_block() is not None
+    a = StreamAnalyzer(_eng(lib, str(gpu_device)), chunk_bytes=chunk, topk=9).run(rb)
+    b = StreamAnalyzer(_eng(lib, str(gpu_device)), chunk_bytes=chunk, topk=9).run(rb[0:len(rb)])
+    assert a.total_lines == b.total_lines and a.chunks == b.chunks > 1
+    for x, y in zip(a.events, b.events):
+        np.testing.assert_array_equal(x, y)
+    assert a.summary == b.summary
+    np.testing.assert_array_equal(a.topk_score, b.topk_score)

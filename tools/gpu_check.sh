@@ -24,7 +24,7 @@ for s in $steps; do
   case $s in
     tests)
       run tests 900 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py \
-        tests/test_nfa.py tests/test_regex.py tests/test_serve_procs.py -m gpu -x -v --durations=15 --timeout 300 \
+        tests/test_nfa.py tests/test_regex.py tests/test_serve_procs.py tests/test_stream.py -m gpu -x -v --durations=15 --timeout 300 \
         --timeout-method thread ;;
     scan)
       run scan16 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 16
@@ -41,6 +41,7 @@ for s in $steps; do
       run ceiling 300 python -u tools/http_ceiling.py --requests 10000 --io 2,8 ;;
     stream)
       run stream_auto 600 python -u benchmarks/bench_configs.py stream
+      run stream_8g 600 python -u benchmarks/bench_configs.py stream --chunk-mb 8192
       run stream_256 600 python -u benchmarks/bench_configs.py stream --chunk-mb 256 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -274,7 +274,7 @@ def test_repeat_buffer_segments():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("chunk", [1 << 16, 1 << 20])
+@pytest.mark.parametrize("chunk", [1 << 16, 1 << 18])
 def test_stream_direct_from_registered_source_equals_staged(gpu_device, chunk):
     """A RepeatBuffer's block is page-locked once and every chunk is copied to the GPU straight
     from it (no staging copy): same events, scores and summary as the staged bytes of that stream."""

@@ -181,8 +181,10 @@ def mode_stream(args):
     # warm-up sizes the pinned pool for it
     chunk = (args.chunk_mb << 20) or auto_chunk_bytes(dev, total)
     sa = StreamAnalyzer(eng, chunk_bytes=chunk, topk=100, keep_events=False)
-    # untimed warm-up stream (3 chunks): pinned pool, kernels, allocator; then a fresh frequency state
-    sa.run(RepeatBuffer(block, min(total, 3 * sa.chunk_bytes)))
+    # untimed warm-up stream: pinned pool, kernels, and the allocator's full-chunk-size buffers (4
+    # chunks of stream: the ramps reach the full chunk size; a first 8 GiB chunk in the timed run
+    # otherwise stalled the copy engine 0.2 s on allocations, profiles/r4_b); then a fresh frequency state
+    sa.run(RepeatBuffer(block, min(total, 4 * sa.chunk_bytes)))
     eng.freq.reset_all()
     _sync(dev)
     t0 = time.perf_counter()

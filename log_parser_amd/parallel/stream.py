@@ -264,12 +264,15 @@ class StreamAnalyzer:
         while pos < eff or (pos == 0 and eff == 0):
             # ramp-up: chunks double from RAMP_MIN, so the staging -> H2D -> compute pipeline fills
             # in milliseconds instead of one full-size host copy; ramp-down: near the end a chunk is
-            # at most half of what remains (down to RAMP_MIN), so the drain -- the last chunk's
-            # analysis after the last copy -- is a small chunk's, not an 8 GiB one's
+            # at most RAMP_DOWN of what remains (down to RAMP_MIN), so the drain -- the last chunk's
+            # analysis after the last copy -- is a small chunk's, not an 8 GiB one's. Successive
+            # ramp-down chunks shrink by 1 - RAMP_DOWN: each chunk's copy must outlast the previous
+            # (larger) chunk's analysis, or the copy engine idles (at 1/2 per chunk it did: ~80 ms
+            # over a 1B-line stream's tail, profiles/r4_b)
             size = min(self.chunk_bytes, self.RAMP_MIN << min(k, 40))
             rest = eff - pos
             if rest > self.RAMP_MIN:
-                size = min(size, max(self.RAMP_MIN, rest // 2))
+                size = min(size, max(self.RAMP_MIN, int(rest * self.RAMP_DOWN)))
             k += 1
             end = min(eff, pos + size)
             if end < eff:
@@ -324,6 +327,7 @@ class StreamAnalyzer:
         keep = ub >= thr
         return [gl[keep]], [pat[keep]], [fac[keep]]
     RAMP_MIN = 64 << 20         # first / last chunk size of the ramps (bytes)
+    RAMP_DOWN = 0.3             # ramp-down: a chunk takes at most this share of what remains
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None,
                   plan=None, direct: bool = False):

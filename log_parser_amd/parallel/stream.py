@@ -20,6 +20,7 @@ chunk k; the H2D copy runs on its own HIP stream.
 from __future__ import annotations
 
 import queue
+from collections import deque
 import threading
 import time
 import warnings
@@ -328,6 +329,7 @@ class StreamAnalyzer:
         return [gl[keep]], [pat[keep]], [fac[keep]]
     RAMP_MIN = 64 << 20         # first / last chunk size of the ramps (bytes)
     RAMP_DOWN = 0.3             # ramp-down: a chunk takes at most this share of what remains
+    PREFETCH = 2                # chunks staged + copied ahead of the one being analysed
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None,
                   plan=None, direct: bool = False):
@@ -500,13 +502,28 @@ class StreamAnalyzer:
                 return d, n, lh, rh, ev, end, pinned
             return pinned, n, lh, rh, None, end, pinned
 
-        nxt = fetch()
-        while nxt is not None:
-            text, n, lh, rh, ev, chunk_end, host = nxt
+        # copies run PREFETCH chunks ahead of the analysis: with one chunk ahead, a copy shorter than
+        # the previous chunk's analysis (the ramp-down) left the copy engine idle until the next
+        # iteration issued the following one
+        ahead: "deque" = deque()
+        ended = False
+
+        def refill():
+            nonlocal ended
+            while not ended and len(ahead) < self.PREFETCH:
+                it = fetch()
+                if it is None:
+                    ended = True
+                else:
+                    ahead.append(it)
+
+        refill()
+        while ahead:
+            text, n, lh, rh, ev, chunk_end, host = ahead.popleft()
             if ev is not None:
                 torch.cuda.current_stream(dev).wait_event(ev)
                 text.record_stream(torch.cuda.current_stream(dev))
-            nxt = fetch()                      # stage + copy the next chunk meanwhile
+            refill()                           # stage + copy the next chunks meanwhile
             ls, ll = K.split_chunk_lines(text, n)
             L = ls.numel()
             own_lo, own_hi = lh, L - rh

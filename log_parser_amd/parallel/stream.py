@@ -332,22 +332,42 @@ class StreamAnalyzer:
     PREFETCH = 2                # chunks staged + copied ahead of the one being analysed
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None,
-                  plan=None, direct: bool = False):
+                  plan=None, direct=None):
         """Stages line-aligned chunks (+ halos) into pinned buffers. On GPU the buffers come from a
         small recycled pool (``free_q``: buffer + the event of the H2D copy that last read it) --
         allocating and pinning a fresh 0.5 GB buffer per chunk costs 30-100 ms, 3x the copy.
         ``plan``: an explicit list of chunks (``_plan`` entries; None = an empty chunk).
-        ``direct``: a source already in page-locked memory (a registered ``RepeatBuffer`` block)
-        is not staged at all -- the item carries the chunk's segments of it (7th field) and the
-        consumer copies them to the device itself: the host then only issues copies, and the
-        stream runs at the PCIe rate instead of the host copy's (a 3.3 GB staged chunk ran at
-        43 GB/s, profiles/r4_a)."""
+        ``direct`` = (device, copy stream, device-buffer pool): a source already in page-locked
+        memory (a registered ``RepeatBuffer`` block) is not staged at all -- this thread copies each
+        chunk's segments of it straight into a recycled device buffer on the copy stream and hands
+        over the device chunk (item tag "dev"). The host only issues copies, the copy engine never
+        waits for the analysis thread's syncs, and the stream runs at the PCIe rate (a 3.3 GB
+        staged chunk ran at 43 GB/s, profiles/r4_a; copies issued by the analysis thread left
+        ~85 ms of gaps in a 1B-line stream's ramp-down, profiles/r4_b)."""
         try:
-            if direct and isinstance(src, RepeatBuffer) and src.pinned_block() is not None:
+            if direct is not None and isinstance(src, RepeatBuffer) and src.pinned_block() is not None:
+                dev, cs, dev_free = direct
+                torch.cuda.set_device(dev)
+                blk = src.pinned_block()
+                cap = K.padded_len(self.chunk_bytes + (self.chunk_bytes >> 4))
                 for ent in (plan if plan is not None else self._plan(src, eff, start)):
                     l_start, pos, end, r_end, lh, rh = ent
                     n = r_end - l_start
-                    q.put((None, n, K.padded_len(n), lh, rh, end, src.segments(l_start, r_end)))
+                    size = K.padded_len(n)
+                    buf, used = dev_free.get()
+                    if used is not None:
+                        used.synchronize()              # the analysis that read it has run
+                    with torch.cuda.stream(cs):
+                        if buf is None or buf.numel() < size:
+                            buf = None
+                            buf = torch.empty(max(size, cap), dtype=torch.uint8, device=dev)
+                        d = buf[:size]
+                        for b, o, take in src.segments(l_start, r_end):
+                            d[o:o + take].copy_(blk[b:b + take], non_blocking=True)
+                        d[n:size].zero_()
+                        ev = torch.cuda.Event()
+                        ev.record(cs)
+                    q.put(("dev", buf, d, n, lh, rh, end, ev))
                 q.put(None)
                 return
             flat = None
@@ -439,20 +459,28 @@ class StreamAnalyzer:
             nbytes_total = 0
         q: "queue.Queue" = queue.Queue(maxsize=2)
         free_q: Optional[queue.Queue] = None
+        dev_free: Optional[queue.Queue] = None
         if dev.type == "cuda" and not resident:
             free_q = queue.Queue()
             for _ in range(self.PINNED_BUFFERS):
                 free_q.put((None, None))
+            dev_free = queue.Queue()
+            for _ in range(self.PREFETCH + 1):
+                dev_free.put((None, None))
+        copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" and not resident else None
+        # the backtracker side path reads the chunk's pinned host bytes: their buffer is recycled
+        # only after this chunk's prepare (and such chunks are staged, not copied directly)
+        hold = bool(lib.host_plan)
         th = None
         if resident:
             if resume:
                 raise ValueError("resume applies to host streams, not resident logs")
             res_iter = iter(src.chunks)
         else:
+            direct = (dev, copy_stream, dev_free) if dev.type == "cuda" and not hold else None
             th = threading.Thread(target=self._producer, args=(src, eff, q, start, free_q),
-                                  kwargs={"direct": dev.type == "cuda" and not lib.host_plan}, daemon=True)
+                                  kwargs={"direct": direct}, daemon=True)
             th.start()
-        copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" and not resident else None
 
         def save(pos_next):
             def cat(xs, dt, shape):
@@ -466,10 +494,6 @@ class StreamAnalyzer:
             import os
             os.replace(tmp, checkpoint)
 
-        # the backtracker side path reads the chunk's pinned host bytes: their buffer is recycled
-        # only after this chunk's prepare
-        hold = bool(lib.host_plan)
-
         def fetch():
             if resident:                        # already in HBM: nothing to stage or copy
                 c = next(res_iter, None)
@@ -479,17 +503,9 @@ class StreamAnalyzer:
                 raise item
             if item is None:
                 return None
-            if len(item) == 7:                  # direct: segments of the registered source
-                _, n, size, lh, rh, end, segs = item
-                blk = src.pinned_block()
-                with torch.cuda.stream(copy_stream):
-                    d = torch.empty(size, dtype=torch.uint8, device=dev)
-                    for b, o, take in segs:
-                        d[o:o + take].copy_(blk[b:b + take], non_blocking=True)
-                    d[n:size].zero_()
-                    ev = torch.cuda.Event()
-                    ev.record(copy_stream)
-                return d, n, lh, rh, ev, end, None
+            if item[0] == "dev":                # copied by the producer into a pooled device buffer
+                _, buf, d, n, lh, rh, end, ev = item
+                return d, n, lh, rh, ev, end, buf
             pinned, n, size, lh, rh, end = item
             if copy_stream is not None:
                 with torch.cuda.stream(copy_stream):
@@ -520,6 +536,9 @@ class StreamAnalyzer:
         refill()
         while ahead:
             text, n, lh, rh, ev, chunk_end, host = ahead.popleft()
+            dev_buf = None
+            if host is not None and host.is_cuda:       # a pooled device buffer (direct copies)
+                dev_buf, host = host, None
             if ev is not None:
                 torch.cuda.current_stream(dev).wait_event(ev)
                 text.record_stream(torch.cuda.current_stream(dev))
@@ -534,6 +553,10 @@ class StreamAnalyzer:
                 free_q.put((host, ev))
             chain = eng.seq_chain_table(prep, own_lo, own_hi)
             res = eng.finish(prep, segs, freq_carry + run_counts, seq_state, with_factors=True)
+            if dev_buf is not None:            # every kernel reading the chunk is queued: recycle
+                used = torch.cuda.Event()
+                used.record(torch.cuda.current_stream(dev))
+                dev_free.put((dev_buf, used))
             if lib.n_seq_events:
                 k = chain.to(torch.int64)
                 prev = seq_state[(self.slot_e0 + k.clamp(min=0))]

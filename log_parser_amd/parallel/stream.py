@@ -272,8 +272,8 @@ class StreamAnalyzer:
             # over a 1B-line stream's tail, profiles/r4_b)
             size = min(self.chunk_bytes, self.RAMP_MIN << min(k, 40))
             rest = eff - pos
-            if rest > self.RAMP_MIN:
-                size = min(size, max(self.RAMP_MIN, int(rest * self.RAMP_DOWN)))
+            if rest > self.RAMP_END:
+                size = min(size, max(self.RAMP_END, int(rest * self.RAMP_DOWN)))
             k += 1
             end = min(eff, pos + size)
             if end < eff:
@@ -328,8 +328,11 @@ class StreamAnalyzer:
         keep = ub >= thr
         return [gl[keep]], [pat[keep]], [fac[keep]]
     RAMP_MIN = 64 << 20         # first / last chunk size of the ramps (bytes)
-    RAMP_DOWN = 0.3             # ramp-down: a chunk takes at most this share of what remains
-    PREFETCH = 2                # chunks staged + copied ahead of the one being analysed
+    RAMP_DOWN = 0.3             # ramp-down: a chunk takes at most this share of what remains ...
+    # ... down to this size: a chunk's analysis has ~5 ms of fixed latency (line count read-back,
+    # launches), so smaller tail chunks made the analysis, not the copy, the bottleneck
+    RAMP_END = 384 << 20
+    PREFETCH = 3                # chunks staged + copied ahead of the one being analysed
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None,
                   plan=None, direct=None):

@@ -328,10 +328,13 @@ class StreamAnalyzer:
         keep = ub >= thr
         return [gl[keep]], [pat[keep]], [fac[keep]]
     RAMP_MIN = 64 << 20         # first / last chunk size of the ramps (bytes)
-    RAMP_DOWN = 0.3             # ramp-down: a chunk takes at most this share of what remains ...
-    # ... down to this size: a chunk's analysis has ~5 ms of fixed latency (line count read-back,
-    # launches), so smaller tail chunks made the analysis, not the copy, the bottleneck
-    RAMP_END = 384 << 20
+    # ramp-down: a chunk takes at most RAMP_DOWN of what remains, down to RAMP_END. A tail chunk
+    # only shortens the drain while its copy outlasts the previous chunk's analysis: s' / copy_rate >=
+    # s / analysis_rate + ~5 ms fixed (line count read-back, launches). With a 4k-pattern library
+    # (analysis ~68 GB/s vs 57 GB/s PCIe) that allows ~16% shrink per chunk and nothing below ~2 GB
+    # (profiles/r4_b: 1/2 per chunk down to 64 MB left 80 ms of copy-engine gaps)
+    RAMP_DOWN = 0.16
+    RAMP_END = 1 << 30
     PREFETCH = 3                # chunks staged + copied ahead of the one being analysed
 
     def _producer(self, src, eff, q: "queue.Queue", start: int = 0, free_q: Optional["queue.Queue"] = None,

@@ -284,7 +284,25 @@ class Stage:
 
 class StagePool:
     """Recycled ``Stage`` buffers, one per batch in flight. ``take`` blocks when ``limit`` stages
-    are out: the back-pressure of the serving pipeline."""
+    are out: the back-pressure of the serving pipeline. ``prewarm`` sizes every stage for a batch
+    of ``nbytes`` up front (a server, before it accepts: no pinned allocation on a request's path)."""
+
+    def prewarm(self, nbytes: int, nlines: int) -> None:
+        with self._cv:
+            free = list(self._free)
+            self._free.clear()
+        stages = []
+        for st in free:
+            if st.buf is not None and st.buf.numel() < nbytes:
+                st.grow_buf(nbytes)
+            if st.idx is not None and st.cap < nlines:
+                st.grow_idx(nlines)
+            stages.append(st)
+        while len(stages) < self.limit:
+            stages.append(Stage(self.pinned, nbytes, nlines))
+        with self._cv:
+            self._free.extend(stages)
+            self._cv.notify_all()
 
     def __init__(self, pinned: bool, initial: int, limit: int = 3):
         self.pinned, self.initial, self.limit = pinned, initial, limit
@@ -995,7 +1013,9 @@ class Engine:
         if r is None:
             return None
         if isinstance(r, int):
-            size = K.padded_len(max(int(r), 1 << 20) * 5 // 4)
+            # geometric: a burst's batches grow from a few requests to thousands, and every
+            # re-pinning of a 100+ MB stage costs tens of ms on the serving path (profiles/r4_b)
+            size = K.padded_len(max(int(r) * 5 // 4, 2 * st.buf.numel(), 1 << 20))
             st.grow_buf(size)
             r = N.pack_split_docs(docs, st.buf.data_ptr(), size - K.TEXT_PAD - K.NL_TILE, self._STAGE_THREADS,
                                   st.idx.data_ptr(), st.cap)
@@ -1006,7 +1026,7 @@ class Engine:
         else:
             ls_h = a
             job.n_lines = -1
-            st.grow_idx(max(ls_h.size * 5 // 4, st.cap))      # fits next time
+            st.grow_idx(max(ls_h.size * 5 // 4, 2 * st.cap))  # fits next time
         n = int(doc_off[-1])
         return st.buf.numpy(), ls_h, ll_h, dl, n
 

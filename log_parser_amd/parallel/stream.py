@@ -43,14 +43,15 @@ def auto_chunk_bytes(device: torch.device, total: Optional[int] = None) -> int:
     arenas, CSR, with the next chunk's copy in flight). On a 288 GB MI355X that is 8 GiB chunks:
     fewer halos, launches and host hand-offs than the 256 MiB of round 2 -- what a resident log
     (analysed from HBM, no copy to hide) wants. A host stream (``total`` = its length) also caps
-    the chunk at 1/32 of the stream: the first chunk's copy and the last chunk's analysis are not
-    overlapped, and on 100 GB 8 GiB chunks ran 8% slower than 256 MiB ones (profiles/r3_d)."""
+    the chunk at 1/8 of the stream, so it still has a steady state between the ramps
+    (``StreamAnalyzer._plan``: the ramps overlap the first copy and the last analysis; 1B lines
+    with 8 GiB chunks ran at 526M lines/s, 256 MiB chunks at 485M, profiles/r4_b)."""
     if device.type != "cuda":
         return CHUNK_MIN
     free, _ = torch.cuda.mem_get_info(device)
     c = max(CHUNK_MIN, min(CHUNK_MAX, free // 16))
     if total is not None:
-        c = max(CHUNK_MIN, min(c, total // 32))
+        c = max(CHUNK_MIN, min(c, total // 8))
     return int(c) & ~((1 << 20) - 1)
 
 

@@ -37,6 +37,7 @@ from ..frequency import MirroredFrequencyState
 from ..models.compiled import CompiledLibrary
 from ..models.library import load_pattern_directory
 from ..native import N
+from ..ops.kernels import padded_len as K_padded
 from .pipeline import BatchPipeline
 from ..utils.config import Config
 from ..utils.metrics import Metrics
@@ -99,6 +100,10 @@ class Batcher:
         # one engine: pack / device / emit of consecutive batches overlap (serve/pipeline.py)
         self.pipe: Optional[BatchPipeline] = (BatchPipeline(self.engine, self.device_stage, metrics.observe_batch)
                                               if len(self.engines) == 1 else None)
+        pre = int(self.engine.config.get("engine.batch.prewarm-bytes", 0) or 0)
+        for e in self.engines:      # pinned stages sized before the first request, not inside a burst
+            if pre > 0 and e.device.type == "cuda":
+                e._stage_pool.prewarm(K_padded(min(pre, max_bytes)), max(1, min(pre, max_bytes) // 40))
         self._threads = [threading.Thread(target=self._loop, args=(e,), name=f"lp-batcher-{i}", daemon=True)
                          for i, e in enumerate(self.engines)]
         for t in self._threads:

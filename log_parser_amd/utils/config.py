@@ -84,6 +84,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # continuous batching
     "engine.batch.max-requests": (2048, int),
     "engine.batch.max-bytes": (256 << 20, int),
+    # serving: size the pinned batch stages for this many bytes at start-up (capped by max-bytes;
+    # 0 = grow on demand): a burst's first large batches then pay no pinned allocation
+    "engine.batch.prewarm-bytes": (128 << 20, int),
     # extra wait for more requests after the first one; 0 = greedy continuous batching (a batch
     # forms from whatever queued while the previous one ran; an idle server answers at once)
     "engine.batch.max-wait-ms": (0.0, float),

@@ -114,12 +114,13 @@ def test_auto_chunk_bytes_cpu():
 
 
 def test_auto_chunk_bytes_policy(monkeypatch):
-    """HBM cap 1/16 of free memory in [256 MiB, 8 GiB]; a host stream also caps at 1/32 of its length."""
+    """HBM cap 1/16 of free memory in [256 MiB, 8 GiB]; a host stream also caps at 1/8 of its length."""
     from log_parser_amd.parallel import stream as S
     monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d: (280 << 30, 288 << 30))
     dev = torch.device("cuda", 0)
     assert S.auto_chunk_bytes(dev) == S.CHUNK_MAX
-    assert S.auto_chunk_bytes(dev, 100 << 30) == (100 << 30) // 32
+    assert S.auto_chunk_bytes(dev, 100 << 30) == S.CHUNK_MAX
+    assert S.auto_chunk_bytes(dev, 20 << 30) == (20 << 30) // 8
     assert S.auto_chunk_bytes(dev, 1 << 30) == S.CHUNK_MIN
     assert S.auto_chunk_bytes(dev, 1 << 40) == S.CHUNK_MAX
     monkeypatch.setattr(torch.cuda, "mem_get_info", lambda d: (1 << 30, 288 << 30))

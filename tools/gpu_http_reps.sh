@@ -1,0 +1,12 @@
+# Config 5 over HTTP, repeated: 1 and 2 serving processes alternately, 3 times each (run-to-run
+# variance on a shared host is large). Logs: gpurun_out/gh_*.log
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+for i in 1 2 3; do
+  for p in 1 2; do
+    timeout -k 10 300 python -u benchmarks/bench_configs.py concurrent_http --processes $p \
+      > gpurun_out/gh_p${p}_$i.log 2>&1
+    rc=$?; echo "p$p rep$i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+done

@@ -36,17 +36,18 @@ from ..utils.config import Config
 
 log = logging.getLogger("log_parser_amd.server")
 
-ENV_SHM, ENV_WORKER, ENV_NPROC = "LP_SERVE_SHM", "LP_SERVE_WORKER", "LP_SERVE_NPROC"
+ENV_SHM, ENV_WORKER, ENV_NPROC, ENV_WINDOW = "LP_SERVE_SHM", "LP_SERVE_WORKER", "LP_SERVE_NPROC", "LP_SERVE_WINDOW"
 
 
 class WorkerContext:
     """This process's place in a serving group (built from the supervisor's environment)."""
 
-    def __init__(self, shared, index: int, nproc: int):
+    def __init__(self, shared, index: int, nproc: int, window: str = "device"):
         self.shared = shared
         self.index = index
         self.nproc = nproc
         self.owner = index == 0
+        self.window = window            # "device" or "host" (decided by the supervisor for all)
 
     @staticmethod
     def from_env() -> Optional["WorkerContext"]:
@@ -54,7 +55,8 @@ class WorkerContext:
         if not name:
             return None
         from ..native import N
-        return WorkerContext(N.ProcShared(name, False), int(os.environ[ENV_WORKER]), int(os.environ[ENV_NPROC]))
+        return WorkerContext(N.ProcShared(name, False), int(os.environ[ENV_WORKER]), int(os.environ[ENV_NPROC]),
+                             os.environ.get(ENV_WINDOW, "device"))
 
     def frequency_state(self, lib, cfg: Config):
         """The shared window: created by worker 0 (on its device), mapped by the others once
@@ -64,19 +66,30 @@ class WorkerContext:
         from ..frequency import SharedFrequencyState
         dev = resolve_device(str(cfg["engine.device"]))
         hours = cfg.scoring.freq_window_hours
+        host = self.window == "host" or dev.type != "cuda"
+        wdev = torch.device("cpu") if host else dev
         if self.owner:
-            return SharedFrequencyState(lib.freq_ids, hours, dev, self.shared, create=True)
+            st = SharedFrequencyState(lib.freq_ids, hours, wdev, self.shared, create=True)
+            return self._placed(st, host, dev)
         deadline = time.monotonic() + 600
         while not self.shared.up(0):
             if time.monotonic() > deadline:
                 raise RuntimeError("serving worker 0 never created the shared frequency window")
             time.sleep(0.01)
-        if dev.type == "cuda":
+        if not host:
             from ..native import N
             me = dev.index if dev.index is not None else torch.cuda.current_device()
             if me != self.shared.home_device and not N.enable_peer_access(me, self.shared.home_device):
                 raise RuntimeError(f"no peer access from {dev} to the window's GPU {self.shared.home_device}")
-        return SharedFrequencyState(lib.freq_ids, hours, dev, self.shared, create=False)
+        return self._placed(SharedFrequencyState(lib.freq_ids, hours, wdev, self.shared, create=False), host, dev)
+
+    @staticmethod
+    def _placed(st, host: bool, dev):
+        if host and dev.type == "cuda":
+            # a GPU engine over the host window: it reads the carry and records counts through the
+            # host (Engine.freq_on_device False), as with an engine-private host FrequencyState
+            st.device_resident = False
+        return st
 
     def window_ready(self) -> None:
         self.shared.mark_up(self.index, os.getpid())
@@ -101,6 +114,18 @@ def worker_devices(cfg: Config, n: int) -> List[str]:
     return [devs[i % len(devs)] for i in range(n)]
 
 
+def window_placement(cfg: Config, devs: Sequence[str]) -> str:
+    """``server.window``: "device" / "host", or auto -- device when every worker is on one GPU or
+    ``engine.serve.peer-window`` is on (workers on other GPUs then map worker 0's HBM over xGMI, a
+    path no multi-GPU run has pinned yet), else host."""
+    w = str(cfg.get("server.window", "auto") or "auto")
+    if w in ("device", "host"):
+        return w
+    if len(set(devs)) <= 1 or bool(cfg.get("engine.serve.peer-window", False)):
+        return "device"
+    return "host"
+
+
 def _worker_argv(argv: Sequence[str], device: str) -> List[str]:
     keep = [a for a in argv if not a.startswith(("-Dserver.processes=", "-Dengine.device=",
                                                   "-Dengine.serve-devices="))]
@@ -115,10 +140,13 @@ def run_processes(argv: Sequence[str], cfg: Config, n: int, stop=None, ready_tim
     name = f"/lp-serve-{os.getpid()}-{int(time.time() * 1e3) % 100000}"
     shared = N.ProcShared(name, True, n)
     procs: List[subprocess.Popen] = []
+    devs = worker_devices(cfg, n)
+    window = window_placement(cfg, devs)
+    log.info("%d serving processes on %s, %s frequency window", n, devs, window)
     try:
-        for i, dev in enumerate(worker_devices(cfg, n)):
+        for i, dev in enumerate(devs):
             env = dict(os.environ)
-            env.update({ENV_SHM: name, ENV_WORKER: str(i), ENV_NPROC: str(n)})
+            env.update({ENV_SHM: name, ENV_WORKER: str(i), ENV_NPROC: str(n), ENV_WINDOW: window})
             procs.append(subprocess.Popen([sys.executable] + _worker_argv(argv, dev), env=env))
         t0, announced = time.monotonic(), False
         while True:

@@ -111,6 +111,11 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # frequency window (GPU memory over IPC) in arrival-ticket order; -1 = one per visible GPU.
     # Process i serves on engine.serve-devices[i % n] (or engine.device when that is empty)
     "server.processes": (1, int),
+    # where the serving processes' shared frequency window lives: "device" (HBM of worker 0's GPU,
+    # IPC-mapped by the others; kernels read / record it in place), "host" (a shared-memory block;
+    # the engines read the carry and record counts through the host, without the native runner) or
+    # "auto": device when every worker is on one GPU or engine.serve.peer-window is on, else host
+    "server.window": ("auto", str),
     # single-GPU service: bind the process to the CPUs of the GPU's NUMA node (serve/__main__.py)
     "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)

@@ -190,14 +190,31 @@ def test_two_gpu_serving_processes_equal_serial_reference(tmp_path):
     _serve_two(tmp_path, "cuda:0", n_req=40)
 
 
-def _serve_two(tmp_path, device, n_req=24):
+@pytest.mark.gpu
+def test_two_gpu_serving_processes_host_window(tmp_path):
+    """server.window=host (the placement for workers on GPUs without a pinned peer path): GPU
+    engines over the shared-memory window, carry and counts through the host -- same responses."""
+    _serve_two(tmp_path, "cuda:0", n_req=30, extra=["-Dserver.window=host"], runner=False)
+
+
+def test_window_placement():
+    from log_parser_amd.serve.procs import window_placement
+    from log_parser_amd.utils.config import Config
+    c = Config.load()
+    assert window_placement(c, ["cuda:0", "cuda:0"]) == "device"
+    assert window_placement(c, ["cuda:0", "cuda:1"]) == "host"
+    assert window_placement(Config.load(overrides={"engine.serve.peer-window": True}), ["cuda:0", "cuda:1"]) == "device"
+    assert window_placement(Config.load(overrides={"server.window": "host"}), ["cuda:0", "cuda:0"]) == "host"
+
+
+def _serve_two(tmp_path, device, n_req=24, extra=(), runner=True):
     sets, trig = make_library(20, seed=91)
     for i, s in enumerate(sets):
         (tmp_path / f"lib{i}.yaml").write_text(yaml.safe_dump(s.model_dump(by_alias=True, exclude_none=True)))
     port = free_port()
     cmd = [sys.executable, "-m", "log_parser_amd.serve", f"-Dpattern.directory={tmp_path}", f"-Dengine.device={device}",
            "-Dserver.processes=2", f"-Dserver.port={port}", "-Dserver.host=127.0.0.1",
-           "-Dscoring.frequency.threshold=1.0", "-Dserver.numa-bind=false"]
+           "-Dscoring.frequency.threshold=1.0", "-Dserver.numa-bind=false"] + list(extra)
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     logf = open(tmp_path / "serve.log", "wb")
     sup = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=logf)
@@ -224,12 +241,12 @@ def _serve_two(tmp_path, device, n_req=24):
             assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o["events"]] == \
                    [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]], i
             assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
-        if device != "cpu":                 # both workers served through the native request runner
+        if device != "cpu":                 # both workers served (through the native runner on a device window)
             seen = {}
             for _ in range(40):
                 r = json.loads(_get(port, "/ready")[1])
                 seen[r["worker"]["pid"]] = r["nativeRunner"]
-            assert len(seen) == 2 and all(seen.values()), seen
+            assert len(seen) == 2 and all(v == runner for v in seen.values()), seen
         # the admin API reads the one window from either process
         stats = [json.loads(_get(port, "/admin/frequency")[1]) for _ in range(4)]
         assert all(s == stats[0] for s in stats) and sum(stats[0].values()) > 0

@@ -381,6 +381,7 @@ static py::tuple split_docs(uint64_t buf, py::array_t<int64_t> doc_off) {
 struct RawLogs {
   std::string body;
   size_t off = 0, len = 0;
+  size_t dlen = 0;            // decoded length (0: unknown, decode serially)
   std::shared_ptr<BufferPool> pool;
   RawLogs() = default;
   RawLogs(const RawLogs&) = delete;
@@ -419,18 +420,34 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
     // escaped length bounds the decoded one; the decoder may write 64 bytes past its output
     std::vector<const RawLogs*> rl(D);
     int64_t bound = 64;
+    bool known = true;                 // decoded lengths counted by the front end's validation
     for (int64_t i = 0; i < D; ++i) {
       rl[i] = &docs[i].cast<const RawLogs&>();
       bound += (int64_t)rl[i]->len;
+      known = known && (rl[i]->dlen > 0 || rl[i]->len == 0);
     }
     if (bound > cap) return py::int_(bound);
     {
       py::gil_scoped_release nogil;
       uint8_t* d = P<uint8_t>(dst);
-      for (int64_t i = 0; i < D; ++i) {
-        off[i + 1] = off[i] + (int64_t)decode_json_string(rl[i]->data(), rl[i]->len, reinterpret_cast<char*>(d + off[i]));
-        src[i] = reinterpret_cast<const char*>(d + off[i]);     // split in place (no copy)
+      if (known) {
+        // every document's output offset is known: decode them side by side (exact-bounds
+        // decoder: no store past a document's end) -- one thread decoded a 1 GB burst serially
+        for (int64_t i = 0; i < D; ++i) off[i + 1] = off[i] + (int64_t)rl[i]->dlen;
+        std::atomic<bool> bad{false};
+        HostPool::get().run(D, std::max(1, nthreads), [&](int64_t i) {
+          const size_t k = rl[i]->len ? decode_json_string_exact(rl[i]->data(), rl[i]->len,
+                                                                 reinterpret_cast<char*>(d + off[i]))
+                                      : 0;
+          if (k != rl[i]->dlen) bad = true;
+        });
+        if (bad) known = false;          // (never: the same grammar counted them) -- redo serially
       }
+      if (!known) {
+        for (int64_t i = 0; i < D; ++i)
+          off[i + 1] = off[i] + (int64_t)decode_json_string(rl[i]->data(), rl[i]->len, reinterpret_cast<char*>(d + off[i]));
+      }
+      for (int64_t i = 0; i < D; ++i) src[i] = reinterpret_cast<const char*>(d + off[i]);   // split in place
     }
   }
   for (int64_t i = 0; i < D && !raw; ++i) {
@@ -645,6 +662,22 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false);
+  // the front end's skip-mode view of a body: (status, logs offset, escaped length, decoded length)
+  m.def("pod_logs_span", [](const py::bytes& body) {
+    std::string b = body;
+    PodRequest pr;
+    const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(b.data()), b.size(), pr, false);
+    return py::make_tuple(st, pr.logs_off, pr.logs_len, pr.logs_dlen);
+  });
+  // the packer's exact-bounds decoder of a string's escaped content (tests)
+  m.def("decode_json_exact", [](const py::bytes& content) {
+    std::string c = content;
+    std::string out(c.size() + 128, '\xAB');
+    const size_t k = decode_json_string_exact(reinterpret_cast<const uint8_t*>(c.data()), c.size(), &out[0]);
+    bool intact = true;                  // nothing stored past the decoded end
+    for (size_t i = k; i < out.size(); ++i) intact = intact && out[i] == '\xAB';
+    return py::make_tuple(py::bytes(out.data(), k), intact);
+  });
 
   // ---- device launchers
   m.def("line_index_tiles", &line_index_tiles);
@@ -1003,6 +1036,7 @@ PYBIND11_MODULE(_lpnative, m) {
               auto* rl = new RawLogs();
               rl->off = r.logs_off;
               rl->len = r.logs_len;
+              rl->dlen = r.logs_dlen;
               rl->body = std::move(r.body);
               rl->pool = s.pool();
               out.append(py::make_tuple(r.id, 0, py::cast(rl, py::return_value_policy::take_ownership), r.pod_name,

@@ -471,6 +471,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
       r.pod_name = pr.has_name ? pr.pod_name : std::string();
       r.logs_off = b0 + pr.logs_off;
       r.logs_len = pr.logs_len;
+      r.logs_dlen = pr.logs_dlen;
       if (c->in.size() == total) {   // the usual case: hand the whole buffer over, no copy
         r.body.swap(c->in);
         c->in = take_buffer();

@@ -26,6 +26,7 @@ struct HttpRequest {
   std::string logs;         // decoded UTF-8 log text (callers of the decode_logs mode)
   size_t logs_off = 0;      // kind 0: `body` is the raw request buffer and the JSON `logs`
   size_t logs_len = 0;      //   string's escaped content is body[logs_off, logs_off + logs_len)
+  size_t logs_dlen = 0;     //   decoded UTF-8 length (counted while validating)
   std::string pod_name;     // kind 0: pod.metadata.name or "" (unknown)
   double t_arrival = 0;     // monotonic seconds, when the body was complete
 };

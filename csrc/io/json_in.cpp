@@ -74,7 +74,7 @@ inline int utf8_len(const uint8_t* p, const uint8_t* e) {
 // With Store = false the block is only validated (skip mode of a string nobody reads).
 template <bool Store>
 __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vbmi2,bmi,bmi2,popcnt")))
-bool block64(const uint8_t*& p, char*& w) {
+bool block64(const uint8_t*& p, char*& w, size_t* kept = nullptr) {
   const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(p));
   const uint64_t B = _mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('\\'));
   const uint64_t Q = _mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('"'));
@@ -100,6 +100,7 @@ bool block64(const uint8_t*& p, char*& w) {
   const __m512i tr = _mm512_permutex2var_epi8(t0, v, t1);                 // low 7 bits index
   const uint64_t bad_esc = escaped & _mm512_cmpeq_epi8_mask(tr, _mm512_setzero_si512());
   if ((Q & ~escaped) | CH | bad_esc | (B >> 63)) return false;
+  if (kept) *kept += (size_t)_mm_popcnt_u64(~initiators);
   if (Store) {
     const __m512i o = _mm512_mask_blend_epi8(escaped, v, tr);
     const uint64_t keep = ~initiators;
@@ -124,9 +125,8 @@ bool have_block64() {
 // ordinary text costs one load, one store and one compare per 16 bytes, and an escape (a log has
 // one "\n" every ~100 bytes) only a few scalar steps -- no per-run append. Returns the end of the
 // decoded bytes, or nullptr on error (c.fallback set when json.loads must decide).
-char* str_into(Cur& c, char* w) {
-  if (c.p >= c.e || *c.p != '"') return nullptr;
-  ++c.p;
+template <bool Span>
+char* str_loop(Cur& c, char* w) {
 #if defined(__x86_64__)
   const bool wide = have_block64();
 #endif
@@ -156,7 +156,7 @@ char* str_into(Cur& c, char* w) {
     }
 #endif
     while (c.p < c.e && *c.p != '"' && *c.p != '\\' && *c.p >= 0x20 && *c.p < 0x80) *w++ = (char)*c.p++;
-    if (c.p >= c.e) return nullptr;
+    if (c.p >= c.e) return Span ? w : nullptr;
     const uint8_t b = *c.p;
     if (b == '"') {
       ++c.p;
@@ -216,10 +216,28 @@ char* str_into(Cur& c, char* w) {
   }
 }
 
-// string at c.p (opening quote); appends the decoded UTF-8 to `out` when non-null
-bool str(Cur& c, std::string* out) {
+char* str_into(Cur& c, char* w) {
+  if (c.p >= c.e || *c.p != '"') return nullptr;
+  ++c.p;
+  return str_loop<false>(c, w);
+}
+
+// the content bytes [c.p, c.e) of a string (no quotes), cut where no escape / UTF-8 sequence
+// straddles c.e: decoded to w (block stores may run past the returned end)
+char* str_into_span(Cur& c, char* w) { return str_loop<true>(c, w); }
+
+// string at c.p (opening quote); appends the decoded UTF-8 to `out` when non-null; adds the
+// decoded length to *dlen when non-null (skip mode: the batch packer decodes later, in parallel,
+// straight to the offsets these lengths give)
+bool str(Cur& c, std::string* out, size_t* dlen = nullptr) {
   if (c.p >= c.e || *c.p != '"') return false;
   ++c.p;
+  size_t dn = 0;
+  struct Flush {
+    size_t* d;
+    size_t& n;
+    ~Flush() { if (d) *d += n; }
+  } flush{dlen, dn};
 #if defined(__x86_64__)
   const bool wide = out == nullptr && have_block64();
   char* none = nullptr;
@@ -227,7 +245,7 @@ bool str(Cur& c, std::string* out) {
   for (;;) {
 #if defined(__x86_64__)
     if (wide)
-      while (c.e - c.p >= 64 && block64<false>(c.p, none)) {
+      while (c.e - c.p >= 64 && block64<false>(c.p, none, &dn)) {
       }
 #endif
     const uint8_t* run = c.p;
@@ -248,6 +266,7 @@ bool str(Cur& c, std::string* out) {
     }
 #endif
     while (c.p < c.e && *c.p != '"' && *c.p != '\\' && *c.p >= 0x20 && *c.p < 0x80) ++c.p;
+    dn += (size_t)(c.p - run);
     if (out && c.p > run) out->append(reinterpret_cast<const char*>(run), c.p - run);
     if (c.p >= c.e) return false;
     const uint8_t b = *c.p;
@@ -263,6 +282,7 @@ bool str(Cur& c, std::string* out) {
         return false;
       }
       if (out) out->append(reinterpret_cast<const char*>(c.p), k);
+      dn += (size_t)k;
       c.p += k;
       continue;
     }
@@ -293,6 +313,7 @@ bool str(Cur& c, std::string* out) {
           c.fallback = true;
           return false;
         }
+        dn += v < 0x80 ? 1 : v < 0x800 ? 2 : 3;
         if (out) {
           if (v < 0x80) {
             out->push_back((char)v);
@@ -310,6 +331,7 @@ bool str(Cur& c, std::string* out) {
       default:
         return false;
     }
+    ++dn;
     if (out) out->push_back(ch);
   }
 }
@@ -444,6 +466,78 @@ size_t decode_json_string(const uint8_t* p, size_t n, char* w) {
   return e ? (size_t)(e - w) : 0;
 }
 
+size_t decode_json_string_exact(const uint8_t* p, size_t n, char* w) {
+  // the block decoders store whole 16 / 64-byte blocks past their write cursor, so they run on a
+  // prefix only: its unconditional stores stay inside this string's output while >= 64 decoded
+  // bytes follow -- 384 encoded bytes are >= 64 decoded ones even if all are 6-byte \u escapes
+  constexpr size_t kTail = 384;
+  const uint8_t* const end = p + n;
+  char* const w0 = w;
+  const uint8_t* q = p;
+  if (n > kTail + 64) {
+    // the prefix ends at a position no escape straddles: walk back over a backslash run
+    const uint8_t* cut = end - kTail;
+    const uint8_t* b = cut;
+    while (b > p && b[-1] == '\\') --b;
+    if (((cut - b) & 1) != 0) --cut;                     // odd run: cut sits on an escaped byte
+    while (cut > p && (*cut & 0xC0) == 0x80) --cut;      // not inside a UTF-8 sequence
+    // a \uXXXX escape: its 4 hex digits must not be split either
+    for (int k = 1; k <= 4 && cut - k >= p; ++k) {
+      if (cut[-k] == 'u' && cut - k - 1 >= p && cut[-k - 1] == '\\') {
+        const uint8_t* bb = cut - k - 1;
+        size_t run = 0;
+        while (bb - run > p && bb[-1 - (ptrdiff_t)run] == '\\') ++run;
+        if ((run & 1) == 0) { cut -= k + 1; break; }   // an initiating backslash
+      }
+    }
+    // decode [p, cut) with the block decoders
+    Cur c{p, cut};
+    char* e = str_into_span(c, w);
+    if (!e) return 0;
+    w = e;
+    q = c.p;
+  }
+  // exact scalar tail: no store past the decoded end
+  while (q < end) {
+    const uint8_t b = *q;
+    if (b != '\\') {
+      *w++ = (char)b;
+      ++q;
+      continue;
+    }
+    const uint8_t x = q[1];
+    q += 2;
+    switch (x) {
+      case '"': *w++ = '"'; break;
+      case '\\': *w++ = '\\'; break;
+      case '/': *w++ = '/'; break;
+      case 'b': *w++ = '\b'; break;
+      case 'f': *w++ = '\f'; break;
+      case 'n': *w++ = '\n'; break;
+      case 'r': *w++ = '\r'; break;
+      case 't': *w++ = '\t'; break;
+      case 'u': {
+        int v = 0;
+        for (int i = 0; i < 4; ++i) v = (v << 4) | hexv(q[i]);
+        q += 4;
+        if (v < 0x80) {
+          *w++ = (char)v;
+        } else if (v < 0x800) {
+          *w++ = (char)(0xC0 | (v >> 6));
+          *w++ = (char)(0x80 | (v & 0x3F));
+        } else {
+          *w++ = (char)(0xE0 | (v >> 12));
+          *w++ = (char)(0x80 | ((v >> 6) & 0x3F));
+          *w++ = (char)(0x80 | (v & 0x3F));
+        }
+        break;
+      }
+      default: return 0;
+    }
+  }
+  return (size_t)(w - w0);
+}
+
 int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs) {
   out = PodRequest{};
   if (n >= 2 && (body[0] == 0 || body[1] == 0)) return JIN_FALLBACK;      // UTF-16/32
@@ -464,7 +558,8 @@ int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decod
         out.logs.clear();
         out.logs_kind = 1;
         const uint8_t* s0 = cc.p;
-        if (!str(cc, nullptr)) return false;
+        out.logs_dlen = 0;
+        if (!str(cc, nullptr, &out.logs_dlen)) return false;
         out.logs_off = (size_t)(s0 + 1 - body);
         out.logs_len = (size_t)(cc.p - s0 - 2);
         return true;

@@ -16,6 +16,7 @@ struct PodRequest {
   std::string logs;           // UTF-8, escapes decoded (decode_logs mode)
   size_t logs_off = 0;        // logs_kind 1: the raw JSON string's content (between the quotes)
   size_t logs_len = 0;        //   as an offset / length into the body
+  size_t logs_dlen = 0;       //   and its decoded UTF-8 length
 };
 
 // Validates the whole body. With decode_logs the `logs` string is unescaped into out.logs;
@@ -26,5 +27,8 @@ int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decod
 // Unescapes the content of a JSON string that parse_pod_request validated (`n` raw bytes between
 // the quotes) into `w`, which must have room for n + 64 bytes; returns the decoded length.
 size_t decode_json_string(const uint8_t* p, size_t n, char* w);
+// the same, writing nothing past the decoded end (documents decoded side by side by several
+// threads into one buffer); returns the decoded length, 0 on an invalid escape
+size_t decode_json_string_exact(const uint8_t* p, size_t n, char* w);
 
 }  // namespace lp

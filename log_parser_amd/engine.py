@@ -43,7 +43,7 @@ import torch
 from .frequency import DeviceFrequencyState, FrequencyState
 from .golden import SEVERITY_ORDER
 from .models.compiled import CompiledLibrary
-from .native import N
+from .native import N, host_thread_budget
 from .ops import kernels as K
 from .regex.javacompat import compile_java
 from .utils import tracing as TR
@@ -997,7 +997,7 @@ class Engine:
             self._stage_pool.give(job.stage)
             job.stage = None
 
-    _STAGE_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 8))
+    _STAGE_THREADS = host_thread_budget()
 
     def _stage_docs(self, job: "BatchJob", docs):
         """Pack request bodies into the job's (pinned) staging buffer and build the per-document

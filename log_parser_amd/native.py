@@ -27,6 +27,15 @@ def _needs_build() -> bool:
     return any(os.path.getmtime(h) > t for h in _build._headers())
 
 
+def host_thread_budget() -> int:
+    """Worker threads for native host loops (packing, JSON emission, CPU twins): this process's
+    share of the CPU budget (cgroup quota aware; one of LP_SERVE_NPROC serving processes gets
+    1/n of it), at most 16."""
+    from .utils.numa import cpu_budget
+    nproc = max(1, int(os.environ.get("LP_SERVE_NPROC", "1") or 1))
+    return max(1, min(16, cpu_budget() // nproc))
+
+
 def load():
     global _mod
     if _mod is not None:
@@ -36,8 +45,7 @@ def load():
         _build.build()
     _mod = importlib.import_module("log_parser_amd._lpnative")
     # CPU-backend worker threads: this process's CPU share, at most 16 (LP_HOST_THREADS overrides)
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 8)
-    _mod.set_host_threads(int(os.environ.get("LP_HOST_THREADS", min(16, n))))
+    _mod.set_host_threads(int(os.environ.get("LP_HOST_THREADS", host_thread_budget())))
     return _mod
 
 

@@ -112,3 +112,28 @@ def test_native_decoder_64_byte_blocks(two_pass):
         body = ('{"pod": {}, "logs": "' + raw + '"}').encode()
         native += _check(body, two_pass)
     assert native > 1000
+
+
+def test_decoded_length_and_exact_decoder():
+    """The front end counts each log's decoded length while validating (skip mode), and the
+    packer's exact-bounds decoder (documents decoded side by side into one buffer) gives the same
+    bytes as json.loads -- escapes and UTF-8 at every position around the decoder's prefix cut."""
+    import json as _json
+    import random
+    from log_parser_amd.native import N
+    rng = random.Random(7)
+    atoms = ["a", "xyz ", "\n", "\r\n", '"', "\\", "/", "\t", "\b", "\f", "é", "€", "😀", "\u0085", " ",
+             "\x01", "\x7f", "ß" * 3]
+    for n in list(range(0, 40)) + list(range(370, 470)) + [1000, 5000, 20000]:
+        s = "".join(rng.choice(atoms) for _ in range(n))
+        for ensure_ascii in (False, True):
+            body = _json.dumps({"pod": {}, "logs": s}, ensure_ascii=ensure_ascii).encode()
+            st, off, ln, dlen = N.pod_logs_span(body)
+            if ensure_ascii and "😀" in s:
+                assert st == 3            # \ud83d\ude00: surrogate escapes go to json.loads
+                continue
+            assert st == 0
+            want = s.encode("utf-8")
+            assert dlen == len(want), (n, ensure_ascii)
+            got, intact = N.decode_json_exact(body[off:off + ln])
+            assert got == want and intact, (n, ensure_ascii)

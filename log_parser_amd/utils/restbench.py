@@ -163,6 +163,25 @@ class ServerProcess:
                 rc.close()
         return lat
 
+    def cpu_seconds(self) -> float:
+        """User + system CPU seconds of the server and its serving processes so far (/proc)."""
+        tck = os.sysconf("SC_CLK_TCK")
+        pids = [self.proc.pid]
+        try:                                      # the supervisor's workers (server.processes)
+            with open(f"/proc/{self.proc.pid}/task/{self.proc.pid}/children") as f:
+                pids += [int(x) for x in f.read().split()]
+        except OSError:
+            pass
+        tot = 0.0
+        for pid in pids:
+            try:
+                with open(f"/proc/{pid}/stat") as f:
+                    fields = f.read().rsplit(")", 1)[1].split()
+                tot += (int(fields[11]) + int(fields[12])) / tck     # utime, stime
+            except (OSError, IndexError, ValueError):
+                pass
+        return tot
+
     def stop(self) -> None:
         if self.conn is not None:
             self.conn.close()

@@ -178,7 +178,14 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     post = head if hr else b""
     nbytes = len(pre) + len(block_b) * reps + len(post)
     size = K.padded_len(nbytes)
-    host = torch.zeros(size, dtype=torch.uint8, pin_memory=use_cuda)
+    # registered pages: the H2D goes to the SDMA engines, not a blit kernel beside the step's
+    # kernels (utils/hostmem.py)
+    if use_cuda:
+        from log_parser_amd.utils.hostmem import registered_empty
+        host = registered_empty(size)
+        host.zero_()
+    else:
+        host = torch.zeros(size, dtype=torch.uint8)
     hv = host.numpy()
     o = 0
     for part in [pre] + [block_b] * reps + [post]:         # fill in place: no whole-shard temporaries

@@ -32,6 +32,7 @@ import torch
 
 from ..engine import Engine, Segments
 from ..ops import kernels as K
+from ..utils.hostmem import registered_empty
 
 
 CHUNK_MIN, CHUNK_MAX = 256 << 20, 8 << 30
@@ -398,7 +399,8 @@ class StreamAnalyzer:
                         ev.synchronize()                      # its previous H2D copy is done
                     if pinned is None or pinned.numel() < size:
                         cap = max(size, K.padded_len(self.chunk_bytes + (self.chunk_bytes >> 4)))
-                        pinned = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+                        pinned = None
+                        pinned = registered_empty(cap)      # SDMA-copied pages (utils/hostmem.py)
                 else:
                     pinned = torch.empty(size, dtype=torch.uint8)
                 if n:

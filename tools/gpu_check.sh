@@ -5,6 +5,7 @@
 #   bench   bench.py (headline, 1 GPU)
 #   http    config 5 over HTTP: 1 and 2 serving processes (stage timelines), and the front end alone
 #   stream  config 4: 1B-line stream, auto (HBM-sized) chunks and 256 MiB chunks (same digest)
+#   configs config 2 (1M lines, 256 patterns, realistic library) and config 1 (CPU-only /parse)
 # Run: gpurun -- bash tools/gpu_check.sh [step ...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -43,6 +44,9 @@ for s in $steps; do
       run stream_auto 600 python -u benchmarks/bench_configs.py stream
       run stream_8g 600 python -u benchmarks/bench_configs.py stream --chunk-mb 8192
       run stream_256 600 python -u benchmarks/bench_configs.py stream --chunk-mb 256 ;;
+    configs)
+      run single 600 python -u benchmarks/bench_configs.py single
+      run rest 600 python -u benchmarks/bench_configs.py rest ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,3 +1,7 @@
+import os
+
+import torch
+
 from log_parser_amd.utils.config import Config, env_name, parse_cli_overrides
 
 
@@ -25,3 +29,23 @@ def test_env_mapping_and_precedence(tmp_path):
 
 def test_cli_overrides():
     assert parse_cli_overrides(["-Dpattern.directory=/x", "foo", "-Da=b=c"]) == {"pattern.directory": "/x", "a": "b=c"}
+
+
+def test_cpu_budget_and_host_threads(monkeypatch):
+    """CPU budget = affinity capped by the cgroup quota; native host threads get 1/n of it per
+    serving process (LP_SERVE_NPROC), at most 16."""
+    from log_parser_amd.native import host_thread_budget
+    from log_parser_amd.utils import numa
+    b = numa.cpu_budget()
+    assert 1 <= b <= (os.cpu_count() or b)
+    monkeypatch.setenv("LP_SERVE_NPROC", "2")
+    assert host_thread_budget() == max(1, min(16, b // 2))
+    monkeypatch.setattr(numa, "cpu_budget", lambda: 40)
+    monkeypatch.setenv("LP_SERVE_NPROC", "1")
+    assert host_thread_budget() == 16
+
+
+def test_registered_empty_falls_back_on_cpu():
+    from log_parser_amd.utils.hostmem import registered_empty
+    t = registered_empty(4096)
+    assert t.numel() == 4096 and t.dtype == torch.uint8 and t.device.type == "cpu"

@@ -98,7 +98,7 @@ class RepeatBuffer:
     def segments(self, start: int, stop: int):
         """[(offset in ``pinned_block()``, offset from start, length)] covering [start, stop): the
         registered copy is the block tiled (the same byte stream), so a chunk is a few large DMA
-        copies instead of one per 20 MB block (per-copy overhead: 52.8 -> GB/s, profiles/r4_b)."""
+        copies instead of one per ~20 MB block."""
         B = len(self.block) * getattr(self, "_reps", 1)
         out, pos = [], start
         while pos < stop:

@@ -326,11 +326,11 @@ def mode_concurrent_http(args):
                             b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
                 lines_of.append(int(s_))
         idx = np.array([sizes_set.index(int(s_)) * 4 + i % 4 for i, s_ in enumerate(sizes)], np.int32)
-        N.http_burst("127.0.0.1", srv.port, msgs, idx[:min(n, 2000)], 300.0)          # warm-up burst
+        N.http_burst("127.0.0.1", srv.port, msgs, idx[:min(n, 2000)], 300.0, args.client_threads)  # warm-up
         workers = max(args.processes, 1)
         st0 = collect_stages(srv.port, workers)
         cpu0, cli0 = srv.cpu_seconds(), time.process_time()
-        lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0)
+        lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0, args.client_threads)
         cpu_srv, cpu_cli = srv.cpu_seconds() - cpu0, time.process_time() - cli0
         st1 = collect_stages(srv.port, workers)
         breakdown = stage_breakdown(st0, st1, wall)
@@ -348,6 +348,7 @@ def mode_concurrent_http(args):
     lines = float(np.array(lines_of)[idx].sum())
     print(json.dumps({"config": f"concurrent-http-{n}-connections-mixed-realistic", "device": dev,
                       "engines": args.engines, "processes": args.processes, "connections": n,
+                      "client_threads": args.client_threads,
                       "completed": int(done),
                       "status_200": int((st == 200).sum()),
                       "p50_ms": round(float(np.median(lat[ok])) * 1e3, 3),
@@ -390,6 +391,8 @@ def main():
     ap.add_argument("--processes", type=int, default=1,
                     help="concurrent_http: serving processes sharing one frequency window (server.processes)")
     ap.add_argument("--server-opt", action="append", help="concurrent_http: extra -Dkey=value for the server")
+    ap.add_argument("--client-threads", type=int, default=8,
+                    help="concurrent_http: load-generator threads (they share the host's CPUs with the server)")
     ap.add_argument("--server-log", default=None, help="concurrent_http: server stdout / stderr to this file")
     ap.add_argument("--http", default="native", choices=["native", "uvicorn"], help="rest: HTTP front end")
     ap.add_argument("--library", default="realistic", choices=["realistic", "synthetic"],

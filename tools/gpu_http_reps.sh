@@ -8,8 +8,10 @@ timeout -k 10 300 python -u -m pytest tests/test_json_in.py -q -x > gpurun_out/g
 rc=$?; echo "json_in rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
   for p in 1 2; do
-    timeout -k 10 300 python -u benchmarks/bench_configs.py concurrent_http --processes $p \
-      > gpurun_out/gh_p${p}_$i.log 2>&1
-    rc=$?; echo "p$p rep$i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    for ct in 8 4; do
+      timeout -k 10 300 python -u benchmarks/bench_configs.py concurrent_http --processes $p --client-threads $ct \
+        > gpurun_out/gh_p${p}_c${ct}_$i.log 2>&1
+      rc=$?; echo "p$p c$ct rep$i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    done
   done
 done

@@ -1,5 +1,6 @@
 # GPU-box validation session. Logs under gpurun_out/. Steps (default: all, in this order):
 #   tests   the regex / serving / MFMA GPU tests
+#   scantest  the literal-free scan kernel's GPU tests (bulk + request variants, CRLF) and the kernel tests
 #   scan    scan-group A/B (16 vs 32 members per multi-regex DFA)
 #   nfa     MFMA vs BPG A/B per regex shape (tools/nfa_ab.py)
 #   bench   bench.py (headline, 1 GPU)
@@ -26,6 +27,9 @@ for s in $steps; do
     tests)
       run tests 900 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py \
         tests/test_nfa.py tests/test_regex.py tests/test_serve_procs.py tests/test_stream.py -m gpu -x -v --durations=15 --timeout 300 \
+        --timeout-method thread ;;
+    scantest)
+      run scantest 600 python -u -m pytest tests/test_scan_multi.py tests/test_gpu.py -m gpu -x -q --timeout 300 \
         --timeout-method thread ;;
     scan)
       run scan16 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 16

@@ -5,7 +5,9 @@ ROCm 7): python tools/kstats_db.py run_results.db [steps] [top] [--median] [--ma
 behind the copy stream's H2D blit under the profiler); otherwise total duration / steps.
 --marker NAME --last K: only the launches from the K-th-from-last launch of kernel NAME (one per
 step, e.g. k_nl_count) to the end of the trace -- the last K steps, without the set-up copies,
-fills and library uploads that otherwise inflate the launch count per step; steps = K."""
+fills and library uploads that otherwise inflate the launch count per step; steps = K.
+--timeline (with --marker): also print one whole step (between the last two marker launches):
+each kernel's start offset from the marker, duration and queue, to read the step's critical path."""
 import sqlite3
 import statistics
 import sys
@@ -36,6 +38,16 @@ c = sqlite3.connect(db)
 cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
 name = "name" if "name" in cols else "kernel_name"
 rows_all = c.execute(f"select {name}, start, end from kernels order by start").fetchall()
+if marker and "--timeline" in sys.argv:
+    marks = [s for n, s, e in rows_all if marker in n]
+    if len(marks) >= 2:
+        a, b = marks[-2], marks[-1]
+        step_rows = [r for r in rows_all if a <= r[1] < b]
+        print(f"one step: {len(step_rows)} launches, marker to last kernel end "
+              f"{(max(e for _, _, e in step_rows) - a) / 1e3:.1f} us, marker period {(b - a) / 1e3:.1f} us")
+        for n, s_, e in step_rows:
+            print(f"  +{(s_ - a) / 1e3:8.1f} us  {(e - s_) / 1e3:8.1f} us  {n[:80]}")
+        print()
 if marker and last:
     marks = [s for n, s, e in rows_all if marker in n]
     k = int(last)

@@ -972,6 +972,13 @@ PYBIND11_MODULE(_lpnative, m) {
     return true;
   });
   m.def("host_unregister", [](uint64_t ptr) { return hipHostUnregister(reinterpret_cast<void*>(ptr)) == hipSuccess; });
+  // one host -> device copy on a HIP stream, HostToDevice kind (the copy-engine probe compares it
+  // with torch's copy_; tools/copy_engine_probe.py)
+  m.def("copy_h2d", [](uint64_t dst, uint64_t src, int64_t n, uint64_t stream) {
+    if (hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), (size_t)n,
+                       hipMemcpyHostToDevice, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+      throw std::runtime_error(std::string("copy_h2d: ") + hipGetErrorString(hipGetLastError()));
+  });
   // peer access for kernels on `device` reading / writing memory of `peer` (a shared window)
   m.def("enable_peer_access", [](int device, int peer) {
     if (device == peer) return true;

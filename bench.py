@@ -178,8 +178,7 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     post = head if hr else b""
     nbytes = len(pre) + len(block_b) * reps + len(post)
     size = K.padded_len(nbytes)
-    # registered pages: the H2D goes to the SDMA engines, not a blit kernel beside the step's
-    # kernels (utils/hostmem.py)
+    # page-locked host shard, registered in place (utils/hostmem.py); the H2D is an SDMA copy
     if use_cuda:
         from log_parser_amd.utils.hostmem import registered_empty
         host = registered_empty(size)

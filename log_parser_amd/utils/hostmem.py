@@ -1,14 +1,13 @@
 """Page-locked host buffers for bulk host-to-device copies.
 
-Two kinds of pinned memory behave differently on the copy path (ROCm 7, MI355X):
-* ``torch.empty(..., pin_memory=True)`` (hipHostMalloc) -- ROCclr moves it with a BLIT KERNEL
-  (``__amd_rocclr_copyBuffer``): a 1.33 GB H2D ran 23 ms as a kernel occupying CUs next to the
-  step's own kernels, which then ran slower (k_prefilter 1.03 vs 0.67 ms, profiles/r4_c);
-* ordinary pages registered with ``hipHostRegister`` -- moved by the SDMA engines, no CU time,
-  at the same ~57 GB/s (profiles/r4_b).
-``registered_empty`` gives the second kind (an anonymous mapping, registered in place, unregistered
-and unmapped when the tensor's owner goes away), or falls back to the first when registration is
-refused or no GPU is present.
+``registered_empty`` gives ordinary pages registered in place with ``hipHostRegister`` (an
+anonymous mapping, unregistered and unmapped when the tensor's owner goes away), or falls back to
+torch's pinned allocator (hipHostMalloc) when registration is refused or no GPU is present. Both
+kinds are copied by the SDMA engines at ~57 GB/s (profiles/r4_c: copy-engine probes over both kinds,
+torch and native copies, queued copies; the HIP runtime's own log of the bench). A blit kernel
+(``__amd_rocclr_copyBuffer``) replaces the SDMA copy only when the HSA copy call fails, which was
+seen only under the profiler. Registration lets a buffer be sized and laid out by the caller (an
+mmap of any size, a page-locked view of memory that already exists).
 """
 from __future__ import annotations
 

@@ -16,7 +16,57 @@ from log_parser_amd.utils.hostmem import registered_empty  # noqa: E402
 MB = 1 << 20
 
 
+def backlog():
+    """Copies queued behind each other (the bench's prefetch: the next step's H2D is queued while the
+    current one still runs): which of them become blit kernels?"""
+    dev = torch.empty(2800 * MB, dtype=torch.uint8, device="cuda")
+    host = registered_empty(1400 * MB)
+    host.fill_(7)
+    side, comp = torch.cuda.Stream(), torch.cuda.Stream()
+    groups = [("2x1333", [1333] * 2), ("3x1333", [1333] * 3), ("8x256", [256] * 8), ("12x64", [64] * 12)]
+    case = 100
+    for name, sizes in groups:
+        torch.cuda.synchronize()
+        time.sleep(0.05)
+        t0 = time.perf_counter()
+        tot = 0
+        with torch.cuda.stream(side):
+            for k, mb in enumerate(sizes):
+                case += 1
+                n = mb * MB + case * 4096
+                o = (k % 2) * 1400 * MB
+                dev[o:o + n].copy_(host[:n], non_blocking=True)
+                tot += n
+        side.synchronize()
+        dt = time.perf_counter() - t0
+        print(json.dumps({"group": name, "last_case": case, "bytes": tot, "GBps": round(tot / dt / 1e9, 2)}), flush=True)
+    # dependencies as in the bench: each copy waits for a compute-stream event, compute waits for it
+    torch.cuda.synchronize()
+    time.sleep(0.05)
+    ev_free = [torch.cuda.Event(), torch.cuda.Event()]
+    x = torch.empty(64 * MB, device="cuda")
+    for k in range(6):
+        case += 1
+        n = 1333 * MB + case * 4096
+        o = (k % 2) * 1400 * MB
+        with torch.cuda.stream(side):
+            if k >= 2:
+                side.wait_event(ev_free[k % 2])
+            dev[o:o + n].copy_(host[:n], non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record(side)
+        comp.wait_event(ready)
+        with torch.cuda.stream(comp):
+            for _ in range(20):
+                x.mul_(1.0001)
+            ev_free[k % 2].record(comp)
+    torch.cuda.synchronize()
+    print(json.dumps({"group": "dep6x1333", "last_case": case}), flush=True)
+
+
 def main():
+    if "--backlog" in sys.argv:
+        return backlog()
     dev = torch.empty(1400 * MB, dtype=torch.uint8, device="cuda")
     side = torch.cuda.Stream()
     big = 1333 * MB

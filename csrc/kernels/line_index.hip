@@ -3,7 +3,7 @@
 // host read.
 //
 //   k_nl_count   per 16 KiB tile: number of '\n' + a 1-bit-per-byte '\n' mask + a '\r' flag
-//   rocprim      exclusive scan of the tile counts (decoupled look-back over ~80k counts)
+//   k_tile_scan  exclusive scan of the tile counts (~80k counts, one workgroup)
 //   k_nl_lines   4 tiles per workgroup, from the mask (text only in '\r'-flagged tiles): every '\n' at p with global index g writes starts[g+1] = p + 1
 //                and, when the previous '\n' is in the same tile, lens[g] = (p minus a '\r' right
 //                before it) - start; staged in LDS, stored coalesced. The tile's FIRST line end is
@@ -21,7 +21,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
-#include <rocprim/rocprim.hpp>
 #include <stdexcept>
 #include <string>
 
@@ -315,6 +314,55 @@ __global__ __launch_bounds__(256) void k_line_trim(const int32_t* __restrict__ l
   if (threadIdx.x == 0) info[2] = 0;
 }
 
+// exclusive prefix of the per-tile '\n' counts (~80k tiles for a 1.3 GB shard) in ONE workgroup:
+// each thread sums a contiguous run of counts (8-byte loads, all in flight), the 1,024 run sums are
+// scanned through the waves' shuffles + LDS, then each thread re-reads its run and writes its
+// offsets. One launch of ~10 us against rocPRIM's look-back scan (an init kernel + the scan,
+// 81 us per step, profiles/r4_c).
+constexpr int LS_THREADS = 1024;
+__global__ __launch_bounds__(LS_THREADS) void k_tile_scan(const int32_t* __restrict__ cnt, int64_t nt,
+                                                          int64_t* __restrict__ off) {
+  __shared__ int64_t wsum[LS_THREADS / 64];
+  const int64_t per = (((nt + LS_THREADS - 1) / LS_THREADS) + 1) & ~(int64_t)1;   // even: 8-byte aligned runs
+  const int64_t a = (int64_t)threadIdx.x * per;
+  const int64_t b = a + per < nt ? a + per : nt;
+  int64_t s = 0;
+  const int2* c2 = reinterpret_cast<const int2*>(cnt);      // cnt is 8-byte aligned (int64 workspace)
+  const int64_t b2 = a < b ? a + ((b - a) & ~(int64_t)1) : a;
+#pragma unroll 8
+  for (int64_t i = a; i < b2; i += 2) {
+    const int2 v = c2[i >> 1];
+    s += (int64_t)v.x + v.y;
+  }
+  if (b2 < b) s += cnt[b2];
+  // block exclusive scan of the run sums
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t inc = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int64_t base = 0;
+  for (int w = 0; w < wv; ++w) base += wsum[w];
+  int64_t run = base + inc - s;                              // exclusive prefix of this thread's run
+  // 16 loads, then 16 stores: loads and stores share one in-order memory counter, so a load issued
+  // after a store waits for it -- an interleaved loop paid one round trip per tile (50 us)
+  for (int64_t i0 = a; i0 < b; i0 += 16) {
+    int32_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = i0 + k < b ? cnt[i0 + k] : 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (i0 + k < b) {
+        off[i0 + k] = run;
+        run += v[k];
+      }
+  }
+}
+
 int64_t line_index_tiles(int64_t nbytes) { return (nbytes + LI_TILE - 1) / LI_TILE; }
 
 NlOut line_index_pass1_views(const LineIndexWs& W, int64_t nbytes, uint64_t stream) {
@@ -343,16 +391,8 @@ void line_index_dev(const uint8_t* text, int64_t nbytes, const LineIndexWs& W, i
   int32_t* cnt = reinterpret_cast<int32_t*>(W.buf + 3 * W.ntiles_cap);
   int32_t* crf = cnt + W.ntiles_cap;               // the int64 slot region holds 2 x ntiles_cap int32
   uint64_t* nlm = reinterpret_cast<uint64_t*>(W.buf + 4 * W.ntiles_cap);   // LI_THREADS words per tile
-  void* tmp = W.buf + (4 + LI_THREADS) * W.ntiles_cap;
-  size_t tmp_bytes = 0;
-  if (rocprim::exclusive_scan(nullptr, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
-          hipSuccess ||
-      tmp_bytes > W.tmp_bytes)
-    throw std::runtime_error("line_index: scan workspace too small");
   if (!counted) hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nt), dim3(LI_THREADS), 0, st, text, nbytes, cnt, nlm, crf);
-  if (rocprim::exclusive_scan(tmp, tmp_bytes, cnt, off, int64_t(0), (size_t)nt, rocprim::plus<int64_t>(), st) !=
-      hipSuccess)
-    throw std::runtime_error("line_index: rocprim scan failed");
+  hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(LS_THREADS), 0, st, cnt, nt, off);
   hipLaunchKernelGGL(k_nl_lines, dim3((unsigned)((nt + LI_LINES_TPB - 1) / LI_LINES_TPB)), dim3(LI_THREADS), 0, st,
                      text, nbytes, (int64_t)nt, nlm, crf, off, starts, lens, cap,
                      fix_g, fix_end, blk, nblk);

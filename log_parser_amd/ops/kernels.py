@@ -41,7 +41,7 @@ class _LineIndexWs:
     """Per (device, stream) scratch of the line index: tile counts + offsets, "\\r\\n" flags and
     each tile's first line end (k_line_fix), the per-tile newline bitmasks (256 words = 2 KiB per
     16 KiB tile), then the scan scratch. Grow-only; stream order makes reuse safe."""
-    SCAN_TMP = 1 << 20           # bytes of rocprim scan scratch (csrc/bind.cpp passes the same)
+    SCAN_TMP = 1 << 20           # bytes of scan scratch in the workspace layout (csrc/bind.cpp passes the same)
     WORDS_PER_TILE = 4 + 256     # int64 words per tile (csrc/kernels/line_index.hip line_index_dev)
     _all: dict = {}
 
@@ -63,7 +63,7 @@ LINE_BLK_SHIFT = 12
 
 
 def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=None, fused=None):
-    """k_nl_count, rocprim scan, k_nl_lines, k_line_fix (+ k_line_trim): (starts, lens, n_newlines,
+    """k_nl_count, k_tile_scan, k_nl_lines, k_line_fix (+ k_line_trim): (starts, lens, n_newlines,
     last_newline, kept, blk) with ONE host read; blk = the coarse 4 KiB block -> line index.
     ``before_read()`` runs once, after the launches and before that read: work it queues (the
     literal prefilter, which needs no line index) runs on the GPU while the host waits.

@@ -89,6 +89,24 @@ def test_line_index_matches_java_split(gpu_device, seed):
     assert got == ref
 
 
+@pytest.mark.parametrize("mb", [37, 301])
+def test_line_index_large_tile_scan(gpu_device, mb):
+    """Many tiles (2.4k / 19k, an odd count): every thread of the one-workgroup tile scan
+    (k_tile_scan) sums a run of several counts, with a scalar tail -- equal to the host index."""
+    rng = np.random.default_rng(mb)
+    n = mb * (1 << 20) + 12345
+    data = rng.integers(32, 127, size=n, dtype=np.uint8)
+    nl = rng.random(n) < 1 / 90                                  # ~90-byte lines, some empty
+    data[nl] = 10
+    data[rng.random(n) < 1 / 5000] = 13
+    b = data.tobytes()
+    td, tc = _text(gpu_device, b)
+    ls_d, ll_d = K.split_lines(td, len(b))
+    ls_c, ll_c = K.split_lines(tc, len(b))
+    assert ls_d.numel() == ls_c.numel() > 1000
+    assert torch.equal(ls_d.cpu(), ls_c) and torch.equal(ll_d.cpu(), ll_c)
+
+
 @pytest.mark.parametrize("n_pat,seed", [(64, 1), (300, 5)])
 def test_hits_gpu_equal_cpu(gpu_device, n_pat, seed):
     sets, trig = make_library(n_pat, seed=seed)

@@ -571,18 +571,18 @@ PYBIND11_MODULE(_lpnative, m) {
     r["nregs"] = d.nregs;
     r["bytemap"] = vbytes(d.bytemap.data(), d.bytemap.size());
     r["trans"] = vbytes(d.trans.data(), d.trans.size() * 4);
-    r["acc"] = vbytes(d.acc.data(), d.acc.size() * 4);
-    r["fin"] = vbytes(d.fin.data(), d.fin.size() * 4);
+    r["acc"] = vbytes(d.acc.data(), d.acc.size() * 8);     // uint64 masks
+    r["fin"] = vbytes(d.fin.data(), d.fin.size() * 8);
     return r;
   }, py::arg("patterns"), py::arg("max_states") = 4096);
-  m.def("multi_find", [](const std::vector<std::string>& pats, const std::string& line) -> int64_t {
+  m.def("multi_find", [](const std::vector<std::string>& pats, const std::string& line) -> py::object {
     MultiDfa d;
     try {
       d = compile_multi(pats, 1 << 16);
     } catch (const Unsupported&) {
-      return -1;
+      return py::object(py::int_(-1));
     }
-    return multi_find(d, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size());
+    return py::object(py::int_(multi_find(d, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size())));
   });
   py::class_<BtSet>(m, "BtSet")
       .def(py::init<const std::vector<std::string>&>())

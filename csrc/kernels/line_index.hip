@@ -314,52 +314,77 @@ __global__ __launch_bounds__(256) void k_line_trim(const int32_t* __restrict__ l
   if (threadIdx.x == 0) info[2] = 0;
 }
 
-// exclusive prefix of the per-tile '\n' counts (~80k tiles for a 1.3 GB shard) in ONE workgroup:
-// each thread sums a contiguous run of counts (8-byte loads, all in flight), the 1,024 run sums are
-// scanned through the waves' shuffles + LDS, then each thread re-reads its run and writes its
-// offsets. One launch of ~10 us against rocPRIM's look-back scan (an init kernel + the scan,
-// 81 us per step, profiles/r4_c).
+// exclusive prefix of the per-tile '\n' counts (~80k tiles for a 1.3 GB shard) in ONE workgroup,
+// in coalesced chunks of 16,384 counts: each thread loads 16 consecutive counts (the next chunk's are
+// loaded before this chunk is scanned), scans them, the 1,024 thread sums are scanned through the
+// waves' shuffles + LDS, and each thread writes its 16 offsets as 8 16-byte stores. ~10 us against
+// rocPRIM's look-back scan (an init kernel + the scan, 81 us per step, profiles/r4_c).
 constexpr int LS_THREADS = 1024;
+constexpr int LS_PER = 16;
 __global__ __launch_bounds__(LS_THREADS) void k_tile_scan(const int32_t* __restrict__ cnt, int64_t nt,
                                                           int64_t* __restrict__ off) {
-  __shared__ int64_t wsum[LS_THREADS / 64];
-  const int64_t per = (((nt + LS_THREADS - 1) / LS_THREADS) + 1) & ~(int64_t)1;   // even: 8-byte aligned runs
-  const int64_t a = (int64_t)threadIdx.x * per;
-  const int64_t b = a + per < nt ? a + per : nt;
-  int64_t s = 0;
-  const int2* c2 = reinterpret_cast<const int2*>(cnt);      // cnt is 8-byte aligned (int64 workspace)
-  const int64_t b2 = a < b ? a + ((b - a) & ~(int64_t)1) : a;
-#pragma unroll 8
-  for (int64_t i = a; i < b2; i += 2) {
-    const int2 v = c2[i >> 1];
-    s += (int64_t)v.x + v.y;
-  }
-  if (b2 < b) s += cnt[b2];
-  // block exclusive scan of the run sums
+  __shared__ int64_t wsum[2][LS_THREADS / 64];
+  constexpr int64_t CH = (int64_t)LS_THREADS * LS_PER;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int64_t inc = s;
+  const int2* c2 = reinterpret_cast<const int2*>(cnt);        // cnt is 8-byte aligned (int64 workspace)
+  auto load = [&](int64_t base, int32_t (&v)[LS_PER]) {
+    const int64_t i0 = base + (int64_t)threadIdx.x * LS_PER;
+    if (i0 + LS_PER <= nt) {
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t o = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += o;
-  }
-  if (lane == 63) wsum[wv] = inc;
-  __syncthreads();
-  int64_t base = 0;
-  for (int w = 0; w < wv; ++w) base += wsum[w];
-  int64_t run = base + inc - s;                              // exclusive prefix of this thread's run
-  // 16 loads, then 16 stores: loads and stores share one in-order memory counter, so a load issued
-  // after a store waits for it -- an interleaved loop paid one round trip per tile (50 us)
-  for (int64_t i0 = a; i0 < b; i0 += 16) {
-    int32_t v[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = i0 + k < b ? cnt[i0 + k] : 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-      if (i0 + k < b) {
-        off[i0 + k] = run;
-        run += v[k];
+      for (int k = 0; k < LS_PER / 2; ++k) {
+        const int2 x = c2[(i0 >> 1) + k];
+        v[2 * k] = x.x;
+        v[2 * k + 1] = x.y;
       }
+    } else {
+#pragma unroll
+      for (int k = 0; k < LS_PER; ++k) v[k] = i0 + k < nt ? cnt[i0 + k] : 0;
+    }
+  };
+  int32_t cur[LS_PER], nxt[LS_PER];
+  load(0, cur);
+  int64_t carry = 0;
+  for (int64_t base = 0, it = 0; base < nt; base += CH, ++it) {
+    if (base + CH < nt) load(base + CH, nxt);
+    int64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < LS_PER; ++k) s += cur[k];
+    int64_t inc = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    int64_t* ws = wsum[it & 1];                               // alternate: no second barrier per chunk
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    int64_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < LS_THREADS / 64; ++w) {
+      const int64_t x = ws[w];
+      wbase += w < wv ? x : 0;
+      tot += x;
+    }
+    int64_t run = carry + wbase + inc - s;
+    const int64_t i0 = base + (int64_t)threadIdx.x * LS_PER;
+    int64_t o[LS_PER];
+#pragma unroll
+    for (int k = 0; k < LS_PER; ++k) {
+      o[k] = run;
+      run += cur[k];
+    }
+    if (i0 + LS_PER <= nt && ((uintptr_t)off & 15) == 0) {
+      longlong2* o2 = reinterpret_cast<longlong2*>(off + i0);
+#pragma unroll
+      for (int k = 0; k < LS_PER / 2; ++k) o2[k] = make_longlong2(o[2 * k], o[2 * k + 1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < LS_PER; ++k)
+        if (i0 + k < nt) off[i0 + k] = o[k];
+    }
+    carry += tot;
+#pragma unroll
+    for (int k = 0; k < LS_PER; ++k) cur[k] = nxt[k];
   }
 }
 

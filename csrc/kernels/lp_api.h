@@ -99,8 +99,8 @@ struct ScanPass {
   int gm_off[4];          // word offset of group g's [state][ncol] accept masks (same indexing)
   int fin_off[4];         // word offset of group g's [state][EOL, FT] accept masks
   int bm_off;             // word offset of bm4
-  int rid_off;            // word offset of the regex ids (32 per group)
-  int am_off;             // word offset of the u32 accept masks laid out like the LDS rows
+  int rid_off;            // word offset of the regex ids (64 per group)
+  int am_off;             // word offset (even) of the u64 accept masks laid out like the LDS rows
 };
 void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                     const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,

@@ -3,7 +3,7 @@
 // The reference runs every primary regex over every line (AnalysisService.java:89-95). Regexes
 // with a usable literal factor are reached through the literal prefilter; the rest (e.g.
 // "\b[A-Z]{3,}_\d{4}\b", IP:port shapes, "^\s+at ..." frames) must scan the whole text. They are
-// compiled at library load into *scan groups*: up to 32 regexes determinised together into one
+// compiled at library load into *scan groups*: up to 64 regexes determinised together into one
 // multi-regex DFA (jregex.h MultiDfa), so one table walk per byte answers all members. A *pass*
 // holds up to 4 groups walked together.
 //
@@ -16,7 +16,7 @@
 //     States are numbered so that every state from which ANY regex can accept
 //     (on some next byte, at end of line or before a final terminator) comes last: "a match may
 //     have happened" is just max(row offset) >= thr[g] -- one v_max per byte, no mask traffic.
-//   * global (rare path): exact rows of next state ids and, indexed alike, uint32 accept masks
+//   * global (rare path): exact rows of next state ids and, indexed alike, uint64 accept masks
 //     (the regexes accepting BEFORE the byte; the '\n' column carries the end-of-line accepts),
 //     the per-state [EOL, before-final-terminator] masks and the regex ids.
 //
@@ -74,19 +74,22 @@ LP_HD uint32_t scan_state_of(const ScanPass& S, int g, uint32_t row_byte) {
 LP_HD uint32_t scan_step(const ScanPass& S, int g, uint32_t st, uint32_t col) {
   return S.blob[S.gt_off[g] + st * (uint32_t)S.ncol[g] + col];
 }
-LP_HD uint32_t scan_mask(const ScanPass& S, int g, uint32_t st, uint32_t col) {
-  return S.blob[S.gm_off[g] + st * (uint32_t)S.ncol[g] + col];
+// 64-bit accept masks (bit r: member r of the group) stored as (lo, hi) word pairs
+LP_HD uint64_t scan_mask(const ScanPass& S, int g, uint32_t st, uint32_t col) {
+  const uint32_t* p = S.blob + S.gm_off[g] + 2 * (st * (uint32_t)S.ncol[g] + col);
+  return (uint64_t)p[0] | ((uint64_t)p[1] << 32);
 }
-LP_HD uint32_t scan_fin(const ScanPass& S, int g, uint32_t st, int ft) {
-  return S.blob[S.fin_off[g] + 2 * st + ft];
+LP_HD uint64_t scan_fin(const ScanPass& S, int g, uint32_t st, int ft) {
+  const uint32_t* p = S.blob + S.fin_off[g] + 4 * st + 2 * ft;
+  return (uint64_t)p[0] | ((uint64_t)p[1] << 32);
 }
 
 template <typename Emit>
-LP_HD void scan_emit(const ScanPass& S, int g, uint32_t m, int64_t line, Emit&& emit) {
+LP_HD void scan_emit(const ScanPass& S, int g, uint64_t m, int64_t line, Emit&& emit) {
   while (m) {
-    const int r = __builtin_ctz(m);
+    const int r = __builtin_ctzll(m);
     m &= m - 1;
-    emit(((int64_t)S.blob[S.rid_off + 32 * g + r] << 32) | line);
+    emit(((int64_t)S.blob[S.rid_off + 64 * g + r] << 32) | line);
   }
 }
 
@@ -96,7 +99,8 @@ template <typename Emit>
 LP_HD void scan_line_exact(const ScanPass& S, const uint32_t* bm, const uint8_t* s, int n, int64_t line, Emit&& emit) {
   const int ft = n - final_term_len(s, n);
   for (int g = 0; g < S.ngroups; ++g) {
-    uint32_t st = S.init_state[g], acc = 0;
+    uint32_t st = S.init_state[g];
+    uint64_t acc = 0;
     for (int t = 0; t < n; ++t) {
       if (t == ft) acc |= scan_fin(S, g, st, 1);
       const uint32_t col = ((bm[s[t]] >> (8 * g)) & 0xFFu) >> 1;
@@ -149,7 +153,7 @@ __device__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, const ui
   const int64_t first = p0 > p_lo ? p0 : p_lo;
   while (l + 1 < x1 && line_start[l + 1] <= first) ++l;
   if (p0 <= p_lo) st = S.init_state[g];
-  uint32_t lacc = 0;
+  uint64_t lacc = 0;
   for (int j = 0; j < 16; ++j) {
     const int64_t pos = p0 + j;
     if (pos < p_lo || pos >= p_end) continue;
@@ -168,7 +172,7 @@ __device__ void scan_block_exact(const ScanPass& S, const uint32_t* bm, const ui
 }
 
 // exact re-walk of one 16-byte block through the LDS rows (the same transitions as the hot
-// walk) with each transition's accept mask from the global mask table laid out like the rows:
+// walk) with each transition's accept mask from the global u64 mask table laid out like the rows:
 // the 16 mask loads depend only on the LDS chain, so they are all in flight together (the
 // exact-table walk above is a chain of 16 dependent global loads). xr = group g's row at p0;
 // positions outside [p_lo, p_end) are walked but not attributed, as in the hot walk.
@@ -177,30 +181,31 @@ __device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32
                                                  int64_t p_lo, int64_t p_end, int64_t x0, int64_t x1,
                                                  const int64_t* __restrict__ line_start, int g, uint32_t xr,
                                                  Emit&& emit) {
-  const uint32_t* __restrict__ am = S.blob + S.am_off;
+  const uint64_t* __restrict__ am = reinterpret_cast<const uint64_t*>(S.blob + S.am_off);   // am_off even
   // in-range positions of the block; a run holds <= SCAN_RUN lines, so an in-range byte belongs
   // to line l0 + k, k = in-range '\n's before it (0..3): per-line masks accumulate branch-free
   const int lo = p_lo > p0 ? (int)(p_lo - p0) : 0;
   const int hi = p_end - p0 < 16 ? (int)(p_end - p0) : 16;
   const uint32_t inr = hi > lo ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u;
-  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, k = 0;
+  uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  uint32_t k = 0;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
     if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;
     const uint32_t b = (lds_ld32(c * 4) >> (8 * g)) & 0xFFu;
-    const uint32_t m = ((inr >> j) & 1u) ? am[(xr + b) >> 1] : 0u;
-    a0 |= k == 0 ? m : 0u;
-    a1 |= k == 1 ? m : 0u;
-    a2 |= k == 2 ? m : 0u;
-    a3 |= k == 3 ? m : 0u;
+    const uint64_t m = ((inr >> j) & 1u) ? am[(xr + b) >> 1] : 0ull;
+    a0 |= k == 0 ? m : 0ull;
+    a1 |= k == 1 ? m : 0ull;
+    a2 |= k == 2 ? m : 0ull;
+    a3 |= k == 3 ? m : 0ull;
     k += (b == 2u && ((inr >> j) & 1u)) ? 1u : 0u;     // column 1 = '\n': the line ends here
     xr = lds_ld16(xr + b);
   }
   int64_t l = x0;
   const int64_t first = p0 > p_lo ? p0 : p_lo;
   while (l + 1 < x1 && line_start[l + 1] <= first) ++l;
-  const uint32_t acc[4] = {a0, a1, a2, a3};
+  const uint64_t acc[4] = {a0, a1, a2, a3};
 #pragma unroll
   for (int q = 0; q < 4; ++q)
     if (acc[q]) scan_emit(S, g, acc[q], l + q < x1 ? l + q : x1 - 1, emit);
@@ -292,19 +297,25 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
   const bool at_zero = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)sm == 0u;
   const int64_t nruns = (nlines + run_len - 1) / run_len;
   const int64_t stride = (int64_t)gridDim.x * THREADS;
-  for (int64_t run = (int64_t)blockIdx.x * THREADS + threadIdx.x; run < nruns; run += stride) {
-    const int64_t x0 = run * run_len;
-    const int64_t x1 = x0 + run_len < nlines ? x0 + run_len : nlines;
-    // stream walk preconditions: "\n" / "\r\n" separators (after every line of the run,
-    // the last one included), the run starts right after a '\n', no content ends in a terminator
-    bool fast = true, crlf = false;
-    int64_t st_next = line_start[x0];
-    const int64_t p_lo = st_next;
-    int64_t p_end = 0;
-    for (int64_t x = x0; x < x1; ++x) {
+  // a run's stream-walk preconditions: "\n" / "\r\n" separators (after every line of the run, the
+  // last one included), the run starts right after a '\n', no content ends in a terminator
+  struct Run {
+    int64_t x0, x1, p_lo, p_end;
+    bool fast, crlf;
+  };
+  auto prep = [&](int64_t run) {
+    Run R;
+    R.x0 = run * run_len;
+    R.x1 = R.x0 + run_len < nlines ? R.x0 + run_len : nlines;
+    R.fast = at_zero;
+    R.crlf = false;
+    int64_t st_next = line_start[R.x0];
+    R.p_lo = st_next;
+    R.p_end = 0;
+    for (int64_t x = R.x0; x < R.x1; ++x) {
       const int64_t st = st_next;
       const int n = line_len[x];
-      if (ends_in_terminator(text, st, n)) fast = false;
+      if (ends_in_terminator(text, st, n)) R.fast = false;
       int64_t sep;
       if (x + 1 < nlines) {
         st_next = line_start[x + 1];
@@ -313,21 +324,23 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
         const int64_t e = st + n;
         sep = (e < nbytes && text[e] == '\n') ? 1 : (e + 1 < nbytes && text[e] == '\r' && text[e + 1] == '\n') ? 2 : 0;
       }
-      if (sep == 2) crlf = true;
-      else if (sep != 1) fast = false;
-      p_end = st + n + sep;                      // after the last line's separator
+      if (sep == 2) R.crlf = true;
+      else if (sep != 1) R.fast = false;
+      R.p_end = st + n + sep;                    // after the last line's separator
     }
-    if (p_lo > 0 && text[p_lo - 1] != '\n') fast = false;   // e.g. a document boundary in a batch
-    if (!at_zero) fast = false;
-    if (!fast) {     // rare: exact per-line walks
-      for (int64_t x = x0; x < x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
-      continue;
+    if (R.p_lo > 0 && text[R.p_lo - 1] != '\n') R.fast = false;   // e.g. a document boundary in a batch
+    return R;
+  };
+  auto walk_one = [&](const Run& R) {
+    if (!R.fast) {     // rare: exact per-line walks
+      for (int64_t x = R.x0; x < R.x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
+    } else if (R.crlf) {
+      scan_run_fast<G, true, REP>(sm, S, text, R.p_lo, R.p_end, R.x0, R.x1, line_start, bm_rep, emit);
+    } else {
+      scan_run_fast<G, false, REP>(sm, S, text, R.p_lo, R.p_end, R.x0, R.x1, line_start, bm_rep, emit);
     }
-    if (crlf)
-      scan_run_fast<G, true, REP>(sm, S, text, p_lo, p_end, x0, x1, line_start, bm_rep, emit);
-    else
-      scan_run_fast<G, false, REP>(sm, S, text, p_lo, p_end, x0, x1, line_start, bm_rep, emit);
-  }
+  };
+  for (int64_t run = (int64_t)blockIdx.x * THREADS + threadIdx.x; run < nruns; run += stride) walk_one(prep(run));
 }
 
 void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int32_t* line_len, int64_t nlines,

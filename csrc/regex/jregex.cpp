@@ -1529,9 +1529,9 @@ struct Member {
   const Nfa* nfa = nullptr;
 };
 
-uint32_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t>& A, int prev, int next) {
+uint64_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t>& A, int prev, int next) {
   const uint32_t bit = 1u << ctx_index(prev, next);
-  uint32_t m = 0;
+  uint64_t m = 0;
   for (size_t r = 0; r < M.size(); ++r) {
     const Nfa& n = *M[r].nfa;
     bool ok = (n.nullable & bit) != 0;
@@ -1539,7 +1539,7 @@ uint32_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t
       const int p = M[r].off + n.last[i].to;
       ok = ((A[p >> 6] >> (p & 63)) & 1) && (n.last[i].cond & bit);
     }
-    if (ok) m |= 1u << r;
+    if (ok) m |= 1ull << r;
   }
   return m;
 }
@@ -1547,7 +1547,7 @@ uint32_t member_accepts(const std::vector<Member>& M, const std::vector<uint64_t
 }  // namespace
 
 MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states) {
-  if (patterns.empty() || patterns.size() > (size_t)MULTI_MAX_REGS) throw Unsupported("multi-DFA: 1..32 regexes");
+  if (patterns.empty() || patterns.size() > (size_t)MULTI_MAX_REGS) throw Unsupported("multi-DFA: 1..64 regexes");
   std::vector<Compiled> comp;
   comp.reserve(patterns.size());
   bool wordb = false;
@@ -1622,14 +1622,15 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
   std::vector<uint64_t> init(nw, 0);
   init[nw - 1] = P_BOS;
   intern(init);
-  std::vector<uint32_t> rows, racc, fin;
+  std::vector<uint32_t> rows;
+  std::vector<uint64_t> racc, fin;
   std::vector<uint64_t> U(nw, 0), B(nw, 0);
   for (size_t si = 0; si < states.size(); ++si) {
     const std::vector<uint64_t> A = states[si];
     const int prev = (int)A[nw - 1];
     fin.push_back(member_accepts(M, A, prev, N_EOS));
     fin.push_back(member_accepts(M, A, prev, N_FT));
-    uint32_t acc_k[6];
+    uint64_t acc_k[6];
     for (int nk = 0; nk < 6; ++nk) acc_k[nk] = member_accepts(M, A, prev, nk);
     T.ungated(A, U);
     for (int k = 0; k < d.nclasses; ++k) {
@@ -1656,10 +1657,11 @@ MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states)
   return d;
 }
 
-uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n) {
+uint64_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n) {
   int64_t ft = n - final_terminator_len(s, n);
   if (ft == n) ft = -1;
-  uint32_t st = 1, acc = 0;
+  uint32_t st = 1;
+  uint64_t acc = 0;
   for (int64_t t = 0; t < n; ++t) {
     if (t == ft) acc |= d.fin[2 * st + 1];
     const size_t i = (size_t)st * d.nclasses + d.bytemap[s[t]];

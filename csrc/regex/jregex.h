@@ -121,18 +121,18 @@ Compiled compile(const std::string& pattern, int max_dfa_states, int max_positio
 //   trans[s * nclasses + cls] = next state (< 65536), acc[same] = accept mask of that transition
 //   fin[2 s] = regexes accepting at end of line, fin[2 s + 1] = before a final line terminator
 // State 0 = DEAD (every member anchored and failed), state 1 = start of line.
-constexpr int MULTI_MAX_REGS = 32;
+constexpr int MULTI_MAX_REGS = 64;
 struct MultiDfa {
   int nstates = 0, nclasses = 0, nregs = 0;
   std::vector<uint8_t> bytemap;
   std::vector<uint32_t> trans;
-  std::vector<uint32_t> acc;
-  std::vector<uint32_t> fin;
+  std::vector<uint64_t> acc;   // bit r: member r (64-bit masks: up to 64 members per walk)
+  std::vector<uint64_t> fin;
 };
 // throws Unsupported (state limit, > MULTI_MAX_REGS, a member without a byte automaton)
 MultiDfa compile_multi(const std::vector<std::string>& patterns, int max_states);
 // bit r set <=> patterns[r] finds a match in s[0..n) (host walk; the device kernel is k_scan_multi)
-uint32_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n);
+uint64_t multi_find(const MultiDfa& d, const uint8_t* s, int64_t n);
 
 // Host-side exact match of one line with a compiled DFA (CPU backend + tests).
 bool dfa_find(const Dfa& d, const uint8_t* s, int64_t n);

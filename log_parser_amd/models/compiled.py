@@ -465,7 +465,8 @@ class CompiledLibrary:
                           if self.host_local[r] >= 0]
 
     # multi-regex DFA scan groups (csrc/kernels/scan_multi.hip)
-    SCAN_GROUP_REGS = 32            # members per multi-regex DFA (32-bit accept masks)
+    SCAN_GROUP_REGS = 32            # members per multi-regex DFA (masks hold 64; one 46-member group
+                                    # walked no faster than two groups in the bench step, profiles/r4_e)
     SCAN_GROUP_BYTES = 24 << 10     # LDS bytes of one group's uint16 transition rows
     SCAN_PASS_ROWS = 48 << 10       # LDS bytes of one pass's rows (+ 1 KiB bm4)
     SCAN_MAX_STATES = 4096
@@ -533,8 +534,8 @@ class CompiledLibrary:
         for g, (regs, d) in enumerate(groups):
             ns, nc = d["nstates"], d["nclasses"]
             t = np.frombuffer(d["trans"], np.uint32).reshape(ns, nc)
-            a = np.frombuffer(d["acc"], np.uint32).reshape(ns, nc)
-            fin = np.frombuffer(d["fin"], np.uint32).reshape(ns, 2)
+            a = np.frombuffer(d["acc"], np.uint64).reshape(ns, nc)
+            fin = np.frombuffer(d["fin"], np.uint64).reshape(ns, 2)
             accepting = (a != 0).any(axis=1) | (fin != 0).any(axis=1)
             order = np.concatenate([np.flatnonzero(~accepting), np.flatnonzero(accepting)])
             new_of = np.empty(ns, np.uint32)
@@ -547,12 +548,12 @@ class CompiledLibrary:
             ex[:, 0] = np.arange(ns, dtype=np.uint32)                         # hold
             ex[:, 1] = np.uint32(init_new)                                    # '\n': restart ...
             ex[:, 2:] = new_of[t[order]]
-            em = np.zeros((ns, ncol), np.uint32)
+            em = np.zeros((ns, ncol), np.uint64)
             em[:, 1] = fin[order, 0]                                          # ... + EOL accepts
             em[:, 2:] = a[order]
             exact.append(ex.reshape(-1))
-            emask.append(em.reshape(-1))
-            fins.append(fin[order].reshape(-1))
+            emask.append(em.reshape(-1).view(np.uint32))              # u64 masks as (lo, hi) words
+            fins.append(np.ascontiguousarray(fin[order]).reshape(-1).view(np.uint32))
             # LDS rows: byte offset of the next state's row
             rowb = (2 * (base + np.arange(ns, dtype=np.int64) * stride)).astype(np.int64)
             r16 = np.zeros((ns, stride), np.uint16)
@@ -586,25 +587,28 @@ class CompiledLibrary:
             fin_off[g] = off
             parts.append(fins[g])
             off += fins[g].size
-        G = 32                                   # regex-id slots per group (scan_multi.hip scan_emit)
+        G = 64                                   # regex-id slots per group (scan_multi.hip scan_emit)
         rid = np.zeros(G * 4, np.uint32)
         for g, (regs, _) in enumerate(groups):
             rid[G * g:G * g + len(regs)] = regs
         rid_off = off
         parts.append(rid)
         off += rid.size
-        # accept masks laid out like the LDS rows (u16 entry i of the LDS blob <-> u32 mask i): the
+        # accept masks laid out like the LDS rows (u16 entry i of the LDS blob <-> u64 mask i): the
         # device's exact re-walk follows the LDS rows and loads each transition's mask with an
         # address known from the LDS chain -- 16 independent global loads per block instead of a
         # chain of 16 dependent exact-row loads
-        am = np.zeros(2 * lds_words, np.uint32)
+        am = np.zeros(2 * lds_words, np.uint64)
         for g, (regs, d) in enumerate(groups):
             ns, ncol, stride = d["nstates"], meta["ncol"][g], meta["stride"][g]
             b0 = meta["row_base"][g] // 2
             idx = b0 + np.arange(ns, dtype=np.int64)[:, None] * stride + np.arange(ncol, dtype=np.int64)[None, :]
-            am[idx] = emask[g].reshape(ns, ncol)
+            am[idx] = emask[g].view(np.uint64).reshape(ns, ncol)
+        if off % 2:                              # 8-byte aligned u64 view on the device
+            parts.append(np.zeros(1, np.uint32))
+            off += 1
         am_off = off
-        parts.append(am)
+        parts.append(am.view(np.uint32))
         blob = np.concatenate(parts)
         return dict(blob=blob, lds_words=lds_words, ngroups=len(groups), gt_off=tuple(gt_off),
                     fin_off=tuple(fin_off), gm_off=tuple(gm_off), bm_off=0, rid_off=rid_off, am_off=am_off,

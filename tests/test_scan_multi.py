@@ -1,6 +1,6 @@
 """Multi-regex DFA scan groups (jregex MultiDfa + csrc/kernels/scan_multi.hip).
 
-Literal-free regexes are determinised together (up to 32 per DFA) and walked over every line.
+Literal-free regexes are determinised together (up to 64 per DFA) and walked over every line.
 Each member's find() must equal its own single-regex DFA (itself fuzzed against the javacompat
 oracle in test_regex.py), on every line shape: anchors, word boundaries, '$' before a final
 '\\r', UTF-8. The device kernel must equal its host twin; a realistic library must give the same
@@ -48,7 +48,7 @@ def _rand_line(rng):
 def test_multi_dfa_equals_single_dfas(seed):
     rng = random.Random(seed)
     pats = []
-    while len(pats) < rng.randint(1, 32):
+    while len(pats) < rng.randint(1, 64):
         p = _rand_regex(rng)
         if N.compile_regex(p)["kind"] == 0 and p not in pats:
             pats.append(p)
@@ -62,7 +62,10 @@ def test_multi_dfa_equals_single_dfas(seed):
 
 
 def test_multi_dfa_limits():
-    assert N.compile_multi([r"a"] * 33, 4096) is None                  # > 32 members
+    assert N.compile_multi([r"a"] * 65, 4096) is None                  # > 64 members
+    d = N.compile_multi([rf"\bq{i}x" for i in range(64)], 1 << 16)     # 64 members: 64-bit masks
+    assert d is not None and d["nregs"] == 64
+    assert N.multi_find([rf"\bq{i}x" for i in range(64)], "a q63x b q0x") == (1 << 63) | 1
     assert N.compile_multi([r"(a)\1"], 4096) is None                   # not an automaton regex
     assert N.compile_multi([r"(a|b)*a(a|b){12}"], 256) is None        # state limit
     assert N.multi_find([r"^\s+at\s", r"x$", r"\bK\d{2}\b"], "\tat K42 x\r") == 0b111

@@ -1,7 +1,7 @@
 # GPU-box validation session. Logs under gpurun_out/. Steps (default: all, in this order):
 #   tests   the regex / serving / MFMA GPU tests
 #   scantest  the literal-free scan kernel's GPU tests (bulk + request variants, CRLF) and the kernel tests
-#   scan    scan-group A/B (16 vs 32 members per multi-regex DFA)
+#   scan    scan-group A/B (32 vs 64 members per multi-regex DFA)
 #   nfa     MFMA vs BPG A/B per regex shape (tools/nfa_ab.py)
 #   bench   bench.py (headline, 1 GPU)
 #   http    config 5 over HTTP: 1 and 2 serving processes (stage timelines), and the front end alone
@@ -32,8 +32,8 @@ for s in $steps; do
       run scantest 600 python -u -m pytest tests/test_scan_multi.py tests/test_gpu.py -m gpu -x -q --timeout 300 \
         --timeout-method thread ;;
     scan)
-      run scan16 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 16
-      run scan32 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 32 ;;
+      run scan32 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 32 --lines 12500000
+      run scan64 300 python -u tools/scan_ab.py --regexes 46 --engine dfa --group-regs 64 --lines 12500000 ;;
     nfa)
       run nfa_ab 400 python -u tools/nfa_ab.py --lines 1000000 ;;
     bench)

@@ -296,7 +296,7 @@ def mode_concurrent_http(args):
     byte. One untimed burst warms the server; the second is reported."""
     from log_parser_amd.native import N
     from log_parser_amd.serve.__main__ import raise_fd_limit
-    from log_parser_amd.utils.numa import cpu_budget
+    from log_parser_amd.utils.numa import cgroup_throttling, cpu_budget, cpu_limits
     from log_parser_amd.utils.restbench import ServerProcess, collect_stages, stage_breakdown, write_library
     from log_parser_amd.utils.synth import realistic_library
     n = args.requests
@@ -329,9 +329,12 @@ def mode_concurrent_http(args):
         N.http_burst("127.0.0.1", srv.port, msgs, idx[:min(n, 2000)], 300.0, args.client_threads)  # warm-up
         workers = max(args.processes, 1)
         st0 = collect_stages(srv.port, workers)
+        thr0 = cgroup_throttling()
         cpu0, cli0 = srv.cpu_seconds(), time.process_time()
         lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0, args.client_threads)
         cpu_srv, cpu_cli = srv.cpu_seconds() - cpu0, time.process_time() - cli0
+        thr1 = cgroup_throttling()
+        throttle = {k: round(thr1[k] - thr0[k], 3) for k in thr1} if thr0 and thr1 else {}
         st1 = collect_stages(srv.port, workers)
         breakdown = stage_breakdown(st0, st1, wall)
         if args.timeline:           # per process: stage intervals of the timed burst, ms from its start
@@ -360,7 +363,9 @@ def mode_concurrent_http(args):
                       # CPUs busy during the burst (server processes / the load generator in this
                       # process): against the host's CPU budget, the measure of a host-bound burst
                       "cpus_busy": {"server": round(cpu_srv / wall, 2), "client": round(cpu_cli / wall, 2),
-                                    "budget": cpu_budget()},
+                                    "budget": cpu_budget(), **cpu_limits()},
+                      # CFS quota throttling during the burst (cgroup cpu.stat deltas)
+                      "cgroup_throttling": throttle,
                       "transport": "native HTTP/1.1 front end, one keep-alive connection per request, 127.0.0.1"}))
 
 

@@ -75,6 +75,36 @@ def bind_to_gpu_numa(index: int) -> Optional[Set[int]]:
     return cpus
 
 
+def cpu_limits() -> dict:
+    """The two limits behind ``cpu_budget``: the affinity set and the cgroup CPU quota (None: none)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "quota_cpus": quota}
+
+
+def cgroup_throttling() -> dict:
+    """CFS bandwidth throttling of this cgroup so far (cgroup v2 ``cpu.stat``, v1 ``cpu/cpu.stat``):
+    periods in which the group ran out of quota and the time its threads were held off -- a burst
+    that runs more threads than the quota stalls every thread for the rest of each period."""
+    for path, scale in (("/sys/fs/cgroup/cpu.stat", 1e-3), ("/sys/fs/cgroup/cpu/cpu.stat", 1e-6)):
+        try:
+            with open(path) as f:
+                kv = dict(line.split()[:2] for line in f if line.strip())
+        except (OSError, ValueError):
+            continue
+        t = kv.get("throttled_usec", kv.get("throttled_time"))
+        return {"periods": int(kv.get("nr_periods", 0)), "throttled_periods": int(kv.get("nr_throttled", 0)),
+                "throttled_ms": float(t) * scale if t is not None else 0.0}
+    return {}
+
+
 def cpu_budget() -> int:
     """CPUs this process can actually use: its affinity set, capped by a cgroup CPU quota
     (``cpu.max``, v2, or ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``, v1) -- a container's

@@ -1,5 +1,5 @@
 """Host-code sanitizer run: the regex compiler and the threaded batch packer under
-ASan+UBSan and TSan (tools/sanitize_host.sh, csrc/tools/selftest.cpp). CPU only."""
+ASan+UBSan and TSan (tools/sanitize_host.sh, tools/native/selftest.cpp). CPU only."""
 import os
 import shutil
 import subprocess

@@ -1,4 +1,4 @@
-"""Dump real context-DFA tables + a covered-line sample for csrc/tools/feat_probe.hip, then run it."""
+"""Dump real context-DFA tables + a covered-line sample for tools/native/feat_probe.hip, then run it."""
 import os
 import subprocess
 import sys

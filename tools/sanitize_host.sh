@@ -5,7 +5,7 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 mkdir -p build/sanitize
-SRC="csrc/tools/selftest.cpp csrc/regex/jregex.cpp csrc/io/docs.cpp csrc/io/json_in.cpp csrc/io/http_server.cpp"
+SRC="tools/native/selftest.cpp csrc/regex/jregex.cpp csrc/io/docs.cpp csrc/io/json_in.cpp csrc/io/http_server.cpp"
 CXX=${CXX:-g++}
 $CXX -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined \
   -pthread -Icsrc $SRC -o build/sanitize/selftest_asan

@@ -304,6 +304,12 @@ def mode_concurrent_http(args):
         raise SystemExit(f"open-file limit too low for {n} connections")
     sets, trig = realistic_library(1000, seed=7)
     dev = "cpu" if args.device == "cpu" else ("cuda:0" if torch.cuda.is_available() else "cpu")
+    if dev != "cpu":
+        # the load generator on the GPU's socket, where the server binds itself (serve/__main__.py):
+        # loopback traffic then stays on one socket (unbound, its threads landed on either socket of
+        # the 256-CPU host and the burst rate halved in about half of the runs, profiles/r4_d)
+        from log_parser_amd.utils.numa import bind_to_gpu_numa
+        bind_to_gpu_numa(0)
     extra = [f"-Dengine.serve-devices={','.join([dev] * args.engines)}"] if args.engines > 1 else []
     if args.processes > 1:          # serving processes sharing one window (serve/procs.py)
         extra = [f"-Dserver.processes={args.processes}"]
@@ -330,11 +336,16 @@ def mode_concurrent_http(args):
         workers = max(args.processes, 1)
         st0 = collect_stages(srv.port, workers)
         thr0 = cgroup_throttling()
+        ss0 = srv.sched_ns()
         cpu0, cli0 = srv.cpu_seconds(), time.process_time()
         lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0, args.client_threads)
         cpu_srv, cpu_cli = srv.cpu_seconds() - cpu0, time.process_time() - cli0
+        ss1 = srv.sched_ns()
         thr1 = cgroup_throttling()
         throttle = {k: round(thr1[k] - thr0[k], 3) for k in thr1} if thr0 and thr1 else {}
+        # server thread-seconds on a CPU vs runnable-but-waiting for one during the burst (schedstat;
+        # the load generator's threads exit with the burst, so only the server is counted)
+        sched = {"server_run_s": round((ss1[0] - ss0[0]) / 1e9, 3), "server_wait_s": round((ss1[1] - ss0[1]) / 1e9, 3)}
         st1 = collect_stages(srv.port, workers)
         breakdown = stage_breakdown(st0, st1, wall)
         if args.timeline:           # per process: stage intervals of the timed burst, ms from its start
@@ -366,6 +377,7 @@ def mode_concurrent_http(args):
                                     "budget": cpu_budget(), **cpu_limits()},
                       # CFS quota throttling during the burst (cgroup cpu.stat deltas)
                       "cgroup_throttling": throttle,
+                      "sched": sched,
                       "transport": "native HTTP/1.1 front end, one keep-alive connection per request, 127.0.0.1"}))
 
 

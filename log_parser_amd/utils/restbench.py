@@ -83,6 +83,25 @@ class RawClient:
         self.sock.close()
 
 
+def sched_ns(pids):
+    """(run ns, runqueue-wait ns) summed over every thread of ``pids`` (``/proc/<pid>/task/*/schedstat``)."""
+    run = wait = 0
+    for pid in pids:
+        try:
+            tids = os.listdir(f"/proc/{pid}/task")
+        except OSError:
+            continue
+        for t in tids:
+            try:
+                with open(f"/proc/{pid}/task/{t}/schedstat") as f:
+                    a, b = f.read().split()[:2]
+                run += int(a)
+                wait += int(b)
+            except (OSError, ValueError):
+                pass
+    return run, wait
+
+
 class ServerProcess:
     def __init__(self, pattern_dir: str, device: str, http: str = "native", extra: Sequence[str] = (),
                  log_path: Optional[str] = None, env: Optional[dict] = None):
@@ -163,15 +182,25 @@ class ServerProcess:
                 rc.close()
         return lat
 
-    def cpu_seconds(self) -> float:
-        """User + system CPU seconds of the server and its serving processes so far (/proc)."""
-        tck = os.sysconf("SC_CLK_TCK")
+    def _pids(self):
         pids = [self.proc.pid]
         try:                                      # the supervisor's workers (server.processes)
             with open(f"/proc/{self.proc.pid}/task/{self.proc.pid}/children") as f:
                 pids += [int(x) for x in f.read().split()]
         except OSError:
             pass
+        return pids
+
+    def sched_ns(self):
+        """(ns on a CPU, ns runnable but waiting for one) summed over every thread of the server's
+        processes (``/proc/<pid>/task/*/schedstat``): the wait is CPU contention -- threads that
+        could run and did not."""
+        return sched_ns(self._pids())
+
+    def cpu_seconds(self) -> float:
+        """User + system CPU seconds of the server and its serving processes so far (/proc)."""
+        tck = os.sysconf("SC_CLK_TCK")
+        pids = self._pids()
         tot = 0.0
         for pid in pids:
             try:

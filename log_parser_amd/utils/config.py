@@ -85,8 +85,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "engine.batch.max-requests": (2048, int),
     "engine.batch.max-bytes": (256 << 20, int),
     # serving: size the pinned batch stages for this many bytes at start-up (capped by max-bytes;
-    # 0 = grow on demand): a burst's first large batches then pay no pinned allocation
-    "engine.batch.prewarm-bytes": (128 << 20, int),
+    # 0 = grow on demand). Default = max-bytes: no batch ever grows a stage. A growth pins a new
+    # buffer (~30 ms for 200+ MB) while holding the GIL, which stalls every Python stage of the
+    # pipeline; in the config-5 burst the first 1,800-2,048-request batches hit it (profiles/r4_d)
+    "engine.batch.prewarm-bytes": (256 << 20, int),
     # extra wait for more requests after the first one; 0 = greedy continuous batching (a batch
     # forms from whatever queued while the previous one ran; an idle server answers at once)
     "engine.batch.max-wait-ms": (0.0, float),

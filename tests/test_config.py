@@ -49,3 +49,21 @@ def test_registered_empty_falls_back_on_cpu():
     from log_parser_amd.utils.hostmem import registered_empty
     t = registered_empty(4096)
     assert t.numel() == 4096 and t.dtype == torch.uint8 and t.device.type == "cpu"
+
+
+def test_cpu_limits_and_sched_counters():
+    """The config-5 bench's host accounting: affinity / quota limits, cgroup throttling counters
+    (empty when the cgroup exposes none) and per-thread run / runqueue-wait nanoseconds."""
+    import os
+    from log_parser_amd.utils import numa
+    from log_parser_amd.utils.restbench import sched_ns
+    lim = numa.cpu_limits()
+    assert lim["affinity"] >= 1 and (lim["quota_cpus"] is None or lim["quota_cpus"] > 0)
+    assert numa.cpu_budget() <= lim["affinity"]
+    thr = numa.cgroup_throttling()
+    assert thr == {} or set(thr) == {"periods", "throttled_periods", "throttled_ms"}
+    run, wait = sched_ns([os.getpid()])
+    sum(i * i for i in range(200_000))                # some CPU time on this thread
+    run2, wait2 = sched_ns([os.getpid()])
+    assert run2 >= run >= 0 and wait2 >= wait >= 0
+    assert sched_ns([2 ** 22 + 12345]) == (0, 0)       # no such process

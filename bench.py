@@ -61,6 +61,8 @@ def parse():
                     help="extra environment of the /parse server process only (A/B knob, repeatable)")
     ap.add_argument("--torch-trace", default="", help="after timing, run one step under torch.profiler -> chrome trace")
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
+    ap.add_argument("--pf-verify-lanes", type=int, default=0, choices=[0, 1, 2, 4, 16],
+                    help="A/B: lanes per gram hit in the bulk literal verify (0: the kernel's default)")
     ap.add_argument("--d2h-stream", default="copy", choices=["copy", "compute"],
                     help="stream of the per-step event D2H (diagnostic A/B)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
@@ -156,6 +158,9 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
             dist.barrier()
         assert dist.get_world_size() == world
 
+    if args.pf_verify_lanes:
+        from log_parser_amd.native import N
+        N.set_pf_verify_lanes(args.pf_verify_lanes)
     params = ScoringParams()
     lib = CompiledLibrary(sets, params)
     cfg = Config.load(overrides={"engine.device": str(device)})

@@ -10,6 +10,8 @@ namespace lp {
 
 // worker threads of the host twins (CPU backend)
 void set_host_threads(int n);
+// lanes per gram hit of the bulk literal verify (k_pf_verify; A/B knob, default 4)
+void set_pf_verify_lanes(int n);
 // line-index pass 1 folded into the bulk prefilter (line_index.hip k_nl_count's outputs): per 16 KiB
 // tile the '\n' count and the "\r\n" flag (both zeroed by the caller), per 64 bytes a '\n' bitmask
 struct NlOut {

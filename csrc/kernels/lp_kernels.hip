@@ -488,20 +488,27 @@ void prefilter_dev(const uint8_t* text, int64_t nbytes, const PfTables& T, const
   LP_CHECK(hipGetLastError());
 }
 
+static int g_pv_lanes_bulk = 4;
+void set_pf_verify_lanes(int n) { g_pv_lanes_bulk = (n == 1 || n == 2 || n == 4 || n == 16) ? n : 4; }
+
 void pf_verify_dev(const int64_t* ghits, int64_t n, const uint8_t* text, int64_t nbytes, const PfTables& T,
                    const int64_t* line_start, int64_t nlines, const int32_t* blk_line, int64_t* cand, int64_t cap,
                    unsigned long long* count, uint64_t stream, const unsigned long long* dn, int max_grid) {
   if (n <= 0) return;
   // with a device-side count the grid is sized for the buffer but capped (grid-stride loop)
-  const int lanes = nbytes >= (int64_t(64) << 20) ? 4 : 16;
+  const int lanes = nbytes >= (int64_t(64) << 20) ? g_pv_lanes_bulk : 16;
   const int64_t need = (n + 256 / lanes - 1) / (256 / lanes);   // blocks for one pass over n hits
   const int g = dn ? (int)std::min<int64_t>(need, std::max(1, max_grid)) : (int)std::max<int64_t>(1, need);
-  if (lanes == 4)
-    hipLaunchKernelGGL(k_pf_verify<4>, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
-                       line_start, nlines, blk_line, cand, cap, count);
-  else
-    hipLaunchKernelGGL(k_pf_verify<16>, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T,
-                       line_start, nlines, blk_line, cand, cap, count);
+#define LP_PV(L)                                                                                                  \
+  hipLaunchKernelGGL(k_pf_verify<L>, dim3(g), dim3(256), 0, as_stream(stream), ghits, n, dn, text, nbytes, T, \
+                     line_start, nlines, blk_line, cand, cap, count)
+  switch (lanes) {
+    case 1: LP_PV(1); break;
+    case 2: LP_PV(2); break;
+    case 4: LP_PV(4); break;
+    default: LP_PV(16); break;
+  }
+#undef LP_PV
   LP_CHECK(hipGetLastError());
 }
 

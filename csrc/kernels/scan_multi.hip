@@ -309,6 +309,31 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
     R.x1 = R.x0 + run_len < nlines ? R.x0 + run_len : nlines;
     R.fast = at_zero;
     R.crlf = false;
+    if (run_len == SCAN_RUN && R.x0 + SCAN_RUN < nlines) {
+      // a full run that is not the text's end (all but the last run): the 5 starts and 4 lengths,
+      // then the 8 terminator words and the byte before the run, each batch loaded in one round
+      // trip (the loop below waits for every line's loads in turn)
+      int64_t s5[SCAN_RUN + 1];
+      int n4[SCAN_RUN];
+#pragma unroll
+      for (int i = 0; i <= SCAN_RUN; ++i) s5[i] = line_start[R.x0 + i];
+#pragma unroll
+      for (int i = 0; i < SCAN_RUN; ++i) n4[i] = line_len[R.x0 + i];
+      bool term = false;
+      int64_t sep = 1;
+#pragma unroll
+      for (int i = 0; i < SCAN_RUN; ++i) {
+        term |= ends_in_terminator(text, s5[i], n4[i]);
+        sep = s5[i + 1] - s5[i] - n4[i];
+        if (sep == 2) R.crlf = true;
+        else if (sep != 1) R.fast = false;
+      }
+      if (term) R.fast = false;
+      R.p_lo = s5[0];
+      R.p_end = s5[SCAN_RUN - 1] + n4[SCAN_RUN - 1] + sep;
+      if (R.p_lo > 0 && text[R.p_lo - 1] != '\n') R.fast = false;
+      return R;
+    }
     int64_t st_next = line_start[R.x0];
     R.p_lo = st_next;
     R.p_end = 0;

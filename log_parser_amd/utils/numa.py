@@ -78,15 +78,26 @@ def bind_to_gpu_numa(index: int) -> Optional[Set[int]]:
 def cpu_limits() -> dict:
     """The two limits behind ``cpu_budget``: the affinity set and the cgroup CPU quota (None: none)."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    quota = None
+    return {"affinity": aff, "quota_cpus": _cgroup_quota()}
+
+
+def _cgroup_quota() -> Optional[float]:
+    """The cgroup CPU quota in CPUs (v2 ``cpu.max``, v1 ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``),
+    None when unlimited or not visible."""
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             q, p = f.read().split()[:2]
-            if q != "max":
-                quota = int(q) / int(p)
+            return None if q == "max" else int(q) / int(p)
     except (OSError, ValueError):
         pass
-    return {"affinity": aff, "quota_cpus": quota}
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return q / p if q > 0 and p > 0 else None
+    except (OSError, ValueError):
+        return None
 
 
 def cgroup_throttling() -> dict:
@@ -110,22 +121,7 @@ def cpu_budget() -> int:
     (``cpu.max``, v2, or ``cpu.cfs_quota_us`` / ``cpu.cfs_period_us``, v1) -- a container's
     ``os.cpu_count()`` shows the whole machine."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    quota = None
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, p = f.read().split()[:2]
-            if q != "max":
-                quota = int(q) / int(p)
-    except (OSError, ValueError):
-        try:
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
-                q = int(f.read())
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
-                p = int(f.read())
-            if q > 0 and p > 0:
-                quota = q / p
-        except (OSError, ValueError):
-            pass
+    quota = _cgroup_quota()
     if quota is not None:
         n = min(n, max(1, int(quota)))
     return max(1, n)

@@ -49,7 +49,10 @@ def parse():
     ap.add_argument("--library", default="realistic", choices=["realistic", "synthetic"],
                     help="realistic: ~10%% short-literal and ~5%% literal-free primaries; synthetic: every "
                          "primary has a long unique literal (the prefilter's best case)")
-    ap.add_argument("--block-lines", type=int, default=250_000, help="unique synthetic lines, tiled to the shard")
+    ap.add_argument("--block-lines", type=int, default=250_000, help="lines of one generated synthetic block")
+    ap.add_argument("--distinct-blocks", type=int, default=4,
+                    help="distinct generated blocks (seeds); the shard tiles them in rotation, rank r starting at "
+                         "block r, so hit / candidate distributions do not repeat one block")
     ap.add_argument("--hit-rate", type=float, default=0.004)
     ap.add_argument("--topk", type=int, default=100)
     ap.add_argument("--profile", action="store_true", help="per-stage HIP-event timings (no extra syncs)")
@@ -69,7 +72,31 @@ def parse():
                     help="process group: auto = nccl (RCCL) on GPUs at every world size, gloo on CPU for world "
                          "size > 1 and none on CPU at world size 1; nccl / gloo / none force one (gloo on GPUs "
                          "= host-staged, to rehearse several ranks on ONE GPU; none = no collectives at world 1)")
+    ap.add_argument("--timeout", type=float, default=1500.0,
+                    help="hang guard: the whole job's deadline in seconds (0 = none)")
+    ap.add_argument("--stall-timeout", type=float, default=300.0,
+                    help="hang guard: seconds without ANY rank advancing a phase (utils/heartbeat.py); on expiry "
+                         "rank 0 prints one JSON line with status 'timeout' and every rank's last phase")
+    ap.add_argument("--pg-timeout", type=float, default=300.0, help="init_process_group / collective timeout (s)")
     return ap.parse_args()
+
+
+def _gen_block(job):
+    """One synthetic block (forked pool worker: no GPU state exists yet)."""
+    trig, n, seed, hit_rate = job
+    from log_parser_amd.utils.synth import make_log
+    return make_log(n, trig, seed=seed, hit_rate=hit_rate, aux_rate=0.01, stack_rate=0.01).encode()
+
+
+def make_blocks(args, trig):
+    """``--distinct-blocks`` blocks of ``--block-lines`` lines, generated in parallel BEFORE any GPU
+    call (forking after HIP initialisation is not allowed)."""
+    jobs = [(trig, args.block_lines, 11 + 7919 * b, args.hit_rate) for b in range(max(1, args.distinct_blocks))]
+    if len(jobs) == 1:
+        return [_gen_block(jobs[0])]
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(min(len(jobs), 4)) as pool:
+        return pool.map(_gen_block, jobs)
 
 
 def library(args):
@@ -87,13 +114,22 @@ def main():
     # stops overlapping the step (23.5 -> 27.1 ms/step at world 1, profiles/r3_f)
     hw_queues = launch.ensure_hw_queues()
     if not launch.under_launcher() and args.gpus > 1:
-        # parent: no GPU call here; N fresh rank processes, one per GPU
-        sys.exit(launch.spawn_local_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus))
+        # parent: no GPU call here; N fresh rank processes, one per GPU, under the same hang guard
+        sys.exit(launch.spawn_local_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
+                                          timeout_s=(args.timeout + 60) if args.timeout else None,
+                                          stall_s=(args.stall_timeout + 60) if args.stall_timeout else None,
+                                          metric=METRIC))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from log_parser_amd.utils.heartbeat import Heartbeat
+    hb = Heartbeat(rank, world)
+    hb.start(METRIC, args.stall_timeout, args.timeout or None)
     sets, trig = library(args)
+    hb.phase("library")
+    blocks = make_blocks(args, trig)
+    hb.phase("blocks")
 
     # p50 /parse server: started BEFORE this process makes any GPU call (rank 0 only)
     server = None
@@ -103,13 +139,15 @@ def main():
         server = restbench.ServerProcess(restbench.write_library(sets), dev, http=args.http,
                                          env=dict(kv.split("=", 1) for kv in args.server_env))
     try:
-        run(args, sets, trig, rank, world, local_rank, server, hw_queues)
+        run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues, hb)
     finally:
         if server is not None:
             server.stop()
+        hb.phase("done")
+        hb.stop()
 
 
-def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
+def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, hb=None):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -119,6 +157,7 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     from log_parser_amd.parallel.dp import ShardedAnalyzer, all_gather_rows
     from log_parser_amd.utils.config import Config, ScoringParams
     from log_parser_amd.utils import tracing as TR
+    from log_parser_amd.utils import launch
     from log_parser_amd.utils.synth import make_log
 
     use_cuda = torch.cuda.is_available() and args.device != "cpu"
@@ -152,10 +191,15 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
             from log_parser_amd.utils.launch import free_port
             os.environ["MASTER_PORT"] = str(free_port())
         kw = {"device_id": device} if backend == "nccl" else {}
+        from datetime import timedelta
         from log_parser_amd.utils.launch import stdout_to_stderr
+        hb.phase("init_process_group")
         with stdout_to_stderr():            # RCCL prints its version banner on stdout: keep ONE JSON line
-            dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=timedelta(seconds=args.pg_timeout),
+                                    **kw)
+            hb.phase("first barrier")
             dist.barrier()
+        hb.phase("process group ready")
         assert dist.get_world_size() == world
 
     if args.pf_verify_lanes:
@@ -167,21 +211,26 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     eng = Engine(lib, cfg, device=device)
     eng.profile = args.profile
     sa = ShardedAnalyzer(eng)
+    hb.phase("engine")
 
-    # ---- synthetic shard: block tiled to lines_per_gpu, plus halo lines from the neighbours
-    block = make_log(args.block_lines, trig, seed=11, hit_rate=args.hit_rate, aux_rate=0.01, stack_rate=0.01)
-    block_b = block.encode()
-    blines = block_b.split(b"\n")[:-1]
-    reps = max(1, args.lines_per_gpu // len(blines))
-    own_lines = len(blines) * reps
+    # ---- synthetic shard: the distinct blocks tiled in rotation to lines_per_gpu (rank r's tiling
+    # continues where rank r-1's ends), plus halo lines from the neighbours' adjacent blocks
+    B = len(blocks)
+    blk_lines = [b.count(b"\n") for b in blocks]
+    reps = max(1, args.lines_per_gpu // blk_lines[0])
+    order = [(rank * reps + i) % B for i in range(reps)]
+    own_lines = sum(blk_lines[j] for j in order)
     H = lib.halo
-    head = b"\n".join(blines[:H]) + b"\n"
-    tail = b"\n".join(blines[-H:]) + b"\n"
+
+    def edge(b, first):
+        ls_ = blocks[b].split(b"\n", H) if first else blocks[b][:-1].rsplit(b"\n", H)
+        return b"\n".join(ls_[:H] if first else ls_[-H:]) + b"\n"
     hl = H if rank > 0 else 0
     hr = H if rank < world - 1 else 0
-    pre = tail if hl else b""
-    post = head if hr else b""
-    nbytes = len(pre) + len(block_b) * reps + len(post)
+    pre = edge(((rank - 1) * reps + reps - 1) % B, False) if hl else b""
+    post = edge(((rank + 1) * reps) % B, True) if hr else b""
+    parts = [pre] + [blocks[j] for j in order] + [post]
+    nbytes = sum(len(x) for x in parts)
     size = K.padded_len(nbytes)
     # page-locked host shard, registered in place (utils/hostmem.py); the H2D is an SDMA copy
     if use_cuda:
@@ -192,7 +241,7 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
         host = torch.zeros(size, dtype=torch.uint8)
     hv = host.numpy()
     o = 0
-    for part in [pre] + [block_b] * reps + [post]:         # fill in place: no whole-shard temporaries
+    for part in parts:                                     # fill in place: no whole-shard temporaries
         hv[o:o + len(part)] = np.frombuffer(part, np.uint8)
         o += len(part)
     # Double-buffered ingest: the PCIe copy of request k+1 runs on its own HIP stream while request
@@ -291,9 +340,13 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     from log_parser_amd.utils.numa import gpu_numa_node
     numa = gpu_numa_node(local_rank) if use_cuda else -1
 
-    for _ in range(args.warmup):
+    hb.phase("shard")
+    for k in range(args.warmup):
+        launch.inject_fault(rank, k)                            # (tests: LP_FAULT_RANK / _STEP / _MODE)
         step()
+        hb.phase(f"warmup {k}")
     barrier()
+    hb.phase("server wait")
     if server is not None and not server.wait_ready():      # server idle before timing starts
         print("warning: /parse server did not come up; p50_parse_ms omitted", file=sys.stderr)
         server.stop()
@@ -302,9 +355,12 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
     state["dev"] = []
     t0 = time.perf_counter()
     last = None
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        launch.inject_fault(rank, args.warmup + k)
         last = step()
+        hb.phase(f"timed {k}")
     barrier()
+    hb.phase("timed loop done")
     dt = time.perf_counter() - t0
     dms_local = float(np.mean([a.elapsed_time(b) for a, b in state["dev"]])) if state.get("dev") else -1.0
     diag = [dt, h2d_gbps, dms_local, float(numa)]
@@ -330,6 +386,7 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
                                 f"(secondary+sequence+context)",
                        "global_batch": total_lines, "seq_len": round(nbytes / max(own_lines, 1), 1),
                        "parallelism": f"dp{world}", "lines_per_gpu": own_lines, "bytes_per_gpu": nbytes,
+                       "distinct_blocks": B, "block_lines": args.block_lines,
                        "events_per_step": int(last.pattern_counts.sum().item()),
                        "events_to_host_rank0": state["events_host"],
                        "library_kind": args.library, "library": lib.summary(), "prefilter_stride": lib.pf["stride"], "device": str(device)},
@@ -352,6 +409,7 @@ def run(args, sets, trig, rank, world, local_rank, server, hw_queues=0):
         if args.profile:
             rec["timings_ms_last_step_rank0"] = {k: round(v, 3) for k, v in TR.resolve(last.result.timings).items()}
         if args.parse_requests > 0:
+            hb.phase("parse latency")
             # second half of the BASELINE metric: one 10k-line /parse request, same library
             req = make_log(10_000, trig, seed=13, hit_rate=0.01)
             if server is not None:

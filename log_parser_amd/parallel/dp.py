@@ -182,7 +182,7 @@ class ShardedAnalyzer:
     def step(self, text: torch.Tensor, nbytes: int, ls: Optional[torch.Tensor], ll: Optional[torch.Tensor],
              halo_left: int, halo_right: int, topk: int = 100, with_factors: bool = False,
              pack_events: bool = False, stream_carry: Optional[StreamCarry] = None,
-             split_trim: bool = True) -> StepOutput:
+             split_trim: bool = True, host_text=None) -> StepOutput:
         """One shard step. ``ls`` / ``ll`` = None: the line index is built here, with the literal
         prefilter queued behind it before its host read (the GPU filters while the host waits).
 
@@ -196,7 +196,10 @@ class ShardedAnalyzer:
         ``stream_carry``: the step is one of a stream of steps -- its carries come from the earlier
         steps, N stays open (factors kept, ``with_factors`` implied), the frequency window is not
         recorded (the stream records once, at its end) and the output carries the sequence state
-        after the step and the step's summed frequency counts."""
+        after the step and the step's summed frequency counts.
+
+        ``host_text``: the shard's bytes in host memory (numpy view), read by the backtracker side
+        path of a library with non-regular regexes instead of a device-to-host copy of the text."""
         eng = self.engine
         rank, wsize = world()
         early = None
@@ -212,7 +215,8 @@ class ShardedAnalyzer:
         for attempt in range(4):
             out, prep, veto = self._step(text, nbytes, ls, ll, halo_left, halo_right, topk,
                                          with_factors or stream_carry is not None, pack_events,
-                                         early if attempt == 0 else None, defer, stream_carry, split_trim)
+                                         early if attempt == 0 else None, defer, stream_carry, split_trim,
+                                         host_text)
             if not defer:
                 return out
             end = torch.cuda.Event(enable_timing=True)
@@ -239,7 +243,7 @@ class ShardedAnalyzer:
         return out
 
     def _step(self, text, nbytes, ls, ll, halo_left, halo_right, topk, with_factors, pack_events, early, defer,
-              sc: Optional[StreamCarry] = None, split_trim: bool = True):
+              sc: Optional[StreamCarry] = None, split_trim: bool = True, host_text=None):
         eng = self.engine
         lib = eng.lib
         rank, wsize = world()
@@ -247,7 +251,8 @@ class ShardedAnalyzer:
         L = ls.numel()
         own_lo, own_hi = halo_left, L - halo_right
         segs = Segments.scalar(0, L, own_lo, own_hi, 0, 1, dev, upload=eng.upload)
-        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early, defer=defer, split_trim=split_trim)
+        prep = eng.prepare(text, nbytes, ls, ll, segs, early=early, defer=defer, split_trim=split_trim,
+                           host_text=host_text)
         chain = eng.seq_chain_table(prep, own_lo, own_hi)
         nk = len(lib.freq_ids)
         ns = chain.numel()

@@ -44,13 +44,8 @@ class RankExcluded(RuntimeError):
 
 
 def _maybe_inject(orig_rank: int, step: int) -> None:
-    r, s = os.environ.get("LP_FAULT_RANK"), os.environ.get("LP_FAULT_STEP")
-    if r is None or s is None or int(r) != orig_rank or int(s) != step:
-        return
-    if os.environ.get("LP_FAULT_MODE", "exit") == "hang":
-        time.sleep(float(os.environ.get("LP_FAULT_HANG_S", "86400")))
-        os._exit(18)
-    os._exit(17)
+    from ..utils.launch import inject_fault
+    inject_fault(orig_rank, step)
 
 
 class ElasticGroup:

@@ -533,9 +533,14 @@ class StreamAnalyzer:
         ahead: "deque" = deque()
         ended = False
 
+        # hold mode keeps every staged chunk's pinned buffer until its prepare: the consumer then holds
+        # the current chunk + the look-ahead, so the look-ahead must leave the producer one buffer of
+        # the pool to fill, or refill() waits on a chunk the producer cannot stage
+        depth = min(self.PREFETCH, self.PINNED_BUFFERS - 1) if hold and free_q is not None else self.PREFETCH
+
         def refill():
             nonlocal ended
-            while not ended and len(ahead) < self.PREFETCH:
+            while not ended and len(ahead) < depth:
                 it = fetch()
                 if it is None:
                     ended = True
@@ -682,6 +687,7 @@ class ShardedStreamAnalyzer:
         th = threading.Thread(target=self.sa._producer, args=(src, eff, q, 0, free_q, mine), daemon=True)
         th.start()
         copy_stream = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        hold = bool(lib.host_plan)             # backtracker side path: reads the pinned host bytes
         ev_gl, ev_pat, ev_fac = [], [], []
         nbytes_total = 0
         for _ in range(steps):
@@ -689,23 +695,33 @@ class ShardedStreamAnalyzer:
             if isinstance(item, BaseException):
                 raise item
             pinned, n, size, lh, rh, _end = item
+            idle = _end < 0                                      # own no line this step: a placeholder
+            recycle = copy_stream is not None and not idle       # (not from the pinned pool)
+            host_text = None
             if copy_stream is not None:
                 with torch.cuda.stream(copy_stream):
                     text = torch.empty(size, dtype=torch.uint8, device=dev)
                     text.copy_(pinned[:size], non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(copy_stream)
-                free_q.put((pinned, ev))
                 torch.cuda.current_stream(dev).wait_event(ev)
                 text.record_stream(torch.cuda.current_stream(dev))
+                if hold and not idle:
+                    host_text = pinned[:n].numpy()              # the side path reads the pinned bytes
+                elif recycle:
+                    free_q.put((pinned, ev))
+                    recycle = False
             else:
                 text = pinned
-            if _end < 0:                                         # idle: own no line this step
+            if idle:
                 ls = torch.zeros(0, dtype=torch.int64, device=dev)
                 ll = torch.zeros(0, dtype=torch.int32, device=dev)
             else:
                 ls, ll = K.split_chunk_lines(text, n)
-            out = self.dp.step(text, n, ls, ll, lh, rh, topk=0, stream_carry=carry, split_trim=False)
+            out = self.dp.step(text, n, ls, ll, lh, rh, topk=0, stream_carry=carry, split_trim=False,
+                               host_text=host_text)
+            if recycle:                                          # hold mode: after the side path's read
+                free_q.put((pinned, ev))
             res = out.result
             if res.ev_line.numel():
                 ev_gl.append(res.ev_line.to(torch.int64) - out.own_lo + out.own_start_dev)

@@ -64,16 +64,29 @@ def rank_env(rank: int, world: int, port: int, base: Optional[dict] = None) -> d
 
 
 def spawn_local_ranks(argv: Sequence[str], world: int, poll_s: float = 0.2,
-                      timeout_s: Optional[float] = None) -> int:
-    """Run ``python argv...`` as ``world`` ranks on this node; returns the job's exit status."""
+                      timeout_s: Optional[float] = None, stall_s: Optional[float] = None,
+                      metric: str = "") -> int:
+    """Run ``python argv...`` as ``world`` ranks on this node; returns the job's exit status.
+
+    Hang guard (backstop of the ranks' own watchdogs, ``utils/heartbeat.py``): the ranks write
+    their phases into a fresh heartbeat directory; past ``timeout_s`` in total, or ``stall_s``
+    without any rank advancing, the parent prints one ``{"status": "timeout", "phases": ...}``
+    JSON line, ends the ranks by their exact handles and returns 124."""
+    import shutil
+    import tempfile
+    from .heartbeat import ENV_DIR, last_progress, read_phases, timeout_record
     port = free_port()
+    hb_dir = tempfile.mkdtemp(prefix="lp-heartbeat-")
     procs: List[subprocess.Popen] = []
     try:
         for r in range(world):
+            env = rank_env(r, world, port)
+            env[ENV_DIR] = hb_dir
             # rank 0 keeps the parent's stdout (the one JSON line); other ranks' stdout -> stderr
-            procs.append(subprocess.Popen([sys.executable] + list(argv), env=rank_env(r, world, port),
+            procs.append(subprocess.Popen([sys.executable] + list(argv), env=env,
                                           stdout=None if r == 0 else sys.stderr))
         t0 = time.monotonic()
+        w0 = time.time()
         while True:
             codes = [p.poll() for p in procs]
             bad = [c for c in codes if c not in (None, 0)]
@@ -81,7 +94,17 @@ def spawn_local_ranks(argv: Sequence[str], world: int, poll_s: float = 0.2,
                 return bad[0]
             if all(c == 0 for c in codes):
                 return 0
+            reason = None
             if timeout_s is not None and time.monotonic() - t0 > timeout_s:
+                reason = f"job exceeded {timeout_s:.0f} s"
+            elif stall_s is not None and time.time() - max(last_progress(hb_dir, world), w0) > stall_s:
+                reason = f"no rank advanced for {stall_s:.0f} s"
+            if reason is not None:
+                import json
+                rec = timeout_record(metric, world, read_phases(hb_dir, world), reason + " (launcher)",
+                                     time.monotonic() - t0)
+                sys.stdout.write(json.dumps(rec) + "\n")
+                sys.stdout.flush()
                 return 124
             time.sleep(poll_s)
     finally:
@@ -94,6 +117,20 @@ def spawn_local_ranks(argv: Sequence[str], world: int, poll_s: float = 0.2,
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
+        shutil.rmtree(hb_dir, ignore_errors=True)
+
+
+def inject_fault(rank: int, step: int) -> None:
+    """Fault injection for the multi-process tests: ``LP_FAULT_RANK=k LP_FAULT_STEP=n`` makes rank
+    ``k`` exit (status 17) at the start of step ``n``; ``LP_FAULT_MODE=hang`` makes it stop
+    responding for ``LP_FAULT_HANG_S`` seconds instead (then exit 18)."""
+    r, s = os.environ.get("LP_FAULT_RANK"), os.environ.get("LP_FAULT_STEP")
+    if r is None or s is None or int(r) != rank or int(s) != step:
+        return
+    if os.environ.get("LP_FAULT_MODE", "exit") == "hang":
+        time.sleep(float(os.environ.get("LP_FAULT_HANG_S", "86400")))
+        os._exit(18)
+    os._exit(17)
 
 
 @contextlib.contextmanager

@@ -99,3 +99,25 @@ def test_bench_single_rank_parse_over_http(tmp_path):
     assert d["n_gpus"] == 1 and d["world_size"] == 1 and d["backend"] == "gloo"
     assert d["p50_parse_ms"] > 0 and d["p50_engine_ms"] > 0
     assert "HTTP" in d["parse_transport"]
+
+
+def test_bench_hang_guard_reports_phases(tmp_path):
+    """A rank that hangs mid-run (rank 1 stops responding at step 2) must not burn the driver's
+    timeout: within the stall limit rank 0 prints ONE JSON line with status 'timeout' and every
+    rank's last completed phase, and the job exits non-zero (utils/heartbeat.py)."""
+    import time
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "3",
+           "--warmup", "1", "--lines-per-gpu", "3000", "--block-lines", "3000", "--distinct-blocks", "1",
+           "--parse-requests", "0", "--library", "synthetic", "--patterns", "50", "--stall-timeout", "12"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", LP_FAULT_RANK="1", LP_FAULT_STEP="2", LP_FAULT_MODE="hang",
+               LP_FAULT_HANG_S="600")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert time.monotonic() - t0 < 200
+    assert r.returncode == 124, (r.returncode, r.stderr[-2000:])
+    d = _json_line(r.stdout)
+    assert d["status"] == "timeout" and d["n_gpus"] == 2 and d["value"] is None
+    assert d["phases"]["1"]["phase"] == "timed 0"           # rank 1 finished timed step 0, hung in step 1
+    assert d["phases"]["0"]["phase"] in ("timed 0", "timed 1")

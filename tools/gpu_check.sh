@@ -48,6 +48,16 @@ for s in $steps; do
       run stream_auto 600 python -u benchmarks/bench_configs.py stream
       run stream_8g 600 python -u benchmarks/bench_configs.py stream --chunk-mb 8192
       run stream_256 600 python -u benchmarks/bench_configs.py stream --chunk-mb 256 ;;
+    reqtrace)
+      # one 10k-line request: wall p50 and the kernel timeline, library with / without the Java shapes
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      for j in 0 0.01; do
+        run rt_wall_$j 300 python -u tools/request_trace.py --requests 400 --java-shape-rate $j
+        run rt_prof_$j 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/rt_prof_$j -o run -- \
+          python3 tools/request_trace.py --requests 200 --java-shape-rate $j
+        db=$(find gpurun_out/rt_prof_$j -name "*.db" | head -1)
+        run rt_sum_$j 120 python3 tools/request_trace.py --db "$db" --requests 200
+      done ;;
     configs)
       run single 600 python -u benchmarks/bench_configs.py single
       run rest 600 python -u benchmarks/bench_configs.py rest ;;

@@ -23,7 +23,7 @@ def run(args):
     from log_parser_amd.utils.config import Config, ScoringParams
     from log_parser_amd.utils.synth import make_log, realistic_library
     dev = torch.device("cuda", 0)
-    sets, trig = realistic_library(args.patterns, seed=7)
+    sets, trig = realistic_library(args.patterns, seed=7, java_shape_rate=args.java_shape_rate)
     lib = CompiledLibrary(sets, ScoringParams())
     ov = {"engine.device": "cuda:0"}
     if args.device_counts:
@@ -38,7 +38,8 @@ def run(args):
         t0 = time.perf_counter()
         eng.analyze_batch_json([logs])
         wall.append((time.perf_counter() - t0) * 1e3)
-    print(json.dumps({"lines": args.lines, "requests": args.requests, "p50_ms": round(statistics.median(wall), 3),
+    print(json.dumps({"lines": args.lines, "requests": args.requests, "java_shape_rate": args.java_shape_rate,
+                      "library": lib.summary(), "p50_ms": round(statistics.median(wall), 3),
                       "p99_ms": round(sorted(wall)[int(0.99 * (len(wall) - 1))], 3)}), flush=True)
 
 
@@ -89,6 +90,8 @@ if __name__ == "__main__":
     ap.add_argument("--patterns", type=int, default=1000)
     ap.add_argument("--requests", type=int, default=200)
     ap.add_argument("--db", default="")
+    ap.add_argument("--java-shape-rate", type=float, default=0.01,
+                    help="share of Java-shape primaries in the realistic library (0 = the round-3 library)")
     ap.add_argument("--device-counts", action="store_true", help="runner device-count mode (no mid-batch read)")
     a = ap.parse_args()
     summarise(a) if a.db else run(a)

@@ -19,8 +19,17 @@
 // ctx = prev * 6 + next) is checked before every code point (accept) and gates edges; extra accept
 // check before a final line terminator; end of line is next kind N_EOS.
 //
+// Counted positions: a bounded repeat of one class C{m,n} (n - m >= BPG_CTR_MIN) is m plain positions
+// plus ONE counted position p for C{0,n-m} (jregex.cpp Glushkov). p has no self edge in the follow
+// relation; the walk keeps a count per counted position -- the characters the YOUNGEST thread in p
+// has consumed (a thread that entered later is never worse: every thread in p reads the same
+// characters and has the same follow set, and only an upper bound applies) -- and p stays active
+// through its own loop only while that count is below the bound; an entry (any edge into p,
+// first-set included) restarts the count at 1. So X.{0,20000}Y costs 3 positions + 1 count.
+//
 // Program layout (uint64 words):
 //   [0] W | E << 8 | ncls << 20 | anchored << 30 | uniform << 31 | nullable(24) << 32 | uword << 56
+//       | ncounters << 57
 //   [1] nranges | total words << 32
 //   [2 ..]           shm[W] selfm[W] src[W] R[W] lo[W] hi[W]
 //   [2 + 6W ..]      first[24][W]           (per boundary context; uniform -> only [0] is read)
@@ -30,20 +39,22 @@
 //   then             exc[E][1 + W]          (src | cond << 16, then the target mask)
 //   then             ranges[nranges]        (lo | class << 21 | kind << 37; kind 0 N, 1 W, 2 T),
 //                                           sorted by lo, first lo = 0x80
+//   then             ctr[ncounters]         (position | bound << 16)
 #pragma once
 #include <stdint.h>
 
 namespace lp {
 
 constexpr int BPG_LANE_MAX_W = 8;      // widest program of the one-lane-per-line walk
+constexpr int BPG_CTR_MAX = 4;         // counted positions per program (jregex.h BPG_MAX_CTR)
 constexpr uint64_t BPG_UNIFORM = 1ull << 31;
 constexpr uint64_t BPG_ANCHORED = 1ull << 30;
 
 struct BpgLayout {
-  int W, E, ncls, nranges;
+  int W, E, ncls, nranges, nctr;
   bool uniform, anchored;
   uint32_t nullm;
-  int o_first, o_last, o_amap, o_cls, o_exc, o_rng;
+  int o_first, o_last, o_amap, o_cls, o_exc, o_rng, o_ctr;
 };
 
 LP_HD BpgLayout bpg_layout(const uint64_t* P) {
@@ -62,7 +73,19 @@ LP_HD BpgLayout bpg_layout(const uint64_t* P) {
   L.o_cls = L.o_amap + 32;
   L.o_exc = L.o_cls + L.ncls * L.W;
   L.o_rng = L.o_exc + L.E * (L.W + 1);
+  L.nctr = (int)((h >> 57) & 7);
+  L.o_ctr = L.o_rng + L.nranges;
   return L;
+}
+
+// one counted position's step (youngest-thread count, see the top): `Fx` = the edges into p this
+// step (first set included) in bit b of word `fw`; `s` = p active before the step; returns the
+// updated word and advances `cnt` (entry -> 1, stay -> +1, saturating at the bound)
+LP_HD uint64_t bpg_ctr_step(uint64_t fw, int b, bool s, uint32_t bound, uint32_t& cnt) {
+  const bool entry = (fw >> b) & 1ull;
+  const bool stay = s && cnt < bound;
+  cnt = entry ? 1u : (cnt < bound ? cnt + 1u : bound);
+  return fw | ((uint64_t)stay << b);
 }
 LP_HD int bpg_words(const uint64_t* P) { return (int)(P[1] >> 32); }
 
@@ -130,6 +153,7 @@ LP_HD bool bpg_find_w(const uint64_t* __restrict__ P, const uint8_t* __restrict_
   const int ftl = final_term_len(s, n);
   const int ft = ftl ? n - ftl : -1;
   int prevk = 0;  // P_BOS
+  uint32_t cnt[BPG_CTR_MAX] = {0, 0, 0, 0};
   for (int t = 0;; ++t) {
     int nk = 0, k = 0;                          // N_EOS at end of line
     if (t < n) {
@@ -172,9 +196,15 @@ LP_HD bool bpg_find_w(const uint64_t* __restrict__ P, const uint8_t* __restrict_
     }
     const uint64_t* C = cls + (size_t)k * W;
     const uint64_t* Fi = first + (L.uniform ? 0 : ctx * W);
+    for (int w = 0; w < W; ++w) F[w] |= Fi[w];
+    for (int c = 0; c < L.nctr; ++c) {            // counted positions
+      const uint64_t e = P[L.o_ctr + c];
+      const int p = (int)(e & 0xFFFF);
+      F[p >> 6] = bpg_ctr_step(F[p >> 6], p & 63, (S[p >> 6] >> (p & 63)) & 1ull, (uint32_t)(e >> 16), cnt[c]);
+    }
     uint64_t alive = 0;
     for (int w = 0; w < W; ++w) {
-      S[w] = (F[w] | Fi[w]) & C[w];
+      S[w] = F[w] & C[w];
       alive |= S[w];
     }
     if (L.anchored && !alive) return false;  // first set only at the line start: nothing can match
@@ -237,6 +267,16 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
   const int ftl = final_term_len(s, n);
   const int ft = ftl ? n - ftl : -1;
   int prevk = 0;  // P_BOS
+  const int nctr = L.nctr;
+  int cpos[BPG_CTR_MAX];
+  uint32_t cbound[BPG_CTR_MAX], cnt[BPG_CTR_MAX];
+#pragma unroll
+  for (int c = 0; c < BPG_CTR_MAX; ++c) {
+    const uint64_t e = c < nctr ? P[L.o_ctr + c] : 0ull;
+    cpos[c] = (int)(e & 0xFFFF);
+    cbound[c] = (uint32_t)(e >> 16);
+    cnt[c] = 0;
+  }
 // accept in boundary context ACTX (a macro, not a lambda: a lambda capturing S by reference kept
 // the state array in scratch memory)
 #define LP_BPG_ACCEPT(ACTX, RES)                                                 \
@@ -316,20 +356,33 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
               for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
             }
           }
-          uint64_t alive = 0;
           if (uniform) {
 #pragma unroll
-            for (int w = 0; w < W; ++w) {
-              S[w] = (F[w] | f0[w]) & Cr[qq][w];
-              alive |= S[w];
-            }
+            for (int w = 0; w < W; ++w) F[w] |= f0[w];
           } else {
             const uint64_t* Fi = first + ctx * W;
 #pragma unroll
+            for (int w = 0; w < W; ++w) F[w] |= Fi[w];
+          }
+#pragma unroll
+          for (int c = 0; c < BPG_CTR_MAX; ++c) {  // counted positions (rare: skipped as a whole)
+            if (c >= nctr) break;
+            const int pw = cpos[c] >> 6;
+            uint64_t fw = 0, sw = 0;
+#pragma unroll
             for (int w = 0; w < W; ++w) {
-              S[w] = (F[w] | Fi[w]) & Cr[qq][w];
-              alive |= S[w];
+              fw = (w == pw) ? F[w] : fw;
+              sw = (w == pw) ? S[w] : sw;
             }
+            fw = bpg_ctr_step(fw, cpos[c] & 63, (sw >> (cpos[c] & 63)) & 1ull, cbound[c], cnt[c]);
+#pragma unroll
+            for (int w = 0; w < W; ++w) F[w] = (w == pw) ? fw : F[w];
+          }
+          uint64_t alive = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            S[w] = F[w] & Cr[qq][w];
+            alive |= S[w];
           }
           if (L.anchored && !alive) return false;
           prevk = prev_of(nk);

@@ -108,7 +108,7 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
   const uint64_t gm = (G >= 64 ? ~0ull : ((1ull << G) - 1ull)) << gb;
   const uint64_t chain = coop_chain_mask(G);
   BpgLayout L = bpg_layout(P);
-  if (!valid) { L.W = 0; L.E = 0; L.uniform = true; L.nullm = 0; }
+  if (!valid) { L.W = 0; L.E = 0; L.uniform = true; L.nullm = 0; L.nctr = 0; }
   const int W = L.W;
   const int E = L.E;
   const bool uniform = L.uniform;
@@ -126,6 +126,18 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
   const uint32_t f0 = wl ? LP_W32(first_o) : 0u, l0 = wl ? LP_W32(last_o) : 0u;
   const int ftl = valid ? final_term_len(s, n) : 0;
   const int ft = ftl ? n - ftl : -1;
+  // counted positions: the lane holding the position's word keeps its count (bpg.h)
+  const int nctr = L.nctr;
+  int cpos[BPG_CTR_MAX];
+  uint32_t cbound[BPG_CTR_MAX], cnt[BPG_CTR_MAX];
+#pragma unroll
+  for (int c = 0; c < BPG_CTR_MAX; ++c) {
+    const uint64_t e = c < nctr ? P[L.o_ctr + c] : 0ull;
+    cpos[c] = c < nctr && j == (int)((e & 0xFFFF) >> 5) ? (int)(e & 31) : -1;   // -1: not this lane's
+    cbound[c] = (uint32_t)(e >> 16);
+    cnt[c] = 0;
+  }
+  const bool wctr = __ballot(nctr > 0) != 0;
   // wave-uniform feature switches: the common program (uniform first/last sets, no exception edges,
   // not nullable, line without a final terminator) walks only the shift / self / spread chain
   const bool wnon = __ballot(valid && !uniform) != 0;
@@ -209,7 +221,18 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
           if (((M >> (gb + (p >> 5))) & 1ull) && ((((uint32_t)(h >> 16) & 0xFFFFFFu) >> ctx) & 1u)) F |= tw;
         }
       }
-      const uint32_t Sn = (F | (wnon ? fw[q] : f0)) & cw[q];
+      F |= wnon ? fw[q] : f0;
+      if (wctr) {
+#pragma unroll
+        for (int c = 0; c < BPG_CTR_MAX; ++c) {
+          if (cpos[c] < 0) continue;
+          uint32_t k = cnt[c];
+          const uint32_t Fc = (uint32_t)bpg_ctr_step(F, cpos[c], (S >> cpos[c]) & 1u, cbound[c], k);
+          F = Fc;
+          cnt[c] = skip ? cnt[c] : k;
+        }
+      }
+      const uint32_t Sn = F & cw[q];
       S = skip ? S : Sn;
     }
     // a group is finished once it accepted or its line ended; the wave stops when all are

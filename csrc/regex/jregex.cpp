@@ -1071,7 +1071,10 @@ struct Info {
 
 class Glushkov {
  public:
-  Glushkov(const std::vector<Node>& N, int max_pos) : N_(N), max_pos_(max_pos) {}
+  // counters: bounded repeats of one code-point class become counted positions (Nfa::ctr; BPG
+  // programs only -- the byte automata expand every repeat)
+  Glushkov(const std::vector<Node>& N, int max_pos, bool counters = false)
+      : N_(N), max_pos_(max_pos), counters_(counters) {}
   Nfa nfa;
 
   Info build(int id) {
@@ -1109,6 +1112,21 @@ class Glushkov {
         int kid = n.kids[0];
         if (n.lo == 0 && n.hi == 0) { r.nullable = CTX_ALL; return r; }
         bool have = false;
+        const int cset = counters_ && n.hi != -1 && n.hi - n.lo >= BPG_CTR_MIN ? single_cset(kid) : -1;
+        if (cset >= 0) {
+          // C{lo,hi} = lo plain copies of C, then ONE counted position for C{0, hi - lo}
+          for (int k = 0; k < n.lo; ++k) {
+            Info c = build(cset);
+            r = have ? cat(r, c) : c;
+            have = true;
+          }
+          Info c = build(cset);
+          const int p = c.first[0].to;
+          nfa.ctr.resize(nfa.npos, 0);
+          nfa.ctr[p] = n.hi - n.lo;
+          c.nullable = CTX_ALL;
+          return have ? cat(r, c) : c;
+        }
         for (int k = 0; k < n.lo; ++k) {
           bool lastcopy_loop = (n.hi == -1 && k == n.lo - 1);
           Info c = build(kid);
@@ -1144,6 +1162,7 @@ class Glushkov {
     nfa.first = top.first;
     nfa.last = top.last;
     nfa.nullable = top.nullable;
+    if (!nfa.ctr.empty()) nfa.ctr.resize(nfa.npos, 0);
     nfa.follow.resize(nfa.npos);
     for (int p = 0; p < nfa.npos; ++p) {
       auto& v = fol_[p];
@@ -1160,7 +1179,19 @@ class Glushkov {
  private:
   const std::vector<Node>& N_;
   int max_pos_;
+  bool counters_ = false;
   std::vector<std::vector<Edge>> fol_;
+
+  // the N_CSET node a repeat's body reduces to (one character class, through single-child
+  // concatenations / alternations), or -1
+  int single_cset(int id) const {
+    for (;;) {
+      const Node& n = N_[id];
+      if (n.t == N_CSET) return id;
+      if ((n.t == N_CAT || n.t == N_ALT) && n.kids.size() == 1) { id = n.kids[0]; continue; }
+      return -1;
+    }
+  }
 
   static void merge(std::vector<Edge>& v) {
     std::sort(v.begin(), v.end(), [](const Edge& a, const Edge& b) { return a.to < b.to; });
@@ -1490,15 +1521,21 @@ Compiled compile_impl(const std::string& pattern, int max_dfa_states, int max_po
   out.kind = Kind::NFA;
   out.error = why;
   if (want_bpg) {
-    try {
-      Glushkov G(nodes, BPG_MAX_POS);
-      Info top = G.build(root);
-      G.finish(top);
-      check_ft(G.nfa);
-      out.bpg = bpg_program(G.nfa, out.uword);
-    } catch (const Unsupported& e) {
-      out.error = why + "; bpg: " + e.what();
-      out.bpg.clear();
+    // with counted positions first (bounded repeats of one class as one position + a count); a
+    // program with more counted repeats than the walk keeps counts for is built expanded
+    for (bool counters : {true, false}) {
+      try {
+        Glushkov G(nodes, BPG_MAX_POS, counters);
+        Info top = G.build(root);
+        G.finish(top);
+        check_ft(G.nfa);
+        out.bpg = bpg_program(G.nfa, out.uword);
+        out.error = why;
+        break;
+      } catch (const Unsupported& e) {
+        out.error = why + "; bpg: " + e.what();
+        out.bpg.clear();
+      }
     }
   }
   if (out.bpg.empty() && !out.byte_nfa) {
@@ -1806,6 +1843,11 @@ std::vector<uint64_t> bpg_program(const Nfa& nf, bool uword) {
     last_kind = kd;
   }
   const int ncls = (int)rows.size();
+  // ---- counted positions (bounded repeats of one class): (position, bound) after the ranges
+  std::vector<uint64_t> ctrs;
+  for (int p = 0; p < (int)nf.ctr.size() && p < np; ++p)
+    if (nf.ctr[p] > 0) ctrs.push_back((uint64_t)p | ((uint64_t)nf.ctr[p] << 16));
+  if ((int)ctrs.size() > BPG_MAX_CTR) throw Unsupported("too many counted repeats");
   // ---- first / last per context, header flags
   std::vector<uint64_t> first((size_t)NCTX * W, 0), last((size_t)NCTX * W, 0);
   for (auto& e : nf.first)
@@ -1821,7 +1863,8 @@ std::vector<uint64_t> bpg_program(const Nfa& nf, bool uword) {
   for (size_t i = 6 * (size_t)W; i < first.size() && anchored; ++i) if (first[i]) anchored = false;
   const uint64_t E = exc.size();
   const uint64_t hdr = (uint64_t)W | (E << 8) | ((uint64_t)ncls << 20) | (anchored ? 1ull << 30 : 0) |
-                       (uniform ? 1ull << 31 : 0) | ((uint64_t)nullable << 32) | (uword ? 1ull << 56 : 0);
+                       (uniform ? 1ull << 31 : 0) | ((uint64_t)nullable << 32) | (uword ? 1ull << 56 : 0) |
+                       ((uint64_t)ctrs.size() << 57);
   std::vector<uint64_t> P;
   P.push_back(hdr);
   P.push_back(0);   // hdr2: nranges | total words << 32 (below)
@@ -1838,6 +1881,7 @@ std::vector<uint64_t> bpg_program(const Nfa& nf, bool uword) {
     put(widen(e.tos));
   }
   P.insert(P.end(), ranges.begin(), ranges.end());
+  P.insert(P.end(), ctrs.begin(), ctrs.end());
   P[1] = (uint64_t)ranges.size() | ((uint64_t)P.size() << 32);
   return P;
 }

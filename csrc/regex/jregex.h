@@ -84,6 +84,11 @@ struct Nfa {
   std::vector<Edge> first;                  // (pos, cond)
   std::vector<Edge> last;                   // (pos, cond)
   uint32_t nullable = 0;                    // contexts in which the empty string matches
+  // code-point NFAs built with counters: ctr[p] = B > 0 makes p a COUNTED position -- the optional
+  // part C{0,B} of a bounded repeat of one character class, one position instead of B. Its self
+  // loop is NOT in follow[p]; it is taken while the youngest thread in p has consumed < B
+  // characters (bpg.h: the walk keeps one count per counted position). Empty: no counters.
+  std::vector<int> ctr;
 };
 
 struct Dfa {
@@ -143,6 +148,11 @@ int final_terminator_len(const uint8_t* s, int64_t n);
 constexpr int BPG_MAX_POS = 2048;         // 32 words of 64 positions
 constexpr int BPG_MAX_EXC = 256;
 constexpr int BPG_MAX_CLS = 1023;
+// bounded repeats C{m,n} of ONE character class with n - m >= BPG_CTR_MIN become m plain positions
+// plus one counted position (Nfa::ctr): X.{0,20000}Y is 3 positions, not 20,002. A program holds
+// at most BPG_MAX_CTR counters (more: the repeats are expanded, the pre-counter behaviour).
+constexpr int BPG_CTR_MIN = 16;
+constexpr int BPG_MAX_CTR = 4;
 // code-point NFA -> program; throws Unsupported when it does not fit
 std::vector<uint64_t> bpg_program(const Nfa& cnfa, bool uword);
 

@@ -12,7 +12,9 @@ The program is built at library load by ``jregex.cpp`` ``bpg_program`` (exposed 
 bytes of ``N.compile_regex``), which decomposes the follow relation into word-parallel parts --
 shift edges p -> p+1, self loops, spread fields (every active source reaches every target above
 it: one multi-word subtraction for all fields), and exception rows -- and checks that the parts
-rebuild every follow set. Layout: ``csrc/kernels/bpg.h``. This module holds the pure-Python twin
+rebuild every follow set. A bounded repeat of one class ``C{m,n}`` (n - m >= 16) is m plain
+positions plus ONE counted position whose self loop holds while the youngest thread in it has
+read fewer than n - m characters (``X.{0,20000}Y`` = 3 positions). Layout: ``csrc/kernels/bpg.h``. This module holds the pure-Python twin
 of the walk (tests) and the header decoder.
 """
 from __future__ import annotations
@@ -34,7 +36,7 @@ def program_info(prog) -> dict:
     return {"words": h & 0xFF, "exceptions": (h >> 8) & 0xFFF, "classes": (h >> 20) & 0x3FF,
             "uniform": bool(h & HDR_UNIFORM), "anchored": bool(h & HDR_ANCHORED),
             "unicode_word": bool((h >> 56) & 1), "ranges": int(prog[1]) & 0xFFFFFFFF,
-            "size": int(prog[1]) >> 32}
+            "counters": (h >> 57) & 7, "size": int(prog[1]) >> 32}
 
 
 def _ascii_kind(c: int) -> int:
@@ -67,6 +69,8 @@ def run_program(prog, line: bytes) -> bool:
         x = int(prog[o_exc + e * (W + 1)])
         exc.append((x & 0xFFFF, (x >> 16) & 0xFFFFFF, big(prog[o_exc + e * (W + 1) + 1:o_exc + (e + 1) * (W + 1)])))
     rng = [int(x) for x in prog[o_rng:o_rng + nr]]
+    # counted positions (bounded repeats of one class): [position, bound, youngest thread's count]
+    ctr = [[int(x) & 0xFFFF, int(x) >> 16, 0] for x in prog[o_rng + nr:o_rng + nr + ((h >> 57) & 7)]]
     rlo = [x & 0x1FFFFF for x in rng]
     full = (1 << (64 * W)) - 1
     n = len(line)
@@ -117,7 +121,14 @@ def run_program(prog, line: bytes) -> bool:
         for p, cond, m in exc:
             if (S >> p) & 1 and (cond >> ctx) & 1:
                 Fo |= m
-        S = (Fo | first[0 if uniform else ctx]) & cls[k]
+        Fo |= first[0 if uniform else ctx]
+        for c in ctr:                                  # entry -> count 1; stay while count < bound
+            p, bound, cnt = c
+            entry = (Fo >> p) & 1
+            stay = (S >> p) & 1 and cnt < bound
+            Fo |= stay << p
+            c[2] = 1 if entry else min(cnt + 1, bound)
+        S = Fo & cls[k]
         if anchored and not S:
             return False
         prevk = 1 if nk == 2 else 3 if nk == 5 else 2

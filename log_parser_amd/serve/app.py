@@ -429,6 +429,8 @@ class Service:
         if path == "/metrics" and method == "GET":
             if self._engine is not None:
                 self.metrics.set_frequency(self._engine.freq.statistics())
+                bt = self._engine.lib.host_bt
+                self.metrics.bt_exhausted = int(bt.exhausted) if bt is not None else 0
             return 200, "text/plain; version=0.0.4", self.metrics.render().encode()
         if path == "/admin/config" and method == "GET":
             return j(dict(self.config.values))

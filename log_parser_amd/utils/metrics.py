@@ -43,6 +43,7 @@ class Metrics:
         self.batches = 0
         self.batched_requests = 0
         self.device_failures = 0
+        self.bt_exhausted = 0          # backtracker finds that hit the step budget (counted "no match")
         self.freq: Dict[str, int] = {}
 
     def observe_request(self, code: int, seconds: float, nbytes: int):
@@ -83,7 +84,9 @@ class Metrics:
                     "# TYPE lp_batched_requests_total counter", f"lp_batched_requests_total {self.batched_requests}",
                     "# TYPE lp_batch_seconds histogram"]
             self.batch_latency.render("lp_batch_seconds", out)
-            out += ["# TYPE lp_device_failures_total counter", f"lp_device_failures_total {self.device_failures}"]
+            out += ["# TYPE lp_device_failures_total counter", f"lp_device_failures_total {self.device_failures}",
+                    "# TYPE lp_backtracker_budget_exhausted_total counter",
+                    f"lp_backtracker_budget_exhausted_total {self.bt_exhausted}"]
             out.append("# TYPE lp_pattern_frequency gauge")
             for k, v in sorted(self.freq.items()):
                 out.append(f'lp_pattern_frequency{{pattern_id="{k}"}} {v}')

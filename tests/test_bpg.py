@@ -66,7 +66,11 @@ def test_decomposition_is_exact_and_compact():
     for p in GAP_PATS[:3] + GAP_PATS[13:16]:
         d = N.compile_regex(p, 2048, 4096)
         assert d["kind"] == 1 and program_info(d["bpg"])["exceptions"] == 0, p
-    assert program_info(N.compile_regex(r"X.{0,1000}Y")["bpg"])["words"] == 16
+    # a bounded repeat of one class is ONE counted position; repeated groups stay expanded
+    info = program_info(N.compile_regex(r"X.{0,1000}Y")["bpg"])
+    assert info["words"] == 1 and info["counters"] == 1
+    info = program_info(N.compile_regex(r"X(?:a.){0,500}Y")["bpg"])
+    assert info["words"] == 16 and info["counters"] == 0
 
 
 @pytest.mark.parametrize("seed", [0, 1])
@@ -174,9 +178,9 @@ COOP_LIBS = [
     ([r"ab.{0,10}cd", r"x.{0,3}y", r"(a|bc)+d.{0,20}e", r"(?i)é.{0,3}z\B"], 8),
     (GAP_PATS[4:6], 64),
     (GAP_PATS[4:], 64),
-    (GAP_PATS[:13] + [r"a.{0,150}b", r"(?i)error.{0,220}\bdisk"], 64),
-    (GAP_PATS, 64),                                   # up to 16 words -> G = 32
-    ([r"a.{0,1500}b", r"(?m)^x$"], 64),               # 24 words -> G = 64
+    (GAP_PATS[:13] + [r"a(?:é.){0,75}b", r"(?i)error(?: .){0,110}\bdisk"], 64),
+    (GAP_PATS + [r"a(?:é.){0,400}b"], 64),            # up to 16 words -> G = 32 (+ counted gaps)
+    ([r"a(?:é.){0,700}b", r"(?m)^x$", r"a.{0,1500}b"], 64),   # 24 words -> G = 64
 ]
 
 
@@ -260,3 +264,68 @@ def test_bpg_candidate_walks_match_host(gpu_device, li):
                 assert fl[i] == (1 if (r, j) in want else 0), (r, j, listed)
             else:
                 assert fl[i] == 7
+
+
+# ---- counted positions: bounded repeats of one class at any bound (no 2,048-position cliff) ----
+CTR_PATS = [r"x{2,5000}", r"[^\n]{0,2500}FATAL", r"(?i)(err|warn).{0,2100}x", r"X.{0,3000}Y", r"X.{0,20000}Y",
+            r"a.{3,40}b", r"^.{0,20}é{5,50}", r"(?i)error.{0,30}tok.{0,30}retry", r"X.{0,17}Y", r"\bX.{0,16}\bY",
+            r"(?:q.{0,40})+Z", r"X[^\r]{0,50}(?m)$", r"X.{0,5000}Y.{0,2100}Z"]
+
+
+def _ctr_lines(rng, gap):
+    """Lines around the bound: k = gap-2 .. gap+2 characters between the anchors (ASCII and
+    2-byte code points), a younger re-entry past an expired older one, a line terminator inside
+    the gap, and random lines up to 2 x gap long."""
+    out = []
+    for k in range(gap - 2, gap + 3):
+        out += ["X" + "z" * k + "Y", "X" + "é" * k + "Y", "X" + "z" * (k + 5) + "X" + "z" * 10 + "Y",
+                "X" + "z" * (k // 2) + "\r" + "z" * (k // 2) + "Y", "a" + "q" * k + "b", "x" * min(k, 6000),
+                "err" + "." * k + "x", "é" * k + "FATAL", "X" + "z" * k + "Y" + "z" * 2000 + "Z"]
+    toks = ["X", "Y", "z", "é", "\r", " ", "FATAL", "err", "WARN", "x", "xx", "a", "b", "q", "1", "22", "error", "tok",
+            "retry", "Z", "日"]
+    for _ in range(12):
+        n = rng.randint(0, 2 * gap)
+        out.append("".join(rng.choice(toks) if rng.random() < 0.05 else "z" for _ in range(n)))
+    return out
+
+
+@pytest.mark.parametrize("gap", [2100, 5000, 20000])
+def test_counted_repeats_match_java_oracle(gap):
+    """Bounded repeats of any size compile to BPG programs (not the host backtracker) whose
+    native host twin -- and the Python twin on short lines -- give Java's find()."""
+    rng = random.Random(gap)
+    lines = _ctr_lines(rng, gap) + _lines(rng, 100)
+    for p in CTR_PATS:
+        d = N.compile_regex(p, 64, 4096)
+        assert d["kind"] == 1 and d["bpg"], (p, d["error"])
+        assert program_info(d["bpg"])["counters"] >= 1 and program_info(d["bpg"])["words"] <= 2, p
+        rx = compile_java(p)
+        for s in lines:
+            if "+Z" in p and len(s) > 400:
+                continue                    # (the oracle backtracks exponentially there)
+            want = rx.search(s) is not None
+            assert N.bpg_find(d["bpg"], s.encode()) == want, (p, len(s), s[:30])
+            if len(s) < 200:
+                assert run_program(d["bpg"], s.encode()) == want, (p, s)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gap", [2100, 5000, 20000])
+def test_counted_repeats_gpu_walks_match_host(gpu_device, gap):
+    """The one-lane scan walk (k_bpg_scan) and the cooperative candidate walk (k_bpg_coop) keep the
+    counts exactly as the host twin does, on lines longer than the bound."""
+    lib = _lib(CTR_PATS)
+    assert len(lib.bpg_regs) == len(CTR_PATS)
+    lines = _ctr_lines(random.Random(gap + 1), gap)
+    assert _scan(lib, lines, gpu_device) == _scan(lib, lines, torch.device("cpu"))
+    text, ls, ll = _text_dev(lines, gpu_device)
+    dfa = lib.device_tables(gpu_device)["dfa"]
+    progs = {r: lib.bpg_program(r).tobytes() for r in lib.bpg_regs}
+    cand = [(r << 32) | j for r in lib.bpg_regs for j in range(len(lines))]
+    ct = torch.tensor(cand, dtype=torch.int64, device=gpu_device)
+    N.bpg_cand_dev(ct.data_ptr(), ct.numel(), text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                   torch.cuda.current_stream().cuda_stream)
+    got = ct.cpu().tolist()
+    for before, after in zip(cand, got):
+        r, j = before >> 32, before & 0xFFFFFFFF
+        assert (after >= 0) == N.bpg_find(progs[r], lines[j].encode()), (lib.regexes[r].pattern, len(lines[j]))

@@ -883,15 +883,15 @@ PYBIND11_MODULE(_lpnative, m) {
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
                      double evict_before, double now, uint64_t stream, int64_t host_cap, Turn* turn, int64_t seq,
-                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> inj) {
-        const FreqRing R = ring_from(ring);
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> inj, SharedWindow* hw) {
+        const FreqRing R = hw ? FreqRing{} : ring_from(ring);
         const int D = (int)lo.shape(0);
         int64_t ne;
         {
           py::gil_scoped_release nogil;
           ne = r.run(P<uint8_t>(text), nbytes, P<const int64_t>(starts), P<const int32_t>(lens), L, lo.data(), hi.data(),
                      g0.data(), n.data(), D, R, evict_before, now, stream, host_cap, turn, seq,
-                     inj.size() ? inj.data() : nullptr, (int64_t)inj.size());
+                     inj.size() ? inj.data() : nullptr, (int64_t)inj.size(), hw);
         }
         py::array_t<uint8_t> out((py::ssize_t)r.result_bytes());
         std::memcpy(out.mutable_data(), r.result(), r.result_bytes());
@@ -903,7 +903,7 @@ PYBIND11_MODULE(_lpnative, m) {
       }, py::arg("text"), py::arg("nbytes"), py::arg("starts"), py::arg("lens"), py::arg("L"), py::arg("lo"),
          py::arg("hi"), py::arg("g0"), py::arg("n"), py::arg("ring"), py::arg("evict_before"), py::arg("now"),
          py::arg("stream"), py::arg("host_cap") = 0, py::arg("turn") = nullptr, py::arg("seq") = 0,
-         py::arg("inj") = py::array_t<int64_t>(0))
+         py::arg("inj") = py::array_t<int64_t>(0), py::arg("hw") = nullptr)
       .def_property_readonly("recorded", &RequestRunner::recorded)
       .def("upload_bytes", &RequestRunner::upload_bytes);
 
@@ -926,40 +926,41 @@ PYBIND11_MODULE(_lpnative, m) {
       .def_property_readonly("nproc", &ProcShared::nproc)
       .def_property_readonly("ticket", [](ProcShared& s) { return s.header()->ticket.load(); })
       .def_property_readonly("released_dead", [](ProcShared& s) { return s.header()->released_dead.load(); })
+      .def_property_readonly("sections", [](ProcShared& s) { return s.header()->sections.load(); })
+      .def_property("restarts", [](ProcShared& s) { return s.header()->restarts.load(); },
+                    [](ProcShared& s, int64_t v) { s.header()->restarts.store(v); })
       .def("mark_up", &ProcShared::mark_up)
       .def("up", &ProcShared::up)
-      .def_property("generation", [](ProcShared& s) { return s.win().generation.load(std::memory_order_acquire); },
-                    [](ProcShared& s, int64_t g) { s.win().generation.store(g, std::memory_order_release); })
-      .def_property("cap", [](ProcShared& s) { return s.win().cap; }, [](ProcShared& s, int64_t v) { s.win().cap = v; })
-      .def_property("tail_bound", [](ProcShared& s) { return s.win().tail_bound; },
-                    [](ProcShared& s, int64_t v) { s.win().tail_bound = v; })
-      .def_property("head_known", [](ProcShared& s) { return s.win().head_known; },
-                    [](ProcShared& s, int64_t v) { s.win().head_known = v; })
-      .def_property("last_now", [](ProcShared& s) { return s.win().last_now; },
-                    [](ProcShared& s, double v) { s.win().last_now = v; })
-      .def_property("block_bytes", [](ProcShared& s) { return s.win().block_bytes; },
-                    [](ProcShared& s, int64_t v) { s.win().block_bytes = v; })
-      .def_property("kind", [](ProcShared& s) { return s.win().kind; }, [](ProcShared& s, int v) { s.win().kind = v; })
-      .def_property("home_device", [](ProcShared& s) { return s.win().home_device; },
-                    [](ProcShared& s, int v) { s.win().home_device = v; })
-      .def_property("handle", [](ProcShared& s) { return py::bytes(reinterpret_cast<const char*>(s.win().handle), 64); },
-                    [](ProcShared& s, const std::string& h) {
-                      if (h.size() > 64) throw std::invalid_argument("handle longer than 64 bytes");
-                      std::memset(s.win().handle, 0, 64);
-                      std::memcpy(s.win().handle, h.data(), h.size());
-                    })
-      .def("host_block", [](py::object self, int64_t gen, int64_t bytes, bool create) {
-        ProcShared& s = self.cast<ProcShared&>();
-        void* p = s.host_block(gen, bytes, create);
-        return py::array(py::dtype("uint8"), {(py::ssize_t)bytes}, {(py::ssize_t)1}, p, self);
-      })
+      .def_property_readonly("generation", [](ProcShared& s) { return s.win().generation.load(std::memory_order_acquire); })
+      .def_property_readonly("cap", [](ProcShared& s) { return s.win().cap; })
+      .def_property_readonly("nkeys", [](ProcShared& s) { return s.win().nkeys; })
+      .def_property_readonly("window_s", [](ProcShared& s) { return s.win().window_s; })
+      .def_property_readonly("last_now", [](ProcShared& s) { return s.win().last_now; })
       .def_static("unlink", &ProcShared::unlink);
-  m.def("ipc_alloc", [](int device, int64_t bytes) {
-    auto r = ipc_alloc(device, bytes);
-    return py::make_tuple(r.first, py::bytes(r.second));
-  });
-  m.def("ipc_open", [](int device, const std::string& h) { return ipc_open(device, h); });
-  // a DLPack view (torch.from_dlpack) of raw memory: an IPC mapping of the shared window
+  // the node's shared frequency window in host shared memory (proc_shared.h): created by the
+  // first worker, attached by the others; every call but arrays() inside a window section
+  py::class_<SharedWindow>(m, "SharedWindow")
+      .def(py::init([](py::object shared, int nkeys, double window_s, bool create, int64_t capacity) {
+             return new SharedWindow(&shared.cast<ProcShared&>(), nkeys, window_s, create, capacity);
+           }), py::arg("shared"), py::arg("nkeys"), py::arg("window_s"), py::arg("create"),
+           py::arg("capacity") = int64_t(1) << 20, py::keep_alive<1, 2>())
+      .def("arrays", [](SharedWindow& w) {       // (t, key, cnt, ht, tot, seen) addresses + capacity
+        const WinArrays a = w.arrays();
+        return py::make_tuple(reinterpret_cast<uint64_t>(a.t), reinterpret_cast<uint64_t>(a.key),
+                              reinterpret_cast<uint64_t>(a.cnt), reinterpret_cast<uint64_t>(a.ht),
+                              reinterpret_cast<uint64_t>(a.tot), reinterpret_cast<uint64_t>(a.seen), a.cap);
+      })
+      .def("ensure_room", &SharedWindow::ensure_room)
+      .def("now", &SharedWindow::now)
+      .def("evict", &SharedWindow::evict)
+      .def("record", [](SharedWindow& w, uint64_t counts, int K, double now) {
+        w.ensure_room(K);
+        w.record(P<const int64_t>(counts), K, now);
+      })
+      .def("enter", [](SharedWindow& w) { py::gil_scoped_release nogil; return w.enter(); })
+      .def("leave", [](SharedWindow& w, int64_t seq) { py::gil_scoped_release nogil; w.leave(seq); })
+      .def_property_readonly("nkeys", &SharedWindow::nkeys);
+  // a DLPack view (torch.from_dlpack) of raw memory: the shared window's arrays
   m.def("dlpack", [](uint64_t ptr, int64_t numel, const std::string& dtype, int device) {
     return dlpack_capsule(ptr, numel, dtype, device);
   }, py::arg("ptr"), py::arg("numel"), py::arg("dtype"), py::arg("device"));

@@ -11,11 +11,11 @@
 #include <time.h>
 #include <unistd.h>
 
-#include <hip/hip_runtime_api.h>
-
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <stdexcept>
 #include <thread>
@@ -49,10 +49,6 @@ void* map_segment(const std::string& name, size_t bytes, bool create) {
   close(fd);
   if (p == MAP_FAILED) throw std::runtime_error("mmap(" + name + "): " + std::strerror(errno));
   return p;
-}
-
-void check(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in " + what);
 }
 
 }  // namespace
@@ -143,15 +139,21 @@ void ProcShared::lock() {
 void ProcShared::unlock() { pthread_mutex_unlock(&h_->mu); }
 
 int64_t ProcShared::take() {
+  lock();
   const int64_t s = h_->ticket.fetch_add(1, std::memory_order_acq_rel);
-  h_->owner[s % PROC_RING].store((int32_t)getpid(), std::memory_order_release);
+  ProcOwner& o = h_->owner[s % PROC_RING];
+  o.seq = s;                                 // (seq, pid) together under the mutex
+  o.pid = (int32_t)getpid();
+  unlock();
   return s;
 }
 
 bool ProcShared::owner_dead(int64_t seq) {
-  const int32_t pid = h_->owner[seq % PROC_RING].load(std::memory_order_acquire);
-  if (pid <= 0) return false;                // not taken yet: nobody to wait for
-  return kill(pid, 0) != 0 && errno == ESRCH;
+  lock();
+  const ProcOwner o = h_->owner[seq % PROC_RING];
+  unlock();
+  if (o.seq != seq || o.pid <= 0) return false;   // not taken yet (or an older ticket's slot)
+  return kill(o.pid, 0) != 0 && errno == ESRCH;
 }
 
 void ProcShared::mark_up(int worker, int32_t pid) {
@@ -175,40 +177,129 @@ void ProcShared::unlink(const std::string& name, int64_t max_gen) {
   shm_unlink(name.c_str());
 }
 
-// ---- GPU memory over IPC --------------------------------------------------------------------
-std::pair<uint64_t, std::string> ipc_alloc(int device, int64_t bytes) {
-  int cur = 0;
-  check(hipGetDevice(&cur), "get device");
-  check(hipSetDevice(device), "set device");
-  void* p = nullptr;
-  hipIpcMemHandle_t h;
-  try {
-    check(hipMalloc(&p, (size_t)bytes), "ipc window malloc");
-    check(hipMemset(p, 0, (size_t)bytes), "ipc window memset");
-    check(hipDeviceSynchronize(), "ipc window sync");
-    check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
-  } catch (...) {
-    if (p) (void)hipFree(p);
-    (void)hipSetDevice(cur);
-    throw;
+// ---- the window in host shared memory ------------------------------------------------------
+size_t SharedWindow::layout(int64_t cap, int K, size_t off[6]) {
+  const size_t isz[6] = {8, 4, 4, 8, 8, 1};
+  const size_t n[6] = {(size_t)cap, (size_t)cap, (size_t)cap, 2, (size_t)std::max(K, 1), (size_t)std::max(K, 1)};
+  size_t o = 0;
+  for (int i = 0; i < 6; ++i) {
+    off[i] = o;
+    o += (isz[i] * n[i] + 255) & ~size_t(255);
   }
-  (void)hipSetDevice(cur);
-  static_assert(sizeof(h) <= 64, "IPC handle fits the segment's slot");
-  return {reinterpret_cast<uint64_t>(p), std::string(reinterpret_cast<const char*>(&h), sizeof(h))};
+  return o;
 }
 
-uint64_t ipc_open(int device, const std::string& handle) {
-  hipIpcMemHandle_t h;
-  if (handle.size() < sizeof(h)) throw std::invalid_argument("short IPC handle");
-  std::memcpy(&h, handle.data(), sizeof(h));
-  int cur = 0;
-  check(hipGetDevice(&cur), "get device");
-  check(hipSetDevice(device), "set device");
-  void* p = nullptr;
-  const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
-  (void)hipSetDevice(cur);
-  check(e, "hipIpcOpenMemHandle");
-  return reinterpret_cast<uint64_t>(p);
+SharedWindow::SharedWindow(ProcShared* s, int nkeys, double window_s, bool create, int64_t capacity)
+    : s_(s), K_(std::max(nkeys, 1)) {
+  if (!create) return;
+  ProcWindowMeta& m = s_->win();
+  m.nkeys = K_;
+  m.window_s = window_s;
+  m.last_now = -std::numeric_limits<double>::infinity();
+  map_gen(1, std::max<int64_t>(capacity, 2 * K_), true);
+  m.generation.store(1, std::memory_order_release);     // published last: the block is complete
+}
+
+void SharedWindow::map_gen(int64_t gen, int64_t cap, bool create) {
+  size_t off[6];
+  const size_t bytes = layout(cap, K_, off);
+  auto* b = static_cast<uint8_t*>(s_->host_block(gen, (int64_t)bytes, create));
+  a_.t = reinterpret_cast<double*>(b + off[0]);
+  a_.key = reinterpret_cast<int32_t*>(b + off[1]);
+  a_.cnt = reinterpret_cast<int32_t*>(b + off[2]);
+  a_.ht = reinterpret_cast<int64_t*>(b + off[3]);
+  a_.tot = reinterpret_cast<int64_t*>(b + off[4]);
+  a_.seen = b + off[5];
+  a_.cap = cap;
+  gen_ = gen;
+  if (create) {
+    s_->win().cap = cap;
+    s_->win().block_bytes = (int64_t)bytes;
+  }
+}
+
+WinArrays SharedWindow::arrays() {
+  const int64_t g = s_->win().generation.load(std::memory_order_acquire);
+  if (g == 0) throw std::runtime_error("the shared frequency window has not been created yet");
+  if (g != gen_) map_gen(g, s_->win().cap, false);
+  return a_;
+}
+
+void SharedWindow::ensure_room(int64_t k) {
+  WinArrays a = arrays();
+  const int64_t h = a.ht[0], tl = a.ht[1], n = tl - h;
+  if (n + k <= a.cap) return;
+  // a new generation: the live records compacted to [0, n), totals and seen flags carried over
+  const int64_t cap = std::max<int64_t>(2 * a.cap, n + 2 * k);
+  const WinArrays old = a;
+  map_gen(gen_ + 1, cap, true);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t so = (h + i) % old.cap;
+    a_.t[i] = old.t[so];
+    a_.key[i] = old.key[so];
+    a_.cnt[i] = old.cnt[so];
+  }
+  std::memcpy(a_.tot, old.tot, sizeof(int64_t) * (size_t)K_);
+  std::memcpy(a_.seen, old.seen, (size_t)K_);
+  a_.ht[0] = 0;
+  a_.ht[1] = n;
+  s_->win().generation.store(gen_, std::memory_order_release);
+}
+
+double SharedWindow::now(double t) {
+  ProcWindowMeta& m = s_->win();
+  if (t > m.last_now) m.last_now = t;
+  return m.last_now;
+}
+
+void SharedWindow::evict(double horizon) {
+  WinArrays a = arrays();
+  int64_t h = a.ht[0];
+  while (h < a.ht[1] && a.t[h % a.cap] <= horizon) {
+    a.tot[a.key[h % a.cap]] -= a.cnt[h % a.cap];
+    ++h;
+  }
+  a.ht[0] = h;
+}
+
+void SharedWindow::record(const int64_t* counts, int K, double t) {
+  WinArrays a = arrays();
+  for (int k = 0; k < std::min(K, K_); ++k) {
+    const int64_t c = counts[k];
+    if (c <= 0) continue;
+    const int64_t sl = a.ht[1]++ % a.cap;       // room: ensure_room() before
+    a.t[sl] = t;
+    a.key[sl] = k;
+    a.cnt[sl] = (int32_t)c;
+    a.tot[k] += c;
+    a.seen[k] = 1;
+  }
+}
+
+int64_t SharedWindow::enter() {
+  const int64_t seq = s_->take();
+  try {
+    s_->host().wait(seq);
+    s_->dev().wait(seq);
+  } catch (...) {
+    leave(seq);
+    throw;
+  }
+  return seq;
+}
+
+void SharedWindow::leave(int64_t seq) {
+  s_->header()->sections.fetch_add(1, std::memory_order_relaxed);
+  s_->host().done(seq);
+  s_->dev().done(seq);
+}
+
+double SharedWindow::evict_carry(double t, int64_t* carry, int K) {
+  const double nw = now(t);
+  evict(nw - s_->win().window_s);
+  const WinArrays a = arrays();
+  std::memcpy(carry, a.tot, sizeof(int64_t) * (size_t)std::min(K, K_));
+  return nw;
 }
 
 }  // namespace lp

@@ -66,6 +66,7 @@ RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
 }
 
 RequestRunner::~RequestRunner() {
+  if (carry_host_) (void)hipHostFree(carry_host_);
   if (ws_) (void)hipFree(ws_);
   if (post_ws_) (void)hipFree(post_ws_);
   if (up_host_) (void)hipHostFree(up_host_);
@@ -91,7 +92,9 @@ int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
                            const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
                            int D, const FreqRing& ring, double evict_before, double now, uint64_t stream,
-                           int64_t host_cap, Turn* turn, int64_t seq, const int64_t* inj, int64_t ninj) {
+                           int64_t host_cap, Turn* turn, int64_t seq, const int64_t* inj, int64_t ninj,
+                           HostWindow* hw) {
+  if (hw && turn) throw std::invalid_argument("request runner: a host window or a turn, not both");
   // a shared window: released on every exit, also when a HIP call throws
   struct Release {
     Turn* t;
@@ -155,8 +158,8 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
 
   // window eviction first (FrequencyState.carry): the totals it leaves are this batch's carry --
   // inside the k_fetch launch when the inputs go up that way, else its own kernel
-  const bool evict_in_fetch = turn == nullptr && text_dev_src != nullptr && evict_in_fetch_;
-  if (!evict_in_fetch && turn == nullptr) freq_evict(ring, evict_before, stream, true);
+  const bool evict_in_fetch = turn == nullptr && hw == nullptr && text_dev_src != nullptr && evict_in_fetch_;
+  if (!evict_in_fetch && turn == nullptr && hw == nullptr) freq_evict(ring, evict_before, stream, true);
   // shared window: wait for the earlier batches' records, then evict (this batch's carry)
   bool in_window = turn == nullptr;
   auto enter_window = [&]() {
@@ -164,6 +167,34 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     turn->wait(seq);
     freq_evict(ring, evict_before, stream, true);
     in_window = true;
+  };
+
+  // host window (several serving processes): the arrival ticket is drawn once everything that does
+  // not read the window has FINISHED on the GPU; the section = host eviction + carry copy, the score
+  // kernel on the pinned carry, the results to the host, the host record. Left on every exit.
+  int64_t hw_seq = -1;
+  double hw_now = now;
+  struct Leave {
+    HostWindow* w;
+    int64_t* s;
+    ~Leave() { if (w && *s >= 0) w->leave(*s); }
+  } leave_guard{hw, &hw_seq};
+  const int K1w = std::max(S_.nkeys, 1);
+  if (hw && !carry_host_) {
+    check(hipHostMalloc(reinterpret_cast<void**>(&carry_host_), 8 * (size_t)K1w, kCoherentHost), "pinned carry");
+    carry_dev_ = device_view(carry_host_);
+  }
+  auto hw_enter = [&]() {
+    check(hipStreamSynchronize(st), "matching before the window section");
+    hw_seq = hw->enter();
+    hw_now = hw->evict_carry(now, carry_host_, K1w);
+  };
+  auto hw_leave = [&]() {
+    if (hw_seq >= 0) {
+      const int64_t q = hw_seq;
+      hw_seq = -1;
+      hw->leave(q);
+    }
   };
 
   RequestCounts c;
@@ -186,9 +217,20 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     ev_fkey = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(E, 1)));
     feat = dev((size_t)std::max<int64_t>(L, 1));
   };
-  // events, context features, frequency ranks into the results buffer, then the fused fp64
-  // score; `dcnt` = device [nh, ne] (device-count mode, E = capacity) or null (E = ne read back)
-  auto run_events = [&](int64_t E, int64_t nh_cap, const int64_t* dcnt) {
+  // events, context features, frequency ranks into the results buffer, then (with_score) the fused
+  // fp64 score; `dcnt` = device [nh, ne] (device-count mode, E = capacity) or null (E = ne read back)
+  auto run_score = [&](int64_t E, const int64_t* dcnt, const int64_t* tot) {
+    if (E <= 0) return;
+    double* score = reinterpret_cast<double*>(out);
+    int32_t* ev_line = reinterpret_cast<int32_t*>(out + 8 * (size_t)E + 8 * (size_t)K1);
+    ScoreTables T = S_.st;
+    T.seq_carry = seq_carry;
+    T.hit_off = hit_off; T.hit_line = hit_line; T.feat = feat;
+    T.seg_lo = dlo; T.seg_hi = dhi; T.seg_own_lo = dlo; T.seg_g0 = dg0; T.seg_n = dn;
+    const FreqIn F{ev_rank, ev_fkey, tot};
+    score_dev(ev_line, ev_line + E, ev_line + 2 * E, F, E, T, S_.sp, score, nullptr, stream, dcnt ? dcnt + 1 : nullptr);
+  };
+  auto run_events = [&](int64_t E, int64_t nh_cap, const int64_t* dcnt, bool with_score) {
     double* score = reinterpret_cast<double*>(out);
     int64_t* freq_counts = reinterpret_cast<int64_t*>(out + 8 * (size_t)E);
     int32_t* ev_line = reinterpret_cast<int32_t*>(out + 8 * (size_t)E + 8 * (size_t)K1);
@@ -209,14 +251,8 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, need);   // the stream is idle since the counter read
       events_dev(A, post_ws_, post_cap_, stream);
     }
-    if (E > 0) {
-      ScoreTables T = S_.st;
-      T.seq_carry = seq_carry;
-      T.hit_off = hit_off; T.hit_line = hit_line; T.feat = feat;
-      T.seg_lo = dlo; T.seg_hi = dhi; T.seg_own_lo = dlo; T.seg_g0 = dg0; T.seg_n = dn;
-      const FreqIn F{ev_rank, ev_fkey, ring.tot};
-      score_dev(ev_line, ev_pat, ev_seg, F, E, T, S_.sp, score, nullptr, stream, dcnt ? dcnt + 1 : nullptr);
-    }
+    (void)score; (void)ev_pat; (void)ev_seg;
+    if (with_score) run_score(E, dcnt, ring.tot);
     return freq_counts;
   };
 
@@ -317,9 +353,19 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, need);
       hits_dev(A, post_ws_, post_cap_, stream);
     }
-    if (fast) {
+    if (fast && hw) {
+      run_events(ecap_small, n, cnt + 3, false);
+      hw_enter();
+      run_score(ecap_small, cnt + 3, carry_dev_);
+      const size_t res = 20 * (size_t)ecap_small + 8 * (size_t)K1;
+      if (res > res_cap_) {
+        grow<true>(res_host_, res_cap_, res, kCoherentHost);
+        res_host_dev_ = device_view(res_host_);
+      }
+      publish_dev(cnt, out, ecap_small, (int)K1, cnt_host_dev_, res_host_dev_, stream);   // recorded on the host
+    } else if (fast) {
       enter_window();
-      int64_t* fc = run_events(ecap_small, n, cnt + 3);
+      int64_t* fc = run_events(ecap_small, n, cnt + 3, true);
       RecordGate G;
       G.cnt = cnt;
       G.cap[0] = cap_g; G.cap[1] = cap_c; G.cap[2] = cap_v; G.cap[3] = ecap_small;
@@ -338,7 +384,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
         res_bytes_ = res;
       }
     }
-    if (!(fast && publish_))
+    if (!(fast && (publish_ || hw)))
       check(hipMemcpyAsync(cnt_host_, cnt, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st), "counters D2H");
     check(hipStreamSynchronize(st), "counters");   // fast: the only host read; else the mid-batch one
     c.gram = cnt_host_[0]; c.cand = cnt_host_[1]; c.ver = cnt_host_[2];
@@ -355,12 +401,17 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     learn(rate_ver_, c.ver);
     if (fast) recorded_ = false;             // the gate held: nothing was recorded on this attempt
     if (ok && fast && ne <= ecap_small) {    // recorded through the gate; results already read
+      if (hw) {                              // the host record of the section (compacted results)
+        if (S_.nkeys > 0) hw->record_batch(reinterpret_cast<const int64_t*>(res_host_ + 8 * (size_t)ne), S_.nkeys, hw_now);
+        hw_leave();
+      }
       recorded_ = true;
       done = true;
-      stride = publish_ ? ne : ecap_small;
-      if (publish_) res_bytes_ = 20 * (size_t)ne + 8 * (size_t)K1;
+      stride = (publish_ || hw) ? ne : ecap_small;
+      if (publish_ || hw) res_bytes_ = 20 * (size_t)ne + 8 * (size_t)K1;
       break;
     }
+    hw_leave();                              // an overflowing attempt records nothing: next ticket
     if (ok && !fast) break;
     if (attempt > 8) throw std::runtime_error("request runner: matcher capacities did not converge");
   }
@@ -390,17 +441,30 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     }
     ws_used_ = base;
     carve_events(ne);
-    enter_window();
-    int64_t* fc = run_events(ne, nh, nullptr);
-    // this batch's per-key counts enter the window (after its own scoring: penalty before record)
-    if (S_.nkeys > 0) freq_record(fc, S_.nkeys, now, ring, stream, true);
-    recorded_ = true;
+    int64_t* fc;
+    if (hw) {
+      fc = run_events(ne, nh, nullptr, false);
+      hw_enter();
+      run_score(ne, nullptr, carry_dev_);
+    } else {
+      enter_window();
+      fc = run_events(ne, nh, nullptr, true);
+      // this batch's per-key counts enter the window (after its own scoring: penalty before record)
+      if (S_.nkeys > 0) freq_record(fc, S_.nkeys, now, ring, stream, true);
+      recorded_ = true;
+    }
     if (res > res_cap_) {
       grow<true>(res_host_, res_cap_, res, kCoherentHost);
       res_host_dev_ = device_view(res_host_);
     }
     check(hipMemcpyAsync(res_host_, out, res, hipMemcpyDeviceToHost, st), "results D2H");
     check(hipStreamSynchronize(st), "results");
+    if (hw) {
+      if (S_.nkeys > 0) hw->record_batch(reinterpret_cast<const int64_t*>(res_host_ + 8 * (size_t)ne), S_.nkeys, hw_now);
+      hw_leave();
+      recorded_ = true;
+    }
+    (void)fc;
     res_bytes_ = res;
     stride = ne;
   }

@@ -69,6 +69,22 @@ class WindowTurn : public Turn {
   std::set<int64_t> done_;
 };
 
+// A frequency window the runner does not own and that lives in HOST memory shared with the other
+// serving processes of the node (proc_shared.h SharedWindow). The runner draws the batch's
+// arrival ticket itself once the batch's matching, events, context features and frequency ranks
+// have FINISHED on its GPU (everything that does not read the window), so the section other
+// processes wait for is short: enter() -> evict + carry copy on the host -> score kernel (reads the
+// pinned carry) -> results to the host -> record_batch() -> leave().
+class HostWindow {
+ public:
+  virtual ~HostWindow() = default;
+  virtual int64_t enter() = 0;                                           // ticket + turns -> seq
+  virtual void leave(int64_t seq) = 0;
+  // in the section: now' = max(last record time, now); evict at now' - window; tot -> carry[K]
+  virtual double evict_carry(double now, int64_t* carry, int K) = 0;
+  virtual void record_batch(const int64_t* counts, int K, double now) = 0;   // in the section
+};
+
 struct RequestStatic {
   PfTables pf;
   DfaPool dfa;
@@ -112,10 +128,13 @@ class RequestRunner {
   // turn / seq: a shared window (WindowTurn above): the eviction moves from the start of the run to
   // the window section, entered through turn->wait(seq) once the matchers are queued and left
   // (turn->done(seq)) when the batch's record has completed -- also on errors.
+  // hw: the window is a HostWindow (`ring` unused): the runner takes the ticket itself once the
+  // carry-independent stages have finished, and records on the host (see HostWindow).
   int64_t run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
               const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0,
-              Turn* turn = nullptr, int64_t seq = 0, const int64_t* inj = nullptr, int64_t ninj = 0);
+              Turn* turn = nullptr, int64_t seq = 0, const int64_t* inj = nullptr, int64_t ninj = 0,
+              HostWindow* hw = nullptr);
   // the batch's frequency record was enqueued (a failure after it must not record the batch again)
   bool recorded() const { return recorded_; }
   // host bytes the single-copy upload needs (text padded, index, segments, counters, carry)
@@ -152,6 +171,8 @@ class RequestRunner {
   RequestCounts counts_;
   int64_t stride_ = 0;
   bool recorded_ = false;
+  int64_t* carry_host_ = nullptr;      // host window: the section's carry (pinned, device-visible)
+  int64_t* carry_dev_ = nullptr;
 };
 
 }  // namespace lp

@@ -223,9 +223,11 @@ class SharedWindowTurn:
 
 class ProcessWindowTurn(SharedWindowTurn):
     """The same two turns across the serving PROCESSES of a node (``serve/procs.py``): both live
-    in the shared segment (``N.ProcShared``: ``host`` / ``dev`` are ``N.ProcTurn``, which the native
-    request runner takes like ``N.WindowTurn``) and a batch's sequence number is its arrival ticket
-    there (``take``), drawn when the batch enters its device stage on whichever process."""
+    in the shared segment (``N.ProcShared``: ``host`` / ``dev`` are ``N.ProcTurn``) and a batch's
+    sequence number is its arrival ticket there (``take``). The ticket is drawn LATE: by the native
+    request runner once the batch's matching has finished on its GPU (``RequestRunner.run(hw=)``),
+    by the Python paths right before their window section -- never when the batch enters its
+    device stage, so no process waits on another's matching."""
 
     def __init__(self, shared):
         self.shared = shared
@@ -768,17 +770,24 @@ class Engine:
         if self.fault_after_record and job.number % self.fault_after_record == 0:
             raise RuntimeError("injected device fault after the frequency record (engine.fault-inject-after-record)")
 
-    def _device_batch(self, job: "BatchJob", turn=None, seq: int = 0) -> None:
+    def _device_batch(self, job: "BatchJob", turn=None, seq: Optional[int] = 0) -> None:
+        """``seq`` None (serving processes): the batch draws its arrival ticket from ``turn`` itself,
+        as late as its path allows, and releases it on every exit."""
         if job.whole:
             if turn is not None:
+                if seq is None:
+                    seq = turn.take()
                 turn.wait(seq)
-            doc = job.logs[0]
-            job.outs = [self.analyze_json(doc.decode() if isinstance(doc, N.RawLogs) else doc,
-                                          record=not job.recorded)]
-            job.recorded = True
-            if turn is not None:
-                self._window_quiet()
-                turn.done(seq)
+            try:
+                doc = job.logs[0]
+                job.outs = [self.analyze_json(doc.decode() if isinstance(doc, N.RawLogs) else doc,
+                                              record=not job.recorded)]
+                job.recorded = True
+                if turn is not None:
+                    self._window_quiet()
+            finally:
+                if turn is not None:
+                    turn.done(seq)
             return
         hb, ls_h, ll_h, dl, n = job.staged
         tm = job.tm
@@ -838,15 +847,21 @@ class Engine:
             if tm is not None:
                 self._tick(tm, "h2d", 0.0)
             prep = self.prepare(text, n, ls, ll, segs, host_text=hb[:n], timings=tm, host_index=(ls_h, ll_h))
+            if seq is None:                    # serving processes: the ticket once matching is queued
+                if self.device.type == "cuda":
+                    torch.cuda.current_stream(self.device).synchronize()
+                seq = turn.take()
             turn.wait(seq)                     # earlier batches have recorded their counts
-            res = self.finish(prep, segs, self._carry_before(job, prep, self.freq_carry()), with_factors=verbose)
-            with TR.HostTimer(tm, "d2h"):
-                job.ev = self._results_to_host(res)
-            if not job.recorded:
-                self.commit_frequency(job.ev[4])
-                job.recorded = True
-            self._window_quiet()               # the record has landed before later batches evict
-            turn.done(seq)
+            try:
+                res = self.finish(prep, segs, self._carry_before(job, prep, self.freq_carry()), with_factors=verbose)
+                with TR.HostTimer(tm, "d2h"):
+                    job.ev = self._results_to_host(res)
+                if not job.recorded:
+                    self.commit_frequency(job.ev[4])
+                    job.recorded = True
+                self._window_quiet()           # the record has landed before later batches evict
+            finally:
+                turn.done(seq)
         if verbose:
             self._log_events(res, dl)
         if tm is not None:
@@ -883,7 +898,9 @@ class Engine:
         if self._runner is False or tm is not None or verbose or job.n_lines < 0 or job.recorded:
             return False
         if self._runner is None:
-            ok = (self.device.type == "cuda" and self.freq_on_device
+            from .frequency import SharedFrequencyState
+            hostwin = isinstance(self.freq, SharedFrequencyState)      # serving processes' host window
+            ok = (self.device.type == "cuda" and (self.freq_on_device or hostwin)
                   and self.context_engine != "mfma" and bool(self.config.get("engine.native-runner", True))
                   and not any(g.numel() for g in self.tabs["nfa_scan_lists"].values()))
             if not ok:
@@ -903,14 +920,19 @@ class Engine:
                 bool(self.config.get("engine.runner-device-counts", True)))
         return True
 
-    def _run_native(self, job: "BatchJob", dl, n: int, turn: Optional[SharedWindowTurn] = None, seq: int = 0) -> None:
+    def _run_native(self, job: "BatchJob", dl, n: int, turn: Optional[SharedWindowTurn] = None,
+                    seq: Optional[int] = 0) -> None:
         """Engine.device_batch through N.RequestRunner: same kernels and order as prepare / finish
         (H2D, eviction, matchers, ONE counter read, events + features + ranks, score, record,
         ONE results read); the frequency state's host bookkeeping stays here, under its lock.
 
         With a shared window (``turn``): the bookkeeping runs in arrival order (``turn.host``) and
         only briefly; the runner queues its matchers, then enters the window section through
-        ``turn.dev`` -- engines on other GPUs / streams overlap everything but that section."""
+        ``turn.dev`` -- engines on other GPUs / streams overlap everything but that section.
+
+        The serving processes' host window (``SharedFrequencyState``): the runner itself draws the
+        arrival ticket once the batch's carry-independent stages have finished, and evicts / reads
+        the carry / records on the host inside its section (``RequestRunner.run(hw=...)``)."""
         lo, hi, g0, nn = Segments.doc_arrays(dl)
         fr = self.freq
         K = len(self.lib.freq_ids)
@@ -921,7 +943,15 @@ class Engine:
         inj = np.zeros(0, np.int64)
         if self.lib.host_plan:              # the backtracker's side path, on the pinned host bytes
             inj = self._host_keys(st.buf[:n].numpy(), n, st.starts(job.n_lines).numpy(), st.lens(job.n_lines).numpy())
-        if turn is None:
+        win = getattr(fr, "win", None)
+        if win is not None:                 # the node's host window (serving processes)
+            try:
+                ne, out, counts, E = self._runner.run(*args, (), 0.0, fr.clock(), stream, st.buf.numel(), inj=inj,
+                                                      hw=win)
+            except BaseException:
+                job.recorded = bool(self._runner.recorded)
+                raise
+        elif turn is None:
             with fr._lock:
                 if K:
                     fr._ensure_room(K)

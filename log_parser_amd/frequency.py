@@ -437,112 +437,68 @@ class MirroredFrequencyState(FrequencyState):
 
 
 class SharedFrequencyState(DeviceFrequencyState):
-    """ONE device-resident window shared by the serving PROCESSES of a node (one process per GPU,
+    """ONE window shared by the serving PROCESSES of a node (one process per GPU,
     ``serve/procs.py``) -- the reference's single process-global window
     (FrequencyTrackingService.java:25) kept across processes instead of across threads.
 
-    The ring, totals and head / tail live in one block of GPU memory on the window's home GPU,
-    allocated by the process that creates (or grows) it and mapped by the others through
-    ``hipIpcGetMemHandle`` / ``hipIpcOpenMemHandle`` (``N.ipc_alloc`` / ``N.ipc_open``; CPU engines
-    use a host shared-memory block instead). The host bookkeeping that ``DeviceFrequencyState``
-    keeps in attributes -- tail bound, known head, last record timestamp, capacity -- lives in the
-    shared segment (``N.ProcShared``), and is only touched inside the cross-process host turn,
-    exactly like the in-process ``SharedWindowTurn`` orders it between engines. A grown ring is a
-    new generation: the other processes re-map it at their next access (the turn orders that after
-    the growth; superseded blocks stay mapped until exit -- at most the final size again).
+    The window lives in HOST shared memory (``N.SharedWindow``, csrc/runtime/proc_shared.h): a ring
+    of (timestamp, key, count) records, in-window totals and seen flags per key, one block per
+    generation (a grown ring is a new block; the others re-map it at their next access). Whatever
+    GPU a process drives, its native request runner evicts, copies the carry and records on the host
+    inside the batch's window section, and its score kernel reads the carry from pinned memory
+    (``RequestRunner.run(hw=...)``): no GPU memory crosses processes, no peer access, and every
+    worker keeps the native runner. The section is entered with an arrival ticket drawn once the
+    batch's matching is DONE, so it holds no other process's matching.
 
-    The admin / snapshot API takes its own arrival ticket and runs between batches."""
+    CPU engines (and the Python paths of GPU engines) use the same window through the
+    ``DeviceFrequencyState`` API on host views of the shared arrays. The admin / snapshot API takes
+    its own ticket and runs between batches."""
 
-    def __init__(self, ids: List[str], window_hours: int, device, shared, clock: Callable[[], float] = time.time,
+    device_resident = False          # host memory: GPU engines reach it through the runner's host window
+
+    def __init__(self, ids: List[str], window_hours: int, shared, clock: Callable[[], float] = time.time,
                  capacity: int = 1 << 20, create: bool = False):
         import torch
+        from .native import N
         self.ids = list(ids)
         self.window_hours = window_hours
         self.window_s = float(window_hours) * 3600.0
         self.clock = clock
-        self.device = torch.device(device)
+        self.device = torch.device("cpu")
         self.sh = shared
         self._K = max(len(self.ids), 1)
         self._lock = threading.RLock()
         self._index = {pid: i for i, pid in enumerate(self.ids)}
-        self._gen = 0
-        self._views: tuple = ()
-        self._keep: list = []                 # mappings of every generation seen (kept until exit)
         self._tls = threading.local()
+        self._views: tuple = ()
+        self._base = 0
+        self._head_known = self._tail_bound = 0       # (DeviceFrequencyState bookkeeping: unused here)
         if create:
-            self._exclusive_enter()
+            seq = self.sh.take()                      # the first ticket: nothing runs before the window
             try:
-                self.sh.home_device = self._dev_index()
-                self.sh.last_now = float("-inf")
-                self._alloc(max(int(capacity), 2 * self._K))
+                self.sh.host.wait(seq)
+                self.sh.dev.wait(seq)
+                self.win = N.SharedWindow(shared, self._K, self.window_s, True, max(int(capacity), 2 * self._K))
             finally:
-                self._exclusive_exit()
-
-    # ---- shared host bookkeeping (DeviceFrequencyState attributes -> the segment)
-    _tail_bound = property(lambda s: s.sh.tail_bound, lambda s, v: setattr(s.sh, "tail_bound", int(v)))
-    _head_known = property(lambda s: s.sh.head_known, lambda s, v: setattr(s.sh, "head_known", int(v)))
-    _last_now = property(lambda s: s.sh.last_now, lambda s, v: setattr(s.sh, "last_now", float(v)))
-
-    @property
-    def cap(self) -> int:
-        return int(self.sh.cap)
-
-    def _dev_index(self) -> int:
-        return -1 if self.device.type != "cuda" else (self.device.index if self.device.index is not None else 0)
-
-    # ---- storage: one block per generation
-    def _layout(self, cap: int):
-        up = lambda n: (n + 255) & ~255  # noqa: E731
-        K = self._K
-        sizes = [("t", "float64", 8, cap), ("key", "int32", 4, cap), ("cnt", "int32", 4, cap),
-                 ("ht", "int64", 8, 2), ("tot", "int64", 8, K), ("seen", "uint8", 1, K)]
-        off, out = 0, []
-        for name, dt, isz, n in sizes:
-            out.append((name, dt, off, n))
-            off += up(isz * n)
-        return out, off
-
-    def _map(self, gen: int, create: bool, cap: int):
-        import torch
-        layout, nbytes = self._layout(cap)
-        dev = self._dev_index()
-        if dev < 0:
-            arr = self.sh.host_block(gen, nbytes, create)
-            self._keep.append(arr)
-            views = tuple(torch.from_numpy(arr[o:o + n * np.dtype(dt).itemsize].view(dt)) for _, dt, o, n in layout)
+                self.sh.host.done(seq)
+                self.sh.dev.done(seq)
         else:
-            from .native import N
-            if create:
-                base, handle = N.ipc_alloc(int(self.sh.home_device), nbytes)
-                self.sh.handle = handle
-            else:
-                base = N.ipc_open(dev, bytes(self.sh.handle))
-            self._keep.append(base)
-            views = tuple(torch.from_dlpack(N.dlpack(base + o, n, dt, dev)) for _, dt, o, n in layout)
-        if create:
-            self.sh.block_bytes = nbytes
-            self.sh.kind = 0 if dev < 0 else 1
-        return views
-
-    def _alloc(self, cap: int) -> None:
-        """A new generation (creation or growth; inside the host turn)."""
-        gen = int(self.sh.generation) + 1
-        old = self._current() if gen > 1 else None
-        self._views = self._map(gen, True, int(cap))
-        if old is not None:                           # totals / seen / head-tail carry over; the
-            for i in (3, 4, 5):                       # records are copied by _ensure_room
-                self._views[i].copy_(old[i])
-        self.sh.cap = int(cap)
-        self._gen = gen
-        self.sh.generation = gen                      # published last: the block is complete
-
-    def _current(self) -> tuple:
-        g = int(self.sh.generation)
-        if g != self._gen:
-            if g == 0:
+            if int(self.sh.generation) == 0:
                 raise RuntimeError("the shared frequency window has not been created yet")
-            self._views = self._map(g, False, self.cap)
-            self._gen = g
+            if int(self.sh.nkeys) != self._K:
+                raise RuntimeError(f"shared window has {self.sh.nkeys} keys, this library {self._K}")
+            self.win = N.SharedWindow(shared, self._K, self.window_s, False)
+
+    # ---- host views of the current generation
+    def _current(self) -> tuple:
+        import torch
+        from .native import N
+        a = self.win.arrays()                         # re-maps after a growth
+        if a[0] != self._base:
+            cap, K = int(a[6]), self._K
+            spec = [("float64", cap), ("int32", cap), ("int32", cap), ("int64", 2), ("int64", K), ("uint8", K)]
+            self._views = tuple(torch.from_dlpack(N.dlpack(int(ptr), n, dt, -1)) for ptr, (dt, n) in zip(a[:6], spec))
+            self._base = a[0]
         return self._views
 
     t = property(lambda s: s._current()[0])
@@ -552,28 +508,51 @@ class SharedFrequencyState(DeviceFrequencyState):
     tot = property(lambda s: s._current()[4])
     seen = property(lambda s: s._current()[5])
 
+    @property
+    def cap(self) -> int:
+        return int(self.win.arrays()[6])
+
+    _last_now = property(lambda s: s.sh.last_now, lambda s, v: s.win.now(float(v)))
+
+    def _alloc(self, cap: int) -> None:
+        raise NotImplementedError("the shared window grows in N.SharedWindow.ensure_room")
+
+    def _ensure_room(self, k: int, quiesce: Optional[Callable[[], None]] = None) -> None:
+        self.win.ensure_room(int(k))
+
+    def _now(self, now: Optional[float] = None) -> float:
+        return self.win.now(self.clock() if now is None else float(now))
+
+    # ---- the window section's steps (the caller holds the turns)
+    def carry_tensor(self, now: Optional[float] = None):
+        with self._lock:
+            self.win.evict(self._now(now) - self.window_s)
+            return self.tot
+
+    def record_tensor(self, counts, now: Optional[float] = None, veto=None) -> None:
+        import torch
+        K = len(self.ids)
+        if K == 0 or (veto is not None and int(veto.item())):
+            return
+        c = counts.to(device="cpu", dtype=torch.int64).contiguous()
+        if c.numel() < K:
+            c = torch.cat([c, torch.zeros(K - c.numel(), dtype=torch.int64)])
+        with self._lock:
+            self.win.record(c.data_ptr(), K, self._now(now))
+
     # ---- the admin API runs between batches, under an arrival ticket of its own
     def _exclusive_enter(self) -> None:
         d = getattr(self._tls, "depth", 0)
         self._tls.depth = d + 1
         if d:
             return
-        seq = self.sh.take()
-        self._tls.seq = seq
-        self.sh.host.wait(seq)
-        self.sh.dev.wait(seq)
+        self._tls.seq = self.win.enter()
 
     def _exclusive_exit(self) -> None:
         self._tls.depth -= 1
         if self._tls.depth:
             return
-        try:
-            if self.device.type == "cuda":
-                import torch
-                torch.cuda.current_stream(self.device).synchronize()
-        finally:
-            self.sh.host.done(self._tls.seq)
-            self.sh.dev.done(self._tls.seq)
+        self.win.leave(self._tls.seq)
 
     def _exclusive(self, fn, *a):
         self._exclusive_enter()

@@ -172,7 +172,7 @@ class Batcher:
                 if self.pipe is not None:
                     outs = self.pipe.run_inline([b[0] for b in batch])      # observes the batch
                 else:
-                    outs = self.analyze(eng, [b[0] for b in batch], seq)
+                    outs = self.analyze(eng, [b[0] for b in batch], None if self.proc else seq)
                     self.metrics.observe_batch(len(batch), time.perf_counter() - t0)
                 for (_, fut, _), o in zip(batch, outs):
                     fut.set_result(o)
@@ -199,21 +199,19 @@ class Batcher:
 
     def device_stage(self, job, eng: Optional[Engine] = None, seq: int = 0) -> None:
         """Pipeline device stage with the same CPU fallback as ``analyze``. Several serving
-        processes: the batch's arrival ticket is drawn here and released on every exit."""
+        processes: the batch draws its arrival ticket itself, late (``seq`` None: the native runner
+        once its matching is done, the Python paths right before their window section), and
+        releases it on every exit."""
         eng = eng or self.engine
         if self.proc:
-            seq = self.turn.take()
+            seq = None
         try:
-            try:
-                eng.device_batch(job, self.turn, seq)
-            except Exception:  # noqa: BLE001
-                if not self.fallback_cpu:
-                    raise
-                log.exception("device batch failed; serving it from the CPU backend")
-                job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq, record=not job.recorded)
-        finally:
-            if self.proc:
-                self.turn.done(seq)
+            eng.device_batch(job, self.turn, seq)
+        except Exception:  # noqa: BLE001
+            if not self.fallback_cpu:
+                raise
+            log.exception("device batch failed; serving it from the CPU backend")
+            job.outs = self._cpu(eng).analyze_batch_json(job.logs, self.turn, seq, record=not job.recorded)
 
     def _cpu(self, eng: Engine) -> Engine:
         """The CPU backend for one failed batch. A device-resident window is not touched by it
@@ -233,7 +231,7 @@ class Batcher:
                 self._cpu_engine = cpu
             return cpu
 
-    def analyze(self, eng: Engine, logs: List[str], seq: int) -> List[bytes]:
+    def analyze(self, eng: Engine, logs: List[str], seq: Optional[int]) -> List[bytes]:
         """GPU batch; on a device failure (HIP error, OOM, lost device) serve the batch from the CPU
         backend — same library tables, a host copy of the frequency window — for availability only
         (SURVEY §5.3), and report it in /metrics. A batch whose counts already entered the window

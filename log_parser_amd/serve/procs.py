@@ -10,17 +10,25 @@ thread and pack / device / emit pipeline, its own GPU (``engine.serve-devices[i 
 shares between its request threads: ONE sliding frequency window (FrequencyTrackingService.java:25
 one map, :41-56 record) with penalty-before-record in arrival order (ScoringService.java:84-88):
 
-* worker 0 allocates the window in its GPU's HBM and publishes an IPC handle
-  (``hipIpcGetMemHandle``); the others map it (``hipIpcOpenMemHandle``) -- ``SharedFrequencyState``;
-* a batch draws an arrival ticket from the segment when it enters its device stage; its window
-  section (eviction, score with the in-window carry, record) runs after every earlier ticket's,
-  whichever process holds them (``ProcessWindowTurn``: cross-process turns on a futex). Matching
-  runs before the turn, concurrently on every process.
+* the window lives in host shared memory (``SharedFrequencyState`` over ``N.SharedWindow``),
+  created by the first worker; every worker's native request runner evicts, copies the carry and
+  records on the host inside its batch's window section, and its score kernel reads the pinned
+  carry -- so the runner serves on every GPU, with no IPC of GPU memory and no peer access;
+* a batch draws its arrival ticket once its MATCHING IS DONE (inside the runner, after the events,
+  context features and ranks have finished on its GPU); its window section (eviction, score with
+  the in-window carry, record) runs after every earlier ticket's, whichever process holds them
+  (cross-process turns on a futex). Matching overlaps freely across processes and GPUs.
 
 So requests sent one after another get exactly the responses one process gives, and concurrent
-ones the responses of SOME arrival order, as in the reference. A worker that dies releases nothing
-by itself: the others release its tickets after they find its pid gone (ProcTurn::wait), and the
-supervisor stops the whole group with the first failing worker's status.
+ones the responses of SOME arrival order, as in the reference.
+
+Failures: a worker that dies holding a ticket has it released by the others once they find its pid
+gone (``ProcTurn::wait``), and the SURVIVORS KEEP SERVING (SO_REUSEPORT sends new connections to the
+live listeners). The supervisor restarts a dead worker on the same device (``server.max-restarts``
+per worker; the restarted process attaches to the existing window) and stops the group only when a
+worker has exhausted its restarts or exits during start-up. A record the dead worker had half
+applied stays as it is -- as a reference request thread that dies mid-request leaves the
+``recordPatternMatch`` calls it already made (ScoringService.java:84-88, per match).
 """
 from __future__ import annotations
 
@@ -36,18 +44,18 @@ from ..utils.config import Config
 
 log = logging.getLogger("log_parser_amd.server")
 
-ENV_SHM, ENV_WORKER, ENV_NPROC, ENV_WINDOW = "LP_SERVE_SHM", "LP_SERVE_WORKER", "LP_SERVE_NPROC", "LP_SERVE_WINDOW"
+ENV_SHM, ENV_WORKER, ENV_NPROC = "LP_SERVE_SHM", "LP_SERVE_WORKER", "LP_SERVE_NPROC"
 
 
 class WorkerContext:
     """This process's place in a serving group (built from the supervisor's environment)."""
 
-    def __init__(self, shared, index: int, nproc: int, window: str = "device"):
+    def __init__(self, shared, index: int, nproc: int):
         self.shared = shared
         self.index = index
         self.nproc = nproc
-        self.owner = index == 0
-        self.window = window            # "device" or "host" (decided by the supervisor for all)
+        # the first worker creates the window; a restarted one (generation > 0) attaches to it
+        self.owner = index == 0 and int(shared.generation) == 0
 
     @staticmethod
     def from_env() -> Optional["WorkerContext"]:
@@ -55,41 +63,21 @@ class WorkerContext:
         if not name:
             return None
         from ..native import N
-        return WorkerContext(N.ProcShared(name, False), int(os.environ[ENV_WORKER]), int(os.environ[ENV_NPROC]),
-                             os.environ.get(ENV_WINDOW, "device"))
+        return WorkerContext(N.ProcShared(name, False), int(os.environ[ENV_WORKER]), int(os.environ[ENV_NPROC]))
 
     def frequency_state(self, lib, cfg: Config):
-        """The shared window: created by worker 0 (on its device), mapped by the others once
-        worker 0 reports it ready (after a snapshot restore, if any)."""
-        import torch
-        from ..engine import resolve_device
+        """The shared window: created by the first worker (after which it restores a snapshot, if
+        configured), attached by the others once it exists."""
         from ..frequency import SharedFrequencyState
-        dev = resolve_device(str(cfg["engine.device"]))
         hours = cfg.scoring.freq_window_hours
-        host = self.window == "host" or dev.type != "cuda"
-        wdev = torch.device("cpu") if host else dev
         if self.owner:
-            st = SharedFrequencyState(lib.freq_ids, hours, wdev, self.shared, create=True)
-            return self._placed(st, host, dev)
+            return SharedFrequencyState(lib.freq_ids, hours, self.shared, create=True)
         deadline = time.monotonic() + 600
-        while not self.shared.up(0):
+        while not self.shared.up(0) or int(self.shared.generation) == 0:
             if time.monotonic() > deadline:
                 raise RuntimeError("serving worker 0 never created the shared frequency window")
             time.sleep(0.01)
-        if not host:
-            from ..native import N
-            me = dev.index if dev.index is not None else torch.cuda.current_device()
-            if me != self.shared.home_device and not N.enable_peer_access(me, self.shared.home_device):
-                raise RuntimeError(f"no peer access from {dev} to the window's GPU {self.shared.home_device}")
-        return self._placed(SharedFrequencyState(lib.freq_ids, hours, wdev, self.shared, create=False), host, dev)
-
-    @staticmethod
-    def _placed(st, host: bool, dev):
-        if host and dev.type == "cuda":
-            # a GPU engine over the host window: it reads the carry and records counts through the
-            # host (Engine.freq_on_device False), as with an engine-private host FrequencyState
-            st.device_resident = False
-        return st
+        return SharedFrequencyState(lib.freq_ids, hours, self.shared, create=False)
 
     def window_ready(self) -> None:
         self.shared.mark_up(self.index, os.getpid())
@@ -114,18 +102,6 @@ def worker_devices(cfg: Config, n: int) -> List[str]:
     return [devs[i % len(devs)] for i in range(n)]
 
 
-def window_placement(cfg: Config, devs: Sequence[str]) -> str:
-    """``server.window``: "device" / "host", or auto -- device when every worker is on one GPU or
-    ``engine.serve.peer-window`` is on (workers on other GPUs then map worker 0's HBM over xGMI, a
-    path no multi-GPU run has pinned yet), else host."""
-    w = str(cfg.get("server.window", "auto") or "auto")
-    if w in ("device", "host"):
-        return w
-    if len(set(devs)) <= 1 or bool(cfg.get("engine.serve.peer-window", False)):
-        return "device"
-    return "host"
-
-
 def _worker_argv(argv: Sequence[str], device: str) -> List[str]:
     keep = [a for a in argv if not a.startswith(("-Dserver.processes=", "-Dengine.device=",
                                                   "-Dengine.serve-devices="))]
@@ -134,29 +110,41 @@ def _worker_argv(argv: Sequence[str], device: str) -> List[str]:
 
 
 def run_processes(argv: Sequence[str], cfg: Config, n: int, stop=None, ready_timeout_s: float = 900.0) -> int:
-    """Supervisor: the shared segment, ``n`` workers, their exit status. ``stop`` (an Event):
-    set to stop the group (signals set it in ``serve.__main__``)."""
+    """Supervisor: the shared segment, ``n`` workers (restarted when they die), their exit status.
+    ``stop`` (an Event): set to stop the group (signals set it in ``serve.__main__``)."""
     from ..native import N
     name = f"/lp-serve-{os.getpid()}-{int(time.time() * 1e3) % 100000}"
     shared = N.ProcShared(name, True, n)
     procs: List[subprocess.Popen] = []
     devs = worker_devices(cfg, n)
-    window = window_placement(cfg, devs)
-    log.info("%d serving processes on %s, %s frequency window", n, devs, window)
+    max_restarts = int(cfg.get("server.max-restarts", 3) or 0)
+    restarts = [0] * n
+    log.info("%d serving processes on %s, one host frequency window", n, devs)
+
+    def spawn(i: int) -> subprocess.Popen:
+        env = dict(os.environ)
+        env.update({ENV_SHM: name, ENV_WORKER: str(i), ENV_NPROC: str(n)})
+        return subprocess.Popen([sys.executable] + _worker_argv(argv, devs[i]), env=env)
     try:
-        for i, dev in enumerate(devs):
-            env = dict(os.environ)
-            env.update({ENV_SHM: name, ENV_WORKER: str(i), ENV_NPROC: str(n), ENV_WINDOW: window})
-            procs.append(subprocess.Popen([sys.executable] + _worker_argv(argv, dev), env=env))
+        for i in range(n):
+            procs.append(spawn(i))
         t0, announced = time.monotonic(), False
         while True:
             codes = [p.poll() for p in procs]
-            bad = [c for c in codes if c not in (None, 0)]
-            if bad:
-                log.error("a serving worker exited with status %s: stopping the group", bad[0])
-                return bad[0]
             if all(c == 0 for c in codes):
                 return 0
+            for i, c in enumerate(codes):
+                if c in (None, 0):
+                    continue
+                if not announced or restarts[i] >= max_restarts:
+                    log.error("serving worker %d exited with status %s (%s): stopping the group", i, c,
+                              "during start-up" if not announced else f"after {restarts[i]} restarts")
+                    return c
+                restarts[i] += 1
+                shared.restarts = int(shared.restarts) + 1
+                log.error("serving worker %d exited with status %s: restarting it (%d/%d); the others keep serving",
+                          i, c, restarts[i], max_restarts)
+                procs[i] = spawn(i)
             if not announced and all(shared.up(i) for i in range(n)):
                 announced = True
                 log.info("%d serving processes up (%.1f s)", n, time.monotonic() - t0)

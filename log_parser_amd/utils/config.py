@@ -110,14 +110,12 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.io-threads": (0, int),
     # serving processes (serve/procs.py): 1 = this process only; N > 1 = N processes started before
     # any GPU call, each with its own SO_REUSEPORT listeners, GIL and pipeline, sharing ONE
-    # frequency window (GPU memory over IPC) in arrival-ticket order; -1 = one per visible GPU.
+    # frequency window (host shared memory) in arrival-ticket order; -1 = one per visible GPU.
     # Process i serves on engine.serve-devices[i % n] (or engine.device when that is empty)
     "server.processes": (1, int),
-    # where the serving processes' shared frequency window lives: "device" (HBM of worker 0's GPU,
-    # IPC-mapped by the others; kernels read / record it in place), "host" (a shared-memory block;
-    # the engines read the carry and record counts through the host, without the native runner) or
-    # "auto": device when every worker is on one GPU or engine.serve.peer-window is on, else host
-    "server.window": ("auto", str),
+    # serving processes: restarts of one dead worker before the supervisor stops the group (the
+    # others keep serving meanwhile)
+    "server.max-restarts": (3, int),
     # single-GPU service: bind the process to the CPUs of the GPU's NUMA node (serve/__main__.py)
     "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)

@@ -1,9 +1,10 @@
 """Node-scale serving over processes (serve/procs.py, csrc/runtime/proc_shared.cpp): arrival tickets
-and cross-process turns in shared memory, ONE frequency window mapped by every serving process
-(SharedFrequencyState; host shared memory for CPU engines, GPU memory over IPC on the device), and
-the supervisor + SO_REUSEPORT workers end to end: serial requests over fresh connections give
-exactly the responses of the sequential reference (golden model, one frequency tracker) --
-FrequencyTrackingService.java:25 one window for every request, ScoringService.java:84-88."""
+and cross-process turns in shared memory, ONE frequency window in host shared memory used by every
+serving process (SharedFrequencyState over N.SharedWindow; GPU workers reach it through the native
+request runner's host-window section), and the supervisor + SO_REUSEPORT workers end to end: serial
+requests over fresh connections give exactly the responses of the sequential reference (golden
+model, one frequency tracker) -- FrequencyTrackingService.java:25 one window for every request,
+ScoringService.java:84-88 -- also across a worker's death and restart."""
 import http.client
 import json
 import multiprocessing as mp
@@ -94,7 +95,7 @@ def _window_worker(name, ids, plan, out_q):
     sh = N.ProcShared(name, False)
     while not sh.up(0):
         time.sleep(0.01)
-    fs = SharedFrequencyState(ids, 1, "cpu", sh, create=False)
+    fs = SharedFrequencyState(ids, 1, sh, create=False)
     res = []
     for seq, counts, now in plan:
         while sh.ticket < seq:           # draw exactly the ticket of this plan entry
@@ -110,14 +111,14 @@ def _window_worker(name, ids, plan, out_q):
 
 
 def test_shared_window_across_processes_matches_one_window():
-    """Two processes record into and read from ONE window (host shared memory here), interleaved
-    by ticket, with a small ring that has to grow (new generation, re-mapped by the other
-    process): every carry equals a single-process FrequencyState fed in ticket order."""
+    """Two processes record into and read from ONE window (host shared memory), interleaved by
+    ticket, with a small ring that has to grow (new generation, re-mapped by the other process):
+    every carry equals a single-process FrequencyState fed in ticket order."""
     name = _name("win")
     sh = N.ProcShared(name, True, 2)
     ids = [f"k{i}" for i in range(7)]
     try:
-        own = SharedFrequencyState(ids, 1, "cpu", sh, create=True, capacity=16)
+        own = SharedFrequencyState(ids, 1, sh, create=True, capacity=16)
         sh.mark_up(0, os.getpid())
         rng = np.random.default_rng(5)
         b = sh.ticket                             # (creating the window took one ticket)
@@ -179,60 +180,66 @@ def test_two_serving_processes_equal_serial_reference(tmp_path):
     another, each on a fresh connection (the kernel spreads them over both processes), get the
     golden model's responses with ONE frequency tracker -- the penalty of every request sees the
     counts recorded by the other process."""
-    _serve_two(tmp_path, "cpu")
+    _serve(tmp_path, "cpu", 2)
+
+
+def test_four_serving_processes_equal_serial_reference(tmp_path):
+    _serve(tmp_path, "cpu", 4, n_req=28)
 
 
 @pytest.mark.gpu
-def test_two_gpu_serving_processes_equal_serial_reference(tmp_path):
-    """The same with both workers on cuda:0 (the one-GPU rehearsal of one process per GPU): the
-    window lives in worker 0's HBM, worker 1 maps it over IPC, both serve through the native
-    request runner inside the cross-process turns."""
-    _serve_two(tmp_path, "cuda:0", n_req=40)
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_gpu_serving_processes_equal_serial_reference(tmp_path, nproc):
+    """The same with every worker on cuda:0 (the one-GPU rehearsal of one process per GPU): the
+    window is host shared memory, each worker's native request runner evicts / reads the carry /
+    records it inside its window section (ticket drawn after its matching) -- /ready reports the
+    native runner in EVERY worker, and the responses equal the golden model's (rtol 1e-12)."""
+    _serve(tmp_path, "cuda:0", nproc, n_req=40)
 
 
-@pytest.mark.gpu
-def test_two_gpu_serving_processes_host_window(tmp_path):
-    """server.window=host (the placement for workers on GPUs without a pinned peer path): GPU
-    engines over the shared-memory window, carry and counts through the host -- same responses."""
-    _serve_two(tmp_path, "cuda:0", n_req=30, extra=["-Dserver.window=host"], runner=False)
+def test_worker_death_survivors_serve_and_restart(tmp_path):
+    """A worker killed with SIGKILL: the survivors keep answering (golden responses, the window
+    intact), the supervisor restarts the dead worker on the same device, the new process attaches
+    to the existing window and serves too."""
+    _serve(tmp_path, "cpu", 2, n_req=16, kill_after=6)
 
 
-def test_window_placement():
-    from log_parser_amd.serve.procs import window_placement
-    from log_parser_amd.utils.config import Config
-    c = Config.load()
-    assert window_placement(c, ["cuda:0", "cuda:0"]) == "device"
-    assert window_placement(c, ["cuda:0", "cuda:1"]) == "host"
-    assert window_placement(Config.load(overrides={"engine.serve.peer-window": True}), ["cuda:0", "cuda:1"]) == "device"
-    assert window_placement(Config.load(overrides={"server.window": "host"}), ["cuda:0", "cuda:0"]) == "host"
+def _ready_pids(port, want, deadline_s=240, sup=None, log=None):
+    pids = set()
+    deadline = time.monotonic() + deadline_s
+    while len(pids) < want:                    # every worker answers (each reports its pid)
+        if sup is not None:
+            assert sup.poll() is None, log.read_text()[-3000:] if log else ""
+        assert time.monotonic() < deadline, "workers did not come up"
+        try:
+            st, body = _get(port, "/ready")
+            if st == 200:
+                pids.add(json.loads(body)["worker"]["pid"])
+        except OSError:
+            time.sleep(0.2)
+    return pids
 
 
-def _serve_two(tmp_path, device, n_req=24, extra=(), runner=True):
+def _serve(tmp_path, device, nproc, n_req=24, extra=(), kill_after=None):
     sets, trig = make_library(20, seed=91)
     for i, s in enumerate(sets):
         (tmp_path / f"lib{i}.yaml").write_text(yaml.safe_dump(s.model_dump(by_alias=True, exclude_none=True)))
     port = free_port()
     cmd = [sys.executable, "-m", "log_parser_amd.serve", f"-Dpattern.directory={tmp_path}", f"-Dengine.device={device}",
-           "-Dserver.processes=2", f"-Dserver.port={port}", "-Dserver.host=127.0.0.1",
+           f"-Dserver.processes={nproc}", f"-Dserver.port={port}", "-Dserver.host=127.0.0.1",
            "-Dscoring.frequency.threshold=1.0", "-Dserver.numa-bind=false"] + list(extra)
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     logf = open(tmp_path / "serve.log", "wb")
     sup = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=logf)
     try:
-        pids = set()
-        deadline = time.monotonic() + 240
-        while len(pids) < 2:                    # both workers answer (each reports its pid)
-            assert sup.poll() is None, (tmp_path / "serve.log").read_text()[-3000:]
-            assert time.monotonic() < deadline, "workers did not come up"
-            try:
-                st, body = _get(port, "/ready")
-                if st == 200:
-                    pids.add(json.loads(body)["worker"]["pid"])
-            except OSError:
-                time.sleep(0.2)
+        pids = _ready_pids(port, nproc, sup=sup, log=tmp_path / "serve.log")
         params = ScoringParams(freq_threshold=1.0)
         tracker = golden.FrequencyTracker(params)
         for i in range(n_req):
+            if kill_after is not None and i == kill_after:
+                victim = sorted(pids)[-1]
+                os.kill(victim, signal.SIGKILL)        # idle: it holds no ticket
+                time.sleep(0.5)
             logs = make_log(150 + 31 * (i % 4), trig, seed=700 + i, hit_rate=0.12)
             st, out = _post(port, json.dumps({"pod": {"metadata": {"name": f"p{i}"}}, "logs": logs}).encode())
             assert st == 200
@@ -241,12 +248,16 @@ def _serve_two(tmp_path, device, n_req=24, extra=(), runner=True):
             assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o["events"]] == \
                    [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]], i
             assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
-        if device != "cpu":                 # both workers served (through the native runner on a device window)
+        if kill_after is not None:             # the dead worker was restarted and attached to the window
+            now = _ready_pids(port, nproc, sup=sup, log=tmp_path / "serve.log")
+            assert victim not in now
+            assert b"restarting it" in (tmp_path / "serve.log").read_bytes()
+        if device != "cpu":                 # every worker serves through the native runner (host window)
             seen = {}
-            for _ in range(40):
+            for _ in range(20 * nproc):
                 r = json.loads(_get(port, "/ready")[1])
                 seen[r["worker"]["pid"]] = r["nativeRunner"]
-            assert len(seen) == 2 and all(v == runner for v in seen.values()), seen
+            assert len(seen) == nproc and all(seen.values()), seen
         # the admin API reads the one window from either process
         stats = [json.loads(_get(port, "/admin/frequency")[1]) for _ in range(4)]
         assert all(s == stats[0] for s in stats) and sum(stats[0].values()) > 0
@@ -258,3 +269,45 @@ def _serve_two(tmp_path, device, n_req=24, extra=(), runner=True):
             sup.kill()
             sup.wait()
         logf.close()
+
+
+@pytest.mark.parametrize("dev", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+def test_engines_over_host_window_equal_golden(dev):
+    """Two GPU engines (as two serving processes would) over ONE host shared window: every batch
+    runs through the native request runner's host-window section -- ticket after the matching,
+    host eviction + pinned carry, score kernel, host record -- and the responses equal the golden
+    model with one tracker (rtol 1e-12), alternating engines batch by batch. On CPU: the Python
+    path's late ticket over the same window."""
+    from log_parser_amd.engine import Engine, ProcessWindowTurn
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.utils.config import Config
+    name = _name("hw")
+    sh = N.ProcShared(name, True, 2)
+    try:
+        sets, trig = make_library(30, seed=93, sequence_rate=0.6)
+        params = ScoringParams(freq_threshold=1.0)
+        lib = CompiledLibrary(sets, params)
+        fs = [SharedFrequencyState(lib.freq_ids, 1, sh, create=True)]
+        fs.append(SharedFrequencyState(lib.freq_ids, 1, sh, create=False))
+        cfg = Config.load(overrides={"engine.device": dev})
+        engs = [Engine(lib, cfg, device=torch.device(dev), freq=f) for f in fs]
+        turn = ProcessWindowTurn(sh)
+        tracker = golden.FrequencyTracker(params)
+        s0 = int(sh.sections)
+        for i in range(14):
+            docs = [make_log(120 + 17 * (i % 3), trig, seed=900 + i, hit_rate=0.15)]
+            if i % 5 == 4:
+                docs.append(make_log(90, trig, seed=950 + i, hit_rate=0.2))      # a 2-request batch
+            outs = engs[i % 2].analyze_batch_json(docs, turn, None)
+            for o, d in zip(outs, docs):
+                o, g = json.loads(o), golden.analyze(d, sets, params, tracker)
+                assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o["events"]] == \
+                       [(e["lineNumber"], e["matchedPattern"]["id"]) for e in g["events"]], i
+                np.testing.assert_allclose([e["score"] for e in o["events"]], [e["score"] for e in g["events"]],
+                                           rtol=1e-12)
+        if dev != "cpu":
+            assert all(e._runner not in (None, False) for e in engs)
+        assert int(sh.sections) - s0 == 14 or dev == "cpu"
+        assert fs[1].statistics() == {k: v for k, v in tracker.statistics().items() if v}
+    finally:
+        N.ProcShared.unlink(name, int(sh.generation))

@@ -45,7 +45,6 @@ from .golden import SEVERITY_ORDER
 from .models.compiled import CompiledLibrary
 from .native import N, host_thread_budget
 from .ops import kernels as K
-from .regex.javacompat import compile_java
 from .utils import tracing as TR
 from .utils.config import Config, ScoringParams
 

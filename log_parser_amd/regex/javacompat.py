@@ -1,9 +1,10 @@
-"""java.util.regex -> Python ``regex`` translation (oracle + host fallback only).
+"""java.util.regex -> Python ``regex`` translation: the TEST ORACLE.
 
-Used by the pure-Python golden model (``golden.py``) and as the *host fallback* for the few
-non-regular constructs the automaton engine refuses (backreferences, lookaround, possessive /
-atomic groups). It is intentionally independent of the C++ regex compiler so that the golden
-oracle does not share a parser with the GPU engine.
+Used by the pure-Python golden model (``golden.py``) and by the regex tests as the independent
+reference for Java's ``find()``. The engine never runs it: regular regexes run on the automata
+(DFA / BPG programs) and the non-regular ones (backreferences, lookaround, possessive / atomic
+groups) on the native C++ backtracker (``jregex.cpp BtRegex``). It is intentionally independent of
+the C++ regex compiler so that the oracle does not share a parser with the engine.
 
 Java 21 defaults reproduced: ``\\w \\d \\s \\b`` and CASE_INSENSITIVE are ASCII-only;
 ``.`` excludes ``\\n \\r \\u0085 \\u2028 \\u2029``; without MULTILINE ``$`` / ``\\Z`` match at the end

@@ -7,6 +7,11 @@
 #   http    config 5 over HTTP: 1 and 2 serving processes (stage timelines), and the front end alone
 #   stream  config 4: 1B-line stream, auto (HBM-sized) chunks and 256 MiB chunks (same digest)
 #   configs config 2 (1M lines, 256 patterns, realistic library) and config 1 (CPU-only /parse)
+#   reqtrace  one 10k-line request: wall p50 + kernel timeline, library with / without Java shapes
+#   prof    kernel table of the bench step (rocprofv3 kernel trace, serialised ingest)
+#   pmcscan PMC counters of the scan walk and prefilter (two counter passes)
+#   httpreps  config 5, 1 process, 5 runs with stage timelines (run-to-run spread)
+#   full    round-end rehearsal: the whole GPU suite, smoke(), the bench
 # Run: gpurun -- bash tools/gpu_check.sh [step ...]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -58,6 +63,29 @@ for s in $steps; do
         db=$(find gpurun_out/rt_prof_$j -name "*.db" | head -1)
         run rt_sum_$j 120 python3 tools/request_trace.py --db "$db" --requests 200
       done ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- \
+        python3 bench.py --steps 6 --warmup 2 --parse-requests 0 --no-overlap
+      db=$(find gpurun_out/prof_bench -name "*.db" | head -1)
+      run kstats 120 python3 tools/kstats_db.py "$db" 6 45 --median --marker k_nl_count --last 6 --timeline ;;
+    pmcscan)
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+      P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_WAIT_ANY"
+      run pmc1 180 rocprofv3 --pmc $P1 --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan/p1 \
+        -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
+      run pmc2 180 rocprofv3 --pmc $P2 --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan/p2 \
+        -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
+      run pmcsum 120 python3 tools/pmc_summary.py gpurun_out/pmc_scan ;;
+    httpreps)
+      for rep in 1 2 3 4 5; do
+        run htl_$rep 300 python -u benchmarks/bench_configs.py concurrent_http --processes 1 --client-threads 8 --timeline
+      done ;;
+    full)
+      run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+      run full_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+      run full_bench 300 python -u bench.py ;;
     configs)
       run single 600 python -u benchmarks/bench_configs.py single
       run rest 600 python -u benchmarks/bench_configs.py rest ;;

@@ -66,12 +66,18 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="serialise H2D ingest with compute")
     ap.add_argument("--pf-verify-lanes", type=int, default=0, choices=[0, 1, 2, 4, 16],
                     help="A/B: lanes per gram hit in the bulk literal verify (0: the kernel's default)")
+    ap.add_argument("--scan-defer-rare", type=int, default=1, choices=[0, 1],
+                    help="A/B: the scan walk's hot blocks re-walked by k_scan_rare (1) or inline (0)")
     ap.add_argument("--d2h-stream", default="copy", choices=["copy", "compute"],
                     help="stream of the per-step event D2H (diagnostic A/B)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
                     help="process group: auto = nccl (RCCL) on GPUs at every world size, gloo on CPU for world "
                          "size > 1 and none on CPU at world size 1; nccl / gloo / none force one (gloo on GPUs "
                          "= host-staged, to rehearse several ranks on ONE GPU; none = no collectives at world 1)")
+    ap.add_argument("--bt-patterns", type=int, default=0,
+                    help="add N primaries only a backtracker decides (backreference / lookaround / atomic; N-1 with "
+                         "a literal, one literal-free): the device feeds them with their relaxed automata and the host "
+                         "checks only the candidate lines, inside the queued step (side_path.hip)")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="hang guard: the whole job's deadline in seconds (0 = none)")
     ap.add_argument("--stall-timeout", type=float, default=300.0,
@@ -100,10 +106,15 @@ def make_blocks(args, trig):
 
 
 def library(args):
-    from log_parser_amd.utils.synth import make_library, realistic_library
+    from log_parser_amd.utils.synth import backtracker_patterns, make_library, realistic_library
     if args.library == "realistic":
-        return realistic_library(args.patterns, seed=7)
-    return make_library(args.patterns, seed=7)
+        sets, trig = realistic_library(args.patterns, seed=7)
+    else:
+        sets, trig = make_library(args.patterns, seed=7)
+    if args.bt_patterns > 0:
+        ps, bt_trig = backtracker_patterns(args.bt_patterns, seed=7)
+        sets, trig = sets + [ps], trig + bt_trig
+    return sets, trig
 
 
 def main():
@@ -202,9 +213,10 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
         hb.phase("process group ready")
         assert dist.get_world_size() == world
 
+    from log_parser_amd.native import N
     if args.pf_verify_lanes:
-        from log_parser_amd.native import N
         N.set_pf_verify_lanes(args.pf_verify_lanes)
+    N.set_scan_defer_rare(bool(args.scan_defer_rare))
     params = ScoringParams()
     lib = CompiledLibrary(sets, params)
     cfg = Config.load(overrides={"engine.device": str(device)})
@@ -305,7 +317,9 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
             ev0 = torch.cuda.Event(enable_timing=True)
             ev0.record()
         # line index + literal prefilter queued before the index's host read (sa.step builds both)
-        out = sa.step(text, nbytes, None, None, hl, hr, topk=args.topk, pack_events=True)
+        # host_text: the shard's bytes on the host (the backtracker regexes' candidate lines are checked there)
+        out = sa.step(text, nbytes, None, None, hl, hr, topk=args.topk, pack_events=True,
+                      host_text=hv[:nbytes] if lib.host_regs else None)
         events_to_host(out, b)                                   # results land on the host
         if rank == 0 and out.topk_rows is not None:
             state["top"] = out.topk_rows.cpu()                   # merged global top-k on the host

@@ -660,6 +660,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("split_docs", &split_docs);
   m.def("set_host_threads", &set_host_threads);
   m.def("set_pf_verify_lanes", &set_pf_verify_lanes);
+  m.def("set_scan_defer_rare", &set_scan_defer_rare);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false);
@@ -721,6 +722,46 @@ PYBIND11_MODULE(_lpnative, m) {
         py::arg("count"), py::arg("s"), py::arg("dn") = 0, py::arg("max_grid") = 8192);
   m.def("append_keys", [](uint64_t dst, int64_t cap, uint64_t count, uint64_t src, int64_t n, uint64_t s) {
     append_keys_dev(P<int64_t>(dst), cap, P<unsigned long long>(count), P<const int64_t>(src), n, s); });
+  // backtracker regexes fed by their relaxed automata (side_path.hip). out: None = drop mode, else
+  // (keys, starts, lens, cap, cnt, done_blocks, host_cnt, host_seq, seq) device-visible addresses
+  m.def("take_host", [](uint64_t cand, uint64_t n1d, int64_t cap1, uint64_t ver, uint64_t n2d, int64_t cap2,
+                        uint64_t text, uint64_t ls, uint64_t ll, py::tuple dfa, py::object out, uint64_t s) {
+    HostSideOut O;
+    if (!out.is_none()) {
+      py::tuple t = out.cast<py::tuple>();
+      O.keys = P<int64_t>(t[0].cast<uint64_t>()); O.starts = P<int64_t>(t[1].cast<uint64_t>());
+      O.lens = P<int64_t>(t[2].cast<uint64_t>()); O.cap = t[3].cast<int64_t>();
+      O.cnt = P<unsigned long long>(t[4].cast<uint64_t>()); O.done_blocks = P<unsigned int>(t[5].cast<uint64_t>());
+      O.host_cnt = P<int64_t>(t[6].cast<uint64_t>()); O.host_seq = P<int64_t>(t[7].cast<uint64_t>());
+      O.seq = t[8].cast<int64_t>();
+    }
+    take_host_dev(P<int64_t>(cand), P<const unsigned long long>(n1d), cap1, P<int64_t>(ver),
+                  P<const unsigned long long>(n2d), cap2, P<const uint8_t>(text), P<const int64_t>(ls),
+                  P<const int32_t>(ll), dfa_from(dfa), O, s); });
+  // in = (keys, host_cnt, host_seq, cap, seq, err) device-visible addresses of pinned host memory
+  m.def("wait_host", [](uint64_t ver, int64_t cap2, uint64_t n2d, py::tuple in, uint64_t s, double timeout_s) {
+    HostSideIn I;
+    I.keys = P<const int64_t>(in[0].cast<uint64_t>()); I.host_cnt = P<const int64_t>(in[1].cast<uint64_t>());
+    I.host_seq = P<const int64_t>(in[2].cast<uint64_t>()); I.cap = in[3].cast<int64_t>(); I.seq = in[4].cast<int64_t>();
+    I.err = P<int64_t>(in[5].cast<uint64_t>());
+    I.timeout_ticks = (long long)(timeout_s * 1e8);
+    wait_host_dev(P<int64_t>(ver), cap2, P<unsigned long long>(n2d), I, s); }, py::arg("ver"), py::arg("cap2"),
+    py::arg("n2d"), py::arg("in"), py::arg("stream"), py::arg("timeout_s") = 2.0);
+  // pinned host memory the GPU reads and writes coherently (fine-grained): (host address, device
+  // address); freed with host_free_coherent
+  m.def("host_alloc_coherent", [](int64_t bytes) {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, (size_t)std::max<int64_t>(bytes, 8), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      throw std::runtime_error("hipHostMalloc (coherent) failed");
+    std::memset(h, 0, (size_t)std::max<int64_t>(bytes, 8));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      throw std::runtime_error("hipHostGetDevicePointer failed");
+    }
+    return py::make_tuple(reinterpret_cast<uint64_t>(h), reinterpret_cast<uint64_t>(d));
+  });
+  m.def("host_free_coherent", [](uint64_t h) { (void)hipHostFree(reinterpret_cast<void*>(h)); });
   m.def("scan_dev", [](uint64_t text, uint64_t ls, uint64_t ll, int64_t nl, uint64_t regs, int nregs, py::tuple dfa,
                        uint64_t out, int64_t cap, uint64_t count, uint64_t s) {
     scan_dev(P<const uint8_t>(text), P<const int64_t>(ls), P<const int32_t>(ll), nl, P<const int32_t>(regs), nregs,
@@ -842,9 +883,10 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<RequestRunner>(m, "RequestRunner")
       .def(py::init([](py::tuple pf, py::tuple dfa, py::list scans, py::list grids, uint64_t scan_regs, int n_scan_regs,
                        py::tuple st12, py::tuple sp, py::tuple ev5, int R, int npat, int nkeys, int nseq, int ctx_trans,
-                       int ctx_acc, int pf_grid, int device, bool device_counts) {
+                       int ctx_acc, int pf_grid, int device, bool device_counts, bool host_dev) {
              RequestStatic S;
              S.device_counts = device_counts;
+             S.host_dev = host_dev;
              S.pf = pf_from(pf);
              S.dfa = dfa_from(dfa);
              for (auto h : scans) S.scans.push_back(scan_pass_from(h.cast<py::tuple>()));
@@ -876,7 +918,7 @@ PYBIND11_MODULE(_lpnative, m) {
            }), py::arg("pf"), py::arg("dfa"), py::arg("scans"), py::arg("grids"), py::arg("scan_regs"),
            py::arg("n_scan_regs"), py::arg("st12"), py::arg("sp"), py::arg("ev5"), py::arg("R"), py::arg("npat"),
            py::arg("nkeys"), py::arg("nseq"), py::arg("ctx_trans"), py::arg("ctx_acc"), py::arg("pf_grid"),
-           py::arg("device"), py::arg("device_counts") = true)
+           py::arg("device"), py::arg("device_counts") = true, py::arg("host_dev") = false)
       .def("run", [](RequestRunner& r, uint64_t text, int64_t nbytes, uint64_t starts, uint64_t lens, int64_t L,
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> lo,
                      py::array_t<int32_t, py::array::c_style | py::array::forcecast> hi,

@@ -12,6 +12,9 @@ namespace lp {
 void set_host_threads(int n);
 // lanes per gram hit of the bulk literal verify (k_pf_verify; A/B knob, default 4)
 void set_pf_verify_lanes(int n);
+// bulk scan walk: hot blocks re-walked by a second kernel (k_scan_rare) instead of inline (A/B knob)
+bool scan_defer_rare();
+void set_scan_defer_rare(bool on);
 // line-index pass 1 folded into the bulk prefilter (line_index.hip k_nl_count's outputs): per 16 KiB
 // tile the '\n' count and the "\r\n" flag (both zeroed by the caller), per 64 bytes a '\n' bitmask
 struct NlOut {
@@ -43,6 +46,35 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,
                   int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
                   uint64_t stream);
+// backtracker regexes fed by their relaxed automata (side_path.hip): export of the candidates to
+// pinned host memory (keys / starts / lens / host_cnt / host_seq are device-visible pointers of
+// pinned host memory; cnt / done_blocks device words, zero between uses). keys == null: drop mode.
+struct HostSideOut {
+  int64_t* keys = nullptr;
+  int64_t* starts = nullptr;
+  int64_t* lens = nullptr;
+  int64_t cap = 0;
+  unsigned long long* cnt = nullptr;
+  unsigned int* done_blocks = nullptr;
+  int64_t* host_cnt = nullptr;
+  int64_t* host_seq = nullptr;
+  int64_t seq = 0;
+};
+// ... and the host's verified keys (pinned, device-visible), published with host_seq == seq
+struct HostSideIn {
+  const int64_t* keys = nullptr;
+  const int64_t* host_cnt = nullptr;
+  const int64_t* host_seq = nullptr;
+  int64_t cap = 0;
+  int64_t seq = 0;
+  long long timeout_ticks = 200000000;   // wall_clock64 ticks (100 MHz): 2 s
+  int64_t* err = nullptr;                // set to 1 when the host did not answer in time
+};
+void take_host_dev(int64_t* cand, const unsigned long long* n1d, int64_t cap1, int64_t* ver,
+                   const unsigned long long* n2d, int64_t cap2, const uint8_t* text, const int64_t* ls,
+                   const int32_t* ll, const DfaPool& P, const HostSideOut& O, uint64_t stream);
+void wait_host_dev(int64_t* ver, int64_t cap2, unsigned long long* n2d, const HostSideIn& I, uint64_t stream);
+
 // host-verified keys appended to a verified-hit buffer at its device counter (k_append_keys)
 void append_keys_dev(int64_t* dst, int64_t cap, unsigned long long* count, const int64_t* src, int64_t n,
                      uint64_t stream);

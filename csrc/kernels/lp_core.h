@@ -136,6 +136,9 @@ __device__ __forceinline__ uint32_t dfa_find_k(const DfaRef (&D)[K], const uint8
 // find() of regex r over one line (java.util.regex Matcher.find semantics, see jregex.h)
 // regex r is a bit-parallel Glushkov program (DFA blow-up), not a DFA of the pool
 LP_HD bool is_bpg(const DfaPool& P, int r) { return (P.meta[4 * r + 3] & 2) != 0; }
+// regex r is a backtracker regex whose automaton is its regular RELAXATION: its device keys are
+// candidates for the host backtracker, never hits (side_path.hip)
+LP_HD bool is_host_dev(const DfaPool& P, int r) { return (P.meta[4 * r + 3] & 4) != 0; }
 
 LP_HD bool dfa_run(const DfaPool& P, int r, const uint8_t* s, int n) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -35,8 +35,11 @@
 // an unusual separator or a document boundary take the exact per-line walk.
 #include <hip/hip_runtime.h>
 
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "lp_api.h"
@@ -211,13 +214,40 @@ __device__ __forceinline__ void scan_block_masks(const ScanPass& S, const uint32
     if (acc[q]) scan_emit(S, g, acc[q], l + q < x1 ? l + q : x1 - 1, emit);
 }
 
+// Deferred rare path (bulk variant): a hot block is not re-walked inline -- the re-walk's 16 mask
+// loads in flight and its accumulators cost ~50 of the walk's ~107 VGPRs -- but appended as a
+// record (block, run bounds, lines, group, the group's row at the block) to a list that
+// k_scan_rare walks afterwards, with the same LDS rows and mask table.
+struct RareList {
+  int64_t* rec;                   // RARE_WORDS int64 per record
+  int64_t cap;
+  unsigned long long* cnt;        // device: records appended (reset by k_scan_rare's last block)
+  unsigned int* done;             // device: k_scan_rare blocks finished
+  int64_t* need;                  // pinned host: the record count of an overflowing launch
+};
+constexpr int RARE_WORDS = 5;
+
+__device__ __forceinline__ void rare_push(const RareList& R, int64_t p0, int64_t p_lo, int64_t p_end, int64_t x0,
+                                          int64_t x1, int g, bool crlf, uint32_t xr) {
+  const unsigned long long i = atomicAdd(R.cnt, 1ull);
+  if ((int64_t)i >= R.cap) return;             // (k_scan_rare reports the overflow)
+  int64_t* q = R.rec + RARE_WORDS * (int64_t)i;
+  q[0] = p0;
+  q[1] = p_lo;
+  q[2] = p_end;
+  q[3] = x0 | ((x1 - x0) << 56);
+  q[4] = (int64_t)g | ((int64_t)crlf << 2) | ((int64_t)xr << 8);
+}
+
 // the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold.
 // REP: the bytemap read goes to this lane's copy of the lane-replicated bytemap at LDS byte bm_rep
-// (entry c at bm_rep + c * 128); otherwise to the blob's bm4 at LDS byte 0
-template <int G, bool CRLF, bool REP, typename Emit>
+// (entry c at bm_rep + c * 128); otherwise to the blob's bm4 at LDS byte 0. DEFER: hot blocks go to
+// the rare list instead of the inline re-walk.
+template <int G, bool CRLF, bool REP, bool DEFER, typename Emit>
 __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass& S, const uint8_t* text, int64_t p_lo,
                                               int64_t p_end, int64_t x0, int64_t x1,
-                                              const int64_t* __restrict__ line_start, uint32_t bm_rep, Emit&& emit) {
+                                              const int64_t* __restrict__ line_start, uint32_t bm_rep, Emit&& emit,
+                                              const RareList& rare) {
   uint32_t xr[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
@@ -266,18 +296,20 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
 #pragma unroll
       for (int q = 1; q < G; ++q)
         if (g == q) xg = xs[q];
-      scan_block_masks<CRLF>(S, w, hold, p0, p_lo, p_end, x0, x1, line_start, g, xg, emit);
+      if constexpr (DEFER) rare_push(rare, p0, p_lo, p_end, x0, x1, g, CRLF, xg);
+      else scan_block_masks<CRLF>(S, w, hold, p0, p_lo, p_end, x0, x1, line_start, g, xg, emit);
     }
     cur = nxt;
   }
 }
 
-template <int G, int THREADS>
+template <int G, int THREADS, bool DEFER>
 __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restrict__ text, int64_t nbytes,
                                                         const int64_t* __restrict__ line_start,
                                                         const int32_t* __restrict__ line_len, int64_t nlines,
                                                         ScanPass S, int64_t* __restrict__ out, int64_t cap,
-                                                        unsigned long long* __restrict__ count, int run_len) {
+                                                        unsigned long long* __restrict__ count, int run_len,
+                                                        RareList rare) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   lds_fill<uint4>(reinterpret_cast<uint4*>(sm), reinterpret_cast<const uint4*>(S.blob), S.lds_words >> 2);  // multiple of 4
   // bulk variant: a lane-replicated copy of bm4 after the blob (SCAN_BM_COPIES copies: entry c of
@@ -360,13 +392,116 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
     if (!R.fast) {     // rare: exact per-line walks
       for (int64_t x = R.x0; x < R.x1; ++x) scan_line_exact(S, sm, text + line_start[x], line_len[x], x, emit);
     } else if (R.crlf) {
-      scan_run_fast<G, true, REP>(sm, S, text, R.p_lo, R.p_end, R.x0, R.x1, line_start, bm_rep, emit);
+      scan_run_fast<G, true, REP, DEFER>(sm, S, text, R.p_lo, R.p_end, R.x0, R.x1, line_start, bm_rep, emit, rare);
     } else {
-      scan_run_fast<G, false, REP>(sm, S, text, R.p_lo, R.p_end, R.x0, R.x1, line_start, bm_rep, emit);
+      scan_run_fast<G, false, REP, DEFER>(sm, S, text, R.p_lo, R.p_end, R.x0, R.x1, line_start, bm_rep, emit, rare);
     }
   };
   for (int64_t run = (int64_t)blockIdx.x * THREADS + threadIdx.x; run < nruns; run += stride) walk_one(prep(run));
 }
+
+// the deferred re-walks: every record is one hot 16-byte block of one group, walked exactly on the
+// pass's LDS rows (staged at LDS address 0 as in k_scan_multi) with the global mask table; a fixed
+// grid strides over the device count; the last block resets the list and reports an overflow
+// (the scan's hit count is pushed past its capacity, so the batch re-runs -- see scan_multi_dev)
+__global__ __launch_bounds__(256) void k_scan_rare(const uint8_t* __restrict__ text,
+                                                   const int64_t* __restrict__ line_start, ScanPass S,
+                                                   int64_t* __restrict__ out, int64_t cap,
+                                                   unsigned long long* __restrict__ count, RareList rare) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];   // the only LDS: the blob at address 0
+  lds_fill<uint4>(reinterpret_cast<uint4*>(sm), reinterpret_cast<const uint4*>(S.blob), S.lds_words >> 2);
+  __syncthreads();
+  const GlobalEmit emit{out, cap, count};
+  const bool at_zero = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)sm == 0u;
+  const int64_t n = (int64_t)*rare.cnt;
+  const int64_t m = n < rare.cap ? n : rare.cap;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t* q = rare.rec + RARE_WORDS * i;
+    const int64_t p0 = q[0], p_lo = q[1], p_end = q[2], xw = q[3], gw = q[4];
+    const int64_t x0 = xw & ((1ll << 56) - 1), x1 = x0 + (xw >> 56);
+    const int g = (int)(gw & 3);
+    const bool crlf = (gw >> 2) & 1;
+    const uint32_t xr = (uint32_t)(gw >> 8);
+    const uint4 cur = *reinterpret_cast<const uint4*>(text + p0);
+    const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, *reinterpret_cast<const uint32_t*>(text + p0 + 16)};
+    if (!at_zero) {                              // (never expected) the exact global-table walk
+      scan_block_exact(S, S.blob + S.bm_off, w, p0, p_lo, p_end, x0, x1, line_start, g, scan_state_of(S, g, xr), emit);
+    } else if (crlf) {
+      uint32_t hold = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = crlf_bits(w[k], w[k + 1]);
+        hold |= (((b >> 7) & 1u) | ((b >> 14) & 2u) | ((b >> 21) & 4u) | ((b >> 28) & 8u)) << (4 * k);
+      }
+      scan_block_masks<true>(S, w, hold, p0, p_lo, p_end, x0, x1, line_start, g, xr, emit);
+    } else {
+      scan_block_masks<false>(S, w, 0u, p0, p_lo, p_end, x0, x1, line_start, g, xr, emit);
+    }
+  }
+  __syncthreads();
+  volatile uint32_t* last = sm + S.lds_words;    // (a word behind the blob: no static LDS)
+  if (threadIdx.x == 0) {
+    __threadfence();
+    *last = atomicAdd(rare.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*last && threadIdx.x == 0) {
+    if (n > rare.cap) {
+      rare.need[0] = n;                          // grown before the re-run
+      __threadfence_system();
+      atomicAdd(count, (unsigned long long)(cap + 1));
+    }
+    *rare.cnt = 0;
+    *rare.done = 0;
+  }
+}
+
+namespace {
+bool g_defer_rare = true;
+}  // namespace
+bool scan_defer_rare() { return g_defer_rare; }
+void set_scan_defer_rare(bool on) { g_defer_rare = on; }
+
+namespace {
+
+// one grow-only rare list per (device, stream); `need` (pinned) carries an overflow's size back
+struct RareBuf {
+  int64_t* rec = nullptr;
+  int64_t cap = 0;
+  unsigned long long* cnt = nullptr;
+  int64_t* need = nullptr;
+};
+std::mutex g_rare_mu;
+std::map<std::pair<int, uint64_t>, RareBuf> g_rare;
+
+RareList rare_list(int64_t want, uint64_t stream) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(g_rare_mu);
+  RareBuf& b = g_rare[{dev, stream}];
+  if (b.need && *b.need > want) want = *b.need;
+  if (!b.cnt) {
+    if (hipMalloc(reinterpret_cast<void**>(&b.cnt), 16) != hipSuccess ||
+        hipMemset(b.cnt, 0, 16) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&b.need), 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      throw std::runtime_error("scan_multi: rare list allocation failed");
+    *b.need = 0;
+  }
+  if (want > b.cap) {              // the stream is idle here: the previous launch's batch has ended
+    if (b.rec) (void)hipFree(b.rec);
+    b.rec = nullptr;
+    const int64_t cap = want + want / 4;
+    if (hipMalloc(reinterpret_cast<void**>(&b.rec), (size_t)cap * RARE_WORDS * 8) != hipSuccess)
+      throw std::runtime_error("scan_multi: rare list allocation failed");
+    b.cap = cap;
+    *b.need = 0;
+  }
+  int64_t* need_dev = nullptr;
+  (void)hipHostGetDevicePointer(reinterpret_cast<void**>(&need_dev), b.need, 0);
+  return RareList{b.rec, b.cap, b.cnt, reinterpret_cast<unsigned int*>(b.cnt + 1), need_dev};
+}
+
+}  // namespace
 
 void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_start, const int32_t* line_len, int64_t nlines,
                     const ScanPass& S, int64_t* out, int64_t cap, unsigned long long* count, int grid,
@@ -383,13 +518,19 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
   const int64_t runs = (nlines + run_len - 1) / run_len;
   const int64_t need = (runs + threads - 1) / threads;
   const int g = (int)std::max<int64_t>(1, std::min<int64_t>(small ? 4 * (int64_t)grid : grid, need));
+  // bulk texts defer the rare re-walks to k_scan_rare (engine.scan-defer-rare, default on)
+  const bool defer = !small && scan_defer_rare();
+  const RareList rare = defer ? rare_list(std::max<int64_t>(65536, runs), stream) : RareList{};
 #define LP_SCAN(GV)                                                                                        \
   if (small)                                                                                               \
-    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS_SMALL>), dim3(g), dim3(SCAN_THREADS_SMALL), lds, st, text, \
-                       nbytes, line_start, line_len, nlines, S, out, cap, count, run_len);                 \
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS_SMALL, false>), dim3(g), dim3(SCAN_THREADS_SMALL), lds, st, \
+                       text, nbytes, line_start, line_len, nlines, S, out, cap, count, run_len, rare);     \
+  else if (defer)                                                                                          \
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS, true>), dim3(g), dim3(SCAN_THREADS), lds, st, text, \
+                       nbytes, line_start, line_len, nlines, S, out, cap, count, run_len, rare);           \
   else                                                                                                     \
-    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS>), dim3(g), dim3(SCAN_THREADS), lds, st, text, nbytes, \
-                       line_start, line_len, nlines, S, out, cap, count, run_len)
+    hipLaunchKernelGGL((k_scan_multi<GV, SCAN_THREADS, false>), dim3(g), dim3(SCAN_THREADS), lds, st, text, \
+                       nbytes, line_start, line_len, nlines, S, out, cap, count, run_len, rare)
   switch (S.ngroups) {
     case 1: LP_SCAN(1); break;
     case 2: LP_SCAN(2); break;
@@ -399,6 +540,12 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
 #undef LP_SCAN
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in scan_multi");
+  if (defer) {
+    hipLaunchKernelGGL(k_scan_rare, dim3(256), dim3(256), (size_t)S.lds_words * 4 + 16, st, text, line_start, S, out,
+                       cap, count, rare);
+    e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in scan_rare");
+  }
 }
 
 // host twin: the exact per-line walk over the same blob

@@ -1471,7 +1471,87 @@ void classify_fallback(Compiled& out, const std::string& pattern, const std::str
   }
 }
 
+// Regular RELAXATION of a backtracker-only regex: the AST of a SUPERSET language the automata run,
+// so the GPU narrows the lines the host backtracker must check (literal-free regexes included):
+// a group -> its body; a backreference -> a copy of its closed, case-sensitive group's body (the
+// captured text is in that language), else any string; lookaround and MULTILINE anchors -> empty
+// (they only restrict); atomic groups / possessive quantifiers -> plain (the same language or a
+// superset). find() of the original implies find() of the relaxation.
+class Relaxer {
+ public:
+  explicit Relaxer(const std::vector<Node>& in) : in_(in) {}
+  std::vector<Node> out;
+  int relax(int id) {
+    const Node& n = in_[id];
+    switch (n.t) {
+      case N_GROUP: {
+        open_.insert(n.idx);
+        const int b = relax(n.kids[0]);
+        open_.erase(n.idx);
+        body_[n.idx] = b;
+        return b;
+      }
+      case N_BACKREF: {
+        auto it = body_.find(n.idx);
+        if (!n.ci && it != body_.end() && !open_.count(n.idx)) return it->second;
+        return any();
+      }
+      case N_LOOK: case N_MLANCHOR: { Node e; e.t = N_EMPTY; return add(e); }
+      case N_ATOMIC: return relax(n.kids[0]);
+      default: {
+        Node c = n;
+        for (auto& k : c.kids) k = relax(k);
+        return add(c);
+      }
+    }
+  }
+
+ private:
+  const std::vector<Node>& in_;
+  std::map<int, int> body_;
+  std::set<int> open_;
+  int any_ = -1;
+  int add(const Node& n) { out.push_back(n); return (int)out.size() - 1; }
+  int any() {
+    if (any_ < 0) {
+      Node c; c.t = N_CSET; c.cs.add_range(0, CpSet::MAX);
+      const int k = add(c);
+      Node r; r.t = N_REP; r.kids = {k}; r.lo = 0; r.hi = -1;
+      any_ = add(r);
+    }
+    return any_;
+  }
+};
+
+Compiled compile_nodes(Compiled out, std::vector<Node> nodes, int root, int max_dfa_states, int max_positions,
+                       bool want_bpg, const std::string& pattern);
+
+// "(?#relax)" + pattern: the automaton of the pattern's relaxation (Relaxer); FALLBACK if even that
+// is not regular enough for the automata. Java rejects "(?#" (no comment groups), so no library
+// regex starts with the marker.
+Compiled compile_relaxed(const std::string& pattern, int max_dfa_states, int max_positions, bool want_bpg) {
+  Compiled out;
+  try {
+    Parser B(pattern, true);
+    const int r = B.parse();
+    out.wordb = B.uses_wordb;
+    out.uword = B.uses_uword;
+    if (B.uses_uword && B.uses_aword) { out.kind = Kind::FALLBACK; out.error = "mixed \\b semantics"; return out; }
+    out.cp_only = B.uses_uword;
+    Relaxer Rx(B.nodes);
+    const int root = Rx.relax(r);
+    return compile_nodes(std::move(out), std::move(Rx.out), root, max_dfa_states, max_positions, want_bpg, pattern);
+  } catch (const std::exception& e) {
+    out.kind = Kind::FALLBACK;
+    out.error = std::string("relaxation: ") + e.what();
+    return out;
+  }
+}
+
 Compiled compile_impl(const std::string& pattern, int max_dfa_states, int max_positions, bool want_bpg) {
+  static const std::string kRelax = "(?#relax)";
+  if (pattern.compare(0, kRelax.size(), kRelax) == 0)
+    return compile_relaxed(pattern.substr(kRelax.size()), max_dfa_states, max_positions, want_bpg);
   Compiled out;
   std::vector<Node> nodes;
   int root;
@@ -1496,6 +1576,11 @@ Compiled compile_impl(const std::string& pattern, int max_dfa_states, int max_po
   } catch (const std::exception& e) {
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   }
+  return compile_nodes(std::move(out), std::move(nodes), root, max_dfa_states, max_positions, want_bpg, pattern);
+}
+
+Compiled compile_nodes(Compiled out, std::vector<Node> nodes, int root, int max_dfa_states, int max_positions,
+                       bool want_bpg, const std::string& pattern) {
   set_literals(out, nodes, root);
   std::string why = out.cp_only ? "code-point contexts" : "";
   if (!out.cp_only) {

@@ -338,6 +338,8 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     pf_verify_dev(gh, cap_g, text, nbytes, S_.pf, ls, L, blk, cand, cap_c, c0 + 1, stream, c0,
                   (int)std::max<int64_t>(16, std::min<int64_t>(8192, nbytes >> 13)));
 
+    if (S_.host_dev)   // the relaxed automata's keys: candidates only, decided by the host side path
+      take_host_dev(cand, c0 + 1, cap_c, ver, c0 + 2, cap_v, text, ls, ll, S_.dfa, HostSideOut{}, stream);
     // hit CSR + event counts: the pipeline reads the matchers' device counters itself
     HitsArgs A;
     A.cand = cand; A.n = n; A.pre_from = cap_c;

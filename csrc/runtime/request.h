@@ -103,6 +103,8 @@ struct RequestStatic {
   int pf_grid = 1;
   int device = 0;
   bool device_counts = true;        // requests: no mid-batch host read (see run())
+  bool host_dev = false;            // backtracker regexes with relaxed automata: drop their device keys
+                                    // (the host side path decided them: `inj`; side_path.hip)
 };
 
 struct RequestCounts {

@@ -34,6 +34,7 @@ SOURCES = [
     ("kernels/lp_post.hip", "hip"),
     ("kernels/post_bulk.hip", "hip"),
     ("kernels/request_io.hip", "hip"),
+    ("kernels/side_path.hip", "hip"),
     ("io/json_emit.cpp", "cpp"),
     ("io/docs.cpp", "cpp"),
     ("io/json_in.cpp", "cpp"),

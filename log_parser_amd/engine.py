@@ -370,6 +370,7 @@ class Engine:
         self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
         # second compute stream: literal-free scans overlap the prefilter chain (K.match_and_hits)
         self._side = None
+        self._host_side = None                      # ops.side_path.HostSide (device-fed backtracker regexes)
         self._runner = None                         # N.RequestRunner (built on first use) / False
         if self.device.type == "cuda":
             props = torch.cuda.get_device_properties(self.device)
@@ -437,11 +438,19 @@ class Engine:
             extra.append(inj)
         if extra:
             t = self._tick(timings, "scan", t)
-            return torch.cat([cand] + extra), cand.numel()
-        return cand, cand.numel()
+            cand, pre = torch.cat([cand] + extra), cand.numel()
+        else:
+            pre = cand.numel()
+        if self.lib.host_dev:              # relaxation keys: the host side path decided these regexes
+            hd = torch.from_numpy(self.lib.host_dev_mask).to(cand.device)
+            drop = (cand >= 0) & hd[(cand >> 32).clamp(min=0, max=hd.numel() - 1)]
+            if inj is not None and inj.numel():
+                drop[cand.numel() - inj.numel():] = False          # (the host side path's own keys)
+            cand = torch.where(drop, torch.full_like(cand, -1), cand)
+        return cand, pre
 
     def host_hits(self, text, nbytes: int, host_text=None, ls_h=None, ll_h=None,
-                  trim: bool = True) -> Optional[torch.Tensor]:
+                  trim: bool = True, plan=None) -> Optional[torch.Tensor]:
         """The host backtracker's side path (non-regular regexes -- backreferences,
         lookaround, atomic groups, possessive quantifiers -- on C++ BtRegex): run BEFORE the device
         pipeline on the host copy of the bytes, so its verified (regex << 32 | line) keys join the
@@ -450,16 +459,19 @@ class Engine:
         Lines holding one of a regex's required literals are checked, every line without one.
         ``ls_h`` / ``ll_h``: the batch's host line index (serving), else a Java split of the one
         document / shard (the device line index's rule; ``trim=False``: a stream chunk's rule, no
-        trailing-empty-line removal). None without backtracker regexes."""
-        if not self.lib.host_plan:
+        trailing-empty-line removal). None without backtracker regexes. ``plan``: the regexes to run
+        (default: every backtracker regex; ``lib.host_plan_undev`` when the device feeds the others)."""
+        plan = self.lib.host_plan if plan is None else plan
+        if not plan:
             return None
         hb = host_text
         if hb is None:
             hb = text[:nbytes].cpu().numpy()
-        return torch.from_numpy(self._host_keys(hb, nbytes, ls_h, ll_h, trim)).to(text.device)
+        return torch.from_numpy(self._host_keys(hb, nbytes, ls_h, ll_h, trim, plan)).to(text.device)
 
-    def _host_keys(self, hb, nbytes: int, ls_h=None, ll_h=None, trim: bool = True) -> np.ndarray:
+    def _host_keys(self, hb, nbytes: int, ls_h=None, ll_h=None, trim: bool = True, plan=None) -> np.ndarray:
         lib = self.lib
+        plan = lib.host_plan if plan is None else plan
         hb = np.ascontiguousarray(np.asarray(hb, dtype=np.uint8)[:nbytes])
         if hb.size == 0:
             hb = np.zeros(1, np.uint8)
@@ -469,7 +481,7 @@ class Engine:
             lsp, llp, nl = ls_h.ctypes.data, ll_h.ctypes.data, ls_h.size
         else:
             lsp = llp = nl = 0
-        loc, glob, lits = zip(*lib.host_plan)
+        loc, glob, lits = zip(*plan)
         keys = lib.host_bt.prepass(hb.ctypes.data, int(nbytes), lsp, llp, nl, trim, list(loc), list(glob),
                                    [list(x) for x in lits])
         if lib.host_bt.exhausted:
@@ -538,11 +550,23 @@ class Engine:
         L = ls.numel()
         t = 0.0
         evt = self._ev_tables(segs)
-        inj = self.host_hits(text, nbytes, host_text, *(host_index or (None, None)), trim=split_trim)
+        hs = None
+        plan = None
+        if self.lib.host_dev and text.is_cuda and host_text is not None:
+            # the device feeds the backtracker regexes with relaxed automata: their candidate lines
+            # go to the host and the verified keys come back inside the queued step (side_path.hip);
+            # the host side path scans the bytes only for regexes without a device relaxation
+            if self._host_side is None:
+                from .ops.side_path import HostSide
+                self._host_side = HostSide(self.lib, text.device)
+            self._host_side.check()
+            hs = (self._host_side, np.asarray(host_text, dtype=np.uint8))
+            plan = self.lib.host_plan_undev
+        inj = self.host_hits(text, nbytes, host_text, *(host_index or (None, None)), trim=split_trim, plan=plan)
         if defer:
             hits, hit_line, hit_off, ev_cnt, ev_end, nh_cap, cnt, caps = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
-                self.scan_grid, side=self._side, early=early, defer=True, inject=inj)
+                self.scan_grid, side=self._side, early=early, defer=True, inject=inj, host_side=hs)
             nkeys = len(self.lib.freq_ids)
             ne_cap = caps["ev"]
             out_buf = K.results_buffer(ne_cap, nkeys, text.device)
@@ -557,7 +581,9 @@ class Engine:
             hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
                 text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
                 self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None,
-                side=self._side, early=early, inject=inj)
+                side=self._side, early=early, inject=inj, host_side=hs)
+            if hs is not None:
+                hs[0].check()
         else:
             cand, pre = self.match_candidates(text, nbytes, ls, ll, host_text, timings,
                                               inj=inj if inj is not None else torch.zeros(0, dtype=torch.int64, device=text.device))
@@ -916,7 +942,7 @@ class Engine:
                 ptr("scan_regs"), t["scan_regs"].numel(), st12, self.sp_tuple, ev5, self.lib.n_regexes,
                 len(self.lib.patterns), len(self.lib.freq_ids), self.lib.n_seq_events, self.lib.ctx_dfa_extent[0],
                 self.lib.ctx_dfa_extent[1], self.pf_grid, dev,
-                bool(self.config.get("engine.runner-device-counts", True)))
+                bool(self.config.get("engine.runner-device-counts", True)), bool(self.lib.host_dev))
         return True
 
     def _run_native(self, job: "BatchJob", dl, n: int, turn: Optional[SharedWindowTurn] = None,

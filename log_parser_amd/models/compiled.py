@@ -39,6 +39,7 @@ from .schema import Pattern, PatternSet, pattern_to_json
 log = logging.getLogger("log_parser_amd.compiled")
 
 KIND_DFA, KIND_NFA, KIND_FALLBACK, KIND_INVALID = 0, 1, 2, 3
+RELAX = "(?#relax)"          # jregex: the automaton of the pattern's regular relaxation (a superset)
 BLOOM_BITS = 18
 
 
@@ -346,9 +347,43 @@ class CompiledLibrary:
         self.host_regs: List[int] = []
         self.host_bt_ok: List[bool] = []
         self.host_lits: List[List[bytes]] = []        # backtracker regexes' required literals (host side path)
+        # backtracker regexes whose REGULAR RELAXATION runs on the device (jregex Relaxer: a superset
+        # language): its hits are only candidates, exported to the host backtracker (meta flag 4)
+        self.host_dev: List[int] = []
+        self.device_pattern: Dict[int, str] = {}
         nfa_members: List[Tuple[int, dict]] = []
         ctx_members: List[Tuple[int, dict]] = []
         self._ctx_ext = (0, 0)
+
+        def add_dfa(d, flags=0):
+            nonlocal toff, aoff
+            meta.append([toff, d["nclasses"], aoff, (1 if d["anchored"] else 0) | flags])
+            bytemaps.append(np.frombuffer(d["bytemap"], np.uint8))
+            t = np.frombuffer(d["trans"], np.uint16)
+            trans.append(t)
+            a = np.frombuffer(d["acc"], np.uint8)
+            accs.append(a)
+            toff += t.size
+            aoff += a.size
+
+        def add_bpg(i, prog, flags=0):
+            nonlocal boff
+            meta.append([boff, 1, 0, 2 | flags])
+            bytemaps.append(np.zeros(256, np.uint8))
+            bpgs.append(prog)
+            boff += prog.size
+            self.bpg_regs.append(i)
+
+        def dfa_literals(d):
+            lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
+            if lits and min(len(x) for x in lits) < MIN_LITERAL:
+                lits = []          # a 1-2-byte factor selects nothing: scan every line
+            # anchored regexes (e.g. '^\\s*at\\s+...') die within a few bytes of every line:
+            # scanning all lines beats a short, unselective literal.
+            if d["anchored"] and lits and min(len(x) for x in lits) < 4:
+                lits = []
+            return lits
+
         for i, ri in enumerate(self.regexes):
             if i == 4:
                 self._ctx_ext = (toff, aoff)     # the context DFAs' tables end here
@@ -360,22 +395,8 @@ class CompiledLibrary:
                 ctx_members.append((i, d))
             if ri.kind == KIND_DFA:
                 ri.nstates = d["nstates"]
-                nc = d["nclasses"]
-                meta.append([toff, nc, aoff, 1 if d["anchored"] else 0])
-                bytemaps.append(np.frombuffer(d["bytemap"], np.uint8))
-                t = np.frombuffer(d["trans"], np.uint16)
-                trans.append(t)
-                a = np.frombuffer(d["acc"], np.uint8)
-                accs.append(a)
-                toff += t.size
-                aoff += a.size
-                lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
-                if lits and min(len(x) for x in lits) < MIN_LITERAL:
-                    lits = []          # a 1-2-byte factor selects nothing: scan every line
-                # anchored regexes (e.g. '^\\s*at\\s+...') die within a few bytes of every line:
-                # scanning all lines beats a short, unselective literal.
-                if d["anchored"] and lits and min(len(x) for x in lits) < 4:
-                    lits = []
+                add_dfa(d)
+                lits = dfa_literals(d)
                 if ri.roles == {"context"}:
                     # built-in context regexes are evaluated lazily, only on lines inside some
                     # event's context window (k_feat), never by the whole-log match stage
@@ -394,11 +415,7 @@ class CompiledLibrary:
                     # (MULTILINE anchors, Unicode \b): a bit-parallel Glushkov program over code
                     # points, dispatched by the verify / scan kernels next to the DFAs (meta bit 1)
                     ri.nstates = int(prog[0] & np.uint64(0xFF)) * 64
-                    meta.append([boff, 1, 0, 2])
-                    bytemaps.append(np.zeros(256, np.uint8))
-                    bpgs.append(prog)
-                    boff += prog.size
-                    self.bpg_regs.append(i)
+                    add_bpg(i, prog)
                     lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
                     if lits and min(len(x) for x in lits) < MIN_LITERAL:
                         lits = []
@@ -406,6 +423,33 @@ class CompiledLibrary:
                     if not ri.literals:
                         self.bpg_scan_regs.append(i)      # every line, one lane per line (k_scan)
                     continue
+                if ri.kind == KIND_FALLBACK and not mfma_ok and d.get("bt_ok") and ri.roles != {"context"}:
+                    # non-regular (backref, lookaround, atomic, possessive): the host backtracker
+                    # decides, but the device finds its candidate lines with the automaton of the
+                    # regex's regular relaxation -- its literals through the prefilter, or, without
+                    # one, its DFA in a literal-free scan group (meta flag 4: exported, never a hit)
+                    dr = N.compile_regex(RELAX + ri.pattern, self.max_dfa_states, 4096)
+                    rprog = np.frombuffer(dr["bpg"], np.uint64) if dr["kind"] == KIND_NFA and dr["bpg"] else None
+                    if dr["kind"] == KIND_DFA or rprog is not None:
+                        log.info("regex %r: host backtracker, device-fed by its relaxation", ri.pattern)
+                        self.host_regs.append(i)
+                        self.host_bt_ok.append(True)
+                        lits = _minimize_literals(list(d["literals"])) if d["has_literals"] else []
+                        self.host_lits.append(lits if lits and min(len(x) for x in lits) >= MIN_LITERAL else [])
+                        self.host_dev.append(i)
+                        self.device_pattern[i] = RELAX + ri.pattern
+                        if rprog is not None:
+                            add_bpg(i, rprog, 4)
+                            lits = _minimize_literals(list(dr["literals"])) if dr["has_literals"] else []
+                            ri.literals = lits if lits and min(len(x) for x in lits) >= MIN_LITERAL else []
+                            if not ri.literals:
+                                self.bpg_scan_regs.append(i)
+                        else:
+                            add_dfa(dr, 4)
+                            ri.literals = dfa_literals(dr)
+                            if not ri.literals:
+                                self.scan_regs.append(i)
+                        continue
                 meta.append([0, 1, 0, 0])
                 bytemaps.append(np.zeros(256, np.uint8))
                 if ri.kind == KIND_INVALID:
@@ -414,9 +458,9 @@ class CompiledLibrary:
                     # engine.nfa-engine=mfma: simulate the NFA with the MFMA state-transition kernel
                     nfa_members.append((i, d))
                 else:
-                    # non-regular (backref, lookaround, atomic, possessive): the native backtracker on
-                    # the host, as a side path before the device pipeline (Engine.host_hits) --
-                    # lines holding a required literal, or every line without one
+                    # no automaton even for its relaxation: the native backtracker on the host, as a
+                    # side path before the device pipeline (Engine.host_hits) -- lines holding a
+                    # required literal, or every line without one
                     log.info("regex %r runs on the host backtracker (%s)", ri.pattern, ri.error)
                     if not d.get("bt_ok"):
                         log.error("regex %r: no engine runs it (%s); it never matches", ri.pattern, ri.error)
@@ -463,6 +507,12 @@ class CompiledLibrary:
         # (local index, global id, required literals) of every runnable backtracker regex
         self.host_plan = [(int(self.host_local[r]), r, lits) for r, lits in zip(self.host_regs, self.host_lits)
                           if self.host_local[r] >= 0]
+        # ... of those the device cannot feed (no automaton even for the relaxation): the host side
+        # path scans the batch's bytes for them when the device feeds the others (side_path.hip)
+        dev = set(self.host_dev)
+        self.host_plan_undev = [x for x in self.host_plan if x[1] not in dev]
+        self.host_dev_mask = np.zeros(max(R, 1), bool)
+        self.host_dev_mask[self.host_dev] = True
 
     # multi-regex DFA scan groups (csrc/kernels/scan_multi.hip)
     SCAN_GROUP_REGS = 32            # members per multi-regex DFA (masks hold 64; one 46-member group
@@ -475,6 +525,10 @@ class CompiledLibrary:
     def _row_stride(d) -> int:
         ncol = d["nclasses"] + 2                      # hold, '\n', classes
         return ncol if ncol % 2 else ncol + 1         # odd: rows start on spread-out banks
+
+    def _dpat(self, r: int) -> str:
+        """The pattern the device automata run for regex ``r`` (a backtracker regex: its relaxation)."""
+        return self.device_pattern.get(r, self.regexes[r].pattern)
 
     def _build_scan_passes(self):
         """Literal-free regexes -> multi-regex DFA groups (greedy, in registry order: a regex joins
@@ -492,14 +546,14 @@ class CompiledLibrary:
 
         for r in self.scan_regs:
             if cur and len(cur) < self.SCAN_GROUP_REGS:
-                d = N.compile_multi([self.regexes[x].pattern for x in cur + [r]], self.SCAN_MAX_STATES)
+                d = N.compile_multi([self._dpat(x) for x in cur + [r]], self.SCAN_MAX_STATES)
                 if fits(d):
                     cur.append(r)
                     cur_d = d
                     continue
             if cur:
                 groups.append((cur, cur_d))
-            d = N.compile_multi([self.regexes[r].pattern], self.SCAN_MAX_STATES)
+            d = N.compile_multi([self._dpat(r)], self.SCAN_MAX_STATES)
             if fits(d):
                 cur, cur_d = [r], d
             else:
@@ -746,6 +800,7 @@ class CompiledLibrary:
         t["prim_cnt"] = T(np.diff(self.prim_off))
         t["freq_key"] = T(self.freq_key)
         t["is_primary"] = T(np.diff(self.prim_off) > 0)
+        t["host_dev"] = bool(self.host_dev)          # backtracker regexes fed by their relaxed automata
         t["nfa_tables"] = T(self.nfa_tables.view(np.int64))
         t["nfa_ctx_list"] = T(np.array(self.nfa_ctx_groups, np.int32))
         t["nfa_scan_lists"] = {k: T(np.array([g for g in self.nfa_scan_groups if self.nfa_group_ncls[g] == k], np.int32))
@@ -771,7 +826,7 @@ class CompiledLibrary:
         kinds = [r.kind for r in self.regexes]
         return {
             "patterns": len(self.patterns), "pattern_sets": len(self.pattern_sets), "regexes": len(self.regexes),
-            "dfa": kinds.count(KIND_DFA), "host_fallback": len(self.host_regs),
+            "dfa": kinds.count(KIND_DFA), "host_fallback": len(self.host_regs), "host_device_fed": len(self.host_dev),
             "host_backtracker": int((self.host_local >= 0).sum()) if self.host_regs else 0,
             "invalid": kinds.count(KIND_INVALID), "scan_all": len(self.scan_regs), "literals": len(self.literals),
             "teddy_literals": int(self.pf["teddy_lits"]), "prefilter_stride": int(self.pf["stride"]),

@@ -446,7 +446,7 @@ class EarlyPrefilter:
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
                    ws: Optional[Workspace], pf_grid: int, scan_grid, timings=None, tick=None, side=None,
                    early: Optional[EarlyPrefilter] = None, defer: bool = False,
-                   inject: Optional[torch.Tensor] = None):
+                   inject: Optional[torch.Tensor] = None, host_side=None):
     """GPU: every matcher appends to the arena, then the post-match hit pipeline reads the device
     counters itself -> (hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne) with ONE host read.
 
@@ -461,7 +461,12 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
     overlap almost fully.
 
     ``inject``: device keys verified elsewhere (the host backtracker's side path,
-    ``Engine.host_hits``), appended to the verified-hit buffer like a self-verifying engine's."""
+    ``Engine.host_hits``), appended to the verified-hit buffer like a self-verifying engine's.
+
+    ``host_side`` = (ops.side_path.HostSide, host bytes): the backtracker regexes fed by their
+    relaxed automata export their device candidates to the host and get the verified keys back,
+    all queued (side_path.hip); without it their device keys are only dropped (the host side path
+    ran for them before, ``inject``)."""
     dev = text.device
     L = line_start.numel()
     st = _s(text)
@@ -501,8 +506,6 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             if glist.numel():
                 N.nfa(tabs["nfa_tables"].data_ptr(), glist.data_ptr(), glist.numel(), ncls, 0, L, text.data_ptr(),
                       line_start.data_ptr(), line_len.data_ptr(), 0, ver.data_ptr(), cap["ver"], c0 + 16, sst, True)
-        if ninj:
-            N.append_keys(ver.data_ptr(), cap["ver"], c0 + 16, inject.data_ptr(), ninj, sst)
         if sst != st:
             side[2].record(side[0])
         elif tick:
@@ -518,6 +521,14 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             tick("prefilter")
         if sst != st:
             torch.cuda.current_stream(dev).wait_event(side[2])
+        if host_side is not None:          # export -> host backtracker -> append, all queued
+            host_side[0].queue(cand, c0 + 8, cap["cand"], ver, c0 + 16, cap["ver"], text, line_start, line_len,
+                               tabs["dfa"], st, host_side[1])
+        elif tabs.get("host_dev"):         # relaxation keys of regexes the host side path decided
+            N.take_host(cand.data_ptr(), c0 + 8, cap["cand"], ver.data_ptr(), c0 + 16, cap["ver"], text.data_ptr(),
+                        line_start.data_ptr(), line_len.data_ptr(), tabs["dfa"], None, st)
+        if ninj:                           # (after the take: these keys are decided, never dropped)
+            N.append_keys(ver.data_ptr(), cap["ver"], c0 + 16, inject.data_ptr(), ninj, st)
         n = cap["cand"] + cap["ver"]
         hits = torch.empty(n, dtype=torch.int64, device=dev)
         hit_line = torch.empty(n, dtype=torch.int32, device=dev)

@@ -210,6 +210,34 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
     return [PatternSet.model_validate(s) for s in sets], triggers
 
 
+def backtracker_patterns(n: int, seed: int = 0) -> Tuple[PatternSet, List[dict]]:
+    """``n`` primaries only a backtracker decides (backreferences, lookaround,
+    possessive / atomic groups) + matching samples: n - 1 carry a pattern-specific literal (the
+    device prefilter narrows them), the last one has none (its relaxed automaton runs in a
+    literal-free scan group). The shapes real libraries use: a repeated id, "Fail" not followed by
+    "ure", an error not preceded by "retrying", a restart loop of the same pod."""
+    rng = random.Random(seed)
+    pats, trig = [], []
+    for i in range(n):
+        tok = _token(rng, 10_000 + i)
+        fam = i % 4
+        if i == n - 1:
+            rx, sm = r"^(\d{3})-(\d{4})-\2-\1$", "415-8812-8812-415"
+        elif fam == 0:
+            rx, sm = rf"(\w+) {tok}Loop \1\b", f"worker7 {tok}Loop worker7 again"
+        elif fam == 1:
+            rx, sm = rf"{tok}Fail(?!ure)\w*", f"{tok}Failed to mount"
+        elif fam == 2:
+            rx, sm = rf"(?<!retrying )\b{tok}Err\b", f"fatal {tok}Err in worker"
+        else:
+            rx, sm = rf"(?i)(?>{tok}Lock)+\s+held", f"{tok.upper()}LOCK held by 7"
+        pats.append({"id": f"bt-{i:04d}", "name": f"backtracker shape {i}", "severity": rng.choice(SEVERITIES),
+                     "primary_pattern": {"regex": rx, "confidence": round(rng.uniform(0.3, 0.95), 3)}})
+        trig.append({"sample": sm, "secondary": [], "sequence": []})
+    ps = PatternSet.model_validate({"metadata": {"library_id": "backtracker", "version": "1.0"}, "patterns": pats})
+    return ps, trig
+
+
 def realistic_library(n_patterns: int, seed: int = 0, **kw):
     """The headline bench library: the synthetic mix plus ~10% primaries with only a 3-6-byte
     literal, ~5% literal-free primaries, ~1.5% bounded-gap primaries (``X.{0,120}Y``, each

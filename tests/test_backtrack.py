@@ -196,3 +196,88 @@ def test_host_regex_side_path_without_host_bytes(gpu_device):
     assert torch.equal(a, b)
     hr = torch.tensor(lib.host_regs)
     assert bool(torch.isin(a >> 32, hr).any())
+
+
+def _bt_library(n_bt=6):
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.utils.config import ScoringParams
+    from log_parser_amd.utils.synth import backtracker_patterns, make_library
+    sets, trig = make_library(40, seed=71, sequence_rate=0.5)
+    ps, bt_trig = backtracker_patterns(n_bt, seed=3)
+    return sets + [ps], trig + bt_trig, CompiledLibrary(sets + [ps], ScoringParams())
+
+
+def test_relaxation_is_a_superset_and_device_fed():
+    """Every backtracker shape of the bench gets a regular relaxation (a DFA / BPG program on the
+    device), whose find() holds wherever the Java-semantics original's does -- so the candidate
+    lines the device hands the host never miss a match."""
+    import random
+    from log_parser_amd.native import N
+    from log_parser_amd.regex.javacompat import compile_java
+    sets, trig, lib = _bt_library(8)
+    assert len(lib.host_dev) == 8 and not lib.host_plan_undev
+    pats = [p.primary_pattern.regex for p in sets[-1].patterns] + [
+        r"(\w+)Aux0 \1", r"^(\w*)\1$", r"(?i)fatal (?=\w+Failure)", r"(?<!INFO )ERROR\b", r"(?>a+)b", r"x++y",
+        r"(?i)(ab)\1", r"(?m)^ERR(?=\w)", r"(?<=id=)(\d+) .* \1"]
+    rng = random.Random(5)
+    toks = ["ab", "AB", "a", "b", "z", "x", "y", "123", "-", "415-8812-8812-415", "ERROR", "INFO ", "fatal ",
+            "FooFailure", "Aux0", "id=", "7", " ", "é"] + [t["sample"] for t in trig[-8:]]
+    lines = ["".join(rng.choice(toks) for _ in range(rng.randint(0, 10))) for _ in range(4000)]
+    from log_parser_amd.models.compiled import CompiledLibrary
+    from log_parser_amd.models.schema import PatternSet
+    from log_parser_amd.utils.config import ScoringParams
+    relaxed = CompiledLibrary([PatternSet.model_validate({"metadata": {"library_id": "r"}, "patterns": [
+        {"id": f"r{i}", "name": p, "severity": "LOW", "primary_pattern": {"regex": "(?#relax)" + p, "confidence": 0.5}}
+        for i, p in enumerate(pats)]})], ScoringParams())
+    from log_parser_amd.engine import Engine
+    from log_parser_amd.ops import kernels as K
+    from log_parser_amd.utils.config import Config
+    for p in pats:
+        d = N.compile_regex("(?#relax)" + p, 2048, 4096)
+        assert d["kind"] in (0, 1), (p, d["error"])
+    eng = Engine(relaxed, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    blob = "\n".join(lines).encode()
+    t = torch.zeros(K.padded_len(len(blob)), dtype=torch.uint8)
+    t[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
+    ls, ll = K.split_lines(t, len(blob))
+    hits = set(eng.match_hits(t, len(blob), ls, ll).tolist())
+    n_orig = 0
+    for i, p in enumerate(pats):
+        rx = compile_java(p)
+        r = int(relaxed.primary_reg[i])
+        for j, s in enumerate(lines):
+            if rx.search(s) is not None:
+                n_orig += 1
+                assert (r << 32 | j) in hits, (p, s)
+    assert n_orig > 200
+
+
+@pytest.mark.gpu
+def test_device_fed_backtracker_bulk_step_equals_cpu(gpu_device):
+    """The bulk step with backtracker primaries: their relaxed automata find candidate lines on the
+    GPU, k_take_host exports them, the host checks them while the step stays queued, k_wait_host
+    appends the verified keys -- events and scores equal the CPU engine's (host side path)."""
+    from log_parser_amd.engine import Engine, Segments
+    from log_parser_amd.ops import kernels as K
+    from log_parser_amd.parallel.dp import ShardedAnalyzer
+    from log_parser_amd.utils.config import Config
+    from log_parser_amd.utils.synth import make_log
+    sets, trig, lib = _bt_library(6)
+    logs = make_log(30000, trig, seed=72, hit_rate=0.06)
+    data = logs.encode()
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    cpu = Engine(lib, Config.load(overrides={"engine.device": "cpu"}), device=torch.device("cpu"))
+    ls, ll = K.split_lines(t, len(data))
+    ref = cpu.run(t, len(data), ls, ll, Segments.single(ls.numel(), t.device), cpu.freq_carry(),
+                  host_text=np.frombuffer(data, np.uint8))
+    bt_ids = {lib.patterns.index(p) for p in sets[-1].patterns}
+    assert sum(int(x) in bt_ids for x in ref.ev_pat.numpy()) >= 20
+    eng = Engine(lib, Config.load(overrides={"engine.device": str(gpu_device)}), device=gpu_device)
+    sa = ShardedAnalyzer(eng)
+    for _ in range(3):                    # repeated steps: sequence numbers, reused export buffers
+        out = sa.step(t.to(gpu_device), len(data), None, None, 0, 0, topk=5, host_text=np.frombuffer(data, np.uint8))
+        r = out.result
+        np.testing.assert_array_equal(r.ev_line.cpu().numpy(), ref.ev_line.numpy())
+        np.testing.assert_array_equal(r.ev_pat.cpu().numpy(), ref.ev_pat.numpy())
+    assert eng._host_side is not None and eng._host_side.seq >= 3

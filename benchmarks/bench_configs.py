@@ -317,6 +317,7 @@ def mode_concurrent_http(args):
         extra.append("-Dserver.stage-timeline=true")
     srv = ServerProcess(write_library(sets), dev, http="native", extra=extra + list(args.server_opt or []),
                         log_path=args.server_log)
+    conn_phases = None
     try:
         if not srv.wait_ready(workers=max(args.processes, 1)):
             raise SystemExit("server did not come up")
@@ -338,7 +339,13 @@ def mode_concurrent_http(args):
         thr0 = cgroup_throttling()
         ss0 = srv.sched_ns()
         cpu0, cli0 = srv.cpu_seconds(), time.process_time()
+        sampler = None
+        if args.sample_threads:      # every server thread's state / wait channel / syscall, every 1 ms
+            from log_parser_amd.utils.threadsample import ThreadSampler
+            sampler = ThreadSampler(srv._pids(), 0.001).start()
         lat, st, wall, done = N.http_burst("127.0.0.1", srv.port, msgs, idx, 600.0, args.client_threads)
+        if sampler is not None:
+            sampler.stop()
         cpu_srv, cpu_cli = srv.cpu_seconds() - cpu0, time.process_time() - cli0
         ss1 = srv.sched_ns()
         thr1 = cgroup_throttling()
@@ -348,7 +355,23 @@ def mode_concurrent_http(args):
         sched = {"server_run_s": round((ss1[0] - ss0[0]) / 1e9, 3), "server_wait_s": round((ss1[1] - ss0[1]) / 1e9, 3)}
         st1 = collect_stages(srv.port, workers)
         breakdown = stage_breakdown(st0, st1, wall)
-        if args.timeline:           # per process: stage intervals of the timed burst, ms from its start
+        conn_phases = None
+        if args.timeline:           # per /parse response of the burst: where its time went (native front end)
+            recs = [r for d in st1.values() for r in d.get("conns", []) if r[5] >= 0]
+            if recs:
+                a = np.array(recs)
+                a = a[a[:, 5] >= a[:, 5].max() - wall - 0.05]          # the timed burst's responses
+                t0 = a[:, 2].min()
+
+                def q(x):
+                    return [round(float(np.percentile(x, k)) * 1e3, 3) for k in (50, 90, 99, 100)]
+                conn_phases = {"responses": int(len(a)),
+                               "ms_p50_p90_p99_max": {"first_byte_after_burst_start": q(a[:, 2] - t0),
+                                                      "receive": q(a[:, 3] - a[:, 2]),
+                                                      "parsed_to_handed_back": q(a[:, 4] - a[:, 3]),
+                                                      "send": q(a[:, 5] - a[:, 4])},
+                               "per_io_thread": {str(int(k)): int((a[:, 0] == k).sum()) for k in np.unique(a[:, 0])},
+                               "parsed_by_ms": np.histogram(a[:, 3] - t0, bins=np.arange(0, wall * 1e3 + 1, 10) / 1e3)[0].tolist()}
             for pid, d in st1.items():
                 t_end = d["now"]
                 ev = [e for e in d.get("timeline", []) if e[3] >= t_end - wall - 0.05]
@@ -378,6 +401,9 @@ def mode_concurrent_http(args):
                       # CFS quota throttling during the burst (cgroup cpu.stat deltas)
                       "cgroup_throttling": throttle,
                       "sched": sched,
+                      "thread_states": sampler.summary() if sampler is not None else None,
+                      "conn_phases": conn_phases,
+                      "thread_samples": sampler.samples if sampler is not None else 0,
                       "transport": "native HTTP/1.1 front end, one keep-alive connection per request, 127.0.0.1"}))
 
 
@@ -404,6 +430,8 @@ def main():
     ap.add_argument("--requests", type=int, default=None)
     ap.add_argument("--chunk-mb", type=int, default=0, help="stream / resident chunk MiB (0 = from free HBM)")
     ap.add_argument("--timeline", action="store_true", help="concurrent: print the pipeline stage timeline")
+    ap.add_argument("--sample-threads", action="store_true",
+                    help="concurrent_http: sample every server thread's state / wait channel every 1 ms")
     ap.add_argument("--engines", type=int, default=1, help="concurrent: serving engines (one per GPU)")
     ap.add_argument("--processes", type=int, default=1,
                     help="concurrent_http: serving processes sharing one frequency window (server.processes)")

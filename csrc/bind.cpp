@@ -1064,14 +1064,26 @@ PYBIND11_MODULE(_lpnative, m) {
 
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init([](const std::string& host, int port, int io_threads, int64_t max_body, double idle,
-                       double io_spin_us, double pump_spin_us, bool quickack, int rcvbuf, bool trace) {
+                       double io_spin_us, double pump_spin_us, bool quickack, int rcvbuf, bool trace,
+                       bool conn_trace) {
              HttpOptions o;
              o.io_spin_us = io_spin_us; o.pump_spin_us = pump_spin_us; o.quickack = quickack; o.rcvbuf = rcvbuf;
              o.trace = trace;
+             o.conn_trace = conn_trace;
              return new HttpServer(host, port, io_threads, max_body, idle, o);
            }), py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30,
            py::arg("idle_timeout_s") = 60.0, py::arg("io_spin_us") = 0.0, py::arg("pump_spin_us") = 1000.0,
-           py::arg("quickack") = true, py::arg("rcvbuf") = 0, py::arg("trace") = false)
+           py::arg("quickack") = true, py::arg("rcvbuf") = 0, py::arg("trace") = false, py::arg("conn_trace") = false)
+      .def("conn_trace", [](HttpServer& s) {
+        std::vector<std::vector<double>> v;
+        {
+          py::gil_scoped_release nogil;
+          v = s.conn_trace();
+        }
+        py::array_t<double> a({(py::ssize_t)v.size(), (py::ssize_t)6});
+        for (size_t i = 0; i < v.size(); ++i) std::memcpy(a.mutable_data(i, 0), v[i].data(), 6 * sizeof(double));
+        return a;
+      })
       .def_property_readonly("port", &HttpServer::port)
       .def("pending", &HttpServer::pending)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms, bool raw) {

@@ -3,6 +3,9 @@
 // in flight per connection (responses therefore stay in request order without pipelining state).
 #include "io/http_server.h"
 
+#include <pthread.h>
+#include <cstdio>
+
 #include <arpa/inet.h>
 #include <fcntl.h>
 #include <netinet/in.h>
@@ -97,6 +100,7 @@ struct HttpServer::Conn {
   double last = 0;          // last read / write activity (idle-timeout sweep)
   double t_first = 0;       // first byte of the request being received
   double t_resp = 0;        // respond() of the response being written (0: none timed)
+  double t_accept = 0, t_parse = 0, t_handoff = 0;   // conn_trace
   int n_recv = 0, n_wake = 0;
 };
 
@@ -114,6 +118,8 @@ struct HttpServer::Io {
     double t_resp;
   };
   std::vector<Out> outbox;
+  std::mutex tm;                          // conn_trace records (HttpOptions.conn_trace)
+  std::vector<std::vector<double>> trace;
 };
 
 HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_t max_body, double idle_timeout_s,
@@ -130,6 +136,7 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
   quickack_ = opt.quickack;
   rcvbuf_ = opt.rcvbuf;
   trace_ = opt.trace;
+  conn_trace_ = opt.conn_trace;
   for (int i = 0; i < io_threads; ++i) {
     auto io = std::make_unique<Io>();
     io->index = i;
@@ -160,7 +167,13 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
     epoll_ctl(io->ep, EPOLL_CTL_ADD, io->efd, &ev);
     ios_.push_back(std::move(io));
   }
-  for (auto& io : ios_) threads_.emplace_back([this, p = io.get()] { io_loop(p); });
+  for (auto& io : ios_)
+    threads_.emplace_back([this, p = io.get(), k = (int)threads_.size()] {
+      char nm[16];
+      std::snprintf(nm, sizeof nm, "lp-io%d", k);
+      pthread_setname_np(pthread_self(), nm);     // (serving diagnostics: utils/threadsample.py)
+      io_loop(p);
+    });
 }
 
 HttpServer::~HttpServer() { stop(); }
@@ -309,9 +322,15 @@ void HttpServer::flush(Io* io, Conn* c) {
     c->out.clear();
     c->out_off = 0;
     if (c->t_resp > 0) {
+      const double ts = now_s();
       stages.sent++;
-      stages.send_ns += (uint64_t)std::max(0.0, (now_s() - c->t_resp) * 1e9);
+      stages.send_ns += (uint64_t)std::max(0.0, (ts - c->t_resp) * 1e9);
       c->t_resp = 0;
+      if (conn_trace_ && c->t_parse > 0) {
+        std::lock_guard<std::mutex> lk(io->tm);
+        io->trace.push_back({(double)io->index, c->t_accept, c->t_first, c->t_parse, c->t_handoff, ts});
+        c->t_parse = 0;
+      }
     }
     if (c->closing) {
       close_conn(io, c);
@@ -443,6 +462,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     // object the engine packs from (bind.cpp next_requests)
     PodRequest pr;
     const double tv = r.t_arrival;
+    c->t_parse = tv;
     const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
     const double tz = now_s();
     stages.parse++;
@@ -565,6 +585,7 @@ void HttpServer::io_loop(Io* io) {
           Conn* c = new Conn();
           c->fd = fd;
           c->last = now_s();
+          c->t_accept = c->last;
           c->id = (io->next_conn++) + 1;  // ids 0 / 1 are the listener / eventfd tags
           io->conns[c->id] = c;
           epoll_event ev{};
@@ -593,6 +614,7 @@ void HttpServer::io_loop(Io* io) {
             set_events(io, c);
           }
           const double tp = now_s();
+          c->t_handoff = tp;
           stages.responses++;
           stages.handoff_ns += (uint64_t)std::max(0.0, (tp - o.t_resp) * 1e9);
           if (c->out.empty()) c->t_resp = tp;
@@ -642,4 +664,16 @@ void HttpServer::io_loop(Io* io) {
   io->graveyard.clear();
 }
 
+}  // namespace lp
+
+namespace lp {
+std::vector<std::vector<double>> HttpServer::conn_trace() {
+  std::vector<std::vector<double>> out;
+  for (auto& io : ios_) {
+    std::lock_guard<std::mutex> lk(io->tm);
+    out.insert(out.end(), io->trace.begin(), io->trace.end());
+    io->trace.clear();
+  }
+  return out;
+}
 }  // namespace lp

@@ -63,6 +63,7 @@ struct HttpOptions {
   bool quickack = true;         // TCP_QUICKACK re-armed per read
   int rcvbuf = 0;               // SO_RCVBUF of accepted sockets (0 = autotuned)
   bool trace = false;           // per-request receive / validate timings on stderr
+  bool conn_trace = false;      // per /parse response: accept / first byte / parsed / handed back / sent times
 };
 
 class HttpServer {
@@ -91,6 +92,10 @@ class HttpServer {
   void stop();
   HttpStats stats;
   HttpStageStats stages;
+  // conn_trace: one record per /parse response sent since the last call -- (IO thread, accept,
+  // first byte, request parsed, response handed to the IO thread, response sent), steady-clock
+  // seconds (= Python time.perf_counter on Linux)
+  std::vector<std::vector<double>> conn_trace();
 
   struct Conn;
   struct Io;
@@ -111,6 +116,7 @@ class HttpServer {
   double idle_timeout_s_;
   double io_spin_s_ = 0;     // HttpOptions (seconds)
   bool trace_ = false;
+  bool conn_trace_ = false;
   double pump_spin_s_ = 0;
   bool quickack_ = true;
   int rcvbuf_ = 0;

@@ -13,6 +13,8 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <pthread.h>
+
 #include <thread>
 #include <vector>
 
@@ -75,7 +77,11 @@ class HostPool {
   HostPool() {
     const unsigned hw = std::thread::hardware_concurrency();
     nworkers_ = (int)std::max(1u, std::min(hw ? hw : 8u, 16u)) - 1;
-    for (int i = 0; i < nworkers_; ++i) std::thread([this, i] { loop(i); }).detach();
+    for (int i = 0; i < nworkers_; ++i)
+      std::thread([this, i] {
+        pthread_setname_np(pthread_self(), "lp-host");
+        loop(i);
+      }).detach();
   }
 
   void work() {

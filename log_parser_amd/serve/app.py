@@ -152,6 +152,8 @@ class Batcher:
             return seq, batch
 
     def _loop(self, eng: Engine):
+        from ..utils.threadsample import set_os_thread_name
+        set_os_thread_name("lp-batcher")
         if eng.device.type == "cuda":
             torch.cuda.set_device(eng.device)
             if len(self.engines) > 1:      # own stream per worker: engines sharing a GPU overlap

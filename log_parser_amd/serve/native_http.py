@@ -39,7 +39,7 @@ class NativeHttpFrontend:
                                 float(cfg["server.idle-timeout-s"]), io_spin_us=float(cfg["server.io-spin-us"]),
                                 pump_spin_us=float(cfg["server.pump-spin-us"]),
                                 quickack=bool(cfg["server.tcp-quickack"]), rcvbuf=int(cfg["server.rcvbuf-bytes"]),
-                                trace=trace)
+                                trace=trace, conn_trace=bool(cfg.get("server.stage-timeline", False)))
         self.port = self.srv.port
         self._stop = threading.Event()
         # server.trace-requests: per /parse request on stderr -- receive / validate (native side),
@@ -67,6 +67,8 @@ class NativeHttpFrontend:
         return cb
 
     def _pump(self) -> None:
+        from ..utils.threadsample import set_os_thread_name
+        set_os_thread_name("lp-pump")
         b = self.svc.batcher()
         direct = b.pipe is not None
         while not self._stop.is_set():
@@ -172,6 +174,9 @@ class NativeHttpFrontend:
             out["requests"] = pipe.requests
             if pipe.timeline is not None:
                 out["timeline"] = list(pipe.timeline)
+                # per /parse response since the last call: (IO thread, accept, first byte, parsed,
+                # handed back, sent) -- perf_counter seconds
+                out["conns"] = self.srv.conn_trace().tolist()
         out["now"] = time.perf_counter()
         return out
 

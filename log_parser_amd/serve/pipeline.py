@@ -100,6 +100,8 @@ class BatchPipeline:
         self._dq.put((job, done, t0))
 
     def _device_loop(self) -> None:
+        from ..utils.threadsample import set_os_thread_name
+        set_os_thread_name("lp-pipe-device")
         eng = self.engine
         if eng.device.type == "cuda":
             torch.cuda.set_device(eng.device)
@@ -122,6 +124,8 @@ class BatchPipeline:
                 self._finish(job, done, None, e, t0)
 
     def _emit_loop(self) -> None:
+        from ..utils.threadsample import set_os_thread_name
+        set_os_thread_name("lp-pipe-emit")
         while True:
             item = self._eq.get()
             if item is None:

@@ -74,6 +74,9 @@ def parse():
                     help="process group: auto = nccl (RCCL) on GPUs at every world size, gloo on CPU for world "
                          "size > 1 and none on CPU at world size 1; nccl / gloo / none force one (gloo on GPUs "
                          "= host-staged, to rehearse several ranks on ONE GPU; none = no collectives at world 1)")
+    ap.add_argument("--counted-repeats", type=int, default=0,
+                    help="add N primaries with a wide bounded repeat (X.{0,2100}Y, X[^;]{0,5000}Y, X\\S{0,20000}Y): "
+                         "counted BPG positions")
     ap.add_argument("--bt-patterns", type=int, default=0,
                     help="add N primaries only a backtracker decides (backreference / lookaround / atomic; N-1 with "
                          "a literal, one literal-free): the device feeds them with their relaxed automata and the host "
@@ -106,7 +109,8 @@ def make_blocks(args, trig):
 
 
 def library(args):
-    from log_parser_amd.utils.synth import backtracker_patterns, make_library, realistic_library
+    from log_parser_amd.utils.synth import (backtracker_patterns, counted_repeat_patterns, make_library,
+                                            realistic_library)
     if args.library == "realistic":
         sets, trig = realistic_library(args.patterns, seed=7)
     else:
@@ -114,6 +118,9 @@ def library(args):
     if args.bt_patterns > 0:
         ps, bt_trig = backtracker_patterns(args.bt_patterns, seed=7)
         sets, trig = sets + [ps], trig + bt_trig
+    if args.counted_repeats > 0:
+        ps, cr_trig = counted_repeat_patterns(args.counted_repeats, seed=7)
+        sets, trig = sets + [ps], trig + cr_trig
     return sets, trig
 
 
@@ -401,6 +408,7 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
                        "global_batch": total_lines, "seq_len": round(nbytes / max(own_lines, 1), 1),
                        "parallelism": f"dp{world}", "lines_per_gpu": own_lines, "bytes_per_gpu": nbytes,
                        "distinct_blocks": B, "block_lines": args.block_lines,
+                       "extra_primaries": {"backtracker": args.bt_patterns, "counted_repeats": args.counted_repeats},
                        "events_per_step": int(last.pattern_counts.sum().item()),
                        "events_to_host_rank0": state["events_host"],
                        "library_kind": args.library, "library": lib.summary(), "prefilter_stride": lib.pf["stride"], "device": str(device)},

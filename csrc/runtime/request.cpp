@@ -325,14 +325,6 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       scan_multi_dev(text, nbytes, ls, ll, L, S_.scans[i], ver, cap_v, c0 + 2, S_.scan_grids[i], stream);
     if (S_.n_scan_regs)
       scan_dev(text, ls, ll, L, S_.scan_regs, S_.n_scan_regs, S_.dfa, ver, cap_v, c0 + 2, stream);
-    if (ninj > 0) {   // the backtracker regexes' host-verified hits (Engine.host_hits), pre-verified
-      if (attempt == 0) {
-        grow<true>(inj_host_, inj_cap_, 8 * (size_t)ninj);
-        std::memcpy(inj_host_, inj, 8 * (size_t)ninj);
-      }
-      check(hipMemcpyAsync(inj_dev, inj_host_, 8 * (size_t)ninj, hipMemcpyHostToDevice, st), "host hits H2D");
-      append_keys_dev(ver, cap_v, c0 + 2, inj_dev, ninj, stream);
-    }
     blk_index_dev(ls, L, nblk, blk, stream);
     prefilter_dev(text, nbytes, S_.pf, ls, L, gh, cap_g, c0, S_.pf_grid, stream);
     pf_verify_dev(gh, cap_g, text, nbytes, S_.pf, ls, L, blk, cand, cap_c, c0 + 1, stream, c0,
@@ -340,6 +332,16 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
 
     if (S_.host_dev)   // the relaxed automata's keys: candidates only, decided by the host side path
       take_host_dev(cand, c0 + 1, cap_c, ver, c0 + 2, cap_v, text, ls, ll, S_.dfa, HostSideOut{}, stream);
+    // the backtracker regexes' host-verified hits (Engine.host_hits), pre-verified: appended AFTER
+    // the relaxed keys are dropped (the drop clears every key of a device-fed regex)
+    if (ninj > 0) {
+      if (attempt == 0) {
+        grow<true>(inj_host_, inj_cap_, 8 * (size_t)ninj);
+        std::memcpy(inj_host_, inj, 8 * (size_t)ninj);
+      }
+      check(hipMemcpyAsync(inj_dev, inj_host_, 8 * (size_t)ninj, hipMemcpyHostToDevice, st), "host hits H2D");
+      append_keys_dev(ver, cap_v, c0 + 2, inj_dev, ninj, stream);
+    }
     // hit CSR + event counts: the pipeline reads the matchers' device counters itself
     HitsArgs A;
     A.cand = cand; A.n = n; A.pre_from = cap_c;

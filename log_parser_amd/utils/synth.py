@@ -238,6 +238,26 @@ def backtracker_patterns(n: int, seed: int = 0) -> Tuple[PatternSet, List[dict]]
     return ps, trig
 
 
+def counted_repeat_patterns(n: int, seed: int = 0) -> Tuple[PatternSet, List[dict]]:
+    """``n`` primaries with a wide bounded repeat of one class (``X.{0,2100}Y``,
+    ``X[^;]{0,5000}Y``, ``X\\S{0,20000}Y``): the regular shapes past the 2,048-position BPG limit
+    that compile to a counted position (csrc/regex/jregex.cpp ``Glushkov`` counters) + matching
+    samples."""
+    rng = random.Random(seed)
+    pats, trig = [], []
+    shapes = ((r"{a}.{{0,2100}}{b}", "{a} then some text {b}"),
+              (r"{a}[^;]{{0,5000}}{b}", "{a} waited {b}"),
+              (r"{a}\S{{0,20000}}{b}", "{a}/x/y/{b}"))
+    for i in range(n):
+        a, b = _token(rng, 20_000 + 2 * i), _token(rng, 20_001 + 2 * i)
+        rx, sm = shapes[i % len(shapes)]
+        pats.append({"id": f"cr-{i:04d}", "name": f"counted repeat {i}", "severity": rng.choice(SEVERITIES),
+                     "primary_pattern": {"regex": rx.format(a=a, b=b), "confidence": round(rng.uniform(0.3, 0.95), 3)}})
+        trig.append({"sample": sm.format(a=a, b=b), "secondary": [], "sequence": []})
+    ps = PatternSet.model_validate({"metadata": {"library_id": "counted", "version": "1.0"}, "patterns": pats})
+    return ps, trig
+
+
 def realistic_library(n_patterns: int, seed: int = 0, **kw):
     """The headline bench library: the synthetic mix plus ~10% primaries with only a 3-6-byte
     literal, ~5% literal-free primaries, ~1.5% bounded-gap primaries (``X.{0,120}Y``, each

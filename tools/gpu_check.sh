@@ -7,6 +7,7 @@
 #   http    config 5 over HTTP: 1 and 2 serving processes (stage timelines), and the front end alone
 #   stream  config 4: 1B-line stream, auto (HBM-sized) chunks and 256 MiB chunks (same digest)
 #   configs config 2 (1M lines, 256 patterns, realistic library) and config 1 (CPU-only /parse)
+#   singletrace  config 2 kernel timeline (the whole-document step is the last one traced)
 #   reqtrace  one 10k-line request: wall p50 + kernel timeline, library with / without Java shapes
 #   prof    kernel table of the bench step (rocprofv3 kernel trace, serialised ingest)
 #   pmcscan PMC counters of the scan walk and prefilter (two counter passes)
@@ -86,6 +87,12 @@ for s in $steps; do
       run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
       run full_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
       run full_bench 300 python -u bench.py ;;
+    singletrace)
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      run single_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_single -o run -- \
+        python3 benchmarks/bench_configs.py single --steps 20
+      db=$(find gpurun_out/prof_single -name "*.db" | head -1)
+      run single_kstats 120 python3 tools/kstats_db.py "$db" 20 40 --median --marker k_nl_count --last 20 --timeline ;;
     configs)
       run single 600 python -u benchmarks/bench_configs.py single
       run rest 600 python -u benchmarks/bench_configs.py rest ;;

@@ -2,11 +2,22 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 700 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_serve_procs.py tests/test_backtrack.py tests/test_stream.py -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/s_pytest.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/s_pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01 > gpurun_out/s_rt.log 2>&1 || exit 1
-tail -1 gpurun_out/s_rt.log | cut -c1-100
-timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > gpurun_out/s_bench.log 2>&1
-echo "bench rc=$?"
-timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --bt-patterns 4 --parse-requests 0 > gpurun_out/s_bench_bt.log 2>&1
-echo "bench bt rc=$?"
+
+run() {   # run NAME SECONDS CMD... : stop the session at the first failure
+  local name=$1 secs=$2
+  shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/s_${name}.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -2 "gpurun_out/s_${name}.log" | cut -c1-160
+  [ $rc -eq 0 ] || exit $rc
+}
+
+run pytest 700 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_serve_procs.py \
+  tests/test_backtrack.py tests/test_stream.py -m gpu -x -v --timeout 200 --timeout-method thread
+run rt 200 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
+run rt0 200 python -u tools/request_trace.py --requests 400 --java-shape-rate 0
+run bench 400 python -u bench.py --steps 10 --warmup 3
+run bench_nodefer 400 python -u bench.py --steps 10 --warmup 3 --parse-requests 0 --scan-defer-rare 0
+run bench_cr 400 python -u bench.py --steps 10 --warmup 3 --parse-requests 0 --counted-repeats 2
+run bench_bt 400 python -u bench.py --steps 10 --warmup 3 --bt-patterns 4 --parse-requests 0
+bash tools/gpu_check.sh singletrace || exit 1

@@ -57,8 +57,9 @@ __global__ __launch_bounds__(256) void k_pack(const int64_t* __restrict__ cand, 
                                               uint64_t* __restrict__ keys) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t k = (uint64_t)cand[i];
-  keys[i] = ((((k >> 32) << lbits) | (k & 0xFFFFFFFFull)) << 1) | (i >= pre_from ? 1ull : 0ull);
+  const int64_t k = cand[i];            // -1: a dropped key (failed verify, a relaxation's candidate)
+  keys[i] = k < 0 ? LP_PAD_KEY
+                  : (((((uint64_t)k >> 32) << lbits) | ((uint64_t)k & 0xFFFFFFFFull)) << 1) | (i >= pre_from ? 1ull : 0ull);
 }
 
 // device-count mode: region 1 (to verify) then region 2 (pre-verified), each a fixed capacity
@@ -76,8 +77,8 @@ __global__ __launch_bounds__(256) void k_pack_dc(const int64_t* __restrict__ can
   const bool pre = i >= cap1;
   const int64_t j = pre ? i - cap1 : i;
   if (j < (pre ? n2 : n1)) {
-    const uint64_t k = (uint64_t)(pre ? cand2[j] : cand[j]);
-    key = ((((k >> 32) << lbits) | (k & 0xFFFFFFFFull)) << 1) | (pre ? 1ull : 0ull);
+    const int64_t k = pre ? cand2[j] : cand[j];
+    if (k >= 0) key = (((((uint64_t)k >> 32) << lbits) | ((uint64_t)k & 0xFFFFFFFFull)) << 1) | (pre ? 1ull : 0ull);
   }
   keys[i] = key;
 }
@@ -391,6 +392,7 @@ __global__ __launch_bounds__(256) void k_cand_verify(HitsArgs A) {
   if (i >= n1) return;
   int64_t* cand = const_cast<int64_t*>(A.cand);
   const int64_t k = cand[i];
+  if (k < 0) return;                           // dropped (a relaxation's key: k_take_host)
   const int r = (int)(k >> 32);
   if (is_bpg(A.dfa, r)) return;                // bit-parallel Glushkov program: k_bpg_cand
   const int64_t x = k & 0xFFFFFFFFll;
@@ -604,7 +606,7 @@ size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   }
   if (hits_bulk_ok(A)) return hits_bulk_dev(A, ws, ws_bytes, stream);   // bucket sorts (post_bulk.hip)
   const bool dc = A.dcount != nullptr;
-  const int kbits = 1 + A.lbits + A.rbits + (dc ? 1 : 0);    // + the pad bit
+  const int kbits = 2 + A.lbits + A.rbits;    // + the pad bit (dropped keys pad in both modes)
   Carve C{static_cast<uint8_t*>(ws)};
   hipStream_t st = pstream(stream);
   uint64_t* kin = C.take<uint64_t>(n);
@@ -727,8 +729,10 @@ void hits_host(const HitsArgs& A) {
   const int64_t n = A.n;
   std::vector<uint64_t> keys(n);
   for (int64_t i = 0; i < n; ++i) {
-    const uint64_t k = (uint64_t)A.cand[i];
-    keys[i] = ((((k >> 32) << A.lbits) | (k & 0xFFFFFFFFull)) << 1) | (i >= A.pre_from ? 1ull : 0ull);
+    const int64_t k = A.cand[i];
+    keys[i] = k < 0 ? LP_PAD_KEY
+                    : (((((uint64_t)k >> 32) << A.lbits) | ((uint64_t)k & 0xFFFFFFFFull)) << 1) |
+                          (i >= A.pre_from ? 1ull : 0ull);
   }
   std::sort(keys.begin(), keys.end());
   std::vector<int64_t> stdk(n);

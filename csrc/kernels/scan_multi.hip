@@ -55,7 +55,9 @@ constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_THREADS_SMALL = 256;
 constexpr int SCAN_RUN = 4;
 constexpr int SCAN_BM_COPIES = 32;                         // lane-replicated bytemap (bulk variant)
-constexpr int SCAN_BM_REP_BYTES = 512 * SCAN_BM_COPIES * 4; // 64 KiB after the blob
+// 256 entries per copy (the CRLF variant's hold entries 256..511 are all 0: a select instead of a
+// read): 32 KiB after the blob, so a pass blob up to 48 KiB leaves room for 2 blocks per CU
+constexpr int SCAN_BM_REP_BYTES = 256 * SCAN_BM_COPIES * 4;
 
 // LDS loads from a 32-bit LDS address. The blob sits at LDS address 0 (the kernel's only LDS is
 // the dynamic blob; checked at entry), so a row offset + a bytemap byte IS the address: one
@@ -241,7 +243,8 @@ __device__ __forceinline__ void rare_push(const RareList& R, int64_t p0, int64_t
 
 // the hot walk of one run over [a0, p_end) in 16-byte blocks; CRLF: separator '\r' -> hold.
 // REP: the bytemap read goes to this lane's copy of the lane-replicated bytemap at LDS byte bm_rep
-// (entry c at bm_rep + c * 128); otherwise to the blob's bm4 at LDS byte 0. DEFER: hot blocks go to
+// (entry c < 256 at bm_rep + c * 128; the CRLF hold entries are 0 without a read); otherwise to the
+// blob's bm4 at LDS byte 0. DEFER: hot blocks go to
 // the rare list instead of the inline re-walk.
 template <int G, bool CRLF, bool REP, bool DEFER, typename Emit>
 __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass& S, const uint8_t* text, int64_t p_lo,
@@ -276,7 +279,13 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
     for (int j = 0; j < 16; ++j) {
       uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
       if constexpr (CRLF) c |= ((hold >> j) & 1u) << 8;        // entry 256 + c: hold
-      const uint32_t b = lds_ld32(REP ? bm_rep + (c << 7) : c * 4);
+      uint32_t b;
+      if constexpr (REP) {
+        b = lds_ld32(bm_rep + ((c & 0xFFu) << 7));
+        if constexpr (CRLF) b = (c >> 8) ? 0u : b;               // entry 256 + c: hold (column 0)
+      } else {
+        b = lds_ld32(c * 4);
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         mx[g] = max(mx[g], xr[g]);
@@ -320,7 +329,7 @@ __global__ __launch_bounds__(THREADS) void k_scan_multi(const uint8_t* __restric
   uint32_t bm_rep = 0;
   if constexpr (REP) {
     uint32_t* rep = sm + S.lds_words;
-    for (int i = threadIdx.x; i < 512 * SCAN_BM_COPIES; i += THREADS) rep[i] = S.blob[i / SCAN_BM_COPIES];
+    for (int i = threadIdx.x; i < 256 * SCAN_BM_COPIES; i += THREADS) rep[i] = S.blob[i / SCAN_BM_COPIES];
     bm_rep = (uint32_t)S.lds_words * 4 + (threadIdx.x & (SCAN_BM_COPIES - 1)) * 4;
   }
   __syncthreads();

@@ -493,8 +493,10 @@ class Engine:
         """Persistent grid of k_scan_multi: as many blocks per CU as the pass's LDS blob allows."""
         if self.device.type != "cuda":
             return 0
-        # sp[1] = LDS words of the blob; + the 64 KiB lane-replicated bytemap of the 1024-thread blocks
-        per_cu = max(1, min(2, (160 << 10) // max(sp[1] * 4 + (64 << 10), 1)))
+        # sp[1] = LDS words of the blob; + the 32 KiB lane-replicated bytemap of the 1024-thread blocks
+        # (scan_multi.hip SCAN_BM_REP_BYTES): a blob up to 48 KiB gives 2 blocks (8 waves / SIMD with
+        # the deferred rare path's <= 64 VGPRs)
+        per_cu = max(1, min(2, (160 << 10) // max(sp[1] * 4 + (32 << 10), 1)))
         return self.n_cus * per_cu
 
     def _ev_tables(self, segs: "Segments") -> tuple:

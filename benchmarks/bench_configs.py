@@ -164,9 +164,12 @@ def mode_single(args):
         return sa.step(text, n, None, None, 0, 0, topk=100).result
 
     out = {"config": f"single-{args.lines}-lines-256-patterns", "device": str(dev), "bytes": n}
-    # the whole-document step last: a kernel trace's last k_nl_count markers then bracket it
+    # Engine.run_document last: a kernel trace's last k_nl_count markers then bracket it
+    def document(_):
+        return eng.run_document(text, n)
+
     runs = (("resident_run_api", lambda _: once(True)), ("with_h2d_from_pageable", lambda _: once(False)),
-            ("resident", whole_step))
+            ("resident_bulk_step", whole_step), ("resident", document))
     for label, fn in runs:
         for _ in range(3):
             fn(None)

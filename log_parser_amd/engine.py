@@ -653,6 +653,47 @@ class Engine:
         prep = self.prepare(text, nbytes, ls, ll, segs, host_text, timings)
         return self.finish(prep, segs, freq_carry, seq_carry, with_factors)
 
+    def run_document(self, text, nbytes: int, host_text=None, with_factors: bool = False,
+                     record: bool = True) -> RunResult:
+        """One device-resident document end to end (config 2): line index, matching, events,
+        score and the frequency record, with the fewest host round trips -- the literal prefilter
+        is queued behind the line index before its one 24-byte read, matching and events run in
+        device-count mode (``prepare(defer=True)``), and the counts come back in ONE read at the
+        end (a buffer overflow re-runs with the learned capacities, as the bulk step does). The
+        frequency window is read before and recorded after the document (AnalysisService.java:
+        50-122 for one request)."""
+        if not self.can_defer(text):
+            ls, ll = K.split_lines(text, nbytes)
+            segs = Segments.single(ls.numel(), text.device)
+            res = self.run(text, nbytes, ls, ll, segs, self.freq_carry(), host_text=host_text, with_factors=with_factors)
+            if record:
+                self.commit_frequency(res.freq_counts)
+            return res
+        box = []
+        ls, ll = K.split_lines(text, nbytes, before_read=lambda: box.append(self.prefilter_early(text, nbytes)))
+        L = ls.numel()
+        segs = Segments.single(L, text.device)
+        early = box[0] if box else None
+        for attempt in range(4):
+            prep = self.prepare(text, nbytes, ls, ll, segs, host_text=host_text, early=early if attempt == 0 else None,
+                                defer=True)
+            res = self.finish(prep, segs, self.freq_carry(), None, with_factors)
+            h = prep.cnt.cpu().tolist()          # the one count read: gram, cand, ver, hits, events
+            counts = h[:5]
+            if not K.MatchArena.overflow(counts, prep.caps):
+                self.arena.learn_deferred(L, counts)
+                ne, nh = h[4], h[3]
+                res.ev_line, res.ev_pat, res.ev_seg, res.score = (res.ev_line[:ne], res.ev_pat[:ne], res.ev_seg[:ne],
+                                                                  res.score[:ne])
+                if res.factors is not None:
+                    res.factors = res.factors[:ne]
+                res.hit_keys = res.hit_keys[:nh]
+                if record:
+                    self.commit_frequency(res.freq_counts)
+                return res
+            self.arena.learn(L, {"gram": h[0], "cand": h[1], "ver": h[2], "ev": h[4]}, overflow=True)
+        raise RuntimeError("run_document: buffers still overflowing after re-runs")
+
     # ------------------------------------------------------------------ request API
     @property
     def freq_on_device(self) -> bool:

@@ -180,6 +180,28 @@ def test_sharded_single_rank_equals_engine(gpu_device):
     torch.testing.assert_close(out.topk_score, top)
 
 
+def test_run_document_equals_run_and_records(gpu_device):
+    """Engine.run_document (config 2's resident path: line index + early prefilter, deferred
+    counts, one read at the end) equals split_lines + run, twice in a row (the second document
+    sees the first one's frequency record in both engines)."""
+    sets, trig = make_library(80, seed=31)
+    lib = CompiledLibrary(sets, ScoringParams())
+    data = make_log(6000, trig, seed=32, hit_rate=0.05).encode()
+    e1, e2 = _eng(lib, gpu_device), _eng(lib, gpu_device)
+    t, _ = _text(gpu_device, data)
+    for _ in range(2):
+        doc = e1.run_document(t, len(data), with_factors=True)
+        ls, ll = K.split_lines(t, len(data))
+        ref = e2.run(t, len(data), ls, ll, Segments.single(ls.numel(), gpu_device), e2.freq_carry(), with_factors=True)
+        e2.commit_frequency(ref.freq_counts)
+        assert doc.ev_line.numel() == ref.ev_line.numel() > 0
+        assert torch.equal(doc.ev_line, ref.ev_line) and torch.equal(doc.ev_pat, ref.ev_pat)
+        assert torch.equal(doc.hit_keys, ref.hit_keys)
+        torch.testing.assert_close(doc.score, ref.score, rtol=0, atol=0)
+        torch.testing.assert_close(doc.factors, ref.factors, rtol=0, atol=0)
+        assert torch.equal(doc.freq_counts, ref.freq_counts)
+
+
 def _strip(o):
     o = dict(o)
     o.pop("analysisId")

@@ -11,7 +11,7 @@
 #   reqtrace  one 10k-line request: wall p50 + kernel timeline, library with / without Java shapes
 #   prof    kernel table of the bench step (rocprofv3 kernel trace, serialised ingest)
 #   pmcscan PMC counters of the scan walk and prefilter (two counter passes)
-#   httpreps  config 5, 1 process, 5 runs with stage timelines (run-to-run spread)
+#   httpreps  config 5, 1 and 2 processes, 5 runs each: stage / connection timelines, thread states
 #   full    round-end rehearsal: the whole GPU suite, smoke(), the bench
 # Run: gpurun -- bash tools/gpu_check.sh [step ...]
 set -o pipefail
@@ -80,8 +80,13 @@ for s in $steps; do
         -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
       run pmcsum 120 python3 tools/pmc_summary.py gpurun_out/pmc_scan ;;
     httpreps)
-      for rep in 1 2 3 4 5; do
-        run htl_$rep 300 python -u benchmarks/bench_configs.py concurrent_http --processes 1 --client-threads 8 --timeline
+      # config 5, 1 and 2 serving processes, 5 runs each: stage + per-connection timelines and the
+      # serving threads' states sampled every 1 ms (run-to-run spread, the slow mode's cause)
+      for np in 1 2; do
+        for rep in 1 2 3 4 5; do
+          run htl_p${np}_$rep 300 python -u benchmarks/bench_configs.py concurrent_http --processes $np \
+            --client-threads 8 --timeline --sample-threads
+        done
       done ;;
     full)
       run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread

@@ -9,8 +9,13 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include "io/docs.h"
 #include "io/json_in.h"
@@ -169,6 +174,136 @@ struct BtSet {
     if (ex) exhausted++;
     return m;
   }
+};
+
+// The host half of the device-fed backtracker regexes (side_path.hip) as a native thread: no
+// Python and no GIL between the export and the answer, so the GPU's k_wait_host is not held up by
+// the Python thread that is still queuing the rest of the step. Per job it polls the export's
+// sequence word in pinned memory (k_take_host publishes the count, then the sequence), checks the
+// candidate lines with the backtracker on the batch's host bytes, and publishes (count or -1, then
+// the sequence). Layouts (int64 words, cap = the job's capacity): out = keys | starts | lens |
+// count | seq; inb = keys | count | seq.
+class SideWorker {
+ public:
+  SideWorker(BtSet& bt, std::vector<int32_t> local) : bt_(bt), local_(std::move(local)) {
+    th_ = std::thread([this] { loop(); });
+  }
+  ~SideWorker() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void submit(int64_t seq, uint64_t text, int64_t cap, uint64_t out, uint64_t inb) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(Job{seq, reinterpret_cast<const uint8_t*>(text), cap, reinterpret_cast<int64_t*>(out),
+                       reinterpret_cast<int64_t*>(inb)});
+    }
+    cv_.notify_one();
+  }
+  int64_t need() const { return need_.load(); }
+  void clear_need() { need_.store(0); }
+  std::string take_error() {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::string e;
+    e.swap(error_);
+    return e;
+  }
+  int64_t done() const { return done_.load(); }
+
+ private:
+  struct Job {
+    int64_t seq;
+    const uint8_t* text;
+    int64_t cap;
+    int64_t* out;
+    int64_t* inb;
+  };
+  static int64_t load_acq(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+  void fail(const std::string& why) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (error_.empty()) error_ = why;
+  }
+  void run(const Job& j) {
+    int64_t res = -1;
+    const int64_t c = j.cap;
+    // the export lands after the matchers: spin briefly, then nap; give up after 5 s (the GPU's own
+    // wait ends at 2 s: the batch then overflows and re-runs)
+    const auto t0 = std::chrono::steady_clock::now();
+    bool seen = false;
+    for (int it = 0;; ++it) {
+      if (load_acq(j.out + 3 * c + 1) == j.seq) {
+        seen = true;
+        break;
+      }
+      if (it < 4096) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+        continue;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (!seen) {
+      fail("side path: no export for batch " + std::to_string(j.seq) + " within 5 s");
+    } else {
+      const int64_t n = load_acq(j.out + 3 * c);
+      if (n > c) {
+        need_.store(n);                      // re-run with a larger buffer (the batch overflows)
+      } else {
+        const int64_t* K = j.out;
+        const int64_t* S = j.out + c;
+        const int64_t* L = j.out + 2 * c;
+        const int64_t ng = (int64_t)local_.size();
+        std::vector<uint8_t> ok(n, 0);
+        host_parallel(n, 64, [&](int, int64_t a, int64_t e) {
+          for (int64_t i = a; i < e; ++i) {
+            const int64_t g = K[i] >> 32;
+            if (g < 0 || g >= ng || local_[g] < 0) continue;
+            ok[i] = bt_.find(local_[g], j.text + S[i], L[i]) ? 1 : 0;
+          }
+        });
+        res = 0;
+        for (int64_t i = 0; i < n; ++i)
+          if (ok[i]) j.inb[res++] = K[i];
+      }
+    }
+    __atomic_store_n(j.inb + c, res, __ATOMIC_RELEASE);
+    __atomic_store_n(j.inb + c + 1, j.seq, __ATOMIC_RELEASE);   // published last
+    done_++;
+  }
+  void loop() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        j = q_.front();
+        q_.pop_front();
+      }
+      try {
+        run(j);
+      } catch (const std::exception& e) {
+        fail(e.what());
+        __atomic_store_n(j.inb + j.cap, (int64_t)-1, __ATOMIC_RELEASE);
+        __atomic_store_n(j.inb + j.cap + 1, j.seq, __ATOMIC_RELEASE);
+      }
+    }
+  }
+  BtSet& bt_;
+  std::vector<int32_t> local_;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  bool stop_ = false;
+  std::atomic<int64_t> need_{0}, done_{0};
+  std::string error_;
 };
 
 // Java String.split("\\r?\\n") line index of ONE document (trim: drop trailing empty lines, as
@@ -584,6 +719,14 @@ PYBIND11_MODULE(_lpnative, m) {
     }
     return py::object(py::int_(multi_find(d, reinterpret_cast<const uint8_t*>(line.data()), (int64_t)line.size())));
   });
+  py::class_<SideWorker>(m, "SideWorker")
+      .def(py::init<BtSet&, std::vector<int32_t>>(), py::keep_alive<1, 2>(), py::arg("bt"), py::arg("local"))
+      .def("submit", &SideWorker::submit, py::arg("seq"), py::arg("text"), py::arg("cap"), py::arg("out"),
+           py::arg("inb"))
+      .def_property_readonly("need", &SideWorker::need)
+      .def("clear_need", &SideWorker::clear_need)
+      .def("take_error", &SideWorker::take_error)
+      .def_property_readonly("done", &SideWorker::done);
   py::class_<BtSet>(m, "BtSet")
       .def(py::init<const std::vector<std::string>&>())
       .def("ok", [](const BtSet& b, int i) { return i >= 0 && i < (int)b.rx.size() && b.rx[i] != nullptr; })

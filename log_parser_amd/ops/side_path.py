@@ -4,7 +4,7 @@ A backtracker regex (backreference, lookaround, atomic group, possessive quantif
 ``java.util.regex`` needs a backtracker for, ``AnalysisService.java:88-95``) carries, on the device,
 the automaton of its regular relaxation (``jregex.cpp Relaxer``). In a bulk step its device keys are
 candidates: ``k_take_host`` exports them (key, line start, length) to pinned host memory, a helper
-thread here checks the lines with the C++ backtracker on the step's host bytes and publishes the
+thread (native: bind.cpp SideWorker) checks the lines with the C++ backtracker on the step's host bytes and publishes the
 verified keys, and ``k_wait_host`` -- queued behind the export, so the rest of the step is queued
 with no host round trip -- appends them to the verified-hit buffer. The host only ever looks at
 candidate lines: never the whole shard, and never a device-to-host copy of the text.
@@ -17,9 +17,6 @@ helper's error (``check``).
 from __future__ import annotations
 
 import logging
-import queue
-import threading
-from typing import Optional
 
 import numpy as np
 import torch
@@ -41,63 +38,44 @@ class HostSide:
     def __init__(self, lib, device: torch.device, cap: int = 1 << 14):
         self.lib = lib
         self.device = device
-        self.local = np.ascontiguousarray(lib.host_local, np.int32)
         self.seq = 0
-        self.error: Optional[BaseException] = None
-        self.need = 0                              # export capacity an overflowing batch asked for
         self.cnt = torch.zeros(2, dtype=torch.int64, device=device)   # [export count, done blocks]
         self._alloc(cap)
-        self._q: "queue.Queue" = queue.Queue()
-        self._th = threading.Thread(target=self._worker, name="lp-bt-side", daemon=True)
-        self._th.start()
+        # the verifying thread is native (bind.cpp SideWorker): no GIL between export and answer
+        self._worker = N.SideWorker(lib.host_bt, [int(x) for x in np.asarray(lib.host_local, np.int32)])
+        self._hold = []                            # host bytes of the queued batches (the worker reads them)
 
     def _alloc(self, cap: int) -> None:
         self.cap = int(cap)
         self.out = _Coherent(3 * self.cap + 2)     # keys | starts | lens | host count | host seq
         self.inb = _Coherent(self.cap + 3)         # keys | host count | host seq | err
 
+    @property
+    def need(self) -> int:
+        return int(self._worker.need)
+
     def queue(self, cand, n1d: int, cap1: int, ver, n2d: int, cap2: int, text, ls, ll, dfa, stream: int,
               host_text: np.ndarray) -> None:
         """Queue export -> (host verification) -> append on ``stream``; host_text: the batch's
-        bytes on the host (the offsets of ``ls`` index it)."""
-        if self.need > self.cap:                   # (the previous attempt's buffers are idle)
-            self._alloc(max(self.need * 5 // 4, 2 * self.cap))
-            self.need = 0
+        bytes on the host (the offsets of ``ls`` index it), read by the worker until it publishes
+        (the batch's end-of-step read comes after k_wait_host, hence after that)."""
+        need = self.need
+        if need > self.cap:                        # (the previous attempt's buffers are idle)
+            self._alloc(max(need * 5 // 4, 2 * self.cap))
+            self._worker.clear_need()
         self.seq += 1
         c, o, i = self.cap, self.out.d, self.inb.d
         N.take_host(cand.data_ptr(), n1d, cap1, ver.data_ptr(), n2d, cap2, text.data_ptr(), ls.data_ptr(),
                     ll.data_ptr(), dfa, (o, o + 8 * c, o + 16 * c, c, self.cnt.data_ptr(), self.cnt.data_ptr() + 8,
                                          o + 24 * c, o + 24 * c + 8, self.seq), stream)
-        ev = torch.cuda.Event()
-        ev.record()                                # (stream = the current stream: kernels.match_and_hits)
-        self._q.put((ev, self.seq, host_text, self.cap, self.out, self.inb))
+        ht = np.ascontiguousarray(host_text)
+        self._hold = (self._hold + [ht])[-4:]
+        self._worker.submit(self.seq, ht.ctypes.data, c, self.out.h, self.inb.h)
         N.wait_host(ver.data_ptr(), cap2, n2d, (i, i + 8 * c, i + 8 * c + 8, c, self.seq, i + 8 * c + 16), stream)
-
-    def _worker(self) -> None:
-        while True:
-            ev, seq, ht, cap, out, inb = self._q.get()
-            res = -1
-            try:
-                ev.synchronize()
-                a = out.a
-                n, s = int(a[3 * cap]), int(a[3 * cap + 1])
-                if s != seq:
-                    raise RuntimeError(f"side path: export {s} published for batch {seq}")
-                if n > cap:
-                    self.need = n                  # re-run with a larger buffer (the step overflows)
-                else:
-                    res = int(self.lib.host_bt.verify(ht.ctypes.data, out.h, out.h + 8 * cap, out.h + 16 * cap, n,
-                                                      self.local.ctypes.data, int(self.local.size), inb.h))
-            except BaseException as e:  # noqa: BLE001 - always publish: the GPU waits for it
-                self.error = e
-                log.exception("backtracker side path failed")
-            finally:
-                b = inb.a
-                b[cap] = res
-                b[cap + 1] = seq                   # published last (x86 stores are ordered)
 
     def check(self) -> None:
         """Raise the helper's error (the step has re-run or failed meanwhile)."""
-        if self.error is not None:
-            e, self.error = self.error, None
-            raise RuntimeError("backtracker side path failed") from e
+        e = self._worker.take_error()
+        if e:
+            log.error("backtracker side path failed: %s", e)
+            raise RuntimeError(f"backtracker side path failed: {e}")

@@ -281,3 +281,44 @@ def test_device_fed_backtracker_bulk_step_equals_cpu(gpu_device):
         np.testing.assert_array_equal(r.ev_line.cpu().numpy(), ref.ev_line.numpy())
         np.testing.assert_array_equal(r.ev_pat.cpu().numpy(), ref.ev_pat.numpy())
     assert eng._host_side is not None and eng._host_side.seq >= 3
+
+
+def test_native_side_worker_verifies_exported_candidates():
+    """bind.cpp SideWorker (the side path's native host half) on plain host memory: it waits for
+    the export's sequence word, checks each exported candidate line with the backtracker and
+    publishes (verified keys, count, then sequence); an export larger than the buffer publishes -1
+    and asks for a bigger one."""
+    import time
+    sets, trig, lib = _bt_library(4)
+    text = "\n".join(t["sample"] for t in trig[-4:]) + "\nno match here\n" + trig[-4]["sample"].upper() + "\n"
+    data = np.frombuffer(text.encode(), np.uint8).copy()
+    lines = text.encode().split(b"\n")[:-1]
+    starts = np.cumsum([0] + [len(x) + 1 for x in lines[:-1]])
+    w = N.SideWorker(lib.host_bt, [int(x) for x in lib.host_local])
+    cap = 64
+    out = np.zeros(3 * cap + 2, np.int64)
+    inb = np.zeros(cap + 3, np.int64)
+    keys = [(r << 32) | x for x in range(len(lines)) for r in lib.host_dev]
+    n = len(keys)
+    out[:n] = keys
+    out[cap:cap + n] = [starts[k & 0xFFFFFFFF] for k in keys]
+    out[2 * cap:2 * cap + n] = [len(lines[k & 0xFFFFFFFF]) for k in keys]
+
+    def wait(seq):
+        t0 = time.time()
+        while inb[cap + 1] != seq:
+            assert time.time() - t0 < 10
+            time.sleep(0.001)
+
+    w.submit(1, data.ctypes.data, cap, out.ctypes.data, inb.ctypes.data)
+    time.sleep(0.01)                       # the worker polls until the export is published
+    out[3 * cap], out[3 * cap + 1] = n, 1
+    wait(1)
+    got = sorted(inb[:inb[cap]].tolist())
+    want = sorted(k for k in keys if lib.host_bt.find(int(lib.host_local[k >> 32]),
+                                                      lines[k & 0xFFFFFFFF].decode()))
+    assert got == want and len(want) >= 4 and w.take_error() == ""
+    out[3 * cap], out[3 * cap + 1] = cap + 5, 2     # an export that overflowed its buffer
+    w.submit(2, data.ctypes.data, cap, out.ctypes.data, inb.ctypes.data)
+    wait(2)
+    assert inb[cap] == -1 and w.need == cap + 5

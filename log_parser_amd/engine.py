@@ -672,7 +672,9 @@ class Engine:
         box = []
         ls, ll = K.split_lines(text, nbytes, before_read=lambda: box.append(self.prefilter_early(text, nbytes)))
         L = ls.numel()
-        segs = Segments.single(L, text.device)
+        # (through the engine's pinned upload buffer: a pageable copy would block the host until the
+        # queued prefilter is done, with the matchers not yet launched)
+        segs = Segments.scalar(0, L, 0, L, 0, L, text.device, upload=self.upload)
         early = box[0] if box else None
         for attempt in range(4):
             prep = self.prepare(text, nbytes, ls, ll, segs, host_text=host_text, early=early if attempt == 0 else None,

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--n", type=int, default=100)
     ap.add_argument("--lines", type=int, default=10_000)
     ap.add_argument("-D", action="append", default=[], help="config override key=value (A/B runs)")
+    ap.add_argument("--bytes", action="store_true", help="request body as bytes (default: str, as bench.py)")
     args = ap.parse_args()
     import torch
     from log_parser_amd import engine as E
@@ -27,10 +28,14 @@ def main():
     from log_parser_amd.models.compiled import CompiledLibrary
     from log_parser_amd.utils.config import Config, ScoringParams
     from log_parser_amd.utils.synth import make_log, realistic_library
+    from log_parser_amd.utils.numa import bind_to_gpu_numa
+    bind_to_gpu_numa(0)                     # as bench.py: pinned stages on the GPU's socket
     dev = torch.device("cuda", 0)
     sets, trig = realistic_library(1000, seed=7)
     eng = E.Engine(CompiledLibrary(sets, ScoringParams()), Config.load(overrides=dict([("engine.device", "cuda:0")] + [tuple(d.split("=", 1)) for d in args.D])), device=dev)
-    logs = make_log(args.lines, trig, seed=13, hit_rate=0.01).encode()
+    logs = make_log(args.lines, trig, seed=13, hit_rate=0.01)
+    if args.bytes:
+        logs = logs.encode()
     acc = defaultdict(list)
     cur = {}
 
@@ -46,6 +51,10 @@ def main():
         setattr(obj, name, g)
 
     wrap(eng, "pack_batch", "pack")
+    wrap(eng, "_stage_docs", "pack.stage_docs")
+    wrap(eng, "device_batch", "device_batch")
+    wrap(eng, "_run_native", "device.run_native")
+    wrap(eng, "_host_keys", "device.host_keys")
     wrap(eng, "_stage_h2d", "stage_h2d")
     wrap(eng.upload.__class__, "__call__", "upload")
     wrap(K, "match_and_hits", "match_and_hits(+read)")

@@ -15,6 +15,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
 run pytest 300 python -u -m pytest tests/test_gpu.py -m gpu -x -v -k "run_document or sharded_single or fetch_publish" \
   --timeout 200 --timeout-method thread
 run single 300 python -u benchmarks/bench_configs.py single
+run phases 300 python -u tools/engine_phases.py --n 200
 bash tools/gpu_check.sh reqtrace prof || exit 1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 run prof_nodefer 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nodefer -o run -- \

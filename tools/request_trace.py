@@ -22,6 +22,8 @@ def run(args):
     from log_parser_amd.models.compiled import CompiledLibrary
     from log_parser_amd.utils.config import Config, ScoringParams
     from log_parser_amd.utils.synth import make_log, realistic_library
+    from log_parser_amd.utils.numa import bind_to_gpu_numa
+    bind_to_gpu_numa(0)                     # as bench.py and the server: pinned stages on the GPU's socket
     dev = torch.device("cuda", 0)
     sets, trig = realistic_library(args.patterns, seed=7, java_shape_rate=args.java_shape_rate)
     lib = CompiledLibrary(sets, ScoringParams())

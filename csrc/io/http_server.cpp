@@ -12,6 +12,7 @@
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -82,6 +83,22 @@ std::string trim(const char* a, size_t n) {
   while (i < j && (a[i] == ' ' || a[i] == '\t')) ++i;
   while (j > i && (a[j - 1] == ' ' || a[j - 1] == '\t')) --j;
   return std::string(a + i, j - i);
+}
+// Grow this process's file-descriptor table to its final size now, before the IO threads run. The
+// kernel grows the table by doubling as accept() hands out higher fds, and in a multi-threaded
+// process every growth waits for an RCU grace period (expand_files -> synchronize_rcu): during a
+// burst of thousands of new connections the IO threads sat in accept4 in D state for tens of ms
+// at a time (utils/threadsample.py: 43% "accept4/expand_files" + 7% "accept4/__wait_rcu_gp" of the
+// IO threads' samples in the slow config-5 runs, none in the fast ones, profiles/r5_b). Raising
+// the table to the fd limit once (dup2 onto the highest fd, then close: the table never shrinks)
+// pays that wait once, at start-up.
+void reserve_fd_table(int fd) {
+  rlimit rl{};
+  if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return;
+  const long top = std::min<long>((long)rl.rlim_cur, 1L << 17) - 1;
+  if (top < 1024) return;
+  const int d = dup2(fd, (int)top);
+  if (d >= 0) close(d);
 }
 }  // namespace
 
@@ -167,6 +184,7 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
     epoll_ctl(io->ep, EPOLL_CTL_ADD, io->efd, &ev);
     ios_.push_back(std::move(io));
   }
+  reserve_fd_table(ios_[0]->lfd);
   for (auto& io : ios_)
     threads_.emplace_back([this, p = io.get(), k = (int)threads_.size()] {
       char nm[16];

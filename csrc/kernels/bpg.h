@@ -270,12 +270,18 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
   const int nctr = L.nctr;
   int cpos[BPG_CTR_MAX];
   uint32_t cbound[BPG_CTR_MAX], cnt[BPG_CTR_MAX];
+  uint64_t cmk[W];                     // the counted positions' bits, per word
+#pragma unroll
+  for (int w = 0; w < W; ++w) cmk[w] = 0;
 #pragma unroll
   for (int c = 0; c < BPG_CTR_MAX; ++c) {
     const uint64_t e = c < nctr ? P[L.o_ctr + c] : 0ull;
     cpos[c] = (int)(e & 0xFFFF);
     cbound[c] = (uint32_t)(e >> 16);
     cnt[c] = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (c < nctr && w == (cpos[c] >> 6)) cmk[w] |= 1ull << (cpos[c] & 63);
   }
 // accept in boundary context ACTX (a macro, not a lambda: a lambda capturing S by reference kept
 // the state array in scratch memory)
@@ -364,9 +370,12 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
 #pragma unroll
             for (int w = 0; w < W; ++w) F[w] |= Fi[w];
           }
+          uint64_t act = 0;                        // a counted position alive or entered: a dead
+#pragma unroll                                     // one's count is never read (restarts at entry)
+          for (int w = 0; w < W; ++w) act |= (F[w] | S[w]) & cmk[w];
 #pragma unroll
           for (int c = 0; c < BPG_CTR_MAX; ++c) {  // counted positions (rare: skipped as a whole)
-            if (c >= nctr) break;
+            if (c >= nctr || !act) break;
             const int pw = cpos[c] >> 6;
             uint64_t fw = 0, sw = 0;
 #pragma unroll

@@ -27,15 +27,32 @@ constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global
 
 inline unsigned nblocks(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
 
+// WMAX: the library's widest program of <= 8 words -- only walks up to that width are compiled
+// into the kernel, so a library of one-word programs (the common case since counted positions)
+// runs at a one-word walk's register count (a W = 8 walk's 256 VGPRs allowed one wave per SIMD)
+template <int WMAX>
 __device__ __forceinline__ bool lane_walk(const uint64_t* prog, const uint8_t* s, int len) {
-  switch ((int)(prog[0] & 0xFF)) {
-    case 1: return bpg_find_dev<1>(prog, s, len);
-    case 2: return bpg_find_dev<2>(prog, s, len);
-    case 3: return bpg_find_dev<3>(prog, s, len);
-    case 4: return bpg_find_dev<4>(prog, s, len);
-    case 6: return bpg_find_dev<6>(prog, s, len);
-    default: return bpg_find_dev<8>(prog, s, len);
+  const int w = (int)(prog[0] & 0xFF);
+  if constexpr (WMAX == 1) return bpg_find_dev<1>(prog, s, len);
+  if (w <= 1) return bpg_find_dev<1>(prog, s, len);
+  if constexpr (WMAX == 2) return bpg_find_dev<2>(prog, s, len);
+  if (w == 2) return bpg_find_dev<2>(prog, s, len);
+  if constexpr (WMAX <= 4) {
+    if (w == 3) return bpg_find_dev<3>(prog, s, len);
+    return bpg_find_dev<4>(prog, s, len);
+  } else {
+    if (w == 3) return bpg_find_dev<3>(prog, s, len);
+    if (w == 4) return bpg_find_dev<4>(prog, s, len);
+    if (w <= 6) return bpg_find_dev<6>(prog, s, len);
+    return bpg_find_dev<8>(prog, s, len);
   }
+}
+
+inline int narrow_wmax(uint32_t widths) {       // WMAX of lane_walk for a bpg_widths mask
+  if (widths & 0x1E0u) return 8;                 // 5 .. 8 words
+  if (widths & 0x18u) return 4;                  // 3 / 4 words
+  if (widths & 0x4u) return 2;
+  return 1;
 }
 
 // bulk path: sorted packed keys ((regex << lbits | line) << 1 | pre-verified); the first key of
@@ -45,6 +62,7 @@ __device__ __forceinline__ bool lane_walk(const uint64_t* prog, const uint8_t* s
 // caller) for k_bpg_coop_list: a regex's keys are contiguous in the sorted array,
 // so walking them where they sit would serialise up to 64 / (64 / G) walks in one wave (a W = 12
 // program's keys cost 1.17 ms per bench step that way).
+template <int WMAX>
 __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restrict__ keys, int64_t n, int lbits,
                                                         const uint8_t* __restrict__ text,
                                                         const int64_t* __restrict__ ls,
@@ -69,7 +87,7 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
     return;
   }
   const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
-  flag[i] = lane_walk(prog, text + ls[x], ll[x]) ? 1 : 0;
+  flag[i] = lane_walk<WMAX>(prog, text + ls[x], ll[x]) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -126,16 +144,32 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
   const uint32_t f0 = wl ? LP_W32(first_o) : 0u, l0 = wl ? LP_W32(last_o) : 0u;
   const int ftl = valid ? final_term_len(s, n) : 0;
   const int ft = ftl ? n - ftl : -1;
-  // counted positions: the lane holding the position's word keeps its count (bpg.h)
+  // counted positions: the lane holding the position's word keeps its count (bpg.h). A lane's own
+  // counters are compacted to the front (ncl of them, bits cmask of its word): the per-character
+  // update runs only while some counted position of the wave is alive or entered -- a dead
+  // position's count is never read (it restarts at 1 on entry), so skipping it changes nothing
   const int nctr = L.nctr;
-  int cpos[BPG_CTR_MAX];
-  uint32_t cbound[BPG_CTR_MAX], cnt[BPG_CTR_MAX];
+  uint32_t cpos[BPG_CTR_MAX], cbound[BPG_CTR_MAX], cnt[BPG_CTR_MAX];
+  int ncl = 0;
+  uint32_t cmask = 0;
+#pragma unroll
+  for (int c = 0; c < BPG_CTR_MAX; ++c) {
+    cpos[c] = 0;
+    cbound[c] = 0;
+    cnt[c] = 0;
+  }
 #pragma unroll
   for (int c = 0; c < BPG_CTR_MAX; ++c) {
     const uint64_t e = c < nctr ? P[L.o_ctr + c] : 0ull;
-    cpos[c] = c < nctr && j == (int)((e & 0xFFFF) >> 5) ? (int)(e & 31) : -1;   // -1: not this lane's
-    cbound[c] = (uint32_t)(e >> 16);
-    cnt[c] = 0;
+    const bool own = c < nctr && j == (int)((e & 0xFFFF) >> 5);
+#pragma unroll
+    for (int q = 0; q < BPG_CTR_MAX; ++q)
+      if (own && q == ncl) {
+        cpos[q] = (uint32_t)(e & 31);
+        cbound[q] = (uint32_t)(e >> 16);
+      }
+    cmask |= own ? 1u << (e & 31) : 0u;
+    ncl += own ? 1 : 0;
   }
   const bool wctr = __ballot(nctr > 0) != 0;
   // wave-uniform feature switches: the common program (uniform first/last sets, no exception edges,
@@ -222,14 +256,18 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
         }
       }
       F |= wnon ? fw[q] : f0;
-      if (wctr) {
+      if (wctr && __ballot(((F | S) & cmask) != 0u) != 0) {   // (bpg_ctr_step, one counter at a time)
 #pragma unroll
         for (int c = 0; c < BPG_CTR_MAX; ++c) {
-          if (cpos[c] < 0) continue;
-          uint32_t k = cnt[c];
-          const uint32_t Fc = (uint32_t)bpg_ctr_step(F, cpos[c], (S >> cpos[c]) & 1u, cbound[c], k);
-          F = Fc;
-          cnt[c] = skip ? cnt[c] : k;
+          if (__ballot(c < ncl) == 0) break;
+          if (c < ncl) {
+            const uint32_t b = cpos[c];
+            const uint32_t entry = (F >> b) & 1u;
+            const uint32_t lt = cnt[c] < cbound[c] ? 1u : 0u;
+            F |= (((S >> b) & 1u) & lt) << b;    // stay while the count is below the bound
+            const uint32_t k = entry ? 1u : cnt[c] + lt;   // saturates at the bound
+            cnt[c] = skip ? cnt[c] : k;
+          }
         }
       }
       const uint32_t Sn = F & cw[q];
@@ -481,8 +519,16 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
   // per-width launches added up their slowest walks where one launch runs them side by side)
   const bool listed = any_wide && wcnt && wlist;
   if ((P.bpg_widths & 0x1FFu) || listed) {
-    hipLaunchKernelGGL(k_bpg_dedupe_all, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag,
-                       listed ? wcnt : nullptr, listed ? wlist : nullptr);
+#define LP_DEDUPE(WM)                                                                                      \
+  hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag, \
+                     listed ? wcnt : nullptr, listed ? wlist : nullptr)
+    switch (narrow_wmax(P.bpg_widths)) {
+      case 1: LP_DEDUPE(1); break;
+      case 2: LP_DEDUPE(2); break;
+      case 4: LP_DEDUPE(4); break;
+      default: LP_DEDUPE(8); break;
+    }
+#undef LP_DEDUPE
     check_launch("k_bpg_dedupe_all");
   }
   if (!any_wide) return;

@@ -12,14 +12,11 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run pytest 300 python -u -m pytest tests/test_gpu.py -m gpu -x -v -k "run_document or sharded_single or fetch_publish" \
+run pytest 600 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py -m gpu -x -v \
   --timeout 200 --timeout-method thread
-run single 300 python -u benchmarks/bench_configs.py single
 run phases 300 python -u tools/engine_phases.py --n 200
-bash tools/gpu_check.sh reqtrace prof || exit 1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-run prof_nodefer 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nodefer -o run -- \
-  python3 bench.py --steps 6 --warmup 2 --parse-requests 0 --no-overlap --scan-defer-rare 0
-db=$(find gpurun_out/prof_nodefer -name "*.db" | head -1)
-run kstats_nodefer 120 python3 tools/kstats_db.py "$db" 6 45 --median --marker k_nl_count --last 6
-bash tools/gpu_check.sh httpreps || exit 1
+bash tools/gpu_check.sh reqtrace || exit 1
+run single 300 python -u benchmarks/bench_configs.py single
+run bench 400 python -u bench.py --steps 10 --warmup 3
+run bench_bt 400 python -u bench.py --steps 10 --warmup 3 --bt-patterns 4 --parse-requests 0
+bash tools/gpu_check.sh prof || exit 1

@@ -68,6 +68,7 @@ static DfaPool dfa_from(const py::tuple& t) {
   D.acc = P<const uint8_t>(t[3].cast<uint64_t>());
   D.bpg = t.size() > 4 ? P<const uint64_t>(t[4].cast<uint64_t>()) : nullptr;
   D.bpg_widths = t.size() > 5 ? t[5].cast<uint32_t>() : 0u;
+  D.bpg_words = t.size() > 6 ? t[6].cast<uint32_t>() : 0u;
   return D;
 }
 
@@ -804,6 +805,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("set_host_threads", &set_host_threads);
   m.def("set_pf_verify_lanes", &set_pf_verify_lanes);
   m.def("set_scan_defer_rare", &set_scan_defer_rare);
+  m.def("set_cand_verify_split", &set_cand_verify_split);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false);

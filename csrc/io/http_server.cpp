@@ -173,7 +173,9 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
       getsockname(io->lfd, reinterpret_cast<sockaddr*>(&a), &len);
       port_ = ntohs(a.sin_port);
     }
-    if (listen(io->lfd, 1024) != 0) throw std::runtime_error("listen() failed");
+    // (the kernel clamps the backlog to net.core.somaxconn: a 10k-connection burst spread over a
+    // few listeners overflowed 1024 per listener while accept was slow)
+    if (listen(io->lfd, 65535) != 0) throw std::runtime_error("listen() failed");
     io->ep = epoll_create1(EPOLL_CLOEXEC);
     io->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     epoll_event ev{};

@@ -24,6 +24,23 @@ namespace {
 constexpr uint64_t kPadKey = ~0ull;   // lp_post.hip LP_PAD_KEY
 constexpr int kScanLines = 256;
 constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global memory)
+// The candidate kernels stage the library's WHOLE program pool in LDS when it fits: a walk's
+// per-character reads (class map, class rows, first / last sets, exceptions) are then LDS hits, not
+// a chain of global-memory round trips (k_bpg_coop / k_bpg_dedupe_all are latency-bound on one
+// line's walk: a request verifies a handful of candidates, a bulk step a few thousand)
+constexpr uint32_t kPoolLdsWords = 8192;   // 64 KiB
+
+inline size_t pool_lds_bytes(const DfaPool& P) {
+  return (P.bpg_words && P.bpg_words <= kPoolLdsWords) ? (size_t)P.bpg_words * 8 : 0;
+}
+
+// every thread of the block calls this (it synchronises): the pool in LDS, or in global memory
+__device__ __forceinline__ const uint64_t* stage_pool(const DfaPool& P, uint64_t* lds) {
+  if (P.bpg_words == 0 || P.bpg_words > kPoolLdsWords) return P.bpg;
+  for (uint32_t i = threadIdx.x; i < P.bpg_words; i += blockDim.x) lds[i] = P.bpg[i];
+  __syncthreads();
+  return lds;
+}
 
 inline unsigned nblocks(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
 
@@ -69,25 +86,34 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
                                                         const int32_t* __restrict__ ll, DfaPool P,
                                                         uint8_t* __restrict__ flag, uint32_t* __restrict__ wcnt,
                                                         uint32_t* __restrict__ wlist) {
+  extern __shared__ uint64_t pool_lds[];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t key = keys[i];
-  if (key == kPadKey) return;
-  const uint64_t k = key >> 1;
-  if (i > 0 && (keys[i - 1] >> 1) == k) return;
-  const int r = (int)(k >> lbits);
-  if (!is_bpg(P, r)) return;
-  const uint64_t* prog = P.bpg + P.meta[4 * r];
-  const bool is_wide = (int)(prog[0] & 0xFF) > BPG_LANE_MAX_W;
-  if (is_wide && !wcnt) return;
-  for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j)
-    if (keys[j] & 1) return;                  // pre-verified: flag already 1
-  if (is_wide) {
-    wlist[atomicAdd(wcnt, 1u)] = (uint32_t)i;
-    return;
+  bool walk = false;
+  int r = 0;
+  int64_t x = 0;
+  if (i < n) {
+    const uint64_t key = keys[i];
+    const uint64_t k = key >> 1;
+    if (key != kPadKey && !(i > 0 && (keys[i - 1] >> 1) == k)) {
+      r = (int)(k >> lbits);
+      if (is_bpg(P, r)) {
+        const bool is_wide = (int)(P.bpg[P.meta[4 * r]] & 0xFF) > BPG_LANE_MAX_W;
+        bool pre = false;
+        for (int64_t j = i; j < n && (keys[j] >> 1) == k; ++j) pre |= (keys[j] & 1) != 0;
+        if (!pre && !(is_wide && !wcnt)) {   // pre-verified: flag already 1
+          if (is_wide) {
+            wlist[atomicAdd(wcnt, 1u)] = (uint32_t)i;
+          } else {
+            walk = true;
+            x = (int64_t)(k & ((1ull << lbits) - 1));
+          }
+        }
+      }
+    }
   }
-  const int64_t x = (int64_t)(k & ((1ull << lbits) - 1));
-  flag[i] = lane_walk<WMAX>(prog, text + ls[x], ll[x]) ? 1 : 0;
+  if (!__syncthreads_or(walk)) return;          // block-uniform: most blocks hold no program key
+  const uint64_t* pool = stage_pool(P, pool_lds);
+  if (walk) flag[i] = lane_walk<WMAX>(pool + P.meta[4 * r], text + ls[x], ll[x]) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -333,6 +359,9 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
       }
     }
   }
+  extern __shared__ uint64_t pool_lds[];
+  if (!__syncthreads_or(need)) return;          // block-uniform (the DFA half returned above)
+  const uint64_t* pool = stage_pool(P, pool_lds);
   uint64_t todo = __ballot(need);                // wave-uniform
   constexpr int NG = 64 / G;
   const int g = lane / G;
@@ -351,7 +380,7 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
     const int rr = __shfl(r, sl, 64);
     const int64_t xx = __shfl(x, sl, 64);
     const bool valid = src >= 0;
-    const uint64_t* prog = P.bpg + (valid ? P.meta[4 * rr] : 0);
+    const uint64_t* prog = pool + (valid ? P.meta[4 * rr] : 0);
     const uint8_t* s = text + (valid ? ls[xx] : 0);
     const int len = valid ? ll[xx] : 0;
     const bool hit = bpg_coop_walk<G>(prog, s, len, valid);
@@ -413,6 +442,7 @@ void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigne
                  const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P, uint8_t* flag,
                  hipStream_t st, int wmin) {
   const dim3 grid(nblocks(cap) * (MODE == 2 ? 2 : 1)), block(256);
+  const size_t lds = pool_lds_bytes(P);
   switch (coop_group(P.bpg_widths)) {
     case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
     case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
@@ -500,9 +530,14 @@ void bpg_cand_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, 
   check_launch("k_bpg_coop<cand>");
 }
 
+namespace {
+bool g_cand_split = false;
+}  // namespace
+void set_cand_verify_split(bool on) { g_cand_split = on; }
+
 bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* dcount, const uint8_t* text,
                          const int64_t* ls, const int32_t* ll, const DfaPool& P, uint64_t stream) {
-  if (!P.bpg_widths || cap <= 0) return false;   // caller runs k_cand_verify
+  if (!P.bpg_widths || cap <= 0 || g_cand_split) return false;   // caller runs k_cand_verify
   launch_coop<2>(cand, nullptr, cap, dcount, 0, text, ls, ll, P, nullptr, reinterpret_cast<hipStream_t>(stream), 0);
   check_launch("k_bpg_coop<cand+dfa>");
   return true;
@@ -520,7 +555,8 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
   const bool listed = any_wide && wcnt && wlist;
   if ((P.bpg_widths & 0x1FFu) || listed) {
 #define LP_DEDUPE(WM)                                                                                      \
-  hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), 0, st, keys, n, lbits, text, ls, ll, P, flag, \
+  hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), pool_lds_bytes(P), st, keys, n, lbits, text, ls, \
+                     ll, P, flag, \
                      listed ? wcnt : nullptr, listed ? wlist : nullptr)
     switch (narrow_wmax(P.bpg_widths)) {
       case 1: LP_DEDUPE(1); break;

@@ -15,6 +15,9 @@ void set_pf_verify_lanes(int n);
 // bulk scan walk: hot blocks re-walked by a second kernel (k_scan_rare) instead of inline (A/B knob)
 bool scan_defer_rare();
 void set_scan_defer_rare(bool on);
+// request path: BPG and DFA candidates verified in ONE launch (k_bpg_coop mode 2, default) or in
+// two (k_cand_verify, then the BPG walk) -- the diagnostic split shows each half's time
+void set_cand_verify_split(bool on);
 // line-index pass 1 folded into the bulk prefilter (line_index.hip k_nl_count's outputs): per 16 KiB
 // tile the '\n' count and the "\r\n" flag (both zeroed by the caller), per 64 bytes a '\n' bitmask
 struct NlOut {

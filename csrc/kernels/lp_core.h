@@ -44,6 +44,7 @@ struct DfaPool {
   const uint8_t* acc;
   const uint64_t* bpg = nullptr;   // bit-parallel Glushkov programs (meta flag bit1, offset in meta[0])
   uint32_t bpg_widths = 0;         // bit W set: some program has W words (which bpg.hip kernels to launch)
+  uint32_t bpg_words = 0;          // length of the program pool (uint64 words): staged in LDS when it fits
 };
 
 LP_HD int final_term_len(const uint8_t* s, int n) {

@@ -781,7 +781,7 @@ class CompiledLibrary:
                            T(self.bpg_pool.view(np.int64))]
         d = t["dfa_arrays"]
         t["dfa"] = (d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), d[4].data_ptr(),
-                    self.bpg_widths)
+                    self.bpg_widths, int(self.bpg_pool.size))
         t["scan_regs"] = T(np.array(self.scan_regs_single, np.int32))
         t["scan_blobs"] = [T(p["blob"]) for p in self.scan_passes]
         t["scan_passes"] = [(b.data_ptr(), p["lds_words"], p["ngroups"], p["row_base"], p["stride"], p["thr"],

@@ -25,6 +25,9 @@ def run(args):
     from log_parser_amd.utils.numa import bind_to_gpu_numa
     bind_to_gpu_numa(0)                     # as bench.py and the server: pinned stages on the GPU's socket
     dev = torch.device("cuda", 0)
+    if args.split_verify:                   # k_cand_verify + the BPG walk as two launches (diagnostic)
+        from log_parser_amd.native import N
+        N.set_cand_verify_split(True)
     sets, trig = realistic_library(args.patterns, seed=7, java_shape_rate=args.java_shape_rate)
     lib = CompiledLibrary(sets, ScoringParams())
     ov = {"engine.device": "cuda:0"}
@@ -94,6 +97,8 @@ if __name__ == "__main__":
     ap.add_argument("--db", default="")
     ap.add_argument("--java-shape-rate", type=float, default=0.01,
                     help="share of Java-shape primaries in the realistic library (0 = the round-3 library)")
+    ap.add_argument("--split-verify", action="store_true",
+                    help="verify DFA and BPG candidates in two launches (shows each half in a trace)")
     ap.add_argument("--device-counts", action="store_true", help="runner device-count mode (no mid-batch read)")
     a = ap.parse_args()
     summarise(a) if a.db else run(a)

@@ -178,12 +178,14 @@ struct BtSet {
 };
 
 // The host half of the device-fed backtracker regexes (side_path.hip) as a native thread: no
-// Python and no GIL between the export and the answer, so the GPU's k_wait_host is not held up by
-// the Python thread that is still queuing the rest of the step. Per job it polls the export's
-// sequence word in pinned memory (k_take_host publishes the count, then the sequence), checks the
-// candidate lines with the backtracker on the batch's host bytes, and publishes (count or -1, then
-// the sequence). Layouts (int64 words, cap = the job's capacity): out = keys | starts | lens |
-// count | seq; inb = keys | count | seq.
+// Python and no GIL between an export and the answer. A job has up to two export regions, each
+// published by its own k_take_host (count, then the job's sequence number): A = the prefilter's
+// candidates, exported as soon as the literal chain is done -- the host verifies them while the
+// GPU is still in the literal-free scan -- and B = the scan engines' keys of relaxed regexes,
+// exported after the scan. The worker polls each region's sequence word in pinned memory, checks
+// the candidate lines with the backtracker on the batch's host bytes, and publishes (verified keys
+// of both regions, their count or -1, then the sequence) for k_wait_host. Layouts (int64 words):
+// region = keys | starts | lens | count | seq (cap entries each); inb = keys | count | seq.
 class SideWorker {
  public:
   SideWorker(BtSet& bt, std::vector<int32_t> local) : bt_(bt), local_(std::move(local)) {
@@ -197,11 +199,12 @@ class SideWorker {
     cv_.notify_all();
     th_.join();
   }
-  void submit(int64_t seq, uint64_t text, int64_t cap, uint64_t out, uint64_t inb) {
+  // outB = 0: one region
+  void submit(int64_t seq, uint64_t text, int64_t cap, uint64_t outA, uint64_t outB, uint64_t inb) {
     {
       std::lock_guard<std::mutex> lk(mu_);
-      q_.push_back(Job{seq, reinterpret_cast<const uint8_t*>(text), cap, reinterpret_cast<int64_t*>(out),
-                       reinterpret_cast<int64_t*>(inb)});
+      q_.push_back(Job{seq, reinterpret_cast<const uint8_t*>(text), cap, {reinterpret_cast<int64_t*>(outA),
+                       reinterpret_cast<int64_t*>(outB)}, reinterpret_cast<int64_t*>(inb)});
     }
     cv_.notify_one();
   }
@@ -220,7 +223,7 @@ class SideWorker {
     int64_t seq;
     const uint8_t* text;
     int64_t cap;
-    int64_t* out;
+    int64_t* out[2];
     int64_t* inb;
   };
   static int64_t load_acq(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
@@ -228,49 +231,66 @@ class SideWorker {
     std::lock_guard<std::mutex> lk(mu_);
     if (error_.empty()) error_ = why;
   }
-  void run(const Job& j) {
-    int64_t res = -1;
-    const int64_t c = j.cap;
-    // the export lands after the matchers: spin briefly, then nap; give up after 5 s (the GPU's own
-    // wait ends at 2 s: the batch then overflows and re-runs)
+  // wait for a region's export: spin briefly, then nap; give up after 5 s (the GPU's own wait ends
+  // at 2 s: the batch then overflows and re-runs)
+  static bool wait_export(const int64_t* seqw, int64_t seq) {
     const auto t0 = std::chrono::steady_clock::now();
-    bool seen = false;
     for (int it = 0;; ++it) {
-      if (load_acq(j.out + 3 * c + 1) == j.seq) {
-        seen = true;
-        break;
-      }
+      if (load_acq(seqw) == seq) return true;
       if (it < 4096) {
 #if defined(__x86_64__)
         __builtin_ia32_pause();
 #endif
         continue;
       }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
     }
-    if (!seen) {
-      fail("side path: no export for batch " + std::to_string(j.seq) + " within 5 s");
-    } else {
-      const int64_t n = load_acq(j.out + 3 * c);
-      if (n > c) {
-        need_.store(n);                      // re-run with a larger buffer (the batch overflows)
-      } else {
-        const int64_t* K = j.out;
-        const int64_t* S = j.out + c;
-        const int64_t* L = j.out + 2 * c;
-        const int64_t ng = (int64_t)local_.size();
-        std::vector<uint8_t> ok(n, 0);
-        host_parallel(n, 64, [&](int, int64_t a, int64_t e) {
-          for (int64_t i = a; i < e; ++i) {
-            const int64_t g = K[i] >> 32;
-            if (g < 0 || g >= ng || local_[g] < 0) continue;
-            ok[i] = bt_.find(local_[g], j.text + S[i], L[i]) ? 1 : 0;
-          }
-        });
-        res = 0;
-        for (int64_t i = 0; i < n; ++i)
-          if (ok[i]) j.inb[res++] = K[i];
+  }
+  // verify region `out` (n <= cap keys) into inb[base..]; returns the verified count
+  int64_t verify(const Job& j, const int64_t* out, int64_t n, int64_t base) {
+    const int64_t c = j.cap;
+    const int64_t* K = out;
+    const int64_t* S = out + c;
+    const int64_t* L = out + 2 * c;
+    const int64_t ng = (int64_t)local_.size();
+    std::vector<uint8_t> ok(n, 0);
+    host_parallel(n, 16, [&](int, int64_t a, int64_t e) {
+      for (int64_t i = a; i < e; ++i) {
+        const int64_t g = K[i] >> 32;
+        if (g < 0 || g >= ng || local_[g] < 0) continue;
+        ok[i] = bt_.find(local_[g], j.text + S[i], L[i]) ? 1 : 0;
+      }
+    });
+    int64_t r = 0;
+    for (int64_t i = 0; i < n; ++i)
+      if (ok[i]) {
+        if (base + r < c) j.inb[base + r] = K[i];
+        ++r;
+      }
+    return r;
+  }
+  void run(const Job& j) {
+    const int64_t c = j.cap;
+    int64_t res = 0;
+    for (int q = 0; q < 2 && res >= 0; ++q) {
+      const int64_t* out = j.out[q];
+      if (!out) continue;
+      if (!wait_export(out + 3 * c + 1, j.seq)) {
+        fail("side path: no export for batch " + std::to_string(j.seq) + " within 5 s");
+        res = -1;
+        break;
+      }
+      const int64_t n = load_acq(out + 3 * c);
+      if (n > c) {                           // re-run with a larger buffer (the batch overflows)
+        need_.store(std::max(need_.load(), n));
+        res = -1;
+        break;
+      }
+      res += verify(j, out, n, res);
+      if (res > c) {
+        need_.store(std::max(need_.load(), res));
+        res = -1;
       }
     }
     __atomic_store_n(j.inb + c, res, __ATOMIC_RELEASE);
@@ -722,8 +742,8 @@ PYBIND11_MODULE(_lpnative, m) {
   });
   py::class_<SideWorker>(m, "SideWorker")
       .def(py::init<BtSet&, std::vector<int32_t>>(), py::keep_alive<1, 2>(), py::arg("bt"), py::arg("local"))
-      .def("submit", &SideWorker::submit, py::arg("seq"), py::arg("text"), py::arg("cap"), py::arg("out"),
-           py::arg("inb"))
+      .def("submit", &SideWorker::submit, py::arg("seq"), py::arg("text"), py::arg("cap"), py::arg("out_a"),
+           py::arg("out_b"), py::arg("inb"))
       .def_property_readonly("need", &SideWorker::need)
       .def("clear_need", &SideWorker::clear_need)
       .def("take_error", &SideWorker::take_error)

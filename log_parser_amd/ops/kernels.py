@@ -519,11 +519,13 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
                         max(16, min(8192, nbytes >> 13)))
         if tick:
             tick("prefilter")
+        if host_side is not None:          # region A: the candidates go to the host during the scans
+            host_side[0].export_candidates(cand, c0 + 8, cap["cand"], text, line_start, line_len, tabs["dfa"], st,
+                                           host_side[1])
         if sst != st:
             torch.cuda.current_stream(dev).wait_event(side[2])
-        if host_side is not None:          # export -> host backtracker -> append, all queued
-            host_side[0].queue(cand, c0 + 8, cap["cand"], ver, c0 + 16, cap["ver"], text, line_start, line_len,
-                               tabs["dfa"], st, host_side[1])
+        if host_side is not None:          # region B (scan keys) -> host backtracker -> append, all queued
+            host_side[0].export_scan_and_wait(ver, c0 + 16, cap["ver"], text, line_start, line_len, tabs["dfa"], st)
         elif tabs.get("host_dev"):         # relaxation keys of regexes the host side path decided
             N.take_host(cand.data_ptr(), c0 + 8, cap["cand"], ver.data_ptr(), c0 + 16, cap["ver"], text.data_ptr(),
                         line_start.data_ptr(), line_len.data_ptr(), tabs["dfa"], None, st)

@@ -3,9 +3,10 @@
 A backtracker regex (backreference, lookaround, atomic group, possessive quantifier: the regexes
 ``java.util.regex`` needs a backtracker for, ``AnalysisService.java:88-95``) carries, on the device,
 the automaton of its regular relaxation (``jregex.cpp Relaxer``). In a bulk step its device keys are
-candidates: ``k_take_host`` exports them (key, line start, length) to pinned host memory, a helper
-thread (native: bind.cpp SideWorker) checks the lines with the C++ backtracker on the step's host bytes and publishes the
-verified keys, and ``k_wait_host`` -- queued behind the export, so the rest of the step is queued
+candidates: ``k_take_host`` exports them (key, line start, length) to pinned host memory -- the
+prefilter's candidates as soon as the literal chain is done, the scan engines' keys after the scan --
+a helper thread (native: bind.cpp SideWorker) checks the lines with the C++ backtracker on the
+step's host bytes and publishes the verified keys, and ``k_wait_host`` -- queued behind the export, so the rest of the step is queued
 with no host round trip -- appends them to the verified-hit buffer. The host only ever looks at
 candidate lines: never the whole shard, and never a device-to-host copy of the text.
 
@@ -35,11 +36,15 @@ class _Coherent:
 
 
 class HostSide:
+    """The device side of one engine's exports: pinned regions A (prefilter candidates) and B (the
+    scan engines' relaxation keys), the verified-key buffer the GPU appends from, and the native
+    verifying thread."""
+
     def __init__(self, lib, device: torch.device, cap: int = 1 << 14):
         self.lib = lib
         self.device = device
         self.seq = 0
-        self.cnt = torch.zeros(2, dtype=torch.int64, device=device)   # [export count, done blocks]
+        self.cnt = torch.zeros(4, dtype=torch.int64, device=device)   # [count, done blocks] x (A, B)
         self._alloc(cap)
         # the verifying thread is native (bind.cpp SideWorker): no GIL between export and answer
         self._worker = N.SideWorker(lib.host_bt, [int(x) for x in np.asarray(lib.host_local, np.int32)])
@@ -47,30 +52,42 @@ class HostSide:
 
     def _alloc(self, cap: int) -> None:
         self.cap = int(cap)
-        self.out = _Coherent(3 * self.cap + 2)     # keys | starts | lens | host count | host seq
+        self.out_a = _Coherent(3 * self.cap + 2)   # keys | starts | lens | host count | host seq
+        self.out_b = _Coherent(3 * self.cap + 2)
         self.inb = _Coherent(self.cap + 3)         # keys | host count | host seq | err
 
     @property
     def need(self) -> int:
         return int(self._worker.need)
 
-    def queue(self, cand, n1d: int, cap1: int, ver, n2d: int, cap2: int, text, ls, ll, dfa, stream: int,
-              host_text: np.ndarray) -> None:
-        """Queue export -> (host verification) -> append on ``stream``; host_text: the batch's
-        bytes on the host (the offsets of ``ls`` index it), read by the worker until it publishes
-        (the batch's end-of-step read comes after k_wait_host, hence after that)."""
+    def _out(self, o, k: int) -> tuple:
+        c, d = self.cap, o.d
+        cnt = self.cnt.data_ptr() + 16 * k
+        return (d, d + 8 * c, d + 16 * c, c, cnt, cnt + 8, d + 24 * c, d + 24 * c + 8, self.seq)
+
+    def export_candidates(self, cand, n1d: int, cap1: int, text, ls, ll, dfa, stream: int,
+                          host_text: np.ndarray) -> None:
+        """Region A, queued right after the literal chain: the prefilter candidates of relaxed
+        regexes leave the candidate buffer for the host, which verifies them while the GPU runs the
+        rest of the matchers. host_text: the batch's bytes on the host (``ls`` offsets index it),
+        read by the worker until it publishes (the step's end-of-step read comes after that)."""
         need = self.need
         if need > self.cap:                        # (the previous attempt's buffers are idle)
             self._alloc(max(need * 5 // 4, 2 * self.cap))
             self._worker.clear_need()
         self.seq += 1
-        c, o, i = self.cap, self.out.d, self.inb.d
-        N.take_host(cand.data_ptr(), n1d, cap1, ver.data_ptr(), n2d, cap2, text.data_ptr(), ls.data_ptr(),
-                    ll.data_ptr(), dfa, (o, o + 8 * c, o + 16 * c, c, self.cnt.data_ptr(), self.cnt.data_ptr() + 8,
-                                         o + 24 * c, o + 24 * c + 8, self.seq), stream)
+        N.take_host(cand.data_ptr(), n1d, cap1, 0, 0, 0, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                    self._out(self.out_a, 0), stream)
         ht = np.ascontiguousarray(host_text)
         self._hold = (self._hold + [ht])[-4:]
-        self._worker.submit(self.seq, ht.ctypes.data, c, self.out.h, self.inb.h)
+        self._worker.submit(self.seq, ht.ctypes.data, self.cap, self.out_a.h, self.out_b.h, self.inb.h)
+
+    def export_scan_and_wait(self, ver, n2d: int, cap2: int, text, ls, ll, dfa, stream: int) -> None:
+        """Region B (the scan engines' relaxation keys, after the scans joined), then k_wait_host:
+        the verified keys of both regions are appended to the verified-hit buffer."""
+        N.take_host(0, 0, 0, ver.data_ptr(), n2d, cap2, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                    self._out(self.out_b, 1), stream)
+        c, i = self.cap, self.inb.d
         N.wait_host(ver.data_ptr(), cap2, n2d, (i, i + 8 * c, i + 8 * c + 8, c, self.seq, i + 8 * c + 16), stream)
 
     def check(self) -> None:

@@ -310,7 +310,7 @@ def test_native_side_worker_verifies_exported_candidates():
             assert time.time() - t0 < 10
             time.sleep(0.001)
 
-    w.submit(1, data.ctypes.data, cap, out.ctypes.data, inb.ctypes.data)
+    w.submit(1, data.ctypes.data, cap, out.ctypes.data, 0, inb.ctypes.data)
     time.sleep(0.01)                       # the worker polls until the export is published
     out[3 * cap], out[3 * cap + 1] = n, 1
     wait(1)
@@ -318,7 +318,19 @@ def test_native_side_worker_verifies_exported_candidates():
     want = sorted(k for k in keys if lib.host_bt.find(int(lib.host_local[k >> 32]),
                                                       lines[k & 0xFFFFFFFF].decode()))
     assert got == want and len(want) >= 4 and w.take_error() == ""
-    out[3 * cap], out[3 * cap + 1] = cap + 5, 2     # an export that overflowed its buffer
-    w.submit(2, data.ctypes.data, cap, out.ctypes.data, inb.ctypes.data)
+    # two regions (prefilter candidates, then scan keys): the answer covers both
+    out_b = np.zeros(3 * cap + 2, np.int64)
+    h = n // 2
+    out_b[:n - h], out_b[cap:cap + n - h], out_b[2 * cap:2 * cap + n - h] = \
+        out[h:n], out[cap + h:cap + n], out[2 * cap + h:2 * cap + n]
+    w.submit(2, data.ctypes.data, cap, out.ctypes.data, out_b.ctypes.data, inb.ctypes.data)
+    out[3 * cap], out[3 * cap + 1] = h, 2
+    time.sleep(0.01)
+    assert inb[cap + 1] != 2                # still waiting for region B
+    out_b[3 * cap], out_b[3 * cap + 1] = n - h, 2
     wait(2)
+    assert sorted(inb[:inb[cap]].tolist()) == want
+    out[3 * cap], out[3 * cap + 1] = cap + 5, 3     # an export that overflowed its buffer
+    w.submit(3, data.ctypes.data, cap, out.ctypes.data, 0, inb.ctypes.data)
+    wait(3)
     assert inb[cap] == -1 and w.need == cap + 5

@@ -12,12 +12,15 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-bash tools/gpu_check.sh httpreps pmcscan || exit 1
+run pytest 600 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py tests/test_gpu.py \
+  -m gpu -x -v --timeout 200 --timeout-method thread
+bash tools/gpu_check.sh reqtrace || exit 1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
-P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_WAIT_ANY"
-run pmc1n 180 rocprofv3 --pmc $P1 --kernel-include-regex "k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan_nodefer/p1 \
-  -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap --scan-defer-rare 0
-run pmc2n 180 rocprofv3 --pmc $P2 --kernel-include-regex "k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan_nodefer/p2 \
-  -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap --scan-defer-rare 0
-run pmcsumn 120 python3 tools/pmc_summary.py gpurun_out/pmc_scan_nodefer
+run rts_prof 300 rocprofv3 --kernel-trace -d gpurun_out/rts_prof -o run -- \
+  python3 tools/request_trace.py --requests 200 --java-shape-rate 0.01 --split-verify
+db=$(find gpurun_out/rts_prof -name "*.db" | head -1)
+run rts_sum 120 python3 tools/request_trace.py --db "$db" --requests 200
+run phases 300 python -u tools/engine_phases.py --n 200
+run single 300 python -u benchmarks/bench_configs.py single
+run bench 400 python -u bench.py --steps 10 --warmup 3
+bash tools/gpu_check.sh pmcscan || exit 1

@@ -11,6 +11,8 @@
 // folding it into dfa_run took those kernels from ~40 to 130 VGPRs plus 580 B of scratch per lane.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <stdexcept>
 #include <string>
 
@@ -30,13 +32,21 @@ constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global
 // line's walk: a request verifies a handful of candidates, a bulk step a few thousand)
 constexpr uint32_t kPoolLdsWords = 8192;   // 64 KiB
 
+bool pool_lds_on() {   // (diagnostic while validating the staging: LP_BPG_POOL_LDS=0 turns it off)
+  static const bool on = [] {
+    const char* e = std::getenv("LP_BPG_POOL_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 inline size_t pool_lds_bytes(const DfaPool& P) {
-  return (P.bpg_words && P.bpg_words <= kPoolLdsWords) ? (size_t)P.bpg_words * 8 : 0;
+  return (pool_lds_on() && P.bpg_words && P.bpg_words <= kPoolLdsWords) ? (size_t)P.bpg_words * 8 : 0;
 }
 
 // every thread of the block calls this (it synchronises): the pool in LDS, or in global memory
-__device__ __forceinline__ const uint64_t* stage_pool(const DfaPool& P, uint64_t* lds) {
-  if (P.bpg_words == 0 || P.bpg_words > kPoolLdsWords) return P.bpg;
+__device__ __forceinline__ const uint64_t* stage_pool(const DfaPool& P, uint64_t* lds, bool staged) {
+  if (!staged) return P.bpg;
   for (uint32_t i = threadIdx.x; i < P.bpg_words; i += blockDim.x) lds[i] = P.bpg[i];
   __syncthreads();
   return lds;
@@ -112,7 +122,7 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
     }
   }
   if (!__syncthreads_or(walk)) return;          // block-uniform: most blocks hold no program key
-  const uint64_t* pool = stage_pool(P, pool_lds);
+  const uint64_t* pool = stage_pool(P, pool_lds, P.bpg_words != 0);
   if (walk) flag[i] = lane_walk<WMAX>(pool + P.meta[4 * r], text + ls[x], ll[x]) ? 1 : 0;
 }
 
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(256) void k_bpg_coop(int64_t* __restrict__ cand, co
   }
   extern __shared__ uint64_t pool_lds[];
   if (!__syncthreads_or(need)) return;          // block-uniform (the DFA half returned above)
-  const uint64_t* pool = stage_pool(P, pool_lds);
+  const uint64_t* pool = stage_pool(P, pool_lds, P.bpg_words != 0);
   uint64_t todo = __ballot(need);                // wave-uniform
   constexpr int NG = 64 / G;
   const int g = lane / G;
@@ -443,13 +453,15 @@ void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigne
                  hipStream_t st, int wmin) {
   const dim3 grid(nblocks(cap) * (MODE == 2 ? 2 : 1)), block(256);
   const size_t lds = pool_lds_bytes(P);
+  DfaPool Q = P;
+  if (!lds) Q.bpg_words = 0;                     // the kernels stage the pool iff bpg_words != 0
   switch (coop_group(P.bpg_widths)) {
-    case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
-    case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
-    case 8: hipLaunchKernelGGL((k_bpg_coop<8, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
-    case 16: hipLaunchKernelGGL((k_bpg_coop<16, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
-    case 32: hipLaunchKernelGGL((k_bpg_coop<32, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
-    default: hipLaunchKernelGGL((k_bpg_coop<64, MODE>), grid, block, 0, st, cand, keys, cap, dcount, lbits, text, ls, ll, P, flag, wmin); break;
+    case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
+    case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
+    case 8: hipLaunchKernelGGL((k_bpg_coop<8, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
+    case 16: hipLaunchKernelGGL((k_bpg_coop<16, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
+    case 32: hipLaunchKernelGGL((k_bpg_coop<32, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
+    default: hipLaunchKernelGGL((k_bpg_coop<64, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
   }
 }
 
@@ -554,9 +566,11 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
   // per-width launches added up their slowest walks where one launch runs them side by side)
   const bool listed = any_wide && wcnt && wlist;
   if ((P.bpg_widths & 0x1FFu) || listed) {
+    DfaPool Q = P;
+    if (!pool_lds_bytes(P)) Q.bpg_words = 0;     // the kernel stages the pool iff bpg_words != 0
 #define LP_DEDUPE(WM)                                                                                      \
   hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), pool_lds_bytes(P), st, keys, n, lbits, text, ls, \
-                     ll, P, flag, \
+                     ll, Q, flag, \
                      listed ? wcnt : nullptr, listed ? wlist : nullptr)
     switch (narrow_wmax(P.bpg_widths)) {
       case 1: LP_DEDUPE(1); break;

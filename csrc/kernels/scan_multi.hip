@@ -522,7 +522,11 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
   // small texts: one line per lane in 256-thread blocks (the grid is sized for 1024-thread blocks)
   const bool small = nlines <= (int64_t)grid * SCAN_THREADS_SMALL;
   const size_t lds = (size_t)S.lds_words * 4 + (small ? 0 : SCAN_BM_REP_BYTES);
-  const int run_len = small ? 1 : SCAN_RUN;
+  // bulk texts of fewer than ~4 lines per lane of the grid (a 1M-line document on 512 blocks of
+  // 1024 lanes) walk shorter runs, so every lane of the grid has a run and each lane's dependent
+  // chain is shorter; a 12.5M-line shard keeps 4-line runs
+  const int64_t lanes = (int64_t)grid * SCAN_THREADS;
+  const int run_len = small ? 1 : nlines < 2 * lanes ? 1 : nlines < 4 * lanes ? 2 : SCAN_RUN;
   const int threads = small ? SCAN_THREADS_SMALL : SCAN_THREADS;
   const int64_t runs = (nlines + run_len - 1) / run_len;
   const int64_t need = (runs + threads - 1) / threads;

@@ -13,6 +13,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
 }
 
 run pytest 600 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py tests/test_gpu.py \
+  tests/test_scan_multi.py \
   -m gpu -x -v --timeout 200 --timeout-method thread
 bash tools/gpu_check.sh reqtrace || exit 1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
@@ -22,5 +23,7 @@ db=$(find gpurun_out/rts_prof -name "*.db" | head -1)
 run rts_sum 120 python3 tools/request_trace.py --db "$db" --requests 200
 run phases 300 python -u tools/engine_phases.py --n 200
 run single 300 python -u benchmarks/bench_configs.py single
+bash tools/gpu_check.sh singletrace || exit 1
 run bench 400 python -u bench.py --steps 10 --warmup 3
+run bench_bt 400 python -u bench.py --steps 10 --warmup 3 --bt-patterns 4 --parse-requests 0
 bash tools/gpu_check.sh pmcscan || exit 1

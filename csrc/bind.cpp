@@ -826,6 +826,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("set_pf_verify_lanes", &set_pf_verify_lanes);
   m.def("set_scan_defer_rare", &set_scan_defer_rare);
   m.def("set_cand_verify_split", &set_cand_verify_split);
+  m.def("set_summ_select", &set_summ_select);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false);

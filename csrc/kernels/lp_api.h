@@ -18,6 +18,9 @@ void set_scan_defer_rare(bool on);
 // request path: BPG and DFA candidates verified in ONE launch (k_bpg_coop mode 2, default) or in
 // two (k_cand_verify, then the BPG walk) -- the diagnostic split shows each half's time
 void set_cand_verify_split(bool on);
+// event top-k by threshold selection (summarize.hip k_sel_*, default) or the chunk-sort levels
+bool summ_select();
+void set_summ_select(bool on);
 // line-index pass 1 folded into the bulk prefilter (line_index.hip k_nl_count's outputs): per 16 KiB
 // tile the '\n' count and the "\r\n" flag (both zeroed by the caller), per 64 bytes a '\n' bitmask
 struct NlOut {

@@ -47,6 +47,7 @@ namespace lp {
 
 constexpr int BPG_LANE_MAX_W = 8;      // widest program of the one-lane-per-line walk
 constexpr int BPG_CTR_MAX = 4;         // counted positions per program (jregex.h BPG_MAX_CTR)
+constexpr int BPG_EXC_REG = 4;         // exception headers the device walks keep in registers
 constexpr uint64_t BPG_UNIFORM = 1ull << 31;
 constexpr uint64_t BPG_ANCHORED = 1ull << 30;
 
@@ -273,6 +274,13 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
   uint64_t cmk[W];                     // the counted positions' bits, per word
 #pragma unroll
   for (int w = 0; w < W; ++w) cmk[w] = 0;
+  // the first BPG_EXC_REG exception headers (source | condition) in registers: a per-character load
+  // of each header sat on the state chain (a handful of candidates per request: the kernel's time
+  // IS one walk's chain)
+  const int E = L.E;
+  uint64_t eh[BPG_EXC_REG];
+#pragma unroll
+  for (int e = 0; e < BPG_EXC_REG; ++e) eh[e] = e < E ? exc[(size_t)e * (W + 1)] : 0ull;
 #pragma unroll
   for (int c = 0; c < BPG_CTR_MAX; ++c) {
     const uint64_t e = c < nctr ? P[L.o_ctr + c] : 0ull;
@@ -311,9 +319,13 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
       // all PF rows are loaded before the first state update (one load latency per PF bytes
       // instead of two dependent loads -- class map, then row -- on every byte's chain)
       constexpr int PF = W <= 4 ? 4 : 2;     // rows in flight (registers: PF x W words)
+      // narrow programs also prefetch the context-dependent first / last rows of the PF
+      // characters (their contexts follow from the text alone)
+      constexpr bool PFX = W <= 2;
       for (int jb = j0; jb < j1; jb += PF) {
-        uint64_t Cr[PF][W];
+        uint64_t Cr[PF][W], Fr[PFX ? PF : 1][W], Lr[PFX ? PF : 1][W];
         int kq[PF], nkq[PF];
+        int pk = prevk;
 #pragma unroll
         for (int qq = 0; qq < PF; ++qq) {
           const int j = jb + qq < 15 ? jb + qq : 15;
@@ -321,6 +333,17 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
           const uint64_t* row = cls + (size_t)(kq[qq] < 0 ? 0 : kq[qq]) * W;
 #pragma unroll
           for (int w = 0; w < W; ++w) Cr[qq][w] = row[w];
+          if constexpr (PFX) {
+            const int cx = pk * 6 + nkq[qq];
+            const uint64_t* fr = uniform ? first : first + cx * W;
+            const uint64_t* lr = uniform ? last : last + cx * W;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              Fr[qq][w] = fr[w];
+              Lr[qq][w] = lr[w];
+            }
+            if (kq[qq] >= 0 && jb + qq < j1) pk = prev_of(nkq[qq]);
+          }
         }
 #pragma unroll
         for (int qq = 0; qq < PF; ++qq) {
@@ -332,8 +355,15 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
             LP_BPG_ACCEPT(prevk * 6 + 1, hit);
             if (hit) return true;
           }
-          LP_BPG_ACCEPT(prevk * 6 + nk, hit);
-          if (hit) return true;
+          if constexpr (PFX) {
+            uint64_t any = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) any |= S[w] & Lr[qq][w];
+            if (((nullm >> (prevk * 6 + nk)) & 1u) || any) return true;
+          } else {
+            LP_BPG_ACCEPT(prevk * 6 + nk, hit);
+            if (hit) return true;
+          }
           const int ctx = prevk * 6 + nk;
           uint64_t F[W];
           uint64_t carry = 0, borrow = 0;
@@ -350,7 +380,21 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
             borrow = b1 | b2;
             F[w] |= R[w] & ~(d ^ df);
           }
-          for (int e = 0; e < L.E; ++e) {
+#pragma unroll
+          for (int e = 0; e < BPG_EXC_REG; ++e) {   // exceptions: headers in registers, the
+            if (e >= E) break;                     // targets loaded only when one fires (rare)
+            const uint64_t h = eh[e];
+            const int p = (int)(h & 0xFFFF);
+            uint64_t sw = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) sw = (w == (p >> 6)) ? S[w] : sw;
+            if (((sw >> (p & 63)) & 1ull) && (((uint32_t)(h >> 16) >> ctx) & 1u)) {
+              const uint64_t* x = exc + (size_t)e * (W + 1);
+#pragma unroll
+              for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
+            }
+          }
+          for (int e = BPG_EXC_REG; e < E; ++e) {
             const uint64_t* x = exc + (size_t)e * (W + 1);
             const uint64_t h = x[0];
             const int p = (int)(h & 0xFFFF);
@@ -362,7 +406,10 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
               for (int w = 0; w < W; ++w) F[w] |= x[1 + w];
             }
           }
-          if (uniform) {
+          if constexpr (PFX) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) F[w] |= Fr[qq][w];
+          } else if (uniform) {
 #pragma unroll
             for (int w = 0; w < W; ++w) F[w] |= f0[w];
           } else {

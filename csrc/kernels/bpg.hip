@@ -208,6 +208,15 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
     ncl += own ? 1 : 0;
   }
   const bool wctr = __ballot(nctr > 0) != 0;
+  // the first BPG_EXC_REG exceptions' headers and this lane's target words, in registers (a load of
+  // each per character sat on the state chain)
+  uint64_t eh[BPG_EXC_REG];
+  uint32_t etw[BPG_EXC_REG];
+#pragma unroll
+  for (int e = 0; e < BPG_EXC_REG; ++e) {
+    eh[e] = e < E ? P[exc_o + e * (W + 1)] : 0ull;
+    etw[e] = (e < E && wl) ? LP_W32(exc_o + e * (W + 1) + 1) : 0u;
+  }
   // wave-uniform feature switches: the common program (uniform first/last sets, no exception edges,
   // not nullable, line without a final terminator) walks only the shift / self / spread chain
   const bool wnon = __ballot(valid && !uniform) != 0;
@@ -283,7 +292,15 @@ __device__ __forceinline__ bool bpg_coop_walk(const uint64_t* __restrict__ P, co
       F |= R & ~(d ^ df);
       if (wexc) {                                // exception edges: the source word's lane votes
         const int ctx = ctxq[q];
-        for (int e = 0; e < E; ++e) {            // E varies across groups: lanes past their E idle
+#pragma unroll
+        for (int e = 0; e < BPG_EXC_REG; ++e) {  // headers / target words in registers
+          const uint64_t h = eh[e];
+          const int p = (int)(h & 0xFFFF);
+          const uint64_t M = __ballot(e < E && j == (p >> 5) && ((S >> (p & 31)) & 1u));
+          if (e < E && ((M >> (gb + (p >> 5))) & 1ull) && ((((uint32_t)(h >> 16) & 0xFFFFFFu) >> ctx) & 1u))
+            F |= etw[e];
+        }
+        for (int e = BPG_EXC_REG; e < E; ++e) {  // E varies across groups: lanes past their E idle
           const uint64_t h = P[exc_o + e * (W + 1)];
           const uint32_t tw = wl ? LP_W32(exc_o + e * (W + 1) + 1) : 0u;
           const int p = (int)(h & 0xFFFF);

@@ -256,9 +256,12 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
   for (int g = 0; g < G; ++g) xr[g] = (uint32_t)S.init_row[g];
   const int64_t a0 = p_lo & ~(int64_t)15;
   const uint4* blk = reinterpret_cast<const uint4*>(text + a0);
-  uint4 cur = blk[0];
+  // the text two blocks ahead: a block's 16 dependent LDS steps (~2k cycles) did not cover an HBM
+  // round trip under load, so one block of look-ahead left the walk waiting on its next load
+  // (texts are padded by TEXT_PAD >= 48 bytes past the last line: the look-ahead stays in bounds)
+  uint4 cur = blk[0], nxt = blk[1];
   for (int64_t p0 = a0; p0 < p_end; p0 += 16) {
-    const uint4 nxt = blk[1];
+    const uint4 nx2 = blk[2];
     ++blk;
     const uint32_t w[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
     uint32_t hold = 0;                    // CRLF: byte j of the block is a separator '\r'
@@ -309,6 +312,7 @@ __device__ __forceinline__ void scan_run_fast(const uint32_t* sm, const ScanPass
       else scan_block_masks<CRLF>(S, w, hold, p0, p_lo, p_end, x0, x1, line_start, g, xg, emit);
     }
     cur = nxt;
+    nxt = nx2;
   }
 }
 

@@ -313,6 +313,7 @@ class SideWorker {
         fail(e.what());
         __atomic_store_n(j.inb + j.cap, (int64_t)-1, __ATOMIC_RELEASE);
         __atomic_store_n(j.inb + j.cap + 1, j.seq, __ATOMIC_RELEASE);
+        done_++;
       }
     }
   }

@@ -290,10 +290,12 @@ struct HbIn {            // candidate entries in the HitsArgs layout
   const int64_t* cand2;
   int64_t n, pre_from, n1, n2;   // n1 / n2: used lengths of the two regions (device-count mode)
   bool dc;
+  uint32_t R, lmask;             // a key outside [0, R) x [0, 2^lbits) is never bucketed
 };
 
 __device__ __forceinline__ HbIn hb_in(const HitsArgs& A) {
-  HbIn S{A.cand, A.cand2, A.n, A.pre_from, A.pre_from, A.n - A.pre_from, A.dcount != nullptr};
+  HbIn S{A.cand, A.cand2, A.n, A.pre_from, A.pre_from, A.n - A.pre_from, A.dcount != nullptr,
+         (uint32_t)A.R, A.lbits >= 32 ? ~0u : ((1u << A.lbits) - 1u)};
   if (S.dc) {
     S.n1 = (int64_t)min((unsigned long long)S.n1, A.dcount[0]);
     S.n2 = (int64_t)min((unsigned long long)S.n2, A.dcount[1]);
@@ -322,7 +324,9 @@ __device__ __forceinline__ bool hb_get(const HbIn& S, int64_t i, uint32_t& r, ui
   }
   if (k < 0) return false;
   r = (uint32_t)(k >> 32);
-  v = ((uint32_t)(k & 0xFFFFFFFFll) << 1) | (pre ? 1u : 0u);
+  const uint32_t x = (uint32_t)(k & 0xFFFFFFFFll);
+  if (r >= S.R || (x & ~S.lmask)) return false;   // (defensive: a key no matcher can produce)
+  v = (x << 1) | (pre ? 1u : 0u);
   return true;
 }
 

@@ -452,21 +452,29 @@ __global__ __launch_bounds__(256) void k_scan_rare(const uint8_t* __restrict__ t
     }
   }
   __syncthreads();
-  volatile uint32_t* last = sm + S.lds_words;    // (a word behind the blob: no static LDS)
+  volatile uint32_t* last = sm + S.lds_words;    // (words behind the blob: no static LDS)
+  volatile unsigned long long* pad = reinterpret_cast<volatile unsigned long long*>(sm + S.lds_words + 2);
   if (threadIdx.x == 0) {
     __threadfence();
     *last = atomicAdd(rare.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+    *pad = ~0ull;
   }
   __syncthreads();
-  if (*last && threadIdx.x == 0) {
+  if (!*last) return;
+  if (threadIdx.x == 0) {
     if (n > rare.cap) {
       rare.need[0] = n;                          // grown before the re-run
       __threadfence_system();
-      atomicAdd(count, (unsigned long long)(cap + 1));
+      *pad = atomicAdd(count, (unsigned long long)(cap + 1));
     }
     *rare.cnt = 0;
     *rare.done = 0;
   }
+  __syncthreads();
+  // the overflow signal pushes the count past the capacity: the hit pipeline then reads the whole
+  // buffer, so its unwritten tail becomes dropped keys (-1), never uninitialised memory
+  const unsigned long long p0 = *pad;
+  for (int64_t i = (int64_t)p0 + threadIdx.x; p0 != ~0ull && i < cap; i += blockDim.x) out[i] = -1;
 }
 
 namespace {
@@ -558,7 +566,7 @@ void scan_multi_dev(const uint8_t* text, int64_t nbytes, const int64_t* line_sta
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in scan_multi");
   if (defer) {
-    hipLaunchKernelGGL(k_scan_rare, dim3(256), dim3(256), (size_t)S.lds_words * 4 + 16, st, text, line_start, S, out,
+    hipLaunchKernelGGL(k_scan_rare, dim3(256), dim3(256), (size_t)S.lds_words * 4 + 32, st, text, line_start, S, out,
                        cap, count, rare);
     e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) + " in scan_rare");

@@ -62,6 +62,7 @@ __global__ __launch_bounds__(kTakeThreads) void k_take_host(int64_t* __restrict_
       O.keys[j] = k;
       O.starts[j] = ls[x];
       O.lens[j] = ll[x];
+      __threadfence_system();                    // host-visible before this block counts as done
     }
   }
   if (!O.keys) return;
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(kTakeThreads) void k_take_host(int64_t* __restrict_
   __syncthreads();
   __shared__ bool last;
   if (threadIdx.x == 0) {
-    __threadfence();
+    __threadfence_system();
     last = atomicAdd(O.done_blocks, 1u) == gridDim.x - 1;
   }
   __syncthreads();
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(kTakeThreads) void k_take_host(int64_t* __restrict_
 __global__ __launch_bounds__(kTakeThreads) void k_wait_host(int64_t* __restrict__ ver, int64_t cap2,
                                                             unsigned long long* __restrict__ n2d, HostSideIn I) {
   __shared__ int64_t n;
-  __shared__ unsigned long long base;
+  __shared__ unsigned long long base, pad_from;
   if (threadIdx.x == 0) {
     const long long t0 = wall_clock64();
     bool ok = true;
@@ -96,14 +97,19 @@ __global__ __launch_bounds__(kTakeThreads) void k_wait_host(int64_t* __restrict_
       __builtin_amdgcn_s_sleep(8);
     }
     const int64_t hc = ok ? load_sys(I.host_cnt) : -1;
+    pad_from = ~0ull;
     if (hc < 0) {            // no answer in time, or the host failed / its export overflowed: the
       I.err[0] = ok ? 2 : 1; // batch overflows (its frequency record is vetoed, the caller re-runs)
-      atomicAdd(n2d, (unsigned long long)(cap2 + 1));
+      pad_from = atomicAdd(n2d, (unsigned long long)(cap2 + 1));
     }
     n = hc < 0 ? 0 : min(hc, I.cap);
     base = n > 0 ? atomicAdd(n2d, (unsigned long long)n) : 0ull;
   }
   __syncthreads();
+  // the overflow signal pushes the count past the capacity, so the hit pipeline (which runs before
+  // the host sees the counts) reads the WHOLE buffer: its unwritten tail becomes dropped keys
+  // (-1), never uninitialised memory
+  for (int64_t i = (int64_t)pad_from + threadIdx.x; pad_from != ~0ull && i < cap2; i += blockDim.x) ver[i] = -1;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x)
     if ((int64_t)(base + i) < cap2) ver[base + i] = I.keys[i];
 }

@@ -474,7 +474,7 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
     scans = bool(tabs["scan_passes"]) or bool(tabs["scan_regs"].numel()) or \
         any(g.numel() for g in tabs["nfa_scan_lists"].values())
     ninj = 0 if inject is None else inject.numel()
-    while True:
+    for attempt in range(8):         # each overflow learns the exact rates: one re-run is the rule
         cap = arena.caps(L)
         cap["ver"] += ninj
         if early is not None:            # prefilter already queued (behind the line index)
@@ -553,6 +553,9 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
         arena.learn(L, {"gram": g, "cand": k, "ver": v}, overflow=not ok)
         if ok:
             return hits[:nh], hit_line, hit_off, ev_cnt, ev_end, nh, ne
+        if host_side is not None:          # the worker answers every job before the re-run's export
+            host_side[0].settle()
+    raise RuntimeError(f"matching: buffers still overflowing after 8 attempts ({arena.last})")
 
 
 def results_buffer(ne: int, nkeys: int, device) -> torch.Tensor:

@@ -49,6 +49,7 @@ class HostSide:
         # the verifying thread is native (bind.cpp SideWorker): no GIL between export and answer
         self._worker = N.SideWorker(lib.host_bt, [int(x) for x in np.asarray(lib.host_local, np.int32)])
         self._hold = []                            # host bytes of the queued batches (the worker reads them)
+        self.waits_failed = 0                      # jobs the GPU stopped waiting for (settle)
 
     def _alloc(self, cap: int) -> None:
         self.cap = int(cap)
@@ -89,6 +90,24 @@ class HostSide:
                     self._out(self.out_b, 1), stream)
         c, i = self.cap, self.inb.d
         N.wait_host(ver.data_ptr(), cap2, n2d, (i, i + 8 * c, i + 8 * c + 8, c, self.seq, i + 8 * c + 16), stream)
+
+    def settle(self, timeout_s: float = 30.0) -> int:
+        """Before an overflowing step re-runs: wait until the worker has answered every queued job
+        (a re-run's export reuses the regions, and a job still reading them would see the next
+        attempt's sequence numbers), then return and clear the GPU's wait status of the last job
+        (0 answered, 1 no answer within the GPU's wait, 2 the host answered -1)."""
+        import time
+        t0 = time.monotonic()
+        while int(self._worker.done) < self.seq and time.monotonic() - t0 < timeout_s:
+            time.sleep(0.0005)
+        err = int(self.inb.a[self.cap + 2])
+        if err:
+            self.waits_failed += 1
+            log.warning("backtracker side path: job %d %s (worker done %d); the step re-runs", self.seq,
+                        "not answered within the GPU's wait" if err == 1 else "answered -1 (export overflow)",
+                        int(self._worker.done))
+            self.inb.a[self.cap + 2] = 0
+        return err
 
     def check(self) -> None:
         """Raise the helper's error (the step has re-run or failed meanwhile)."""

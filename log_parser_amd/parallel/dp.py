@@ -229,6 +229,8 @@ class ShardedAnalyzer:
                 return self._trim(out, prep, counts[4])
             # some rank overflowed a buffer: every rank learns its exact rates and re-runs
             eng.arena.learn(L, {"gram": counts[0], "cand": counts[1], "ver": counts[2], "ev": counts[4]}, overflow=True)
+            if eng._host_side is not None:      # the side path's worker answers before the re-run's export
+                eng._host_side.settle()
         raise RuntimeError("DP step: buffers still overflowing after re-runs")
 
     @staticmethod

@@ -451,6 +451,214 @@ __device__ __forceinline__ bool bpg_find_dev(const uint64_t* __restrict__ P, con
   return hit;
 #undef LP_BPG_ACCEPT
 }
+
+// class of a non-ASCII code point through the range table at P[o] (bpg_cp_class over any pointer)
+template <typename PT>
+__device__ __forceinline__ int bpg_cp_class_p(PT P, int o, int nr, uint32_t cp, int* kind) {
+  int lo = 0, hi = nr - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if ((uint32_t)(P[o + mid] & 0x1FFFFFu) <= cp) lo = mid; else hi = mid - 1;
+  }
+  const uint64_t e = P[o + lo];
+  const int kd = (int)((e >> 37) & 3);
+  *kind = kd == 1 ? 2 : kd == 2 ? 5 : 3;
+  return (int)((e >> 21) & 0xFFFF);
+}
+
+// Lean one-lane walk of a ONE-WORD program (<= 64 positions -- every program of the realistic
+// library since counted positions), same find() semantics as bpg_find_dev / bpg_find_w.
+// bpg_find_dev<1> above compiles to ~150 instructions per character (every optional feature an
+// exec-mask branch, SGPR spills) and a request's candidate walk ran at 340-440 ns per byte
+// (tools/bpg_probe.py). Here the common character is the structural chain (~25 VALU ops on 64-bit
+// masks) plus operands that depend on the TEXT only -- class row, and the first / last rows of the
+// character's boundary context (a uniform program stores all 24 identical rows, so no branch on
+// uniformity) -- loaded four characters ahead. The optional features (exception edges, counted
+// positions, a final line terminator, multi-byte characters) run behind WAVE-uniform ballots: a
+// wave none of whose lanes needs one skips it with a scalar branch. `valid` false: the lane takes
+// part in the ballots and walks nothing (P must still point at readable program words).
+// PT: pointer to the program's words -- LDS (ds_read) when the pool is staged, else global.
+template <typename PT>
+__device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, int n, bool valid) {
+  const uint64_t h = P[0];
+  const int E = valid ? (int)((h >> 8) & 0xFFF) : 0;
+  const int ncls = (int)((h >> 20) & 0x3FF);
+  const uint32_t nullm = valid ? (uint32_t)(h >> 32) & 0xFFFFFFu : 0u;
+  const int nranges = (int)(P[1] & 0xFFFFFFFFu);
+  const int nctr = valid ? (int)((h >> 57) & 7) : 0;
+  if (!valid) n = 0;
+  constexpr int oF = 8, oL = 32, oA = 56, oC = 88;          // bpg_layout for W = 1
+  const int oE = oC + ncls, oR = oE + 2 * E, oT = oR + nranges;
+  const uint64_t shm = P[2], selfm = P[3], src = P[4], R = P[5], lo = P[6], hi = P[7];
+  // exception edges / counted positions: the first BPG_EXC_REG / all BPG_CTR_MAX in registers;
+  // mexc / mctr = the wave's largest counts (uniform trip counts, per-lane predicates)
+  uint64_t eh[BPG_EXC_REG], et[BPG_EXC_REG], ebit[BPG_EXC_REG];
+  int mexc = 0, mctr = 0;
+#pragma unroll
+  for (int e = 0; e < BPG_EXC_REG; ++e) {
+    eh[e] = e < E ? P[oE + 2 * e] : 0ull;                  // (0 past E: no source bit, no condition)
+    et[e] = e < E ? P[oE + 2 * e + 1] : 0ull;
+    ebit[e] = e < E ? 1ull << (eh[e] & 63) : 0ull;
+    mexc = __ballot(E > e) ? e + 1 : mexc;
+  }
+  const bool wexc_more = __ballot(E > BPG_EXC_REG) != 0;
+  uint64_t cbit[BPG_CTR_MAX];
+  uint32_t cbound[BPG_CTR_MAX], cnt[BPG_CTR_MAX];
+#pragma unroll
+  for (int c = 0; c < BPG_CTR_MAX; ++c) {
+    const uint64_t e = c < nctr ? P[oT + c] : 0ull;
+    cbit[c] = c < nctr ? 1ull << (e & 63) : 0ull;          // (no bit past nctr: never enters, stays)
+    cbound[c] = (uint32_t)(e >> 16);
+    cnt[c] = 0;
+    mctr = __ballot(nctr > c) ? c + 1 : mctr;
+  }
+  const int ftl = n > 0 ? final_term_len(s, n) : 0;
+  const int ft = ftl ? n - ftl : -1;
+  const bool wft = __ballot(ftl > 0) != 0;
+  // simple wave: every lane's program has context-free first / last sets, no nullable context and no
+  // exception edge -- its characters need no boundary context (kind, previous kind) at all
+  const bool uni = (h & BPG_UNIFORM) != 0;
+  const bool wsimple = __ballot(valid && !(uni && nullm == 0u && E == 0)) == 0;
+  const uint64_t f0 = P[oF], l0 = P[oL];
+  uint64_t S = 0, acc = 0, Sft = 0;
+  uint32_t nullhit = 0;
+  int ftctx = 0;
+  int prevk = 0;                                           // P_BOS
+  const int sh = (int)((uintptr_t)s & 15);
+  const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
+  uint4 cur = n > 0 ? blk[0] : make_uint4(0, 0, 0, 0);
+  for (int b0 = 0;; b0 += 16) {                            // wave-uniform (the break below)
+    const bool live = b0 < sh + n;
+    const uint4 nxt = live ? blk[(b0 >> 4) + 1] : make_uint4(0, 0, 0, 0);   // (texts are padded)
+    const bool wmb = __ballot(live && ((cur.x | cur.y | cur.z | cur.w) & 0x80808080u) != 0) != 0;
+    // text-only operands of the block's 16 characters, all loads in flight before the chain
+    uint64_t Cq[16], Fq[16], Lq[16];
+    int ctxq[16];
+    uint32_t onm = 0;
+    int pk = prevk;
+    if (wsimple && !wmb) {                                 // ASCII block, context-free programs
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int t = b0 + j - sh;
+        const int c = blk_byte(cur, j);
+        const bool on = t >= 0 && t < n;
+        const int k = (int)((P[oA + (c >> 2)] >> (16 * (c & 3))) & 0xFFFFu);
+        ctxq[j] = 0;
+        onm |= on ? 1u << j : 0u;
+        Cq[j] = on ? P[oC + k] : 0ull;
+        Fq[j] = f0;
+        Lq[j] = l0;
+      }
+    } else if (!wmb) {                                     // ASCII block
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int t = b0 + j - sh;
+        const int c = blk_byte(cur, j);
+        const bool on = t >= 0 && t < n;
+        const int k = (int)((P[oA + (c >> 2)] >> (16 * (c & 3))) & 0xFFFFu);
+        const int nk = ascii_kind(c);
+        const int ctx = pk * 6 + nk;
+        ctxq[j] = ctx;
+        onm |= on ? 1u << j : 0u;
+        Cq[j] = on ? P[oC + k] : 0ull;
+        Fq[j] = P[oF + ctx];
+        Lq[j] = P[oL + ctx];
+        if (wft && on && t == ft) ftctx = pk * 6 + 1;
+        pk = on ? prev_of(nk) : pk;
+      }
+    } else {                                               // multi-byte characters in some lane
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int t = b0 + j - sh;
+        const int c = blk_byte(cur, j);
+        bool on = t >= 0 && t < n;
+        int k = 0, nk = 3;
+        if (c < 0x80) {
+          k = (int)((P[oA + (c >> 2)] >> (16 * (c & 3))) & 0xFFFFu);
+          nk = ascii_kind(c);
+        } else if (c < 0xC0) {
+          on = false;                                      // continuation byte: inside a code point
+        } else if (on) {
+          const int b1 = t + 1 < n ? win_byte(cur, nxt, j + 1) : 0x80;
+          const int b2 = t + 2 < n ? win_byte(cur, nxt, j + 2) : 0x80;
+          const int b3 = t + 3 < n ? win_byte(cur, nxt, j + 3) : 0x80;
+          k = bpg_cp_class_p(P, oR, nranges, utf8_cp(c, b1, b2, b3), &nk);
+        }
+        const int ctx = pk * 6 + nk;
+        ctxq[j] = ctx;
+        onm |= on ? 1u << j : 0u;
+        Cq[j] = on ? P[oC + k] : 0ull;
+        Fq[j] = P[oF + ctx];
+        Lq[j] = P[oL + ctx];
+        if (wft && on && t == ft) ftctx = pk * 6 + 1;
+        pk = on ? prev_of(nk) : pk;
+      }
+    }
+    // the state chain of the 16 characters, specialised by what the wave needs (a scalar branch per
+    // block): CTX -- boundary contexts (context-dependent first / last rows, nullable contexts,
+    // exception conditions), EXC -- exception edges, CTR -- counted positions
+#define LP_W1_CHAIN(CTX, EXC, CTR)                                                                  \
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) {                                                \
+    const bool on = (onm >> j) & 1u;                                                               \
+    const int ctx = ctxq[j];                                                                       \
+    const uint64_t keep = on ? 0ull : ~0ull;             /* off the line: S stays (no branch) */    \
+    acc |= S & (CTX ? Lq[j] : l0) & ~keep;               /* accept before this character */        \
+    if (CTX) nullhit |= on ? (nullm >> ctx) & 1u : 0u;                                             \
+    if (wft) Sft = (on && b0 + j - sh == ft) ? S : Sft;                                            \
+    uint64_t F = ((S & shm) << 1) | (S & selfm) | (CTX ? Fq[j] : f0);                              \
+    const uint64_t df = (S & src) | hi;                                                            \
+    F |= R & ~((df - lo) ^ df);                          /* spread fields: one word, no borrow */   \
+    if (EXC) {                                                                                     \
+      _Pragma("unroll") for (int e = 0; e < BPG_EXC_REG; ++e) {                                    \
+        if (e >= mexc) break;                                                                      \
+        const uint64_t hh = eh[e];                                                                 \
+        const bool fire = ((S & ebit[e]) != 0ull) & (((((uint32_t)(hh >> 16) & 0xFFFFFFu) >> ctx) & 1u) != 0u); \
+        F |= fire ? et[e] : 0ull;                                                                  \
+      }                                                                                            \
+      if (wexc_more)                                                                               \
+        for (int e = BPG_EXC_REG; e < E; ++e) {                                                    \
+          const uint64_t hh = P[oE + 2 * e];                                                       \
+          if (((S >> (hh & 63)) & 1ull) && ((((uint32_t)(hh >> 16) & 0xFFFFFFu) >> ctx) & 1u)) F |= P[oE + 2 * e + 1]; \
+        }                                                                                          \
+    }                                                                                              \
+    if (CTR) {                                           /* bpg_ctr_step; a dead position's count */ \
+      _Pragma("unroll") for (int c = 0; c < BPG_CTR_MAX; ++c) { /* is never read: every count   */ \
+        if (c >= mctr) break;                            /* advances unconditionally          */ \
+        const uint64_t cb = cbit[c];                                                               \
+        const bool lt = cnt[c] < cbound[c];                                                        \
+        const bool entry = (F & cb) != 0ull;                                                       \
+        F |= (lt && (S & cb) != 0ull) ? cb : 0ull;                                                 \
+        cnt[c] = on ? (entry ? 1u : cnt[c] + (lt ? 1u : 0u)) : cnt[c];                             \
+      }                                                                                            \
+    }                                                                                              \
+    S = (F & Cq[j]) | (S & keep);                        /* Cq = 0 off the line */                 \
+  }
+    if (wsimple && !wmb) {
+      if (mctr) { LP_W1_CHAIN(false, false, true) } else { LP_W1_CHAIN(false, false, false) }
+    } else if (mexc) {
+      if (mctr) { LP_W1_CHAIN(true, true, true) } else { LP_W1_CHAIN(true, true, false) }
+    } else {
+      if (mctr) { LP_W1_CHAIN(true, false, true) } else { LP_W1_CHAIN(true, false, false) }
+    }
+#undef LP_W1_CHAIN
+    prevk = pk;
+    cur = nxt;
+    const bool fin = !live || acc != 0 || nullhit != 0 || b0 + 16 >= sh + n;
+    if (__ballot(!fin) == 0) break;
+  }
+  if (valid && wsimple) {                                  // (every context row is row 0)
+    acc |= (S | Sft) & l0;
+  } else if (valid) {
+    const int ce = prevk * 6 + 0;                          // end of line (N_EOS)
+    acc |= S & P[oL + ce];
+    nullhit |= (nullm >> ce) & 1u;
+    if (ft >= 0) {
+      acc |= Sft & P[oL + ftctx];
+      nullhit |= (nullm >> ftctx) & 1u;
+    }
+  }
+  return valid && (acc != 0 || nullhit != 0);
+}
 #endif
 
 // host twin: find() of one BPG program over s[0, n) (width from the header). On the device the

@@ -40,6 +40,14 @@ bool pool_lds_on() {   // (diagnostic while validating the staging: LP_BPG_POOL_
   return on;
 }
 
+bool lean_on() {   // (A/B while validating the lean one-word walk: LP_BPG_LEAN=0 keeps the old walks)
+  static const bool on = [] {
+    const char* e = std::getenv("LP_BPG_LEAN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 inline size_t pool_lds_bytes(const DfaPool& P) {
   return (pool_lds_on() && P.bpg_words && P.bpg_words <= kPoolLdsWords) ? (size_t)P.bpg_words * 8 : 0;
 }
@@ -53,6 +61,11 @@ __device__ __forceinline__ const uint64_t* stage_pool(const DfaPool& P, uint64_t
 }
 
 inline unsigned nblocks(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+// the staged pool as an LDS pointer: the walks' reads compile to ds_read (a generic pointer that may
+// be LDS or global compiles to flat loads, which wait on both the LDS and the vector-memory counters)
+typedef const __attribute__((address_space(3))) uint64_t* LdsWords;
+__device__ __forceinline__ LdsWords lds_words(const uint64_t* lds) { return (LdsWords)lds; }
 
 // WMAX: the library's widest program of <= 8 words -- only walks up to that width are compiled
 // into the kernel, so a library of one-word programs (the common case since counted positions)
@@ -122,8 +135,63 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
     }
   }
   if (!__syncthreads_or(walk)) return;          // block-uniform: most blocks hold no program key
-  const uint64_t* pool = stage_pool(P, pool_lds, P.bpg_words != 0);
-  if (walk) flag[i] = lane_walk<WMAX>(pool + P.meta[4 * r], text + ls[x], ll[x]) ? 1 : 0;
+  const bool staged = P.bpg_words != 0;
+  const uint64_t* pool = stage_pool(P, pool_lds, staged);
+  if constexpr (WMAX == 1) {                    // one-word programs: the lean walk, every lane in
+    if (__ballot(walk) == 0) return;
+    const int off = walk ? P.meta[4 * r] : 0;
+    const uint8_t* s = text + (walk ? ls[x] : 0);
+    const int len = walk ? ll[x] : 0;
+    const bool hit = staged ? bpg_walk1(lds_words(pool_lds) + off, s, len, walk) : bpg_walk1(P.bpg + off, s, len, walk);
+    if (walk) flag[i] = hit ? 1 : 0;
+  } else {
+    if (walk) flag[i] = lane_walk<WMAX>(pool + P.meta[4 * r], text + ls[x], ll[x]) ? 1 : 0;
+  }
+}
+
+// Request path for libraries of one-word programs (bpg_widths == 1 << 1, the common case): ONE lane
+// per BPG candidate with the lean walk (bpg_walk1) over the pool staged in LDS -- the cooperative
+// walk's two lanes per line cost ~340 ns per byte at one word (profiles/r5_c) -- and, MODE 2, the
+// DFA candidates in the grid's upper half (k_bpg_coop's layout).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_bpg_cand1(int64_t* __restrict__ cand, int64_t cap,
+                                                   const unsigned long long* __restrict__ dcount,
+                                                   const uint8_t* __restrict__ text, const int64_t* __restrict__ ls,
+                                                   const int32_t* __restrict__ ll, DfaPool P) {
+  const int64_t n = dcount ? (int64_t)min((unsigned long long)cap, dcount[0]) : cap;
+  if (MODE == 2 && blockIdx.x >= (gridDim.x >> 1)) {
+    const int64_t jj = (int64_t)(blockIdx.x - (gridDim.x >> 1)) * blockDim.x + threadIdx.x;
+    if (jj >= n) return;
+    const int64_t k = cand[jj];
+    if (k < 0) return;
+    const int r = (int)(k >> 32);
+    if (is_bpg(P, r)) return;
+    const int64_t x = k & 0xFFFFFFFFll;
+    if (!dfa_run(P, r, text + ls[x], ll[x])) cand[jj] = -1;
+    return;
+  }
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int r = 0;
+  int64_t x = 0;
+  bool need = false;
+  if (i < n) {
+    const int64_t k = cand[i];
+    if (k >= 0) {
+      r = (int)(k >> 32);
+      x = k & 0xFFFFFFFFll;
+      need = is_bpg(P, r);
+    }
+  }
+  extern __shared__ uint64_t pool_lds[];
+  if (!__syncthreads_or(need)) return;          // block-uniform (the DFA half returned above)
+  const bool staged = P.bpg_words != 0;
+  stage_pool(P, pool_lds, staged);
+  if (__ballot(need) == 0) return;              // wave-uniform
+  const int off = need ? P.meta[4 * r] : 0;
+  const uint8_t* s = text + (need ? ls[x] : 0);
+  const int len = need ? ll[x] : 0;
+  const bool hit = staged ? bpg_walk1(lds_words(pool_lds) + off, s, len, need) : bpg_walk1(P.bpg + off, s, len, need);
+  if (need && !hit) cand[i] = -1;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -472,6 +540,11 @@ void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigne
   const size_t lds = pool_lds_bytes(P);
   DfaPool Q = P;
   if (!lds) Q.bpg_words = 0;                     // the kernels stage the pool iff bpg_words != 0
+  if (MODE != 1 && P.bpg_widths == (1u << 1) && lean_on()) {
+    if (MODE == 2) hipLaunchKernelGGL((k_bpg_cand1<2>), grid, block, lds, st, cand, cap, dcount, text, ls, ll, Q);
+    else hipLaunchKernelGGL((k_bpg_cand1<0>), grid, block, lds, st, cand, cap, dcount, text, ls, ll, Q);
+    return;
+  }
   switch (coop_group(P.bpg_widths)) {
     case 2: hipLaunchKernelGGL((k_bpg_coop<2, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
     case 4: hipLaunchKernelGGL((k_bpg_coop<4, MODE>), grid, block, lds, st, cand, keys, cap, dcount, lbits, text, ls, ll, Q, flag, wmin); break;
@@ -501,7 +574,12 @@ __global__ __launch_bounds__(kScanLines) void k_bpg_scan(const uint8_t* __restri
   if (nw <= kLdsProgWords) {
     for (int i = threadIdx.x; i < nw; i += blockDim.x) sp[i] = prog[i];
     __syncthreads();
-    if (line < L) m = bpg_find_dev<W>(sp, text + ls[line], ll[line]);
+    if constexpr (W == 1) {
+      const bool v = line < L;
+      m = bpg_walk1(lds_words(sp), text + (v ? ls[line] : 0), v ? ll[line] : 0, v);
+    } else if (line < L) {
+      m = bpg_find_dev<W>(sp, text + ls[line], ll[line]);
+    }
   } else if (line < L) {
     m = bpg_find_dev<W>(prog, text + ls[line], ll[line]);
   }
@@ -589,7 +667,7 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
   hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), pool_lds_bytes(P), st, keys, n, lbits, text, ls, \
                      ll, Q, flag, \
                      listed ? wcnt : nullptr, listed ? wlist : nullptr)
-    switch (narrow_wmax(P.bpg_widths)) {
+    switch (narrow_wmax(P.bpg_widths) == 1 && !lean_on() ? 2 : narrow_wmax(P.bpg_widths)) {
       case 1: LP_DEDUPE(1); break;
       case 2: LP_DEDUPE(2); break;
       case 4: LP_DEDUPE(4); break;

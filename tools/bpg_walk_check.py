@@ -25,14 +25,24 @@ def main():
     from log_parser_amd.models.compiled import CompiledLibrary
     from log_parser_amd.ops.kernels import padded_len
     from log_parser_amd.utils.config import ScoringParams
+    from log_parser_amd.native import N
+    from test_java_shapes import ALPHA, UNI_PATS, VERDICT_SHAPES
+    import random
     sets, trig = _shape_library(a.seed)
     lib = CompiledLibrary(sets, ScoringParams())
     docs = _docs(trig, a.seed)
-    data = "".join(docs).encode()
+    rng = random.Random(a.seed)
+    # Unicode / boundary-context shapes as code-point programs, counted repeats, random lines full of
+    # non-ASCII code points and terminators next to the documents' lines
+    extra = UNI_PATS + VERDICT_SHAPES + [r"X.{0,100}Y", r"a[^\n]{0,40}FATAL", r"(?i)(err|warn).{0,30}x",
+                                         r"x{2,40}", r"(?m)^ab.{0,20}c$", r"\bqq.{0,25}zz\b"]
+    rand = ["".join(rng.choice(ALPHA + "XYxqz") for _ in range(rng.randint(0, 60))) for _ in range(600)]
+    docs = docs + ["\n".join(rand) + "\n"]
+    data = "".join(docs).encode("utf-8", errors="surrogatepass")
     lines = golden.split_lines("".join(docs))
     starts, pos = [], 0
     for ln in lines:                               # byte offsets of Java's split("\r?\n") lines
-        b = ln.encode()
+        b = ln.encode("utf-8", errors="surrogatepass")
         starts.append((pos, len(b)))
         pos += len(b)
         if data[pos:pos + 2] == b"\r\n":
@@ -41,6 +51,10 @@ def main():
             pos += 1
     tmp = tempfile.mkdtemp()
     progs = [lib.bpg_program(r) for r in lib.bpg_regs]
+    for p in extra:
+        d = N.compile_regex(p, 2, 4096)              # DFA refused: the code-point program
+        if d.get("bpg"):
+            progs.append(np.frombuffer(d["bpg"], np.uint64))
     with open(os.path.join(tmp, "progs.bin"), "wb") as f:
         f.write(np.array([len(progs)], np.uint64).tobytes())
         for p in progs:

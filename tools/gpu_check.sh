@@ -9,6 +9,7 @@
 #   configs config 2 (1M lines, 256 patterns, realistic library) and config 1 (CPU-only /parse)
 #   singletrace  config 2 kernel timeline (the whole-document step is the last one traced)
 #   reqtrace  one 10k-line request: wall p50 + kernel timeline, library with / without Java shapes
+#   splitverify  request path with the DFA / BPG candidate verification split, one BPG walk's cost
 #   prof    kernel table of the bench step (rocprofv3 kernel trace, serialised ingest)
 #   pmcscan PMC counters of the scan walk and prefilter (two counter passes)
 #   httpreps  config 5, 1 and 2 processes, 5 runs each: stage / connection timelines, thread states
@@ -64,6 +65,18 @@ for s in $steps; do
         db=$(find gpurun_out/rt_prof_$j -name "*.db" | head -1)
         run rt_sum_$j 120 python3 tools/request_trace.py --db "$db" --requests 200
       done ;;
+    splitverify)
+      # request path with DFA and BPG candidates verified in two launches (each half's time), and
+      # one BPG walk's cost per program (tools/bpg_probe.py)
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      for j in 0 0.01; do
+        run sv_prof_$j 300 rocprofv3 --kernel-trace -d gpurun_out/sv_prof_$j -o run -- \
+          python3 tools/request_trace.py --requests 200 --java-shape-rate $j --split-verify
+        db=$(find gpurun_out/sv_prof_$j -name "*.db" | head -1)
+        run sv_sum_$j 120 python3 tools/request_trace.py --db "$db" --requests 200
+        rm -rf gpurun_out/sv_prof_$j
+      done
+      run bpg_probe 300 python3 tools/bpg_probe.py --lens 32,128,512 --java-shape-rate 0.01 ;;
     prof)
       cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
       run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bench -o run -- \

@@ -1,4 +1,4 @@
-// Host build of the DEVICE one-lane BPG walk (bpg.h bpg_find_dev<W>) for bounds checking under
+// Host build of the DEVICE one-lane BPG walks (bpg.h bpg_find_dev<W>, bpg_walk1) for bounds checking under
 // AddressSanitizer (GPU ASan is not available): every program in its own exact-size allocation,
 // the text padded as the engine pads it (ops/kernels.py padded_len), each (program, line) walked
 // by bpg_find_dev<W> and by the host twin bpg_find_w<W>; prints the number of disagreements.
@@ -17,6 +17,7 @@
 #define __restrict__
 #define LP_HD inline
 #define __HIP__ 1
+#define __ballot(x) ((unsigned long long)((x) ? 1 : 0))   // one lane: the wave is this lane
 struct uint4 {
   uint32_t x, y, z, w;
 };
@@ -86,10 +87,12 @@ int main(int argc, char** argv) {
       const int n = (int)lw[2 + 2 * x];
       const bool d = walk(progs[i], s, n);
       const bool h = lp::bpg_find_host(progs[i], s, n);
+      const bool l = W == 1 ? lp::bpg_walk1<const uint64_t*>(progs[i], s, n, true) : h;
       ++walks;
       hits += h;
-      if (d != h) {
-        if (bad < 10) std::printf("mismatch prog %lu line %ld: dev %d host %d\n", (unsigned long)i, (long)x, d, h);
+      if (d != h || l != h) {
+        if (bad < 10)
+          std::printf("mismatch prog %lu line %ld: dev %d lean %d host %d\n", (unsigned long)i, (long)x, d, l, h);
         ++bad;
       }
     }

@@ -281,6 +281,7 @@ struct HitsArgs {
   // outputs (capacity n; hit_off R+1)
   int64_t* hits; int32_t* hit_line; int64_t* hit_off; int64_t* ev_cnt; int64_t* ev_end;
   int64_t* counters;         // [0] unique verified hits, [1] events
+  bool cand_verified = false;  // small path: the caller ran cand_verify_all_dev already
 };
 
 struct EventsArgs {

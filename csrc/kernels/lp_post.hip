@@ -596,7 +596,8 @@ void feat_cov_dev(const int32_t* cov, int64_t L, const uint8_t* text, const int6
 size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
   if (hits_small_ok(A)) {          // a request: verify on the grid, the rest in one workgroup
-    if (!cand_verify_all_dev(const_cast<int64_t*>(A.cand), A.pre_from, A.dcount, A.text, A.ls, A.ll, A.dfa, stream)) {
+    if (!A.cand_verified &&
+        !cand_verify_all_dev(const_cast<int64_t*>(A.cand), A.pre_from, A.dcount, A.text, A.ls, A.ll, A.dfa, stream)) {
       hipLaunchKernelGGL(k_cand_verify, dim3(nblk(A.pre_from)), dim3(256), 0, pstream(stream), A);
       bpg_cand_dev(const_cast<int64_t*>(A.cand), A.pre_from, A.dcount, A.text, A.ls, A.ll, A.dfa, stream);
     }

@@ -63,9 +63,19 @@ RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
   publish_ = true;
   fetch_ = true;
   evict_in_fetch_ = false;
+  const char* e = std::getenv("LP_RUNNER_SIDE_SCAN");   // (A/B: 0 = scans on the caller's stream)
+  side_on_ = !(e && e[0] == '0');
+  if (side_on_) {
+    check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "side stream");
+    check(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "fork event");
+    check(hipEventCreateWithFlags(&join_, hipEventDisableTiming), "join event");
+  }
 }
 
 RequestRunner::~RequestRunner() {
+  if (fork_) (void)hipEventDestroy(fork_);
+  if (join_) (void)hipEventDestroy(join_);
+  if (side_) (void)hipStreamDestroy(side_);
   if (carry_host_) (void)hipHostFree(carry_host_);
   if (ws_) (void)hipFree(ws_);
   if (post_ws_) (void)hipFree(post_ws_);
@@ -320,15 +330,30 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     ev.nseg = D;
     unsigned long long* c0 = reinterpret_cast<unsigned long long*>(cnt);
 
-    // matchers: literal-free scan groups, single-DFA scans, then the literal prefilter chain
+    // matchers: literal-free scan groups and single-DFA scans (on the side stream when there is
+    // one: they overlap the literal chain and the candidate verification), then the literal
+    // prefilter chain
+    const bool side = side_on_ && (!S_.scans.empty() || S_.n_scan_regs);
+    const uint64_t sst = side ? reinterpret_cast<uint64_t>(side_) : stream;
+    if (side) {
+      check(hipEventRecord(fork_, st), "fork");
+      check(hipStreamWaitEvent(side_, fork_, 0), "fork wait");
+    }
     for (size_t i = 0; i < S_.scans.size(); ++i)
-      scan_multi_dev(text, nbytes, ls, ll, L, S_.scans[i], ver, cap_v, c0 + 2, S_.scan_grids[i], stream);
+      scan_multi_dev(text, nbytes, ls, ll, L, S_.scans[i], ver, cap_v, c0 + 2, S_.scan_grids[i], sst);
     if (S_.n_scan_regs)
-      scan_dev(text, ls, ll, L, S_.scan_regs, S_.n_scan_regs, S_.dfa, ver, cap_v, c0 + 2, stream);
+      scan_dev(text, ls, ll, L, S_.scan_regs, S_.n_scan_regs, S_.dfa, ver, cap_v, c0 + 2, sst);
+    if (side) check(hipEventRecord(join_, side_), "join");
     blk_index_dev(ls, L, nblk, blk, stream);
     prefilter_dev(text, nbytes, S_.pf, ls, L, gh, cap_g, c0, S_.pf_grid, stream);
     pf_verify_dev(gh, cap_g, text, nbytes, S_.pf, ls, L, blk, cand, cap_c, c0 + 1, stream, c0,
                   (int)std::max<int64_t>(16, std::min<int64_t>(8192, nbytes >> 13)));
+    // the prefilter candidates' verification does not read the scans' buffer: it runs before the join
+    bool verified = false;
+    if (side && fast && n <= request_event_cap())
+      verified = cand_verify_all_dev(cand, cap_c, reinterpret_cast<unsigned long long*>(c0 + 1), text, ls, ll, S_.dfa,
+                                     stream);
+    if (side) check(hipStreamWaitEvent(st, join_, 0), "join wait");
 
     if (S_.host_dev)   // the relaxed automata's keys: candidates only, decided by the host side path
       take_host_dev(cand, c0 + 1, cap_c, ver, c0 + 2, cap_v, text, ls, ll, S_.dfa, HostSideOut{}, stream);
@@ -350,6 +375,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     A.text = text; A.ls = ls; A.ll = ll; A.dfa = S_.dfa; A.ev = ev;
     A.hits = hits; A.hit_line = hit_line; A.hit_off = hit_off; A.ev_cnt = ev_cnt; A.ev_end = ev_end;
     A.counters = cnt + 3;
+    A.cand_verified = verified;
     size_t need = hits_dev(A, post_ws_, post_cap_, stream);
     if (need > post_cap_) {       // post_ws_ is not used by anything in flight yet
       if (fast) throw std::runtime_error("request runner: hit workspace on the small path");

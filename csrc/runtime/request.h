@@ -175,6 +175,11 @@ class RequestRunner {
   bool recorded_ = false;
   int64_t* carry_host_ = nullptr;      // host window: the section's carry (pinned, device-visible)
   int64_t* carry_dev_ = nullptr;
+  // literal-free scans on a second stream of the device, beside the literal chain and the
+  // candidate verification (fork after the inputs, join before the hit pipeline)
+  hipStream_t side_ = nullptr;
+  hipEvent_t fork_ = nullptr, join_ = nullptr;
+  bool side_on_ = true;
 };
 
 }  // namespace lp

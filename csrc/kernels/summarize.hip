@@ -335,7 +335,10 @@ __global__ __launch_bounds__(256) void k_rescore(const int64_t* __restrict__ gl,
 }
 
 namespace {
-bool g_summ_select = true;
+// off by default: on the bench step's 45k events the selection path measured 63.5 (k_sel_hist: its
+// global bin atomics collide -- equal scores share a bin) + 13.5 + 5 + 8.6 us against ~63 us for
+// the three chunk-sort levels (profiles/r5_c/bench_kernels.txt vs profiles/r4_e)
+bool g_summ_select = false;
 }  // namespace
 bool summ_select() { return g_summ_select; }
 void set_summ_select(bool on) { g_summ_select = on; }

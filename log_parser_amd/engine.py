@@ -370,6 +370,7 @@ class Engine:
         self._stage_pool = StagePool(pinned=self.device.type == "cuda", initial=K.padded_len(1 << 20))
         # second compute stream: literal-free scans overlap the prefilter chain (K.match_and_hits)
         self._side = None
+        self._pf_stream = None
         self._host_side = None                      # ops.side_path.HostSide (device-fed backtracker regexes)
         self._runner = None                         # N.RequestRunner (built on first use) / False
         if self.device.type == "cuda":
@@ -378,6 +379,9 @@ class Engine:
             self.pf_grid = self.n_cus * 4
             if bool(self.config.get("engine.scan-stream", True)):
                 self._side = (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
+            # the early literal prefilter's own stream (prefilter_early)
+            if bool(self.config.get("engine.prefilter-stream", True)):
+                self._pf_stream = torch.cuda.Stream(self.device)
         else:
             self.n_cus = 1
             self.pf_grid = 1
@@ -517,7 +521,7 @@ class Engine:
         ``fuses_line_index``)."""
         if not text.is_cuda or self.profile:
             return None
-        return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid, nlp)
+        return K.EarlyPrefilter(text, nbytes, self.tabs, self.arena, self.pf_grid, nlp, stream=self._pf_stream)
 
     def fuses_line_index(self, text) -> bool:
         """The bulk step folds the line index's first pass into the literal prefilter (one read of the

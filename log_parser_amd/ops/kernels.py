@@ -434,13 +434,29 @@ class EarlyPrefilter:
     """The literal prefilter launched before the line index is known on the host (it reads only
     the text): gram hits + the arena counters, handed to ``match_and_hits``."""
 
-    def __init__(self, text, nbytes: int, tabs: dict, arena: "MatchArena", pf_grid: int, nlp=None):
+    def __init__(self, text, nbytes: int, tabs: dict, arena: "MatchArena", pf_grid: int, nlp=None,
+                 stream: Optional["torch.cuda.Stream"] = None):
         L_est = int(nbytes * _LINES_PER_BYTE[0]) + 1
         self.cap = arena.caps(L_est)["gram"]
         self.gh = torch.empty(self.cap, dtype=torch.int64, device=text.device)
         self.cnt = torch.zeros(7, dtype=torch.int64, device=text.device)
+        self.done = None
+        st = _s(text)
+        if stream is not None and nlp is None and text.is_cuda:
+            # on its own stream: the rest of the line index (line starts / lengths, after the host's
+            # line-count read) and the literal-free scans run beside it; match_and_hits waits for
+            # `done` before the candidates' verification (config 2: the chains overlap)
+            fork = torch.cuda.Event()
+            fork.record(torch.cuda.current_stream(text.device))
+            stream.wait_event(fork)
+            st = stream.cuda_stream
+            for t in (self.gh, self.cnt, text):
+                t.record_stream(stream)
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
-                        pf_grid, _s(text), nlp)
+                        pf_grid, st, nlp)
+        if st != _s(text):
+            self.done = torch.cuda.Event()
+            self.done.record(stream)
 
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,
@@ -477,9 +493,11 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
     for attempt in range(8):         # each overflow learns the exact rates: one re-run is the rule
         cap = arena.caps(L)
         cap["ver"] += ninj
+        early_done = None
         if early is not None:            # prefilter already queued (behind the line index)
             cap["gram"] = early.cap
             gh, cnt = early.gh, early.cnt
+            early_done = early.done
         else:
             gh = torch.empty(cap["gram"], dtype=torch.int64, device=dev)
             # [gram hits, candidates, verified hits] then [unique hits, events] (post_hits counters),
@@ -514,6 +532,8 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L, gh.data_ptr(), cap["gram"],
                             c0, pf_grid, st)
         early = None                     # an overflow re-run launches everything itself
+        if early_done is not None:       # the early prefilter ran on its own stream
+            torch.cuda.current_stream(dev).wait_event(early_done)
         N.pf_verify_dev(gh.data_ptr(), cap["gram"], text.data_ptr(), nbytes, tabs["pf"], line_start.data_ptr(), L,
                         blk.data_ptr(), cand.data_ptr(), cap["cand"], c0 + 8, st, c0,
                         max(16, min(8192, nbytes >> 13)))

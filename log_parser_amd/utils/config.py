@@ -63,6 +63,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # (off: the cross-stream event wait cost more than the overlap saved -- 10k-line request
     # 0.362 -> 0.382-0.408 ms on the MI355X box, tools/engine_phases.py A/B)
     "engine.scan-stream": (False, bool),
+    # bulk / document steps: the early literal prefilter on its own HIP stream, beside the rest of
+    # the line index and the literal-free scans (prefilter_early; config 2's chains overlap)
+    "engine.prefilter-stream": (True, bool),
     # bulk steps: fold the line index's first pass into the literal prefilter (one read of the text
     # fewer; opt-in until a GPU A/B is in)
     "engine.fused-line-index": (False, bool),

@@ -95,10 +95,18 @@ def test_rescore_matches_reference_order():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("select", [False, True])
 @pytest.mark.parametrize("n,k", CASES)
-def test_summarize_gpu_equals_cpu(gpu_device, n, k):
+def test_summarize_gpu_equals_cpu(gpu_device, n, k, select):
+    """Both device top-k paths: the chunk-sort levels (default) and the threshold selection
+    (summarize.hip k_sel_*, N.set_summ_select)."""
+    from log_parser_amd.native import N
     score, line, pat, sev_index = _events(n, 61, 4, seed=n + k)
-    got = _run(gpu_device, score, line, pat, sev_index, k, 61, 4, 77)
+    N.set_summ_select(select)
+    try:
+        got = _run(gpu_device, score, line, pat, sev_index, k, 61, 4, 77)
+    finally:
+        N.set_summ_select(False)
     ref = _ref(score, line, pat, 77, k, sev_index, 61, 4)
     for g, r in zip(got, ref):
         np.testing.assert_array_equal(g, r)

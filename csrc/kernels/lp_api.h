@@ -304,11 +304,16 @@ struct EventsArgs {
   int64_t* freq_counts;      // [nkeys]
   uint8_t* feat;             // [L] context features (nullptr: coverage only)
   int32_t* cov;              // [L] optional: window coverage out
+  bool feat_ready = false;   // feat already holds every line's features (feat_all_dev): skip them
 };
 
 int bits_for(int64_t n);
 // device versions return the workspace bytes they need; they only run when ws_bytes suffices
 size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
+// context features of EVERY line (k_feat_cov without a coverage filter): the request runner computes
+// them on its side stream while the matchers run, so the event stage needs no feature pass
+void feat_all_dev(int64_t L, const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P,
+                  int ctx_trans, int ctx_acc, uint8_t* feat, uint64_t stream);
 size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
 // capacities of the single-workgroup request path (events, lines): a batch within them can run
 // the event stage in device-count mode

@@ -302,8 +302,8 @@ __global__ __launch_bounds__(256) void k_feat_cov(const int32_t* __restrict__ co
   const int64_t base = (int64_t)blockIdx.x * per_block;
   for (int k = threadIdx.x; k < per_block; k += blockDim.x) {
     const int64_t x = base + k;
-    if (x < L) {
-      if (cov[x] > 0) list[atomicAdd(&n, 1)] = (uint16_t)k;
+    if (x < L) {                                 // (no coverage array: every line)
+      if (!cov || cov[x] > 0) list[atomicAdd(&n, 1)] = (uint16_t)k;
       else feat[x] = 0;
     }
   }
@@ -582,6 +582,11 @@ void dedupe_verify_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t
   LP_PCHECK(hipGetLastError());
 }
 
+void feat_all_dev(int64_t L, const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P,
+                  int ctx_trans, int ctx_acc, uint8_t* feat, uint64_t stream) {
+  feat_cov_dev(nullptr, L, text, ls, ll, P, ctx_trans, ctx_acc, feat, stream);
+}
+
 void feat_cov_dev(const int32_t* cov, int64_t L, const uint8_t* text, const int64_t* ls, const int32_t* ll,
                   const DfaPool& P, int ctx_trans, int ctx_acc, uint8_t* feat, uint64_t stream) {
   if (L <= 0 || !feat) return;
@@ -670,7 +675,7 @@ size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t strea
     if (!A.cov && (!ws || D.used > ws_bytes)) return D.used;
     hipLaunchKernelGGL(k_events_small, dim3(1), dim3(SB_THREADS), 0, pstream(stream), A, cov_s);
     LP_PCHECK(hipGetLastError());
-    if (L > 0 && A.feat) {
+    if (L > 0 && A.feat && !A.feat_ready) {
       int per = (int)std::min<int64_t>(FC_MAX_LINES, std::max<int64_t>(256, L / 1024));
       per = (per + 255) / 256 * 256;
       hipLaunchKernelGGL(k_feat_cov, dim3(nblk(L, per)), dim3(256), 0, pstream(stream), cov_s, L, per, A.text, A.ls,

@@ -828,7 +828,7 @@ size_t events_bulk_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t 
     if (nk > 0) PB_CHECK(hipMemsetAsync(A.freq_counts, 0, (size_t)nk * sizeof(int64_t), st));
     if (A.ne_fit) PB_CHECK(hipMemsetAsync(A.ne_fit, 0, sizeof(int64_t), st));
   }
-  if (A.feat) feat_cov_dev(cov, L, A.text, A.ls, A.ll, A.dfa, A.ctx_trans, A.ctx_acc, A.feat, stream);
+  if (A.feat && !A.feat_ready) feat_cov_dev(cov, L, A.text, A.ls, A.ll, A.dfa, A.ctx_trans, A.ctx_acc, A.feat, stream);
   return C.used;
 }
 

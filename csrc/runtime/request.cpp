@@ -221,6 +221,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   int64_t *ev_rank = nullptr, *ev_fkey = nullptr;
   EvTables ev = S_.ev;
   bool done = false;   // events + score already ran (device-count mode)
+  bool feat_ready = false;   // every line's features computed on the side stream (this attempt)
   auto carve_events = [&](int64_t E) {
     out = dev(20 * (size_t)E + 8 * (size_t)K1);
     ev_rank = reinterpret_cast<int64_t*>(dev(8 * (size_t)std::max<int64_t>(E, 1)));
@@ -255,6 +256,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     A.lbits = lbits; A.ev = ev; A.text = text; A.ls = ls; A.ll = ll; A.dfa = S_.dfa;
     A.ev_line = ev_line; A.ev_pat = ev_pat; A.ev_seg = ev_seg; A.ev_rank = ev_rank; A.ev_fkey = ev_fkey;
     A.freq_counts = freq_counts; A.feat = feat; A.cov = nullptr; A.dcounts = dcnt;
+    A.feat_ready = feat_ready;
     const size_t need = events_dev(A, post_ws_, post_cap_, stream);
     if (need > post_cap_) {
       if (dcnt) throw std::runtime_error("request runner: event workspace not pre-sized");
@@ -333,7 +335,10 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     // matchers: literal-free scan groups and single-DFA scans (on the side stream when there is
     // one: they overlap the literal chain and the candidate verification), then the literal
     // prefilter chain
-    const bool side = side_on_ && (!S_.scans.empty() || S_.n_scan_regs);
+    // fast (request-sized) batches also compute every line's context features there, so the event
+    // stage needs no feature pass (k_feat_cov over the covered lines sat on the critical path)
+    const bool side = side_on_ && (!S_.scans.empty() || S_.n_scan_regs || (fast && L > 0));
+    const bool feat_side = side && fast && L > 0;
     const uint64_t sst = side ? reinterpret_cast<uint64_t>(side_) : stream;
     if (side) {
       check(hipEventRecord(fork_, st), "fork");
@@ -343,6 +348,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       scan_multi_dev(text, nbytes, ls, ll, L, S_.scans[i], ver, cap_v, c0 + 2, S_.scan_grids[i], sst);
     if (S_.n_scan_regs)
       scan_dev(text, ls, ll, L, S_.scan_regs, S_.n_scan_regs, S_.dfa, ver, cap_v, c0 + 2, sst);
+    if (feat_side) feat_all_dev(L, text, ls, ll, S_.dfa, S_.ctx_trans, S_.ctx_acc, feat, sst);
     if (side) check(hipEventRecord(join_, side_), "join");
     blk_index_dev(ls, L, nblk, blk, stream);
     prefilter_dev(text, nbytes, S_.pf, ls, L, gh, cap_g, c0, S_.pf_grid, stream);
@@ -354,6 +360,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       verified = cand_verify_all_dev(cand, cap_c, reinterpret_cast<unsigned long long*>(c0 + 1), text, ls, ll, S_.dfa,
                                      stream);
     if (side) check(hipStreamWaitEvent(st, join_, 0), "join wait");
+    feat_ready = feat_side;
 
     if (S_.host_dev)   // the relaxed automata's keys: candidates only, decided by the host side path
       take_host_dev(cand, c0 + 1, cap_c, ver, c0 + 2, cap_v, text, ls, ll, S_.dfa, HostSideOut{}, stream);

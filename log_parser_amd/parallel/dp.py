@@ -207,10 +207,9 @@ class ShardedAnalyzer:
             box = []
             if eng.fuses_line_index(text):      # the prefilter's read of the text also counts the lines
                 ls, ll = K.split_lines(text, nbytes, fused=lambda nlp: box.append(eng.prefilter_early(text, nbytes, nlp)))
+                early = box[0] if box else None
             else:
-                ls, ll = K.split_lines(text, nbytes, before_read=(lambda: box.append(eng.prefilter_early(text, nbytes)))
-                                       if text.is_cuda else None)
-            early = box[0] if box else None
+                ls, ll, early = eng.split_with_prefilter(text, nbytes)
         defer = eng.can_defer(text)
         for attempt in range(4):
             out, prep, veto = self._step(text, nbytes, ls, ll, halo_left, halo_right, topk,

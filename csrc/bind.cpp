@@ -231,22 +231,6 @@ class SideWorker {
     std::lock_guard<std::mutex> lk(mu_);
     if (error_.empty()) error_ = why;
   }
-  // wait for a region's export: spin briefly, then nap; give up after 5 s (the GPU's own wait ends
-  // at 2 s: the batch then overflows and re-runs)
-  static bool wait_export(const int64_t* seqw, int64_t seq) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (int it = 0;; ++it) {
-      if (load_acq(seqw) == seq) return true;
-      if (it < 4096) {
-#if defined(__x86_64__)
-        __builtin_ia32_pause();
-#endif
-        continue;
-      }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return false;
-      std::this_thread::sleep_for(std::chrono::microseconds(10));
-    }
-  }
   // verify region `out` (n <= cap keys) into inb[base..]; returns the verified count
   int64_t verify(const Job& j, const int64_t* out, int64_t n, int64_t base) {
     const int64_t c = j.cap;
@@ -270,17 +254,42 @@ class SideWorker {
       }
     return r;
   }
+  // the job's next region to verify: whichever published export comes first (the scan engines'
+  // region B is exported as soon as the scans end, often before the literal chain's region A);
+  // -1 when none arrives within 5 s
+  int next_region(const Job& j, bool (&seen)[2]) {
+    // spin (pause) for the first 50 ms: the exports come ~1-2 ms into a step, and a sleeping
+    // poll wakes up to ~60 us late (timer slack) -- each late wake-up sat on the GPU's k_wait_host
+    const int64_t c = j.cap;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int it = 0;; ++it) {
+      for (int q = 0; q < 2; ++q)
+        if (!seen[q] && j.out[q] && load_acq(j.out[q] + 3 * c + 1) == j.seq) return q;
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt < std::chrono::milliseconds(50)) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+        continue;
+      }
+      if (dt > std::chrono::seconds(5)) return -1;
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
+    }
+  }
   void run(const Job& j) {
     const int64_t c = j.cap;
     int64_t res = 0;
-    for (int q = 0; q < 2 && res >= 0; ++q) {
-      const int64_t* out = j.out[q];
-      if (!out) continue;
-      if (!wait_export(out + 3 * c + 1, j.seq)) {
+    bool seen[2] = {j.out[0] == nullptr, j.out[1] == nullptr};
+    for (int k = 0; k < 2 && res >= 0; ++k) {
+      if (seen[0] && seen[1]) break;
+      const int q = next_region(j, seen);
+      if (q < 0) {
         fail("side path: no export for batch " + std::to_string(j.seq) + " within 5 s");
         res = -1;
         break;
       }
+      seen[q] = true;
+      const int64_t* out = j.out[q];
       const int64_t n = load_acq(out + 3 * c);
       if (n > c) {                           // re-run with a larger buffer (the batch overflows)
         need_.store(std::max(need_.load(), n));

@@ -524,6 +524,9 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
             if glist.numel():
                 N.nfa(tabs["nfa_tables"].data_ptr(), glist.data_ptr(), glist.numel(), ncls, 0, L, text.data_ptr(),
                       line_start.data_ptr(), line_len.data_ptr(), 0, ver.data_ptr(), cap["ver"], c0 + 16, sst, True)
+        if host_side is not None:          # region B: the scans' relaxation keys leave as the scans end
+            host_side[0].begin(host_side[1])
+            host_side[0].export_scan(ver, c0 + 16, cap["ver"], text, line_start, line_len, tabs["dfa"], sst)
         if sst != st:
             side[2].record(side[0])
         elif tick:
@@ -539,13 +542,12 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
                         max(16, min(8192, nbytes >> 13)))
         if tick:
             tick("prefilter")
-        if host_side is not None:          # region A: the candidates go to the host during the scans
-            host_side[0].export_candidates(cand, c0 + 8, cap["cand"], text, line_start, line_len, tabs["dfa"], st,
-                                           host_side[1])
+        if host_side is not None:          # region A: the prefilter candidates, right after the literal chain
+            host_side[0].export_candidates(cand, c0 + 8, cap["cand"], text, line_start, line_len, tabs["dfa"], st)
         if sst != st:
             torch.cuda.current_stream(dev).wait_event(side[2])
-        if host_side is not None:          # region B (scan keys) -> host backtracker -> append, all queued
-            host_side[0].export_scan_and_wait(ver, c0 + 16, cap["ver"], text, line_start, line_len, tabs["dfa"], st)
+        if host_side is not None:          # host backtracker answers for both regions -> append, all queued
+            host_side[0].wait(ver, c0 + 16, cap["ver"], st)
         elif tabs.get("host_dev"):         # relaxation keys of regexes the host side path decided
             N.take_host(cand.data_ptr(), c0 + 8, cap["cand"], ver.data_ptr(), c0 + 16, cap["ver"], text.data_ptr(),
                         line_start.data_ptr(), line_len.data_ptr(), tabs["dfa"], None, st)

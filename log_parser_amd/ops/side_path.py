@@ -66,28 +66,35 @@ class HostSide:
         cnt = self.cnt.data_ptr() + 16 * k
         return (d, d + 8 * c, d + 16 * c, c, cnt, cnt + 8, d + 24 * c, d + 24 * c + 8, self.seq)
 
-    def export_candidates(self, cand, n1d: int, cap1: int, text, ls, ll, dfa, stream: int,
-                          host_text: np.ndarray) -> None:
-        """Region A, queued right after the literal chain: the prefilter candidates of relaxed
-        regexes leave the candidate buffer for the host, which verifies them while the GPU runs the
-        rest of the matchers. host_text: the batch's bytes on the host (``ls`` offsets index it),
-        read by the worker until it publishes (the step's end-of-step read comes after that)."""
+    def begin(self, host_text: np.ndarray) -> None:
+        """A new job (one attempt of a step): buffers sized for the worker's last request, a new
+        sequence number, the worker told where the step's host bytes are (``ls`` offsets index them;
+        it reads them until it publishes, and the step's end-of-step read comes after that)."""
         need = self.need
         if need > self.cap:                        # (the previous attempt's buffers are idle)
             self._alloc(max(need * 5 // 4, 2 * self.cap))
             self._worker.clear_need()
         self.seq += 1
-        N.take_host(cand.data_ptr(), n1d, cap1, 0, 0, 0, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
-                    self._out(self.out_a, 0), stream)
         ht = np.ascontiguousarray(host_text)
         self._hold = (self._hold + [ht])[-4:]
         self._worker.submit(self.seq, ht.ctypes.data, self.cap, self.out_a.h, self.out_b.h, self.inb.h)
 
-    def export_scan_and_wait(self, ver, n2d: int, cap2: int, text, ls, ll, dfa, stream: int) -> None:
-        """Region B (the scan engines' relaxation keys, after the scans joined), then k_wait_host:
-        the verified keys of both regions are appended to the verified-hit buffer."""
+    def export_scan(self, ver, n2d: int, cap2: int, text, ls, ll, dfa, stream: int) -> None:
+        """Region B, queued on the scans' stream as soon as they end: the scan engines' keys of
+        relaxed regexes go to the host, which verifies them while the literal chain still runs."""
         N.take_host(0, 0, 0, ver.data_ptr(), n2d, cap2, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
                     self._out(self.out_b, 1), stream)
+
+    def export_candidates(self, cand, n1d: int, cap1: int, text, ls, ll, dfa, stream: int) -> None:
+        """Region A, queued right after the literal chain: the prefilter candidates of relaxed
+        regexes leave the candidate buffer for the host (the worker verifies the regions in the
+        order their exports arrive)."""
+        N.take_host(cand.data_ptr(), n1d, cap1, 0, 0, 0, text.data_ptr(), ls.data_ptr(), ll.data_ptr(), dfa,
+                    self._out(self.out_a, 0), stream)
+
+    def wait(self, ver, n2d: int, cap2: int, stream: int) -> None:
+        """k_wait_host, queued after both exports (and after the scans joined): the verified keys of
+        both regions are appended to the verified-hit buffer."""
         c, i = self.cap, self.inb.d
         N.wait_host(ver.data_ptr(), cap2, n2d, (i, i + 8 * c, i + 8 * c + 8, c, self.seq, i + 8 * c + 16), stream)
 

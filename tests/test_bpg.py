@@ -329,3 +329,22 @@ def test_counted_repeats_gpu_walks_match_host(gpu_device, gap):
     for before, after in zip(cand, got):
         r, j = before >> 32, before & 0xFFFFFFFF
         assert (after >= 0) == N.bpg_find(progs[r], lines[j].encode()), (lib.regexes[r].pattern, len(lines[j]))
+
+
+def test_lean_device_walk_bounds_and_parity_under_asan():
+    """The DEVICE one-lane walks (bpg.h bpg_find_dev<W> and the lean one-word bpg_walk1) built for
+    the host with AddressSanitizer (GPU ASan is unavailable): every program of the Java-shape test
+    library plus Unicode / boundary-context / counted-repeat shapes in exact-size allocations, over
+    padded text with non-ASCII code points and terminators -- no out-of-bounds read, and the same
+    answer as the host twin bpg_find_w on every (program, line)."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "bpg_walk_check.py"), "--seed", "5", "--quick"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "mismatches 0" in r.stdout

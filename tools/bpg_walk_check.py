@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-asan", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="one document and 200 random lines (the CPU test)")
     a = ap.parse_args()
     from test_java_shapes import _docs, _shape_library  # noqa: E402
 
@@ -30,13 +31,13 @@ def main():
     import random
     sets, trig = _shape_library(a.seed)
     lib = CompiledLibrary(sets, ScoringParams())
-    docs = _docs(trig, a.seed)
+    docs = _docs(trig, a.seed)[:1] if a.quick else _docs(trig, a.seed)
     rng = random.Random(a.seed)
     # Unicode / boundary-context shapes as code-point programs, counted repeats, random lines full of
     # non-ASCII code points and terminators next to the documents' lines
     extra = UNI_PATS + VERDICT_SHAPES + [r"X.{0,100}Y", r"a[^\n]{0,40}FATAL", r"(?i)(err|warn).{0,30}x",
                                          r"x{2,40}", r"(?m)^ab.{0,20}c$", r"\bqq.{0,25}zz\b"]
-    rand = ["".join(rng.choice(ALPHA + "XYxqz") for _ in range(rng.randint(0, 60))) for _ in range(600)]
+    rand = ["".join(rng.choice(ALPHA + "XYxqz") for _ in range(rng.randint(0, 60))) for _ in range(200 if a.quick else 600)]
     docs = docs + ["\n".join(rand) + "\n"]
     data = "".join(docs).encode("utf-8", errors="surrogatepass")
     lines = golden.split_lines("".join(docs))

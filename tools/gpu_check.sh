@@ -11,6 +11,7 @@
 #   reqtrace  one 10k-line request: wall p50 + kernel timeline, library with / without Java shapes
 #   splitverify  request path with the DFA / BPG candidate verification split, one BPG walk's cost
 #   prof    kernel table of the bench step (rocprofv3 kernel trace, serialised ingest)
+#   pmcbpg  PMC counters of one lean BPG walk (two passes)
 #   pmcscan PMC counters of the scan walk and prefilter (two counter passes)
 #   httpreps  config 5, 1 and 2 processes, 5 runs each: stage / connection timelines, thread states
 #   full    round-end rehearsal: the whole GPU suite, smoke(), the bench
@@ -96,6 +97,15 @@ for s in $steps; do
       run pmc3 180 rocprofv3 --pmc $P3 --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan/p3 \
         -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
       run pmcsum 120 python3 tools/pmc_summary.py gpurun_out/pmc_scan ;;
+    pmcbpg)
+      # PMC of ONE lean BPG walk (tools/bpg_probe.py, 512-byte line): instructions and waits per walk
+      cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+      run pmcbpg1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+        SQ_WAIT_INST_ANY SQ_WAIT_ANY --kernel-include-regex "k_bpg_dedupe_all" -d gpurun_out/pmc_bpg/p1 -o run \
+        --output-format csv -- python3 tools/bpg_probe.py --lens 512 --reps 3
+      run pmcbpg2 120 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU \
+        SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH --kernel-include-regex "k_bpg_dedupe_all" \
+        -d gpurun_out/pmc_bpg/p2 -o run --output-format csv -- python3 tools/bpg_probe.py --lens 512 --reps 3 ;;
     httpreps)
       # config 5, 1 and 2 serving processes, 5 runs each: stage + per-connection timelines and the
       # serving threads' states sampled every 1 ms (run-to-run spread, the slow mode's cause)

@@ -409,18 +409,21 @@ __global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
   const bool dc = A.dcount != nullptr;
   const int64_t n1 = dc ? (int64_t)min((unsigned long long)A.pre_from, A.dcount[0]) : A.pre_from;
   const int64_t n2 = dc ? (int64_t)min((unsigned long long)(n - A.pre_from), A.dcount[1]) : n - A.pre_from;
-  // the used entries of both regions, packed: the sort covers pow2(used), not the capacities
-  const int np = sb_pow2(n1 + n2);
-  for (int i = threadIdx.x; i < np; i += SB_THREADS) {
-    uint64_t key = LP_PAD_KEY;
-    if (i < n1 + n2) {
-      const bool pre = i >= n1;
-      const int64_t k = pre ? (dc ? A.cand2[i - n1] : A.cand[A.pre_from + i - n1]) : A.cand[i];
-      if (k >= 0)                   // -1: failed k_cand_verify; every other key counts as verified
-        key = (((((uint64_t)k >> 32) << A.lbits) | ((uint64_t)k & 0xFFFFFFFFull)) << 1) | 1ull;
-    }
-    keys[i] = key;
+  // the live entries of both regions, compacted (most prefilter candidates failed their verify and
+  // are -1): the sort covers pow2(live), not pow2(used) or the capacities
+  __shared__ int s_live;
+  if (threadIdx.x == 0) s_live = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n1 + n2; i += SB_THREADS) {
+    const bool pre = i >= n1;
+    const int64_t k = pre ? (dc ? A.cand2[i - n1] : A.cand[A.pre_from + i - n1]) : A.cand[i];
+    if (k >= 0)                     // -1: failed k_cand_verify; every other key counts as verified
+      keys[atomicAdd(&s_live, 1)] = (((((uint64_t)k >> 32) << A.lbits) | ((uint64_t)k & 0xFFFFFFFFull)) << 1) | 1ull;
   }
+  __syncthreads();
+  const int live = s_live;
+  const int np = sb_pow2(live);
+  for (int i = live + threadIdx.x; i < np; i += SB_THREADS) keys[i] = LP_PAD_KEY;
   __syncthreads();
   sb_sort(keys, np);
   // dedupe + DFA verify, then compaction in sorted order: 4 consecutive keys per thread

@@ -479,7 +479,11 @@ __device__ __forceinline__ int bpg_cp_class_p(PT P, int o, int nr, uint32_t cp, 
 // part in the ballots and walks nothing (P must still point at readable program words).
 // PT: pointer to the program's words -- LDS (ds_read) when the pool is staged, else global.
 template <typename PT>
-__device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, int n, bool valid) {
+__device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, int n, bool valid, int prevk0 = 0,
+                                          int inj_end = 0x7FFFFFFF) {
+  // (split walks: `prevk0` = previous kind before s[0] -- a walk of a line's second part; `inj_end`:
+  // no thread starts at or after that position, and the walk stops once no thread is alive past it
+  // -- the first part. The two parts' results OR to the whole line's: every thread starts in one.)
   const uint64_t h = P[0];
   const int E = valid ? (int)((h >> 8) & 0xFFF) : 0;
   const int ncls = (int)((h >> 20) & 0x3FF);
@@ -523,7 +527,7 @@ __device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, i
   uint64_t S = 0, acc = 0, Sft = 0;
   uint32_t nullhit = 0;
   int ftctx = 0;
-  int prevk = 0;                                           // P_BOS
+  int prevk = prevk0;                                      // P_BOS, or the split point's
   const int sh = (int)((uintptr_t)s & 15);
   const uint4* blk = reinterpret_cast<const uint4*>(s - sh);
   uint4 cur = n > 0 ? blk[0] : make_uint4(0, 0, 0, 0);
@@ -561,7 +565,7 @@ __device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, i
         ctxq[j] = ctx;
         onm |= on ? 1u << j : 0u;
         Cq[j] = on ? P[oC + k] : 0ull;
-        Fq[j] = P[oF + ctx];
+        Fq[j] = t < inj_end ? P[oF + ctx] : 0ull;
         Lq[j] = P[oL + ctx];
         if (wft && on && t == ft) ftctx = pk * 6 + 1;
         pk = on ? prev_of(nk) : pk;
@@ -588,7 +592,7 @@ __device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, i
         ctxq[j] = ctx;
         onm |= on ? 1u << j : 0u;
         Cq[j] = on ? P[oC + k] : 0ull;
-        Fq[j] = P[oF + ctx];
+        Fq[j] = t < inj_end ? P[oF + ctx] : 0ull;
         Lq[j] = P[oL + ctx];
         if (wft && on && t == ft) ftctx = pk * 6 + 1;
         pk = on ? prev_of(nk) : pk;
@@ -605,7 +609,7 @@ __device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, i
     acc |= S & (CTX ? Lq[j] : l0) & ~keep;               /* accept before this character */        \
     if (CTX) nullhit |= on ? (nullm >> ctx) & 1u : 0u;                                             \
     if (wft) Sft = (on && b0 + j - sh == ft) ? S : Sft;                                            \
-    uint64_t F = ((S & shm) << 1) | (S & selfm) | (CTX ? Fq[j] : f0);                              \
+    uint64_t F = ((S & shm) << 1) | (S & selfm) | (CTX ? Fq[j] : (b0 + j - sh < inj_end ? f0 : 0ull)); \
     const uint64_t df = (S & src) | hi;                                                            \
     F |= R & ~((df - lo) ^ df);                          /* spread fields: one word, no borrow */   \
     if (EXC) {                                                                                     \
@@ -643,7 +647,8 @@ __device__ __forceinline__ bool bpg_walk1(PT P, const uint8_t* __restrict__ s, i
 #undef LP_W1_CHAIN
     prevk = pk;
     cur = nxt;
-    const bool fin = !live || acc != 0 || nullhit != 0 || b0 + 16 >= sh + n;
+    const bool fin = !live || acc != 0 || nullhit != 0 || b0 + 16 >= sh + n ||
+                     (b0 + 16 - sh >= inj_end && S == 0ull);   // a first part with no thread left
     if (__ballot(!fin) == 0) break;
   }
   if (valid && wsimple) {                                  // (every context row is row 0)

@@ -67,6 +67,66 @@ inline unsigned nblocks(int64_t n, int t = 256) { return (unsigned)std::max<int6
 typedef const __attribute__((address_space(3))) uint64_t* LdsWords;
 __device__ __forceinline__ LdsWords lds_words(const uint64_t* lds) { return (LdsWords)lds; }
 
+// The lean walks of a wave's pending one-word program keys, TWO lanes per key: a line of >= 64 bytes
+// (program not nullable) is split at an ASCII character pair near its middle -- the even lane walks
+// the first part (only threads that start there, each followed to its end), the odd lane the second
+// part from an empty state with the split point's previous kind -- so one lane's chain is about half
+// a line (bpg_walk1's prevk0 / inj_end; exact: every thread starts in one part). need / r / x: this
+// lane's own key (regex, line); done(src_lane, hit) runs on the even lane of the pair that walked the
+// key of lane src_lane. Every lane of the wave calls this (ballots inside).
+template <typename F>
+__device__ __forceinline__ void bpg_walk1_pairs(bool staged, const uint64_t* pool_lds, const DfaPool& P, bool need,
+                                                int r, int64_t x, const uint8_t* __restrict__ text,
+                                                const int64_t* __restrict__ ls, const int32_t* __restrict__ ll,
+                                                F&& done) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int pair = lane >> 1, part = lane & 1;
+  uint64_t todo = __ballot(need);
+  while (todo) {                                 // wave-uniform
+    int src = -1;
+    uint64_t m = todo;
+#pragma unroll 1
+    for (int k = 0; k < 32; ++k) {               // pair k takes the k-th lowest pending slot
+      const int b = m ? __builtin_ctzll(m) : -1;
+      if (k == pair) src = b;
+      m &= m ? m - 1 : 0ull;
+    }
+    todo = m;
+    const int sl = src < 0 ? lane : src;
+    const int rr = __shfl(r, sl, 64);
+    const long long xx = __shfl((long long)x, sl, 64);
+    const bool valid = src >= 0;
+    const int off = valid ? P.meta[4 * rr] : 0;
+    const uint8_t* s = text + (valid ? ls[xx] : 0);
+    const int len = valid ? ll[xx] : 0;
+    const uint64_t h0 = valid ? (staged ? pool_lds[off] : P.bpg[off]) : 0ull;
+    int mid = -1;
+    if (valid && len >= 64 && ((h0 >> 32) & 0xFFFFFFu) == 0u) {
+      // the split point: the first t in [len/2, len/2 + 16) with s[t-1] and s[t] ASCII (a 32-byte
+      // aligned window around it; texts are padded)
+      const uint8_t* w = reinterpret_cast<const uint8_t*>((uintptr_t)(s + len / 2 - 1) & ~(uintptr_t)15);
+      const uint4 c0 = reinterpret_cast<const uint4*>(w)[0], c1 = reinterpret_cast<const uint4*>(w)[1];
+      const int j0 = (int)((s + len / 2) - w);   // window index of t = len / 2 (1..16)
+#pragma unroll 1
+      for (int q = 0; q < 16 && mid < 0; ++q) {
+        const int t = len / 2 + q;
+        if (t >= len - 4 || j0 + q >= 32) break;
+        if (win_byte(c0, c1, j0 + q - 1) < 0x80 && win_byte(c0, c1, j0 + q) < 0x80) mid = t;
+      }
+    }
+    const bool split = mid > 0;
+    const bool v = valid && (part == 0 || split);
+    const uint8_t* ws = (part == 1 && split) ? s + mid : s;
+    const int wn = part == 0 ? len : (split ? len - mid : 0);
+    const int wpk = (part == 1 && split) ? prev_of(ascii_kind(s[mid - 1])) : 0;
+    const int wend = (part == 0 && split) ? mid : 0x7FFFFFFF;
+    const bool hit = staged ? bpg_walk1(lds_words(pool_lds) + off, ws, wn, v, wpk, wend)
+                            : bpg_walk1(P.bpg + off, ws, wn, v, wpk, wend);
+    const bool other = __shfl_xor(hit ? 1 : 0, 1, 64) != 0;
+    if (valid && part == 0) done(src, hit || other);
+  }
+}
+
 // WMAX: the library's widest program of <= 8 words -- only walks up to that width are compiled
 // into the kernel, so a library of one-word programs (the common case since counted positions)
 // runs at a one-word walk's register count (a W = 8 walk's 256 VGPRs allowed one wave per SIMD)
@@ -138,6 +198,8 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
   const bool staged = P.bpg_words != 0;
   const uint64_t* pool = stage_pool(P, pool_lds, staged);
   if constexpr (WMAX == 1) {                    // one-word programs: the lean walk, every lane in
+    // (one lane per key: the bulk path's keys are dense, so two lanes per key -- bpg_walk1_pairs --
+    // measured slower here: device step 2.81 -> 2.86 ms, config 2 0.51 -> 0.57 ms)
     if (__ballot(walk) == 0) return;
     const int off = walk ? P.meta[4 * r] : 0;
     const uint8_t* s = text + (walk ? ls[x] : 0);
@@ -149,10 +211,11 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
   }
 }
 
-// Request path for libraries of one-word programs (bpg_widths == 1 << 1, the common case): ONE lane
-// per BPG candidate with the lean walk (bpg_walk1) over the pool staged in LDS -- the cooperative
-// walk's two lanes per line cost ~340 ns per byte at one word (profiles/r5_c) -- and, MODE 2, the
-// DFA candidates in the grid's upper half (k_bpg_coop's layout).
+// Request path for libraries of one-word programs (bpg_widths == 1 << 1, the common case): the lean
+// walk (bpg_walk1) over the pool staged in LDS, two lanes per BPG candidate that split a long line
+// (bpg_walk1_pairs: a request's candidates are sparse, so the lanes are free and one walk's chain
+// halves) -- the cooperative walk cost ~340 ns per byte at one word (profiles/r5_c) -- and, MODE 2,
+// the DFA candidates in the grid's upper half (k_bpg_coop's layout).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_bpg_cand1(int64_t* __restrict__ cand, int64_t cap,
                                                    const unsigned long long* __restrict__ dcount,
@@ -187,11 +250,10 @@ __global__ __launch_bounds__(256) void k_bpg_cand1(int64_t* __restrict__ cand, i
   const bool staged = P.bpg_words != 0;
   stage_pool(P, pool_lds, staged);
   if (__ballot(need) == 0) return;              // wave-uniform
-  const int off = need ? P.meta[4 * r] : 0;
-  const uint8_t* s = text + (need ? ls[x] : 0);
-  const int len = need ? ll[x] : 0;
-  const bool hit = staged ? bpg_walk1(lds_words(pool_lds) + off, s, len, need) : bpg_walk1(P.bpg + off, s, len, need);
-  if (need && !hit) cand[i] = -1;
+  const int64_t base = i - (int64_t)(threadIdx.x & 63);
+  bpg_walk1_pairs(staged, pool_lds, P, need, r, x, text, ls, ll, [&](int src, bool hit) {
+    if (!hit) cand[base + src] = -1;
+  });
 }
 
 // ---------------------------------------------------------------------------------------------

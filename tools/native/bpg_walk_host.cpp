@@ -88,11 +88,24 @@ int main(int argc, char** argv) {
       const bool d = walk(progs[i], s, n);
       const bool h = lp::bpg_find_host(progs[i], s, n);
       const bool l = W == 1 ? lp::bpg_walk1<const uint64_t*>(progs[i], s, n, true) : h;
+      // the split walk (two parts OR'ed), as the device kernels run it on long lines
+      bool sp = h;
+      int mid = -1;
+      if (W == 1 && n >= 32 && ((progs[i][0] >> 32) & 0xFFFFFFu) == 0) {
+        for (int m = n / 2; m < n / 2 + 16 && m < n - 4; ++m)
+          if (s[m - 1] < 0x80 && s[m] < 0x80) { mid = m; break; }
+        if (mid > 0) {
+          const int pk = lp::prev_of(lp::ascii_kind(s[mid - 1]));
+          sp = lp::bpg_walk1<const uint64_t*>(progs[i], s, n, true, 0, mid) ||
+               lp::bpg_walk1<const uint64_t*>(progs[i], s + mid, n - mid, true, pk);
+        }
+      }
       ++walks;
       hits += h;
-      if (d != h || l != h) {
+      if (d != h || l != h || sp != h) {
         if (bad < 10)
-          std::printf("mismatch prog %lu line %ld: dev %d lean %d host %d\n", (unsigned long)i, (long)x, d, l, h);
+          std::printf("mismatch prog %lu line %ld (n %d mid %d): dev %d lean %d split %d host %d\n", (unsigned long)i,
+                      (long)x, n, mid, d, l, sp, h);
         ++bad;
       }
     }

@@ -18,6 +18,7 @@
 
 #include "lp_api.h"
 #include "lp_core.h"
+#include "post_core.h"
 
 namespace lp {
 
@@ -168,9 +169,14 @@ __global__ __launch_bounds__(256) void k_bpg_dedupe_all(const uint64_t* __restri
                                                         const int64_t* __restrict__ ls,
                                                         const int32_t* __restrict__ ll, DfaPool P,
                                                         uint8_t* __restrict__ flag, uint32_t* __restrict__ wcnt,
-                                                        uint32_t* __restrict__ wlist) {
+                                                        uint32_t* __restrict__ wlist, int64_t* __restrict__ std_key) {
   extern __shared__ uint64_t pool_lds[];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (std_key && i < n) {                       // fused k_dedupe_verify: the DFA keys' walks run beside
+    int64_t sk = 0;                             // the BPG walks (one launch: the two tails overlap)
+    flag[i] = dedupe_verify_one(keys, n, i, lbits, text, ls, ll, P, &sk) ? 1 : 0;
+    std_key[i] = sk;
+  }
   bool walk = false;
   int r = 0;
   int64_t x = 0;
@@ -712,23 +718,28 @@ bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* d
   return true;
 }
 
-void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
+bool bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
                     const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream, uint32_t* wcnt,
-                    uint32_t* wlist) {
-  if (!P.bpg_widths || n <= 0) return;
+                    uint32_t* wlist, int64_t* std_key) {
+  if (!P.bpg_widths || n <= 0) return false;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const bool any_wide = (P.bpg_widths & kWideMask) != 0;
   // programs of <= 8 words: ONE launch for every width, a lane per key (a step's BPG candidates are
   // few -- hundreds to thousands, a handful of waves -- and each walk is a serial chain, so
   // per-width launches added up their slowest walks where one launch runs them side by side)
   const bool listed = any_wide && wcnt && wlist;
-  if ((P.bpg_widths & 0x1FFu) || listed) {
+  const bool fused = (P.bpg_widths & 0x1FFu) || listed;
+  if (std_key && !fused) {                      // only in-place wide walks: the DFA verify goes first
+    dedupe_verify_dev(keys, n, lbits, text, ls, ll, P, std_key, flag, stream);
+    std_key = nullptr;
+  }
+  if (fused) {
     DfaPool Q = P;
     if (!pool_lds_bytes(P)) Q.bpg_words = 0;     // the kernel stages the pool iff bpg_words != 0
 #define LP_DEDUPE(WM)                                                                                      \
   hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), pool_lds_bytes(P), st, keys, n, lbits, text, ls, \
                      ll, Q, flag, \
-                     listed ? wcnt : nullptr, listed ? wlist : nullptr)
+                     listed ? wcnt : nullptr, listed ? wlist : nullptr, std_key)
     switch (narrow_wmax(P.bpg_widths) == 1 && !lean_on() ? 2 : narrow_wmax(P.bpg_widths)) {
       case 1: LP_DEDUPE(1); break;
       case 2: LP_DEDUPE(2); break;
@@ -738,7 +749,7 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
 #undef LP_DEDUPE
     check_launch("k_bpg_dedupe_all");
   }
-  if (!any_wide) return;
+  if (!any_wide) return true;
   if (listed) {                                 // wider programs: a lane group per listed key
     const int G = coop_group(P.bpg_widths);
     const dim3 grid(256), block(256);
@@ -752,6 +763,7 @@ void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
     launch_coop<1>(nullptr, keys, n, nullptr, lbits, text, ls, ll, P, flag, st, BPG_LANE_MAX_W + 1);
     check_launch("k_bpg_coop<dedupe>");
   }
+  return true;
 }
 
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,

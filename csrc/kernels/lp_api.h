@@ -46,9 +46,12 @@ bool cand_verify_all_dev(int64_t* cand, int64_t cap, const unsigned long long* d
                          const int64_t* ls, const int32_t* ll, const DfaPool& P, uint64_t stream);
 // wcnt / wlist (optional): a counter zeroed in stream order before the call and n uint32 of scratch --
 // keys of programs wider than 8 words are listed there and walked one lane group per key
-void bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
+// std_key (optional): the DFA dedupe-verify of every key (k_dedupe_verify's flag / std_key) runs in
+// the same launch; returns false when nothing was launched (no BPG program) -- the caller then runs
+// the DFA dedupe-verify itself
+bool bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
                     const int32_t* ll, const DfaPool& P, uint8_t* flag, uint64_t stream, uint32_t* wcnt = nullptr,
-                    uint32_t* wlist = nullptr);
+                    uint32_t* wlist = nullptr, int64_t* std_key = nullptr);
 void bpg_scan_dev(const uint8_t* text, const int64_t* ls, const int32_t* ll, int64_t L, const int32_t* regs,
                   int nregs, const DfaPool& P, int64_t* out, int64_t cap, unsigned long long* count,
                   uint64_t stream);

@@ -1040,11 +1040,18 @@ PYBIND11_MODULE(_lpnative, m) {
     dp_carry(A, s, dev);
   });
   // veto (optional, device int64): no record when *veto != 0 (a DP step that re-runs)
-  m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev, uint64_t veto) {
+  // gate_cnt / gate_caps (device counters [gram, cand, ver, hits, events] + the 4 capacities of
+  // gram, cand, ver, events): nothing is recorded when a count exceeds its capacity (a deferred step
+  // that re-runs), decided on the device so the record can be queued before the host's count read
+  m.def("freq_record", [](uint64_t counts, int K, double now, py::tuple ring, uint64_t s, bool dev, uint64_t veto,
+                          uint64_t gate_cnt, py::tuple gate_caps) {
     RecordGate G;
     G.veto = P<const int64_t>(veto);
+    G.cnt = P<const int64_t>(gate_cnt);
+    for (size_t i = 0; i < 4 && i < gate_caps.size(); ++i) G.cap[i] = gate_caps[i].cast<int64_t>();
     freq_record(P<const int64_t>(counts), K, now, ring_from(ring), s, dev, G);
-  }, py::arg("counts"), py::arg("K"), py::arg("now"), py::arg("ring"), py::arg("s"), py::arg("dev"), py::arg("veto") = 0);
+  }, py::arg("counts"), py::arg("K"), py::arg("now"), py::arg("ring"), py::arg("s"), py::arg("dev"), py::arg("veto") = 0,
+     py::arg("gate_cnt") = 0, py::arg("gate_caps") = py::tuple());
   m.def("score_host", [](uint64_t el, uint64_t ep, uint64_t es, uint64_t rank, uint64_t fkey, uint64_t carry,
                          int64_t n, py::tuple st, py::tuple sp, uint64_t out, uint64_t fac) {
     const FreqIn F{P<const int64_t>(rank), P<const int64_t>(fkey), P<const int64_t>(carry)};

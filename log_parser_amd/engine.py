@@ -694,6 +694,10 @@ class Engine:
             prep = self.prepare(text, nbytes, ls, ll, segs, host_text=host_text, early=early if attempt == 0 else None,
                                 defer=True)
             res = self.finish(prep, segs, self.freq_carry(), None, with_factors)
+            queued = record and self.freq_on_device and len(self.lib.freq_ids) > 0
+            if queued:                           # the record, gated on the device by the capacities,
+                c = prep.caps                    # before the read (not behind a host round trip)
+                self.freq.record_tensor(res.freq_counts, gate=(prep.cnt, (c["gram"], c["cand"], c["ver"], c["ev"])))
             h = prep.cnt.cpu().tolist()          # the one count read: gram, cand, ver, hits, events
             counts = h[:5]
             if not K.MatchArena.overflow(counts, prep.caps):
@@ -704,7 +708,7 @@ class Engine:
                 if res.factors is not None:
                     res.factors = res.factors[:ne]
                 res.hit_keys = res.hit_keys[:nh]
-                if record:
+                if record and not queued:
                     self.commit_frequency(res.freq_counts)
                 return res
             self.arena.learn(L, {"gram": h[0], "cand": h[1], "ver": h[2], "ev": h[4]}, overflow=True)

@@ -269,10 +269,11 @@ class DeviceFrequencyState:
             N.freq_evict(self._ring(), self._now(now) - self.window_s, self._stream(), self.device.type == "cuda")
             return self.tot
 
-    def record_tensor(self, counts, now: Optional[float] = None, veto=None) -> None:
+    def record_tensor(self, counts, now: Optional[float] = None, veto=None, gate=None) -> None:
         """Append this batch's per-key counts (int64 tensor on the state's device, >= K entries).
         ``veto`` (device int64[1], optional): nothing is recorded when it is non-zero (a DP step
-        whose buffers overflowed and that re-runs)."""
+        whose buffers overflowed and that re-runs). ``gate`` = (device counters int64[>=5], (gram,
+        cand, ver, events) capacities): nothing is recorded when a counter exceeds its capacity."""
         from .native import N
         K = len(self.ids)
         if K == 0:
@@ -281,7 +282,8 @@ class DeviceFrequencyState:
         with self._lock:
             self._ensure_room(K)
             N.freq_record(c.data_ptr(), K, self._now(now), self._ring(), self._stream(), self.device.type == "cuda",
-                          veto.data_ptr() if veto is not None else 0)
+                          veto.data_ptr() if veto is not None else 0,
+                          gate[0].data_ptr() if gate is not None else 0, tuple(gate[1]) if gate is not None else ())
             self._tail_bound += K
 
     # host-array compatibility with FrequencyState (CPU callers, tests)
@@ -529,11 +531,15 @@ class SharedFrequencyState(DeviceFrequencyState):
             self.win.evict(self._now(now) - self.window_s)
             return self.tot
 
-    def record_tensor(self, counts, now: Optional[float] = None, veto=None) -> None:
+    def record_tensor(self, counts, now: Optional[float] = None, veto=None, gate=None) -> None:
         import torch
         K = len(self.ids)
         if K == 0 or (veto is not None and int(veto.item())):
             return
+        if gate is not None:             # (DeviceFrequencyState.record_tensor's gate, read here)
+            g, k, v, _, ne = gate[0][:5].tolist()
+            if g > gate[1][0] or k > gate[1][1] or v > gate[1][2] or ne > gate[1][3]:
+                return
         c = counts.to(device="cpu", dtype=torch.int64).contiguous()
         if c.numel() < K:
             c = torch.cat([c, torch.zeros(K - c.numel(), dtype=torch.int64)])

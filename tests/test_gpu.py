@@ -202,6 +202,26 @@ def test_run_document_equals_run_and_records(gpu_device):
         assert torch.equal(doc.freq_counts, ref.freq_counts)
 
 
+def test_run_document_overflow_rerun_records_once(gpu_device):
+    """run_document queues the frequency record before its count read, gated on the device by the
+    buffer capacities: a first attempt that overflows (capacities forced tiny) records nothing and
+    the re-run records once -- the next document's scores see exactly one record."""
+    sets, trig = make_library(80, seed=33)
+    lib = CompiledLibrary(sets, ScoringParams())
+    data = make_log(6000, trig, seed=34, hit_rate=0.2).encode()
+    e1, e2 = _eng(lib, gpu_device), _eng(lib, gpu_device)
+    t, _ = _text(gpu_device, data)
+    for _ in range(3):
+        e1.arena.rate = {k: 1e-4 for k in e1.arena.rate}   # every document overflows its first attempt
+        doc = e1.run_document(t, len(data))
+        ls, ll = K.split_lines(t, len(data))
+        ref = e2.run(t, len(data), ls, ll, Segments.single(ls.numel(), gpu_device), e2.freq_carry())
+        e2.commit_frequency(ref.freq_counts)
+        assert doc.ev_line.numel() == ref.ev_line.numel() > 600
+        torch.testing.assert_close(doc.score, ref.score, rtol=0, atol=0)
+        assert torch.equal(e1.freq_carry(), e2.freq_carry())
+
+
 def _strip(o):
     o = dict(o)
     o.pop("analysisId")

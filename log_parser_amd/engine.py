@@ -371,6 +371,7 @@ class Engine:
         # second compute stream: literal-free scans overlap the prefilter chain (K.match_and_hits)
         self._side = None
         self._pf_stream = None
+        self._doc_segs = None                       # run_document: (L, Segments) of the last document
         self._host_side = None                      # ops.side_path.HostSide (device-fed backtracker regexes)
         self._runner = None                         # N.RequestRunner (built on first use) / False
         if self.device.type == "cuda":
@@ -689,7 +690,9 @@ class Engine:
         L = ls.numel()
         # (through the engine's pinned upload buffer: a pageable copy would block the host until the
         # queued prefilter is done, with the matchers not yet launched)
-        segs = Segments.scalar(0, L, 0, L, 0, L, text.device, upload=self.upload)
+        if self._doc_segs is None or self._doc_segs[0] != L:   # (read-only: reused while L repeats)
+            self._doc_segs = (L, Segments.scalar(0, L, 0, L, 0, L, text.device, upload=self.upload))
+        segs = self._doc_segs[1]
         for attempt in range(4):
             prep = self.prepare(text, nbytes, ls, ll, segs, host_text=host_text, early=early if attempt == 0 else None,
                                 defer=True)

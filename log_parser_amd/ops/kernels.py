@@ -59,6 +59,23 @@ class _LineIndexWs:
 # lines per byte seen so far (grows only): capacity of the line index outputs, so the one-pass
 # kernel rarely needs a second pass; a text with more lines than that re-runs with the exact count
 _LINES_PER_BYTE = [1.0 / 48]
+
+import threading as _threading
+
+_count_read = _threading.local()     # per thread: the pinned 24-byte count buffer + its event
+
+
+def _count_read_slot(device: torch.device):
+    """(pinned int64[3], event) reused by this thread's line-index count reads on ``device`` (a
+    fresh pinned allocation and event per call cost host time on config 2's critical path; the
+    buffer is read before the call returns, so one per thread and device suffices)."""
+    slots = getattr(_count_read, "slots", None)
+    if slots is None:
+        slots = _count_read.slots = {}
+    slot = slots.get(device.index)
+    if slot is None:
+        slot = slots[device.index] = (torch.empty(3, dtype=torch.int64, pin_memory=True), torch.cuda.Event())
+    return slot
 LINE_BLK_SHIFT = 12
 
 
@@ -89,9 +106,8 @@ def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=Non
         if before_read is not None:
             # the counts travel to pinned memory behind the line index only; the host then waits
             # for that copy, not for the work before_read() queued after it
-            hinfo = torch.empty(3, dtype=torch.int64, pin_memory=True)
+            hinfo, done = _count_read_slot(dev)
             hinfo.copy_(info, non_blocking=True)
-            done = torch.cuda.Event()
             done.record()
             before_read()
             before_read = None
@@ -430,6 +446,19 @@ class MatchArena:
             self.rate[k] = max(r, self.rate[k] if overflow else self.rate[k] * 0.5, 1e-4)
 
 
+def _pf_events(stream: "torch.cuda.Stream"):
+    """(fork, done) events of this thread's early prefilter on ``stream`` (EarlyPrefilter): a
+    consumer that waits on a later record of `done` waits on a later point of the same stream, so
+    reuse never waits too little."""
+    ev = getattr(_count_read, "pf_events", None)
+    if ev is None:
+        ev = _count_read.pf_events = {}
+    e = ev.get(stream.cuda_stream)
+    if e is None:
+        e = ev[stream.cuda_stream] = (torch.cuda.Event(), torch.cuda.Event())
+    return e
+
+
 class EarlyPrefilter:
     """The literal prefilter launched before the line index is known on the host (it reads only
     the text): gram hits + the arena counters, handed to ``match_and_hits``."""
@@ -446,7 +475,8 @@ class EarlyPrefilter:
             # on its own stream: the rest of the line index (line starts / lengths, after the host's
             # line-count read) and the literal-free scans run beside it; match_and_hits waits for
             # `done` before the candidates' verification (config 2: the chains overlap)
-            fork = torch.cuda.Event()
+            # (this thread's two events of this stream, reused)
+            fork, done = _pf_events(stream)
             fork.record(torch.cuda.current_stream(text.device))
             stream.wait_event(fork)
             st = stream.cuda_stream
@@ -455,7 +485,7 @@ class EarlyPrefilter:
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
                         pf_grid, st, nlp)
         if st != _s(text):
-            self.done = torch.cuda.Event()
+            self.done = done
             self.done.record(stream)
 
 

@@ -50,6 +50,8 @@ def main():
         setattr(owner, name, g)
 
     wrap(K, "split_lines", "split_lines")
+    wrap(K, "EarlyPrefilter", "early_pf")
+    wrap(K, "_line_index_dev", "line_index")
     wrap(E.Segments, "scalar", "segments")
     wrap(E.Engine, "prepare", "prepare")
     wrap(E.Engine, "_ev_tables", "ev_tables")

@@ -104,11 +104,12 @@ def test_bench_single_rank_parse_over_http(tmp_path):
 def test_bench_hang_guard_reports_phases(tmp_path):
     """A rank that hangs mid-run (rank 1 stops responding at step 2) must not burn the driver's
     timeout: within the stall limit rank 0 prints ONE JSON line with status 'timeout' and every
-    rank's last completed phase, and the job exits non-zero (utils/heartbeat.py)."""
+    rank's last completed phase, and the job exits non-zero (utils/heartbeat.py). (Stall limit
+    30 s: at 12 s a loaded CPU box could stall in the set-up phases before the injected hang.)"""
     import time
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu", "--steps", "3",
            "--warmup", "1", "--lines-per-gpu", "3000", "--block-lines", "3000", "--distinct-blocks", "1",
-           "--parse-requests", "0", "--library", "synthetic", "--patterns", "50", "--stall-timeout", "12"]
+           "--parse-requests", "0", "--library", "synthetic", "--patterns", "50", "--stall-timeout", "30"]
     env = dict(os.environ, OMP_NUM_THREADS="1", LP_FAULT_RANK="1", LP_FAULT_STEP="2", LP_FAULT_MODE="hang",
                LP_FAULT_HANG_S="600")
     env.pop("WORLD_SIZE", None)

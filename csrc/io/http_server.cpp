@@ -65,6 +65,7 @@ const char* reason(int s) {
     case 415: return "Unsupported Media Type";
     case 431: return "Request Header Fields Too Large";
     case 500: return "Internal Server Error";
+    case 501: return "Not Implemented";
     case 503: return "Service Unavailable";
     default: return "Status";
   }
@@ -97,10 +98,139 @@ void reserve_fd_table(int fd) {
   if (getrlimit(RLIMIT_NOFILE, &rl) != 0 || rl.rlim_cur == RLIM_INFINITY) return;
   const long top = std::min<long>((long)rl.rlim_cur, 1L << 17) - 1;
   if (top < 1024) return;
-  const int d = dup2(fd, (int)top);
+  // F_DUPFD_CLOEXEC takes the lowest FREE fd >= top: unlike dup2 it never closes a descriptor that
+  // is already open there (inherited, or a library's), and the probe fd is close-on-exec meanwhile
+  const int d = fcntl(fd, F_DUPFD_CLOEXEC, (int)top);
   if (d >= 0) close(d);
 }
+
+// Transfer-Encoding of a request (RFC 9112 §6.1): a comma-separated list of codings, applied in
+// order. `identity` entries are no coding; the body is framed by chunked when it is the last
+// coding. Any other coding (gzip, deflate, ...) is not decoded here (501).
+enum { TE_NONE = 0, TE_CHUNKED = 1, TE_BAD_LAST = 2, TE_UNSUPPORTED = 3 };
+int transfer_coding(const std::string& v) {
+  int r = TE_NONE;
+  size_t a = 0;
+  while (a <= v.size()) {
+    size_t e = v.find(',', a);
+    if (e == std::string::npos) e = v.size();
+    size_t i = a, j = e;
+    while (i < j && (v[i] == ' ' || v[i] == '\t')) ++i;
+    while (j > i && (v[j - 1] == ' ' || v[j - 1] == '\t')) --j;
+    const size_t sc = v.find(';', i);   // transfer parameters are not meaningful for these codings
+    if (sc != std::string::npos && sc < j) j = sc;
+    while (j > i && (v[j - 1] == ' ' || v[j - 1] == '\t')) --j;
+    if (j > i && !ieq(v.data() + i, j - i, "identity")) {
+      if (!ieq(v.data() + i, j - i, "chunked")) return TE_UNSUPPORTED;
+      r = (r == TE_NONE) ? TE_CHUNKED : TE_BAD_LAST;   // chunked applied twice
+    }
+    a = e + 1;
+  }
+  return r;
+}
+
+int hexval(char ch) {
+  if (ch >= '0' && ch <= '9') return ch - '0';
+  if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+  if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
+  return -1;
+}
+
+enum { CH_MORE = 0, CH_DONE = 1, CH_BAD = -1, CH_BIG = -2 };
 }  // namespace
+
+// Incremental, in-place decoder of a chunked request body (RFC 9112 §7.1: size line with optional
+// extensions, data, CRLF, ..., a zero-size chunk, trailer fields, empty line). The decoded bytes are
+// compacted to [b0, dst) of the connection's receive buffer, directly behind the headers, so a
+// complete body leaves the buffer laid out exactly like a Content-Length request (headers, body,
+// pipelined bytes) and the rest of parse_one -- validation in place, zero-copy hand-off -- is
+// shared. Each call resumes where the last one stopped and drops the framing it consumed, so the
+// buffer holds at most one partial size / trailer line of framing and the decoded size, not the
+// encoded one, is what `server.max-body-bytes` bounds (413).
+struct ChunkDecoder {
+  size_t dst = 0, src = 0;   // 0: not started (b0 > 0 always: the headers precede the body)
+  uint64_t left = 0;         // bytes of the current chunk's data still to come
+  int phase = 0;             // 0 size line, 1 data, 2 CRLF after the data, 3 trailer fields
+
+  void reset() { *this = ChunkDecoder(); }
+
+  int step(std::string& in, size_t b0, int64_t max_body) {
+    if (src == 0) dst = src = b0;
+    char* p = &in[0];
+    const size_t n = in.size();
+    int rc = CH_MORE;
+    for (;;) {
+      if (phase == 1) {
+        const size_t k = (size_t)std::min<uint64_t>(left, n - src);
+        if (k == 0) break;
+        if (dst != src) memmove(p + dst, p + src, k);
+        dst += k;
+        src += k;
+        left -= k;
+        if (left == 0) phase = 2;
+        continue;
+      }
+      if (phase == 2) {
+        if (n - src < 2) break;
+        if (p[src] != '\r' || p[src + 1] != '\n') {
+          rc = CH_BAD;
+          break;
+        }
+        src += 2;
+        phase = 0;
+        continue;
+      }
+      const char* nl = (const char*)memchr(p + src, '\n', n - src);
+      if (!nl) {
+        if (n - src > kMaxHeader) rc = CH_BAD;   // an unbounded size / trailer line
+        break;
+      }
+      const size_t e = (size_t)(nl - p);           // index of the '\n'
+      if (e == src || p[e - 1] != '\r') {
+        rc = CH_BAD;
+        break;
+      }
+      if (phase == 3) {                            // trailer fields: skipped up to the empty line
+        const bool empty = e == src + 1;
+        src = e + 1;
+        if (empty) {
+          rc = CH_DONE;
+          break;
+        }
+        continue;
+      }
+      // phase 0: chunk-size [ BWS ; chunk-ext ] CRLF
+      size_t i = src;
+      uint64_t v = 0;
+      int nd = 0;
+      for (int h; i < e - 1 && (h = hexval(p[i])) >= 0; ++i) {
+        if (++nd > 15) break;                      // > 2^60: refused below
+        v = (v << 4) | (uint64_t)h;
+      }
+      while (i < e - 1 && (p[i] == ' ' || p[i] == '\t')) ++i;
+      if (nd == 0 || nd > 15 || (i < e - 1 && p[i] != ';')) {
+        rc = CH_BAD;
+        break;
+      }
+      src = e + 1;
+      if (v == 0) {
+        phase = 3;
+        continue;
+      }
+      if ((int64_t)(dst - b0) + (int64_t)v > max_body) {
+        rc = CH_BIG;
+        break;
+      }
+      left = v;
+      phase = 1;
+    }
+    if (src > dst) {                               // drop the consumed framing
+      in.erase(dst, src - dst);
+      src = dst;
+    }
+    return rc;
+  }
+};
 
 struct HttpServer::Conn {
   int fd = -1;
@@ -119,6 +249,7 @@ struct HttpServer::Conn {
   double t_resp = 0;        // respond() of the response being written (0: none timed)
   double t_accept = 0, t_parse = 0, t_handoff = 0;   // conn_trace
   int n_recv = 0, n_wake = 0;
+  ChunkDecoder chunk;       // Transfer-Encoding: chunked body being received
 };
 
 struct HttpServer::Io {
@@ -400,7 +531,8 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
   std::string method(s, sp1 - s), path(sp1 + 1, sp2 - sp1 - 1), version(sp2 + 1, s + le - sp2 - 1);
   bool keep = version != "HTTP/1.0";
   int64_t clen = 0;
-  bool has_len = false, chunked = false, expect = false, json_ctype = true;
+  bool has_len = false, expect = false, json_ctype = true, has_te = false;
+  std::string te_list;
   size_t p = le + 2;
   while (p < he) {
     const size_t e = c->in.find("\r\n", p);
@@ -426,7 +558,9 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
         if (lv.find("close") != std::string::npos) keep = false;
         if (lv.find("keep-alive") != std::string::npos) keep = true;
       } else if (ieq(l, kn, "transfer-encoding")) {
-        chunked = true;
+        if (has_te) te_list += ',';    // several header lines form one list (RFC 9110 §5.3)
+        te_list += v;
+        has_te = true;
       } else if (ieq(l, kn, "expect")) {
         expect = true;
       } else if (ieq(l, kn, "content-type")) {
@@ -435,10 +569,39 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     }
     p = e + 2;
   }
-  if (chunked) {
-    send_now(io, c, 411, "application/json", "{\"error\":\"chunked bodies are not supported; send Content-Length\"}",
-             false);
+  const int te = has_te ? transfer_coding(te_list) : TE_NONE;
+  if (te == TE_UNSUPPORTED) {
+    c->chunk.reset();
+    send_now(io, c, 501, "application/json", "{\"error\":\"unsupported Transfer-Encoding\"}", false);
     return false;
+  }
+  if (te == TE_BAD_LAST) {   // RFC 9112 §6.3: a request whose final coding is not chunked is a 400
+    c->chunk.reset();
+    send_now(io, c, 400, "application/json", "{\"error\":\"chunked must be the final transfer coding\"}", false);
+    return false;
+  }
+  if (te == TE_CHUNKED) {    // framing by chunks: Content-Length, if any, is ignored (RFC 9112 §6.3)
+    const int rc = c->chunk.step(c->in, he + 4, max_body_);
+    if (rc == CH_BAD) {
+      c->chunk.reset();
+      send_now(io, c, 400, "application/json", "{\"error\":\"malformed chunked body\"}", false);
+      return false;
+    }
+    if (rc == CH_BIG) {
+      c->chunk.reset();
+      send_now(io, c, 413, "application/json", "{\"error\":\"request body too large\"}", false);
+      return false;
+    }
+    if (rc == CH_MORE) {
+      if (expect && !c->sent_continue) {
+        c->out += "HTTP/1.1 100 Continue\r\n\r\n";
+        c->sent_continue = true;
+        flush(io, c);
+      }
+      return false;
+    }
+    clen = (int64_t)(c->chunk.dst - (he + 4));   // the buffer is now headers + body + pipelined bytes
+    c->chunk.reset();
   }
   if (clen < 0) {
     send_now(io, c, 400, "application/json", "{\"error\":\"bad Content-Length\"}", false);

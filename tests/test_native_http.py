@@ -1,7 +1,7 @@
 """Native HTTP/1.1 front end (csrc/io/http_server.cpp + serve/native_http.py): the reference's
 REST contract (Parse.java:23-61) over real sockets -- 200 + AnalysisResult equal to the golden
 model, 400 for null body/pod, keep-alive, pipelining, Expect: 100-continue, Connection: close,
-413 / 411, admin + metrics routes through the shared Service, concurrent clients."""
+413, chunked bodies, admin + metrics routes through the shared Service, concurrent clients."""
 import http.client
 import json
 import socket
@@ -140,7 +140,131 @@ def test_pipelining_continue_close_limits(server):
     out = _raw(fe.port, b"POST /parse HTTP/1.1\r\nContent-Length: %d\r\n\r\n" % (5 << 20) + big)
     assert out.startswith(b"HTTP/1.1 413")
     out = _raw(fe.port, b"POST /parse HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n0\r\n\r\n")
-    assert out.startswith(b"HTTP/1.1 411")
+    assert out.startswith(b"HTTP/1.1 400")                          # decoded, then refused as JSON
+
+
+def _chunked(body: bytes, sizes, ext: bool = False, trailers: bytes = b"") -> bytes:
+    """`body` in Transfer-Encoding: chunked framing, chunk sizes cycling through `sizes`."""
+    out, i, k = [], 0, 0
+    while i < len(body):
+        n = sizes[k % len(sizes)]
+        k += 1
+        part = body[i:i + n]
+        i += n
+        out.append(b"%x%s\r\n%s\r\n" % (len(part), b" ;name=\"v\"" if ext and k % 2 else b"", part))
+    out.append(b"0\r\n" + trailers + b"\r\n")
+    return b"".join(out)
+
+
+def _strip(o):
+    o.pop("analysisId")
+    o["metadata"].pop("analyzedAt")
+    o["metadata"].pop("processingTimeMs")
+    return o
+
+
+def _recv_responses(s, n):
+    got = b""
+    while not _complete(got, n):
+        chunk = s.recv(1 << 16)
+        if not chunk:
+            break
+        got += chunk
+    out, pos = [], 0
+    while len(out) < n:
+        he = got.index(b"\r\n\r\n", pos)
+        head = got[pos:he].decode()
+        if head.startswith("HTTP/1.1 100"):
+            pos = he + 4
+            continue
+        cl = int([l.split(":")[1] for l in head.lower().split("\r\n") if l.startswith("content-length")][0])
+        out.append((int(head.split()[1]), got[he + 4:he + 4 + cl]))
+        pos = he + 4 + cl
+    return out
+
+
+def test_chunked_bodies_equal_content_length(server):
+    """Transfer-Encoding: chunked (Vert.x under Quarkus REST reads it: Parse.java:41-44, pom.xml:43-54):
+    the same request framed by 1-byte, 4 KiB and mixed chunks -- with chunk extensions, trailer
+    fields, a body delivered in slow segments, pipelined behind a chunked request -- answers the
+    same AnalysisResult as the Content-Length request (ids and times stripped)."""
+    import time
+    fe, _, trig = server
+    body = json.dumps({"pod": {"metadata": {"name": "ch"}}, "logs": make_log(120, trig, seed=26, hit_rate=0.1)}).encode()
+    hdr = b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+    plain = hdr + b"Content-Length: %d\r\n\r\n" % len(body) + body
+
+    def ask(raw, slow=False):
+        _raw(fe.port, b"DELETE /admin/frequency HTTP/1.1\r\nHost: x\r\n\r\n")
+        s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+        if slow:                                      # segments split mid size-line / mid CRLF
+            for i in range(0, len(raw), 997):
+                s.sendall(raw[i:i + 997])
+                time.sleep(0.001)
+        else:
+            s.sendall(raw)
+        (st, out), = _recv_responses(s, 1)
+        s.close()
+        return st, out
+
+    st, ref = ask(plain)
+    assert st == 200
+    ref = _strip(json.loads(ref))
+    assert ref["summary"]["significantEvents"] > 0
+    cases = [
+        hdr + b"Transfer-Encoding: chunked\r\n\r\n" + _chunked(body, [1]),
+        hdr + b"Transfer-Encoding: chunked\r\n\r\n" + _chunked(body, [4096]),
+        hdr + b"Transfer-Encoding: Chunked\r\n\r\n" + _chunked(body, [1, 7, 4096, 300, 2], ext=True,
+                                                                 trailers=b"X-Sum: 1\r\nX-B: 2\r\n"),
+        hdr + b"Transfer-Encoding: identity, chunked\r\nContent-Length: 5\r\n\r\n" + _chunked(body, [65536]),
+        hdr + b"Transfer-Encoding: identity\r\nContent-Length: %d\r\n\r\n" % len(body) + body,
+    ]
+    for k, raw in enumerate(cases):
+        st, out = ask(raw)
+        assert st == 200, (k, out[:200])
+        assert _strip(json.loads(out)) == ref, k
+    st, out = ask(cases[2], slow=True)
+    assert st == 200 and _strip(json.loads(out)) == ref
+    # pipelined: chunked request, a GET, then a Content-Length request on one connection
+    s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+    s.sendall(cases[0] + b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n" + plain)
+    r = _recv_responses(s, 3)
+    s.close()
+    assert [x[0] for x in r] == [200, 200, 200] and r[1][1] == b'{"status":"UP"}'
+    # Expect: 100-continue before a chunked body
+    s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+    s.sendall(hdr + b"Transfer-Encoding: chunked\r\nExpect: 100-continue\r\n\r\n")
+    assert s.recv(1024).startswith(b"HTTP/1.1 100 Continue")
+    s.sendall(_chunked(body, [333]))
+    (st, out), = _recv_responses(s, 1)
+    s.close()
+    assert st == 200 and "analysisId" in json.loads(out)
+
+
+def test_chunked_errors(server):
+    """Malformed chunked framing -> 400 (connection closed); a decoded size above
+    server.max-body-bytes -> 413 (the encoded size does not count); codings other than chunked /
+    identity -> 501; an invalid JSON body that arrived chunked -> the reference's 400."""
+    fe, _, _ = server
+    hdr = b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n"
+    for bad in [b"zz\r\nhello\r\n0\r\n\r\n", b"5\r\nhelloXX0\r\n\r\n", b"5\nhello\r\n0\r\n\r\n",
+                b"5 x\r\nhello\r\n0\r\n\r\n", b"1000000000000000\r\n", b"\r\n"]:
+        out = _raw(fe.port, hdr + bad)
+        assert out.startswith(b"HTTP/1.1 400"), (bad, out[:80])
+        assert b"malformed chunked body" in out and b"Connection: close" in out
+    big = (b"x" * 65536)
+    # 64 x 64 KiB = 4 MiB decoded is allowed (4.2 MB encoded); one byte more is not
+    out = _raw(fe.port, hdr + b"".join(b"10000\r\n" + big + b"\r\n" for _ in range(64)) + b"1\r\n")
+    assert out.startswith(b"HTTP/1.1 413")
+    out = _raw(fe.port, hdr + b"500000\r\n")                          # declared size alone is refused
+    assert out.startswith(b"HTTP/1.1 413")
+    for te in [b"gzip, chunked", b"deflate"]:
+        out = _raw(fe.port, b"POST /parse HTTP/1.1\r\nTransfer-Encoding: " + te + b"\r\nContent-Length: 2\r\n\r\n{}")
+        assert out.startswith(b"HTTP/1.1 501"), te
+    out = _raw(fe.port, b"POST /parse HTTP/1.1\r\nTransfer-Encoding: chunked, chunked\r\n\r\n0\r\n\r\n")
+    assert out.startswith(b"HTTP/1.1 400")
+    out = _raw(fe.port, hdr + _chunked(b'{"pod":null,"logs":"x"}', [3]))
+    assert out.endswith(b'{"error":"Invalid PodFailureData provided"}')
 
 
 def test_concurrent_clients(server):

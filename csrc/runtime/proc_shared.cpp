@@ -173,9 +173,16 @@ void* ProcShared::host_block(int64_t gen, int64_t bytes, bool create) {
 }
 
 void ProcShared::unlink(const std::string& name, int64_t max_gen) {
-  for (int64_t g = 1; g <= max_gen; ++g) shm_unlink((name + ".w" + std::to_string(g)).c_str());
+  // every published generation, then any block past it: a worker that died inside ensure_room,
+  // between creating generation max_gen + 1 and publishing it, left that block behind
+  for (int64_t g = 1;; ++g) {
+    const int r = shm_unlink((name + ".w" + std::to_string(g)).c_str());
+    if (g > max_gen && r != 0) break;
+  }
   shm_unlink(name.c_str());
 }
+
+void ProcShared::drop_block(int64_t gen) { shm_unlink((name_ + ".w" + std::to_string(gen)).c_str()); }
 
 // ---- the window in host shared memory ------------------------------------------------------
 size_t SharedWindow::layout(int64_t cap, int K, size_t off[6]) {
@@ -232,6 +239,10 @@ void SharedWindow::ensure_room(int64_t k) {
   // a new generation: the live records compacted to [0, n), totals and seen flags carried over
   const int64_t cap = std::max<int64_t>(2 * a.cap, n + 2 * k);
   const WinArrays old = a;
+  // the next generation is not published yet, so a block of that name can only be left over from
+  // a process that died between creating and publishing it (this runs inside the window section:
+  // no live process is building it): drop it, or O_EXCL would refuse every later growth
+  s_->drop_block(gen_ + 1);
   map_gen(gen_ + 1, cap, true);
   for (int64_t i = 0; i < n; ++i) {
     const int64_t so = (h + i) % old.cap;
@@ -263,16 +274,27 @@ void SharedWindow::evict(double horizon) {
 }
 
 void SharedWindow::record(const int64_t* counts, int K, double t) {
+  // a ring record holds an int32 count (the device ring's layout): a larger per-key batch count is
+  // split over several records, so eviction subtracts exactly what was added to the total
+  constexpr int64_t kMaxRec = std::numeric_limits<int32_t>::max();
+  int64_t extra = 0;
+  for (int k = 0; k < std::min(K, K_); ++k)
+    if (counts[k] > kMaxRec) extra += (counts[k] - 1) / kMaxRec;
+  if (extra > 0) ensure_room(K_ + extra);      // (the caller's ensure_room counted one per key)
   WinArrays a = arrays();
   for (int k = 0; k < std::min(K, K_); ++k) {
-    const int64_t c = counts[k];
+    int64_t c = counts[k];
     if (c <= 0) continue;
-    const int64_t sl = a.ht[1]++ % a.cap;       // room: ensure_room() before
-    a.t[sl] = t;
-    a.key[sl] = k;
-    a.cnt[sl] = (int32_t)c;
     a.tot[k] += c;
     a.seen[k] = 1;
+    while (c > 0) {
+      const int32_t part = (int32_t)std::min(c, kMaxRec);
+      const int64_t sl = a.ht[1]++ % a.cap;     // room: ensure_room() before
+      a.t[sl] = t;
+      a.key[sl] = k;
+      a.cnt[sl] = part;
+      c -= part;
+    }
   }
 }
 

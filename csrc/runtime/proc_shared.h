@@ -125,6 +125,7 @@ class ProcShared {
   // the ProcShared is destroyed)
   void* host_block(int64_t gen, int64_t bytes, bool create);
   static void unlink(const std::string& name, int64_t max_gen);
+  void drop_block(int64_t gen);   // unlink the host block of generation `gen` (an unpublished orphan)
 
  private:
   std::string name_;

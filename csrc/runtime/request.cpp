@@ -1,6 +1,8 @@
 // Native request runner (see request.h).
 #include "runtime/request.h"
 
+#include <cstdio>
+
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -187,7 +189,14 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   struct Leave {
     HostWindow* w;
     int64_t* s;
-    ~Leave() { if (w && *s >= 0) w->leave(*s); }
+    ~Leave() {             // (a destructor must not throw: a failing turn advance is reported)
+      if (!w || *s < 0) return;
+      try {
+        w->leave(*s);
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "[lp] leaving the shared window section failed: %s\n", e.what());
+      }
+    }
   } leave_guard{hw, &hw_seq};
   const int K1w = std::max(S_.nkeys, 1);
   if (hw && !carry_host_) {

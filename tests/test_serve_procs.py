@@ -155,6 +155,54 @@ def test_shared_window_across_processes_matches_one_window():
         N.ProcShared.unlink(name, int(sh.generation))
 
 
+def _die_in_growth(name):
+    """What a worker leaves behind when it dies inside SharedWindow::ensure_room after creating the
+    next generation's block (shm_open O_EXCL + ftruncate) and before publishing it."""
+    sh = N.ProcShared(name, False)
+    fd = os.open(f"/dev/shm{name}.w{int(sh.generation) + 1}", os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+    os.ftruncate(fd, 1 << 16)
+    os.close(fd)
+    os._exit(5)
+
+
+def test_window_grows_past_a_dead_workers_orphan_block_and_huge_counts():
+    """A worker killed between creating and publishing a generation must not block later growth
+    (the orphan block is replaced), the supervisor's unlink removes blocks past the published
+    generation, and a per-key batch count above 2^31 is split over int32 ring records so that
+    eviction takes back exactly what was added."""
+    name = _name("orph")
+    sh = N.ProcShared(name, True, 2)
+    ids = ["a", "b", "c"]
+    try:
+        own = SharedFrequencyState(ids, 1, sh, create=True, capacity=6)
+        p = mp.get_context("spawn").Process(target=_die_in_growth, args=(name,))
+        p.start()
+        p.join(timeout=60)
+        assert p.exitcode == 5 and os.path.exists(f"/dev/shm{name}.w2")
+        g0 = int(sh.generation)
+        for s in range(8):                                      # 8 x 3 records through a 6-slot ring
+            seq = sh.take()
+            sh.host.wait(seq)
+            sh.dev.wait(seq)
+            own.carry_tensor(1000.0 + s)
+            own.record_tensor(torch.tensor([1, 2, s], dtype=torch.int64), 1000.0 + s)
+            sh.host.done(seq)
+            sh.dev.done(seq)
+        assert int(sh.generation) > g0
+        assert own.tot.tolist() == [8, 16, sum(range(8))]
+        big = 3 * (1 << 31) + 5
+        own.record_tensor(torch.tensor([big, 0, 1], dtype=torch.int64), 2000.0)
+        assert own.tot.tolist() == [8 + big, 16, sum(range(8)) + 1]
+        assert own.carry_tensor(2000.0 + 7200.0).tolist() == [0, 0, 0]     # everything evicted, exactly
+        # an orphan past the published generation is removed by the supervisor's unlink
+        g = int(sh.generation)
+        fd = os.open(f"/dev/shm{name}.w{g + 1}", os.O_CREAT | os.O_RDWR, 0o600)
+        os.close(fd)
+    finally:
+        N.ProcShared.unlink(name, int(sh.generation))
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith(name.lstrip("/"))]
+
+
 def _post(port, body):
     c = http.client.HTTPConnection("127.0.0.1", port, timeout=120)
     try:

@@ -9,9 +9,12 @@ primaries). A timed step is the complete pipeline for the shard:
 
   pinned host -> HBM copy of the raw log bytes (PCIe ingest, H2D)
   -> line index -> literal prefilter -> DFA verify / scan -> hit CSR -> events
-  -> packed RCCL all_gather (global N, frequency carry, sequence-chain carry)
-  -> fused fp64 scoring -> RCCL all_reduce (severity + frequency histograms)
-  -> RCCL all_gather top-k -> persistent frequency-state update
+  -> collective 1: packed in-place RCCL all_gather (global N, frequency carry, sequence-chain
+     carry, overflow veto)
+  -> fused fp64 scoring -> summary kernel
+  -> collective 2: in-place RCCL all_gather of [pattern + severity histograms | frequency counts |
+     top-k rows], summed / merged locally (~20 KB per rank: one all_gather instead of an
+     all_reduce + an all_gather) -> persistent frequency-state update
   -> every event record (line, pattern, score) copied to pinned host memory.
 
 Launch: ``python bench.py --gpus N`` starts N rank processes itself (``utils/launch.py``; the

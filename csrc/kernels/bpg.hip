@@ -33,24 +33,8 @@ constexpr int kLdsProgWords = 1024;   // 8 KiB (larger programs read from global
 // line's walk: a request verifies a handful of candidates, a bulk step a few thousand)
 constexpr uint32_t kPoolLdsWords = 8192;   // 64 KiB
 
-bool pool_lds_on() {   // (diagnostic while validating the staging: LP_BPG_POOL_LDS=0 turns it off)
-  static const bool on = [] {
-    const char* e = std::getenv("LP_BPG_POOL_LDS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-bool lean_on() {   // (A/B while validating the lean one-word walk: LP_BPG_LEAN=0 keeps the old walks)
-  static const bool on = [] {
-    const char* e = std::getenv("LP_BPG_LEAN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 inline size_t pool_lds_bytes(const DfaPool& P) {
-  return (pool_lds_on() && P.bpg_words && P.bpg_words <= kPoolLdsWords) ? (size_t)P.bpg_words * 8 : 0;
+  return (P.bpg_words && P.bpg_words <= kPoolLdsWords) ? (size_t)P.bpg_words * 8 : 0;
 }
 
 // every thread of the block calls this (it synchronises): the pool in LDS, or in global memory
@@ -608,7 +592,7 @@ void launch_coop(int64_t* cand, const uint64_t* keys, int64_t cap, const unsigne
   const size_t lds = pool_lds_bytes(P);
   DfaPool Q = P;
   if (!lds) Q.bpg_words = 0;                     // the kernels stage the pool iff bpg_words != 0
-  if (MODE != 1 && P.bpg_widths == (1u << 1) && lean_on()) {
+  if (MODE != 1 && P.bpg_widths == (1u << 1)) {
     if (MODE == 2) hipLaunchKernelGGL((k_bpg_cand1<2>), grid, block, lds, st, cand, cap, dcount, text, ls, ll, Q);
     else hipLaunchKernelGGL((k_bpg_cand1<0>), grid, block, lds, st, cand, cap, dcount, text, ls, ll, Q);
     return;
@@ -740,7 +724,7 @@ bool bpg_dedupe_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* t
   hipLaunchKernelGGL(k_bpg_dedupe_all<WM>, dim3(nblocks(n)), dim3(256), pool_lds_bytes(P), st, keys, n, lbits, text, ls, \
                      ll, Q, flag, \
                      listed ? wcnt : nullptr, listed ? wlist : nullptr, std_key)
-    switch (narrow_wmax(P.bpg_widths) == 1 && !lean_on() ? 2 : narrow_wmax(P.bpg_widths)) {
+    switch (narrow_wmax(P.bpg_widths)) {
       case 1: LP_DEDUPE(1); break;
       case 2: LP_DEDUPE(2); break;
       case 4: LP_DEDUPE(4); break;

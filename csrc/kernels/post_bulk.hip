@@ -692,14 +692,6 @@ bool hits_bulk_ok(const HitsArgs& A) { return A.lbits <= 30 && A.R > 0; }
 
 
 constexpr int64_t kFuseDedupeKeys = int64_t(1) << 16;
-static bool fuse_dedupe_on() {   // (A/B: LP_FUSE_DEDUPE=0 runs the DFA dedupe-verify as its own launch)
-  static const bool on = [] {
-    const char* e = std::getenv("LP_FUSE_DEDUPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream) {
   const int64_t n = A.n;
   const int R = A.R;
@@ -757,8 +749,8 @@ size_t hits_bulk_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stre
   // kernels are then tails of a few long walks, which overlap instead of adding up (config 2, 23k
   // keys: 26 + 49 -> 63 us, resident 0.519 -> 0.493 ms). With many keys the DFA walks need the
   // occupancy the BPG walk's 140 VGPRs take away (bench, ~180k keys: 48 + 62 -> 121 us): two launches.
-  // (tmp: free after k_hb_sort; LP_FUSE_DEDUPE=0: always two launches, for A/B)
-  if (!fuse_dedupe_on() || n > kFuseDedupeKeys) {
+  // (tmp: free after k_hb_sort)
+  if (n > kFuseDedupeKeys) {
     dedupe_verify_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, stdk, flag, stream);
     bpg_dedupe_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, flag, stream, wide_cnt, tmp);
   } else if (!bpg_dedupe_dev(kout, n, A.lbits, A.text, A.ls, A.ll, A.dfa, flag, stream, wide_cnt, tmp, stdk)) {

@@ -65,8 +65,7 @@ RequestRunner::RequestRunner(const RequestStatic& S) : S_(S) {
   publish_ = true;
   fetch_ = true;
   evict_in_fetch_ = false;
-  const char* e = std::getenv("LP_RUNNER_SIDE_SCAN");   // (A/B: 0 = scans on the caller's stream)
-  side_on_ = !(e && e[0] == '0');
+  side_on_ = true;   // (literal-free scans + context features beside the literal chain, r5_c)
   if (side_on_) {
     check(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking), "side stream");
     check(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "fork event");

@@ -577,10 +577,12 @@ class Engine:
             # the host side path scans the bytes only for regexes without a device relaxation
             if self._host_side is None:
                 from .ops.side_path import HostSide
-                self._host_side = HostSide(self.lib, text.device)
+                self._host_side = HostSide(self.lib, text.device,
+                                           wait_s=float(self.config.get("engine.side-path-wait-s", 2.0)))
             self._host_side.check()
-            hs = (self._host_side, np.asarray(host_text, dtype=np.uint8))
-            plan = self.lib.host_plan_undev
+            if not self._host_side.take_fallback():   # (after a GPU wait timed out: the host-verified path)
+                hs = (self._host_side, np.asarray(host_text, dtype=np.uint8))
+                plan = self.lib.host_plan_undev
         inj = self.host_hits(text, nbytes, host_text, *(host_index or (None, None)), trim=split_trim, plan=plan)
         if defer:
             hits, hit_line, hit_off, ev_cnt, ev_end, nh_cap, cnt, caps = K.match_and_hits(
@@ -597,10 +599,14 @@ class Engine:
         if text.is_cuda:
             # every matcher appends to fixed-capacity device buffers; ONE host read after the CSR
             self._start(timings)
-            hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
-                text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
-                self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None,
-                side=self._side, early=early, inject=inj, host_side=hs)
+            try:
+                hits, hit_line, hit_off, ev_cnt, ev_end, nh, ne = K.match_and_hits(
+                    text, nbytes, ls, ll, self.tabs, self.lib.n_regexes, evt, self.arena, self.ws, self.pf_grid,
+                    self.scan_grid, tick=(lambda name: self._tick(timings, name, 0.0)) if self.profile else None,
+                    side=self._side, early=early, inject=inj, host_side=hs)
+            except K.SidePathTimeout:       # settle() armed the host-verified fallback for this re-run
+                return self.prepare(text, nbytes, ls, ll, segs, host_text, timings, None, defer, host_index,
+                                    split_trim)
             if hs is not None:
                 hs[0].check()
         else:

@@ -606,8 +606,14 @@ def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, 
         if ok:
             return hits[:nh], hit_line, hit_off, ev_cnt, ev_end, nh, ne
         if host_side is not None:          # the worker answers every job before the re-run's export
-            host_side[0].settle()
+            if host_side[0].settle() == 1:  # the GPU stopped waiting: the caller re-runs host-verified
+                raise SidePathTimeout()
     raise RuntimeError(f"matching: buffers still overflowing after 8 attempts ({arena.last})")
+
+
+class SidePathTimeout(RuntimeError):
+    """The GPU's wait for the backtracker side path's host answer timed out (ops/side_path.py):
+    the batch re-runs on the host-verified path (``Engine.prepare``)."""
 
 
 def results_buffer(ne: int, nkeys: int, device) -> torch.Tensor:

@@ -76,6 +76,9 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # k_publish writes the counters + compacted results into pinned host memory (no copies back):
     # 10k-line request GPU span 352 -> 326 us, engine p50 0.310 -> 0.302 ms (profiles/r2_v10)
     "engine.runner-device-counts": (True, bool),
+    # backtracker side path (ops/side_path.py): the GPU's first wall-clock wait for the host's
+    # verified keys (k_wait_host); a timeout re-runs that step on the host-verified path and doubles it
+    "engine.side-path-wait-s": (2.0, float),
     # serve a batch from the CPU backend when the device path fails (availability)
     "engine.fallback-cpu": (True, bool),
     # per-stage HIP-event timers, reported in response metadata as stageTimingsMs (opt-in)

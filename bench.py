@@ -84,6 +84,9 @@ def parse():
                     help="add N primaries only a backtracker decides (backreference / lookaround / atomic; N-1 with "
                          "a literal, one literal-free): the device feeds them with their relaxed automata and the host "
                          "checks only the candidate lines, inside the queued step (side_path.hip)")
+    ap.add_argument("--lookaround-patterns", type=int, default=0,
+                    help="add N primaries with lookaround line filters (X(?!ure), (?<!retrying )X, X(?!.*retry), "
+                         "(?=.*FATAL)X, (?<!\\S)X(?!\\S)): exact find() DFAs, no backtracker")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="hang guard: the whole job's deadline in seconds (0 = none)")
     ap.add_argument("--stall-timeout", type=float, default=300.0,
@@ -112,8 +115,8 @@ def make_blocks(args, trig):
 
 
 def library(args):
-    from log_parser_amd.utils.synth import (backtracker_patterns, counted_repeat_patterns, make_library,
-                                            realistic_library)
+    from log_parser_amd.utils.synth import (backtracker_patterns, counted_repeat_patterns, lookaround_patterns,
+                                            make_library, realistic_library)
     if args.library == "realistic":
         sets, trig = realistic_library(args.patterns, seed=7)
     else:
@@ -124,6 +127,9 @@ def library(args):
     if args.counted_repeats > 0:
         ps, cr_trig = counted_repeat_patterns(args.counted_repeats, seed=7)
         sets, trig = sets + [ps], trig + cr_trig
+    if args.lookaround_patterns > 0:
+        ps, la_trig = lookaround_patterns(args.lookaround_patterns, seed=7)
+        sets, trig = sets + [ps], trig + la_trig
     return sets, trig
 
 
@@ -411,7 +417,8 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
                        "global_batch": total_lines, "seq_len": round(nbytes / max(own_lines, 1), 1),
                        "parallelism": f"dp{world}", "lines_per_gpu": own_lines, "bytes_per_gpu": nbytes,
                        "distinct_blocks": B, "block_lines": args.block_lines,
-                       "extra_primaries": {"backtracker": args.bt_patterns, "counted_repeats": args.counted_repeats},
+                       "extra_primaries": {"backtracker": args.bt_patterns, "counted_repeats": args.counted_repeats,
+                                           "lookaround": args.lookaround_patterns},
                        "events_per_step": int(last.pattern_counts.sum().item()),
                        "events_to_host_rank0": state["events_host"],
                        "library_kind": args.library, "library": lib.summary(), "prefilter_stride": lib.pf["stride"], "device": str(device)},

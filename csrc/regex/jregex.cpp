@@ -1526,6 +1526,463 @@ class Relaxer {
 Compiled compile_nodes(Compiled out, std::vector<Node> nodes, int root, int max_dfa_states, int max_positions,
                        bool want_bpg, const std::string& pattern);
 
+// ---- find()-equivalence ----------------------------------------------------------------------
+// The reference only asks find() (AnalysisService.java:95, ScoringService.java:281,300,330):
+// whether SOME substring of the line is in L(R), i.e. membership of the line in Σ*·R·Σ*. There a
+// LEADING repeat keeps only its minimum count: Σ*·X{m,n}·S = Σ*·X{m}·S, because the extra copies
+// of X are matches of X at real text positions and fold into the Σ* prefix (any assertion inside
+// them is still evaluated at the position it sits on); symmetrically for a TRAILING repeat and the
+// Σ* suffix. X{0,n} and X* vanish, and the element after them becomes the leading one. This keeps
+// repeated groups such as (?:ab.){0,1000}Z (= Z) or (?:ERROR \d+ ){1,300} (= ERROR \d+ ) on the
+// automata instead of past the position limit. `lead`: the leading edge, else the trailing one.
+// Returns whether node `id` now matches only the empty string (the caller moves on to the next
+// element). The parser builds a tree (every node has one parent), so nodes are edited in place.
+bool trim_edge(std::vector<Node>& N, int id, bool lead) {
+  switch (N[id].t) {
+    case N_EMPTY: return true;
+    case N_REP: {
+      if (N[id].lo == 0) {
+        N[id] = Node();
+        N[id].t = N_EMPTY;
+        return true;
+      }
+      N[id].hi = N[id].lo;
+      return false;
+    }
+    case N_GROUP: return trim_edge(N, N[id].kids[0], lead);
+    case N_ALT: {                  // Σ*(A|B)S = Σ*AS ∪ Σ*BS: each alternative on its own
+      bool all = true;
+      const std::vector<int> kids = N[id].kids;
+      for (int k : kids) all = trim_edge(N, k, lead) && all;
+      return all;
+    }
+    case N_CAT: {
+      const std::vector<int> kids = N[id].kids;
+      const int n = (int)kids.size();
+      for (int j = 0; j < n; ++j)
+        if (!trim_edge(N, kids[lead ? j : n - 1 - j], lead)) return false;
+      return true;
+    }
+    default: return false;         // a character, an assertion, a backtracker-only construct
+  }
+}
+
+void trim_find(std::vector<Node>& N, int root) {
+  trim_edge(N, root, true);
+  trim_edge(N, root, false);
+}
+
+// ---- lookaround on the automata -------------------------------------------------------------
+// A regex R0 · L1 · R1 · L2 · ... · LK · RK whose only non-regular-looking parts are clusters Ls of
+// lookarounds between regular segments (R0 and RK may be empty) -- \bERROR\b(?!.*retry),
+// (?=.*FATAL)ERR, (?<!a)b, (?<=a)b, (?<!\S)x(?!\S) -- still has a regular find() language, and
+// Java matches it exactly as this definition says: the line matches iff there are positions
+// p1 <= ... <= pK with
+//   * R0 ending at p1 (Σ*·R0 accepts there; an empty R0: any position), Rs matching [ps, ps+1),
+//     RK matching from pK (to any end),
+//   * at each ps every lookbehind (?<=A) of Ls with some A match ending there, every (?<!A) none,
+//     every lookahead (?=Y) matching from ps, every (?!Y) not.
+// The find() DFA is built directly by a subset construction whose state is
+//   (prev character kind, the unanchored position sets of Σ*R0 and of every lookbehind's Σ*A,
+//    the set of live INSTANCES),
+// an instance being (stage s, the anchored position set of Rs, one anchored set per lookahead of
+// the clusters reached so far), each part DONE once it accepted or DEAD once empty. A segment
+// that ends where the next cluster's lookbehinds hold moves a copy of its instance to the next
+// stage (the instance goes on, looking for other ends). An instance succeeds when RK is DONE, every
+// positive lookahead DONE and every negative one DEAD (at the end of the line a running part that
+// does not accept there is DEAD); a negative lookahead that is DONE, or a positive one that is
+// DEAD, drops it. Lookarounds and acceptance are only evaluated between whole characters (never
+// before a UTF-8 continuation byte). No Unicode \b, no MULTILINE anchors and no '$'-type condition
+// (final-terminator contexts) in any part; anything else -- nested lookarounds, backreferences,
+// atomic groups, a construction past the state limit -- stays on the backtracker.
+struct LookPart {
+  Nfa nfa;
+  std::vector<const ByteSet*> clsp;
+  SubsetTables T;
+  bool neg = false;                            // (?!Y) / (?<!A)
+  std::unordered_map<std::vector<uint64_t>, int, KeyHash> ids;
+  std::vector<std::vector<uint64_t>> sets;
+  int intern(const std::vector<uint64_t>& s) {
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    const int id = (int)sets.size();
+    ids.emplace(s, id);
+    sets.push_back(s);
+    return id;
+  }
+  bool accepts(const std::vector<uint64_t>* A, uint32_t bit) const {   // A == nullptr: fresh (nothing consumed)
+    if (!A) return (nfa.nullable & bit) != 0;
+    for (auto& e : nfa.last)
+      if (((*A)[e.to >> 6] >> (e.to & 63) & 1) && (e.cond & bit)) return true;
+    return false;
+  }
+  // successors on class k (rep byte c) in context `bit`; `first`: also the first positions (a fresh
+  // anchored part, or an unanchored part that restarts everywhere)
+  std::vector<uint64_t> advance(const std::vector<uint64_t>* A, bool first, int k, int c, uint32_t bit) const {
+    std::vector<uint64_t> B(T.nw, 0), U(T.nw, 0);
+    const uint64_t* m = T.cm.data() + (size_t)k * T.nw;
+    if (A) {
+      T.ungated(*A, U);
+      for (int w = 0; w < T.nw; ++w) {
+        uint64_t a = (*A)[w];
+        while (a) {
+          const int p = w * 64 + __builtin_ctzll(a);
+          a &= a - 1;
+          for (auto& e : T.fg[p])
+            if ((e.cond & bit) && clsp[e.to]->test(c)) B[e.to >> 6] |= 1ull << (e.to & 63);
+        }
+      }
+    }
+    if (first) {
+      for (int w = 0; w < T.nw; ++w) U[w] |= T.first_u[w];
+      for (auto& e : T.first_g)
+        if ((e.cond & bit) && clsp[e.to]->test(c)) B[e.to >> 6] |= 1ull << (e.to & 63);
+    }
+    for (int w = 0; w < T.nw; ++w) B[w] |= U[w] & m[w];
+    return B;
+  }
+};
+
+constexpr int LK_FRESH = -1, LK_DONE = -2, LK_DEAD = -3;
+
+bool any_ft(const Nfa& nfa) {
+  if (ft_sensitive(nfa.nullable)) return true;
+  for (auto& e : nfa.first) if (ft_sensitive(e.cond)) return true;
+  for (auto& e : nfa.last) if (ft_sensitive(e.cond)) return true;
+  for (auto& v : nfa.follow) for (auto& e : v) if (ft_sensitive(e.cond)) return true;
+  return false;
+}
+
+class LookaroundDfa {
+ public:
+  LookaroundDfa(const std::vector<Node>& in, int root, int max_states, int max_positions, bool wordb)
+      : in_(in), max_states_(max_states), max_pos_(max_positions), wordb_(wordb) {
+    std::vector<int> items;
+    flatten(root, items);
+    // segments and clusters: R0 L1 R1 L2 R2 ... LK RK (contiguous lookarounds form one cluster)
+    std::vector<std::vector<int>> segs(1), clus;
+    for (int id : items) {
+      if (in_[id].t == N_LOOK) {
+        if (segs.size() == clus.size() + 1) clus.emplace_back();   // a new cluster after a segment
+        clus.back().push_back(id);
+      } else {
+        if (segs.size() == clus.size()) segs.emplace_back();
+        segs.back().push_back(id);
+      }
+    }
+    K_ = (int)clus.size();
+    if (K_ == 0) throw Unsupported("no lookaround");
+    if (K_ > 4) throw Unsupported("more than 4 lookaround positions");
+    segs.resize(K_ + 1);
+    Lowerer Lw(plain_, false);
+    auto part = [&](int cp_root, bool neg) {
+      LookPart P;
+      P.neg = neg;
+      Glushkov G(Lw.out, max_pos_);
+      Info top = G.build(Lw.lower(cp_root));
+      G.finish(top);
+      if (any_ft(G.nfa)) throw Unsupported("end anchor in a lookaround pattern");
+      P.nfa = std::move(G.nfa);
+      return P;
+    };
+    if (!segs[0].empty()) {
+      const int c = cat(segs[0]);
+      trim_edge(plain_, c, true);            // Σ*·R0: its leading repeat keeps its minimum
+      main_.push_back(part(c, false));
+      r0_ = 0;
+    }
+    seg_.assign(K_ + 1, -1);
+    behind_.resize(K_ + 1);
+    ahead_.resize(K_ + 1);
+    for (int s = 1; s <= K_; ++s) {
+      for (int id : clus[s - 1]) {
+        const Node& n = in_[id];
+        const int body = strip(n.kids[0]);
+        if (n.behind) {
+          behind_[s].push_back((int)main_.size());
+          main_.push_back(part(body, n.neg));
+        } else {
+          trim_edge(plain_, body, false);    // Y·Σ*: a lookahead matches a prefix of the rest
+          ahead_[s].push_back((int)ahd_.size());
+          ahd_.push_back(part(body, n.neg));
+        }
+      }
+      if (!segs[s].empty()) {
+        const int c = cat(segs[s]);
+        if (s == K_) trim_edge(plain_, c, false);   // RK·Σ*
+        seg_[s] = (int)sgp_.size();
+        sgp_.push_back(part(c, false));
+      }
+    }
+  }
+
+  Dfa build() {
+    // byte classes: membership in every distinct position class of every part, word bit, cont bit
+    std::vector<ByteSet> dcls;
+    auto each = [&](auto&& f) { for (auto& p : main_) f(p); for (auto& p : sgp_) f(p); for (auto& p : ahd_) f(p); };
+    each([&](LookPart& P) {
+      for (auto& c : P.nfa.cls) {
+        bool f = false;
+        for (auto& x : dcls) if (x == c) { f = true; break; }
+        if (!f) dcls.push_back(c);
+      }
+    });
+    Dfa d;
+    std::map<std::vector<bool>, int> sig2cls;
+    d.bytemap.assign(256, 0);
+    for (int b = 0; b < 256; ++b) {
+      std::vector<bool> sig;
+      for (auto& x : dcls) sig.push_back(x.test(b));
+      sig.push_back(is_word_byte(b));
+      sig.push_back(b >= 0x80 && b <= 0xBF);
+      auto it = sig2cls.find(sig);
+      int k;
+      if (it == sig2cls.end()) { k = (int)rep_.size(); sig2cls[sig] = k; rep_.push_back(b); }
+      else k = it->second;
+      d.bytemap[b] = (uint8_t)k;
+    }
+    d.nclasses = (int)rep_.size();
+    if (d.nclasses > 256) throw Unsupported("too many byte classes");
+    each([&](LookPart& P) {
+      P.clsp.resize(P.nfa.npos);
+      for (int p = 0; p < P.nfa.npos; ++p) P.clsp[p] = &P.nfa.cls[p];
+      P.T.init(P.nfa.npos, P.clsp, P.nfa.follow, P.nfa.first, rep_);
+    });
+
+    State s0;
+    s0.prev = P_BOS;
+    for (auto& P : main_) s0.main.push_back(P.intern(std::vector<uint64_t>(P.T.nw, 0)));
+    intern(s0);
+    std::vector<std::vector<uint16_t>> rows;
+    std::vector<uint8_t> acc;
+    for (size_t si = 0; si < states_.size(); ++si) {
+      const State S = states_[si];
+      acc.push_back(accepts_at_end(S) ? 1 : 0);
+      std::vector<uint16_t> row(d.nclasses, 0);
+      for (int k = 0; k < d.nclasses; ++k) row[k] = (uint16_t)step(S, k);
+      rows.push_back(std::move(row));
+    }
+    d.nstates = (int)states_.size() + 2;
+    d.trans.assign((size_t)d.nstates * d.nclasses, 0);
+    d.accflags.assign(d.nstates, 0);
+    for (int k = 0; k < d.nclasses; ++k) d.trans[1 * d.nclasses + k] = 1;
+    d.accflags[1] = 3;
+    for (size_t si = 0; si < rows.size(); ++si) {
+      for (int k = 0; k < d.nclasses; ++k) d.trans[(si + 2) * d.nclasses + k] = rows[si][k];
+      d.accflags[si + 2] = acc[si];
+    }
+    d.anchored = false;
+    return d;
+  }
+
+ private:
+  // an instance: [stage s (1..K), its segment's state, the state of every lookahead part (NOTYET
+  // until its cluster is reached)]
+  static constexpr int NOTYET = -4;
+  struct State {
+    int prev = P_BOS;
+    std::vector<int> main;                      // set ids of the unanchored parts
+    std::vector<std::vector<int>> insts;
+    std::vector<int64_t> key() const {
+      std::vector<int64_t> k{prev, (int64_t)main.size()};
+      k.insert(k.end(), main.begin(), main.end());
+      for (auto& t : insts) k.insert(k.end(), t.begin(), t.end());
+      return k;
+    }
+  };
+  struct VHash {
+    size_t operator()(const std::vector<int64_t>& v) const {
+      size_t h = 1469598103934665603ull;
+      for (auto x : v) { h ^= (size_t)x; h *= 1099511628211ull; h ^= h >> 29; }
+      return h;
+    }
+  };
+
+  const std::vector<Node>& in_;
+  std::vector<Node> plain_;                     // regular copies of the segments and the bodies
+  int max_states_, max_pos_;
+  bool wordb_;
+  int K_ = 0, r0_ = -1;                         // clusters; main_ index of R0 (-1: empty)
+  std::vector<LookPart> main_, sgp_, ahd_;      // unanchored (R0, lookbehinds), segments, lookaheads
+  std::vector<int> seg_;                        // stage s -> sgp_ index (-1: empty segment)
+  std::vector<std::vector<int>> behind_, ahead_;   // stage s -> its cluster's main_ / ahd_ indices
+  std::vector<int> rep_;
+  std::unordered_map<std::vector<int64_t>, int, VHash> sids_;
+  std::vector<State> states_;
+
+  void flatten(int id, std::vector<int>& items) {
+    const Node& n = in_[id];
+    if (n.t == N_CAT) { for (int k : n.kids) flatten(k, items); return; }
+    if (n.t == N_GROUP) { flatten(n.kids[0], items); return; }
+    items.push_back(id);
+  }
+  int add(Node n) { plain_.push_back(std::move(n)); return (int)plain_.size() - 1; }
+  int cat(const std::vector<int>& items) {
+    std::vector<int> k;
+    for (int i : items) k.push_back(strip(i));
+    if (k.size() == 1) return k[0];
+    Node n; n.t = N_CAT; n.kids = std::move(k);
+    return add(n);
+  }
+  // a regular copy of a sub-pattern: capturing groups are transparent (no backreference can refer
+  // to them: those throw); lookaround, atomic groups, backreferences, MULTILINE anchors throw
+  int strip(int id) {
+    const Node& n = in_[id];
+    switch (n.t) {
+      case N_GROUP: return strip(n.kids[0]);
+      case N_LOOK: throw Unsupported("nested lookaround");
+      case N_ATOMIC: throw Unsupported("atomic group / possessive quantifier");
+      case N_BACKREF: throw Unsupported("backreference");
+      case N_MLANCHOR: throw Unsupported("MULTILINE anchor with lookaround");
+      default: {
+        Node c = n;
+        for (auto& k : c.kids) k = strip(k);
+        return add(c);
+      }
+    }
+  }
+
+  int intern(State& S) {
+    std::sort(S.insts.begin(), S.insts.end());
+    S.insts.erase(std::unique(S.insts.begin(), S.insts.end()), S.insts.end());
+    const std::vector<int64_t> k = S.key();
+    auto it = sids_.find(k);
+    if (it != sids_.end()) return it->second;
+    const int id = (int)states_.size() + 2;
+    if (id >= max_states_ || id > 0xFFFF) throw Unsupported("DFA state limit");
+    sids_.emplace(k, id);
+    states_.push_back(S);
+    return id;
+  }
+
+  static const std::vector<uint64_t>* set_of(const LookPart& P, int v) { return v >= 0 ? &P.sets[v] : nullptr; }
+  static bool runs(int v) { return v >= 0 || v == LK_FRESH; }
+
+  bool main_ends(const State& S, int j, uint32_t bit) const {
+    return main_[j].accepts(&main_[j].sets[S.main[j]], bit) || (main_[j].nfa.nullable & bit);
+  }
+  // cluster s's lookbehinds hold here ((?<=A): some A ends here, (?<!A): none)
+  bool behind_ok(const State& S, int s, uint32_t bit) const {
+    for (int j : behind_[s])
+      if (main_ends(S, j, bit) == main_[j].neg) return false;
+    return true;
+  }
+  // an instance entering stage s here: its segment and cluster s's lookaheads start fresh
+  std::vector<int> enter(std::vector<int> t, int s) const {
+    t[0] = s;
+    t[1] = seg_[s] < 0 ? LK_DONE : LK_FRESH;
+    for (int j : ahead_[s]) t[2 + j] = LK_FRESH;
+    return t;
+  }
+  bool alive(const std::vector<int>& t) const {
+    for (size_t j = 0; j < ahd_.size(); ++j) {
+      if (ahd_[j].neg && t[2 + j] == LK_DONE) return false;
+      if (!ahd_[j].neg && t[2 + j] == LK_DEAD) return false;
+    }
+    return true;
+  }
+  bool success(const std::vector<int>& t) const {
+    if (t[0] != K_ || t[1] != LK_DONE) return false;
+    for (size_t j = 0; j < ahd_.size(); ++j)
+      if (t[2 + j] != (ahd_[j].neg ? LK_DEAD : LK_DONE)) return false;
+    return true;
+  }
+
+  // the instances at a character boundary (or the end) before the next character: lookaheads that
+  // accept here are DONE, segments that end here move their instance on to the next stage (the
+  // instance itself goes on looking for other ends), the last stage's segment is DONE. Returns the
+  // live instances; `won` when one succeeded.
+  std::vector<std::vector<int>> boundary(const State& S, uint32_t bit, bool& won) const {
+    std::vector<std::vector<int>> work = S.insts, out;
+    if ((r0_ < 0 || main_ends(S, r0_, bit)) && behind_ok(S, 1, bit))
+      work.push_back(enter(std::vector<int>(2 + ahd_.size(), NOTYET), 1));
+    won = false;
+    while (!work.empty()) {
+      std::vector<int> t = std::move(work.back());
+      work.pop_back();
+      for (size_t j = 0; j < ahd_.size(); ++j)
+        if (runs(t[2 + j]) && ahd_[j].accepts(set_of(ahd_[j], t[2 + j]), bit)) t[2 + j] = LK_DONE;
+      if (!alive(t)) continue;
+      const int s = t[0];
+      const bool ends = t[1] == LK_DONE || (runs(t[1]) && sgp_[seg_[s]].accepts(set_of(sgp_[seg_[s]], t[1]), bit));
+      if (ends) {
+        if (s == K_) {
+          t[1] = LK_DONE;
+        } else if (behind_ok(S, s + 1, bit)) {
+          work.push_back(enter(t, s + 1));
+        }
+      }
+      if (success(t)) { won = true; return out; }
+      if (s < K_ && t[1] == LK_DONE) continue;     // an empty middle segment: only its next stage lives
+      out.push_back(std::move(t));
+    }
+    return out;
+  }
+
+  bool accepts_at_end(const State& S) {
+    bool won = false;
+    std::vector<std::vector<int>> insts = boundary(S, 1u << ctx_index(S.prev, N_EOS), won);
+    if (won) return true;
+    for (auto& t : insts) {
+      for (size_t j = 0; j < ahd_.size(); ++j)
+        if (t[2 + j] != LK_DONE) t[2 + j] = LK_DEAD;      // nothing follows the end
+      if (success(t)) return true;
+    }
+    return false;
+  }
+
+  int step(const State& S, int k) {
+    const int c = rep_[k];
+    const int nk = next_kind_of_byte(c);
+    const uint32_t bit = 1u << ctx_index(S.prev, nk);
+    std::vector<std::vector<int>> insts;
+    if (nk != N_C) {                             // lookarounds sit between whole characters
+      bool won = false;
+      insts = boundary(S, bit, won);
+      if (won) return 1;                         // ACCEPT
+    } else {
+      insts = S.insts;
+    }
+    State N;
+    N.prev = (nk == N_W && wordb_) ? P_W : P_N;
+    for (size_t j = 0; j < main_.size(); ++j)
+      N.main.push_back(main_[j].intern(main_[j].advance(&main_[j].sets[S.main[j]], true, k, c, bit)));
+    auto adv = [&](LookPart& P, int v) {
+      std::vector<uint64_t> B = P.advance(set_of(P, v), v == LK_FRESH, k, c, bit);
+      bool any = false;
+      for (auto w : B) any |= w != 0;
+      return any ? P.intern(B) : LK_DEAD;
+    };
+    for (auto& t : insts) {
+      if (runs(t[1])) t[1] = adv(sgp_[seg_[t[0]]], t[1]);
+      if (t[1] == LK_DEAD) continue;             // its segment can no longer end
+      for (size_t j = 0; j < ahd_.size(); ++j)
+        if (runs(t[2 + j])) t[2 + j] = adv(ahd_[j], t[2 + j]);
+      if (!alive(t)) continue;
+      if (success(t)) return 1;
+      N.insts.push_back(std::move(t));
+    }
+    return intern(N);
+  }
+};
+
+// A regex the automaton parser refused (lookaround, ...): its find() DFA when it is a lookaround
+// cluster LookaroundDfa covers; throws Unsupported otherwise
+void compile_lookaround(Compiled& out, const std::string& pattern, int max_dfa_states, int max_positions) {
+  Parser B(pattern, true);
+  const int r = B.parse();
+  if (B.uses_uword) throw Unsupported("lookaround with Unicode \\b");
+  LookaroundDfa L(B.nodes, r, max_dfa_states, max_positions, B.uses_wordb);
+  Dfa d = L.build();
+  set_literals(out, B.nodes, r);
+  out.wordb = B.uses_wordb;
+  out.uword = false;
+  out.cp_only = false;
+  out.dfa = std::move(d);
+  out.kind = Kind::DFA;
+  out.error.clear();
+}
+
 // "(?#relax)" + pattern: the automaton of the pattern's relaxation (Relaxer); FALLBACK if even that
 // is not regular enough for the automata. Java rejects "(?#" (no comment groups), so no library
 // regex starts with the marker.
@@ -1572,10 +2029,22 @@ Compiled compile_impl(const std::string& pattern, int max_dfa_states, int max_po
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   } catch (const Unsupported& e) {
     classify_fallback(out, pattern, e.what());
+    if (out.kind == Kind::FALLBACK) {
+      // a lookaround cluster (the backtracker accepted the pattern, so Java does): its exact
+      // find() DFA when the construction applies and fits
+      try {
+        Compiled lk = out;
+        compile_lookaround(lk, pattern, max_dfa_states, max_positions);
+        return lk;
+      } catch (const std::exception& e2) {
+        out.error += std::string("; lookaround DFA: ") + e2.what();
+      }
+    }
     return out;
   } catch (const std::exception& e) {
     out.kind = Kind::INVALID; out.error = e.what(); return out;
   }
+  trim_find(nodes, root);   // (not for relaxations: the Relaxer shares one any-string node)
   return compile_nodes(std::move(out), std::move(nodes), root, max_dfa_states, max_positions, want_bpg, pattern);
 }
 

@@ -211,11 +211,13 @@ def make_library(n_patterns: int, seed: int = 0, n_sets: int = 4, secondary_rate
 
 
 def backtracker_patterns(n: int, seed: int = 0) -> Tuple[PatternSet, List[dict]]:
-    """``n`` primaries only a backtracker decides (backreferences, lookaround,
-    possessive / atomic groups) + matching samples: n - 1 carry a pattern-specific literal (the
-    device prefilter narrows them), the last one has none (its relaxed automaton runs in a
-    literal-free scan group). The shapes real libraries use: a repeated id, "Fail" not followed by
-    "ure", an error not preceded by "retrying", a restart loop of the same pod."""
+    """``n`` primaries only a backtracker decides (backreferences, atomic groups /
+    possessive quantifiers, lookarounds the automata do not express -- nested, or around a '$') +
+    matching samples: n - 1 carry a pattern-specific literal (the device prefilter narrows them), the
+    last one has none (its relaxed automaton runs in a literal-free scan group). The shapes real
+    libraries use: a repeated id, "Fail" not followed by "ure", an error not preceded by "retrying",
+    a restart loop of the same pod. (Plain lookaround clusters compile to DFAs: see
+    ``lookaround_patterns``.)"""
     rng = random.Random(seed)
     pats, trig = [], []
     for i in range(n):
@@ -226,15 +228,42 @@ def backtracker_patterns(n: int, seed: int = 0) -> Tuple[PatternSet, List[dict]]
         elif fam == 0:
             rx, sm = rf"(\w+) {tok}Loop \1\b", f"worker7 {tok}Loop worker7 again"
         elif fam == 1:
-            rx, sm = rf"{tok}Fail(?!ure)\w*", f"{tok}Failed to mount"
+            rx, sm = rf"{tok}Fail(?!ure(?=\s))\w*", f"{tok}Failed to mount"
         elif fam == 2:
-            rx, sm = rf"(?<!retrying )\b{tok}Err\b", f"fatal {tok}Err in worker"
+            rx, sm = rf"(?<!retrying )\b{tok}Err\b(?!.*done$)", f"fatal {tok}Err in worker"
         else:
             rx, sm = rf"(?i)(?>{tok}Lock)+\s+held", f"{tok.upper()}LOCK held by 7"
         pats.append({"id": f"bt-{i:04d}", "name": f"backtracker shape {i}", "severity": rng.choice(SEVERITIES),
                      "primary_pattern": {"regex": rx, "confidence": round(rng.uniform(0.3, 0.95), 3)}})
         trig.append({"sample": sm, "secondary": [], "sequence": []})
     ps = PatternSet.model_validate({"metadata": {"library_id": "backtracker", "version": "1.0"}, "patterns": pats})
+    return ps, trig
+
+
+def lookaround_patterns(n: int, seed: int = 0) -> Tuple[PatternSet, List[dict]]:
+    """``n`` primaries with lookaround clusters used as line filters -- "Fail" not followed by "ure",
+    an error not preceded by "retrying", ERROR with no "retry" later on the line, a token followed
+    later by FATAL, an isolated word -- which compile to exact find() DFAs (jregex.cpp
+    ``LookaroundDfa``), + matching samples."""
+    rng = random.Random(seed)
+    pats, trig = [], []
+    for i in range(n):
+        tok = _token(rng, 30_000 + i)
+        fam = i % 5
+        if fam == 0:
+            rx, sm = rf"{tok}Fail(?!ure)\w*", f"{tok}Failed to mount"
+        elif fam == 1:
+            rx, sm = rf"(?<!retrying )\b{tok}Err\b", f"fatal {tok}Err in worker"
+        elif fam == 2:
+            rx, sm = rf"\b{tok}ERROR\b(?!.*retry)", f"{tok}ERROR disk full"
+        elif fam == 3:
+            rx, sm = rf"(?=.*FATAL){tok}Err", f"{tok}Err then FATAL"
+        else:
+            rx, sm = rf"(?<!\S){tok}x(?!\S)", f"got {tok}x here"
+        pats.append({"id": f"la-{i:04d}", "name": f"lookaround shape {i}", "severity": rng.choice(SEVERITIES),
+                     "primary_pattern": {"regex": rx, "confidence": round(rng.uniform(0.3, 0.95), 3)}})
+        trig.append({"sample": sm, "secondary": [], "sequence": []})
+    ps = PatternSet.model_validate({"metadata": {"library_id": "lookaround", "version": "1.0"}, "patterns": pats})
     return ps, trig
 
 

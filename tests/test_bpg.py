@@ -267,7 +267,9 @@ def test_bpg_candidate_walks_match_host(gpu_device, li):
 
 
 # ---- counted positions: bounded repeats of one class at any bound (no 2,048-position cliff) ----
-CTR_PATS = [r"x{2,5000}", r"[^\n]{0,2500}FATAL", r"(?i)(err|warn).{0,2100}x", r"X.{0,3000}Y", r"X.{0,20000}Y",
+# (a leading / trailing repeat is trimmed to its minimum by find()-equivalence -- x{2,5000} is x{2},
+# a DFA -- so these repeats sit behind an anchor alternative that keeps them counted)
+CTR_PATS = [r"(?:^|=)x{2,5000}(?:$|=)", r"(?:^|=)[^\n]{0,2500}FATAL", r"(?i)(err|warn).{0,2100}x", r"X.{0,3000}Y", r"X.{0,20000}Y",
             r"a.{3,40}b", r"^.{0,20}é{5,50}", r"(?i)error.{0,30}tok.{0,30}retry", r"X.{0,17}Y", r"\bX.{0,16}\bY",
             r"(?:q.{0,40})+Z", r"X[^\r]{0,50}(?m)$", r"X.{0,5000}Y.{0,2100}Z"]
 

@@ -48,7 +48,9 @@ def test_corpus_dfa_matches_oracle(pat):
 
 def test_unsupported_and_invalid_are_classified():
     assert N.compile_regex(r"(a)\1")["kind"] == 2          # backreference -> host fallback
-    assert N.compile_regex(r"foo(?=bar)")["kind"] == 2     # lookahead -> host fallback
+    assert N.compile_regex(r"foo(?=bar)")["kind"] == 0     # lookaround cluster -> exact find() DFA
+    assert N.compile_regex(r"a(?=b(?!c))")["kind"] == 2    # nested lookaround -> host fallback
+    assert N.compile_regex(r"a(?!.*x$)")["kind"] == 2      # '$' inside a lookaround -> host fallback
     assert N.compile_regex(r"a*+b")["kind"] == 2           # possessive -> host fallback
     assert N.compile_regex(r"(abc")["kind"] == 3           # syntax error
     assert N.compile_regex(r"a**")["kind"] == 3

@@ -254,7 +254,8 @@ def test_sharded_stream_with_backtracker_regexes_gpu(gpu_device):
 
 def _bt_set():
     from log_parser_amd.models.schema import PatternSet
-    bt = [r"^(\w*)\1$", r"(\w+)Aux0 \1", r"(?i)fatal (?=\w+Failure)"]
+    # (a nested lookaround: plain lookaround clusters compile to DFAs, jregex.cpp LookaroundDfa)
+    bt = [r"^(\w*)\1$", r"(\w+)Aux0 \1", r"(?i)fatal (?=\w+Fail(?!ed))"]
     return PatternSet.model_validate({"metadata": {"library_id": "bt"}, "patterns": [
         {"id": f"bt{i}", "name": rx, "severity": "LOW", "primary_pattern": {"regex": rx, "confidence": 0.5}}
         for i, rx in enumerate(bt)]})

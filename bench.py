@@ -87,6 +87,12 @@ def parse():
     ap.add_argument("--lookaround-patterns", type=int, default=0,
                     help="add N primaries with lookaround line filters (X(?!ure), (?<!retrying )X, X(?!.*retry), "
                          "(?=.*FATAL)X, (?<!\\S)X(?!\\S)): exact find() DFAs, no backtracker")
+    ap.add_argument("--ranks-per-gpu", type=int, default=1,
+                    help="REHEARSAL of a multi-GPU run on fewer GPUs: --gpus N ranks share N / R GPUs (R ranks "
+                         "each), with gloo (host-staged) collectives -- RCCL takes one rank per GPU. Same spawn, "
+                         "heartbeats, shards, halos and both collectives as the N-GPU run; n_gpus reports N / R")
+    ap.add_argument("--phase-log", default="",
+                    help="append every rank's phases (JSON lines) to PATH.rank<r>.jsonl")
     ap.add_argument("--timeout", type=float, default=1500.0,
                     help="hang guard: the whole job's deadline in seconds (0 = none)")
     ap.add_argument("--stall-timeout", type=float, default=300.0,
@@ -133,6 +139,19 @@ def library(args):
     return sets, trig
 
 
+def _digest(out, top) -> str:
+    """sha256 (16 hex) of a step's global results: pattern / severity / frequency histograms and the
+    merged top-k rows -- equal for any world size over the same concatenated log."""
+    if out is None:
+        return ""
+    import hashlib
+    h = hashlib.sha256()
+    for t in (out.pattern_counts, out.severity_counts, out.freq_counts, top):
+        if t is not None:
+            h.update(t.detach().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
 def main():
     args = parse()
     from log_parser_amd.utils import launch
@@ -151,7 +170,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     from log_parser_amd.utils.heartbeat import Heartbeat
-    hb = Heartbeat(rank, world)
+    hb = Heartbeat(rank, world, log_path=args.phase_log)
     hb.start(METRIC, args.stall_timeout, args.timeout or None)
     sets, trig = library(args)
     hb.phase("library")
@@ -190,9 +209,11 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
     use_cuda = torch.cuda.is_available() and args.device != "cpu"
     if use_cuda:
         ngpu = torch.cuda.device_count()
-        if world > ngpu:
-            raise SystemExit(f"{world} ranks but {ngpu} visible GPU(s): one rank per GPU")
-        local_gpu = local_rank
+        rpg = max(1, args.ranks_per_gpu)
+        if world > ngpu * rpg:
+            raise SystemExit(f"{world} ranks but {ngpu} visible GPU(s) x {rpg} rank(s) per GPU "
+                             f"(a rehearsal on fewer GPUs: --ranks-per-gpu)")
+        local_gpu = local_rank // rpg
         torch.cuda.set_device(local_gpu)
         device = torch.device("cuda", local_gpu)
         # the ingest copy stream is created before RCCL creates its own: HIP maps streams to a few
@@ -212,6 +233,8 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
         backend = "nccl" if use_cuda else ("gloo" if world > 1 else "none")
     if backend == "none" and world > 1:
         backend = "nccl" if use_cuda else "gloo"
+    if args.ranks_per_gpu > 1 and backend == "nccl":
+        backend = "gloo"                    # RCCL: one rank per GPU; the rehearsal stages through the host
     if backend != "none":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if "MASTER_PORT" not in os.environ:
@@ -239,6 +262,7 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
     eng = Engine(lib, cfg, device=device)
     eng.profile = args.profile
     sa = ShardedAnalyzer(eng)
+    sa.time_reduce = use_cuda and rank == 0        # rank 0's local sum + top-k merge of collective 2 (events)
     hb.phase("engine")
 
     # ---- synthetic shard: the distinct blocks tiled in rotation to lines_per_gpu (rank r's tiling
@@ -339,6 +363,8 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
         events_to_host(out, b)                                   # results land on the host
         if rank == 0 and out.topk_rows is not None:
             state["top"] = out.topk_rows.cpu()                   # merged global top-k on the host
+        if rank == 0:
+            state["last_out"] = out
         if use_cuda:
             # device span: to the step's last kernel (the step records it before its count read)
             ev1 = out.end_event
@@ -406,9 +432,10 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
     ms = dt / args.steps * 1e3
     value = total_lines * args.steps / dt
     if rank == 0:
+        n_gpus = world // max(1, args.ranks_per_gpu) if use_cuda else world
         rec = {
             "metric": METRIC,
-            "value": round(value, 1), "unit": "lines/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 1), "unit": "lines/s", "n_gpus": max(1, n_gpus), "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp64", "data": "synthetic",
             "ingest": "h2d-serial" if args.no_overlap else "h2d-overlapped(2 buffers, copy stream)",
@@ -430,7 +457,15 @@ def run(args, sets, trig, blocks, rank, world, local_rank, server, hw_queues=0, 
             "collectives_per_step": 2 if dist.is_initialized() else 0,
             "hip_hw_queues": hw_queues,
             "matcher_counts_rank0": dict(eng.arena.last),
+            "result_digest": _digest(state.get("last_out"), state.get("top")),
         }
+        if args.ranks_per_gpu > 1:
+            rec["rehearsal"] = (f"{world} ranks on {rec['n_gpus']} GPU(s), {args.ranks_per_gpu} per GPU, "
+                                f"{rec['backend']} collectives staged through host memory (readiness, not a scaling point)")
+        if sa.reduce_us:
+            rec["reduce_merge_us_rank0"] = {"sum_over_ranks": round(float(np.median([a for a, _ in sa.reduce_us])), 1),
+                                            "topk_merge": round(float(np.median([b for _, b in sa.reduce_us])), 1),
+                                            "rows": world}
         if state.get("dev"):
             # compute-stream time of the device pipeline per step (line index .. collectives .. top-k
             # .. event copy), i.e. what the GPU sustains when the log is already resident (the timed

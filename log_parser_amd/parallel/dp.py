@@ -167,6 +167,8 @@ class ShardedAnalyzer:
     def __init__(self, engine: Engine, group=None):
         self.engine = engine
         self.group = group
+        self.time_reduce = False          # events around collective 2's local sum / top-k merge
+        self._reduce_ev: list = []
         lib = engine.lib
         # per sequence-event slot: first slot of its sequence and its event index
         off = lib.seq_ev_off
@@ -291,7 +293,12 @@ class ShardedAnalyzer:
                                       line_add=segs.g0, ws=eng.ws, pack_events=pack_events, hist_out=mine[:H],
                                       rows_out=rows_out, dn=prep.ne_dev)
         all_gather_inplace(red2, self.group)                       # collective 2: C5 + C6 + C7
+        tev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if self.time_reduce and dev.type == "cuda" else None
+        if tev:
+            tev[0].record()
         red = red2[:, :H].sum(0) if wsize > 1 else red2[0, :H]
+        if tev:
+            tev[1].record()
         if sc is None:
             eng.commit_frequency(red[P + S:], veto=veto if defer else None)
         out = StepOutput(res, own_counts, rank, red[:P], severity_counts=red[P:P + S], own_lo=own_lo,
@@ -300,7 +307,20 @@ class ShardedAnalyzer:
         if topk > 0 and rank == 0:
             allrows = red2[:, H:].contiguous().view(torch.float64).view(-1, 3)
             out.topk_rows = K.topk_rows(allrows, k, ws=eng.ws) if allrows.shape[0] > k else allrows
+        if tev:
+            tev[2].record()
+            self._reduce_ev.append(tev)
         return out, prep, veto
+
+    @property
+    def reduce_us(self) -> list:
+        """Per step with ``time_reduce``: (local sum over the [world, H] histogram rows, rank-0 top-k
+        merge of world x k rows) in us, from events (read after the steps, no sync inside them)."""
+        out = []
+        for a, b, c in self._reduce_ev:
+            c.synchronize()
+            out.append((a.elapsed_time(b) * 1e3, b.elapsed_time(c) * 1e3))
+        return out
 
     def summary(self, pattern_counts: torch.Tensor, first_pat: Optional[int] = None,
                 severity_counts: Optional[torch.Tensor] = None) -> dict:

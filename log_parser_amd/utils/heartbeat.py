@@ -70,8 +70,10 @@ def timeout_record(metric: str, world: int, phases: Dict[str, dict], reason: str
 class Heartbeat:
     """This rank's phase file + the watchdog (``start``)."""
 
-    def __init__(self, rank: int, world: int, directory: Optional[str] = None):
+    def __init__(self, rank: int, world: int, directory: Optional[str] = None, log_path: str = ""):
         self.rank, self.world = rank, world
+        # optional per-rank phase history (one JSON line per phase; the rehearsal runs commit it)
+        self.log_path = f"{log_path}.rank{rank}.jsonl" if log_path else ""
         self.dir = directory or default_dir()
         os.makedirs(self.dir, exist_ok=True)
         self.path = os.path.join(self.dir, f"rank{rank}")
@@ -85,6 +87,9 @@ class Heartbeat:
         with open(tmp, "w") as f:
             json.dump({"phase": name, "t": time.time(), "pid": os.getpid()}, f)
         os.replace(tmp, self.path)
+        if self.log_path:
+            with open(self.log_path, "a") as f:
+                f.write(json.dumps({"rank": self.rank, "phase": name, "t": round(time.time(), 4)}) + "\n")
 
     def start(self, metric: str, stall_s: float, total_s: Optional[float] = None,
               on_timeout: Optional[Callable[[dict], None]] = None, poll_s: float = 1.0) -> None:

@@ -122,3 +122,25 @@ def test_bench_hang_guard_reports_phases(tmp_path):
     assert d["status"] == "timeout" and d["n_gpus"] == 2 and d["value"] is None
     assert d["phases"]["1"]["phase"] == "timed 0"           # rank 1 finished timed step 0, hung in step 1
     assert d["phases"]["0"]["phase"] in ("timed 0", "timed 1")
+
+
+def test_bench_result_digest_world4_equals_world1_over_the_same_log(tmp_path):
+    """The node-wide DP step is exact: 4 ranks over 4 consecutive shards (halos, both collectives,
+    the local sum + top-k merge) give the same global histograms and merged top-k rows as ONE rank
+    over the concatenated log (bench.py tiles rank r's blocks where rank r-1's end)."""
+    base = [sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--steps", "1", "--warmup", "1",
+            "--block-lines", "1500", "--parse-requests", "0", "--library", "synthetic", "--patterns", "120",
+            "--phase-log", str(tmp_path / "phases")]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    out = {}
+    for w, lines in ((4, 3000), (1, 12000)):
+        r = subprocess.run(base + ["--gpus", str(w), "--lines-per-gpu", str(lines)], cwd=str(tmp_path), env=env,
+                           capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[w] = _json_line(r.stdout)
+    assert out[4]["config"]["global_batch"] == out[1]["config"]["global_batch"] == 12000
+    assert out[4]["result_digest"] and out[4]["result_digest"] == out[1]["result_digest"]
+    phases = [json.loads(l)["phase"] for l in open(tmp_path / "phases.rank3.jsonl")]
+    assert "process group ready" in phases and "timed 0" in phases

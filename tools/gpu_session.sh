@@ -12,16 +12,11 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run pytest 800 python -u -m pytest tests/test_bpg.py tests/test_java_shapes.py tests/test_backtrack.py tests/test_gpu.py \
-  tests/test_scan_multi.py tests/test_summarize.py tests/test_stream.py -m gpu -x -v --timeout 300 --timeout-method thread
-run probe 300 python -u tools/bpg_probe.py --lens 32,128,512
-bash tools/gpu_check.sh reqtrace || exit 1
-run phases 300 python -u tools/engine_phases.py --n 200
-run single 300 python -u benchmarks/bench_configs.py single
-bash tools/gpu_check.sh singletrace || exit 1
-run bench 400 python -u bench.py --steps 10 --warmup 3
-run bench_bt 400 python -u bench.py --steps 10 --warmup 3 --bt-patterns 4 --parse-requests 0
-bash tools/gpu_check.sh prof || exit 1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-run pmcl 180 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --kernel-include-regex "k_scan_multi" \
-  -d gpurun_out/pmc_lds/p1 -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
+run pytest 600 python -u -m pytest tests/test_java_shapes.py tests/test_backtrack.py tests/test_stream.py tests/test_regex.py \
+  -m gpu -x -v --timeout 300 --timeout-method thread
+run bench_la0 300 python -u bench.py --steps 10 --warmup 3 --parse-requests 0
+run bench_la5 300 python -u bench.py --steps 10 --warmup 3 --parse-requests 0 --lookaround-patterns 5
+run bench_bt3 300 python -u bench.py --steps 10 --warmup 3 --parse-requests 0 --bt-patterns 3
+run nfa_lib 300 python -u tools/nfa_ab.py --library realistic --lines 1000000
+run nfa_shapes 400 python -u tools/nfa_ab.py --lines 1000000
+bash tools/gpu_check.sh pmcscan || exit 1

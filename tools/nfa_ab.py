@@ -82,7 +82,13 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--engine", default="both", choices=["both", "bpg", "mfma"])
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--library", default="", choices=["", "realistic"],
+                    help="instead of --shapes: the bench library's own BPG programs (realistic_library(1000, "
+                         "seed=7), bench.py's), one record per program: MFMA-runnable or why not, and for "
+                         "the runnable ones the same scan / verify A/B on the bench's own text")
     args = ap.parse_args()
+    if args.library:
+        return library_ab(args)
     dev = torch.device("cuda", 0)
     rng = random.Random(7)
     blob = make_text(rng, min(args.lines, 200_000), TOKS)
@@ -171,6 +177,75 @@ def main():
             rec["verify_agree"] = bool(torch.equal(vh["bpg"], vh["mfma"]))
         rec["verify_pairs"] = int(pairs.numel())
         print(json.dumps(rec), flush=True)
+
+
+def library_ab(args):
+    """The production question: which of the bench library's BPG programs could the MFMA engine
+    take at all (<= 64 byte-level positions, no code-point contexts: fits_group), and where it can,
+    which engine is faster on the bench's own log text (request-sized candidate verify, bulk
+    verify of every candidate line, literal-free scan of every line)."""
+    from log_parser_amd.utils.synth import make_log, realistic_library
+    dev = torch.device("cuda", 0)
+    sets, trig = realistic_library(1000, seed=7)
+    full = CompiledLibrary(sets, ScoringParams())
+    blob = make_log(250_000, trig, seed=11, hit_rate=0.05, aux_rate=0.01, stack_rate=0.01).encode()
+    reps = max(1, args.lines // (blob.count(b"\n") + 1))
+    data = b"\n".join([blob] * reps)
+    t = torch.zeros(K.padded_len(len(data)), dtype=torch.uint8)
+    t[:len(data)] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    t = t.to(dev)
+    ls, ll = K.split_lines(t, len(data))
+    L = ls.numel()
+    stream = torch.cuda.current_stream().cuda_stream
+    rng = random.Random(7)
+    summary = {"library_bpg_programs": len(full.bpg_regs), "mfma_runnable": 0, "lines": L}
+    for r in full.bpg_regs:
+        pat = full.regexes[r].pattern
+        d = N.compile_regex(pat, 4, 4096)
+        rec = {"regex": pat, "bpg_words": int(np.frombuffer(N.compile_regex(pat)["bpg"], np.uint64)[0] & np.uint64(0xFF))
+               if N.compile_regex(pat)["bpg"] else None, "byte_positions": int(d["npos"]), "cp_only": bool(d["cp_only"])}
+        if not fits_group(d):
+            rec["mfma"] = ("code-point contexts (no byte NFA)" if d["cp_only"] or not d["npos"]
+                           else f"{int(d['npos'])} byte positions > 64 per MFMA group")
+            print(json.dumps(rec), flush=True)
+            continue
+        summary["mfma_runnable"] += 1
+        ps = PatternSet.model_validate({"metadata": {"library_id": "one"}, "patterns": [
+            {"id": "p", "name": pat, "severity": "HIGH", "primary_pattern": {"regex": pat, "confidence": 0.5}}]})
+        lib = CompiledLibrary([ps], ScoringParams(), max_dfa_states=4)
+        groups = pack_groups([(lib.bpg_regs[0], d)])
+        tabs_np, ncls = zip(*[build_group(g) for g in groups])
+        gt = torch.from_numpy(np.concatenate(tabs_np).view(np.int64)).to(dev)
+        gl = torch.zeros(1, dtype=torch.int32, device=dev)
+        btabs = lib.device_tables(dev)
+        regs = torch.tensor(lib.bpg_regs, dtype=torch.int32, device=dev)
+        cap = max(4096, L // 2)
+        us_b, hb = timed(lambda: K.scan(t, ls, ll, regs, btabs["dfa"], cap), args.reps)
+        us_m, hm = timed(lambda: K.nfa_scan(gt, gl, ncls[0], t, ls, ll, cap), args.reps)
+        rec.update(scan_bpg_us=round(us_b, 1), scan_mfma_us=round(us_m, 1),
+                   scan_agree=bool(torch.equal(torch.sort(hb).values.cpu(), torch.sort(hm).values.cpu())))
+        for name, C in (("request", min(200, L)), ("bulk", min(args.cands, L))):
+            lines = torch.tensor(sorted(rng.sample(range(L), C)), dtype=torch.int32, device=dev)
+            pairs = regs.to(torch.int64)[:, None] << 32 | lines.to(torch.int64)[None, :]
+            pairs = pairs.reshape(-1)
+
+            def run_bpg():
+                c = pairs.clone()
+                N.bpg_cand_dev(c.data_ptr(), c.numel(), t.data_ptr(), ls.data_ptr(), ll.data_ptr(), btabs["dfa"], stream)
+                return c[c >= 0]
+
+            def run_mfma():
+                out = torch.empty(C + 1, dtype=torch.int64, device=dev)
+                cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+                N.nfa(gt.data_ptr(), gl.data_ptr(), 1, ncls[0], lines.data_ptr(), C, t.data_ptr(), ls.data_ptr(),
+                      ll.data_ptr(), 0, out.data_ptr(), out.numel(), cnt.data_ptr(), stream, True)
+                return out[:int(cnt.item())]
+            ub, vb = timed(run_bpg, args.reps)
+            um, vm = timed(run_mfma, args.reps)
+            rec.update({f"verify_{name}_bpg_us": round(ub, 1), f"verify_{name}_mfma_us": round(um, 1),
+                        f"verify_{name}_agree": bool(torch.equal(torch.sort(vb).values.cpu(), torch.sort(vm).values.cpu()))})
+        print(json.dumps(rec), flush=True)
+    print(json.dumps(summary), flush=True)
 
 
 if __name__ == "__main__":

@@ -86,16 +86,18 @@ for s in $steps; do
       run kstats 120 python3 tools/kstats_db.py "$db" 6 45 --median --marker k_nl_count --last 6 --timeline ;;
     pmcscan)
       cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-      P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
-      # (the 8-counter second pass of round 4 was refused by the profiler this round: two passes of 4)
-      P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY"
-      P3="SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_WAIT_ANY"
-      run pmc1 180 rocprofv3 --pmc $P1 --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan/p1 \
-        -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
-      run pmc2 180 rocprofv3 --pmc $P2 --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan/p2 \
-        -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
-      run pmc3 180 rocprofv3 --pmc $P3 --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" -d gpurun_out/pmc_scan/p3 \
-        -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --parse-requests 0 --no-overlap
+      # four counters per pass (larger passes were refused on this pool in rounds 5 and 6)
+      P1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU"
+      P2="SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+      P3="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY"
+      P4="SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_ANY SQ_WAIT_ANY"
+      k=1
+      for P in "$P1" "$P2" "$P3" "$P4"; do
+        run pmc$k 180 rocprofv3 --pmc $P --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" \
+          -d gpurun_out/pmc_scan/p$k -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 \
+          --parse-requests 0 --no-overlap
+        k=$((k + 1))
+      done
       run pmcsum 120 python3 tools/pmc_summary.py gpurun_out/pmc_scan ;;
     pmcbpg)
       # PMC of ONE lean BPG walk (tools/bpg_probe.py, 512-byte line): instructions and waits per walk

@@ -12,11 +12,10 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run pytest 600 python -u -m pytest tests/test_java_shapes.py tests/test_backtrack.py tests/test_stream.py tests/test_regex.py \
-  -m gpu -x -v --timeout 300 --timeout-method thread
-run bench_la0 300 python -u bench.py --steps 10 --warmup 3 --parse-requests 0
-run bench_la5 300 python -u bench.py --steps 10 --warmup 3 --parse-requests 0 --lookaround-patterns 5
-run bench_bt3 300 python -u bench.py --steps 10 --warmup 3 --parse-requests 0 --bt-patterns 3
-run nfa_lib 300 python -u tools/nfa_ab.py --library realistic --lines 1000000
-run nfa_shapes 400 python -u tools/nfa_ab.py --lines 1000000
+mkdir -p gpurun_out/rehearsal
+# world-8 rehearsal on the one GPU: 8 real rank processes, 12.5M lines each, gloo (host-staged)
+run reh8 600 python -u bench.py --gpus 8 --ranks-per-gpu 8 --steps 3 --warmup 1 --parse-requests 0 \
+  --phase-log gpurun_out/rehearsal/phases
+# the same 8 shards concatenated, one rank (digest must equal)
+run reh1 600 python -u bench.py --gpus 1 --lines-per-gpu 100000000 --steps 3 --warmup 1 --parse-requests 0
 bash tools/gpu_check.sh pmcscan || exit 1

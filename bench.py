@@ -91,6 +91,9 @@ def parse():
                     help="REHEARSAL of a multi-GPU run on fewer GPUs: --gpus N ranks share N / R GPUs (R ranks "
                          "each), with gloo (host-staged) collectives -- RCCL takes one rank per GPU. Same spawn, "
                          "heartbeats, shards, halos and both collectives as the N-GPU run; n_gpus reports N / R")
+    ap.add_argument("--gen-workers", type=int, default=4,
+                    help="forked processes generating the synthetic blocks (0: in this process -- under "
+                         "rocprofv3 --pmc, whose preloaded library has initialised the GPU before main)")
     ap.add_argument("--phase-log", default="",
                     help="append every rank's phases (JSON lines) to PATH.rank<r>.jsonl")
     ap.add_argument("--timeout", type=float, default=1500.0,
@@ -113,10 +116,10 @@ def make_blocks(args, trig):
     """``--distinct-blocks`` blocks of ``--block-lines`` lines, generated in parallel BEFORE any GPU
     call (forking after HIP initialisation is not allowed)."""
     jobs = [(trig, args.block_lines, 11 + 7919 * b, args.hit_rate) for b in range(max(1, args.distinct_blocks))]
-    if len(jobs) == 1:
-        return [_gen_block(jobs[0])]
+    if len(jobs) == 1 or args.gen_workers <= 0:
+        return [_gen_block(j) for j in jobs]
     import multiprocessing as mp
-    with mp.get_context("fork").Pool(min(len(jobs), 4)) as pool:
+    with mp.get_context("fork").Pool(min(len(jobs), args.gen_workers)) as pool:
         return pool.map(_gen_block, jobs)
 
 

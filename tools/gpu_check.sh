@@ -95,7 +95,7 @@ for s in $steps; do
       for P in "$P1" "$P2" "$P3" "$P4"; do
         run pmc$k 180 rocprofv3 --pmc $P --kernel-include-regex "k_prefilter|k_scan_multi|k_scan_rare" \
           -d gpurun_out/pmc_scan/p$k -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 \
-          --parse-requests 0 --no-overlap
+          --parse-requests 0 --no-overlap --gen-workers 0
         k=$((k + 1))
       done
       run pmcsum 120 python3 tools/pmc_summary.py gpurun_out/pmc_scan ;;

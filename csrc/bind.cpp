@@ -549,16 +549,21 @@ struct RawLogs {
   size_t off = 0, len = 0;
   size_t dlen = 0;            // decoded length (0: unknown, decode serially)
   std::shared_ptr<BufferPool> pool;
+  DecodeBuf dec;              // dec.p: already decoded by the IO thread (dlen bytes): plain text
+  std::shared_ptr<DecodePool> dpool;
   RawLogs() = default;
   RawLogs(const RawLogs&) = delete;
   RawLogs& operator=(const RawLogs&) = delete;
   ~RawLogs() {
     if (pool) pool->give(std::move(body));
+    if (dpool && dec.p) dpool->give(std::move(dec));
   }
   const uint8_t* data() const { return reinterpret_cast<const uint8_t*>(body.data()) + off; }
+  bool decoded() const { return dec.p != nullptr; }
 };
 
 static py::bytes raw_logs_decode(const RawLogs& r) {
+  if (r.decoded()) return py::bytes(r.dec.p.get(), r.dlen);
   PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(r.len + 64));
   if (!b) throw py::error_already_set();
   size_t n;
@@ -582,6 +587,18 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   std::vector<int64_t> off(D + 1, 0);
   bool raw = D > 0;
   for (int64_t i = 0; i < D && raw; ++i) raw = py::isinstance<RawLogs>(docs[i]);
+  // every body decoded by the IO threads already: plain text sources, packed like bytes (one
+  // copy + newline scan pass into the stage, no unescape on this thread)
+  bool predecoded = raw;
+  for (int64_t i = 0; i < D && predecoded; ++i) predecoded = docs[i].cast<const RawLogs&>().decoded();
+  if (predecoded) {
+    for (int64_t i = 0; i < D; ++i) {
+      const RawLogs& r = docs[i].cast<const RawLogs&>();
+      src[i] = r.dec.p.get();
+      off[i + 1] = off[i] + (int64_t)r.dlen;
+    }
+    raw = false;
+  }
   if (raw) {
     // escaped length bounds the decoded one; the decoder may write 64 bytes past its output
     std::vector<const RawLogs*> rl(D);
@@ -602,6 +619,10 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
         for (int64_t i = 0; i < D; ++i) off[i + 1] = off[i] + (int64_t)rl[i]->dlen;
         std::atomic<bool> bad{false};
         HostPool::get().run(D, std::max(1, nthreads), [&](int64_t i) {
+          if (rl[i]->decoded()) {             // (a mix: this one was decoded by the IO thread)
+            std::memcpy(d + off[i], rl[i]->dec.p.get(), rl[i]->dlen);
+            return;
+          }
           const size_t k = rl[i]->len ? decode_json_string_exact(rl[i]->data(), rl[i]->len,
                                                                  reinterpret_cast<char*>(d + off[i]))
                                       : 0;
@@ -610,13 +631,19 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
         if (bad) known = false;          // (never: the same grammar counted them) -- redo serially
       }
       if (!known) {
-        for (int64_t i = 0; i < D; ++i)
+        for (int64_t i = 0; i < D; ++i) {
+          if (rl[i]->decoded()) {
+            std::memcpy(d + off[i], rl[i]->dec.p.get(), rl[i]->dlen);
+            off[i + 1] = off[i] + (int64_t)rl[i]->dlen;
+            continue;
+          }
           off[i + 1] = off[i] + (int64_t)decode_json_string(rl[i]->data(), rl[i]->len, reinterpret_cast<char*>(d + off[i]));
+        }
       }
       for (int64_t i = 0; i < D; ++i) src[i] = reinterpret_cast<const char*>(d + off[i]);   // split in place
     }
   }
-  for (int64_t i = 0; i < D && !raw; ++i) {
+  for (int64_t i = 0; i < D && !raw && !predecoded; ++i) {
     PyObject* o = docs[i].ptr();
     Py_ssize_t n = 0;
     const char* p = nullptr;
@@ -667,7 +694,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
 
 // POST /parse body -> (status, pod_nonnull, pod_name | None, logs_kind, logs bytes | None);
 // status: 0 ok, 1 invalid JSON, 2 JSON but not an object, 3 fall back to json.loads
-static py::tuple parse_pod_request_py(py::bytes body, bool two_pass) {
+static py::tuple parse_pod_request_py(py::bytes body, bool two_pass, bool into) {
   char* p = nullptr;
   Py_ssize_t n = 0;
   PyBytes_AsStringAndSize(body.ptr(), &p, &n);
@@ -675,9 +702,18 @@ static py::tuple parse_pod_request_py(py::bytes body, bool two_pass) {
   int st;
   {
     py::gil_scoped_release nogil;
-    // two_pass: what the HTTP front end does -- validate, then unescape the recorded span
+    if (into) {     // what the HTTP front end's IO thread does: validate + decode into its buffer
+      std::unique_ptr<char[]> dst(new char[(size_t)n + 64]);
+      st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(p), (size_t)n, r, dst.get(), (size_t)n + 64);
+      if (st == JIN_OK && r.logs_kind == 1) {
+        if (!r.logs_decoded) throw std::runtime_error("parse_pod_request_into: logs string not decoded");
+        r.logs.assign(dst.get(), r.logs_dlen);
+      }
+    } else {
+    // two_pass: what the HTTP front end did before -- validate, then unescape the recorded span
     st = parse_pod_request(reinterpret_cast<const uint8_t*>(p), (size_t)n, r, !two_pass);
-    if (two_pass && st == JIN_OK && r.logs_kind == 1) {
+    }
+    if (!into && two_pass && st == JIN_OK && r.logs_kind == 1) {
       r.logs.resize(r.logs_len + 64);
       r.logs.resize(decode_json_string(reinterpret_cast<const uint8_t*>(p) + r.logs_off, r.logs_len, &r.logs[0]));
     }
@@ -839,7 +875,8 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("set_summ_select", &set_summ_select);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
-  m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false);
+  m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false,
+        py::arg("into") = false);
   // the front end's skip-mode view of a body: (status, logs offset, escaped length, decoded length)
   m.def("pod_logs_span", [](const py::bytes& body) {
     std::string b = body;
@@ -1285,6 +1322,12 @@ PYBIND11_MODULE(_lpnative, m) {
               rl->dlen = r.logs_dlen;
               rl->body = std::move(r.body);
               rl->pool = s.pool();
+              if (r.dec.p) {
+                rl->dec = std::move(r.dec);
+                rl->dpool = s.decode_pool();
+                rl->pool->give(std::move(rl->body));   // the escaped body is not needed any more
+                rl->pool = nullptr;
+              }
               out.append(py::make_tuple(r.id, 0, py::cast(rl, py::return_value_policy::take_ownership), r.pod_name,
                                         r.t_arrival));
             } else {
@@ -1310,8 +1353,14 @@ PYBIND11_MODULE(_lpnative, m) {
           py::gil_scoped_release nogil;
           for (size_t i = 0; i < v.size(); ++i)
             if (v[i].kind == 0) {
-              lens[i] = decode_json_string(reinterpret_cast<const uint8_t*>(v[i].body.data()) + v[i].logs_off,
-                                           v[i].logs_len, PyBytes_AS_STRING(bufs[i]));
+              if (v[i].dec.p) {
+                std::memcpy(PyBytes_AS_STRING(bufs[i]), v[i].dec.p.get(), v[i].logs_dlen);
+                lens[i] = v[i].logs_dlen;
+                s.decode_pool()->give(std::move(v[i].dec));
+              } else {
+                lens[i] = decode_json_string(reinterpret_cast<const uint8_t*>(v[i].body.data()) + v[i].logs_off,
+                                             v[i].logs_len, PyBytes_AS_STRING(bufs[i]));
+              }
               s.recycle(std::move(v[i].body));
             }
         }

@@ -91,7 +91,7 @@ std::string trim(const char* a, size_t n) {
 // burst of thousands of new connections the IO threads sat in accept4 in D state for tens of ms
 // at a time (utils/threadsample.py: 43% "accept4/expand_files" + 7% "accept4/__wait_rcu_gp" of the
 // IO threads' samples in the slow config-5 runs, none in the fast ones, profiles/r5_b). Raising
-// the table to the fd limit once (dup2 onto the highest fd, then close: the table never shrinks)
+// the table to the fd limit once (a descriptor at the highest fd, then closed: the table never shrinks)
 // pays that wait once, at start-up.
 void reserve_fd_table(int fd) {
   rlimit rl{};
@@ -448,6 +448,28 @@ void BufferPool::give(std::string&& buf) {
 
 std::string HttpServer::take_buffer() { return pool_->take(); }
 
+DecodeBuf DecodePool::take(size_t need) {
+  {
+    std::lock_guard<std::mutex> g(m);
+    for (size_t i = v.size(); i-- > 0;)
+      if (v[i].cap >= need) {
+        DecodeBuf b = std::move(v[i]);
+        v.erase(v.begin() + (std::ptrdiff_t)i);
+        return b;
+      }
+  }
+  DecodeBuf b;
+  b.cap = std::max<size_t>(need + need / 8, 64 << 10);
+  b.p.reset(new char[b.cap]);
+  return b;
+}
+
+void DecodePool::give(DecodeBuf&& b) {
+  if (!b.p || b.cap > (size_t(256) << 20)) return;
+  std::lock_guard<std::mutex> g(m);
+  if (v.size() < 64) v.push_back(std::move(b));
+}
+
 void HttpServer::send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body,
                           bool keep) {
   c->out += head(status, ctype, body.size(), keep);
@@ -646,7 +668,19 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     PodRequest pr;
     const double tv = r.t_arrival;
     c->t_parse = tv;
-    const int st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
+    // bodies of >= 4 KiB: the logs text is decoded by this thread in the validating pass, while the
+    // bytes are in its cache -- the engine's packer then copies plain text instead of unescaping
+    // bytes received on another core (server-side pack of a 1 MB body: 107 us, profiles/r6_c)
+    DecodeBuf dec;
+    int st;
+    if (clen >= (4 << 10)) {
+      dec = dpool_->take((size_t)clen + 64);
+      st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr,
+                                  dec.p.get(), dec.cap);
+    } else {
+      st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
+    }
+    if (st != JIN_OK || pr.logs_kind != 1 || !pr.logs_decoded) dpool_->give(std::move(dec));
     const double tz = now_s();
     stages.parse++;
     stages.receive_ns += (uint64_t)std::max(0.0, (tv - c->t_first) * 1e9);
@@ -675,6 +709,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
       r.logs_off = b0 + pr.logs_off;
       r.logs_len = pr.logs_len;
       r.logs_dlen = pr.logs_dlen;
+      if (dec.p) r.dec = std::move(dec);
       if (c->in.size() == total) {   // the usual case: hand the whole buffer over, no copy
         r.body.swap(c->in);
         c->in = take_buffer();

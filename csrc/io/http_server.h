@@ -19,6 +19,19 @@
 
 namespace lp {
 
+// Uninitialised, recycled storage for a body's `logs` text decoded by the IO thread (no memset of
+// a fresh megabyte per request, as a std::string resize would do).
+struct DecodeBuf {
+  std::unique_ptr<char[]> p;
+  size_t cap = 0;
+};
+struct DecodePool {
+  std::mutex m;
+  std::vector<DecodeBuf> v;
+  DecodeBuf take(size_t need);
+  void give(DecodeBuf&& b);
+};
+
 struct HttpRequest {
   uint64_t id = 0;          // reply handle
   int kind = 0;             // 0 = decoded POST /parse, 1 = other route (raw method/path/body)
@@ -27,6 +40,7 @@ struct HttpRequest {
   size_t logs_off = 0;      // kind 0: `body` is the raw request buffer and the JSON `logs`
   size_t logs_len = 0;      //   string's escaped content is body[logs_off, logs_off + logs_len)
   size_t logs_dlen = 0;     //   decoded UTF-8 length (counted while validating)
+  DecodeBuf dec;            //   the decoded text (dec.p valid: decoded by the IO thread while validating)
   std::string pod_name;     // kind 0: pod.metadata.name or "" (unknown)
   double t_arrival = 0;     // monotonic seconds, when the body was complete
 };
@@ -89,6 +103,7 @@ class HttpServer {
   // of a fresh megabyte-sized allocation per request)
   void recycle(std::string&& buf) { pool_->give(std::move(buf)); }
   const std::shared_ptr<BufferPool>& pool() const { return pool_; }
+  const std::shared_ptr<DecodePool>& decode_pool() const { return dpool_; }
   void stop();
   HttpStats stats;
   HttpStageStats stages;
@@ -130,6 +145,7 @@ class HttpServer {
   std::atomic<size_t> qn_{0};   // q_.size(), for the pump's lock-free spin
   std::atomic<uint64_t> next_id_{1};
   std::shared_ptr<BufferPool> pool_ = std::make_shared<BufferPool>();
+  std::shared_ptr<DecodePool> dpool_ = std::make_shared<DecodePool>();
 };
 
 }  // namespace lp

@@ -538,7 +538,20 @@ size_t decode_json_string_exact(const uint8_t* p, size_t n, char* w) {
   return (size_t)(w - w0);
 }
 
+namespace {
+int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap);
+}  // namespace
+
 int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs) {
+  return parse_pod_impl(body, n, out, decode_logs, nullptr, 0);
+}
+
+int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap) {
+  return parse_pod_impl(body, n, out, false, dst, cap);
+}
+
+namespace {
+int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap) {
   out = PodRequest{};
   if (n >= 2 && (body[0] == 0 || body[1] == 0)) return JIN_FALLBACK;      // UTF-16/32
   if (n >= 3 && body[0] == 0xEF && body[1] == 0xBB && body[2] == 0xBF) return JIN_FALLBACK;  // BOM
@@ -554,6 +567,24 @@ int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decod
   }
   ok = object(c, [&](const std::string& key, Cur& cc) {
     if (key == "logs") {
+      if (cc.p < cc.e && *cc.p == '"' && dst && (size_t)(cc.e - cc.p) + 64 <= cap) {
+        // validated and decoded in one pass into the caller's buffer (a later duplicate key
+        // overwrites it: the last one wins, as in json.loads)
+        const uint8_t* s0 = cc.p;
+        char* end = str_into(cc, dst);
+        if (!end) {
+          out.logs_decoded = false;
+          return false;
+        }
+        out.logs.clear();
+        out.logs_kind = 1;
+        out.logs_decoded = true;
+        out.logs_dlen = (size_t)(end - dst);
+        out.logs_off = (size_t)(s0 + 1 - body);
+        out.logs_len = (size_t)(cc.p - s0 - 2);
+        return true;
+      }
+      out.logs_decoded = false;
       if (cc.p < cc.e && *cc.p == '"' && !decode_logs) {
         out.logs.clear();
         out.logs_kind = 1;
@@ -623,5 +654,6 @@ int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decod
   if (c.p != c.e) return JIN_INVALID;
   return JIN_OK;
 }
+}  // namespace
 
 }  // namespace lp

@@ -17,12 +17,19 @@ struct PodRequest {
   size_t logs_off = 0;        // logs_kind 1: the raw JSON string's content (between the quotes)
   size_t logs_len = 0;        //   as an offset / length into the body
   size_t logs_dlen = 0;       //   and its decoded UTF-8 length
+  bool logs_decoded = false;  // parse_pod_request_into: the text is decoded in the caller's buffer
 };
 
 // Validates the whole body. With decode_logs the `logs` string is unescaped into out.logs;
 // without it only its raw span is recorded (decode later with decode_json_string, e.g. straight
 // into a Python bytes object -- the HTTP front end's one-copy path).
 int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs = true);
+
+// Validates the whole body like parse_pod_request and decodes the `logs` string into `dst` in the
+// same pass (the HTTP front end's IO thread, while the bytes are in its cache): logs_decoded is set
+// and logs_dlen is the decoded length. `dst` needs room for the escaped length + 64 bytes (block
+// stores run past the decoded end); a string that does not fit is only validated (skip mode).
+int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap);
 
 // Unescapes the content of a JSON string that parse_pod_request validated (`n` raw bytes between
 // the quotes) into `w`, which must have room for n + 64 bytes; returns the decoded length.

@@ -25,8 +25,10 @@ def _ref(body: bytes):
             logs.encode() if kind == 1 else None)
 
 
-def _check(body: bytes, two_pass: bool = False):
-    got = N.parse_pod_request(body, two_pass)
+def _check(body: bytes, two_pass="one"):
+    # "one": validate + decode in one pass into a string; "two": validate, then unescape the span;
+    # "into": validate + decode into the caller's buffer (the HTTP IO thread's mode)
+    got = N.parse_pod_request(body, two_pass == "two", two_pass == "into")
     if got[0] == 3:
         return False
     ref = _ref(body)
@@ -59,7 +61,7 @@ def _rand_value(rng, depth=0):
     return {_rand_str(rng): _rand_value(rng, depth + 1) for _ in range(rng.randint(0, 4))}
 
 
-@pytest.mark.parametrize("two_pass", [False, True])
+@pytest.mark.parametrize("two_pass", ["one", "two", "into"])
 @pytest.mark.parametrize("seed", range(4))
 def test_native_decoder_matches_json_loads_on_random_requests(seed, two_pass):
     rng = random.Random(seed)
@@ -98,7 +100,7 @@ def test_native_decoder_edge_cases():
         assert N.parse_pod_request(c)[0] == 3, c      # handed to json.loads
 
 
-@pytest.mark.parametrize("two_pass", [False, True])
+@pytest.mark.parametrize("two_pass", ["one", "two", "into"])
 def test_native_decoder_64_byte_blocks(two_pass):
     """Long logs go through the 64-byte branch-free block decoder (AVX-512 VBMI2 hosts): backslash
     runs of every length at every offset, runs crossing a block boundary, escaped quotes, a closing

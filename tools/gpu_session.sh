@@ -12,7 +12,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run stages_a 300 python -u tools/parse_stages.py --n 300
-run stages_spin 300 python -u tools/parse_stages.py --n 300 -D server.io-spin-us=300
-run stages_b 300 python -u tools/parse_stages.py --n 300
-bash tools/gpu_check.sh splitverify || exit 1
+run stages_c 300 python -u tools/parse_stages.py --n 300
+run stages_d 300 python -u tools/parse_stages.py --n 300
+run gpu_http 300 python -u -m pytest tests/test_gpu_serving.py tests/test_serve_procs.py -m gpu -x -q --timeout 200 --timeout-method thread
+run bench 300 python -u bench.py --steps 10 --warmup 3

@@ -12,7 +12,8 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run stages_c 300 python -u tools/parse_stages.py --n 300
-run stages_d 300 python -u tools/parse_stages.py --n 300
-run gpu_http 300 python -u -m pytest tests/test_gpu_serving.py tests/test_serve_procs.py -m gpu -x -q --timeout 200 --timeout-method thread
-run bench 300 python -u bench.py --steps 10 --warmup 3
+run bench1 300 python -u bench.py --steps 10 --warmup 3
+run stages_e 300 python -u tools/parse_stages.py --n 400
+run stages_f 300 python -u tools/parse_stages.py --n 400
+run bench2 300 python -u bench.py --steps 10 --warmup 3
+run stages_g 300 python -u tools/parse_stages.py --n 400

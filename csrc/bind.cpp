@@ -563,7 +563,7 @@ struct RawLogs {
 };
 
 static py::bytes raw_logs_decode(const RawLogs& r) {
-  if (r.decoded()) return py::bytes(r.dec.p, r.dlen);
+  if (r.decoded()) return py::bytes(r.dec.p.get(), r.dlen);
   PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(r.len + 64));
   if (!b) throw py::error_already_set();
   size_t n;
@@ -594,7 +594,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   if (predecoded) {
     for (int64_t i = 0; i < D; ++i) {
       const RawLogs& r = docs[i].cast<const RawLogs&>();
-      src[i] = r.dec.p;
+      src[i] = r.dec.p.get();
       off[i + 1] = off[i] + (int64_t)r.dlen;
     }
     raw = false;
@@ -620,7 +620,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
         std::atomic<bool> bad{false};
         HostPool::get().run(D, std::max(1, nthreads), [&](int64_t i) {
           if (rl[i]->decoded()) {             // (a mix: this one was decoded by the IO thread)
-            std::memcpy(d + off[i], rl[i]->dec.p, rl[i]->dlen);
+            std::memcpy(d + off[i], rl[i]->dec.p.get(), rl[i]->dlen);
             return;
           }
           const size_t k = rl[i]->len ? decode_json_string_exact(rl[i]->data(), rl[i]->len,
@@ -633,7 +633,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
       if (!known) {
         for (int64_t i = 0; i < D; ++i) {
           if (rl[i]->decoded()) {
-            std::memcpy(d + off[i], rl[i]->dec.p, rl[i]->dlen);
+            std::memcpy(d + off[i], rl[i]->dec.p.get(), rl[i]->dlen);
             off[i + 1] = off[i] + (int64_t)rl[i]->dlen;
             continue;
           }
@@ -1280,14 +1280,7 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<RawLogs>(m, "RawLogs")
       .def("__len__", [](const RawLogs& r) { return r.len; })
       .def("decode", &raw_logs_decode, "the unescaped UTF-8 log text")
-      .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; })
-      // decoded by the IO thread into a pinned buffer: (address, capacity) -- the engine stages
-      // this request in place; (0, 0) otherwise
-      .def_property_readonly("pinned_text", [](const RawLogs& r) {
-        const bool pin = r.decoded() && r.dec.pinned;
-        return py::make_tuple(pin ? reinterpret_cast<uint64_t>(r.dec.p) : uint64_t(0),
-                              pin ? (uint64_t)r.dec.cap : uint64_t(0));
-      });
+      .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; });
 
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init([](const std::string& host, int port, int io_threads, int64_t max_body, double idle,
@@ -1312,7 +1305,6 @@ PYBIND11_MODULE(_lpnative, m) {
         return a;
       })
       .def_property_readonly("port", &HttpServer::port)
-      .def("set_pinned_decode", &HttpServer::set_pinned_decode, py::arg("limit"), py::arg("min_bytes") = 256 << 10)
       .def("pending", &HttpServer::pending)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms, bool raw) {
         std::vector<HttpRequest> v;
@@ -1362,7 +1354,7 @@ PYBIND11_MODULE(_lpnative, m) {
           for (size_t i = 0; i < v.size(); ++i)
             if (v[i].kind == 0) {
               if (v[i].dec.p) {
-                std::memcpy(PyBytes_AS_STRING(bufs[i]), v[i].dec.p, v[i].logs_dlen);
+                std::memcpy(PyBytes_AS_STRING(bufs[i]), v[i].dec.p.get(), v[i].logs_dlen);
                 lens[i] = v[i].logs_dlen;
                 s.decode_pool()->give(std::move(v[i].dec));
               } else {

@@ -24,8 +24,6 @@
 #include <cstring>
 #include <stdexcept>
 
-#include <hip/hip_runtime_api.h>
-
 #include "io/json_in.h"
 
 namespace lp {
@@ -450,66 +448,26 @@ void BufferPool::give(std::string&& buf) {
 
 std::string HttpServer::take_buffer() { return pool_->take(); }
 
-void DecodeBuf::release() {
-  if (!p) return;
-  if (pinned) (void)hipHostFree(p);
-  else delete[] p;
-  p = nullptr;
-  cap = 0;
-}
-
 DecodeBuf DecodePool::take(size_t need) {
-  const bool want_pinned = pinned_limit > 0 && need >= pinned_min;
   {
     std::lock_guard<std::mutex> g(m);
-    // a pooled buffer that fits: pinned first when wanted (the engine stages in place), else the
-    // smallest pageable one
-    int best = -1;
-    for (int i = (int)v.size() - 1; i >= 0; --i) {
-      if (v[i].cap < need) continue;
-      if (best < 0 || (v[i].pinned == want_pinned && v[best].pinned != want_pinned)) best = i;
-    }
-    if (best >= 0) {
-      DecodeBuf b = std::move(v[best]);
-      v.erase(v.begin() + best);
-      return b;
-    }
+    for (size_t i = v.size(); i-- > 0;)
+      if (v[i].cap >= need) {
+        DecodeBuf b = std::move(v[i]);
+        v.erase(v.begin() + (std::ptrdiff_t)i);
+        return b;
+      }
   }
   DecodeBuf b;
-  if (want_pinned && pinned_live.fetch_add(1) < pinned_limit) {
-    // room for the engine's staging layout behind the text: padding, the line index (~12 bytes a
-    // line), segments and counters (request.cpp single-copy upload)
-    const size_t cap = (need + need / 4 + (96 << 10) + 4095) & ~size_t(4095);
-    void* q = nullptr;
-    if (hipHostMalloc(&q, cap, hipHostMallocDefault) == hipSuccess && q) {
-      b.p = static_cast<char*>(q);
-      b.cap = cap;
-      b.pinned = true;
-      return b;
-    }
-    (void)hipGetLastError();
-    pinned_limit = 0;                      // no pinned memory here: pageable from now on
-  }
-  if (want_pinned) pinned_live.fetch_sub(1);
   b.cap = std::max<size_t>(need + need / 8, 64 << 10);
-  b.p = new char[b.cap];
+  b.p.reset(new char[b.cap]);
   return b;
 }
 
 void DecodePool::give(DecodeBuf&& b) {
-  if (!b.p) return;
-  if (b.cap > (size_t(256) << 20)) {
-    if (b.pinned) pinned_live.fetch_sub(1);
-    b.release();
-    return;
-  }
+  if (!b.p || b.cap > (size_t(256) << 20)) return;
   std::lock_guard<std::mutex> g(m);
-  if (v.size() < 64) {
-    v.push_back(std::move(b));
-    return;
-  }
-  if (b.pinned) pinned_live.fetch_sub(1);
-  b.release();
+  if (v.size() < 64) v.push_back(std::move(b));
 }
 
 void HttpServer::send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body,
@@ -718,7 +676,7 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     if (clen >= (4 << 10)) {
       dec = dpool_->take((size_t)clen + 64);
       st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr,
-                                  dec.p, dec.cap);
+                                  dec.p.get(), dec.cap);
     } else {
       st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
     }

@@ -20,34 +20,14 @@
 namespace lp {
 
 // Uninitialised, recycled storage for a body's `logs` text decoded by the IO thread (no memset of
-// a fresh megabyte per request, as a std::string resize would do). Pinned (page-locked, GPU-mapped)
-// for large bodies when the server feeds a GPU engine: the engine then uses the decoded text as its
-// staging buffer in place (no copy into its own stage).
+// a fresh megabyte per request, as a std::string resize would do).
 struct DecodeBuf {
-  char* p = nullptr;
+  std::unique_ptr<char[]> p;
   size_t cap = 0;
-  bool pinned = false;
-  DecodeBuf() = default;
-  DecodeBuf(const DecodeBuf&) = delete;
-  DecodeBuf& operator=(const DecodeBuf&) = delete;
-  DecodeBuf(DecodeBuf&& o) noexcept : p(o.p), cap(o.cap), pinned(o.pinned) { o.p = nullptr; o.cap = 0; }
-  DecodeBuf& operator=(DecodeBuf&& o) noexcept {
-    if (this != &o) {
-      release();
-      p = o.p; cap = o.cap; pinned = o.pinned;
-      o.p = nullptr; o.cap = 0;
-    }
-    return *this;
-  }
-  ~DecodeBuf() { release(); }
-  void release();
 };
 struct DecodePool {
   std::mutex m;
   std::vector<DecodeBuf> v;
-  std::atomic<int> pinned_live{0};  // pinned buffers in existence (pooled or in flight)
-  std::atomic<int> pinned_limit{0};  // 0: never pinned (set_pinned_decode)
-  size_t pinned_min = 256 << 10;    // bodies at least this large get a pinned buffer
   DecodeBuf take(size_t need);
   void give(DecodeBuf&& b);
 };
@@ -124,11 +104,6 @@ class HttpServer {
   void recycle(std::string&& buf) { pool_->give(std::move(buf)); }
   const std::shared_ptr<BufferPool>& pool() const { return pool_; }
   const std::shared_ptr<DecodePool>& decode_pool() const { return dpool_; }
-  // up to `limit` pinned decode buffers for bodies >= min_bytes (a GPU engine serves this server)
-  void set_pinned_decode(int limit, size_t min_bytes) {
-    dpool_->pinned_limit = limit;
-    dpool_->pinned_min = min_bytes;
-  }
   void stop();
   HttpStats stats;
   HttpStageStats stages;

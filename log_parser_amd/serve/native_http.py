@@ -41,11 +41,6 @@ class NativeHttpFrontend:
                                 quickack=bool(cfg["server.tcp-quickack"]), rcvbuf=int(cfg["server.rcvbuf-bytes"]),
                                 trace=trace, conn_trace=bool(cfg.get("server.stage-timeline", False)))
         self.port = self.srv.port
-        eng = self.svc.engine() if hasattr(self.svc, "engine") else None
-        if eng is not None and eng.device.type == "cuda" and b.pipe is not None:
-            # large bodies are decoded by the IO threads into pinned buffers that the engine stages in
-            # place (Engine._stage_docs): up to 8 such buffers, then pageable ones
-            self.srv.set_pinned_decode(8, 256 << 10)
         self._stop = threading.Event()
         # server.trace-requests: per /parse request on stderr -- receive / validate (native side),
         # queue (body complete -> drained by the pump) and engine (drained -> response queued)

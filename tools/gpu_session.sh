@@ -12,8 +12,8 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run gpu_serv 400 python -u -m pytest tests/test_gpu_serving.py tests/test_serve_procs.py tests/test_native_http.py -m gpu -x -v --timeout 200 --timeout-method thread
-run stages_h 300 python -u tools/parse_stages.py --n 400
-run stages_i 300 python -u tools/parse_stages.py --n 400
-run bench3 300 python -u bench.py --steps 10 --warmup 3
-run stages_j 300 python -u tools/parse_stages.py --n 400
+run bench1 300 python -u bench.py --steps 10 --warmup 3
+run stages_e 300 python -u tools/parse_stages.py --n 400
+run stages_f 300 python -u tools/parse_stages.py --n 400
+run bench2 300 python -u bench.py --steps 10 --warmup 3
+run stages_g 300 python -u tools/parse_stages.py --n 400

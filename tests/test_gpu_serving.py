@@ -106,6 +106,21 @@ def test_native_http_over_gpu_engine_equals_golden(gpu_device):
             assert [(e["lineNumber"], e["context"]) for e in o["events"]] == \
                    [(e["lineNumber"], e["context"]) for e in g["events"]]
             assert o["summary"] == g["summary"]
+        # bodies of 300-500 KB: the logs text decoded by the IO thread while validating, copied by the
+        # packer into the stage (csrc/io/http_server.cpp DecodePool)
+        for i in range(4):
+            logs = make_log(3500 + 500 * i, trig, seed=400 + i, hit_rate=0.05, crlf_rate=0.1) + "\n\ntail é\u2028x"
+            c.request("POST", "/parse", body=json.dumps({"pod": {"metadata": {"name": f"q{i}"}}, "logs": logs}),
+                      headers={"content-type": "application/json"})
+            r = c.getresponse()
+            assert r.status == 200
+            o = json.loads(r.read())
+            g = golden.analyze(logs, sets, params, fz)
+            assert o["metadata"]["totalLines"] == g["metadata"]["totalLines"]
+            assert [(e["lineNumber"], e["context"]) for e in o["events"]] == \
+                   [(e["lineNumber"], e["context"]) for e in g["events"]]
+            assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
+            assert o["summary"] == g["summary"]
         c.close()
     finally:
         fe.close()

@@ -35,6 +35,35 @@ class NativeHttpFrontend:
             b.pipe.timeline = []
         cfg = service.config
         trace = bool(cfg.get("server.trace-requests", False))
+        restore = self._l3_affinity(cfg, io_threads, b)
+        try:
+            self._start(cfg, host, port, io_threads, trace)
+        finally:
+            if restore is not None:
+                os.sched_setaffinity(0, restore)
+        log.info("native HTTP front end on %s:%d (%d IO threads)", host, self.port, io_threads)
+
+    @staticmethod
+    def _l3_affinity(cfg, io_threads: int, b):
+        """``server.l3-affinity``: this (creating) thread moves onto the CPUs of one last-level cache
+        while the IO threads and the pump start -- they inherit it -- and returns the set to restore.
+        Only with a GPU engine in direct mode and an L3 group that holds them all."""
+        if not bool(cfg.get("server.l3-affinity", True)) or b.pipe is None or not hasattr(os, "sched_getaffinity"):
+            return None
+        eng = b.pipe.engine
+        if eng.device.type != "cuda":
+            return None
+        from ..utils.numa import l3_groups
+        allowed = os.sched_getaffinity(0)
+        groups = l3_groups(allowed)
+        if len(groups) < 2 or len(groups[0]) < io_threads + 2:
+            return None
+        os.sched_setaffinity(0, groups[0])
+        log.info("IO threads and pump on the %d CPUs of one L3: %s", len(groups[0]), sorted(groups[0]))
+        return allowed
+
+    def _start(self, cfg, host: str, port: int, io_threads: int, trace: bool) -> None:
+        b = self.svc.batcher()
         self.srv = N.HttpServer(host, port, io_threads, int(cfg["server.max-body-bytes"]),
                                 float(cfg["server.idle-timeout-s"]), io_spin_us=float(cfg["server.io-spin-us"]),
                                 pump_spin_us=float(cfg["server.pump-spin-us"]),
@@ -51,7 +80,6 @@ class NativeHttpFrontend:
         self._pump_s = {"dispatch": 0.0, "complete_inline": 0.0}
         self._t = threading.Thread(target=self._pump, name="lp-http-pump", daemon=True)
         self._t.start()
-        log.info("native HTTP front end on %s:%d (%d IO threads)", host, self.port, io_threads)
 
     def _reply(self, rid: int, r) -> None:
         code, ctype, data = r

@@ -126,6 +126,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)
     "server.idle-timeout-s": (60.0, float),
+    # native front end over a GPU engine: start the IO threads and the pump on the CPUs of ONE last-level
+    # cache (a CCD): the IO thread decodes a request body that the pump then packs -- across CCDs that
+    # hand-off of ~1 MB ran 2-3x slower (profiles/r6_d)
+    "server.l3-affinity": (True, bool),
     # native front end: IO threads poll this long after activity before sleeping in epoll_wait
     "server.io-spin-us": (0.0, float),
     # native front end: the pump polls for the next request this long before sleeping on the queue

@@ -75,6 +75,20 @@ def bind_to_gpu_numa(index: int) -> Optional[Set[int]]:
     return cpus
 
 
+def l3_groups(cpus: Set[int]) -> list:
+    """``cpus`` grouped by shared last-level cache (an EPYC CCD's L3: the cores that exchange a
+    request's bytes cheaply), largest group first; one group when the topology is not visible."""
+    groups = {}
+    for c in sorted(cpus):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                key = frozenset(_parse_cpulist(f.read().strip()))
+        except OSError:
+            key = frozenset()
+        groups.setdefault(key, set()).add(c)
+    return sorted(groups.values(), key=lambda g: (-len(g), min(g)))
+
+
 def cpu_limits() -> dict:
     """The two limits behind ``cpu_budget``: the affinity set and the cgroup CPU quota (None: none)."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)

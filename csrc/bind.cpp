@@ -723,6 +723,39 @@ static py::tuple parse_pod_request_py(py::bytes body, bool two_pass, bool into) 
   return py::make_tuple(st, r.pod_nonnull, name, r.logs_kind, logs);
 }
 
+// The front end's arrival path on one body: logs_prefetch after each prefix length in `cuts`
+// (as the IO thread runs it between reads), then the final parse resuming the prefetch.
+// -> (status, pod_nonnull, pod_name | None, logs_kind, logs bytes | None, prefetch state, prefetched
+// escaped bytes) -- equal to parse_pod_request(body, into=True) in the first five fields
+static py::tuple parse_pod_request_stream_py(py::bytes body, std::vector<size_t> cuts) {
+  char* p = nullptr;
+  Py_ssize_t n = 0;
+  PyBytes_AsStringAndSize(body.ptr(), &p, &n);
+  PodRequest r;
+  LogsPrefetch pf;
+  int st;
+  {
+    py::gil_scoped_release nogil;
+    // each prefix is its own allocation: nothing past the arrived bytes is readable
+    std::unique_ptr<char[]> dst(new char[(size_t)n + 64]);
+    for (size_t c : cuts) {
+      c = std::min(c, (size_t)n);
+      std::unique_ptr<uint8_t[]> pre(new uint8_t[std::max<size_t>(c, 1)]);
+      std::memcpy(pre.get(), p, c);
+      logs_prefetch(pre.get(), c, pf, dst.get(), (size_t)n + 64);
+    }
+    st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(p), (size_t)n, r, dst.get(), (size_t)n + 64, &pf);
+    if (st == JIN_OK && r.logs_kind == 1) {
+      if (!r.logs_decoded) throw std::runtime_error("parse_pod_request_into: logs string not decoded");
+      r.logs.assign(dst.get(), r.logs_dlen);
+    }
+  }
+  py::object name = r.has_name ? py::object(py::str(r.pod_name)) : py::object(py::none());
+  py::object logs = r.logs_kind == 1 ? py::object(py::bytes(r.logs)) : py::object(py::none());
+  return py::make_tuple(st, r.pod_nonnull, name, r.logs_kind, logs, pf.state,
+                        pf.state >= 1 ? pf.src - pf.s0 : (size_t)0);
+}
+
 // ---- DLPack (v0.8 ABI, unversioned "dltensor" capsule) ---------------------------------------
 namespace dl {
 struct Device { int32_t device_type; int32_t device_id; };
@@ -877,6 +910,7 @@ PYBIND11_MODULE(_lpnative, m) {
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false,
         py::arg("into") = false);
+  m.def("parse_pod_request_stream", &parse_pod_request_stream_py, py::arg("body"), py::arg("cuts"));
   // the front end's skip-mode view of a body: (status, logs offset, escaped length, decoded length)
   m.def("pod_logs_span", [](const py::bytes& body) {
     std::string b = body;
@@ -1285,15 +1319,17 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init([](const std::string& host, int port, int io_threads, int64_t max_body, double idle,
                        double io_spin_us, double pump_spin_us, bool quickack, int rcvbuf, bool trace,
-                       bool conn_trace) {
+                       bool conn_trace, bool prefetch) {
              HttpOptions o;
+             o.prefetch = prefetch;
              o.io_spin_us = io_spin_us; o.pump_spin_us = pump_spin_us; o.quickack = quickack; o.rcvbuf = rcvbuf;
              o.trace = trace;
              o.conn_trace = conn_trace;
              return new HttpServer(host, port, io_threads, max_body, idle, o);
            }), py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30,
            py::arg("idle_timeout_s") = 60.0, py::arg("io_spin_us") = 0.0, py::arg("pump_spin_us") = 1000.0,
-           py::arg("quickack") = true, py::arg("rcvbuf") = 0, py::arg("trace") = false, py::arg("conn_trace") = false)
+           py::arg("quickack") = true, py::arg("rcvbuf") = 0, py::arg("trace") = false, py::arg("conn_trace") = false,
+           py::arg("prefetch") = true)
       .def("conn_trace", [](HttpServer& s) {
         std::vector<std::vector<double>> v;
         {
@@ -1417,6 +1453,7 @@ PYBIND11_MODULE(_lpnative, m) {
         d["validate_s"] = g.validate_ns.load() * 1e-9; d["drained"] = g.drained.load();
         d["queue_s"] = g.queue_ns.load() * 1e-9; d["responses"] = g.responses.load();
         d["handoff_s"] = g.handoff_ns.load() * 1e-9; d["sent"] = g.sent.load(); d["send_s"] = g.send_ns.load() * 1e-9;
+        d["prefetch_s"] = g.prefetch_ns.load() * 1e-9; d["prefetched"] = g.prefetched.load();
         return d;
       })
       .def("stop", [](HttpServer& s) {

@@ -31,6 +31,8 @@ namespace lp {
 namespace {
 constexpr size_t kMaxHeader = 64 << 10;
 constexpr int kMaxIo = 255;
+// /parse bodies from this size on have their logs string decoded while they arrive
+constexpr int64_t kPrefetchMin = 64 << 10;
 const char kInvalid[] = "{\"error\":\"Invalid PodFailureData provided\"}";
 const char kUnsupported[] = "{\"error\":\"Content-Type must be application/json\"}";
 
@@ -250,6 +252,8 @@ struct HttpServer::Conn {
   double t_accept = 0, t_parse = 0, t_handoff = 0;   // conn_trace
   int n_recv = 0, n_wake = 0;
   ChunkDecoder chunk;       // Transfer-Encoding: chunked body being received
+  LogsPrefetch pf;          // POST /parse body being received: its logs string decoded so far
+  DecodeBuf pdec;           //   into this buffer (handed to the request when the body completes)
 };
 
 struct HttpServer::Io {
@@ -285,6 +289,7 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
   rcvbuf_ = opt.rcvbuf;
   trace_ = opt.trace;
   conn_trace_ = opt.conn_trace;
+  prefetch_ = opt.prefetch;
   for (int i = 0; i < io_threads; ++i) {
     auto io = std::make_unique<Io>();
     io->index = i;
@@ -634,6 +639,9 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     return false;
   }
   const size_t total = he + 4 + (size_t)clen;
+  const size_t q = path.find('?');
+  const std::string route = q == std::string::npos ? path : path.substr(0, q);
+  const size_t b0 = he + 4;
   if (c->in.size() < total) {
     if (c->in.capacity() < total) c->in.reserve(total);   // one allocation, not log2(n) regrowths
     if (expect && !c->sent_continue) {
@@ -641,13 +649,31 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
       c->sent_continue = true;
       flush(io, c);
     }
+    // a large /parse body: decode the part of its logs string that has arrived now, while this
+    // thread would otherwise wait for the rest (the validation then ends with the last read)
+    if (prefetch_ && te == TE_NONE && clen >= kPrefetchMin && method == "POST" && route == "/parse" && json_ctype &&
+        c->pf.state >= 0 && c->in.size() > b0) {
+      const double t0 = now_s();
+      if (!c->pdec.p) c->pdec = dpool_->take((size_t)clen + 64);
+      logs_prefetch(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, c->in.size() - b0, c->pf, c->pdec.p.get(),
+                    c->pdec.cap);
+      stages.prefetch_ns += (uint64_t)std::max(0.0, (now_s() - t0) * 1e9);
+    }
     return false;
   }
   c->sent_continue = false;
   stats.requests++;
-  const size_t q = path.find('?');
-  const std::string route = q == std::string::npos ? path : path.substr(0, q);
-  const size_t b0 = he + 4;
+  // the body's prefetch state (only for this request: reset whatever the outcome)
+  LogsPrefetch pf = c->pf;
+  DecodeBuf pdec = std::move(c->pdec);
+  c->pf.reset();
+  struct GiveBack {   // a prefetch buffer the request did not take goes back to the pool
+    DecodePool* pool;
+    DecodeBuf& b;
+    ~GiveBack() {
+      if (b.p) pool->give(std::move(b));
+    }
+  } give_back{dpool_.get(), pdec};
   auto consume = [&] { c->in.erase(0, total); };
   if (method == "GET" && route == "/health") {
     consume();
@@ -674,9 +700,11 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     DecodeBuf dec;
     int st;
     if (clen >= (4 << 10)) {
-      dec = dpool_->take((size_t)clen + 64);
+      const bool resume = pdec.p && pf.state >= 1;
+      dec = pdec.p ? std::move(pdec) : dpool_->take((size_t)clen + 64);
       st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr,
-                                  dec.p.get(), dec.cap);
+                                  dec.p.get(), dec.cap, resume ? &pf : nullptr);
+      if (resume) stages.prefetched++;
     } else {
       st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);
     }
@@ -686,8 +714,9 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     stages.receive_ns += (uint64_t)std::max(0.0, (tv - c->t_first) * 1e9);
     stages.validate_ns += (uint64_t)std::max(0.0, (tz - tv) * 1e9);
     if (trace_)
-      fprintf(stderr, "lp-http-trace bytes %zu receive_us %.1f recvs %d wakeups %d validate_us %.1f\n", total,
-              (tv - c->t_first) * 1e6, c->n_recv, c->n_wake, (tz - tv) * 1e6);
+      fprintf(stderr, "lp-http-trace bytes %zu receive_us %.1f recvs %d wakeups %d validate_us %.1f prefetched %zu\n",
+              total, (tv - c->t_first) * 1e6, c->n_recv, c->n_wake, (tz - tv) * 1e6,
+              pf.state >= 1 ? pf.src - pf.s0 : (size_t)0);
     if (st == JIN_OK && (!pr.pod_nonnull || pr.logs_kind != 1)) {
       stats.native_400++;
       consume();

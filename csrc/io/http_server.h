@@ -17,6 +17,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "io/json_in.h"
+
 namespace lp {
 
 // Uninitialised, recycled storage for a body's `logs` text decoded by the IO thread (no memset of
@@ -63,9 +65,11 @@ struct HttpStats {
 // side -- pack / device / emit -- is added by serve/native_http.py): receive = first byte -> body
 // complete, validate = the JSON validation, queue = body complete -> drained by the pump,
 // handoff = respond() -> the IO thread picks the response up, send = picked up -> last byte
-// written to the socket.
+// written to the socket; prefetch = the logs-string decoding done while bodies were arriving
+// (inside `receive`), prefetched = bodies whose final validation resumed a prefetch.
 struct HttpStageStats {
   std::atomic<uint64_t> parse{0}, receive_ns{0}, validate_ns{0}, drained{0}, queue_ns{0};
+  std::atomic<uint64_t> prefetch_ns{0}, prefetched{0};
   std::atomic<uint64_t> responses{0}, handoff_ns{0}, sent{0}, send_ns{0};
 };
 
@@ -78,6 +82,7 @@ struct HttpOptions {
   int rcvbuf = 0;               // SO_RCVBUF of accepted sockets (0 = autotuned)
   bool trace = false;           // per-request receive / validate timings on stderr
   bool conn_trace = false;      // per /parse response: accept / first byte / parsed / handed back / sent times
+  bool prefetch = true;         // decode a large /parse body's logs string while it arrives
 };
 
 class HttpServer {
@@ -132,6 +137,7 @@ class HttpServer {
   double io_spin_s_ = 0;     // HttpOptions (seconds)
   bool trace_ = false;
   bool conn_trace_ = false;
+  bool prefetch_ = true;
   double pump_spin_s_ = 0;
   bool quickack_ = true;
   int rcvbuf_ = 0;

@@ -28,6 +28,7 @@ struct Cur {
   const uint8_t* e;
   int depth = 0;
   bool fallback = false;
+  bool closed = false;   // str_loop consumed the closing quote (span mode: the string ended in the span)
 };
 
 inline void ws(Cur& c) {
@@ -160,6 +161,7 @@ char* str_loop(Cur& c, char* w) {
     const uint8_t b = *c.p;
     if (b == '"') {
       ++c.p;
+      c.closed = true;
       return w;
     }
     if (b < 0x20) return nullptr;  // json.loads(strict=True) rejects raw control characters
@@ -539,19 +541,103 @@ size_t decode_json_string_exact(const uint8_t* p, size_t n, char* w) {
 }
 
 namespace {
-int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap);
-}  // namespace
+int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap,
+                   const LogsPrefetch* pf);
 
-int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs) {
-  return parse_pod_impl(body, n, out, decode_logs, nullptr, 0);
+// Body offset of the opening quote of the top-level `logs` string, found by the validating parser
+// over the prefix [body, body + avail); 0 when the prefix does not reach it (truncated before it,
+// invalid so far, or `logs` not a string). The parser is the one parse_pod_impl runs, so on the
+// same bytes it reaches the same member at the same offset.
+size_t locate_logs(const uint8_t* body, size_t avail) {
+  if (avail >= 2 && (body[0] == 0 || body[1] == 0)) return 0;
+  if (avail >= 3 && body[0] == 0xEF && body[1] == 0xBB && body[2] == 0xBF) return 0;
+  Cur c{body, body + avail};
+  ws(c);
+  if (c.p >= c.e || *c.p != '{') return 0;
+  size_t at = 0;
+  object(c, [&](const std::string& key, Cur& cc) {
+    if (key == "logs" && cc.p < cc.e && *cc.p == '"') {
+      at = (size_t)(cc.p - body);
+      return false;   // stop: the rest of the body has not arrived
+    }
+    return value(cc);
+  });
+  return at;
 }
 
-int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap) {
-  return parse_pod_impl(body, n, out, false, dst, cap);
+// [lo, cut) of a string's content still arriving, moved back so that no escape sequence, \u
+// escape or UTF-8 sequence straddles `cut` (the byte at `cut` must be readable)
+const uint8_t* safe_cut(const uint8_t* lo, const uint8_t* cut) {
+  const uint8_t* b = cut;
+  while (b > lo && b[-1] == '\\') --b;
+  if (((cut - b) & 1) != 0) --cut;                       // odd run: the byte at cut is escaped
+  while (cut > lo && (*cut & 0xC0) == 0x80) --cut;       // inside a UTF-8 sequence
+  for (int k = 1; k <= 4 && cut - k > lo; ++k) {         // inside the 4 hex digits of a \u escape
+    if (cut[-k] == 'u' && cut[-k - 1] == '\\') {
+      const uint8_t* bb = cut - k - 1;
+      size_t run = 0;
+      while (bb - run > lo && bb[-1 - (ptrdiff_t)run] == '\\') ++run;
+      if ((run & 1) == 0) {
+        cut -= k + 1;
+        break;
+      }
+    }
+  }
+  return cut;
+}
+}  // namespace
+
+void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* dst, size_t cap) {
+  if (st.state < 0 || st.state == 2 || !dst) return;
+  if (st.state == 0) {
+    // locate the member at geometrically growing prefixes (the locating parses cost at most twice
+    // the prefix); a body whose `logs` member is not within its first 256 KiB is not prefetched
+    if (st.tries > 0 && avail < 2 * st.tried_at) return;
+    if (st.tried_at > (256u << 10)) {
+      st.state = -1;
+      return;
+    }
+    ++st.tries;
+    st.tried_at = avail;
+    const size_t at = locate_logs(body, avail);
+    if (at == 0) return;
+    st.state = 1;
+    st.s0 = at;
+    st.src = at + 1;
+    st.dlen = 0;
+  }
+  // decode [src, cut): 8 bytes stay behind the arrival front so the cut test reads arrived bytes
+  if (avail < st.src + 64 + 8) return;
+  const uint8_t* lo = body + st.s0 + 1;
+  const uint8_t* cut = safe_cut(lo, body + avail - 8);
+  if (cut <= body + st.src) return;
+  if ((size_t)(cut - lo) + 64 > cap) {
+    st.state = -1;
+    return;
+  }
+  Cur c{body + st.src, cut};
+  char* w = str_into_span(c, dst + st.dlen);
+  if (!w) {        // invalid or json.loads territory: the final parse decides (and answers)
+    st.state = -1;
+    return;
+  }
+  st.dlen = (size_t)(w - dst);
+  st.src = (size_t)(c.p - body);
+  if (c.closed) st.state = 2;
+}
+
+int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs) {
+  return parse_pod_impl(body, n, out, decode_logs, nullptr, 0, nullptr);
+}
+
+int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap,
+                           const LogsPrefetch* pf) {
+  return parse_pod_impl(body, n, out, false, dst, cap, pf && pf->state >= 1 ? pf : nullptr);
 }
 
 namespace {
-int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap) {
+int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap,
+                   const LogsPrefetch* pf) {
   out = PodRequest{};
   if (n >= 2 && (body[0] == 0 || body[1] == 0)) return JIN_FALLBACK;      // UTF-16/32
   if (n >= 3 && body[0] == 0xEF && body[1] == 0xBB && body[2] == 0xBF) return JIN_FALLBACK;  // BOM
@@ -569,9 +655,16 @@ int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_l
     if (key == "logs") {
       if (cc.p < cc.e && *cc.p == '"' && dst && (size_t)(cc.e - cc.p) + 64 <= cap) {
         // validated and decoded in one pass into the caller's buffer (a later duplicate key
-        // overwrites it: the last one wins, as in json.loads)
+        // overwrites it: the last one wins, as in json.loads). A prefix decoded while the body
+        // arrived (logs_prefetch, same member: same offset) resumes at its end.
         const uint8_t* s0 = cc.p;
-        char* end = str_into(cc, dst);
+        char* end;
+        if (pf && (size_t)(s0 - body) == pf->s0 && pf->src <= n) {
+          cc.p = body + pf->src;
+          end = pf->state == 2 ? dst + pf->dlen : str_loop<false>(cc, dst + pf->dlen);
+        } else {
+          end = str_into(cc, dst);
+        }
         if (!end) {
           out.logs_decoded = false;
           return false;

@@ -25,11 +25,34 @@ struct PodRequest {
 // into a Python bytes object -- the HTTP front end's one-copy path).
 int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs = true);
 
+// Decoding of the top-level `logs` string while a body is still arriving (the HTTP front end's IO
+// thread between reads: the 1 MB string's validation and unescaping overlap the receive instead of
+// following its last byte). The prefix [s0 + 1, src) of the string is decoded to dst[0, dlen);
+// `src` is always a token boundary, so the final parse resumes there and produces exactly the
+// bytes and verdict of a one-pass parse. Nothing here decides a request: an invalid or unusual
+// prefix only turns the prefetch off (state -1), and the final parse answers.
+struct LogsPrefetch {
+  int state = 0;        // 0 locating the member, 1 decoding, 2 closing quote consumed, -1 off
+  int tries = 0;        // locate attempts (at prefixes of doubling length)
+  size_t tried_at = 0;  // bytes available at the last attempt
+  size_t s0 = 0;        // body offset of the string's opening quote
+  size_t src = 0;       // body offset decoded up to (state 2: one past the closing quote)
+  size_t dlen = 0;      // decoded bytes in dst
+  void reset() { *this = LogsPrefetch(); }
+};
+
+// Advances `st` over the first `avail` arrived bytes of a body. `dst` / `cap` as for
+// parse_pod_request_into (the same buffer must be passed there with `st`).
+void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* dst, size_t cap);
+
 // Validates the whole body like parse_pod_request and decodes the `logs` string into `dst` in the
 // same pass (the HTTP front end's IO thread, while the bytes are in its cache): logs_decoded is set
 // and logs_dlen is the decoded length. `dst` needs room for the escaped length + 64 bytes (block
 // stores run past the decoded end); a string that does not fit is only validated (skip mode).
-int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap);
+// With `pf` (a logs_prefetch state over a prefix of this body, into this dst) the string's
+// decoding resumes where the prefetch stopped.
+int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap,
+                           const LogsPrefetch* pf = nullptr);
 
 // Unescapes the content of a JSON string that parse_pod_request validated (`n` raw bytes between
 // the quotes) into `w`, which must have room for n + 64 bytes; returns the decoded length.

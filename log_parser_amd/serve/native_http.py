@@ -68,7 +68,8 @@ class NativeHttpFrontend:
                                 float(cfg["server.idle-timeout-s"]), io_spin_us=float(cfg["server.io-spin-us"]),
                                 pump_spin_us=float(cfg["server.pump-spin-us"]),
                                 quickack=bool(cfg["server.tcp-quickack"]), rcvbuf=int(cfg["server.rcvbuf-bytes"]),
-                                trace=trace, conn_trace=bool(cfg.get("server.stage-timeline", False)))
+                                trace=trace, conn_trace=bool(cfg.get("server.stage-timeline", False)),
+                                prefetch=bool(cfg["server.prefetch-logs"]))
         self.port = self.srv.port
         self._stop = threading.Event()
         # server.trace-requests: per /parse request on stderr -- receive / validate (native side),

@@ -130,6 +130,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # cache (a CCD): the IO thread decodes a request body that the pump then packs -- across CCDs that
     # hand-off of ~1 MB ran 2-3x slower (profiles/r6_d)
     "server.l3-affinity": (True, bool),
+    # native front end: a POST /parse body of >= 64 KiB has its `logs` string validated and decoded
+    # by the IO thread between reads while it arrives; the final parse resumes there (csrc/io/json_in.h
+    # LogsPrefetch). The request's verdict (400 / 200) is still the final parse's.
+    "server.prefetch-logs": (True, bool),
     # native front end: IO threads poll this long after activity before sleeping in epoll_wait
     "server.io-spin-us": (0.0, float),
     # native front end: the pump polls for the next request this long before sleeping on the queue

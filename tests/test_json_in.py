@@ -139,3 +139,81 @@ def test_decoded_length_and_exact_decoder():
             assert dlen == len(want), (n, ensure_ascii)
             got, intact = N.decode_json_exact(body[off:off + ln])
             assert got == want and intact, (n, ensure_ascii)
+
+
+def _stream_cuts(rng, n):
+    """Arrival prefix lengths of an n-byte body: a few large reads, many tiny ones, or every byte."""
+    k = rng.randrange(3)
+    if k == 0:
+        cuts = sorted(rng.sample(range(n + 1), min(n + 1, rng.randint(1, 12))))
+    elif k == 1:
+        cuts, c = [], 0
+        while c < n:
+            c += rng.randint(1, 300)
+            cuts.append(min(c, n))
+    else:
+        cuts = list(range(0, n + 1, max(1, n // 400)))
+    return cuts
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_logs_prefetch_while_arriving_equals_one_pass(seed):
+    """The HTTP IO thread decodes a /parse body's logs string between reads (logs_prefetch) and the
+    final parse resumes there: for any arrival pattern -- reads ending inside escapes, backslash runs,
+    \\u escapes, UTF-8 sequences, before / inside / after the string -- the status, pod fields and
+    decoded bytes equal the one-pass parse, and invalid bodies (also ones made invalid by the LAST
+    byte) get the same verdict. Most valid bodies are really resumed (prefetch state >= 1)."""
+    rng = random.Random(100 + seed)
+    atoms = ["a" * 70, "line of text ", "\n", "\r\n", '"', "\\", "\\\\", "/", "\t", "é", "€", "😀", "日本",
+             "\x7f", "z" * 130]
+    resumed = 0
+    for it in range(250):
+        s = "".join(rng.choice(atoms) for _ in range(rng.randint(0, 160)))
+        d = {}
+        for key in rng.sample(["pod", "logs", "x"], 3):
+            if key == "pod":
+                d[key] = rng.choice([{"metadata": {"name": "p-" + str(it)}}, None, {"spec": _rand_value(rng)}])
+            elif key == "logs":
+                d[key] = s
+            else:
+                d[key] = _rand_value(rng)
+        body = json.dumps(d, ensure_ascii=rng.random() < 0.3).encode()
+        k = rng.random()
+        if k < 0.1:                                   # invalid at the last byte
+            body = body[:-1] + rng.choice([b"]", b",", b"x"])
+        elif k < 0.15:                                # duplicate member after the string
+            body = body[:-1] + b', "logs": "dup\\nlast"}'
+        elif k < 0.2 and len(body) > 10:              # a control byte inside the string
+            i = body.find(b'"logs"')
+            if i >= 0:
+                j = body.find(b'"', i + 7) + 1 + rng.randrange(max(1, len(s) // 2 + 1))
+                body = body[:j] + b"\x01" + body[j:]
+        want = N.parse_pod_request(body, False, True)
+        got = N.parse_pod_request_stream(body, _stream_cuts(rng, len(body)))
+        assert tuple(got[:5]) == tuple(want), (body[:120], got[:5], want)
+        if want[0] == 0 and want[3] == 1 and got[5] >= 1:
+            resumed += 1
+    assert resumed > 50
+
+
+def test_logs_prefetch_large_body_every_boundary():
+    """A 200 KB log string (escapes every ~100 bytes, multi-byte characters, \\u escapes) arriving in
+    reads of every length 1..67 bytes around its escapes decodes identically and is prefetched to its
+    closing quote once the last read is in."""
+    rng = random.Random(3)
+    atoms = ["INFO service started ok ", "\n", "\r\n", "é", "€", "\\", '"', "\t", "😀", "\x00"]
+    s = "".join(rng.choice(atoms) for _ in range(25_000))
+    body = json.dumps({"pod": {"metadata": {"name": "big"}}, "logs": s}, ensure_ascii=False).encode()
+    want = N.parse_pod_request(body, False, True)
+    assert want[0] == 0 and want[4] == s.encode()
+    for step in (1, 7, 64, 67, 4096, 65536):
+        cuts = list(range(0, len(body), step)) if step > 1 else list(range(0, 3000)) + [len(body) - 1]
+        got = N.parse_pod_request_stream(body, cuts)
+        assert tuple(got[:5]) == tuple(want), step
+        assert got[5] >= 1 and got[6] > len(body) // 2 if step > 1 else got[5] >= 1
+    # \u escapes (ensure_ascii): reads ending inside the 4 hex digits
+    body = json.dumps({"pod": {}, "logs": s.replace("😀", "")}, ensure_ascii=True).encode()
+    want = N.parse_pod_request(body, False, True)
+    for off in range(0, 12):
+        got = N.parse_pod_request_stream(body, list(range(off, len(body), 61)))
+        assert tuple(got[:5]) == tuple(want), off

@@ -241,6 +241,58 @@ def test_chunked_bodies_equal_content_length(server):
     assert st == 200 and "analysisId" in json.loads(out)
 
 
+def test_large_body_decoded_while_arriving(server):
+    """A >= 64 KiB /parse body is validated and decoded by the IO thread between reads (LogsPrefetch,
+    server.prefetch-logs): delivered in slow segments that end inside escapes and multi-byte
+    characters, it answers the same AnalysisResult as the body sent at once, and the prefetch really
+    ran (stage counter). A body that becomes invalid only at its LAST byte still answers the
+    reference's 400 (Parse.java:45-49) and records nothing in the frequency window."""
+    import time
+    fe, _, trig = server
+    logs = make_log(2500, trig, seed=31, hit_rate=0.05) + '\n"quoted" \\ tab\t é€😀 end'
+    body = json.dumps({"pod": {"metadata": {"name": "big"}}, "logs": logs}, ensure_ascii=False).encode()
+    assert len(body) >= 64 << 10
+    hdr = b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+
+    def ask(b, seg=None):
+        s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+        raw = hdr % len(b) + b
+        if seg:
+            i = 0
+            while i < len(raw):
+                n = seg[i % len(seg)]
+                s.sendall(raw[i:i + n])
+                i += n
+                time.sleep(0.0005)
+        else:
+            s.sendall(raw)
+        (st, out), = _recv_responses(s, 1)
+        s.close()
+        return st, out
+
+    _raw(fe.port, b"DELETE /admin/frequency HTTP/1.1\r\nHost: x\r\n\r\n")
+    st, ref = ask(body)
+    assert st == 200
+    ref = _strip(json.loads(ref))
+    assert ref["summary"]["significantEvents"] > 0 and ref["metadata"]["totalLines"] == logs.count("\n") + 1
+    before = fe.srv.stage_stats()["prefetched"]
+    for seg in ([4093], [1, 2, 3, 997, 65536], [12289, 7, 8191]):
+        _raw(fe.port, b"DELETE /admin/frequency HTTP/1.1\r\nHost: x\r\n\r\n")
+        st, out = ask(body, seg)
+        assert st == 200 and _strip(json.loads(out)) == ref, seg
+    assert fe.srv.stage_stats()["prefetched"] >= before + 3
+    # invalid at the last byte: 400, and the frequency window is exactly as before
+    c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=60)
+    c.request("GET", "/admin/frequency")
+    win0 = c.getresponse().read()
+    for bad in (body[:-1] + b"]", body[:-1], body + b"x"):
+        st, out = ask(bad, [8191, 3])
+        assert (st, out) == (400, b'{"error":"Invalid PodFailureData provided"}'), bad[-8:]
+    c.request("GET", "/admin/frequency")
+    assert c.getresponse().read() == win0
+    c.close()
+
+
 def test_chunked_errors(server):
     """Malformed chunked framing -> 400 (connection closed); a decoded size above
     server.max-body-bytes -> 413 (the encoded size does not count); codings other than chunked /

@@ -12,15 +12,8 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-python - > gpurun_out/s_topo.log 2>&1 <<'PY'
-import os
-from log_parser_amd.utils.numa import l3_groups, gpu_numa_cpus, cpu_limits
-a = os.sched_getaffinity(0)
-print("allowed", len(a), "limits", cpu_limits(), "gpu0 node cpus", len(gpu_numa_cpus(0)))
-print("l3 groups of gpu0 node cpus", [len(g) for g in l3_groups(gpu_numa_cpus(0) & a)][:16])
-PY
 for k in 1 2 3; do
-  run l3_$k 300 python -u tools/parse_stages.py --n 400
-  run nol3_$k 300 python -u tools/parse_stages.py --n 400 -D server.l3-affinity=false
+  run pf_$k 300 python -u tools/parse_stages.py --n 400
+  run nopf_$k 300 python -u tools/parse_stages.py --n 400 -D server.prefetch-logs=false
 done
-run bench4 300 python -u bench.py --steps 10 --warmup 3
+run bench5 300 python -u bench.py --steps 10 --warmup 3

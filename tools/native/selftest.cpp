@@ -13,7 +13,10 @@
 //    thread playing the Python side and 8 client threads on keep-alive connections (TSan watches
 //    the queue / outbox / eventfd hand-offs, ASan the connection lifetime).
 #include <cstdio>
+#include <chrono>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <random>
 #include <string>
 #include <vector>
@@ -142,6 +145,97 @@ static void fuzz_json_in(int iters, uint32_t seed) {
   }
 }
 
+// logs_prefetch over exact-size prefix copies (ASan flags a read past the arrived bytes), then the
+// resumed final parse: same status and bytes as the one-pass parse
+static void fuzz_prefetch(int iters, uint32_t seed) {
+  std::mt19937 rng(seed);
+  static const char* atoms[] = {"abc ", "\\n", "\\\\", "\\\"", "\\u00e9", "\\u20AC", "\xc3\xa9", "\xf0\x9f\x98\x80",
+                                "xxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxx", "\\t", "\x01", "\\q"};
+  int resumed = 0;
+  for (int it = 0; it < iters; ++it) {
+    std::string logs;
+    const int na = (int)(rng() % 400);
+    const size_t nat = sizeof(atoms) / sizeof(atoms[0]) - (rng() % 8 ? 2 : 0);   // 1 in 8: invalid atoms too
+    for (int a = 0; a < na; ++a) logs += atoms[rng() % nat];
+    std::string body = "{\"pod\":{\"metadata\":{\"name\":\"p\"}},\"logs\":\"" + logs + "\"}";
+    if (rng() % 10 == 0) body.back() = ']';
+    const size_t n = body.size();
+    std::unique_ptr<char[]> d1(new char[n + 64]), d2(new char[n + 64]);
+    PodRequest r1, r2;
+    const int s1 = parse_pod_request_into(reinterpret_cast<const uint8_t*>(body.data()), n, r1, d1.get(), n + 64);
+    LogsPrefetch pf;
+    size_t at = 0;
+    while (at < n) {
+      at = std::min(n, at + 1 + (size_t)(rng() % (rng() % 4 ? 97 : 4000)));
+      std::vector<uint8_t> pre(body.begin(), body.begin() + (ptrdiff_t)at);
+      logs_prefetch(pre.data(), pre.size(), pf, d2.get(), n + 64);
+    }
+    const int s2 = parse_pod_request_into(reinterpret_cast<const uint8_t*>(body.data()), n, r2, d2.get(), n + 64, &pf);
+    CHECK(s1 == s2 && r1.logs_kind == r2.logs_kind, "prefetch status %d vs %d", s2, s1);
+    if (s1 == JIN_OK && r1.logs_kind == 1) {
+      CHECK(r1.logs_dlen == r2.logs_dlen && memcmp(d1.get(), d2.get(), r1.logs_dlen) == 0, "prefetch bytes differ");
+      resumed += pf.state >= 1;
+    }
+  }
+  CHECK(resumed > iters / 2, "prefetch resumed only %d of %d", resumed, iters);
+  std::printf("prefetch: %d bodies, %d resumed\n", iters, resumed);
+}
+
+// large /parse bodies written in small pieces with pauses: the IO thread prefetches between reads
+static void http_prefetch_selftest(int rounds) {
+  HttpServer srv("127.0.0.1", 0, 2, 8 << 20);
+  std::atomic<bool> done{false};
+  std::thread responder([&] {
+    while (!done)
+      for (auto& r : srv.next_requests(16, 20)) {
+        const size_t n = r.kind == 0 && r.dec.p ? r.logs_dlen : (size_t)-1;
+        const uint64_t h = n == (size_t)-1 ? 0 : std::hash<std::string>()(std::string(r.dec.p.get(), n));
+        srv.respond(r.id, 200, "application/json", "{\"n\":" + std::to_string(n) + ",\"h\":" + std::to_string(h) + "}");
+      }
+  });
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)srv.port());
+  inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+  int ok = 0;
+  if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0) {
+    for (int i = 0; i < rounds; ++i) {
+      std::string logs, raw;
+      for (int k = 0; k < 3000 + 500 * i; ++k) {
+        logs += "ERROR line " + std::to_string(k) + " \xc3\xa9\"q\"\n";
+        raw += "ERROR line " + std::to_string(k) + " \xc3\xa9\\\"q\\\"\\n";
+      }
+      const std::string body = "{\"pod\":{},\"logs\":\"" + raw + "\"}";
+      const std::string req = "POST /parse HTTP/1.1\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+      size_t off = 0;
+      while (off < req.size()) {
+        const size_t k = std::min(req.size() - off, (size_t)(1000 + 7919 * (off % 13)));
+        if (send(fd, req.data() + off, k, 0) != (ssize_t)k) break;
+        off += k;
+        if (off % 5 == 0) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+      std::string resp;
+      char b[4096];
+      while (resp.find("\r\n\r\n") == std::string::npos || resp.back() != '}') {
+        const ssize_t k = recv(fd, b, sizeof(b), 0);
+        if (k <= 0) break;
+        resp.append(b, (size_t)k);
+      }
+      const std::string want = "{\"n\":" + std::to_string(logs.size()) + ",\"h\":" + std::to_string(std::hash<std::string>()(logs)) + "}";
+      ok += resp.rfind(want) != std::string::npos;
+    }
+    close(fd);
+  }
+  done = true;
+  responder.join();
+  const uint64_t pre = srv.stages.prefetched.load();
+  srv.stop();
+  CHECK(ok == rounds, "http prefetch: %d of %d responses", ok, rounds);
+  CHECK(pre > 0, "http prefetch: no body was prefetched");
+  std::printf("http prefetch: %d large bodies, %llu prefetched\n", ok, (unsigned long long)pre);
+}
+
 static void http_selftest(int rounds) {
   HttpServer srv("127.0.0.1", 0, 2, 1 << 20);
   std::atomic<bool> done{false};
@@ -203,7 +297,9 @@ int main(int argc, char** argv) {
   fuzz_regex(iters, 12345);
   docs_threads(777);
   fuzz_json_in(iters * 10, 4242);
+  fuzz_prefetch(iters / 3 + 50, 99);
   http_selftest(iters / 20 + 10);
+  http_prefetch_selftest(12);
   const uint8_t t[] = {'a', 0xE2, 0x80, 0xA8};
   CHECK(final_terminator_len(t, 4) == 3, "U+2028 final terminator");
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);

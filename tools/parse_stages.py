@@ -54,6 +54,7 @@ def main():
             cnt = {"receive_s": "parse", "validate_s": "parse", "queue_s": "drained", "handoff_s": "responses",
                    "send_s": "sent"}.get(k, "parse")
             nat[k[:-2] + "_us"] = round(1e6 * (v - bn.get(k, 0.0)) / max(an.get(cnt, 0) - bn.get(cnt, 0), 1), 1)
+    nat["prefetched"] = an.get("prefetched", 0) - bn.get("prefetched", 0)
     print(json.dumps({"requests": n, "p50_ms": round(float(np.median(lat)), 3),
                       "p99_ms": round(float(np.percentile(lat, 99)), 3), "wall_s": round(wall, 3),
                       "native": nat, "server_threads": per, "overrides": a.D}), flush=True)

@@ -563,7 +563,7 @@ struct RawLogs {
 };
 
 static py::bytes raw_logs_decode(const RawLogs& r) {
-  if (r.decoded()) return py::bytes(r.dec.p.get(), r.dlen);
+  if (r.decoded()) return py::bytes(r.dec.p, r.dlen);
   PyObject* b = PyBytes_FromStringAndSize(nullptr, (Py_ssize_t)(r.len + 64));
   if (!b) throw py::error_already_set();
   size_t n;
@@ -591,11 +591,20 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   // copy + newline scan pass into the stage, no unescape on this thread)
   bool predecoded = raw;
   for (int64_t i = 0; i < D && predecoded; ++i) predecoded = docs[i].cast<const RawLogs&>().decoded();
+  // ... whose decoder recorded the newline positions: no newline scan either
+  std::vector<const int64_t*> nlp;
+  std::vector<int64_t> nlc;
   if (predecoded) {
+    nlp.assign(D, nullptr);
+    nlc.assign(D, 0);
     for (int64_t i = 0; i < D; ++i) {
       const RawLogs& r = docs[i].cast<const RawLogs&>();
-      src[i] = r.dec.p.get();
+      src[i] = r.dec.p;
       off[i + 1] = off[i] + (int64_t)r.dlen;
+      if (r.dec.has_nl) {
+        nlp[i] = r.dec.nl.p ? r.dec.nl.p.get() : reinterpret_cast<const int64_t*>(&nlc[i]);   // (non-null: none)
+        nlc[i] = (int64_t)r.dec.nl.n;
+      }
     }
     raw = false;
   }
@@ -620,7 +629,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
         std::atomic<bool> bad{false};
         HostPool::get().run(D, std::max(1, nthreads), [&](int64_t i) {
           if (rl[i]->decoded()) {             // (a mix: this one was decoded by the IO thread)
-            std::memcpy(d + off[i], rl[i]->dec.p.get(), rl[i]->dlen);
+            std::memcpy(d + off[i], rl[i]->dec.p, rl[i]->dlen);
             return;
           }
           const size_t k = rl[i]->len ? decode_json_string_exact(rl[i]->data(), rl[i]->len,
@@ -633,7 +642,7 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
       if (!known) {
         for (int64_t i = 0; i < D; ++i) {
           if (rl[i]->decoded()) {
-            std::memcpy(d + off[i], rl[i]->dec.p.get(), rl[i]->dlen);
+            std::memcpy(d + off[i], rl[i]->dec.p, rl[i]->dlen);
             off[i + 1] = off[i] + (int64_t)rl[i]->dlen;
             continue;
           }
@@ -672,7 +681,8 @@ static py::object pack_split_docs_py(py::list docs, uint64_t dst, int64_t cap, i
   }
   {
     py::gil_scoped_release nogil;   // `docs` keeps every buffer alive
-    pack_split_docs(src.data(), off.data(), D, P<uint8_t>(dst), nthreads, ix);
+    pack_split_docs(src.data(), off.data(), D, P<uint8_t>(dst), nthreads, ix, int64_t(4) << 20,
+                    nlp.empty() ? nullptr : nlp.data(), nlc.empty() ? nullptr : nlc.data());
   }
   // hand the native buffers to numpy (capsule owns them): no copy of the line index
   auto own = [](auto& buf) {
@@ -726,13 +736,15 @@ static py::tuple parse_pod_request_py(py::bytes body, bool two_pass, bool into) 
 // The front end's arrival path on one body: logs_prefetch after each prefix length in `cuts`
 // (as the IO thread runs it between reads), then the final parse resuming the prefetch.
 // -> (status, pod_nonnull, pod_name | None, logs_kind, logs bytes | None, prefetch state, prefetched
-// escaped bytes) -- equal to parse_pod_request(body, into=True) in the first five fields
+// escaped bytes, the decoder's '\n' positions) -- equal to parse_pod_request(body, into=True) in the
+// first five fields
 static py::tuple parse_pod_request_stream_py(py::bytes body, std::vector<size_t> cuts) {
   char* p = nullptr;
   Py_ssize_t n = 0;
   PyBytes_AsStringAndSize(body.ptr(), &p, &n);
   PodRequest r;
   LogsPrefetch pf;
+  NlPos nl;
   int st;
   {
     py::gil_scoped_release nogil;
@@ -742,9 +754,10 @@ static py::tuple parse_pod_request_stream_py(py::bytes body, std::vector<size_t>
       c = std::min(c, (size_t)n);
       std::unique_ptr<uint8_t[]> pre(new uint8_t[std::max<size_t>(c, 1)]);
       std::memcpy(pre.get(), p, c);
-      logs_prefetch(pre.get(), c, pf, dst.get(), (size_t)n + 64);
+      logs_prefetch(pre.get(), c, pf, dst.get(), (size_t)n + 64, &nl);
     }
-    st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(p), (size_t)n, r, dst.get(), (size_t)n + 64, &pf);
+    st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(p), (size_t)n, r, dst.get(), (size_t)n + 64, &pf,
+                                &nl);
     if (st == JIN_OK && r.logs_kind == 1) {
       if (!r.logs_decoded) throw std::runtime_error("parse_pod_request_into: logs string not decoded");
       r.logs.assign(dst.get(), r.logs_dlen);
@@ -752,8 +765,9 @@ static py::tuple parse_pod_request_stream_py(py::bytes body, std::vector<size_t>
   }
   py::object name = r.has_name ? py::object(py::str(r.pod_name)) : py::object(py::none());
   py::object logs = r.logs_kind == 1 ? py::object(py::bytes(r.logs)) : py::object(py::none());
+  std::vector<int64_t> nlv(nl.p.get(), nl.p.get() + (st == JIN_OK && r.logs_kind == 1 ? nl.n : 0));
   return py::make_tuple(st, r.pod_nonnull, name, r.logs_kind, logs, pf.state,
-                        pf.state >= 1 ? pf.src - pf.s0 : (size_t)0);
+                        pf.state >= 1 ? pf.src - pf.s0 : (size_t)0, nlv);
 }
 
 // ---- DLPack (v0.8 ABI, unversioned "dltensor" capsule) ---------------------------------------
@@ -906,6 +920,7 @@ PYBIND11_MODULE(_lpnative, m) {
   m.def("set_scan_defer_rare", &set_scan_defer_rare);
   m.def("set_cand_verify_split", &set_cand_verify_split);
   m.def("set_summ_select", &set_summ_select);
+  m.def("set_small_profile", &set_small_profile);
   m.def("pack_split_docs", &pack_split_docs_py, py::arg("docs"), py::arg("dst"), py::arg("cap"),
         py::arg("nthreads") = 8, py::arg("idx") = 0, py::arg("idx_cap") = 0);
   m.def("parse_pod_request", &parse_pod_request_py, py::arg("body"), py::arg("two_pass") = false,
@@ -1314,7 +1329,14 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<RawLogs>(m, "RawLogs")
       .def("__len__", [](const RawLogs& r) { return r.len; })
       .def("decode", &raw_logs_decode, "the unescaped UTF-8 log text")
-      .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; });
+      .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; })
+      // decoded by the IO thread into a pinned buffer: (address, capacity) -- the engine stages this
+      // request in place; (0, 0) otherwise
+      .def_property_readonly("pinned_text", [](const RawLogs& r) {
+        const bool pin = r.decoded() && r.dec.pinned;
+        return py::make_tuple(pin ? reinterpret_cast<uint64_t>(r.dec.p) : uint64_t(0),
+                              pin ? (uint64_t)r.dec.cap : uint64_t(0));
+      });
 
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init([](const std::string& host, int port, int io_threads, int64_t max_body, double idle,
@@ -1341,6 +1363,18 @@ PYBIND11_MODULE(_lpnative, m) {
         return a;
       })
       .def_property_readonly("port", &HttpServer::port)
+      .def("set_pinned_decode", [](HttpServer& s, int limit, size_t min_bytes) {
+             s.set_pinned_decode(limit, min_bytes,
+                                 [](size_t n) -> void* {
+                                   void* q = nullptr;
+                                   if (hipHostMalloc(&q, n, hipHostMallocDefault) != hipSuccess) {
+                                     (void)hipGetLastError();
+                                     return nullptr;
+                                   }
+                                   return q;
+                                 },
+                                 [](void* q) { (void)hipHostFree(q); });
+           }, py::arg("limit"), py::arg("min_bytes") = size_t(256) << 10)
       .def("pending", &HttpServer::pending)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms, bool raw) {
         std::vector<HttpRequest> v;
@@ -1390,7 +1424,7 @@ PYBIND11_MODULE(_lpnative, m) {
           for (size_t i = 0; i < v.size(); ++i)
             if (v[i].kind == 0) {
               if (v[i].dec.p) {
-                std::memcpy(PyBytes_AS_STRING(bufs[i]), v[i].dec.p.get(), v[i].logs_dlen);
+                std::memcpy(PyBytes_AS_STRING(bufs[i]), v[i].dec.p, v[i].logs_dlen);
                 lens[i] = v[i].logs_dlen;
                 s.decode_pool()->give(std::move(v[i].dec));
               } else {

@@ -44,8 +44,11 @@ struct DocBatchIndex {
 };
 
 // src[d], len[d]: document bytes; dst receives them back to back at doc_off (D+1, prefix sums).
-// nthreads <= 1 runs inline.
+// nthreads <= 1 runs inline. nlpos[d] (optional, non-null per document): the positions of document
+// d's '\n' bytes, nlcnt[d] of them, already known (the HTTP front end's decoder recorded them) --
+// that document is copied without a newline scan.
 void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, uint8_t* dst, int nthreads,
-                     DocBatchIndex& out, int64_t min_bytes_per_thread = int64_t(4) << 20);
+                     DocBatchIndex& out, int64_t min_bytes_per_thread = int64_t(4) << 20,
+                     const int64_t* const* nlpos = nullptr, const int64_t* nlcnt = nullptr);
 
 }  // namespace lp

@@ -453,26 +453,64 @@ void BufferPool::give(std::string&& buf) {
 
 std::string HttpServer::take_buffer() { return pool_->take(); }
 
+void DecodeBuf::release() {
+  if (!p) return;
+  if (pinned)
+    pfree(p);
+  else
+    delete[] p;
+  p = nullptr;
+  cap = 0;
+}
+
 DecodeBuf DecodePool::take(size_t need) {
+  const bool want_pinned = pinned_limit.load() > 0 && need >= pinned_min;
   {
     std::lock_guard<std::mutex> g(m);
-    for (size_t i = v.size(); i-- > 0;)
-      if (v[i].cap >= need) {
-        DecodeBuf b = std::move(v[i]);
-        v.erase(v.begin() + (std::ptrdiff_t)i);
-        return b;
-      }
+    // a pooled buffer that fits: pinned first when wanted (the engine stages in place)
+    int best = -1;
+    for (int i = (int)v.size() - 1; i >= 0; --i) {
+      if (v[i].cap < need) continue;
+      if (best < 0 || (v[i].pinned == want_pinned && v[best].pinned != want_pinned)) best = i;
+    }
+    if (best >= 0 && (v[best].pinned || !want_pinned || pinned_live.load() >= pinned_limit.load())) {
+      DecodeBuf b = std::move(v[best]);
+      v.erase(v.begin() + best);
+      b.has_nl = false;
+      return b;
+    }
   }
   DecodeBuf b;
+  if (want_pinned && pinned_live.fetch_add(1) < pinned_limit.load()) {
+    // room for the engine's staging layout behind the text: padding, the line index (~12 bytes a
+    // line), segments and counters (request.cpp single-copy upload)
+    const size_t cap = (need + need / 4 + (96 << 10) + 4095) & ~size_t(4095);
+    if (void* q = palloc(cap)) {
+      b.p = static_cast<char*>(q);
+      b.cap = cap;
+      b.pinned = true;
+      b.pfree = pfree;
+      return b;
+    }
+    pinned_limit = 0;                      // no pinned memory here: pageable from now on
+  }
+  if (want_pinned) pinned_live.fetch_sub(1);
   b.cap = std::max<size_t>(need + need / 8, 64 << 10);
-  b.p.reset(new char[b.cap]);
+  b.p = new char[b.cap];
   return b;
 }
 
 void DecodePool::give(DecodeBuf&& b) {
-  if (!b.p || b.cap > (size_t(256) << 20)) return;
-  std::lock_guard<std::mutex> g(m);
-  if (v.size() < 64) v.push_back(std::move(b));
+  if (!b.p) return;
+  if (b.cap <= (size_t(256) << 20)) {
+    std::lock_guard<std::mutex> g(m);
+    if (v.size() < 64) {
+      v.push_back(std::move(b));
+      return;
+    }
+  }
+  if (b.pinned) pinned_live.fetch_sub(1);
+  b.release();
 }
 
 void HttpServer::send_now(Io* io, Conn* c, int status, const std::string& ctype, const std::string& body,
@@ -655,8 +693,8 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
         c->pf.state >= 0 && c->in.size() > b0) {
       const double t0 = now_s();
       if (!c->pdec.p) c->pdec = dpool_->take((size_t)clen + 64);
-      logs_prefetch(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, c->in.size() - b0, c->pf, c->pdec.p.get(),
-                    c->pdec.cap);
+      logs_prefetch(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, c->in.size() - b0, c->pf, c->pdec.p,
+                    c->pdec.cap, &c->pdec.nl);
       stages.prefetch_ns += (uint64_t)std::max(0.0, (now_s() - t0) * 1e9);
     }
     return false;
@@ -703,7 +741,8 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
       const bool resume = pdec.p && pf.state >= 1;
       dec = pdec.p ? std::move(pdec) : dpool_->take((size_t)clen + 64);
       st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr,
-                                  dec.p.get(), dec.cap, resume ? &pf : nullptr);
+                                  dec.p, dec.cap, resume ? &pf : nullptr, &dec.nl);
+      dec.has_nl = st == JIN_OK && pr.logs_kind == 1 && pr.logs_decoded;
       if (resume) stages.prefetched++;
     } else {
       st = parse_pod_request(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr, false);

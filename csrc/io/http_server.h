@@ -22,14 +22,52 @@
 namespace lp {
 
 // Uninitialised, recycled storage for a body's `logs` text decoded by the IO thread (no memset of
-// a fresh megabyte per request, as a std::string resize would do).
+// a fresh megabyte per request, as a std::string resize would do). Pinned (page-locked, GPU-mapped)
+// for large bodies when the server feeds a GPU engine: the engine then uses the decoded text as its
+// staging buffer in place -- with the decoder's newline positions, packing a 1 MB request is the
+// line index alone, not a 40 us copy of the text across cores (profiles/r6_e).
 struct DecodeBuf {
-  std::unique_ptr<char[]> p;
+  char* p = nullptr;
   size_t cap = 0;
+  bool pinned = false;
+  void (*pfree)(void*) = nullptr;   // pinned: how to free it (the allocator of set_pinned_decode)
+  NlPos nl;             // positions of the decoded text's '\n' bytes (recorded by the decoder)
+  bool has_nl = false;  //   valid for this text
+  DecodeBuf() = default;
+  DecodeBuf(const DecodeBuf&) = delete;
+  DecodeBuf& operator=(const DecodeBuf&) = delete;
+  DecodeBuf(DecodeBuf&& o) noexcept
+      : p(o.p), cap(o.cap), pinned(o.pinned), pfree(o.pfree), nl(std::move(o.nl)), has_nl(o.has_nl) {
+    o.p = nullptr;
+    o.cap = 0;
+    o.has_nl = false;
+  }
+  DecodeBuf& operator=(DecodeBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p;
+      cap = o.cap;
+      pinned = o.pinned;
+      pfree = o.pfree;
+      nl = std::move(o.nl);
+      has_nl = o.has_nl;
+      o.p = nullptr;
+      o.cap = 0;
+      o.has_nl = false;
+    }
+    return *this;
+  }
+  ~DecodeBuf() { release(); }
+  void release();
 };
 struct DecodePool {
   std::mutex m;
   std::vector<DecodeBuf> v;
+  std::atomic<int> pinned_live{0};   // pinned buffers in existence (pooled or in flight)
+  std::atomic<int> pinned_limit{0};  // 0: never pinned (set_pinned_decode)
+  size_t pinned_min = 256 << 10;     // bodies at least this large get a pinned buffer
+  void* (*palloc)(size_t) = nullptr; // pinned allocator / deallocator (the bindings pass HIP's):
+  void (*pfree)(void*) = nullptr;    //   this file stays free of GPU runtime calls
   DecodeBuf take(size_t need);
   void give(DecodeBuf&& b);
 };
@@ -109,6 +147,13 @@ class HttpServer {
   void recycle(std::string&& buf) { pool_->give(std::move(buf)); }
   const std::shared_ptr<BufferPool>& pool() const { return pool_; }
   const std::shared_ptr<DecodePool>& decode_pool() const { return dpool_; }
+  // up to `limit` pinned decode buffers for bodies >= min_bytes (a GPU engine serves this server)
+  void set_pinned_decode(int limit, size_t min_bytes, void* (*alloc)(size_t), void (*release)(void*)) {
+    dpool_->pinned_min = min_bytes;
+    dpool_->palloc = alloc;
+    dpool_->pfree = release;
+    dpool_->pinned_limit = alloc && release ? limit : 0;
+  }
   void stop();
   HttpStats stats;
   HttpStageStats stages;

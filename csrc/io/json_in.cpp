@@ -29,7 +29,16 @@ struct Cur {
   int depth = 0;
   bool fallback = false;
   bool closed = false;   // str_loop consumed the closing quote (span mode: the string ended in the span)
+  NlPos* nl = nullptr;   // str_loop records the decoded '\n' positions (relative to w0)
+  const char* w0 = nullptr;
 };
+
+// one decoded '\n' at w (scalar escapes)
+inline void nl_push(Cur& c, const char* w) {
+  if (!c.nl) return;
+  if (c.nl->n + 1 > c.nl->cap) c.nl->reserve(c.nl->n + 4096);
+  c.nl->p[c.nl->n++] = (int64_t)(w - c.w0);
+}
 
 inline void ws(Cur& c) {
   while (c.p < c.e && (*c.p == ' ' || *c.p == '\t' || *c.p == '\n' || *c.p == '\r')) ++c.p;
@@ -75,7 +84,7 @@ inline int utf8_len(const uint8_t* p, const uint8_t* e) {
 // With Store = false the block is only validated (skip mode of a string nobody reads).
 template <bool Store>
 __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vbmi2,bmi,bmi2,popcnt")))
-bool block64(const uint8_t*& p, char*& w, size_t* kept = nullptr) {
+bool block64(const uint8_t*& p, char*& w, size_t* kept = nullptr, NlPos* nl = nullptr, const char* w0 = nullptr) {
   const __m512i v = _mm512_loadu_si512(reinterpret_cast<const void*>(p));
   const uint64_t B = _mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('\\'));
   const uint64_t Q = _mm512_cmpeq_epi8_mask(v, _mm512_set1_epi8('"'));
@@ -105,8 +114,35 @@ bool block64(const uint8_t*& p, char*& w, size_t* kept = nullptr) {
   if (Store) {
     const __m512i o = _mm512_mask_blend_epi8(escaped, v, tr);
     const uint64_t keep = ~initiators;
-    _mm512_storeu_si512(reinterpret_cast<void*>(w), _mm512_maskz_compress_epi8(keep, o));
-    w += _mm_popcnt_u64(keep);
+    const __m512i out = _mm512_maskz_compress_epi8(keep, o);
+    _mm512_storeu_si512(reinterpret_cast<void*>(w), out);
+    const int nk = (int)_mm_popcnt_u64(keep);
+    if (nl) {   // the block's decoded newlines: offsets compressed out of an iota, 8 stored per step
+      const uint64_t valid = nk >= 64 ? ~0ull : ((1ull << nk) - 1);
+      uint64_t m = _mm512_cmpeq_epi8_mask(out, _mm512_set1_epi8('\n')) & valid;
+      if (m) {
+        alignas(64) static const uint8_t kIota[64] = {
+            0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
+            22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43,
+            44, 45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63};
+        if (nl->n + 72 > nl->cap) nl->reserve(nl->n + 4096);
+        const __m512i offs = _mm512_maskz_compress_epi8(m, _mm512_load_si512(reinterpret_cast<const void*>(kIota)));
+        const int64_t base = (int64_t)(w - w0);
+        _mm512_storeu_si512(reinterpret_cast<void*>(nl->p.get() + nl->n),
+                            _mm512_add_epi64(_mm512_cvtepu8_epi64(_mm512_castsi512_si128(offs)), _mm512_set1_epi64(base)));
+        const int c = (int)_mm_popcnt_u64(m);
+        if (c > 8) {
+          for (int j = 0; j < 8; ++j) m &= m - 1;
+          size_t q = nl->n + 8;
+          while (m) {
+            nl->p[q++] = base + __builtin_ctzll(m);
+            m &= m - 1;
+          }
+        }
+        nl->n += (size_t)c;
+      }
+    }
+    w += nk;
   }
   p += 64;
   return true;
@@ -134,7 +170,7 @@ char* str_loop(Cur& c, char* w) {
   for (;;) {
 #if defined(__x86_64__)
     if (wide)
-      while (c.e - c.p >= 64 && block64<true>(c.p, w)) {
+      while (c.e - c.p >= 64 && block64<true>(c.p, w, nullptr, c.nl, c.w0)) {
       }
 #endif
 #if defined(__SSE2__)
@@ -184,7 +220,7 @@ char* str_loop(Cur& c, char* w) {
       case '/': *w++ = '/'; break;
       case 'b': *w++ = '\b'; break;
       case 'f': *w++ = '\f'; break;
-      case 'n': *w++ = '\n'; break;
+      case 'n': nl_push(c, w); *w++ = '\n'; break;
       case 'r': *w++ = '\r'; break;
       case 't': *w++ = '\t'; break;
       case 'u': {
@@ -201,6 +237,7 @@ char* str_loop(Cur& c, char* w) {
           return nullptr;
         }
         if (v < 0x80) {
+          if (v == '\n') nl_push(c, w);
           *w++ = (char)v;
         } else if (v < 0x800) {
           *w++ = (char)(0xC0 | (v >> 6));
@@ -542,7 +579,7 @@ size_t decode_json_string_exact(const uint8_t* p, size_t n, char* w) {
 
 namespace {
 int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap,
-                   const LogsPrefetch* pf);
+                   const LogsPrefetch* pf, NlPos* nl);
 
 // Body offset of the opening quote of the top-level `logs` string, found by the validating parser
 // over the prefix [body, body + avail); 0 when the prefix does not reach it (truncated before it,
@@ -587,7 +624,7 @@ const uint8_t* safe_cut(const uint8_t* lo, const uint8_t* cut) {
 }
 }  // namespace
 
-void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* dst, size_t cap) {
+void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* dst, size_t cap, NlPos* nl) {
   if (st.state < 0 || st.state == 2 || !dst) return;
   if (st.state == 0) {
     // locate the member at geometrically growing prefixes (the locating parses cost at most twice
@@ -605,6 +642,7 @@ void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* ds
     st.s0 = at;
     st.src = at + 1;
     st.dlen = 0;
+    if (nl) nl->n = 0;
   }
   // decode [src, cut): 8 bytes stay behind the arrival front so the cut test reads arrived bytes
   if (avail < st.src + 64 + 8) return;
@@ -616,6 +654,8 @@ void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* ds
     return;
   }
   Cur c{body + st.src, cut};
+  c.nl = nl;
+  c.w0 = dst;
   char* w = str_into_span(c, dst + st.dlen);
   if (!w) {        // invalid or json.loads territory: the final parse decides (and answers)
     st.state = -1;
@@ -627,17 +667,17 @@ void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* ds
 }
 
 int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs) {
-  return parse_pod_impl(body, n, out, decode_logs, nullptr, 0, nullptr);
+  return parse_pod_impl(body, n, out, decode_logs, nullptr, 0, nullptr, nullptr);
 }
 
 int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap,
-                           const LogsPrefetch* pf) {
-  return parse_pod_impl(body, n, out, false, dst, cap, pf && pf->state >= 1 ? pf : nullptr);
+                           const LogsPrefetch* pf, NlPos* nl) {
+  return parse_pod_impl(body, n, out, false, dst, cap, pf && pf->state >= 1 ? pf : nullptr, nl);
 }
 
 namespace {
 int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs, char* dst, size_t cap,
-                   const LogsPrefetch* pf) {
+                   const LogsPrefetch* pf, NlPos* nl) {
   out = PodRequest{};
   if (n >= 2 && (body[0] == 0 || body[1] == 0)) return JIN_FALLBACK;      // UTF-16/32
   if (n >= 3 && body[0] == 0xEF && body[1] == 0xBB && body[2] == 0xBF) return JIN_FALLBACK;  // BOM
@@ -659,12 +699,16 @@ int parse_pod_impl(const uint8_t* body, size_t n, PodRequest& out, bool decode_l
         // arrived (logs_prefetch, same member: same offset) resumes at its end.
         const uint8_t* s0 = cc.p;
         char* end;
+        cc.w0 = dst;
+        cc.nl = nl;
         if (pf && (size_t)(s0 - body) == pf->s0 && pf->src <= n) {
           cc.p = body + pf->src;
           end = pf->state == 2 ? dst + pf->dlen : str_loop<false>(cc, dst + pf->dlen);
         } else {
+          if (nl) nl->n = 0;
           end = str_into(cc, dst);
         }
+        cc.nl = nullptr;
         if (!end) {
           out.logs_decoded = false;
           return false;

@@ -2,6 +2,8 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
+#include <memory>
 #include <string>
 
 namespace lp {
@@ -25,6 +27,23 @@ struct PodRequest {
 // into a Python bytes object -- the HTTP front end's one-copy path).
 int parse_pod_request(const uint8_t* body, size_t n, PodRequest& out, bool decode_logs = true);
 
+// Positions (offsets into the decoded text) of the '\n' bytes the decoder writes -- in a JSON string
+// every newline is an escape (\n or \u000a: raw control bytes are invalid), so the decoder sees each
+// one anyway and the batch packer need not scan the text again (pack_split_docs `nlpos`).
+// Grow-only, uninitialised storage; the block decoder stores 8 positions unconditionally per block.
+struct NlPos {
+  std::unique_ptr<int64_t[]> p;
+  size_t n = 0, cap = 0;
+  void reserve(size_t c) {
+    if (c <= cap) return;
+    const size_t k = c < 2 * cap ? 2 * cap : c;
+    std::unique_ptr<int64_t[]> q(new int64_t[k]);
+    if (n) std::memcpy(q.get(), p.get(), n * sizeof(int64_t));
+    p = std::move(q);
+    cap = k;
+  }
+};
+
 // Decoding of the top-level `logs` string while a body is still arriving (the HTTP front end's IO
 // thread between reads: the 1 MB string's validation and unescaping overlap the receive instead of
 // following its last byte). The prefix [s0 + 1, src) of the string is decoded to dst[0, dlen);
@@ -43,7 +62,9 @@ struct LogsPrefetch {
 
 // Advances `st` over the first `avail` arrived bytes of a body. `dst` / `cap` as for
 // parse_pod_request_into (the same buffer must be passed there with `st`).
-void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* dst, size_t cap);
+// `nl` (optional): the decoded newlines' positions (kept in step with dlen; reset when the decoding
+// restarts).
+void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* dst, size_t cap, NlPos* nl = nullptr);
 
 // Validates the whole body like parse_pod_request and decodes the `logs` string into `dst` in the
 // same pass (the HTTP front end's IO thread, while the bytes are in its cache): logs_decoded is set
@@ -51,8 +72,10 @@ void logs_prefetch(const uint8_t* body, size_t avail, LogsPrefetch& st, char* ds
 // stores run past the decoded end); a string that does not fit is only validated (skip mode).
 // With `pf` (a logs_prefetch state over a prefix of this body, into this dst) the string's
 // decoding resumes where the prefetch stopped.
+// `nl` (optional): the positions of the '\n' bytes in dst[0, logs_dlen) (with `pf`: the prefetch's
+// sink, continued).
 int parse_pod_request_into(const uint8_t* body, size_t n, PodRequest& out, char* dst, size_t cap,
-                           const LogsPrefetch* pf = nullptr);
+                           const LogsPrefetch* pf = nullptr, NlPos* nl = nullptr);
 
 // Unescapes the content of a JSON string that parse_pod_request validated (`n` raw bytes between
 // the quotes) into `w`, which must have room for n + 64 bytes; returns the decoded length.

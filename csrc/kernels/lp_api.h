@@ -21,6 +21,8 @@ void set_cand_verify_split(bool on);
 // event top-k by threshold selection (summarize.hip k_sel_*, default) or the chunk-sort levels
 bool summ_select();
 void set_summ_select(bool on);
+// diagnostic: phase clocks of k_hits_small / k_events_small into a device int64[16] (0: off)
+void set_small_profile(uint64_t dev_ptr);
 // line-index pass 1 folded into the bulk prefilter (line_index.hip k_nl_count's outputs): per 16 KiB
 // tile the '\n' count and the "\r\n" flag (both zeroed by the caller), per 64 bytes a '\n' bitmask
 struct NlOut {

@@ -340,6 +340,16 @@ constexpr int SB_THREADS = 1024;
 constexpr int SB_MAX = 4096;           // keys / events held in LDS
 constexpr int SB_MAX_LINES = 16384;    // window-coverage difference array in LDS
 
+// Diagnostic phase clock of the two single-workgroup kernels (set_small_profile): thread 0 stores
+// wall_clock64() after each phase into g_sb_prof[slot] (null: off, one scalar load per phase).
+// Slots 0-7 k_hits_small, 8-15 k_events_small.
+__device__ int64_t* g_sb_prof = nullptr;
+#define LP_SB_STAMP(slot)                                                    \
+  do {                                                                     \
+    int64_t* pp_ = g_sb_prof;                                              \
+    if (pp_ && threadIdx.x == 0) pp_[slot] = (int64_t)wall_clock64();     \
+  } while (0)
+
 __device__ __forceinline__ int sb_pow2(int64_t n) {
   int p = 64;
   while (p < n) p <<= 1;
@@ -360,6 +370,46 @@ __device__ void sb_sort(uint64_t* s, int n) {
       }
       __syncthreads();
     }
+}
+
+constexpr int SB_RANK_MAX = 512;   // live keys up to which sb_sort_live ranks instead of sorting
+
+// Ascending sort of the n live keys s[0, n) (the slots past n keep their pad keys), whole block.
+// Up to SB_RANK_MAX keys by RANKS: key t goes to #{j : s[j] < s[t]} + #{j < t : s[j] == s[t]}
+// (duplicates keep distinct slots), G = 2..64 lanes per key count a share of the j's and reduce by
+// shuffles -- one pass of independent broadcast LDS reads and two barriers. A request's 90-250 keys
+// sorted by the bitonic network took 4.6-6 us in its 28-36 dependent LDS + barrier steps
+// (tools/small_phases.py; a register / shuffle network measured the same per step). Larger n:
+// the bitonic sort of the padded power of two np.
+__device__ void sb_sort_live(uint64_t* s, int n, int np) {
+  if (n > SB_RANK_MAX) {
+    sb_sort(s, np);
+    return;
+  }
+  int G = 2;
+  while (G < 64 && 2 * G * n <= SB_THREADS) G <<= 1;
+  const int t = (int)threadIdx.x / G, part = (int)threadIdx.x & (G - 1);
+  const uint64_t key = t < n ? s[t] : 0ull;
+  int cnt = 0;
+  if (t < n) {
+    // 8 independent broadcast reads in flight per step (a loop of one read at a time waited on each)
+    int j = part;
+    for (; j + 7 * G < n; j += 8 * G) {
+      uint64_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = s[j + u * G];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) cnt += (v[u] < key || (v[u] == key && j + u * G < t)) ? 1 : 0;
+    }
+    for (; j < n; j += G) {
+      const uint64_t v = s[j];
+      cnt += (v < key || (v == key && j < t)) ? 1 : 0;
+    }
+  }
+  for (int d = 1; d < G; d <<= 1) cnt += __shfl_xor(cnt, d, 64);
+  __syncthreads();
+  if (t < n && part == 0) s[cnt] = key;
+  __syncthreads();
 }
 
 // exclusive prefix of v over the block (thread order); *total = block sum. Uses scratch[SB_THREADS/64 + 1].
@@ -412,6 +462,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
   // the live entries of both regions, compacted (most prefilter candidates failed their verify and
   // are -1): the sort covers pow2(live), not pow2(used) or the capacities
   __shared__ int s_live;
+  LP_SB_STAMP(0);
   if (threadIdx.x == 0) s_live = 0;
   __syncthreads();
   for (int64_t i = threadIdx.x; i < n1 + n2; i += SB_THREADS) {
@@ -425,7 +476,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
   const int np = sb_pow2(live);
   for (int i = live + threadIdx.x; i < np; i += SB_THREADS) keys[i] = LP_PAD_KEY;
   __syncthreads();
-  sb_sort(keys, np);
+  LP_SB_STAMP(1);
+  sb_sort_live(keys, live, np);
+  LP_SB_STAMP(2);
   // dedupe + DFA verify, then compaction in sorted order: 4 consecutive keys per thread
   constexpr int PER = SB_MAX / SB_THREADS;
   bool keep[PER];
@@ -447,6 +500,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
       ++o;
     }
   __syncthreads();
+  LP_SB_STAMP(3);
   // CSR per regex, hit lines, events per hit and their inclusive scan (4 consecutive per thread)
   for (int r = threadIdx.x; r <= A.R; r += SB_THREADS) A.hit_off[r] = lower_bound64(hk, nh, (int64_t)r << 32);
   int64_t ec[PER], e = 0;
@@ -473,6 +527,8 @@ __global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
     A.counters[0] = nh;
     A.counters[1] = ne;
   }
+  LP_SB_STAMP(4);
+  if (threadIdx.x == 0 && g_sb_prof) g_sb_prof[5] = live;
 }
 
 __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32_t* __restrict__ cov_out) {
@@ -490,6 +546,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
     if (over) return;                     // over capacity: the host re-runs with read counts
   }
   const int np = sb_pow2(ne);
+  LP_SB_STAMP(8);
   for (int i = threadIdx.x; i <= L; i += SB_THREADS) diff[i] = 0;
   for (int k = threadIdx.x; k < E.nkeys; k += SB_THREADS) A.freq_counts[k] = 0;
   for (int i = threadIdx.x; i < np; i += SB_THREADS) keys[i] = LP_PAD_KEY;
@@ -505,7 +562,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
     for (int64_t j = 0; j < c; ++j) keys[b0 + j] = (x << E.pbits) | (uint64_t)E.prim_pats[p0 + j];
   }
   __syncthreads();
-  sb_sort(keys, np);
+  LP_SB_STAMP(9);
+  sb_sort_live(keys, (int)ne, np);
+  LP_SB_STAMP(10);
   // per event: outputs + window coverage; then re-key by (frequency key, event) for the ranks
   for (int e = threadIdx.x; e < ne; e += SB_THREADS) {
     int32_t a, b;
@@ -517,7 +576,9 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
     keys[e] = ((uint64_t)fs << 32) | (uint32_t)e;
   }
   __syncthreads();
-  sb_sort(keys, np);
+  LP_SB_STAMP(11);
+  sb_sort_live(keys, (int)ne, np);
+  LP_SB_STAMP(12);
   for (int j = threadIdx.x; j < ne; j += SB_THREADS) {
     const uint32_t fk = (uint32_t)(keys[j] >> 32);
     const int32_t e = (int32_t)(keys[j] & 0xFFFFFFFFull);
@@ -546,6 +607,13 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
     run += diff[i];
     cov_out[i] = (int32_t)run;
   }
+  LP_SB_STAMP(13);
+  if (threadIdx.x == 0 && g_sb_prof) g_sb_prof[14] = ne;
+}
+
+void set_small_profile(uint64_t dev_ptr) {
+  int64_t* p = reinterpret_cast<int64_t*>(dev_ptr);
+  LP_PCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sb_prof), &p, sizeof(p)));
 }
 
 bool hits_small_ok(const HitsArgs& A) { return A.n > 0 && A.n <= SB_MAX; }

@@ -263,6 +263,7 @@ class Stage:
         self.pinned = pinned
         self.buf = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pinned)
         self.want = 0                       # bytes the request runner's single-copy upload wants
+        self.own_buf: Optional[torch.Tensor] = None   # buf while a request's pinned buffer stands in
         self.cap = 0
         self.idx: Optional[torch.Tensor] = None
         self.grow_idx(nlines)
@@ -1116,6 +1117,9 @@ class Engine:
     def release_batch(self, job: "BatchJob") -> None:
         """Return the job's staging buffer to the pool (after its H2D and emission are done)."""
         if job.stage is not None:
+            if job.stage.own_buf is not None:   # staged in place in a request's pinned buffer
+                job.stage.buf, job.stage.own_buf = job.stage.own_buf, None
+                job.stage.want = 0
             if job.stage.want > job.stage.buf.numel():
                 try:
                     job.stage.grow_buf(job.stage.want)
@@ -1125,6 +1129,8 @@ class Engine:
             job.stage = None
 
     _STAGE_THREADS = host_thread_budget()
+    inplace_stages = 0          # batches staged in place in a request's pinned decode buffer
+    _pinned_views: dict = {}    # (address, capacity) of a pinned decode buffer -> its uint8 tensor view
 
     def _stage_docs(self, job: "BatchJob", docs):
         """Pack request bodies into the job's (pinned) staging buffer and build the per-document
@@ -1135,8 +1141,30 @@ class Engine:
         raw = [isinstance(d, N.RawLogs) for d in docs]
         if any(raw) and not all(raw):   # escaped request logs are unescaped in place only as a batch
             docs = [d.decode() if r else d for d, r in zip(docs, raw)]
-        cap = st.buf.numel() - K.TEXT_PAD - K.NL_TILE
-        r = N.pack_split_docs(docs, st.buf.data_ptr(), cap, self._STAGE_THREADS, st.idx.data_ptr(), st.cap)
+        r = None
+        if len(docs) == 1 and raw[0] and self.device.type == "cuda":
+            # decoded by the HTTP IO thread into a pinned buffer: that buffer IS this batch's stage
+            # (the decoder recorded its newlines, so packing is the line index alone; the runner
+            # uploads from it and the emitter reads it). The RawLogs in job.logs keeps it alive.
+            addr, pcap = docs[0].pinned_text
+            if addr:
+                r = N.pack_split_docs(docs, addr, pcap - K.TEXT_PAD - K.NL_TILE, self._STAGE_THREADS,
+                                      st.idx.data_ptr(), st.cap)
+                if isinstance(r, tuple) and r[1] is None:
+                    st.own_buf = st.buf
+                    views = self._pinned_views       # (the server recycles a few such buffers)
+                    v = views.get((addr, pcap))
+                    if v is None:
+                        if len(views) > 32:
+                            views.clear()
+                        v = views[(addr, pcap)] = torch.from_dlpack(N.dlpack(addr, pcap, "uint8", -1))
+                    st.buf = v
+                    self.inplace_stages += 1
+                else:
+                    r = None
+        if r is None:
+            cap = st.buf.numel() - K.TEXT_PAD - K.NL_TILE
+            r = N.pack_split_docs(docs, st.buf.data_ptr(), cap, self._STAGE_THREADS, st.idx.data_ptr(), st.cap)
         if r is None:
             return None
         if isinstance(r, int):

@@ -71,6 +71,12 @@ class NativeHttpFrontend:
                                 trace=trace, conn_trace=bool(cfg.get("server.stage-timeline", False)),
                                 prefetch=bool(cfg["server.prefetch-logs"]))
         self.port = self.srv.port
+        eng = b.pipe.engine if b.pipe is not None else None
+        npin = int(cfg["server.pinned-decode-buffers"])
+        if npin > 0 and eng is not None and eng.device.type == "cuda":
+            # bodies >= 256 KiB are decoded by the IO threads into pinned buffers that the engine stages
+            # in place (Engine._stage_docs): up to `npin` such buffers, then pageable ones
+            self.srv.set_pinned_decode(npin, 256 << 10)
         self._stop = threading.Event()
         # server.trace-requests: per /parse request on stderr -- receive / validate (native side),
         # queue (body complete -> drained by the pump) and engine (drained -> response queued)

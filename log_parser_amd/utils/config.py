@@ -134,6 +134,11 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # by the IO thread between reads while it arrives; the final parse resumes there (csrc/io/json_in.h
     # LogsPrefetch). The request's verdict (400 / 200) is still the final parse's.
     "server.prefetch-logs": (True, bool),
+    # native front end over a GPU engine: up to this many pinned (page-locked) buffers receive the
+    # decoded logs of bodies >= 256 KiB; the engine stages such a request in place (no copy of the
+    # text into its own stage, and the decoder's newline positions replace the packer's scan:
+    # /parse p50 0.42-0.43 -> 0.40 ms, profiles/r6_e). 0: pageable buffers, copied.
+    "server.pinned-decode-buffers": (8, int),
     # native front end: IO threads poll this long after activity before sleeping in epoll_wait
     "server.io-spin-us": (0.0, float),
     # native front end: the pump polls for the next request this long before sleeping on the queue

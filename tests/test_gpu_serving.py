@@ -106,8 +106,11 @@ def test_native_http_over_gpu_engine_equals_golden(gpu_device):
             assert [(e["lineNumber"], e["context"]) for e in o["events"]] == \
                    [(e["lineNumber"], e["context"]) for e in g["events"]]
             assert o["summary"] == g["summary"]
-        # bodies of 300-500 KB: the logs text decoded by the IO thread while validating, copied by the
-        # packer into the stage (csrc/io/http_server.cpp DecodePool)
+        # bodies of 300-500 KB: the logs text decoded by the IO thread while it arrives, into pinned
+        # buffers the engine stages in place with the decoder's newline positions (DecodePool,
+        # Engine._stage_docs); duplicates of the newline-heavy tail and CRLF lines included
+        eng = fe.svc.engine()
+        n0 = eng.inplace_stages
         for i in range(4):
             logs = make_log(3500 + 500 * i, trig, seed=400 + i, hit_rate=0.05, crlf_rate=0.1) + "\n\ntail é\u2028x"
             c.request("POST", "/parse", body=json.dumps({"pod": {"metadata": {"name": f"q{i}"}}, "logs": logs}),
@@ -121,6 +124,7 @@ def test_native_http_over_gpu_engine_equals_golden(gpu_device):
                    [(e["lineNumber"], e["context"]) for e in g["events"]]
             assert [e["score"] for e in o["events"]] == pytest.approx([e["score"] for e in g["events"]], rel=1e-12)
             assert o["summary"] == g["summary"]
+        assert eng.inplace_stages - n0 == 4
         c.close()
     finally:
         fe.close()

@@ -217,3 +217,21 @@ def test_logs_prefetch_large_body_every_boundary():
     for off in range(0, 12):
         got = N.parse_pod_request_stream(body, list(range(off, len(body), 61)))
         assert tuple(got[:5]) == tuple(want), off
+
+
+def test_decoder_records_newline_positions():
+    """The decoder records where it writes every '\\n' (escapes \\n and \\u000a, the block decoder's
+    compressed output and the scalar path alike), so the packer skips its newline scan: the positions
+    equal a scan of the decoded bytes for one-pass and prefetched (resumed) decodes."""
+    rng = random.Random(11)
+    atoms = ["x" * 61, "\n", "\n\n\n\n\n\n\n\n\n\n", "\r\n", "é", "😀", '"', "\\", "ab\ncd", "\t"]
+    for it in range(300):
+        s = "".join(rng.choice(atoms) for _ in range(rng.randint(0, 120)))
+        body = json.dumps({"pod": {}, "logs": s}, ensure_ascii=rng.random() < 0.3).encode()
+        if rng.random() < 0.3:
+            body = body.replace(b"\\n", b"\\u000a", rng.randint(0, 5))
+        got = N.parse_pod_request_stream(body, _stream_cuts(rng, len(body)) if it % 2 else [])
+        if got[0] == 3:                               # surrogate-pair escapes: json.loads decides
+            continue
+        assert got[0] == 0 and got[4] == s.encode()
+        assert list(got[7]) == [i for i, b in enumerate(got[4]) if b == 10], it

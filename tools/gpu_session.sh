@@ -8,12 +8,12 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   shift 2
   timeout -k 10 "$secs" "$@" > "gpurun_out/s_${name}.log" 2>&1
   local rc=$?
-  echo "$name rc=$rc"; tail -2 "gpurun_out/s_${name}.log" | cut -c1-200
+  echo "$name rc=$rc"; tail -2 "gpurun_out/s_${name}.log" | cut -c1-300
   [ $rc -eq 0 ] || exit $rc
 }
 
+run gpuserve 600 python -u -m pytest tests/test_gpu_serving.py tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread
 for k in 1 2 3; do
-  run pf_$k 300 python -u tools/parse_stages.py --n 400
-  run nopf_$k 300 python -u tools/parse_stages.py --n 400 -D server.prefetch-logs=false
+  run inpl_$k 300 python -u tools/parse_stages.py --n 400
+  run noinpl_$k 300 python -u tools/parse_stages.py --n 400 -D server.ab-inplace=false -D server.ab-known-nl=false
 done
-run bench5 300 python -u bench.py --steps 10 --warmup 3

@@ -189,7 +189,7 @@ static void http_prefetch_selftest(int rounds) {
     while (!done)
       for (auto& r : srv.next_requests(16, 20)) {
         const size_t n = r.kind == 0 && r.dec.p ? r.logs_dlen : (size_t)-1;
-        const uint64_t h = n == (size_t)-1 ? 0 : std::hash<std::string>()(std::string(r.dec.p.get(), n));
+        const uint64_t h = n == (size_t)-1 ? 0 : std::hash<std::string>()(std::string(r.dec.p, n));
         srv.respond(r.id, 200, "application/json", "{\"n\":" + std::to_string(n) + ",\"h\":" + std::to_string(h) + "}");
       }
   });

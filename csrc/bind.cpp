@@ -1488,6 +1488,7 @@ PYBIND11_MODULE(_lpnative, m) {
         d["queue_s"] = g.queue_ns.load() * 1e-9; d["responses"] = g.responses.load();
         d["handoff_s"] = g.handoff_ns.load() * 1e-9; d["sent"] = g.sent.load(); d["send_s"] = g.send_ns.load() * 1e-9;
         d["prefetch_s"] = g.prefetch_ns.load() * 1e-9; d["prefetched"] = g.prefetched.load();
+        d["pump_prefetch_s"] = g.pump_prefetch_ns.load() * 1e-9;
         return d;
       })
       .def("stop", [](HttpServer& s) {

@@ -254,6 +254,9 @@ struct HttpServer::Conn {
   ChunkDecoder chunk;       // Transfer-Encoding: chunked body being received
   LogsPrefetch pf;          // POST /parse body being received: its logs string decoded so far
   DecodeBuf pdec;           //   into this buffer (handed to the request when the body completes)
+  int slot = -1;            // arrival slot the pump decodes this body in (-1: none)
+  bool early = false;       // parse_one already ran inside the receive loop for this request
+  size_t slot_b0 = 0, slot_len = 0;   //   body offset in `in` and Content-Length
 };
 
 struct HttpServer::Io {
@@ -323,6 +326,11 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
     ios_.push_back(std::move(io));
   }
   reserve_fd_table(ios_[0]->lfd);
+  if (prefetch_)
+    helper_ = std::thread([this] {
+      pthread_setname_np(pthread_self(), "lp-decode");
+      helper_loop();
+    });
   for (auto& io : ios_)
     threads_.emplace_back([this, p = io.get(), k = (int)threads_.size()] {
       char nm[16];
@@ -342,7 +350,18 @@ void HttpServer::stop() {
   }
   for (auto& t : threads_)
     if (t.joinable()) t.join();
+  {
+    std::lock_guard<std::mutex> g(hm_);
+  }
+  hcv_.notify_all();
+  if (helper_.joinable()) helper_.join();
   for (auto& io : ios_) {
+    for (auto& kv : io->conns)
+      if (kv.second->slot >= 0) {   // (a pump step in progress finishes first)
+        acquire_slot(kv.second)->state.store(ArrivalSlot::FREE, std::memory_order_release);
+        arrivals_.fetch_sub(1);
+        kv.second->slot = -1;
+      }
     for (auto& kv : io->conns) {
       close(kv.second->fd);
       delete kv.second;
@@ -356,18 +375,31 @@ void HttpServer::stop() {
 }
 
 std::vector<HttpRequest> HttpServer::next_requests(int max_n, int timeout_ms) {
-  if (pump_spin_s_ > 0) {
-    const double until = now_s() + pump_spin_s_;
-    while (qn_.load(std::memory_order_acquire) == 0 && !stop_ && now_s() <= until) {
-      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
-    }
-  }
-  std::unique_lock<std::mutex> lk(qm_);
   // system_clock deadline: pthread_cond_timedwait (steady-clock waits map to pthread_cond_clockwait,
   // which the ThreadSanitizer runtime of this toolchain does not intercept); a short poll anyway
-  if (q_.empty())
-    qcv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms)),
-                    [&] { return !q_.empty() || stop_; });
+  const auto deadline = std::chrono::system_clock::now() + std::chrono::milliseconds(std::max(0, timeout_ms));
+  std::unique_lock<std::mutex> lk(qm_, std::defer_lock);
+  for (;;) {
+    // while waiting, decode the arriving bodies registered in the arrival slots
+    double until = now_s() + pump_spin_s_;
+    while (qn_.load(std::memory_order_acquire) == 0 && !stop_ && now_s() <= until) {
+      if (advance_arrivals()) {
+        until = now_s() + pump_spin_s_;
+        continue;
+      }
+      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+    }
+    const uint64_t gen = arr_gen_.load(std::memory_order_acquire);
+    lk.lock();
+    if (!q_.empty() || stop_) break;
+    pump_waiting_.store(true, std::memory_order_seq_cst);
+    const bool woke = qcv_.wait_until(lk, deadline, [&] {
+      return !q_.empty() || stop_ || arr_gen_.load(std::memory_order_acquire) != gen;
+    });
+    pump_waiting_.store(false, std::memory_order_relaxed);
+    if (!woke || !q_.empty() || stop_) break;
+    lk.unlock();                                 // new arrivals only: decode them, then wait again
+  }
   std::vector<HttpRequest> r;
   const double t = now_s();
   uint64_t qns = 0;
@@ -569,11 +601,88 @@ void HttpServer::set_events(Io* io, Conn* c) {
 
 void HttpServer::close_conn(Io* io, Conn* c) {
   if (c->dead) return;
+  if (c->slot >= 0) {                            // the body's buffers die with the connection
+    acquire_slot(c)->state.store(ArrivalSlot::FREE, std::memory_order_release);
+    arrivals_.fetch_sub(1);
+    c->slot = -1;
+  }
   c->dead = true;
   epoll_ctl(io->ep, EPOLL_CTL_DEL, c->fd, nullptr);
   close(c->fd);
   io->conns.erase(c->id);
   io->graveyard.push_back(c);
+}
+
+void HttpServer::helper_loop() {
+  while (!stop_) {
+    // spin while registered bodies make progress (a step per 32-64 KiB of arrival); sleep after
+    // 2 ms without work (no body, or a stalled client) until the next arrival is published
+    double last = now_s();
+    uint64_t gen = arr_gen_.load(std::memory_order_acquire);
+    while (!stop_ && now_s() - last < 2e-3) {
+      gen = arr_gen_.load(std::memory_order_acquire);
+      if (advance_arrivals()) {
+        last = now_s();
+        continue;
+      }
+      for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+    }
+    std::unique_lock<std::mutex> lk(hm_);
+    helper_waiting_.store(true, std::memory_order_seq_cst);
+    // (system_clock deadline: see next_requests)
+    hcv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(100),
+                    [&] { return stop_.load() || arr_gen_.load(std::memory_order_acquire) != gen; });
+    helper_waiting_.store(false, std::memory_order_relaxed);
+  }
+}
+
+void HttpServer::publish_arrival(Conn* c) {
+  ArrivalSlot& sl = slots_[c->slot];
+  const size_t got = c->in.size() > c->slot_b0 ? std::min(c->in.size() - c->slot_b0, c->slot_len) : 0;
+  if (got < sl.avail.load(std::memory_order_relaxed) + (32 << 10) && got < c->slot_len) return;   // (batched)
+  sl.avail.store(got, std::memory_order_release);
+  arr_gen_.fetch_add(1, std::memory_order_release);
+  if (helper_waiting_.load(std::memory_order_seq_cst)) {
+    { std::lock_guard<std::mutex> g(hm_); }
+    hcv_.notify_one();
+  }
+  if (pump_waiting_.load(std::memory_order_seq_cst)) {
+    { std::lock_guard<std::mutex> g(qm_); }      // (no lost wake-up against the pump's predicate)
+    qcv_.notify_one();
+  }
+}
+
+bool HttpServer::advance_arrivals() {
+  if (arrivals_.load(std::memory_order_acquire) == 0) return false;
+  bool worked = false;
+  for (ArrivalSlot& sl : slots_) {
+    if (sl.state.load(std::memory_order_relaxed) != ArrivalSlot::IDLE) continue;
+    // a step per >= 32 KiB of new bytes (the body's tail is the IO thread's, at completion)
+    if (sl.avail.load(std::memory_order_acquire) < sl.seen.load(std::memory_order_relaxed) + (32 << 10)) continue;
+    int e = ArrivalSlot::IDLE;
+    if (!sl.state.compare_exchange_strong(e, ArrivalSlot::PUMP, std::memory_order_acquire)) continue;
+    // at most 64 KiB of new bytes per step: the IO thread that completes the body waits for the
+    // step in progress (a step over everything that had arrived cost it ~60 us: the pump decodes
+    // slower than a loopback body arrives), then decodes the remainder itself
+    const size_t av = std::min(sl.avail.load(std::memory_order_acquire),
+                               sl.seen.load(std::memory_order_relaxed) + (64 << 10));
+    const double t0 = now_s();
+    logs_prefetch(sl.body, av, sl.pf, sl.dst, sl.cap, sl.nl);
+    stages.pump_prefetch_ns += (uint64_t)std::max(0.0, (now_s() - t0) * 1e9);
+    sl.seen.store(sl.pf.state < 0 || sl.pf.state == 2 ? ~size_t(0) >> 1 : av, std::memory_order_relaxed);
+    sl.state.store(ArrivalSlot::IDLE, std::memory_order_release);
+    worked = true;
+  }
+  return worked;
+}
+
+ArrivalSlot* HttpServer::acquire_slot(Conn* c) {
+  ArrivalSlot& sl = slots_[c->slot];
+  for (;;) {                                     // a pump step is short (<= a few 10 us)
+    int e = ArrivalSlot::IDLE;
+    if (sl.state.compare_exchange_weak(e, ArrivalSlot::IO, std::memory_order_acquire)) return &sl;
+    __builtin_ia32_pause();
+  }
 }
 
 // Parses one complete request from c->in; false when more bytes are needed or the connection
@@ -689,18 +798,53 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     }
     // a large /parse body: decode the part of its logs string that has arrived now, while this
     // thread would otherwise wait for the rest (the validation then ends with the last read)
-    if (prefetch_ && te == TE_NONE && clen >= kPrefetchMin && method == "POST" && route == "/parse" && json_ctype &&
-        c->pf.state >= 0 && c->in.size() > b0) {
-      const double t0 = now_s();
+    if (c->slot >= 0) {
+      publish_arrival(c);
+    } else if (prefetch_ && te == TE_NONE && clen >= kPrefetchMin && method == "POST" && route == "/parse" &&
+               json_ctype && c->pf.state >= 0 && c->in.size() > b0) {
       if (!c->pdec.p) c->pdec = dpool_->take((size_t)clen + 64);
-      logs_prefetch(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, c->in.size() - b0, c->pf, c->pdec.p,
-                    c->pdec.cap, &c->pdec.nl);
-      stages.prefetch_ns += (uint64_t)std::max(0.0, (now_s() - t0) * 1e9);
+      // hand the body to the pump thread (arrival slot): it decodes while this thread receives.
+      // The receive buffer must not move while registered -- room for some pipelined bytes too
+      if (c->in.capacity() < total + (64 << 10)) c->in.reserve(total + (64 << 10));
+      int k = -1;
+      for (int i = 0; i < kSlots && k < 0; ++i) {
+        int e = ArrivalSlot::FREE;
+        if (slots_[i].state.compare_exchange_strong(e, ArrivalSlot::IO, std::memory_order_acquire)) k = i;
+      }
+      if (k >= 0) {
+        ArrivalSlot& sl = slots_[k];
+        sl.body = reinterpret_cast<const uint8_t*>(c->in.data()) + b0;
+        sl.dst = c->pdec.p;
+        sl.cap = c->pdec.cap;
+        sl.nl = &c->pdec.nl;
+        sl.pf = c->pf;
+        sl.avail.store(0, std::memory_order_relaxed);   // (the slot's previous body's length)
+        sl.seen.store(0, std::memory_order_relaxed);
+        c->slot = k;
+        c->slot_b0 = b0;
+        c->slot_len = (size_t)clen;
+        arrivals_.fetch_add(1);
+        sl.state.store(ArrivalSlot::IDLE, std::memory_order_release);
+        publish_arrival(c);
+      } else {                                   // every slot taken: decode here between reads
+        const double t0 = now_s();
+        logs_prefetch(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, c->in.size() - b0, c->pf, c->pdec.p,
+                      c->pdec.cap, &c->pdec.nl);
+        stages.prefetch_ns += (uint64_t)std::max(0.0, (now_s() - t0) * 1e9);
+      }
     }
     return false;
   }
   c->sent_continue = false;
   stats.requests++;
+  if (c->slot >= 0) {                            // the pump's part of the decoding is done
+    ArrivalSlot* sl = acquire_slot(c);
+    c->pf = sl->pf;
+    sl->state.store(ArrivalSlot::FREE, std::memory_order_release);
+    arrivals_.fetch_sub(1);
+    c->slot = -1;
+  }
+  c->early = false;
   // the body's prefetch state (only for this request: reset whatever the outcome)
   LogsPrefetch pf = c->pf;
   DecodeBuf pdec = std::move(c->pdec);
@@ -827,7 +971,26 @@ void HttpServer::handle_readable(Io* io, Conn* c) {
         c->n_wake = 1;
       }
       c->n_recv++;
-      c->in.append(buf, (size_t)k);
+      if (c->slot >= 0 && c->in.size() + (size_t)k > c->in.capacity()) {
+        // the buffer moves: take the body back from the pump for the append
+        ArrivalSlot* sl = acquire_slot(c);
+        c->in.append(buf, (size_t)k);
+        sl->body = reinterpret_cast<const uint8_t*>(c->in.data()) + c->slot_b0;
+        sl->state.store(ArrivalSlot::IDLE, std::memory_order_release);
+      } else {
+        c->in.append(buf, (size_t)k);
+      }
+      if (c->slot >= 0) {
+        publish_arrival(c);
+      } else if (!c->early && !c->busy && !c->closing && c->in.size() >= (64u << 10) && prefetch_) {
+        // a large body is streaming in faster than this loop drains the socket: parse its headers
+        // now (once), so its arrival slot is registered while the rest is still coming
+        c->early = true;
+        if (parse_one(io, c) || c->dead) {
+          c->early = false;                      // (a complete request was dispatched here)
+          if (c->dead) return;
+        }
+      }
       if ((int64_t)c->in.size() > max_body_ + (int64_t)kMaxHeader + 4) {
         if (c->busy) {  // stop reading until the in-flight request is answered
           c->paused = true;

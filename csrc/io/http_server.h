@@ -107,7 +107,7 @@ struct HttpStats {
 // (inside `receive`), prefetched = bodies whose final validation resumed a prefetch.
 struct HttpStageStats {
   std::atomic<uint64_t> parse{0}, receive_ns{0}, validate_ns{0}, drained{0}, queue_ns{0};
-  std::atomic<uint64_t> prefetch_ns{0}, prefetched{0};
+  std::atomic<uint64_t> prefetch_ns{0}, prefetched{0}, pump_prefetch_ns{0};
   std::atomic<uint64_t> responses{0}, handoff_ns{0}, sent{0}, send_ns{0};
 };
 
@@ -121,6 +121,26 @@ struct HttpOptions {
   bool trace = false;           // per-request receive / validate timings on stderr
   bool conn_trace = false;      // per /parse response: accept / first byte / parsed / handed back / sent times
   bool prefetch = true;         // decode a large /parse body's logs string while it arrives
+};
+
+// A large /parse body still arriving, registered by its IO thread so that the PUMP thread -- idle,
+// spinning in next_requests while it waits for the next request -- decodes the arrived part of its
+// logs string (logs_prefetch) on another core while the IO thread keeps receiving (the IO thread
+// was the receive's bottleneck: decoding there moved ~40-70 us per MB into the receive, profiles/r6_e).
+// Slots are never freed, so a thread reading one never dereferences a dead object; the state word
+// decides who may touch the body, the decode buffer and the prefetch state:
+//   FREE -> (IO thread registers) -> IDLE <-> PUMP (one prefetch step) ; IDLE -> IO (the IO thread
+//   takes it back: body complete, buffer about to grow, connection closing) -> FREE.
+struct ArrivalSlot {
+  enum { FREE = 0, IDLE = 1, PUMP = 2, IO = 3 };
+  std::atomic<int> state{FREE};
+  std::atomic<size_t> avail{0};   // body bytes arrived (release-stored by the IO thread)
+  std::atomic<size_t> seen{0};    // avail at the pump's last step (~0: nothing more to do)
+  const uint8_t* body = nullptr;  // the connection's receive buffer at the body start
+  char* dst = nullptr;            // the decode buffer
+  size_t cap = 0;
+  NlPos* nl = nullptr;
+  LogsPrefetch pf;
 };
 
 class HttpServer {
@@ -174,6 +194,9 @@ class HttpServer {
   void set_events(Io* io, Conn* c);
   void close_conn(Io* io, Conn* c);
   std::string take_buffer();
+  bool advance_arrivals();                 // pump: one prefetch step per arrival slot with new bytes
+  void publish_arrival(Conn* c);           // IO thread: the registered body's arrived length
+  ArrivalSlot* acquire_slot(Conn* c);      // IO thread: take the connection's slot back (IO state)
 
   std::string host_;
   int port_;
@@ -197,6 +220,18 @@ class HttpServer {
   std::atomic<uint64_t> next_id_{1};
   std::shared_ptr<BufferPool> pool_ = std::make_shared<BufferPool>();
   std::shared_ptr<DecodePool> dpool_ = std::make_shared<DecodePool>();
+  static constexpr int kSlots = 32;
+  ArrivalSlot slots_[kSlots];
+  std::atomic<int> arrivals_{0};           // registered slots (the pump wakes up for them)
+  std::atomic<uint64_t> arr_gen_{0};       // bumped on every arrival the pump could act on
+  std::atomic<bool> pump_waiting_{false};  // the pump sleeps on qcv_ (an arrival then notifies)
+  // the decode helper: a thread that only advances the arrival slots (the pump helps while it
+  // waits, but it is often still finishing the previous request when the next body starts)
+  std::thread helper_;
+  std::mutex hm_;
+  std::condition_variable hcv_;
+  std::atomic<bool> helper_waiting_{false};
+  void helper_loop();
 };
 
 }  // namespace lp

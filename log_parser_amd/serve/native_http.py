@@ -53,13 +53,18 @@ class NativeHttpFrontend:
         eng = b.pipe.engine
         if eng.device.type != "cuda":
             return None
-        from ..utils.numa import l3_groups
+        from ..utils.numa import l3_groups, one_per_core
         allowed = os.sched_getaffinity(0)
         groups = l3_groups(allowed)
         if len(groups) < 2 or len(groups[0]) < io_threads + 2:
             return None
-        os.sched_setaffinity(0, groups[0])
-        log.info("IO threads and pump on the %d CPUs of one L3: %s", len(groups[0]), sorted(groups[0]))
+        # one hardware thread per core: the pump decodes a body while an IO thread receives it
+        # (arrival slots), and on SMT siblings the two slowed each other
+        cpus = one_per_core(groups[0])
+        if len(cpus) < io_threads + 2:
+            cpus = groups[0]
+        os.sched_setaffinity(0, cpus)
+        log.info("IO threads and pump on %d CPUs (one per core) of one L3: %s", len(cpus), sorted(cpus))
         return allowed
 
     def _start(self, cfg, host: str, port: int, io_threads: int, trace: bool) -> None:

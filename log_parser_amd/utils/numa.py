@@ -89,6 +89,25 @@ def l3_groups(cpus: Set[int]) -> list:
     return sorted(groups.values(), key=lambda g: (-len(g), min(g)))
 
 
+def one_per_core(cpus: Set[int]) -> Set[int]:
+    """``cpus`` with one hardware thread per physical core (the lowest sibling present): threads that
+    work at the same time -- the HTTP IO thread receiving a body and the pump decoding it -- on SMT
+    siblings of one core share its execution units (the receive ran ~2x slower, profiles/r6_e)."""
+    out: Set[int] = set()
+    seen = set()
+    for c in sorted(cpus):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib = frozenset(_parse_cpulist(f.read().strip()))
+        except OSError:
+            sib = frozenset([c])
+        if sib in seen:
+            continue
+        seen.add(sib)
+        out.add(c)
+    return out
+
+
 def cpu_limits() -> dict:
     """The two limits behind ``cpu_budget``: the affinity set and the cgroup CPU quota (None: none)."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)

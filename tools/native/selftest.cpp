@@ -229,10 +229,11 @@ static void http_prefetch_selftest(int rounds) {
   }
   done = true;
   responder.join();
-  const uint64_t pre = srv.stages.prefetched.load();
+  const uint64_t pre = srv.stages.prefetched.load(), pump_ns = srv.stages.pump_prefetch_ns.load();
   srv.stop();
   CHECK(ok == rounds, "http prefetch: %d of %d responses", ok, rounds);
   CHECK(pre > 0, "http prefetch: no body was prefetched");
+  CHECK(pump_ns > 0, "http prefetch: the responder (pump) thread decoded nothing while bodies arrived");
   std::printf("http prefetch: %d large bodies, %llu prefetched\n", ok, (unsigned long long)pre);
 }
 

@@ -1194,7 +1194,8 @@ PYBIND11_MODULE(_lpnative, m) {
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> g0,
                      py::array_t<int64_t, py::array::c_style | py::array::forcecast> n, py::tuple ring,
                      double evict_before, double now, uint64_t stream, int64_t host_cap, Turn* turn, int64_t seq,
-                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> inj, SharedWindow* hw) {
+                     py::array_t<int64_t, py::array::c_style | py::array::forcecast> inj, SharedWindow* hw,
+                     int64_t pre_token) {
         const FreqRing R = hw ? FreqRing{} : ring_from(ring);
         const int D = (int)lo.shape(0);
         int64_t ne;
@@ -1202,7 +1203,7 @@ PYBIND11_MODULE(_lpnative, m) {
           py::gil_scoped_release nogil;
           ne = r.run(P<uint8_t>(text), nbytes, P<const int64_t>(starts), P<const int32_t>(lens), L, lo.data(), hi.data(),
                      g0.data(), n.data(), D, R, evict_before, now, stream, host_cap, turn, seq,
-                     inj.size() ? inj.data() : nullptr, (int64_t)inj.size(), hw);
+                     inj.size() ? inj.data() : nullptr, (int64_t)inj.size(), hw, pre_token);
         }
         py::array_t<uint8_t> out((py::ssize_t)r.result_bytes());
         std::memcpy(out.mutable_data(), r.result(), r.result_bytes());
@@ -1214,8 +1215,12 @@ PYBIND11_MODULE(_lpnative, m) {
       }, py::arg("text"), py::arg("nbytes"), py::arg("starts"), py::arg("lens"), py::arg("L"), py::arg("lo"),
          py::arg("hi"), py::arg("g0"), py::arg("n"), py::arg("ring"), py::arg("evict_before"), py::arg("now"),
          py::arg("stream"), py::arg("host_cap") = 0, py::arg("turn") = nullptr, py::arg("seq") = 0,
-         py::arg("inj") = py::array_t<int64_t>(0), py::arg("hw") = nullptr)
+         py::arg("inj") = py::array_t<int64_t>(0), py::arg("hw") = nullptr, py::arg("pre_token") = 0)
       .def_property_readonly("recorded", &RequestRunner::recorded)
+      .def("prefetch_text", [](RequestRunner& r, uint64_t text, int64_t nbytes, int64_t host_cap, uint64_t stream) {
+        py::gil_scoped_release nogil;
+        return r.prefetch_text(P<uint8_t>(text), nbytes, host_cap, stream);   // token for run(pre_token=)
+      }, py::arg("text"), py::arg("nbytes"), py::arg("host_cap"), py::arg("stream"))
       .def("upload_bytes", &RequestRunner::upload_bytes);
 
   // arrival-order gate of a window shared by several runners (csrc/runtime/request.h)
@@ -1330,6 +1335,7 @@ PYBIND11_MODULE(_lpnative, m) {
       .def("__len__", [](const RawLogs& r) { return r.len; })
       .def("decode", &raw_logs_decode, "the unescaped UTF-8 log text")
       .def_property_readonly("escaped_len", [](const RawLogs& r) { return r.len; })
+      .def_property_readonly("decoded_len", [](const RawLogs& r) { return r.dlen; })
       // decoded by the IO thread into a pinned buffer: (address, capacity) -- the engine stages this
       // request in place; (0, 0) otherwise
       .def_property_readonly("pinned_text", [](const RawLogs& r) {

@@ -100,11 +100,44 @@ int64_t RequestRunner::upload_bytes(int64_t nbytes, int64_t L, int D) const {
   return (int64_t)((n + 15) & ~size_t(15));
 }
 
+bool RequestRunner::map_fetch(uint8_t* host_text, int64_t host_cap) {
+  if (host_text != fetch_host_ || host_cap != fetch_cap_) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, host_text, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      d = nullptr;
+    }
+    fetch_host_ = host_text;
+    fetch_cap_ = host_cap;
+    fetch_dev_ = static_cast<uint8_t*>(d);
+  }
+  return fetch_dev_ != nullptr;
+}
+
+int64_t RequestRunner::prefetch_text(uint8_t* host_text, int64_t nbytes, int64_t host_cap, uint64_t stream) {
+  pre_host_ = nullptr;
+  pre_n_ = -1;
+  pre_token_ = 0;
+  const int64_t tsize = padded_len(nbytes);
+  if (!fetch_ || !ws_ || (size_t)tsize > ws_cap_ || host_cap < tsize || (size_t)tsize > kFetchMaxBytes ||
+      ((uintptr_t)host_text & 15) != 0)
+    return 0;
+  check(hipSetDevice(S_.device), "set device");
+  if (!map_fetch(host_text, host_cap)) return 0;
+  std::memset(host_text + nbytes, 0, (size_t)(tsize - nbytes));       // vector loads past the end
+  fetch_dev(fetch_dev_, ws_, tsize / 16, stream, nullptr, 0.0);       // the text is the carve's first region
+  pre_host_ = host_text;
+  pre_n_ = nbytes;
+  pre_ws_ = ws_;
+  pre_token_ = ++pre_next_;
+  return pre_token_;
+}
+
 int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* starts, const int32_t* lens, int64_t L,
                            const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n,
                            int D, const FreqRing& ring, double evict_before, double now, uint64_t stream,
                            int64_t host_cap, Turn* turn, int64_t seq, const int64_t* inj, int64_t ninj,
-                           HostWindow* hw) {
+                           HostWindow* hw, int64_t pre_token) {
   if (hw && turn) throw std::invalid_argument("request runner: a host window or a turn, not both");
   // a shared window: released on every exit, also when a HIP call throws
   struct Release {
@@ -137,18 +170,14 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
   const uint8_t* text_dev_src = nullptr;
   // (request-sized uploads only: a multi-MB batch moves faster on the SDMA engine, ~50 vs ~37 GB/s)
   if (one_copy && fetch_ && up_total <= kFetchMaxBytes && ((uintptr_t)host_text & 15) == 0) {
-    if (host_text != fetch_host_ || host_cap != fetch_cap_) {
-      void* d = nullptr;
-      if (hipHostGetDevicePointer(&d, host_text, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        d = nullptr;
-      }
-      fetch_host_ = host_text;
-      fetch_cap_ = host_cap;
-      fetch_dev_ = static_cast<uint8_t*>(d);
-    }
+    map_fetch(host_text, host_cap);
     text_dev_src = fetch_dev_;
   }
+  // the text already on its way (prefetch_text, same buffer and length): upload what follows it
+  bool text_up = pre_token > 0 && pre_token == pre_token_ && pre_host_ == host_text && pre_n_ == nbytes;
+  pre_host_ = nullptr;
+  pre_n_ = -1;
+  pre_token_ = 0;
   uint8_t* segh;
   if (one_copy) {
     if (L > 0) {
@@ -319,7 +348,12 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, 4 * (size_t)std::max<int64_t>(L, 1) + 4096);
     }
     // inputs: packed text, line index, segments (all pinned -> async)
-    if (one_copy && text_dev_src) {   // (a re-run's eviction is a no-op: the window's head moved)
+    if (text_up && (ws_ != pre_ws_ || text != ws_)) text_up = false;   // (the workspace moved: all again)
+    if (one_copy && text_dev_src && text_up && attempt == 0) {
+      const size_t o_rest = o_ls;                // 256-aligned: the index, segments, counters, carry
+      fetch_dev(text_dev_src + o_rest, text + o_rest, (int64_t)((up_total - o_rest) / 16), stream,
+                evict_in_fetch ? &ring : nullptr, evict_before);
+    } else if (one_copy && text_dev_src) {   // (a re-run's eviction is a no-op: the window's head moved)
       fetch_dev(text_dev_src, text, (int64_t)(up_total / 16), stream, attempt == 0 && evict_in_fetch ? &ring : nullptr,
                 evict_before);
     } else if (one_copy) {

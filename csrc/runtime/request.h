@@ -136,7 +136,15 @@ class RequestRunner {
               const int32_t* seg_lo, const int32_t* seg_hi, const int64_t* seg_g0, const int64_t* seg_n, int D,
               const FreqRing& ring, double evict_before, double now, uint64_t stream, int64_t host_cap = 0,
               Turn* turn = nullptr, int64_t seq = 0, const int64_t* inj = nullptr, int64_t ninj = 0,
-              HostWindow* hw = nullptr);
+              HostWindow* hw = nullptr, int64_t pre_token = 0);
+  // Queue the upload of a request's packed TEXT (host_text[0, nbytes), pinned, 16-byte aligned) into
+  // the workspace ahead of run(): the caller still builds the line index meanwhile (the text of a
+  // /parse body is in its pinned decode buffer as soon as the body is validated). run() with the
+  // same host_text / nbytes then uploads only what follows the text. Only when nothing in flight
+  // uses the workspace (a lone request; the caller's job) and the workspace already holds the
+  // text.
+  // Returns a token (> 0) for run(pre_token = ...), 0 when nothing was queued.
+  int64_t prefetch_text(uint8_t* host_text, int64_t nbytes, int64_t host_cap, uint64_t stream);
   // the batch's frequency record was enqueued (a failure after it must not record the batch again)
   bool recorded() const { return recorded_; }
   // host bytes the single-copy upload needs (text padded, index, segments, counters, carry)
@@ -170,6 +178,11 @@ class RequestRunner {
   uint8_t* fetch_host_ = nullptr;      // last stage buffer seen ...
   uint8_t* fetch_dev_ = nullptr;       // ... and its device address (null: not mapped, SDMA copy)
   int64_t fetch_cap_ = 0;
+  uint8_t* pre_host_ = nullptr;        // prefetch_text: the text queued ahead of run() ...
+  int64_t pre_n_ = -1;                 // ... its length ...
+  uint8_t* pre_ws_ = nullptr;          // ... into this workspace ...
+  int64_t pre_token_ = 0, pre_next_ = 0;   // ... under this token (run() must name it)
+  bool map_fetch(uint8_t* host_text, int64_t host_cap);   // fetch_dev_ for host_text (k_fetch source)
   RequestCounts counts_;
   int64_t stride_ = 0;
   bool recorded_ = false;

@@ -252,6 +252,7 @@ class BatchJob:
     timings: Optional[dict] = None
     outs: Optional[List[bytes]] = None  # responses computed by the device stage itself
     recorded: bool = False              # its counts entered the frequency window (a fallback must not re-record)
+    pre_token: int = 0                  # RequestRunner.prefetch_text token (its text already uploading)
 
 
 class Stage:
@@ -839,8 +840,10 @@ class Engine:
         finally:
             self.release_batch(job)
 
-    def pack_batch(self, logs_list: Sequence) -> "BatchJob":
-        """Stage 1 (host): pack the request bodies into a pinned staging buffer + line index."""
+    def pack_batch(self, logs_list: Sequence, early_upload: bool = False) -> "BatchJob":
+        """Stage 1 (host): pack the request bodies into a pinned staging buffer + line index.
+        ``early_upload``: nothing else uses the device half (a lone batch run inline) -- a request
+        staged in place has its text queued for upload before the line index is built."""
         t0 = time.time()
         self._batches += 1
         job = BatchJob(logs=logs_list, t0=t0, tm={} if self.profile else None, number=self._batches)
@@ -850,7 +853,7 @@ class Engine:
         job.stage = self._stage_pool.take()
         try:
             with TR.HostTimer(job.tm, "line_index"):
-                staged = self._stage_docs(job, logs_list)
+                staged = self._stage_docs(job, logs_list, early_upload)
                 if staged is None:              # lone surrogates: encode in Python
                     staged = self._stage_docs(job, [l if isinstance(l, (bytes, bytearray)) else
                                                     l.encode("utf-8", errors="surrogatepass") for l in logs_list])
@@ -1045,7 +1048,7 @@ class Engine:
         if win is not None:                 # the node's host window (serving processes)
             try:
                 ne, out, counts, E = self._runner.run(*args, (), 0.0, fr.clock(), stream, st.buf.numel(), inj=inj,
-                                                      hw=win)
+                                                      hw=win, pre_token=job.pre_token)
             except BaseException:
                 job.recorded = bool(self._runner.recorded)
                 raise
@@ -1058,7 +1061,7 @@ class Engine:
                 # host_cap: the stage's room behind the text lets the runner send text, line index,
                 # segments and zeroed counters in ONE H2D copy (request.cpp, single-copy layout)
                 ne, out, counts, E = self._runner.run(*args, fr._ring(), evict_before, now, stream, st.buf.numel(),
-                                                      inj=inj)
+                                                      inj=inj, pre_token=job.pre_token)
                 if K:
                     fr._tail_bound += K
         else:
@@ -1076,7 +1079,7 @@ class Engine:
                 turn.host.done(seq)
             try:
                 ne, out, counts, E = self._runner.run(*args, ring, evict_before, now, stream, st.buf.numel(),
-                                                      turn=turn.dev, seq=seq, inj=inj)
+                                                      turn=turn.dev, seq=seq, inj=inj, pre_token=job.pre_token)
             except BaseException:
                 job.recorded = bool(self._runner.recorded)
                 raise
@@ -1132,7 +1135,7 @@ class Engine:
     inplace_stages = 0          # batches staged in place in a request's pinned decode buffer
     _pinned_views: dict = {}    # (address, capacity) of a pinned decode buffer -> its uint8 tensor view
 
-    def _stage_docs(self, job: "BatchJob", docs):
+    def _stage_docs(self, job: "BatchJob", docs, early_upload: bool = False):
         """Pack request bodies into the job's (pinned) staging buffer and build the per-document
         line index, in native code with the GIL released (csrc/io/docs.cpp): one host copy per
         byte; the index goes straight into the stage's pinned index buffer when it fits.
@@ -1148,6 +1151,11 @@ class Engine:
             # uploads from it and the emitter reads it). The RawLogs in job.logs keeps it alive.
             addr, pcap = docs[0].pinned_text
             if addr:
+                if early_upload and self._runner:
+                    # the text is final: its upload runs while the line index is built (RequestRunner
+                    # .prefetch_text; run(pre_token=) then sends only what follows the text)
+                    job.pre_token = self._runner.prefetch_text(addr, docs[0].decoded_len, pcap,
+                                                               torch.cuda.current_stream(self.device).cuda_stream)
                 r = N.pack_split_docs(docs, addr, pcap - K.TEXT_PAD - K.NL_TILE, self._STAGE_THREADS,
                                       st.idx.data_ptr(), st.cap)
                 if isinstance(r, tuple) and r[1] is None:

@@ -62,7 +62,7 @@ class BatchPipeline:
         """All three stages on the calling thread (lowest latency for a lone batch)."""
         assert self.idle(), "inline batch while the pipeline is busy would reorder frequency updates"
         t0 = time.perf_counter()
-        job = self.engine.pack_batch(logs)
+        job = self.engine.pack_batch(logs, early_upload=True)
         try:
             t1 = time.perf_counter()
             self._device_fn(job)

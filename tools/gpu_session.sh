@@ -14,6 +14,6 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
 
 run gpuserve 600 python -u -m pytest tests/test_gpu_serving.py tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread
 for k in 1 2 3; do
-  run pump_$k 300 python -u tools/parse_stages.py --n 400
-  run nopf_$k 300 python -u tools/parse_stages.py --n 400 -D server.prefetch-logs=false
+  run early_$k 300 python -u tools/parse_stages.py --n 400
 done
+run bench7 300 python -u bench.py --steps 10 --warmup 3

@@ -126,9 +126,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     "server.numa-bind": (True, bool),
     # native front end: close keep-alive connections idle this long (no request in flight)
     "server.idle-timeout-s": (60.0, float),
-    # native front end over a GPU engine: start the IO threads and the pump on the CPUs of ONE last-level
-    # cache (a CCD): the IO thread decodes a request body that the pump then packs -- across CCDs that
-    # hand-off of ~1 MB ran 2-3x slower (profiles/r6_d)
+    # native front end over a GPU engine: start the IO threads, the pump and the decode helper on one
+    # hardware thread per core of ONE last-level cache (a CCD): a body received by an IO thread is
+    # decoded by the helper and packed by the pump (a lone-body A/B was within run-to-run spread,
+    # profiles/r6_d; on SMT siblings the receiving and the decoding thread share a core)
     "server.l3-affinity": (True, bool),
     # native front end: a POST /parse body of >= 64 KiB has its `logs` string validated and decoded
     # by the IO thread between reads while it arrives; the final parse resumes there (csrc/io/json_in.h

@@ -12,8 +12,4 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run gpuserve 600 python -u -m pytest tests/test_gpu_serving.py tests/test_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread
-for k in 1 2 3; do
-  run early_$k 300 python -u tools/parse_stages.py --n 400
-done
-run bench7 300 python -u bench.py --steps 10 --warmup 3
+run single 600 python -u benchmarks/bench_configs.py single

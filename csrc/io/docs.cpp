@@ -191,6 +191,16 @@ static void parallel_units(std::vector<Unit>& U, int64_t total, int nthreads, in
   HostPool::get().run(n, T, [&](int64_t u) { fn(U[u]); });
 }
 
+void copy_cached(uint8_t* dst, const uint8_t* src, int64_t n) {
+#if defined(__x86_64__)
+  if (__builtin_cpu_supports("avx512f")) {
+    copy_cached_512(dst, src, n);
+    return;
+  }
+#endif
+  std::memcpy(dst, src, (size_t)n);
+}
+
 void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, uint8_t* dst, int nthreads,
                      DocBatchIndex& out, int64_t min_bytes_per_thread, const int64_t* const* nlpos,
                      const int64_t* nlcnt) {
@@ -209,14 +219,8 @@ void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, 
     const int64_t s0 = doc_off[u.doc];
     if (nlpos && nlpos[u.doc]) {
       const int64_t c = nlcnt[u.doc];
-      if (src[u.doc] != reinterpret_cast<const char*>(dst + u.a)) {
-#if defined(__x86_64__)
-        if (__builtin_cpu_supports("avx512f"))
-          copy_cached_512(dst + u.a, reinterpret_cast<const uint8_t*>(src[u.doc]), u.b - u.a);
-        else
-#endif
-          std::memcpy(dst + u.a, src[u.doc], (size_t)(u.b - u.a));
-      }
+      if (src[u.doc] != reinterpret_cast<const char*>(dst + u.a))
+        copy_cached(dst + u.a, reinterpret_cast<const uint8_t*>(src[u.doc]), u.b - u.a);
       u.nl.reserve(c + 1);
       const int64_t* q = nlpos[u.doc];
       for (int64_t j = 0; j < c; ++j) u.nl.p[j] = q[j] + u.a;

@@ -47,6 +47,10 @@ struct DocBatchIndex {
 // nthreads <= 1 runs inline. nlpos[d] (optional, non-null per document): the positions of document
 // d's '\n' bytes, nlcnt[d] of them, already known (the HTTP front end's decoder recorded them) --
 // that document is copied without a newline scan.
+// dst[0, n) = src[0, n) through the cache (AVX-512 stores; glibc's memcpy streams megabyte copies
+// past it, and the packed text is read again right after)
+void copy_cached(uint8_t* dst, const uint8_t* src, int64_t n);
+
 void pack_split_docs(const char* const* src, const int64_t* doc_off, int64_t D, uint8_t* dst, int nthreads,
                      DocBatchIndex& out, int64_t min_bytes_per_thread = int64_t(4) << 20,
                      const int64_t* const* nlpos = nullptr, const int64_t* nlcnt = nullptr);

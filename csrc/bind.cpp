@@ -1381,6 +1381,8 @@ PYBIND11_MODULE(_lpnative, m) {
                                  },
                                  [](void* q) { (void)hipHostFree(q); });
            }, py::arg("limit"), py::arg("min_bytes") = size_t(256) << 10)
+      .def("set_affinity_sets", &HttpServer::set_affinity_sets, py::arg("narrow"), py::arg("wide"), py::arg("hi"),
+           py::arg("lo"))
       .def("pending", &HttpServer::pending)
       .def("next_requests", [](HttpServer& s, int max_n, int timeout_ms, bool raw) {
         std::vector<HttpRequest> v;

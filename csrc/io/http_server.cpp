@@ -33,6 +33,8 @@ constexpr size_t kMaxHeader = 64 << 10;
 constexpr int kMaxIo = 255;
 // /parse bodies from this size on have their logs string decoded while they arrive
 constexpr int64_t kPrefetchMin = 64 << 10;
+// ... while its IO thread holds at most this many connections
+constexpr size_t kPrefetchMaxConns = 64;
 const char kInvalid[] = "{\"error\":\"Invalid PodFailureData provided\"}";
 const char kUnsupported[] = "{\"error\":\"Content-Type must be application/json\"}";
 
@@ -261,6 +263,8 @@ struct HttpServer::Conn {
 
 struct HttpServer::Io {
   int ep = -1, lfd = -1, efd = -1, index = 0;
+  int wide = -1;                          // CPU set in force: -1 none set, 0 narrow, 1 wide
+  uint64_t aff_gen = 0;
   uint64_t next_conn = 1;
   std::unordered_map<uint64_t, Conn*> conns;
   std::vector<Conn*> graveyard;   // closed this iteration (callers may still hold the pointer)
@@ -613,6 +617,26 @@ void HttpServer::close_conn(Io* io, Conn* c) {
   io->graveyard.push_back(c);
 }
 
+void HttpServer::set_affinity_sets(const std::vector<int>& narrow, const std::vector<int>& wide, int hi, int lo) {
+  {
+    std::lock_guard<std::mutex> g(qm_);          // (read by the IO threads under the same lock)
+    aff_narrow_ = narrow;
+    aff_wide_ = wide;
+  }
+  aff_hi_ = hi;
+  aff_lo_ = lo;
+  aff_gen_.fetch_add(1);
+}
+
+static void apply_cpus(const std::vector<int>& cpus) {
+  if (cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus)
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
+}
+
 void HttpServer::helper_loop() {
   while (!stop_) {
     // spin while registered bodies make progress (a step per 32-64 KiB of arrival); sleep after
@@ -801,7 +825,9 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     if (c->slot >= 0) {
       publish_arrival(c);
     } else if (prefetch_ && te == TE_NONE && clen >= kPrefetchMin && method == "POST" && route == "/parse" &&
-               json_ctype && c->pf.state >= 0 && c->in.size() > b0) {
+               json_ctype && c->pf.state >= 0 && c->in.size() > b0 && io->conns.size() <= kPrefetchMaxConns) {
+      // (a burst of connections: every IO thread is busy and decodes its own bodies at completion,
+      // side by side; one helper core decoding them all would serialise them)
       if (!c->pdec.p) c->pdec = dpool_->take((size_t)clen + 64);
       // hand the body to the pump thread (arrival slot): it decodes while this thread receives.
       // The receive buffer must not move while registered -- room for some pipelined bytes too
@@ -982,7 +1008,8 @@ void HttpServer::handle_readable(Io* io, Conn* c) {
       }
       if (c->slot >= 0) {
         publish_arrival(c);
-      } else if (!c->early && !c->busy && !c->closing && c->in.size() >= (64u << 10) && prefetch_) {
+      } else if (!c->early && !c->busy && !c->closing && c->in.size() >= (64u << 10) && prefetch_ &&
+                 io->conns.size() <= kPrefetchMaxConns) {
         // a large body is streaming in faster than this loop drains the socket: parse its headers
         // now (once), so its arrival slot is registered while the rest is still coming
         c->early = true;
@@ -1095,6 +1122,26 @@ void HttpServer::io_loop(Io* io) {
         }
         handle_readable(io, c);
       }
+    }
+    // CPU set by load (set_affinity_sets): wide under a burst of connections, narrow again when few
+    const uint64_t ag = aff_gen_.load(std::memory_order_relaxed);
+    if (ag != 0) {
+      const size_t nc = io->conns.size();
+      int want = io->wide;
+      if (ag != io->aff_gen) want = -1;          // (new sets: re-apply)
+      if (want != 1 && (int64_t)nc > aff_hi_.load(std::memory_order_relaxed)) want = 1;
+      else if (want != 0 && (int64_t)nc < aff_lo_.load(std::memory_order_relaxed)) want = 0;
+      else if (want < 0) want = 0;
+      if (want != io->wide) {
+        std::vector<int> cpus;
+        {
+          std::lock_guard<std::mutex> g(qm_);
+          cpus = want == 1 ? aff_wide_ : aff_narrow_;
+        }
+        apply_cpus(cpus);
+        io->wide = want;
+      }
+      io->aff_gen = ag;
     }
     // idle sweep (slow / stalled clients): a connection without a request in flight and without
     // traffic for idle_timeout_s is closed

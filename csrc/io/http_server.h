@@ -167,6 +167,10 @@ class HttpServer {
   void recycle(std::string&& buf) { pool_->give(std::move(buf)); }
   const std::shared_ptr<BufferPool>& pool() const { return pool_; }
   const std::shared_ptr<DecodePool>& decode_pool() const { return dpool_; }
+  // IO-thread CPU sets by load: an IO thread holding more than `hi` connections moves itself to
+  // `wide` (a burst needs every core), back to `narrow` (the cores of the decode helper's L3) below
+  // `lo`. Empty sets: no change.
+  void set_affinity_sets(const std::vector<int>& narrow, const std::vector<int>& wide, int hi, int lo);
   // up to `limit` pinned decode buffers for bodies >= min_bytes (a GPU engine serves this server)
   void set_pinned_decode(int limit, size_t min_bytes, void* (*alloc)(size_t), void (*release)(void*)) {
     dpool_->pinned_min = min_bytes;
@@ -232,6 +236,10 @@ class HttpServer {
   std::condition_variable hcv_;
   std::atomic<bool> helper_waiting_{false};
   void helper_loop();
+  // set_affinity_sets
+  std::vector<int> aff_narrow_, aff_wide_;
+  std::atomic<int> aff_hi_{0}, aff_lo_{0};
+  std::atomic<uint64_t> aff_gen_{0};       // bumped by set_affinity_sets (IO threads re-apply)
 };
 
 }  // namespace lp

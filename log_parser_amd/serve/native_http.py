@@ -38,6 +38,10 @@ class NativeHttpFrontend:
         restore = self._l3_affinity(cfg, io_threads, b)
         try:
             self._start(cfg, host, port, io_threads, trace)
+            if restore is not None:
+                # IO threads leave the L3 group under a burst of connections (config 5: ~80k vs 63-69k
+                # req/s squeezed onto one CCD, profiles/r6_g) and come back when few remain
+                self.srv.set_affinity_sets(sorted(os.sched_getaffinity(0)), sorted(restore), 64, 8)
         finally:
             if restore is not None:
                 os.sched_setaffinity(0, restore)
@@ -58,10 +62,12 @@ class NativeHttpFrontend:
         groups = l3_groups(allowed)
         if len(groups) < 2 or len(groups[0]) < io_threads + 2:
             return None
-        # one hardware thread per core: the pump decodes a body while an IO thread receives it
-        # (arrival slots), and on SMT siblings the two slowed each other
+        # one hardware thread per core when that leaves a core for each IO thread, the pump and the
+        # decode helper (a body's receiving IO thread and the helper decoding it share a core's units
+        # on SMT siblings); else the whole L3 group: a burst of many connections needs every IO thread
+        # (config 5 on 8 single-thread cores: 66-69k req/s against 80k unpinned, profiles/r6_g)
         cpus = one_per_core(groups[0])
-        if len(cpus) < io_threads + 2:
+        if len(cpus) < io_threads + 3:
             cpus = groups[0]
         os.sched_setaffinity(0, cpus)
         log.info("IO threads and pump on %d CPUs (one per core) of one L3: %s", len(cpus), sorted(cpus))

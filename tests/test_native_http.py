@@ -431,3 +431,60 @@ def test_load_generator_burst_over_many_connections(server):
     idx = np.arange(256, dtype=np.int32) % 3
     lat, st, wall, done = N.http_burst("127.0.0.1", fe.port, msgs, idx, 120.0)
     assert done == 256 and (st == 200).all() and (lat > 0).all() and wall >= lat.max() * 0.5
+
+
+def _io_thread_cpus():
+    """CPU lists of this process's native HTTP IO threads (named lp-io<k>)."""
+    import os
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                name = f.read().strip()
+            if not name.startswith("lp-io"):
+                continue
+            with open(f"/proc/self/task/{tid}/status") as f:
+                for line in f:
+                    if line.startswith("Cpus_allowed_list:"):
+                        out[name] = line.split(":", 1)[1].strip()
+        except OSError:
+            pass
+    return out
+
+
+def test_io_threads_widen_under_a_burst_and_narrow_back():
+    """server.l3-affinity keeps the IO threads on one L3 (a lone /parse body is decoded by a helper
+    core beside its IO thread), but a burst of connections needs every core: an IO thread holding more
+    than `hi` connections moves to the wide CPU set, and back below `lo` (HttpServer.set_affinity_sets)."""
+    import os
+    import time
+    from log_parser_amd.native import N
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < 2:
+        pytest.skip("needs two CPUs")
+    narrow = allowed[:1]
+    srv = N.HttpServer("127.0.0.1", 0, 1, 1 << 20)
+    try:
+        srv.set_affinity_sets(narrow, allowed, 4, 2)
+        s0 = socket.create_connection(("127.0.0.1", srv.port), timeout=10)
+        deadline = time.time() + 10
+        while time.time() < deadline and _io_thread_cpus().get("lp-io0") != str(narrow[0]):
+            time.sleep(0.05)
+        assert _io_thread_cpus().get("lp-io0") == str(narrow[0])
+        burst = [socket.create_connection(("127.0.0.1", srv.port), timeout=10) for _ in range(12)]
+        deadline = time.time() + 10
+        while time.time() < deadline and _io_thread_cpus().get("lp-io0") == str(narrow[0]):
+            for s in burst:                           # traffic wakes the IO thread's loop
+                s.sendall(b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n")
+            time.sleep(0.05)
+        assert _io_thread_cpus().get("lp-io0") != str(narrow[0])
+        for s in burst:
+            s.close()
+        deadline = time.time() + 10
+        while time.time() < deadline and _io_thread_cpus().get("lp-io0") != str(narrow[0]):
+            s0.sendall(b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n")
+            time.sleep(0.05)
+        assert _io_thread_cpus().get("lp-io0") == str(narrow[0])
+        s0.close()
+    finally:
+        srv.stop()

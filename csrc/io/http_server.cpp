@@ -610,6 +610,7 @@ void HttpServer::close_conn(Io* io, Conn* c) {
     arrivals_.fetch_sub(1);
     c->slot = -1;
   }
+  if (c->pdec.p) dpool_->give(std::move(c->pdec));   // (a pinned one keeps the pool's count right)
   c->dead = true;
   epoll_ctl(io->ep, EPOLL_CTL_DEL, c->fd, nullptr);
   close(c->fd);

@@ -12,10 +12,10 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-for k in 1 2 3; do
-  run c5cur_$k 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8
-  run c5none_$k 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8 --server-opt=-Dserver.l3-affinity=false --server-opt=-Dserver.prefetch-logs=false
-done
+run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+run full_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+run full_bench 300 python -u bench.py
 for k in 1 2; do
+  run c5cur_$k 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8
   run l3on_$k 300 python -u tools/parse_stages.py --n 400
 done

@@ -12,10 +12,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-run full_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-run full_bench 300 python -u bench.py
-for k in 1 2; do
-  run c5cur_$k 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8
+run emit 300 python -u tools/emit_time.py
+for k in 1 2 3; do
   run l3on_$k 300 python -u tools/parse_stages.py --n 400
 done

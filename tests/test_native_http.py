@@ -488,3 +488,89 @@ def test_io_threads_widen_under_a_burst_and_narrow_back():
         s0.close()
     finally:
         srv.stop()
+
+
+def test_arrival_slots_pipelined_expect_disconnect_and_exhaustion(server):
+    """Large bodies go through the arrival slots (decoded on the helper core while they arrive):
+    two pipelined in one write (the second one's bytes move the receive buffer while the first is
+    registered), Expect: 100-continue, a client that disconnects mid-body (its slot and buffer are
+    released: later bodies still prefetch), and more bodies in flight at once than there are slots
+    (the rest decode on their IO thread) -- every response equal to the one-shot request's."""
+    import time
+    fe, _, trig = server
+    hdr = b"POST /parse HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n"
+    bodies = [json.dumps({"pod": {"metadata": {"name": f"a{i}"}},
+                          "logs": make_log(900 + 37 * i, trig, seed=60 + i, hit_rate=0.05)}).encode() for i in range(3)]
+    assert all(len(b) >= 64 << 10 for b in bodies)
+
+    def reset():
+        _raw(fe.port, b"DELETE /admin/frequency HTTP/1.1\r\nHost: x\r\n\r\n")
+
+    refs = []
+    for b in bodies:
+        reset()
+        (st, out), = _recv_responses(_conn_send(fe.port, hdr % len(b) + b), 1)
+        assert st == 200
+        refs.append(_strip(json.loads(out)))
+    # two large requests pipelined in one write
+    reset()
+    s = _conn_send(fe.port, hdr % len(bodies[0]) + bodies[0] + hdr % len(bodies[1]) + bodies[1])
+    r = _recv_responses(s, 2)
+    s.close()
+    assert [x[0] for x in r] == [200, 200]
+    assert _strip(json.loads(r[0][1])) == refs[0]
+    # (the second one saw the first one's record in the window: compare everything but the scores)
+    o1 = _strip(json.loads(r[1][1]))
+    assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o1["events"]] == \
+           [(e["lineNumber"], e["matchedPattern"]["id"]) for e in refs[1]["events"]]
+    # Expect: 100-continue, then the body in two halves
+    reset()
+    b = bodies[2]
+    s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+    s.sendall((hdr % len(b)).replace(b"\r\n\r\n", b"\r\nExpect: 100-continue\r\n\r\n"))
+    assert s.recv(1024).startswith(b"HTTP/1.1 100 Continue")
+    s.sendall(b[:len(b) // 2])
+    time.sleep(0.01)
+    s.sendall(b[len(b) // 2:])
+    (st, out), = _recv_responses(s, 1)
+    s.close()
+    assert st == 200 and _strip(json.loads(out)) == refs[2]
+    # a client that leaves mid-body
+    for _ in range(3):
+        s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+        s.sendall(hdr % len(b) + b[:len(b) // 2])
+        time.sleep(0.01)
+        s.close()
+    before = fe.srv.stage_stats()["prefetched"]
+    reset()
+    (st, out), = _recv_responses(_conn_send(fe.port, hdr % len(b) + b, slow=True), 1)
+    assert st == 200 and _strip(json.loads(out)) == refs[2]
+    assert fe.srv.stage_stats()["prefetched"] > before
+    # more bodies in flight than arrival slots (32): all half-sent first, then completed
+    socks = []
+    for i in range(40):
+        s = socket.create_connection(("127.0.0.1", fe.port), timeout=60)
+        s.sendall(hdr % len(bodies[0]) + bodies[0][:len(bodies[0]) // 2])
+        socks.append(s)
+    time.sleep(0.05)
+    for s in socks:
+        s.sendall(bodies[0][len(bodies[0]) // 2:])
+    for s in socks:
+        (st, out), = _recv_responses(s, 1)
+        s.close()
+        o = _strip(json.loads(out))
+        assert st == 200
+        assert [(e["lineNumber"], e["matchedPattern"]["id"]) for e in o["events"]] == \
+               [(e["lineNumber"], e["matchedPattern"]["id"]) for e in refs[0]["events"]]
+
+
+def _conn_send(port, raw: bytes, slow: bool = False):
+    import time
+    s = socket.create_connection(("127.0.0.1", port), timeout=60)
+    if slow:
+        for i in range(0, len(raw), 8191):
+            s.sendall(raw[i:i + 8191])
+            time.sleep(0.0005)
+    else:
+        s.sendall(raw)
+    return s

@@ -320,6 +320,26 @@ size_t hits_dev(const HitsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
 void feat_all_dev(int64_t L, const uint8_t* text, const int64_t* ls, const int32_t* ll, const DfaPool& P,
                   int ctx_trans, int ctx_acc, uint8_t* feat, uint64_t stream);
 size_t events_dev(const EventsArgs& A, void* ws, size_t ws_bytes, uint64_t stream);
+
+// A request's tail in one workgroup (lp_post.hip k_request_tail): hits_dev's and events_dev's small
+// paths (device-count mode, features computed already), score_dev and publish_record_dev in one
+// launch. The results layout is publish_record_dev's.
+struct RequestTailOut {
+  double* score;             // = (double*)out: the score column of the results buffer
+  const uint8_t* out;        // results [score f64 x E | counts i64 x K1 | line | pattern | seg i32 x E]
+  int64_t E;                 // the results' event capacity
+  int K1;                    // max(nkeys, 1)
+  const int64_t* cnt;        // device counters [gram, cand, ver, hits, events]
+  int64_t* cnt_host;         // device views of the pinned host counters / results
+  uint8_t* res_host;
+  const int64_t* counts;     // the batch's per-key counts (results buffer) for the record
+  int K;                     // frequency keys
+  double now;
+  FreqRing ring;
+  RecordGate gate;
+};
+void request_tail_dev(const HitsArgs& HA, const EventsArgs& EA, const ScoreTables& T, const ScoreParams& S,
+                      const FreqIn& F, const RequestTailOut& P, void* ws, size_t ws_bytes, uint64_t stream);
 // capacities of the single-workgroup request path (events, lines): a batch within them can run
 // the event stage in device-count mode
 int64_t request_event_cap();

@@ -451,17 +451,17 @@ __global__ __launch_bounds__(256) void k_cand_verify(HitsArgs A) {
 
 // small path, step 2 (one workgroup): every remaining candidate is verified; sort, keep the first
 // of each (regex, line) run, CSR, event counts and their scan
-__global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
-  __shared__ uint64_t keys[SB_MAX];
-  __shared__ int64_t hk[SB_MAX];
-  __shared__ int64_t scratch[SB_THREADS / 64 + 1];
+// the body of k_hits_small on LDS arrays the caller declares (keys / hk: SB_MAX entries, scratch:
+// SB_THREADS / 64 + 1); *s_nh / *s_ne (LDS) receive the hit and event counts
+__device__ __forceinline__ void hits_small_body(const HitsArgs& A, uint64_t* keys, int64_t* hk, int64_t* scratch,
+                                                int* s_live_p, int64_t* s_nh, int64_t* s_ne) {
+  int& s_live = *s_live_p;
   const int64_t n = A.n;
   const bool dc = A.dcount != nullptr;
   const int64_t n1 = dc ? (int64_t)min((unsigned long long)A.pre_from, A.dcount[0]) : A.pre_from;
   const int64_t n2 = dc ? (int64_t)min((unsigned long long)(n - A.pre_from), A.dcount[1]) : n - A.pre_from;
   // the live entries of both regions, compacted (most prefilter candidates failed their verify and
   // are -1): the sort covers pow2(live), not pow2(used) or the capacities
-  __shared__ int s_live;
   LP_SB_STAMP(0);
   if (threadIdx.x == 0) s_live = 0;
   __syncthreads();
@@ -526,25 +526,30 @@ __global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
   if (threadIdx.x == 0) {
     A.counters[0] = nh;
     A.counters[1] = ne;
+    *s_nh = nh;
+    *s_ne = ne;
   }
   LP_SB_STAMP(4);
   if (threadIdx.x == 0 && g_sb_prof) g_sb_prof[5] = live;
 }
 
-__global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32_t* __restrict__ cov_out) {
+__global__ __launch_bounds__(SB_THREADS) void k_hits_small(HitsArgs A) {
   __shared__ uint64_t keys[SB_MAX];
-  __shared__ int32_t diff[SB_MAX_LINES + 1];
+  __shared__ int64_t hk[SB_MAX];
   __shared__ int64_t scratch[SB_THREADS / 64 + 1];
+  __shared__ int s_live;
+  __shared__ int64_t s_nh, s_ne;
+  hits_small_body(A, keys, hk, scratch, &s_live, &s_nh, &s_ne);
+}
+
+
+
+// the body of k_events_small for nh hits and ne events (both within the capacities) on LDS arrays the
+// caller declares (keys: SB_MAX, diff: SB_MAX_LINES + 1, scratch: SB_THREADS / 64 + 1)
+__device__ __forceinline__ void events_small_body(const EventsArgs& A, int32_t* __restrict__ cov_out, uint64_t* keys,
+                                                  int32_t* diff, int64_t* scratch, int64_t nh, int64_t ne) {
   const EvTables& E = A.ev;
-  int64_t ne = A.ne, nh = A.nh;
   const int64_t L = A.L;
-  if (A.dcounts) {                 // device-count mode: A.ne / A.nh are capacities
-    nh = A.dcounts[0];
-    ne = A.dcounts[1];
-    const bool over = ne > A.ne || nh > A.nh;
-    if (A.ne_fit && threadIdx.x == 0) A.ne_fit[0] = over ? 0 : ne;
-    if (over) return;                     // over capacity: the host re-runs with read counts
-  }
   const int np = sb_pow2(ne);
   LP_SB_STAMP(8);
   for (int i = threadIdx.x; i <= L; i += SB_THREADS) diff[i] = 0;
@@ -611,6 +616,95 @@ __global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32
   if (threadIdx.x == 0 && g_sb_prof) g_sb_prof[14] = ne;
 }
 
+__global__ __launch_bounds__(SB_THREADS) void k_events_small(EventsArgs A, int32_t* __restrict__ cov_out) {
+  __shared__ uint64_t keys[SB_MAX];
+  __shared__ int32_t diff[SB_MAX_LINES + 1];
+  __shared__ int64_t scratch[SB_THREADS / 64 + 1];
+  int64_t ne = A.ne, nh = A.nh;
+  if (A.dcounts) {                 // device-count mode: A.ne / A.nh are capacities
+    nh = A.dcounts[0];
+    ne = A.dcounts[1];
+    const bool over = ne > A.ne || nh > A.nh;
+    if (A.ne_fit && threadIdx.x == 0) A.ne_fit[0] = over ? 0 : ne;
+    if (over) return;                     // over capacity: the host re-runs with read counts
+  }
+  events_small_body(A, cov_out, keys, diff, scratch, nh, ne);
+}
+
+// A request's whole tail in ONE workgroup (the runner's device-count fast path with its own window):
+// hit CSR, events, the fp64 score, then the capacity-gated frequency record and the results
+// published to pinned host memory -- the work of k_hits_small, k_events_small, k_score and
+// k_publish_record, without the three kernel boundaries between them (each a dispatch plus a
+// drain of the chip for a kernel that fills one CU). An over-capacity batch publishes its counters
+// only (the host re-runs it).
+__global__ __launch_bounds__(SB_THREADS) void k_request_tail(HitsArgs HA, EventsArgs EA, int32_t* __restrict__ cov_out,
+                                                             ScoreTables T, ScoreParams S, FreqIn F,
+                                                             RequestTailOut P) {
+  __shared__ uint64_t keys[SB_MAX];
+  __shared__ int32_t raw[SB_MAX_LINES + 1];                // the events' diff; the hits' hk before it
+  static_assert(sizeof(raw) >= SB_MAX * sizeof(int64_t), "hk fits the diff array");
+  __shared__ int64_t scratch[SB_THREADS / 64 + 1];
+  __shared__ int s_live;
+  __shared__ int64_t s_nh, s_ne;
+  hits_small_body(HA, keys, reinterpret_cast<int64_t*>(raw), scratch, &s_live, &s_nh, &s_ne);
+  __syncthreads();
+  const int64_t nh = s_nh, ne = s_ne;
+  const bool over = ne > EA.ne || nh > EA.nh;
+  if (!over) {
+    events_small_body(EA, cov_out, keys, raw, scratch, nh, ne);
+    __syncthreads();
+    for (int64_t e = threadIdx.x; e < ne; e += SB_THREADS)
+      P.score[e] = score_event(T, S, EA.ev_line[e], EA.ev_pat[e], EA.ev_seg[e], freq_before(F, e), nullptr);
+    __syncthreads();
+  }
+  // the frequency record of the batch's per-key counts (penalty before record: after the score),
+  // gated on the matcher capacities as k_publish_record / k_freq_record
+  const int64_t* cnt = P.cnt;
+  const RecordGate& G = P.gate;
+  const bool fits = !over && !(G.cnt && (G.cnt[0] > G.cap[0] || G.cnt[1] > G.cap[1] || G.cnt[2] > G.cap[2] ||
+                                         ne > G.cap[3]));
+  if (fits) {
+    const FreqRing& R = P.ring;
+    for (int k = threadIdx.x; k < P.K; k += SB_THREADS) {
+      const int64_t c = P.counts[k];
+      if (c <= 0) continue;
+      const int64_t q = (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(R.ht + 1), 1ull);
+      const int64_t s = q % R.cap;
+      R.t[s] = P.now;
+      R.key[s] = k;
+      R.cnt[s] = (int32_t)c;
+      R.tot[k] += c;
+      R.seen[k] = 1;
+    }
+  }
+  // counters + compacted results into pinned host memory (k_publish_record's layout)
+  if (threadIdx.x < 5) P.cnt_host[threadIdx.x] = threadIdx.x == 3 ? nh : threadIdx.x == 4 ? ne : cnt[threadIdx.x];
+  const int64_t E = P.E;
+  if (over || ne < 0 || ne > E) return;
+  const uint8_t* out = P.out;
+  const double* score = reinterpret_cast<const double*>(out);
+  const int64_t* counts_e = reinterpret_cast<const int64_t*>(out + 8 * E);
+  const int32_t* cols = reinterpret_cast<const int32_t*>(out + 8 * E + 8 * (int64_t)P.K1);
+  double* h_score = reinterpret_cast<double*>(P.res_host);
+  int64_t* h_counts = reinterpret_cast<int64_t*>(P.res_host + 8 * ne);
+  int32_t* h_cols = reinterpret_cast<int32_t*>(P.res_host + 8 * ne + 8 * (int64_t)P.K1);
+  const int64_t total = ne + P.K1 + 3 * ne;
+  for (int64_t i = threadIdx.x; i < total; i += SB_THREADS) {
+    if (i < ne) {
+      h_score[i] = score[i];
+    } else if (i < ne + P.K1) {
+      h_counts[i - ne] = counts_e[i - ne];
+    } else {
+      const int64_t j = i - ne - P.K1;
+      const int64_t c = j / ne, r = j - c * ne;
+      h_cols[j] = cols[c * E + r];
+    }
+  }
+}
+
+
+
+
 void set_small_profile(uint64_t dev_ptr) {
   int64_t* p = reinterpret_cast<int64_t*>(dev_ptr);
   LP_PCHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_sb_prof), &p, sizeof(p)));
@@ -644,6 +738,15 @@ struct Carve {
   }
   void* take_bytes(size_t n) { return take<uint8_t>(n); }
 };
+
+void request_tail_dev(const HitsArgs& HA, const EventsArgs& EA, const ScoreTables& T, const ScoreParams& S,
+                      const FreqIn& F, const RequestTailOut& P, void* ws, size_t ws_bytes, uint64_t stream) {
+  Carve D{static_cast<uint8_t*>(ws)};
+  int32_t* cov_s = EA.cov ? EA.cov : D.take<int32_t>(EA.L);
+  if (!EA.cov && (!ws || D.used > ws_bytes)) throw std::runtime_error("request_tail_dev: coverage workspace");
+  hipLaunchKernelGGL(k_request_tail, dim3(1), dim3(SB_THREADS), 0, pstream(stream), HA, EA, cov_s, T, S, F, P);
+  LP_PCHECK(hipGetLastError());
+}
 
 void dedupe_verify_dev(const uint64_t* keys, int64_t n, int lbits, const uint8_t* text, const int64_t* ls,
                        const int32_t* ll, const DfaPool& P, int64_t* stdk, uint8_t* flag, uint64_t stream) {

@@ -425,6 +425,44 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
     A.hits = hits; A.hit_line = hit_line; A.hit_off = hit_off; A.ev_cnt = ev_cnt; A.ev_end = ev_end;
     A.counters = cnt + 3;
     A.cand_verified = verified;
+    // the request's whole tail (hits, events, score, record, publish) as ONE single-workgroup kernel:
+    // the device-count fast path with its own window, the candidates verified and every line's
+    // features computed before the join
+    const bool tail = fast && !hw && publish_ && verified && feat_ready && L > 0;
+    if (tail) {
+      enter_window();
+      const int64_t E = ecap_small;
+      double* score = reinterpret_cast<double*>(out);
+      int64_t* freq_counts = reinterpret_cast<int64_t*>(out + 8 * (size_t)E);
+      int32_t* ev_line = reinterpret_cast<int32_t*>(out + 8 * (size_t)E + 8 * (size_t)K1);
+      if (S_.nkeys == 0) check(hipMemsetAsync(freq_counts, 0, 8, st), "counts");
+      if (!one_copy) check(hipMemsetAsync(seq_carry, 0, nseq1, st), "seq carry");
+      EventsArgs EA;
+      EA.ctx_trans = S_.ctx_trans; EA.ctx_acc = S_.ctx_acc;
+      EA.hits = hits; EA.nh = n; EA.ev_cnt = ev_cnt; EA.ev_end = ev_end; EA.ne = E; EA.L = L;
+      EA.lbits = lbits; EA.ev = ev; EA.text = text; EA.ls = ls; EA.ll = ll; EA.dfa = S_.dfa;
+      EA.ev_line = ev_line; EA.ev_pat = ev_line + E; EA.ev_seg = ev_line + 2 * E; EA.ev_rank = ev_rank;
+      EA.ev_fkey = ev_fkey; EA.freq_counts = freq_counts; EA.feat = feat; EA.cov = nullptr; EA.dcounts = cnt + 3;
+      EA.feat_ready = true;
+      ScoreTables T = S_.st;
+      T.seq_carry = seq_carry;
+      T.hit_off = hit_off; T.hit_line = hit_line; T.feat = feat;
+      T.seg_lo = dlo; T.seg_hi = dhi; T.seg_own_lo = dlo; T.seg_g0 = dg0; T.seg_n = dn;
+      const FreqIn F{ev_rank, ev_fkey, ring.tot};
+      const size_t res = 20 * (size_t)E + 8 * (size_t)K1;
+      if (res > res_cap_) {
+        grow<true>(res_host_, res_cap_, res, kCoherentHost);
+        res_host_dev_ = device_view(res_host_);
+      }
+      RequestTailOut P;
+      P.score = score; P.out = out; P.E = E; P.K1 = (int)K1; P.cnt = cnt;
+      P.cnt_host = cnt_host_dev_; P.res_host = res_host_dev_;
+      P.counts = freq_counts; P.K = S_.nkeys; P.now = now; P.ring = ring;
+      P.gate.cnt = cnt;
+      P.gate.cap[0] = cap_g; P.gate.cap[1] = cap_c; P.gate.cap[2] = cap_v; P.gate.cap[3] = E;
+      request_tail_dev(A, EA, T, S_.sp, F, P, post_ws_, post_cap_, stream);
+      recorded_ = true;            // (gated on the device: an overflowing attempt records nothing)
+    } else {
     size_t need = hits_dev(A, post_ws_, post_cap_, stream);
     if (need > post_cap_) {       // post_ws_ is not used by anything in flight yet
       if (fast) throw std::runtime_error("request runner: hit workspace on the small path");
@@ -432,7 +470,9 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
       grow<false>(post_ws_, post_cap_, need);
       hits_dev(A, post_ws_, post_cap_, stream);
     }
-    if (fast && hw) {
+    }
+    if (tail) {
+    } else if (fast && hw) {
       run_events(ecap_small, n, cnt + 3, false);
       hw_enter();
       run_score(ecap_small, cnt + 3, carry_dev_);
@@ -463,7 +503,7 @@ int64_t RequestRunner::run(uint8_t* host_text, int64_t nbytes, const int64_t* st
         res_bytes_ = res;
       }
     }
-    if (!(fast && (publish_ || hw)))
+    if (!(fast && (publish_ || hw)) && !tail)
       check(hipMemcpyAsync(cnt_host_, cnt, 5 * sizeof(int64_t), hipMemcpyDeviceToHost, st), "counters D2H");
     check(hipStreamSynchronize(st), "counters");   // fast: the only host read; else the mid-batch one
     c.gram = cnt_host_[0]; c.cand = cnt_host_[1]; c.ver = cnt_host_[2];

@@ -535,7 +535,7 @@ class Engine:
         # the host waits on, then shares the chip with the prefilter)
         box = []
         ls, ll = K.split_lines(text, nbytes, before_read=(lambda: box.append(self.prefilter_early(text, nbytes)))
-                               if text.is_cuda else None)
+                               if text.is_cuda else None, early_first=self._pf_stream is not None)
         return ls, ll, (box[0] if box else None)
 
     def fuses_line_index(self, text) -> bool:

@@ -79,13 +79,16 @@ def _count_read_slot(device: torch.device):
 LINE_BLK_SHIFT = 12
 
 
-def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=None, fused=None):
+def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=None, fused=None,
+                    early_first: bool = False):
     """k_nl_count, k_tile_scan, k_nl_lines, k_line_fix (+ k_line_trim): (starts, lens, n_newlines,
     last_newline, kept, blk) with ONE host read; blk = the coarse 4 KiB block -> line index.
     ``before_read()`` runs once, after the launches and before that read: work it queues (the
     literal prefilter, which needs no line index) runs on the GPU while the host waits.
     ``fused(nlp)`` instead launches the literal prefilter FIRST with the line index's first pass
-    folded into its read of the text (nlp = the pass-1 outputs, zeroed): k_nl_count does not run."""
+    folded into its read of the text (nlp = the pass-1 outputs, zeroed): k_nl_count does not run.
+    ``early_first``: before_read() queues its work on ANOTHER stream -- it then runs before the
+    count copy is even set up, so that work is launched as soon as the line index is."""
     dev = text.device
     nt = N.line_index_tiles(nbytes)
     cap = int(nbytes * _LINES_PER_BYTE[0] * 1.25) + 1024
@@ -106,10 +109,13 @@ def _line_index_dev(text: torch.Tensor, nbytes: int, trim: bool, before_read=Non
         if before_read is not None:
             # the counts travel to pinned memory behind the line index only; the host then waits
             # for that copy, not for the work before_read() queued after it
+            if early_first:
+                before_read()
             hinfo, done = _count_read_slot(dev)
             hinfo.copy_(info, non_blocking=True)
             done.record()
-            before_read()
+            if not early_first:
+                before_read()
             before_read = None
             done.synchronize()
             n_nl, last, kept = hinfo.tolist()
@@ -128,7 +134,8 @@ def _with_blk(ls: torch.Tensor, blk: torch.Tensor, nbytes: int) -> torch.Tensor:
     return ls
 
 
-def split_lines(text: torch.Tensor, nbytes: int, before_read=None, fused=None) -> Tuple[torch.Tensor, torch.Tensor]:
+def split_lines(text: torch.Tensor, nbytes: int, before_read=None, fused=None,
+                early_first: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """Java ``logs.split("\\\\r?\\\\n")`` line index (AnalysisService.java:53).
 
     Returns (line_start int64[L], line_len int32[L]); trailing empty lines removed; input
@@ -139,7 +146,8 @@ def split_lines(text: torch.Tensor, nbytes: int, before_read=None, fused=None) -
     if text.is_cuda:
         if nbytes == 0:
             return torch.zeros(1, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)
-        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True, before_read=before_read, fused=fused)
+        starts, lens, _, _, L, blk = _line_index_dev(text, nbytes, trim=True, before_read=before_read, fused=fused,
+                                                     early_first=early_first)
         return _with_blk(starts[:L], blk, nbytes), lens[:L]
     nl = newline_positions(text, nbytes)
     if nl.numel() == 0:
@@ -480,13 +488,13 @@ class EarlyPrefilter:
             fork.record(torch.cuda.current_stream(text.device))
             stream.wait_event(fork)
             st = stream.cuda_stream
-            for t in (self.gh, self.cnt, text):
-                t.record_stream(stream)
         N.prefilter_dev(text.data_ptr(), nbytes, tabs["pf"], 0, 0, self.gh.data_ptr(), self.cap, self.cnt.data_ptr(),
                         pf_grid, st, nlp)
         if st != _s(text):
             self.done = done
             self.done.record(stream)
+            for t in (self.gh, self.cnt, text):     # (allocator bookkeeping: after the launch)
+                t.record_stream(stream)
 
 
 def match_and_hits(text, nbytes: int, line_start, line_len, tabs: dict, R: int, evt: tuple, arena: MatchArena,

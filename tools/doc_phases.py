@@ -61,6 +61,10 @@ def main():
     wrap(N, "scan_multi", "scan_launch")
     wrap(K, "post_events", "post_events")
     wrap(E.Engine, "finish", "finish")
+    wrap(N, "line_index_dev", "n_line_index")
+    wrap(N, "prefilter_dev", "n_prefilter")
+    wrap(K, "_pf_events", "pf_events")
+    wrap(E.Engine, "freq_carry", "freq_carry")
     for _ in range(5):
         eng.run_document(text, len(data))
     torch.cuda.synchronize()

@@ -12,15 +12,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run gputests 900 python -u -m pytest tests/test_gpu.py tests/test_gpu_serving.py tests/test_multi_engine.py -m gpu -x -q --timeout 300 --timeout-method thread
-run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-run rt 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
-run small 300 python -u tools/small_phases.py --requests 200
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-run lagprof 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d gpurun_out/lag -o run -- \
-  python3 tools/request_trace.py --requests 200 --java-shape-rate 0.01
-run lag 120 python3 tools/launch_lag.py gpurun_out/lag --requests 200
-rm -rf gpurun_out/lag
-for k in 1 2; do
-  run l3on_$k 300 python -u tools/parse_stages.py --n 400
+for k in 1 2 3; do
+  run new_$k 300 python -u tools/parse_stages.py --n 400
+  run old_$k 300 python -u ab_old/tools/parse_stages.py --n 400
 done

@@ -1347,9 +1347,10 @@ PYBIND11_MODULE(_lpnative, m) {
   py::class_<HttpServer>(m, "HttpServer")
       .def(py::init([](const std::string& host, int port, int io_threads, int64_t max_body, double idle,
                        double io_spin_us, double pump_spin_us, bool quickack, int rcvbuf, bool trace,
-                       bool conn_trace, bool prefetch) {
+                       bool conn_trace, bool prefetch, int64_t io_decode_max_conns) {
              HttpOptions o;
              o.prefetch = prefetch;
+             o.io_decode_max_conns = io_decode_max_conns;
              o.io_spin_us = io_spin_us; o.pump_spin_us = pump_spin_us; o.quickack = quickack; o.rcvbuf = rcvbuf;
              o.trace = trace;
              o.conn_trace = conn_trace;
@@ -1357,7 +1358,7 @@ PYBIND11_MODULE(_lpnative, m) {
            }), py::arg("host"), py::arg("port"), py::arg("io_threads") = 2, py::arg("max_body") = int64_t(1) << 30,
            py::arg("idle_timeout_s") = 60.0, py::arg("io_spin_us") = 0.0, py::arg("pump_spin_us") = 1000.0,
            py::arg("quickack") = true, py::arg("rcvbuf") = 0, py::arg("trace") = false, py::arg("conn_trace") = false,
-           py::arg("prefetch") = true)
+           py::arg("prefetch") = true, py::arg("io_decode_max_conns") = int64_t(64))
       .def("conn_trace", [](HttpServer& s) {
         std::vector<std::vector<double>> v;
         {

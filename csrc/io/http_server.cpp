@@ -297,6 +297,7 @@ HttpServer::HttpServer(const std::string& host, int port, int io_threads, int64_
   trace_ = opt.trace;
   conn_trace_ = opt.conn_trace;
   prefetch_ = opt.prefetch;
+  io_decode_max_ = opt.io_decode_max_conns < 0 ? SIZE_MAX : (size_t)opt.io_decode_max_conns;
   for (int i = 0; i < io_threads; ++i) {
     auto io = std::make_unique<Io>();
     io->index = i;
@@ -905,10 +906,12 @@ bool HttpServer::parse_one(Io* io, Conn* c) {
     c->t_parse = tv;
     // bodies of >= 4 KiB: the logs text is decoded by this thread in the validating pass, while the
     // bytes are in its cache -- the engine's packer then copies plain text instead of unescaping
-    // bytes received on another core (server-side pack of a 1 MB body: 107 us, profiles/r6_c)
+    // bytes received on another core (server-side pack of a 1 MB body: 107 us, profiles/r6_c).
+    // Not under a burst of connections (server.io-decode-max-conns): the IO threads are then the
+    // front's bottleneck and the packer unescapes the batch's bodies instead.
     DecodeBuf dec;
     int st;
-    if (clen >= (4 << 10)) {
+    if (clen >= (4 << 10) && (pdec.p || io->conns.size() <= io_decode_max_)) {
       const bool resume = pdec.p && pf.state >= 1;
       dec = pdec.p ? std::move(pdec) : dpool_->take((size_t)clen + 64);
       st = parse_pod_request_into(reinterpret_cast<const uint8_t*>(c->in.data()) + b0, (size_t)clen, pr,

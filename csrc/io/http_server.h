@@ -121,6 +121,9 @@ struct HttpOptions {
   bool trace = false;           // per-request receive / validate timings on stderr
   bool conn_trace = false;      // per /parse response: accept / first byte / parsed / handed back / sent times
   bool prefetch = true;         // decode a large /parse body's logs string while it arrives
+  // an IO thread decodes a /parse body's logs string itself only while it holds at most this many
+  // connections; under a burst the bodies go to the packer undecoded (IO threads then only receive)
+  int64_t io_decode_max_conns = 64;
 };
 
 // A large /parse body still arriving, registered by its IO thread so that the PUMP thread -- idle,
@@ -210,6 +213,7 @@ class HttpServer {
   bool trace_ = false;
   bool conn_trace_ = false;
   bool prefetch_ = true;
+  size_t io_decode_max_ = 64;
   double pump_spin_s_ = 0;
   bool quickack_ = true;
   int rcvbuf_ = 0;

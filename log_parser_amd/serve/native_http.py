@@ -80,7 +80,8 @@ class NativeHttpFrontend:
                                 pump_spin_us=float(cfg["server.pump-spin-us"]),
                                 quickack=bool(cfg["server.tcp-quickack"]), rcvbuf=int(cfg["server.rcvbuf-bytes"]),
                                 trace=trace, conn_trace=bool(cfg.get("server.stage-timeline", False)),
-                                prefetch=bool(cfg["server.prefetch-logs"]))
+                                prefetch=bool(cfg["server.prefetch-logs"]),
+                                io_decode_max_conns=int(cfg["server.io-decode-max-conns"]))
         self.port = self.srv.port
         eng = b.pipe.engine if b.pipe is not None else None
         npin = int(cfg["server.pinned-decode-buffers"])

@@ -140,6 +140,10 @@ ENGINE_KEYS: Dict[str, tuple] = {
     # text into its own stage, and the decoder's newline positions replace the packer's scan:
     # /parse p50 0.42-0.43 -> 0.40 ms, profiles/r6_e). 0: pageable buffers, copied.
     "server.pinned-decode-buffers": (8, int),
+    # native front end: an IO thread decodes a /parse body's `logs` string itself (bodies >= 4 KiB)
+    # only while it holds at most this many connections; under a burst the bodies reach the packer
+    # undecoded and the IO threads only receive and validate. -1: always decode on the IO thread.
+    "server.io-decode-max-conns": (64, int),
     # native front end: IO threads poll this long after activity before sleeping in epoll_wait
     "server.io-spin-us": (0.0, float),
     # native front end: the pump polls for the next request this long before sleeping on the queue

@@ -574,3 +574,37 @@ def _conn_send(port, raw: bytes, slow: bool = False):
     else:
         s.sendall(raw)
     return s
+
+
+def test_burst_mode_bodies_reach_the_packer_undecoded():
+    """server.io-decode-max-conns: above that many connections an IO thread stops decoding /parse
+    bodies itself (under a burst it is the front's bottleneck) and the packer unescapes them. With
+    the limit at 0 (and the arrival-time decode off) every body takes that route: large bodies --
+    escapes, multi-byte characters, several on one keep-alive connection -- answer the same
+    AnalysisResult as through the IO-thread decode with its arrival-time prefetch."""
+    sets, trig = make_library(15, seed=23)
+    logs = [make_log(n, trig, seed=40 + n, hit_rate=0.05) + '\n"q" \\ tab\t é€😀 end' for n in (60, 900, 2600)]
+    bodies = [json.dumps({"pod": {"metadata": {"name": f"b{i}"}}, "logs": l}, ensure_ascii=False).encode()
+              for i, l in enumerate(logs)]
+    assert len(bodies[-1]) >= 64 << 10
+    outs = {}
+    for limit in (-1, 0):
+        lib = CompiledLibrary(sets, ScoringParams())
+        cfg = Config.load(overrides={"engine.device": "cpu", "server.max-body-bytes": 4 << 20,
+                                     "server.io-decode-max-conns": limit, "server.prefetch-logs": limit != 0})
+        eng = Engine(lib, cfg, device=torch.device("cpu"))
+        fe = NativeHttpFrontend(Service(cfg, eng), "127.0.0.1", 0, io_threads=1)
+        try:
+            c = http.client.HTTPConnection("127.0.0.1", fe.port, timeout=60)
+            res = []
+            for b in bodies:
+                st, out = _post(c, b)
+                assert st == 200
+                res.append(_strip(json.loads(out)))
+            c.close()
+            outs[limit] = res
+            assert (fe.srv.stage_stats()["prefetched"] > 0) == (limit != 0)
+        finally:
+            fe.close()
+    assert outs[0] == outs[-1]
+    assert all(r["summary"]["significantEvents"] > 0 for r in outs[0])

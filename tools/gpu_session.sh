@@ -12,9 +12,6 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-for k in 1 2 3; do
-  run c5new_$k 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8
-  run c5always_$k 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8 --server-opt=-Dserver.io-decode-max-conns=-1
-  run c5r5_$k 300 python -u ab_old/benchmarks/bench_configs.py concurrent_http --client-threads 8
-done
-run ps 300 python -u tools/parse_stages.py --n 400
+run bnew 400 python -u bench.py
+run br5 400 python -u ab_old/bench.py
+run bnew2 400 python -u bench.py

@@ -342,7 +342,8 @@ constexpr int SB_MAX_LINES = 16384;    // window-coverage difference array in LD
 
 // Diagnostic phase clock of the two single-workgroup kernels (set_small_profile): thread 0 stores
 // wall_clock64() after each phase into g_sb_prof[slot] (null: off, one scalar load per phase).
-// Slots 0-7 k_hits_small, 8-15 k_events_small.
+// Slots 0-4 k_hits_small, 8-13 k_events_small (5: live keys, 14: events); k_request_tail runs both
+// bodies and adds 6 (score), 7 (frequency record), 15 (publish).
 __device__ int64_t* g_sb_prof = nullptr;
 #define LP_SB_STAMP(slot)                                                    \
   do {                                                                     \
@@ -657,6 +658,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_request_tail(HitsArgs HA, Events
       P.score[e] = score_event(T, S, EA.ev_line[e], EA.ev_pat[e], EA.ev_seg[e], freq_before(F, e), nullptr);
     __syncthreads();
   }
+  LP_SB_STAMP(6);
   // the frequency record of the batch's per-key counts (penalty before record: after the score),
   // gated on the matcher capacities as k_publish_record / k_freq_record
   const int64_t* cnt = P.cnt;
@@ -677,6 +679,7 @@ __global__ __launch_bounds__(SB_THREADS) void k_request_tail(HitsArgs HA, Events
       R.seen[k] = 1;
     }
   }
+  LP_SB_STAMP(7);
   // counters + compacted results into pinned host memory (k_publish_record's layout)
   if (threadIdx.x < 5) P.cnt_host[threadIdx.x] = threadIdx.x == 3 ? nh : threadIdx.x == 4 ? ne : cnt[threadIdx.x];
   const int64_t E = P.E;
@@ -700,6 +703,8 @@ __global__ __launch_bounds__(SB_THREADS) void k_request_tail(HitsArgs HA, Events
       h_cols[j] = cols[c * E + r];
     }
   }
+  __syncthreads();
+  LP_SB_STAMP(15);
 }
 
 

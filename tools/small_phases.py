@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Where the request path's two single-workgroup kernels spend their time: phase clocks
-(wall_clock64, 100 MHz on gfx950) written by k_hits_small / k_events_small (N.set_small_profile)
+"""Where the request path's single-workgroup kernels spend their time: phase clocks
+(wall_clock64, 100 MHz on gfx950) written by k_hits_small / k_events_small, or the fused
+k_request_tail (its score / record / publish phases too) (N.set_small_profile)
 over R 10k-line requests, medians in microseconds.
 
     python tools/small_phases.py --requests 200
@@ -39,6 +40,7 @@ def main():
     buf = torch.zeros(16, dtype=torch.int64, device=dev)
     N.set_small_profile(buf.data_ptr())
     ph = {k: [] for k in HITS + EVENTS + ["hits kernel", "events kernel"]}
+    tail = {k: [] for k in ("tail: score", "tail: record", "tail: publish", "tail kernel")}
     live, nev = [], []
     try:
         for _ in range(a.requests):
@@ -55,9 +57,14 @@ def main():
             ph["events kernel"].append((t[13] - t[8]) * us)
             live.append(t[5])
             nev.append(t[14])
+            if t[15]:       # the fused k_request_tail ran (score / record / publish stamps)
+                tail["tail: score"].append((t[6] - t[13]) * us)
+                tail["tail: record"].append((t[7] - t[6]) * us)
+                tail["tail: publish"].append((t[15] - t[7]) * us)
+                tail["tail kernel"].append((t[15] - t[0]) * us)
     finally:
         N.set_small_profile(0)
-    out = {k: round(statistics.median(v), 2) for k, v in ph.items()}
+    out = {k: round(statistics.median(v), 2) for k, v in list(ph.items()) + list(tail.items()) if v}
     out["live_keys"] = statistics.median(live)
     out["events"] = statistics.median(nev)
     print(json.dumps(out), flush=True)

@@ -504,6 +504,87 @@ LP_HD int32_t pred_hit(const ScoreTables& T, int r, int32_t a, int32_t c) {
   return -1;
 }
 
+// The factors of one event's score, each a function of its own: the request tail runs them in
+// different waves (one chain of dependent loads each) and multiplies them as score_event does.
+// proximity (ScoringService.java:161-190,315-347)
+LP_HD double prox_factor(const ScoreTables& T, const ScoreParams& S, int32_t x, int32_t p, int32_t lo, int32_t hi) {
+  double prox = 1.0;
+  const int32_t a0 = T.sec_off[p], a1 = T.sec_off[p + 1];
+  if (a1 > a0) {
+    double tot = 0.0;
+    for (int32_t k = a0; k < a1; ++k) {
+      const int32_t w = T.sec_w[k];
+      const int64_t aa = (int64_t)x - w, bb = (int64_t)x + w + 1;
+      const int32_t a = (int32_t)(aa < lo ? lo : aa), b = (int32_t)(bb > hi ? hi : bb);
+      const int32_t d = nearest_hit(T, T.sec_reg[k], x, a, b);
+      if (d >= 0) tot += T.sec_weight[k] * exp(-(double)d / S.decay);
+    }
+    prox = 1.0 + tot;
+  }
+  return prox;
+}
+
+// temporal (ScoringService.java:199-305)
+LP_HD double temp_factor(const ScoreTables& T, int32_t x, int32_t p, int32_t lo, int32_t hi, int32_t own_lo) {
+  double temp = 1.0;
+  const int32_t q0 = T.seq_off[p], q1 = T.seq_off[p + 1];
+  if (q1 > q0) {
+    double tot = 0.0;
+    for (int32_t q = q0; q < q1; ++q) {
+      const int32_t e0 = T.seq_ev_off[q], e1 = T.seq_ev_off[q + 1];
+      const int n = e1 - e0;
+      if (n <= 0) continue;
+      const int32_t a = x - 5 < lo ? lo : x - 5, b = x + 6 > hi ? hi : x + 6;
+      if (!any_hit(T, T.seq_ev_reg[e1 - 1], a, b)) continue;
+      bool ok = true;
+      int32_t cur = x;
+      for (int k = n - 2; k >= 0; --k) {
+        const int32_t f = pred_hit(T, T.seq_ev_reg[e0 + k], own_lo, cur);
+        if (f < 0) { ok = T.seq_carry[e0 + k] != 0; break; }
+        cur = f;
+      }
+      if (ok) tot += T.seq_bonus[q];
+    }
+    temp = 1.0 + tot;
+  }
+  return temp;
+}
+
+// context (ContextAnalysisService.java:46-117)
+LP_HD double ctx_factor(const ScoreTables& T, const ScoreParams& S, int32_t x, int32_t p, int32_t lo, int32_t hi) {
+  int32_t a = x, b = x + 1;
+  const int32_t before = T.ctx_before[p], after = T.ctx_after[p];
+  if (before >= 0) {
+    a = x - before < lo ? lo : x - before;
+    b = x + 1 + after > hi ? hi : x + 1 + after;
+  }
+  double sc = 0.0;
+  int err = 0, stack = 0;
+  for (int32_t j = a; j < b; ++j) {
+    const uint8_t f = T.feat[j];
+    if (f & 1) { ++err; sc += 0.4; }
+    else if (f & 2) { sc += 0.2; }
+    if (f & 4) { ++stack; sc += 0.1; }
+    if (f & 8) { sc += 0.3; }
+  }
+  if (stack > 0) { const double sb = stack * 0.1; sc += sb < 0.5 ? sb : 0.5; }
+  const int total = b - a;
+  if (total > 10 && (double)(stack + err) > total * 0.7) sc *= 0.8;
+  double ctx = 1.0 + sc;
+  if (ctx > S.max_ctx) ctx = S.max_ctx;
+  return ctx;
+}
+
+// frequency penalty (FrequencyTrackingService.java:64-93), penalty before record
+LP_HD double pen_factor(const ScoreParams& S, int64_t freq_before) {
+  double pen = 0.0;
+  if (freq_before >= 0) {
+    const double rate = (double)freq_before / S.fwin;
+    if (rate > S.fthr) { const double v = (rate - S.fthr) / S.fthr; pen = v < S.fmaxp ? v : S.fmaxp; }
+  }
+  return pen;
+}
+
 LP_HD double score_event(const ScoreTables& T, const ScoreParams& S, int32_t x, int32_t p, int32_t s,
                          int64_t freq_before, double* factors /* optional [7] */) {
   const int32_t lo = T.seg_lo[s], hi = T.seg_hi[s], own_lo = T.seg_own_lo[s];
@@ -511,76 +592,10 @@ LP_HD double score_event(const ScoreTables& T, const ScoreParams& S, int32_t x, 
   const double conf = T.conf[p];
   const double sev = T.sev[p];
   const double chrono = chrono_factor(gi, T.seg_n[s], S);
-  // proximity (ScoringService.java:161-190,315-347)
-  double prox = 1.0;
-  {
-    const int32_t a0 = T.sec_off[p], a1 = T.sec_off[p + 1];
-    if (a1 > a0) {
-      double tot = 0.0;
-      for (int32_t k = a0; k < a1; ++k) {
-        const int32_t w = T.sec_w[k];
-        const int64_t aa = (int64_t)x - w, bb = (int64_t)x + w + 1;
-        const int32_t a = (int32_t)(aa < lo ? lo : aa), b = (int32_t)(bb > hi ? hi : bb);
-        const int32_t d = nearest_hit(T, T.sec_reg[k], x, a, b);
-        if (d >= 0) tot += T.sec_weight[k] * exp(-(double)d / S.decay);
-      }
-      prox = 1.0 + tot;
-    }
-  }
-  // temporal (ScoringService.java:199-305)
-  double temp = 1.0;
-  {
-    const int32_t q0 = T.seq_off[p], q1 = T.seq_off[p + 1];
-    if (q1 > q0) {
-      double tot = 0.0;
-      for (int32_t q = q0; q < q1; ++q) {
-        const int32_t e0 = T.seq_ev_off[q], e1 = T.seq_ev_off[q + 1];
-        const int n = e1 - e0;
-        if (n <= 0) continue;
-        const int32_t a = x - 5 < lo ? lo : x - 5, b = x + 6 > hi ? hi : x + 6;
-        if (!any_hit(T, T.seq_ev_reg[e1 - 1], a, b)) continue;
-        bool ok = true;
-        int32_t cur = x;
-        for (int k = n - 2; k >= 0; --k) {
-          const int32_t f = pred_hit(T, T.seq_ev_reg[e0 + k], own_lo, cur);
-          if (f < 0) { ok = T.seq_carry[e0 + k] != 0; break; }
-          cur = f;
-        }
-        if (ok) tot += T.seq_bonus[q];
-      }
-      temp = 1.0 + tot;
-    }
-  }
-  // context (ContextAnalysisService.java:46-117)
-  double ctx;
-  {
-    int32_t a = x, b = x + 1;
-    const int32_t before = T.ctx_before[p], after = T.ctx_after[p];
-    if (before >= 0) {
-      a = x - before < lo ? lo : x - before;
-      b = x + 1 + after > hi ? hi : x + 1 + after;
-    }
-    double sc = 0.0;
-    int err = 0, stack = 0;
-    for (int32_t j = a; j < b; ++j) {
-      const uint8_t f = T.feat[j];
-      if (f & 1) { ++err; sc += 0.4; }
-      else if (f & 2) { sc += 0.2; }
-      if (f & 4) { ++stack; sc += 0.1; }
-      if (f & 8) { sc += 0.3; }
-    }
-    if (stack > 0) { const double sb = stack * 0.1; sc += sb < 0.5 ? sb : 0.5; }
-    const int total = b - a;
-    if (total > 10 && (double)(stack + err) > total * 0.7) sc *= 0.8;
-    ctx = 1.0 + sc;
-    if (ctx > S.max_ctx) ctx = S.max_ctx;
-  }
-  // frequency penalty (FrequencyTrackingService.java:64-93), penalty before record
-  double pen = 0.0;
-  if (freq_before >= 0) {
-    const double rate = (double)freq_before / S.fwin;
-    if (rate > S.fthr) { const double v = (rate - S.fthr) / S.fthr; pen = v < S.fmaxp ? v : S.fmaxp; }
-  }
+  const double prox = prox_factor(T, S, x, p, lo, hi);
+  const double temp = temp_factor(T, x, p, lo, hi, own_lo);
+  const double ctx = ctx_factor(T, S, x, p, lo, hi);
+  const double pen = pen_factor(S, freq_before);
   if (factors) {
     factors[0] = conf; factors[1] = sev; factors[2] = chrono; factors[3] = prox;
     factors[4] = temp; factors[5] = ctx; factors[6] = pen;

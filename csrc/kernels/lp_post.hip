@@ -654,9 +654,37 @@ __global__ __launch_bounds__(SB_THREADS) void k_request_tail(HitsArgs HA, Events
   if (!over) {
     events_small_body(EA, cov_out, keys, raw, scratch, nh, ne);
     __syncthreads();
-    for (int64_t e = threadIdx.x; e < ne; e += SB_THREADS)
-      P.score[e] = score_event(T, S, EA.ev_line[e], EA.ev_pat[e], EA.ev_seg[e], freq_before(F, e), nullptr);
-    __syncthreads();
+    // the score's factors in different waves: proximity, temporal and context are each a chain of
+    // dependent table / hit-list loads, so they run side by side (waves 0-3, 4-7, 8-11) while waves
+    // 12-15 load the event's own factors and multiply in score_event's order (bit-identical)
+    constexpr int SC_EV = SB_THREADS / 4;                      // events per pass
+    double* fx = reinterpret_cast<double*>(keys);              // [3][SC_EV] (the sorts' LDS is free)
+    static_assert(sizeof(keys) >= 3 * SC_EV * sizeof(double), "score factors fit keys");
+    const int part = (int)threadIdx.x / SC_EV, i = (int)threadIdx.x % SC_EV;   // part: wave-uniform
+    for (int64_t b0 = 0; b0 < ne; b0 += SC_EV) {
+      const int64_t e = b0 + i;
+      double conf = 0.0, sev = 0.0, chrono = 0.0, pen = 0.0;
+      if (e < ne) {
+        const int32_t x = EA.ev_line[e], p = EA.ev_pat[e], sg = EA.ev_seg[e];
+        const int32_t lo = T.seg_lo[sg], hi = T.seg_hi[sg];
+        if (part == 0) {
+          fx[i] = prox_factor(T, S, x, p, lo, hi);
+        } else if (part == 1) {
+          fx[SC_EV + i] = temp_factor(T, x, p, lo, hi, T.seg_own_lo[sg]);
+        } else if (part == 2) {
+          fx[2 * SC_EV + i] = ctx_factor(T, S, x, p, lo, hi);
+        } else {
+          conf = T.conf[p];
+          sev = T.sev[p];
+          chrono = chrono_factor(T.seg_g0[sg] + (x - lo), T.seg_n[sg], S);
+          pen = pen_factor(S, freq_before(F, e));
+        }
+      }
+      __syncthreads();
+      if (part == 3 && e < ne)
+        P.score[e] = conf * sev * chrono * fx[i] * fx[SC_EV + i] * fx[2 * SC_EV + i] * (1.0 - pen);
+      __syncthreads();
+    }
   }
   LP_SB_STAMP(6);
   // the frequency record of the batch's per-key counts (penalty before record: after the score),

@@ -12,8 +12,10 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run gt 600 python -u -m pytest tests/test_gpu.py tests/test_gpu_serving.py -m gpu -x -q --timeout 300 --timeout-method thread
+run gt 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 run small 300 python -u tools/small_phases.py --requests 300
 run rt 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
 run eph 300 python -u tools/engine_phases.py --n 300
+run rt2 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
+run ps 300 python -u tools/parse_stages.py --n 400

@@ -387,13 +387,47 @@ __global__ __launch_bounds__(256) void k_scan(const uint8_t* __restrict__ text,
 
 // ------------------------------------------------------------------------------------------
 // K7-K9: fused score epilogue, one lane per event
-__global__ __launch_bounds__(256) void k_score(const int32_t* __restrict__ ev_line, const int32_t* __restrict__ ev_pat,
-                                               const int32_t* __restrict__ ev_seg, FreqIn F,
-                                               int64_t n, ScoreTables T, ScoreParams S, double* __restrict__ out,
-                                               double* __restrict__ factors, const int64_t* __restrict__ dn) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || (dn && i >= dn[0])) return;
-  out[i] = score_event(T, S, ev_line[i], ev_pat[i], ev_seg[i], freq_before(F, i), factors ? factors + 7 * i : nullptr);
+// 64 events per workgroup, one wave per factor group: proximity (wave 0), temporal (wave 1) and
+// context (wave 2) are each a chain of dependent table / hit-list loads and run side by side; wave 3
+// loads the event's own factors and multiplies in score_event's order (bit-identical). A batch of a
+// few thousand events is latency-bound (a handful of waves per CU), so the chains' overlap is what
+// the kernel's time is made of.
+constexpr int kScoreEv = 64;
+__global__ __launch_bounds__(4 * kScoreEv) void k_score(const int32_t* __restrict__ ev_line,
+                                                        const int32_t* __restrict__ ev_pat,
+                                                        const int32_t* __restrict__ ev_seg, FreqIn F,
+                                                        int64_t n, ScoreTables T, ScoreParams S,
+                                                        double* __restrict__ out, double* __restrict__ factors,
+                                                        const int64_t* __restrict__ dn) {
+  __shared__ double fx[3][kScoreEv];
+  const int part = (int)threadIdx.x / kScoreEv, j = (int)threadIdx.x % kScoreEv;   // part: wave-uniform
+  const int64_t i = (int64_t)blockIdx.x * kScoreEv + j;
+  const bool on = i < n && !(dn && i >= dn[0]);
+  double conf = 0.0, sev = 0.0, chrono = 0.0, pen = 0.0;
+  if (on) {
+    const int32_t x = ev_line[i], p = ev_pat[i], sg = ev_seg[i];
+    const int32_t lo = T.seg_lo[sg], hi = T.seg_hi[sg];
+    if (part == 0) {
+      fx[0][j] = prox_factor(T, S, x, p, lo, hi);
+    } else if (part == 1) {
+      fx[1][j] = temp_factor(T, x, p, lo, hi, T.seg_own_lo[sg]);
+    } else if (part == 2) {
+      fx[2][j] = ctx_factor(T, S, x, p, lo, hi);
+    } else {
+      conf = T.conf[p];
+      sev = T.sev[p];
+      chrono = chrono_factor(T.seg_g0[sg] + (x - lo), T.seg_n[sg], S);
+      pen = pen_factor(S, freq_before(F, i));
+    }
+  }
+  __syncthreads();
+  if (part != 3 || !on) return;
+  const double prox = fx[0][j], temp = fx[1][j], ctx = fx[2][j];
+  if (factors) {
+    double* f = factors + 7 * i;
+    f[0] = conf; f[1] = sev; f[2] = chrono; f[3] = prox; f[4] = temp; f[5] = ctx; f[6] = pen;
+  }
+  out[i] = conf * sev * chrono * prox * temp * ctx * (1.0 - pen);
 }
 
 
@@ -549,8 +583,8 @@ void score_dev(const int32_t* ev_line, const int32_t* ev_pat, const int32_t* ev_
                const ScoreTables& T, const ScoreParams& S, double* out, double* factors, uint64_t stream,
                const int64_t* dn) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_score, dim3(num_blocks(n, 256)), dim3(256), 0, as_stream(stream), ev_line, ev_pat, ev_seg,
-                     F, n, T, S, out, factors, dn);
+  hipLaunchKernelGGL(k_score, dim3(num_blocks(n, kScoreEv)), dim3(4 * kScoreEv), 0, as_stream(stream), ev_line, ev_pat,
+                     ev_seg, F, n, T, S, out, factors, dn);
   LP_CHECK(hipGetLastError());
 }
 

@@ -13,9 +13,9 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
 }
 
 run gt 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-run small 300 python -u tools/small_phases.py --requests 300
-run rt 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
-run eph 300 python -u tools/engine_phases.py --n 300
-run rt2 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
-run ps 300 python -u tools/parse_stages.py --n 400
+run single 300 python -u benchmarks/bench_configs.py single
+run bench 400 python -u bench.py
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+run cprof 300 rocprofv3 --kernel-trace -d gpurun_out/cp -o run -- python3 benchmarks/bench_configs.py single --steps 8
+run ctl 120 python3 tools/kstats_db.py $(find gpurun_out/cp -name "*.db" | head -1) 5 40 --marker k_nl_count --last 5 --timeline
+rm -rf gpurun_out/cp

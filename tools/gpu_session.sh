@@ -12,7 +12,14 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-for k in 1 2 3; do
-  run dnew_$k 300 python -u tools/doc_ab.py --rounds 2 --steps 30
-  run dold_$k 300 python -u ab_old/tools/doc_ab.py --rounds 2 --steps 30
-done
+run gt 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+run rt 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
+run single 300 python -u benchmarks/bench_configs.py single
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+run lagprof 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d gpurun_out/lag -o run -- \
+  python3 tools/request_trace.py --requests 200 --java-shape-rate 0.01
+run lag 120 python3 tools/launch_lag.py gpurun_out/lag --requests 200
+rm -rf gpurun_out/lag
+run cprof 300 rocprofv3 --kernel-trace -d gpurun_out/cp -o run -- python3 benchmarks/bench_configs.py single --steps 8
+run ctl 120 python3 tools/kstats_db.py $(find gpurun_out/cp -name "*.db" | head -1) 5 40 --marker k_nl_count --last 5 --timeline
+rm -rf gpurun_out/cp

@@ -12,14 +12,10 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run gt 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-run rt 300 python -u tools/request_trace.py --requests 400 --java-shape-rate 0.01
+run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+run full_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+run full_bench 400 python -u bench.py
 run single 300 python -u benchmarks/bench_configs.py single
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-run lagprof 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d gpurun_out/lag -o run -- \
-  python3 tools/request_trace.py --requests 200 --java-shape-rate 0.01
-run lag 120 python3 tools/launch_lag.py gpurun_out/lag --requests 200
-rm -rf gpurun_out/lag
-run cprof 300 rocprofv3 --kernel-trace -d gpurun_out/cp -o run -- python3 benchmarks/bench_configs.py single --steps 8
-run ctl 120 python3 tools/kstats_db.py $(find gpurun_out/cp -name "*.db" | head -1) 5 40 --marker k_nl_count --last 5 --timeline
-rm -rf gpurun_out/cp
+run c5 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8
+run ps 300 python -u tools/parse_stages.py --n 400
+run small 300 python -u tools/small_phases.py --requests 300

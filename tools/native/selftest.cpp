@@ -237,6 +237,69 @@ static void http_prefetch_selftest(int rounds) {
   std::printf("http prefetch: %d large bodies, %llu prefetched\n", ok, (unsigned long long)pre);
 }
 
+// burst mode (server.io-decode-max-conns exceeded; here the limit is 0 and the arrival-time decode
+// off): large bodies reach the consumer undecoded -- no decode buffer -- and the raw logs span
+// decodes to the same text
+static void http_undecoded_selftest(int rounds) {
+  HttpOptions o;
+  o.prefetch = false;
+  o.io_decode_max_conns = 0;
+  HttpServer srv("127.0.0.1", 0, 2, 8 << 20, 60.0, o);
+  std::atomic<bool> done{false};
+  std::atomic<int> with_dec{0};
+  std::thread responder([&] {
+    while (!done)
+      for (auto& r : srv.next_requests(16, 20)) {
+        size_t n = (size_t)-1;
+        uint64_t h = 0;
+        if (r.kind == 0) {
+          if (r.dec.p) ++with_dec;
+          std::string logs(r.logs_len + 64, '\0');
+          n = decode_json_string(reinterpret_cast<const uint8_t*>(r.body.data()) + r.logs_off, r.logs_len, &logs[0]);
+          h = std::hash<std::string>()(std::string(logs.data(), n));
+          srv.recycle(std::move(r.body));
+        }
+        srv.respond(r.id, 200, "application/json", "{\"n\":" + std::to_string(n) + ",\"h\":" + std::to_string(h) + "}");
+      }
+  });
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)srv.port());
+  inet_pton(AF_INET, "127.0.0.1", &a.sin_addr);
+  int ok = 0;
+  if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0) {
+    for (int i = 0; i < rounds; ++i) {
+      std::string logs, raw;
+      for (int k = 0; k < 500 + 700 * i; ++k) {
+        logs += "WARN line " + std::to_string(k) + " \xc3\xa9\t\"q\"\n";
+        raw += "WARN line " + std::to_string(k) + " \xc3\xa9\\t\\\"q\\\"\\n";
+      }
+      const std::string body = "{\"pod\":{},\"logs\":\"" + raw + "\"}";
+      const std::string req = "POST /parse HTTP/1.1\r\nContent-Length: " + std::to_string(body.size()) + "\r\n\r\n" + body;
+      if (send(fd, req.data(), req.size(), 0) != (ssize_t)req.size()) break;
+      std::string resp;
+      char b[4096];
+      while (resp.find("\r\n\r\n") == std::string::npos || resp.back() != '}') {
+        const ssize_t k = recv(fd, b, sizeof(b), 0);
+        if (k <= 0) break;
+        resp.append(b, (size_t)k);
+      }
+      const std::string want = "{\"n\":" + std::to_string(logs.size()) + ",\"h\":" + std::to_string(std::hash<std::string>()(logs)) + "}";
+      ok += resp.rfind(want) != std::string::npos;
+    }
+    close(fd);
+  }
+  done = true;
+  responder.join();
+  const uint64_t pre = srv.stages.prefetched.load();
+  srv.stop();
+  CHECK(ok == rounds, "http undecoded: %d of %d responses", ok, rounds);
+  CHECK(with_dec.load() == 0, "http undecoded: %d bodies were decoded by the IO thread", with_dec.load());
+  CHECK(pre == 0, "http undecoded: a body was prefetched");
+  std::printf("http undecoded (burst mode): %d bodies\n", ok);
+}
+
 static void http_selftest(int rounds) {
   HttpServer srv("127.0.0.1", 0, 2, 1 << 20);
   std::atomic<bool> done{false};
@@ -301,6 +364,7 @@ int main(int argc, char** argv) {
   fuzz_prefetch(iters / 3 + 50, 99);
   http_selftest(iters / 20 + 10);
   http_prefetch_selftest(12);
+  http_undecoded_selftest(8);
   const uint8_t t[] = {'a', 0xE2, 0x80, 0xA8};
   CHECK(final_terminator_len(t, 4) == 3, "U+2028 final terminator");
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);

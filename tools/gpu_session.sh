@@ -12,10 +12,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run full_pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-run full_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-run full_bench 400 python -u bench.py
-run single 300 python -u benchmarks/bench_configs.py single
-run c5 300 python -u benchmarks/bench_configs.py concurrent_http --client-threads 8
-run ps 300 python -u tools/parse_stages.py --n 400
-run small 300 python -u tools/small_phases.py --requests 300
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+run bprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/bp -o run -- python3 bench.py --steps 6 --warmup 2 --parse-requests 0 --no-overlap
+run btl 120 python3 tools/kstats_db.py $(find gpurun_out/bp -name "*.db" | head -1) 6 40 --marker k_nl_count --last 6 --timeline
+rm -rf gpurun_out/bp

@@ -12,7 +12,7 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-run bprof 400 rocprofv3 --kernel-trace --stats -d gpurun_out/bp -o run -- python3 bench.py --steps 6 --warmup 2 --parse-requests 0 --no-overlap
-run btl 120 python3 tools/kstats_db.py $(find gpurun_out/bp -name "*.db" | head -1) 6 40 --marker k_nl_count --last 6 --timeline
-rm -rf gpurun_out/bp
+run gt 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+run bench 400 python -u bench.py
+run single 300 python -u benchmarks/bench_configs.py single
+run small 300 python -u tools/small_phases.py --requests 300

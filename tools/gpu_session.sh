@@ -12,7 +12,6 @@ run() {   # run NAME SECONDS CMD... : stop the session at the first failure
   [ $rc -eq 0 ] || exit $rc
 }
 
-run gt 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+run ps1 300 python -u tools/parse_stages.py --n 400
 run bench 400 python -u bench.py
-run single 300 python -u benchmarks/bench_configs.py single
-run small 300 python -u tools/small_phases.py --requests 300
+run ps2 300 python -u tools/parse_stages.py --n 400
